@@ -1,0 +1,175 @@
+/*
+ * mgenx.h -- C ABI of the MI355X MgenMsg pack/parse engine (libmgenx.so).
+ *
+ * Plain pointers and sizes only.  Every `dev_*` pointer is device (HBM) memory; the
+ * caller owns every buffer (the library never allocates or frees them, matching the
+ * reference's caller-owned UINT32 buffers, mgenTransport.cpp:944,1023).  Calls are
+ * asynchronous on the caller's hipStream_t (passed as void*), never synchronise and
+ * never allocate, so they can be captured in a hipGraph.  One mgenx_ctx per device.
+ *
+ * Return value: 0 = launched, <0 = argument/launch error (MGENX_E*).  Per-record
+ * outcomes go to the `err` column with MgenMsg::Error codes (include/mgenMsg.h:63-70).
+ *
+ * Reference interfaces replaced (USNavalResearchLaboratory/mgen):
+ *   mgenx_unpack_batch  <- MgenMsg::Unpack            include/mgenMsg.h:110
+ *                          + receive CRC check        src/common/mgenTransport.cpp:958-975
+ *                          (SINK 2092-2112, TCP CalcRxChecksum 1516-1564)
+ *   mgenx_pack_batch    <- MgenMsg::Pack              include/mgenMsg.h:108
+ *                          + MgenMsg::WriteChecksum   include/mgenMsg.h:111
+ *                          + UDP/SINK send sequence   src/common/mgenTransport.cpp:1011-1031
+ *   mgenx_stream_scan   <- TCP/SINK record framing    src/common/mgenTransport.cpp:1683-1760,
+ *                                                     mgenAppSinkTransport.cpp:369-434
+ *   mgenx_flow_reduce   <- MgenAnalytic::Update       include/mgenAnalytic.h:91-94
+ *                          via Mgen::UpdateRecvAnalytics src/common/mgen.cpp:1027-1070
+ *   mgenx_crc32         <- MgenMsg::ComputeCRC32      include/mgenMsg.h:201-203
+ */
+#ifndef MGENX_H
+#define MGENX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MGENX_ABI_VERSION 1
+
+/* ---- status codes ---- */
+#define MGENX_OK          0
+#define MGENX_EINVAL     -1   /* bad argument (null pointer, zero stride ...) */
+#define MGENX_EDEVICE    -2   /* HIP error (no device, launch failure) */
+#define MGENX_ENOMEM     -3   /* context workspace allocation failed (create only) */
+
+/* ---- wire constants (include/mgenGlobals.h:70-80, include/mgenMsg.h:60-103) ---- */
+#define MGENX_MIN_SIZE        28
+#define MGENX_MAX_SIZE        8192
+#define MGENX_TX_BUFFER_SIZE  8192
+#define MGENX_MAX_FRAG_SIZE   65535
+#define MGENX_FLAG_CONTINUES      0x01
+#define MGENX_FLAG_END_OF_MSG     0x02
+#define MGENX_FLAG_CHECKSUM       0x04
+#define MGENX_FLAG_LAST_BUFFER    0x08
+#define MGENX_FLAG_CHECKSUM_ERROR 0x10
+#define MGENX_ERROR_NONE      0
+#define MGENX_ERROR_VERSION   1
+#define MGENX_ERROR_CHECKSUM  2
+#define MGENX_ERROR_LENGTH    3
+#define MGENX_ERROR_DSTADDR   4
+#define MGENX_ERROR_OOB       0x80  /* record lies outside the slab: not touched */
+
+/* ---- unpack options ---- */
+#define MGENX_OPT_CHECKSUM_FORCE  0x1  /* Mgen checksum_force (mgen.cpp:2076-2087) */
+#define MGENX_OPT_TCP             0x2  /* TCP receive rules: Unpack sees min(len, 8192)
+                                          bytes; a CRC mismatch also sets
+                                          CHECKSUM_ERROR in flags (mgenTransport.cpp:1555) */
+#define MGENX_OPT_SKIP_CRC        0x4  /* header-only decode (benchmark mode; NOT the
+                                          reference receive path) */
+
+typedef struct mgenx_ctx mgenx_ctx;
+
+int  mgenx_abi_version(void);
+int  mgenx_ctx_create(int device, mgenx_ctx** out);
+int  mgenx_ctx_destroy(mgenx_ctx* ctx);
+/* Last HIP error string seen by this context (static storage). */
+const char* mgenx_last_error(const mgenx_ctx* ctx);
+
+/* ------------------------------------------------------------------ */
+/* Columns written by unpack: the MgenMsg state after Unpack() on a    */
+/* fresh MgenMsg (mgenMsg.cpp:315-500), one element per record.        */
+/* Core columns (32 bytes per record) are required; extended columns   */
+/* may be NULL (not written).                                          */
+/* ------------------------------------------------------------------ */
+typedef struct {
+    /* core */
+    uint32_t* flow_id;
+    uint32_t* seq_num;
+    uint32_t* tx_sec;
+    uint32_t* tx_usec;
+    uint16_t* msg_len;
+    uint16_t* dst_port;
+    uint8_t*  flags;
+    uint8_t*  err;          /* MgenMsg::Error (+ MGENX_ERROR_OOB) */
+    uint8_t*  dst_type;     /* ProtoAddress type (0 = not decoded, 1 IPv4, 2 IPv6) */
+    uint8_t*  dst_len;      /* dst address length byte from the wire */
+    uint32_t* dst_addr4;    /* first 4 address bytes, in wire order in memory */
+    uint16_t* payload_len;
+    uint8_t*  payload_type;
+    uint8_t*  gps_status;
+    /* extended (optional) */
+    uint16_t* hdr_len;      /* packet_header_len */
+    uint32_t* payload_off;  /* payload_data - record start = (hdr_len/4)*4 */
+    uint16_t* host_port;
+    uint8_t*  host_type;
+    uint8_t*  host_len;
+    uint8_t*  host_addr;    /* 16 bytes per record */
+    uint8_t*  dst_addr;     /* 16 bytes per record */
+    uint32_t* lat_raw;      /* ntohl(latitude word): degrees = raw/60000 - 180 */
+    uint32_t* lon_raw;
+    int32_t*  alt;
+} mgenx_cols;
+
+/* Decode n records.  Record i starts at dev_slab + (dev_rec_off ? dev_rec_off[i] :
+ * i*stride) and is (dev_rec_len ? dev_rec_len[i] : fixed_len) bytes long (the receive
+ * length: recvfrom's len for UDP, the framed msg_len for TCP/SINK).  Records extending
+ * past slab_bytes are flagged MGENX_ERROR_OOB and not read. */
+int mgenx_unpack_batch(mgenx_ctx* ctx, const uint8_t* dev_slab, uint64_t slab_bytes,
+                       const uint64_t* dev_rec_off, uint64_t stride,
+                       const uint32_t* dev_rec_len, uint32_t fixed_len, uint32_t n,
+                       const mgenx_cols* cols, uint32_t opts, void* stream);
+
+/* ------------------------------------------------------------------ */
+/* Pack.  A per-flow template table holds what MgenFlow::SendMessage    */
+/* takes from flow state (mgenFlow.cpp:946-983, 1039-1129); a 20-byte   */
+/* descriptor per record holds the per-message fields.                 */
+/* ------------------------------------------------------------------ */
+typedef struct {
+    uint32_t flow_id;
+    uint8_t  dst_type, dst_len; uint16_t dst_port;    /* dst_type: 1 IPv4, 2 IPv6 */
+    uint8_t  dst_addr[16];
+    uint8_t  host_type, host_len; uint16_t host_port;  /* host_type 0 = invalid (no host) */
+    uint8_t  host_addr[16];
+    uint32_t lat_raw, lon_raw;   /* (UINT32)((deg + 180.0) * 60000.0), mgenMsg.cpp:221,225 */
+    int32_t  alt;
+    uint8_t  gps_status, payload_type; uint16_t payload_len;
+    uint32_t payload_off;        /* into dev_pool */
+    uint8_t  has_payload, rsv0; uint16_t rsv1;
+} mgenx_flow_tmpl;               /* 68 bytes */
+
+typedef struct {
+    uint32_t tmpl;               /* index into the template table */
+    uint32_t seq_num, tx_sec, tx_usec;
+    uint16_t msg_len;            /* MgenMsg::msg_len = the record length */
+    uint8_t  flags;              /* MgenMsg flags before the transport sets LAST_BUFFER */
+    uint8_t  rsv;
+} mgenx_pack_desc;               /* 20 bytes */
+
+#define MGENX_PACK_CHECKSUM    0x1   /* Mgen checksum_enable */
+#define MGENX_PACK_RANDOM_FILL 0x2   /* the RANDOM_FILL build: fill = glibc rand() bytes
+                                        after srand(fill_time) (mgenMsg.cpp:277-292) */
+
+/* Pack n records with the UDP/SINK send sequence (LAST_BUFFER, Pack, WriteChecksum)
+ * into dev_slab at dev_rec_off[i] (or i*stride).  dev_out_len[i] = Pack()'s return
+ * (0 = MSG_SEND_FAILED).  Template CRCs must be prepared by mgenx_pack_prepare when
+ * the template table or pool changes. */
+int mgenx_pack_prepare(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl, uint32_t n_tmpl,
+                       const uint8_t* dev_pool, uint32_t* dev_tmpl_crc, void* stream);
+/* Select the RANDOM_FILL stream (time(NULL) value the reference would seed srand with).
+ * Host-side table setup (synchronous); call when fill_time changes. */
+int mgenx_set_fill_time(mgenx_ctx* ctx, uint32_t fill_time);
+
+int mgenx_pack_batch(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
+                     const uint32_t* dev_tmpl_crc, const mgenx_pack_desc* dev_desc, uint32_t n,
+                     const uint8_t* dev_pool, uint8_t* dev_slab, uint64_t slab_bytes,
+                     const uint64_t* dev_rec_off, uint64_t stride, uint32_t* dev_out_len,
+                     uint32_t opts, uint32_t fill_time, void* stream);
+
+/* Standard CRC-32 (MgenMsg::ComputeCRC32 from a zero state + CRC32_XOROT) of n
+ * byte ranges: out[i] = crc(dev_data[off[i] .. off[i]+len[i])). */
+int mgenx_crc32_batch(mgenx_ctx* ctx, const uint8_t* dev_data, const uint64_t* dev_off,
+                      const uint32_t* dev_len, uint32_t n, uint32_t* dev_out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

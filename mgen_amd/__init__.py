@@ -1,0 +1,171 @@
+"""mgen_amd -- MI355X-native MgenMsg pack/parse engine (host binding).
+
+Thin ctypes binding of the C ABI in ``include/mgenx.h`` (libmgenx.so, built from
+``mgen_amd/csrc`` for gfx950).  PyTorch is used only for device memory and streams.
+There is no CPU fallback: if the HIP library is missing, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from ._abi import (  # noqa: F401
+    COLS_CORE, COLS_EXT, DESC_DTYPE, TMPL_DTYPE, MgenxCols, ERROR_CHECKSUM, ERROR_DSTADDR,
+    ERROR_LENGTH, ERROR_NONE, ERROR_OOB, ERROR_VERSION, FLAG_CHECKSUM, FLAG_CHECKSUM_ERROR,
+    FLAG_LAST_BUFFER, OPT_CHECKSUM_FORCE, OPT_SKIP_CRC, OPT_TCP, PACK_CHECKSUM,
+    PACK_RANDOM_FILL,
+)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmgenx.so")
+
+EXPORTED_SYMBOLS = (
+    "mgenx_abi_version", "mgenx_ctx_create", "mgenx_ctx_destroy", "mgenx_last_error",
+    "mgenx_unpack_batch", "mgenx_pack_prepare", "mgenx_set_fill_time", "mgenx_pack_batch",
+    "mgenx_crc32_batch", "mgenx_stream_scan", "mgenx_flow_reduce",
+)
+
+
+class MgenxError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load():
+    """Load libmgenx.so (fails loudly when the HIP build is missing)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise MgenxError(f"{LIB_PATH} not built: run __graft_entry__.build() "
+                         "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    P, u32, u64, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+    L.mgenx_abi_version.restype = i32
+    L.mgenx_ctx_create.argtypes = [i32, ctypes.POINTER(P)]
+    L.mgenx_ctx_destroy.argtypes = [P]
+    L.mgenx_last_error.argtypes = [P]
+    L.mgenx_last_error.restype = ctypes.c_char_p
+    L.mgenx_unpack_batch.argtypes = [P, P, u64, P, u64, P, u32, u32,
+                                     ctypes.POINTER(MgenxCols), u32, P]
+    L.mgenx_pack_prepare.argtypes = [P, P, u32, P, P, P]
+    L.mgenx_set_fill_time.argtypes = [P, u32]
+    L.mgenx_pack_batch.argtypes = [P, P, P, P, u32, P, P, u64, P, u64, P, u32, u32, P]
+    L.mgenx_crc32_batch.argtypes = [P, P, P, P, u32, P, P]
+    if hasattr(L, "mgenx_stream_scan"):
+        L.mgenx_stream_scan.argtypes = [P, P, u64, u64, u32, u32, P, P, P, P, P, u32, P]
+    _lib = L
+    return L
+
+
+def _ptr(t):
+    """Raw device pointer of a torch tensor (or None)."""
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(device):
+    import torch
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class Engine:
+    """One mgenx context on one GPU (``mgenx_ctx``)."""
+
+    def __init__(self, device: int = 0):
+        import torch
+        self.torch = torch
+        self.device = device
+        self.lib = load()
+        self.ctx = ctypes.c_void_p()
+        rc = self.lib.mgenx_ctx_create(device, ctypes.byref(self.ctx))
+        if rc != 0:
+            raise MgenxError(f"mgenx_ctx_create({device}) failed: {rc}")
+
+    def close(self):
+        if self.ctx:
+            self.lib.mgenx_ctx_destroy(self.ctx)
+            self.ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != 0:
+            msg = self.lib.mgenx_last_error(self.ctx)
+            raise MgenxError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+    # ------------------------------------------------------------ columns
+    def alloc_cols(self, n: int, ext: bool = False):
+        torch = self.torch
+        dev = f"cuda:{self.device}"
+        cols = {name: torch.empty(n * w if w > 1 else n, dtype=getattr(torch, dt), device=dev)
+                for name, dt, w in COLS_CORE}
+        if ext:
+            for name, dt, w in COLS_EXT:
+                cols[name] = torch.empty(n * w if w > 1 else n, dtype=getattr(torch, dt),
+                                         device=dev)
+        return cols
+
+    @staticmethod
+    def _cols_struct(cols):
+        s = MgenxCols()
+        for name, _ in MgenxCols._fields_:
+            t = cols.get(name)
+            setattr(s, name, t.data_ptr() if t is not None else None)
+        return s
+
+    # ------------------------------------------------------------ unpack
+    def unpack(self, slab, n, *, rec_off=None, stride=0, rec_len=None, fixed_len=0, opts=0,
+               cols=None, ext=False, slab_bytes=None):
+        """MgenMsg::Unpack + receive CRC check over n records (async on the current stream)."""
+        if cols is None:
+            cols = self.alloc_cols(n, ext)
+        cs = self._cols_struct(cols)
+        nbytes = slab.numel() if slab_bytes is None else slab_bytes
+        rc = self.lib.mgenx_unpack_batch(self.ctx, _ptr(slab), nbytes, _ptr(rec_off), stride,
+                                         _ptr(rec_len), fixed_len, n, ctypes.byref(cs), opts,
+                                         _stream(self.device))
+        self._check(rc, "mgenx_unpack_batch")
+        return cols
+
+    # ------------------------------------------------------------ pack
+    def pack_prepare(self, tmpl, n_tmpl, pool, tmpl_crc):
+        rc = self.lib.mgenx_pack_prepare(self.ctx, _ptr(tmpl), n_tmpl, _ptr(pool),
+                                         _ptr(tmpl_crc), _stream(self.device))
+        self._check(rc, "mgenx_pack_prepare")
+
+    def set_fill_time(self, fill_time: int):
+        self._check(self.lib.mgenx_set_fill_time(self.ctx, fill_time), "mgenx_set_fill_time")
+
+    def pack(self, tmpl, tmpl_crc, desc, n, pool, slab, *, rec_off=None, stride=0, opts=0,
+             fill_time=0, out_len=None):
+        if out_len is None:
+            out_len = self.torch.empty(n, dtype=self.torch.int32, device=slab.device)
+        rc = self.lib.mgenx_pack_batch(self.ctx, _ptr(tmpl), _ptr(tmpl_crc), _ptr(desc), n,
+                                       _ptr(pool), _ptr(slab), slab.numel(), _ptr(rec_off),
+                                       stride, _ptr(out_len), opts, fill_time,
+                                       _stream(self.device))
+        self._check(rc, "mgenx_pack_batch")
+        return out_len
+
+    def crc32(self, data, off, length, n, out=None):
+        if out is None:
+            out = self.torch.empty(n, dtype=self.torch.int32, device=data.device)
+        rc = self.lib.mgenx_crc32_batch(self.ctx, _ptr(data), _ptr(off), _ptr(length), n,
+                                        _ptr(out), _stream(self.device))
+        self._check(rc, "mgenx_crc32_batch")
+        return out
+
+
+def to_device(arr: np.ndarray, device=0):
+    """Copy a numpy (structured) array to the GPU as raw bytes (uint8 tensor)."""
+    import torch
+    b = np.ascontiguousarray(arr).view(np.uint8).reshape(-1)
+    return torch.from_numpy(b.copy()).to(f"cuda:{device}")

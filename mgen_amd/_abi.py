@@ -1,0 +1,76 @@
+"""Python mirror of the C ABI layouts in include/mgenx.h (no torch, no HIP needed)."""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+# MgenMsg::Error (include/mgenMsg.h:63-70) and flags (:89-97)
+ERROR_NONE, ERROR_VERSION, ERROR_CHECKSUM, ERROR_LENGTH, ERROR_DSTADDR = 0, 1, 2, 3, 4
+ERROR_OOB = 0x80
+FLAG_CONTINUES, FLAG_END_OF_MSG, FLAG_CHECKSUM, FLAG_LAST_BUFFER, FLAG_CHECKSUM_ERROR = (
+    0x01, 0x02, 0x04, 0x08, 0x10)
+OPT_CHECKSUM_FORCE, OPT_TCP, OPT_SKIP_CRC = 0x1, 0x2, 0x4
+PACK_CHECKSUM, PACK_RANDOM_FILL = 0x1, 0x2
+SCAN_TCP, SCAN_SINK = 0, 1
+
+# mgenx_flow_tmpl (68 bytes) and mgenx_pack_desc (20 bytes)
+TMPL_DTYPE = np.dtype([
+    ("flow_id", "<u4"),
+    ("dst_type", "u1"), ("dst_len", "u1"), ("dst_port", "<u2"),
+    ("dst_addr", "u1", 16),
+    ("host_type", "u1"), ("host_len", "u1"), ("host_port", "<u2"),
+    ("host_addr", "u1", 16),
+    ("lat_raw", "<u4"), ("lon_raw", "<u4"), ("alt", "<i4"),
+    ("gps_status", "u1"), ("payload_type", "u1"), ("payload_len", "<u2"),
+    ("payload_off", "<u4"),
+    ("has_payload", "u1"), ("rsv0", "u1"), ("rsv1", "<u2"),
+], align=True)
+assert TMPL_DTYPE.itemsize == 68
+
+DESC_DTYPE = np.dtype([
+    ("tmpl", "<u4"), ("seq_num", "<u4"), ("tx_sec", "<u4"), ("tx_usec", "<u4"),
+    ("msg_len", "<u2"), ("flags", "u1"), ("rsv", "u1"),
+], align=True)
+assert DESC_DTYPE.itemsize == 20
+
+# (name, torch dtype name, elements per record)
+COLS_CORE = (
+    ("flow_id", "int32", 1), ("seq_num", "int32", 1), ("tx_sec", "int32", 1),
+    ("tx_usec", "int32", 1), ("msg_len", "int16", 1), ("dst_port", "int16", 1),
+    ("flags", "uint8", 1), ("err", "uint8", 1), ("dst_type", "uint8", 1),
+    ("dst_len", "uint8", 1), ("dst_addr4", "int32", 1), ("payload_len", "int16", 1),
+    ("payload_type", "uint8", 1), ("gps_status", "uint8", 1),
+)
+COLS_EXT = (
+    ("hdr_len", "int16", 1), ("payload_off", "int32", 1), ("host_port", "int16", 1),
+    ("host_type", "uint8", 1), ("host_len", "uint8", 1), ("host_addr", "uint8", 16),
+    ("dst_addr", "uint8", 16), ("lat_raw", "int32", 1), ("lon_raw", "int32", 1),
+    ("alt", "int32", 1),
+)
+CORE_BYTES_PER_RECORD = 32
+
+
+class MgenxCols(ctypes.Structure):
+    _fields_ = [(name, ctypes.c_void_p) for name, _, _ in COLS_CORE + COLS_EXT]
+
+
+def gps_raw(deg: float) -> int:
+    """(UINT32)((deg + 180.0) * 60000.0) as MgenMsg::Pack computes it (mgenMsg.cpp:221,225)."""
+    v = (deg + 180.0) * 60000.0
+    return int(v) & 0xFFFFFFFF
+
+
+def hex_payload(hexstr: str) -> bytes:
+    """MgenPayload::SetPayloadString (mgenPayload.cpp:24-55): odd length reads the NUL as 0,
+    non-hex characters decode as 0."""
+    def nib(c):
+        c = c.upper()
+        return int(c, 16) if c in "0123456789ABCDEF" else 0
+    n = len(hexstr) // 2 + len(hexstr) % 2
+    out = bytearray(n)
+    for i in range(n):
+        hi = nib(hexstr[2 * i])
+        lo = nib(hexstr[2 * i + 1]) if 2 * i + 1 < len(hexstr) else 0
+        out[i] = (hi << 4) | lo
+    return bytes(out)

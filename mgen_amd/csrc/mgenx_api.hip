@@ -1,0 +1,269 @@
+// mgenx_api.hip -- C ABI (include/mgenx.h) over the gfx950 kernels.
+//
+// The context owns only constant tables (CRC shift operators, x^(8n) mod P, the random
+// fill stream); every data buffer belongs to the caller.  No entry point allocates,
+// synchronises or copies from host memory except mgenx_ctx_create and
+// mgenx_pack_prepare (table setup), so batch calls can be captured in a hipGraph.
+#include <stdio.h>
+#include <string.h>
+
+#include <vector>
+
+
+#include "mgenx_kernels.hpp"
+
+struct mgenx_ctx {
+  int device = 0;
+  int cu_count = 0;
+  uint32_t* d_tabs = nullptr;     // [A64 | A4 | A16 | A32] 4 x 1024
+  uint32_t* d_expect = nullptr;   // [65536]
+  uint32_t* d_xpow = nullptr;     // [65536]
+  uint32_t* d_ia = nullptr;       // [65536]
+  uint32_t* d_bytetab = nullptr;  // [256]
+  uint8_t* d_rtab = nullptr;      // 16 + 65536 + 32 bytes
+  uint32_t* d_rcrc = nullptr;     // [65536]
+  bool rand_ready = false;
+  uint32_t rand_time = 0;
+  char err[256] = {0};
+};
+
+namespace {
+
+constexpr uint32_t kN = 65536;
+
+void byte_table(uint32_t t[256]) {
+  for (uint32_t i = 0; i < 256; i++) {
+    uint32_t c = i;
+    for (int k = 0; k < 8; k++) c = (c & 1u) ? (mgenx::kPoly ^ (c >> 1)) : (c >> 1);
+    t[i] = c;
+  }
+}
+
+// A_n(s): the state after n zero bytes.
+uint32_t shift_n(const uint32_t t[256], uint32_t s, uint32_t n) {
+  for (uint32_t i = 0; i < n; i++) s = t[s & 0xffu] ^ (s >> 8);
+  return s;
+}
+
+void op_table(const uint32_t t[256], uint32_t n, uint32_t* out /*1024*/) {
+  for (uint32_t k = 0; k < 4; k++)
+    for (uint32_t v = 0; v < 256; v++) out[k * 256 + v] = shift_n(t, v << (8 * k), n);
+}
+
+// glibc random_r TYPE_3 after srand(seed): the RANDOM_FILL byte source
+// (src/common/mgenMsg.cpp:277-292 calls srand(time(NULL)) then (char)rand()).
+void glibc_rand_bytes(uint32_t seed, uint32_t n, uint8_t* out) {
+  int32_t r[31];
+  int32_t word = (int32_t)(seed == 0 ? 1u : seed);
+  r[0] = word;
+  for (int i = 1; i < 31; i++) {
+    const long hi = word / 127773, lo = word % 127773;
+    word = (int32_t)(16807 * lo - 2836 * hi);
+    if (word < 0) word += 2147483647;
+    r[i] = word;
+  }
+  uint32_t ring[34];
+  for (int i = 0; i < 31; i++) ring[i] = (uint32_t)r[i];
+  for (int i = 31; i < 34; i++) ring[i] = ring[i - 31];
+  uint32_t made = 0;
+  for (uint64_t i = 34; made < n; i++) {
+    const uint32_t v = ring[(i - 31) % 34] + ring[(i - 3) % 34];
+    ring[i % 34] = v;
+    if (i >= 344) out[made++] = (uint8_t)(v >> 1);
+  }
+}
+
+int set_err(mgenx_ctx* c, hipError_t e, const char* where) {
+  if (c) snprintf(c->err, sizeof(c->err), "%s: %s", where, hipGetErrorString(e));
+  return MGENX_EDEVICE;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mgenx_abi_version(void) { return MGENX_ABI_VERSION; }
+
+const char* mgenx_last_error(const mgenx_ctx* ctx) { return ctx ? ctx->err : "null ctx"; }
+
+int mgenx_ctx_create(int device, mgenx_ctx** out) {
+  if (!out) return MGENX_EINVAL;
+  *out = nullptr;
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) return MGENX_EDEVICE;
+  hipDeviceProp_t prop;
+  e = hipGetDeviceProperties(&prop, device);
+  if (e != hipSuccess) return MGENX_EDEVICE;
+  mgenx_ctx* c = new mgenx_ctx();
+  c->device = device;
+  c->cu_count = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+
+  uint32_t t[256];
+  byte_table(t);
+  std::vector<uint32_t> tabs(4096), xpow(kN), ia(kN), expect(kN, 0);
+  op_table(t, 64, &tabs[0]);
+  op_table(t, 4, &tabs[1024]);
+  op_table(t, 16, &tabs[2048]);
+  op_table(t, 32, &tabs[3072]);
+  xpow[0] = 0x80000000u;  // x^0
+  for (uint32_t n = 1; n < kN; n++) xpow[n] = mgenx::multmodp(xpow[n - 1], 0x00800000u);
+  for (uint32_t n = 0; n < kN; n++) ia[n] = mgenx::multmodp(xpow[n], 0xFFFFFFFFu);
+  // self-check: x^(8n) multiplication is the n-zero-byte shift operator
+  for (uint32_t n : {1u, 3u, 64u, 1000u}) {
+    if (mgenx::multmodp(xpow[n], 0x12345678u) != shift_n(t, 0x12345678u, n)) {
+      delete c;
+      return MGENX_EINVAL;
+    }
+  }
+  for (uint32_t L = 4; L < kN; L++) expect[L] = shift_n(t, ia[L - 4] ^ 0xFFFFFFFFu, 4);
+
+  struct {
+    void** p;
+    size_t bytes;
+    const void* src;
+  } allocs[] = {
+      {(void**)&c->d_tabs, 4096 * 4, tabs.data()},
+      {(void**)&c->d_expect, kN * 4, expect.data()},
+      {(void**)&c->d_xpow, kN * 4, xpow.data()},
+      {(void**)&c->d_ia, kN * 4, ia.data()},
+      {(void**)&c->d_bytetab, 256 * 4, t},
+      {(void**)&c->d_rtab, 16 + kN + 32, nullptr},
+      {(void**)&c->d_rcrc, kN * 4, nullptr},
+  };
+  for (auto& a : allocs) {
+    if (hipMalloc(a.p, a.bytes) != hipSuccess) {
+      mgenx_ctx_destroy(c);
+      return MGENX_ENOMEM;
+    }
+    e = a.src ? hipMemcpy(*a.p, a.src, a.bytes, hipMemcpyHostToDevice)
+              : hipMemset(*a.p, 0, a.bytes);
+    if (e != hipSuccess) {
+      mgenx_ctx_destroy(c);
+      return MGENX_EDEVICE;
+    }
+  }
+  *out = c;
+  return MGENX_OK;
+}
+
+int mgenx_ctx_destroy(mgenx_ctx* c) {
+  if (!c) return MGENX_EINVAL;
+  hipSetDevice(c->device);
+  void* ps[] = {c->d_tabs, c->d_expect, c->d_xpow, c->d_ia, c->d_bytetab, c->d_rtab, c->d_rcrc};
+  for (void* p : ps)
+    if (p) hipFree(p);
+  delete c;
+  return MGENX_OK;
+}
+
+int mgenx_unpack_batch(mgenx_ctx* ctx, const uint8_t* dev_slab, uint64_t slab_bytes,
+                       const uint64_t* dev_rec_off, uint64_t stride,
+                       const uint32_t* dev_rec_len, uint32_t fixed_len, uint32_t n,
+                       const mgenx_cols* cols, uint32_t opts, void* stream) {
+  if (!ctx || !cols) return MGENX_EINVAL;
+  if (n == 0) return MGENX_OK;
+  if (!dev_slab) return MGENX_EINVAL;
+  if (!dev_rec_off && stride == 0 && n > 1) return MGENX_EINVAL;
+  const mgenx_cols& k = *cols;
+  if (!k.flow_id || !k.seq_num || !k.tx_sec || !k.tx_usec || !k.msg_len || !k.dst_port ||
+      !k.flags || !k.err || !k.dst_type || !k.dst_len || !k.dst_addr4 || !k.payload_len ||
+      !k.payload_type || !k.gps_status)
+    return MGENX_EINVAL;
+  mgenx::UnpackParams p;
+  p.slab = dev_slab;
+  p.slab_bytes = slab_bytes;
+  p.rec_off = dev_rec_off;
+  p.stride = stride;
+  p.rec_len = dev_rec_len;
+  p.fixed_len = fixed_len;
+  p.n = n;
+  p.opts = opts;
+  p.tabs = ctx->d_tabs;
+  p.expect = ctx->d_expect;
+  p.cols = k;
+  const uint64_t groups = ((uint64_t)n + 15) / 16;
+  const uint64_t per_block = 16;  // waves per 1024-thread block
+  uint64_t grid = (groups + per_block - 1) / per_block;
+  if (grid > (uint64_t)ctx->cu_count) grid = ctx->cu_count;
+  hipError_t e = mgenx::launch_unpack(p, (int)grid, (hipStream_t)stream);
+  return e == hipSuccess ? MGENX_OK : set_err(ctx, e, "unpack");
+}
+
+int mgenx_pack_prepare(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl, uint32_t n_tmpl,
+                       const uint8_t* dev_pool, uint32_t* dev_tmpl_crc, void* stream) {
+  if (!ctx || (n_tmpl && (!dev_tmpl || !dev_tmpl_crc))) return MGENX_EINVAL;
+  hipError_t e = mgenx::launch_pack_prepare(dev_tmpl, n_tmpl, dev_pool, ctx->d_bytetab,
+                                            dev_tmpl_crc, (hipStream_t)stream);
+  return e == hipSuccess ? MGENX_OK : set_err(ctx, e, "pack_prepare");
+}
+
+int mgenx_set_fill_time(mgenx_ctx* ctx, uint32_t fill_time) {
+  if (!ctx) return MGENX_EINVAL;
+  if (ctx->rand_ready && ctx->rand_time == fill_time) return MGENX_OK;
+  std::vector<uint8_t> rt(16 + kN + 32, 0);
+  glibc_rand_bytes(fill_time, kN, &rt[16]);
+  uint32_t t[256];
+  byte_table(t);
+  std::vector<uint32_t> rc(kN);
+  uint32_t c = 0;
+  for (uint32_t k = 0; k < kN; k++) {
+    rc[k] = c;
+    c = t[(c ^ rt[16 + k]) & 0xffu] ^ (c >> 8);
+  }
+  hipSetDevice(ctx->device);
+  hipError_t e = hipMemcpy(ctx->d_rtab, rt.data(), rt.size(), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(ctx->d_rcrc, rc.data(), kN * 4, hipMemcpyHostToDevice);
+  if (e != hipSuccess) return set_err(ctx, e, "set_fill_time");
+  ctx->rand_ready = true;
+  ctx->rand_time = fill_time;
+  return MGENX_OK;
+}
+
+int mgenx_pack_batch(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
+                     const uint32_t* dev_tmpl_crc, const mgenx_pack_desc* dev_desc, uint32_t n,
+                     const uint8_t* dev_pool, uint8_t* dev_slab, uint64_t slab_bytes,
+                     const uint64_t* dev_rec_off, uint64_t stride, uint32_t* dev_out_len,
+                     uint32_t opts, uint32_t fill_time, void* stream) {
+  if (!ctx) return MGENX_EINVAL;
+  if (n == 0) return MGENX_OK;
+  if (!dev_tmpl || !dev_tmpl_crc || !dev_desc || !dev_slab || !dev_out_len) return MGENX_EINVAL;
+  if (!dev_rec_off && stride == 0 && n > 1) return MGENX_EINVAL;
+  if (opts & MGENX_PACK_RANDOM_FILL) {
+    if (!ctx->rand_ready || ctx->rand_time != fill_time) return MGENX_EINVAL;
+  }
+  mgenx::PackParams p;
+  p.tmpl = dev_tmpl;
+  p.tmpl_crc = dev_tmpl_crc;
+  p.desc = dev_desc;
+  p.n = n;
+  p.pool = dev_pool;
+  p.slab = dev_slab;
+  p.slab_bytes = slab_bytes;
+  p.rec_off = dev_rec_off;
+  p.stride = stride;
+  p.out_len = dev_out_len;
+  p.opts = opts;
+  p.byte_tab = ctx->d_bytetab;
+  p.xpow = ctx->d_xpow;
+  p.ia = ctx->d_ia;
+  p.rtab = ctx->d_rtab;
+  p.rcrc = ctx->d_rcrc;
+  const uint64_t batches = ((uint64_t)n + 63) / 64;
+  uint64_t grid = (batches + 3) / 4;
+  const uint64_t cap = (uint64_t)ctx->cu_count * 4;
+  if (grid > cap) grid = cap;
+  hipError_t e = mgenx::launch_pack(p, (int)grid, (hipStream_t)stream);
+  return e == hipSuccess ? MGENX_OK : set_err(ctx, e, "pack");
+}
+
+int mgenx_crc32_batch(mgenx_ctx* ctx, const uint8_t* dev_data, const uint64_t* dev_off,
+                      const uint32_t* dev_len, uint32_t n, uint32_t* dev_out, void* stream) {
+  if (!ctx) return MGENX_EINVAL;
+  if (n == 0) return MGENX_OK;
+  if (!dev_data || !dev_off || !dev_len || !dev_out) return MGENX_EINVAL;
+  hipError_t e = mgenx::launch_crc32(dev_data, dev_off, dev_len, n, ctx->d_bytetab, ctx->d_xpow,
+                                     dev_out, (hipStream_t)stream);
+  return e == hipSuccess ? MGENX_OK : set_err(ctx, e, "crc32");
+}
+
+}  // extern "C"

@@ -1,0 +1,64 @@
+// mgenx_common.hpp -- shared device helpers for the MI355X MgenMsg engine.
+//
+// CRC-32 here is the reference's reflected CRC (poly 0x04C11DB7 reflected = 0xEDB88320,
+// init/xorout 0xFFFFFFFF; src/common/mgenMsg.cpp:524-554, table :576-642), evaluated with
+// GF(2)-linear "shift operators": A_n(s) is the CRC state after feeding n zero bytes to
+// state s with the byte-table update s = T[(s ^ b) & 0xff] ^ (s >> 8).  A_n is linear, so
+// it is applied as four 256-entry tables (one per state byte), and
+//     crc_raw(X || Y) = A_|Y|(crc_raw(X)) ^ crc_raw(Y)       (crc_raw = zero initial state)
+//     crc_init(X)     = crc_raw(X) ^ A_|X|(0xFFFFFFFF)
+// which lets lanes compute disjoint pieces of one record independently.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "mgenx.h"
+
+namespace mgenx {
+
+constexpr uint32_t kPoly = 0xEDB88320u;
+constexpr int kWave = 64;
+
+// ---- unaligned global access (gfx950 runs in unaligned-access mode: one dword / dwordx4
+//      instruction per access, split by the TA when it straddles lines) ----
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4_u1 __attribute__((ext_vector_type(4), aligned(1)));
+typedef uint32_t u32_u1 __attribute__((aligned(1)));
+typedef uint16_t u16_u1 __attribute__((aligned(1)));
+
+__device__ __forceinline__ u32x4_t ldu128(const uint8_t* p) {
+  return *reinterpret_cast<const u32x4_u1*>(p);
+}
+__device__ __forceinline__ uint32_t ldu32(const uint8_t* p) {
+  return *reinterpret_cast<const u32_u1*>(p);
+}
+__device__ __forceinline__ uint16_t ldu16(const uint8_t* p) {
+  return *reinterpret_cast<const u16_u1*>(p);
+}
+__device__ __forceinline__ void stu128(uint8_t* p, u32x4_t v) {
+  *reinterpret_cast<u32x4_u1*>(p) = v;
+}
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+__device__ __forceinline__ uint16_t bswap16(uint16_t x) { return __builtin_bswap16(x); }
+
+// GF(2) multiply mod P in reflected representation (bit 31 = x^0), branch-free.
+__host__ __device__ inline uint32_t multmodp(uint32_t a, uint32_t b) {
+  uint32_t p = 0;
+#pragma unroll
+  for (int i = 0; i < 32; i++) {
+    p ^= ((a >> (31 - i)) & 1u) ? b : 0u;
+    b = (b >> 1) ^ ((b & 1u) ? kPoly : 0u);
+  }
+  return p;
+}
+
+// Byte-mask helpers: bytes [lo, hi) of a little-endian 32-bit word, lo/hi in [0,4].
+__device__ __forceinline__ uint32_t byte_range_mask(int lo, int hi) {
+  uint32_t m_hi = hi >= 4 ? 0xFFFFFFFFu : ((1u << (8 * hi)) - 1u);
+  uint32_t m_lo = lo >= 4 ? 0xFFFFFFFFu : ((1u << (8 * lo)) - 1u);
+  return lo >= hi ? 0u : (m_hi & ~m_lo);
+}
+
+}  // namespace mgenx

@@ -1,0 +1,49 @@
+// mgenx_kernels.hpp -- kernel parameter blocks and launchers shared with mgenx_api.hip.
+#pragma once
+
+#include "mgenx_common.hpp"
+
+namespace mgenx {
+
+struct UnpackParams {
+  const uint8_t* slab;
+  uint64_t slab_bytes;
+  const uint64_t* rec_off;
+  uint64_t stride;
+  const uint32_t* rec_len;
+  uint32_t fixed_len;
+  uint32_t n;
+  uint32_t opts;
+  const uint32_t* tabs;    // [A64 | A4 | A16 | A32], each 4 x 256 (k-major)
+  const uint32_t* expect;  // [65536]
+  mgenx_cols cols;
+};
+
+struct PackParams {
+  const mgenx_flow_tmpl* tmpl;
+  const uint32_t* tmpl_crc;
+  const mgenx_pack_desc* desc;
+  uint32_t n;
+  const uint8_t* pool;
+  uint8_t* slab;
+  uint64_t slab_bytes;
+  const uint64_t* rec_off;
+  uint64_t stride;
+  uint32_t* out_len;
+  uint32_t opts;
+  const uint32_t* byte_tab;  // [256] reference CRC table
+  const uint32_t* xpow;      // [65536] x^(8n) mod P
+  const uint32_t* ia;        // [65536] A_n(0xFFFFFFFF)
+  const uint8_t* rtab;       // 16 zero bytes + glibc rand() byte stream (random fill)
+  const uint32_t* rcrc;      // [65536] crc_raw of the first k rand bytes
+};
+
+hipError_t launch_unpack(const UnpackParams& p, int grid, hipStream_t stream);
+hipError_t launch_pack(const PackParams& p, int grid, hipStream_t stream);
+hipError_t launch_pack_prepare(const mgenx_flow_tmpl* tmpl, uint32_t n_tmpl, const uint8_t* pool,
+                               const uint32_t* byte_tab, uint32_t* out, hipStream_t stream);
+hipError_t launch_crc32(const uint8_t* data, const uint64_t* off, const uint32_t* len, uint32_t n,
+                        const uint32_t* byte_tab, const uint32_t* xpow, uint32_t* out,
+                        hipStream_t stream);
+
+}  // namespace mgenx

@@ -1,0 +1,83 @@
+"""Synthetic MGEN batches for the BASELINE.json configurations.
+
+These build the *inputs* of the pack path (per-flow templates + per-record descriptors),
+the way MgenFlow::SendMessage fills an MgenMsg (src/common/mgenFlow.cpp:946-983): dst
+127.0.0.1/5000, GPS 999/999/-999 INVALID, optional DATA payload, per-flow sequence
+numbers, microsecond tx timestamps.  Seed base 0x4D47454E ("MGEN").
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from ._abi import DESC_DTYPE, TMPL_DTYPE, gps_raw
+
+SEED = 0x4D47454E
+T0 = 1_700_000_000
+
+
+def make_templates(n_flows: int, *, dst=(127, 0, 0, 1), dst_port=5000, payload: bytes = b"",
+                   host=None, ipv6=False):
+    """One template per flow (flow ids 1..n_flows).  Returns (tmpl, pool)."""
+    t = np.zeros(n_flows, TMPL_DTYPE)
+    t["flow_id"] = np.arange(1, n_flows + 1, dtype=np.uint32)
+    if ipv6:
+        t["dst_type"], t["dst_len"] = 2, 16
+        a = np.zeros(16, np.uint8)
+        a[15] = 1
+        t["dst_addr"][:] = a
+    else:
+        t["dst_type"], t["dst_len"] = 1, 4
+        t["dst_addr"][:, :4] = np.array(dst, np.uint8)
+    t["dst_port"] = dst_port
+    if host is not None:
+        kind, raw, port = host
+        t["host_type"] = 1 if kind == "4" else 2
+        t["host_len"] = len(raw)
+        t["host_addr"][:, :len(raw)] = np.frombuffer(bytes(raw), np.uint8)
+        t["host_port"] = port
+    t["lat_raw"] = gps_raw(999.0)
+    t["lon_raw"] = gps_raw(999.0)
+    t["alt"] = -999
+    t["gps_status"] = 0
+    pool = np.frombuffer(bytes(payload) if payload else b"\0", np.uint8).copy()
+    if payload:
+        t["has_payload"] = 1
+        t["payload_len"] = len(payload)
+        t["payload_off"] = 0
+    return t, pool
+
+
+def udp_fixed(n: int, size: int = 1024, n_flows: int = 64):
+    """Config 2: n records of `size` bytes, flow = 1 + (i mod n_flows), per-flow seq
+    0,1,2..., tx = T0 s + i us, dst 127.0.0.1/5000, no payload, zero fill."""
+    tmpl, pool = make_templates(n_flows)
+    i = np.arange(n, dtype=np.uint64)
+    d = np.zeros(n, DESC_DTYPE)
+    d["tmpl"] = (i % n_flows).astype(np.uint32)
+    d["seq_num"] = (i // n_flows).astype(np.uint32)
+    t_us = i + 0
+    d["tx_sec"] = (T0 + t_us // 1_000_000).astype(np.uint32)
+    d["tx_usec"] = (t_us % 1_000_000).astype(np.uint32)
+    d["msg_len"] = size
+    return tmpl, pool, d
+
+
+def udp_mixed(n: int, lo: int = 64, hi: int = 1472, n_flows: int = 64, payload_hex="",
+              seed=SEED):
+    """Config 3: flow = i mod n_flows, size ~ U{lo..hi}, per-flow DATA payload.
+    Returns (tmpl, pool, desc, offsets, sizes) with offsets = exclusive prefix sum."""
+    from ._abi import hex_payload
+    payload = hex_payload(payload_hex) if payload_hex else b""
+    tmpl, pool = make_templates(n_flows, payload=payload)
+    rng = np.random.default_rng(seed)
+    sizes = rng.integers(lo, hi + 1, size=n, dtype=np.int64)
+    i = np.arange(n, dtype=np.uint64)
+    d = np.zeros(n, DESC_DTYPE)
+    d["tmpl"] = (i % n_flows).astype(np.uint32)
+    d["seq_num"] = (i // n_flows).astype(np.uint32)
+    d["tx_sec"] = (T0 + i // 1_000_000).astype(np.uint32)
+    d["tx_usec"] = (i % 1_000_000).astype(np.uint32)
+    d["msg_len"] = sizes.astype(np.uint16)
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(sizes[:-1], dtype=np.uint64)
+    return tmpl, pool, d, offs, sizes.astype(np.uint32)

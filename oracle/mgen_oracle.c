@@ -1,0 +1,914 @@
+/*
+ * mgen_oracle.c -- TEST INFRASTRUCTURE ONLY (the checker, never the product).
+ *
+ * Plain-C restatement of the reference MGEN hot path.  Every function cites the
+ * reference file:line whose behaviour it restates.  See mgen_oracle.h for the
+ * parity-pinning status.
+ */
+#include "mgen_oracle.h"
+
+#include <math.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------ */
+/* helpers: network byte order                                         */
+/* ------------------------------------------------------------------ */
+static void put16(uint8_t* b, uint16_t v) { b[0] = (uint8_t)(v >> 8); b[1] = (uint8_t)v; }
+static void put32(uint8_t* b, uint32_t v)
+{
+    b[0] = (uint8_t)(v >> 24); b[1] = (uint8_t)(v >> 16); b[2] = (uint8_t)(v >> 8); b[3] = (uint8_t)v;
+}
+static uint16_t get16(const uint8_t* b) { return (uint16_t)((b[0] << 8) | b[1]); }
+static uint32_t get32(const uint8_t* b)
+{
+    return ((uint32_t)b[0] << 24) | ((uint32_t)b[1] << 16) | ((uint32_t)b[2] << 8) | b[3];
+}
+
+/* ------------------------------------------------------------------ */
+/* CRC-32: reflected poly 0x04C11DB7 (0xEDB88320), init/xorout ~0      */
+/* mgenMsg.cpp:524-554 (incremental ComputeCRC32), table :576-642      */
+/* ------------------------------------------------------------------ */
+static uint32_t g_table[256];
+static int g_table_ready = 0;
+
+void or_crc32_table(uint32_t table[256])
+{
+    for (uint32_t i = 0; i < 256; i++) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; k++) c = (c & 1) ? (0xEDB88320u ^ (c >> 1)) : (c >> 1);
+        table[i] = c;
+    }
+}
+
+static const uint32_t* table(void)
+{
+    if (!g_table_ready) { or_crc32_table(g_table); g_table_ready = 1; }
+    return g_table;
+}
+
+/* mgenMsg.cpp:524-541: a running value of exactly 0 restarts from CRC32_XINIT. */
+void or_crc32_update(uint32_t* checksum, const uint8_t* buf, uint32_t len)
+{
+    const uint32_t* t = table();
+    uint32_t c = *checksum;
+    if (c == 0) c = 0xFFFFFFFFu;
+    for (uint32_t i = 0; i < len; i++) c = t[(c ^ buf[i]) & 0xFFu] ^ (c >> 8);
+    *checksum = c;
+}
+
+/* mgenMsg.cpp:502-522: xor-out, stored big-endian at buflen-4. */
+int or_write_checksum(uint32_t* tx_checksum, uint8_t* buf, uint32_t buflen)
+{
+    if (buflen < 4) return 0;
+    *tx_checksum ^= 0xFFFFFFFFu;
+    put32(buf + buflen - 4, *tx_checksum);
+    return 1;
+}
+
+/* ------------------------------------------------------------------ */
+/* glibc random_r TYPE_3 (srand/rand) -- the RANDOM_FILL byte source   */
+/* (mgenMsg.cpp:277-292: srand(time(NULL)) then (char)rand() per byte) */
+/* ------------------------------------------------------------------ */
+void or_glibc_rand_bytes(uint32_t seed, uint32_t n, uint8_t* out)
+{
+    int32_t r[34];
+    int32_t word = (int32_t)(seed == 0 ? 1u : seed);
+    r[0] = word;
+    for (int i = 1; i < 31; i++) {
+        long hi = word / 127773;
+        long lo = word % 127773;
+        word = (int32_t)(16807 * lo - 2836 * hi);
+        if (word < 0) word += 2147483647;
+        r[i] = word;
+    }
+    /* ring of the last 34 values; r[i] = r[i-31] + r[i-3] (mod 2^32) */
+    uint32_t ring[34];
+    for (int i = 0; i < 31; i++) ring[i] = (uint32_t)r[i];
+    for (int i = 31; i < 34; i++) ring[i] = ring[i - 31];
+    uint64_t i = 34;
+    uint32_t produced = 0;
+    while (produced < n) {
+        uint32_t v = ring[(i - 31) % 34] + ring[(i - 3) % 34];
+        ring[i % 34] = v;
+        if (i >= 344) out[produced++] = (uint8_t)((v >> 1) & 0xFFu);
+        i++;
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* MgenMsg::Pack  (mgenMsg.cpp:83-313)                                 */
+/* ------------------------------------------------------------------ */
+static uint8_t wire_addr_type(uint8_t protoType)
+{
+    /* mgenMsg.cpp:131-149 / 161-177: ProtoAddress::IPv4 -> 1, IPv6 -> 2 */
+    return (protoType == OR_ADDR_IPV4 || protoType == OR_ADDR_IPV6) ? protoType : 0;
+}
+
+uint16_t or_pack(or_msg* m, uint8_t* buf, uint16_t bufferLen, int includeChecksum,
+                 uint32_t* tx_checksum, int random_fill, uint32_t fill_time, uint16_t* hdr_len)
+{
+    uint32_t len = 0;
+    const uint32_t msgLen = bufferLen;
+    uint16_t dummy;
+    if (!hdr_len) hdr_len = &dummy;
+
+    put16(buf + len, m->msg_len); len += 2;            /* :97-100 */
+    buf[len++] = m->version;                          /* :103 */
+    buf[len++] = m->flags;                            /* :106 */
+    put32(buf + len, m->flow_id); len += 4;           /* :109-112 */
+    put32(buf + len, m->seq_num); len += 4;           /* :114-117 */
+    put32(buf + len, m->tx_sec); len += 4;            /* :119-122 */
+    put32(buf + len, m->tx_usec); len += 4;           /* :124-127 */
+    put16(buf + len, m->dst.port); len += 2;          /* :129-131 */
+    uint8_t dtype = wire_addr_type(m->dst.type);
+    if (!dtype) return 0;                             /* :146-148 unsupported type */
+    uint8_t addrLen = m->dst.len;
+    buf[len++] = dtype;
+    buf[len++] = addrLen;
+    memcpy(buf + len, m->dst.addr, addrLen);          /* :155-157 */
+    len += addrLen;
+
+    /* host_addr (:163-216) */
+    const int hostValid = (m->host.type == OR_ADDR_IPV4 || m->host.type == OR_ADDR_IPV6);
+    uint8_t htype = hostValid ? m->host.type : 0;
+    addrLen = hostValid ? m->host.len : 0;
+    if (msgLen >= len + addrLen + 4) {
+        put16(buf + len, hostValid ? m->host.port : 0); len += 2;
+        buf[len++] = htype;
+        buf[len++] = addrLen;
+        if (addrLen) memcpy(buf + len, m->host.addr, addrLen);
+        len += addrLen;
+    } else {
+        if (msgLen < len) return 0;                   /* :207-210 */
+        memset(buf + len, 0, msgLen - len);
+        *hdr_len = (uint16_t)len;
+        return (uint16_t)msgLen;
+    }
+    /* GPS (:219-241) */
+    if (msgLen >= len + 13) {
+        put32(buf + len, (uint32_t)((m->latitude + 180.0) * 60000.0)); len += 4;
+        put32(buf + len, (uint32_t)((m->longitude + 180.0) * 60000.0)); len += 4;
+        put32(buf + len, (uint32_t)m->altitude); len += 4;
+        buf[len++] = m->gps_status;
+    } else {
+        memset(buf + len, 0, msgLen - len);
+        *hdr_len = (uint16_t)len;
+        return (uint16_t)msgLen;
+    }
+    /* payload_type (:243-251) */
+    if (msgLen >= len + 1) {
+        buf[len++] = m->payload_type;
+    } else {
+        *hdr_len = (uint16_t)len;
+        return (uint16_t)msgLen;
+    }
+    /* payload_len (:252-263) */
+    if (msgLen >= len + 2) {
+        put16(buf + len, m->payload_len);
+        len += 2;
+    } else {
+        memset(buf + len, 0, msgLen - len);
+        *hdr_len = (uint16_t)len;
+        return (uint16_t)msgLen;
+    }
+    *hdr_len = (uint16_t)len;
+    /* payload (:264-273) */
+    if (m->payload_data && msgLen >= len + m->payload_len) {
+        memcpy(buf + len, m->payload_data, m->payload_len);
+        len += m->payload_len;
+    } else {
+        buf[len - 2] = 0;
+        buf[len - 1] = 0;
+    }
+    /* fill (:275-294) */
+    if (msgLen > len) {
+        if (random_fill) {
+            if (msgLen >= 2 + len) {
+                buf[len] = 0;
+                buf[len + 1] = 0;
+                or_glibc_rand_bytes(fill_time, msgLen - (len + 2), buf + len + 2);
+            } else if (msgLen != len) {
+                buf[len] = 0;
+            }
+        } else {
+            memset(buf + len, 0, msgLen - len);
+        }
+    }
+    /* checksum (:295-310) */
+    if (includeChecksum) {
+        if (msgLen > len + 4) {
+            buf[3] |= OR_FLAG_CHECKSUM;
+            m->flags |= OR_FLAG_CHECKSUM;
+        }
+        if (m->flags & OR_FLAG_LAST_BUFFER)
+            or_crc32_update(tx_checksum, buf, msgLen - 4);
+        else
+            or_crc32_update(tx_checksum, buf, msgLen);
+        m->flags &= (uint8_t)~OR_FLAG_LAST_BUFFER;   /* ClearFlag (mgenMsg.h:126) */
+    }
+    return (uint16_t)msgLen;
+}
+
+/* MgenUdpTransport::SendMessage (mgenTransport.cpp:1011-1031);
+ * MgenAppSinkTransport::SendMessage (mgenAppSinkTransport.cpp:159-169). */
+uint32_t or_udp_pack(const or_msg* msg, uint8_t* out, int checksum_enable, int random_fill,
+                     uint32_t fill_time)
+{
+    or_msg m = *msg;
+    uint32_t tx = 0;
+    m.flags |= OR_FLAG_LAST_BUFFER;
+    uint32_t len = or_pack(&m, out, m.msg_len, checksum_enable, &tx, random_fill, fill_time, NULL);
+    if (len == 0) return 0;
+    if (checksum_enable && (m.flags & OR_FLAG_CHECKSUM)) or_write_checksum(&tx, out, len);
+    return len;
+}
+
+/* ------------------------------------------------------------------ */
+/* MgenTcpTransport transmit state machine                             */
+/* SendMessage :1320-1400, GetNextTxBuffer :1762-1816,                 */
+/* SetupNextTxBuffer :1818-1852, CalcTxChecksum :1854-1876,            */
+/* GetNextTxFragment :1878-1951, GetNextTxFragmentSize :1960-1993      */
+/* ------------------------------------------------------------------ */
+typedef struct {
+    or_msg   tx;
+    uint8_t  buf[OR_TX_BUFFER_SIZE + 4];
+    uint32_t tx_checksum;
+    uint32_t tx_buffer_index, tx_buffer_pending, tx_msg_offset;
+    uint16_t tx_fragment_pending;
+    int      ck, rf;
+    uint32_t T;
+} tcp_tx_state;
+
+static uint16_t tcp_next_fragment_size(tcp_tx_state* s)
+{
+    s->tx.flags &= (uint8_t)~OR_FLAG_CONTINUES;
+    s->tx.msg_len = 0;
+    uint32_t remaining = s->tx.mgen_msg_len - s->tx_msg_offset;
+    if (!remaining) return 0;
+    if (remaining > OR_MAX_FRAG_SIZE) {
+        if (remaining < (uint32_t)(OR_MAX_FRAG_SIZE + OR_MIN_FRAG_SIZE))
+            s->tx.msg_len = OR_MAX_FRAG_SIZE - OR_MIN_FRAG_SIZE;
+        else
+            s->tx.msg_len = OR_MAX_FRAG_SIZE;
+    } else {
+        s->tx.msg_len = (uint16_t)remaining;
+    }
+    if (s->tx.mgen_msg_len > OR_MAX_FRAG_SIZE) {
+        if ((s->tx.mgen_msg_len - s->tx_msg_offset) > s->tx.msg_len)
+            s->tx.flags |= OR_FLAG_CONTINUES;
+        else
+            s->tx.flags |= OR_FLAG_END_OF_MSG;
+    }
+    return s->tx.msg_len;
+}
+
+static uint16_t tcp_next_fragment(tcp_tx_state* s)
+{
+    uint16_t tx_buffer_size = OR_TX_BUFFER_SIZE;
+    s->buf[0] = 0;
+    s->tx_checksum = 0;
+    s->tx_buffer_index = 0;
+    if (!tcp_next_fragment_size(s)) return 0;
+    if (s->ck) {
+        /* int arithmetic: (msg_len - 8192) < 4 */
+        if (((int)s->tx.msg_len - OR_TX_BUFFER_SIZE) < 4 && s->tx.msg_len != OR_MIN_FRAG_SIZE)
+            tx_buffer_size = OR_TX_BUFFER_SIZE - 4;
+    }
+    if (s->tx.msg_len > OR_TX_BUFFER_SIZE) {
+        s->tx_buffer_pending = or_pack(&s->tx, s->buf, tx_buffer_size, s->ck, &s->tx_checksum,
+                                       s->rf, s->T, NULL);
+        s->tx_msg_offset += s->tx_buffer_pending;
+    } else if (s->tx.msg_len > 0) {
+        s->tx.flags |= OR_FLAG_LAST_BUFFER;
+        s->tx_buffer_pending = or_pack(&s->tx, s->buf, s->tx.msg_len, s->ck, &s->tx_checksum,
+                                       s->rf, s->T, NULL);
+        s->tx_msg_offset += s->tx_buffer_pending;
+        if (s->ck && (s->tx.flags & OR_FLAG_CHECKSUM))
+            or_write_checksum(&s->tx_checksum, s->buf, s->tx.msg_len);
+    } else {
+        s->tx_buffer_pending = 0;
+    }
+    return s->tx.msg_len;
+}
+
+static void tcp_calc_tx_checksum(tcp_tx_state* s)
+{
+    if (s->tx.flags & OR_FLAG_LAST_BUFFER) {
+        if (s->tx_buffer_pending < 4) return;
+        or_crc32_update(&s->tx_checksum, s->buf, s->tx_buffer_pending - 4);
+    } else {
+        or_crc32_update(&s->tx_checksum, s->buf, s->tx_buffer_pending);
+    }
+}
+
+static void tcp_setup_next_buffer(tcp_tx_state* s)
+{
+    if ((s->ck && s->tx_fragment_pending <= (OR_TX_BUFFER_SIZE - 4)) ||
+        (!s->ck && s->tx_fragment_pending <= OR_TX_BUFFER_SIZE)) {
+        s->tx_buffer_pending = s->tx_fragment_pending;
+        s->tx.flags |= OR_FLAG_LAST_BUFFER;
+        if (s->ck) tcp_calc_tx_checksum(s);
+        s->tx.flags &= (uint8_t)~OR_FLAG_LAST_BUFFER;
+        if (s->ck) or_write_checksum(&s->tx_checksum, s->buf, s->tx_fragment_pending);
+    } else {
+        if (s->ck && ((int)s->tx_fragment_pending - OR_TX_BUFFER_SIZE) < 4)
+            s->tx_buffer_pending = s->tx_fragment_pending - 4u;
+        else
+            s->tx_buffer_pending = OR_TX_BUFFER_SIZE;
+        if (s->ck) tcp_calc_tx_checksum(s);
+    }
+    s->tx_buffer_index = 0;
+    s->tx_msg_offset += s->tx_buffer_pending;
+}
+
+uint32_t or_tcp_tx(const or_msg* msg, uint8_t* out, int checksum_enable, int random_fill,
+                   uint32_t fill_time)
+{
+    static tcp_tx_state s;   /* 8 KB buffer; single-threaded test use */
+    memset(&s, 0, sizeof(s));
+    s.tx = *msg;
+    s.ck = checksum_enable;
+    s.rf = random_fill;
+    s.T = fill_time;
+    uint32_t outn = 0;
+    s.tx_fragment_pending = tcp_next_fragment(&s);
+    if (!s.tx_fragment_pending || !s.tx_buffer_pending) return 0;
+    for (uint32_t guard = 0; guard < (1u << 24); guard++) {
+        uint32_t numBytes = s.tx_buffer_pending;   /* Send() moves everything */
+        memcpy(out + outn, s.buf + s.tx_buffer_index, numBytes);
+        outn += numBytes;
+        s.tx_buffer_index += numBytes;
+        s.tx_buffer_pending -= numBytes;
+        s.tx_fragment_pending = (uint16_t)(s.tx_fragment_pending - numBytes);
+        if (s.tx_buffer_pending) continue;
+        if (0 == s.tx_buffer_pending && s.tx_fragment_pending) {
+            tcp_setup_next_buffer(&s);
+            if (s.tx_buffer_pending) continue;
+        }
+        if (s.tx_buffer_pending == 0 && s.tx_fragment_pending == 0) {
+            s.tx_fragment_pending = tcp_next_fragment(&s);
+            if (s.tx_buffer_pending) continue;
+        }
+        if (!s.tx_fragment_pending && s.tx_msg_offset > 0) return outn;
+    }
+    return outn;
+}
+
+/* ------------------------------------------------------------------ */
+/* MgenMsg::Unpack (mgenMsg.cpp:315-500) on a fresh MgenMsg            */
+/* (defaults from the constructor, mgenMsg.cpp:38-49)                  */
+/* ------------------------------------------------------------------ */
+static const uint32_t GPS_RAW_ZERO = 10800000u;   /* (0.0 + 180) * 60000 */
+
+void or_unpack(const uint8_t* buf, uint32_t bufferLen, or_fields* f)
+{
+    memset(f, 0, sizeof(*f));
+    f->version = OR_VERSION;
+    f->lat_raw = f->lon_raw = GPS_RAW_ZERO;
+    uint32_t len = 0;
+    if (bufferLen < OR_MIN_SIZE) { f->err = OR_ERROR_LENGTH; return; }   /* :323-328 */
+    f->msg_len = get16(buf); len += 2;
+    f->version = buf[len++];
+    if (f->version != OR_VERSION) { f->err = OR_ERROR_VERSION; return; } /* :336-343 */
+    f->flags = buf[len++];
+    f->flow_id = get32(buf + len); len += 4;
+    f->seq_num = get32(buf + len); len += 4;
+    f->tx_sec = get32(buf + len); len += 4;
+    f->tx_usec = get32(buf + len); len += 4;
+    uint16_t dstPort = get16(buf + len); len += 2;
+    uint8_t t = buf[len++];
+    if (t != OR_ADDR_IPV4 && t != OR_ADDR_IPV6) { f->err = OR_ERROR_DSTADDR; return; } /* :374-392 */
+    uint32_t addrLen = buf[len++];
+    /* :394-398 -- no bounds check in the reference; bytes past the record are
+     * undefined there (stale receive buffer) and read as zero here. */
+    f->dst_type = t;
+    f->dst_len = (uint8_t)addrLen;
+    for (uint32_t i = 0; i < addrLen && i < 16; i++)
+        f->dst_addr[i] = (len + i < bufferLen) ? buf[len + i] : 0;
+    f->dst_port = dstPort;
+    len += addrLen;
+    /* host (:400-443) */
+    if ((len + 4) <= bufferLen) {
+        uint16_t hostPort = get16(buf + len); len += 2;
+        uint8_t ht = buf[len++];
+        if (ht != OR_ADDR_IPV4 && ht != OR_ADDR_IPV6) ht = OR_ADDR_INVALID;
+        addrLen = buf[len++];
+        if ((len + addrLen) <= bufferLen) {
+            if (ht != OR_ADDR_INVALID) {
+                f->host_type = ht;
+                f->host_len = (uint8_t)addrLen;
+                for (uint32_t i = 0; i < addrLen && i < 16; i++) f->host_addr[i] = buf[len + i];
+                f->host_port = hostPort;
+            }
+            len += addrLen;
+        } else {
+            f->hdr_len = (uint16_t)len; f->ok = 1; return;
+        }
+    } else {
+        f->hdr_len = (uint16_t)len; f->ok = 1; return;
+    }
+    /* GPS (:446-465) */
+    if ((len + 13) <= bufferLen) {
+        f->lat_raw = get32(buf + len); len += 4;
+        f->lon_raw = get32(buf + len); len += 4;
+        f->alt = (int32_t)get32(buf + len); len += 4;
+        f->gps_status = buf[len++];
+    } else {
+        f->hdr_len = (uint16_t)len; f->ok = 1; return;
+    }
+    /* payload_type (:467-475) */
+    if ((len + 1) <= bufferLen) {
+        f->payload_type = buf[len++];
+    } else {
+        f->hdr_len = (uint16_t)len; f->ok = 1; return;
+    }
+    /* payload_len + data (:477-497) */
+    if ((len + 2) <= bufferLen) {
+        f->payload_len = get16(buf + len);
+        len += 2;
+        f->hdr_len = (uint16_t)len;
+        if (f->payload_len != 0 && (len + f->payload_len) <= bufferLen) {
+            f->payload_off = (len / 4) * 4;   /* alignedBuffer + len/4 (word floor) */
+        } else {
+            f->payload_len = 0;
+        }
+    }
+    f->ok = 1;
+}
+
+static int crc_ok(const uint8_t* rec, uint32_t len)
+{
+    if (len < 4) return 0;
+    uint32_t c = 0;
+    or_crc32_update(&c, rec, len - 4);
+    c ^= 0xFFFFFFFFu;
+    return c == get32(rec + len - 4);
+}
+
+/* mgenTransport.cpp:958-975 (UDP) and :2092-2112 (SINK HandleMgenMessage) */
+void or_udp_recv(const uint8_t* rec, uint32_t len, int checksum_force, or_fields* f)
+{
+    or_unpack(rec, len, f);
+    if (f->ok && (checksum_force || (f->flags & OR_FLAG_CHECKSUM))) {
+        if (!crc_ok(rec, len)) f->err = OR_ERROR_CHECKSUM;
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* TCP receive framing                                                 */
+/* Records are [p, p + msg_len); Unpack sees min(msg_len, 8192) bytes  */
+/* (CopyMsgBuffer :1996-2031); CRC over msg_len-4 vs the BE trailer   */
+/* (CalcRxChecksum :1516-1564), decided on the Unpacked flags or the   */
+/* force option; a mismatch sets ERROR_CHECKSUM and CHECKSUM_ERROR.    */
+/* The running CRC is evaluated over the whole span at once (the       */
+/* reference's read boundaries depend on partial socket reads).        */
+/* ------------------------------------------------------------------ */
+void or_tcp_recv(const uint8_t* rec, uint32_t L, int checksum_force, or_fields* o)
+{
+    or_unpack(rec, L < OR_TX_BUFFER_SIZE ? L : OR_TX_BUFFER_SIZE, o);
+    if (L >= 4 && (checksum_force || (o->flags & OR_FLAG_CHECKSUM))) {
+        if (!crc_ok(rec, L)) {
+            o->err = OR_ERROR_CHECKSUM;
+            o->flags |= OR_FLAG_CHECKSUM_ERROR;
+        }
+    }
+}
+
+uint32_t or_tcp_scan(const uint8_t* stream, uint64_t nbytes, int checksum_force,
+                     uint64_t* offs, uint32_t* lens, or_fields* f, uint32_t cap,
+                     uint64_t* consumed, int* status)
+{
+    uint64_t p = 0;
+    uint32_t n = 0;
+    if (status) *status = 0;
+    while (p + 2 <= nbytes) {
+        uint32_t L = get16(stream + p);
+        if (L < 4) { if (status) *status = 1; break; }
+        if (p + L > nbytes) break;
+        const uint8_t* rec = stream + p;
+        if (n < cap) {
+            or_tcp_recv(rec, L, checksum_force, &f[n]);
+            offs[n] = p;
+            lens[n] = L;
+        }
+        n++;
+        p += L;
+    }
+    if (consumed) *consumed = p;
+    return n;
+}
+
+/* MgenAppSinkTransport::OnInputReady (mgenAppSinkTransport.cpp:369-434): a length
+ * outside [MIN_SIZE, MAX_SIZE] discards the two length bytes and resynchronises. */
+uint32_t or_sink_scan(const uint8_t* stream, uint64_t nbytes, int checksum_force,
+                      uint64_t* offs, uint32_t* lens, or_fields* f, uint32_t cap,
+                      uint64_t* consumed)
+{
+    uint64_t p = 0;
+    uint32_t n = 0;
+    while (p + 2 <= nbytes) {
+        uint32_t L = get16(stream + p);
+        if (L < OR_MIN_SIZE || L > OR_MAX_SIZE) { p += 2; continue; }
+        if (p + L > nbytes) break;
+        if (n < cap) {
+            or_udp_recv(stream + p, L, checksum_force, &f[n]);
+            offs[n] = p;
+            lens[n] = L;
+        }
+        n++;
+        p += L;
+    }
+    if (consumed) *consumed = p;
+    return n;
+}
+
+/* ------------------------------------------------------------------ */
+/* MgenPayload::SetPayloadString (mgenPayload.cpp:24-55, :127-166)     */
+/* ------------------------------------------------------------------ */
+static uint8_t from_hex(char c)
+{
+    if (c >= '0' && c <= '9') return (uint8_t)(c - '0');
+    if (c >= 'a' && c <= 'f') return (uint8_t)(c - 'a' + 10);
+    if (c >= 'A' && c <= 'F') return (uint8_t)(c - 'A' + 10);
+    return 0;
+}
+
+uint32_t or_payload_from_hex(const char* hex, uint8_t* out, uint32_t cap)
+{
+    if (!hex) return 0;
+    size_t sl = strlen(hex);
+    uint32_t n = (uint32_t)(sl / 2 + sl % 2);
+    for (uint32_t i = 0; i < n && i < cap; i++) {
+        uint8_t hi = from_hex(hex[2 * i]);
+        uint8_t lo = (2 * i + 1 < sl) ? from_hex(hex[2 * i + 1]) : 0;  /* odd: reads NUL */
+        out[i] = (uint8_t)((hi << 4) | lo);
+    }
+    return n;
+}
+
+/* ------------------------------------------------------------------ */
+/* protolib restatements (UNPINNED: no reference fixture covers them)  */
+/* ProtoTime: struct timeval; Delta = sec diff + 1e-6 * usec diff.     */
+/* ProtoSlidingMask(num_bits, range 0xffffffff): a set of indices that */
+/* always spans fewer than num_bits; Set() of an index that would      */
+/* break the span fails; Difference() is the signed 32-bit difference. */
+/* ------------------------------------------------------------------ */
+double or_time_delta(or_time a, or_time b)
+{
+    return (double)(a.sec - b.sec) + 1.0e-06 * (double)(a.usec - b.usec);
+}
+
+static void time_add(or_time* t, double s)
+{
+    double whole = floor(s);
+    int64_t us = (int64_t)((s - whole) * 1.0e06 + 0.5);
+    t->sec += (int64_t)whole;
+    t->usec += us;
+    while (t->usec >= 1000000) { t->usec -= 1000000; t->sec += 1; }
+}
+
+static int time_ge(or_time a, or_time b)
+{
+    return (a.sec > b.sec) || (a.sec == b.sec && a.usec >= b.usec);
+}
+
+static int32_t mask_diff(uint32_t a, uint32_t b) { return (int32_t)(a - b); }
+
+static int mask_bit(const or_analytic* a, uint32_t i) { return (a->bits[i >> 3] >> (i & 7)) & 1; }
+static void mask_setbit(or_analytic* a, uint32_t i) { a->bits[i >> 3] |= (uint8_t)(1u << (i & 7)); }
+static void mask_clrbit(or_analytic* a, uint32_t i) { a->bits[i >> 3] &= (uint8_t)~(1u << (i & 7)); }
+
+static uint32_t mask_last(const or_analytic* a)
+{
+    for (int32_t i = (int32_t)a->depth - 1; i >= 0; i--)
+        if (mask_bit(a, (uint32_t)i)) return a->first + (uint32_t)i;
+    return a->first;
+}
+
+static int mask_test(const or_analytic* a, uint32_t idx)
+{
+    if (!a->nset) return 0;
+    int32_t d = mask_diff(idx, a->first);
+    if (d < 0 || (uint32_t)d >= a->depth) return 0;
+    return mask_bit(a, (uint32_t)d);
+}
+
+static void mask_clear(or_analytic* a)
+{
+    memset(a->bits, 0, sizeof(a->bits));
+    a->nset = 0;
+}
+
+static int mask_set(or_analytic* a, uint32_t idx)
+{
+    if (!a->nset) {
+        memset(a->bits, 0, sizeof(a->bits));
+        a->first = idx;
+        mask_setbit(a, 0);
+        a->nset = 1;
+        return 1;
+    }
+    int32_t d = mask_diff(idx, a->first);
+    if (d >= 0) {
+        if ((uint32_t)d >= a->depth) return 0;
+        if (!mask_bit(a, (uint32_t)d)) { mask_setbit(a, (uint32_t)d); a->nset++; }
+        return 1;
+    }
+    /* precedes first: allowed while the span stays < depth */
+    uint32_t last = mask_last(a);
+    uint32_t span = (uint32_t)mask_diff(last, idx);
+    if (span >= a->depth) return 0;
+    uint32_t shift = (uint32_t)(-d);
+    uint8_t nb[1024 / 8];
+    memset(nb, 0, sizeof(nb));
+    for (uint32_t i = 0; i + shift < a->depth; i++)
+        if (mask_bit(a, i)) nb[(i + shift) >> 3] |= (uint8_t)(1u << ((i + shift) & 7));
+    memcpy(a->bits, nb, sizeof(nb));
+    a->first = idx;
+    mask_setbit(a, 0);
+    a->nset++;
+    return 1;
+}
+
+static void mask_unset_bits(or_analytic* a, uint32_t idx, uint32_t count)
+{
+    if (!a->nset) return;
+    /* clear every set index x with idx <= x < idx + count (mod 2^32) */
+    for (uint32_t i = 0; i < a->depth; i++) {
+        if (!mask_bit(a, i)) continue;
+        if ((uint32_t)(a->first + i - idx) < count) {
+            mask_clrbit(a, i);
+            a->nset--;
+        }
+    }
+    if (!a->nset) { mask_clear(a); return; }
+    /* re-base on the new first set bit */
+    uint32_t s = 0;
+    while (!mask_bit(a, s)) s++;
+    if (s) {
+        uint8_t nb[1024 / 8];
+        memset(nb, 0, sizeof(nb));
+        for (uint32_t i = s; i < a->depth; i++)
+            if (mask_bit(a, i)) nb[(i - s) >> 3] |= (uint8_t)(1u << ((i - s) & 7));
+        memcpy(a->bits, nb, sizeof(nb));
+        a->first += s;
+    }
+}
+
+/* Report::QuantizeTimeValue / UnquantizeTimeValue (mgenAnalytic.cpp:621-642) */
+double or_quantized_window(double value)
+{
+    const double STRETCH = 1.1, TMIN = 1.0e-06, TMAX = 600.0;
+    const double SCALE = 1.0 / (pow(STRETCH, 254) - STRETCH);
+    unsigned q;
+    if (value > STRETCH * TMAX) q = 0xff;
+    else if (value < TMIN / 2.0) q = 0;
+    else if (value < TMIN) q = 1;
+    else q = (uint8_t)((log(STRETCH + (value - TMIN) / (SCALE * (TMAX - TMIN))) / log(STRETCH)) + 0.5);
+    if (q == 0) return 0.0;
+    return (TMAX - TMIN) * (pow(STRETCH, q) - STRETCH) * SCALE + TMIN;
+}
+
+/* MgenAnalytic::MgenAnalytic / Init (mgenAnalytic.cpp:8-71), DEFAULT_HISTORY 1024 */
+void or_analytic_init(or_analytic* a, double window)
+{
+    memset(a, 0, sizeof(*a));
+    a->depth = 1024;
+    a->window_size = or_quantized_window(window);
+}
+
+/* MgenAnalytic::Update (mgenAnalytic.cpp:74-258) */
+int or_analytic_update(or_analytic* a, or_time rx, uint32_t msgSize, or_time tx, uint32_t seq)
+{
+    if (!a->window_valid) {
+        a->window_valid = 1;
+        a->window_start = rx;
+        a->window_end = rx;
+        time_add(&a->window_end, a->window_size);
+        if (msgSize != 0) {
+            mask_set(a, seq);
+            a->seq_start = seq;
+            a->msg_count = 1;
+            a->byte_count = msgSize;
+            a->latency_sum = a->latency_min = a->latency_max = or_time_delta(rx, tx);
+        } else {
+            a->msg_count = a->byte_count = 0;
+            a->latency_sum = a->latency_min = a->latency_max = 0.0;
+        }
+        return 0;
+    }
+    double latency = 0.0;
+    if (msgSize != 0) {
+        if (a->nset) {
+            if (mask_test(a, seq)) {
+                a->dup_msg_count++;
+            } else if (mask_diff(seq, a->seq_start) < 0) {
+                mask_set(a, seq);
+            } else {
+                if (!mask_set(a, seq)) {
+                    uint32_t firstSet = a->first;
+                    uint32_t numBits = (uint32_t)mask_diff(seq, firstSet);
+                    mask_unset_bits(a, firstSet, numBits);
+                    mask_set(a, seq);
+                }
+                if (1 == a->msg_count)
+                    a->byte_count = msgSize;
+                else
+                    a->byte_count += msgSize;
+                latency = or_time_delta(rx, tx);
+                if (0 == a->msg_count) {
+                    a->latency_sum = a->latency_min = a->latency_max = latency;
+                } else {
+                    a->latency_sum += latency;
+                    if (latency < a->latency_min)
+                        a->latency_min = latency;
+                    else if (latency > a->latency_max)
+                        a->latency_max = latency;
+                }
+                a->msg_count++;
+            }
+        } else {
+            mask_clear(a);
+            mask_set(a, seq);
+            a->seq_start = seq;
+            a->byte_count = msgSize;
+            a->latency_sum = a->latency_min = a->latency_max = or_time_delta(rx, tx);
+            a->msg_count = 1;
+        }
+    }
+    if (time_ge(rx, a->window_end)) {
+        a->report_valid = 1;
+        a->n_reports++;
+        a->report_start = a->window_start;
+        a->report_duration = or_time_delta(rx, a->window_start);
+        uint32_t seqMax = a->nset ? mask_last(a) : a->seq_start;
+        switch (a->msg_count) {
+            case 0:
+                a->report_msg_count = 0;
+                a->report_rate_ave = 0.0;
+                a->report_loss_ave = 1.0;
+                a->report_latency_ave = a->report_latency_min = a->report_latency_max = -1.0;
+                break;
+            case 1:
+                a->report_msg_count = 1;
+                a->report_rate_ave = (double)a->byte_count / a->report_duration;
+                a->report_loss_ave = 0.0;
+                a->report_latency_ave = a->latency_sum;
+                a->report_latency_min = a->latency_min;
+                a->report_latency_max = a->latency_max;
+                break;
+            default: {
+                a->report_msg_count = a->msg_count - 1;
+                a->report_rate_ave = (double)a->byte_count / a->report_duration;
+                uint32_t seqDelta = seqMax - a->seq_start;
+                if (seqDelta <= 1)
+                    a->report_loss_ave = 0.0;
+                else
+                    a->report_loss_ave = 1.0 - (double)a->msg_count / (double)(seqDelta + 1);
+                a->report_latency_ave = a->latency_sum / (double)a->msg_count;
+                a->report_latency_min = a->latency_min;
+                a->report_latency_max = a->latency_max;
+                break;
+            }
+        }
+        a->window_start = rx;
+        a->window_end = rx;
+        time_add(&a->window_end, a->window_size);
+        a->seq_start = seqMax;
+        if (msgSize != 0) {
+            a->byte_count = 0;
+            a->msg_count = 1;
+            a->latency_sum = a->latency_min = a->latency_max = latency;
+        } else {
+            a->byte_count = a->msg_count = 0;
+            a->latency_sum = a->latency_min = a->latency_max = 0.0;
+        }
+        return 1;
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* Batch layer                                                         */
+/* ------------------------------------------------------------------ */
+#include <pthread.h>
+
+/* A double d with (UINT32)((d + 180.0) * 60000.0) == raw, so Pack's own conversion
+ * (mgenMsg.cpp:221,225) reproduces the template's raw word exactly. */
+static double raw_to_deg(uint32_t raw)
+{
+    double d = (double)raw / 60000.0 - 180.0;
+    for (int k = 0; k < 64 && (uint32_t)((d + 180.0) * 60000.0) < raw; k++) d = nextafter(d, 1e300);
+    for (int k = 0; k < 64 && (uint32_t)((d + 180.0) * 60000.0) > raw; k++) d = nextafter(d, -1e300);
+    return d;
+}
+
+static void tmpl_to_msg(const or_tmpl* t, const or_desc* d, const uint8_t* pool, or_msg* m)
+{
+    memset(m, 0, sizeof(*m));
+    m->msg_len = d->msg_len;
+    m->mgen_msg_len = d->msg_len;
+    m->version = OR_VERSION;
+    m->flags = d->flags;
+    m->flow_id = t->flow_id;
+    m->seq_num = d->seq_num;
+    m->tx_sec = d->tx_sec;
+    m->tx_usec = d->tx_usec;
+    m->dst.type = t->dst_type; m->dst.len = t->dst_len; m->dst.port = t->dst_port;
+    memcpy(m->dst.addr, t->dst_addr, 16);
+    m->host.type = t->host_type; m->host.len = t->host_len; m->host.port = t->host_port;
+    memcpy(m->host.addr, t->host_addr, 16);
+    /* the template carries the already-converted raw words; invert exactly:
+     * raw/60000 - 180 reproduces the same (UINT32)((x+180)*60000) for raw < 2^32 */
+    m->latitude = raw_to_deg(t->lat_raw);
+    m->longitude = raw_to_deg(t->lon_raw);
+    m->altitude = t->alt;
+    m->gps_status = t->gps_status;
+    m->payload_type = t->payload_type;
+    m->payload_len = t->payload_len;
+    m->payload_data = t->has_payload ? pool + t->payload_off : NULL;
+}
+
+void or_udp_pack_batch(const or_tmpl* tmpl, const or_desc* desc, uint32_t n,
+                       const uint8_t* pool, uint8_t* slab, const uint64_t* rec_off,
+                       uint64_t stride, int checksum_enable, int random_fill, uint32_t fill_time,
+                       uint32_t* out_len)
+{
+    for (uint32_t i = 0; i < n; i++) {
+        or_msg m;
+        tmpl_to_msg(&tmpl[desc[i].tmpl], &desc[i], pool, &m);
+        uint64_t off = rec_off ? rec_off[i] : (uint64_t)i * stride;
+        /* Pack works in the transport's scratch txBuffer (mgenTransport.cpp:1023); a failed
+         * Pack (return 0) is never sent, so its slot in the batch slab stays untouched. */
+        static uint8_t scratch[65536 + 512];
+        out_len[i] = or_udp_pack(&m, scratch, checksum_enable, random_fill, fill_time);
+        if (out_len[i]) memcpy(slab + off, scratch, out_len[i]);
+    }
+}
+
+typedef struct {
+    const uint8_t* slab; const uint64_t* rec_off; uint64_t stride;
+    const uint32_t* rec_len; uint32_t fixed_len; uint32_t lo, hi; int force; or_fields* out;
+} recv_job;
+
+static void* recv_worker(void* p)
+{
+    recv_job* j = (recv_job*)p;
+    for (uint32_t i = j->lo; i < j->hi; i++) {
+        uint64_t off = j->rec_off ? j->rec_off[i] : (uint64_t)i * j->stride;
+        uint32_t len = j->rec_len ? j->rec_len[i] : j->fixed_len;
+        if (j->force & 2)
+            or_tcp_recv(j->slab + off, len, j->force & 1, &j->out[i]);
+        else
+            or_udp_recv(j->slab + off, len, j->force & 1, &j->out[i]);
+    }
+    return NULL;
+}
+
+void or_udp_recv_batch(const uint8_t* slab, const uint64_t* rec_off, uint64_t stride,
+                       const uint32_t* rec_len, uint32_t fixed_len, uint32_t n,
+                       int checksum_force, or_fields* out, int nthreads)
+{
+    (void)table();
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    recv_job jobs[256];
+    pthread_t th[256];
+    for (int t = 0; t < nthreads; t++) {
+        jobs[t].slab = slab; jobs[t].rec_off = rec_off; jobs[t].stride = stride;
+        jobs[t].rec_len = rec_len; jobs[t].fixed_len = fixed_len;
+        jobs[t].lo = (uint32_t)((uint64_t)n * t / nthreads);
+        jobs[t].hi = (uint32_t)((uint64_t)n * (t + 1) / nthreads);
+        jobs[t].force = checksum_force; jobs[t].out = out;
+    }
+    if (nthreads == 1) { recv_worker(&jobs[0]); return; }
+    for (int t = 0; t < nthreads; t++) pthread_create(&th[t], NULL, recv_worker, &jobs[t]);
+    for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+}
+
+uint64_t or_tcp_tx_batch(const or_tmpl* tmpl, const or_desc* desc, const uint32_t* msg_total,
+                         uint32_t n, const uint8_t* pool, uint8_t* stream,
+                         int checksum_enable, int random_fill, uint32_t fill_time)
+{
+    uint64_t p = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        or_msg m;
+        tmpl_to_msg(&tmpl[desc[i].tmpl], &desc[i], pool, &m);
+        m.mgen_msg_len = msg_total[i];
+        m.msg_len = (uint16_t)(msg_total[i] > 65535 ? 65535 : msg_total[i]);
+        p += or_tcp_tx(&m, stream + p, checksum_enable, random_fill, fill_time);
+    }
+    return p;
+}
+
+/* layout check for the Python/ctypes mirrors */
+uint32_t or_sizeof(int which)
+{
+    switch (which) {
+        case 0: return (uint32_t)sizeof(or_tmpl);
+        case 1: return (uint32_t)sizeof(or_desc);
+        case 2: return (uint32_t)sizeof(or_fields);
+        case 3: return (uint32_t)sizeof(or_analytic);
+        default: return 0;
+    }
+}

@@ -1,0 +1,326 @@
+"""TEST INFRASTRUCTURE ONLY -- ctypes front end of the C restatement (mgen_oracle.c).
+
+This module is the parity CHECKER.  Only tests/, ``__graft_entry__.smoke()`` and
+bench.py's ``cpu_baseline`` leg may import it; the product (``mgen_amd`` and
+libmgenx.so) never does.  Parity status: see mgen_oracle.h / DESIGN.md.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
+
+# ---- numpy mirrors of the C structs (aligned like the C compiler lays them out) ----
+TMPL_DTYPE = np.dtype([
+    ("flow_id", "<u4"),
+    ("dst_type", "u1"), ("dst_len", "u1"), ("dst_port", "<u2"),
+    ("dst_addr", "u1", 16),
+    ("host_type", "u1"), ("host_len", "u1"), ("host_port", "<u2"),
+    ("host_addr", "u1", 16),
+    ("lat_raw", "<u4"), ("lon_raw", "<u4"), ("alt", "<i4"),
+    ("gps_status", "u1"), ("payload_type", "u1"), ("payload_len", "<u2"),
+    ("payload_off", "<u4"),
+    ("has_payload", "u1"), ("rsv0", "u1"), ("rsv1", "<u2"),
+], align=True)
+
+DESC_DTYPE = np.dtype([
+    ("tmpl", "<u4"), ("seq_num", "<u4"), ("tx_sec", "<u4"), ("tx_usec", "<u4"),
+    ("msg_len", "<u2"), ("flags", "u1"), ("rsv", "u1"),
+], align=True)
+
+FIELDS_DTYPE = np.dtype([
+    ("ok", "u1"), ("err", "u1"), ("version", "u1"), ("flags", "u1"),
+    ("msg_len", "<u2"), ("hdr_len", "<u2"),
+    ("flow_id", "<u4"), ("seq_num", "<u4"), ("tx_sec", "<u4"), ("tx_usec", "<u4"),
+    ("dst_port", "<u2"), ("dst_type", "u1"), ("dst_len", "u1"), ("dst_addr", "u1", 16),
+    ("host_port", "<u2"), ("host_type", "u1"), ("host_len", "u1"), ("host_addr", "u1", 16),
+    ("lat_raw", "<u4"), ("lon_raw", "<u4"), ("alt", "<i4"),
+    ("gps_status", "u1"), ("payload_type", "u1"), ("payload_len", "<u2"),
+    ("payload_off", "<u4"),
+], align=True)
+
+
+class _Addr(ctypes.Structure):
+    _fields_ = [("type", ctypes.c_uint8), ("len", ctypes.c_uint8), ("port", ctypes.c_uint16),
+                ("addr", ctypes.c_uint8 * 16)]
+
+
+class Msg(ctypes.Structure):
+    """or_msg: the MgenMsg members Pack() serialises."""
+    _fields_ = [("msg_len", ctypes.c_uint16), ("mgen_msg_len", ctypes.c_uint32),
+                ("version", ctypes.c_uint8), ("flags", ctypes.c_uint8),
+                ("flow_id", ctypes.c_uint32), ("seq_num", ctypes.c_uint32),
+                ("tx_sec", ctypes.c_uint32), ("tx_usec", ctypes.c_uint32),
+                ("dst", _Addr), ("host", _Addr),
+                ("latitude", ctypes.c_double), ("longitude", ctypes.c_double),
+                ("altitude", ctypes.c_int32), ("gps_status", ctypes.c_uint8),
+                ("payload_type", ctypes.c_uint8), ("payload_len", ctypes.c_uint16),
+                ("payload_data", ctypes.c_void_p)]
+
+
+class Time(ctypes.Structure):
+    _fields_ = [("sec", ctypes.c_int64), ("usec", ctypes.c_int64)]
+
+
+class Analytic(ctypes.Structure):
+    _fields_ = [("depth", ctypes.c_uint32), ("first", ctypes.c_uint32), ("nset", ctypes.c_uint32),
+                ("bits", ctypes.c_uint8 * 128),
+                ("window_size", ctypes.c_double), ("window_valid", ctypes.c_int),
+                ("window_start", Time), ("window_end", Time), ("seq_start", ctypes.c_uint32),
+                ("msg_count", ctypes.c_uint64), ("byte_count", ctypes.c_uint64),
+                ("dup_msg_count", ctypes.c_uint64),
+                ("latency_sum", ctypes.c_double), ("latency_min", ctypes.c_double),
+                ("latency_max", ctypes.c_double),
+                ("report_valid", ctypes.c_int), ("n_reports", ctypes.c_uint64),
+                ("report_start", Time), ("report_duration", ctypes.c_double),
+                ("report_msg_count", ctypes.c_uint64),
+                ("report_rate_ave", ctypes.c_double), ("report_loss_ave", ctypes.c_double),
+                ("report_latency_ave", ctypes.c_double), ("report_latency_min", ctypes.c_double),
+                ("report_latency_max", ctypes.c_double)]
+
+
+_lib = None
+
+
+def build():
+    """Compile the restatement (gcc) into oracle/build/liboracle.so."""
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        P = ctypes.c_void_p
+        u32, u64, i32 = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+        L.or_crc32_update.argtypes = [ctypes.POINTER(u32), P, u32]
+        L.or_crc32_table.argtypes = [P]
+        L.or_glibc_rand_bytes.argtypes = [u32, u32, P]
+        L.or_pack.argtypes = [ctypes.POINTER(Msg), P, ctypes.c_uint16, i32, ctypes.POINTER(u32),
+                              i32, u32, ctypes.POINTER(ctypes.c_uint16)]
+        L.or_pack.restype = ctypes.c_uint16
+        L.or_udp_pack.argtypes = [ctypes.POINTER(Msg), P, i32, i32, u32]
+        L.or_udp_pack.restype = u32
+        L.or_tcp_tx.argtypes = [ctypes.POINTER(Msg), P, i32, i32, u32]
+        L.or_tcp_tx.restype = u32
+        L.or_unpack.argtypes = [P, u32, P]
+        L.or_udp_recv.argtypes = [P, u32, i32, P]
+        L.or_tcp_recv.argtypes = [P, u32, i32, P]
+        L.or_tcp_scan.argtypes = [P, u64, i32, P, P, P, u32, ctypes.POINTER(u64),
+                                  ctypes.POINTER(i32)]
+        L.or_tcp_scan.restype = u32
+        L.or_sink_scan.argtypes = [P, u64, i32, P, P, P, u32, ctypes.POINTER(u64)]
+        L.or_sink_scan.restype = u32
+        L.or_payload_from_hex.argtypes = [ctypes.c_char_p, P, u32]
+        L.or_payload_from_hex.restype = u32
+        L.or_udp_pack_batch.argtypes = [P, P, u32, P, P, P, u64, i32, i32, u32, P]
+        L.or_udp_recv_batch.argtypes = [P, P, u64, P, u32, u32, i32, P, i32]
+        L.or_tcp_tx_batch.argtypes = [P, P, P, u32, P, P, i32, i32, u32]
+        L.or_tcp_tx_batch.restype = u64
+        L.or_quantized_window.argtypes = [ctypes.c_double]
+        L.or_quantized_window.restype = ctypes.c_double
+        L.or_analytic_init.argtypes = [ctypes.POINTER(Analytic), ctypes.c_double]
+        L.or_analytic_update.argtypes = [ctypes.POINTER(Analytic), Time, u32, Time, u32]
+        L.or_analytic_update.restype = i32
+        L.or_time_delta.argtypes = [Time, Time]
+        L.or_time_delta.restype = ctypes.c_double
+        L.or_sizeof.argtypes = [i32]
+        L.or_sizeof.restype = u32
+        assert L.or_sizeof(0) == TMPL_DTYPE.itemsize, "or_tmpl layout mismatch"
+        assert L.or_sizeof(1) == DESC_DTYPE.itemsize, "or_desc layout mismatch"
+        assert L.or_sizeof(2) == FIELDS_DTYPE.itemsize, "or_fields layout mismatch"
+        assert L.or_sizeof(3) == ctypes.sizeof(Analytic), "or_analytic layout mismatch"
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+# ---------------------------------------------------------------- CRC
+def crc_table():
+    t = np.zeros(256, np.uint32)
+    lib().or_crc32_table(_ptr(t))
+    return t
+
+
+def crc32_update(state: int, data: bytes) -> int:
+    """MgenMsg::ComputeCRC32 (incremental, reset-on-zero)."""
+    c = ctypes.c_uint32(state)
+    buf = np.frombuffer(bytes(data), np.uint8)
+    lib().or_crc32_update(ctypes.byref(c), _ptr(buf) if len(buf) else None, len(buf))
+    return c.value
+
+
+def glibc_rand_bytes(seed: int, n: int) -> bytes:
+    out = np.zeros(max(n, 1), np.uint8)
+    lib().or_glibc_rand_bytes(seed, n, _ptr(out))
+    return out[:n].tobytes()
+
+
+# ---------------------------------------------------------------- messages
+def make_msg(*, msg_len, flow_id=1, seq=0, tx_sec=0, tx_usec=0, flags=0, version=2,
+             dst=("4", bytes([127, 0, 0, 1]), 5000), host=None, lat=999.0, lon=999.0, alt=-999,
+             gps_status=0, payload_type=0, payload=None, payload_len=None, mgen_msg_len=None):
+    """Build an or_msg the way MgenFlow::SendMessage does (mgenFlow.cpp:946-983)."""
+    m = Msg()
+    keep = []
+    m.msg_len = msg_len & 0xFFFF
+    m.mgen_msg_len = msg_len if mgen_msg_len is None else mgen_msg_len
+    m.version = version
+    m.flags = flags
+    m.flow_id, m.seq_num, m.tx_sec, m.tx_usec = flow_id, seq, tx_sec, tx_usec
+
+    def fill(a, spec):
+        if spec is None:
+            a.type = 0
+            return
+        kind, raw, port = spec
+        a.type = {"4": 1, "6": 2, "x": 7}[kind]
+        a.len = len(raw)
+        a.port = port
+        for i, b in enumerate(raw[:16]):
+            a.addr[i] = b
+    fill(m.dst, dst)
+    fill(m.host, host)
+    m.latitude, m.longitude, m.altitude, m.gps_status = lat, lon, alt, gps_status
+    m.payload_type = payload_type
+    if payload is not None:
+        pb = ctypes.create_string_buffer(bytes(payload), max(len(payload), 1))
+        keep.append(pb)
+        m.payload_data = ctypes.cast(pb, ctypes.c_void_p)
+        m.payload_len = len(payload) if payload_len is None else payload_len
+    else:
+        m.payload_data = None
+        m.payload_len = payload_len or 0
+    m._keep = keep
+    return m
+
+
+def udp_pack(m: Msg, checksum=True, random_fill=False, fill_time=0) -> bytes:
+    cap = max(m.msg_len, 64) + 64
+    out = np.zeros(cap, np.uint8)
+    n = lib().or_udp_pack(ctypes.byref(m), _ptr(out), int(checksum), int(random_fill), fill_time)
+    return out[:n].tobytes()
+
+
+def pack(m: Msg, buffer_len, checksum=False, tx_checksum=0, random_fill=False, fill_time=0):
+    """Raw MgenMsg::Pack; returns (ret, bytes[:buffer_len], tx_checksum, flags, hdr_len)."""
+    out = np.zeros(max(buffer_len, 64) + 64, np.uint8)
+    ck = ctypes.c_uint32(tx_checksum)
+    hl = ctypes.c_uint16(0)
+    r = lib().or_pack(ctypes.byref(m), _ptr(out), buffer_len, int(checksum), ctypes.byref(ck),
+                      int(random_fill), fill_time, ctypes.byref(hl))
+    return r, out[:buffer_len].tobytes(), ck.value, m.flags, hl.value
+
+
+def tcp_tx(m: Msg, checksum=True, random_fill=False, fill_time=0) -> bytes:
+    out = np.zeros(m.mgen_msg_len + 16, np.uint8)
+    n = lib().or_tcp_tx(ctypes.byref(m), _ptr(out), int(checksum), int(random_fill), fill_time)
+    return out[:n].tobytes()
+
+
+def _fields_one(fn, rec, *args):
+    buf = np.frombuffer(bytes(rec), np.uint8).copy() if len(rec) else np.zeros(1, np.uint8)
+    f = np.zeros(1, FIELDS_DTYPE)
+    fn(_ptr(buf), len(rec), *args, _ptr(f))
+    return f[0]
+
+
+def unpack(rec: bytes):
+    return _fields_one(lib().or_unpack, rec)
+
+
+def udp_recv(rec: bytes, force=False):
+    return _fields_one(lib().or_udp_recv, rec, int(force))
+
+
+def _scan(fn, stream, force, extra_status):
+    buf = np.frombuffer(bytes(stream), np.uint8).copy() if len(stream) else np.zeros(1, np.uint8)
+    cap = len(stream) // 2 + 1
+    offs = np.zeros(cap, np.uint64)
+    lens = np.zeros(cap, np.uint32)
+    f = np.zeros(cap, FIELDS_DTYPE)
+    consumed = ctypes.c_uint64(0)
+    if extra_status:
+        st = ctypes.c_int(0)
+        n = fn(_ptr(buf), len(stream), int(force), _ptr(offs), _ptr(lens), _ptr(f), cap,
+               ctypes.byref(consumed), ctypes.byref(st))
+        return offs[:n], lens[:n], f[:n], consumed.value, st.value
+    n = fn(_ptr(buf), len(stream), int(force), _ptr(offs), _ptr(lens), _ptr(f), cap,
+           ctypes.byref(consumed))
+    return offs[:n], lens[:n], f[:n], consumed.value
+
+
+def tcp_scan(stream: bytes, force=False):
+    return _scan(lib().or_tcp_scan, stream, force, True)
+
+
+def sink_scan(stream: bytes, force=False):
+    return _scan(lib().or_sink_scan, stream, force, False)
+
+
+def payload_from_hex(hexstr: str) -> bytes:
+    out = np.zeros(len(hexstr) // 2 + 2, np.uint8)
+    n = lib().or_payload_from_hex(hexstr.encode(), _ptr(out), len(out))
+    return out[:n].tobytes()
+
+
+# ---------------------------------------------------------------- batches
+def udp_pack_batch(tmpl, desc, pool, slab_bytes, rec_off=None, stride=0, checksum=True,
+                   random_fill=False, fill_time=0):
+    n = len(desc)
+    slab = np.zeros(slab_bytes, np.uint8)
+    lens = np.zeros(n, np.uint32)
+    pool = np.ascontiguousarray(pool if pool is not None and len(pool) else np.zeros(1, np.uint8))
+    lib().or_udp_pack_batch(_ptr(tmpl), _ptr(desc), n, _ptr(pool), _ptr(slab),
+                            _ptr(rec_off), stride, int(checksum), int(random_fill), fill_time,
+                            _ptr(lens))
+    return slab, lens
+
+
+def udp_recv_batch(slab, n, rec_off=None, stride=0, rec_len=None, fixed_len=0, force=False,
+                   nthreads=1, tcp=False):
+    out = np.zeros(n, FIELDS_DTYPE)
+    lib().or_udp_recv_batch(_ptr(slab), _ptr(rec_off), stride, _ptr(rec_len), fixed_len, n,
+                            int(force) | (2 if tcp else 0), _ptr(out), nthreads)
+    return out
+
+
+def tcp_recv(rec: bytes, force=False):
+    return _fields_one(lib().or_tcp_recv, rec, int(force))
+
+
+def tcp_tx_batch(tmpl, desc, msg_total, pool, checksum=True, random_fill=False, fill_time=0):
+    total = int(np.asarray(msg_total, np.uint64).sum())
+    stream = np.zeros(total + 16, np.uint8)
+    pool = np.ascontiguousarray(pool if pool is not None and len(pool) else np.zeros(1, np.uint8))
+    mt = np.ascontiguousarray(msg_total, np.uint32)
+    n = lib().or_tcp_tx_batch(_ptr(tmpl), _ptr(desc), _ptr(mt), len(desc), _ptr(pool),
+                              _ptr(stream), int(checksum), int(random_fill), fill_time)
+    return stream[:n]
+
+
+# ---------------------------------------------------------------- analytics
+def quantized_window(w=1.0):
+    return lib().or_quantized_window(w)
+
+
+class AnalyticOracle:
+    """MgenAnalytic restated (parity unpinned at the protolib boundary)."""
+
+    def __init__(self, window=1.0):
+        self.a = Analytic()
+        lib().or_analytic_init(ctypes.byref(self.a), window)
+
+    def update(self, rx_sec, rx_usec, msg_size, tx_sec, tx_usec, seq):
+        return bool(lib().or_analytic_update(ctypes.byref(self.a), Time(rx_sec, rx_usec),
+                                             msg_size, Time(tx_sec, tx_usec), seq))

@@ -1,0 +1,216 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle's golden vectors, plus
+size-independent properties at BASELINE.json's full sizes.  Bit-exact everywhere."""
+import os
+import zlib
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden", "udp_matrix.npz")
+
+# GPU column -> (oracle field, numpy view dtype)
+COLMAP = [
+    ("flow_id", "flow_id", np.uint32), ("seq_num", "seq_num", np.uint32),
+    ("tx_sec", "tx_sec", np.uint32), ("tx_usec", "tx_usec", np.uint32),
+    ("msg_len", "msg_len", np.uint16), ("dst_port", "dst_port", np.uint16),
+    ("flags", "flags", np.uint8), ("err", "err", np.uint8), ("dst_type", "dst_type", np.uint8),
+    ("dst_len", "dst_len", np.uint8), ("payload_len", "payload_len", np.uint16),
+    ("payload_type", "payload_type", np.uint8), ("gps_status", "gps_status", np.uint8),
+    ("hdr_len", "hdr_len", np.uint16), ("payload_off", "payload_off", np.uint32),
+    ("host_port", "host_port", np.uint16), ("host_type", "host_type", np.uint8),
+    ("host_len", "host_len", np.uint8), ("lat_raw", "lat_raw", np.uint32),
+    ("lon_raw", "lon_raw", np.uint32), ("alt", "alt", np.int32),
+]
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    return torch
+
+
+@pytest.fixture(scope="module")
+def eng(torch):
+    from mgen_amd import Engine
+    e = Engine(0)
+    yield e
+    e.close()
+
+
+@pytest.fixture(scope="module")
+def gold():
+    return dict(np.load(GOLD, allow_pickle=False))
+
+
+def dev(torch, a):
+    from mgen_amd import to_device
+    return to_device(np.asarray(a))
+
+
+def host_cols(cols, n):
+    out = {}
+    for name, t in cols.items():
+        a = t.cpu().numpy()
+        out[name] = a
+    return out
+
+
+def compare_cols(cols, f, n, what):
+    c = host_cols(cols, n)
+    for gname, oname, dt in COLMAP:
+        got = c[gname].view(dt)[:n]
+        want = f[oname].astype(dt)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, (what, gname, bad[:10], got[bad[:5]], want[bad[:5]])
+    got4 = c["dst_addr4"].view(np.uint8).reshape(-1, 4)[:n]
+    assert np.array_equal(got4, f["dst_addr"][:, :4]), (what, "dst_addr4")
+    assert np.array_equal(c["dst_addr"].reshape(-1, 16)[:n], f["dst_addr"]), (what, "dst_addr")
+    assert np.array_equal(c["host_addr"].reshape(-1, 16)[:n], f["host_addr"]), (what, "host_addr")
+
+
+def test_unpack_matrix_all_receive_rules(torch, eng, gold):
+    from mgen_amd import OPT_CHECKSUM_FORCE, OPT_TCP
+    n = len(gold["unpack_lens"])
+    slab = dev(torch, gold["unpack_slab"]).view(torch.uint8)
+    offs = dev(torch, gold["unpack_offs"]).view(torch.int64)
+    lens = dev(torch, gold["unpack_lens"]).view(torch.int32)
+    for mode, opts in (("udp", 0), ("udp_force", OPT_CHECKSUM_FORCE),
+                       ("tcp_force", OPT_TCP | OPT_CHECKSUM_FORCE)):
+        cols = eng.unpack(slab, n, rec_off=offs, rec_len=lens, opts=opts, ext=True)
+        torch.cuda.synchronize()
+        compare_cols(cols, gold[f"unpack_fields_{mode}"], n, mode)
+
+
+def test_unpack_core_only_matches_ext(torch, eng, gold):
+    """Core-column path (no extended pointers) decodes the same as the full path."""
+    n = len(gold["unpack_lens"])
+    slab = dev(torch, gold["unpack_slab"]).view(torch.uint8)
+    offs = dev(torch, gold["unpack_offs"]).view(torch.int64)
+    lens = dev(torch, gold["unpack_lens"]).view(torch.int32)
+    a = host_cols(eng.unpack(slab, n, rec_off=offs, rec_len=lens, ext=False), n)
+    f = gold["unpack_fields_udp"]
+    for gname, oname, dt in COLMAP[:13]:
+        assert np.array_equal(a[gname].view(dt)[:n], f[oname].astype(dt)), gname
+    assert np.array_equal(a["dst_addr4"].view(np.uint8).reshape(-1, 4), f["dst_addr"][:, :4])
+
+
+@pytest.mark.parametrize("ck,rf", [(0, 0), (1, 0), (0, 1), (1, 1)])
+def test_pack_matrix(torch, eng, gold, ck, rf):
+    from mgen_amd import PACK_CHECKSUM, PACK_RANDOM_FILL
+    desc, tmpl = gold["desc"], gold["tmpl"]
+    n = len(desc)
+    d_tmpl = dev(torch, tmpl)
+    d_pool = dev(torch, gold["pool"])
+    d_desc = dev(torch, desc)
+    d_offs = dev(torch, gold["offs"]).view(torch.int64)
+    crc = torch.empty(len(tmpl), dtype=torch.int32, device="cuda")
+    eng.pack_prepare(d_tmpl, len(tmpl), d_pool, crc)
+    ft = int(gold["fill_time"][0])
+    if rf:
+        eng.set_fill_time(ft)
+    slab = torch.zeros(int(gold["slab_bytes"][0]), dtype=torch.uint8, device="cuda")
+    opts = (PACK_CHECKSUM if ck else 0) | (PACK_RANDOM_FILL if rf else 0)
+    out_len = eng.pack(d_tmpl, crc, d_desc, n, d_pool, slab, rec_off=d_offs, opts=opts,
+                       fill_time=ft)
+    torch.cuda.synchronize()
+    want = gold[f"pack_slab_ck{ck}_rf{rf}"]
+    got = slab.cpu().numpy()
+    lens = out_len.cpu().numpy().view(np.uint32)
+    assert np.array_equal(lens, gold[f"pack_lens_ck{ck}_rf{rf}"])
+    bad = np.nonzero(got != want)[0]
+    if bad.size:
+        offs = gold["offs"]
+        rec = np.searchsorted(offs, bad[0], side="right") - 1
+        pytest.fail(f"pack mismatch ck={ck} rf={rf}: {bad.size} bytes, first at {bad[0]} "
+                    f"(record {rec}, size {desc['msg_len'][rec]}, tmpl {desc['tmpl'][rec]}, "
+                    f"pos {bad[0] - offs[rec]})")
+
+
+def _config2(torch, eng, n, size=1024):
+    from mgen_amd import PACK_CHECKSUM
+    from mgen_amd.workloads import udp_fixed
+    tmpl, pool, desc = udp_fixed(n, size)
+    d_tmpl, d_pool, d_desc = dev(torch, tmpl), dev(torch, pool), dev(torch, desc)
+    crc = torch.empty(len(tmpl), dtype=torch.int32, device="cuda")
+    eng.pack_prepare(d_tmpl, len(tmpl), d_pool, crc)
+    slab = torch.empty(n * size, dtype=torch.uint8, device="cuda")
+    out_len = eng.pack(d_tmpl, crc, d_desc, n, d_pool, slab, stride=size, opts=PACK_CHECKSUM)
+    return desc, slab, out_len
+
+
+def test_config2_full_size_roundtrip(torch, eng):
+    """1M x 1024-B UDP records: pack -> unpack recovers every descriptor; flipping one bit
+    in sampled records is caught as ERROR_CHECKSUM exactly there (size-independent)."""
+    n, size = 1 << 20, 1024
+    desc, slab, out_len = _config2(torch, eng, n, size)
+    assert int((out_len != size).sum()) == 0
+    cols = eng.unpack(slab, n, stride=size, fixed_len=size)
+    c = host_cols(cols, n)
+    assert int(c["err"].astype(np.int64).sum()) == 0
+    assert np.array_equal(c["seq_num"].view(np.uint32), desc["seq_num"])
+    assert np.array_equal(c["flow_id"].view(np.uint32), desc["tmpl"] + 1)
+    assert np.array_equal(c["tx_sec"].view(np.uint32), desc["tx_sec"])
+    assert np.array_equal(c["tx_usec"].view(np.uint32), desc["tx_usec"])
+    assert np.all(c["flags"] == 0x0C) and np.all(c["msg_len"].view(np.uint16) == size)
+    # spot-check bytes against zlib for a few records
+    host = slab[: 8 * size].cpu().numpy()
+    for i in range(8):
+        r = host[i * size:(i + 1) * size].tobytes()
+        assert int.from_bytes(r[-4:], "big") == zlib.crc32(r[:-4])
+    # corruption property
+    rng = np.random.default_rng(7)
+    victims = np.unique(rng.integers(0, n, 4096))
+    pos = rng.integers(0, size, victims.size)
+    bits = rng.integers(0, 8, victims.size)
+    idx = torch.from_numpy((victims * size + pos).astype(np.int64)).cuda()
+    flip = torch.from_numpy((1 << bits).astype(np.uint8)).cuda()
+    slab[idx] ^= flip
+    cols = eng.unpack(slab, n, stride=size, fixed_len=size)
+    c = host_cols(cols, n)
+    err = c["err"]
+    # a flip in the version byte / dst type turns into that error instead
+    # clearing the CHECKSUM flag bit (byte 3, bit 2) disables the check (mgenTransport.cpp:960)
+    unchecked = (pos == 3) & (bits == 2)
+    expect_bad = set(victims[~unchecked].tolist())
+    assert set(np.nonzero(err != 0)[0].tolist()) == expect_bad
+    assert np.all(err[victims[pos == 2]] == 1)          # version byte
+    assert np.all(err[victims[pos == 22]] == 4)         # dst type byte
+    crc_class = (pos != 2) & (pos != 22) & ~unchecked
+    assert np.all(err[victims[crc_class]] == 2)
+
+
+def test_unpack_stride_matches_offsets(torch, eng):
+    """Fixed-stride addressing == explicit offsets (same records)."""
+    n, size = 4096, 256
+    desc, slab, _ = _config2(torch, eng, n, size)
+    a = host_cols(eng.unpack(slab, n, stride=size, fixed_len=size), n)
+    offs = torch.arange(n, dtype=torch.int64, device="cuda") * size
+    lens = torch.full((n,), size, dtype=torch.int32, device="cuda")
+    b = host_cols(eng.unpack(slab, n, rec_off=offs, rec_len=lens), n)
+    for k in a:
+        assert np.array_equal(a[k], b[k]), k
+
+
+def test_crc32_batch_vs_zlib(torch, eng):
+    rng = np.random.default_rng(3)
+    data = rng.integers(0, 256, 100000, dtype=np.uint8)
+    lens = rng.integers(0, 3000, 64).astype(np.uint32)
+    offs = rng.integers(0, 100000 - 3000, 64).astype(np.uint64)
+    out = eng.crc32(dev(torch, data), dev(torch, offs).view(torch.int64),
+                    dev(torch, lens).view(torch.int32), 64)
+    got = out.cpu().numpy().view(np.uint32)
+    for i in range(64):
+        assert got[i] == zlib.crc32(data[offs[i]:offs[i] + lens[i]].tobytes())
+
+
+def test_oob_records_are_flagged_not_read(torch, eng):
+    from mgen_amd import ERROR_OOB
+    slab = torch.zeros(4096, dtype=torch.uint8, device="cuda")
+    offs = torch.tensor([0, 4000, 5000], dtype=torch.int64, device="cuda")
+    lens = torch.tensor([64, 200, 10], dtype=torch.int32, device="cuda")
+    c = host_cols(eng.unpack(slab, 3, rec_off=offs, rec_len=lens), 3)
+    assert c["err"].tolist() == [1, ERROR_OOB, ERROR_OOB]
