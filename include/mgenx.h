@@ -169,6 +169,14 @@ int mgenx_pack_batch(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
 int mgenx_crc32_batch(mgenx_ctx* ctx, const uint8_t* dev_data, const uint64_t* dev_off,
                       const uint32_t* dev_len, uint32_t n, uint32_t* dev_out, void* stream);
 
+/* Tuning knobs (process-wide; for benchmarking kernel variants). */
+#define MGENX_TUNE_UNPACK_VARIANT 1
+int mgenx_set_tuning(mgenx_ctx* ctx, int key, int value);
+/* Diagnostic: plain 16-B-per-lane streaming read of `bytes` (the achievable-HBM reference
+ * next to the roofline); dev_scratch holds `grid` words. */
+int mgenx_diag_stream_read(mgenx_ctx* ctx, const uint8_t* dev_data, uint64_t bytes,
+                           uint32_t* dev_scratch, int grid, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -24,7 +24,7 @@ LIB_PATH = os.path.join(HERE, "libmgenx.so")
 EXPORTED_SYMBOLS = (
     "mgenx_abi_version", "mgenx_ctx_create", "mgenx_ctx_destroy", "mgenx_last_error",
     "mgenx_unpack_batch", "mgenx_pack_prepare", "mgenx_set_fill_time", "mgenx_pack_batch",
-    "mgenx_crc32_batch", "mgenx_stream_scan", "mgenx_flow_reduce",
+    "mgenx_crc32_batch", "mgenx_set_tuning", "mgenx_diag_stream_read", "mgenx_stream_scan", "mgenx_flow_reduce",
 )
 
 
@@ -56,6 +56,8 @@ def load():
     L.mgenx_set_fill_time.argtypes = [P, u32]
     L.mgenx_pack_batch.argtypes = [P, P, P, P, u32, P, P, u64, P, u64, P, u32, u32, P]
     L.mgenx_crc32_batch.argtypes = [P, P, P, P, u32, P, P]
+    L.mgenx_set_tuning.argtypes = [P, i32, i32]
+    L.mgenx_diag_stream_read.argtypes = [P, P, u64, P, i32, P]
     if hasattr(L, "mgenx_stream_scan"):
         L.mgenx_stream_scan.argtypes = [P, P, u64, u64, u32, u32, P, P, P, P, P, u32, P]
     _lib = L
@@ -154,6 +156,16 @@ class Engine:
                                        _stream(self.device))
         self._check(rc, "mgenx_pack_batch")
         return out_len
+
+    def set_unpack_variant(self, v: int):
+        self._check(self.lib.mgenx_set_tuning(self.ctx, 1, v), "mgenx_set_tuning")
+
+    def stream_read(self, data, grid=2048, scratch=None):
+        if scratch is None:
+            scratch = self.torch.empty(grid, dtype=self.torch.int32, device=data.device)
+        rc = self.lib.mgenx_diag_stream_read(self.ctx, _ptr(data), data.numel(), _ptr(scratch),
+                                             grid, _stream(self.device))
+        self._check(rc, "mgenx_diag_stream_read")
 
     def crc32(self, data, off, length, n, out=None):
         if out is None:

@@ -15,7 +15,7 @@
 struct mgenx_ctx {
   int device = 0;
   int cu_count = 0;
-  uint32_t* d_tabs = nullptr;     // [A64 | A4 | A16 | A32] 4 x 1024
+  uint32_t* d_tabs = nullptr;     // [A64 | A4 | A8 | A12 | A16 | A32 | A48] 7 x 1024
   uint32_t* d_expect = nullptr;   // [65536]
   uint32_t* d_xpow = nullptr;     // [65536]
   uint32_t* d_ia = nullptr;       // [65536]
@@ -100,11 +100,10 @@ int mgenx_ctx_create(int device, mgenx_ctx** out) {
 
   uint32_t t[256];
   byte_table(t);
-  std::vector<uint32_t> tabs(4096), xpow(kN), ia(kN), expect(kN, 0);
-  op_table(t, 64, &tabs[0]);
-  op_table(t, 4, &tabs[1024]);
-  op_table(t, 16, &tabs[2048]);
-  op_table(t, 32, &tabs[3072]);
+  // unpack operator tables: [A64 | A4 | A8 | A12 | A16 | A32 | A48]
+  std::vector<uint32_t> tabs(7 * 1024), xpow(kN), ia(kN), expect(kN, 0);
+  const uint32_t ops[7] = {64, 4, 8, 12, 16, 32, 48};
+  for (int i = 0; i < 7; i++) op_table(t, ops[i], &tabs[1024 * i]);
   xpow[0] = 0x80000000u;  // x^0
   for (uint32_t n = 1; n < kN; n++) xpow[n] = mgenx::multmodp(xpow[n - 1], 0x00800000u);
   for (uint32_t n = 0; n < kN; n++) ia[n] = mgenx::multmodp(xpow[n], 0xFFFFFFFFu);
@@ -122,7 +121,7 @@ int mgenx_ctx_create(int device, mgenx_ctx** out) {
     size_t bytes;
     const void* src;
   } allocs[] = {
-      {(void**)&c->d_tabs, 4096 * 4, tabs.data()},
+      {(void**)&c->d_tabs, tabs.size() * 4, tabs.data()},
       {(void**)&c->d_expect, kN * 4, expect.data()},
       {(void**)&c->d_xpow, kN * 4, xpow.data()},
       {(void**)&c->d_ia, kN * 4, ia.data()},
@@ -182,7 +181,7 @@ int mgenx_unpack_batch(mgenx_ctx* ctx, const uint8_t* dev_slab, uint64_t slab_by
   p.expect = ctx->d_expect;
   p.cols = k;
   const uint64_t groups = ((uint64_t)n + 15) / 16;
-  const uint64_t per_block = 16;  // waves per 1024-thread block
+  const uint64_t per_block = (uint64_t)mgenx::unpack_threads() / 64;  // waves per block
   uint64_t grid = (groups + per_block - 1) / per_block;
   if (grid > (uint64_t)ctx->cu_count) grid = ctx->cu_count;
   hipError_t e = mgenx::launch_unpack(p, (int)grid, (hipStream_t)stream);
@@ -254,6 +253,24 @@ int mgenx_pack_batch(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
   if (grid > cap) grid = cap;
   hipError_t e = mgenx::launch_pack(p, (int)grid, (hipStream_t)stream);
   return e == hipSuccess ? MGENX_OK : set_err(ctx, e, "pack");
+}
+
+int mgenx_set_tuning(mgenx_ctx* ctx, int key, int value) {
+  if (!ctx) return MGENX_EINVAL;
+  if (key == MGENX_TUNE_UNPACK_VARIANT) {
+    if (value < 0 || value > 2) return MGENX_EINVAL;
+    mgenx::unpack_variant = value;
+    return MGENX_OK;
+  }
+  return MGENX_EINVAL;
+}
+
+int mgenx_diag_stream_read(mgenx_ctx* ctx, const uint8_t* dev_data, uint64_t bytes,
+                           uint32_t* dev_scratch, int grid, void* stream) {
+  if (!ctx || !dev_data || !dev_scratch || grid <= 0) return MGENX_EINVAL;
+  hipError_t e = mgenx::launch_stream_read(dev_data, bytes, dev_scratch, grid,
+                                           (hipStream_t)stream);
+  return e == hipSuccess ? MGENX_OK : set_err(ctx, e, "stream_read");
 }
 
 int mgenx_crc32_batch(mgenx_ctx* ctx, const uint8_t* dev_data, const uint64_t* dev_off,

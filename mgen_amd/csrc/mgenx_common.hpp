@@ -30,6 +30,11 @@ typedef uint16_t u16_u1 __attribute__((aligned(1)));
 __device__ __forceinline__ u32x4_t ldu128(const uint8_t* p) {
   return *reinterpret_cast<const u32x4_u1*>(p);
 }
+// Same load, but pinned in program order (volatile): used for software-pipelined
+// prefetches that the compiler would otherwise sink next to their first use.
+__device__ __forceinline__ u32x4_t ldu128_pinned(const uint8_t* p) {
+  return *reinterpret_cast<const volatile u32x4_u1*>(p);
+}
 __device__ __forceinline__ uint32_t ldu32(const uint8_t* p) {
   return *reinterpret_cast<const u32_u1*>(p);
 }

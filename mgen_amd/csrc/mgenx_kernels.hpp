@@ -14,7 +14,7 @@ struct UnpackParams {
   uint32_t fixed_len;
   uint32_t n;
   uint32_t opts;
-  const uint32_t* tabs;    // [A64 | A4 | A16 | A32], each 4 x 256 (k-major)
+  const uint32_t* tabs;    // [A64 | A4 | A8 | A12 | A16 | A32 | A48], 4 x 256 each
   const uint32_t* expect;  // [65536]
   mgenx_cols cols;
 };
@@ -39,6 +39,10 @@ struct PackParams {
 };
 
 hipError_t launch_unpack(const UnpackParams& p, int grid, hipStream_t stream);
+extern int unpack_variant;  // tuning knob (mgenx_set_tuning)
+int unpack_threads();
+hipError_t launch_stream_read(const uint8_t* p, uint64_t bytes, uint32_t* out, int grid,
+                              hipStream_t stream);
 hipError_t launch_pack(const PackParams& p, int grid, hipStream_t stream);
 hipError_t launch_pack_prepare(const mgenx_flow_tmpl* tmpl, uint32_t n_tmpl, const uint8_t* pool,
                                const uint32_t* byte_tab, uint32_t* out, hipStream_t stream);

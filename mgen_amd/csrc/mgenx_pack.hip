@@ -211,15 +211,21 @@ pack_kernel(PackParams p) {
     if (lane == 0) s_pre[wv][0] = 0;
     __syncthreads();
     const uint32_t total = s_pre[wv][64];
+    // Each lane walks units lane, lane+64, ...; its record index only moves forward, so
+    // one LDS probe per unit replaces a binary search.
+    int ri = 0;
+    uint32_t next_start = s_pre[wv][1];
+    PackMeta r = s_meta[wv][0];
     for (uint32_t u = lane; u < total; u += 64) {
-      int lo = 0, hi = 64;
-      while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (s_pre[wv][mid] <= u) lo = mid; else hi = mid;
+      bool moved = false;
+      while (next_start <= u) {
+        ri++;
+        next_start = s_pre[wv][ri + 1];
+        moved = true;
       }
-      const PackMeta& r = s_meta[wv][lo];
-      const uint32_t pos = (u - s_pre[wv][lo]) << 4;
-      const uint8_t* rimg = &s_img[wv][lo * kImg];
+      if (moved) r = s_meta[wv][ri];
+      const uint32_t pos = (u - s_pre[wv][ri]) << 4;
+      const uint8_t* rimg = &s_img[wv][ri * kImg];
       uint32_t v[4] = {0u, 0u, 0u, 0u};
       // fill (zero, or the rand() stream after two zero bytes: mgenMsg.cpp:277-292)
       if (r.rf) {

@@ -18,6 +18,8 @@
 //     reads bank l).  The last row folds the braids with A_4 and the quad folds its four
 //     lanes with A_16 / A_32 (shuffles);
 //   * lane 0 of the quad decodes the header fields and writes the SoA columns.
+#include <type_traits>
+
 #include "mgenx_kernels.hpp"
 
 namespace mgenx {
@@ -26,7 +28,9 @@ constexpr int kUnpackThreads = 1024;
 constexpr int kRep = 32;                       // A_64 replicas (one per LDS bank)
 constexpr int kRepDwords = 4 * 256 * kRep;     // 32768 dwords = 128 KiB
 constexpr int kSmallTabDwords = 1024;          // one shift operator: 4 x 256 dwords
-constexpr size_t kUnpackLdsBytes = (size_t)(kRepDwords + 3 * kSmallTabDwords) * 4u;
+// fold operators A_4, A_8, A_12, A_16, A_32, A_48 (not replicated)
+constexpr int kFoldTabs = 6;
+constexpr size_t kUnpackLdsBytes = (size_t)(kRepDwords + kFoldTabs * kSmallTabDwords) * 4u;
 
 
 // A_64(x) from the replicated tables: layout [(k*256 + v) * 32 + copy], copy = lane & 31.
@@ -89,8 +93,33 @@ struct Hdr {
   bool ok;
 };
 
-// MgenMsg::Unpack on a fresh MgenMsg (mgenMsg.cpp:315-500); buf_len = bufferLen.
-__device__ void parse_header(const uint8_t* r, uint32_t buf_len, bool want_ext, Hdr& h) {
+// The first 32 bytes of a record (or 28..31 when shorter), loaded up front so the CRC
+// decision costs one load latency.  w[7] (bytes 28..31) is valid only if buf_len >= 32.
+__device__ __forceinline__ void load_fixed(const uint8_t* r, uint32_t buf_len, uint32_t w[8]) {
+  if (buf_len >= 32) {
+    const u32x4_t a = ldu128(r), b = ldu128(r + 16);
+    w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+    w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+  } else if (buf_len >= MGENX_MIN_SIZE) {
+    const u32x4_t a = ldu128(r);
+    w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+    w[4] = ldu32(r + 16); w[5] = ldu32(r + 20); w[6] = ldu32(r + 24); w[7] = 0;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; j++) w[j] = 0;
+  }
+}
+
+// Unpack()'s return value from the fixed prefix alone (mgenMsg.cpp:323-392).
+__device__ __forceinline__ bool fixed_ok(uint32_t buf_len, const uint32_t w[8]) {
+  const uint32_t t = (w[5] >> 16) & 0xffu;
+  return buf_len >= MGENX_MIN_SIZE && ((w[0] >> 16) & 0xffu) == 2u && (t == 1u || t == 2u);
+}
+
+// MgenMsg::Unpack on a fresh MgenMsg (mgenMsg.cpp:315-500); buf_len = bufferLen,
+// w = load_fixed(r, buf_len).
+__device__ void parse_header(const uint8_t* r, uint32_t buf_len, bool want_ext,
+                             const uint32_t w[8], Hdr& h) {
   h.flow = h.seq = h.sec = h.usec = h.dst4 = h.poff = 0;
   h.lat = h.lon = 10800000u;  // (0.0 + 180) * 60000: the constructor's 0.0 degrees
   h.alt = 0;
@@ -101,39 +130,31 @@ __device__ void parse_header(const uint8_t* r, uint32_t buf_len, bool want_ext, 
   h.flags = h.err = h.dst_type = h.dst_len = h.ptype = h.gps = h.host_type = h.host_len = 0;
   h.ok = false;
   if (buf_len < MGENX_MIN_SIZE) { h.err = MGENX_ERROR_LENGTH; return; }      // :323-328
-  const u32x4_t a = ldu128(r);
-  const uint32_t w4 = ldu32(r + 16), w5 = ldu32(r + 20);
-  h.msg_len = bswap16((uint16_t)(a.x & 0xffffu));
-  h.version = (uint8_t)(a.x >> 16);
+  h.msg_len = bswap16((uint16_t)(w[0] & 0xffffu));
+  h.version = (uint8_t)(w[0] >> 16);
   if (h.version != 2) { h.err = MGENX_ERROR_VERSION; return; }              // :336-343
-  h.flags = (uint8_t)(a.x >> 24);
-  h.flow = bswap32(a.y);
-  h.seq = bswap32(a.z);
-  h.sec = bswap32(a.w);
-  h.usec = bswap32(w4);
-  const uint16_t dport = bswap16((uint16_t)(w5 & 0xffffu));
-  const uint32_t t = (w5 >> 16) & 0xffu;
-  const uint32_t D = w5 >> 24;
+  h.flags = (uint8_t)(w[0] >> 24);
+  h.flow = bswap32(w[1]);
+  h.seq = bswap32(w[2]);
+  h.sec = bswap32(w[3]);
+  h.usec = bswap32(w[4]);
+  const uint16_t dport = bswap16((uint16_t)(w[5] & 0xffffu));
+  const uint32_t t = (w[5] >> 16) & 0xffu;
+  const uint32_t D = w[5] >> 24;
   if (t != 1u && t != 2u) { h.err = MGENX_ERROR_DSTADDR; return; }          // :374-392
   h.dst_type = (uint8_t)t;
   h.dst_len = (uint8_t)D;
   h.dst_port = dport;
-  {
-    // :394-398 has no bounds check; bytes past the record read as zero here.
-    uint32_t d[4];
-    if (want_ext) {
-      load_addr16(r + 24, D, buf_len - 24, d);
-#pragma unroll
-      for (int j = 0; j < 4; j++) h.dst_addr[j] = d[j];
-      h.dst4 = d[0];
-    } else {
-      const uint32_t w6 = ldu32(r + 24);   // 24 + 4 <= 28 <= buf_len
-      h.dst4 = D >= 4 ? w6 : (w6 & byte_range_mask(0, (int)D));
-    }
+  // :394-398 has no bounds check; bytes past the record read as zero here.
+  if (want_ext) {
+    load_addr16(r + 24, D, buf_len - 24, h.dst_addr);
+    h.dst4 = h.dst_addr[0];
+  } else {
+    h.dst4 = D >= 4 ? w[6] : (w[6] & byte_range_mask(0, (int)D));
   }
   uint32_t len = 24u + D;
   if (len + 4u <= buf_len) {                                                  // :400-443
-    const uint32_t hw = ldu32(r + len);
+    const uint32_t hw = (len == 28u) ? w[7] : ldu32(r + len);
     const uint16_t hport = bswap16((uint16_t)(hw & 0xffffu));
     const uint32_t ht = (hw >> 16) & 0xffu;
     const uint32_t H = hw >> 24;
@@ -151,6 +172,22 @@ __device__ void parse_header(const uint8_t* r, uint32_t buf_len, bool want_ext, 
     }
   } else {
     h.hdr_len = (uint16_t)len; h.ok = true; return;
+  }
+  if (len + 16u <= buf_len) {                                                 // :446-497
+    // GPS, payload_type and payload_len in one 16-byte load (the common case)
+    const u32x4_t g = ldu128(r + len);
+    h.lat = bswap32(g.x);
+    h.lon = bswap32(g.y);
+    h.alt = (int32_t)bswap32(g.z);
+    h.gps = (uint8_t)g.w;
+    h.ptype = (uint8_t)(g.w >> 8);
+    h.plen = bswap16((uint16_t)(g.w >> 16));
+    len += 16u;
+    h.hdr_len = (uint16_t)len;
+    if (h.plen != 0 && len + h.plen <= buf_len) h.poff = (len >> 2) << 2;
+    else h.plen = 0;
+    h.ok = true;
+    return;
   }
   if (len + 13u <= buf_len) {                                                 // :446-465
     h.lat = bswap32(ldu32(r + len));
@@ -177,6 +214,19 @@ __device__ void parse_header(const uint8_t* r, uint32_t buf_len, bool want_ext, 
   h.ok = true;
 }
 
+
+// Layouts the register-only parse handles (given the first 64 bytes pw[0..15] of a record
+// with buf_len >= 64): version 2, dst type IPv4/IPv6, dst and host address lengths in
+// {0,4,16} (every later field is then word-aligned) and header <= 64 bytes (so not IPv6
+// dst + IPv6 host).  Field meaning follows mgenMsg.cpp:323-497 as in parse_header.
+__device__ __forceinline__ bool fast_layout(uint32_t w0, uint32_t w5, uint32_t hw) {
+  const uint32_t t = (w5 >> 16) & 0xffu;
+  const uint32_t D = w5 >> 24;
+  const uint32_t H = hw >> 24;
+  return ((w0 >> 16) & 0xffu) == 2u && (t == 1u || t == 2u) && (D == 4u || D == 16u) &&
+         (H == 0u || H == 4u || H == 16u) && D + H <= 20u;
+}
+
 // CRC-32 (init/xorout ~0) computed bit by bit: used only for records shorter than 32 B.
 __device__ bool small_crc_ok(const uint8_t* r, uint32_t L) {
   if (L < 4) return false;
@@ -192,24 +242,38 @@ __device__ bool small_crc_ok(const uint8_t* r, uint32_t L) {
   return c == t;
 }
 
+// MODE (diagnostic ablations, never the product path): 0 = full kernel, 1 = row loads +
+// XOR only (no LDS table lookups), 2 = table lookups on one L1-resident row (no streaming).
+// pw[4*LN .. 4*LN+3] = quad lane LN's 16-byte prefix chunk (DPP quad_perm broadcast; all
+// four lanes of the quad must be active).
+template <int LN>
+__device__ __forceinline__ void quad_bcast(const u32x4_t& pf, uint32_t (&pw)[16]) {
+  constexpr int ctrl = LN | (LN << 2) | (LN << 4) | (LN << 6);
+  pw[4 * LN + 0] = (uint32_t)__builtin_amdgcn_mov_dpp((int)pf.x, ctrl, 0xf, 0xf, false);
+  pw[4 * LN + 1] = (uint32_t)__builtin_amdgcn_mov_dpp((int)pf.y, ctrl, 0xf, 0xf, false);
+  pw[4 * LN + 2] = (uint32_t)__builtin_amdgcn_mov_dpp((int)pf.z, ctrl, 0xf, 0xf, false);
+  pw[4 * LN + 3] = (uint32_t)__builtin_amdgcn_mov_dpp((int)pf.w, ctrl, 0xf, 0xf, false);
+}
+
+template <bool kCrc, int MODE = 0>
 __global__ void __launch_bounds__(kUnpackThreads)
 unpack_kernel(UnpackParams p) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t* rep = lds;
-  uint32_t* a4 = lds + kRepDwords;
-  uint32_t* a16 = a4 + kSmallTabDwords;
-  uint32_t* a32 = a16 + kSmallTabDwords;
+  uint32_t* fold = lds + kRepDwords;  // [A4 | A8 | A12 | A16 | A32 | A48]
 
   // ---- stage the shift-operator tables (A_64 replicated 32x) ----
-  for (int e = threadIdx.x; e < 1024; e += blockDim.x) {
-    const uint32_t v = p.tabs[e];
-    u32x4_t s = {v, v, v, v};
-    u32x4_t* dst = reinterpret_cast<u32x4_t*>(rep + (size_t)e * kRep);
+  if (kCrc) {
+    for (int e = threadIdx.x; e < 1024; e += blockDim.x) {
+      const uint32_t v = p.tabs[e];
+      u32x4_t s = {v, v, v, v};
+      u32x4_t* dst = reinterpret_cast<u32x4_t*>(rep + (size_t)e * kRep);
 #pragma unroll
-    for (int c = 0; c < kRep / 4; c++) dst[c] = s;
+      for (int c = 0; c < kRep / 4; c++) dst[c] = s;
+    }
+    for (int e = threadIdx.x; e < kFoldTabs * 1024; e += blockDim.x) fold[e] = p.tabs[1024 + e];
+    __syncthreads();
   }
-  for (int e = threadIdx.x; e < 3 * 1024; e += blockDim.x) a4[e] = p.tabs[1024 + e];
-  __syncthreads();
 
   const int lane = threadIdx.x & 63;
   const int q = lane & 3;
@@ -220,9 +284,12 @@ unpack_kernel(UnpackParams p) {
   const uint64_t n_groups = ((uint64_t)p.n + 15) >> 4;
   const bool force = (p.opts & MGENX_OPT_CHECKSUM_FORCE) != 0;
   const bool tcp = (p.opts & MGENX_OPT_TCP) != 0;
-  const bool skip_crc = (p.opts & MGENX_OPT_SKIP_CRC) != 0;
   const bool want_ext = p.cols.dst_addr || p.cols.host_addr;
 
+  // Per-wave predictor: while recent groups carried checksummed records, issue the row
+  // loads speculatively together with the header load (one memory round per group); a
+  // group without any CRC work turns speculation off (header first, body only if needed).
+  bool spec = true;
   for (uint64_t g = wave_id; g < n_groups; g += n_waves) {
     const uint64_t rec_idx = (g << 4) + (uint64_t)(lane >> 2);
     const bool valid = rec_idx < p.n;
@@ -235,68 +302,183 @@ unpack_kernel(UnpackParams p) {
     const bool oob = valid && (L > 65535u || off > p.slab_bytes || L > p.slab_bytes - off);
     const bool live = valid && !oob;
     const uint8_t* rec = p.slab + off;
+    const uint32_t buf_len = tcp ? min(L, (uint32_t)MGENX_TX_BUFFER_SIZE) : L;
 
-    // ---- header decode (quad lane 0) ----
-    Hdr h;
+    // Header prefix: lane q of the quad loads bytes [16q, 16q+16) (64 bytes per record,
+    // enough for every layout but IPv6 dst + IPv6 host); quad lane 0 gathers the words by
+    // DPP quad broadcast when it parses.  Loads are unconditional (clamped to a dummy line)
+    // so no divergent branch forces a full vmcnt wait.
+    const bool pfx = live && L >= 32;           // prefix words 0..7 valid
+    const bool pfx64 = live && buf_len >= 64;   // prefix words 0..15 valid
+    const uint8_t* dummy = reinterpret_cast<const uint8_t*>(p.tabs);
+    u32x4_t pf = {0u, 0u, 0u, 0u};
+    uint32_t w[8];
+    uint32_t expect = 0;
+    auto load_header = [&]() {
+      pf = ldu128((live && L >= 16u * (q + 1)) ? rec + 16 * q : dummy);
+      if (kCrc) expect = p.expect[live ? L : 0u];
+    };
+    // word j of the quad's prefix: lane j/4's pf component j%4 (all lanes must be active)
+    auto gather = [&](uint32_t (&pw)[16]) {
+      quad_bcast<0>(pf, pw);
+      quad_bcast<1>(pf, pw);
+      quad_bcast<2>(pf, pw);
+      quad_bcast<3>(pf, pw);
+    };
+    auto unpack_words = [&](const uint32_t (&pw)[16]) {
+      if (pfx) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) w[j] = pw[j];
+      } else if (live && L >= MGENX_MIN_SIZE) {
+        load_fixed(rec, buf_len, w);  // 28..31-byte records
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; j++) w[j] = 0;
+      }
+    };
     bool needs_crc = false;
-    if (live && q == 0) {
-      const uint32_t buf_len = tcp ? min(L, (uint32_t)MGENX_TX_BUFFER_SIZE) : L;
-      parse_header(rec, buf_len, want_ext, h);
-      const bool flagged = force || (h.flags & MGENX_FLAG_CHECKSUM);
-      needs_crc = !skip_crc && flagged && (tcp ? (L >= 4) : h.ok);
-    }
-    needs_crc = __shfl(needs_crc, lane & ~3);
+    auto decide = [&]() {
+      uint32_t pw[16];
+      gather(pw);
+      if (kCrc && live && q == 0) {
+        unpack_words(pw);
+        const bool flagged = force || (((w[0] >> 24) & MGENX_FLAG_CHECKSUM) != 0 &&
+                                       buf_len >= MGENX_MIN_SIZE &&
+                                       ((w[0] >> 16) & 0xffu) == 2u);
+        needs_crc = flagged && (tcp ? (L >= 4) : fixed_ok(buf_len, w));
+      }
+    };
 
-    // ---- CRC residue over end-aligned 64-byte rows (quads with L >= 32) ----
-    const bool vec = needs_crc && L >= 32;
-    const int R = vec ? (int)((L + 63u) >> 6) : 0;
-    const int64_t row0 = (int64_t)L - 64 * (int64_t)R + 16 * q;  // position of row 0 unit
-    u32x4_t w = {0u, 0u, 0u, 0u};
-    if (vec) {
-      if (row0 >= 0) {
-        w = ldu128(rec + row0);
-      } else if (row0 > -16) {
-        w = shl_bytes(ldu128(rec), (int)(-row0));
+    uint32_t tot = 0;
+    const bool speculate = kCrc && (spec || force);
+    bool run_crc = speculate;
+    if (!speculate) {
+      load_header();
+      if (kCrc) {
+        decide();
+        run_crc = __any(needs_crc);
       }
     }
-    uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
-    int r = 0;
-    while (__any(vec && r < R - 1)) {
-      const bool g1 = vec && r + 1 < R, g2 = vec && r + 2 < R;
-      const bool g3 = vec && r + 3 < R, g4 = vec && r + 4 < R;
-      const int64_t b = row0 + 64 * (int64_t)r;
-      u32x4_t d1 = w, d2 = w, d3 = w, d4 = w;
-      if (g1) d1 = ldu128(rec + b + 64);
-      if (g2) d2 = ldu128(rec + b + 128);
-      if (g3) d3 = ldu128(rec + b + 192);
-      if (g4) d4 = ldu128(rec + b + 256);
-#define MGENX_ROW_STEP(DN, GN)                                   \
-      if (GN) {                                                  \
-        h0 = shift_rep(rep, h0 ^ w.x, copy);                     \
-        h1 = shift_rep(rep, h1 ^ w.y, copy);                     \
-        h2 = shift_rep(rep, h2 ^ w.z, copy);                     \
-        h3 = shift_rep(rep, h3 ^ w.w, copy);                     \
-        w = DN;                                                  \
-        r++;                                                     \
+    if (kCrc && run_crc) {
+      // ---- braid CRC over end-aligned 64-byte rows ----
+      // R depends only on L, so the row loads need nothing from the header.  Quads are
+      // front-padded with zero rows to the wave-uniform count V (leading zeros leave a
+      // zero-initialised CRC unchanged): all lanes run the same updates.
+      const int R = (live && L >= 32) ? (int)((L + 63u) >> 6) : 0;
+      const bool vec = R > 0;
+      const int64_t row0 = (int64_t)L - 64 * (int64_t)R + 16 * q;  // position of row 0
+      int Rmax = R;
+#pragma unroll
+      for (int sft = 1; sft < 64; sft <<= 1) Rmax = max(Rmax, __shfl_xor(Rmax, sft));
+      const int V = __builtin_amdgcn_readfirstlane(Rmax);  // virtual rows 0..V-1 (V-1 final)
+      const int pad = V - R;
+      const bool multi = R >= 2;
+      const uint8_t* base = multi ? rec + row0 : reinterpret_cast<const uint8_t*>(p.tabs);
+      const int hi_row = multi ? R - 1 : 0;
+      auto row_addr = [&](int j) {
+        const int real = j - pad;
+        const int rr = real < 1 ? 1 : (real > hi_row ? hi_row : real);
+        return base + 64 * (multi ? (MODE == 2 ? 1 : rr) : 0);
+      };
+      uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+      const u32x4_t zero = {0u, 0u, 0u, 0u};
+      u32x4_t xr = zero, xf = zero;
+      // row 0 may start before the record: it is loaded from max(row0, 0) and its bytes
+      // shifted up by s0 (0 when aligned); a row entirely before the record is padding
+      const int s0 = row0 >= 0 ? 0 : (int)(-row0);
+      auto load_row0 = [&]() { xr = ldu128(vec ? rec + (row0 >= 0 ? row0 : 0) : dummy); };
+      auto load_final = [&]() { xf = ldu128(base + 64 * hi_row); };  // unused if R < 2
+      auto row0_data = [&]() { return (vec && s0 < 16) ? shl_bytes(xr, s0) : zero; };
+      auto consume = [&](const u32x4_t& dv, int j) {
+        const int real = j - pad;
+        const u32x4_t x = (real == 0) ? row0_data() : zero;
+        u32x4_t xin;
+        xin.x = real > 0 ? dv.x : (real == 0 ? x.x : 0u);
+        xin.y = real > 0 ? dv.y : (real == 0 ? x.y : 0u);
+        xin.z = real > 0 ? dv.z : (real == 0 ? x.z : 0u);
+        xin.w = real > 0 ? dv.w : (real == 0 ? x.w : 0u);
+        if (MODE == 1) {
+          h0 = (h0 << 1) ^ xin.x; h1 = (h1 << 1) ^ xin.y;
+          h2 = (h2 << 1) ^ xin.z; h3 = (h3 << 1) ^ xin.w;
+        } else {
+          // all 16 lookups of the row are independent: compute every address, issue the
+          // 16 LDS reads back to back, then fold them (one LDS round trip per row)
+          const uint32_t c4[4] = {h0 ^ xin.x, h1 ^ xin.y, h2 ^ xin.z, h3 ^ xin.w};
+          uint32_t t[16];
+#pragma unroll
+          for (int b = 0; b < 4; b++) {
+            t[4 * b + 0] = rep[((c4[b] & 0xffu) << 5) | copy];
+            t[4 * b + 1] = rep[8192 + ((((c4[b] >> 8) & 0xffu) << 5) | copy)];
+            t[4 * b + 2] = rep[16384 + ((((c4[b] >> 16) & 0xffu) << 5) | copy)];
+            t[4 * b + 3] = rep[24576 + (((c4[b] >> 24) << 5) | copy)];
+          }
+          h0 = t[0] ^ t[1] ^ t[2] ^ t[3];
+          h1 = t[4] ^ t[5] ^ t[6] ^ t[7];
+          h2 = t[8] ^ t[9] ^ t[10] ^ t[11];
+          h3 = t[12] ^ t[13] ^ t[14] ^ t[15];
+        }
+      };
+      // One block of N middle rows (virtual rows j0..j0+N-1, all in 1..V-2): all loads
+      // issued first (unconditional, clamped addresses), then -- first block only -- row 0,
+      // the final row and the header, then consumption in order with counted waits.  The
+      // empty asm with a memory clobber keeps LLVM from sinking a load into its consumer.
+      auto block = [&](auto n_tag, int j0, int cnt, bool first) {
+        constexpr int N = decltype(n_tag)::value;
+        u32x4_t d[N];
+        // issue order = consumption order: row 0, the block, then the final row + header
+        if (first) load_row0();
+#pragma unroll
+        for (int k = 0; k < N; k++) d[k] = ldu128(row_addr(j0 + k));
+        if (first) {
+          load_final();
+          if (speculate) load_header();
+        }
+        asm volatile("" ::: "memory");
+        if (first && V >= 2) consume(zero, 0);  // virtual row 0: row 0 (from xr) or padding
+#pragma unroll
+        for (int k = 0; k < N; k++)
+          if (k < cnt) consume(d[k], j0 + k);
+      };
+      using B14 = std::integral_constant<int, 14>;
+      using B6 = std::integral_constant<int, 6>;
+      using B2 = std::integral_constant<int, 2>;
+      const int mid = V - 2;  // middle rows 1..V-2 (wave-uniform)
+      if (mid <= 2) {
+        block(B2{}, 1, mid, true);
+      } else if (mid <= 6) {
+        block(B6{}, 1, mid, true);
+      } else {
+        block(B14{}, 1, min(14, mid), true);
+        for (int j0 = 15; j0 <= mid; j0 += 14) block(B14{}, j0, min(14, mid + 1 - j0), false);
       }
-      MGENX_ROW_STEP(d1, g1)
-      MGENX_ROW_STEP(d2, g2)
-      MGENX_ROW_STEP(d3, g3)
-      MGENX_ROW_STEP(d4, g4)
-#undef MGENX_ROW_STEP
+      u32x4_t x = multi ? xf : row0_data();
+      if (speculate) decide();
+      // last row: byte-swap the big-endian trailer into little-endian stream order
+      if (q == 3) x.w = bswap32(x.w);
+      // fold: word b of lane q sits 64-16q-4b bytes before the record end, so
+      //   v_q = A16(g0) ^ A12(g1) ^ A8(g2) ^ A4(g3),  tot = XOR_q A_{48-16q}(v_q)
+      // (16 independent lookups, then one per-lane lookup and a quad XOR-reduce)
+      const uint32_t v = shift_tab(fold + 3 * 1024, h0 ^ x.x) ^
+                         shift_tab(fold + 2 * 1024, h1 ^ x.y) ^
+                         shift_tab(fold + 1 * 1024, h2 ^ x.z) ^ shift_tab(fold, h3 ^ x.w);
+      const uint32_t* lt = fold + (q == 0 ? 5 : (q == 1 ? 4 : 3)) * 1024;  // A48/A32/A16
+      uint32_t s = (q == 3) ? v : shift_tab(lt, v);
+      s ^= __shfl_xor(s, 1);
+      s ^= __shfl_xor(s, 2);
+      tot = s;
+      spec = __any(needs_crc);
+    } else if (kCrc) {
+      spec = false;
     }
-    // last row: byte-swap the big-endian trailer into little-endian stream order
-    if (q == 3) w.w = bswap32(w.w);
-    uint32_t v = shift_tab(a4, h0 ^ w.x);
-    v = shift_tab(a4, v ^ h1 ^ w.y);
-    v = shift_tab(a4, v ^ h2 ^ w.z);
-    v = shift_tab(a4, v ^ h3 ^ w.w);
-    const uint32_t t = shift_tab(a16, v) ^ __shfl_down(v, 1);
-    const uint32_t tot = shift_tab(a32, t) ^ __shfl_down(t, 2);
+    if (!kCrc) load_header();
+    const bool vec_crc = needs_crc && live && L >= 32;
 
-    if (live && q == 0) {
+    uint32_t pw[16];
+    gather(pw);
+    // each parse path stores its own columns (no join merging two Hdr values)
+    auto store = [&](const Hdr& h) {
       bool crc_ok = true;
-      if (needs_crc) crc_ok = vec ? (tot == p.expect[L]) : small_crc_ok(rec, L);
+      if (needs_crc) crc_ok = vec_crc ? (tot == expect) : small_crc_ok(rec, L);
       uint8_t err = h.err;
       uint8_t flags = h.flags;
       if (!crc_ok) {
@@ -334,37 +516,160 @@ unpack_kernel(UnpackParams p) {
         u32x4_t* dp = reinterpret_cast<u32x4_t*>(c.dst_addr + rec_idx * 16);
         *dp = u32x4_t{h.dst_addr[0], h.dst_addr[1], h.dst_addr[2], h.dst_addr[3]};
       }
+    };
+    // fast path: fields straight from the gathered prefix words to the columns, stored as
+    // soon as each is extracted (no Hdr value live across the stores)
+    auto store_fast = [&]() {
+      const mgenx_cols& c = p.cols;
+      const uint32_t D = pw[5] >> 24;
+      const uint32_t hw = (D == 4u) ? pw[7] : pw[10];
+      const uint32_t H = hw >> 24;
+      const uint32_t ht = (hw >> 16) & 0xffu;
+      const bool hv = ht == 1u || ht == 2u;
+      bool crc_ok = true;
+      if (needs_crc) crc_ok = tot == expect;  // buf_len >= 64: always the vector CRC
+      uint8_t flags = (uint8_t)(pw[0] >> 24);
+      uint8_t err = 0;
+      if (!crc_ok) {
+        err = MGENX_ERROR_CHECKSUM;
+        if (tcp) flags |= MGENX_FLAG_CHECKSUM_ERROR;
+      }
+      c.msg_len[rec_idx] = bswap16((uint16_t)(pw[0] & 0xffffu));
+      c.flags[rec_idx] = flags;
+      c.err[rec_idx] = err;
+      c.flow_id[rec_idx] = bswap32(pw[1]);
+      c.seq_num[rec_idx] = bswap32(pw[2]);
+      c.tx_sec[rec_idx] = bswap32(pw[3]);
+      c.tx_usec[rec_idx] = bswap32(pw[4]);
+      c.dst_port[rec_idx] = bswap16((uint16_t)(pw[5] & 0xffffu));
+      c.dst_type[rec_idx] = (uint8_t)((pw[5] >> 16) & 0xffu);
+      c.dst_len[rec_idx] = (uint8_t)D;
+      c.dst_addr4[rec_idx] = pw[6];
+      // GPS + payload_type + payload_len: 16 bytes at word gi = (28 + D + H) / 4
+      const uint32_t gi = (28u + D + H) >> 2;  // 8, 9, 11 or 12
+      // AND/OR masks, not selects: LLVM folds a select chain over pw back into pw[gi + k],
+      // a dynamic index that puts pw in scratch memory
+      const uint32_t m8 = 0u - (uint32_t)(gi == 8u), m9 = 0u - (uint32_t)(gi == 9u);
+      const uint32_t m11 = 0u - (uint32_t)(gi == 11u), m12 = 0u - (uint32_t)(gi == 12u);
+      auto gword = [&](int k) {
+        return (pw[8 + k] & m8) | (pw[9 + k] & m9) | (pw[11 + k] & m11) | (pw[12 + k] & m12);
+      };
+      const uint32_t g3 = gword(3);
+      const uint32_t len = 44u + D + H;
+      uint16_t plen = bswap16((uint16_t)(g3 >> 16));
+      const bool pl_ok = plen != 0 && len + plen <= buf_len;
+      if (!pl_ok) plen = 0;
+      c.payload_len[rec_idx] = plen;
+      c.payload_type[rec_idx] = (uint8_t)(g3 >> 8);
+      c.gps_status[rec_idx] = (uint8_t)g3;
+      if (c.hdr_len) c.hdr_len[rec_idx] = (uint16_t)len;
+      if (c.payload_off) c.payload_off[rec_idx] = pl_ok ? len : 0u;  // len % 4 == 0
+      if (c.host_port) c.host_port[rec_idx] = hv ? bswap16((uint16_t)(hw & 0xffffu)) : 0;
+      if (c.host_type) c.host_type[rec_idx] = hv ? (uint8_t)ht : 0;
+      if (c.host_len) c.host_len[rec_idx] = hv ? (uint8_t)H : 0;
+      if (c.lat_raw)
+        c.lat_raw[rec_idx] = bswap32(gword(0));
+      if (c.lon_raw)
+        c.lon_raw[rec_idx] = bswap32(gword(1));
+      if (c.alt)
+        c.alt[rec_idx] = (int32_t)bswap32(gword(2));
+      if (c.dst_addr) {
+        u32x4_t* dp = reinterpret_cast<u32x4_t*>(c.dst_addr + rec_idx * 16);
+        const bool d16 = D == 16u;
+        *dp = u32x4_t{pw[6], d16 ? pw[7] : 0u, d16 ? pw[8] : 0u, d16 ? pw[9] : 0u};
+      }
+      if (c.host_addr) {
+        // host address at word 8 (dst IPv4) or 11 (dst IPv6); zero unless a valid type
+        const uint32_t a0 = (!hv || H == 0u) ? 0u : (D == 4u ? pw[8] : pw[11]);
+        const bool h16 = hv && H == 16u;  // only with dst IPv4 (D + H <= 20)
+        u32x4_t* hp = reinterpret_cast<u32x4_t*>(c.host_addr + rec_idx * 16);
+        *hp = u32x4_t{a0, h16 ? pw[9] : 0u, h16 ? pw[10] : 0u, h16 ? pw[11] : 0u};
+      }
+    };
+    if (live && q == 0) {
+      if (pfx64 && fast_layout(pw[0], pw[5], (pw[5] >> 24) == 4u ? pw[7] : pw[10])) {
+        store_fast();
+      } else {
+        Hdr h;
+        unpack_words(pw);
+        parse_header(rec, buf_len, want_ext, w, h);
+        store(h);
+      }
     } else if (oob && q == 0) {
-      p.cols.err[rec_idx] = MGENX_ERROR_OOB;
-      p.cols.flags[rec_idx] = 0;
-      p.cols.msg_len[rec_idx] = 0;
-      p.cols.flow_id[rec_idx] = 0;
-      p.cols.seq_num[rec_idx] = 0;
-      p.cols.tx_sec[rec_idx] = 0;
-      p.cols.tx_usec[rec_idx] = 0;
-      p.cols.dst_port[rec_idx] = 0;
-      p.cols.dst_type[rec_idx] = 0;
-      p.cols.dst_len[rec_idx] = 0;
-      p.cols.dst_addr4[rec_idx] = 0;
-      p.cols.payload_len[rec_idx] = 0;
-      p.cols.payload_type[rec_idx] = 0;
-      p.cols.gps_status[rec_idx] = 0;
+      const mgenx_cols& c = p.cols;
+      c.err[rec_idx] = MGENX_ERROR_OOB;
+      c.flags[rec_idx] = 0;
+      c.msg_len[rec_idx] = 0;
+      c.flow_id[rec_idx] = 0;
+      c.seq_num[rec_idx] = 0;
+      c.tx_sec[rec_idx] = 0;
+      c.tx_usec[rec_idx] = 0;
+      c.dst_port[rec_idx] = 0;
+      c.dst_type[rec_idx] = 0;
+      c.dst_len[rec_idx] = 0;
+      c.dst_addr4[rec_idx] = 0;
+      c.payload_len[rec_idx] = 0;
+      c.payload_type[rec_idx] = 0;
+      c.gps_status[rec_idx] = 0;
     }
   }
 }
 
-hipError_t launch_unpack(const UnpackParams& p, int grid, hipStream_t stream) {
+int unpack_variant = 0;
+
+template <int MODE>
+static hipError_t launch_mode(const UnpackParams& p, int grid, hipStream_t stream) {
   static bool attr_done = false;
   if (!attr_done) {
-    hipError_t e = hipFuncSetAttribute((const void*)unpack_kernel,
+    hipError_t e = hipFuncSetAttribute((const void*)unpack_kernel<true, MODE>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)kUnpackLdsBytes);
     if (e != hipSuccess) return e;
     attr_done = true;
   }
-  hipLaunchKernelGGL(unpack_kernel, dim3(grid), dim3(kUnpackThreads), kUnpackLdsBytes, stream,
-                     p);
+  hipLaunchKernelGGL((unpack_kernel<true, MODE>), dim3(grid), dim3(kUnpackThreads),
+                     kUnpackLdsBytes, stream, p);
   return hipGetLastError();
 }
+
+hipError_t launch_unpack(const UnpackParams& p, int grid, hipStream_t stream) {
+  if (p.opts & MGENX_OPT_SKIP_CRC) {
+    hipLaunchKernelGGL((unpack_kernel<false>), dim3(grid), dim3(kUnpackThreads), 0, stream, p);
+    return hipGetLastError();
+  }
+  switch (unpack_variant) {
+    case 1: return launch_mode<1>(p, grid, stream);
+    case 2: return launch_mode<2>(p, grid, stream);
+    default: return launch_mode<0>(p, grid, stream);
+  }
+}
+
+// Diagnostic: streaming read of `bytes` (16 B per lane per load, grid-stride), XOR-folded
+// into one word per block so the loads are not dead.  Reference for achievable HBM rate.
+__global__ void __launch_bounds__(256) stream_read_kernel(const u32x4_t* p, uint64_t n16,
+                                                          uint32_t* out) {
+  uint32_t acc = 0;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < n16; i += 4 * stride) {
+    const u32x4_t a = p[i], b = p[i + stride], c = p[i + 2 * stride], d = p[i + 3 * stride];
+    acc ^= a.x ^ a.y ^ a.z ^ a.w ^ b.x ^ b.y ^ b.z ^ b.w ^ c.x ^ c.y ^ c.z ^ c.w ^ d.x ^ d.y ^
+           d.z ^ d.w;
+  }
+  for (; i < n16; i += stride) {
+    const u32x4_t a = p[i];
+    acc ^= a.x ^ a.y ^ a.z ^ a.w;
+  }
+  if (acc == 0x9E3779B9u) out[blockIdx.x] = acc;  // practically never taken
+}
+
+hipError_t launch_stream_read(const uint8_t* p, uint64_t bytes, uint32_t* out, int grid,
+                              hipStream_t stream) {
+  hipLaunchKernelGGL(stream_read_kernel, dim3(grid), dim3(256), 0, stream,
+                     reinterpret_cast<const u32x4_t*>(p), bytes / 16, out);
+  return hipGetLastError();
+}
+
+int unpack_threads() { return kUnpackThreads; }
 
 }  // namespace mgenx
