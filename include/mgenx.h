@@ -169,7 +169,11 @@ int mgenx_pack_batch(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
 int mgenx_crc32_batch(mgenx_ctx* ctx, const uint8_t* dev_data, const uint64_t* dev_off,
                       const uint32_t* dev_len, uint32_t n, uint32_t* dev_out, void* stream);
 
-/* Tuning knobs (process-wide; for benchmarking kernel variants). */
+/* Tuning knobs (process-wide; for benchmarking kernel variants).  MGENX_TUNE_UNPACK_VARIANT:
+ * 0 = automatic (pipelined fixed-length kernel when the batch qualifies), 1/2 = ablations
+ * of the general kernel (loads+XOR only / lookups on cached rows), 3 = general kernel,
+ * 4 = loads+XOR ablation of the fixed-length kernel, 5 = the same without decode/stores
+ * (1024-B records only). */
 #define MGENX_TUNE_UNPACK_VARIANT 1
 int mgenx_set_tuning(mgenx_ctx* ctx, int key, int value);
 /* Diagnostic: plain 16-B-per-lane streaming read of `bytes` (the achievable-HBM reference

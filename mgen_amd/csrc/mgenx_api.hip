@@ -17,11 +17,13 @@ struct mgenx_ctx {
   int cu_count = 0;
   uint32_t* d_tabs = nullptr;     // [A64 | A4 | A8 | A12 | A16 | A32 | A48] 7 x 1024
   uint32_t* d_expect = nullptr;   // [65536]
+  std::vector<uint32_t> h_expect;  // host copy of the expect table
   uint32_t* d_xpow = nullptr;     // [65536]
   uint32_t* d_ia = nullptr;       // [65536]
   uint32_t* d_bytetab = nullptr;  // [256]
   uint8_t* d_rtab = nullptr;      // 16 + 65536 + 32 bytes
   uint32_t* d_rcrc = nullptr;     // [65536]
+  uint8_t* d_sink = nullptr;      // 1 KiB: column stores of lanes past the batch end
   bool rand_ready = false;
   uint32_t rand_time = 0;
   char err[256] = {0};
@@ -115,6 +117,7 @@ int mgenx_ctx_create(int device, mgenx_ctx** out) {
     }
   }
   for (uint32_t L = 4; L < kN; L++) expect[L] = shift_n(t, ia[L - 4] ^ 0xFFFFFFFFu, 4);
+  c->h_expect = expect;
 
   struct {
     void** p;
@@ -128,6 +131,7 @@ int mgenx_ctx_create(int device, mgenx_ctx** out) {
       {(void**)&c->d_bytetab, 256 * 4, t},
       {(void**)&c->d_rtab, 16 + kN + 32, nullptr},
       {(void**)&c->d_rcrc, kN * 4, nullptr},
+      {(void**)&c->d_sink, 1024, nullptr},
   };
   for (auto& a : allocs) {
     if (hipMalloc(a.p, a.bytes) != hipSuccess) {
@@ -148,7 +152,8 @@ int mgenx_ctx_create(int device, mgenx_ctx** out) {
 int mgenx_ctx_destroy(mgenx_ctx* c) {
   if (!c) return MGENX_EINVAL;
   hipSetDevice(c->device);
-  void* ps[] = {c->d_tabs, c->d_expect, c->d_xpow, c->d_ia, c->d_bytetab, c->d_rtab, c->d_rcrc};
+  void* ps[] = {c->d_tabs, c->d_expect, c->d_xpow, c->d_ia, c->d_bytetab, c->d_rtab, c->d_rcrc,
+                c->d_sink};
   for (void* p : ps)
     if (p) hipFree(p);
   delete c;
@@ -179,6 +184,8 @@ int mgenx_unpack_batch(mgenx_ctx* ctx, const uint8_t* dev_slab, uint64_t slab_by
   p.opts = opts;
   p.tabs = ctx->d_tabs;
   p.expect = ctx->d_expect;
+  p.expect_fixed = fixed_len < ctx->h_expect.size() ? ctx->h_expect[fixed_len] : 0u;
+  p.sink = ctx->d_sink;
   p.cols = k;
   const uint64_t groups = ((uint64_t)n + 15) / 16;
   const uint64_t per_block = (uint64_t)mgenx::unpack_threads() / 64;  // waves per block
@@ -258,7 +265,7 @@ int mgenx_pack_batch(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
 int mgenx_set_tuning(mgenx_ctx* ctx, int key, int value) {
   if (!ctx) return MGENX_EINVAL;
   if (key == MGENX_TUNE_UNPACK_VARIANT) {
-    if (value < 0 || value > 2) return MGENX_EINVAL;
+    if (value < 0 || value > 5) return MGENX_EINVAL;
     mgenx::unpack_variant = value;
     return MGENX_OK;
   }

@@ -35,6 +35,11 @@ __device__ __forceinline__ u32x4_t ldu128(const uint8_t* p) {
 __device__ __forceinline__ u32x4_t ldu128_pinned(const uint8_t* p) {
   return *reinterpret_cast<const volatile u32x4_u1*>(p);
 }
+// Streaming (non-temporal) 16-byte load: record bodies are read once.  gfx950 runs in
+// unaligned-access mode, so the aligned vector type only fixes the instruction choice.
+__device__ __forceinline__ u32x4_t ldnt128(const uint8_t* p) {
+  return __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+}
 __device__ __forceinline__ uint32_t ldu32(const uint8_t* p) {
   return *reinterpret_cast<const u32_u1*>(p);
 }
@@ -43,6 +48,23 @@ __device__ __forceinline__ uint16_t ldu16(const uint8_t* p) {
 }
 __device__ __forceinline__ void stu128(uint8_t* p, u32x4_t v) {
   *reinterpret_cast<u32x4_u1*>(p) = v;
+}
+
+// Stores through an integer address known to be global memory (a per-lane choice of
+// column base pointers is computed as integers: see unpack_fixed_kernel's tail).
+typedef __attribute__((address_space(1))) uint8_t g_u8;
+typedef __attribute__((address_space(1))) uint16_t g_u16;
+typedef __attribute__((address_space(1))) uint32_t g_u32;
+__device__ __forceinline__ void st_g8(uint64_t a, uint32_t v) { *(g_u8*)a = (uint8_t)v; }
+__device__ __forceinline__ void st_g16(uint64_t a, uint32_t v) { *(g_u16*)a = (uint16_t)v; }
+__device__ __forceinline__ void st_g32(uint64_t a, uint32_t v) { *(g_u32*)a = v; }
+// a[k] for k = sel in 0..3, as AND/OR masks (a select chain over struct fields or arrays
+// can be folded back into a dynamic index into a stack copy)
+__device__ __forceinline__ uint64_t pick4(int sel, uint64_t a0, uint64_t a1, uint64_t a2,
+                                          uint64_t a3) {
+  const uint64_t m0 = 0ull - (uint64_t)(sel == 0), m1 = 0ull - (uint64_t)(sel == 1);
+  const uint64_t m2 = 0ull - (uint64_t)(sel == 2), m3 = 0ull - (uint64_t)(sel == 3);
+  return (a0 & m0) | (a1 & m1) | (a2 & m2) | (a3 & m3);
 }
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }

@@ -16,6 +16,8 @@ struct UnpackParams {
   uint32_t opts;
   const uint32_t* tabs;    // [A64 | A4 | A8 | A12 | A16 | A32 | A48], 4 x 256 each
   const uint32_t* expect;  // [65536]
+  uint32_t expect_fixed;   // expect[fixed_len] (host copy, fixed-length kernel)
+  uint8_t* sink;           // 1 KiB scratch: stores of lanes past the batch end
   mgenx_cols cols;
 };
 
@@ -39,7 +41,9 @@ struct PackParams {
 };
 
 hipError_t launch_unpack(const UnpackParams& p, int grid, hipStream_t stream);
-extern int unpack_variant;  // tuning knob (mgenx_set_tuning)
+// tuning knob (mgenx_set_tuning): 0 = auto (pipelined fixed-length kernel when the batch
+// qualifies), 1/2 = ablations of the general kernel, 3 = general kernel only
+extern int unpack_variant;
 int unpack_threads();
 hipError_t launch_stream_read(const uint8_t* p, uint64_t bytes, uint32_t* out, int grid,
                               hipStream_t stream);

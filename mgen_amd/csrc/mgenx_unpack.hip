@@ -242,6 +242,183 @@ __device__ bool small_crc_ok(const uint8_t* r, uint32_t L) {
   return c == t;
 }
 
+// Word k (0..15) of the quad's 64-byte header prefix, read from quad lane k/4's chunk by
+// DPP at the point of use (k is a constant after inlining, so the switch folds away).
+// All four lanes of the quad must be active.
+__device__ __forceinline__ uint32_t prefix_word(const u32x4_t& pf, int k) {
+#define MGENX_PW(K, C, LN) \
+  case K: return (uint32_t)__builtin_amdgcn_mov_dpp((int)pf.C, LN * 0x55, 0xf, 0xf, false);
+  switch (k) {
+    MGENX_PW(0, x, 0) MGENX_PW(1, y, 0) MGENX_PW(2, z, 0) MGENX_PW(3, w, 0)
+    MGENX_PW(4, x, 1) MGENX_PW(5, y, 1) MGENX_PW(6, z, 1) MGENX_PW(7, w, 1)
+    MGENX_PW(8, x, 2) MGENX_PW(9, y, 2) MGENX_PW(10, z, 2) MGENX_PW(11, w, 2)
+    MGENX_PW(12, x, 3) MGENX_PW(13, y, 3) MGENX_PW(14, z, 3) MGENX_PW(15, w, 3)
+    default: return 0u;
+  }
+#undef MGENX_PW
+}
+
+// ---- column stores (quad lane 0 of the record) ----
+
+// The caller's receive check: a CRC mismatch becomes ERROR_CHECKSUM, plus the
+// CHECKSUM_ERROR flag on TCP (mgenTransport.cpp:971-975, 1552-1560).
+__device__ __forceinline__ void crc_verdict(bool crc_ok, bool tcp, uint8_t& err,
+                                            uint8_t& flags) {
+  if (!crc_ok) {
+    err = MGENX_ERROR_CHECKSUM;
+    if (tcp) flags |= MGENX_FLAG_CHECKSUM_ERROR;
+  }
+}
+
+// Fast path: fields straight from the 64-byte prefix words pw (layout accepted by
+// fast_layout) to the columns, each stored as soon as it is extracted so no decoded
+// header is live across the stores.
+template <typename PW>
+__device__ __forceinline__ void store_fast(const mgenx_cols& c, uint64_t i, const PW& pw,
+                                           uint32_t buf_len, bool crc_ok, bool tcp) {
+  const uint32_t D = pw(5) >> 24;
+  const uint32_t hw = (D == 4u) ? pw(7) : pw(10);
+  const uint32_t H = hw >> 24;
+  const uint32_t ht = (hw >> 16) & 0xffu;
+  const bool hv = ht == 1u || ht == 2u;
+  uint8_t flags = (uint8_t)(pw(0) >> 24);
+  uint8_t err = 0;
+  crc_verdict(crc_ok, tcp, err, flags);
+  c.msg_len[i] = bswap16((uint16_t)(pw(0) & 0xffffu));
+  c.flags[i] = flags;
+  c.err[i] = err;
+  c.flow_id[i] = bswap32(pw(1));
+  c.seq_num[i] = bswap32(pw(2));
+  c.tx_sec[i] = bswap32(pw(3));
+  c.tx_usec[i] = bswap32(pw(4));
+  c.dst_port[i] = bswap16((uint16_t)(pw(5) & 0xffffu));
+  c.dst_type[i] = (uint8_t)((pw(5) >> 16) & 0xffu);
+  c.dst_len[i] = (uint8_t)D;
+  c.dst_addr4[i] = pw(6);
+  // GPS + payload_type + payload_len: 16 bytes at word gi = (28 + D + H) / 4
+  const uint32_t gi = (28u + D + H) >> 2;  // 8, 9, 11 or 12
+  // AND/OR masks, not selects: LLVM folds a select chain over pw back into pw[gi + k],
+  // a dynamic index that puts pw in scratch memory
+  const uint32_t m8 = 0u - (uint32_t)(gi == 8u), m9 = 0u - (uint32_t)(gi == 9u);
+  const uint32_t m11 = 0u - (uint32_t)(gi == 11u), m12 = 0u - (uint32_t)(gi == 12u);
+  auto gword = [&](int k) {
+    return (pw(8 + k) & m8) | (pw(9 + k) & m9) | (pw(11 + k) & m11) | (pw(12 + k) & m12);
+  };
+  const uint32_t g3 = gword(3);
+  const uint32_t len = 44u + D + H;
+  uint16_t plen = bswap16((uint16_t)(g3 >> 16));
+  const bool pl_ok = plen != 0 && len + plen <= buf_len;  // mgenMsg.cpp:488-497
+  if (!pl_ok) plen = 0;
+  c.payload_len[i] = plen;
+  c.payload_type[i] = (uint8_t)(g3 >> 8);
+  c.gps_status[i] = (uint8_t)g3;
+  if (c.hdr_len) c.hdr_len[i] = (uint16_t)len;
+  if (c.payload_off) c.payload_off[i] = pl_ok ? len : 0u;  // len % 4 == 0
+  if (c.host_port) c.host_port[i] = hv ? bswap16((uint16_t)(hw & 0xffffu)) : 0;
+  if (c.host_type) c.host_type[i] = hv ? (uint8_t)ht : 0;
+  if (c.host_len) c.host_len[i] = hv ? (uint8_t)H : 0;
+  if (c.lat_raw) c.lat_raw[i] = bswap32(gword(0));
+  if (c.lon_raw) c.lon_raw[i] = bswap32(gword(1));
+  if (c.alt) c.alt[i] = (int32_t)bswap32(gword(2));
+  if (c.dst_addr) {
+    u32x4_t* dp = reinterpret_cast<u32x4_t*>(c.dst_addr + i * 16);
+    const bool d16 = D == 16u;
+    *dp = u32x4_t{pw(6), d16 ? pw(7) : 0u, d16 ? pw(8) : 0u, d16 ? pw(9) : 0u};
+  }
+  if (c.host_addr) {
+    // host address at word 8 (dst IPv4) or 11 (dst IPv6); zero unless a valid type
+    const uint32_t a0 = (!hv || H == 0u) ? 0u : (D == 4u ? pw(8) : pw(11));
+    const bool h16 = hv && H == 16u;  // only with dst IPv4 (D + H <= 20)
+    u32x4_t* hp = reinterpret_cast<u32x4_t*>(c.host_addr + i * 16);
+    *hp = u32x4_t{a0, h16 ? pw(9) : 0u, h16 ? pw(10) : 0u, h16 ? pw(11) : 0u};
+  }
+}
+
+// Fast path, core columns only (the fixed-length kernel): words 0..7 of the prefix, the
+// host word hw and the GPS block's last word g3 (payload_type, payload_len, gps_status).
+__device__ __forceinline__ void store_fast_core(const mgenx_cols& c, uint32_t i,
+                                                const uint32_t (&w)[8], uint32_t hw,
+                                                uint32_t g3, uint32_t buf_len, bool crc_ok,
+                                                bool tcp) {
+  const uint32_t D = w[5] >> 24;
+  uint8_t flags = (uint8_t)(w[0] >> 24);
+  uint8_t err = 0;
+  crc_verdict(crc_ok, tcp, err, flags);
+  c.msg_len[i] = bswap16((uint16_t)(w[0] & 0xffffu));
+  c.flags[i] = flags;
+  c.err[i] = err;
+  c.flow_id[i] = bswap32(w[1]);
+  c.seq_num[i] = bswap32(w[2]);
+  c.tx_sec[i] = bswap32(w[3]);
+  c.tx_usec[i] = bswap32(w[4]);
+  c.dst_port[i] = bswap16((uint16_t)(w[5] & 0xffffu));
+  c.dst_type[i] = (uint8_t)((w[5] >> 16) & 0xffu);
+  c.dst_len[i] = (uint8_t)D;
+  c.dst_addr4[i] = w[6];
+  const uint32_t len = 44u + D + (hw >> 24);
+  uint16_t plen = bswap16((uint16_t)(g3 >> 16));
+  if (!(plen != 0 && len + plen <= buf_len)) plen = 0;  // mgenMsg.cpp:488-497
+  c.payload_len[i] = plen;
+  c.payload_type[i] = (uint8_t)(g3 >> 8);
+  c.gps_status[i] = (uint8_t)g3;
+}
+
+// General path: a header decoded by parse_header.
+__device__ __forceinline__ void store_hdr(const mgenx_cols& c, uint64_t i, const Hdr& h,
+                                          bool crc_ok, bool tcp) {
+  uint8_t err = h.err;
+  uint8_t flags = h.flags;
+  crc_verdict(crc_ok, tcp, err, flags);
+  c.flow_id[i] = h.flow;
+  c.seq_num[i] = h.seq;
+  c.tx_sec[i] = h.sec;
+  c.tx_usec[i] = h.usec;
+  c.msg_len[i] = h.msg_len;
+  c.dst_port[i] = h.dst_port;
+  c.flags[i] = flags;
+  c.err[i] = err;
+  c.dst_type[i] = h.dst_type;
+  c.dst_len[i] = h.dst_len;
+  c.dst_addr4[i] = h.dst4;
+  c.payload_len[i] = h.plen;
+  c.payload_type[i] = h.ptype;
+  c.gps_status[i] = h.gps;
+  if (c.hdr_len) c.hdr_len[i] = h.hdr_len;
+  if (c.payload_off) c.payload_off[i] = h.poff;
+  if (c.host_port) c.host_port[i] = h.host_port;
+  if (c.host_type) c.host_type[i] = h.host_type;
+  if (c.host_len) c.host_len[i] = h.host_len;
+  if (c.lat_raw) c.lat_raw[i] = h.lat;
+  if (c.lon_raw) c.lon_raw[i] = h.lon;
+  if (c.alt) c.alt[i] = h.alt;
+  if (c.host_addr) {
+    u32x4_t* hp = reinterpret_cast<u32x4_t*>(c.host_addr + i * 16);
+    *hp = u32x4_t{h.host_addr[0], h.host_addr[1], h.host_addr[2], h.host_addr[3]};
+  }
+  if (c.dst_addr) {
+    u32x4_t* dp = reinterpret_cast<u32x4_t*>(c.dst_addr + i * 16);
+    *dp = u32x4_t{h.dst_addr[0], h.dst_addr[1], h.dst_addr[2], h.dst_addr[3]};
+  }
+}
+
+// A descriptor pointing outside the slab: ERROR_OOB and zeroed core columns.
+__device__ __forceinline__ void store_oob(const mgenx_cols& c, uint64_t i) {
+  c.err[i] = MGENX_ERROR_OOB;
+  c.flags[i] = 0;
+  c.msg_len[i] = 0;
+  c.flow_id[i] = 0;
+  c.seq_num[i] = 0;
+  c.tx_sec[i] = 0;
+  c.tx_usec[i] = 0;
+  c.dst_port[i] = 0;
+  c.dst_type[i] = 0;
+  c.dst_len[i] = 0;
+  c.dst_addr4[i] = 0;
+  c.payload_len[i] = 0;
+  c.payload_type[i] = 0;
+  c.gps_status[i] = 0;
+}
+
 // MODE (diagnostic ablations, never the product path): 0 = full kernel, 1 = row loads +
 // XOR only (no LDS table lookups), 2 = table lookups on one L1-resident row (no streaming).
 // pw[4*LN .. 4*LN+3] = quad lane LN's 16-byte prefix chunk (DPP quad_perm broadcast; all
@@ -475,168 +652,353 @@ unpack_kernel(UnpackParams p) {
 
     uint32_t pw[16];
     gather(pw);
-    // each parse path stores its own columns (no join merging two Hdr values)
-    auto store = [&](const Hdr& h) {
-      bool crc_ok = true;
-      if (needs_crc) crc_ok = vec_crc ? (tot == expect) : small_crc_ok(rec, L);
-      uint8_t err = h.err;
-      uint8_t flags = h.flags;
-      if (!crc_ok) {
-        err = MGENX_ERROR_CHECKSUM;
-        if (tcp) flags |= MGENX_FLAG_CHECKSUM_ERROR;
-      }
-      const mgenx_cols& c = p.cols;
-      c.flow_id[rec_idx] = h.flow;
-      c.seq_num[rec_idx] = h.seq;
-      c.tx_sec[rec_idx] = h.sec;
-      c.tx_usec[rec_idx] = h.usec;
-      c.msg_len[rec_idx] = h.msg_len;
-      c.dst_port[rec_idx] = h.dst_port;
-      c.flags[rec_idx] = flags;
-      c.err[rec_idx] = err;
-      c.dst_type[rec_idx] = h.dst_type;
-      c.dst_len[rec_idx] = h.dst_len;
-      c.dst_addr4[rec_idx] = h.dst4;
-      c.payload_len[rec_idx] = h.plen;
-      c.payload_type[rec_idx] = h.ptype;
-      c.gps_status[rec_idx] = h.gps;
-      if (c.hdr_len) c.hdr_len[rec_idx] = h.hdr_len;
-      if (c.payload_off) c.payload_off[rec_idx] = h.poff;
-      if (c.host_port) c.host_port[rec_idx] = h.host_port;
-      if (c.host_type) c.host_type[rec_idx] = h.host_type;
-      if (c.host_len) c.host_len[rec_idx] = h.host_len;
-      if (c.lat_raw) c.lat_raw[rec_idx] = h.lat;
-      if (c.lon_raw) c.lon_raw[rec_idx] = h.lon;
-      if (c.alt) c.alt[rec_idx] = h.alt;
-      if (c.host_addr) {
-        u32x4_t* hp = reinterpret_cast<u32x4_t*>(c.host_addr + rec_idx * 16);
-        *hp = u32x4_t{h.host_addr[0], h.host_addr[1], h.host_addr[2], h.host_addr[3]};
-      }
-      if (c.dst_addr) {
-        u32x4_t* dp = reinterpret_cast<u32x4_t*>(c.dst_addr + rec_idx * 16);
-        *dp = u32x4_t{h.dst_addr[0], h.dst_addr[1], h.dst_addr[2], h.dst_addr[3]};
-      }
-    };
-    // fast path: fields straight from the gathered prefix words to the columns, stored as
-    // soon as each is extracted (no Hdr value live across the stores)
-    auto store_fast = [&]() {
-      const mgenx_cols& c = p.cols;
-      const uint32_t D = pw[5] >> 24;
-      const uint32_t hw = (D == 4u) ? pw[7] : pw[10];
-      const uint32_t H = hw >> 24;
-      const uint32_t ht = (hw >> 16) & 0xffu;
-      const bool hv = ht == 1u || ht == 2u;
-      bool crc_ok = true;
-      if (needs_crc) crc_ok = tot == expect;  // buf_len >= 64: always the vector CRC
-      uint8_t flags = (uint8_t)(pw[0] >> 24);
-      uint8_t err = 0;
-      if (!crc_ok) {
-        err = MGENX_ERROR_CHECKSUM;
-        if (tcp) flags |= MGENX_FLAG_CHECKSUM_ERROR;
-      }
-      c.msg_len[rec_idx] = bswap16((uint16_t)(pw[0] & 0xffffu));
-      c.flags[rec_idx] = flags;
-      c.err[rec_idx] = err;
-      c.flow_id[rec_idx] = bswap32(pw[1]);
-      c.seq_num[rec_idx] = bswap32(pw[2]);
-      c.tx_sec[rec_idx] = bswap32(pw[3]);
-      c.tx_usec[rec_idx] = bswap32(pw[4]);
-      c.dst_port[rec_idx] = bswap16((uint16_t)(pw[5] & 0xffffu));
-      c.dst_type[rec_idx] = (uint8_t)((pw[5] >> 16) & 0xffu);
-      c.dst_len[rec_idx] = (uint8_t)D;
-      c.dst_addr4[rec_idx] = pw[6];
-      // GPS + payload_type + payload_len: 16 bytes at word gi = (28 + D + H) / 4
-      const uint32_t gi = (28u + D + H) >> 2;  // 8, 9, 11 or 12
-      // AND/OR masks, not selects: LLVM folds a select chain over pw back into pw[gi + k],
-      // a dynamic index that puts pw in scratch memory
-      const uint32_t m8 = 0u - (uint32_t)(gi == 8u), m9 = 0u - (uint32_t)(gi == 9u);
-      const uint32_t m11 = 0u - (uint32_t)(gi == 11u), m12 = 0u - (uint32_t)(gi == 12u);
-      auto gword = [&](int k) {
-        return (pw[8 + k] & m8) | (pw[9 + k] & m9) | (pw[11 + k] & m11) | (pw[12 + k] & m12);
-      };
-      const uint32_t g3 = gword(3);
-      const uint32_t len = 44u + D + H;
-      uint16_t plen = bswap16((uint16_t)(g3 >> 16));
-      const bool pl_ok = plen != 0 && len + plen <= buf_len;
-      if (!pl_ok) plen = 0;
-      c.payload_len[rec_idx] = plen;
-      c.payload_type[rec_idx] = (uint8_t)(g3 >> 8);
-      c.gps_status[rec_idx] = (uint8_t)g3;
-      if (c.hdr_len) c.hdr_len[rec_idx] = (uint16_t)len;
-      if (c.payload_off) c.payload_off[rec_idx] = pl_ok ? len : 0u;  // len % 4 == 0
-      if (c.host_port) c.host_port[rec_idx] = hv ? bswap16((uint16_t)(hw & 0xffffu)) : 0;
-      if (c.host_type) c.host_type[rec_idx] = hv ? (uint8_t)ht : 0;
-      if (c.host_len) c.host_len[rec_idx] = hv ? (uint8_t)H : 0;
-      if (c.lat_raw)
-        c.lat_raw[rec_idx] = bswap32(gword(0));
-      if (c.lon_raw)
-        c.lon_raw[rec_idx] = bswap32(gword(1));
-      if (c.alt)
-        c.alt[rec_idx] = (int32_t)bswap32(gword(2));
-      if (c.dst_addr) {
-        u32x4_t* dp = reinterpret_cast<u32x4_t*>(c.dst_addr + rec_idx * 16);
-        const bool d16 = D == 16u;
-        *dp = u32x4_t{pw[6], d16 ? pw[7] : 0u, d16 ? pw[8] : 0u, d16 ? pw[9] : 0u};
-      }
-      if (c.host_addr) {
-        // host address at word 8 (dst IPv4) or 11 (dst IPv6); zero unless a valid type
-        const uint32_t a0 = (!hv || H == 0u) ? 0u : (D == 4u ? pw[8] : pw[11]);
-        const bool h16 = hv && H == 16u;  // only with dst IPv4 (D + H <= 20)
-        u32x4_t* hp = reinterpret_cast<u32x4_t*>(c.host_addr + rec_idx * 16);
-        *hp = u32x4_t{a0, h16 ? pw[9] : 0u, h16 ? pw[10] : 0u, h16 ? pw[11] : 0u};
-      }
-    };
     if (live && q == 0) {
+      // each parse path stores its own columns (no join merging two header values)
       if (pfx64 && fast_layout(pw[0], pw[5], (pw[5] >> 24) == 4u ? pw[7] : pw[10])) {
-        store_fast();
+        store_fast(p.cols, rec_idx, [&](int k) { return pw[k]; }, buf_len,
+                   !needs_crc || tot == expect, tcp);
       } else {
         Hdr h;
         unpack_words(pw);
         parse_header(rec, buf_len, want_ext, w, h);
-        store(h);
+        const bool crc_ok =
+            !needs_crc || (vec_crc ? (tot == expect) : small_crc_ok(rec, L));
+        store_hdr(p.cols, rec_idx, h, crc_ok, tcp);
       }
     } else if (oob && q == 0) {
-      const mgenx_cols& c = p.cols;
-      c.err[rec_idx] = MGENX_ERROR_OOB;
-      c.flags[rec_idx] = 0;
-      c.msg_len[rec_idx] = 0;
-      c.flow_id[rec_idx] = 0;
-      c.seq_num[rec_idx] = 0;
-      c.tx_sec[rec_idx] = 0;
-      c.tx_usec[rec_idx] = 0;
-      c.dst_port[rec_idx] = 0;
-      c.dst_type[rec_idx] = 0;
-      c.dst_len[rec_idx] = 0;
-      c.dst_addr4[rec_idx] = 0;
-      c.payload_len[rec_idx] = 0;
-      c.payload_type[rec_idx] = 0;
-      c.gps_status[rec_idx] = 0;
+      store_oob(p.cols, rec_idx);
+    }
+  }
+}
+
+
+// ---------------------------------------------------------------------------------------
+// Fixed-length records (fixed stride, one length L in [65, 1024]; BASELINE config 2 and
+// the recvmmsg fixed-slot layout), software-pipelined across groups.  With one L every
+// group has the same row geometry (V = ceil(L/64) rows, padded to the template's NR), so
+// while a wave consumes row j of group g it reloads the register with row j of its next
+// group g' = g + n_waves: the wave keeps ~NR x 1 KiB of loads in flight through its own
+// LDS-bound CRC work and tail, at no register cost.  The header of g' is issued at the top
+// of g (before g's reloads), so with in-order completion the CRC decision for g' waits for
+// that header only, and row j of g' waits only for row j.
+// Semantics are those of unpack_kernel<true> (same helpers, same column stores).
+// MODE (ablations): 1 = loads + XOR only (no LDS lookups), 5 = MODE 1 without the tail
+// (no decode, no column stores; the CRC word is kept alive through one store per wave)
+template <int NR, int MODE = 0>
+__global__ void __launch_bounds__(kUnpackThreads)
+unpack_fixed_kernel(UnpackParams p, uint32_t expect) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  uint32_t* rep = lds;
+  uint32_t* fold = lds + kRepDwords;  // [A4 | A8 | A12 | A16 | A32 | A48]
+  for (int e = threadIdx.x; e < 1024; e += blockDim.x) {
+    const uint32_t v = p.tabs[e];
+    u32x4_t s = {v, v, v, v};
+    u32x4_t* dst = reinterpret_cast<u32x4_t*>(rep + (size_t)e * kRep);
+#pragma unroll
+    for (int c = 0; c < kRep / 4; c++) dst[c] = s;
+  }
+  for (int e = threadIdx.x; e < kFoldTabs * 1024; e += blockDim.x) fold[e] = p.tabs[1024 + e];
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  const int q = lane & 3;
+  const uint32_t copy = (uint32_t)(lane & 31);
+  const uint32_t wave_id = __builtin_amdgcn_readfirstlane(
+      blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  const uint32_t n_waves = gridDim.x * (blockDim.x >> 6);
+  const uint32_t n_groups = (p.n + 15u) >> 4;
+  const bool force = (p.opts & MGENX_OPT_CHECKSUM_FORCE) != 0;
+  const bool tcp = (p.opts & MGENX_OPT_TCP) != 0;
+  const uint32_t L = p.fixed_len;          // host guarantees 65 <= L <= 1024
+  constexpr int V = NR;                    // rows: ceil(L / 64), 2..16 (host-checked)
+
+  // Each wave owns a contiguous run of groups, so the column lines it writes (16 records
+  // per group: 16..64 B of a 128-B line) are completed by consecutive iterations of one
+  // wave instead of by up to 8 waves at different times.
+  const uint32_t chunk = (n_groups + n_waves - 1) / n_waves;
+  uint32_t g = wave_id * chunk;
+  const uint32_t g_end = min(n_groups, g + chunk);
+  if (g >= g_end) return;
+
+  // Geometry.  Every load is slab (uniform SGPR base) + 32-bit per-lane offset + constant:
+  // the saddr form, one VGPR per address (host guarantees slab_bytes < 4 GiB).  A dead
+  // lane (past the batch or outside the slab) reads at base offset 64 instead, inside the
+  // slab (host guarantees slab_bytes >= 64 (NR + 1) + 16).
+  auto rec_idx = [&](uint32_t gg) { return (gg << 4) + (uint32_t)(lane >> 2); };
+  auto rec_ptr = [&](uint32_t i) { return p.slab + (uint64_t)i * p.stride; };
+  auto is_live = [&](uint32_t i) {
+    const uint64_t off = (uint64_t)i * p.stride;
+    return i < p.n && off <= p.slab_bytes && L <= p.slab_bytes - off;
+  };
+  auto base_off = [&](bool lv, uint32_t i) { return lv ? i * (uint32_t)p.stride : 64u; };
+  // lane's byte offset of row 0 (> -64; < 0 when row 0 starts before the record)
+  const int pos0 = (int)L - 64 * V + 16 * q;
+  auto ld = [&](uint32_t off, int imm) { return ldu128(p.slab + (uint64_t)off + imm); };
+  // row j of the record at boff (row 0 clamped to the record start).  Rows j >= 1 start at
+  // boff + pos0 + 64 j with pos0 + 64 > 0: the 32-bit part must stay non-negative (it is
+  // zero-extended), so the constant part is 64 (j - 1).
+  auto ld_row = [&](uint32_t boff, int j) {
+    return j == 0 ? ld(boff + (uint32_t)(pos0 > 0 ? pos0 : 0), 0)
+                  : ld(boff + (uint32_t)(pos0 + 64), 64 * (j - 1));
+  };
+  auto ld_hdr = [&](uint32_t boff) { return ld(boff + 16u * (uint32_t)q, 0); };
+
+  u32x4_t d[NR];
+  // Decode + store one record per quad.  Every lane runs the same instructions: the header
+  // words come by DPP from the quad's prefix chunks (a DPP read of an inactive lane returns
+  // stale data), the rare general layouts are parsed by quad lane 0 and broadcast, and the
+  // four lanes of a quad store four different columns, five store instructions per group
+  // with no branch around them.  (gfx950 counts stores in vmcnt: a store that might be
+  // skipped makes LLVM's wait counts assume it was, so the next row wait would also wait
+  // for the store's acknowledgement.)  Lanes past the batch end write to the sink.
+  auto tail = [&](const u32x4_t& pf, uint32_t idx, bool live, bool needs_crc, uint32_t tot) {
+    uint32_t w[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) w[j] = prefix_word(pf, j);
+    const uint32_t w10 = prefix_word(pf, 10);
+    const uint32_t D = w[5] >> 24;
+    const uint32_t hw = (D == 4u) ? w[7] : w10;
+    const uint32_t gi = (28u + D + (hw >> 24)) >> 2;  // GPS block word (fast layouts)
+    const uint32_t g3 = (prefix_word(pf, 11) & (0u - (uint32_t)(gi == 8u))) |
+                        (prefix_word(pf, 12) & (0u - (uint32_t)(gi == 9u))) |
+                        (prefix_word(pf, 14) & (0u - (uint32_t)(gi == 11u))) |
+                        (prefix_word(pf, 15) & (0u - (uint32_t)(gi == 12u)));
+    // fast layout (mgenMsg.cpp:323-497 with every field word-aligned)
+    uint32_t flow = bswap32(w[1]), seq = bswap32(w[2]), sec = bswap32(w[3]);
+    uint32_t usec = bswap32(w[4]), dst4 = w[6];
+    uint32_t msg_len = bswap16((uint16_t)(w[0] & 0xffffu));
+    uint32_t dport = bswap16((uint16_t)(w[5] & 0xffffu));
+    const uint32_t hlen = 44u + D + (hw >> 24);
+    uint32_t plen = bswap16((uint16_t)(g3 >> 16));
+    if (!(plen != 0 && hlen + plen <= L)) plen = 0;  // mgenMsg.cpp:488-497
+    uint32_t flags = w[0] >> 24, err = 0, dtype = (w[5] >> 16) & 0xffu, dlen = D;
+    uint32_t ptype = (g3 >> 8) & 0xffu, gps = g3 & 0xffu;
+    // general layouts: quad lane 0 parses (with loads), then broadcasts to its quad
+    const bool slow = live && !fast_layout(w[0], w[5], hw);
+    if (__any(slow)) {
+      Hdr h;
+      if (slow && q == 0) parse_header(rec_ptr(idx), L, false, w, h);
+      auto bc = [&](uint32_t& dst, uint32_t v) {
+        v = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x00, 0xf, 0xf, false);
+        if (slow) dst = v;
+      };
+      bc(flow, h.flow); bc(seq, h.seq); bc(sec, h.sec); bc(usec, h.usec); bc(dst4, h.dst4);
+      bc(msg_len, h.msg_len); bc(dport, h.dst_port); bc(plen, h.plen); bc(flags, h.flags);
+      bc(err, h.err); bc(dtype, h.dst_type); bc(dlen, h.dst_len); bc(ptype, h.ptype);
+      bc(gps, h.gps);
+    }
+    if (needs_crc && tot != expect) {  // the caller's receive check (mgenTransport.cpp:971)
+      err = MGENX_ERROR_CHECKSUM;
+      if (tcp) flags |= MGENX_FLAG_CHECKSUM_ERROR;
+    }
+    if (!live) {  // descriptor outside the slab (or past the batch end)
+      flow = seq = sec = usec = dst4 = msg_len = dport = plen = flags = dtype = dlen = 0;
+      ptype = gps = 0;
+      err = MGENX_ERROR_OOB;
+    }
+    const bool in = idx < p.n;
+    const uint64_t sink = (uint64_t)p.sink + 4u * (uint32_t)lane;
+    auto at = [&](uint64_t base, uint32_t size) {
+      return in ? base + (uint64_t)idx * size : sink;
+    };
+    const mgenx_cols& c = p.cols;
+    const uint64_t u32 = pick4(q, (uint64_t)c.flow_id, (uint64_t)c.seq_num, (uint64_t)c.tx_sec,
+                               (uint64_t)c.tx_usec);
+    const uint64_t u16 = pick4(q, (uint64_t)c.msg_len, (uint64_t)c.dst_port,
+                               (uint64_t)c.payload_len, (uint64_t)c.payload_len);
+    const uint64_t u8a = pick4(q, (uint64_t)c.flags, (uint64_t)c.err, (uint64_t)c.dst_type,
+                               (uint64_t)c.dst_len);
+    const uint64_t u8b = pick4(q, (uint64_t)c.payload_type, (uint64_t)c.gps_status,
+                               (uint64_t)c.payload_type, (uint64_t)c.gps_status);
+    // u32: flow, seq, tx_sec, tx_usec (lane q -> column q); then dst_addr4 (all lanes)
+    st_g32(at(u32, 4), q == 0 ? flow : q == 1 ? seq : q == 2 ? sec : usec);
+    st_g32(at((uint64_t)c.dst_addr4, 4), dst4);
+    // u16: msg_len, dst_port, payload_len (lane 3 repeats lane 2's store)
+    st_g16(at(u16, 2), q == 0 ? msg_len : q == 1 ? dport : plen);
+    // u8: flags, err, dst_type, dst_len; then payload_type, gps_status (lanes 2,3 repeat)
+    st_g8(at(u8a, 1), q == 0 ? flags : q == 1 ? err : q == 2 ? dtype : dlen);
+    st_g8(at(u8b, 1), (q & 1) == 0 ? ptype : gps);
+  };
+  // the receive-side CRC decision from words 0 and 5 (mgenTransport.cpp:960-963)
+  auto decide = [&](const u32x4_t& pf, bool live) {
+    const uint32_t w0 = prefix_word(pf, 0);
+    const uint32_t w5 = prefix_word(pf, 5);
+    const bool v2 = ((w0 >> 16) & 0xffu) == 2u;
+    const bool flagged = force || ((((w0 >> 24) & MGENX_FLAG_CHECKSUM) != 0) && v2);
+    const uint32_t t = (w5 >> 16) & 0xffu;
+    return live && flagged && (tcp || (v2 && (t == 1u || t == 2u)));
+  };
+
+  u32x4_t pf;
+  while (g < g_end) {
+    // ---- pipelined mode: rows of every group speculatively in flight one group ahead.
+    // No load in this loop is conditional (a conditional reload makes LLVM copy the row
+    // registers at the join, and a copy of an in-flight load drains the whole queue).
+    uint32_t idx = rec_idx(g);
+    bool live = is_live(idx);
+    {
+      const uint32_t boff = base_off(live, idx);
+      pf = ld_hdr(boff);
+#pragma unroll
+      for (int j = 0; j < NR; j++) d[j] = ld_row(boff, j);
+    }
+    // one pipelined group; the header registers alternate between two variables (the loop
+    // is unrolled twice) so the next header never needs a register copy
+    auto step = [&](const u32x4_t& pf_cur, u32x4_t& pf_nxt) {
+      const uint32_t gn = g + 1;
+      const bool has_next = gn < g_end;
+      const uint32_t idx_n = rec_idx(has_next ? gn : g);
+      const bool live_n = has_next && is_live(idx_n);
+      // next group's header first (completes before any of its rows)
+      const uint32_t boff_n = base_off(live_n, idx_n);
+      pf_nxt = ld_hdr(boff_n);
+      asm volatile("" ::: "memory");
+      const bool needs_crc = decide(pf_cur, live);
+      const bool any = __any(needs_crc);
+
+      uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+#pragma unroll
+      for (int j = 0; j < NR - 1; j++) {
+        u32x4_t x = d[j];
+        if (j == 0) {
+          const int s0 = -pos0;
+          if (s0 > 0) {
+            const u32x4_t zero = {0u, 0u, 0u, 0u};
+            x = s0 < 16 ? shl_bytes(x, s0) : zero;
+          }
+        }
+        uint32_t c4[4];
+        if (MODE == 1 || MODE == 5) {
+          c4[0] = (h0 << 1) ^ x.x; c4[1] = (h1 << 1) ^ x.y;
+          c4[2] = (h2 << 1) ^ x.z; c4[3] = (h3 << 1) ^ x.w;
+        } else {
+          c4[0] = h0 ^ x.x; c4[1] = h1 ^ x.y; c4[2] = h2 ^ x.z; c4[3] = h3 ^ x.w;
+        }
+        // row j of g is dead now: reload its register for g' (same physical register, so
+        // no loop-carried copy -- a copy of an in-flight load would drain the queue)
+        __builtin_amdgcn_sched_barrier(0);
+        d[j] = ld_row(boff_n, j);
+        __builtin_amdgcn_sched_barrier(0);
+        if (MODE == 1 || MODE == 5) {
+          h0 = c4[0]; h1 = c4[1]; h2 = c4[2]; h3 = c4[3];
+          continue;
+        }
+        uint32_t t[16];
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          t[4 * b + 0] = rep[((c4[b] & 0xffu) << 5) | copy];
+          t[4 * b + 1] = rep[8192 + ((((c4[b] >> 8) & 0xffu) << 5) | copy)];
+          t[4 * b + 2] = rep[16384 + ((((c4[b] >> 16) & 0xffu) << 5) | copy)];
+          t[4 * b + 3] = rep[24576 + (((c4[b] >> 24) << 5) | copy)];
+        }
+        h0 = t[0] ^ t[1] ^ t[2] ^ t[3];
+        h1 = t[4] ^ t[5] ^ t[6] ^ t[7];
+        h2 = t[8] ^ t[9] ^ t[10] ^ t[11];
+        h3 = t[12] ^ t[13] ^ t[14] ^ t[15];
+      }
+      // final row (V >= 2, so never row 0): the big-endian trailer goes to stream order
+      const u32x4_t xf = d[NR - 1];
+      const uint32_t f0 = h0 ^ xf.x, f1 = h1 ^ xf.y, f2 = h2 ^ xf.z;
+      const uint32_t f3 = h3 ^ (q == 3 ? bswap32(xf.w) : xf.w);
+      __builtin_amdgcn_sched_barrier(0);
+      d[NR - 1] = ld_row(boff_n, NR - 1);
+      __builtin_amdgcn_sched_barrier(0);
+      const uint32_t v = shift_tab(fold + 3 * 1024, f0) ^ shift_tab(fold + 2 * 1024, f1) ^
+                         shift_tab(fold + 1 * 1024, f2) ^ shift_tab(fold, f3);
+      const uint32_t* lt = fold + (q == 0 ? 5 : (q == 1 ? 4 : 3)) * 1024;  // A48/A32/A16
+      uint32_t s = (q == 3) ? v : shift_tab(lt, v);
+      s ^= __shfl_xor(s, 1);
+      s ^= __shfl_xor(s, 2);
+      if (MODE == 5) {
+        if (s == 0x9E3779B9u && lane == 0) p.cols.err[idx] = (uint8_t)needs_crc;  // keep alive
+      } else {
+        tail(pf_cur, idx, live, needs_crc, s);
+      }
+      g = gn;
+      idx = idx_n;
+      live = live_n;
+      // a group without any checksummed record: stop streaming bodies (the rows of g' in
+      // flight are simply overwritten later)
+      return has_next && any;
+    };
+    u32x4_t pf2;
+    for (;;) {
+      if (!step(pf, pf2)) break;
+      if (!step(pf2, pf)) break;
+    }
+    // ---- header-only mode: header first, bodies only for groups that need the CRC
+    for (; g < g_end; g++) {
+      const uint32_t i = rec_idx(g);
+      const bool lv = is_live(i);
+      const u32x4_t ph = ld_hdr(base_off(lv, i));
+      const bool nc = decide(ph, lv);
+      if (__any(nc)) break;  // back to pipelined mode at this group
+      tail(ph, i, lv, false, 0u);
     }
   }
 }
 
 int unpack_variant = 0;
 
-template <int MODE>
-static hipError_t launch_mode(const UnpackParams& p, int grid, hipStream_t stream) {
-  static bool attr_done = false;
+template <typename K>
+static hipError_t launch_lds(K kernel, bool& attr_done, const UnpackParams& p, int grid,
+                             hipStream_t stream) {
   if (!attr_done) {
-    hipError_t e = hipFuncSetAttribute((const void*)unpack_kernel<true, MODE>,
+    hipError_t e = hipFuncSetAttribute((const void*)kernel,
                                        hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)kUnpackLdsBytes);
     if (e != hipSuccess) return e;
     attr_done = true;
   }
-  hipLaunchKernelGGL((unpack_kernel<true, MODE>), dim3(grid), dim3(kUnpackThreads),
-                     kUnpackLdsBytes, stream, p);
+  hipLaunchKernelGGL(kernel, dim3(grid), dim3(kUnpackThreads), kUnpackLdsBytes, stream, p);
   return hipGetLastError();
 }
+
+template <int MODE>
+static hipError_t launch_mode(const UnpackParams& p, int grid, hipStream_t stream) {
+  static bool attr_done = false;
+  return launch_lds(unpack_kernel<true, MODE>, attr_done, p, grid, stream);
+}
+
+template <int NR, int MODE = 0>
+static hipError_t launch_fixed(const UnpackParams& p, int grid, hipStream_t stream) {
+  static bool attr_done = false;
+  if (!attr_done) {
+    hipError_t e = hipFuncSetAttribute((const void*)unpack_fixed_kernel<NR, MODE>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)kUnpackLdsBytes);
+    if (e != hipSuccess) return e;
+    attr_done = true;
+  }
+  hipLaunchKernelGGL((unpack_fixed_kernel<NR, MODE>), dim3(grid), dim3(kUnpackThreads),
+                     kUnpackLdsBytes, stream, p, p.expect_fixed);
+  return hipGetLastError();
+}
+
+typedef hipError_t (*fixed_launcher)(const UnpackParams&, int, hipStream_t);
+static const fixed_launcher kFixedLaunch[17] = {
+    nullptr,          nullptr,          launch_fixed<2>,  launch_fixed<3>,  launch_fixed<4>,
+    launch_fixed<5>,  launch_fixed<6>,  launch_fixed<7>,  launch_fixed<8>,  launch_fixed<9>,
+    launch_fixed<10>, launch_fixed<11>, launch_fixed<12>, launch_fixed<13>, launch_fixed<14>,
+    launch_fixed<15>, launch_fixed<16>};
 
 hipError_t launch_unpack(const UnpackParams& p, int grid, hipStream_t stream) {
   if (p.opts & MGENX_OPT_SKIP_CRC) {
     hipLaunchKernelGGL((unpack_kernel<false>), dim3(grid), dim3(kUnpackThreads), 0, stream, p);
     return hipGetLastError();
   }
+  // fixed stride + one length in [65, 1024] + core columns: the pipelined kernel
+  const mgenx_cols& c = p.cols;
+  const bool ext = c.hdr_len || c.payload_off || c.host_port || c.host_type || c.host_len ||
+                   c.lat_raw || c.lon_raw || c.alt || c.dst_addr || c.host_addr;
+  const uint32_t nr = (p.fixed_len + 63) / 64;
+  const bool fixed = !p.rec_off && !p.rec_len && p.fixed_len >= 65 && p.fixed_len <= 1024 &&
+                     p.stride > 0 && p.n <= 0xFFFFFFF0u && !ext &&
+                     p.slab_bytes < 0xFFFF0000ull && p.slab_bytes >= 64ull * (nr + 1) + 16 &&
+                     p.slab_bytes >= p.fixed_len;
+  if (unpack_variant == 0 && fixed) return kFixedLaunch[(p.fixed_len + 63) / 64](p, grid, stream);
+  if (unpack_variant == 4 && fixed && p.fixed_len == 1024) return launch_fixed<16, 1>(p, grid, stream);
+  if (unpack_variant == 5 && fixed && p.fixed_len == 1024) return launch_fixed<16, 5>(p, grid, stream);
   switch (unpack_variant) {
     case 1: return launch_mode<1>(p, grid, stream);
     case 2: return launch_mode<2>(p, grid, stream);

@@ -214,3 +214,54 @@ def test_oob_records_are_flagged_not_read(torch, eng):
     lens = torch.tensor([64, 200, 10], dtype=torch.int32, device="cuda")
     c = host_cols(eng.unpack(slab, 3, rec_off=offs, rec_len=lens), 3)
     assert c["err"].tolist() == [1, ERROR_OOB, ERROR_OOB]
+
+
+FIXED_SIZES = [65, 100, 127, 128, 200, 255, 256, 511, 777, 1000, 1023, 1024]
+
+
+@pytest.mark.parametrize("size", FIXED_SIZES)
+def test_fixed_len_pipelined_vs_oracle(torch, eng, gold, size):
+    """The pipelined fixed-length kernel (fixed stride, one length, core columns) against the
+    oracle: every golden template layout, checksum on/off and caller CHECKSUM flag mixed,
+    bit flips / bad version / bad dst type, a partial last group and records past the end
+    of the slab (ERROR_OOB), under the UDP, forced-UDP and TCP receive rules."""
+    from mgen_amd import ERROR_OOB, OPT_CHECKSUM_FORCE, OPT_TCP
+    from oracle import oracle as O
+    tmpl, pool = gold["tmpl"], gold["pool"]
+    n = 16 * 37 + 7
+    rng = np.random.default_rng(size)
+    desc = np.zeros(n, gold["desc"].dtype)
+    desc["tmpl"] = rng.integers(0, len(tmpl), n)
+    desc["seq_num"] = np.arange(n) * 3 + 1
+    desc["tx_sec"] = 1_700_000_000 + np.arange(n) // 100
+    desc["tx_usec"] = rng.integers(0, 1_000_000, n)
+    desc["msg_len"] = size
+    desc["flags"] = rng.choice([0, 4], n)
+    a, _ = O.udp_pack_batch(tmpl, desc, pool, n * size, stride=size, checksum=True)
+    b, _ = O.udp_pack_batch(tmpl, desc, pool, n * size, stride=size, checksum=False)
+    recs = np.where((rng.random(n) < 0.7)[:, None], a.reshape(n, size), b.reshape(n, size))
+    flip = np.nonzero(rng.random(n) < 0.1)[0]
+    pos = rng.integers(0, size, flip.size)
+    recs[flip, pos] ^= (1 << rng.integers(0, 8, flip.size)).astype(np.uint8)
+    recs[rng.random(n) < 0.02, 2] = 3          # version
+    recs[rng.random(n) < 0.02, 22] = 7         # dst type
+    host = np.ascontiguousarray(recs).reshape(-1)
+    n_oob = 3
+    slab_bytes = (n - n_oob) * size + size // 2   # last record straddles the end
+    slab = dev(torch, host).view(torch.uint8)
+    for opts in (0, OPT_CHECKSUM_FORCE, OPT_TCP | OPT_CHECKSUM_FORCE):
+        f = O.udp_recv_batch(host, n, stride=size, fixed_len=size,
+                             force=bool(opts & OPT_CHECKSUM_FORCE), tcp=bool(opts & OPT_TCP))
+        cols = eng.unpack(slab, n, stride=size, fixed_len=size, opts=opts,
+                          slab_bytes=slab_bytes)
+        c = host_cols(cols, n)
+        live = n - n_oob
+        for gname, oname, dt in COLMAP[:13]:
+            got = c[gname].view(dt)[:live]
+            want = f[oname].astype(dt)[:live]
+            bad = np.nonzero(got != want)[0]
+            assert bad.size == 0, (size, opts, gname, bad[:8], got[bad[:4]], want[bad[:4]])
+        assert np.array_equal(c["dst_addr4"].view(np.uint8).reshape(-1, 4)[:live],
+                              f["dst_addr"][:live, :4])
+        assert np.all(c["err"][live:] == ERROR_OOB)
+        assert np.all(c["msg_len"].view(np.uint16)[live:] == 0)
