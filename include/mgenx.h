@@ -169,6 +169,29 @@ int mgenx_pack_batch(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
 int mgenx_crc32_batch(mgenx_ctx* ctx, const uint8_t* dev_data, const uint64_t* dev_off,
                       const uint32_t* dev_len, uint32_t n, uint32_t* dev_out, void* stream);
 
+/* ---- stream framing (TCP / SINK record boundaries) ----
+ * mgenx_stream_scan finds the record chain of a byte stream from offset 0 exactly as the
+ * reference receivers frame it -- TCP: MgenTcpTransport::GetRxNumBytes / OnRecvMsg
+ * (src/common/mgenTransport.cpp:1683-1760; msg_len < 4 is a stream error that stops the
+ * scan); SINK: MgenAppSinkTransport::OnInputReady (src/common/mgenAppSinkTransport.cpp:
+ * 369-434; msg_len outside [28, 8192] skips the 2 length bytes) -- and writes the records'
+ * offsets and lengths in stream order (the first `cap` of them).  The output feeds
+ * mgenx_unpack_batch directly (rec_off / rec_len; MGENX_OPT_TCP for TCP streams).
+ * Synchronous on `stream` (the record count decides the launches); the context keeps a
+ * workspace that grows with the stream (about 1/32 of its size). */
+#define MGENX_SCAN_TCP  0
+#define MGENX_SCAN_SINK 1
+typedef struct mgenx_scan_info {
+  uint64_t n_records;   /* records found (only the first `cap` are written) */
+  uint64_t consumed;    /* bytes consumed: offset just past the last whole record/skip */
+  int32_t  status;      /* 0 = ok, 1 = TCP record with msg_len < 4 (scan stopped there) */
+  uint32_t candidates;  /* diagnostic: plausible starts found by the parallel pass */
+  uint64_t resolved;    /* diagnostic: records framed by the sequential resolver */
+} mgenx_scan_info;
+int mgenx_stream_scan(mgenx_ctx* ctx, const uint8_t* dev_stream, uint64_t nbytes, int mode,
+                      uint64_t* dev_rec_off, uint32_t* dev_rec_len, uint64_t cap,
+                      mgenx_scan_info* info, void* stream);
+
 /* Tuning knobs (process-wide; for benchmarking kernel variants).  MGENX_TUNE_UNPACK_VARIANT:
  * 0 = automatic (pipelined fixed-length kernel when the batch qualifies), 1/2 = ablations
  * of the general kernel (loads+XOR only / lookups on cached rows), 3 = general kernel,

@@ -15,7 +15,7 @@ from ._abi import (  # noqa: F401
     COLS_CORE, COLS_EXT, DESC_DTYPE, TMPL_DTYPE, MgenxCols, ERROR_CHECKSUM, ERROR_DSTADDR,
     ERROR_LENGTH, ERROR_NONE, ERROR_OOB, ERROR_VERSION, FLAG_CHECKSUM, FLAG_CHECKSUM_ERROR,
     FLAG_LAST_BUFFER, OPT_CHECKSUM_FORCE, OPT_SKIP_CRC, OPT_TCP, PACK_CHECKSUM,
-    PACK_RANDOM_FILL,
+    PACK_RANDOM_FILL, SCAN_SINK, SCAN_TCP, ScanInfo,
 )
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -58,8 +58,7 @@ def load():
     L.mgenx_crc32_batch.argtypes = [P, P, P, P, u32, P, P]
     L.mgenx_set_tuning.argtypes = [P, i32, i32]
     L.mgenx_diag_stream_read.argtypes = [P, P, u64, P, i32, P]
-    if hasattr(L, "mgenx_stream_scan"):
-        L.mgenx_stream_scan.argtypes = [P, P, u64, u64, u32, u32, P, P, P, P, P, u32, P]
+    L.mgenx_stream_scan.argtypes = [P, P, u64, i32, P, P, u64, ctypes.POINTER(ScanInfo), P]
     _lib = L
     return L
 
@@ -166,6 +165,23 @@ class Engine:
         rc = self.lib.mgenx_diag_stream_read(self.ctx, _ptr(data), data.numel(), _ptr(scratch),
                                              grid, _stream(self.device))
         self._check(rc, "mgenx_diag_stream_read")
+
+    def stream_scan(self, data, mode=SCAN_TCP, cap=None, nbytes=None):
+        """TCP / SINK record framing of a device byte stream (mgenx_stream_scan).  Returns
+        (rec_off int64 tensor, rec_len int32 tensor, ScanInfo); synchronous."""
+        torch = self.torch
+        nbytes = data.numel() if nbytes is None else nbytes
+        if cap is None:
+            cap = nbytes // 4 + 1
+        offs = torch.empty(cap, dtype=torch.int64, device=data.device)
+        lens = torch.empty(cap, dtype=torch.int32, device=data.device)
+        info = ScanInfo()
+        rc = self.lib.mgenx_stream_scan(self.ctx, _ptr(data), nbytes, mode, _ptr(offs),
+                                        _ptr(lens), cap, ctypes.byref(info),
+                                        _stream(self.device))
+        self._check(rc, "mgenx_stream_scan")
+        n = min(int(info.n_records), cap)
+        return offs[:n], lens[:n], info
 
     def crc32(self, data, off, length, n, out=None):
         if out is None:

@@ -74,3 +74,14 @@ def hex_payload(hexstr: str) -> bytes:
         lo = nib(hexstr[2 * i + 1]) if 2 * i + 1 < len(hexstr) else 0
         out[i] = (hi << 4) | lo
     return bytes(out)
+
+
+# stream framing (mgenx_stream_scan)
+SCAN_TCP = 0
+SCAN_SINK = 1
+
+
+class ScanInfo(ctypes.Structure):
+    _fields_ = [("n_records", ctypes.c_uint64), ("consumed", ctypes.c_uint64),
+                ("status", ctypes.c_int32), ("candidates", ctypes.c_uint32),
+                ("resolved", ctypes.c_uint64)]

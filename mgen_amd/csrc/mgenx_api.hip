@@ -12,6 +12,12 @@
 
 #include "mgenx_kernels.hpp"
 
+extern "C" void* mgenx_scan_ws_new();
+extern "C" void mgenx_scan_ws_free(void* p);
+extern "C" int mgenx_scan_run(void* ws, const uint8_t* s, uint64_t nbytes, int mode,
+                              uint64_t* rec_off, uint32_t* rec_len, uint64_t cap,
+                              mgenx_scan_info* info, hipStream_t stream, char* err, size_t errn);
+
 struct mgenx_ctx {
   int device = 0;
   int cu_count = 0;
@@ -24,6 +30,7 @@ struct mgenx_ctx {
   uint8_t* d_rtab = nullptr;      // 16 + 65536 + 32 bytes
   uint32_t* d_rcrc = nullptr;     // [65536]
   uint8_t* d_sink = nullptr;      // 1 KiB: column stores of lanes past the batch end
+  void* scan_ws = nullptr;        // stream-scan workspace (mgenx_scan.hip), grown on demand
   bool rand_ready = false;
   uint32_t rand_time = 0;
   char err[256] = {0};
@@ -154,6 +161,7 @@ int mgenx_ctx_destroy(mgenx_ctx* c) {
   hipSetDevice(c->device);
   void* ps[] = {c->d_tabs, c->d_expect, c->d_xpow, c->d_ia, c->d_bytetab, c->d_rtab, c->d_rcrc,
                 c->d_sink};
+  if (c->scan_ws) mgenx_scan_ws_free(c->scan_ws);
   for (void* p : ps)
     if (p) hipFree(p);
   delete c;
@@ -278,6 +286,22 @@ int mgenx_diag_stream_read(mgenx_ctx* ctx, const uint8_t* dev_data, uint64_t byt
   hipError_t e = mgenx::launch_stream_read(dev_data, bytes, dev_scratch, grid,
                                            (hipStream_t)stream);
   return e == hipSuccess ? MGENX_OK : set_err(ctx, e, "stream_read");
+}
+
+int mgenx_stream_scan(mgenx_ctx* ctx, const uint8_t* dev_stream, uint64_t nbytes, int mode,
+                      uint64_t* dev_rec_off, uint32_t* dev_rec_len, uint64_t cap,
+                      mgenx_scan_info* info, void* stream) {
+  if (!ctx || (nbytes && !dev_stream) || (cap && (!dev_rec_off || !dev_rec_len)) ||
+      (mode != MGENX_SCAN_TCP && mode != MGENX_SCAN_SINK))
+    return MGENX_EINVAL;
+  if (nbytes == 0) {
+    if (info) memset(info, 0, sizeof(*info));
+    return MGENX_OK;
+  }
+  hipSetDevice(ctx->device);
+  if (!ctx->scan_ws) ctx->scan_ws = mgenx_scan_ws_new();
+  return mgenx_scan_run(ctx->scan_ws, dev_stream, nbytes, mode, dev_rec_off, dev_rec_len, cap,
+                        info, (hipStream_t)stream, ctx->err, sizeof(ctx->err));
 }
 
 int mgenx_crc32_batch(mgenx_ctx* ctx, const uint8_t* dev_data, const uint64_t* dev_off,
