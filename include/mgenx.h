@@ -195,8 +195,9 @@ int mgenx_stream_scan(mgenx_ctx* ctx, const uint8_t* dev_stream, uint64_t nbytes
 /* Tuning knobs (process-wide; for benchmarking kernel variants).  MGENX_TUNE_UNPACK_VARIANT:
  * 0 = automatic (pipelined fixed-length kernel when the batch qualifies), 1/2 = ablations
  * of the general kernel (loads+XOR only / lookups on cached rows), 3 = general kernel,
- * 4 = loads+XOR ablation of the fixed-length kernel, 5 = the same without decode/stores
- * (1024-B records only). */
+ * 4 = loads+XOR ablation of the fixed-length kernel, 5 = the same without decode/stores,
+ * 6 = mode 4 with every column store sent to a scratch line, 7 = mode 4 without the stores
+ * (modes 4-7: 1024-B records only). */
 #define MGENX_TUNE_UNPACK_VARIANT 1
 int mgenx_set_tuning(mgenx_ctx* ctx, int key, int value);
 /* Diagnostic: plain 16-B-per-lane streaming read of `bytes` (the achievable-HBM reference

@@ -31,6 +31,7 @@ struct mgenx_ctx {
   uint32_t* d_rcrc = nullptr;     // [65536]
   uint8_t* d_sink = nullptr;      // 1 KiB: column stores of lanes past the batch end
   void* scan_ws = nullptr;        // stream-scan workspace (mgenx_scan.hip), grown on demand
+  uint8_t* d_rows_diag = nullptr; // ablation 8 only: 32-B rows for 1M records
   bool rand_ready = false;
   uint32_t rand_time = 0;
   char err[256] = {0};
@@ -162,6 +163,7 @@ int mgenx_ctx_destroy(mgenx_ctx* c) {
   void* ps[] = {c->d_tabs, c->d_expect, c->d_xpow, c->d_ia, c->d_bytetab, c->d_rtab, c->d_rcrc,
                 c->d_sink};
   if (c->scan_ws) mgenx_scan_ws_free(c->scan_ws);
+  if (c->d_rows_diag) hipFree(c->d_rows_diag);
   for (void* p : ps)
     if (p) hipFree(p);
   delete c;
@@ -194,6 +196,7 @@ int mgenx_unpack_batch(mgenx_ctx* ctx, const uint8_t* dev_slab, uint64_t slab_by
   p.expect = ctx->d_expect;
   p.expect_fixed = fixed_len < ctx->h_expect.size() ? ctx->h_expect[fixed_len] : 0u;
   p.sink = ctx->d_sink;
+  p.sink2 = mgenx::unpack_variant == 8 ? ctx->d_rows_diag : nullptr;
   p.cols = k;
   const uint64_t groups = ((uint64_t)n + 15) / 16;
   const uint64_t per_block = (uint64_t)mgenx::unpack_threads() / 64;  // waves per block
@@ -273,8 +276,11 @@ int mgenx_pack_batch(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
 int mgenx_set_tuning(mgenx_ctx* ctx, int key, int value) {
   if (!ctx) return MGENX_EINVAL;
   if (key == MGENX_TUNE_UNPACK_VARIANT) {
-    if (value < 0 || value > 5) return MGENX_EINVAL;
+    if (value < 0 || value > 8) return MGENX_EINVAL;
     mgenx::unpack_variant = value;
+    if (value == 8 && !ctx->d_rows_diag &&
+        hipMalloc((void**)&ctx->d_rows_diag, (size_t)32 << 20) != hipSuccess)
+      return MGENX_ENOMEM;
     return MGENX_OK;
   }
   return MGENX_EINVAL;

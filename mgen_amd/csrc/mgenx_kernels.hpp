@@ -18,6 +18,7 @@ struct UnpackParams {
   const uint32_t* expect;  // [65536]
   uint32_t expect_fixed;   // expect[fixed_len] (host copy, fixed-length kernel)
   uint8_t* sink;           // 1 KiB scratch: stores of lanes past the batch end
+  uint8_t* sink2;          // ablation 8: 32-B record rows (diag buffer set via tuning)
   mgenx_cols cols;
 };
 

@@ -795,7 +795,7 @@ unpack_fixed_kernel(UnpackParams p, uint32_t expect) {
       ptype = gps = 0;
       err = MGENX_ERROR_OOB;
     }
-    const bool in = idx < p.n;
+    const bool in = idx < p.n && MODE != 6;  // MODE 6 (ablation): every store to the sink
     const uint64_t sink = (uint64_t)p.sink + 4u * (uint32_t)lane;
     auto at = [&](uint64_t base, uint32_t size) {
       return in ? base + (uint64_t)idx * size : sink;
@@ -809,6 +809,22 @@ unpack_fixed_kernel(UnpackParams p, uint32_t expect) {
                                (uint64_t)c.dst_len);
     const uint64_t u8b = pick4(q, (uint64_t)c.payload_type, (uint64_t)c.gps_status,
                                (uint64_t)c.payload_type, (uint64_t)c.gps_status);
+    if (MODE == 8) {  // ablation: one 32-B record per quad (lane q writes bytes 8q..8q+7)
+      const uint64_t v =
+          q == 0 ? ((uint64_t)seq << 32 | flow)
+        : q == 1 ? ((uint64_t)usec << 32 | sec)
+        : q == 2 ? ((uint64_t)(msg_len | dport << 16) << 32 | dst4)
+                 : ((uint64_t)(dtype | dlen << 8 | ptype << 16 | gps << 24) << 32 |
+                    (plen | flags << 16 | err << 24));
+      st_g64(in ? (uint64_t)p.sink2 + (uint64_t)idx * 32 + 8 * q : sink, v);
+      return;
+    }
+    if (MODE == 7) {  // ablation: the tail's work without its stores (kept alive)
+      const uint32_t all = flow ^ seq ^ sec ^ usec ^ dst4 ^ msg_len ^ dport ^ plen ^ flags ^
+                           err ^ dtype ^ dlen ^ ptype ^ gps;
+      if (all == 0x9E3779B9u) st_g32(at(u32, 4), all);
+      return;
+    }
     // u32: flow, seq, tx_sec, tx_usec (lane q -> column q); then dst_addr4 (all lanes)
     st_g32(at(u32, 4), q == 0 ? flow : q == 1 ? seq : q == 2 ? sec : usec);
     st_g32(at((uint64_t)c.dst_addr4, 4), dst4);
@@ -867,7 +883,7 @@ unpack_fixed_kernel(UnpackParams p, uint32_t expect) {
           }
         }
         uint32_t c4[4];
-        if (MODE == 1 || MODE == 5) {
+        if (MODE == 1 || MODE >= 5) {
           c4[0] = (h0 << 1) ^ x.x; c4[1] = (h1 << 1) ^ x.y;
           c4[2] = (h2 << 1) ^ x.z; c4[3] = (h3 << 1) ^ x.w;
         } else {
@@ -878,7 +894,7 @@ unpack_fixed_kernel(UnpackParams p, uint32_t expect) {
         __builtin_amdgcn_sched_barrier(0);
         d[j] = ld_row(boff_n, j);
         __builtin_amdgcn_sched_barrier(0);
-        if (MODE == 1 || MODE == 5) {
+        if (MODE == 1 || MODE >= 5) {
           h0 = c4[0]; h1 = c4[1]; h2 = c4[2]; h3 = c4[3];
           continue;
         }
@@ -998,6 +1014,9 @@ hipError_t launch_unpack(const UnpackParams& p, int grid, hipStream_t stream) {
   if (unpack_variant == 0 && fixed) return kFixedLaunch[(p.fixed_len + 63) / 64](p, grid, stream);
   if (unpack_variant == 4 && fixed && p.fixed_len == 1024) return launch_fixed<16, 1>(p, grid, stream);
   if (unpack_variant == 5 && fixed && p.fixed_len == 1024) return launch_fixed<16, 5>(p, grid, stream);
+  if (unpack_variant == 6 && fixed && p.fixed_len == 1024) return launch_fixed<16, 6>(p, grid, stream);
+  if (unpack_variant == 7 && fixed && p.fixed_len == 1024) return launch_fixed<16, 7>(p, grid, stream);
+  if (unpack_variant == 8 && fixed && p.fixed_len == 1024 && p.sink2) return launch_fixed<16, 8>(p, grid, stream);
   switch (unpack_variant) {
     case 1: return launch_mode<1>(p, grid, stream);
     case 2: return launch_mode<2>(p, grid, stream);

@@ -40,7 +40,7 @@ def run(name):
         eng.stream_read(slab, grid=int(name.split("_")[1]))
 
 
-names = ["mode0", "mode4", "mode5", "mode3", "mode1", "mode2", "hdr_only", "read_1024", "read_2048", "read_4096",
+names = ["mode0", "mode4", "mode5", "mode7", "mode8", "mode3", "mode1", "mode2", "hdr_only", "read_1024", "read_2048", "read_4096",
          "read_8192"]
 res = {k: [] for k in names}
 for rnd in range(5):
