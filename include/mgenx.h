@@ -192,6 +192,61 @@ int mgenx_stream_scan(mgenx_ctx* ctx, const uint8_t* dev_stream, uint64_t nbytes
                       uint64_t* dev_rec_off, uint32_t* dev_rec_len, uint64_t cap,
                       mgenx_scan_info* info, void* stream);
 
+/* ---- per-flow receive analytics (MgenAnalytic::Update) ----
+ * Restates MgenAnalytic::Init/Update (src/common/mgenAnalytic.cpp:28-258) as called by
+ * Mgen::UpdateRecvAnalytics (src/common/mgen.cpp:1027-1070): per flow, an order-dependent
+ * window state machine with a 1024-bit ProtoSlidingMask of received sequence numbers
+ * (duplicate detection), FP64 latency sum/min/max and a report when rx >= window end.
+ * The caller maps its flow key (src addr, dst addr, flow id: FindFlow, mgenAnalytic.cpp:
+ * 312-328) to a dense flow index; records are passed in receive order.  State persists in
+ * the caller's mgenx_flow_state array across calls (streaming batches).
+ * Parity: bit-exact (FP64 included, no contraction) with the oracle restatement; the
+ * protolib primitives themselves are unpinned (ProtoSlidingMask, ProtoTime::Delta). */
+typedef struct mgenx_flow_state {   /* 256 B; set up by mgenx_flow_init */
+  uint32_t mask[32];                /* bit i <-> sequence number mask_first + i */
+  uint32_t mask_first, mask_n;      /* lowest set sequence number, number of set bits */
+  uint32_t seq_start, window_valid;
+  int64_t  win_start_sec, win_start_usec, win_end_sec, win_end_usec;
+  double   window_size;             /* quantized as Report::Quantize/UnquantizeTimeValue */
+  uint64_t msg_count, byte_count, dup_count;
+  double   latency_sum, latency_min, latency_max;
+  uint64_t n_reports;
+  uint64_t rsv[2];
+} mgenx_flow_state;
+
+typedef struct mgenx_flow_report {  /* one closed window (MgenAnalytic::Report) */
+  uint32_t flow, index;             /* flow index, report number within the flow */
+  int64_t  start_sec, start_usec;   /* window start */
+  double   duration;
+  uint64_t msg_count;
+  double   rate, loss, latency_ave, latency_min, latency_max;
+  int64_t  rx_sec, rx_usec;         /* receive time of the message that closed it */
+} mgenx_flow_report;
+
+/* Packed per-flow counters for the multi-GPU merge (one RCCL all-reduce(sum) of
+ * n_flows x 64 B: flows are owned by one rank, the others contribute zeros). */
+typedef struct mgenx_flow_counters {
+  uint64_t msg_count, byte_count, dup_count, n_reports;
+  double   latency_sum, latency_min, latency_max;
+  uint64_t seq_start;
+} mgenx_flow_counters;
+
+int mgenx_flow_init(mgenx_ctx* ctx, mgenx_flow_state* dev_flows, uint32_t n_flows,
+                    double window_sec, void* stream);
+/* Records i < n with dev_flow_idx[i] < n_flows update flow dev_flow_idx[i], in order.
+ * Columns: seq_num, tx_sec, tx_usec, msg_len (from mgenx_unpack_batch); rx time per
+ * record in dev_rx_sec/dev_rx_usec.  Reports go to dev_reports[f * per_flow + k] for
+ * k < per_flow; dev_report_count[f] (zeroed by the caller) counts all of them.
+ * Synchronous on `stream` only when its workspace must grow. */
+int mgenx_flow_reduce(mgenx_ctx* ctx, const uint32_t* dev_flow_idx, const uint32_t* dev_seq,
+                      const uint32_t* dev_tx_sec, const uint32_t* dev_tx_usec,
+                      const uint16_t* dev_msg_len, const uint32_t* dev_rx_sec,
+                      const uint32_t* dev_rx_usec, uint32_t n, mgenx_flow_state* dev_flows,
+                      uint32_t n_flows, mgenx_flow_report* dev_reports, uint32_t per_flow,
+                      uint32_t* dev_report_count, void* stream);
+int mgenx_flow_export(mgenx_ctx* ctx, const mgenx_flow_state* dev_flows, uint32_t n_flows,
+                      mgenx_flow_counters* dev_out, void* stream);
+
 /* Tuning knobs (process-wide; for benchmarking kernel variants).  MGENX_TUNE_UNPACK_VARIANT:
  * 0 = automatic (pipelined fixed-length kernel when the batch qualifies), 1/2 = ablations
  * of the general kernel (loads+XOR only / lookups on cached rows), 3 = general kernel,

@@ -15,7 +15,8 @@ from ._abi import (  # noqa: F401
     COLS_CORE, COLS_EXT, DESC_DTYPE, TMPL_DTYPE, MgenxCols, ERROR_CHECKSUM, ERROR_DSTADDR,
     ERROR_LENGTH, ERROR_NONE, ERROR_OOB, ERROR_VERSION, FLAG_CHECKSUM, FLAG_CHECKSUM_ERROR,
     FLAG_LAST_BUFFER, OPT_CHECKSUM_FORCE, OPT_SKIP_CRC, OPT_TCP, PACK_CHECKSUM,
-    PACK_RANDOM_FILL, SCAN_SINK, SCAN_TCP, ScanInfo,
+    PACK_RANDOM_FILL, SCAN_SINK, SCAN_TCP, ScanInfo, FLOW_COUNTERS_DTYPE, FLOW_REPORT_DTYPE,
+    FLOW_STATE_BYTES, FLOW_STATE_DTYPE,
 )
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -59,6 +60,9 @@ def load():
     L.mgenx_set_tuning.argtypes = [P, i32, i32]
     L.mgenx_diag_stream_read.argtypes = [P, P, u64, P, i32, P]
     L.mgenx_stream_scan.argtypes = [P, P, u64, i32, P, P, u64, ctypes.POINTER(ScanInfo), P]
+    L.mgenx_flow_init.argtypes = [P, P, u32, ctypes.c_double, P]
+    L.mgenx_flow_reduce.argtypes = [P, P, P, P, P, P, P, P, u32, P, u32, P, u32, P, P]
+    L.mgenx_flow_export.argtypes = [P, P, u32, P, P]
     _lib = L
     return L
 
@@ -182,6 +186,37 @@ class Engine:
         self._check(rc, "mgenx_stream_scan")
         n = min(int(info.n_records), cap)
         return offs[:n], lens[:n], info
+
+    # ------------------------------------------------------------ analytics
+    def flow_init(self, n_flows, window=1.0):
+        """Fresh MgenAnalytic state for n_flows flows (mgenx_flow_init); a uint8 tensor of
+        n_flows x 256 B."""
+        flows = self.torch.empty(n_flows * FLOW_STATE_BYTES, dtype=self.torch.uint8,
+                                 device=f"cuda:{self.device}")
+        self._check(self.lib.mgenx_flow_init(self.ctx, _ptr(flows), n_flows, window,
+                                             _stream(self.device)), "mgenx_flow_init")
+        return flows
+
+    def flow_reduce(self, flows, n_flows, flow_idx, seq, tx_sec, tx_usec, msg_len, rx_sec,
+                    rx_usec, n=None, reports=None, per_flow=0, report_count=None):
+        """MgenAnalytic::Update over records in receive order (mgenx_flow_reduce)."""
+        torch = self.torch
+        n = flow_idx.numel() if n is None else n
+        if report_count is None:
+            report_count = torch.zeros(n_flows, dtype=torch.int32, device=flows.device)
+        rc = self.lib.mgenx_flow_reduce(self.ctx, _ptr(flow_idx), _ptr(seq), _ptr(tx_sec),
+                                        _ptr(tx_usec), _ptr(msg_len), _ptr(rx_sec),
+                                        _ptr(rx_usec), n, _ptr(flows), n_flows, _ptr(reports),
+                                        per_flow, _ptr(report_count), _stream(self.device))
+        self._check(rc, "mgenx_flow_reduce")
+        return report_count
+
+    def flow_export(self, flows, n_flows, out=None):
+        if out is None:
+            out = self.torch.empty(n_flows * 64, dtype=self.torch.uint8, device=flows.device)
+        self._check(self.lib.mgenx_flow_export(self.ctx, _ptr(flows), n_flows, _ptr(out),
+                                               _stream(self.device)), "mgenx_flow_export")
+        return out
 
     def crc32(self, data, off, length, n, out=None):
         if out is None:

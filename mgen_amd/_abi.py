@@ -85,3 +85,25 @@ class ScanInfo(ctypes.Structure):
     _fields_ = [("n_records", ctypes.c_uint64), ("consumed", ctypes.c_uint64),
                 ("status", ctypes.c_int32), ("candidates", ctypes.c_uint32),
                 ("resolved", ctypes.c_uint64)]
+
+
+# per-flow analytics (mgenx_flow_*): layouts of include/mgenx.h
+FLOW_STATE_BYTES = 256
+FLOW_REPORT_DTYPE = np.dtype([
+    ("flow", "<u4"), ("index", "<u4"), ("start_sec", "<i8"), ("start_usec", "<i8"),
+    ("duration", "<f8"), ("msg_count", "<u8"), ("rate", "<f8"), ("loss", "<f8"),
+    ("latency_ave", "<f8"), ("latency_min", "<f8"), ("latency_max", "<f8"),
+    ("rx_sec", "<i8"), ("rx_usec", "<i8")])
+FLOW_COUNTERS_DTYPE = np.dtype([
+    ("msg_count", "<u8"), ("byte_count", "<u8"), ("dup_count", "<u8"), ("n_reports", "<u8"),
+    ("latency_sum", "<f8"), ("latency_min", "<f8"), ("latency_max", "<f8"),
+    ("seq_start", "<u8")])
+FLOW_STATE_DTYPE = np.dtype([
+    ("mask", "<u4", (32,)), ("mask_first", "<u4"), ("mask_n", "<u4"), ("seq_start", "<u4"),
+    ("window_valid", "<u4"), ("win_start_sec", "<i8"), ("win_start_usec", "<i8"),
+    ("win_end_sec", "<i8"), ("win_end_usec", "<i8"), ("window_size", "<f8"),
+    ("msg_count", "<u8"), ("byte_count", "<u8"), ("dup_count", "<u8"),
+    ("latency_sum", "<f8"), ("latency_min", "<f8"), ("latency_max", "<f8"),
+    ("n_reports", "<u8"), ("rsv", "<u8", (2,))])
+assert FLOW_STATE_DTYPE.itemsize == FLOW_STATE_BYTES
+assert FLOW_REPORT_DTYPE.itemsize == 96 and FLOW_COUNTERS_DTYPE.itemsize == 64

@@ -18,6 +18,20 @@ extern "C" int mgenx_scan_run(void* ws, const uint8_t* s, uint64_t nbytes, int m
                               uint64_t* rec_off, uint32_t* rec_len, uint64_t cap,
                               mgenx_scan_info* info, hipStream_t stream, char* err, size_t errn);
 
+extern "C" void* mgenx_flow_ws_new();
+extern "C" void mgenx_flow_ws_free(void* p);
+extern "C" int mgenx_flow_init_run(mgenx_flow_state* flows, uint32_t n_flows, double window,
+                                   hipStream_t stream);
+extern "C" int mgenx_flow_export_run(const mgenx_flow_state* flows, uint32_t n_flows,
+                                     mgenx_flow_counters* out, hipStream_t stream);
+extern "C" int mgenx_flow_reduce_run(void* ws, const uint32_t* flow_idx, const uint32_t* seq,
+                                     const uint32_t* txs, const uint32_t* txu, const uint16_t* len,
+                                     const uint32_t* rxs, const uint32_t* rxu, uint32_t n,
+                                     mgenx_flow_state* flows, uint32_t n_flows,
+                                     mgenx_flow_report* reports, uint32_t per_flow,
+                                     uint32_t* report_count, hipStream_t stream, char* err,
+                                     size_t errn);
+
 struct mgenx_ctx {
   int device = 0;
   int cu_count = 0;
@@ -31,6 +45,7 @@ struct mgenx_ctx {
   uint32_t* d_rcrc = nullptr;     // [65536]
   uint8_t* d_sink = nullptr;      // 1 KiB: column stores of lanes past the batch end
   void* scan_ws = nullptr;        // stream-scan workspace (mgenx_scan.hip), grown on demand
+  void* flow_ws = nullptr;        // flow-reduce workspace (mgenx_analytic.hip), grown on demand
   uint8_t* d_rows_diag = nullptr; // ablation 8 only: 32-B rows for 1M records
   bool rand_ready = false;
   uint32_t rand_time = 0;
@@ -163,6 +178,7 @@ int mgenx_ctx_destroy(mgenx_ctx* c) {
   void* ps[] = {c->d_tabs, c->d_expect, c->d_xpow, c->d_ia, c->d_bytetab, c->d_rtab, c->d_rcrc,
                 c->d_sink};
   if (c->scan_ws) mgenx_scan_ws_free(c->scan_ws);
+  if (c->flow_ws) mgenx_flow_ws_free(c->flow_ws);
   if (c->d_rows_diag) hipFree(c->d_rows_diag);
   for (void* p : ps)
     if (p) hipFree(p);
@@ -308,6 +324,38 @@ int mgenx_stream_scan(mgenx_ctx* ctx, const uint8_t* dev_stream, uint64_t nbytes
   if (!ctx->scan_ws) ctx->scan_ws = mgenx_scan_ws_new();
   return mgenx_scan_run(ctx->scan_ws, dev_stream, nbytes, mode, dev_rec_off, dev_rec_len, cap,
                         info, (hipStream_t)stream, ctx->err, sizeof(ctx->err));
+}
+
+int mgenx_flow_init(mgenx_ctx* ctx, mgenx_flow_state* dev_flows, uint32_t n_flows,
+                    double window_sec, void* stream) {
+  if (!ctx || (n_flows && !dev_flows) || !(window_sec >= 0.0)) return MGENX_EINVAL;
+  return mgenx_flow_init_run(dev_flows, n_flows, window_sec, (hipStream_t)stream);
+}
+
+int mgenx_flow_reduce(mgenx_ctx* ctx, const uint32_t* dev_flow_idx, const uint32_t* dev_seq,
+                      const uint32_t* dev_tx_sec, const uint32_t* dev_tx_usec,
+                      const uint16_t* dev_msg_len, const uint32_t* dev_rx_sec,
+                      const uint32_t* dev_rx_usec, uint32_t n, mgenx_flow_state* dev_flows,
+                      uint32_t n_flows, mgenx_flow_report* dev_reports, uint32_t per_flow,
+                      uint32_t* dev_report_count, void* stream) {
+  if (!ctx) return MGENX_EINVAL;
+  if (n == 0 || n_flows == 0) return MGENX_OK;
+  if (!dev_flow_idx || !dev_seq || !dev_tx_sec || !dev_tx_usec || !dev_msg_len ||
+      !dev_rx_sec || !dev_rx_usec || !dev_flows || !dev_report_count ||
+      (per_flow && !dev_reports) || n > 0x7FFFFFFFu)
+    return MGENX_EINVAL;
+  hipSetDevice(ctx->device);
+  if (!ctx->flow_ws) ctx->flow_ws = mgenx_flow_ws_new();
+  return mgenx_flow_reduce_run(ctx->flow_ws, dev_flow_idx, dev_seq, dev_tx_sec, dev_tx_usec,
+                               dev_msg_len, dev_rx_sec, dev_rx_usec, n, dev_flows, n_flows,
+                               dev_reports, per_flow, dev_report_count, (hipStream_t)stream,
+                               ctx->err, sizeof(ctx->err));
+}
+
+int mgenx_flow_export(mgenx_ctx* ctx, const mgenx_flow_state* dev_flows, uint32_t n_flows,
+                      mgenx_flow_counters* dev_out, void* stream) {
+  if (!ctx || (n_flows && (!dev_flows || !dev_out))) return MGENX_EINVAL;
+  return mgenx_flow_export_run(dev_flows, n_flows, dev_out, (hipStream_t)stream);
 }
 
 int mgenx_crc32_batch(mgenx_ctx* ctx, const uint8_t* dev_data, const uint64_t* dev_off,

@@ -81,3 +81,36 @@ def udp_mixed(n: int, lo: int = 64, hi: int = 1472, n_flows: int = 64, payload_h
     offs = np.zeros(n, np.uint64)
     offs[1:] = np.cumsum(sizes[:-1], dtype=np.uint64)
     return tmpl, pool, d, offs, sizes.astype(np.uint32)
+
+
+def poisson_flows(n, n_flows=1024, seed=SEED, loss=0.01, dup=0.001, reorder=8,
+                  mean_gap_us=1000, msg_len=256, t0=1_700_000_000):
+    """BASELINE config 4 shape: n_flows flows (ids 1..n_flows), per-flow tx interarrival
+    Exp(mean_gap_us) (MgenPattern POISSON, mgenPattern.h:73-77), rx = tx + U[50, 500] us,
+    `loss` of the sends dropped, `dup` duplicated, and records reordered within +-`reorder`
+    positions of the global receive order.  Returns dict of columns in receive order
+    (about n records)."""
+    rng = np.random.default_rng(seed)
+    per = max(1, int(n / n_flows / (1 - loss + dup)) + 1)
+    flow = np.repeat(np.arange(1, n_flows + 1, dtype=np.uint32), per)
+    seq = np.tile(np.arange(per, dtype=np.uint32), n_flows)
+    gaps = rng.exponential(mean_gap_us, (n_flows, per))
+    tx_us = (np.cumsum(gaps, axis=1) + rng.uniform(0, 1e6, (n_flows, 1))).reshape(-1)
+    keep = rng.random(flow.size) >= loss
+    d = rng.random(flow.size) < dup
+    idx = np.concatenate([np.nonzero(keep)[0], np.nonzero(keep & d)[0]])
+    tx_us = tx_us[idx]
+    rx_us = tx_us + rng.uniform(50, 500, idx.size)
+    order = np.argsort(rx_us, kind="stable")
+    if reorder:
+        jitter = order.astype(np.float64) * 0 + rng.uniform(-reorder, reorder, order.size)
+        order = order[np.argsort(np.arange(order.size) + jitter, kind="stable")]
+    idx, tx_us, rx_us = idx[order][:n], tx_us[order][:n], rx_us[order][:n]
+    tx_i = (t0 * 10**6 + tx_us.astype(np.int64))
+    rx_i = (t0 * 10**6 + rx_us.astype(np.int64))
+    return {
+        "flow_id": flow[idx], "seq": seq[idx],
+        "tx_sec": (tx_i // 10**6).astype(np.uint32), "tx_usec": (tx_i % 10**6).astype(np.uint32),
+        "rx_sec": (rx_i // 10**6).astype(np.uint32), "rx_usec": (rx_i % 10**6).astype(np.uint32),
+        "msg_len": np.full(idx.size, msg_len, np.uint16),
+    }

@@ -788,6 +788,40 @@ int or_analytic_update(or_analytic* a, or_time rx, uint32_t msgSize, or_time tx,
     return 0;
 }
 
+void or_flow_reduce_batch(or_analytic* flows, uint32_t n_flows, const uint32_t* flow_idx,
+                          const uint32_t* seq, const uint32_t* tx_sec, const uint32_t* tx_usec,
+                          const uint16_t* msg_len, const uint32_t* rx_sec,
+                          const uint32_t* rx_usec, uint32_t n, or_report* reports,
+                          uint32_t cap, uint32_t* counts)
+{
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t f = flow_idx[i];
+        if (f >= n_flows) continue;
+        or_analytic* a = &flows[f];
+        or_time rx = {(int64_t)rx_sec[i], (int64_t)rx_usec[i]};
+        or_time tx = {(int64_t)tx_sec[i], (int64_t)tx_usec[i]};
+        if (or_analytic_update(a, rx, msg_len[i], tx, seq[i])) {
+            const uint32_t k = counts[f]++;
+            if (k < cap) {
+                or_report* r = &reports[(size_t)f * cap + k];
+                r->flow = f;
+                r->index = k;
+                r->start_sec = a->report_start.sec;
+                r->start_usec = a->report_start.usec;
+                r->duration = a->report_duration;
+                r->msg_count = a->report_msg_count;
+                r->rate = a->report_rate_ave;
+                r->loss = a->report_loss_ave;
+                r->latency_ave = a->report_latency_ave;
+                r->latency_min = a->report_latency_min;
+                r->latency_max = a->report_latency_max;
+                r->rx_sec = rx.sec;
+                r->rx_usec = rx.usec;
+            }
+        }
+    }
+}
+
 /* ------------------------------------------------------------------ */
 /* Batch layer                                                         */
 /* ------------------------------------------------------------------ */
@@ -904,6 +938,8 @@ uint64_t or_tcp_tx_batch(const or_tmpl* tmpl, const or_desc* desc, const uint32_
 /* layout check for the Python/ctypes mirrors */
 uint32_t or_sizeof(int which)
 {
+    if (which == 100) return (uint32_t)sizeof(or_report);
+    if (which == 101) return (uint32_t)sizeof(or_analytic);
     switch (which) {
         case 0: return (uint32_t)sizeof(or_tmpl);
         case 1: return (uint32_t)sizeof(or_desc);

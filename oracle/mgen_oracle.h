@@ -173,6 +173,23 @@ int      or_analytic_update(or_analytic* a, or_time rx, uint32_t msg_size, or_ti
                             uint32_t seq);
 double   or_time_delta(or_time a, or_time b);
 
+/* Batch analytics (Mgen::UpdateRecvAnalytics, mgen.cpp:1027-1070, over many flows):
+ * records in rx order, flow_idx = dense flow index (>= n_flows: skipped); every closed
+ * window is appended to reports[f * cap + k] (k < cap; counts[f] counts all). */
+typedef struct {
+    uint32_t flow, index;
+    int64_t  start_sec, start_usec;
+    double   duration;
+    uint64_t msg_count;
+    double   rate, loss, latency_ave, latency_min, latency_max;
+    int64_t  rx_sec, rx_usec;
+} or_report;
+void or_flow_reduce_batch(or_analytic* flows, uint32_t n_flows, const uint32_t* flow_idx,
+                          const uint32_t* seq, const uint32_t* tx_sec, const uint32_t* tx_usec,
+                          const uint16_t* msg_len, const uint32_t* rx_sec,
+                          const uint32_t* rx_usec, uint32_t n, or_report* reports,
+                          uint32_t cap, uint32_t* counts);
+
 /* ---- Batch layer (same descriptor layout as the product's include/mgenx.h) ---- */
 /* Per-flow template: what MgenFlow::SendMessage fills from flow state
  * (mgenFlow.cpp:946-983, 1039-1129).  64 bytes. */

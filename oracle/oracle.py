@@ -131,6 +131,7 @@ def lib():
         L.or_analytic_update.restype = i32
         L.or_time_delta.argtypes = [Time, Time]
         L.or_time_delta.restype = ctypes.c_double
+        L.or_flow_reduce_batch.argtypes = [P, u32, P, P, P, P, P, P, P, u32, P, u32, P]
         L.or_sizeof.argtypes = [i32]
         L.or_sizeof.restype = u32
         assert L.or_sizeof(0) == TMPL_DTYPE.itemsize, "or_tmpl layout mismatch"
@@ -324,3 +325,30 @@ class AnalyticOracle:
     def update(self, rx_sec, rx_usec, msg_size, tx_sec, tx_usec, seq):
         return bool(lib().or_analytic_update(ctypes.byref(self.a), Time(rx_sec, rx_usec),
                                              msg_size, Time(tx_sec, tx_usec), seq))
+
+
+REPORT_DTYPE = np.dtype([
+    ("flow", "<u4"), ("index", "<u4"), ("start_sec", "<i8"), ("start_usec", "<i8"),
+    ("duration", "<f8"), ("msg_count", "<u8"), ("rate", "<f8"), ("loss", "<f8"),
+    ("latency_ave", "<f8"), ("latency_min", "<f8"), ("latency_max", "<f8"),
+    ("rx_sec", "<i8"), ("rx_usec", "<i8")])
+
+
+def flow_reduce_batch(n_flows, flow_idx, seq, tx_sec, tx_usec, msg_len, rx_sec, rx_usec,
+                      window=1.0, per_flow=64, flows=None):
+    """or_flow_reduce_batch: MgenAnalytic::Update per record (receive order) over n_flows
+    flows.  Returns (flows ctypes array, reports[n_flows, per_flow], counts[n_flows])."""
+    assert lib().or_sizeof(100) == REPORT_DTYPE.itemsize
+    if flows is None:
+        flows = (Analytic * n_flows)()
+        for f in range(n_flows):
+            lib().or_analytic_init(ctypes.byref(flows[f]), window)
+    n = len(flow_idx)
+    cols = [np.ascontiguousarray(x, dt) for x, dt in
+            ((flow_idx, np.uint32), (seq, np.uint32), (tx_sec, np.uint32), (tx_usec, np.uint32),
+             (msg_len, np.uint16), (rx_sec, np.uint32), (rx_usec, np.uint32))]
+    reports = np.zeros(n_flows * max(per_flow, 1), REPORT_DTYPE)
+    counts = np.zeros(n_flows, np.uint32)
+    lib().or_flow_reduce_batch(flows, n_flows, *[_ptr(c) for c in cols], n, _ptr(reports),
+                               per_flow, _ptr(counts))
+    return flows, reports.reshape(n_flows, max(per_flow, 1)), counts

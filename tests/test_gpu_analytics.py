@@ -1,0 +1,103 @@
+"""GPU parity of mgenx_flow_reduce (MgenAnalytic::Update per flow) with the oracle's
+or_flow_reduce_batch: per-flow state (counters, FP64 latency sums, the 1024-bit duplicate
+mask) and every report, bit-exact; one call == the same records in several calls."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    return torch
+
+
+@pytest.fixture(scope="module")
+def eng(torch):
+    from mgen_amd import Engine
+    e = Engine(0)
+    yield e
+    e.close()
+
+
+def dev(torch, a):
+    return torch.from_numpy(np.ascontiguousarray(a).copy()).cuda()
+
+
+def run_gpu(torch, eng, d, n_flows, window, per_flow, splits=(0,)):
+    from mgen_amd import FLOW_REPORT_DTYPE
+    flows = eng.flow_init(n_flows, window)
+    reports = torch.zeros(n_flows * per_flow * 96, dtype=torch.uint8, device="cuda")
+    count = torch.zeros(n_flows, dtype=torch.int32, device="cuda")
+    n = len(d["seq"])
+    bounds = list(splits) + [n]
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        cols = {k: dev(torch, v[a:b]) for k, v in d.items()}
+        idx = dev(torch, (d["flow_id"][a:b] - 1).astype(np.uint32))
+        eng.flow_reduce(flows, n_flows, idx, cols["seq"], cols["tx_sec"], cols["tx_usec"],
+                        cols["msg_len"], cols["rx_sec"], cols["rx_usec"], reports=reports,
+                        per_flow=per_flow, report_count=count)
+    torch.cuda.synchronize()
+    from mgen_amd import FLOW_STATE_DTYPE
+    st = flows.cpu().numpy().view(FLOW_STATE_DTYPE)
+    rep = reports.cpu().numpy().view(FLOW_REPORT_DTYPE).reshape(n_flows, per_flow)
+    return st, rep, count.cpu().numpy().view(np.uint32), flows
+
+
+def compare(st, rep, cnt, oflows, orep, ocnt, per_flow):
+    assert np.array_equal(cnt, ocnt)
+    for f, a in enumerate(oflows):
+        s = st[f]
+        assert s["msg_count"] == a.msg_count and s["byte_count"] == a.byte_count, f
+        assert s["dup_count"] == a.dup_msg_count and s["n_reports"] == a.n_reports, f
+        assert s["seq_start"] == a.seq_start and s["window_valid"] == a.window_valid, f
+        assert s["latency_sum"] == a.latency_sum, (f, s["latency_sum"], a.latency_sum)
+        assert s["latency_min"] == a.latency_min and s["latency_max"] == a.latency_max, f
+        assert (s["win_start_sec"], s["win_start_usec"]) == (a.window_start.sec,
+                                                             a.window_start.usec), f
+        assert (s["win_end_sec"], s["win_end_usec"]) == (a.window_end.sec, a.window_end.usec)
+        assert s["mask_n"] == a.nset, f
+        if a.nset:
+            assert s["mask_first"] == a.first, f
+            assert s["mask"].tobytes() == bytes(a.bits), f
+        k = min(int(ocnt[f]), per_flow)
+        assert rep[f, :k].tobytes() == orep[f, :k].tobytes(), f
+
+
+@pytest.mark.parametrize("n_flows,window", [(64, 0.25), (1024, 0.05)])
+def test_flow_reduce_vs_oracle(torch, eng, n_flows, window):
+    from mgen_amd.workloads import poisson_flows
+    from oracle import oracle as O
+    per_flow = 32
+    d = poisson_flows(300_000, n_flows, mean_gap_us=1000, seed=n_flows)
+    st, rep, cnt, _ = run_gpu(torch, eng, d, n_flows, window, per_flow)
+    of, orep, ocnt = O.flow_reduce_batch(n_flows, d["flow_id"] - 1, d["seq"], d["tx_sec"],
+                                         d["tx_usec"], d["msg_len"], d["rx_sec"],
+                                         d["rx_usec"], window=window, per_flow=per_flow)
+    assert int(ocnt.sum()) > n_flows           # windows closed
+    assert sum(a.dup_msg_count for a in of) > 0
+    compare(st, rep, cnt, of, orep, ocnt, per_flow)
+
+
+def test_flow_reduce_streaming_batches(torch, eng):
+    from mgen_amd.workloads import poisson_flows
+    from oracle import oracle as O
+    d = poisson_flows(120_000, 48, mean_gap_us=500, seed=5, loss=0.05, dup=0.01, reorder=30)
+    st, rep, cnt, _ = run_gpu(torch, eng, d, 48, 0.1, 16, splits=(0, 1, 777, 50_000))
+    of, orep, ocnt = O.flow_reduce_batch(48, d["flow_id"] - 1, d["seq"], d["tx_sec"],
+                                         d["tx_usec"], d["msg_len"], d["rx_sec"],
+                                         d["rx_usec"], window=0.1, per_flow=16)
+    compare(st, rep, cnt, of, orep, ocnt, 16)
+
+
+def test_flow_export_counters(torch, eng):
+    from mgen_amd import FLOW_COUNTERS_DTYPE
+    from mgen_amd.workloads import poisson_flows
+    d = poisson_flows(50_000, 32, seed=9)
+    st, _, _, flows = run_gpu(torch, eng, d, 32, 0.5, 4)
+    c = eng.flow_export(flows, 32).cpu().numpy().view(FLOW_COUNTERS_DTYPE)
+    assert np.array_equal(c["msg_count"], st["msg_count"])
+    assert np.array_equal(c["latency_sum"], st["latency_sum"])
+    assert np.array_equal(c["n_reports"], st["n_reports"])
