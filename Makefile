@@ -6,10 +6,16 @@ SRC := mgen_amd/csrc/mgenx_api.hip mgen_amd/csrc/mgenx_unpack.hip mgen_amd/csrc/
        mgen_amd/csrc/mgenx_scan.hip mgen_amd/csrc/mgenx_analytic.hip
 HDR := include/mgenx.h mgen_amd/csrc/mgenx_common.hpp mgen_amd/csrc/mgenx_kernels.hpp
 
-all: mgen_amd/libmgenx.so oracle
+all: mgen_amd/libmgenx.so oracle tests/cpp/host_roundtrip
 
 mgen_amd/libmgenx.so: $(SRC) $(HDR)
 	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -shared -Iinclude -Imgen_amd/csrc $(SRC) -o $@
+
+# C++ host-layer test program (include/mgenx.hpp), plain g++ against the C ABI
+tests/cpp/host_roundtrip: tests/cpp/host_roundtrip.cpp include/mgenx.hpp include/mgenx.h mgen_amd/libmgenx.so
+	g++ -O2 -std=c++17 -D__HIP_PLATFORM_AMD__ -Iinclude -I/opt/rocm/include $< -o $@ \
+	    -Lmgen_amd -lmgenx -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,'$$ORIGIN/../../mgen_amd' \
+	    -Wl,-rpath,/opt/rocm/lib
 
 oracle:
 	$(MAKE) -s -C oracle

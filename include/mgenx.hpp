@@ -1,0 +1,433 @@
+// mgenx.hpp -- C++ host layer over the mgenx C ABI (header-only, C++17, HIP runtime).
+//
+// Mirrors the reference's per-message C++ surface at batch granularity, so the batching
+// points of mgenTransport / mgen read like the code they replace:
+//   MgenMsgView    the getters of MgenMsg (include/mgenMsg.h:115-163) over one decoded
+//                  record of a batch (GetMsgLen, GetFlowId, GetSeqNum, GetTxTime,
+//                  FlagIsSet, GetError, GetPayloadLength ...), same meaning and values;
+//   RecvBatch      MgenMsg::Unpack + the caller's CRC check for a recvmmsg-shaped batch
+//                  (mgenTransport.cpp:948-997 UDP, :2092-2112 SINK, :1516-1564 TCP);
+//   SendBatch      MgenFlow::SendMessage's fields (mgenFlow.cpp:924-1130) + MgenMsg::Pack
+//                  + WriteChecksum in the UDP/SINK send order (mgenTransport.cpp:1011-1031);
+//   FlowAnalytics  Mgen::UpdateRecvAnalytics (mgen.cpp:1027-1070): FindFlow by
+//                  (src, dst, flow id) -> MgenAnalytic::Update per record, reports out.
+// Errors: argument/launch failures throw mgenx::Error (the C ABI returns codes); per-record
+// outcomes are MgenMsg::Error values, as in the reference.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+#include <sys/time.h>
+
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "mgenx.h"
+
+namespace mgenx {
+
+struct Error : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+inline void check_hip(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw Error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// MgenMsg enums (include/mgenMsg.h:60-103)
+enum MsgError { ERROR_NONE = 0, ERROR_VERSION, ERROR_CHECKSUM, ERROR_LENGTH, ERROR_DSTADDR };
+enum MsgFlag : uint8_t {
+  CONTINUES = 0x01, END_OF_MSG = 0x02, CHECKSUM = 0x04, LAST_BUFFER = 0x08,
+  CHECKSUM_ERROR = 0x10
+};
+enum AddressType : uint8_t { INVALID_ADDRESS = 0, IPv4 = 1, IPv6 = 2 };
+
+// ---- one mgenx context + stream per device -------------------------------------------
+class Context {
+ public:
+  explicit Context(int device = 0) : device_(device) {
+    check_hip(hipSetDevice(device), "hipSetDevice");
+    if (mgenx_ctx_create(device, &ctx_) != MGENX_OK) throw Error("mgenx_ctx_create failed");
+    check_hip(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
+  }
+  ~Context() {
+    if (stream_) (void)hipStreamDestroy(stream_);
+    if (ctx_) mgenx_ctx_destroy(ctx_);
+  }
+  Context(const Context&) = delete;
+  Context& operator=(const Context&) = delete;
+  mgenx_ctx* get() const { return ctx_; }
+  hipStream_t stream() const { return stream_; }
+  int device() const { return device_; }
+  void Sync() const { check_hip(hipStreamSynchronize(stream_), "hipStreamSynchronize"); }
+  void Check(int rc, const char* what) const {
+    if (rc != MGENX_OK) {
+      const char* m = mgenx_last_error(ctx_);
+      throw Error(std::string(what) + " failed (" + std::to_string(rc) + ")" +
+                  (m && *m ? std::string(": ") + m : std::string()));
+    }
+  }
+
+ private:
+  int device_;
+  mgenx_ctx* ctx_ = nullptr;
+  hipStream_t stream_ = nullptr;
+};
+
+// ---- RAII device / pinned-host arrays -------------------------------------------------
+template <typename T>
+class DeviceArray {
+ public:
+  DeviceArray() = default;
+  explicit DeviceArray(size_t n) { Resize(n); }
+  ~DeviceArray() { Free(); }
+  DeviceArray(const DeviceArray&) = delete;
+  DeviceArray& operator=(const DeviceArray&) = delete;
+  DeviceArray(DeviceArray&& o) noexcept : p_(o.p_), n_(o.n_) { o.p_ = nullptr; o.n_ = 0; }
+  void Resize(size_t n) {
+    if (n == n_) return;
+    Free();
+    if (n) check_hip(hipMalloc((void**)&p_, n * sizeof(T)), "hipMalloc");
+    n_ = n;
+  }
+  T* data() const { return p_; }
+  size_t size() const { return n_; }
+
+ private:
+  void Free() {
+    if (p_) (void)hipFree(p_);
+    p_ = nullptr;
+    n_ = 0;
+  }
+  T* p_ = nullptr;
+  size_t n_ = 0;
+};
+
+template <typename T>
+class PinnedArray {
+ public:
+  explicit PinnedArray(size_t n = 0) { Resize(n); }
+  ~PinnedArray() {
+    if (p_) (void)hipHostFree(p_);
+  }
+  PinnedArray(const PinnedArray&) = delete;
+  PinnedArray& operator=(const PinnedArray&) = delete;
+  void Resize(size_t n) {
+    if (n == n_) return;
+    if (p_) (void)hipHostFree(p_);
+    p_ = nullptr;
+    if (n) check_hip(hipHostMalloc((void**)&p_, n * sizeof(T)), "hipHostMalloc");
+    n_ = n;
+  }
+  T* data() const { return p_; }
+  T& operator[](size_t i) const { return p_[i]; }
+  size_t size() const { return n_; }
+
+ private:
+  T* p_ = nullptr;
+  size_t n_ = 0;
+};
+
+// ---- decoded records ------------------------------------------------------------------
+// Host copies of the core columns of one batch (32 B per record).
+struct CoreColumns {
+  std::vector<uint32_t> flow_id, seq_num, tx_sec, tx_usec, dst_addr4;
+  std::vector<uint16_t> msg_len, dst_port, payload_len;
+  std::vector<uint8_t> flags, err, dst_type, dst_len, payload_type, gps_status;
+  void Resize(size_t n) {
+    for (auto* v : {&flow_id, &seq_num, &tx_sec, &tx_usec, &dst_addr4}) v->resize(n);
+    for (auto* v : {&msg_len, &dst_port, &payload_len}) v->resize(n);
+    for (auto* v : {&flags, &err, &dst_type, &dst_len, &payload_type, &gps_status}) v->resize(n);
+  }
+};
+
+// MgenMsg's getters over record i of a decoded batch (include/mgenMsg.h:115-163).
+class MgenMsgView {
+ public:
+  MgenMsgView(const CoreColumns& c, size_t i) : c_(c), i_(i) {}
+  uint16_t GetMsgLen() const { return c_.msg_len[i_]; }
+  uint32_t GetFlowId() const { return c_.flow_id[i_]; }
+  unsigned int GetSeqNum() const { return c_.seq_num[i_]; }
+  struct timeval GetTxTime() const {
+    struct timeval tv;
+    tv.tv_sec = (time_t)c_.tx_sec[i_];
+    tv.tv_usec = (suseconds_t)c_.tx_usec[i_];
+    return tv;
+  }
+  bool FlagIsSet(uint8_t flag) const { return (c_.flags[i_] & flag) != 0; }
+  MsgError GetError() const {  // MgenMsg::GetError; 0x80 (outside the slab) -> ERROR_LENGTH
+    const uint8_t e = c_.err[i_];
+    return e == MGENX_ERROR_OOB ? ERROR_LENGTH : (MsgError)e;
+  }
+  uint16_t GetDstPort() const { return c_.dst_port[i_]; }
+  AddressType GetDstAddrType() const { return (AddressType)c_.dst_type[i_]; }
+  uint8_t GetDstAddrLen() const { return c_.dst_len[i_]; }
+  uint32_t GetDstAddr4() const { return c_.dst_addr4[i_]; }  // network byte order
+  uint8_t GetPayloadType() const { return c_.payload_type[i_]; }
+  uint16_t GetPayloadLength() const { return c_.payload_len[i_]; }
+  uint8_t GetGPSStatus() const { return c_.gps_status[i_]; }
+
+ private:
+  const CoreColumns& c_;
+  size_t i_;
+};
+
+// ---- receive: MgenMsg::Unpack + CRC check over a batch ---------------------------------
+class RecvBatch {
+ public:
+  // capacity records in fixed slots of `slot` bytes (recvmmsg layout)
+  RecvBatch(Context& ctx, uint32_t capacity, uint32_t slot = MGENX_MAX_SIZE)
+      : ctx_(ctx), cap_(capacity), slot_(slot), h_slab_((size_t)capacity * slot),
+        h_len_(capacity), d_slab_((size_t)capacity * slot), d_len_(capacity) {
+    for (auto* a : {&d_flow_, &d_seq_, &d_txs_, &d_txu_, &d_dst4_}) a->Resize(capacity);
+    for (auto* a : {&d_mlen_, &d_dport_, &d_plen_}) a->Resize(capacity);
+    for (auto* a : {&d_flags_, &d_err_, &d_dtype_, &d_dlen_, &d_ptype_, &d_gps_}) a->Resize(capacity);
+  }
+  uint8_t* Slot(uint32_t i) { return h_slab_.data() + (size_t)i * slot_; }  // recv target
+  void SetLength(uint32_t i, uint32_t len) { h_len_[i] = len; }
+  uint32_t Capacity() const { return cap_; }
+
+  // n received datagrams (lengths set): H2D, unpack + CRC check, core columns D2H.
+  // forceChecksum = MgenTransport's checksum_force; tcp = MgenTcpTransport's rules.
+  void Unpack(uint32_t n, bool forceChecksum = false, bool tcp = false) {
+    if (n > cap_) throw Error("RecvBatch::Unpack: n > capacity");
+    n_ = n;
+    hipStream_t s = ctx_.stream();
+    check_hip(hipMemcpyAsync(d_slab_.data(), h_slab_.data(), (size_t)n * slot_,
+                             hipMemcpyHostToDevice, s), "H2D slab");
+    check_hip(hipMemcpyAsync(d_len_.data(), h_len_.data(), (size_t)n * 4, hipMemcpyHostToDevice,
+                             s), "H2D lengths");
+    UnpackDevice(n, forceChecksum, tcp);
+    Download();
+  }
+  // slab already in d_slab (device-resident path): decode only, columns stay on device
+  void UnpackDevice(uint32_t n, bool forceChecksum = false, bool tcp = false) {
+    n_ = n;
+    mgenx_cols c;
+    memset(&c, 0, sizeof(c));
+    c.flow_id = d_flow_.data(); c.seq_num = d_seq_.data(); c.tx_sec = d_txs_.data();
+    c.tx_usec = d_txu_.data(); c.dst_addr4 = d_dst4_.data(); c.msg_len = d_mlen_.data();
+    c.dst_port = d_dport_.data(); c.payload_len = d_plen_.data(); c.flags = d_flags_.data();
+    c.err = d_err_.data(); c.dst_type = d_dtype_.data(); c.dst_len = d_dlen_.data();
+    c.payload_type = d_ptype_.data(); c.gps_status = d_gps_.data();
+    const uint32_t opts = (forceChecksum ? MGENX_OPT_CHECKSUM_FORCE : 0) | (tcp ? MGENX_OPT_TCP : 0);
+    ctx_.Check(mgenx_unpack_batch(ctx_.get(), d_slab_.data(), (uint64_t)n * slot_, nullptr, slot_,
+                                  d_len_.data(), 0, n, &c, opts, ctx_.stream()),
+               "mgenx_unpack_batch");
+  }
+  void Download() {
+    cols_.Resize(n_);
+    hipStream_t s = ctx_.stream();
+    auto d2h = [&](auto& host, auto& dev) {
+      check_hip(hipMemcpyAsync(host.data(), dev.data(), n_ * sizeof(host[0]),
+                               hipMemcpyDeviceToHost, s), "D2H column");
+    };
+    d2h(cols_.flow_id, d_flow_); d2h(cols_.seq_num, d_seq_); d2h(cols_.tx_sec, d_txs_);
+    d2h(cols_.tx_usec, d_txu_); d2h(cols_.dst_addr4, d_dst4_); d2h(cols_.msg_len, d_mlen_);
+    d2h(cols_.dst_port, d_dport_); d2h(cols_.payload_len, d_plen_); d2h(cols_.flags, d_flags_);
+    d2h(cols_.err, d_err_); d2h(cols_.dst_type, d_dtype_); d2h(cols_.dst_len, d_dlen_);
+    d2h(cols_.payload_type, d_ptype_); d2h(cols_.gps_status, d_gps_);
+    ctx_.Sync();
+  }
+  uint32_t Size() const { return n_; }
+  MgenMsgView operator[](uint32_t i) const { return MgenMsgView(cols_, i); }
+  const CoreColumns& Columns() const { return cols_; }
+  // device columns for FlowAnalytics
+  const uint32_t* DevSeq() const { return d_seq_.data(); }
+  const uint32_t* DevTxSec() const { return d_txs_.data(); }
+  const uint32_t* DevTxUsec() const { return d_txu_.data(); }
+  const uint16_t* DevMsgLen() const { return d_mlen_.data(); }
+  uint8_t* DevSlab() const { return d_slab_.data(); }
+
+ private:
+  Context& ctx_;
+  uint32_t cap_, slot_, n_ = 0;
+  PinnedArray<uint8_t> h_slab_;
+  PinnedArray<uint32_t> h_len_;
+  DeviceArray<uint8_t> d_slab_;
+  DeviceArray<uint32_t> d_len_;
+  DeviceArray<uint32_t> d_flow_, d_seq_, d_txs_, d_txu_, d_dst4_;
+  DeviceArray<uint16_t> d_mlen_, d_dport_, d_plen_;
+  DeviceArray<uint8_t> d_flags_, d_err_, d_dtype_, d_dlen_, d_ptype_, d_gps_;
+  CoreColumns cols_;
+};
+
+// ---- send: flows + per-message descriptors -> packed datagrams --------------------------
+class SendBatch {
+ public:
+  explicit SendBatch(Context& ctx) : ctx_(ctx) {}
+  // A flow's constant fields (what MgenFlow keeps across messages).  Addresses are raw
+  // bytes in network order (ProtoAddress::GetRawHostAddress); lat/lon in degrees are
+  // converted as Pack does, (UINT32)((deg + 180) * 60000) (mgenMsg.cpp:221,225).
+  uint32_t AddFlow(uint32_t flowId, AddressType dstType, const uint8_t* dst, uint16_t dstPort,
+                   AddressType hostType = INVALID_ADDRESS, const uint8_t* host = nullptr,
+                   uint16_t hostPort = 0, double lat = 999.0, double lon = 999.0,
+                   int32_t alt = -999, uint8_t gpsStatus = 0,
+                   const std::vector<uint8_t>& payload = {}, uint8_t payloadType = 0) {
+    mgenx_flow_tmpl t;
+    memset(&t, 0, sizeof(t));
+    t.flow_id = flowId;
+    t.dst_type = dstType;
+    t.dst_len = dstType == IPv6 ? 16 : (dstType == IPv4 ? 4 : 0);
+    t.dst_port = dstPort;
+    if (dst) memcpy(t.dst_addr, dst, t.dst_len);
+    t.host_type = hostType;
+    t.host_len = hostType == IPv6 ? 16 : (hostType == IPv4 ? 4 : 0);
+    t.host_port = hostPort;
+    if (host) memcpy(t.host_addr, host, t.host_len);
+    t.lat_raw = (uint32_t)((lat + 180.0) * 60000.0);
+    t.lon_raw = (uint32_t)((lon + 180.0) * 60000.0);
+    t.alt = alt;
+    t.gps_status = gpsStatus;
+    t.payload_type = payloadType;
+    t.payload_len = (uint16_t)payload.size();
+    t.has_payload = payload.empty() ? 0 : 1;
+    t.payload_off = (uint32_t)pool_.size();
+    pool_.insert(pool_.end(), payload.begin(), payload.end());
+    tmpl_.push_back(t);
+    return (uint32_t)tmpl_.size() - 1;
+  }
+  // one message (MgenFlow::SendMessage: seq post-increment, tx time, msg_len, flags)
+  void Add(uint32_t flow, uint32_t seq, const struct timeval& txTime, uint16_t msgLen,
+           uint8_t flags = 0) {
+    mgenx_pack_desc d;
+    memset(&d, 0, sizeof(d));
+    d.tmpl = flow;
+    d.seq_num = seq;
+    d.tx_sec = (uint32_t)txTime.tv_sec;
+    d.tx_usec = (uint32_t)txTime.tv_usec;
+    d.msg_len = msgLen;
+    d.flags = flags;
+    desc_.push_back(d);
+  }
+  // Pack every message into slots of `slot` bytes; returns the packed lengths
+  // (0 = Pack failed, as MgenMsg::Pack returns 0).  fillTime: the time(NULL) the
+  // reference would seed RANDOM_FILL with.
+  const std::vector<uint32_t>& Pack(bool checksum, bool randomFill = false,
+                                    uint32_t fillTime = 0, uint32_t slot = MGENX_MAX_SIZE) {
+    const uint32_t n = (uint32_t)desc_.size();
+    slot_ = slot;
+    hipStream_t s = ctx_.stream();
+    d_tmpl_.Resize(tmpl_.size());
+    d_crc_.Resize(tmpl_.size());
+    d_pool_.Resize(pool_.empty() ? 1 : pool_.size());
+    d_desc_.Resize(n);
+    d_slab_.Resize((size_t)n * slot);
+    d_len_.Resize(n);
+    check_hip(hipMemcpyAsync(d_tmpl_.data(), tmpl_.data(), tmpl_.size() * sizeof(tmpl_[0]),
+                             hipMemcpyHostToDevice, s), "H2D tmpl");
+    if (!pool_.empty())
+      check_hip(hipMemcpyAsync(d_pool_.data(), pool_.data(), pool_.size(), hipMemcpyHostToDevice,
+                               s), "H2D pool");
+    check_hip(hipMemcpyAsync(d_desc_.data(), desc_.data(), n * sizeof(desc_[0]),
+                             hipMemcpyHostToDevice, s), "H2D desc");
+    ctx_.Check(mgenx_pack_prepare(ctx_.get(), d_tmpl_.data(), (uint32_t)tmpl_.size(),
+                                  d_pool_.data(), d_crc_.data(), s), "mgenx_pack_prepare");
+    if (randomFill) ctx_.Check(mgenx_set_fill_time(ctx_.get(), fillTime), "mgenx_set_fill_time");
+    const uint32_t opts = (checksum ? MGENX_PACK_CHECKSUM : 0) | (randomFill ? MGENX_PACK_RANDOM_FILL : 0);
+    ctx_.Check(mgenx_pack_batch(ctx_.get(), d_tmpl_.data(), d_crc_.data(), d_desc_.data(), n,
+                                d_pool_.data(), d_slab_.data(), (uint64_t)n * slot, nullptr,
+                                slot, d_len_.data(), opts, fillTime, s),
+               "mgenx_pack_batch");
+    h_slab_.Resize((size_t)n * slot);
+    len_.resize(n);
+    check_hip(hipMemcpyAsync(h_slab_.data(), d_slab_.data(), (size_t)n * slot,
+                             hipMemcpyDeviceToHost, s), "D2H slab");
+    check_hip(hipMemcpyAsync(len_.data(), d_len_.data(), n * 4, hipMemcpyDeviceToHost, s),
+              "D2H lengths");
+    ctx_.Sync();
+    return len_;
+  }
+  const uint8_t* Datagram(uint32_t i) const { return h_slab_.data() + (size_t)i * slot_; }
+  size_t Size() const { return desc_.size(); }
+  void Clear() { desc_.clear(); }
+
+ private:
+  Context& ctx_;
+  std::vector<mgenx_flow_tmpl> tmpl_;
+  std::vector<uint8_t> pool_;
+  std::vector<mgenx_pack_desc> desc_;
+  std::vector<uint32_t> len_;
+  uint32_t slot_ = MGENX_MAX_SIZE;
+  DeviceArray<mgenx_flow_tmpl> d_tmpl_;
+  DeviceArray<uint32_t> d_crc_;
+  DeviceArray<uint8_t> d_pool_;
+  DeviceArray<mgenx_pack_desc> d_desc_;
+  DeviceArray<uint8_t> d_slab_;
+  DeviceArray<uint32_t> d_len_;
+  PinnedArray<uint8_t> h_slab_;
+};
+
+// ---- analytics: Mgen::UpdateRecvAnalytics over batches ---------------------------------
+class FlowAnalytics {
+ public:
+  FlowAnalytics(Context& ctx, uint32_t maxFlows, double windowSec, uint32_t reportsPerFlow = 16)
+      : ctx_(ctx), max_(maxFlows), per_(reportsPerFlow), flows_(maxFlows),
+        reports_((size_t)maxFlows * reportsPerFlow), count_(maxFlows) {
+    ctx_.Check(mgenx_flow_init(ctx_.get(), flows_.data(), maxFlows, windowSec, ctx_.stream()),
+               "mgenx_flow_init");
+    check_hip(hipMemsetAsync(count_.data(), 0, maxFlows * 4, ctx_.stream()), "memset");
+  }
+  // MgenAnalyticTable::FindFlow (mgenAnalytic.cpp:312-328): key = (src addr+port, dst
+  // addr+port, flow id) -> dense index, created on first use.
+  uint32_t FindFlow(const std::string& src, const std::string& dst, uint32_t flowId) {
+    auto key = std::make_tuple(src, dst, flowId);
+    auto it = index_.find(key);
+    if (it != index_.end()) return it->second;
+    if (index_.size() >= max_) throw Error("FlowAnalytics: too many flows");
+    const uint32_t f = (uint32_t)index_.size();
+    index_.emplace(key, f);
+    return f;
+  }
+  // Update every record of a decoded batch, in receive order.  flowIdx[i] = FindFlow of
+  // record i (>= maxFlows skips it, e.g. for records with an error); rx times per record.
+  void Update(const RecvBatch& b, const std::vector<uint32_t>& flowIdx,
+              const std::vector<uint32_t>& rxSec, const std::vector<uint32_t>& rxUsec) {
+    const uint32_t n = b.Size();
+    d_idx_.Resize(n);
+    d_rxs_.Resize(n);
+    d_rxu_.Resize(n);
+    hipStream_t s = ctx_.stream();
+    check_hip(hipMemcpyAsync(d_idx_.data(), flowIdx.data(), n * 4, hipMemcpyHostToDevice, s), "H2D");
+    check_hip(hipMemcpyAsync(d_rxs_.data(), rxSec.data(), n * 4, hipMemcpyHostToDevice, s), "H2D");
+    check_hip(hipMemcpyAsync(d_rxu_.data(), rxUsec.data(), n * 4, hipMemcpyHostToDevice, s), "H2D");
+    ctx_.Check(mgenx_flow_reduce(ctx_.get(), d_idx_.data(), b.DevSeq(), b.DevTxSec(),
+                                 b.DevTxUsec(), b.DevMsgLen(), d_rxs_.data(), d_rxu_.data(), n,
+                                 flows_.data(), max_, reports_.data(), per_, count_.data(), s),
+               "mgenx_flow_reduce");
+  }
+  // all reports so far (the first reportsPerFlow of each flow), flow by flow
+  std::vector<mgenx_flow_report> Reports() {
+    std::vector<uint32_t> cnt(max_);
+    std::vector<mgenx_flow_report> all((size_t)max_ * per_), out;
+    check_hip(hipMemcpyAsync(cnt.data(), count_.data(), max_ * 4, hipMemcpyDeviceToHost,
+                             ctx_.stream()), "D2H");
+    check_hip(hipMemcpyAsync(all.data(), reports_.data(), all.size() * sizeof(all[0]),
+                             hipMemcpyDeviceToHost, ctx_.stream()), "D2H");
+    ctx_.Sync();
+    for (uint32_t f = 0; f < max_; f++)
+      for (uint32_t k = 0; k < cnt[f] && k < per_; k++) out.push_back(all[(size_t)f * per_ + k]);
+    return out;
+  }
+  // packed counters for the multi-GPU merge (all-reduce sum over ranks)
+  void Export(mgenx_flow_counters* dev_out) {
+    ctx_.Check(mgenx_flow_export(ctx_.get(), flows_.data(), max_, dev_out, ctx_.stream()),
+               "mgenx_flow_export");
+  }
+  mgenx_flow_state* DevState() const { return flows_.data(); }
+
+ private:
+  Context& ctx_;
+  uint32_t max_, per_;
+  DeviceArray<mgenx_flow_state> flows_;
+  DeviceArray<mgenx_flow_report> reports_;
+  DeviceArray<uint32_t> count_;
+  DeviceArray<uint32_t> d_idx_, d_rxs_, d_rxu_;
+  std::map<std::tuple<std::string, std::string, uint32_t>, uint32_t> index_;
+};
+
+}  // namespace mgenx
