@@ -1,14 +1,19 @@
 #!/usr/bin/env python3
 """Benchmark: device-resident MgenMsg unpack (+ receive CRC-32 check) on MI355X.
 
-Workload (BASELINE.json configs[1]): 1,048,576 pre-generated 1024-B UDP MgenMsg records
-(flow = 1 + i mod 64, per-flow seq, tx = 1.7e9 s + i us, dst 127.0.0.1/5000, checksum
-on: flags 0x0C), packed on the GPU by mgenx_pack_batch, resident in HBM.  One step =
-one mgenx_unpack_batch over the whole batch (CRC-validating decode into SoA columns).
+Headline (BASELINE.json configs[1]): 1,048,576 pre-generated 1024-B UDP MgenMsg records
+(flow = 1 + i mod 64, per-flow seq, tx = 1.7e9 s + i us, dst 127.0.0.1/5000, checksum on:
+flags 0x0C), packed on the GPU by mgenx_pack_batch, resident in HBM.  One step = one
+mgenx_unpack_batch over the whole batch (CRC-validating decode into SoA columns).
 
 Algorithmic bytes per step: read 1,073,741,824 B of records + write
 N x 32 B core columns = 1,107,296,256 B.  value = whole-job GB/s over all ranks (weak
 scaling: each rank owns its own 1M-record slab; no data-path collective).
+
+Extras (same JSON line, "extra"): header-only decode, pack (config 2), config 3 (mixed-size
+pack + unpack with DATA payload), config 4 (per-flow analytics + the RCCL all-reduce of the
+per-flow counters across ranks), config 5 (TCP stream scan + TCP-rule unpack), and the
+PCIe-inclusive rate (pinned host slab -> H2D -> unpack -> columns D2H).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
 (N > 1: launched by torch.distributed.run, one rank per GPU.)
@@ -34,18 +39,17 @@ ROUND = "r01"
 
 def cpu_baseline(budget_s=8.0):
     """Oracle (C restatement, byte-table CRC as in mgenMsg.cpp:538-539) on host cores:
-    MgenUdpTransport receive path = Unpack + CRC check per record, single thread."""
+    MgenUdpTransport receive path = Unpack + CRC check per record, single thread (the
+    reference's ProtoDispatcher is single-threaded), plus the same on 16 threads."""
     from oracle import oracle as O
     from mgen_amd.workloads import udp_fixed
-    # pack a sample with the oracle itself (CPU-side inputs for the CPU baseline)
     n0 = 4096
     tmpl, pool, desc = udp_fixed(n0, REC)
     slab, _ = O.udp_pack_batch(tmpl, desc, pool, n0 * REC, stride=REC, checksum=True)
     t = time.perf_counter()
     O.udp_recv_batch(slab, n0, stride=REC, fixed_len=REC, nthreads=1)
     dt = time.perf_counter() - t
-    reps = max(1, int(budget_s / max(dt, 1e-6)))
-    reps = min(reps, 400)
+    reps = max(1, min(400, int(budget_s / max(dt, 1e-6))))
     t = time.perf_counter()
     for _ in range(reps):
         f = O.udp_recv_batch(slab, n0, stride=REC, fixed_len=REC, nthreads=1)
@@ -53,10 +57,20 @@ def cpu_baseline(budget_s=8.0):
     assert int(f["err"].sum()) == 0
     n = n0 * reps
     gbps = n * (REC + 32) / dt / 1e9
+    # 16 threads (the GPU box's CPU share per GPU) on a 16x larger slab
+    n16 = n0 * 16
+    tmpl, pool, desc = udp_fixed(n16, REC)
+    slab16, _ = O.udp_pack_batch(tmpl, desc, pool, n16 * REC, stride=REC, checksum=True)
+    reps16 = max(1, reps // 4)
+    t = time.perf_counter()
+    for _ in range(reps16):
+        O.udp_recv_batch(slab16, n16, stride=REC, fixed_len=REC, nthreads=16)
+    dt16 = time.perf_counter() - t
     return {"value": round(gbps, 4), "unit": "GB/s", "cores": 1, "kind": "port",
             "sample": f"{n} x 1024-B checksummed UDP records ({reps} passes over a "
                       f"{n0}-record slab), oracle or_udp_recv, 1 thread, {dt:.1f} s",
-            "mmsg_per_s": round(n / dt / 1e6, 4)}
+            "mmsg_per_s": round(n / dt / 1e6, 4),
+            "threads16_gbps": round(n16 * reps16 * (REC + 32) / dt16 / 1e9, 3)}
 
 
 def load_traffic():
@@ -70,12 +84,164 @@ def load_traffic():
         return None
 
 
+def timed(torch, fn, reps=10):
+    """Mean time (ms) of fn() on the current stream, HIP events around reps calls."""
+    fn()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+# ------------------------------------------------------------------------ extras
+def extra_config3(torch, eng, dev):
+    """64 flows, sizes U{64..1472}, 16-B DATA payload, checksum on: pack + unpack."""
+    from mgen_amd import PACK_CHECKSUM, to_device
+    from mgen_amd.workloads import udp_mixed
+    n = N_REC
+    tmpl, pool, desc, offs, sizes = udp_mixed(n, 64, 1472, 64,
+                                              payload_hex="00112233445566778899aabbccddeeff")
+    total = int(offs[-1] + sizes[-1])
+    d_tmpl, d_pool, d_desc = to_device(tmpl), to_device(pool), to_device(desc)
+    d_offs = to_device(offs).view(torch.int64)
+    d_len = to_device(sizes).view(torch.int32)
+    crc = torch.empty(len(tmpl), dtype=torch.int32, device=dev)
+    eng.pack_prepare(d_tmpl, len(tmpl), d_pool, crc)
+    slab = torch.empty(total + 64, dtype=torch.uint8, device=dev)
+    out_len = torch.empty(n, dtype=torch.int32, device=dev)
+    cols = eng.alloc_cols(n)
+    pack = lambda: eng.pack(d_tmpl, crc, d_desc, n, d_pool, slab, rec_off=d_offs,  # noqa
+                            opts=PACK_CHECKSUM, out_len=out_len)
+    unpack = lambda: eng.unpack(slab, n, rec_off=d_offs, rec_len=d_len, cols=cols)  # noqa
+    pms, ums = timed(torch, pack), timed(torch, unpack)
+    assert int((cols["err"] != 0).sum()) == 0
+    pack_b = n * 20 + n * 16 + total
+    unpack_b = total + n * 32
+    return {"records": n, "bytes": total, "pack_ms": round(pms, 4), "unpack_ms": round(ums, 4),
+            "pack_gbps": round(pack_b / pms / 1e6, 1), "unpack_gbps": round(unpack_b / ums / 1e6, 1),
+            "combined_gbps": round((pack_b + unpack_b) / (pms + ums) / 1e6, 1)}
+
+
+def extra_config4(torch, eng, dev, world, rank, dist):
+    """1024 POISSON flows of 256-B messages; rank r owns flows with flow_id % world == r.
+    Per-flow MgenAnalytic::Update on the GPU, counters exported, one all-reduce(sum) of
+    1024 x 64 B across ranks (RCCL when world > 1)."""
+    from mgen_amd.workloads import poisson_flows
+    n_flows, n_total = 1024, 2 * N_REC
+    d = poisson_flows(n_total, n_flows, mean_gap_us=1000)
+    own = (d["flow_id"] % world) == rank
+    idx = np.where(own, d["flow_id"] - 1, n_flows).astype(np.uint32)
+    t = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in d.items()}
+    t_idx = torch.from_numpy(idx).to(dev)
+    n = len(idx)
+    state = {}
+
+    def run():
+        flows = eng.flow_init(n_flows, 1.0)
+        state["flows"] = flows
+        eng.flow_reduce(flows, n_flows, t_idx, t["seq"], t["tx_sec"], t["tx_usec"],
+                        t["msg_len"], t["rx_sec"], t["rx_usec"], n=n)
+    ms = timed(torch, run, reps=5)
+    counters = eng.flow_export(state["flows"], n_flows).view(torch.int64)
+    ar_ms = None
+    if world > 1:
+        dist.all_reduce(counters)  # warm
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(20):
+            dist.all_reduce(counters)
+        torch.cuda.synchronize()
+        ar_ms = (time.perf_counter() - t0) / 20 * 1e3
+    return {"records_per_rank": int(own.sum()), "records_total": n, "flows": n_flows,
+            "reduce_ms": round(ms, 4), "mrec_per_s": round(int(own.sum()) / ms / 1e3, 2),
+            "allreduce_bytes": n_flows * 64,
+            "allreduce_ms": None if ar_ms is None else round(ar_ms, 4)}
+
+
+def extra_config5(torch, eng, dev):
+    """TCP stream of 16 KiB records (checksum on): boundary scan + TCP-rule unpack over
+    1 GiB (a 64 MiB oracle-built stream tiled 16x: framing and CRCs stay valid)."""
+    from mgen_amd import OPT_TCP, SCAN_TCP, to_device
+    from mgen_amd.workloads import make_templates
+    from mgen_amd._abi import DESC_DTYPE
+    from oracle import oracle as O
+    n0 = 4096
+    tmpl, pool = make_templates(64)
+    desc = np.zeros(n0, DESC_DTYPE)
+    desc["tmpl"] = np.arange(n0) % 64
+    desc["seq_num"] = np.arange(n0) // 64
+    desc["tx_sec"] = 1_700_000_000
+    desc["tx_usec"] = np.arange(n0)
+    desc["msg_len"] = 16384
+    desc["flags"] = 4
+    s0 = np.asarray(O.tcp_tx_batch(tmpl, desc, np.full(n0, 16384, np.uint32), pool), np.uint8)
+    stream = to_device(s0).repeat(16)
+    n = n0 * 16
+    state = {}
+
+    def scan():
+        state["r"] = eng.stream_scan(stream, SCAN_TCP, cap=n + 1)
+    t0 = time.perf_counter()
+    reps = 5
+    for _ in range(reps):
+        scan()
+    scan_ms = (time.perf_counter() - t0) / reps * 1e3
+    offs, lens, info = state["r"]
+    assert int(info.n_records) == n and int(info.consumed) == stream.numel()
+    cols = eng.alloc_cols(n)
+    ums = timed(torch, lambda: eng.unpack(stream, n, rec_off=offs, rec_len=lens, opts=OPT_TCP,
+                                          cols=cols), reps=10)
+    assert int((cols["err"] != 0).sum()) == 0
+    b = stream.numel()
+    return {"records": n, "bytes": b, "scan_ms": round(scan_ms, 4),
+            "scan_gbps": round(b / scan_ms / 1e6, 1), "unpack_ms": round(ums, 4),
+            "unpack_gbps": round((b + n * 32) / ums / 1e6, 1), "candidates": int(info.candidates)}
+
+
+def extra_pcie(torch, eng, dev, slab):
+    """Config 2 from pinned host memory: 8 chunks of 128 MiB, two streams (copy of chunk
+    k+1 overlaps the unpack of chunk k), core columns copied back.  Wall-clock GB/s of
+    record bytes: the rate of a path that starts and ends in host memory."""
+    host = torch.empty(slab.numel(), dtype=torch.uint8, pin_memory=True)
+    host.copy_(slab)
+    chunks = 8
+    per = N_REC // chunks
+    streams = [torch.cuda.Stream(dev) for _ in range(2)]
+    dbuf = [torch.empty(per * REC, dtype=torch.uint8, device=dev) for _ in range(2)]
+    cols = [eng.alloc_cols(per) for _ in range(2)]
+    hcols = [{k: torch.empty(v.numel(), dtype=v.dtype, pin_memory=True) for k, v in c.items()}
+             for c in cols]
+
+    def run():
+        for c in range(chunks):
+            j = c % 2
+            with torch.cuda.stream(streams[j]):
+                dbuf[j].copy_(host[c * per * REC:(c + 1) * per * REC], non_blocking=True)
+                eng.unpack(dbuf[j], per, stride=REC, fixed_len=REC, cols=cols[j])
+                for k, v in cols[j].items():
+                    hcols[j][k].copy_(v, non_blocking=True)
+        torch.cuda.synchronize()
+    run()
+    t0 = time.perf_counter()
+    reps = 3
+    for _ in range(reps):
+        run()
+    dt = (time.perf_counter() - t0) / reps
+    assert int(hcols[0]["err"].sum()) == 0
+    return {"gbps": round(N_REC * REC / dt / 1e9, 2), "ms": round(dt * 1e3, 3),
+            "chunks": chunks, "note": "pinned H2D + unpack + core columns D2H, 2 streams"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true")
     args = ap.parse_args()
 
     import torch
@@ -91,7 +257,7 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device(f"cuda:{local}")
 
-    from mgen_amd import PACK_CHECKSUM, OPT_SKIP_CRC, Engine, MgenxCols, to_device
+    from mgen_amd import OPT_SKIP_CRC, PACK_CHECKSUM, Engine, to_device
     from mgen_amd.workloads import udp_fixed
 
     eng = Engine(local)
@@ -155,21 +321,28 @@ def main():
     torch.cuda.synchronize()
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
 
-    # secondary measurements (same stream, same events): header-only decode and pack
-    def timed(fn, reps=20):
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        fn()
-        a.record()
-        for _ in range(reps):
-            fn()
-        b.record()
-        torch.cuda.synchronize()
-        return a.elapsed_time(b) / reps
-    hdr_ms = timed(lambda: step(OPT_SKIP_CRC))
-    pack_ms = timed(do_pack)
+    hdr_ms = timed(torch, lambda: step(OPT_SKIP_CRC), reps=20)
+    pack_ms = timed(torch, do_pack, reps=20)
     step()
     torch.cuda.synchronize()
     assert int((cols["err"] != 0).sum()) == 0
+
+    extra = {"header_only_unpack_ms": round(hdr_ms, 4),
+             "header_only_mmsg_per_s": round(N_REC / (hdr_ms * 1e-3) / 1e6, 1),
+             "pack_ms": round(pack_ms, 4),
+             "pack_gbps": round((N_REC * REC + N_REC * 20) / (pack_ms * 1e-3) / 1e9, 1)}
+    if not args.no_extras:
+        def guard(name, fn):
+            try:
+                extra[name] = fn()
+            except Exception as e:  # an extra never hides the headline line
+                extra[name] = {"error": f"{type(e).__name__}: {e}"[:300]}
+        # config 4 on every rank (it has a collective); the rest on rank 0 only
+        guard("config4_flow_reduce", lambda: extra_config4(torch, eng, dev, world, rank, dist))
+        if rank == 0:
+            guard("config3_mixed_pack_unpack", lambda: extra_config3(torch, eng, dev))
+            guard("config5_tcp_scan_unpack", lambda: extra_config5(torch, eng, dev))
+            guard("pcie_inclusive_config2", lambda: extra_pcie(torch, eng, dev, slab))
 
     ms_per_step = elapsed / args.steps * 1e3
     value = world * ALGO_BYTES * args.steps / elapsed / 1e9
@@ -195,13 +368,9 @@ def main():
             "mmsg_per_s": round(world * N_REC * args.steps / elapsed / 1e6, 2),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBPS,
                          "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBPS, 4),
-                         "traffic": load_traffic(), "kernel": "mgenx::unpack_kernel",
+                         "traffic": load_traffic(), "kernel": "mgenx::unpack_fixed_kernel<16>",
                          "kernel_ms": round(kern_ms, 4)},
-            "extra": {"header_only_unpack_ms": round(hdr_ms, 4),
-                      "header_only_mmsg_per_s": round(N_REC / (hdr_ms * 1e-3) / 1e6, 1),
-                      "pack_ms": round(pack_ms, 4),
-                      "pack_gbps": round((N_REC * REC + N_REC * 20) / (pack_ms * 1e-3) / 1e9,
-                                         1)},
+            "extra": extra,
         }
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline()

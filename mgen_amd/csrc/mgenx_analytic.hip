@@ -11,8 +11,11 @@
 //   2. their fields are gathered flow-contiguous (24 B per record);
 //   3. one lane per flow runs Update over its records (prefetched 8 at a time), its
 //      1024-bit mask in LDS, transposed (word k of lane t at k * 64 + t: conflict-free).
-// FP64 arithmetic uses explicit round-to-nearest intrinsics so no multiply-add is fused:
-// results are bit-identical to the oracle compiled for x86-64.
+// FP64: every product that feeds an add goes through mul_rounded (an empty asm keeps the
+// backend from fusing them into an FMA: neither __dadd_rn/__dmul_rn nor `#pragma clang fp
+// contract(off)` prevented it -- a 1-ulp difference in a report's duration was the
+// symptom), so results are bit-identical to the oracle built for x86-64.
+#pragma clang fp contract(off)
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -30,12 +33,18 @@ struct Tm {
   int64_t sec, usec;
 };
 
+// a rounded product the following add cannot fuse with (an FMA would round once)
+__device__ __forceinline__ double mul_rounded(double a, double b) {
+  double p = a * b;
+  asm volatile("" : "+v"(p));
+  return p;
+}
 __device__ __forceinline__ double tdelta(Tm a, Tm b) {  // ProtoTime::Delta(a, b)
-  return __dadd_rn((double)(a.sec - b.sec), __dmul_rn(1.0e-06, (double)(a.usec - b.usec)));
+  return (double)(a.sec - b.sec) + mul_rounded(1.0e-06, (double)(a.usec - b.usec));
 }
 __device__ __forceinline__ Tm tadd(Tm t, double s) {  // ProtoTime += double
   const double whole = floor(s);
-  const int64_t us = (int64_t)__dadd_rn(__dmul_rn(__dsub_rn(s, whole), 1.0e06), 0.5);
+  const int64_t us = (int64_t)(mul_rounded(s - whole, 1.0e06) + 0.5);
   t.sec += (int64_t)whole;
   t.usec += us;
   while (t.usec >= 1000000) { t.usec -= 1000000; t.sec += 1; }
@@ -387,7 +396,7 @@ extern "C" void* mgenx_flow_ws_new() { return new mgenx_flow_ws(); }
 extern "C" void mgenx_flow_ws_free(void* p) {
   mgenx_flow_ws* w = static_cast<mgenx_flow_ws*>(p);
   if (!w) return;
-  if (w->mem) hipFree(w->mem);
+  if (w->mem) (void)hipFree(w->mem);
   delete w;
 }
 
@@ -435,14 +444,14 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
   int end_bit = 1;
   while (end_bit < 32 && (1ull << end_bit) <= n_flows) end_bit++;
   size_t cub_bytes = 0;
-  hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, (const uint32_t*)nullptr,
-                                     (uint32_t*)nullptr, (const uint32_t*)nullptr,
-                                     (uint32_t*)nullptr, (int)n, 0, end_bit, stream);
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, (const uint32_t*)nullptr,
+                                           (uint32_t*)nullptr, (const uint32_t*)nullptr,
+                                           (uint32_t*)nullptr, (int)n, 0, end_bit, stream);
   // layout: keys_in, keys_out, vals_in, vals_out, begin, end, 5 x u32 fields, u16 len, cub
   const size_t nb = a256((size_t)n * 4), fb = a256((size_t)n_flows * 4);
   const size_t need = 4 * nb + 2 * fb + 5 * nb + a256((size_t)n * 2) + a256(cub_bytes);
   if (ws.bytes < need) {
-    if (ws.mem) hipFree(ws.mem);
+    if (ws.mem) (void)hipFree(ws.mem);
     ws.mem = nullptr;
     ws.bytes = 0;
     if (hipMalloc(&ws.mem, need) != hipSuccess) {
@@ -475,8 +484,8 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
     snprintf(err, errn, "flow_reduce sort: %s", hipGetErrorString(e));
     return MGENX_EDEVICE;
   }
-  hipMemsetAsync(d_begin, 0, fb, stream);
-  hipMemsetAsync(d_end, 0, fb, stream);
+  (void)hipMemsetAsync(d_begin, 0, fb, stream);
+  (void)hipMemsetAsync(d_end, 0, fb, stream);
   hipLaunchKernelGGL(flow_gather_kernel, g, dim3(256), 0, stream, keys_out, vals_out, n, n_flows,
                      d_begin, d_end, seq, txs, txu, len, rxs, rxu, o_seq, o_txs, o_txu, o_len,
                      o_rxs, o_rxu);
