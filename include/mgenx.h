@@ -74,6 +74,18 @@ int  mgenx_ctx_destroy(mgenx_ctx* ctx);
 /* Last HIP error string seen by this context (static storage). */
 const char* mgenx_last_error(const mgenx_ctx* ctx);
 
+/* One decoded record's core fields, packed (32 B): the row-major alternative to the core
+ * columns -- the batch analogue of one unpacked MgenMsg object.  Written whole lines at a
+ * time (16 records = 512 contiguous bytes per wave store), it is the fastest output. */
+typedef struct {
+    uint32_t flow_id, seq_num, tx_sec, tx_usec;
+    uint32_t dst_addr4;              /* first 4 address bytes, in wire order in memory */
+    uint16_t msg_len, dst_port;
+    uint16_t payload_len;
+    uint8_t  flags, err;             /* err: MgenMsg::Error (+ MGENX_ERROR_OOB) */
+    uint8_t  dst_type, dst_len, payload_type, gps_status;
+} mgenx_rec;                         /* 32 bytes */
+
 /* ------------------------------------------------------------------ */
 /* Columns written by unpack: the MgenMsg state after Unpack() on a    */
 /* fresh MgenMsg (mgenMsg.cpp:315-500), one element per record.        */
@@ -107,6 +119,9 @@ typedef struct {
     uint32_t* lat_raw;      /* ntohl(latitude word): degrees = raw/60000 - 180 */
     uint32_t* lon_raw;
     int32_t*  alt;
+    /* row-major output: when set, unpack writes these 32-B records instead of the core
+     * columns (which may then be NULL); extended columns still go to their arrays */
+    mgenx_rec* rows;
 } mgenx_cols;
 
 /* Decode n records.  Record i starts at dev_slab + (dev_rec_off ? dev_rec_off[i] :

@@ -16,7 +16,7 @@ from ._abi import (  # noqa: F401
     ERROR_LENGTH, ERROR_NONE, ERROR_OOB, ERROR_VERSION, FLAG_CHECKSUM, FLAG_CHECKSUM_ERROR,
     FLAG_LAST_BUFFER, OPT_CHECKSUM_FORCE, OPT_SKIP_CRC, OPT_TCP, PACK_CHECKSUM,
     PACK_RANDOM_FILL, SCAN_SINK, SCAN_TCP, ScanInfo, FLOW_COUNTERS_DTYPE, FLOW_REPORT_DTYPE,
-    FLOW_STATE_BYTES, FLOW_STATE_DTYPE,
+    FLOW_STATE_BYTES, FLOW_STATE_DTYPE, REC_DTYPE,
 )
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -117,6 +117,10 @@ class Engine:
                 cols[name] = torch.empty(n * w if w > 1 else n, dtype=getattr(torch, dt),
                                          device=dev)
         return cols
+
+    def alloc_rows(self, n: int):
+        """mgenx_rec rows (32 B per record) as a uint8 tensor; pass as cols={"rows": t}."""
+        return self.torch.empty(n * 32, dtype=self.torch.uint8, device=f"cuda:{self.device}")
 
     @staticmethod
     def _cols_struct(cols):

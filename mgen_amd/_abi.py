@@ -52,7 +52,17 @@ CORE_BYTES_PER_RECORD = 32
 
 
 class MgenxCols(ctypes.Structure):
-    _fields_ = [(name, ctypes.c_void_p) for name, _, _ in COLS_CORE + COLS_EXT]
+    _fields_ = [(name, ctypes.c_void_p) for name, _, _ in COLS_CORE + COLS_EXT] + \
+        [("rows", ctypes.c_void_p)]
+
+
+# mgenx_rec: one decoded record's core fields (32 B, row-major alternative to the columns)
+REC_DTYPE = np.dtype([
+    ("flow_id", "<u4"), ("seq_num", "<u4"), ("tx_sec", "<u4"), ("tx_usec", "<u4"),
+    ("dst_addr4", "<u4"), ("msg_len", "<u2"), ("dst_port", "<u2"), ("payload_len", "<u2"),
+    ("flags", "u1"), ("err", "u1"), ("dst_type", "u1"), ("dst_len", "u1"),
+    ("payload_type", "u1"), ("gps_status", "u1")])
+assert REC_DTYPE.itemsize == 32
 
 
 def gps_raw(deg: float) -> int:

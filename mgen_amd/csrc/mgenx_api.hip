@@ -195,9 +195,9 @@ int mgenx_unpack_batch(mgenx_ctx* ctx, const uint8_t* dev_slab, uint64_t slab_by
   if (!dev_slab) return MGENX_EINVAL;
   if (!dev_rec_off && stride == 0 && n > 1) return MGENX_EINVAL;
   const mgenx_cols& k = *cols;
-  if (!k.flow_id || !k.seq_num || !k.tx_sec || !k.tx_usec || !k.msg_len || !k.dst_port ||
-      !k.flags || !k.err || !k.dst_type || !k.dst_len || !k.dst_addr4 || !k.payload_len ||
-      !k.payload_type || !k.gps_status)
+  if (!k.rows && (!k.flow_id || !k.seq_num || !k.tx_sec || !k.tx_usec || !k.msg_len ||
+                  !k.dst_port || !k.flags || !k.err || !k.dst_type || !k.dst_len ||
+                  !k.dst_addr4 || !k.payload_len || !k.payload_type || !k.gps_status))
     return MGENX_EINVAL;
   mgenx::UnpackParams p;
   p.slab = dev_slab;
@@ -212,7 +212,7 @@ int mgenx_unpack_batch(mgenx_ctx* ctx, const uint8_t* dev_slab, uint64_t slab_by
   p.expect = ctx->d_expect;
   p.expect_fixed = fixed_len < ctx->h_expect.size() ? ctx->h_expect[fixed_len] : 0u;
   p.sink = ctx->d_sink;
-  p.sink2 = mgenx::unpack_variant == 8 ? ctx->d_rows_diag : nullptr;
+  p.sink2 = mgenx::unpack_variant >= 8 ? ctx->d_rows_diag : nullptr;
   p.cols = k;
   const uint64_t groups = ((uint64_t)n + 15) / 16;
   const uint64_t per_block = (uint64_t)mgenx::unpack_threads() / 64;  // waves per block
@@ -292,9 +292,9 @@ int mgenx_pack_batch(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
 int mgenx_set_tuning(mgenx_ctx* ctx, int key, int value) {
   if (!ctx) return MGENX_EINVAL;
   if (key == MGENX_TUNE_UNPACK_VARIANT) {
-    if (value < 0 || value > 8) return MGENX_EINVAL;
+    if (value < 0 || value > 9) return MGENX_EINVAL;
     mgenx::unpack_variant = value;
-    if (value == 8 && !ctx->d_rows_diag &&
+    if ((value == 8 || value == 9) && !ctx->d_rows_diag &&
         hipMalloc((void**)&ctx->d_rows_diag, (size_t)32 << 20) != hipSuccess)
       return MGENX_ENOMEM;
     return MGENX_OK;

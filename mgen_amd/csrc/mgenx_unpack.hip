@@ -270,119 +270,53 @@ __device__ __forceinline__ void crc_verdict(bool crc_ok, bool tcp, uint8_t& err,
   }
 }
 
-// Fast path: fields straight from the 64-byte prefix words pw (layout accepted by
-// fast_layout) to the columns, each stored as soon as it is extracted so no decoded
-// header is live across the stores.
+// Extended columns of a fast-layout record: every word is read with all lanes active (the
+// DPP reads cross the quad), then only `do_store` lanes (quad lane 0) store.
 template <typename PW>
-__device__ __forceinline__ void store_fast(const mgenx_cols& c, uint64_t i, const PW& pw,
-                                           uint32_t buf_len, bool crc_ok, bool tcp) {
-  const uint32_t D = pw(5) >> 24;
-  const uint32_t hw = (D == 4u) ? pw(7) : pw(10);
+__device__ __forceinline__ void store_fast_ext(const mgenx_cols& c, uint64_t i, const PW& pw,
+                                               uint32_t buf_len, bool do_store) {
+  uint32_t wd[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) wd[k] = pw(k);
+  const uint32_t D = wd[5] >> 24;
+  const uint32_t hw = (D == 4u) ? wd[7] : wd[10];
   const uint32_t H = hw >> 24;
   const uint32_t ht = (hw >> 16) & 0xffu;
   const bool hv = ht == 1u || ht == 2u;
-  uint8_t flags = (uint8_t)(pw(0) >> 24);
-  uint8_t err = 0;
-  crc_verdict(crc_ok, tcp, err, flags);
-  c.msg_len[i] = bswap16((uint16_t)(pw(0) & 0xffffu));
-  c.flags[i] = flags;
-  c.err[i] = err;
-  c.flow_id[i] = bswap32(pw(1));
-  c.seq_num[i] = bswap32(pw(2));
-  c.tx_sec[i] = bswap32(pw(3));
-  c.tx_usec[i] = bswap32(pw(4));
-  c.dst_port[i] = bswap16((uint16_t)(pw(5) & 0xffffu));
-  c.dst_type[i] = (uint8_t)((pw(5) >> 16) & 0xffu);
-  c.dst_len[i] = (uint8_t)D;
-  c.dst_addr4[i] = pw(6);
-  // GPS + payload_type + payload_len: 16 bytes at word gi = (28 + D + H) / 4
-  const uint32_t gi = (28u + D + H) >> 2;  // 8, 9, 11 or 12
-  // AND/OR masks, not selects: LLVM folds a select chain over pw back into pw[gi + k],
-  // a dynamic index that puts pw in scratch memory
+  const uint32_t gi = (28u + D + H) >> 2;  // GPS block word: 8, 9, 11 or 12
+  // AND/OR masks, not selects: LLVM folds a select chain over an array back into a
+  // dynamic index, which puts the array in scratch memory
   const uint32_t m8 = 0u - (uint32_t)(gi == 8u), m9 = 0u - (uint32_t)(gi == 9u);
   const uint32_t m11 = 0u - (uint32_t)(gi == 11u), m12 = 0u - (uint32_t)(gi == 12u);
   auto gword = [&](int k) {
-    return (pw(8 + k) & m8) | (pw(9 + k) & m9) | (pw(11 + k) & m11) | (pw(12 + k) & m12);
+    return (wd[8 + k] & m8) | (wd[9 + k] & m9) | (wd[11 + k] & m11) | (wd[12 + k] & m12);
   };
   const uint32_t g3 = gword(3);
   const uint32_t len = 44u + D + H;
-  uint16_t plen = bswap16((uint16_t)(g3 >> 16));
+  const uint16_t plen = bswap16((uint16_t)(g3 >> 16));
   const bool pl_ok = plen != 0 && len + plen <= buf_len;  // mgenMsg.cpp:488-497
-  if (!pl_ok) plen = 0;
-  c.payload_len[i] = plen;
-  c.payload_type[i] = (uint8_t)(g3 >> 8);
-  c.gps_status[i] = (uint8_t)g3;
+  const uint32_t lat = bswap32(gword(0)), lon = bswap32(gword(1)), alt = bswap32(gword(2));
+  const bool d16 = D == 16u;
+  const u32x4_t dst = {wd[6], d16 ? wd[7] : 0u, d16 ? wd[8] : 0u, d16 ? wd[9] : 0u};
+  // host address at word 8 (dst IPv4) or 11 (dst IPv6); zero unless a valid type
+  const uint32_t a0 = (!hv || H == 0u) ? 0u : (D == 4u ? wd[8] : wd[11]);
+  const bool h16 = hv && H == 16u;  // only with dst IPv4 (D + H <= 20)
+  const u32x4_t host = {a0, h16 ? wd[9] : 0u, h16 ? wd[10] : 0u, h16 ? wd[11] : 0u};
+  if (!do_store) return;
   if (c.hdr_len) c.hdr_len[i] = (uint16_t)len;
   if (c.payload_off) c.payload_off[i] = pl_ok ? len : 0u;  // len % 4 == 0
   if (c.host_port) c.host_port[i] = hv ? bswap16((uint16_t)(hw & 0xffffu)) : 0;
   if (c.host_type) c.host_type[i] = hv ? (uint8_t)ht : 0;
   if (c.host_len) c.host_len[i] = hv ? (uint8_t)H : 0;
-  if (c.lat_raw) c.lat_raw[i] = bswap32(gword(0));
-  if (c.lon_raw) c.lon_raw[i] = bswap32(gword(1));
-  if (c.alt) c.alt[i] = (int32_t)bswap32(gword(2));
-  if (c.dst_addr) {
-    u32x4_t* dp = reinterpret_cast<u32x4_t*>(c.dst_addr + i * 16);
-    const bool d16 = D == 16u;
-    *dp = u32x4_t{pw(6), d16 ? pw(7) : 0u, d16 ? pw(8) : 0u, d16 ? pw(9) : 0u};
-  }
-  if (c.host_addr) {
-    // host address at word 8 (dst IPv4) or 11 (dst IPv6); zero unless a valid type
-    const uint32_t a0 = (!hv || H == 0u) ? 0u : (D == 4u ? pw(8) : pw(11));
-    const bool h16 = hv && H == 16u;  // only with dst IPv4 (D + H <= 20)
-    u32x4_t* hp = reinterpret_cast<u32x4_t*>(c.host_addr + i * 16);
-    *hp = u32x4_t{a0, h16 ? pw(9) : 0u, h16 ? pw(10) : 0u, h16 ? pw(11) : 0u};
-  }
+  if (c.lat_raw) c.lat_raw[i] = lat;
+  if (c.lon_raw) c.lon_raw[i] = lon;
+  if (c.alt) c.alt[i] = (int32_t)alt;
+  if (c.dst_addr) *reinterpret_cast<u32x4_t*>(c.dst_addr + i * 16) = dst;
+  if (c.host_addr) *reinterpret_cast<u32x4_t*>(c.host_addr + i * 16) = host;
 }
 
-// Fast path, core columns only (the fixed-length kernel): words 0..7 of the prefix, the
-// host word hw and the GPS block's last word g3 (payload_type, payload_len, gps_status).
-__device__ __forceinline__ void store_fast_core(const mgenx_cols& c, uint32_t i,
-                                                const uint32_t (&w)[8], uint32_t hw,
-                                                uint32_t g3, uint32_t buf_len, bool crc_ok,
-                                                bool tcp) {
-  const uint32_t D = w[5] >> 24;
-  uint8_t flags = (uint8_t)(w[0] >> 24);
-  uint8_t err = 0;
-  crc_verdict(crc_ok, tcp, err, flags);
-  c.msg_len[i] = bswap16((uint16_t)(w[0] & 0xffffu));
-  c.flags[i] = flags;
-  c.err[i] = err;
-  c.flow_id[i] = bswap32(w[1]);
-  c.seq_num[i] = bswap32(w[2]);
-  c.tx_sec[i] = bswap32(w[3]);
-  c.tx_usec[i] = bswap32(w[4]);
-  c.dst_port[i] = bswap16((uint16_t)(w[5] & 0xffffu));
-  c.dst_type[i] = (uint8_t)((w[5] >> 16) & 0xffu);
-  c.dst_len[i] = (uint8_t)D;
-  c.dst_addr4[i] = w[6];
-  const uint32_t len = 44u + D + (hw >> 24);
-  uint16_t plen = bswap16((uint16_t)(g3 >> 16));
-  if (!(plen != 0 && len + plen <= buf_len)) plen = 0;  // mgenMsg.cpp:488-497
-  c.payload_len[i] = plen;
-  c.payload_type[i] = (uint8_t)(g3 >> 8);
-  c.gps_status[i] = (uint8_t)g3;
-}
-
-// General path: a header decoded by parse_header.
-__device__ __forceinline__ void store_hdr(const mgenx_cols& c, uint64_t i, const Hdr& h,
-                                          bool crc_ok, bool tcp) {
-  uint8_t err = h.err;
-  uint8_t flags = h.flags;
-  crc_verdict(crc_ok, tcp, err, flags);
-  c.flow_id[i] = h.flow;
-  c.seq_num[i] = h.seq;
-  c.tx_sec[i] = h.sec;
-  c.tx_usec[i] = h.usec;
-  c.msg_len[i] = h.msg_len;
-  c.dst_port[i] = h.dst_port;
-  c.flags[i] = flags;
-  c.err[i] = err;
-  c.dst_type[i] = h.dst_type;
-  c.dst_len[i] = h.dst_len;
-  c.dst_addr4[i] = h.dst4;
-  c.payload_len[i] = h.plen;
-  c.payload_type[i] = h.ptype;
-  c.gps_status[i] = h.gps;
+// Extended columns of a record decoded by parse_header (quad lane 0).
+__device__ __forceinline__ void store_hdr_ext(const mgenx_cols& c, uint64_t i, const Hdr& h) {
   if (c.hdr_len) c.hdr_len[i] = h.hdr_len;
   if (c.payload_off) c.payload_off[i] = h.poff;
   if (c.host_port) c.host_port[i] = h.host_port;
@@ -401,22 +335,76 @@ __device__ __forceinline__ void store_hdr(const mgenx_cols& c, uint64_t i, const
   }
 }
 
-// A descriptor pointing outside the slab: ERROR_OOB and zeroed core columns.
-__device__ __forceinline__ void store_oob(const mgenx_cols& c, uint64_t i) {
-  c.err[i] = MGENX_ERROR_OOB;
-  c.flags[i] = 0;
-  c.msg_len[i] = 0;
-  c.flow_id[i] = 0;
-  c.seq_num[i] = 0;
-  c.tx_sec[i] = 0;
-  c.tx_usec[i] = 0;
-  c.dst_port[i] = 0;
-  c.dst_type[i] = 0;
-  c.dst_len[i] = 0;
-  c.dst_addr4[i] = 0;
-  c.payload_len[i] = 0;
-  c.payload_type[i] = 0;
-  c.gps_status[i] = 0;
+// A record decoded by parse_header, stored whole by quad lane 0 (the rare general
+// layouts and short records): core fields as a row or as columns, then extended columns.
+__device__ __forceinline__ void store_hdr_q0(const mgenx_cols& c, uint64_t i, const Hdr& h,
+                                             bool crc_ok, bool tcp) {
+  uint8_t err = h.err, flags = h.flags;
+  crc_verdict(crc_ok, tcp, err, flags);
+  if (c.rows) {
+    u32x4_t* r = reinterpret_cast<u32x4_t*>(c.rows + i);
+    r[0] = u32x4_t{h.flow, h.seq, h.sec, h.usec};
+    r[1] = u32x4_t{h.dst4, (uint32_t)h.msg_len | ((uint32_t)h.dst_port << 16),
+                   (uint32_t)h.plen | ((uint32_t)flags << 16) | ((uint32_t)err << 24),
+                   (uint32_t)h.dst_type | ((uint32_t)h.dst_len << 8) |
+                       ((uint32_t)h.ptype << 16) | ((uint32_t)h.gps << 24)};
+  } else {
+    c.flow_id[i] = h.flow;
+    c.seq_num[i] = h.seq;
+    c.tx_sec[i] = h.sec;
+    c.tx_usec[i] = h.usec;
+    c.msg_len[i] = h.msg_len;
+    c.dst_port[i] = h.dst_port;
+    c.flags[i] = flags;
+    c.err[i] = err;
+    c.dst_type[i] = h.dst_type;
+    c.dst_len[i] = h.dst_len;
+    c.dst_addr4[i] = h.dst4;
+    c.payload_len[i] = h.plen;
+    c.payload_type[i] = h.ptype;
+    c.gps_status[i] = h.gps;
+  }
+  store_hdr_ext(c, i, h);
+}
+
+// The core fields of one record, as every lane of its quad holds them.
+struct Core {
+  uint32_t flow, seq, sec, usec, dst4, msg_len, dport, plen, flags, err, dtype, dlen, ptype, gps;
+};
+
+// Branch-free core output of a quad: lane q stores column q (u32 / u16 / u8 groups, five
+// store instructions), or bytes 8q..8q+7 of the record's mgenx_rec row.  Lanes whose
+// record is past the batch end store to the sink.  Every lane must call it (no branch
+// around the stores: see unpack_fixed_kernel on vmcnt and skipped stores).
+template <bool kRows>
+__device__ __forceinline__ void store_core_quad(const UnpackParams& p, uint64_t idx, bool in,
+                                                int lane, int q, const Core& v) {
+  const uint64_t sink = (uint64_t)p.sink + 8u * (uint32_t)lane;
+  if (kRows) {
+    const uint64_t x =
+        q == 0 ? ((uint64_t)v.seq << 32 | v.flow)
+      : q == 1 ? ((uint64_t)v.usec << 32 | v.sec)
+      : q == 2 ? ((uint64_t)((v.msg_len & 0xffffu) | v.dport << 16) << 32 | v.dst4)
+               : ((uint64_t)(v.dtype | v.dlen << 8 | v.ptype << 16 | v.gps << 24) << 32 |
+                  ((v.plen & 0xffffu) | v.flags << 16 | v.err << 24));
+    st_g64(in ? (uint64_t)p.cols.rows + idx * 32 + 8u * q : sink, x);
+    return;
+  }
+  const mgenx_cols& c = p.cols;
+  auto at = [&](uint64_t base, uint32_t size) { return in ? base + idx * size : sink; };
+  const uint64_t u32 = pick4(q, (uint64_t)c.flow_id, (uint64_t)c.seq_num, (uint64_t)c.tx_sec,
+                             (uint64_t)c.tx_usec);
+  const uint64_t u16 = pick4(q, (uint64_t)c.msg_len, (uint64_t)c.dst_port,
+                             (uint64_t)c.payload_len, (uint64_t)c.payload_len);
+  const uint64_t u8a = pick4(q, (uint64_t)c.flags, (uint64_t)c.err, (uint64_t)c.dst_type,
+                             (uint64_t)c.dst_len);
+  const uint64_t u8b = pick4(q, (uint64_t)c.payload_type, (uint64_t)c.gps_status,
+                             (uint64_t)c.payload_type, (uint64_t)c.gps_status);
+  st_g32(at(u32, 4), q == 0 ? v.flow : q == 1 ? v.seq : q == 2 ? v.sec : v.usec);
+  st_g32(at((uint64_t)c.dst_addr4, 4), v.dst4);
+  st_g16(at(u16, 2), q == 0 ? v.msg_len : q == 1 ? v.dport : v.plen);
+  st_g8(at(u8a, 1), q == 0 ? v.flags : q == 1 ? v.err : q == 2 ? v.dtype : v.dlen);
+  st_g8(at(u8b, 1), (q & 1) == 0 ? v.ptype : v.gps);
 }
 
 // MODE (diagnostic ablations, never the product path): 0 = full kernel, 1 = row loads +
@@ -462,6 +450,10 @@ unpack_kernel(UnpackParams p) {
   const bool force = (p.opts & MGENX_OPT_CHECKSUM_FORCE) != 0;
   const bool tcp = (p.opts & MGENX_OPT_TCP) != 0;
   const bool want_ext = p.cols.dst_addr || p.cols.host_addr;
+  const mgenx_cols& cc = p.cols;
+  const bool any_ext = cc.hdr_len || cc.payload_off || cc.host_port || cc.host_type ||
+                       cc.host_len || cc.lat_raw || cc.lon_raw || cc.alt || cc.dst_addr ||
+                       cc.host_addr;
 
   // Per-wave predictor: while recent groups carried checksummed records, issue the row
   // loads speculatively together with the header load (one memory round per group); a
@@ -495,17 +487,10 @@ unpack_kernel(UnpackParams p) {
       pf = ldu128((live && L >= 16u * (q + 1)) ? rec + 16 * q : dummy);
       if (kCrc) expect = p.expect[live ? L : 0u];
     };
-    // word j of the quad's prefix: lane j/4's pf component j%4 (all lanes must be active)
-    auto gather = [&](uint32_t (&pw)[16]) {
-      quad_bcast<0>(pf, pw);
-      quad_bcast<1>(pf, pw);
-      quad_bcast<2>(pf, pw);
-      quad_bcast<3>(pf, pw);
-    };
-    auto unpack_words = [&](const uint32_t (&pw)[16]) {
+    auto unpack_words = [&]() {
       if (pfx) {
 #pragma unroll
-        for (int j = 0; j < 8; j++) w[j] = pw[j];
+        for (int j = 0; j < 8; j++) w[j] = prefix_word(pf, j);
       } else if (live && L >= MGENX_MIN_SIZE) {
         load_fixed(rec, buf_len, w);  // 28..31-byte records
       } else {
@@ -515,10 +500,8 @@ unpack_kernel(UnpackParams p) {
     };
     bool needs_crc = false;
     auto decide = [&]() {
-      uint32_t pw[16];
-      gather(pw);
-      if (kCrc && live && q == 0) {
-        unpack_words(pw);
+      if (kCrc && live) {  // every lane of the quad: the tail's stores are per quad
+        unpack_words();
         const bool flagged = force || (((w[0] >> 24) & MGENX_FLAG_CHECKSUM) != 0 &&
                                        buf_len >= MGENX_MIN_SIZE &&
                                        ((w[0] >> 16) & 0xffu) == 2u);
@@ -650,24 +633,61 @@ unpack_kernel(UnpackParams p) {
     if (!kCrc) load_header();
     const bool vec_crc = needs_crc && live && L >= 32;
 
-    uint32_t pw[16];
-    gather(pw);
-    if (live && q == 0) {
-      // each parse path stores its own columns (no join merging two header values)
-      if (pfx64 && fast_layout(pw[0], pw[5], (pw[5] >> 24) == 4u ? pw[7] : pw[10])) {
-        store_fast(p.cols, rec_idx, [&](int k) { return pw[k]; }, buf_len,
-                   !needs_crc || tot == expect, tcp);
-      } else {
+    auto pw = [&](int j) { return prefix_word(pf, j); };  // all lanes active here
+    // Decode: every lane of a quad computes its record's core fields from the prefix words
+    // (fast layouts in registers); general layouts and short records are parsed by quad
+    // lane 0 and broadcast.  Then the quad stores branch-free (store_core_quad).
+    const uint32_t D = pw(5) >> 24;
+    const uint32_t hw = (D == 4u) ? pw(7) : pw(10);
+    const bool fast = pfx64 && fast_layout(pw(0), pw(5), hw);
+    const uint32_t gi = (28u + D + (hw >> 24)) >> 2;
+    const uint32_t g3 = (pw(11) & (0u - (uint32_t)(gi == 8u))) |
+                        (pw(12) & (0u - (uint32_t)(gi == 9u))) |
+                        (pw(14) & (0u - (uint32_t)(gi == 11u))) |
+                        (pw(15) & (0u - (uint32_t)(gi == 12u)));
+    Core v;
+    v.flow = bswap32(pw(1));
+    v.seq = bswap32(pw(2));
+    v.sec = bswap32(pw(3));
+    v.usec = bswap32(pw(4));
+    v.dst4 = pw(6);
+    v.msg_len = bswap16((uint16_t)(pw(0) & 0xffffu));
+    v.dport = bswap16((uint16_t)(pw(5) & 0xffffu));
+    const uint32_t hlen = 44u + D + (hw >> 24);
+    v.plen = bswap16((uint16_t)(g3 >> 16));
+    if (!(v.plen != 0 && hlen + v.plen <= buf_len)) v.plen = 0;  // mgenMsg.cpp:488-497
+    v.flags = pw(0) >> 24;
+    v.err = 0;
+    v.dtype = (pw(5) >> 16) & 0xffu;
+    v.dlen = D;
+    v.ptype = (g3 >> 8) & 0xffu;
+    v.gps = g3 & 0xffu;
+    uint32_t crc_ok = (!needs_crc || tot == expect) ? 1u : 0u;
+    // general layouts / short records: parsed and stored whole by quad lane 0 (rare); their
+    // quad's branch-free stores below go to the sink
+    const bool slow = live && !fast;
+    if (__any(slow)) {
+      unpack_words();  // every lane active: its DPP reads lanes 1..3 of the quad
+      if (slow && q == 0) {
         Hdr h;
-        unpack_words(pw);
         parse_header(rec, buf_len, want_ext, w, h);
-        const bool crc_ok =
-            !needs_crc || (vec_crc ? (tot == expect) : small_crc_ok(rec, L));
-        store_hdr(p.cols, rec_idx, h, crc_ok, tcp);
+        const bool ok = !needs_crc || (vec_crc ? (tot == expect) : small_crc_ok(rec, L));
+        store_hdr_q0(p.cols, rec_idx, h, ok, tcp);
       }
-    } else if (oob && q == 0) {
-      store_oob(p.cols, rec_idx);
     }
+    if (!crc_ok) {  // the caller's receive check (mgenTransport.cpp:971-975, 1552-1560)
+      v.err = MGENX_ERROR_CHECKSUM;
+      if (tcp) v.flags |= MGENX_FLAG_CHECKSUM_ERROR;
+    }
+    if (!live) {  // outside the slab (or past the batch end: those lanes store to the sink)
+      v.flow = v.seq = v.sec = v.usec = v.dst4 = v.msg_len = v.dport = v.plen = v.flags = 0;
+      v.dtype = v.dlen = v.ptype = v.gps = 0;
+      v.err = MGENX_ERROR_OOB;
+    }
+    const bool in = valid && !slow;
+    if (p.cols.rows) store_core_quad<true>(p, rec_idx, in, lane, q, v);
+    else store_core_quad<false>(p, rec_idx, in, lane, q, v);
+    if (any_ext) store_fast_ext(p.cols, rec_idx, pw, buf_len, fast && q == 0);
   }
 }
 
@@ -684,7 +704,7 @@ unpack_kernel(UnpackParams p) {
 // Semantics are those of unpack_kernel<true> (same helpers, same column stores).
 // MODE (ablations): 1 = loads + XOR only (no LDS lookups), 5 = MODE 1 without the tail
 // (no decode, no column stores; the CRC word is kept alive through one store per wave)
-template <int NR, int MODE = 0>
+template <int NR, int MODE = 0, bool kRows = false>
 __global__ void __launch_bounds__(kUnpackThreads)
 unpack_fixed_kernel(UnpackParams p, uint32_t expect) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -797,7 +817,12 @@ unpack_fixed_kernel(UnpackParams p, uint32_t expect) {
     }
     const bool in = idx < p.n && MODE != 6;  // MODE 6 (ablation): every store to the sink
     const uint64_t sink = (uint64_t)p.sink + 4u * (uint32_t)lane;
+    // MODE 9 (ablation): the same stores to distinct per-wave addresses that stay in L2
+    // (2 KiB per wave: 8 MiB total), so they never reach HBM during the kernel
+    int store_no = 0;
     auto at = [&](uint64_t base, uint32_t size) {
+      if (MODE == 9)
+        return (uint64_t)p.sink2 + (uint64_t)wave_id * 2048 + 256u * (store_no++) + 4u * lane;
       return in ? base + (uint64_t)idx * size : sink;
     };
     const mgenx_cols& c = p.cols;
@@ -809,14 +834,16 @@ unpack_fixed_kernel(UnpackParams p, uint32_t expect) {
                                (uint64_t)c.dst_len);
     const uint64_t u8b = pick4(q, (uint64_t)c.payload_type, (uint64_t)c.gps_status,
                                (uint64_t)c.payload_type, (uint64_t)c.gps_status);
-    if (MODE == 8) {  // ablation: one 32-B record per quad (lane q writes bytes 8q..8q+7)
+    if (kRows || MODE == 8) {  // mgenx_rec rows: lane q writes bytes 8q..8q+7 of its record
+      // (16 records = 512 contiguous bytes per store instruction: whole lines)
       const uint64_t v =
           q == 0 ? ((uint64_t)seq << 32 | flow)
         : q == 1 ? ((uint64_t)usec << 32 | sec)
         : q == 2 ? ((uint64_t)(msg_len | dport << 16) << 32 | dst4)
                  : ((uint64_t)(dtype | dlen << 8 | ptype << 16 | gps << 24) << 32 |
                     (plen | flags << 16 | err << 24));
-      st_g64(in ? (uint64_t)p.sink2 + (uint64_t)idx * 32 + 8 * q : sink, v);
+      const uint64_t rbase = kRows ? (uint64_t)p.cols.rows : (uint64_t)p.sink2;
+      st_g64(in ? rbase + (uint64_t)idx * 32 + 8 * q : (uint64_t)p.sink + 8u * lane, v);
       return;
     }
     if (MODE == 7) {  // ablation: the tail's work without its stores (kept alive)
@@ -883,7 +910,7 @@ unpack_fixed_kernel(UnpackParams p, uint32_t expect) {
           }
         }
         uint32_t c4[4];
-        if (MODE == 1 || MODE >= 5) {
+        if (MODE == 1 || (MODE >= 5 && MODE != 8 && MODE != 9)) {
           c4[0] = (h0 << 1) ^ x.x; c4[1] = (h1 << 1) ^ x.y;
           c4[2] = (h2 << 1) ^ x.z; c4[3] = (h3 << 1) ^ x.w;
         } else {
@@ -894,7 +921,7 @@ unpack_fixed_kernel(UnpackParams p, uint32_t expect) {
         __builtin_amdgcn_sched_barrier(0);
         d[j] = ld_row(boff_n, j);
         __builtin_amdgcn_sched_barrier(0);
-        if (MODE == 1 || MODE >= 5) {
+        if (MODE == 1 || (MODE >= 5 && MODE != 8 && MODE != 9)) {
           h0 = c4[0]; h1 = c4[1]; h2 = c4[2]; h3 = c4[3];
           continue;
         }
@@ -975,27 +1002,31 @@ static hipError_t launch_mode(const UnpackParams& p, int grid, hipStream_t strea
   return launch_lds(unpack_kernel<true, MODE>, attr_done, p, grid, stream);
 }
 
-template <int NR, int MODE = 0>
+template <int NR, int MODE = 0, bool kRows = false>
 static hipError_t launch_fixed(const UnpackParams& p, int grid, hipStream_t stream) {
   static bool attr_done = false;
   if (!attr_done) {
-    hipError_t e = hipFuncSetAttribute((const void*)unpack_fixed_kernel<NR, MODE>,
+    hipError_t e = hipFuncSetAttribute((const void*)unpack_fixed_kernel<NR, MODE, kRows>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)kUnpackLdsBytes);
     if (e != hipSuccess) return e;
     attr_done = true;
   }
-  hipLaunchKernelGGL((unpack_fixed_kernel<NR, MODE>), dim3(grid), dim3(kUnpackThreads),
+  hipLaunchKernelGGL((unpack_fixed_kernel<NR, MODE, kRows>), dim3(grid), dim3(kUnpackThreads),
                      kUnpackLdsBytes, stream, p, p.expect_fixed);
   return hipGetLastError();
 }
 
 typedef hipError_t (*fixed_launcher)(const UnpackParams&, int, hipStream_t);
-static const fixed_launcher kFixedLaunch[17] = {
-    nullptr,          nullptr,          launch_fixed<2>,  launch_fixed<3>,  launch_fixed<4>,
-    launch_fixed<5>,  launch_fixed<6>,  launch_fixed<7>,  launch_fixed<8>,  launch_fixed<9>,
-    launch_fixed<10>, launch_fixed<11>, launch_fixed<12>, launch_fixed<13>, launch_fixed<14>,
-    launch_fixed<15>, launch_fixed<16>};
+#define MGENX_FIXED_TABLE(R)                                                              \
+  {nullptr, nullptr, launch_fixed<2, 0, R>, launch_fixed<3, 0, R>, launch_fixed<4, 0, R>,    \
+   launch_fixed<5, 0, R>, launch_fixed<6, 0, R>, launch_fixed<7, 0, R>, launch_fixed<8, 0, R>, \
+   launch_fixed<9, 0, R>, launch_fixed<10, 0, R>, launch_fixed<11, 0, R>,                    \
+   launch_fixed<12, 0, R>, launch_fixed<13, 0, R>, launch_fixed<14, 0, R>,                   \
+   launch_fixed<15, 0, R>, launch_fixed<16, 0, R>}
+static const fixed_launcher kFixedLaunch[17] = MGENX_FIXED_TABLE(false);
+static const fixed_launcher kFixedLaunchRows[17] = MGENX_FIXED_TABLE(true);
+#undef MGENX_FIXED_TABLE
 
 hipError_t launch_unpack(const UnpackParams& p, int grid, hipStream_t stream) {
   if (p.opts & MGENX_OPT_SKIP_CRC) {
@@ -1011,12 +1042,14 @@ hipError_t launch_unpack(const UnpackParams& p, int grid, hipStream_t stream) {
                      p.stride > 0 && p.n <= 0xFFFFFFF0u && !ext &&
                      p.slab_bytes < 0xFFFF0000ull && p.slab_bytes >= 64ull * (nr + 1) + 16 &&
                      p.slab_bytes >= p.fixed_len;
-  if (unpack_variant == 0 && fixed) return kFixedLaunch[(p.fixed_len + 63) / 64](p, grid, stream);
+  if (unpack_variant == 0 && fixed)
+    return (c.rows ? kFixedLaunchRows : kFixedLaunch)[(p.fixed_len + 63) / 64](p, grid, stream);
   if (unpack_variant == 4 && fixed && p.fixed_len == 1024) return launch_fixed<16, 1>(p, grid, stream);
   if (unpack_variant == 5 && fixed && p.fixed_len == 1024) return launch_fixed<16, 5>(p, grid, stream);
   if (unpack_variant == 6 && fixed && p.fixed_len == 1024) return launch_fixed<16, 6>(p, grid, stream);
   if (unpack_variant == 7 && fixed && p.fixed_len == 1024) return launch_fixed<16, 7>(p, grid, stream);
   if (unpack_variant == 8 && fixed && p.fixed_len == 1024 && p.sink2) return launch_fixed<16, 8>(p, grid, stream);
+  if (unpack_variant == 9 && fixed && p.fixed_len == 1024 && p.sink2) return launch_fixed<16, 9>(p, grid, stream);
   switch (unpack_variant) {
     case 1: return launch_mode<1>(p, grid, stream);
     case 2: return launch_mode<2>(p, grid, stream);
