@@ -60,6 +60,9 @@ __device__ __forceinline__ void st_g16(uint64_t a, uint32_t v) { *(g_u16*)a = (u
 __device__ __forceinline__ void st_g32(uint64_t a, uint32_t v) { *(g_u32*)a = v; }
 typedef __attribute__((address_space(1))) uint64_t g_u64;
 __device__ __forceinline__ void st_g64(uint64_t a, uint64_t v) { *(g_u64*)a = v; }
+__device__ __forceinline__ void st_g64_nt(uint64_t a, uint64_t v) {
+  __builtin_nontemporal_store(v, (g_u64*)a);
+}
 // a[k] for k = sel in 0..3, as AND/OR masks (a select chain over struct fields or arrays
 // can be folded back into a dynamic index into a stack copy)
 __device__ __forceinline__ uint64_t pick4(int sel, uint64_t a0, uint64_t a1, uint64_t a2,

@@ -367,6 +367,74 @@ __device__ __forceinline__ void store_hdr_q0(const mgenx_cols& c, uint64_t i, co
   store_hdr_ext(c, i, h);
 }
 
+// Fast-layout record stored whole by quad lane 0 from the gathered prefix words pw[16]
+// (general kernel): core fields as a row or as columns, then extended columns.
+__device__ __forceinline__ void store_fast_q0(const mgenx_cols& c, uint64_t i,
+                                              const uint32_t (&pw)[16], uint32_t buf_len,
+                                              bool crc_ok, bool tcp) {
+  const uint32_t D = pw[5] >> 24;
+  const uint32_t hw = (D == 4u) ? pw[7] : pw[10];
+  const uint32_t gi = (28u + D + (hw >> 24)) >> 2;
+  const uint32_t g3 = (pw[11] & (0u - (uint32_t)(gi == 8u))) |
+                      (pw[12] & (0u - (uint32_t)(gi == 9u))) |
+                      (pw[14] & (0u - (uint32_t)(gi == 11u))) |
+                      (pw[15] & (0u - (uint32_t)(gi == 12u)));
+  const uint32_t len = 44u + D + (hw >> 24);
+  uint32_t plen = bswap16((uint16_t)(g3 >> 16));
+  if (!(plen != 0 && len + plen <= buf_len)) plen = 0;  // mgenMsg.cpp:488-497
+  uint8_t flags = (uint8_t)(pw[0] >> 24), err = 0;
+  crc_verdict(crc_ok, tcp, err, flags);
+  const uint32_t msg_len = bswap16((uint16_t)(pw[0] & 0xffffu));
+  const uint32_t dport = bswap16((uint16_t)(pw[5] & 0xffffu));
+  const uint32_t dtype = (pw[5] >> 16) & 0xffu;
+  if (c.rows) {
+    u32x4_t* r = reinterpret_cast<u32x4_t*>(c.rows + i);
+    r[0] = u32x4_t{bswap32(pw[1]), bswap32(pw[2]), bswap32(pw[3]), bswap32(pw[4])};
+    r[1] = u32x4_t{pw[6], msg_len | (dport << 16), plen | ((uint32_t)flags << 16) |
+                   ((uint32_t)err << 24),
+                   dtype | (D << 8) | (((g3 >> 8) & 0xffu) << 16) | ((g3 & 0xffu) << 24)};
+  } else {
+    c.msg_len[i] = (uint16_t)msg_len;
+    c.flags[i] = flags;
+    c.err[i] = err;
+    c.flow_id[i] = bswap32(pw[1]);
+    c.seq_num[i] = bswap32(pw[2]);
+    c.tx_sec[i] = bswap32(pw[3]);
+    c.tx_usec[i] = bswap32(pw[4]);
+    c.dst_port[i] = (uint16_t)dport;
+    c.dst_type[i] = (uint8_t)dtype;
+    c.dst_len[i] = (uint8_t)D;
+    c.dst_addr4[i] = pw[6];
+    c.payload_len[i] = (uint16_t)plen;
+    c.payload_type[i] = (uint8_t)(g3 >> 8);
+    c.gps_status[i] = (uint8_t)g3;
+  }
+}
+
+// A descriptor outside the slab: ERROR_OOB and zeroed core fields (quad lane 0).
+__device__ __forceinline__ void store_oob_q0(const mgenx_cols& c, uint64_t i) {
+  if (c.rows) {
+    u32x4_t* r = reinterpret_cast<u32x4_t*>(c.rows + i);
+    r[0] = u32x4_t{0u, 0u, 0u, 0u};
+    r[1] = u32x4_t{0u, 0u, (uint32_t)MGENX_ERROR_OOB << 24, 0u};
+    return;
+  }
+  c.err[i] = MGENX_ERROR_OOB;
+  c.flags[i] = 0;
+  c.msg_len[i] = 0;
+  c.flow_id[i] = 0;
+  c.seq_num[i] = 0;
+  c.tx_sec[i] = 0;
+  c.tx_usec[i] = 0;
+  c.dst_port[i] = 0;
+  c.dst_type[i] = 0;
+  c.dst_len[i] = 0;
+  c.dst_addr4[i] = 0;
+  c.payload_len[i] = 0;
+  c.payload_type[i] = 0;
+  c.gps_status[i] = 0;
+}
+
 // The core fields of one record, as every lane of its quad holds them.
 struct Core {
   uint32_t flow, seq, sec, usec, dst4, msg_len, dport, plen, flags, err, dtype, dlen, ptype, gps;
@@ -487,10 +555,17 @@ unpack_kernel(UnpackParams p) {
       pf = ldu128((live && L >= 16u * (q + 1)) ? rec + 16 * q : dummy);
       if (kCrc) expect = p.expect[live ? L : 0u];
     };
-    auto unpack_words = [&]() {
+    // prefix words 0..15 of the quad's record, gathered by DPP with every lane active
+    auto gather = [&](uint32_t (&pw)[16]) {
+      quad_bcast<0>(pf, pw);
+      quad_bcast<1>(pf, pw);
+      quad_bcast<2>(pf, pw);
+      quad_bcast<3>(pf, pw);
+    };
+    auto unpack_words = [&](const uint32_t (&pw)[16]) {
       if (pfx) {
 #pragma unroll
-        for (int j = 0; j < 8; j++) w[j] = prefix_word(pf, j);
+        for (int j = 0; j < 8; j++) w[j] = pw[j];
       } else if (live && L >= MGENX_MIN_SIZE) {
         load_fixed(rec, buf_len, w);  // 28..31-byte records
       } else {
@@ -500,8 +575,10 @@ unpack_kernel(UnpackParams p) {
     };
     bool needs_crc = false;
     auto decide = [&]() {
-      if (kCrc && live) {  // every lane of the quad: the tail's stores are per quad
-        unpack_words();
+      uint32_t pw[16];
+      gather(pw);
+      if (kCrc && live && q == 0) {  // quad lane 0 decides and stores
+        unpack_words(pw);
         const bool flagged = force || (((w[0] >> 24) & MGENX_FLAG_CHECKSUM) != 0 &&
                                        buf_len >= MGENX_MIN_SIZE &&
                                        ((w[0] >> 16) & 0xffu) == 2u);
@@ -633,61 +710,24 @@ unpack_kernel(UnpackParams p) {
     if (!kCrc) load_header();
     const bool vec_crc = needs_crc && live && L >= 32;
 
-    auto pw = [&](int j) { return prefix_word(pf, j); };  // all lanes active here
-    // Decode: every lane of a quad computes its record's core fields from the prefix words
-    // (fast layouts in registers); general layouts and short records are parsed by quad
-    // lane 0 and broadcast.  Then the quad stores branch-free (store_core_quad).
-    const uint32_t D = pw(5) >> 24;
-    const uint32_t hw = (D == 4u) ? pw(7) : pw(10);
-    const bool fast = pfx64 && fast_layout(pw(0), pw(5), hw);
-    const uint32_t gi = (28u + D + (hw >> 24)) >> 2;
-    const uint32_t g3 = (pw(11) & (0u - (uint32_t)(gi == 8u))) |
-                        (pw(12) & (0u - (uint32_t)(gi == 9u))) |
-                        (pw(14) & (0u - (uint32_t)(gi == 11u))) |
-                        (pw(15) & (0u - (uint32_t)(gi == 12u)));
-    Core v;
-    v.flow = bswap32(pw(1));
-    v.seq = bswap32(pw(2));
-    v.sec = bswap32(pw(3));
-    v.usec = bswap32(pw(4));
-    v.dst4 = pw(6);
-    v.msg_len = bswap16((uint16_t)(pw(0) & 0xffffu));
-    v.dport = bswap16((uint16_t)(pw(5) & 0xffffu));
-    const uint32_t hlen = 44u + D + (hw >> 24);
-    v.plen = bswap16((uint16_t)(g3 >> 16));
-    if (!(v.plen != 0 && hlen + v.plen <= buf_len)) v.plen = 0;  // mgenMsg.cpp:488-497
-    v.flags = pw(0) >> 24;
-    v.err = 0;
-    v.dtype = (pw(5) >> 16) & 0xffu;
-    v.dlen = D;
-    v.ptype = (g3 >> 8) & 0xffu;
-    v.gps = g3 & 0xffu;
-    uint32_t crc_ok = (!needs_crc || tot == expect) ? 1u : 0u;
-    // general layouts / short records: parsed and stored whole by quad lane 0 (rare); their
-    // quad's branch-free stores below go to the sink
-    const bool slow = live && !fast;
-    if (__any(slow)) {
-      unpack_words();  // every lane active: its DPP reads lanes 1..3 of the quad
-      if (slow && q == 0) {
+    uint32_t pw[16];
+    gather(pw);
+    if (live && q == 0) {
+      // each parse path stores its own record (no join merging two decoded headers)
+      if (pfx64 && fast_layout(pw[0], pw[5], (pw[5] >> 24) == 4u ? pw[7] : pw[10])) {
+        store_fast_q0(p.cols, rec_idx, pw, buf_len, !needs_crc || tot == expect, tcp);
+        if (any_ext) store_fast_ext(p.cols, rec_idx, [&](int k) { return pw[k]; }, buf_len, true);
+      } else {
         Hdr h;
+        unpack_words(pw);
         parse_header(rec, buf_len, want_ext, w, h);
-        const bool ok = !needs_crc || (vec_crc ? (tot == expect) : small_crc_ok(rec, L));
-        store_hdr_q0(p.cols, rec_idx, h, ok, tcp);
+        const bool crc_ok =
+            !needs_crc || (vec_crc ? (tot == expect) : small_crc_ok(rec, L));
+        store_hdr_q0(p.cols, rec_idx, h, crc_ok, tcp);
       }
+    } else if (oob && q == 0) {
+      store_oob_q0(p.cols, rec_idx);
     }
-    if (!crc_ok) {  // the caller's receive check (mgenTransport.cpp:971-975, 1552-1560)
-      v.err = MGENX_ERROR_CHECKSUM;
-      if (tcp) v.flags |= MGENX_FLAG_CHECKSUM_ERROR;
-    }
-    if (!live) {  // outside the slab (or past the batch end: those lanes store to the sink)
-      v.flow = v.seq = v.sec = v.usec = v.dst4 = v.msg_len = v.dport = v.plen = v.flags = 0;
-      v.dtype = v.dlen = v.ptype = v.gps = 0;
-      v.err = MGENX_ERROR_OOB;
-    }
-    const bool in = valid && !slow;
-    if (p.cols.rows) store_core_quad<true>(p, rec_idx, in, lane, q, v);
-    else store_core_quad<false>(p, rec_idx, in, lane, q, v);
-    if (any_ext) store_fast_ext(p.cols, rec_idx, pw, buf_len, fast && q == 0);
   }
 }
 
@@ -843,7 +883,9 @@ unpack_fixed_kernel(UnpackParams p, uint32_t expect) {
                  : ((uint64_t)(dtype | dlen << 8 | ptype << 16 | gps << 24) << 32 |
                     (plen | flags << 16 | err << 24));
       const uint64_t rbase = kRows ? (uint64_t)p.cols.rows : (uint64_t)p.sink2;
-      st_g64(in ? rbase + (uint64_t)idx * 32 + 8 * q : (uint64_t)p.sink + 8u * lane, v);
+      const uint64_t ra = in ? rbase + (uint64_t)idx * 32 + 8 * q : (uint64_t)p.sink + 8u * lane;
+      if (MODE == 10) st_g64_nt(ra, v);  // ablation: non-temporal row stores
+      else st_g64(ra, v);
       return;
     }
     if (MODE == 7) {  // ablation: the tail's work without its stores (kept alive)
@@ -1050,6 +1092,7 @@ hipError_t launch_unpack(const UnpackParams& p, int grid, hipStream_t stream) {
   if (unpack_variant == 7 && fixed && p.fixed_len == 1024) return launch_fixed<16, 7>(p, grid, stream);
   if (unpack_variant == 8 && fixed && p.fixed_len == 1024 && p.sink2) return launch_fixed<16, 8>(p, grid, stream);
   if (unpack_variant == 9 && fixed && p.fixed_len == 1024 && p.sink2) return launch_fixed<16, 9>(p, grid, stream);
+  if (unpack_variant == 10 && fixed && p.fixed_len == 1024 && c.rows) return launch_fixed<16, 10, true>(p, grid, stream);
   switch (unpack_variant) {
     case 1: return launch_mode<1>(p, grid, stream);
     case 2: return launch_mode<2>(p, grid, stream);

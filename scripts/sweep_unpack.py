@@ -23,6 +23,7 @@ eng.pack_prepare(d_tmpl, len(tmpl), d_pool, crc)
 slab = torch.empty(N * REC, dtype=torch.uint8, device="cuda")
 eng.pack(d_tmpl, crc, d_desc, N, d_pool, slab, stride=REC, opts=PACK_CHECKSUM)
 cols = eng.alloc_cols(N)
+rows = {"rows": eng.alloc_rows(N)}
 eng.set_unpack_variant(0)
 eng.unpack(slab, N, stride=REC, fixed_len=REC, cols=cols)
 torch.cuda.synchronize()
@@ -30,7 +31,19 @@ assert int((cols["err"] != 0).sum()) == 0
 
 
 def run(name):
-    if name.startswith("mode"):
+    if name == "rows0":
+        eng.set_unpack_variant(0)
+        eng.unpack(slab, N, stride=REC, fixed_len=REC, cols=rows)
+    elif name == "rows_nt":
+        eng.set_unpack_variant(10)
+        eng.unpack(slab, N, stride=REC, fixed_len=REC, cols=rows)
+    elif name == "hdr_rows":
+        eng.set_unpack_variant(0)
+        eng.unpack(slab, N, stride=REC, fixed_len=REC, cols=rows, opts=OPT_SKIP_CRC)
+    elif name == "rows3":
+        eng.set_unpack_variant(3)
+        eng.unpack(slab, N, stride=REC, fixed_len=REC, cols=rows)
+    elif name.startswith("mode"):
         eng.set_unpack_variant(int(name[4:]))
         eng.unpack(slab, N, stride=REC, fixed_len=REC, cols=cols)
     elif name == "hdr_only":
@@ -40,7 +53,7 @@ def run(name):
         eng.stream_read(slab, grid=int(name.split("_")[1]))
 
 
-names = ["mode0", "mode4", "mode5", "mode7", "mode8", "mode3", "mode1", "mode2", "hdr_only", "read_1024", "read_2048", "read_4096",
+names = ["mode0", "rows0", "rows_nt", "mode3", "rows3", "hdr_rows", "mode5", "mode1", "mode2", "hdr_only", "read_1024", "read_2048", "read_4096",
          "read_8192"]
 res = {k: [] for k in names}
 for rnd in range(5):
