@@ -292,7 +292,7 @@ int mgenx_pack_batch(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
 int mgenx_set_tuning(mgenx_ctx* ctx, int key, int value) {
   if (!ctx) return MGENX_EINVAL;
   if (key == MGENX_TUNE_UNPACK_VARIANT) {
-    if (value < 0 || value > 10) return MGENX_EINVAL;
+    if (value < 0 || value > 12) return MGENX_EINVAL;
     mgenx::unpack_variant = value;
     if ((value == 8 || value == 9) && !ctx->d_rows_diag &&
         hipMalloc((void**)&ctx->d_rows_diag, (size_t)32 << 20) != hipSuccess)

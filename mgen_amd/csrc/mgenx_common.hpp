@@ -63,6 +63,15 @@ __device__ __forceinline__ void st_g64(uint64_t a, uint64_t v) { *(g_u64*)a = v;
 __device__ __forceinline__ void st_g64_nt(uint64_t a, uint64_t v) {
   __builtin_nontemporal_store(v, (g_u64*)a);
 }
+__device__ __forceinline__ void st_g32_nt(uint64_t a, uint32_t v) {
+  __builtin_nontemporal_store(v, (g_u32*)a);
+}
+__device__ __forceinline__ void st_g16_nt(uint64_t a, uint32_t v) {
+  __builtin_nontemporal_store((uint16_t)v, (g_u16*)a);
+}
+__device__ __forceinline__ void st_g8_nt(uint64_t a, uint32_t v) {
+  __builtin_nontemporal_store((uint8_t)v, (g_u8*)a);
+}
 // a[k] for k = sel in 0..3, as AND/OR masks (a select chain over struct fields or arrays
 // can be folded back into a dynamic index into a stack copy)
 __device__ __forceinline__ uint64_t pick4(int sel, uint64_t a0, uint64_t a1, uint64_t a2,

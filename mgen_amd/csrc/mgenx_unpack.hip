@@ -744,7 +744,10 @@ unpack_kernel(UnpackParams p) {
 // Semantics are those of unpack_kernel<true> (same helpers, same column stores).
 // MODE (ablations): 1 = loads + XOR only (no LDS lookups), 5 = MODE 1 without the tail
 // (no decode, no column stores; the CRC word is kept alive through one store per wave)
-template <int NR, int MODE = 0, bool kRows = false>
+// kAligned (L == 64 NR): row 0 of a record is its 64-byte header prefix in lane order
+// (lane q: bytes 16q..16q+15), so the header comes with the rows -- no separate header load,
+// and the loop needs no second header register (no unrolled ping-pong).
+template <int NR, int MODE = 0, bool kRows = false, bool kAligned = false>
 __global__ void __launch_bounds__(kUnpackThreads)
 unpack_fixed_kernel(UnpackParams p, uint32_t expect) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -803,14 +806,13 @@ unpack_fixed_kernel(UnpackParams p, uint32_t expect) {
   auto ld_hdr = [&](uint32_t boff) { return ld(boff + 16u * (uint32_t)q, 0); };
 
   u32x4_t d[NR];
-  // Decode + store one record per quad.  Every lane runs the same instructions: the header
-  // words come by DPP from the quad's prefix chunks (a DPP read of an inactive lane returns
-  // stale data), the rare general layouts are parsed by quad lane 0 and broadcast, and the
-  // four lanes of a quad store four different columns, five store instructions per group
-  // with no branch around them.  (gfx950 counts stores in vmcnt: a store that might be
-  // skipped makes LLVM's wait counts assume it was, so the next row wait would also wait
-  // for the store's acknowledgement.)  Lanes past the batch end write to the sink.
-  auto tail = [&](const u32x4_t& pf, uint32_t idx, bool live, bool needs_crc, uint32_t tot) {
+  // The tail is split in two so the aligned loop can decode a group's header as soon as its
+  // row 0 arrives (then reload row 0 at once): decode() turns the quad's header into the
+  // lane's store values, emit() applies the checksum verdict and stores.
+  struct Out {
+    uint32_t o[5];
+  };
+  auto decode = [&](const u32x4_t& pf, uint32_t idx, bool live) {
     uint32_t w[8];
 #pragma unroll
     for (int j = 0; j < 8; j++) w[j] = prefix_word(pf, j);
@@ -846,14 +848,40 @@ unpack_fixed_kernel(UnpackParams p, uint32_t expect) {
       bc(err, h.err); bc(dtype, h.dst_type); bc(dlen, h.dst_len); bc(ptype, h.ptype);
       bc(gps, h.gps);
     }
-    if (needs_crc && tot != expect) {  // the caller's receive check (mgenTransport.cpp:971)
-      err = MGENX_ERROR_CHECKSUM;
-      if (tcp) flags |= MGENX_FLAG_CHECKSUM_ERROR;
-    }
     if (!live) {  // descriptor outside the slab (or past the batch end)
       flow = seq = sec = usec = dst4 = msg_len = dport = plen = flags = dtype = dlen = 0;
       ptype = gps = 0;
       err = MGENX_ERROR_OOB;
+    }
+    Out r;
+    if (kRows || MODE == 8) {  // mgenx_rec: lane q holds bytes 8q..8q+7 of its record
+      r.o[0] = q == 0 ? flow : q == 1 ? sec : q == 2 ? dst4 : (plen | flags << 16 | err << 24);
+      r.o[1] = q == 0 ? seq : q == 1 ? usec : q == 2 ? (msg_len | dport << 16)
+                                                    : (dtype | dlen << 8 | ptype << 16 | gps << 24);
+      r.o[2] = r.o[3] = r.o[4] = 0;
+    } else {  // the lane's column values: u32 (column q), dst_addr4, u16, u8a, u8b
+      r.o[0] = q == 0 ? flow : q == 1 ? seq : q == 2 ? sec : usec;
+      r.o[1] = dst4;
+      r.o[2] = q == 0 ? msg_len : q == 1 ? dport : plen;
+      r.o[3] = q == 0 ? flags : q == 1 ? err : q == 2 ? dtype : dlen;
+      r.o[4] = (q & 1) == 0 ? ptype : gps;
+    }
+    return r;
+  };
+  // Store one record per quad.  Every lane runs the same instructions: the four lanes of a
+  // quad store four different columns (or the four 8-byte parts of a row), with no branch
+  // around the stores.  (gfx950 counts stores in vmcnt: a store that might be skipped makes
+  // LLVM's wait counts assume it was, so the next row wait would also wait for the store's
+  // acknowledgement.)  Lanes past the batch end write to the sink.
+  auto emit = [&](Out r, uint32_t idx, bool crc_bad) {
+    if (crc_bad) {  // the caller's receive check (mgenTransport.cpp:971): err, TCP flag
+      const uint32_t fl = tcp ? (uint32_t)MGENX_FLAG_CHECKSUM_ERROR : 0u;
+      if (kRows || MODE == 8) {
+        if (q == 3) r.o[0] = (r.o[0] & 0x00ffffffu) | fl << 16 | (uint32_t)MGENX_ERROR_CHECKSUM << 24;
+      } else {
+        if (q == 0) r.o[3] |= fl;
+        if (q == 1) r.o[3] = MGENX_ERROR_CHECKSUM;
+      }
     }
     const bool in = idx < p.n && MODE != 6;  // MODE 6 (ablation): every store to the sink
     const uint64_t sink = (uint64_t)p.sink + 4u * (uint32_t)lane;
@@ -866,6 +894,20 @@ unpack_fixed_kernel(UnpackParams p, uint32_t expect) {
       return in ? base + (uint64_t)idx * size : sink;
     };
     const mgenx_cols& c = p.cols;
+    if (kRows || MODE == 8) {  // 16 records = 512 contiguous bytes per store instruction
+      const uint64_t v = (uint64_t)r.o[1] << 32 | r.o[0];
+      const uint64_t rbase = kRows ? (uint64_t)p.cols.rows : (uint64_t)p.sink2;
+      const uint64_t ra = in ? rbase + (uint64_t)idx * 32 + 8 * q : (uint64_t)p.sink + 8u * lane;
+      // non-temporal: the streamed output must not compete with the read stream in L2
+      if (MODE == 10) st_g64(ra, v);  // ablation: ordinary (temporal) row stores
+      else st_g64_nt(ra, v);
+      return;
+    }
+    if (MODE == 7) {  // ablation: the tail's work without its stores (kept alive)
+      const uint32_t all = r.o[0] ^ r.o[1] ^ r.o[2] ^ r.o[3] ^ r.o[4];
+      if (all == 0x9E3779B9u) st_g32(at((uint64_t)c.flow_id, 4), all);
+      return;
+    }
     const uint64_t u32 = pick4(q, (uint64_t)c.flow_id, (uint64_t)c.seq_num, (uint64_t)c.tx_sec,
                                (uint64_t)c.tx_usec);
     const uint64_t u16 = pick4(q, (uint64_t)c.msg_len, (uint64_t)c.dst_port,
@@ -874,34 +916,22 @@ unpack_fixed_kernel(UnpackParams p, uint32_t expect) {
                                (uint64_t)c.dst_len);
     const uint64_t u8b = pick4(q, (uint64_t)c.payload_type, (uint64_t)c.gps_status,
                                (uint64_t)c.payload_type, (uint64_t)c.gps_status);
-    if (kRows || MODE == 8) {  // mgenx_rec rows: lane q writes bytes 8q..8q+7 of its record
-      // (16 records = 512 contiguous bytes per store instruction: whole lines)
-      const uint64_t v =
-          q == 0 ? ((uint64_t)seq << 32 | flow)
-        : q == 1 ? ((uint64_t)usec << 32 | sec)
-        : q == 2 ? ((uint64_t)(msg_len | dport << 16) << 32 | dst4)
-                 : ((uint64_t)(dtype | dlen << 8 | ptype << 16 | gps << 24) << 32 |
-                    (plen | flags << 16 | err << 24));
-      const uint64_t rbase = kRows ? (uint64_t)p.cols.rows : (uint64_t)p.sink2;
-      const uint64_t ra = in ? rbase + (uint64_t)idx * 32 + 8 * q : (uint64_t)p.sink + 8u * lane;
-      if (MODE == 10) st_g64_nt(ra, v);  // ablation: non-temporal row stores
-      else st_g64(ra, v);
+    if (MODE == 11) {  // ablation: non-temporal column stores
+      st_g32_nt(at(u32, 4), r.o[0]);
+      st_g32_nt(at((uint64_t)c.dst_addr4, 4), r.o[1]);
+      st_g16_nt(at(u16, 2), r.o[2]);
+      st_g8_nt(at(u8a, 1), r.o[3]);
+      st_g8_nt(at(u8b, 1), r.o[4]);
       return;
     }
-    if (MODE == 7) {  // ablation: the tail's work without its stores (kept alive)
-      const uint32_t all = flow ^ seq ^ sec ^ usec ^ dst4 ^ msg_len ^ dport ^ plen ^ flags ^
-                           err ^ dtype ^ dlen ^ ptype ^ gps;
-      if (all == 0x9E3779B9u) st_g32(at(u32, 4), all);
-      return;
-    }
-    // u32: flow, seq, tx_sec, tx_usec (lane q -> column q); then dst_addr4 (all lanes)
-    st_g32(at(u32, 4), q == 0 ? flow : q == 1 ? seq : q == 2 ? sec : usec);
-    st_g32(at((uint64_t)c.dst_addr4, 4), dst4);
-    // u16: msg_len, dst_port, payload_len (lane 3 repeats lane 2's store)
-    st_g16(at(u16, 2), q == 0 ? msg_len : q == 1 ? dport : plen);
+    // u32: flow, seq, tx_sec, tx_usec (lane q -> column q); then dst_addr4 (all lanes);
+    // u16: msg_len, dst_port, payload_len (lane 3 repeats lane 2's store);
     // u8: flags, err, dst_type, dst_len; then payload_type, gps_status (lanes 2,3 repeat)
-    st_g8(at(u8a, 1), q == 0 ? flags : q == 1 ? err : q == 2 ? dtype : dlen);
-    st_g8(at(u8b, 1), (q & 1) == 0 ? ptype : gps);
+    st_g32(at(u32, 4), r.o[0]);
+    st_g32(at((uint64_t)c.dst_addr4, 4), r.o[1]);
+    st_g16(at(u16, 2), r.o[2]);
+    st_g8(at(u8a, 1), r.o[3]);
+    st_g8(at(u8b, 1), r.o[4]);
   };
   // the receive-side CRC decision from words 0 and 5 (mgenTransport.cpp:960-963)
   auto decide = [&](const u32x4_t& pf, bool live) {
@@ -922,9 +952,13 @@ unpack_fixed_kernel(UnpackParams p, uint32_t expect) {
     bool live = is_live(idx);
     {
       const uint32_t boff = base_off(live, idx);
-      pf = ld_hdr(boff);
+      if (!kAligned) pf = ld_hdr(boff);
+      // in row order (the loop's first wait is for row 0 alone)
 #pragma unroll
-      for (int j = 0; j < NR; j++) d[j] = ld_row(boff, j);
+      for (int j = 0; j < NR; j++) {
+        d[j] = ld_row(boff, j);
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
     // one pipelined group; the header registers alternate between two variables (the loop
     // is unrolled twice) so the next header never needs a register copy
@@ -935,10 +969,14 @@ unpack_fixed_kernel(UnpackParams p, uint32_t expect) {
       const bool live_n = has_next && is_live(idx_n);
       // next group's header first (completes before any of its rows)
       const uint32_t boff_n = base_off(live_n, idx_n);
-      pf_nxt = ld_hdr(boff_n);
+      if (!kAligned) pf_nxt = ld_hdr(boff_n);
       asm volatile("" ::: "memory");
-      const bool needs_crc = decide(pf_cur, live);
+      const u32x4_t hdr = kAligned ? d[0] : pf_cur;  // aligned: row 0 is the header
+      const bool needs_crc = decide(hdr, live);
       const bool any = __any(needs_crc);
+      // aligned: decode now, so row 0's registers are free for its reload
+      Out early;
+      if (kAligned && MODE != 5) early = decode(hdr, idx, live);
 
       uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
 #pragma unroll
@@ -952,7 +990,7 @@ unpack_fixed_kernel(UnpackParams p, uint32_t expect) {
           }
         }
         uint32_t c4[4];
-        if (MODE == 1 || (MODE >= 5 && MODE != 8 && MODE != 9)) {
+        if (MODE == 1 || MODE == 4 || MODE == 5 || MODE == 6 || MODE == 7) {
           c4[0] = (h0 << 1) ^ x.x; c4[1] = (h1 << 1) ^ x.y;
           c4[2] = (h2 << 1) ^ x.z; c4[3] = (h3 << 1) ^ x.w;
         } else {
@@ -963,7 +1001,7 @@ unpack_fixed_kernel(UnpackParams p, uint32_t expect) {
         __builtin_amdgcn_sched_barrier(0);
         d[j] = ld_row(boff_n, j);
         __builtin_amdgcn_sched_barrier(0);
-        if (MODE == 1 || (MODE >= 5 && MODE != 8 && MODE != 9)) {
+        if (MODE == 1 || MODE == 4 || MODE == 5 || MODE == 6 || MODE == 7) {
           h0 = c4[0]; h1 = c4[1]; h2 = c4[2]; h3 = c4[3];
           continue;
         }
@@ -982,8 +1020,11 @@ unpack_fixed_kernel(UnpackParams p, uint32_t expect) {
       }
       // final row (V >= 2, so never row 0): the big-endian trailer goes to stream order
       const u32x4_t xf = d[NR - 1];
-      const uint32_t f0 = h0 ^ xf.x, f1 = h1 ^ xf.y, f2 = h2 ^ xf.z;
-      const uint32_t f3 = h3 ^ (q == 3 ? bswap32(xf.w) : xf.w);
+      uint32_t f0 = h0 ^ xf.x, f1 = h1 ^ xf.y, f2 = h2 ^ xf.z;
+      uint32_t f3 = h3 ^ (q == 3 ? bswap32(xf.w) : xf.w);
+      // opaque: later index math must not reach back to the row registers (which would keep
+      // them live across their reload and cost a loop-carried copy of the in-flight load)
+      asm volatile("" : "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3));
       __builtin_amdgcn_sched_barrier(0);
       d[NR - 1] = ld_row(boff_n, NR - 1);
       __builtin_amdgcn_sched_barrier(0);
@@ -996,8 +1037,13 @@ unpack_fixed_kernel(UnpackParams p, uint32_t expect) {
       if (MODE == 5) {
         if (s == 0x9E3779B9u && lane == 0) p.cols.err[idx] = (uint8_t)needs_crc;  // keep alive
       } else {
-        tail(pf_cur, idx, live, needs_crc, s);
+        const Out r = kAligned ? early : decode(hdr, idx, live);
+        emit(r, idx, needs_crc && s != expect);
       }
+      // keep the row base of g' alive past its last reload: otherwise the register allocator
+      // gives that load the dying address register as destination, and the loop needs a copy
+      // of the in-flight row at its back edge (a full drain)
+      asm volatile("" ::"v"(boff_n + (uint32_t)(pos0 + 64)));
       g = gn;
       idx = idx_n;
       live = live_n;
@@ -1006,9 +1052,14 @@ unpack_fixed_kernel(UnpackParams p, uint32_t expect) {
       return has_next && any;
     };
     u32x4_t pf2;
-    for (;;) {
-      if (!step(pf, pf2)) break;
-      if (!step(pf2, pf)) break;
+    if (kAligned) {
+      while (step(pf, pf2)) {
+      }
+    } else {
+      for (;;) {
+        if (!step(pf, pf2)) break;
+        if (!step(pf2, pf)) break;
+      }
     }
     // ---- header-only mode: header first, bodies only for groups that need the CRC
     for (; g < g_end; g += n_waves) {
@@ -1017,7 +1068,7 @@ unpack_fixed_kernel(UnpackParams p, uint32_t expect) {
       const u32x4_t ph = ld_hdr(base_off(lv, i));
       const bool nc = decide(ph, lv);
       if (__any(nc)) break;  // back to pipelined mode at this group
-      tail(ph, i, lv, false, 0u);
+      emit(decode(ph, i, lv), i, false);
     }
   }
 }
@@ -1044,18 +1095,18 @@ static hipError_t launch_mode(const UnpackParams& p, int grid, hipStream_t strea
   return launch_lds(unpack_kernel<true, MODE>, attr_done, p, grid, stream);
 }
 
-template <int NR, int MODE = 0, bool kRows = false>
+template <int NR, int MODE = 0, bool kRows = false, bool kAligned = false>
 static hipError_t launch_fixed(const UnpackParams& p, int grid, hipStream_t stream) {
   static bool attr_done = false;
   if (!attr_done) {
-    hipError_t e = hipFuncSetAttribute((const void*)unpack_fixed_kernel<NR, MODE, kRows>,
+    hipError_t e = hipFuncSetAttribute((const void*)unpack_fixed_kernel<NR, MODE, kRows, kAligned>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)kUnpackLdsBytes);
     if (e != hipSuccess) return e;
     attr_done = true;
   }
-  hipLaunchKernelGGL((unpack_fixed_kernel<NR, MODE, kRows>), dim3(grid), dim3(kUnpackThreads),
-                     kUnpackLdsBytes, stream, p, p.expect_fixed);
+  hipLaunchKernelGGL((unpack_fixed_kernel<NR, MODE, kRows, kAligned>), dim3(grid),
+                     dim3(kUnpackThreads), kUnpackLdsBytes, stream, p, p.expect_fixed);
   return hipGetLastError();
 }
 
@@ -1084,8 +1135,22 @@ hipError_t launch_unpack(const UnpackParams& p, int grid, hipStream_t stream) {
                      p.stride > 0 && p.n <= 0xFFFFFFF0u && !ext &&
                      p.slab_bytes < 0xFFFF0000ull && p.slab_bytes >= 64ull * (nr + 1) + 16 &&
                      p.slab_bytes >= p.fixed_len;
-  if (unpack_variant == 0 && fixed)
+  if (unpack_variant == 0 && fixed) {
+    // 256 / 512 / 1024-byte records: the aligned variant (header = row 0)
+    switch (p.fixed_len) {
+      case 256: return c.rows ? launch_fixed<4, 0, true, true>(p, grid, stream)
+                              : launch_fixed<4, 0, false, true>(p, grid, stream);
+      case 512: return c.rows ? launch_fixed<8, 0, true, true>(p, grid, stream)
+                              : launch_fixed<8, 0, false, true>(p, grid, stream);
+      case 1024: return c.rows ? launch_fixed<16, 0, true, true>(p, grid, stream)
+                               : launch_fixed<16, 0, false, true>(p, grid, stream);
+      default: break;
+    }
     return (c.rows ? kFixedLaunchRows : kFixedLaunch)[(p.fixed_len + 63) / 64](p, grid, stream);
+  }
+  // ablation 12: the unaligned (separate header load) path on 1024-B records
+  if (unpack_variant == 12 && fixed && p.fixed_len == 1024)
+    return c.rows ? launch_fixed<16, 0, true>(p, grid, stream) : launch_fixed<16, 0>(p, grid, stream);
   if (unpack_variant == 4 && fixed && p.fixed_len == 1024) return launch_fixed<16, 1>(p, grid, stream);
   if (unpack_variant == 5 && fixed && p.fixed_len == 1024) return launch_fixed<16, 5>(p, grid, stream);
   if (unpack_variant == 6 && fixed && p.fixed_len == 1024) return launch_fixed<16, 6>(p, grid, stream);
@@ -1093,6 +1158,7 @@ hipError_t launch_unpack(const UnpackParams& p, int grid, hipStream_t stream) {
   if (unpack_variant == 8 && fixed && p.fixed_len == 1024 && p.sink2) return launch_fixed<16, 8>(p, grid, stream);
   if (unpack_variant == 9 && fixed && p.fixed_len == 1024 && p.sink2) return launch_fixed<16, 9>(p, grid, stream);
   if (unpack_variant == 10 && fixed && p.fixed_len == 1024 && c.rows) return launch_fixed<16, 10, true>(p, grid, stream);
+  if (unpack_variant == 11 && fixed && p.fixed_len == 1024 && !c.rows) return launch_fixed<16, 11>(p, grid, stream);
   switch (unpack_variant) {
     case 1: return launch_mode<1>(p, grid, stream);
     case 2: return launch_mode<2>(p, grid, stream);

@@ -34,9 +34,18 @@ def run(name):
     if name == "rows0":
         eng.set_unpack_variant(0)
         eng.unpack(slab, N, stride=REC, fixed_len=REC, cols=rows)
-    elif name == "rows_nt":
+    elif name == "rows_t":
         eng.set_unpack_variant(10)
         eng.unpack(slab, N, stride=REC, fixed_len=REC, cols=rows)
+    elif name == "cols_nt":
+        eng.set_unpack_variant(11)
+        eng.unpack(slab, N, stride=REC, fixed_len=REC, cols=cols)
+    elif name == "rows12":
+        eng.set_unpack_variant(12)
+        eng.unpack(slab, N, stride=REC, fixed_len=REC, cols=rows)
+    elif name == "cols12":
+        eng.set_unpack_variant(12)
+        eng.unpack(slab, N, stride=REC, fixed_len=REC, cols=cols)
     elif name == "hdr_rows":
         eng.set_unpack_variant(0)
         eng.unpack(slab, N, stride=REC, fixed_len=REC, cols=rows, opts=OPT_SKIP_CRC)
@@ -53,8 +62,9 @@ def run(name):
         eng.stream_read(slab, grid=int(name.split("_")[1]))
 
 
-names = ["mode0", "rows0", "rows_nt", "mode3", "rows3", "hdr_rows", "mode5", "mode1", "mode2", "hdr_only", "read_1024", "read_2048", "read_4096",
-         "read_8192"]
+names = os.environ.get("SWEEP_NAMES", "").split(",") if os.environ.get("SWEEP_NAMES") else [
+    "mode0", "cols12", "rows0", "rows12", "mode3", "rows3", "hdr_rows", "mode5", "mode1", "mode2",
+    "hdr_only", "read_1024", "read_2048", "read_4096", "read_8192"]
 res = {k: [] for k in names}
 for rnd in range(5):
     for k in names:

@@ -219,8 +219,9 @@ def test_oob_records_are_flagged_not_read(torch, eng):
 FIXED_SIZES = [65, 100, 127, 128, 200, 255, 256, 511, 777, 1000, 1023, 1024]
 
 
+@pytest.mark.parametrize("out", ["cols", "rows"])
 @pytest.mark.parametrize("size", FIXED_SIZES)
-def test_fixed_len_pipelined_vs_oracle(torch, eng, gold, size):
+def test_fixed_len_pipelined_vs_oracle(torch, eng, gold, size, out):
     """The pipelined fixed-length kernel (fixed stride, one length, core columns) against the
     oracle: every golden template layout, checksum on/off and caller CHECKSUM flag mixed,
     bit flips / bad version / bad dst type, a partial last group and records past the end
@@ -252,9 +253,16 @@ def test_fixed_len_pipelined_vs_oracle(torch, eng, gold, size):
     for opts in (0, OPT_CHECKSUM_FORCE, OPT_TCP | OPT_CHECKSUM_FORCE):
         f = O.udp_recv_batch(host, n, stride=size, fixed_len=size,
                              force=bool(opts & OPT_CHECKSUM_FORCE), tcp=bool(opts & OPT_TCP))
-        cols = eng.unpack(slab, n, stride=size, fixed_len=size, opts=opts,
-                          slab_bytes=slab_bytes)
-        c = host_cols(cols, n)
+        if out == "rows":  # mgenx_rec output (256/512/1024: the aligned kernel)
+            rows = eng.alloc_rows(n)
+            eng.unpack(slab, n, stride=size, fixed_len=size, opts=opts, slab_bytes=slab_bytes,
+                       cols={"rows": rows})
+            torch.cuda.synchronize()
+            c = rows_to_cols(rows, n)
+        else:
+            cols = eng.unpack(slab, n, stride=size, fixed_len=size, opts=opts,
+                              slab_bytes=slab_bytes)
+            c = host_cols(cols, n)
         live = n - n_oob
         for gname, oname, dt in COLMAP[:13]:
             got = c[gname].view(dt)[:live]
