@@ -262,18 +262,27 @@ int mgenx_flow_reduce(mgenx_ctx* ctx, const uint32_t* dev_flow_idx, const uint32
 int mgenx_flow_export(mgenx_ctx* ctx, const mgenx_flow_state* dev_flows, uint32_t n_flows,
                       mgenx_flow_counters* dev_out, void* stream);
 
-/* Tuning knobs (process-wide; for benchmarking kernel variants).  MGENX_TUNE_UNPACK_VARIANT:
+/* Tuning knobs (per context; for benchmarking kernel variants).  MGENX_TUNE_UNPACK_VARIANT:
  * 0 = automatic (pipelined fixed-length kernel when the batch qualifies), 1/2 = ablations
  * of the general kernel (loads+XOR only / lookups on cached rows), 3 = general kernel,
- * 4 = loads+XOR ablation of the fixed-length kernel, 5 = the same without decode/stores,
- * 6 = mode 4 with every column store sent to a scratch line, 7 = mode 4 without the stores
- * (modes 4-7: 1024-B records only). */
+ * 12 = fixed-length kernel with a separate header load (1024-B records), 1024 + M =
+ * ablation bit mask M of the aligned 1024-B kernel (1 = no LDS lookups, 2 = no decode and
+ * no stores, 4 = decode without stores, 8 = stores to a scratch line, 16 = the other store
+ * cache policy, 32 = stores wrapped onto the first 16K records, 64 = write-through stores,
+ * 128 = non-temporal row loads, 256 (with 4) = dummy rows stored after each wave's last
+ * group). */
 #define MGENX_TUNE_UNPACK_VARIANT 1
 int mgenx_set_tuning(mgenx_ctx* ctx, int key, int value);
 /* Diagnostic: plain 16-B-per-lane streaming read of `bytes` (the achievable-HBM reference
  * next to the roofline); dev_scratch holds `grid` words. */
 int mgenx_diag_stream_read(mgenx_ctx* ctx, const uint8_t* dev_data, uint64_t bytes,
                            uint32_t* dev_scratch, int grid, void* stream);
+/* Diagnostic: the fixed-length unpack's memory pattern without its compute -- waves take
+ * 16-KiB groups of `data` round-robin (16 loads of 1 KiB each, consumed by XOR) and, when
+ * `mode` & 1, store 512 B per group to dev_out (bytes / 32 bytes); `mode` & 2: the stores
+ * are write-through (sc1). */
+int mgenx_diag_group_rw(mgenx_ctx* ctx, const uint8_t* dev_data, uint64_t bytes,
+                        uint8_t* dev_out, int mode, void* stream);
 
 #ifdef __cplusplus
 }

@@ -25,7 +25,7 @@ LIB_PATH = os.path.join(HERE, "libmgenx.so")
 EXPORTED_SYMBOLS = (
     "mgenx_abi_version", "mgenx_ctx_create", "mgenx_ctx_destroy", "mgenx_last_error",
     "mgenx_unpack_batch", "mgenx_pack_prepare", "mgenx_set_fill_time", "mgenx_pack_batch",
-    "mgenx_crc32_batch", "mgenx_set_tuning", "mgenx_diag_stream_read", "mgenx_stream_scan", "mgenx_flow_reduce",
+    "mgenx_crc32_batch", "mgenx_set_tuning", "mgenx_diag_stream_read", "mgenx_diag_group_rw", "mgenx_stream_scan", "mgenx_flow_reduce",
 )
 
 
@@ -59,6 +59,7 @@ def load():
     L.mgenx_crc32_batch.argtypes = [P, P, P, P, u32, P, P]
     L.mgenx_set_tuning.argtypes = [P, i32, i32]
     L.mgenx_diag_stream_read.argtypes = [P, P, u64, P, i32, P]
+    L.mgenx_diag_group_rw.argtypes = [P, P, u64, P, i32, P]
     L.mgenx_stream_scan.argtypes = [P, P, u64, i32, P, P, u64, ctypes.POINTER(ScanInfo), P]
     L.mgenx_flow_init.argtypes = [P, P, u32, ctypes.c_double, P]
     L.mgenx_flow_reduce.argtypes = [P, P, P, P, P, P, P, P, u32, P, u32, P, u32, P, P]
@@ -173,6 +174,12 @@ class Engine:
         rc = self.lib.mgenx_diag_stream_read(self.ctx, _ptr(data), data.numel(), _ptr(scratch),
                                              grid, _stream(self.device))
         self._check(rc, "mgenx_diag_stream_read")
+
+    def group_rw(self, data, out, mode=1):
+        """Diagnostic: the fixed unpack's read pattern (+ 512-B stores per 16-KiB group)."""
+        rc = self.lib.mgenx_diag_group_rw(self.ctx, _ptr(data), data.numel(), _ptr(out), mode,
+                                          _stream(self.device))
+        self._check(rc, "mgenx_diag_group_rw")
 
     def stream_scan(self, data, mode=SCAN_TCP, cap=None, nbytes=None):
         """TCP / SINK record framing of a device byte stream (mgenx_stream_scan).  Returns

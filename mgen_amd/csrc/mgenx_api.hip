@@ -46,7 +46,7 @@ struct mgenx_ctx {
   uint8_t* d_sink = nullptr;      // 1 KiB: column stores of lanes past the batch end
   void* scan_ws = nullptr;        // stream-scan workspace (mgenx_scan.hip), grown on demand
   void* flow_ws = nullptr;        // flow-reduce workspace (mgenx_analytic.hip), grown on demand
-  uint8_t* d_rows_diag = nullptr; // ablation 8 only: 32-B rows for 1M records
+  int unpack_variant = 0;          // diagnostic kernel ablation (mgenx_set_tuning)
   bool rand_ready = false;
   uint32_t rand_time = 0;
   char err[256] = {0};
@@ -179,7 +179,6 @@ int mgenx_ctx_destroy(mgenx_ctx* c) {
                 c->d_sink};
   if (c->scan_ws) mgenx_scan_ws_free(c->scan_ws);
   if (c->flow_ws) mgenx_flow_ws_free(c->flow_ws);
-  if (c->d_rows_diag) hipFree(c->d_rows_diag);
   for (void* p : ps)
     if (p) hipFree(p);
   delete c;
@@ -212,7 +211,7 @@ int mgenx_unpack_batch(mgenx_ctx* ctx, const uint8_t* dev_slab, uint64_t slab_by
   p.expect = ctx->d_expect;
   p.expect_fixed = fixed_len < ctx->h_expect.size() ? ctx->h_expect[fixed_len] : 0u;
   p.sink = ctx->d_sink;
-  p.sink2 = mgenx::unpack_variant >= 8 ? ctx->d_rows_diag : nullptr;
+  p.variant = ctx->unpack_variant;
   p.cols = k;
   const uint64_t groups = ((uint64_t)n + 15) / 16;
   const uint64_t per_block = (uint64_t)mgenx::unpack_threads() / 64;  // waves per block
@@ -292,11 +291,8 @@ int mgenx_pack_batch(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
 int mgenx_set_tuning(mgenx_ctx* ctx, int key, int value) {
   if (!ctx) return MGENX_EINVAL;
   if (key == MGENX_TUNE_UNPACK_VARIANT) {
-    if (value < 0 || value > 12) return MGENX_EINVAL;
-    mgenx::unpack_variant = value;
-    if ((value == 8 || value == 9) && !ctx->d_rows_diag &&
-        hipMalloc((void**)&ctx->d_rows_diag, (size_t)32 << 20) != hipSuccess)
-      return MGENX_ENOMEM;
+    if (value < 0 || value > 2047) return MGENX_EINVAL;
+    ctx->unpack_variant = value;
     return MGENX_OK;
   }
   return MGENX_EINVAL;
@@ -308,6 +304,14 @@ int mgenx_diag_stream_read(mgenx_ctx* ctx, const uint8_t* dev_data, uint64_t byt
   hipError_t e = mgenx::launch_stream_read(dev_data, bytes, dev_scratch, grid,
                                            (hipStream_t)stream);
   return e == hipSuccess ? MGENX_OK : set_err(ctx, e, "stream_read");
+}
+
+int mgenx_diag_group_rw(mgenx_ctx* ctx, const uint8_t* dev_data, uint64_t bytes,
+                        uint8_t* dev_out, int mode, void* stream) {
+  if (!ctx || !dev_data || !dev_out || bytes % 16384 != 0) return MGENX_EINVAL;
+  hipError_t e = mgenx::launch_group_rw(dev_data, bytes, dev_out, mode, ctx->cu_count,
+                                        (hipStream_t)stream);
+  return e == hipSuccess ? MGENX_OK : set_err(ctx, e, "group_rw");
 }
 
 int mgenx_stream_scan(mgenx_ctx* ctx, const uint8_t* dev_stream, uint64_t nbytes, int mode,

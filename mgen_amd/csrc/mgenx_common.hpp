@@ -72,6 +72,20 @@ __device__ __forceinline__ void st_g16_nt(uint64_t a, uint32_t v) {
 __device__ __forceinline__ void st_g8_nt(uint64_t a, uint32_t v) {
   __builtin_nontemporal_store((uint8_t)v, (g_u8*)a);
 }
+// Write-through stores (`sc1`: the line leaves L2 with the store instead of staying dirty
+// there; MI355X_MICROARCH.md, store flavours)
+__device__ __forceinline__ void st_g64_wt(uint64_t a, uint64_t v) {
+  __hip_atomic_store((g_u64*)a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_g32_wt(uint64_t a, uint32_t v) {
+  __hip_atomic_store((g_u32*)a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_g16_wt(uint64_t a, uint32_t v) {
+  __hip_atomic_store((g_u16*)a, (uint16_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_g8_wt(uint64_t a, uint32_t v) {
+  __hip_atomic_store((g_u8*)a, (uint8_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 // a[k] for k = sel in 0..3, as AND/OR masks (a select chain over struct fields or arrays
 // can be folded back into a dynamic index into a stack copy)
 __device__ __forceinline__ uint64_t pick4(int sel, uint64_t a0, uint64_t a1, uint64_t a2,

@@ -18,7 +18,7 @@ struct UnpackParams {
   const uint32_t* expect;  // [65536]
   uint32_t expect_fixed;   // expect[fixed_len] (host copy, fixed-length kernel)
   uint8_t* sink;           // 1 KiB scratch: stores of lanes past the batch end
-  uint8_t* sink2;          // ablation 8: 32-B record rows (diag buffer set via tuning)
+  int variant;             // diagnostic ablation (0 = product path)
   mgenx_cols cols;
 };
 
@@ -44,8 +44,9 @@ struct PackParams {
 hipError_t launch_unpack(const UnpackParams& p, int grid, hipStream_t stream);
 // tuning knob (mgenx_set_tuning): 0 = auto (pipelined fixed-length kernel when the batch
 // qualifies), 1/2 = ablations of the general kernel, 3 = general kernel only
-extern int unpack_variant;
 int unpack_threads();
+hipError_t launch_group_rw(const uint8_t* p, uint64_t bytes, uint8_t* out, int mode, int grid,
+                           hipStream_t stream);
 hipError_t launch_stream_read(const uint8_t* p, uint64_t bytes, uint32_t* out, int grid,
                               hipStream_t stream);
 hipError_t launch_pack(const PackParams& p, int grid, hipStream_t stream);

@@ -33,13 +33,68 @@ constexpr int kFoldTabs = 6;
 constexpr size_t kUnpackLdsBytes = (size_t)(kRepDwords + kFoldTabs * kSmallTabDwords) * 4u;
 
 
-// A_64(x) from the replicated tables: layout [(k*256 + v) * 32 + copy], copy = lane & 31.
-__device__ __forceinline__ uint32_t shift_rep(const uint32_t* rep, uint32_t x, uint32_t copy) {
-  const uint32_t i0 = ((x & 0xffu) << 5) | copy;
-  const uint32_t i1 = (((x >> 8) & 0xffu) << 5) | copy;
-  const uint32_t i2 = (((x >> 16) & 0xffu) << 5) | copy;
-  const uint32_t i3 = ((x >> 24) << 5) | copy;
-  return rep[i0] ^ rep[8192 + i1] ^ rep[16384 + i2] ^ rep[24576 + i3];
+// Replicated A_64 tables.  Entry (k, v, copy) -- table k (byte k of the state), byte value v,
+// replica copy = lane & 31 -- sits at LDS byte address
+//     (k >> 1) * 65536 + v * 256 + (k & 1) * 128 + copy * 4,
+// so lane l always reads bank l (conflict-free ds_read_b32), and ONE v_perm_b32 forms each
+// address from the state word: byte 1 <- byte k of the state, byte 0 <- copy * 4 and
+// byte 2 <- k >> 1 (both from the lane constant s1 = copy * 4 | 1 << 16); (k & 1) * 128 is
+// the ds_read immediate.  That is one VALU op per lookup, plus one v_bitop3 (XOR3) per
+// three lookups to combine them.
+__device__ __forceinline__ uint32_t a64_s1(uint32_t lane) { return ((lane & 31u) << 2) | (1u << 16); }
+
+// The tables are addressed by absolute LDS address: these kernels have no static LDS, so the
+// dynamic allocation starts at 0.  (Going through the extern array pointer would cost one
+// v_add of its link-time base, 0, per lookup.)
+typedef __attribute__((address_space(3))) uint32_t lds_u32_t;
+__device__ __forceinline__ uint32_t lds_u32(const uint8_t*, uint32_t addr, uint32_t imm) {
+  return *(const lds_u32_t*)(addr + imm);
+}
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// A_64(c) as two partial words (A_64(c) = ha ^ hb), so the caller folds them together with
+// the next row's data in one XOR3.
+__device__ __forceinline__ void a64_parts(const uint8_t* ldsb, uint32_t c, uint32_t s1,
+                                          uint32_t& ha, uint32_t& hb) {
+  const uint32_t t0 = lds_u32(ldsb, __builtin_amdgcn_perm(c, s1, 0x0c0c0400u), 0);
+  const uint32_t t1 = lds_u32(ldsb, __builtin_amdgcn_perm(c, s1, 0x0c0c0500u), 128);
+  const uint32_t t2 = lds_u32(ldsb, __builtin_amdgcn_perm(c, s1, 0x0c020600u), 0);
+  const uint32_t t3 = lds_u32(ldsb, __builtin_amdgcn_perm(c, s1, 0x0c020700u), 128);
+  ha = xor3(t0, t1, t2);
+  hb = t3;
+}
+
+// Stage the replicated A_64 tables (tabs[0..1023] = table k entry v at k * 256 + v) and the
+// fold tables (tabs[1024..]) into LDS, in two halves so a caller can put other loads in
+// flight between them: table_loads() reads this thread's entries (1024-thread blocks:
+// one A_64 entry and six fold entries), table_writes() stores them.  Caller synchronises.
+struct TableRegs {
+  uint32_t a64, fold[kFoldTabs];
+};
+__device__ __forceinline__ TableRegs table_loads(const uint32_t* tabs) {
+  TableRegs r;
+  r.a64 = tabs[threadIdx.x];
+#pragma unroll
+  for (int k = 0; k < kFoldTabs; k++) r.fold[k] = tabs[1024 + k * 1024 + threadIdx.x];
+  return r;
+}
+__device__ __forceinline__ void table_writes(uint32_t* lds, const TableRegs& r) {
+  typedef __attribute__((address_space(3))) u32x4_t lds_u32x4_t;
+  const uint32_t e = threadIdx.x;
+  const uint32_t k = e >> 8, val = e & 255u;
+  const u32x4_t s = {r.a64, r.a64, r.a64, r.a64};
+  lds_u32x4_t* dst = (lds_u32x4_t*)((k >> 1) * 65536u + val * 256u + (k & 1u) * 128u);
+#pragma unroll
+  for (int c = 0; c < kRep / 4; c++) dst[c] = s;
+  uint32_t* fold = lds + kRepDwords;
+#pragma unroll
+  for (int k2 = 0; k2 < kFoldTabs; k2++) fold[k2 * 1024 + e] = r.fold[k2];
+}
+__device__ __forceinline__ void stage_tables(uint32_t* lds, const uint32_t* tabs) {
+  table_writes(lds, table_loads(tabs));
 }
 
 __device__ __forceinline__ uint32_t shift_tab(const uint32_t* t, uint32_t x) {
@@ -497,20 +552,14 @@ unpack_kernel(UnpackParams p) {
 
   // ---- stage the shift-operator tables (A_64 replicated 32x) ----
   if (kCrc) {
-    for (int e = threadIdx.x; e < 1024; e += blockDim.x) {
-      const uint32_t v = p.tabs[e];
-      u32x4_t s = {v, v, v, v};
-      u32x4_t* dst = reinterpret_cast<u32x4_t*>(rep + (size_t)e * kRep);
-#pragma unroll
-      for (int c = 0; c < kRep / 4; c++) dst[c] = s;
-    }
-    for (int e = threadIdx.x; e < kFoldTabs * 1024; e += blockDim.x) fold[e] = p.tabs[1024 + e];
+    stage_tables(lds, p.tabs);
     __syncthreads();
   }
+  const uint8_t* ldsb = reinterpret_cast<const uint8_t*>(rep);
 
   const int lane = threadIdx.x & 63;
   const int q = lane & 3;
-  const uint32_t copy = (uint32_t)(lane & 31);
+  const uint32_t s1 = a64_s1((uint32_t)lane);
   const uint32_t waves_per_block = blockDim.x >> 6;
   const uint64_t wave_id = (uint64_t)blockIdx.x * waves_per_block + (threadIdx.x >> 6);
   const uint64_t n_waves = (uint64_t)gridDim.x * waves_per_block;
@@ -617,7 +666,8 @@ unpack_kernel(UnpackParams p) {
         const int rr = real < 1 ? 1 : (real > hi_row ? hi_row : real);
         return base + 64 * (multi ? (MODE == 2 ? 1 : rr) : 0);
       };
-      uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+      // braid state word b = ha[b] ^ hb[b] (kept split so the next row folds in one XOR3)
+      uint32_t ha[4] = {0u, 0u, 0u, 0u}, hb[4] = {0u, 0u, 0u, 0u};
       const u32x4_t zero = {0u, 0u, 0u, 0u};
       u32x4_t xr = zero, xf = zero;
       // row 0 may start before the record: it is loaded from max(row0, 0) and its bytes
@@ -634,25 +684,15 @@ unpack_kernel(UnpackParams p) {
         xin.y = real > 0 ? dv.y : (real == 0 ? x.y : 0u);
         xin.z = real > 0 ? dv.z : (real == 0 ? x.z : 0u);
         xin.w = real > 0 ? dv.w : (real == 0 ? x.w : 0u);
+        const uint32_t xw[4] = {xin.x, xin.y, xin.z, xin.w};
         if (MODE == 1) {
-          h0 = (h0 << 1) ^ xin.x; h1 = (h1 << 1) ^ xin.y;
-          h2 = (h2 << 1) ^ xin.z; h3 = (h3 << 1) ^ xin.w;
-        } else {
-          // all 16 lookups of the row are independent: compute every address, issue the
-          // 16 LDS reads back to back, then fold them (one LDS round trip per row)
-          const uint32_t c4[4] = {h0 ^ xin.x, h1 ^ xin.y, h2 ^ xin.z, h3 ^ xin.w};
-          uint32_t t[16];
 #pragma unroll
-          for (int b = 0; b < 4; b++) {
-            t[4 * b + 0] = rep[((c4[b] & 0xffu) << 5) | copy];
-            t[4 * b + 1] = rep[8192 + ((((c4[b] >> 8) & 0xffu) << 5) | copy)];
-            t[4 * b + 2] = rep[16384 + ((((c4[b] >> 16) & 0xffu) << 5) | copy)];
-            t[4 * b + 3] = rep[24576 + (((c4[b] >> 24) << 5) | copy)];
-          }
-          h0 = t[0] ^ t[1] ^ t[2] ^ t[3];
-          h1 = t[4] ^ t[5] ^ t[6] ^ t[7];
-          h2 = t[8] ^ t[9] ^ t[10] ^ t[11];
-          h3 = t[12] ^ t[13] ^ t[14] ^ t[15];
+          for (int b = 0; b < 4; b++) ha[b] = (ha[b] << 1) ^ xw[b];
+        } else {
+          // all 16 lookups of the row are independent: every address first, the 16 LDS
+          // reads back to back, then the folds (one LDS round trip per row)
+#pragma unroll
+          for (int b = 0; b < 4; b++) a64_parts(ldsb, xor3(ha[b], hb[b], xw[b]), s1, ha[b], hb[b]);
         }
       };
       // One block of N middle rows (virtual rows j0..j0+N-1, all in 1..V-2): all loads
@@ -695,9 +735,10 @@ unpack_kernel(UnpackParams p) {
       // fold: word b of lane q sits 64-16q-4b bytes before the record end, so
       //   v_q = A16(g0) ^ A12(g1) ^ A8(g2) ^ A4(g3),  tot = XOR_q A_{48-16q}(v_q)
       // (16 independent lookups, then one per-lane lookup and a quad XOR-reduce)
-      const uint32_t v = shift_tab(fold + 3 * 1024, h0 ^ x.x) ^
-                         shift_tab(fold + 2 * 1024, h1 ^ x.y) ^
-                         shift_tab(fold + 1 * 1024, h2 ^ x.z) ^ shift_tab(fold, h3 ^ x.w);
+      const uint32_t v = shift_tab(fold + 3 * 1024, xor3(ha[0], hb[0], x.x)) ^
+                         shift_tab(fold + 2 * 1024, xor3(ha[1], hb[1], x.y)) ^
+                         shift_tab(fold + 1 * 1024, xor3(ha[2], hb[2], x.z)) ^
+                         shift_tab(fold, xor3(ha[3], hb[3], x.w));
       const uint32_t* lt = fold + (q == 0 ? 5 : (q == 1 ? 4 : 3)) * 1024;  // A48/A32/A16
       uint32_t s = (q == 3) ? v : shift_tab(lt, v);
       s ^= __shfl_xor(s, 1);
@@ -742,30 +783,31 @@ unpack_kernel(UnpackParams p) {
 // of g (before g's reloads), so with in-order completion the CRC decision for g' waits for
 // that header only, and row j of g' waits only for row j.
 // Semantics are those of unpack_kernel<true> (same helpers, same column stores).
-// MODE (ablations): 1 = loads + XOR only (no LDS lookups), 5 = MODE 1 without the tail
-// (no decode, no column stores; the CRC word is kept alive through one store per wave)
-// kAligned (L == 64 NR): row 0 of a record is its 64-byte header prefix in lane order
-// (lane q: bytes 16q..16q+15), so the header comes with the rows -- no separate header load,
-// and the loop needs no second header register (no unrolled ping-pong).
+// MODE (diagnostic ablations, never the product path) is a bit mask:
+//   1 = loads + XOR only (no LDS lookups)       2 = no tail (no decode, no stores)
+//   4 = decode but no stores (kept alive)       8 = every store to the sink
+//   16 = the other store flavour (rows: temporal; columns: non-temporal)
 template <int NR, int MODE = 0, bool kRows = false, bool kAligned = false>
 __global__ void __launch_bounds__(kUnpackThreads)
 unpack_fixed_kernel(UnpackParams p, uint32_t expect) {
+  constexpr bool kAblXor = (MODE & 1) != 0, kAblNoTail = (MODE & 2) != 0;
+  constexpr bool kAblNoStore = (MODE & 4) != 0, kAblSink = (MODE & 8) != 0;
+  constexpr bool kAblAltStore = (MODE & 16) != 0;
+  constexpr bool kAblWrap = (MODE & 32) != 0;  // stores wrapped onto the first 16K records
+  constexpr bool kAblWt = (MODE & 64) != 0;    // write-through (sc1) stores
+  constexpr bool kAblNtLoad = (MODE & 128) != 0;  // non-temporal row loads
+  constexpr bool kAblBurst = (MODE & 256) != 0;  // (with 4) dummy rows written at the end
+  constexpr bool kAblBurstSeq = (MODE & 512) != 0;  // ... to one contiguous span per wave
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t* rep = lds;
   uint32_t* fold = lds + kRepDwords;  // [A4 | A8 | A12 | A16 | A32 | A48]
-  for (int e = threadIdx.x; e < 1024; e += blockDim.x) {
-    const uint32_t v = p.tabs[e];
-    u32x4_t s = {v, v, v, v};
-    u32x4_t* dst = reinterpret_cast<u32x4_t*>(rep + (size_t)e * kRep);
-#pragma unroll
-    for (int c = 0; c < kRep / 4; c++) dst[c] = s;
-  }
-  for (int e = threadIdx.x; e < kFoldTabs * 1024; e += blockDim.x) fold[e] = p.tabs[1024 + e];
-  __syncthreads();
+  const uint8_t* ldsb = reinterpret_cast<const uint8_t*>(rep);
+  const TableRegs tab_regs = table_loads(p.tabs);  // staged below, after the first rows
+  asm volatile("" ::: "memory");  // these loads issue before the rows (in-order vmcnt)
 
   const int lane = threadIdx.x & 63;
   const int q = lane & 3;
-  const uint32_t copy = (uint32_t)(lane & 31);
+  const uint32_t s1 = a64_s1((uint32_t)lane);
   const uint32_t wave_id = __builtin_amdgcn_readfirstlane(
       blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
   const uint32_t n_waves = gridDim.x * (blockDim.x >> 6);
@@ -780,7 +822,6 @@ unpack_fixed_kernel(UnpackParams p, uint32_t expect) {
   // streams spread worse over the HBM channels.
   uint32_t g = wave_id;
   const uint32_t g_end = n_groups;
-  if (g >= g_end) return;
 
   // Geometry.  Every load is slab (uniform SGPR base) + 32-bit per-lane offset + constant:
   // the saddr form, one VGPR per address (host guarantees slab_bytes < 4 GiB).  A dead
@@ -795,7 +836,10 @@ unpack_fixed_kernel(UnpackParams p, uint32_t expect) {
   auto base_off = [&](bool lv, uint32_t i) { return lv ? i * (uint32_t)p.stride : 64u; };
   // lane's byte offset of row 0 (> -64; < 0 when row 0 starts before the record)
   const int pos0 = (int)L - 64 * V + 16 * q;
-  auto ld = [&](uint32_t off, int imm) { return ldu128(p.slab + (uint64_t)off + imm); };
+  auto ld = [&](uint32_t off, int imm) {
+    if (kAblNtLoad) return ldnt128(p.slab + (uint64_t)off + imm);
+    return ldu128(p.slab + (uint64_t)off + imm);
+  };
   // row j of the record at boff (row 0 clamped to the record start).  Rows j >= 1 start at
   // boff + pos0 + 64 j with pos0 + 64 > 0: the 32-bit part must stay non-negative (it is
   // zero-extended), so the constant part is 64 (j - 1).
@@ -854,7 +898,7 @@ unpack_fixed_kernel(UnpackParams p, uint32_t expect) {
       err = MGENX_ERROR_OOB;
     }
     Out r;
-    if (kRows || MODE == 8) {  // mgenx_rec: lane q holds bytes 8q..8q+7 of its record
+    if (kRows) {  // mgenx_rec: lane q holds bytes 8q..8q+7 of its record
       r.o[0] = q == 0 ? flow : q == 1 ? sec : q == 2 ? dst4 : (plen | flags << 16 | err << 24);
       r.o[1] = q == 0 ? seq : q == 1 ? usec : q == 2 ? (msg_len | dport << 16)
                                                     : (dtype | dlen << 8 | ptype << 16 | gps << 24);
@@ -876,36 +920,31 @@ unpack_fixed_kernel(UnpackParams p, uint32_t expect) {
   auto emit = [&](Out r, uint32_t idx, bool crc_bad) {
     if (crc_bad) {  // the caller's receive check (mgenTransport.cpp:971): err, TCP flag
       const uint32_t fl = tcp ? (uint32_t)MGENX_FLAG_CHECKSUM_ERROR : 0u;
-      if (kRows || MODE == 8) {
+      if (kRows) {
         if (q == 3) r.o[0] = (r.o[0] & 0x00ffffffu) | fl << 16 | (uint32_t)MGENX_ERROR_CHECKSUM << 24;
       } else {
         if (q == 0) r.o[3] |= fl;
         if (q == 1) r.o[3] = MGENX_ERROR_CHECKSUM;
       }
     }
-    const bool in = idx < p.n && MODE != 6;  // MODE 6 (ablation): every store to the sink
+    const bool in = idx < p.n && !kAblSink;
     const uint64_t sink = (uint64_t)p.sink + 4u * (uint32_t)lane;
-    // MODE 9 (ablation): the same stores to distinct per-wave addresses that stay in L2
-    // (2 KiB per wave: 8 MiB total), so they never reach HBM during the kernel
-    int store_no = 0;
-    auto at = [&](uint64_t base, uint32_t size) {
-      if (MODE == 9)
-        return (uint64_t)p.sink2 + (uint64_t)wave_id * 2048 + 256u * (store_no++) + 4u * lane;
-      return in ? base + (uint64_t)idx * size : sink;
-    };
+    const uint32_t sidx = kAblWrap ? (idx & 0x3fffu) : idx;
+    auto at = [&](uint64_t base, uint32_t size) { return in ? base + (uint64_t)sidx * size : sink; };
     const mgenx_cols& c = p.cols;
-    if (kRows || MODE == 8) {  // 16 records = 512 contiguous bytes per store instruction
-      const uint64_t v = (uint64_t)r.o[1] << 32 | r.o[0];
-      const uint64_t rbase = kRows ? (uint64_t)p.cols.rows : (uint64_t)p.sink2;
-      const uint64_t ra = in ? rbase + (uint64_t)idx * 32 + 8 * q : (uint64_t)p.sink + 8u * lane;
-      // non-temporal: the streamed output must not compete with the read stream in L2
-      if (MODE == 10) st_g64(ra, v);  // ablation: ordinary (temporal) row stores
-      else st_g64_nt(ra, v);
+    if (kAblNoStore) {  // the tail's work without its stores (kept alive)
+      const uint32_t all = r.o[0] ^ r.o[1] ^ r.o[2] ^ r.o[3] ^ r.o[4];
+      if (all == 0x9E3779B9u) st_g32(sink, all);
       return;
     }
-    if (MODE == 7) {  // ablation: the tail's work without its stores (kept alive)
-      const uint32_t all = r.o[0] ^ r.o[1] ^ r.o[2] ^ r.o[3] ^ r.o[4];
-      if (all == 0x9E3779B9u) st_g32(at((uint64_t)c.flow_id, 4), all);
+    if (kRows) {  // 16 records = 512 contiguous bytes per store instruction
+      const uint64_t v = (uint64_t)r.o[1] << 32 | r.o[0];
+      const uint64_t ra = in ? (uint64_t)p.cols.rows + (uint64_t)sidx * 32 + 8 * q
+                             : (uint64_t)p.sink + 8u * lane;
+      // non-temporal: the streamed output must not compete with the read stream in L2
+      if (kAblWt) st_g64_wt(ra, v);
+      else if (kAblAltStore) st_g64(ra, v);  // ablation: ordinary (temporal) row stores
+      else st_g64_nt(ra, v);
       return;
     }
     const uint64_t u32 = pick4(q, (uint64_t)c.flow_id, (uint64_t)c.seq_num, (uint64_t)c.tx_sec,
@@ -916,7 +955,15 @@ unpack_fixed_kernel(UnpackParams p, uint32_t expect) {
                                (uint64_t)c.dst_len);
     const uint64_t u8b = pick4(q, (uint64_t)c.payload_type, (uint64_t)c.gps_status,
                                (uint64_t)c.payload_type, (uint64_t)c.gps_status);
-    if (MODE == 11) {  // ablation: non-temporal column stores
+    if (kAblWt) {  // ablation: write-through column stores
+      st_g32_wt(at(u32, 4), r.o[0]);
+      st_g32_wt(at((uint64_t)c.dst_addr4, 4), r.o[1]);
+      st_g16_wt(at(u16, 2), r.o[2]);
+      st_g8_wt(at(u8a, 1), r.o[3]);
+      st_g8_wt(at(u8b, 1), r.o[4]);
+      return;
+    }
+    if (kAblAltStore) {  // ablation: non-temporal column stores
       st_g32_nt(at(u32, 4), r.o[0]);
       st_g32_nt(at((uint64_t)c.dst_addr4, 4), r.o[1]);
       st_g16_nt(at(u16, 2), r.o[2]);
@@ -944,22 +991,43 @@ unpack_fixed_kernel(UnpackParams p, uint32_t expect) {
   };
 
   u32x4_t pf;
+  // The first group's rows go in flight before the tables are written to LDS (the staging's
+  // load latency and LDS writes then overlap the first HBM round trip); a wave without a
+  // group still loads (dummy rows) and joins the barrier.
+  auto load_group = [&](uint32_t gg) {
+    const uint32_t i = rec_idx(gg);
+    const uint32_t boff = base_off(is_live(i), i);
+    if (!kAligned) pf = ld_hdr(boff);
+    // in row order (the loop's first wait is for row 0 alone)
+#pragma unroll
+    for (int j = 0; j < NR; j++) {
+      d[j] = ld_row(boff, j);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  load_group(g);  // unconditional (a wave past the end reads the dummy rows at offset 64)
+  table_writes(lds, tab_regs);
+  // barrier without __syncthreads()'s fence: its vmcnt(0) would wait for the rows above
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (g >= g_end) return;
+  bool first = true;
   while (g < g_end) {
     // ---- pipelined mode: rows of every group speculatively in flight one group ahead.
     // No load in this loop is conditional (a conditional reload makes LLVM copy the row
     // registers at the join, and a copy of an in-flight load drains the whole queue).
     uint32_t idx = rec_idx(g);
     bool live = is_live(idx);
-    {
+    if (!first) {
       const uint32_t boff = base_off(live, idx);
       if (!kAligned) pf = ld_hdr(boff);
-      // in row order (the loop's first wait is for row 0 alone)
 #pragma unroll
       for (int j = 0; j < NR; j++) {
         d[j] = ld_row(boff, j);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
+    first = false;
     // one pipelined group; the header registers alternate between two variables (the loop
     // is unrolled twice) so the next header never needs a register copy
     auto step = [&](const u32x4_t& pf_cur, u32x4_t& pf_nxt) {
@@ -976,9 +1044,10 @@ unpack_fixed_kernel(UnpackParams p, uint32_t expect) {
       const bool any = __any(needs_crc);
       // aligned: decode now, so row 0's registers are free for its reload
       Out early;
-      if (kAligned && MODE != 5) early = decode(hdr, idx, live);
+      if (kAligned && !kAblNoTail) early = decode(hdr, idx, live);
 
-      uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+      // braid state word b = ha[b] ^ hb[b] (split so the next row folds in one XOR3)
+      uint32_t ha[4] = {0u, 0u, 0u, 0u}, hb[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
       for (int j = 0; j < NR - 1; j++) {
         u32x4_t x = d[j];
@@ -989,39 +1058,33 @@ unpack_fixed_kernel(UnpackParams p, uint32_t expect) {
             x = s0 < 16 ? shl_bytes(x, s0) : zero;
           }
         }
+        const uint32_t xw[4] = {x.x, x.y, x.z, x.w};
         uint32_t c4[4];
-        if (MODE == 1 || MODE == 4 || MODE == 5 || MODE == 6 || MODE == 7) {
-          c4[0] = (h0 << 1) ^ x.x; c4[1] = (h1 << 1) ^ x.y;
-          c4[2] = (h2 << 1) ^ x.z; c4[3] = (h3 << 1) ^ x.w;
-        } else {
-          c4[0] = h0 ^ x.x; c4[1] = h1 ^ x.y; c4[2] = h2 ^ x.z; c4[3] = h3 ^ x.w;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          if (kAblXor)
+            c4[b] = (ha[b] << 1) ^ xw[b];
+          else
+            c4[b] = xor3(ha[b], hb[b], xw[b]);
         }
         // row j of g is dead now: reload its register for g' (same physical register, so
         // no loop-carried copy -- a copy of an in-flight load would drain the queue)
         __builtin_amdgcn_sched_barrier(0);
         d[j] = ld_row(boff_n, j);
         __builtin_amdgcn_sched_barrier(0);
-        if (MODE == 1 || MODE == 4 || MODE == 5 || MODE == 6 || MODE == 7) {
-          h0 = c4[0]; h1 = c4[1]; h2 = c4[2]; h3 = c4[3];
+        if (kAblXor) {
+#pragma unroll
+          for (int b = 0; b < 4; b++) ha[b] = c4[b];
           continue;
         }
-        uint32_t t[16];
 #pragma unroll
-        for (int b = 0; b < 4; b++) {
-          t[4 * b + 0] = rep[((c4[b] & 0xffu) << 5) | copy];
-          t[4 * b + 1] = rep[8192 + ((((c4[b] >> 8) & 0xffu) << 5) | copy)];
-          t[4 * b + 2] = rep[16384 + ((((c4[b] >> 16) & 0xffu) << 5) | copy)];
-          t[4 * b + 3] = rep[24576 + (((c4[b] >> 24) << 5) | copy)];
-        }
-        h0 = t[0] ^ t[1] ^ t[2] ^ t[3];
-        h1 = t[4] ^ t[5] ^ t[6] ^ t[7];
-        h2 = t[8] ^ t[9] ^ t[10] ^ t[11];
-        h3 = t[12] ^ t[13] ^ t[14] ^ t[15];
+        for (int b = 0; b < 4; b++) a64_parts(ldsb, c4[b], s1, ha[b], hb[b]);
       }
       // final row (V >= 2, so never row 0): the big-endian trailer goes to stream order
       const u32x4_t xf = d[NR - 1];
-      uint32_t f0 = h0 ^ xf.x, f1 = h1 ^ xf.y, f2 = h2 ^ xf.z;
-      uint32_t f3 = h3 ^ (q == 3 ? bswap32(xf.w) : xf.w);
+      uint32_t f0 = xor3(ha[0], hb[0], xf.x), f1 = xor3(ha[1], hb[1], xf.y);
+      uint32_t f2 = xor3(ha[2], hb[2], xf.z);
+      uint32_t f3 = xor3(ha[3], hb[3], q == 3 ? bswap32(xf.w) : xf.w);
       // opaque: later index math must not reach back to the row registers (which would keep
       // them live across their reload and cost a loop-carried copy of the in-flight load)
       asm volatile("" : "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3));
@@ -1034,7 +1097,7 @@ unpack_fixed_kernel(UnpackParams p, uint32_t expect) {
       uint32_t s = (q == 3) ? v : shift_tab(lt, v);
       s ^= __shfl_xor(s, 1);
       s ^= __shfl_xor(s, 2);
-      if (MODE == 5) {
+      if (kAblNoTail) {
         if (s == 0x9E3779B9u && lane == 0) p.cols.err[idx] = (uint8_t)needs_crc;  // keep alive
       } else {
         const Out r = kAligned ? early : decode(hdr, idx, live);
@@ -1071,9 +1134,17 @@ unpack_fixed_kernel(UnpackParams p, uint32_t expect) {
       emit(decode(ph, i, lv), i, false);
     }
   }
+  if (kAblBurst) {  // every group's row stores in one burst after the wave's last group
+    uint32_t k = 0;
+    for (uint32_t gg = wave_id; gg < g_end; gg += n_waves, k++) {
+      const uint32_t i = rec_idx(gg);
+      const uint64_t seq = (uint64_t)wave_id * 8192u + k * 512u + 8u * (uint32_t)lane;
+      if (i < p.n)
+        st_g64_nt((uint64_t)p.cols.rows + (kAblBurstSeq ? seq : (uint64_t)i * 32 + 8 * q),
+                  (uint64_t)gg);
+    }
+  }
 }
-
-int unpack_variant = 0;
 
 template <typename K>
 static hipError_t launch_lds(K kernel, bool& attr_done, const UnpackParams& p, int grid,
@@ -1122,6 +1193,7 @@ static const fixed_launcher kFixedLaunchRows[17] = MGENX_FIXED_TABLE(true);
 #undef MGENX_FIXED_TABLE
 
 hipError_t launch_unpack(const UnpackParams& p, int grid, hipStream_t stream) {
+  const int unpack_variant = p.variant;
   if (p.opts & MGENX_OPT_SKIP_CRC) {
     hipLaunchKernelGGL((unpack_kernel<false>), dim3(grid), dim3(kUnpackThreads), 0, stream, p);
     return hipGetLastError();
@@ -1151,14 +1223,19 @@ hipError_t launch_unpack(const UnpackParams& p, int grid, hipStream_t stream) {
   // ablation 12: the unaligned (separate header load) path on 1024-B records
   if (unpack_variant == 12 && fixed && p.fixed_len == 1024)
     return c.rows ? launch_fixed<16, 0, true>(p, grid, stream) : launch_fixed<16, 0>(p, grid, stream);
-  if (unpack_variant == 4 && fixed && p.fixed_len == 1024) return launch_fixed<16, 1>(p, grid, stream);
-  if (unpack_variant == 5 && fixed && p.fixed_len == 1024) return launch_fixed<16, 5>(p, grid, stream);
-  if (unpack_variant == 6 && fixed && p.fixed_len == 1024) return launch_fixed<16, 6>(p, grid, stream);
-  if (unpack_variant == 7 && fixed && p.fixed_len == 1024) return launch_fixed<16, 7>(p, grid, stream);
-  if (unpack_variant == 8 && fixed && p.fixed_len == 1024 && p.sink2) return launch_fixed<16, 8>(p, grid, stream);
-  if (unpack_variant == 9 && fixed && p.fixed_len == 1024 && p.sink2) return launch_fixed<16, 9>(p, grid, stream);
-  if (unpack_variant == 10 && fixed && p.fixed_len == 1024 && c.rows) return launch_fixed<16, 10, true>(p, grid, stream);
-  if (unpack_variant == 11 && fixed && p.fixed_len == 1024 && !c.rows) return launch_fixed<16, 11>(p, grid, stream);
+  // ablations of the aligned 1024-B kernel: variant 1024 + MODE (see unpack_fixed_kernel)
+  if (unpack_variant >= 1024 && fixed && p.fixed_len == 1024) {
+    switch (unpack_variant - 1024) {
+#define MGENX_ABL(M) \
+  case M: return c.rows ? launch_fixed<16, M, true, true>(p, grid, stream) \
+                        : launch_fixed<16, M, false, true>(p, grid, stream);
+      MGENX_ABL(1) MGENX_ABL(2) MGENX_ABL(3) MGENX_ABL(4) MGENX_ABL(5) MGENX_ABL(8)
+      MGENX_ABL(16) MGENX_ABL(32) MGENX_ABL(64)
+      MGENX_ABL(128) MGENX_ABL(144) MGENX_ABL(130) MGENX_ABL(136) MGENX_ABL(260) MGENX_ABL(772)
+#undef MGENX_ABL
+      default: break;
+    }
+  }
   switch (unpack_variant) {
     case 1: return launch_mode<1>(p, grid, stream);
     case 2: return launch_mode<2>(p, grid, stream);
@@ -1183,6 +1260,59 @@ __global__ void __launch_bounds__(256) stream_read_kernel(const u32x4_t* p, uint
     acc ^= a.x ^ a.y ^ a.z ^ a.w;
   }
   if (acc == 0x9E3779B9u) out[blockIdx.x] = acc;  // practically never taken
+}
+
+// Diagnostic: unpack_fixed_kernel's memory pattern alone (groups of 16 x 1 KiB dealt to waves
+// round-robin, rows reloaded one group ahead, 512 B stored per group when MODE & 1).
+template <int MODE>
+__global__ void __launch_bounds__(1024) group_rw_kernel(const uint8_t* p, uint32_t n_groups,
+                                                        uint8_t* out) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave_id = __builtin_amdgcn_readfirstlane(blockIdx.x * 16 + (threadIdx.x >> 6));
+  const uint32_t n_waves = gridDim.x * 16;
+  uint32_t g = wave_id;
+  if (g >= n_groups) return;
+  // lane l of row j: record l/4 of the group, bytes 64 j + 16 (l & 3)
+  const uint32_t lo = (uint32_t)(lane >> 2) * 1024u + 16u * (lane & 3);
+  u32x4_t d[16];
+#pragma unroll
+  for (int j = 0; j < 16; j++) d[j] = ldu128(p + (uint64_t)g * 16384u + lo + 64 * j);
+  uint32_t acc = 0;
+  while (g < n_groups) {
+    const uint32_t gn = g + n_waves;
+    const uint32_t gl = gn < n_groups ? gn : g;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      acc = (acc << 1) ^ d[j].x ^ d[j].y ^ d[j].z ^ d[j].w;
+      __builtin_amdgcn_sched_barrier(0);
+      d[j] = ldu128(p + (uint64_t)gl * 16384u + lo + 64 * j);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (MODE & 4) {  // 16-B stores from half the lanes
+      if (lane < 32) {
+        u32x4_t v = {acc, g, acc, g};
+        *reinterpret_cast<u32x4_t*>(out + (uint64_t)g * 512u + 16u * lane) = v;
+      }
+    } else if (MODE & 1) {
+      const uint64_t a = (uint64_t)out + (uint64_t)g * 512u + 8u * lane;
+      const uint64_t v = (uint64_t)acc << 32 | g;
+      if (MODE & 2) st_g64_wt(a, v); else st_g64(a, v);
+    }
+    g = gn;
+  }
+  if (!(MODE & 1) && acc == 0x9E3779B9u) out[lane] = 1;
+}
+
+hipError_t launch_group_rw(const uint8_t* p, uint64_t bytes, uint8_t* out, int mode, int grid,
+                           hipStream_t stream) {
+  const uint32_t ng = (uint32_t)(bytes / 16384);
+  switch (mode & 7) {
+    case 4: hipLaunchKernelGGL(group_rw_kernel<4>, dim3(grid), dim3(1024), 0, stream, p, ng, out); break;
+    case 0: hipLaunchKernelGGL(group_rw_kernel<0>, dim3(grid), dim3(1024), 0, stream, p, ng, out); break;
+    case 1: hipLaunchKernelGGL(group_rw_kernel<1>, dim3(grid), dim3(1024), 0, stream, p, ng, out); break;
+    default: hipLaunchKernelGGL(group_rw_kernel<3>, dim3(grid), dim3(1024), 0, stream, p, ng, out); break;
+  }
+  return hipGetLastError();
 }
 
 hipError_t launch_stream_read(const uint8_t* p, uint64_t bytes, uint32_t* out, int grid,

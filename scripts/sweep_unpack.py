@@ -31,42 +31,30 @@ assert int((cols["err"] != 0).sum()) == 0
 
 
 def run(name):
-    if name == "rows0":
-        eng.set_unpack_variant(0)
-        eng.unpack(slab, N, stride=REC, fixed_len=REC, cols=rows)
-    elif name == "rows_t":
-        eng.set_unpack_variant(10)
-        eng.unpack(slab, N, stride=REC, fixed_len=REC, cols=rows)
-    elif name == "cols_nt":
-        eng.set_unpack_variant(11)
-        eng.unpack(slab, N, stride=REC, fixed_len=REC, cols=cols)
-    elif name == "rows12":
-        eng.set_unpack_variant(12)
-        eng.unpack(slab, N, stride=REC, fixed_len=REC, cols=rows)
-    elif name == "cols12":
-        eng.set_unpack_variant(12)
-        eng.unpack(slab, N, stride=REC, fixed_len=REC, cols=cols)
+    """c<V> / r<V>: columns / 32-B rows with unpack variant V; hdr_*: checksum off;
+    read_<G>: plain streaming read of the slab with grid G."""
+    if name[0] in "cr" and name[1:].isdigit():
+        eng.set_unpack_variant(int(name[1:]))
+        eng.unpack(slab, N, stride=REC, fixed_len=REC, cols=cols if name[0] == "c" else rows)
     elif name == "hdr_rows":
         eng.set_unpack_variant(0)
         eng.unpack(slab, N, stride=REC, fixed_len=REC, cols=rows, opts=OPT_SKIP_CRC)
-    elif name == "rows3":
-        eng.set_unpack_variant(3)
-        eng.unpack(slab, N, stride=REC, fixed_len=REC, cols=rows)
-    elif name.startswith("mode"):
-        eng.set_unpack_variant(int(name[4:]))
-        eng.unpack(slab, N, stride=REC, fixed_len=REC, cols=cols)
     elif name == "hdr_only":
         eng.set_unpack_variant(0)
         eng.unpack(slab, N, stride=REC, fixed_len=REC, cols=cols, opts=OPT_SKIP_CRC)
+    elif name.startswith("grw"):  # grw<mode>: group read (+ row stores)
+        eng.group_rw(slab, rows["rows"], int(name[3:]))
+    elif name == "fill_rows":
+        rows["rows"].fill_(1)
     else:
         eng.stream_read(slab, grid=int(name.split("_")[1]))
 
 
 names = os.environ.get("SWEEP_NAMES", "").split(",") if os.environ.get("SWEEP_NAMES") else [
-    "mode0", "cols12", "rows0", "rows12", "mode3", "rows3", "hdr_rows", "mode5", "mode1", "mode2",
-    "hdr_only", "read_1024", "read_2048", "read_4096", "read_8192"]
+    "c0", "r0", "c12", "c33", "c34", "c35", "c36", "c37", "c40", "c48", "r48", "hdr_only",
+    "read_8192"]
 res = {k: [] for k in names}
-for rnd in range(5):
+for rnd in range(7):
     for k in names:
         run(k)
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -80,6 +68,6 @@ eng.set_unpack_variant(0)
 out = {}
 for k, t in res.items():
     ms = float(np.median(t))
-    byts = N * REC if k.startswith("read") else ALGO
+    byts = N * REC if k.startswith("read") else (N * 32 if k == "fill_rows" else ALGO)
     out[k] = {"ms": round(ms, 4), "GBps": round(byts / ms / 1e6, 1)}
 print(json.dumps(out))
