@@ -272,6 +272,8 @@ int mgenx_flow_export(mgenx_ctx* ctx, const mgenx_flow_state* dev_flows, uint32_
  * 128 = non-temporal row loads, 256 (with 4) = dummy rows stored after each wave's last
  * group). */
 #define MGENX_TUNE_UNPACK_VARIANT 1
+/* MGENX_TUNE_PACK_VARIANT: 0 = product; ablations 1 = no unit stores, 2 = no CRC work. */
+#define MGENX_TUNE_PACK_VARIANT 2
 int mgenx_set_tuning(mgenx_ctx* ctx, int key, int value);
 /* Diagnostic: plain 16-B-per-lane streaming read of `bytes` (the achievable-HBM reference
  * next to the roofline); dev_scratch holds `grid` words. */

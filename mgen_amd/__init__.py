@@ -165,6 +165,9 @@ class Engine:
         self._check(rc, "mgenx_pack_batch")
         return out_len
 
+    def set_pack_variant(self, v: int):
+        self._check(self.lib.mgenx_set_tuning(self.ctx, 2, v), "mgenx_set_tuning")
+
     def set_unpack_variant(self, v: int):
         self._check(self.lib.mgenx_set_tuning(self.ctx, 1, v), "mgenx_set_tuning")
 

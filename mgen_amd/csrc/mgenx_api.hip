@@ -47,6 +47,7 @@ struct mgenx_ctx {
   void* scan_ws = nullptr;        // stream-scan workspace (mgenx_scan.hip), grown on demand
   void* flow_ws = nullptr;        // flow-reduce workspace (mgenx_analytic.hip), grown on demand
   int unpack_variant = 0;          // diagnostic kernel ablation (mgenx_set_tuning)
+  int pack_variant = 0;
   bool rand_ready = false;
   uint32_t rand_time = 0;
   char err[256] = {0};
@@ -276,6 +277,8 @@ int mgenx_pack_batch(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
   p.out_len = dev_out_len;
   p.opts = opts;
   p.byte_tab = ctx->d_bytetab;
+  p.a4_tab = ctx->d_tabs + 1024;  // [A_64 | A_4 | ...]
+  p.variant = ctx->pack_variant;
   p.xpow = ctx->d_xpow;
   p.ia = ctx->d_ia;
   p.rtab = ctx->d_rtab;
@@ -290,6 +293,11 @@ int mgenx_pack_batch(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
 
 int mgenx_set_tuning(mgenx_ctx* ctx, int key, int value) {
   if (!ctx) return MGENX_EINVAL;
+  if (key == MGENX_TUNE_PACK_VARIANT) {
+    if (value < 0 || value > 3) return MGENX_EINVAL;
+    ctx->pack_variant = value;
+    return MGENX_OK;
+  }
   if (key == MGENX_TUNE_UNPACK_VARIANT) {
     if (value < 0 || value > 2047) return MGENX_EINVAL;
     ctx->unpack_variant = value;

@@ -35,10 +35,12 @@ struct PackParams {
   uint32_t* out_len;
   uint32_t opts;
   const uint32_t* byte_tab;  // [256] reference CRC table
+  const uint32_t* a4_tab;    // [4][256] A_4 (x -> x * x^32 mod P): four bytes per step
   const uint32_t* xpow;      // [65536] x^(8n) mod P
   const uint32_t* ia;        // [65536] A_n(0xFFFFFFFF)
   const uint8_t* rtab;       // 16 zero bytes + glibc rand() byte stream (random fill)
   const uint32_t* rcrc;      // [65536] crc_raw of the first k rand bytes
+  int variant;               // diagnostic ablation (0 = product path)
 };
 
 hipError_t launch_unpack(const UnpackParams& p, int grid, hipStream_t stream);

@@ -10,7 +10,8 @@
 //         crc_raw(H || P || F) = A_|P|+|F|(crc_raw(H)) ^ A_|F|(crc_raw(P)) ^ crc_raw(F)
 //      with crc_raw(P) precomputed per template (mgenx_pack_prepare), crc_raw(zero fill)=0,
 //      crc_raw(random fill prefix) from a per-fill_time table, A_n(x) = x * x^(8n) mod P.
-//      Only the <= 76 header bytes are fed through the byte table.
+//      Only the <= 76 header bytes are fed through tables, four at a time:
+//      c <- A_4(c ^ word) (the <= 3 trailing bytes through the byte table).
 //   2. write (lane = 16-byte unit): the wave's records are cut into 16-byte units; every
 //      lane composes one unit from fill / header image / payload / trailer and stores it.
 #include "mgenx_kernels.hpp"
@@ -53,14 +54,16 @@ pack_kernel(PackParams p) {
   __shared__ PackMeta s_meta[kWaves][64];
   __shared__ uint32_t s_pre[kWaves][65];
   __shared__ uint32_t s_tab[256];
+  __shared__ uint32_t s_a4[1024];
 
   for (int e = threadIdx.x; e < 256; e += blockDim.x) s_tab[e] = p.byte_tab[e];
+  for (int e = threadIdx.x; e < 1024; e += blockDim.x) s_a4[e] = p.a4_tab[e];
   __syncthreads();
 
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   uint8_t* img = &s_img[wv][lane * kImg];
-  const bool ck = (p.opts & MGENX_PACK_CHECKSUM) != 0;
+  const bool ck = (p.opts & MGENX_PACK_CHECKSUM) != 0 && p.variant != 2;
   const bool rf = (p.opts & MGENX_PACK_RANDOM_FILL) != 0;
   const uint64_t n_batches = ((uint64_t)p.n + 63) >> 6;
   const uint64_t n_waves = (uint64_t)gridDim.x * kWaves;
@@ -75,70 +78,109 @@ pack_kernel(PackParams p) {
 
     // ------------------------------ phase 1: meta ------------------------------
     if (b < n_batches && i < p.n) {
+      // Every global read of the record is issued up front, in two dependent rounds:
+      // descriptor, then the template (68 B, as 17 words in registers) and the CRC tables
+      // indexed by lengths the template fixes.  (Field reads through the template pointer
+      // inside the layout walk would each be a serialised round trip.)
       const mgenx_pack_desc d = p.desc[i];
-      const mgenx_flow_tmpl& t = p.tmpl[d.tmpl];
+      const uint32_t* tp = reinterpret_cast<const uint32_t*>(p.tmpl + d.tmpl);
+      uint32_t tw[17];
+#pragma unroll
+      for (int k = 0; k < 17; k++) tw[k] = tp[k];
       m.off = p.rec_off ? p.rec_off[i] : i * p.stride;
       const uint32_t msgLen = d.msg_len;
+      const uint32_t t_flow = tw[0], t_dtype = tw[1] & 0xffu, t_dlen = (tw[1] >> 8) & 0xffu;
+      const uint32_t t_dport = tw[1] >> 16;
+      const uint32_t t_htype = tw[6] & 0xffu, t_hlen = (tw[6] >> 8) & 0xffu;
+      const uint32_t t_hport = tw[6] >> 16;
+      const uint32_t t_gps = tw[14] & 0xffu, t_ptype = (tw[14] >> 8) & 0xffu;
+      const uint32_t t_plen = tw[14] >> 16, t_poff = tw[15], t_has = tw[16] & 0xffu;
       uint32_t flags = d.flags | MGENX_FLAG_LAST_BUFFER;      // mgenTransport.cpp:1017
-      bool failed = false, trunc = false;
-      uint32_t len = 0;
-      img_put16(img, 0, d.msg_len);                            // mgenMsg.cpp:97-131
+
+      // ---- layout walk (mgenMsg.cpp:97-273), arithmetic only ----
+      const bool dst_ok = t_dtype == 1u || t_dtype == 2u;     // :146-148
+      const uint32_t D = t_dlen > 16u ? 16u : t_dlen;
+      const bool hv = t_htype == 1u || t_htype == 2u;
+      const uint32_t H = hv ? (t_hlen > 16u ? 16u : t_hlen) : 0u;
+      uint32_t len = 24u + D;
+      const bool host_in = msgLen >= len + H + 4u;              // :182-200
+      const bool failed = !dst_ok || (!host_in && msgLen < len);  // :207-210
+      bool trunc = !host_in;
+      const uint32_t host_at = len;
+      if (!trunc) len += 4u + H;
+      const uint32_t gps_at = len;
+      const bool gps_in = !trunc && msgLen >= len + 13u;        // :219-241
+      trunc = trunc || !gps_in;
+      if (!trunc) len += 13u;
+      const uint32_t pt_at = len;
+      const bool pt_in = !trunc && msgLen >= len + 1u;          // :243-251
+      trunc = trunc || !pt_in;
+      if (!trunc) len += 1u;
+      const uint32_t pl_at = len;
+      const bool pl_in = !trunc && msgLen >= len + 2u;          // :252-263
+      trunc = trunc || !pl_in;
+      if (!trunc) len += 2u;
+      const bool pay = !trunc && t_has && msgLen >= len + t_plen;  // :264-273
+      const uint32_t pend = pay ? len + t_plen : len;
+      const uint32_t crc_len = msgLen - 4u;
+      const bool full_pay = crc_len > len && crc_len >= pend && pend > len;
+      const uint32_t f = crc_len > pend ? crc_len - pend : 0u;
+      const bool crc_on = ck && !failed && !trunc;
+      // ---- the CRC-side reads, independent of the image ----
+      uint32_t x_seg = 0, x_f = 0, ia_v = 0, rc_v = 0, tcrc = 0;
+      if (crc_on) {
+        if (full_pay) { x_seg = p.xpow[pend - len]; tcrc = p.tmpl_crc[d.tmpl]; }
+        if (crc_len > pend) { x_f = p.xpow[f]; if (rf && f >= 2) rc_v = p.rcrc[f - 2]; }
+        ia_v = p.ia[crc_len];
+      }
+      // payload bytes that land in the header image (statically unrolled: one round trip)
+      const uint32_t pimg = pay ? min(t_plen, (uint32_t)kImg > len ? (uint32_t)kImg - len : 0u) : 0u;
+      // (whole words by dword loads, the last partial word byte by byte: no read past it)
+      uint32_t pw[(kImg - 44) / 4];  // the header is >= 44 bytes when a payload follows
+#pragma unroll
+      for (int k = 0; k < (kImg - 44) / 4; k++) {
+        const uint8_t* src = p.pool + t_poff + 4 * k;
+        uint32_t w = 0;
+        if ((uint32_t)(4 * k + 4) <= pimg) {
+          w = ldu32(src);
+        } else if ((uint32_t)(4 * k) < pimg) {
+          const uint32_t nb = pimg - 4 * k;
+          w = src[0] | (nb > 1 ? (uint32_t)src[1] << 8 : 0u) | (nb > 2 ? (uint32_t)src[2] << 16 : 0u);
+        }
+        pw[k] = w;
+      }
+
+      // ---- header image in LDS ----
+      img_put16(img, 0, msgLen);                               // mgenMsg.cpp:97-131
       img_put8(img, 2, 2);
       img_put8(img, 3, flags);
-      img_put32(img, 4, t.flow_id);
+      img_put32(img, 4, t_flow);
       img_put32(img, 8, d.seq_num);
       img_put32(img, 12, d.tx_sec);
       img_put32(img, 16, d.tx_usec);
-      img_put16(img, 20, t.dst_port);
-      len = 22;
-      if (t.dst_type != 1 && t.dst_type != 2) {
-        failed = true;                                         // :146-148
-      } else {
-        const uint32_t D = t.dst_len > 16 ? 16u : t.dst_len;
-        img_put8(img, 22, t.dst_type);
+      img_put16(img, 20, t_dport);
+      if (dst_ok) {
+        img_put8(img, 22, t_dtype);
         img_put8(img, 23, D);
-        for (uint32_t k = 0; k < D; k++) img_put8(img, 24 + k, t.dst_addr[k]);
-        len = 24 + D;
-        const bool hv = (t.host_type == 1 || t.host_type == 2);
-        const uint32_t H = hv ? (t.host_len > 16 ? 16u : t.host_len) : 0u;
-        if (msgLen >= len + H + 4) {                           // :182-200
-          img_put16(img, len, hv ? t.host_port : 0);
-          img_put8(img, len + 2, hv ? t.host_type : 0);
-          img_put8(img, len + 3, H);
-          for (uint32_t k = 0; k < H; k++) img_put8(img, len + 4 + k, t.host_addr[k]);
-          len += 4 + H;
-        } else if (msgLen < len) {
-          failed = true;                                       // :207-210
-        } else {
-          trunc = true;
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+          if ((uint32_t)k < D) img_put8(img, 24 + k, tw[2 + (k >> 2)] >> (8 * (k & 3)));
+        if (host_in) {
+          img_put16(img, host_at, hv ? t_hport : 0u);
+          img_put8(img, host_at + 2, hv ? t_htype : 0u);
+          img_put8(img, host_at + 3, H);
+#pragma unroll
+          for (int k = 0; k < 16; k++)
+            if ((uint32_t)k < H) img_put8(img, host_at + 4 + k, tw[7 + (k >> 2)] >> (8 * (k & 3)));
         }
-        if (!failed && !trunc) {
-          if (msgLen >= len + 13) {                            // :219-241
-            img_put32(img, len, t.lat_raw);
-            img_put32(img, len + 4, t.lon_raw);
-            img_put32(img, len + 8, (uint32_t)t.alt);
-            img_put8(img, len + 12, t.gps_status);
-            len += 13;
-          } else {
-            trunc = true;
-          }
+        if (gps_in) {
+          img_put32(img, gps_at, tw[11]);
+          img_put32(img, gps_at + 4, tw[12]);
+          img_put32(img, gps_at + 8, tw[13]);
+          img_put8(img, gps_at + 12, t_gps);
         }
-        if (!failed && !trunc) {
-          if (msgLen >= len + 1) {                             // :243-251
-            img_put8(img, len, t.payload_type);
-            len += 1;
-          } else {
-            trunc = true;
-          }
-        }
-        if (!failed && !trunc) {
-          if (msgLen >= len + 2) {                             // :252-263
-            img_put16(img, len, t.payload_len);
-            len += 2;
-          } else {
-            trunc = true;
-          }
-        }
+        if (pt_in) img_put8(img, pt_at, t_ptype);
+        if (pl_in) img_put16(img, pl_at, t_plen);
       }
       if (failed) {
         m.ret = 0;
@@ -146,45 +188,44 @@ pack_kernel(PackParams p) {
         m.ret = msgLen;
         m.rf = (rf && !trunc) ? 1 : 0;   // truncated records are zero-filled (:205-262)
         m.hdr = (uint16_t)len;
-        m.pend = len;
+        m.pend = pend;
         uint32_t tx_checksum = 0;
         if (!trunc) {
-          // payload (:264-273)
-          if (t.has_payload && msgLen >= len + t.payload_len) {
-            m.poff = t.payload_off;
-            for (uint32_t k = 0; k < t.payload_len && len + k < (uint32_t)kImg; k++)
-              img_put8(img, len + k, p.pool[t.payload_off + k]);
-            m.pend = len + t.payload_len;
+          if (pay) {
+            m.poff = t_poff;
+#pragma unroll
+            for (int k = 0; k < kImg - 44; k++)
+              if ((uint32_t)k < pimg) img_put8(img, len + k, pw[k >> 2] >> (8 * (k & 3)));
           } else {
-            img_put8(img, len - 2, 0);
+            img_put8(img, len - 2, 0);                           // payload_len field zeroed
             img_put8(img, len - 1, 0);
           }
           if (ck) {                                            // :295-310
-            if (msgLen > m.pend + 4) {
+            if (msgLen > pend + 4) {
               flags |= MGENX_FLAG_CHECKSUM;
               img_put8(img, 3, flags & 0xffu);
             }
             // ComputeCRC32 over msgLen-4 bytes (LAST_BUFFER is set)
-            const uint32_t crc_len = msgLen - 4;
-            const uint32_t hb = crc_len < (uint32_t)m.hdr ? crc_len : (uint32_t)m.hdr;
+            const uint32_t hb = crc_len < len ? crc_len : len;
             uint32_t c = 0;
-            for (uint32_t k = 0; k < hb; k++) c = s_tab[(c ^ img[k]) & 0xffu] ^ (c >> 8);
-            if (crc_len > m.hdr) {
-              const uint32_t seg_end = crc_len < m.pend ? crc_len : m.pend;
-              const uint32_t seg = seg_end - m.hdr;
-              if (seg == m.pend - m.hdr && seg > 0) {
-                c = multmodp(p.xpow[seg], c) ^ p.tmpl_crc[d.tmpl];
-              } else {
-                for (uint32_t k = 0; k < seg; k++)
-                  c = s_tab[(c ^ p.pool[m.poff + k]) & 0xffu] ^ (c >> 8);
-              }
-              if (crc_len > m.pend) {
-                const uint32_t f = crc_len - m.pend;
-                c = multmodp(p.xpow[f], c);
-                if (rf && f >= 2) c ^= p.rcrc[f - 2];
-              }
+            const uint32_t nw = hb >> 2;
+            for (uint32_t k = 0; k < nw; k++) {
+              const uint32_t x = c ^ *reinterpret_cast<const uint32_t*>(img + 4 * k);
+              c = s_a4[x & 0xffu] ^ s_a4[256 + ((x >> 8) & 0xffu)] ^
+                  s_a4[512 + ((x >> 16) & 0xffu)] ^ s_a4[768 + (x >> 24)];
             }
-            tx_checksum = c ^ p.ia[crc_len];
+            for (uint32_t k = nw << 2; k < hb; k++) c = s_tab[(c ^ img[k]) & 0xffu] ^ (c >> 8);
+            if (crc_len > len) {
+              if (full_pay) {
+                c = multmodp(x_seg, c) ^ tcrc;
+              } else {  // the CRC ends inside the payload (msgLen - 4 < pend)
+                const uint32_t seg = (crc_len < pend ? crc_len : pend) - len;
+                for (uint32_t k = 0; k < seg; k++)
+                  c = s_tab[(c ^ p.pool[t_poff + k]) & 0xffu] ^ (c >> 8);
+              }
+              if (crc_len > pend) c = multmodp(x_f, c) ^ rc_v;
+            }
+            tx_checksum = c ^ ia_v;
             flags &= ~(uint32_t)MGENX_FLAG_LAST_BUFFER;
           }
         }
@@ -212,19 +253,20 @@ pack_kernel(PackParams p) {
     __syncthreads();
     const uint32_t total = s_pre[wv][64];
     // Each lane walks units lane, lane+64, ...; its record index only moves forward, so
-    // one LDS probe per unit replaces a binary search.
+    // LDS is probed only when the unit leaves the current record.
     int ri = 0;
-    uint32_t next_start = s_pre[wv][1];
+    uint32_t rstart = 0, next_start = s_pre[wv][1];
     PackMeta r = s_meta[wv][0];
-    for (uint32_t u = lane; u < total; u += 64) {
-      bool moved = false;
-      while (next_start <= u) {
-        ri++;
-        next_start = s_pre[wv][ri + 1];
-        moved = true;
+    for (uint32_t u = lane; u < (p.variant == 1 ? 0u : total); u += 64) {
+      if (next_start <= u) {
+        do {
+          ri++;
+          rstart = next_start;
+          next_start = s_pre[wv][ri + 1];
+        } while (next_start <= u);
+        r = s_meta[wv][ri];
       }
-      if (moved) r = s_meta[wv][ri];
-      const uint32_t pos = (u - s_pre[wv][ri]) << 4;
+      const uint32_t pos = (u - rstart) << 4;
       const uint8_t* rimg = &s_img[wv][ri * kImg];
       uint32_t v[4] = {0u, 0u, 0u, 0u};
       // fill (zero, or the rand() stream after two zero bytes: mgenMsg.cpp:277-292)
@@ -258,17 +300,23 @@ pack_kernel(PackParams p) {
           }
         }
       }
-      // trailer (big-endian CRC at ret-4)
+      // trailer (big-endian CRC at ret-4), merged word by word with masks: a per-lane
+      // register index (v[at >> 2]) would compile to a waterfall loop over the wave
       if (r.trailer_on && pos + 16 > r.ret - 4) {
         const uint32_t be = bswap32(r.trailer);  // memory order b0..b3 = MSB..LSB
+        const int t = (int)r.ret - 4 - (int)pos;
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-          const int64_t at = (int64_t)r.ret - 4 + j - (int64_t)pos;
-          if (at >= 0 && at < 16) {
-            const int k = (int)at >> 2, sh = ((int)at & 3) * 8;
-            const uint32_t byte = (be >> (8 * j)) & 0xffu;
-            v[k] = (v[k] & ~(0xffu << sh)) | (byte << sh);
+        for (int k = 0; k < 4; k++) {
+          const int o = t - 4 * k;
+          uint32_t val = 0u, msk = 0u;
+          if (o >= 0 && o < 4) {
+            val = be << (8 * o);
+            msk = 0xFFFFFFFFu << (8 * o);
+          } else if (o < 0 && o > -4) {
+            val = be >> (-8 * o);
+            msk = 0xFFFFFFFFu >> (-8 * o);
           }
+          v[k] = (v[k] & ~msk) | val;
         }
       }
       uint8_t* dst = p.slab + r.off + pos;
@@ -276,7 +324,9 @@ pack_kernel(PackParams p) {
         stu128(dst, u32x4_t{v[0], v[1], v[2], v[3]});
       } else {
         const uint32_t rem = r.ret - pos;
-        for (uint32_t j = 0; j < rem; j++) dst[j] = (uint8_t)(v[j >> 2] >> ((j & 3) * 8));
+#pragma unroll
+        for (int j = 0; j < 16; j++)
+          if ((uint32_t)j < rem) dst[j] = (uint8_t)(v[j >> 2] >> ((j & 3) * 8));
       }
     }
     __syncthreads();
