@@ -211,7 +211,7 @@ def extra_pcie(torch, eng, dev, slab):
     per = N_REC // chunks
     streams = [torch.cuda.Stream(dev) for _ in range(2)]
     dbuf = [torch.empty(per * REC, dtype=torch.uint8, device=dev) for _ in range(2)]
-    cols = [eng.alloc_cols(per) for _ in range(2)]
+    cols = [{"rows": eng.alloc_rows(per)} for _ in range(2)]
     hcols = [{k: torch.empty(v.numel(), dtype=v.dtype, pin_memory=True) for k, v in c.items()}
              for c in cols]
 
@@ -230,9 +230,10 @@ def extra_pcie(torch, eng, dev, slab):
     for _ in range(reps):
         run()
     dt = (time.perf_counter() - t0) / reps
-    assert int(hcols[0]["err"].sum()) == 0
+    err = (hcols[0]["rows"].view(torch.int32).view(per, 8)[:, 6] >> 24) & 0xFF
+    assert int((err != 0).sum()) == 0
     return {"gbps": round(N_REC * REC / dt / 1e9, 2), "ms": round(dt * 1e3, 3),
-            "chunks": chunks, "note": "pinned H2D + unpack + core columns D2H, 2 streams"}
+            "chunks": chunks, "note": "pinned H2D + unpack + 32-B rows D2H, 2 streams"}
 
 
 def main():
@@ -274,7 +275,11 @@ def main():
 
     do_pack()
     torch.cuda.synchronize()
-    cols = eng.alloc_cols(N_REC)
+    # Headline output layout: mgenx_rec rows (the 32-B core record, written as whole lines --
+    # 512 contiguous bytes per wave store).  The SoA column layout carries the same 32 B per
+    # record in 14 arrays of 1-4 B elements and is timed beside it (extra.columns_layout).
+    rows = eng.alloc_rows(N_REC)
+    cols = {"rows": rows}
     cs = eng._cols_struct(cols)
     lib, ctx = eng.lib, eng.ctx
     stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
@@ -286,12 +291,18 @@ def main():
         if rc != 0:
             raise RuntimeError(f"mgenx_unpack_batch rc={rc}")
 
+    def rows_ok():
+        r = rows.view(torch.int32).view(N_REC, 8)
+        err = (r[:, 6] >> 24) & 0xFF            # mgenx_rec.err
+        seq = r[:, 1]                           # mgenx_rec.seq_num
+        want = torch.arange(N_REC, device=dev, dtype=torch.int32) // 64
+        return int((err != 0).sum()) == 0 and bool(torch.equal(seq, want))
+
     # correctness gate before timing
     step()
     torch.cuda.synchronize()
-    bad = int((cols["err"] != 0).sum())
-    if bad or int((out_len != REC).sum()):
-        raise RuntimeError(f"unpack found {bad} bad records in a freshly packed slab")
+    if not rows_ok() or int((out_len != REC).sum()):
+        raise RuntimeError("unpack found bad records in a freshly packed slab")
 
     for _ in range(args.warmup):
         step()
@@ -325,9 +336,24 @@ def main():
     pack_ms = timed(torch, do_pack, reps=20)
     step()
     torch.cuda.synchronize()
-    assert int((cols["err"] != 0).sum()) == 0
+    assert rows_ok()
+    # the same decode into the 14 SoA core columns
+    ccols = eng.alloc_cols(N_REC)
+    col_ms = timed(torch, lambda: eng.unpack(slab, N_REC, stride=REC, fixed_len=REC,
+                                             cols=ccols), reps=20)
+    assert int((ccols["err"] != 0).sum()) == 0
+    # memory-system probes on this box: the unpack's read pattern alone, and with 512-B
+    # row stores per 16-KiB group (mgenx_diag_group_rw)
+    probe_out = torch.empty(N_REC * 32, dtype=torch.uint8, device=dev)
+    rd_ms = timed(torch, lambda: eng.group_rw(slab, probe_out, 0), reps=20)
+    rw_ms = timed(torch, lambda: eng.group_rw(slab, probe_out, 1), reps=20)
+    del probe_out, ccols
 
-    extra = {"header_only_unpack_ms": round(hdr_ms, 4),
+    extra = {"columns_layout": {"unpack_ms": round(col_ms, 4),
+                                "gbps": round(ALGO_BYTES / (col_ms * 1e-3) / 1e9, 1)},
+             "probe_read_pattern_gbps": round(N_REC * REC / (rd_ms * 1e-3) / 1e9, 1),
+             "probe_read_plus_row_stores_gbps": round(ALGO_BYTES / (rw_ms * 1e-3) / 1e9, 1),
+             "header_only_unpack_ms": round(hdr_ms, 4),
              "header_only_mmsg_per_s": round(N_REC / (hdr_ms * 1e-3) / 1e6, 1),
              "pack_ms": round(pack_ms, 4),
              "pack_gbps": round((N_REC * REC + N_REC * 20) / (pack_ms * 1e-3) / 1e9, 1)}
@@ -362,13 +388,14 @@ def main():
             "dtype": "u8",
             "data": "synthetic (GPU-packed MgenMsg records, reference Pack semantics)",
             "config": {"workload": "udp_unpack_crc_1M_x_1024B", "records_per_gpu": N_REC,
-                       "record_bytes": REC, "checksum": True,
+                       "record_bytes": REC, "checksum": True, "output": "mgenx_rec rows (32 B)",
                        "algorithmic_bytes_per_step_per_gpu": ALGO_BYTES,
                        "parallelism": f"flow-sharded x{world} (independent slabs)"},
             "mmsg_per_s": round(world * N_REC * args.steps / elapsed / 1e6, 2),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBPS,
                          "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBPS, 4),
-                         "traffic": load_traffic(), "kernel": "mgenx::unpack_fixed_kernel<16>",
+                         "traffic": load_traffic(),
+                         "kernel": "mgenx::unpack_fixed_kernel<16, 0, rows, aligned>",
                          "kernel_ms": round(kern_ms, 4)},
             "extra": extra,
         }

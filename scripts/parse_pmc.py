@@ -51,22 +51,26 @@ def find(pat):
 out = {"note": ("median over launches (each after a 512 MiB flush > Infinity Cache).  "
                 "FETCH_SIZE is calibrated per access shape (MI355X_MICROARCH.md: only wide "
                 "coalesced streaming reads are known to tally 1/2): the stream read shows "
-                "the guide's factor, and the loads-only unpack ablation (mode 5), which reads "
-                "exactly the 1 GiB slab in the unpack's own shape, calibrates that shape.  "
+                "the guide's factor, and mgenx_diag_group_rw mode 0, which reads exactly the "
+                "1 GiB slab in the unpack's own access shape, calibrates that shape.  "
                 "WRITE_SIZE is taken as exact."),
        "kernels": res}
 sr = find("stream_read_kernel")
-m5 = find("unpack_fixed_kernelILi16ELi5E") or find("unpack_fixed_kernel<16, 5>")
-m0 = find("unpack_fixed_kernelILi16ELi0E") or find("unpack_fixed_kernel<16, 0>")
+g0 = find("group_rw_kernel<0>")
+rows = find("unpack_fixed_kernel<16, 0, true, true>")
+cols = find("unpack_fixed_kernel<16, 0, false, true>")
 if sr:
     out["stream_read_fetch_factor"] = round(SLAB / (sr["fetch_kb_raw"] * 1024), 4)
-if m5 and m0:
-    factor = SLAB / (m5["fetch_kb_raw"] * 1024)
-    hbm = int(m0["fetch_kb_raw"] * 1024 * factor + m0["write_kb"] * 1024)
+if g0:
+    factor = SLAB / (g0["fetch_kb_raw"] * 1024)
     out["unpack_shape_fetch_factor"] = round(factor, 4)
-    out["unpack_crc_1M_x_1024B"] = {"hbm_bytes_per_launch": hbm, "algorithmic_bytes": algo,
-                                    "ratio": round(hbm / algo, 4),
-                                    "kernel": "mgenx::unpack_fixed_kernel<16>"}
+    for key, k in (("unpack_crc_1M_x_1024B", rows), ("unpack_crc_1M_x_1024B_columns", cols)):
+        if k:
+            hbm = int(k["fetch_kb_raw"] * 1024 * factor + k["write_kb"] * 1024)
+            out[key] = {"hbm_bytes_per_launch": hbm, "algorithmic_bytes": algo,
+                        "ratio": round(hbm / algo, 4),
+                        "read_bytes": int(k["fetch_kb_raw"] * 1024 * factor),
+                        "write_bytes": int(k["write_kb"] * 1024)}
 os.makedirs("profiles", exist_ok=True)
 json.dump(out, open(f"profiles/traffic_{ROUND}.json", "w"), indent=1)
 print(json.dumps({k: v for k, v in out.items() if k != "kernels"}))
