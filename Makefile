@@ -3,7 +3,8 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -Wno-unused-value
 SRC := mgen_amd/csrc/mgenx_api.hip mgen_amd/csrc/mgenx_unpack.hip mgen_amd/csrc/mgenx_pack.hip \
-       mgen_amd/csrc/mgenx_scan.hip mgen_amd/csrc/mgenx_analytic.hip
+       mgen_amd/csrc/mgenx_scan.hip mgen_amd/csrc/mgenx_analytic.hip \
+       mgen_amd/csrc/mgenx_log.hip
 HDR := include/mgenx.h mgen_amd/csrc/mgenx_common.hpp mgen_amd/csrc/mgenx_kernels.hpp
 
 all: mgen_amd/libmgenx.so oracle tests/cpp/host_roundtrip

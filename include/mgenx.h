@@ -262,6 +262,40 @@ int mgenx_flow_reduce(mgenx_ctx* ctx, const uint32_t* dev_flow_idx, const uint32
 int mgenx_flow_export(mgenx_ctx* ctx, const mgenx_flow_state* dev_flows, uint32_t n_flows,
                       mgenx_flow_counters* dev_out, void* stream);
 
+/* ---- event log (MgenMsg::LogRecvEvent / LogRecvError, text form) ----
+ * One line per record, as the UDP receive path logs it (src/common/mgenTransport.cpp:
+ * 976-994): "RECV proto>... flow>... seq>... src>... dst>... sent>... size>... [host>...]
+ * [ttl>...] [gps>...] [data>...] [flags>...]" for a good record
+ * (src/common/mgenMsg.cpp:1034-1102), "RERR type>... src>..." for a record with an error
+ * (:711-735); timestamps GMT "HH:MM:SS.usec" or epoch "sec.usec" (src/common/mgen.cpp:55-83).
+ * Byte-exact with the reference's fprintf output on x86-64 Linux.
+ * Inputs: the unpack outputs for the same records -- core fields (rows or columns) plus the
+ * extended columns dst_addr, host_addr, host_port, host_type, host_len, lat_raw, lon_raw,
+ * alt, payload_off (all required) --, the slab and record placement (for the data> hex),
+ * the recvfrom source address, the receive time and (optional, NULL = unknown) TTL.
+ * Output: dev_line_off[i] = byte offset of record i's line, dev_line_off[n] = total bytes;
+ * the lines are written to dev_text only when the total fits text_cap (read
+ * dev_line_off[n] and call again with a larger buffer otherwise).  No NUL terminator. */
+typedef struct {
+    uint8_t  type;      /* MgenMsg::AddressType: 1 IPv4, 2 IPv6 */
+    uint8_t  len;       /* address length (4 / 16) */
+    uint16_t port;
+    uint8_t  addr[16];  /* network byte order */
+} mgenx_addr;           /* 20 bytes */
+
+#define MGENX_PROTO_UDP  1   /* Protocol (include/mgenGlobals.h:61-68) */
+#define MGENX_PROTO_TCP  2
+#define MGENX_PROTO_SINK 3
+#define MGENX_LOG_EPOCH   0x1  /* Mgen::SetEpochTimestamp(true) */
+#define MGENX_LOG_NO_DATA 0x2  /* log_data off */
+#define MGENX_LOG_NO_GPS  0x4  /* log_gps_data off */
+
+int mgenx_log_recv_text(mgenx_ctx* ctx, const uint8_t* dev_slab, const uint64_t* dev_rec_off,
+                        uint64_t stride, const mgenx_cols* cols, const mgenx_addr* dev_src,
+                        const uint32_t* dev_rx_sec, const uint32_t* dev_rx_usec,
+                        const int32_t* dev_ttl, uint32_t n, int protocol, uint32_t opts,
+                        char* dev_text, uint64_t text_cap, uint64_t* dev_line_off, void* stream);
+
 /* Tuning knobs (per context; for benchmarking kernel variants).  MGENX_TUNE_UNPACK_VARIANT:
  * 0 = automatic (pipelined fixed-length kernel when the batch qualifies), 1/2 = ablations
  * of the general kernel (loads+XOR only / lookups on cached rows), 3 = general kernel,

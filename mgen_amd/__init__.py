@@ -25,7 +25,7 @@ LIB_PATH = os.path.join(HERE, "libmgenx.so")
 EXPORTED_SYMBOLS = (
     "mgenx_abi_version", "mgenx_ctx_create", "mgenx_ctx_destroy", "mgenx_last_error",
     "mgenx_unpack_batch", "mgenx_pack_prepare", "mgenx_set_fill_time", "mgenx_pack_batch",
-    "mgenx_crc32_batch", "mgenx_set_tuning", "mgenx_diag_stream_read", "mgenx_diag_group_rw", "mgenx_stream_scan", "mgenx_flow_reduce",
+    "mgenx_crc32_batch", "mgenx_set_tuning", "mgenx_diag_stream_read", "mgenx_diag_group_rw", "mgenx_log_recv_text", "mgenx_stream_scan", "mgenx_flow_reduce",
 )
 
 
@@ -64,6 +64,8 @@ def load():
     L.mgenx_flow_init.argtypes = [P, P, u32, ctypes.c_double, P]
     L.mgenx_flow_reduce.argtypes = [P, P, P, P, P, P, P, P, u32, P, u32, P, u32, P, P]
     L.mgenx_flow_export.argtypes = [P, P, u32, P, P]
+    L.mgenx_log_recv_text.argtypes = [P, P, P, u64, ctypes.POINTER(MgenxCols), P, P, P, P, u32,
+                                      i32, u32, P, u64, P, P]
     _lib = L
     return L
 
@@ -144,6 +146,31 @@ class Engine:
                                          _stream(self.device))
         self._check(rc, "mgenx_unpack_batch")
         return cols
+
+    # ------------------------------------------------------------ event log
+    def log_recv_text(self, slab, n, cols, src, rx_sec, rx_usec, *, rec_off=None, stride=0,
+                      ttl=None, protocol=1, opts=0, text_cap=None):
+        """RECV / RERR text log lines of n decoded records (mgenx_log_recv_text).  cols: the
+        unpack outputs with the extended columns; src: uint8 tensor of n x 20 (mgenx_addr).
+        Returns (text tensor, line offsets tensor of n + 1)."""
+        torch = self.torch
+        dev = slab.device
+        line_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        cap = text_cap if text_cap is not None else max(1, n) * 160
+        for _ in range(2):
+            text = torch.empty(max(cap, 1), dtype=torch.uint8, device=dev)
+            cs = self._cols_struct(cols)
+            rc = self.lib.mgenx_log_recv_text(self.ctx, _ptr(slab), _ptr(rec_off), stride,
+                                              ctypes.byref(cs), _ptr(src), _ptr(rx_sec),
+                                              _ptr(rx_usec), _ptr(ttl), n, protocol, opts,
+                                              _ptr(text), cap, _ptr(line_off),
+                                              _stream(self.device))
+            self._check(rc, "mgenx_log_recv_text")
+            total = int(line_off[n].item())
+            if total <= cap:
+                return text[:total], line_off
+            cap = total
+        raise MgenxError("mgenx_log_recv_text: text did not fit")
 
     # ------------------------------------------------------------ pack
     def pack_prepare(self, tmpl, n_tmpl, pool, tmpl_crc):

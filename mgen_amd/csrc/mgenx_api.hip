@@ -18,6 +18,15 @@ extern "C" int mgenx_scan_run(void* ws, const uint8_t* s, uint64_t nbytes, int m
                               uint64_t* rec_off, uint32_t* rec_len, uint64_t cap,
                               mgenx_scan_info* info, hipStream_t stream, char* err, size_t errn);
 
+extern "C" void* mgenx_log_ws_new();
+extern "C" void mgenx_log_ws_free(void* p);
+extern "C" int mgenx_log_recv_text_run(void* ws, const uint8_t* slab, const uint64_t* rec_off,
+                                       uint64_t stride, const mgenx_cols* cols,
+                                       const mgenx_addr* src, const uint32_t* rx_sec,
+                                       const uint32_t* rx_usec, const int32_t* ttl, uint32_t n,
+                                       int protocol, uint32_t opts, char* text,
+                                       uint64_t text_cap, uint64_t* line_off,
+                                       hipStream_t stream, char* err, size_t errn);
 extern "C" void* mgenx_flow_ws_new();
 extern "C" void mgenx_flow_ws_free(void* p);
 extern "C" int mgenx_flow_init_run(mgenx_flow_state* flows, uint32_t n_flows, double window,
@@ -46,6 +55,7 @@ struct mgenx_ctx {
   uint8_t* d_sink = nullptr;      // 1 KiB: column stores of lanes past the batch end
   void* scan_ws = nullptr;        // stream-scan workspace (mgenx_scan.hip), grown on demand
   void* flow_ws = nullptr;        // flow-reduce workspace (mgenx_analytic.hip), grown on demand
+  void* log_ws = nullptr;         // log-format workspace (mgenx_log.hip), grown on demand
   int unpack_variant = 0;          // diagnostic kernel ablation (mgenx_set_tuning)
   int pack_variant = 0;
   bool rand_ready = false;
@@ -180,6 +190,7 @@ int mgenx_ctx_destroy(mgenx_ctx* c) {
                 c->d_sink};
   if (c->scan_ws) mgenx_scan_ws_free(c->scan_ws);
   if (c->flow_ws) mgenx_flow_ws_free(c->flow_ws);
+  if (c->log_ws) mgenx_log_ws_free(c->log_ws);
   for (void* p : ps)
     if (p) hipFree(p);
   delete c;
@@ -362,6 +373,32 @@ int mgenx_flow_reduce(mgenx_ctx* ctx, const uint32_t* dev_flow_idx, const uint32
                                dev_msg_len, dev_rx_sec, dev_rx_usec, n, dev_flows, n_flows,
                                dev_reports, per_flow, dev_report_count, (hipStream_t)stream,
                                ctx->err, sizeof(ctx->err));
+}
+
+int mgenx_log_recv_text(mgenx_ctx* ctx, const uint8_t* dev_slab, const uint64_t* dev_rec_off,
+                        uint64_t stride, const mgenx_cols* cols, const mgenx_addr* dev_src,
+                        const uint32_t* dev_rx_sec, const uint32_t* dev_rx_usec,
+                        const int32_t* dev_ttl, uint32_t n, int protocol, uint32_t opts,
+                        char* dev_text, uint64_t text_cap, uint64_t* dev_line_off,
+                        void* stream) {
+  if (!ctx || !cols || !dev_line_off) return MGENX_EINVAL;
+  if (n == 0) return hipMemsetAsync(dev_line_off, 0, 8, (hipStream_t)stream) == hipSuccess
+                         ? MGENX_OK : MGENX_EDEVICE;
+  const mgenx_cols& k = *cols;
+  const bool core = k.rows || (k.flow_id && k.seq_num && k.tx_sec && k.tx_usec && k.msg_len &&
+                               k.dst_port && k.flags && k.err && k.dst_type && k.dst_len &&
+                               k.payload_len && k.payload_type && k.gps_status);
+  const bool ext = k.dst_addr && k.host_addr && k.host_port && k.host_type && k.host_len &&
+                   k.lat_raw && k.lon_raw && k.alt && k.payload_off;
+  if (!core || !ext || !dev_slab || !dev_src || !dev_rx_sec || !dev_rx_usec ||
+      (!dev_rec_off && stride == 0 && n > 1) || (text_cap && !dev_text) || n > 0x7FFFFFFEu)
+    return MGENX_EINVAL;
+  hipSetDevice(ctx->device);
+  if (!ctx->log_ws) ctx->log_ws = mgenx_log_ws_new();
+  return mgenx_log_recv_text_run(ctx->log_ws, dev_slab, dev_rec_off, stride, cols, dev_src,
+                                 dev_rx_sec, dev_rx_usec, dev_ttl, n, protocol, opts, dev_text,
+                                 text_cap, dev_line_off, (hipStream_t)stream, ctx->err,
+                                 sizeof(ctx->err));
 }
 
 int mgenx_flow_export(mgenx_ctx* ctx, const mgenx_flow_state* dev_flows, uint32_t n_flows,

@@ -1,3 +1,4 @@
+#define _GNU_SOURCE 1  /* gmtime_r, inet_ntop under -std=c11 */
 /*
  * mgen_oracle.c -- TEST INFRASTRUCTURE ONLY (the checker, never the product).
  *
@@ -947,4 +948,111 @@ uint32_t or_sizeof(int which)
         case 3: return (uint32_t)sizeof(or_analytic);
         default: return 0;
     }
+}
+
+/* ------------------------------------------------------------------ */
+/* RECV / RERR text log lines                                          */
+/*   MgenMsg::LogRecvEvent text branch  mgenMsg.cpp:1034-1102          */
+/*   MgenMsg::LogRecvError text branch  mgenMsg.cpp:711-735            */
+/*   Mgen::LogLegacyTimestamp / LogEpochTimestamp  mgen.cpp:55-83      */
+/* as glibc formats the reference's fprintf calls on x86-64.  Two ABI  */
+/* details are pinned by the doc's own output (doc/mgen.xml:2948):     */
+/* "%ld" of the INT32 altitude receives it zero-extended (-999 prints  */
+/* as 4294966297), and hex payload digits are upper case.              */
+/* ProtoAddress::GetHostString (protolib, absent) is taken as          */
+/* inet_ntop: "dotted decimal IPv4 addresses or colon-delimited IPv6   */
+/* addresses" (doc/mgen.xml:3674-3675) -- unpinned beyond IPv4.        */
+/* ------------------------------------------------------------------ */
+#include <arpa/inet.h>
+#include <stdio.h>
+#include <time.h>
+
+static int log_ts(char* out, uint32_t sec, uint32_t usec, int epoch)
+{
+    if (epoch) return sprintf(out, "%lu.%06lu ", (unsigned long)sec, (unsigned long)usec);
+    time_t t = (time_t)sec;
+    struct tm tmv;
+    gmtime_r(&t, &tmv);
+    return sprintf(out, "%02d:%02d:%02d.%06lu ", tmv.tm_hour, tmv.tm_min, tmv.tm_sec,
+                   (unsigned long)usec);
+}
+
+static int log_addr(char* out, uint8_t type, uint8_t len, const uint8_t* addr)
+{
+    char s[64];
+    if (type == OR_ADDR_IPV6 && len == 16) inet_ntop(AF_INET6, addr, s, sizeof s);
+    else if (type == OR_ADDR_IPV4 && len == 4) inet_ntop(AF_INET, addr, s, sizeof s);
+    else strcpy(s, "(invalid)");   /* protolib behaviour for other lengths: unpinned */
+    return sprintf(out, "%s", s);
+}
+
+static const char* log_proto(int protocol)
+{
+    switch (protocol) {   /* MgenBaseEvent::PROTOCOL_LIST, mgenEvent.cpp:75-81, 116-126 */
+        case 1: return "UDP";
+        case 2: return "TCP";
+        case 3: return "SINK";
+        default: return "UNKNOWN";
+    }
+}
+
+uint32_t or_log_recv_text(const or_fields* f, const uint8_t* rec, const or_addr* src,
+                          uint32_t rx_sec, uint32_t rx_usec, int protocol, int ttl,
+                          uint32_t opts, char* out)
+{
+    const int epoch = (opts & OR_LOG_EPOCH) != 0;
+    char* p = out;
+    if (!f->ok || f->err) {          /* RERR (mgenTransport.cpp:976-979, 990-994) */
+        static const char* names[5] = {"none", "version", "checksum", "length", "dstAddr"};
+        p += log_ts(p, rx_sec, rx_usec, epoch);
+        p += sprintf(p, "RERR type>%s src>", f->err <= 4 ? names[f->err] : "");
+        p += log_addr(p, src->type, src->len, src->addr);
+        p += sprintf(p, "/%hu\n", src->port);
+        return (uint32_t)(p - out);
+    }
+    p += log_ts(p, rx_sec, rx_usec, epoch);
+    p += sprintf(p, "RECV proto>%s flow>%lu seq>%lu src>", log_proto(protocol),
+                 (unsigned long)f->flow_id, (unsigned long)f->seq_num);
+    p += log_addr(p, src->type, src->len, src->addr);
+    p += sprintf(p, "/%hu dst>", src->port);
+    p += log_addr(p, f->dst_type, f->dst_len, f->dst_addr);
+    p += sprintf(p, "/%hu sent>", f->dst_port);
+    p += log_ts(p, f->tx_sec, f->tx_usec, epoch);
+    p += sprintf(p, "size>%u ", (unsigned)f->msg_len);
+    if (f->host_type == OR_ADDR_IPV4 || f->host_type == OR_ADDR_IPV6) {
+        p += sprintf(p, "host>");
+        p += log_addr(p, f->host_type, f->host_len, f->host_addr);
+        p += sprintf(p, "/%hu ", f->host_port);
+    }
+    if (ttl >= 0) p += sprintf(p, "ttl>%d ", ttl);
+    const char* status;
+    switch (f->gps_status) {
+        case 0: status = "INVALID"; break;
+        case 1: status = "STALE"; break;
+        case 2: status = "CURRENT"; break;
+        default:                      /* mgenMsg.cpp:1068-1071: newline, nothing more */
+            p += sprintf(p, "\n");
+            return (uint32_t)(p - out);
+    }
+    if (!(opts & OR_LOG_NO_GPS)) {
+        const double lat = ((double)f->lat_raw) / 60000.0 - 180.0;   /* mgenMsg.cpp:453 */
+        const double lon = ((double)f->lon_raw) / 60000.0 - 180.0;   /* mgenMsg.cpp:457 */
+        p += sprintf(p, "gps>%s,%f,%f,%lu ", status, lat, lon,
+                     (unsigned long)(uint32_t)f->alt);
+    }
+    if (f->payload_len && !(opts & OR_LOG_NO_DATA) && f->payload_type == 0) {  /* USER_DATA */
+        static const char hx[] = "0123456789ABCDEF";   /* MgenPayload::toHex */
+        p += sprintf(p, "data>%hu:", f->payload_len);
+        const uint8_t* d = rec + f->payload_off;          /* payload_data (word floor) */
+        for (uint32_t i = 0; i < f->payload_len; i++) {
+            *p++ = hx[d[i] >> 4];
+            *p++ = hx[d[i] & 15];
+        }
+        *p++ = ' ';
+    }
+    if (f->flags & OR_FLAG_CONTINUES) p += sprintf(p, "flags>0x%02x ", OR_FLAG_CONTINUES);
+    if (f->flags & OR_FLAG_END_OF_MSG) p += sprintf(p, "flags>0x%02x ", OR_FLAG_END_OF_MSG);
+    if (f->flags & OR_FLAG_CHECKSUM_ERROR) p += sprintf(p, "flags>0x%02x ", OR_FLAG_CHECKSUM_ERROR);
+    p += sprintf(p, "\n");
+    return (uint32_t)(p - out);
 }

@@ -236,6 +236,15 @@ uint64_t or_tcp_tx_batch(const or_tmpl* tmpl, const or_desc* desc, const uint32_
 
 uint32_t or_sizeof(int which);
 
+/* ---- RECV / RERR text log lines (MgenMsg::LogRecvEvent / LogRecvError text form,
+ * mgenMsg.cpp:711-735, 1034-1102; timestamps mgen.cpp:55-83).  f = the record after the
+ * receive path (Unpack + CRC check); rec = its bytes (for the data> field); src = recvfrom's
+ * source; ttl < 0 = unknown.  Writes the line(s) to out (no NUL), returns the length. ---- */
+enum { OR_LOG_EPOCH = 0x1, OR_LOG_NO_DATA = 0x2, OR_LOG_NO_GPS = 0x4 };
+uint32_t or_log_recv_text(const or_fields* f, const uint8_t* rec, const or_addr* src,
+                          uint32_t rx_sec, uint32_t rx_usec, int protocol, int ttl,
+                          uint32_t opts, char* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -132,6 +132,8 @@ def lib():
         L.or_time_delta.argtypes = [Time, Time]
         L.or_time_delta.restype = ctypes.c_double
         L.or_flow_reduce_batch.argtypes = [P, u32, P, P, P, P, P, P, P, u32, P, u32, P]
+        L.or_log_recv_text.argtypes = [P, P, P, u32, u32, i32, i32, u32, P]
+        L.or_log_recv_text.restype = u32
         L.or_sizeof.argtypes = [i32]
         L.or_sizeof.restype = u32
         assert L.or_sizeof(0) == TMPL_DTYPE.itemsize, "or_tmpl layout mismatch"
@@ -352,3 +354,29 @@ def flow_reduce_batch(n_flows, flow_idx, seq, tx_sec, tx_usec, msg_len, rx_sec, 
     lib().or_flow_reduce_batch(flows, n_flows, *[_ptr(c) for c in cols], n, _ptr(reports),
                                per_flow, _ptr(counts))
     return flows, reports.reshape(n_flows, max(per_flow, 1)), counts
+
+
+# ---------------------------------------------------------------- event log
+ADDR_DTYPE = np.dtype([("type", "u1"), ("len", "u1"), ("port", "<u2"), ("addr", "u1", 16)])
+LOG_EPOCH, LOG_NO_DATA, LOG_NO_GPS = 0x1, 0x2, 0x4
+
+
+def log_recv_text(fields, slab, rec_off, src, rx_sec, rx_usec, protocol=1, ttl=None, opts=0):
+    """MgenMsg::LogRecvEvent / LogRecvError text lines for n received records (or_fields
+    array `fields`, record i at slab[rec_off[i]:]); src: ADDR_DTYPE array; ttl: int array
+    or None (unknown).  Returns the concatenated log bytes."""
+    L = lib()
+    slab = np.ascontiguousarray(slab, np.uint8)
+    fields = np.ascontiguousarray(fields)
+    src = np.ascontiguousarray(src, ADDR_DTYPE)
+    out = []
+    buf = np.zeros(65536 * 2 + 1024, np.uint8)
+    base = slab.ctypes.data
+    for i in range(len(fields)):
+        n = L.or_log_recv_text(ctypes.c_void_p(fields.ctypes.data + i * fields.itemsize),
+                               ctypes.c_void_p(base + int(rec_off[i])),
+                               ctypes.c_void_p(src.ctypes.data + i * src.itemsize),
+                               int(rx_sec[i]), int(rx_usec[i]), protocol,
+                               -1 if ttl is None else int(ttl[i]), opts, _ptr(buf))
+        out.append(buf[:n].tobytes())
+    return b"".join(out)

@@ -1,0 +1,137 @@
+"""GPU parity of mgenx_log_recv_text (MgenMsg::LogRecvEvent / LogRecvError text lines)
+against the oracle restatement, which itself reproduces the reference's printed output
+(tests/test_log_cpu.py).  Inputs: the golden unpack matrix decoded on the GPU (every error
+class, truncated headers, IPv4/IPv6 dst and host, GPS values, payloads), with varied source
+addresses, receive times and TTLs; byte-exact, every option combination."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+GOLD = "tests/golden/udp_matrix.npz"
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    return torch
+
+
+@pytest.fixture(scope="module")
+def eng(torch):
+    from mgen_amd import Engine
+    e = Engine(0)
+    yield e
+    e.close()
+
+
+@pytest.fixture(scope="module")
+def gold():
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    return dict(np.load(os.path.join(root, GOLD), allow_pickle=False))
+
+
+def _sources(oracle, n, rng):
+    src = np.zeros(n, oracle.ADDR_DTYPE)
+    v6 = rng.random(n) < 0.3
+    src["type"] = np.where(v6, 2, 1)
+    src["len"] = np.where(v6, 16, 4)
+    src["port"] = rng.integers(0, 65536, n)
+    src["addr"] = rng.integers(0, 256, (n, 16))
+    # IPv6 shapes inet_ntop treats specially: zero runs, ::1, IPv4-mapped / -compatible
+    k = np.nonzero(v6)[0]
+    for j, i in enumerate(k):
+        a = src["addr"][i]
+        kind = j % 6
+        if kind == 0:
+            a[:] = 0; a[15] = 1                               # ::1
+        elif kind == 1:
+            a[:10] = 0; a[10:12] = 0xFF                        # ::ffff:a.b.c.d
+        elif kind == 2:
+            a[:12] = 0                                        # ::a.b.c.d
+        elif kind == 3:
+            a[2:8] = 0                                        # x::y
+        elif kind == 4:
+            a[4:6] = 0; a[10:14] = 0                          # two runs
+        src["addr"][i] = a
+    return src
+
+
+@pytest.mark.parametrize("mode,opts,proto", [("udp", 0, 1), ("udp_force", 0x1, 1),
+                                             ("tcp_force", 0x6, 2), ("udp", 0x7, 3)])
+def test_log_lines_match_oracle(torch, eng, gold, oracle, mode, opts, proto):
+    from mgen_amd import OPT_CHECKSUM_FORCE, OPT_TCP, to_device
+    uopts = {"udp": 0, "udp_force": OPT_CHECKSUM_FORCE, "tcp_force": OPT_TCP | OPT_CHECKSUM_FORCE}
+    n = len(gold["unpack_lens"])
+    slab = to_device(gold["unpack_slab"]).view(torch.uint8)
+    offs = to_device(gold["unpack_offs"]).view(torch.int64)
+    lens = to_device(gold["unpack_lens"]).view(torch.int32)
+    cols = eng.unpack(slab, n, rec_off=offs, rec_len=lens, opts=uopts[mode], ext=True)
+    rng = np.random.default_rng(17 + opts)
+    src = _sources(oracle, n, rng)
+    rx_sec = rng.integers(1_600_000_000, 1_800_000_000, n, dtype=np.int64).astype(np.uint32)
+    rx_usec = rng.integers(0, 1_000_000, n).astype(np.uint32)
+    ttl = rng.integers(-1, 256, n).astype(np.int32)
+    text, line_off = eng.log_recv_text(
+        slab, n, cols, to_device(src.view(np.uint8)), to_device(rx_sec), to_device(rx_usec),
+        rec_off=offs, ttl=to_device(ttl), protocol=proto, opts=opts)
+    got = text.cpu().numpy().tobytes()
+    want = oracle.log_recv_text(gold[f"unpack_fields_{mode}"], gold["unpack_slab"],
+                                gold["unpack_offs"], src, rx_sec, rx_usec, protocol=proto,
+                                ttl=ttl, opts=opts)
+    if got != want:
+        g, w = got.split(b"\n"), want.split(b"\n")
+        bad = [i for i in range(min(len(g), len(w))) if g[i] != w[i]][:3]
+        raise AssertionError([(g[i], w[i]) for i in bad] or (len(got), len(want)))
+    offs_h = line_off.cpu().numpy()
+    assert offs_h[0] == 0 and offs_h[-1] == len(want)
+
+
+def test_log_rows_input_and_gps_values(torch, eng, oracle):
+    """Row-major unpack output as the formatter's core input; GPS raw words across the whole
+    u32 range (the exactly rounded %f)."""
+    from mgen_amd import PACK_CHECKSUM, to_device
+    from mgen_amd._abi import TMPL_DTYPE, DESC_DTYPE
+    rng = np.random.default_rng(5)
+    n_t = 64
+    t = np.zeros(n_t, TMPL_DTYPE)
+    t["flow_id"] = np.arange(1, n_t + 1)
+    t["dst_type"], t["dst_len"], t["dst_port"] = 1, 4, 5000
+    t["dst_addr"][:, :4] = [10, 1, 2, 3]
+    raws = np.concatenate([[0, 1, 10800000, 10800001, 10799999, 70740000, 0xFFFFFFFF],
+                           rng.integers(0, 2**32, n_t - 7, dtype=np.uint64)]).astype(np.uint32)
+    t["lat_raw"] = raws
+    t["lon_raw"] = raws[::-1]
+    t["alt"] = rng.integers(-2**31, 2**31, n_t, dtype=np.int64).astype(np.int32)
+    t["gps_status"] = np.arange(n_t) % 3
+    n = 4096
+    d = np.zeros(n, DESC_DTYPE)
+    d["tmpl"] = np.arange(n) % n_t
+    d["seq_num"] = np.arange(n)
+    d["tx_sec"] = 1_700_000_000
+    d["tx_usec"] = rng.integers(0, 1_000_000, n)
+    d["msg_len"] = 256
+    pool = np.zeros(16, np.uint8)
+    dt, dp, dd = to_device(t), to_device(pool), to_device(d)
+    crc = torch.empty(n_t, dtype=torch.int32, device="cuda")
+    eng.pack_prepare(dt, n_t, dp, crc)
+    slab = torch.zeros(n * 256, dtype=torch.uint8, device="cuda")
+    eng.pack(dt, crc, dd, n, dp, slab, stride=256, opts=PACK_CHECKSUM)
+    from mgen_amd._abi import COLS_EXT
+    full = eng.alloc_cols(n, ext=True)
+    cols = {name: full[name] for name, _, _ in COLS_EXT}   # extended columns + core rows
+    cols["rows"] = eng.alloc_rows(n)
+    eng.unpack(slab, n, stride=256, fixed_len=256, cols=cols)
+    src = np.zeros(n, oracle.ADDR_DTYPE)
+    src["type"], src["len"], src["port"] = 1, 4, 40000
+    src["addr"][:, :4] = [192, 168, 0, 9]
+    rx_s = np.full(n, 1_700_000_001, np.uint32)
+    rx_u = np.arange(n, dtype=np.uint32)
+    text, _ = eng.log_recv_text(slab, n, cols, to_device(src.view(np.uint8)), to_device(rx_s),
+                                to_device(rx_u), stride=256)
+    h = slab.cpu().numpy()
+    f = oracle.udp_recv_batch(h, n, stride=256, fixed_len=256)
+    want = oracle.log_recv_text(f, h, np.arange(n, dtype=np.uint64) * 256, src, rx_s, rx_u)
+    assert text.cpu().numpy().tobytes() == want
