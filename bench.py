@@ -201,6 +201,28 @@ def extra_config5(torch, eng, dev):
             "unpack_gbps": round((b + n * 32) / ums / 1e6, 1), "candidates": int(info.candidates)}
 
 
+def extra_log(torch, eng, dev, slab):
+    """RECV event log lines (mgenx_log_recv_text) for the config-2 batch: the decoded records
+    (rows + extended columns) formatted as the reference's text log, GPU-resident."""
+    from mgen_amd._abi import COLS_EXT
+    full = eng.alloc_cols(N_REC, ext=True)
+    cols = {name: full[name] for name, _, _ in COLS_EXT}
+    cols["rows"] = eng.alloc_rows(N_REC)
+    eng.unpack(slab, N_REC, stride=REC, fixed_len=REC, cols=cols)
+    src = torch.zeros(N_REC, 20, dtype=torch.uint8, device=dev)
+    src[:, 0], src[:, 1], src[:, 2], src[:, 3] = 1, 4, 0x89, 0xE7    # IPv4 127.0.0.1/59273
+    src[:, 4], src[:, 7] = 127, 1
+    rx_s = torch.full((N_REC,), 1_700_000_001, dtype=torch.int32, device=dev)
+    rx_u = torch.arange(N_REC, dtype=torch.int32, device=dev) % 1_000_000
+    text, line_off = eng.log_recv_text(slab, N_REC, cols, src, rx_s, rx_u, stride=REC)
+    cap = text.numel()
+    ms = timed(torch, lambda: eng.log_recv_text(slab, N_REC, cols, src, rx_s, rx_u, stride=REC,
+                                                text_cap=cap), reps=5)
+    return {"records": N_REC, "text_bytes": cap, "ms": round(ms, 4),
+            "mlines_per_s": round(N_REC / ms / 1e3, 1),
+            "note": "two passes (length, write) + scan; includes one D2H read of the total"}
+
+
 def extra_pcie(torch, eng, dev, slab):
     """Config 2 from pinned host memory: 8 chunks of 128 MiB, two streams (copy of chunk
     k+1 overlaps the unpack of chunk k), core columns copied back.  Wall-clock GB/s of
@@ -369,6 +391,7 @@ def main():
             guard("config3_mixed_pack_unpack", lambda: extra_config3(torch, eng, dev))
             guard("config5_tcp_scan_unpack", lambda: extra_config5(torch, eng, dev))
             guard("pcie_inclusive_config2", lambda: extra_pcie(torch, eng, dev, slab))
+            guard("recv_log_text", lambda: extra_log(torch, eng, dev, slab))
 
     ms_per_step = elapsed / args.steps * 1e3
     value = world * ALGO_BYTES * args.steps / elapsed / 1e9

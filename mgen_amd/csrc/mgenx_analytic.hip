@@ -54,102 +54,104 @@ __device__ __forceinline__ bool tge(Tm a, Tm b) {
   return a.sec > b.sec || (a.sec == b.sec && a.usec >= b.usec);
 }
 
-// ProtoSlidingMask(1024) restated exactly as oracle/mgen_oracle.c (mask_*): a set of u32
-// indices with span < 1024, stored as bits relative to `first`.
-struct Mask {
+// ProtoSlidingMask(1024) with the semantics of oracle/mgen_oracle.c (mask_*): a set of u32
+// indices with span < 1024.  Kept as a 1024-bit RING (index s at bit s mod 1024) plus the
+// lowest (first) and highest (last) set index, so set / test are O(1) and nothing shifts;
+// the state array stores it relative to `first` (bit i <-> first + i), converted on entry
+// and exit.  (The shifting form scanned and moved 32 words whenever an index arrived below
+// `first` -- every reordered message after a window slide -- and dominated the kernel.)
+struct Ring {
   uint32_t* w;  // word k at w[k * kFlowThreads]
-  uint32_t first, n;
-  __device__ uint32_t& word(int k) { return w[k * kFlowThreads]; }
-  __device__ bool bit(uint32_t i) { return (word(i >> 5) >> (i & 31)) & 1u; }
-  __device__ void setbit(uint32_t i) { word(i >> 5) |= 1u << (i & 31); }
-  __device__ void clear() {
+  uint32_t first, last, n;
+  __device__ uint32_t& word(uint32_t k) { return w[(k & 31u) * kFlowThreads]; }
+  __device__ bool bit(uint32_t s) { return (word(s >> 5 & 31u) >> (s & 31u)) & 1u; }
+  __device__ void setbit(uint32_t s) { word(s >> 5 & 31u) |= 1u << (s & 31u); }
+  __device__ void clear() {  // `first` is kept (stale), as the restatement keeps it
     for (int k = 0; k < 32; k++) word(k) = 0;
     n = 0;
   }
-  __device__ uint32_t last() {
-    for (int k = 31; k >= 0; k--) {
-      const uint32_t x = word(k);
-      if (x) return first + 32u * k + (31u - __clz(x));
-    }
-    return first;
-  }
+  __device__ uint32_t get_last() { return n ? last : first; }
   __device__ bool test(uint32_t idx) {
     if (!n) return false;
     const int32_t d = (int32_t)(idx - first);
     if (d < 0 || (uint32_t)d >= kDepth) return false;
-    return bit((uint32_t)d);
-  }
-  // bits move up by s (bit i -> i + s; bits shifted past the top are dropped)
-  __device__ void shift_up(uint32_t s) {
-    const int ws = (int)(s >> 5), bs = (int)(s & 31);
-    for (int k = 31; k >= 0; k--) {
-      const int hi = k - ws, lo = k - ws - 1;
-      uint32_t v = hi >= 0 ? word(hi) << bs : 0u;
-      if (bs && lo >= 0) v |= word(lo) >> (32 - bs);
-      word(k) = v;
-    }
-  }
-  // bits move down by s (bit i -> i - s)
-  __device__ void shift_down(uint32_t s) {
-    const int ws = (int)(s >> 5), bs = (int)(s & 31);
-    for (int k = 0; k < 32; k++) {
-      const int lo = k + ws, hi = k + ws + 1;
-      uint32_t v = lo < 32 ? word(lo) >> bs : 0u;
-      if (bs && hi < 32) v |= word(hi) << (32 - bs);
-      word(k) = v;
-    }
+    return bit(idx);
   }
   __device__ bool set(uint32_t idx) {
     if (!n) {
       clear();
-      first = idx;
-      setbit(0);
+      first = last = idx;
+      setbit(idx);
       n = 1;
       return true;
     }
     const int32_t d = (int32_t)(idx - first);
     if (d >= 0) {
       if ((uint32_t)d >= kDepth) return false;
-      if (!bit((uint32_t)d)) { setbit((uint32_t)d); n++; }
+      if (!bit(idx)) {
+        setbit(idx);
+        n++;
+        if ((uint32_t)d > last - first) last = idx;
+      }
       return true;
     }
-    const uint32_t span = last() - idx;  // precedes first: allowed while span < depth
-    if (span >= kDepth) return false;
-    shift_up((uint32_t)(-d));
+    if (last - idx >= kDepth) return false;  // precedes first: allowed while span < depth
+    setbit(idx);
     first = idx;
-    setbit(0);
     n++;
     return true;
   }
-  // clear every set index x with (x - idx) mod 2^32 < count, then re-base on the first set
-  __device__ void unset_bits(uint32_t idx, uint32_t count) {
+  // clear indices first .. first + count - 1, then re-base `first` on the lowest left
+  __device__ void unset_from_first(uint32_t count) {
     if (!n) return;
-    const uint32_t a = idx - first;
-    for (int k = 0; k < 32; k++) {
-      uint32_t x = word(k);
-      if (!x) continue;
-      uint32_t clr = 0;
-      if (a == 0) {  // the only form Update uses: bits [0, count)
-        const uint64_t lo = 32u * k;
-        if ((uint64_t)count >= lo + 32) clr = x;
-        else if ((uint64_t)count > lo) clr = x & ((1u << (count - (uint32_t)lo)) - 1u);
-      } else {
-        for (int b = 0; b < 32; b++)
-          if (((x >> b) & 1u) && (uint32_t)(32u * k + b - a) < count) clr |= 1u << b;
+    if ((uint64_t)count > (uint64_t)(last - first)) {
+      clear();
+      return;
+    }
+    uint32_t s = first;
+    uint32_t left = count;
+    while (left) {
+      const uint32_t b = s & 31u, take = min(32u - b, left);
+      const uint32_t m = (take == 32u ? 0xFFFFFFFFu : ((1u << take) - 1u)) << b;
+      uint32_t& x = word(s >> 5 & 31u);
+      n -= __popc(x & m);
+      x &= ~m;
+      s += take;
+      left -= take;
+    }
+    // lowest set index at or after s (last is still set)
+    for (;;) {
+      const uint32_t b = s & 31u;
+      const uint32_t x = word(s >> 5 & 31u) >> b;
+      if (x) {
+        first = s + (uint32_t)(__ffs(x) - 1);
+        return;
       }
-      word(k) = x & ~clr;
-      n -= __popc(clr);
+      s += 32u - b;
     }
-    if (!n) { clear(); return; }
-    uint32_t s = 0;
-    for (int k = 0; k < 32; k++) {
-      const uint32_t x = word(k);
-      if (x) { s = 32u * k + __ffs(x) - 1; break; }
+  }
+  // relative form (bit i of words rel <-> first + i) <-> ring
+  __device__ void load_relative(const uint32_t* rel) {
+    for (int k = 0; k < 32; k++) word(k) = 0;
+    const uint32_t fs = first & 1023u, fw = fs >> 5, bs = fs & 31u;
+    for (uint32_t k = 0; k < 32; k++) {
+      const uint32_t v = rel[k];
+      word(fw + k) |= v << bs;
+      if (bs) word(fw + k + 1) |= v >> (32u - bs);
     }
-    if (s) {
-      shift_down(s);
-      first += s;
+    last = first;
+    for (int k = 31; k >= 0; k--)
+      if (rel[k]) { last = first + 32u * k + (31u - __clz(rel[k])); break; }
+  }
+  __device__ void store_relative(uint32_t* rel) {
+    const uint32_t fs = first & 1023u, fw = fs >> 5, bs = fs & 31u;
+    for (uint32_t k = 0; k < 32; k++) {
+      uint32_t v = word(fw + k) >> bs;
+      if (bs) v |= word(fw + k + 1) << (32u - bs);
+      rel[k] = n ? v : 0u;
     }
+    if (!n) return;
+    // bits of the ring that lie past `last` (none: the span is < 1024) stay zero
   }
 };
 
@@ -171,11 +173,11 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
   const uint32_t b = begin[f], e = end[f];
   if (b >= e) return;
   mgenx_flow_state st = flows[f];
-  Mask m;
+  Ring m;
   m.w = lds + threadIdx.x;
-  for (int k = 0; k < 32; k++) m.word(k) = st.mask[k];
   m.first = st.mask_first;
   m.n = st.mask_n;
+  m.load_relative(flows[f].mask);  // straight from memory: no 128-B local copy
   bool valid = st.window_valid != 0;
   Tm ws = {st.win_start_sec, st.win_start_usec}, we = {st.win_end_sec, st.win_end_usec};
   uint32_t seq_start = st.seq_start;
@@ -211,9 +213,8 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
         } else if ((int32_t)(r.seq - seq_start) < 0) {
           m.set(r.seq);
         } else {
-          if (!m.set(r.seq)) {
-            const uint32_t first_set = m.first;
-            m.unset_bits(first_set, r.seq - first_set);
+          if (!m.set(r.seq)) {  // UnsetBits(first, seq - first), then Set (:120-127)
+            m.unset_from_first(r.seq - m.first);
             m.set(r.seq);
           }
           if (1 == msg_count) byte_count = msg;
@@ -246,7 +247,7 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
       rep.duration = tdelta(rx, ws);
       rep.rx_sec = rx.sec;
       rep.rx_usec = rx.usec;
-      const uint32_t seq_max = m.n ? m.last() : seq_start;
+      const uint32_t seq_max = m.n ? m.get_last() : seq_start;
       if (msg_count == 0) {
         rep.msg_count = 0;
         rep.rate = 0.0;
@@ -299,7 +300,7 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
       if (i0 + k < e) update(r[k]);
   }
 
-  for (int k = 0; k < 32; k++) st.mask[k] = m.word(k);
+  m.store_relative(flows[f].mask);
   st.mask_first = m.first;
   st.mask_n = m.n;
   st.window_valid = valid ? 1u : 0u;
@@ -315,7 +316,14 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
   st.latency_min = lmin;
   st.latency_max = lmax;
   st.n_reports = nrep;
-  flows[f] = st;
+  // scalar fields back (the mask words were written in place above)
+  mgenx_flow_state& o = flows[f];
+  o.mask_first = st.mask_first; o.mask_n = st.mask_n; o.seq_start = st.seq_start;
+  o.window_valid = st.window_valid; o.win_start_sec = st.win_start_sec;
+  o.win_start_usec = st.win_start_usec; o.win_end_sec = st.win_end_sec;
+  o.win_end_usec = st.win_end_usec; o.msg_count = st.msg_count; o.byte_count = st.byte_count;
+  o.dup_count = st.dup_count; o.latency_sum = st.latency_sum; o.latency_min = st.latency_min;
+  o.latency_max = st.latency_max; o.n_reports = st.n_reports;
   report_count[f] = rcount;
 }
 
