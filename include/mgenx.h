@@ -295,6 +295,20 @@ int mgenx_log_recv_text(mgenx_ctx* ctx, const uint8_t* dev_slab, const uint64_t*
                         const uint32_t* dev_rx_sec, const uint32_t* dev_rx_usec,
                         const int32_t* dev_ttl, uint32_t n, int protocol, uint32_t opts,
                         char* dev_text, uint64_t text_cap, uint64_t* dev_line_off, void* stream);
+/* The binary log form of the same events (MgenMsg::LogRecvEvent / LogRecvError binary
+ * branches, src/common/mgenMsg.cpp:652-710, 958-1033): per record an event header (type,
+ * protocol, BE length, BE rx time, BE source port, source type/length/address) followed, for
+ * RECV, by hdr_len + payload_len + 2 message bytes with CHECKSUM cleared in the flags byte
+ * (the hdr_len extended column is also required); RERR ends with the BE error code.
+ * Message bytes past slab_bytes are written as zero (the reference's stale receive buffer).
+ * dev_rec_pos has the same meaning as dev_line_off.  The file header line the reference
+ * writes once per log file is the caller's. */
+int mgenx_log_recv_binary(mgenx_ctx* ctx, const uint8_t* dev_slab, uint64_t slab_bytes,
+                          const uint64_t* dev_rec_off, uint64_t stride, const mgenx_cols* cols,
+                          const mgenx_addr* dev_src, const uint32_t* dev_rx_sec,
+                          const uint32_t* dev_rx_usec, uint32_t n, int protocol,
+                          uint8_t* dev_out, uint64_t out_cap, uint64_t* dev_rec_pos,
+                          void* stream);
 
 /* Tuning knobs (per context; for benchmarking kernel variants).  MGENX_TUNE_UNPACK_VARIANT:
  * 0 = automatic (pipelined fixed-length kernel when the batch qualifies), 1/2 = ablations

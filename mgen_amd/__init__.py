@@ -25,7 +25,7 @@ LIB_PATH = os.path.join(HERE, "libmgenx.so")
 EXPORTED_SYMBOLS = (
     "mgenx_abi_version", "mgenx_ctx_create", "mgenx_ctx_destroy", "mgenx_last_error",
     "mgenx_unpack_batch", "mgenx_pack_prepare", "mgenx_set_fill_time", "mgenx_pack_batch",
-    "mgenx_crc32_batch", "mgenx_set_tuning", "mgenx_diag_stream_read", "mgenx_diag_group_rw", "mgenx_log_recv_text", "mgenx_stream_scan", "mgenx_flow_reduce",
+    "mgenx_crc32_batch", "mgenx_set_tuning", "mgenx_diag_stream_read", "mgenx_diag_group_rw", "mgenx_log_recv_text", "mgenx_log_recv_binary", "mgenx_stream_scan", "mgenx_flow_reduce",
 )
 
 
@@ -66,6 +66,8 @@ def load():
     L.mgenx_flow_export.argtypes = [P, P, u32, P, P]
     L.mgenx_log_recv_text.argtypes = [P, P, P, u64, ctypes.POINTER(MgenxCols), P, P, P, P, u32,
                                       i32, u32, P, u64, P, P]
+    L.mgenx_log_recv_binary.argtypes = [P, P, u64, P, u64, ctypes.POINTER(MgenxCols), P, P, P,
+                                        u32, i32, P, u64, P, P]
     _lib = L
     return L
 
@@ -171,6 +173,29 @@ class Engine:
                 return text[:total], line_off
             cap = total
         raise MgenxError("mgenx_log_recv_text: text did not fit")
+
+    def log_recv_binary(self, slab, n, cols, src, rx_sec, rx_usec, *, rec_off=None, stride=0,
+                        protocol=1, slab_bytes=None, cap=None):
+        """Binary RECV / RERR log records (mgenx_log_recv_binary).  Returns (bytes tensor,
+        record positions tensor of n + 1)."""
+        torch = self.torch
+        dev = slab.device
+        pos = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        cap = cap if cap is not None else max(1, n) * 128
+        sb = slab.numel() if slab_bytes is None else slab_bytes
+        for _ in range(2):
+            out = torch.empty(max(cap, 1), dtype=torch.uint8, device=dev)
+            cs = self._cols_struct(cols)
+            rc = self.lib.mgenx_log_recv_binary(self.ctx, _ptr(slab), sb, _ptr(rec_off), stride,
+                                                ctypes.byref(cs), _ptr(src), _ptr(rx_sec),
+                                                _ptr(rx_usec), n, protocol, _ptr(out), cap,
+                                                _ptr(pos), _stream(self.device))
+            self._check(rc, "mgenx_log_recv_binary")
+            total = int(pos[n].item())
+            if total <= cap:
+                return out[:total], pos
+            cap = total
+        raise MgenxError("mgenx_log_recv_binary: output did not fit")
 
     # ------------------------------------------------------------ pack
     def pack_prepare(self, tmpl, n_tmpl, pool, tmpl_crc):

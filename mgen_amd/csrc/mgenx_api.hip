@@ -20,7 +20,8 @@ extern "C" int mgenx_scan_run(void* ws, const uint8_t* s, uint64_t nbytes, int m
 
 extern "C" void* mgenx_log_ws_new();
 extern "C" void mgenx_log_ws_free(void* p);
-extern "C" int mgenx_log_recv_text_run(void* ws, const uint8_t* slab, const uint64_t* rec_off,
+extern "C" int mgenx_log_recv_run(void* ws, bool binary, const uint8_t* slab,
+                                  uint64_t slab_bytes, const uint64_t* rec_off,
                                        uint64_t stride, const mgenx_cols* cols,
                                        const mgenx_addr* src, const uint32_t* rx_sec,
                                        const uint32_t* rx_usec, const int32_t* ttl, uint32_t n,
@@ -375,12 +376,12 @@ int mgenx_flow_reduce(mgenx_ctx* ctx, const uint32_t* dev_flow_idx, const uint32
                                ctx->err, sizeof(ctx->err));
 }
 
-int mgenx_log_recv_text(mgenx_ctx* ctx, const uint8_t* dev_slab, const uint64_t* dev_rec_off,
-                        uint64_t stride, const mgenx_cols* cols, const mgenx_addr* dev_src,
-                        const uint32_t* dev_rx_sec, const uint32_t* dev_rx_usec,
-                        const int32_t* dev_ttl, uint32_t n, int protocol, uint32_t opts,
-                        char* dev_text, uint64_t text_cap, uint64_t* dev_line_off,
-                        void* stream) {
+static int log_recv(mgenx_ctx* ctx, bool binary, const uint8_t* dev_slab, uint64_t slab_bytes,
+                    const uint64_t* dev_rec_off, uint64_t stride, const mgenx_cols* cols,
+                    const mgenx_addr* dev_src, const uint32_t* dev_rx_sec,
+                    const uint32_t* dev_rx_usec, const int32_t* dev_ttl, uint32_t n,
+                    int protocol, uint32_t opts, char* dev_text, uint64_t text_cap,
+                    uint64_t* dev_line_off, void* stream) {
   if (!ctx || !cols || !dev_line_off) return MGENX_EINVAL;
   if (n == 0) return hipMemsetAsync(dev_line_off, 0, 8, (hipStream_t)stream) == hipSuccess
                          ? MGENX_OK : MGENX_EDEVICE;
@@ -389,16 +390,38 @@ int mgenx_log_recv_text(mgenx_ctx* ctx, const uint8_t* dev_slab, const uint64_t*
                                k.dst_port && k.flags && k.err && k.dst_type && k.dst_len &&
                                k.payload_len && k.payload_type && k.gps_status);
   const bool ext = k.dst_addr && k.host_addr && k.host_port && k.host_type && k.host_len &&
-                   k.lat_raw && k.lon_raw && k.alt && k.payload_off;
+                   k.lat_raw && k.lon_raw && k.alt && k.payload_off && (!binary || k.hdr_len);
   if (!core || !ext || !dev_slab || !dev_src || !dev_rx_sec || !dev_rx_usec ||
       (!dev_rec_off && stride == 0 && n > 1) || (text_cap && !dev_text) || n > 0x7FFFFFFEu)
     return MGENX_EINVAL;
   hipSetDevice(ctx->device);
   if (!ctx->log_ws) ctx->log_ws = mgenx_log_ws_new();
-  return mgenx_log_recv_text_run(ctx->log_ws, dev_slab, dev_rec_off, stride, cols, dev_src,
-                                 dev_rx_sec, dev_rx_usec, dev_ttl, n, protocol, opts, dev_text,
-                                 text_cap, dev_line_off, (hipStream_t)stream, ctx->err,
-                                 sizeof(ctx->err));
+  return mgenx_log_recv_run(ctx->log_ws, binary, dev_slab, slab_bytes, dev_rec_off, stride, cols,
+                            dev_src, dev_rx_sec, dev_rx_usec, dev_ttl, n, protocol, opts,
+                            dev_text, text_cap, dev_line_off, (hipStream_t)stream, ctx->err,
+                            sizeof(ctx->err));
+}
+
+int mgenx_log_recv_text(mgenx_ctx* ctx, const uint8_t* dev_slab, const uint64_t* dev_rec_off,
+                        uint64_t stride, const mgenx_cols* cols, const mgenx_addr* dev_src,
+                        const uint32_t* dev_rx_sec, const uint32_t* dev_rx_usec,
+                        const int32_t* dev_ttl, uint32_t n, int protocol, uint32_t opts,
+                        char* dev_text, uint64_t text_cap, uint64_t* dev_line_off,
+                        void* stream) {
+  return log_recv(ctx, false, dev_slab, ~0ull, dev_rec_off, stride, cols, dev_src, dev_rx_sec,
+                  dev_rx_usec, dev_ttl, n, protocol, opts, dev_text, text_cap, dev_line_off,
+                  stream);
+}
+
+int mgenx_log_recv_binary(mgenx_ctx* ctx, const uint8_t* dev_slab, uint64_t slab_bytes,
+                          const uint64_t* dev_rec_off, uint64_t stride, const mgenx_cols* cols,
+                          const mgenx_addr* dev_src, const uint32_t* dev_rx_sec,
+                          const uint32_t* dev_rx_usec, uint32_t n, int protocol,
+                          uint8_t* dev_out, uint64_t out_cap, uint64_t* dev_rec_pos,
+                          void* stream) {
+  return log_recv(ctx, true, dev_slab, slab_bytes, dev_rec_off, stride, cols, dev_src,
+                  dev_rx_sec, dev_rx_usec, nullptr, n, protocol, 0, (char*)dev_out, out_cap,
+                  dev_rec_pos, stream);
 }
 
 int mgenx_flow_export(mgenx_ctx* ctx, const mgenx_flow_state* dev_flows, uint32_t n_flows,

@@ -26,7 +26,7 @@ constexpr int kLogThreads = 256;
 // the fields LogRecvEvent prints, gathered from rows or core columns + extended columns
 struct LogRec {
   uint32_t flow, seq, sec, usec, lat, lon, alt, poff;
-  uint16_t msg_len, dport, plen, hport;
+  uint16_t msg_len, dport, plen, hport, hdr;
   uint8_t flags, err, dtype, dlen, ptype, gps, htype, hlen;
   uint8_t daddr[16], haddr[16];
 };
@@ -272,8 +272,58 @@ __device__ void format_line(S& s, const LogRec& r, const uint8_t* rec, const mge
   s.put('\n');
 }
 
+// Binary RECV / RERR records (MgenMsg::LogRecvEvent binary branch, mgenMsg.cpp:958-1033;
+// LogRecvError binary branch, :652-710): BE header fields, the source address, then for RECV
+// recordLength - index + 4 = hdr + payload_len + 2 message bytes with CHECKSUM cleared in
+// the flags byte.  Bytes past the slab (the reference's stale receive buffer) are written 0.
+template <typename S>
+__device__ void put_be(S& s, uint32_t v, int bytes) {
+  for (int k = bytes - 1; k >= 0; k--) s.put((uint8_t)(v >> (8 * k)));
+}
+
+template <typename S>
+__device__ void format_binary(S& s, const LogRec& r, const uint8_t* rec, uint64_t avail,
+                              const mgenx_addr& src, uint32_t rx_sec, uint32_t rx_usec,
+                              int protocol) {
+  const bool av = src.type == 1 || src.type == 2;
+  const uint32_t alen = av ? src.len : 0u;
+  if (r.err) {
+    s.put(2);  // RERR_EVENT
+    s.put(0);
+    put_be(s, 12u + alen + 4u, 2);
+    put_be(s, rx_sec, 4);
+    put_be(s, rx_usec, 4);
+    put_be(s, src.port, 2);
+    s.put(av ? src.type : 0);
+    s.put((uint8_t)alen);
+    for (uint32_t k = 0; k < alen && k < 16; k++) s.put(src.addr[k]);
+    put_be(s, r.err, 4);  // htonl(msg_error)
+    return;
+  }
+  const uint32_t rl = (12u + alen + r.hdr + r.plen) & 0xFFFFu;
+  s.put(1);  // RECV_EVENT
+  s.put((uint8_t)protocol);
+  put_be(s, rl, 2);
+  put_be(s, rx_sec, 4);
+  put_be(s, rx_usec, 4);
+  put_be(s, src.port, 2);
+  s.put(av ? src.type : 0);
+  s.put((uint8_t)alen);
+  for (uint32_t k = 0; k < alen && k < 16; k++) s.put(src.addr[k]);
+  const uint32_t ml = (rl - (14u + alen) + 4u) & 0xFFFFu;
+  for (uint32_t k = 0; k < ml; k++) {
+    uint8_t b = k < avail ? rec[k] : (uint8_t)0;
+    if (k == 3) {
+      b &= (uint8_t)~MGENX_FLAG_CHECKSUM;
+      if (r.flags & MGENX_FLAG_CHECKSUM_ERROR) b |= MGENX_FLAG_CHECKSUM_ERROR;
+    }
+    s.put(b);
+  }
+}
+
 struct LogParams {
   const uint8_t* slab;
+  uint64_t slab_bytes;
   const uint64_t* rec_off;
   uint64_t stride;
   mgenx_cols cols;
@@ -312,25 +362,37 @@ __device__ LogRec gather(const LogParams& p, uint32_t i) {
   r.hport = c.host_port[i]; r.htype = c.host_type[i]; r.hlen = c.host_len[i];
   r.lat = c.lat_raw[i]; r.lon = c.lon_raw[i]; r.alt = (uint32_t)c.alt[i];
   r.poff = c.payload_off[i];
+  r.hdr = c.hdr_len ? c.hdr_len[i] : 0;
   return r;
 }
 
-template <bool kWrite>
+template <typename S, bool kBinary>
+__device__ __forceinline__ void format_any(S& s, const LogParams& p, uint32_t i, const LogRec& r) {
+  const uint64_t off = p.rec_off ? p.rec_off[i] : (uint64_t)i * p.stride;
+  const uint8_t* rec = p.slab + off;
+  if (kBinary) {
+    const uint64_t avail = off < p.slab_bytes ? p.slab_bytes - off : 0u;
+    format_binary(s, r, rec, avail, p.src[i], p.rx_sec[i], p.rx_usec[i], p.protocol);
+  } else {
+    const int ttl = p.ttl ? p.ttl[i] : -1;
+    format_line(s, r, rec, p.src[i], p.rx_sec[i], p.rx_usec[i], p.protocol, ttl, p.opts);
+  }
+}
+
+template <bool kWrite, bool kBinary>
 __global__ void __launch_bounds__(kLogThreads) log_kernel(LogParams p) {
   const uint32_t i = blockIdx.x * kLogThreads + threadIdx.x;
   if (i >= p.n) return;
   const LogRec r = gather(p, i);
-  const uint8_t* rec = p.slab + (p.rec_off ? p.rec_off[i] : (uint64_t)i * p.stride);
-  const int ttl = p.ttl ? p.ttl[i] : -1;
   if (!kWrite) {
     CountSink s;
-    format_line(s, r, rec, p.src[i], p.rx_sec[i], p.rx_usec[i], p.protocol, ttl, p.opts);
+    format_any<CountSink, kBinary>(s, p, i, r);
     p.lens[i] = s.n;
   } else {
     const uint64_t off = p.line_off[i], end = p.line_off[i + 1];
     if (end > p.text_cap) return;  // does not fit: the caller sees line_off[n] > capacity
     WriteSink s{p.text + off};
-    format_line(s, r, rec, p.src[i], p.rx_sec[i], p.rx_usec[i], p.protocol, ttl, p.opts);
+    format_any<WriteSink, kBinary>(s, p, i, r);
   }
 }
 
@@ -355,7 +417,8 @@ extern "C" void mgenx_log_ws_free(void* p) {
   delete w;
 }
 
-extern "C" int mgenx_log_recv_text_run(void* wsp, const uint8_t* slab, const uint64_t* rec_off,
+extern "C" int mgenx_log_recv_run(void* wsp, bool binary, const uint8_t* slab,
+                                  uint64_t slab_bytes, const uint64_t* rec_off,
                                        uint64_t stride, const mgenx_cols* cols,
                                        const mgenx_addr* src, const uint32_t* rx_sec,
                                        const uint32_t* rx_usec, const int32_t* ttl, uint32_t n,
@@ -364,7 +427,7 @@ extern "C" int mgenx_log_recv_text_run(void* wsp, const uint8_t* slab, const uin
                                        hipStream_t stream, char* err, size_t errn) {
   mgenx_log_ws& ws = *static_cast<mgenx_log_ws*>(wsp);
   LogParams p;
-  p.slab = slab; p.rec_off = rec_off; p.stride = stride; p.cols = *cols; p.src = src;
+  p.slab = slab; p.slab_bytes = slab_bytes; p.rec_off = rec_off; p.stride = stride; p.cols = *cols; p.src = src;
   p.rx_sec = rx_sec; p.rx_usec = rx_usec; p.ttl = ttl; p.n = n; p.protocol = protocol;
   p.opts = opts; p.text = reinterpret_cast<uint8_t*>(text); p.text_cap = text_cap;
   p.line_off = line_off;
@@ -387,7 +450,8 @@ extern "C" int mgenx_log_recv_text_run(void* wsp, const uint8_t* slab, const uin
   }
   p.lens = static_cast<uint64_t*>(ws.mem);
   // pass 1: lengths; line_off = exclusive scan of the n + 1 lengths (lens[n] = 0)
-  hipLaunchKernelGGL(log_kernel<false>, dim3(grid), dim3(kLogThreads), 0, stream, p);
+  if (binary) hipLaunchKernelGGL((log_kernel<false, true>), dim3(grid), dim3(kLogThreads), 0, stream, p);
+  else hipLaunchKernelGGL((log_kernel<false, false>), dim3(grid), dim3(kLogThreads), 0, stream, p);
   hipLaunchKernelGGL(log_tail_kernel, dim3(1), dim3(64), 0, stream, p.lens, n);
   size_t have = scan_bytes;
   if (hipcub::DeviceScan::ExclusiveSum(static_cast<uint8_t*>(ws.mem) + len_bytes, have, p.lens,
@@ -396,7 +460,8 @@ extern "C" int mgenx_log_recv_text_run(void* wsp, const uint8_t* slab, const uin
     return MGENX_EDEVICE;
   }
   // pass 2: the lines
-  hipLaunchKernelGGL(log_kernel<true>, dim3(grid), dim3(kLogThreads), 0, stream, p);
+  if (binary) hipLaunchKernelGGL((log_kernel<true, true>), dim3(grid), dim3(kLogThreads), 0, stream, p);
+  else hipLaunchKernelGGL((log_kernel<true, false>), dim3(grid), dim3(kLogThreads), 0, stream, p);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     snprintf(err, errn, "log: %s", hipGetErrorString(e));

@@ -1056,3 +1056,60 @@ uint32_t or_log_recv_text(const or_fields* f, const uint8_t* rec, const or_addr*
     p += sprintf(p, "\n");
     return (uint32_t)(p - out);
 }
+
+/* ------------------------------------------------------------------ */
+/* Binary RECV / RERR log records                                     */
+/*   MgenMsg::LogRecvEvent binary branch  mgenMsg.cpp:958-1033        */
+/*   MgenMsg::LogRecvError binary branch  mgenMsg.cpp:652-710         */
+/* RECV: eventType, protocol, BE recordLength = 12 + srcLen + hdr +    */
+/* payload_len, BE rx sec/usec, BE src port, src type/len/address,     */
+/* then recordLength - index + 4 = hdr + payload_len + 2 bytes of the  */
+/* message with CHECKSUM cleared in the flags byte (CHECKSUM_ERROR set */
+/* when flagged).  Bytes past avail (the reference's stale receive     */
+/* buffer) read as zero here: unpinned.                                */
+/* ------------------------------------------------------------------ */
+static uint32_t put_be16(uint8_t* p, uint32_t v) { p[0] = (uint8_t)(v >> 8); p[1] = (uint8_t)v; return 2; }
+static uint32_t put_be32(uint8_t* p, uint32_t v) { put32(p, v); return 4; }
+
+uint32_t or_log_recv_binary(const or_fields* f, const uint8_t* rec, uint64_t avail,
+                            const or_addr* src, uint32_t rx_sec, uint32_t rx_usec, int protocol,
+                            uint8_t* out)
+{
+    uint8_t* p = out;
+    const uint32_t alen = (src->type == OR_ADDR_IPV4 || src->type == OR_ADDR_IPV6) ? src->len : 0;
+    const uint8_t atype = (src->type == OR_ADDR_IPV4 || src->type == OR_ADDR_IPV6) ? src->type : 0;
+    if (!f->ok || f->err) {
+        *p++ = 2;                                   /* RERR_EVENT */
+        *p++ = 0;
+        p += put_be16(p, 12 + alen + 4);
+        p += put_be32(p, rx_sec);
+        p += put_be32(p, rx_usec);
+        p += put_be16(p, src->port);
+        *p++ = atype;
+        *p++ = (uint8_t)alen;
+        memcpy(p, src->addr, alen); p += alen;
+        p += put_be32(p, f->err);
+        return (uint32_t)(p - out);
+    }
+    const uint32_t rl = (12 + alen + f->hdr_len + f->payload_len) & 0xFFFF;
+    *p++ = 1;                                       /* RECV_EVENT */
+    *p++ = (uint8_t)protocol;
+    p += put_be16(p, rl);
+    p += put_be32(p, rx_sec);
+    p += put_be32(p, rx_usec);
+    p += put_be16(p, src->port);
+    *p++ = atype;
+    *p++ = (uint8_t)alen;
+    memcpy(p, src->addr, alen); p += alen;
+    const uint32_t index = 14 + alen;
+    const uint32_t ml = (rl - index + 4) & 0xFFFF;
+    for (uint32_t i = 0; i < ml; i++) {
+        uint8_t b = i < avail ? rec[i] : 0;
+        if (i == 3) {
+            b &= (uint8_t)~OR_FLAG_CHECKSUM;
+            if (f->flags & OR_FLAG_CHECKSUM_ERROR) b |= OR_FLAG_CHECKSUM_ERROR;
+        }
+        *p++ = b;
+    }
+    return (uint32_t)(p - out);
+}

@@ -244,6 +244,10 @@ enum { OR_LOG_EPOCH = 0x1, OR_LOG_NO_DATA = 0x2, OR_LOG_NO_GPS = 0x4 };
 uint32_t or_log_recv_text(const or_fields* f, const uint8_t* rec, const or_addr* src,
                           uint32_t rx_sec, uint32_t rx_usec, int protocol, int ttl,
                           uint32_t opts, char* out);
+/* Binary RECV / RERR records (mgenMsg.cpp:652-710, 958-1033); avail = bytes readable at rec. */
+uint32_t or_log_recv_binary(const or_fields* f, const uint8_t* rec, uint64_t avail,
+                            const or_addr* src, uint32_t rx_sec, uint32_t rx_usec, int protocol,
+                            uint8_t* out);
 
 #ifdef __cplusplus
 }

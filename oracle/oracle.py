@@ -134,6 +134,8 @@ def lib():
         L.or_flow_reduce_batch.argtypes = [P, u32, P, P, P, P, P, P, P, u32, P, u32, P]
         L.or_log_recv_text.argtypes = [P, P, P, u32, u32, i32, i32, u32, P]
         L.or_log_recv_text.restype = u32
+        L.or_log_recv_binary.argtypes = [P, P, u64, P, u32, u32, i32, P]
+        L.or_log_recv_binary.restype = u32
         L.or_sizeof.argtypes = [i32]
         L.or_sizeof.restype = u32
         assert L.or_sizeof(0) == TMPL_DTYPE.itemsize, "or_tmpl layout mismatch"
@@ -378,5 +380,23 @@ def log_recv_text(fields, slab, rec_off, src, rx_sec, rx_usec, protocol=1, ttl=N
                                ctypes.c_void_p(src.ctypes.data + i * src.itemsize),
                                int(rx_sec[i]), int(rx_usec[i]), protocol,
                                -1 if ttl is None else int(ttl[i]), opts, _ptr(buf))
+        out.append(buf[:n].tobytes())
+    return b"".join(out)
+
+
+def log_recv_binary(fields, slab, rec_off, src, rx_sec, rx_usec, protocol=1):
+    """Binary RECV / RERR log records for n received records (bytes past the slab read 0)."""
+    L = lib()
+    slab = np.ascontiguousarray(slab, np.uint8)
+    fields = np.ascontiguousarray(fields)
+    src = np.ascontiguousarray(src, ADDR_DTYPE)
+    out = []
+    buf = np.zeros(65536 + 256, np.uint8)
+    for i in range(len(fields)):
+        off = int(rec_off[i])
+        n = L.or_log_recv_binary(ctypes.c_void_p(fields.ctypes.data + i * fields.itemsize),
+                                 ctypes.c_void_p(slab.ctypes.data + off), len(slab) - off,
+                                 ctypes.c_void_p(src.ctypes.data + i * src.itemsize),
+                                 int(rx_sec[i]), int(rx_usec[i]), protocol, _ptr(buf))
         out.append(buf[:n].tobytes())
     return b"".join(out)

@@ -135,3 +135,28 @@ def test_log_rows_input_and_gps_values(torch, eng, oracle):
     f = oracle.udp_recv_batch(h, n, stride=256, fixed_len=256)
     want = oracle.log_recv_text(f, h, np.arange(n, dtype=np.uint64) * 256, src, rx_s, rx_u)
     assert text.cpu().numpy().tobytes() == want
+
+
+@pytest.mark.parametrize("mode", ["udp", "tcp_force"])
+def test_binary_log_matches_oracle(torch, eng, gold, oracle, mode):
+    """Binary RECV / RERR records (LogRecvEvent / LogRecvError binary form) == the oracle."""
+    from mgen_amd import OPT_CHECKSUM_FORCE, OPT_TCP, to_device
+    uopts = {"udp": 0, "tcp_force": OPT_TCP | OPT_CHECKSUM_FORCE}
+    n = len(gold["unpack_lens"])
+    slab = to_device(gold["unpack_slab"]).view(torch.uint8)
+    offs = to_device(gold["unpack_offs"]).view(torch.int64)
+    lens = to_device(gold["unpack_lens"]).view(torch.int32)
+    cols = eng.unpack(slab, n, rec_off=offs, rec_len=lens, opts=uopts[mode], ext=True)
+    rng = np.random.default_rng(23)
+    src = _sources(oracle, n, rng)
+    rx_sec = rng.integers(1_600_000_000, 1_800_000_000, n, dtype=np.int64).astype(np.uint32)
+    rx_usec = rng.integers(0, 1_000_000, n).astype(np.uint32)
+    proto = 1 if mode == "udp" else 2
+    out, pos = eng.log_recv_binary(slab, n, cols, to_device(src.view(np.uint8)),
+                                   to_device(rx_sec), to_device(rx_usec), rec_off=offs,
+                                   protocol=proto)
+    want = oracle.log_recv_binary(gold[f"unpack_fields_{mode}"], gold["unpack_slab"],
+                                  gold["unpack_offs"], src, rx_sec, rx_usec, protocol=proto)
+    got = out.cpu().numpy().tobytes()
+    assert len(got) == len(want)
+    assert got == want
