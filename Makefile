@@ -1,36 +1,57 @@
-# Builds the product library (gfx950) and the test-only oracle.
+# Builds the product library (gfx950), the diagnostics library and the test-only oracle.
+#   mgen_amd/libmgenx.so       product: the C ABI of include/mgenx.h (nothing else exported)
+#   mgen_amd/libmgenx_diag.so  the same kernels plus the ablation variants and memory probes
+#                              of include/mgenx_diag.h (benchmark scripts only)
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
-HIPFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -Wno-unused-value
-SRC := mgen_amd/csrc/mgenx_api.hip mgen_amd/csrc/mgenx_unpack.hip mgen_amd/csrc/mgenx_pack.hip \
-       mgen_amd/csrc/mgenx_scan.hip mgen_amd/csrc/mgenx_analytic.hip \
-       mgen_amd/csrc/mgenx_log.hip
-HDR := include/mgenx.h mgen_amd/csrc/mgenx_common.hpp mgen_amd/csrc/mgenx_kernels.hpp
+HIPFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -Wno-unused-value -Wno-int-to-pointer-cast
+NAMES := mgenx_api mgenx_unpack mgenx_pack mgenx_scan mgenx_analytic mgenx_log mgenx_comm
+HDR := include/mgenx.h include/mgenx_diag.h mgen_amd/csrc/mgenx_common.hpp mgen_amd/csrc/mgenx_kernels.hpp
+OBJ := $(addprefix build/product/,$(addsuffix .o,$(NAMES)))
+DOBJ := $(addprefix build/diag/,$(addsuffix .o,$(NAMES)))
+LIBS := -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
-all: mgen_amd/libmgenx.so oracle tests/cpp/host_roundtrip tests/cpp/loopback
+all: mgen_amd/libmgenx.so mgen_amd/libmgenx_diag.so oracle tests/cpp/host_roundtrip \
+     tests/cpp/loopback tests/cpp/compat_shapes
 
-mgen_amd/libmgenx.so: $(SRC) $(HDR)
-	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -shared -Iinclude -Imgen_amd/csrc $(SRC) -o $@
+build/product/%.o: mgen_amd/csrc/%.hip $(HDR)
+	@mkdir -p build/product
+	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -DMGENX_DIAG=0 -Iinclude -Imgen_amd/csrc -c $< -o $@
+
+build/diag/%.o: mgen_amd/csrc/%.hip $(HDR)
+	@mkdir -p build/diag
+	$(HIPCC) --offload-arch=$(ARCH) $(HIPFLAGS) -DMGENX_DIAG=1 -Iinclude -Imgen_amd/csrc -c $< -o $@
+
+mgen_amd/libmgenx.so: $(OBJ)
+	$(HIPCC) --offload-arch=$(ARCH) -shared $(OBJ) -o $@ $(LIBS)
+
+mgen_amd/libmgenx_diag.so: $(DOBJ)
+	$(HIPCC) --offload-arch=$(ARCH) -shared $(DOBJ) -o $@ $(LIBS)
+
+HOSTCXX := g++ -O2 -std=c++17 -D__HIP_PLATFORM_AMD__ -Iinclude -I/opt/rocm/include
+HOSTLD := -Lmgen_amd -lmgenx -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,'$$ORIGIN/../../mgen_amd' \
+          -Wl,-rpath,/opt/rocm/lib
 
 # C++ host-layer test program (include/mgenx.hpp), plain g++ against the C ABI
 tests/cpp/host_roundtrip: tests/cpp/host_roundtrip.cpp include/mgenx.hpp include/mgenx.h mgen_amd/libmgenx.so
-	g++ -O2 -std=c++17 -D__HIP_PLATFORM_AMD__ -Iinclude -I/opt/rocm/include $< -o $@ \
-	    -Lmgen_amd -lmgenx -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,'$$ORIGIN/../../mgen_amd' \
-	    -Wl,-rpath,/opt/rocm/lib
+	$(HOSTCXX) $< -o $@ $(HOSTLD)
 
 # config 1 (UDP over loopback): CPU path through the test-only oracle, GPU path through libmgenx
 tests/cpp/loopback: tests/cpp/loopback.cpp include/mgenx.hpp include/mgenx_io.hpp include/mgenx.h \
 		mgen_amd/libmgenx.so oracle
-	g++ -O2 -std=c++17 -D__HIP_PLATFORM_AMD__ -Iinclude -Ioracle -I/opt/rocm/include $< -o $@ \
-	    -Lmgen_amd -lmgenx -Loracle/build -loracle -L/opt/rocm/lib -lamdhip64 \
-	    -Wl,-rpath,'$$ORIGIN/../../mgen_amd' -Wl,-rpath,'$$ORIGIN/../../oracle/build' \
-	    -Wl,-rpath,/opt/rocm/lib
+	$(HOSTCXX) -Ioracle $< -o $@ -Loracle/build -loracle -Wl,-rpath,'$$ORIGIN/../../oracle/build' \
+	    $(HOSTLD)
+
+# the reference's own call shapes compiled against the MgenMsg/MgenPayload/MgenAnalytic shim
+tests/cpp/compat_shapes: tests/cpp/compat_shapes.cpp $(wildcard include/mgenx_compat/*.h) \
+		include/mgenx.h mgen_amd/libmgenx.so
+	$(HOSTCXX) -Iinclude/mgenx_compat $< -o $@ $(HOSTLD)
 
 oracle:
 	$(MAKE) -s -C oracle
 
 clean:
-	rm -f mgen_amd/libmgenx.so
+	rm -rf build mgen_amd/libmgenx.so mgen_amd/libmgenx_diag.so
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all oracle clean

@@ -367,8 +367,10 @@ def main():
     # memory-system probes on this box: the unpack's read pattern alone, and with 512-B
     # row stores per 16-KiB group (mgenx_diag_group_rw)
     probe_out = torch.empty(N_REC * 32, dtype=torch.uint8, device=dev)
-    rd_ms = timed(torch, lambda: eng.group_rw(slab, probe_out, 0), reps=20)
-    rw_ms = timed(torch, lambda: eng.group_rw(slab, probe_out, 1), reps=20)
+    probe = Engine(local, diag=True)   # libmgenx_diag.so: the memory-pattern probes
+    rd_ms = timed(torch, lambda: probe.group_rw(slab, probe_out, 0), reps=20)
+    rw_ms = timed(torch, lambda: probe.group_rw(slab, probe_out, 1), reps=20)
+    probe.close()
     del probe_out, ccols
 
     extra = {"columns_layout": {"unpack_ms": round(col_ms, 4),

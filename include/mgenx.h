@@ -21,7 +21,9 @@
  *                                                     mgenAppSinkTransport.cpp:369-434
  *   mgenx_flow_reduce   <- MgenAnalytic::Update       include/mgenAnalytic.h:91-94
  *                          via Mgen::UpdateRecvAnalytics src/common/mgen.cpp:1027-1070
- *   mgenx_crc32         <- MgenMsg::ComputeCRC32      include/mgenMsg.h:201-203
+ *   mgenx_pack_msgs     <- MgenMsg::Pack alone (TCP fragments, the MgenMsg shim)
+ *   mgenx_crc32_update  <- MgenMsg::ComputeCRC32      include/mgenMsg.h:201-203
+ *   mgenx_allreduce_flows  the per-flow counter merge of flow-sharded analytics (RCCL)
  */
 #ifndef MGENX_H
 #define MGENX_H
@@ -73,6 +75,8 @@ int  mgenx_ctx_create(int device, mgenx_ctx** out);
 int  mgenx_ctx_destroy(mgenx_ctx* ctx);
 /* Last HIP error string seen by this context (static storage). */
 const char* mgenx_last_error(const mgenx_ctx* ctx);
+/* The HIP device of a context. */
+int  mgenx_ctx_device(const mgenx_ctx* ctx);
 
 /* One decoded record's core fields, packed (32 B): the row-major alternative to the core
  * columns -- the batch analogue of one unpacked MgenMsg object.  Written whole lines at a
@@ -122,7 +126,20 @@ typedef struct {
     /* row-major output: when set, unpack writes these 32-B records instead of the core
      * columns (which may then be NULL); extended columns still go to their arrays */
     mgenx_rec* rows;
+    /* extended (optional): MGENX_DEC_* mask of the MgenMsg members this record's Unpack
+     * assigned.  Unpack leaves the other members as they were, which matters on a reused
+     * MgenMsg (the TCP receiver's rx_msg, mgenTransport.cpp:1501-1513) and for the shim. */
+    uint8_t*  decoded;
 } mgenx_cols;
+
+#define MGENX_DEC_MSGLEN 0x01  /* msg_len, version (bufferLen >= MIN_SIZE, mgenMsg.cpp:323-336) */
+#define MGENX_DEC_BASE   0x02  /* flags, flow_id, seq_num, tx_time (version 2, :345-366) */
+#define MGENX_DEC_DST    0x04  /* dst_addr and port (dst type IPv4/IPv6, :373-398) */
+#define MGENX_DEC_HDRLEN 0x08  /* packet_header_len (:437-487) */
+#define MGENX_DEC_HOST   0x10  /* host_addr set (valid type, fits: :425-431) */
+#define MGENX_DEC_GPS    0x20  /* latitude, longitude, altitude, gps_status (:449-465) */
+#define MGENX_DEC_PTYPE  0x40  /* payload_type (:472-475) */
+#define MGENX_DEC_PLEN   0x80  /* payload_len, payload_data (:482-497) */
 
 /* Decode n records.  Record i starts at dev_slab + (dev_rec_off ? dev_rec_off[i] :
  * i*stride) and is (dev_rec_len ? dev_rec_len[i] : fixed_len) bytes long (the receive
@@ -162,6 +179,7 @@ typedef struct {
 #define MGENX_PACK_CHECKSUM    0x1   /* Mgen checksum_enable */
 #define MGENX_PACK_RANDOM_FILL 0x2   /* the RANDOM_FILL build: fill = glibc rand() bytes
                                         after srand(fill_time) (mgenMsg.cpp:277-292) */
+#define MGENX_PACK_RAW         0x4   /* (set by mgenx_pack_msgs) MgenMsg::Pack alone */
 
 /* Pack n records with the UDP/SINK send sequence (LAST_BUFFER, Pack, WriteChecksum)
  * into dev_slab at dev_rec_off[i] (or i*stride).  dev_out_len[i] = Pack()'s return
@@ -178,6 +196,32 @@ int mgenx_pack_batch(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
                      const uint8_t* dev_pool, uint8_t* dev_slab, uint64_t slab_bytes,
                      const uint64_t* dev_rec_off, uint64_t stride, uint32_t* dev_out_len,
                      uint32_t opts, uint32_t fill_time, void* stream);
+
+/* MgenMsg::Pack alone (mgenMsg.cpp:83-313), without the UDP send sequence: the
+ * descriptor's flags are used as given (the caller sets LAST_BUFFER or not: with it the CRC
+ * runs over bufferLen - 4 bytes, without it over bufferLen), no trailer is written
+ * (MgenMsg::WriteChecksum is the caller's), and the MgenMsg state Pack leaves is returned:
+ *   dev_buf_len[i]  (optional) Pack's bufferLen argument; NULL = the descriptor's msg_len
+ *                   (the TCP fragment path packs msg_len 16384 into bufferLen 8192/8188,
+ *                   mgenTransport.cpp:1915-1926);
+ *   dev_crc_in[i]   (optional) the tx_checksum argument on entry (NULL = 0);
+ *   dev_tx_crc[i]   (optional) tx_checksum after Pack (unchanged when Pack returned early);
+ *   dev_state[i]    (optional) packet_header_len | flags member << 16 after Pack
+ *                   (packet_header_len 0xFFFF when Pack failed: not assigned).
+ * A failed Pack (return 0) writes no bytes (the reference leaves a partial header). */
+int mgenx_pack_msgs(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
+                    const uint32_t* dev_tmpl_crc, const mgenx_pack_desc* dev_desc, uint32_t n,
+                    const uint8_t* dev_pool, uint8_t* dev_slab, uint64_t slab_bytes,
+                    const uint64_t* dev_rec_off, uint64_t stride, const uint32_t* dev_buf_len,
+                    const uint32_t* dev_crc_in, uint32_t* dev_out_len, uint32_t* dev_tx_crc,
+                    uint32_t* dev_state, uint32_t opts, uint32_t fill_time, void* stream);
+
+/* MgenMsg::ComputeCRC32(checksum, buffer, len) (mgenMsg.cpp:524-541) over n byte ranges:
+ * dev_state_out[i] = the running CRC after feeding dev_data[off[i] .. off[i]+len[i]) to
+ * dev_state_in[i] (0 restarts from CRC32_XINIT; no final xor). */
+int mgenx_crc32_update(mgenx_ctx* ctx, const uint8_t* dev_data, const uint64_t* dev_off,
+                       const uint32_t* dev_len, uint32_t n, const uint32_t* dev_state_in,
+                       uint32_t* dev_state_out, void* stream);
 
 /* Standard CRC-32 (MgenMsg::ComputeCRC32 from a zero state + CRC32_XOROT) of n
  * byte ranges: out[i] = crc(dev_data[off[i] .. off[i]+len[i])). */
@@ -310,29 +354,25 @@ int mgenx_log_recv_binary(mgenx_ctx* ctx, const uint8_t* dev_slab, uint64_t slab
                           uint8_t* dev_out, uint64_t out_cap, uint64_t* dev_rec_pos,
                           void* stream);
 
-/* Tuning knobs (per context; for benchmarking kernel variants).  MGENX_TUNE_UNPACK_VARIANT:
- * 0 = automatic (pipelined fixed-length kernel when the batch qualifies), 1/2 = ablations
- * of the general kernel (loads+XOR only / lookups on cached rows), 3 = general kernel,
- * 12 = fixed-length kernel with a separate header load (1024-B records), 1024 + M =
- * ablation bit mask M of the aligned 1024-B kernel (1 = no LDS lookups, 2 = no decode and
- * no stores, 4 = decode without stores, 8 = stores to a scratch line, 16 = the other store
- * cache policy, 32 = stores wrapped onto the first 16K records, 64 = write-through stores,
- * 128 = non-temporal row loads, 256 (with 4) = dummy rows stored after each wave's last
- * group). */
-#define MGENX_TUNE_UNPACK_VARIANT 1
-/* MGENX_TUNE_PACK_VARIANT: 0 = product; ablations 1 = no unit stores, 2 = no CRC work. */
-#define MGENX_TUNE_PACK_VARIANT 2
-int mgenx_set_tuning(mgenx_ctx* ctx, int key, int value);
-/* Diagnostic: plain 16-B-per-lane streaming read of `bytes` (the achievable-HBM reference
- * next to the roofline); dev_scratch holds `grid` words. */
-int mgenx_diag_stream_read(mgenx_ctx* ctx, const uint8_t* dev_data, uint64_t bytes,
-                           uint32_t* dev_scratch, int grid, void* stream);
-/* Diagnostic: the fixed-length unpack's memory pattern without its compute -- waves take
- * 16-KiB groups of `data` round-robin (16 loads of 1 KiB each, consumed by XOR) and, when
- * `mode` & 1, store 512 B per group to dev_out (bytes / 32 bytes); `mode` & 2: the stores
- * are write-through (sc1). */
-int mgenx_diag_group_rw(mgenx_ctx* ctx, const uint8_t* dev_data, uint64_t bytes,
-                        uint8_t* dev_out, int mode, void* stream);
+/* ---- multi-GPU exchange (RCCL over xGMI) ----
+ * One communicator per rank (one process per GPU): rank 0 calls mgenx_comm_unique_id and
+ * hands the MGENX_COMM_ID_BYTES bytes to every rank (any out-of-band channel), then every
+ * rank calls mgenx_comm_init.  Collectives are asynchronous on `stream`. */
+typedef struct mgenx_comm mgenx_comm;
+#define MGENX_COMM_ID_BYTES 128
+int mgenx_comm_unique_id(void* id_out);
+int mgenx_comm_init(mgenx_ctx* ctx, int nranks, int rank, const void* id, mgenx_comm** out);
+int mgenx_comm_destroy(mgenx_comm* comm);
+/* The per-flow counter merge after flow-sharded mgenx_flow_reduce: in-place SUM of
+ * n_flows x 64 B over the ranks (one ncclAllReduce).  Exact when every flow has one owner and
+ * the other ranks export zeros for it (mgenx_flow_export of a flow never updated there):
+ * integer sums of the 64-bit words leave the owner's counters, FP64 fields included, bit for
+ * bit. */
+int mgenx_allreduce_flows(mgenx_ctx* ctx, mgenx_comm* comm, mgenx_flow_counters* dev_counters,
+                          uint32_t n_flows, void* stream);
+/* dev_out[r * count + k] = rank r's dev_in[k] (the stream-shard stitch). */
+int mgenx_allgather_u64(mgenx_ctx* ctx, mgenx_comm* comm, const uint64_t* dev_in,
+                        uint64_t* dev_out, uint32_t count, void* stream);
 
 #ifdef __cplusplus
 }

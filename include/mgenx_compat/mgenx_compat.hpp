@@ -1,0 +1,442 @@
+// mgenx_compat.hpp -- the batching engine behind the MgenMsg / MgenPayload / MgenAnalytic
+// shim (mgenMsg.h, mgenPayload.h, mgenAnalytic.h in this directory).
+//
+// Every shim call is a batch: MgenMsg::Pack / Unpack / ComputeCRC32 and MgenAnalytic::Update
+// on one object are batches of one, and MgenMsg::PackBatch / UnpackBatch /
+// MgenAnalyticTable::UpdateBatch hand whole batches (the recvmmsg / sendmmsg handoff of
+// SURVEY.md 8(b)) to the same code.  A batch is staged in one pinned host arena, copied to
+// the device in one hipMemcpyAsync, processed by libmgenx's gfx950 kernels
+// (mgenx_pack_msgs, mgenx_unpack_batch, mgenx_crc32_update, mgenx_flow_reduce) and copied
+// back in one more; the call returns when the results are in the caller's buffers.  There
+// is no host implementation of the codec here: without a GPU the calls throw.
+//
+// One engine per process (device MGENX_DEVICE, default 0), serialised by a mutex: the
+// reference's callers run on one dispatcher thread.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "mgenx.h"
+
+namespace mgenx {
+namespace compat {
+
+struct Error : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+// One message for mgenx_pack_msgs: the MgenMsg members as a template + descriptor, Pack's
+// bufferLen and the tx_checksum argument.
+struct PackIn {
+  mgenx_flow_tmpl tmpl;
+  const uint8_t* payload;  // tmpl.payload_len bytes when tmpl.has_payload
+  mgenx_pack_desc desc;
+  uint32_t buf_len, crc_in;
+};
+struct PackOut {
+  uint32_t ret, tx_crc, state;  // Pack() return, tx_checksum after, hdr_len | flags << 16
+};
+
+// One decoded record: the MgenMsg members Unpack can assign, plus which it did.
+struct UnpackOut {
+  uint32_t flow_id, seq_num, tx_sec, tx_usec, payload_off;
+  uint32_t lat_raw, lon_raw;
+  int32_t alt;
+  uint16_t msg_len, dst_port, payload_len, hdr_len, host_port;
+  uint8_t flags, err, dst_type, dst_len, payload_type, gps_status, host_type, host_len, decoded;
+  uint8_t dst_addr[16], host_addr[16];
+};
+
+class Engine {
+ public:
+  static Engine& Get() {
+    static Engine e;
+    return e;
+  }
+  std::mutex& Lock() { return mu_; }
+
+  // ---- MgenMsg::Pack (mgenx_pack_msgs) over n messages -------------------------------
+  // dst[i] receives out[i].ret bytes (nothing when Pack fails).
+  void Pack(const PackIn* in, unsigned n, uint32_t opts, uint32_t fill_time, uint8_t* const* dst,
+            PackOut* out) {
+    if (n == 0) return;
+    Init();
+    if ((opts & MGENX_PACK_RANDOM_FILL) && (!fill_set_ || fill_time_ != fill_time)) {
+      Check(mgenx_set_fill_time(ctx_, fill_time), "mgenx_set_fill_time");
+      fill_set_ = true;
+      fill_time_ = fill_time;
+    }
+    // host staging: [tmpl | desc | buf_len | crc_in | rec_off | pool]
+    size_t pool = 0, slab = 0;
+    for (unsigned i = 0; i < n; i++) {
+      if (in[i].tmpl.has_payload) pool += in[i].tmpl.payload_len;
+      slab += Align(in[i].buf_len ? in[i].buf_len : in[i].desc.msg_len, 16);
+    }
+    Layout L;
+    const size_t o_tmpl = L.Add(n * sizeof(mgenx_flow_tmpl));
+    const size_t o_desc = L.Add(n * sizeof(mgenx_pack_desc));
+    const size_t o_blen = L.Add(n * 4u), o_cin = L.Add(n * 4u), o_off = L.Add(n * 8u);
+    const size_t o_pool = L.Add(pool ? pool : 16);
+    const size_t in_bytes = L.size;
+    // device outputs: [tmpl_crc | out_len | tx_crc | state | slab]
+    const size_t o_tcrc = L.Add(n * 4u), o_len = L.Add(n * 4u), o_tx = L.Add(n * 4u);
+    const size_t o_state = L.Add(n * 4u), o_slab = L.Add(slab + 64);
+    Reserve(L.size);
+    uint8_t* h = host_;
+    mgenx_flow_tmpl* t = (mgenx_flow_tmpl*)(h + o_tmpl);
+    mgenx_pack_desc* d = (mgenx_pack_desc*)(h + o_desc);
+    uint32_t* blen = (uint32_t*)(h + o_blen);
+    uint32_t* cin = (uint32_t*)(h + o_cin);
+    uint64_t* off = (uint64_t*)(h + o_off);
+    size_t p = 0, s = 0;
+    for (unsigned i = 0; i < n; i++) {
+      t[i] = in[i].tmpl;
+      if (in[i].tmpl.has_payload) {
+        t[i].payload_off = (uint32_t)p;
+        memcpy(h + o_pool + p, in[i].payload, in[i].tmpl.payload_len);
+        p += in[i].tmpl.payload_len;
+      }
+      d[i] = in[i].desc;
+      d[i].tmpl = i;
+      blen[i] = in[i].buf_len ? in[i].buf_len : in[i].desc.msg_len;
+      cin[i] = in[i].crc_in;
+      off[i] = s;
+      s += Align(blen[i], 16);
+    }
+    uint8_t* g = dev_;
+    H2D(g, h, in_bytes);
+    Check(mgenx_pack_prepare(ctx_, (const mgenx_flow_tmpl*)(g + o_tmpl), n, g + o_pool,
+                             (uint32_t*)(g + o_tcrc), stream_), "mgenx_pack_prepare");
+    Check(mgenx_pack_msgs(ctx_, (const mgenx_flow_tmpl*)(g + o_tmpl), (const uint32_t*)(g + o_tcrc),
+                          (const mgenx_pack_desc*)(g + o_desc), n, g + o_pool, g + o_slab,
+                          slab + 64, (const uint64_t*)(g + o_off), 0, (const uint32_t*)(g + o_blen),
+                          (const uint32_t*)(g + o_cin), (uint32_t*)(g + o_len),
+                          (uint32_t*)(g + o_tx), (uint32_t*)(g + o_state), opts, fill_time,
+                          stream_),
+          "mgenx_pack_msgs");
+    D2H(h + o_len, g + o_len, L.size - o_len);
+    Sync();
+    const uint32_t* len = (const uint32_t*)(h + o_len);
+    const uint32_t* tx = (const uint32_t*)(h + o_tx);
+    const uint32_t* st = (const uint32_t*)(h + o_state);
+    for (unsigned i = 0; i < n; i++) {
+      out[i].ret = len[i];
+      out[i].tx_crc = tx[i];
+      out[i].state = st[i];
+      if (len[i] && dst[i]) memcpy(dst[i], h + o_slab + off[i], len[i]);
+    }
+  }
+
+  // ---- MgenMsg::Unpack alone (mgenx_unpack_batch, MGENX_OPT_SKIP_CRC) ---------------
+  void Unpack(const uint8_t* const* bufs, const uint16_t* lens, unsigned n, UnpackOut* out) {
+    if (n == 0) return;
+    Init();
+    size_t slab = 0;
+    for (unsigned i = 0; i < n; i++) slab += Align(lens[i], 16);
+    Layout L;
+    const size_t o_off = L.Add(n * 8u), o_len = L.Add(n * 4u), o_slab = L.Add(slab + 64);
+    const size_t in_bytes = L.size;
+    // outputs, one array per column
+    struct Col {
+      size_t off, w;
+    };
+    const size_t w4[] = {4, 4, 4, 4, 4, 4, 4, 4};  // flow seq txs txu dst4 poff lat lon
+    size_t c4[8];
+    for (int k = 0; k < 8; k++) c4[k] = L.Add(n * w4[k]);
+    const size_t c_alt = L.Add(n * 4u);
+    size_t c2[5];  // msg_len dst_port payload_len hdr_len host_port
+    for (int k = 0; k < 5; k++) c2[k] = L.Add(n * 2u);
+    size_t c1[9];  // flags err dst_type dst_len payload_type gps host_type host_len decoded
+    for (int k = 0; k < 9; k++) c1[k] = L.Add(n * 1u);
+    const size_t c_da = L.Add(n * 16u), c_ha = L.Add(n * 16u);
+    Reserve(L.size);
+    uint8_t* h = host_;
+    uint64_t* off = (uint64_t*)(h + o_off);
+    uint32_t* rl = (uint32_t*)(h + o_len);
+    size_t s = 0;
+    for (unsigned i = 0; i < n; i++) {
+      off[i] = s;
+      rl[i] = lens[i];
+      memcpy(h + o_slab + s, bufs[i], lens[i]);
+      s += Align(lens[i], 16);
+    }
+    uint8_t* g = dev_;
+    H2D(g, h, in_bytes);
+    mgenx_cols c;
+    memset(&c, 0, sizeof(c));
+    c.flow_id = (uint32_t*)(g + c4[0]);
+    c.seq_num = (uint32_t*)(g + c4[1]);
+    c.tx_sec = (uint32_t*)(g + c4[2]);
+    c.tx_usec = (uint32_t*)(g + c4[3]);
+    c.dst_addr4 = (uint32_t*)(g + c4[4]);
+    c.payload_off = (uint32_t*)(g + c4[5]);
+    c.lat_raw = (uint32_t*)(g + c4[6]);
+    c.lon_raw = (uint32_t*)(g + c4[7]);
+    c.alt = (int32_t*)(g + c_alt);
+    c.msg_len = (uint16_t*)(g + c2[0]);
+    c.dst_port = (uint16_t*)(g + c2[1]);
+    c.payload_len = (uint16_t*)(g + c2[2]);
+    c.hdr_len = (uint16_t*)(g + c2[3]);
+    c.host_port = (uint16_t*)(g + c2[4]);
+    c.flags = g + c1[0];
+    c.err = g + c1[1];
+    c.dst_type = g + c1[2];
+    c.dst_len = g + c1[3];
+    c.payload_type = g + c1[4];
+    c.gps_status = g + c1[5];
+    c.host_type = g + c1[6];
+    c.host_len = g + c1[7];
+    c.decoded = g + c1[8];
+    c.dst_addr = g + c_da;
+    c.host_addr = g + c_ha;
+    Check(mgenx_unpack_batch(ctx_, g + o_slab, slab + 64, (const uint64_t*)(g + o_off), 0,
+                             (const uint32_t*)(g + o_len), 0, n, &c, MGENX_OPT_SKIP_CRC, stream_),
+          "mgenx_unpack_batch");
+    D2H(h + c4[0], g + c4[0], L.size - c4[0]);
+    Sync();
+    auto u32 = [&](size_t o, unsigned i) { return ((const uint32_t*)(h + o))[i]; };
+    auto u16 = [&](size_t o, unsigned i) { return ((const uint16_t*)(h + o))[i]; };
+    for (unsigned i = 0; i < n; i++) {
+      UnpackOut& r = out[i];
+      r.flow_id = u32(c4[0], i);
+      r.seq_num = u32(c4[1], i);
+      r.tx_sec = u32(c4[2], i);
+      r.tx_usec = u32(c4[3], i);
+      r.payload_off = u32(c4[5], i);
+      r.lat_raw = u32(c4[6], i);
+      r.lon_raw = u32(c4[7], i);
+      r.alt = (int32_t)u32(c_alt, i);
+      r.msg_len = u16(c2[0], i);
+      r.dst_port = u16(c2[1], i);
+      r.payload_len = u16(c2[2], i);
+      r.hdr_len = u16(c2[3], i);
+      r.host_port = u16(c2[4], i);
+      r.flags = h[c1[0] + i];
+      r.err = h[c1[1] + i];
+      r.dst_type = h[c1[2] + i];
+      r.dst_len = h[c1[3] + i];
+      r.payload_type = h[c1[4] + i];
+      r.gps_status = h[c1[5] + i];
+      r.host_type = h[c1[6] + i];
+      r.host_len = h[c1[7] + i];
+      r.decoded = h[c1[8] + i];
+      memcpy(r.dst_addr, h + c_da + 16u * i, 16);
+      memcpy(r.host_addr, h + c_ha + 16u * i, 16);
+    }
+  }
+
+  // ---- MgenMsg::ComputeCRC32 (mgenx_crc32_update) over n spans -------------------------
+  void Crc32Update(const uint8_t* const* bufs, const uint32_t* lens, const uint32_t* state_in,
+                   unsigned n, uint32_t* state_out) {
+    if (n == 0) return;
+    Init();
+    size_t bytes = 0;
+    for (unsigned i = 0; i < n; i++) bytes += Align(lens[i], 16);
+    Layout L;
+    const size_t o_off = L.Add(n * 8u), o_len = L.Add(n * 4u), o_in = L.Add(n * 4u);
+    const size_t o_data = L.Add(bytes + 16), in_bytes = L.size, o_out = L.Add(n * 4u);
+    Reserve(L.size);
+    uint8_t* h = host_;
+    uint64_t* off = (uint64_t*)(h + o_off);
+    size_t s = 0;
+    for (unsigned i = 0; i < n; i++) {
+      off[i] = s;
+      ((uint32_t*)(h + o_len))[i] = lens[i];
+      ((uint32_t*)(h + o_in))[i] = state_in[i];
+      if (lens[i]) memcpy(h + o_data + s, bufs[i], lens[i]);
+      s += Align(lens[i], 16);
+    }
+    uint8_t* g = dev_;
+    H2D(g, h, in_bytes);
+    Check(mgenx_crc32_update(ctx_, g + o_data, (const uint64_t*)(g + o_off),
+                             (const uint32_t*)(g + o_len), n, (const uint32_t*)(g + o_in),
+                             (uint32_t*)(g + o_out), stream_),
+          "mgenx_crc32_update");
+    D2H(h + o_out, g + o_out, n * 4u);
+    Sync();
+    memcpy(state_out, h + o_out, n * 4u);
+  }
+
+  // ---- MgenAnalytic state slots (mgenx_flow_init / mgenx_flow_reduce) -----------------
+  uint32_t FlowAlloc(double window) {
+    Init();
+    uint32_t slot;
+    if (!free_slots_.empty()) {
+      slot = free_slots_.back();
+      free_slots_.pop_back();
+    } else {
+      slot = n_slots_++;
+      if (n_slots_ > slot_cap_) GrowSlots(n_slots_ * 2 < 64 ? 64 : n_slots_ * 2);
+    }
+    Check(mgenx_flow_init(ctx_, flows_ + slot, 1, window, stream_), "mgenx_flow_init");
+    Sync();
+    return slot;
+  }
+  void FlowFree(uint32_t slot) { free_slots_.push_back(slot); }
+  void FlowReinit(uint32_t slot, double window) {
+    Init();
+    Check(mgenx_flow_init(ctx_, flows_ + slot, 1, window, stream_), "mgenx_flow_init");
+    Sync();
+  }
+  // records i < n (slot[i], rx, msgSize, tx, seq) in receive order; updated[i] = a window of
+  // slot[i] closed at record i, with its report in rep[i]
+  void FlowUpdate(const uint32_t* slot, const uint32_t* rx_sec, const uint32_t* rx_usec,
+                  const uint16_t* msg_size, const uint32_t* tx_sec, const uint32_t* tx_usec,
+                  const uint32_t* seq, unsigned n, bool* updated, mgenx_flow_report* rep) {
+    if (n == 0) return;
+    Init();
+    // one batch per run of distinct flows keeps "which record closed which window" exact:
+    // a flow closes at most one window per record, and a chunk holds each flow once
+    unsigned i0 = 0;
+    while (i0 < n) {
+      unsigned i1 = i0;
+      std::vector<uint32_t> seen;
+      while (i1 < n) {
+        bool dup = false;
+        for (uint32_t s2 : seen) dup |= (s2 == slot[i1]);
+        if (dup) break;
+        seen.push_back(slot[i1]);
+        i1++;
+      }
+      FlowChunk(slot + i0, rx_sec + i0, rx_usec + i0, msg_size + i0, tx_sec + i0, tx_usec + i0,
+                seq + i0, i1 - i0, updated + i0, rep + i0);
+      i0 = i1;
+    }
+  }
+  const mgenx_flow_state* DevFlows() const { return flows_; }
+  mgenx_ctx* Ctx() {
+    Init();
+    return ctx_;
+  }
+  hipStream_t Stream() {
+    Init();
+    return stream_;
+  }
+
+ private:
+  struct Layout {
+    size_t size = 0;
+    size_t Add(size_t bytes) {
+      const size_t o = size;
+      size += Align(bytes, 256);
+      return o;
+    }
+  };
+  static size_t Align(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+  Engine() = default;
+  ~Engine() {
+    // process teardown: the HIP runtime may already be gone, so nothing is freed here
+  }
+  void Init() {
+    if (ctx_) return;
+    const char* dv = getenv("MGENX_DEVICE");
+    const int device = dv ? atoi(dv) : 0;
+    if (hipSetDevice(device) != hipSuccess) throw Error("mgenx compat: no HIP device");
+    if (mgenx_ctx_create(device, &ctx_) != MGENX_OK) throw Error("mgenx_ctx_create failed");
+    if (hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess)
+      throw Error("hipStreamCreate failed");
+  }
+  void Reserve(size_t bytes) {
+    if (bytes <= cap_) return;
+    size_t c = cap_ ? cap_ : (1u << 20);
+    while (c < bytes) c *= 2;
+    if (host_) (void)hipHostFree(host_);
+    if (dev_) (void)hipFree(dev_);
+    host_ = nullptr;
+    dev_ = nullptr;
+    if (hipHostMalloc((void**)&host_, c) != hipSuccess || hipMalloc((void**)&dev_, c) != hipSuccess)
+      throw Error("mgenx compat: staging allocation failed");
+    cap_ = c;
+  }
+  void GrowSlots(uint32_t cap) {
+    mgenx_flow_state* f = nullptr;
+    if (hipMalloc((void**)&f, (size_t)cap * sizeof(mgenx_flow_state)) != hipSuccess)
+      throw Error("mgenx compat: flow state allocation failed");
+    if (flows_) {
+      if (hipMemcpyAsync(f, flows_, (size_t)slot_cap_ * sizeof(mgenx_flow_state),
+                         hipMemcpyDeviceToDevice, stream_) != hipSuccess)
+        throw Error("mgenx compat: flow state copy failed");
+      Sync();
+      (void)hipFree(flows_);
+    }
+    flows_ = f;
+    slot_cap_ = cap;
+  }
+  void FlowChunk(const uint32_t* slot, const uint32_t* rx_sec, const uint32_t* rx_usec,
+                 const uint16_t* msg_size, const uint32_t* tx_sec, const uint32_t* tx_usec,
+                 const uint32_t* seq, unsigned n, bool* updated, mgenx_flow_report* rep) {
+    Layout L;
+    const size_t o_idx = L.Add(n * 4u), o_seq = L.Add(n * 4u), o_txs = L.Add(n * 4u);
+    const size_t o_txu = L.Add(n * 4u), o_len = L.Add(n * 2u), o_rxs = L.Add(n * 4u);
+    const size_t o_rxu = L.Add(n * 4u), o_cnt = L.Add((size_t)slot_cap_ * 4u);
+    const size_t in_bytes = L.size;
+    const size_t o_rep = L.Add((size_t)slot_cap_ * sizeof(mgenx_flow_report));
+    Reserve(L.size);
+    uint8_t* h = host_;
+    memcpy(h + o_idx, slot, n * 4u);
+    memcpy(h + o_seq, seq, n * 4u);
+    memcpy(h + o_txs, tx_sec, n * 4u);
+    memcpy(h + o_txu, tx_usec, n * 4u);
+    memcpy(h + o_len, msg_size, n * 2u);
+    memcpy(h + o_rxs, rx_sec, n * 4u);
+    memcpy(h + o_rxu, rx_usec, n * 4u);
+    memset(h + o_cnt, 0, (size_t)slot_cap_ * 4u);
+    uint8_t* g = dev_;
+    H2D(g, h, in_bytes);
+    Check(mgenx_flow_reduce(ctx_, (const uint32_t*)(g + o_idx), (const uint32_t*)(g + o_seq),
+                            (const uint32_t*)(g + o_txs), (const uint32_t*)(g + o_txu),
+                            (const uint16_t*)(g + o_len), (const uint32_t*)(g + o_rxs),
+                            (const uint32_t*)(g + o_rxu), n, flows_, slot_cap_,
+                            (mgenx_flow_report*)(g + o_rep), 1, (uint32_t*)(g + o_cnt), stream_),
+          "mgenx_flow_reduce");
+    D2H(h + o_cnt, g + o_cnt, L.size - o_cnt);
+    Sync();
+    const uint32_t* cnt = (const uint32_t*)(h + o_cnt);
+    const mgenx_flow_report* r = (const mgenx_flow_report*)(h + o_rep);
+    for (unsigned i = 0; i < n; i++) {
+      updated[i] = cnt[slot[i]] != 0;
+      if (updated[i]) rep[i] = r[slot[i]];
+    }
+  }
+  void H2D(void* d, const void* s, size_t b) {
+    if (hipMemcpyAsync(d, s, b, hipMemcpyHostToDevice, stream_) != hipSuccess)
+      throw Error("mgenx compat: H2D failed");
+  }
+  void D2H(void* d, const void* s, size_t b) {
+    if (hipMemcpyAsync(d, s, b, hipMemcpyDeviceToHost, stream_) != hipSuccess)
+      throw Error("mgenx compat: D2H failed");
+  }
+  void Sync() {
+    if (hipStreamSynchronize(stream_) != hipSuccess) throw Error("mgenx compat: sync failed");
+  }
+  void Check(int rc, const char* what) {
+    if (rc != MGENX_OK) {
+      const char* m = mgenx_last_error(ctx_);
+      throw Error(std::string(what) + " failed (" + std::to_string(rc) + ")" +
+                  (m && *m ? std::string(": ") + m : std::string()));
+    }
+  }
+
+  std::mutex mu_;
+  mgenx_ctx* ctx_ = nullptr;
+  hipStream_t stream_ = nullptr;
+  uint8_t* host_ = nullptr;
+  uint8_t* dev_ = nullptr;
+  size_t cap_ = 0;
+  bool fill_set_ = false;
+  uint32_t fill_time_ = 0;
+  mgenx_flow_state* flows_ = nullptr;
+  uint32_t n_slots_ = 0, slot_cap_ = 0;
+  std::vector<uint32_t> free_slots_;
+};
+
+}  // namespace compat
+}  // namespace mgenx

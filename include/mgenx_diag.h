@@ -1,0 +1,44 @@
+/*
+ * mgenx_diag.h -- diagnostics of libmgenx_diag.so (NOT part of the product ABI).
+ *
+ * libmgenx_diag.so is built from the same sources as libmgenx.so with the kernel ablation
+ * variants and the memory-pattern probes compiled in; benchmark and tuning scripts load it
+ * (mgen_amd.Engine(diag=True)).  The product library exports none of these symbols.
+ */
+#ifndef MGENX_DIAG_H
+#define MGENX_DIAG_H
+
+#include "mgenx.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Tuning knobs (per context; for benchmarking kernel variants).  MGENX_TUNE_UNPACK_VARIANT:
+ * 0 = automatic (pipelined fixed-length kernel when the batch qualifies), 1/2 = ablations
+ * of the general kernel (loads+XOR only / lookups on cached rows), 3 = general kernel,
+ * 12 = fixed-length kernel with a separate header load (1024-B records), 1024 + M =
+ * ablation bit mask M of the aligned 1024-B kernel (1 = no LDS lookups, 2 = no decode and
+ * no stores, 4 = decode without stores, 8 = stores to a scratch line, 16 = the other store
+ * cache policy, 32 = stores wrapped onto the first 16K records, 64 = write-through stores,
+ * 128 = non-temporal row loads, 256 (with 4) = dummy rows stored after each wave's last
+ * group). */
+#define MGENX_TUNE_UNPACK_VARIANT 1
+/* MGENX_TUNE_PACK_VARIANT: 0 = product; ablations 1 = no unit stores, 2 = no CRC work. */
+#define MGENX_TUNE_PACK_VARIANT 2
+int mgenx_set_tuning(mgenx_ctx* ctx, int key, int value);
+/* Diagnostic: plain 16-B-per-lane streaming read of `bytes` (the achievable-HBM reference
+ * next to the roofline); dev_scratch holds `grid` words. */
+int mgenx_diag_stream_read(mgenx_ctx* ctx, const uint8_t* dev_data, uint64_t bytes,
+                           uint32_t* dev_scratch, int grid, void* stream);
+/* Diagnostic: the fixed-length unpack's memory pattern without its compute -- waves take
+ * 16-KiB groups of `data` round-robin (16 loads of 1 KiB each, consumed by XOR) and, when
+ * `mode` & 1, store 512 B per group to dev_out (bytes / 32 bytes); `mode` & 2: the stores
+ * are write-through (sc1). */
+int mgenx_diag_group_rw(mgenx_ctx* ctx, const uint8_t* dev_data, uint64_t bytes,
+                        uint8_t* dev_out, int mode, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -12,39 +12,47 @@ import os
 import numpy as np
 
 from ._abi import (  # noqa: F401
-    COLS_CORE, COLS_EXT, DESC_DTYPE, TMPL_DTYPE, MgenxCols, ERROR_CHECKSUM, ERROR_DSTADDR,
+    COLS_CORE, COLS_DEC, COLS_EXT, DESC_DTYPE, TMPL_DTYPE, MgenxCols, ERROR_CHECKSUM, ERROR_DSTADDR,
     ERROR_LENGTH, ERROR_NONE, ERROR_OOB, ERROR_VERSION, FLAG_CHECKSUM, FLAG_CHECKSUM_ERROR,
     FLAG_LAST_BUFFER, OPT_CHECKSUM_FORCE, OPT_SKIP_CRC, OPT_TCP, PACK_CHECKSUM,
     PACK_RANDOM_FILL, SCAN_SINK, SCAN_TCP, ScanInfo, FLOW_COUNTERS_DTYPE, FLOW_REPORT_DTYPE,
-    FLOW_STATE_BYTES, FLOW_STATE_DTYPE, REC_DTYPE,
+    FLOW_STATE_BYTES, FLOW_STATE_DTYPE, REC_DTYPE, PACK_RAW, DEC_MSGLEN, DEC_BASE, DEC_DST,
+    DEC_HDRLEN, DEC_HOST, DEC_GPS, DEC_PTYPE, DEC_PLEN,
 )
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libmgenx.so")
+DIAG_LIB_PATH = os.path.join(HERE, "libmgenx_diag.so")   # + include/mgenx_diag.h
 
+# every function include/mgenx.h declares (tests/test_abi_cpu.py checks the header agrees)
 EXPORTED_SYMBOLS = (
     "mgenx_abi_version", "mgenx_ctx_create", "mgenx_ctx_destroy", "mgenx_last_error",
-    "mgenx_unpack_batch", "mgenx_pack_prepare", "mgenx_set_fill_time", "mgenx_pack_batch",
-    "mgenx_crc32_batch", "mgenx_set_tuning", "mgenx_diag_stream_read", "mgenx_diag_group_rw", "mgenx_log_recv_text", "mgenx_log_recv_binary", "mgenx_stream_scan", "mgenx_flow_reduce",
+    "mgenx_ctx_device", "mgenx_unpack_batch", "mgenx_pack_prepare", "mgenx_set_fill_time",
+    "mgenx_pack_batch", "mgenx_pack_msgs", "mgenx_crc32_update", "mgenx_crc32_batch",
+    "mgenx_stream_scan", "mgenx_flow_init", "mgenx_flow_reduce", "mgenx_flow_export",
+    "mgenx_log_recv_text", "mgenx_log_recv_binary", "mgenx_comm_unique_id", "mgenx_comm_init",
+    "mgenx_comm_destroy", "mgenx_allreduce_flows", "mgenx_allgather_u64",
 )
+DIAG_SYMBOLS = ("mgenx_set_tuning", "mgenx_diag_stream_read", "mgenx_diag_group_rw")
 
 
 class MgenxError(RuntimeError):
     pass
 
 
-_lib = None
+_libs = {}
 
 
-def load():
-    """Load libmgenx.so (fails loudly when the HIP build is missing)."""
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
-        raise MgenxError(f"{LIB_PATH} not built: run __graft_entry__.build() "
+def load(diag: bool = False):
+    """Load libmgenx.so (or the diagnostics build libmgenx_diag.so); fails loudly when the
+    HIP build is missing."""
+    path = DIAG_LIB_PATH if diag else LIB_PATH
+    if path in _libs:
+        return _libs[path]
+    if not os.path.exists(path):
+        raise MgenxError(f"{path} not built: run __graft_entry__.build() "
                          "(hipcc --offload-arch=gfx950); there is no CPU fallback")
-    L = ctypes.CDLL(LIB_PATH)
+    L = ctypes.CDLL(path)
     P, u32, u64, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
     L.mgenx_abi_version.restype = i32
     L.mgenx_ctx_create.argtypes = [i32, ctypes.POINTER(P)]
@@ -56,10 +64,20 @@ def load():
     L.mgenx_pack_prepare.argtypes = [P, P, u32, P, P, P]
     L.mgenx_set_fill_time.argtypes = [P, u32]
     L.mgenx_pack_batch.argtypes = [P, P, P, P, u32, P, P, u64, P, u64, P, u32, u32, P]
+    L.mgenx_pack_msgs.argtypes = [P, P, P, P, u32, P, P, u64, P, u64, P, P, P, P, P, u32, u32,
+                                  P]
     L.mgenx_crc32_batch.argtypes = [P, P, P, P, u32, P, P]
-    L.mgenx_set_tuning.argtypes = [P, i32, i32]
-    L.mgenx_diag_stream_read.argtypes = [P, P, u64, P, i32, P]
-    L.mgenx_diag_group_rw.argtypes = [P, P, u64, P, i32, P]
+    L.mgenx_crc32_update.argtypes = [P, P, P, P, u32, P, P, P]
+    L.mgenx_ctx_device.argtypes = [P]
+    L.mgenx_comm_unique_id.argtypes = [P]
+    L.mgenx_comm_init.argtypes = [P, i32, i32, P, ctypes.POINTER(P)]
+    L.mgenx_comm_destroy.argtypes = [P]
+    L.mgenx_allreduce_flows.argtypes = [P, P, P, u32, P]
+    L.mgenx_allgather_u64.argtypes = [P, P, P, P, u32, P]
+    if diag:
+        L.mgenx_set_tuning.argtypes = [P, i32, i32]
+        L.mgenx_diag_stream_read.argtypes = [P, P, u64, P, i32, P]
+        L.mgenx_diag_group_rw.argtypes = [P, P, u64, P, i32, P]
     L.mgenx_stream_scan.argtypes = [P, P, u64, i32, P, P, u64, ctypes.POINTER(ScanInfo), P]
     L.mgenx_flow_init.argtypes = [P, P, u32, ctypes.c_double, P]
     L.mgenx_flow_reduce.argtypes = [P, P, P, P, P, P, P, P, u32, P, u32, P, u32, P, P]
@@ -68,7 +86,7 @@ def load():
                                       i32, u32, P, u64, P, P]
     L.mgenx_log_recv_binary.argtypes = [P, P, u64, P, u64, ctypes.POINTER(MgenxCols), P, P, P,
                                         u32, i32, P, u64, P, P]
-    _lib = L
+    _libs[path] = L
     return L
 
 
@@ -85,11 +103,11 @@ def _stream(device):
 class Engine:
     """One mgenx context on one GPU (``mgenx_ctx``)."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, diag: bool = False):
         import torch
         self.torch = torch
         self.device = device
-        self.lib = load()
+        self.lib = load(diag)
         self.ctx = ctypes.c_void_p()
         rc = self.lib.mgenx_ctx_create(device, ctypes.byref(self.ctx))
         if rc != 0:
@@ -118,7 +136,7 @@ class Engine:
         cols = {name: torch.empty(n * w if w > 1 else n, dtype=getattr(torch, dt), device=dev)
                 for name, dt, w in COLS_CORE}
         if ext:
-            for name, dt, w in COLS_EXT:
+            for name, dt, w in COLS_EXT + COLS_DEC:
                 cols[name] = torch.empty(n * w if w > 1 else n, dtype=getattr(torch, dt),
                                          device=dev)
         return cols
@@ -217,6 +235,29 @@ class Engine:
         self._check(rc, "mgenx_pack_batch")
         return out_len
 
+    def pack_msgs(self, tmpl, tmpl_crc, desc, n, pool, slab, *, rec_off=None, stride=0,
+                  buf_len=None, crc_in=None, opts=0, fill_time=0):
+        """MgenMsg::Pack alone (mgenx_pack_msgs): returns (out_len, tx_crc, state) tensors."""
+        torch = self.torch
+        out_len = torch.empty(n, dtype=torch.int32, device=slab.device)
+        tx_crc = torch.empty(n, dtype=torch.int32, device=slab.device)
+        state = torch.empty(n, dtype=torch.int32, device=slab.device)
+        rc = self.lib.mgenx_pack_msgs(self.ctx, _ptr(tmpl), _ptr(tmpl_crc), _ptr(desc), n,
+                                      _ptr(pool), _ptr(slab), slab.numel(), _ptr(rec_off), stride,
+                                      _ptr(buf_len), _ptr(crc_in), _ptr(out_len), _ptr(tx_crc),
+                                      _ptr(state), opts, fill_time, _stream(self.device))
+        self._check(rc, "mgenx_pack_msgs")
+        return out_len, tx_crc, state
+
+    def crc32_update(self, data, off, length, n, state_in, out=None):
+        """MgenMsg::ComputeCRC32 running states (mgenx_crc32_update)."""
+        if out is None:
+            out = self.torch.empty(n, dtype=self.torch.int32, device=data.device)
+        rc = self.lib.mgenx_crc32_update(self.ctx, _ptr(data), _ptr(off), _ptr(length), n,
+                                         _ptr(state_in), _ptr(out), _stream(self.device))
+        self._check(rc, "mgenx_crc32_update")
+        return out
+
     def set_pack_variant(self, v: int):
         self._check(self.lib.mgenx_set_tuning(self.ctx, 2, v), "mgenx_set_tuning")
 
@@ -283,6 +324,32 @@ class Engine:
         self._check(self.lib.mgenx_flow_export(self.ctx, _ptr(flows), n_flows, _ptr(out),
                                                _stream(self.device)), "mgenx_flow_export")
         return out
+
+    # ------------------------------------------------------------ multi-GPU (RCCL)
+    def comm_unique_id(self) -> bytes:
+        """mgenx_comm_unique_id: the 128-byte id rank 0 hands to every rank."""
+        buf = ctypes.create_string_buffer(128)
+        self._check(self.lib.mgenx_comm_unique_id(buf), "mgenx_comm_unique_id")
+        return buf.raw
+
+    def comm_init(self, nranks: int, rank: int, uid: bytes):
+        comm = ctypes.c_void_p()
+        buf = ctypes.create_string_buffer(bytes(uid), 128)
+        self._check(self.lib.mgenx_comm_init(self.ctx, nranks, rank, buf, ctypes.byref(comm)),
+                    "mgenx_comm_init")
+        return comm
+
+    def comm_destroy(self, comm):
+        self.lib.mgenx_comm_destroy(comm)
+
+    def allreduce_flows(self, comm, counters, n_flows):
+        """In-place SUM of n_flows x 64-B mgenx_flow_counters over the ranks (RCCL)."""
+        self._check(self.lib.mgenx_allreduce_flows(self.ctx, comm, _ptr(counters), n_flows,
+                                                   _stream(self.device)), "mgenx_allreduce_flows")
+
+    def allgather_u64(self, comm, src, dst, count):
+        self._check(self.lib.mgenx_allgather_u64(self.ctx, comm, _ptr(src), _ptr(dst), count,
+                                                 _stream(self.device)), "mgenx_allgather_u64")
 
     def crc32(self, data, off, length, n, out=None):
         if out is None:

@@ -11,7 +11,10 @@ ERROR_OOB = 0x80
 FLAG_CONTINUES, FLAG_END_OF_MSG, FLAG_CHECKSUM, FLAG_LAST_BUFFER, FLAG_CHECKSUM_ERROR = (
     0x01, 0x02, 0x04, 0x08, 0x10)
 OPT_CHECKSUM_FORCE, OPT_TCP, OPT_SKIP_CRC = 0x1, 0x2, 0x4
-PACK_CHECKSUM, PACK_RANDOM_FILL = 0x1, 0x2
+PACK_CHECKSUM, PACK_RANDOM_FILL, PACK_RAW = 0x1, 0x2, 0x4
+# MGENX_DEC_*: members an Unpack assigned (mgenx_cols.decoded)
+DEC_MSGLEN, DEC_BASE, DEC_DST, DEC_HDRLEN = 0x01, 0x02, 0x04, 0x08
+DEC_HOST, DEC_GPS, DEC_PTYPE, DEC_PLEN = 0x10, 0x20, 0x40, 0x80
 SCAN_TCP, SCAN_SINK = 0, 1
 
 # mgenx_flow_tmpl (68 bytes) and mgenx_pack_desc (20 bytes)
@@ -48,12 +51,13 @@ COLS_EXT = (
     ("dst_addr", "uint8", 16), ("lat_raw", "int32", 1), ("lon_raw", "int32", 1),
     ("alt", "int32", 1),
 )
+COLS_DEC = (("decoded", "uint8", 1),)   # after `rows` in the struct
 CORE_BYTES_PER_RECORD = 32
 
 
 class MgenxCols(ctypes.Structure):
     _fields_ = [(name, ctypes.c_void_p) for name, _, _ in COLS_CORE + COLS_EXT] + \
-        [("rows", ctypes.c_void_p)]
+        [("rows", ctypes.c_void_p), ("decoded", ctypes.c_void_p)]
 
 
 # mgenx_rec: one decoded record's core fields (32 B, row-major alternative to the columns)

@@ -11,6 +11,9 @@
 
 
 #include "mgenx_kernels.hpp"
+#if MGENX_DIAG
+#include "mgenx_diag.h"
+#endif
 
 extern "C" void* mgenx_scan_ws_new();
 extern "C" void mgenx_scan_ws_free(void* p);
@@ -224,7 +227,7 @@ int mgenx_unpack_batch(mgenx_ctx* ctx, const uint8_t* dev_slab, uint64_t slab_by
   p.expect = ctx->d_expect;
   p.expect_fixed = fixed_len < ctx->h_expect.size() ? ctx->h_expect[fixed_len] : 0u;
   p.sink = ctx->d_sink;
-  p.variant = ctx->unpack_variant;
+  p.variant = MGENX_DIAG ? ctx->unpack_variant : 0;
   p.cols = k;
   const uint64_t groups = ((uint64_t)n + 15) / 16;
   const uint64_t per_block = (uint64_t)mgenx::unpack_threads() / 64;  // waves per block
@@ -264,11 +267,12 @@ int mgenx_set_fill_time(mgenx_ctx* ctx, uint32_t fill_time) {
   return MGENX_OK;
 }
 
-int mgenx_pack_batch(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
-                     const uint32_t* dev_tmpl_crc, const mgenx_pack_desc* dev_desc, uint32_t n,
-                     const uint8_t* dev_pool, uint8_t* dev_slab, uint64_t slab_bytes,
-                     const uint64_t* dev_rec_off, uint64_t stride, uint32_t* dev_out_len,
-                     uint32_t opts, uint32_t fill_time, void* stream) {
+static int pack_common(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
+                       const uint32_t* dev_tmpl_crc, const mgenx_pack_desc* dev_desc, uint32_t n,
+                       const uint8_t* dev_pool, uint8_t* dev_slab, uint64_t slab_bytes,
+                       const uint64_t* dev_rec_off, uint64_t stride, const uint32_t* dev_buf_len,
+                       const uint32_t* dev_crc_in, uint32_t* dev_out_len, uint32_t* dev_tx_crc,
+                       uint32_t* dev_state, uint32_t opts, uint32_t fill_time, void* stream) {
   if (!ctx) return MGENX_EINVAL;
   if (n == 0) return MGENX_OK;
   if (!dev_tmpl || !dev_tmpl_crc || !dev_desc || !dev_slab || !dev_out_len) return MGENX_EINVAL;
@@ -290,11 +294,15 @@ int mgenx_pack_batch(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
   p.opts = opts;
   p.byte_tab = ctx->d_bytetab;
   p.a4_tab = ctx->d_tabs + 1024;  // [A_64 | A_4 | ...]
-  p.variant = ctx->pack_variant;
+  p.variant = MGENX_DIAG ? ctx->pack_variant : 0;
   p.xpow = ctx->d_xpow;
   p.ia = ctx->d_ia;
   p.rtab = ctx->d_rtab;
   p.rcrc = ctx->d_rcrc;
+  p.buf_len = dev_buf_len;
+  p.crc_in = dev_crc_in;
+  p.tx_crc = dev_tx_crc;
+  p.state = dev_state;
   const uint64_t batches = ((uint64_t)n + 63) / 64;
   uint64_t grid = (batches + 3) / 4;
   const uint64_t cap = (uint64_t)ctx->cu_count * 4;
@@ -303,6 +311,31 @@ int mgenx_pack_batch(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
   return e == hipSuccess ? MGENX_OK : set_err(ctx, e, "pack");
 }
 
+int mgenx_pack_batch(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
+                     const uint32_t* dev_tmpl_crc, const mgenx_pack_desc* dev_desc, uint32_t n,
+                     const uint8_t* dev_pool, uint8_t* dev_slab, uint64_t slab_bytes,
+                     const uint64_t* dev_rec_off, uint64_t stride, uint32_t* dev_out_len,
+                     uint32_t opts, uint32_t fill_time, void* stream) {
+  if (opts & MGENX_PACK_RAW) return MGENX_EINVAL;  // mgenx_pack_msgs is the raw form
+  return pack_common(ctx, dev_tmpl, dev_tmpl_crc, dev_desc, n, dev_pool, dev_slab, slab_bytes,
+                     dev_rec_off, stride, nullptr, nullptr, dev_out_len, nullptr, nullptr, opts,
+                     fill_time, stream);
+}
+
+int mgenx_pack_msgs(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
+                    const uint32_t* dev_tmpl_crc, const mgenx_pack_desc* dev_desc, uint32_t n,
+                    const uint8_t* dev_pool, uint8_t* dev_slab, uint64_t slab_bytes,
+                    const uint64_t* dev_rec_off, uint64_t stride, const uint32_t* dev_buf_len,
+                    const uint32_t* dev_crc_in, uint32_t* dev_out_len, uint32_t* dev_tx_crc,
+                    uint32_t* dev_state, uint32_t opts, uint32_t fill_time, void* stream) {
+  return pack_common(ctx, dev_tmpl, dev_tmpl_crc, dev_desc, n, dev_pool, dev_slab, slab_bytes,
+                     dev_rec_off, stride, dev_buf_len, dev_crc_in, dev_out_len, dev_tx_crc,
+                     dev_state, opts | MGENX_PACK_RAW, fill_time, stream);
+}
+
+int mgenx_ctx_device(const mgenx_ctx* ctx) { return ctx ? ctx->device : -1; }
+
+#if MGENX_DIAG
 int mgenx_set_tuning(mgenx_ctx* ctx, int key, int value) {
   if (!ctx) return MGENX_EINVAL;
   if (key == MGENX_TUNE_PACK_VARIANT) {
@@ -333,6 +366,8 @@ int mgenx_diag_group_rw(mgenx_ctx* ctx, const uint8_t* dev_data, uint64_t bytes,
                                         (hipStream_t)stream);
   return e == hipSuccess ? MGENX_OK : set_err(ctx, e, "group_rw");
 }
+
+#endif  // MGENX_DIAG
 
 int mgenx_stream_scan(mgenx_ctx* ctx, const uint8_t* dev_stream, uint64_t nbytes, int mode,
                       uint64_t* dev_rec_off, uint32_t* dev_rec_len, uint64_t cap,
@@ -435,9 +470,20 @@ int mgenx_crc32_batch(mgenx_ctx* ctx, const uint8_t* dev_data, const uint64_t* d
   if (!ctx) return MGENX_EINVAL;
   if (n == 0) return MGENX_OK;
   if (!dev_data || !dev_off || !dev_len || !dev_out) return MGENX_EINVAL;
-  hipError_t e = mgenx::launch_crc32(dev_data, dev_off, dev_len, n, ctx->d_bytetab, ctx->d_xpow,
+  hipError_t e = mgenx::launch_crc32(dev_data, dev_off, dev_len, n, ctx->d_bytetab, nullptr,
                                      dev_out, (hipStream_t)stream);
   return e == hipSuccess ? MGENX_OK : set_err(ctx, e, "crc32");
+}
+
+int mgenx_crc32_update(mgenx_ctx* ctx, const uint8_t* dev_data, const uint64_t* dev_off,
+                       const uint32_t* dev_len, uint32_t n, const uint32_t* dev_state_in,
+                       uint32_t* dev_state_out, void* stream) {
+  if (!ctx) return MGENX_EINVAL;
+  if (n == 0) return MGENX_OK;
+  if (!dev_data || !dev_off || !dev_len || !dev_state_in || !dev_state_out) return MGENX_EINVAL;
+  hipError_t e = mgenx::launch_crc32(dev_data, dev_off, dev_len, n, ctx->d_bytetab, dev_state_in,
+                                     dev_state_out, (hipStream_t)stream);
+  return e == hipSuccess ? MGENX_OK : set_err(ctx, e, "crc32_update");
 }
 
 }  // extern "C"

@@ -3,6 +3,10 @@
 
 #include "mgenx_common.hpp"
 
+#ifndef MGENX_DIAG
+#define MGENX_DIAG 0
+#endif
+
 namespace mgenx {
 
 struct UnpackParams {
@@ -40,6 +44,10 @@ struct PackParams {
   const uint32_t* ia;        // [65536] A_n(0xFFFFFFFF)
   const uint8_t* rtab;       // 16 zero bytes + glibc rand() byte stream (random fill)
   const uint32_t* rcrc;      // [65536] crc_raw of the first k rand bytes
+  const uint32_t* buf_len;   // MGENX_PACK_RAW: Pack's bufferLen per record (NULL = msg_len)
+  const uint32_t* crc_in;    // MGENX_PACK_RAW: tx_checksum argument on entry (NULL = 0)
+  uint32_t* tx_crc;          // optional: tx_checksum after Pack
+  uint32_t* state;           // optional: packet_header_len | flags << 16 after Pack
   int variant;               // diagnostic ablation (0 = product path)
 };
 
@@ -47,15 +55,17 @@ hipError_t launch_unpack(const UnpackParams& p, int grid, hipStream_t stream);
 // tuning knob (mgenx_set_tuning): 0 = auto (pipelined fixed-length kernel when the batch
 // qualifies), 1/2 = ablations of the general kernel, 3 = general kernel only
 int unpack_threads();
+#if MGENX_DIAG
 hipError_t launch_group_rw(const uint8_t* p, uint64_t bytes, uint8_t* out, int mode, int grid,
                            hipStream_t stream);
 hipError_t launch_stream_read(const uint8_t* p, uint64_t bytes, uint32_t* out, int grid,
                               hipStream_t stream);
+#endif
 hipError_t launch_pack(const PackParams& p, int grid, hipStream_t stream);
 hipError_t launch_pack_prepare(const mgenx_flow_tmpl* tmpl, uint32_t n_tmpl, const uint8_t* pool,
                                const uint32_t* byte_tab, uint32_t* out, hipStream_t stream);
 hipError_t launch_crc32(const uint8_t* data, const uint64_t* off, const uint32_t* len, uint32_t n,
-                        const uint32_t* byte_tab, const uint32_t* xpow, uint32_t* out,
+                        const uint32_t* byte_tab, const uint32_t* state_in, uint32_t* out,
                         hipStream_t stream);
 
 }  // namespace mgenx

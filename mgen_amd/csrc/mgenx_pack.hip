@@ -63,8 +63,10 @@ pack_kernel(PackParams p) {
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   uint8_t* img = &s_img[wv][lane * kImg];
-  const bool ck = (p.opts & MGENX_PACK_CHECKSUM) != 0 && p.variant != 2;
+  const int variant = MGENX_DIAG ? p.variant : 0;  // ablations: diagnostics build only
+  const bool ck = (p.opts & MGENX_PACK_CHECKSUM) != 0 && variant != 2;
   const bool rf = (p.opts & MGENX_PACK_RANDOM_FILL) != 0;
+  const bool raw = (p.opts & MGENX_PACK_RAW) != 0;  // Pack alone (no UDP send sequence)
   const uint64_t n_batches = ((uint64_t)p.n + 63) >> 6;
   const uint64_t n_waves = (uint64_t)gridDim.x * kWaves;
 
@@ -88,14 +90,18 @@ pack_kernel(PackParams p) {
 #pragma unroll
       for (int k = 0; k < 17; k++) tw[k] = tp[k];
       m.off = p.rec_off ? p.rec_off[i] : i * p.stride;
-      const uint32_t msgLen = d.msg_len;
+      // Pack's bufferLen (= msgLen in mgenMsg.cpp:95) and the msg_len member written at
+      // byte 0 differ on the TCP fragment path (mgenTransport.cpp:1924: bufferLen 8192 or
+      // 8188, msg_len the fragment length)
+      const uint32_t msgLen = (raw && p.buf_len) ? p.buf_len[i] : d.msg_len;
+      const uint32_t crc_in = (raw && p.crc_in) ? p.crc_in[i] : 0u;
       const uint32_t t_flow = tw[0], t_dtype = tw[1] & 0xffu, t_dlen = (tw[1] >> 8) & 0xffu;
       const uint32_t t_dport = tw[1] >> 16;
       const uint32_t t_htype = tw[6] & 0xffu, t_hlen = (tw[6] >> 8) & 0xffu;
       const uint32_t t_hport = tw[6] >> 16;
       const uint32_t t_gps = tw[14] & 0xffu, t_ptype = (tw[14] >> 8) & 0xffu;
       const uint32_t t_plen = tw[14] >> 16, t_poff = tw[15], t_has = tw[16] & 0xffu;
-      uint32_t flags = d.flags | MGENX_FLAG_LAST_BUFFER;      // mgenTransport.cpp:1017
+      uint32_t flags = raw ? d.flags : (d.flags | MGENX_FLAG_LAST_BUFFER);  // mgenTransport.cpp:1017
 
       // ---- layout walk (mgenMsg.cpp:97-273), arithmetic only ----
       const bool dst_ok = t_dtype == 1u || t_dtype == 2u;     // :146-148
@@ -122,7 +128,8 @@ pack_kernel(PackParams p) {
       if (!trunc) len += 2u;
       const bool pay = !trunc && t_has && msgLen >= len + t_plen;  // :264-273
       const uint32_t pend = pay ? len + t_plen : len;
-      const uint32_t crc_len = msgLen - 4u;
+      // ComputeCRC32 over msgLen - 4 bytes with LAST_BUFFER, else over msgLen (:305-308)
+      const uint32_t crc_len = (flags & MGENX_FLAG_LAST_BUFFER) ? msgLen - 4u : msgLen;
       const bool full_pay = crc_len > len && crc_len >= pend && pend > len;
       const uint32_t f = crc_len > pend ? crc_len - pend : 0u;
       const bool crc_on = ck && !failed && !trunc;
@@ -131,7 +138,9 @@ pack_kernel(PackParams p) {
       if (crc_on) {
         if (full_pay) { x_seg = p.xpow[pend - len]; tcrc = p.tmpl_crc[d.tmpl]; }
         if (crc_len > pend) { x_f = p.xpow[f]; if (rf && f >= 2) rc_v = p.rcrc[f - 2]; }
-        ia_v = p.ia[crc_len];
+        // A_len(init): init = ~0 (ComputeCRC32 restarts from a zero state, :530-533) or
+        // the caller's running value
+        ia_v = crc_in == 0u ? p.ia[crc_len] : multmodp(p.xpow[crc_len], crc_in);
       }
       // payload bytes that land in the header image (statically unrolled: one round trip)
       const uint32_t pimg = pay ? min(t_plen, (uint32_t)kImg > len ? (uint32_t)kImg - len : 0u) : 0u;
@@ -151,7 +160,7 @@ pack_kernel(PackParams p) {
       }
 
       // ---- header image in LDS ----
-      img_put16(img, 0, msgLen);                               // mgenMsg.cpp:97-131
+      img_put16(img, 0, d.msg_len);                            // mgenMsg.cpp:97-131
       img_put8(img, 2, 2);
       img_put8(img, 3, flags);
       img_put32(img, 4, t_flow);
@@ -182,6 +191,7 @@ pack_kernel(PackParams p) {
         if (pt_in) img_put8(img, pt_at, t_ptype);
         if (pl_in) img_put16(img, pl_at, t_plen);
       }
+      uint32_t tx_out = crc_in;   // unchanged unless the CRC runs
       if (failed) {
         m.ret = 0;
       } else {
@@ -226,17 +236,22 @@ pack_kernel(PackParams p) {
               if (crc_len > pend) c = multmodp(x_f, c) ^ rc_v;
             }
             tx_checksum = c ^ ia_v;
+            tx_out = tx_checksum;
             flags &= ~(uint32_t)MGENX_FLAG_LAST_BUFFER;
           }
         }
         // caller: WriteChecksum when checksum_enable and the CHECKSUM member flag is set
-        if (ck && (flags & MGENX_FLAG_CHECKSUM) && m.ret >= 4) {
+        if (!raw && ck && (flags & MGENX_FLAG_CHECKSUM) && m.ret >= 4) {
           m.trailer_on = 1;
           m.trailer = tx_checksum ^ 0xFFFFFFFFu;
         }
       }
       if (m.off > p.slab_bytes || m.ret > p.slab_bytes - m.off) m.ret = 0;  // never write OOB
       p.out_len[i] = m.ret;
+      if (p.tx_crc) p.tx_crc[i] = tx_out;
+      // the MgenMsg members Pack leaves behind: packet_header_len (set on every return but
+      // the failing ones) and the flags member (CHECKSUM set, LAST_BUFFER cleared)
+      if (p.state) p.state[i] = (m.ret ? (uint32_t)m.hdr : 0xFFFFu) | (flags & 0xffu) << 16;
     }
     s_meta[wv][lane] = m;
 
@@ -257,7 +272,7 @@ pack_kernel(PackParams p) {
     int ri = 0;
     uint32_t rstart = 0, next_start = s_pre[wv][1];
     PackMeta r = s_meta[wv][0];
-    for (uint32_t u = lane; u < (p.variant == 1 ? 0u : total); u += 64) {
+    for (uint32_t u = lane; u < (variant == 1 ? 0u : total); u += 64) {
       if (next_start <= u) {
         do {
           ri++;
@@ -363,26 +378,31 @@ hipError_t launch_pack_prepare(const mgenx_flow_tmpl* tmpl, uint32_t n_tmpl, con
 
 }  // namespace mgenx
 
-// Utility: standard CRC-32 of n byte ranges, one thread per range (byte table in LDS).
+// Utility: CRC-32 of n byte ranges, one thread per range (byte table in LDS).
+//   state_in == NULL: the standard CRC (init ~0, xorout ~0) -- mgenx_crc32_batch;
+//   state_in != NULL: MgenMsg::ComputeCRC32(checksum, buf, len) (mgenMsg.cpp:524-541): the
+//   running state continues from state_in[i] (0 restarts from ~0), no final xor.
 namespace mgenx {
 __global__ void crc32_kernel(const uint8_t* data, const uint64_t* off, const uint32_t* len,
-                             uint32_t n, const uint32_t* byte_tab, uint32_t* out) {
+                             uint32_t n, const uint32_t* byte_tab, const uint32_t* state_in,
+                             uint32_t* out) {
   __shared__ uint32_t s_tab[256];
   for (int e = threadIdx.x; e < 256; e += blockDim.x) s_tab[e] = byte_tab[e];
   __syncthreads();
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint8_t* s = data + off[i];
-  uint32_t c = 0xFFFFFFFFu;
+  uint32_t c = state_in ? state_in[i] : 0u;
+  if (c == 0u) c = 0xFFFFFFFFu;
   for (uint32_t k = 0; k < len[i]; k++) c = s_tab[(c ^ s[k]) & 0xffu] ^ (c >> 8);
-  out[i] = c ^ 0xFFFFFFFFu;
+  out[i] = state_in ? c : (c ^ 0xFFFFFFFFu);
 }
 
 hipError_t launch_crc32(const uint8_t* data, const uint64_t* off, const uint32_t* len, uint32_t n,
-                        const uint32_t* byte_tab, const uint32_t* /*xpow*/, uint32_t* out,
+                        const uint32_t* byte_tab, const uint32_t* state_in, uint32_t* out,
                         hipStream_t stream) {
   hipLaunchKernelGGL(crc32_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, data, off, len, n,
-                     byte_tab, out);
+                     byte_tab, state_in, out);
   return hipGetLastError();
 }
 }  // namespace mgenx

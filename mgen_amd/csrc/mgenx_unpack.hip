@@ -145,6 +145,7 @@ struct Hdr {
   uint32_t dst_addr[4], host_addr[4];
   uint16_t msg_len, dst_port, plen, hdr_len, host_port;
   uint8_t version, flags, err, dst_type, dst_len, ptype, gps, host_type, host_len;
+  uint8_t dec;  // MGENX_DEC_* of the fields Unpack assigned
   bool ok;
 };
 
@@ -183,11 +184,14 @@ __device__ void parse_header(const uint8_t* r, uint32_t buf_len, bool want_ext,
   h.msg_len = h.dst_port = h.plen = h.hdr_len = h.host_port = 0;
   h.version = 2;
   h.flags = h.err = h.dst_type = h.dst_len = h.ptype = h.gps = h.host_type = h.host_len = 0;
+  h.dec = 0;
   h.ok = false;
   if (buf_len < MGENX_MIN_SIZE) { h.err = MGENX_ERROR_LENGTH; return; }      // :323-328
   h.msg_len = bswap16((uint16_t)(w[0] & 0xffffu));
   h.version = (uint8_t)(w[0] >> 16);
+  h.dec = MGENX_DEC_MSGLEN;
   if (h.version != 2) { h.err = MGENX_ERROR_VERSION; return; }              // :336-343
+  h.dec |= MGENX_DEC_BASE;
   h.flags = (uint8_t)(w[0] >> 24);
   h.flow = bswap32(w[1]);
   h.seq = bswap32(w[2]);
@@ -197,6 +201,7 @@ __device__ void parse_header(const uint8_t* r, uint32_t buf_len, bool want_ext,
   const uint32_t t = (w[5] >> 16) & 0xffu;
   const uint32_t D = w[5] >> 24;
   if (t != 1u && t != 2u) { h.err = MGENX_ERROR_DSTADDR; return; }          // :374-392
+  h.dec |= MGENX_DEC_DST | MGENX_DEC_HDRLEN;  // every later return sets packet_header_len
   h.dst_type = (uint8_t)t;
   h.dst_len = (uint8_t)D;
   h.dst_port = dport;
@@ -216,6 +221,7 @@ __device__ void parse_header(const uint8_t* r, uint32_t buf_len, bool want_ext,
     len += 4u;
     if (len + H <= buf_len) {
       if (ht == 1u || ht == 2u) {
+        h.dec |= MGENX_DEC_HOST;
         h.host_type = (uint8_t)ht;
         h.host_len = (uint8_t)H;
         h.host_port = hport;
@@ -237,6 +243,7 @@ __device__ void parse_header(const uint8_t* r, uint32_t buf_len, bool want_ext,
     h.gps = (uint8_t)g.w;
     h.ptype = (uint8_t)(g.w >> 8);
     h.plen = bswap16((uint16_t)(g.w >> 16));
+    h.dec |= MGENX_DEC_GPS | MGENX_DEC_PTYPE | MGENX_DEC_PLEN;
     len += 16u;
     h.hdr_len = (uint16_t)len;
     if (h.plen != 0 && len + h.plen <= buf_len) h.poff = (len >> 2) << 2;
@@ -249,18 +256,21 @@ __device__ void parse_header(const uint8_t* r, uint32_t buf_len, bool want_ext,
     h.lon = bswap32(ldu32(r + len + 4));
     h.alt = (int32_t)bswap32(ldu32(r + len + 8));
     h.gps = r[len + 12];
+    h.dec |= MGENX_DEC_GPS;
     len += 13u;
   } else {
     h.hdr_len = (uint16_t)len; h.ok = true; return;
   }
   if (len + 1u <= buf_len) {                                                  // :467-475
     h.ptype = r[len];
+    h.dec |= MGENX_DEC_PTYPE;
     len += 1u;
   } else {
     h.hdr_len = (uint16_t)len; h.ok = true; return;
   }
   if (len + 2u <= buf_len) {                                                  // :477-497
     h.plen = bswap16(ldu16(r + len));
+    h.dec |= MGENX_DEC_PLEN;
     len += 2u;
     h.hdr_len = (uint16_t)len;
     if (h.plen != 0 && len + h.plen <= buf_len) h.poff = (len >> 2) << 2;
@@ -358,6 +368,10 @@ __device__ __forceinline__ void store_fast_ext(const mgenx_cols& c, uint64_t i, 
   const bool h16 = hv && H == 16u;  // only with dst IPv4 (D + H <= 20)
   const u32x4_t host = {a0, h16 ? wd[9] : 0u, h16 ? wd[10] : 0u, h16 ? wd[11] : 0u};
   if (!do_store) return;
+  if (c.decoded)  // a fast layout decodes every field (header <= 64 <= buf_len)
+    c.decoded[i] = (uint8_t)(MGENX_DEC_MSGLEN | MGENX_DEC_BASE | MGENX_DEC_DST | MGENX_DEC_HDRLEN |
+                             MGENX_DEC_GPS | MGENX_DEC_PTYPE | MGENX_DEC_PLEN |
+                             (hv ? MGENX_DEC_HOST : 0));
   if (c.hdr_len) c.hdr_len[i] = (uint16_t)len;
   if (c.payload_off) c.payload_off[i] = pl_ok ? len : 0u;  // len % 4 == 0
   if (c.host_port) c.host_port[i] = hv ? bswap16((uint16_t)(hw & 0xffffu)) : 0;
@@ -372,6 +386,7 @@ __device__ __forceinline__ void store_fast_ext(const mgenx_cols& c, uint64_t i, 
 
 // Extended columns of a record decoded by parse_header (quad lane 0).
 __device__ __forceinline__ void store_hdr_ext(const mgenx_cols& c, uint64_t i, const Hdr& h) {
+  if (c.decoded) c.decoded[i] = h.dec;
   if (c.hdr_len) c.hdr_len[i] = h.hdr_len;
   if (c.payload_off) c.payload_off[i] = h.poff;
   if (c.host_port) c.host_port[i] = h.host_port;
@@ -468,6 +483,7 @@ __device__ __forceinline__ void store_fast_q0(const mgenx_cols& c, uint64_t i,
 
 // A descriptor outside the slab: ERROR_OOB and zeroed core fields (quad lane 0).
 __device__ __forceinline__ void store_oob_q0(const mgenx_cols& c, uint64_t i) {
+  if (c.decoded) c.decoded[i] = 0;
   if (c.rows) {
     u32x4_t* r = reinterpret_cast<u32x4_t*>(c.rows + i);
     r[0] = u32x4_t{0u, 0u, 0u, 0u};
@@ -570,7 +586,7 @@ unpack_kernel(UnpackParams p) {
   const mgenx_cols& cc = p.cols;
   const bool any_ext = cc.hdr_len || cc.payload_off || cc.host_port || cc.host_type ||
                        cc.host_len || cc.lat_raw || cc.lon_raw || cc.alt || cc.dst_addr ||
-                       cc.host_addr;
+                       cc.host_addr || cc.decoded;
 
   // Per-wave predictor: while recent groups carried checksummed records, issue the row
   // loads speculatively together with the header load (one memory round per group); a
@@ -1139,9 +1155,12 @@ unpack_fixed_kernel(UnpackParams p, uint32_t expect) {
     for (uint32_t gg = wave_id; gg < g_end; gg += n_waves, k++) {
       const uint32_t i = rec_idx(gg);
       const uint64_t seq = (uint64_t)wave_id * 8192u + k * 512u + 8u * (uint32_t)lane;
-      if (i < p.n)
-        st_g64_nt((uint64_t)p.cols.rows + (kAblBurstSeq ? seq : (uint64_t)i * 32 + 8 * q),
-                  (uint64_t)gg);
+      const uint64_t a = (uint64_t)p.cols.rows + (kAblBurstSeq ? seq : (uint64_t)i * 32 + 8 * q);
+      if (i < p.n) {
+        if (kAblWt) st_g64_wt(a, (uint64_t)gg);
+        else if (kAblAltStore) st_g64(a, (uint64_t)gg);
+        else st_g64_nt(a, (uint64_t)gg);
+      }
     }
   }
 }
@@ -1201,7 +1220,7 @@ hipError_t launch_unpack(const UnpackParams& p, int grid, hipStream_t stream) {
   // fixed stride + one length in [65, 1024] + core columns: the pipelined kernel
   const mgenx_cols& c = p.cols;
   const bool ext = c.hdr_len || c.payload_off || c.host_port || c.host_type || c.host_len ||
-                   c.lat_raw || c.lon_raw || c.alt || c.dst_addr || c.host_addr;
+                   c.lat_raw || c.lon_raw || c.alt || c.dst_addr || c.host_addr || c.decoded;
   const uint32_t nr = (p.fixed_len + 63) / 64;
   const bool fixed = !p.rec_off && !p.rec_len && p.fixed_len >= 65 && p.fixed_len <= 1024 &&
                      p.stride > 0 && p.n <= 0xFFFFFFF0u && !ext &&
@@ -1220,6 +1239,7 @@ hipError_t launch_unpack(const UnpackParams& p, int grid, hipStream_t stream) {
     }
     return (c.rows ? kFixedLaunchRows : kFixedLaunch)[(p.fixed_len + 63) / 64](p, grid, stream);
   }
+#if MGENX_DIAG
   // ablation 12: the unaligned (separate header load) path on 1024-B records
   if (unpack_variant == 12 && fixed && p.fixed_len == 1024)
     return c.rows ? launch_fixed<16, 0, true>(p, grid, stream) : launch_fixed<16, 0>(p, grid, stream);
@@ -1232,6 +1252,7 @@ hipError_t launch_unpack(const UnpackParams& p, int grid, hipStream_t stream) {
       MGENX_ABL(1) MGENX_ABL(2) MGENX_ABL(3) MGENX_ABL(4) MGENX_ABL(5) MGENX_ABL(8)
       MGENX_ABL(16) MGENX_ABL(32) MGENX_ABL(64)
       MGENX_ABL(128) MGENX_ABL(144) MGENX_ABL(130) MGENX_ABL(136) MGENX_ABL(260) MGENX_ABL(772)
+      MGENX_ABL(276) MGENX_ABL(324) MGENX_ABL(788)
 #undef MGENX_ABL
       default: break;
     }
@@ -1239,10 +1260,13 @@ hipError_t launch_unpack(const UnpackParams& p, int grid, hipStream_t stream) {
   switch (unpack_variant) {
     case 1: return launch_mode<1>(p, grid, stream);
     case 2: return launch_mode<2>(p, grid, stream);
-    default: return launch_mode<0>(p, grid, stream);
+    default: break;
   }
+#endif  // MGENX_DIAG
+  return launch_mode<0>(p, grid, stream);
 }
 
+#if MGENX_DIAG
 // Diagnostic: streaming read of `bytes` (16 B per lane per load, grid-stride), XOR-folded
 // into one word per block so the loads are not dead.  Reference for achievable HBM rate.
 __global__ void __launch_bounds__(256) stream_read_kernel(const u32x4_t* p, uint64_t n16,
@@ -1303,9 +1327,67 @@ __global__ void __launch_bounds__(1024) group_rw_kernel(const uint8_t* p, uint32
   if (!(MODE & 1) && acc == 0x9E3779B9u) out[lane] = 1;
 }
 
+// Diagnostic: group_rw with the row stores held back in registers and issued K groups at a
+// time (K = 1 << LK), at each group's own row position; POL 0 = non-temporal, 1 = temporal,
+// 2 = write-through stores.
+template <int LK, int POL>
+__global__ void __launch_bounds__(1024) group_rw_buf_kernel(const uint8_t* p, uint32_t n_groups,
+                                                            uint8_t* out) {
+  constexpr int K = 1 << LK;
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave_id = __builtin_amdgcn_readfirstlane(blockIdx.x * 16 + (threadIdx.x >> 6));
+  const uint32_t n_waves = gridDim.x * 16;
+  uint32_t g = wave_id;
+  if (g >= n_groups) return;
+  const uint32_t lo = (uint32_t)(lane >> 2) * 1024u + 16u * (lane & 3);
+  u32x4_t d[16];
+#pragma unroll
+  for (int j = 0; j < 16; j++) d[j] = ldu128(p + (uint64_t)g * 16384u + lo + 64 * j);
+  uint32_t acc = 0;
+  while (g < n_groups) {
+    uint64_t buf[K];
+    uint32_t gs[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      const uint32_t gn = g + n_waves;
+      const uint32_t gl = gn < n_groups ? gn : g;
+#pragma unroll
+      for (int j = 0; j < 16; j++) {
+        acc = (acc << 1) ^ d[j].x ^ d[j].y ^ d[j].z ^ d[j].w;
+        __builtin_amdgcn_sched_barrier(0);
+        d[j] = ldu128(p + (uint64_t)gl * 16384u + lo + 64 * j);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      buf[k] = (uint64_t)acc << 32 | g;
+      gs[k] = g;
+      g = gn;
+    }
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      const uint64_t a = (uint64_t)out + (uint64_t)(gs[k] < n_groups ? gs[k] : 0u) * 512u + 8u * lane;
+      if (POL == 0) st_g64_nt(a, buf[k]);
+      else if (POL == 1) st_g64(a, buf[k]);
+      else st_g64_wt(a, buf[k]);
+    }
+  }
+}
+
 hipError_t launch_group_rw(const uint8_t* p, uint64_t bytes, uint8_t* out, int mode, int grid,
                            hipStream_t stream) {
   const uint32_t ng = (uint32_t)(bytes / 16384);
+  if (mode >= 16) {
+    const int lk = ((mode >> 4) & 7) - 1, pol = (mode >> 8) & 3;
+#define MGENX_GRB(LK, POL)                                                                   \
+  if (lk == LK && pol == POL) {                                                              \
+    hipLaunchKernelGGL((group_rw_buf_kernel<LK, POL>), dim3(grid), dim3(1024), 0, stream, p, ng, \
+                       out);                                                                 \
+    return hipGetLastError();                                                                \
+  }
+    MGENX_GRB(0, 0) MGENX_GRB(1, 0) MGENX_GRB(2, 0) MGENX_GRB(3, 0) MGENX_GRB(4, 0)
+    MGENX_GRB(2, 1) MGENX_GRB(4, 1) MGENX_GRB(2, 2) MGENX_GRB(4, 2)
+#undef MGENX_GRB
+    return hipErrorInvalidValue;
+  }
   switch (mode & 7) {
     case 4: hipLaunchKernelGGL(group_rw_kernel<4>, dim3(grid), dim3(1024), 0, stream, p, ng, out); break;
     case 0: hipLaunchKernelGGL(group_rw_kernel<0>, dim3(grid), dim3(1024), 0, stream, p, ng, out); break;
@@ -1321,6 +1403,8 @@ hipError_t launch_stream_read(const uint8_t* p, uint64_t bytes, uint32_t* out, i
                      reinterpret_cast<const u32x4_t*>(p), bytes / 16, out);
   return hipGetLastError();
 }
+
+#endif  // MGENX_DIAG
 
 int unpack_threads() { return kUnpackThreads; }
 

@@ -13,7 +13,7 @@ from mgen_amd import COLS_CORE, PACK_CHECKSUM, Engine, to_device  # noqa: E402
 from mgen_amd.workloads import udp_fixed  # noqa: E402
 
 N, REC = 1 << 20, 1024
-eng = Engine(0)
+eng = Engine(0, diag=True)
 tmpl, pool, desc = udp_fixed(N, REC)
 d_tmpl, d_pool, d_desc = to_device(tmpl), to_device(pool), to_device(desc)
 crc = torch.empty(len(tmpl), dtype=torch.int32, device="cuda")

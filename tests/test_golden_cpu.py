@@ -39,8 +39,18 @@ def test_oracle_reproduces_unpack_vectors(oracle, gold):
 def test_golden_covers_every_error_class(gold):
     errs = set(np.unique(gold["unpack_fields_udp_force"]["err"]).tolist())
     assert {0, 1, 2, 3, 4} <= errs
-    lens = gold["pack_lens_ck1_rf0"]
-    assert (lens == 0).sum() == 0 or True
+    # Pack returns 0 exactly for an unsupported dst type (mgenMsg.cpp:146-148) or a msg_len
+    # short of the dst section (:207-210)
+    tmpl, desc = gold["tmpl"], gold["desc"]
+    t = tmpl[desc["tmpl"]]
+    host_len = np.where(np.isin(t["host_type"], (1, 2)), t["host_len"], 0)
+    failed = (~np.isin(t["dst_type"], (1, 2))) | (
+        (desc["msg_len"] < 24 + t["dst_len"].astype(int) + host_len + 4) &
+        (desc["msg_len"] < 24 + t["dst_len"].astype(int)))
+    for key in ("pack_lens_ck0_rf0", "pack_lens_ck1_rf0", "pack_lens_ck1_rf1"):
+        lens = gold[key]
+        assert np.array_equal(lens == 0, failed), key
+        assert np.array_equal(lens[~failed], desc["msg_len"][~failed]), key
     # truncation boundaries are present: records with hdr_len < 48 exist
     f = gold["unpack_fields_udp"]
     assert ((f["hdr_len"] > 0) & (f["hdr_len"] < 48)).any()
@@ -60,6 +70,25 @@ def test_capi_library_exports_header_symbols():
     missing = [s for s in _header_functions() if not hasattr(lib, s)]
     assert not missing, missing
     assert lib.mgenx_abi_version() == 1
+
+
+def test_python_symbol_list_matches_header():
+    from mgen_amd import EXPORTED_SYMBOLS
+    assert sorted(EXPORTED_SYMBOLS) == _header_functions()
+
+
+def test_diagnostics_are_not_in_the_product_library():
+    """mgenx_diag.h symbols live only in libmgenx_diag.so (the product ABI is mgenx.h)."""
+    from mgen_amd import DIAG_LIB_PATH, DIAG_SYMBOLS, load
+    text = open(os.path.join(ROOT, "include", "mgenx_diag.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    declared = sorted(set(re.findall(r"\b(mgenx_[a-z0-9_]+)\s*\(", text)))
+    assert declared == sorted(DIAG_SYMBOLS)
+    prod = ctypes.CDLL(os.path.join(ROOT, "mgen_amd", "libmgenx.so"))
+    assert not [s for s in DIAG_SYMBOLS if hasattr(prod, s)]
+    assert os.path.exists(DIAG_LIB_PATH)
+    diag = load(diag=True)
+    assert all(hasattr(diag, s) for s in DIAG_SYMBOLS + tuple(_header_functions()))
 
 
 def test_capi_rejects_bad_arguments_without_gpu():
