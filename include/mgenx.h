@@ -24,6 +24,7 @@
  *   mgenx_pack_msgs     <- MgenMsg::Pack alone (TCP fragments, the MgenMsg shim)
  *   mgenx_crc32_update  <- MgenMsg::ComputeCRC32      include/mgenMsg.h:201-203
  *   mgenx_allreduce_flows  the per-flow counter merge of flow-sharded analytics (RCCL)
+ *   mgenx_flow_lookup   <- MgenAnalyticTable::FindFlow  include/mgenAnalytic.h:387
  */
 #ifndef MGENX_H
 #define MGENX_H
@@ -306,6 +307,30 @@ int mgenx_flow_reduce(mgenx_ctx* ctx, const uint32_t* dev_flow_idx, const uint32
 int mgenx_flow_export(mgenx_ctx* ctx, const mgenx_flow_state* dev_flows, uint32_t n_flows,
                       mgenx_flow_counters* dev_out, void* stream);
 
+/* A socket address as recvfrom reports it (ProtoAddress type / length / port / bytes). */
+typedef struct {
+    uint8_t  type;      /* MgenMsg::AddressType: 1 IPv4, 2 IPv6 */
+    uint8_t  len;       /* address length (4 / 16) */
+    uint16_t port;
+    uint8_t  addr[16];  /* network byte order */
+} mgenx_addr;           /* 20 bytes */
+
+/* ---- MgenAnalyticTable::FindFlow for batches (mgenAnalytic.cpp:312-328) ----
+ * A device hash table from the reference's flow key -- dst addr | dst port | src addr |
+ * src port | flowId -- to dense flow indices 0, 1, ... (new keys are numbered in the order
+ * of their first record, so the mapping is deterministic).  mgenx_flow_lookup maps n decoded
+ * records (columns dst_addr, dst_len, dst_port, flow_id, and err when given: err != 0 maps
+ * to MGENX_FLOW_NONE) with their recvfrom source addresses to dev_flow_idx[i] -- the input
+ * mgenx_flow_reduce takes -- and copies the table's flow count to dev_n_flows[0] (optional,
+ * device memory).  Keys persist across calls (streaming batches). */
+#define MGENX_FLOW_NONE 0xFFFFFFFFu
+typedef struct mgenx_flow_table mgenx_flow_table;
+int mgenx_flow_table_create(mgenx_ctx* ctx, uint32_t max_flows, mgenx_flow_table** out);
+int mgenx_flow_table_destroy(mgenx_flow_table* table);
+int mgenx_flow_lookup(mgenx_ctx* ctx, mgenx_flow_table* table, const mgenx_cols* cols,
+                      const mgenx_addr* dev_src, uint32_t n, uint32_t* dev_flow_idx,
+                      uint32_t* dev_n_flows, void* stream);
+
 /* ---- event log (MgenMsg::LogRecvEvent / LogRecvError, text form) ----
  * One line per record, as the UDP receive path logs it (src/common/mgenTransport.cpp:
  * 976-994): "RECV proto>... flow>... seq>... src>... dst>... sent>... size>... [host>...]
@@ -320,12 +345,6 @@ int mgenx_flow_export(mgenx_ctx* ctx, const mgenx_flow_state* dev_flows, uint32_
  * Output: dev_line_off[i] = byte offset of record i's line, dev_line_off[n] = total bytes;
  * the lines are written to dev_text only when the total fits text_cap (read
  * dev_line_off[n] and call again with a larger buffer otherwise).  No NUL terminator. */
-typedef struct {
-    uint8_t  type;      /* MgenMsg::AddressType: 1 IPv4, 2 IPv6 */
-    uint8_t  len;       /* address length (4 / 16) */
-    uint16_t port;
-    uint8_t  addr[16];  /* network byte order */
-} mgenx_addr;           /* 20 bytes */
 
 #define MGENX_PROTO_UDP  1   /* Protocol (include/mgenGlobals.h:61-68) */
 #define MGENX_PROTO_TCP  2

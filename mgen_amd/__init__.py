@@ -32,6 +32,7 @@ EXPORTED_SYMBOLS = (
     "mgenx_stream_scan", "mgenx_flow_init", "mgenx_flow_reduce", "mgenx_flow_export",
     "mgenx_log_recv_text", "mgenx_log_recv_binary", "mgenx_comm_unique_id", "mgenx_comm_init",
     "mgenx_comm_destroy", "mgenx_allreduce_flows", "mgenx_allgather_u64",
+    "mgenx_flow_table_create", "mgenx_flow_table_destroy", "mgenx_flow_lookup",
 )
 DIAG_SYMBOLS = ("mgenx_set_tuning", "mgenx_diag_stream_read", "mgenx_diag_group_rw")
 
@@ -74,6 +75,9 @@ def load(diag: bool = False):
     L.mgenx_comm_destroy.argtypes = [P]
     L.mgenx_allreduce_flows.argtypes = [P, P, P, u32, P]
     L.mgenx_allgather_u64.argtypes = [P, P, P, P, u32, P]
+    L.mgenx_flow_table_create.argtypes = [P, u32, ctypes.POINTER(P)]
+    L.mgenx_flow_table_destroy.argtypes = [P]
+    L.mgenx_flow_lookup.argtypes = [P, P, ctypes.POINTER(MgenxCols), P, u32, P, P, P]
     if diag:
         L.mgenx_set_tuning.argtypes = [P, i32, i32]
         L.mgenx_diag_stream_read.argtypes = [P, P, u64, P, i32, P]
@@ -350,6 +354,30 @@ class Engine:
     def allgather_u64(self, comm, src, dst, count):
         self._check(self.lib.mgenx_allgather_u64(self.ctx, comm, _ptr(src), _ptr(dst), count,
                                                  _stream(self.device)), "mgenx_allgather_u64")
+
+    # ------------------------------------------------------------ FindFlow
+    def flow_table(self, max_flows: int):
+        t = ctypes.c_void_p()
+        self._check(self.lib.mgenx_flow_table_create(self.ctx, max_flows, ctypes.byref(t)),
+                    "mgenx_flow_table_create")
+        return t
+
+    def flow_table_destroy(self, t):
+        self.lib.mgenx_flow_table_destroy(t)
+
+    def flow_lookup(self, table, cols, src, n, flow_idx=None, n_flows=None):
+        """Dense flow index per record (mgenx_flow_lookup); returns (flow_idx, n_flows)."""
+        torch = self.torch
+        dev = src.device
+        if flow_idx is None:
+            flow_idx = torch.empty(n, dtype=torch.int32, device=dev)
+        if n_flows is None:
+            n_flows = torch.zeros(1, dtype=torch.int32, device=dev)
+        cs = self._cols_struct(cols)
+        self._check(self.lib.mgenx_flow_lookup(self.ctx, table, ctypes.byref(cs), _ptr(src), n,
+                                               _ptr(flow_idx), _ptr(n_flows),
+                                               _stream(self.device)), "mgenx_flow_lookup")
+        return flow_idx, n_flows
 
     def crc32(self, data, off, length, n, out=None):
         if out is None:

@@ -26,7 +26,6 @@
 
 namespace mgenx {
 
-constexpr int kFlowThreads = 64;
 constexpr uint32_t kDepth = 1024;
 
 struct Tm {
@@ -60,18 +59,28 @@ __device__ __forceinline__ bool tge(Tm a, Tm b) {
 // the state array stores it relative to `first` (bit i <-> first + i), converted on entry
 // and exit.  (The shifting form scanned and moved 32 words whenever an index arrived below
 // `first` -- every reordered message after a window slide -- and dominated the kernel.)
-struct Ring {
-  uint32_t* w;  // word k at w[k * kFlowThreads]
+// The same ring with one WAVE per flow: ring word w (0..31) lives in lane w's register, every
+// scalar of the state machine is wave-uniform (SGPRs, scalar branches), a bit is read with
+// one v_readlane and set with one masked VALU op, and the rare range clears and searches
+// are lane-parallel with a wave reduction.  Records of the flow are loaded 64 at a time
+// (lane k holds record i0 + k, coalesced) and walked in order through v_readlane.
+struct WRing {
+  uint32_t w;           // this lane's ring word (lanes 32..63 hold 0)
   uint32_t first, last, n;
-  __device__ uint32_t& word(uint32_t k) { return w[(k & 31u) * kFlowThreads]; }
-  __device__ bool bit(uint32_t s) { return (word(s >> 5 & 31u) >> (s & 31u)) & 1u; }
-  __device__ void setbit(uint32_t s) { word(s >> 5 & 31u) |= 1u << (s & 31u); }
-  __device__ void clear() {  // `first` is kept (stale), as the restatement keeps it
-    for (int k = 0; k < 32; k++) word(k) = 0;
+  uint32_t lane;
+  __device__ uint32_t word(uint32_t k) const {  // k uniform
+    return (uint32_t)__builtin_amdgcn_readlane((int)w, (int)(k & 31u));
+  }
+  __device__ bool bit(uint32_t s) const { return (word(s >> 5) >> (s & 31u)) & 1u; }
+  __device__ void setbit(uint32_t s) {
+    w |= (lane == ((s >> 5) & 31u)) ? (1u << (s & 31u)) : 0u;
+  }
+  __device__ void clear() {
+    w = 0;
     n = 0;
   }
-  __device__ uint32_t get_last() { return n ? last : first; }
-  __device__ bool test(uint32_t idx) {
+  __device__ uint32_t get_last() const { return n ? last : first; }
+  __device__ bool test(uint32_t idx) const {
     if (!n) return false;
     const int32_t d = (int32_t)(idx - first);
     if (d < 0 || (uint32_t)d >= kDepth) return false;
@@ -95,11 +104,33 @@ struct Ring {
       }
       return true;
     }
-    if (last - idx >= kDepth) return false;  // precedes first: allowed while span < depth
+    if (last - idx >= kDepth) return false;
     setbit(idx);
     first = idx;
     n++;
     return true;
+  }
+  // lane mask of ring positions p with (p - a) mod 1024 < len (len < 1024) in this lane's
+  // word: bit j has distance d0 + j, which wraps to 0 at j = 1024 - d0 when d0 > 992
+  __device__ uint32_t range_mask(uint32_t a, uint32_t len) const {
+    auto low = [](uint32_t k) { return k >= 32u ? 0xFFFFFFFFu : ((1u << k) - 1u); };
+    const uint32_t d0 = (lane * 32u - a) & 1023u;
+    uint32_t m = len > d0 ? low(min(min(32u, 1024u - d0), len - d0)) : 0u;
+    if (d0 > 992u) {
+      const uint32_t w0 = 1024u - d0;
+      m |= low(min(32u - w0, len)) << w0;
+    }
+    return lane < 32u ? m : 0u;
+  }
+  __device__ static uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
+    return v;
+  }
+  __device__ static uint32_t wave_min(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o));
+    return v;
   }
   // clear indices first .. first + count - 1, then re-base `first` on the lowest left
   __device__ void unset_from_first(uint32_t count) {
@@ -108,97 +139,109 @@ struct Ring {
       clear();
       return;
     }
-    uint32_t s = first;
-    uint32_t left = count;
-    while (left) {
-      const uint32_t b = s & 31u, take = min(32u - b, left);
-      const uint32_t m = (take == 32u ? 0xFFFFFFFFu : ((1u << take) - 1u)) << b;
-      uint32_t& x = word(s >> 5 & 31u);
-      n -= __popc(x & m);
-      x &= ~m;
-      s += take;
-      left -= take;
+    w &= ~range_mask(first & 1023u, count);
+    n = (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_sum((uint32_t)__popc(w)));
+    // lowest set index at or after s = first + count, in ring order from s (last is set)
+    const uint32_t s = first + count;
+    const uint32_t a = s & 1023u;
+    uint32_t best = 0xFFFFFFFFu;
+    if (w) {
+      // the set bit of this word with the smallest distance from a (mod 1024)
+      const uint32_t lo = lane * 32u;
+      const uint32_t sh = (a >= lo && a < lo + 32u) ? (a - lo) : 0u;
+      const uint32_t hi_part = w & (0xFFFFFFFFu << sh);  // bits at/after a in this word
+      if (a >= lo && a < lo + 32u && hi_part) best = (uint32_t)(__ffs(hi_part) - 1) + lo - a;
+      else if (a >= lo && a < lo + 32u) best = (uint32_t)(__ffs(w) - 1) + lo + 1024u - a;
+      else best = ((uint32_t)(__ffs(w) - 1) + lo - a) & 1023u;
     }
-    // lowest set index at or after s (last is still set)
-    for (;;) {
-      const uint32_t b = s & 31u;
-      const uint32_t x = word(s >> 5 & 31u) >> b;
-      if (x) {
-        first = s + (uint32_t)(__ffs(x) - 1);
-        return;
-      }
-      s += 32u - b;
-    }
+    first = s + (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_min(best));
   }
-  // relative form (bit i of words rel <-> first + i) <-> ring
-  __device__ void load_relative(const uint32_t* rel) {
-    for (int k = 0; k < 32; k++) word(k) = 0;
+  __device__ void load_relative(const uint32_t* rel) {  // bit i of rel <-> first + i
     const uint32_t fs = first & 1023u, fw = fs >> 5, bs = fs & 31u;
-    for (uint32_t k = 0; k < 32; k++) {
-      const uint32_t v = rel[k];
-      word(fw + k) |= v << bs;
-      if (bs) word(fw + k + 1) |= v >> (32u - bs);
-    }
+    const uint32_t k = (lane - fw) & 31u;
+    const uint32_t a = rel[k], b = rel[(k - 1u) & 31u];
+    // ring word = this relative word shifted up by bs, plus the previous relative word's top
+    // bits (relative word 31's land in ring word fw: relative indices wrap at 1024)
+    uint32_t v = a << bs;
+    if (bs) v |= b >> (32u - bs);
+    w = lane < 32u ? v : 0u;
     last = first;
-    for (int k = 31; k >= 0; k--)
-      if (rel[k]) { last = first + 32u * k + (31u - __clz(rel[k])); break; }
+    // highest set relative bit
+    uint32_t top = 0;
+    const uint32_t rk = lane < 32u ? rel[lane] : 0u;
+    const uint32_t cand = rk ? lane * 32u + (31u - __clz(rk)) + 1u : 0u;  // +1: 0 = none
+    uint32_t mx = cand;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+    top = (uint32_t)__builtin_amdgcn_readfirstlane((int)mx);
+    if (top) last = first + top - 1u;
   }
-  __device__ void store_relative(uint32_t* rel) {
+  __device__ void store_relative(uint32_t* rel) const {
     const uint32_t fs = first & 1023u, fw = fs >> 5, bs = fs & 31u;
-    for (uint32_t k = 0; k < 32; k++) {
-      uint32_t v = word(fw + k) >> bs;
-      if (bs) v |= word(fw + k + 1) << (32u - bs);
-      rel[k] = n ? v : 0u;
-    }
-    if (!n) return;
-    // bits of the ring that lie past `last` (none: the span is < 1024) stay zero
+    const uint32_t src0 = (fw + lane) & 31u, src1 = (fw + lane + 1u) & 31u;
+    const uint32_t x0 = (uint32_t)__shfl((int)w, (int)src0), x1 = (uint32_t)__shfl((int)w, (int)src1);
+    uint32_t v = x0 >> bs;
+    if (bs) v |= x1 << (32u - bs);
+    if (lane < 32u) rel[lane] = n ? v : 0u;
   }
 };
 
-struct Rec {
-  uint32_t seq, txs, txu, rxs, rxu, len;
+// One received record as the update kernel reads it (written by flow_keys_kernel in input
+// order, read through the flow-sorted order): 24 bytes.  The latency ProtoTime::Delta(rx, tx)
+// depends on the record alone, so it is computed there, in parallel.
+struct FRec {
+  uint32_t seq, rxs, rxu, len;
+  double latency;
 };
 
-__global__ void __launch_bounds__(kFlowThreads)
-flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
-                   const uint32_t* __restrict__ begin, const uint32_t* __restrict__ end,
-                   const uint32_t* __restrict__ s_seq, const uint32_t* __restrict__ s_txs,
-                   const uint32_t* __restrict__ s_txu, const uint32_t* __restrict__ s_rxs,
-                   const uint32_t* __restrict__ s_rxu, const uint16_t* __restrict__ s_len,
-                   mgenx_flow_report* __restrict__ reports, uint32_t per_flow,
-                   uint32_t* __restrict__ report_count) {
-  __shared__ uint32_t lds[32 * kFlowThreads];
-  const uint32_t f = blockIdx.x * kFlowThreads + threadIdx.x;
+// Wave-uniform values: the window times come out of FP64 arithmetic (VALU), so without
+// these the compiler treats every later compare and branch on them as divergent.
+__device__ __forceinline__ int64_t uni64(int64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)v >> 32));
+  return (int64_t)((uint64_t)hi << 32 | lo);
+}
+__device__ __forceinline__ Tm uni_t(Tm t) { return Tm{uni64(t.sec), uni64(t.usec)}; }
+
+__global__ void __launch_bounds__(256)
+flow_update_wave_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
+                        const uint32_t* __restrict__ begin, const uint32_t* __restrict__ end,
+                        const uint32_t* __restrict__ order, const FRec* __restrict__ recs,
+                        mgenx_flow_report* __restrict__ reports, uint32_t per_flow,
+                        uint32_t* __restrict__ report_count) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t f = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
   if (f >= n_flows) return;
   const uint32_t b = begin[f], e = end[f];
   if (b >= e) return;
-  mgenx_flow_state st = flows[f];
-  Ring m;
-  m.w = lds + threadIdx.x;
-  m.first = st.mask_first;
-  m.n = st.mask_n;
-  m.load_relative(flows[f].mask);  // straight from memory: no 128-B local copy
-  bool valid = st.window_valid != 0;
-  Tm ws = {st.win_start_sec, st.win_start_usec}, we = {st.win_end_sec, st.win_end_usec};
-  uint32_t seq_start = st.seq_start;
-  uint64_t msg_count = st.msg_count, byte_count = st.byte_count, dups = st.dup_count;
-  double lsum = st.latency_sum, lmin = st.latency_min, lmax = st.latency_max;
-  uint64_t nrep = st.n_reports;
+  mgenx_flow_state* sp = flows + f;
+  const double window = sp->window_size;
+  WRing m;
+  m.lane = lane;
+  m.first = sp->mask_first;
+  m.n = sp->mask_n;
+  m.load_relative(sp->mask);
+  if (!m.n) m.w = 0;
+  bool valid = sp->window_valid != 0;
+  Tm ws = {sp->win_start_sec, sp->win_start_usec}, we = {sp->win_end_sec, sp->win_end_usec};
+  uint32_t seq_start = sp->seq_start;
+  uint64_t msg_count = sp->msg_count, byte_count = sp->byte_count, dups = sp->dup_count;
+  double lsum = sp->latency_sum, lmin = sp->latency_min, lmax = sp->latency_max;
+  uint64_t nrep = sp->n_reports;
   uint32_t rcount = report_count[f];
 
-  auto update = [&](const Rec& r) {
-    const Tm rx = {(int64_t)r.rxs, (int64_t)r.rxu}, tx = {(int64_t)r.txs, (int64_t)r.txu};
-    const uint32_t msg = r.len;
+  auto update = [&](uint32_t seq, uint32_t rxs, uint32_t rxu, uint32_t msg, double lat) {
+    const Tm rx = {(int64_t)rxs, (int64_t)rxu};
     if (!valid) {  // mgenAnalytic.cpp:80-99
       valid = true;
       ws = rx;
-      we = tadd(rx, st.window_size);
+      we = uni_t(tadd(rx, window));
       if (msg != 0) {
-        m.set(r.seq);
-        seq_start = r.seq;
+        m.set(seq);
+        seq_start = seq;
         msg_count = 1;
         byte_count = msg;
-        lsum = lmin = lmax = tdelta(rx, tx);
+        lsum = lmin = lmax = lat;
       } else {
         msg_count = byte_count = 0;
         lsum = lmin = lmax = 0.0;
@@ -208,73 +251,88 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
     double latency = 0.0;
     if (msg != 0) {  // :102-178
       if (m.n) {
-        if (m.test(r.seq)) {
+        if (m.test(seq)) {
           dups++;
-        } else if ((int32_t)(r.seq - seq_start) < 0) {
-          m.set(r.seq);
+        } else if ((int32_t)(seq - seq_start) < 0) {
+          m.set(seq);
         } else {
-          if (!m.set(r.seq)) {  // UnsetBits(first, seq - first), then Set (:120-127)
-            m.unset_from_first(r.seq - m.first);
-            m.set(r.seq);
+          if (!m.set(seq)) {  // UnsetBits(first, seq - first), then Set (:120-127)
+            m.unset_from_first(seq - m.first);
+            m.set(seq);
           }
           if (1 == msg_count) byte_count = msg;
           else byte_count += msg;
-          latency = tdelta(rx, tx);
+          latency = lat;
           if (0 == msg_count) {
             lsum = lmin = lmax = latency;
           } else {
             lsum = __dadd_rn(lsum, latency);
-            if (latency < lmin) lmin = latency;
-            else if (latency > lmax) lmax = latency;
+            // if (latency < lmin) lmin = latency; else if (latency > lmax) lmax = latency;
+            // as value selects (a branch here lets LLVM fold the two stores into one store
+            // through a selected pointer, which sends lmin/lmax to scratch memory)
+            const bool lo = latency < lmin;
+            const bool hi = !lo && latency > lmax;
+            lmin = lo ? latency : lmin;
+            lmax = hi ? latency : lmax;
           }
           msg_count++;
         }
       } else {
         m.clear();
-        m.set(r.seq);
-        seq_start = r.seq;
+        m.set(seq);
+        seq_start = seq;
         byte_count = msg;
-        lsum = lmin = lmax = tdelta(rx, tx);
+        lsum = lmin = lmax = lat;
         msg_count = 1;
       }
     }
     if (tge(rx, we)) {  // :180-256: report and restart the window
-      mgenx_flow_report rep;
-      rep.flow = f;
-      rep.index = rcount;
-      rep.start_sec = ws.sec;
-      rep.start_usec = ws.usec;
-      rep.duration = tdelta(rx, ws);
-      rep.rx_sec = rx.sec;
-      rep.rx_usec = rx.usec;
       const uint32_t seq_max = m.n ? m.get_last() : seq_start;
+      const double duration = tdelta(rx, ws);
+      uint64_t r_count;
+      double r_rate, r_loss, r_ave, r_min, r_max;
       if (msg_count == 0) {
-        rep.msg_count = 0;
-        rep.rate = 0.0;
-        rep.loss = 1.0;
-        rep.latency_ave = rep.latency_min = rep.latency_max = -1.0;
+        r_count = 0;
+        r_rate = 0.0;
+        r_loss = 1.0;
+        r_ave = r_min = r_max = -1.0;
       } else if (msg_count == 1) {
-        rep.msg_count = 1;
-        rep.rate = __ddiv_rn((double)byte_count, rep.duration);
-        rep.loss = 0.0;
-        rep.latency_ave = lsum;
-        rep.latency_min = lmin;
-        rep.latency_max = lmax;
+        r_count = 1;
+        r_rate = __ddiv_rn((double)byte_count, duration);
+        r_loss = 0.0;
+        r_ave = lsum;
+        r_min = lmin;
+        r_max = lmax;
       } else {
-        rep.msg_count = msg_count - 1;
-        rep.rate = __ddiv_rn((double)byte_count, rep.duration);
+        r_count = msg_count - 1;
+        r_rate = __ddiv_rn((double)byte_count, duration);
         const uint32_t delta = seq_max - seq_start;
-        rep.loss = delta <= 1 ? 0.0
-                              : __dsub_rn(1.0, __ddiv_rn((double)msg_count, (double)(delta + 1)));
-        rep.latency_ave = __ddiv_rn(lsum, (double)msg_count);
-        rep.latency_min = lmin;
-        rep.latency_max = lmax;
+        r_loss = delta <= 1 ? 0.0
+                            : __dsub_rn(1.0, __ddiv_rn((double)msg_count, (double)(delta + 1)));
+        r_ave = __ddiv_rn(lsum, (double)msg_count);
+        r_min = lmin;
+        r_max = lmax;
       }
-      if (rcount < per_flow) reports[(size_t)f * per_flow + rcount] = rep;
+      if (rcount < per_flow && lane == 0) {
+        mgenx_flow_report* rp = reports + (size_t)f * per_flow + rcount;
+        rp->flow = f;
+        rp->index = rcount;
+        rp->start_sec = ws.sec;
+        rp->start_usec = ws.usec;
+        rp->duration = duration;
+        rp->msg_count = r_count;
+        rp->rate = r_rate;
+        rp->loss = r_loss;
+        rp->latency_ave = r_ave;
+        rp->latency_min = r_min;
+        rp->latency_max = r_max;
+        rp->rx_sec = rx.sec;
+        rp->rx_usec = rx.usec;
+      }
       rcount++;
       nrep++;
       ws = rx;
-      we = tadd(rx, st.window_size);
+      we = uni_t(tadd(rx, window));
       seq_start = seq_max;
       if (msg != 0) {
         byte_count = 0;
@@ -287,65 +345,77 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
     }
   };
 
-  constexpr int kPre = 8;
-  for (uint32_t i0 = b; i0 < e; i0 += kPre) {
-    Rec r[kPre];
-#pragma unroll
-    for (int k = 0; k < kPre; k++) {
-      const uint32_t i = min(i0 + k, e - 1);  // clamped: no divergent loads
-      r[k] = {s_seq[i], s_txs[i], s_txu[i], s_rxs[i], s_rxu[i], (uint32_t)s_len[i]};
+  // 64 records per round: lane k loads record order[i0 + k]; the next round's loads are
+  // issued before this round is walked
+  auto ld = [&](uint32_t base, FRec& r) {
+    r = recs[order[min(base + lane, e - 1u)]];
+  };
+  FRec cur, nxt;
+  uint32_t i0 = b;
+  ld(i0, cur);
+  while (i0 < e) {
+    const uint32_t cnt = min(64u, e - i0);
+    ld(i0 + 64u < e ? i0 + 64u : i0, nxt);
+    const uint64_t lbits = __builtin_bit_cast(uint64_t, cur.latency);
+    const uint32_t llo = (uint32_t)lbits, lhi = (uint32_t)(lbits >> 32);
+    for (uint32_t k = 0; k < cnt; k++) {
+      const uint64_t lb = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)lhi, (int)k) << 32 |
+                          (uint32_t)__builtin_amdgcn_readlane((int)llo, (int)k);
+      update((uint32_t)__builtin_amdgcn_readlane((int)cur.seq, (int)k),
+             (uint32_t)__builtin_amdgcn_readlane((int)cur.rxs, (int)k),
+             (uint32_t)__builtin_amdgcn_readlane((int)cur.rxu, (int)k),
+             (uint32_t)__builtin_amdgcn_readlane((int)cur.len, (int)k),
+             __builtin_bit_cast(double, lb));
     }
-#pragma unroll
-    for (int k = 0; k < kPre; k++)
-      if (i0 + k < e) update(r[k]);
+    cur = nxt;
+    i0 += 64u;
   }
 
-  m.store_relative(flows[f].mask);
-  st.mask_first = m.first;
-  st.mask_n = m.n;
-  st.window_valid = valid ? 1u : 0u;
-  st.win_start_sec = ws.sec;
-  st.win_start_usec = ws.usec;
-  st.win_end_sec = we.sec;
-  st.win_end_usec = we.usec;
-  st.seq_start = seq_start;
-  st.msg_count = msg_count;
-  st.byte_count = byte_count;
-  st.dup_count = dups;
-  st.latency_sum = lsum;
-  st.latency_min = lmin;
-  st.latency_max = lmax;
-  st.n_reports = nrep;
-  // scalar fields back (the mask words were written in place above)
-  mgenx_flow_state& o = flows[f];
-  o.mask_first = st.mask_first; o.mask_n = st.mask_n; o.seq_start = st.seq_start;
-  o.window_valid = st.window_valid; o.win_start_sec = st.win_start_sec;
-  o.win_start_usec = st.win_start_usec; o.win_end_sec = st.win_end_sec;
-  o.win_end_usec = st.win_end_usec; o.msg_count = st.msg_count; o.byte_count = st.byte_count;
-  o.dup_count = st.dup_count; o.latency_sum = st.latency_sum; o.latency_min = st.latency_min;
-  o.latency_max = st.latency_max; o.n_reports = st.n_reports;
-  report_count[f] = rcount;
+  m.store_relative(sp->mask);
+  if (lane == 0) {
+    sp->mask_first = m.first;
+    sp->mask_n = m.n;
+    sp->window_valid = valid ? 1u : 0u;
+    sp->win_start_sec = ws.sec;
+    sp->win_start_usec = ws.usec;
+    sp->win_end_sec = we.sec;
+    sp->win_end_usec = we.usec;
+    sp->seq_start = seq_start;
+    sp->msg_count = msg_count;
+    sp->byte_count = byte_count;
+    sp->dup_count = dups;
+    sp->latency_sum = lsum;
+    sp->latency_min = lmin;
+    sp->latency_max = lmax;
+    sp->n_reports = nrep;
+    report_count[f] = rcount;
+  }
 }
 
-// keys: flow index clamped to n_flows (records to skip sort last); vals: record index
+// keys: flow index clamped to n_flows (records to skip sort last); vals: record index;
+// recs: the record as the update kernel reads it, with its latency
 __global__ void flow_keys_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows,
-                                 uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+                                 const uint32_t* __restrict__ seq, const uint32_t* __restrict__ txs,
+                                 const uint32_t* __restrict__ txu, const uint16_t* __restrict__ len,
+                                 const uint32_t* __restrict__ rxs, const uint32_t* __restrict__ rxu,
+                                 uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
+                                 FRec* __restrict__ recs) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   keys[i] = min(idx[i], n_flows);
   vals[i] = i;
+  FRec r;
+  r.seq = seq[i];
+  r.rxs = rxs[i];
+  r.rxu = rxu[i];
+  r.len = len[i];
+  r.latency = tdelta(Tm{(int64_t)r.rxs, (int64_t)r.rxu}, Tm{(int64_t)txs[i], (int64_t)txu[i]});
+  recs[i] = r;
 }
 
-// segment bounds of each flow in the sorted keys, and the flow-contiguous record fields
-__global__ void flow_gather_kernel(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ order,
-                                   uint32_t n, uint32_t n_flows, uint32_t* __restrict__ begin,
-                                   uint32_t* __restrict__ end, const uint32_t* __restrict__ seq,
-                                   const uint32_t* __restrict__ txs, const uint32_t* __restrict__ txu,
-                                   const uint16_t* __restrict__ len, const uint32_t* __restrict__ rxs,
-                                   const uint32_t* __restrict__ rxu, uint32_t* __restrict__ o_seq,
-                                   uint32_t* __restrict__ o_txs, uint32_t* __restrict__ o_txu,
-                                   uint16_t* __restrict__ o_len, uint32_t* __restrict__ o_rxs,
-                                   uint32_t* __restrict__ o_rxu) {
+// segment bounds of each flow in the sorted keys
+__global__ void flow_bounds_kernel(const uint32_t* __restrict__ keys, uint32_t n, uint32_t n_flows,
+                                   uint32_t* __restrict__ begin, uint32_t* __restrict__ end) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t k = keys[i];
@@ -353,13 +423,6 @@ __global__ void flow_gather_kernel(const uint32_t* __restrict__ keys, const uint
     if (i == 0 || keys[i - 1] != k) begin[k] = i;
     if (i + 1 == n || keys[i + 1] != k) end[k] = i + 1;
   }
-  const uint32_t r = order[i];
-  o_seq[i] = seq[r];
-  o_txs[i] = txs[r];
-  o_txu[i] = txu[r];
-  o_len[i] = len[r];
-  o_rxs[i] = rxs[r];
-  o_rxu[i] = rxu[r];
 }
 
 __global__ void flow_init_kernel(mgenx_flow_state* flows, uint32_t n_flows, double window) {
@@ -455,9 +518,10 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
   (void)hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, (const uint32_t*)nullptr,
                                            (uint32_t*)nullptr, (const uint32_t*)nullptr,
                                            (uint32_t*)nullptr, (int)n, 0, end_bit, stream);
-  // layout: keys_in, keys_out, vals_in, vals_out, begin, end, 5 x u32 fields, u16 len, cub
+  // layout: keys_in, keys_out, vals_in, vals_out, begin, end, records (24 B), cub
   const size_t nb = a256((size_t)n * 4), fb = a256((size_t)n_flows * 4);
-  const size_t need = 4 * nb + 2 * fb + 5 * nb + a256((size_t)n * 2) + a256(cub_bytes);
+  const size_t rb = a256((size_t)n * sizeof(FRec));
+  const size_t need = 4 * nb + 2 * fb + rb + a256(cub_bytes);
   if (ws.bytes < need) {
     if (ws.mem) (void)hipFree(ws.mem);
     ws.mem = nullptr;
@@ -476,16 +540,11 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
   uint32_t* vals_out = (uint32_t*)take(nb);
   uint32_t* d_begin = (uint32_t*)take(fb);
   uint32_t* d_end = (uint32_t*)take(fb);
-  uint32_t* o_seq = (uint32_t*)take(nb);
-  uint32_t* o_txs = (uint32_t*)take(nb);
-  uint32_t* o_txu = (uint32_t*)take(nb);
-  uint32_t* o_rxs = (uint32_t*)take(nb);
-  uint32_t* o_rxu = (uint32_t*)take(nb);
-  uint16_t* o_len = (uint16_t*)take(a256((size_t)n * 2));
+  FRec* recs = (FRec*)take(rb);
   void* cub_tmp = take(a256(cub_bytes));
   const dim3 g((n + 255) / 256);
-  hipLaunchKernelGGL(flow_keys_kernel, g, dim3(256), 0, stream, flow_idx, n, n_flows, keys_in,
-                     vals_in);
+  hipLaunchKernelGGL(flow_keys_kernel, g, dim3(256), 0, stream, flow_idx, n, n_flows, seq, txs,
+                     txu, len, rxs, rxu, keys_in, vals_in, recs);
   hipError_t e = hipcub::DeviceRadixSort::SortPairs(cub_tmp, cub_bytes, keys_in, keys_out,
                                                     vals_in, vals_out, (int)n, 0, end_bit, stream);
   if (e != hipSuccess) {
@@ -494,12 +553,11 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
   }
   (void)hipMemsetAsync(d_begin, 0, fb, stream);
   (void)hipMemsetAsync(d_end, 0, fb, stream);
-  hipLaunchKernelGGL(flow_gather_kernel, g, dim3(256), 0, stream, keys_out, vals_out, n, n_flows,
-                     d_begin, d_end, seq, txs, txu, len, rxs, rxu, o_seq, o_txs, o_txu, o_len,
-                     o_rxs, o_rxu);
-  hipLaunchKernelGGL(flow_update_kernel, dim3((n_flows + kFlowThreads - 1) / kFlowThreads),
-                     dim3(kFlowThreads), 0, stream, flows, n_flows, d_begin, d_end, o_seq, o_txs,
-                     o_txu, o_rxs, o_rxu, o_len, reports, per_flow, report_count);
+  hipLaunchKernelGGL(flow_bounds_kernel, g, dim3(256), 0, stream, keys_out, n, n_flows, d_begin,
+                     d_end);
+  hipLaunchKernelGGL(flow_update_wave_kernel, dim3((n_flows + 3) / 4), dim3(256), 0, stream,
+                     flows, n_flows, d_begin, d_end, vals_out, recs, reports, per_flow,
+                     report_count);
   e = hipGetLastError();
   if (e != hipSuccess) {
     snprintf(err, errn, "flow_reduce: %s", hipGetErrorString(e));

@@ -1,0 +1,267 @@
+// mgenx_flowtab.hip -- MgenAnalyticTable::FindFlow for whole batches on gfx950.
+//
+// Reference: MgenAnalyticTable::FindFlow (src/common/mgenAnalytic.cpp:312-328) looks a flow
+// up by the key dst addr | dst port | src addr | src port | flowId (ProtoIndexedQueue over
+// at most 320 bits), and Mgen::UpdateRecvAnalytics (src/common/mgen.cpp:1034-1053) creates
+// the MgenAnalytic on first sight.  Here one call maps n records to dense flow indices:
+//   1. insert: open addressing (linear probing) over 64-byte slots in HBM; a slot is claimed
+//      by CAS on its state word, the claimant writes the key, then publishes it; lookups of
+//      the same key spin (bounded) until it is published.  The first record of each new key
+//      is kept with atomicMin;
+//   2. number: new keys get the next dense indices in the order of their first record (an
+//      exclusive scan over the "first record of a new key" flags), so the mapping does not
+//      depend on thread timing;
+//   3. resolve: every record reads its slot's index.
+// Records with an error (err != 0) map to MGENX_FLOW_NONE, as the reference only updates
+// analytics for good messages (mgenTransport.cpp:976-985).
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <stdio.h>
+#include <string.h>
+
+#include "mgenx_kernels.hpp"
+
+namespace mgenx {
+
+constexpr uint32_t kSlotEmpty = 0u, kSlotBusy = 0xFFFFFFFFu;
+
+struct FlowKey {  // 48 bytes: the reference key's fields, zero-padded
+  uint32_t w[12];
+};
+
+struct FlowSlot {  // 64 bytes
+  FlowKey key;
+  uint32_t state;      // 0 empty, kSlotBusy being written, else 1 + slot tag
+  uint32_t index;      // dense flow index (kSlotBusy until numbered)
+  uint32_t first_rec;  // first record of this call that inserted/looked it up when new
+  uint32_t is_new;     // created by the current call
+};
+
+__device__ __forceinline__ uint32_t mix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x7feb352du;
+  h ^= h >> 15;
+  h *= 0x846ca68bu;
+  h ^= h >> 16;
+  return h;
+}
+
+// key of record i: dst (len, port, 16 addr bytes), src (mgenx_addr), flow id
+__device__ __forceinline__ FlowKey make_key(const mgenx_cols& c, const mgenx_addr* src, uint32_t i) {
+  FlowKey k;
+  const uint32_t* da = reinterpret_cast<const uint32_t*>(c.dst_addr + (size_t)i * 16);
+  const uint32_t* sa = reinterpret_cast<const uint32_t*>(src[i].addr);
+  const uint32_t dl = c.dst_len[i], sl = src[i].len;
+  // bytes past an address's length are not part of the reference key: masked to zero
+  auto mask_to = [](uint32_t word, uint32_t wi, uint32_t len) {
+    const uint32_t lo = 4u * wi;
+    if (len >= lo + 4u) return word;
+    if (len <= lo) return 0u;
+    return word & ((1u << (8u * (len - lo))) - 1u);
+  };
+#pragma unroll
+  for (int j = 0; j < 4; j++) k.w[j] = mask_to(da[j], j, dl);
+#pragma unroll
+  for (int j = 0; j < 4; j++) k.w[4 + j] = mask_to(sa[j], j, sl);
+  k.w[8] = dl | (uint32_t)c.dst_port[i] << 16;
+  k.w[9] = sl | (uint32_t)src[i].port << 16;
+  k.w[10] = c.flow_id[i];
+  k.w[11] = 0x4D47u;
+  return k;
+}
+
+__device__ __forceinline__ uint32_t key_hash(const FlowKey& k) {
+  uint32_t h = 0x9E3779B9u;
+#pragma unroll
+  for (int j = 0; j < 11; j++) h = mix32(h ^ k.w[j]) + (uint32_t)j;
+  return h;
+}
+
+// a published slot's key never changes: after the acquire load of its state, plain
+// (vector) loads of the key words are safe
+__device__ __forceinline__ bool key_eq(const FlowKey& a, const FlowSlot& s) {
+  const u32x4_t* kw = reinterpret_cast<const u32x4_t*>(s.key.w);
+  bool eq = true;
+#pragma unroll
+  for (int j = 0; j < 3; j++) {
+    const u32x4_t v = kw[j];
+    eq &= a.w[4 * j] == v.x && a.w[4 * j + 1] == v.y && a.w[4 * j + 2] == v.z &&
+          a.w[4 * j + 3] == v.w;
+  }
+  return eq;
+}
+
+__global__ void flowtab_insert_kernel(FlowSlot* __restrict__ tab, uint32_t cap_mask, mgenx_cols c,
+                                      const mgenx_addr* __restrict__ src, uint32_t n,
+                                      uint32_t* __restrict__ rec_slot, uint32_t* __restrict__ overflow) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (c.err && c.err[i] != 0) {
+    rec_slot[i] = kSlotBusy;
+    return;
+  }
+  const FlowKey k = make_key(c, src, i);
+  uint32_t s = key_hash(k) & cap_mask;
+  for (uint32_t probe = 0; probe <= cap_mask; probe++, s = (s + 1) & cap_mask) {
+    FlowSlot& sl = tab[s];
+    uint32_t st = __hip_atomic_load(&sl.state, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    if (st == kSlotEmpty) {
+      uint32_t exp = kSlotEmpty;
+      if (__hip_atomic_compare_exchange_strong(&sl.state, &exp, kSlotBusy, __ATOMIC_ACQ_REL,
+                                               __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) {
+#pragma unroll
+        for (int j = 0; j < 12; j++)
+          __hip_atomic_store(&sl.key.w[j], k.w[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&sl.first_rec, i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&sl.is_new, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&sl.index, kSlotBusy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&sl.state, 1u + s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        rec_slot[i] = s;
+        return;
+      }
+      st = exp;
+    }
+    // a slot being written: wait (bounded) until its key is published
+    for (int spin = 0; st == kSlotBusy && spin < 1 << 20; spin++) {
+      __builtin_amdgcn_s_sleep(1);
+      st = __hip_atomic_load(&sl.state, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (st == kSlotBusy) break;  // never published: report and give up on this record
+    if (key_eq(k, sl)) {
+      // a key new in this call keeps its first record (most lookups see a smaller one
+      // already and skip the atomic)
+      if (__hip_atomic_load(&sl.is_new, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &&
+          __hip_atomic_load(&sl.first_rec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > i)
+        __hip_atomic_fetch_min(&sl.first_rec, i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      rec_slot[i] = s;
+      return;
+    }
+  }
+  rec_slot[i] = kSlotBusy;
+  __hip_atomic_fetch_add(overflow, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// flag[i] = 1 when record i is the first record of a key created by this call
+__global__ void flowtab_first_kernel(const FlowSlot* __restrict__ tab, const uint32_t* __restrict__ rec_slot,
+                                     uint32_t n, uint32_t* __restrict__ flag) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t s = rec_slot[i];
+  flag[i] = (s != kSlotBusy && tab[s].is_new && tab[s].first_rec == i) ? 1u : 0u;
+}
+
+__global__ void flowtab_number_kernel(FlowSlot* __restrict__ tab, const uint32_t* __restrict__ rec_slot,
+                                      const uint32_t* __restrict__ flag, const uint32_t* __restrict__ pos,
+                                      uint32_t n, uint32_t* __restrict__ n_flows) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (flag[i]) tab[rec_slot[i]].index = n_flows[0] + pos[i];
+}
+
+__global__ void flowtab_resolve_kernel(FlowSlot* __restrict__ tab, const uint32_t* __restrict__ rec_slot,
+                                       const uint32_t* __restrict__ flag, const uint32_t* __restrict__ pos,
+                                       uint32_t n, uint32_t* __restrict__ flow_idx,
+                                       uint32_t* __restrict__ n_flows) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t s = rec_slot[i];
+  flow_idx[i] = s == kSlotBusy ? MGENX_FLOW_NONE : tab[s].index;
+  if (i == n - 1) n_flows[1] = n_flows[0] + pos[i] + flag[i];  // new total (published below)
+}
+
+__global__ void flowtab_commit_kernel(FlowSlot* __restrict__ tab, const uint32_t* __restrict__ rec_slot,
+                                      const uint32_t* __restrict__ flag, uint32_t n,
+                                      uint32_t* __restrict__ n_flows) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && flag[i]) tab[rec_slot[i]].is_new = 0u;
+  if (i == 0) n_flows[0] = n_flows[1];
+}
+
+}  // namespace mgenx
+
+using namespace mgenx;
+
+struct mgenx_flow_table {
+  int device = 0;
+  uint32_t cap = 0;          // slots (power of two)
+  FlowSlot* slots = nullptr;
+  uint32_t* counters = nullptr;  // [0] = flows, [1] = scratch, [2] = overflow
+  void* ws = nullptr;        // per-call scratch: rec_slot, flag, pos, cub temp
+  size_t ws_bytes = 0;
+};
+
+extern "C" {
+
+int mgenx_flow_table_create(mgenx_ctx* ctx, uint32_t max_flows, mgenx_flow_table** out) {
+  if (!ctx || !out || max_flows == 0 || max_flows > (1u << 28)) return MGENX_EINVAL;
+  *out = nullptr;
+  mgenx_flow_table* t = new mgenx_flow_table();
+  t->device = mgenx_ctx_device(ctx);
+  uint32_t cap = 64;
+  while (cap < 2u * max_flows) cap <<= 1;
+  t->cap = cap;
+  if (hipSetDevice(t->device) != hipSuccess ||
+      hipMalloc((void**)&t->slots, (size_t)cap * sizeof(FlowSlot)) != hipSuccess ||
+      hipMalloc((void**)&t->counters, 256) != hipSuccess ||
+      hipMemset(t->slots, 0, (size_t)cap * sizeof(FlowSlot)) != hipSuccess ||
+      hipMemset(t->counters, 0, 256) != hipSuccess) {
+    mgenx_flow_table_destroy(t);
+    return MGENX_ENOMEM;
+  }
+  *out = t;
+  return MGENX_OK;
+}
+
+int mgenx_flow_table_destroy(mgenx_flow_table* t) {
+  if (!t) return MGENX_EINVAL;
+  if (t->slots) (void)hipFree(t->slots);
+  if (t->counters) (void)hipFree(t->counters);
+  if (t->ws) (void)hipFree(t->ws);
+  delete t;
+  return MGENX_OK;
+}
+
+int mgenx_flow_lookup(mgenx_ctx* ctx, mgenx_flow_table* t, const mgenx_cols* cols,
+                      const mgenx_addr* dev_src, uint32_t n, uint32_t* dev_flow_idx,
+                      uint32_t* dev_n_flows, void* stream) {
+  if (!ctx || !t || !cols) return MGENX_EINVAL;
+  if (n == 0) return MGENX_OK;
+  const mgenx_cols& c = *cols;
+  if (!c.dst_addr || !c.dst_len || !c.dst_port || !c.flow_id || !dev_src || !dev_flow_idx)
+    return MGENX_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  size_t cub_bytes = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, cub_bytes, (const uint32_t*)nullptr,
+                                         (uint32_t*)nullptr, (int)n, s);
+  const size_t nb = ((size_t)n * 4 + 255) & ~(size_t)255;
+  const size_t need = 3 * nb + cub_bytes + 256;
+  if (t->ws_bytes < need) {
+    if (t->ws) (void)hipFree(t->ws);
+    t->ws = nullptr;
+    t->ws_bytes = 0;
+    if (hipMalloc(&t->ws, need) != hipSuccess) return MGENX_ENOMEM;
+    t->ws_bytes = need;
+  }
+  uint32_t* rec_slot = (uint32_t*)t->ws;
+  uint32_t* flag = (uint32_t*)((char*)t->ws + nb);
+  uint32_t* pos = (uint32_t*)((char*)t->ws + 2 * nb);
+  void* cub_tmp = (char*)t->ws + 3 * nb;
+  const dim3 g((n + 255) / 256), b(256);
+  hipLaunchKernelGGL(flowtab_insert_kernel, g, b, 0, s, t->slots, t->cap - 1, c, dev_src, n,
+                     rec_slot, t->counters + 2);
+  hipLaunchKernelGGL(flowtab_first_kernel, g, b, 0, s, t->slots, rec_slot, n, flag);
+  if (hipcub::DeviceScan::ExclusiveSum(cub_tmp, cub_bytes, flag, pos, (int)n, s) != hipSuccess)
+    return MGENX_EDEVICE;
+  hipLaunchKernelGGL(flowtab_number_kernel, g, b, 0, s, t->slots, rec_slot, flag, pos, n,
+                     t->counters);
+  hipLaunchKernelGGL(flowtab_resolve_kernel, g, b, 0, s, t->slots, rec_slot, flag, pos, n,
+                     dev_flow_idx, t->counters);
+  hipLaunchKernelGGL(flowtab_commit_kernel, g, b, 0, s, t->slots, rec_slot, flag, n, t->counters);
+  if (dev_n_flows &&
+      hipMemcpyAsync(dev_n_flows, t->counters, 4, hipMemcpyDeviceToDevice, s) != hipSuccess)
+    return MGENX_EDEVICE;
+  return hipGetLastError() == hipSuccess ? MGENX_OK : MGENX_EDEVICE;
+}
+
+}  // extern "C"

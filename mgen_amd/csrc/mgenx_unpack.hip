@@ -1165,6 +1165,221 @@ unpack_fixed_kernel(UnpackParams p, uint32_t expect) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Aligned fixed-length records of NR = 8 or 16 rows (512 / 1024 B) with row output -- the
+// headline layout -- reading and writing in separate phases.  On the MI355X boxes where
+// mixing the 32-B row stores into the 1 GiB read stream costs most (config 2): the read
+// pattern alone takes 168 us, with the row stores interleaved 201 us.  So each wave keeps
+// the rows of its last K = 16 groups in registers (a shift register, 2 dwords per group and
+// lane) and stores them in one burst every K groups and at its end: for config 2 (16 groups
+// per wave) one burst, after the wave's reads (measured 0.194 ms against 0.215 ms for the
+// interleaved kernel on the same box; K = 12 with two bursts: 0.204 ms).  The registers come
+// from a shorter load ring: RS = 4 rows in flight per wave (row r + 4 of the wave's row stream
+// is loaded as row r is consumed; 4 KiB per wave, 64 KiB per CU).
+// Semantics are those of unpack_fixed_kernel<NR, 0, true, true>.
+template <int NR, int RS = 4, int K = 16>
+__global__ void __launch_bounds__(kUnpackThreads)
+unpack_fixed_ring_kernel(UnpackParams p, uint32_t expect) {
+  static_assert(NR == 8 || NR == 16, "ring kernel: 512- or 1024-byte records");
+  static_assert(NR % RS == 0, "the ring divides the record's rows");
+  // RS: rows in flight per wave; K: groups of row output held per wave before a burst
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const uint32_t* fold = lds + kRepDwords;  // [A4 | A8 | A12 | A16 | A32 | A48]
+  const uint8_t* ldsb = reinterpret_cast<const uint8_t*>(lds);
+  const TableRegs tab_regs = table_loads(p.tabs);
+  asm volatile("" ::: "memory");
+
+  const int lane = threadIdx.x & 63;
+  const int q = lane & 3;
+  const uint32_t s1 = a64_s1((uint32_t)lane);
+  const uint32_t wave_id = __builtin_amdgcn_readfirstlane(
+      blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  const uint32_t n_waves = gridDim.x * (blockDim.x >> 6);
+  const uint32_t g_end = (p.n + 15u) >> 4;
+  const bool force = (p.opts & MGENX_OPT_CHECKSUM_FORCE) != 0;
+  const bool tcp = (p.opts & MGENX_OPT_TCP) != 0;
+  const uint32_t L = p.fixed_len;  // == 64 * NR (host-checked)
+
+  auto rec_idx = [&](uint32_t gg) { return (gg << 4) + (uint32_t)(lane >> 2); };
+  auto is_live = [&](uint32_t i) {
+    const uint64_t off = (uint64_t)i * p.stride;
+    return i < p.n && off <= p.slab_bytes && L <= p.slab_bytes - off;
+  };
+  // lane's row base (32-bit offset, saddr form); a dead lane reads inside the slab at 64
+  auto row_base = [&](uint32_t gg) {
+    const uint32_t i = rec_idx(gg);
+    return (is_live(i) ? i * (uint32_t)p.stride : 64u) + 16u * (uint32_t)q;
+  };
+  auto ld = [&](uint32_t base, int j) { return ldu128(p.slab + (uint64_t)base + 64 * j); };
+  auto decide = [&](const u32x4_t& pf, bool live) {
+    const uint32_t w0 = prefix_word(pf, 0);
+    const uint32_t w5 = prefix_word(pf, 5);
+    const bool v2 = ((w0 >> 16) & 0xffu) == 2u;
+    const bool flagged = force || ((((w0 >> 24) & MGENX_FLAG_CHECKSUM) != 0) && v2);
+    const uint32_t t = (w5 >> 16) & 0xffu;
+    return live && flagged && (tcp || (v2 && (t == 1u || t == 2u)));
+  };
+  // the quad's 32-B mgenx_rec: lane q holds bytes 8q .. 8q+7 (as unpack_fixed_kernel)
+  auto decode = [&](const u32x4_t& pf, uint32_t idx, bool live, uint32_t& o0, uint32_t& o1) {
+    uint32_t w[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) w[j] = prefix_word(pf, j);
+    const uint32_t w10 = prefix_word(pf, 10);
+    const uint32_t D = w[5] >> 24;
+    const uint32_t hw = (D == 4u) ? w[7] : w10;
+    const uint32_t gi = (28u + D + (hw >> 24)) >> 2;
+    const uint32_t g3 = (prefix_word(pf, 11) & (0u - (uint32_t)(gi == 8u))) |
+                        (prefix_word(pf, 12) & (0u - (uint32_t)(gi == 9u))) |
+                        (prefix_word(pf, 14) & (0u - (uint32_t)(gi == 11u))) |
+                        (prefix_word(pf, 15) & (0u - (uint32_t)(gi == 12u)));
+    uint32_t flow = bswap32(w[1]), seq = bswap32(w[2]), sec = bswap32(w[3]);
+    uint32_t usec = bswap32(w[4]), dst4 = w[6];
+    uint32_t msg_len = bswap16((uint16_t)(w[0] & 0xffffu));
+    uint32_t dport = bswap16((uint16_t)(w[5] & 0xffffu));
+    const uint32_t hlen = 44u + D + (hw >> 24);
+    uint32_t plen = bswap16((uint16_t)(g3 >> 16));
+    if (!(plen != 0 && hlen + plen <= L)) plen = 0;  // mgenMsg.cpp:488-497
+    uint32_t flags = w[0] >> 24, err = 0, dtype = (w[5] >> 16) & 0xffu, dlen = D;
+    uint32_t ptype = (g3 >> 8) & 0xffu, gps = g3 & 0xffu;
+    const bool slow = live && !fast_layout(w[0], w[5], hw);
+    if (__any(slow)) {
+      Hdr h;
+      if (slow && q == 0) parse_header(p.slab + (uint64_t)idx * p.stride, L, false, w, h);
+      auto bc = [&](uint32_t& dst, uint32_t v) {
+        v = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x00, 0xf, 0xf, false);
+        if (slow) dst = v;
+      };
+      bc(flow, h.flow); bc(seq, h.seq); bc(sec, h.sec); bc(usec, h.usec); bc(dst4, h.dst4);
+      bc(msg_len, h.msg_len); bc(dport, h.dst_port); bc(plen, h.plen); bc(flags, h.flags);
+      bc(err, h.err); bc(dtype, h.dst_type); bc(dlen, h.dst_len); bc(ptype, h.ptype);
+      bc(gps, h.gps);
+    }
+    if (!live) {
+      flow = seq = sec = usec = dst4 = msg_len = dport = plen = flags = dtype = dlen = 0;
+      ptype = gps = 0;
+      err = MGENX_ERROR_OOB;
+    }
+    o0 = q == 0 ? flow : q == 1 ? sec : q == 2 ? dst4 : (plen | flags << 16 | err << 24);
+    o1 = q == 0 ? seq : q == 1 ? usec : q == 2 ? (msg_len | dport << 16)
+                                              : (dtype | dlen << 8 | ptype << 16 | gps << 24);
+  };
+  // the caller's receive check (mgenTransport.cpp:971): ERROR_CHECKSUM (+ TCP flag) in word 6
+  auto verdict = [&](uint32_t& o0, bool crc_bad) {
+    const uint32_t fl = tcp ? (uint32_t)MGENX_FLAG_CHECKSUM_ERROR : 0u;
+    if (crc_bad && q == 3) o0 = (o0 & 0x00ffffffu) | fl << 16 | (uint32_t)MGENX_ERROR_CHECKSUM << 24;
+  };
+
+  // ---- output shift register: buf[K-1] = the newest group, `held` groups pending
+  uint32_t b0[K], b1[K];
+#pragma unroll
+  for (int k = 0; k < K; k++) b0[k] = b1[k] = 0u;
+  uint32_t held = 0, last_g = 0;
+  auto push = [&](uint32_t o0, uint32_t o1, uint32_t gg) {
+#pragma unroll
+    for (int k = 0; k < K - 1; k++) {
+      b0[k] = b0[k + 1];
+      b1[k] = b1[k + 1];
+    }
+    b0[K - 1] = o0;
+    b1[K - 1] = o1;
+    held++;
+    last_g = gg;
+  };
+  auto flush = [&]() {  // buf[k] belongs to group last_g - (K - 1 - k) * n_waves
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      const uint32_t back = (uint32_t)(K - 1 - k);
+      const uint32_t gg = last_g - back * n_waves;
+      const uint32_t idx = rec_idx(gg);
+      const bool in = back < held && idx < p.n;
+      const uint64_t v = (uint64_t)b1[k] << 32 | b0[k];
+      if (back < held)  // wave-uniform
+        st_g64_nt(in ? (uint64_t)p.cols.rows + (uint64_t)idx * 32 + 8 * q
+                     : (uint64_t)p.sink + 8u * (uint32_t)lane, v);
+    }
+    held = 0;
+  };
+
+  u32x4_t d[RS];
+  uint32_t g = wave_id;
+  const uint32_t base0 = row_base(g < g_end ? g : 0u);
+#pragma unroll
+  for (int j = 0; j < RS; j++) {
+    d[j] = ld(base0, j);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  table_writes(lds, tab_regs);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (g >= g_end) return;
+
+  bool pipelined = true;
+  while (g < g_end) {
+    const uint32_t gn = g + n_waves;
+    const bool has_next = gn < g_end;
+    const uint32_t idx = rec_idx(g);
+    const bool live = is_live(idx);
+    if (pipelined) {
+      const uint32_t base = row_base(g), base_n = row_base(has_next ? gn : g);
+      const u32x4_t hdr = d[0];  // row 0 = the 64-byte header prefix (aligned)
+      const bool needs_crc = decide(hdr, live);
+      const bool any = __any(needs_crc);
+      uint32_t o0, o1;
+      decode(hdr, idx, live, o0, o1);
+      uint32_t ha[4] = {0u, 0u, 0u, 0u}, hb[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int j = 0; j < NR - 1; j++) {
+        const u32x4_t x = d[j % RS];
+        const uint32_t xw[4] = {x.x, x.y, x.z, x.w};
+        uint32_t c4[4];
+#pragma unroll
+        for (int b = 0; b < 4; b++) c4[b] = xor3(ha[b], hb[b], xw[b]);
+        __builtin_amdgcn_sched_barrier(0);
+        // row j + RS of the stream: this group's row, or the next group's
+        d[j % RS] = (j + RS < NR) ? ld(base, j + RS) : ld(base_n, j + RS - NR);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int b = 0; b < 4; b++) a64_parts(ldsb, c4[b], s1, ha[b], hb[b]);
+      }
+      const u32x4_t xf = d[(NR - 1) % RS];
+      uint32_t f0 = xor3(ha[0], hb[0], xf.x), f1 = xor3(ha[1], hb[1], xf.y);
+      uint32_t f2 = xor3(ha[2], hb[2], xf.z);
+      uint32_t f3 = xor3(ha[3], hb[3], q == 3 ? bswap32(xf.w) : xf.w);
+      asm volatile("" : "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3));
+      __builtin_amdgcn_sched_barrier(0);
+      d[(NR - 1) % RS] = ld(base_n, NR - 1 + RS - NR);
+      __builtin_amdgcn_sched_barrier(0);
+      const uint32_t v = shift_tab(fold + 3 * 1024, f0) ^ shift_tab(fold + 2 * 1024, f1) ^
+                         shift_tab(fold + 1 * 1024, f2) ^ shift_tab(fold, f3);
+      const uint32_t* lt = fold + (q == 0 ? 5 : (q == 1 ? 4 : 3)) * 1024;  // A48/A32/A16
+      uint32_t sum = (q == 3) ? v : shift_tab(lt, v);
+      sum ^= __shfl_xor(sum, 1);
+      sum ^= __shfl_xor(sum, 2);
+      verdict(o0, needs_crc && sum != expect);
+      push(o0, o1, g);
+      asm volatile("" ::"v"(base_n));
+      pipelined = has_next && any;  // a group without checksummed records: header-only
+    } else {
+      // header-only mode: header first, body only when a record needs the CRC
+      const u32x4_t ph = ld(row_base(g), 0);
+      if (__any(decide(ph, live))) {
+        // back to the pipelined mode at this group: its first RS rows, then re-run it
+        const uint32_t bb = row_base(g);
+#pragma unroll
+        for (int j = 0; j < RS; j++) d[j] = ld(bb, j);
+        pipelined = true;
+        continue;
+      }
+      uint32_t o0, o1;
+      decode(ph, idx, live, o0, o1);
+      push(o0, o1, g);
+    }
+    if (held == (uint32_t)K) flush();
+    g = gn;
+  }
+  if (held) flush();
+}
+
 template <typename K>
 static hipError_t launch_lds(K kernel, bool& attr_done, const UnpackParams& p, int grid,
                              hipStream_t stream) {
@@ -1200,6 +1415,21 @@ static hipError_t launch_fixed(const UnpackParams& p, int grid, hipStream_t stre
   return hipGetLastError();
 }
 
+template <int NR, int RS = 4, int K = 16>
+static hipError_t launch_ring(const UnpackParams& p, int grid, hipStream_t stream) {
+  static bool attr_done = false;
+  if (!attr_done) {
+    hipError_t e = hipFuncSetAttribute((const void*)unpack_fixed_ring_kernel<NR, RS, K>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)kUnpackLdsBytes);
+    if (e != hipSuccess) return e;
+    attr_done = true;
+  }
+  hipLaunchKernelGGL((unpack_fixed_ring_kernel<NR, RS, K>), dim3(grid), dim3(kUnpackThreads),
+                     kUnpackLdsBytes, stream, p, p.expect_fixed);
+  return hipGetLastError();
+}
+
 typedef hipError_t (*fixed_launcher)(const UnpackParams&, int, hipStream_t);
 #define MGENX_FIXED_TABLE(R)                                                              \
   {nullptr, nullptr, launch_fixed<2, 0, R>, launch_fixed<3, 0, R>, launch_fixed<4, 0, R>,    \
@@ -1231,15 +1461,25 @@ hipError_t launch_unpack(const UnpackParams& p, int grid, hipStream_t stream) {
     switch (p.fixed_len) {
       case 256: return c.rows ? launch_fixed<4, 0, true, true>(p, grid, stream)
                               : launch_fixed<4, 0, false, true>(p, grid, stream);
-      case 512: return c.rows ? launch_fixed<8, 0, true, true>(p, grid, stream)
+      case 512: return c.rows ? launch_ring<8>(p, grid, stream)
                               : launch_fixed<8, 0, false, true>(p, grid, stream);
-      case 1024: return c.rows ? launch_fixed<16, 0, true, true>(p, grid, stream)
+      case 1024: return c.rows ? launch_ring<16>(p, grid, stream)
                                : launch_fixed<16, 0, false, true>(p, grid, stream);
       default: break;
     }
     return (c.rows ? kFixedLaunchRows : kFixedLaunch)[(p.fixed_len + 63) / 64](p, grid, stream);
   }
 #if MGENX_DIAG
+  // ablation 13: the interleaved-store aligned kernel (before the ring kernel)
+  if (unpack_variant == 13 && fixed && p.fixed_len == 1024)
+    return c.rows ? launch_fixed<16, 0, true, true>(p, grid, stream)
+                  : launch_fixed<16, 0, false, true>(p, grid, stream);
+  // ring-kernel shapes (rows in flight, groups held): 14 = (8, 12), 15 = (8, 8), 16 = (4, 12)
+  if (unpack_variant >= 14 && unpack_variant <= 16 && fixed && p.fixed_len == 1024 && c.rows) {
+    if (unpack_variant == 14) return launch_ring<16, 8, 12>(p, grid, stream);
+    if (unpack_variant == 15) return launch_ring<16, 8, 8>(p, grid, stream);
+    return launch_ring<16, 4, 12>(p, grid, stream);
+  }
   // ablation 12: the unaligned (separate header load) path on 1024-B records
   if (unpack_variant == 12 && fixed && p.fixed_len == 1024)
     return c.rows ? launch_fixed<16, 0, true>(p, grid, stream) : launch_fixed<16, 0>(p, grid, stream);
@@ -1372,9 +1612,84 @@ __global__ void __launch_bounds__(1024) group_rw_buf_kernel(const uint8_t* p, ui
   }
 }
 
+// Diagnostic: every wave keeps the row stores of its (<= 16) groups in registers; RING rows
+// in flight per wave (16 = one group ahead, 8 = half a group); BAR: a grid-wide arrival
+// barrier (bounded spin) between the last read and the stores, so the chip reads, then
+// writes.  POL as group_rw_buf_kernel.
+template <int RING, bool BAR, int POL>
+__global__ void __launch_bounds__(1024) group_rw_phase_kernel(const uint8_t* p, uint32_t n_groups,
+                                                              uint8_t* out, uint32_t* counter) {
+  constexpr int K = 16;
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave_id = __builtin_amdgcn_readfirstlane(blockIdx.x * 16 + (threadIdx.x >> 6));
+  const uint32_t n_waves = gridDim.x * 16;
+  const uint32_t lo = (uint32_t)(lane >> 2) * 1024u + 16u * (lane & 3);
+  const uint32_t my_groups = wave_id < n_groups ? (n_groups - wave_id + n_waves - 1) / n_waves : 0;
+  // 32-bit byte offsets (slab < 4 GiB); group k of this wave, clamped to its last group
+  auto goff = [&](int k) {
+    const uint32_t kk = (uint32_t)k < my_groups ? (uint32_t)k : (my_groups ? my_groups - 1 : 0);
+    const uint32_t g = wave_id + kk * n_waves;
+    return (g < n_groups ? g : 0u) * 16384u + lo;
+  };
+  u32x4_t d[RING];
+  uint32_t cur = goff(0), nxt = goff(1);
+#pragma unroll
+  for (int j = 0; j < RING; j++) d[j] = ldu128(p + (uint64_t)(cur + 64u * j));
+  // a shift register of the last K groups' row words: buf[K-1] = the newest group
+  uint64_t buf[K];
+#pragma unroll
+  for (int k = 0; k < K; k++) buf[k] = 0;
+  uint32_t acc = 0;
+  // two groups per trip keep the ring index static when RING does not divide 16
+  for (uint32_t k = 0; k < my_groups; k++) {
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      u32x4_t& x = d[j % RING];
+      acc = (acc << 1) ^ x.x ^ x.y ^ x.z ^ x.w;
+      __builtin_amdgcn_sched_barrier(0);
+      const int jn = j + RING;  // row r + RING: this group or the next
+      x = ldu128(p + (uint64_t)(jn < 16 ? cur + 64u * jn : nxt + 64u * (jn - 16)));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int q = 0; q < K - 1; q++) buf[q] = buf[q + 1];
+    buf[K - 1] = (uint64_t)acc << 32 | k;
+    cur = nxt;
+    nxt = goff((int)k + 2);
+  }
+#pragma unroll
+  for (int k = 0; k < K; k++) {  // buf[k] holds group my_groups - K + k
+    const int kg = (int)my_groups - K + k;
+    const uint32_t g = wave_id + (uint32_t)kg * n_waves;
+    if (kg >= 0 && g < n_groups) {
+      const uint64_t a = (uint64_t)out + (uint64_t)g * 512u + 8u * lane;
+      if (POL == 0) st_g64_nt(a, buf[k]);
+      else if (POL == 1) st_g64(a, buf[k]);
+      else st_g64_wt(a, buf[k]);
+    }
+  }
+}
+
 hipError_t launch_group_rw(const uint8_t* p, uint64_t bytes, uint8_t* out, int mode, int grid,
                            hipStream_t stream) {
   const uint32_t ng = (uint32_t)(bytes / 16384);
+  if (mode >= 4096) {  // 4096 + 16 * ring_sel + 4 * bar + pol
+    static uint32_t* counter = nullptr;
+    if (!counter && hipMalloc((void**)&counter, 256) != hipSuccess) return hipErrorOutOfMemory;
+    hipError_t e = hipMemsetAsync(counter, 0, 16, stream);
+    if (e != hipSuccess) return e;
+    const int m = mode - 4096;
+#define MGENX_GPH(RING, BAR, POL, CODE)                                                         \
+  if (m == CODE) {                                                                              \
+    hipLaunchKernelGGL((group_rw_phase_kernel<RING, BAR, POL>), dim3(grid), dim3(1024), 0, stream, \
+                       p, ng, out, counter);                                                    \
+    return hipGetLastError();                                                                   \
+  }
+    MGENX_GPH(16, false, 0, 0) MGENX_GPH(16, true, 0, 4) MGENX_GPH(8, false, 0, 16)
+    MGENX_GPH(8, true, 0, 20) MGENX_GPH(16, true, 1, 5) MGENX_GPH(8, true, 1, 21)
+#undef MGENX_GPH
+    return hipErrorInvalidValue;
+  }
   if (mode >= 16) {
     const int lk = ((mode >> 4) & 7) - 1, pol = (mode >> 8) & 3;
 #define MGENX_GRB(LK, POL)                                                                   \

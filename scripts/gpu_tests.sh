@@ -4,7 +4,7 @@
 set -u
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-(rocm-smi --showclocks --showpower --showmemuse --showtemp > gpurun_out/smi.log 2>&1 || true)
+(rocm-smi --showserial --showuniqueid --showclocks > gpurun_out/smi.log 2>&1 || true)
 timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -m gpu -q --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} > gpurun_out/pt.log 2>&1
 rc=$?
 tail -40 gpurun_out/pt.log

@@ -3,7 +3,7 @@
 gfx950 correction (MI355X_MICROARCH.md HBM section): FETCH_SIZE counts 64 B per
 128-B request of a wide coalesced streaming read, i.e. reports 1/2 of the bytes; it is
 doubled here.  WRITE_SIZE is exact for 16-B-per-lane streaming stores.  Units: KB.
-Writes profiles/traffic_r01.json keyed by bench workload.
+Writes profiles/traffic_<ROUND>.json keyed by bench workload.
 """
 import csv
 import glob
@@ -13,7 +13,7 @@ import sys
 from collections import defaultdict
 
 out_dir = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
-ROUND = os.environ.get("ROUND", "r01")
+ROUND = os.environ.get("ROUND", "r02")
 
 
 def load(counter):
@@ -57,7 +57,7 @@ out = {"note": ("median over launches (each after a 512 MiB flush > Infinity Cac
        "kernels": res}
 sr = find("stream_read_kernel")
 g0 = find("group_rw_kernel<0>")
-rows = find("unpack_fixed_kernel<16, 0, true, true>")
+rows = find("unpack_fixed_ring_kernel<16")
 cols = find("unpack_fixed_kernel<16, 0, false, true>")
 if sr:
     out["stream_read_fetch_factor"] = round(SLAB / (sr["fetch_kb_raw"] * 1024), 4)

@@ -1,0 +1,87 @@
+"""GPU: mgenx_flow_lookup (MgenAnalyticTable::FindFlow for batches, mgenAnalytic.cpp:312-328)
+against a Python dict keyed exactly like the reference key (dst addr, dst port, src addr,
+src port, flowId): dense indices in order of first appearance, records with an error
+skipped, keys persisting across calls, IPv4 and IPv6 addresses."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    return torch
+
+
+@pytest.fixture(scope="module")
+def eng(torch):
+    from mgen_amd import Engine
+    e = Engine(0)
+    yield e
+    e.close()
+
+
+def _batch(rng, n, n_src, n_dst, n_fid):
+    srcs = []
+    for k in range(n_src):
+        if k % 3 == 2:
+            srcs.append((2, 16, 7000 + k, bytes(rng.integers(0, 256, 16, dtype=np.uint8))))
+        else:
+            srcs.append((1, 4, 7000 + k, bytes([10, 0, k >> 8, k & 255])))
+    dsts = [(1, 4, 5000 + k, bytes([127, 0, 0, 1 + k])) for k in range(n_dst)]
+    dsts.append((2, 16, 5999, bytes(range(16))))
+    si = rng.integers(0, len(srcs), n)
+    di = rng.integers(0, len(dsts), n)
+    fid = rng.integers(1, n_fid + 1, n).astype(np.uint32)
+    err = (rng.random(n) < 0.05).astype(np.uint8)
+    return srcs, dsts, si, di, fid, err
+
+
+def _device_inputs(torch, srcs, dsts, si, di, fid, err):
+    n = len(si)
+    src = np.zeros((n, 20), np.uint8)
+    dst_addr = np.zeros((n, 16), np.uint8)
+    dst_len = np.zeros(n, np.uint8)
+    dst_port = np.zeros(n, np.uint16)
+    for i in range(n):
+        t, ln, port, a = srcs[si[i]]
+        src[i, 0], src[i, 1] = t, ln
+        src[i, 2:4] = np.frombuffer(np.uint16(port).tobytes(), np.uint8)
+        src[i, 4:4 + ln] = np.frombuffer(a, np.uint8)
+        t, ln, port, a = dsts[di[i]]
+        dst_addr[i, :ln] = np.frombuffer(a, np.uint8)
+        dst_len[i], dst_port[i] = ln, port
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a).copy()).cuda()  # noqa: E731
+    cols = {"dst_addr": t(dst_addr.reshape(-1)), "dst_len": t(dst_len),
+            "dst_port": t(dst_port.view(np.int16)), "flow_id": t(fid.view(np.int32)),
+            "err": t(err)}
+    return cols, t(src.reshape(-1))
+
+
+def test_flow_lookup_matches_reference_key(torch, eng):
+    rng = np.random.default_rng(11)
+    table = eng.flow_table(8192)
+    ref = {}
+    try:
+        for call in range(3):   # keys persist across batches
+            srcs, dsts, si, di, fid, err = _batch(np.random.default_rng(100 + call), 50_000,
+                                                  40, 6, 12)
+            cols, src = _device_inputs(torch, srcs, dsts, si, di, fid, err)
+            idx, nf = eng.flow_lookup(table, cols, src, len(si))
+            torch.cuda.synchronize()
+            idx = idx.cpu().numpy().view(np.uint32)
+            want = np.zeros(len(si), np.uint32)
+            for i in range(len(si)):
+                if err[i]:
+                    want[i] = 0xFFFFFFFF
+                    continue
+                s, d = srcs[si[i]], dsts[di[i]]
+                key = (d[3][:d[1]], d[2], s[3][:s[1]], s[2], int(fid[i]))
+                want[i] = ref.setdefault(key, len(ref))
+            assert np.array_equal(idx, want), call
+            assert int(nf.cpu()[0]) == len(ref)
+    finally:
+        eng.flow_table_destroy(table)
+    assert 1000 < len(ref) < 8192

@@ -183,6 +183,52 @@ def test_config2_full_size_roundtrip(torch, eng):
     assert np.all(err[victims[crc_class]] == 2)
 
 
+@pytest.mark.parametrize("size", [1024, 512])
+def test_full_size_rows_ring_kernel(torch, eng, size):
+    """The headline row-output kernel (unpack_fixed_ring_kernel: 8-row load ring, row output
+    held per wave and stored in bursts) at full size, where every wave runs 16+ groups and
+    bursts: rows == the column kernel's output field by field, with sampled bit flips and
+    runs of groups whose CHECKSUM flag is cleared (the header-only mode and the switch back)."""
+    n = (1 << 20) if size == 1024 else (3 << 19)
+    desc, slab, out_len = _config2(torch, eng, n, size)
+    assert int((out_len != size).sum()) == 0
+    rng = np.random.default_rng(size)
+    victims = np.unique(rng.integers(0, n, 8192))
+    pos = rng.integers(0, size, victims.size)
+    bits = rng.integers(0, 8, victims.size)
+    idx = torch.from_numpy((victims * size + pos).astype(np.int64)).cuda()
+    slab[idx] ^= torch.from_numpy((1 << bits).astype(np.uint8)).cuda()
+    # groups (16 records) 1000..1299 and every 7th group after 5000: CHECKSUM flag cleared
+    groups = np.concatenate([np.arange(1000, 1300), np.arange(5000, n // 16, 7)])
+    recs = (groups[:, None] * 16 + np.arange(16)[None, :]).reshape(-1)
+    flag_at = torch.from_numpy((recs * size + 3).astype(np.int64)).cuda()
+    slab[flag_at] &= 0xFB
+    from oracle import oracle as O
+    cols = eng.unpack(slab, n, stride=size, fixed_len=size)
+    c = host_cols(cols, n)
+    rows = eng.alloc_rows(n)
+    eng.unpack(slab, n, stride=size, fixed_len=size, cols={"rows": rows})
+    torch.cuda.synchronize()
+    r = rows_to_cols(rows, n)
+    # every record the flips or the flag clears touched, against the oracle; the rest
+    # against the descriptors they were packed from
+    touched = np.unique(np.concatenate([victims, recs]))
+    host = slab.cpu().numpy()
+    sub = np.ascontiguousarray(host.reshape(n, size)[touched]).reshape(-1)
+    f = O.udp_recv_batch(sub, touched.size, stride=size, fixed_len=size)
+    for out, label in ((r, "rows"), (c, "cols")):
+        for gname, oname, dt in COLMAP[:13]:
+            got = out[gname].view(dt)[touched]
+            want = f[oname].astype(dt)
+            bad = np.nonzero(got != want)[0]
+            assert bad.size == 0, (size, label, gname, touched[bad[:8]], got[bad[:4]], want[bad[:4]])
+        rest = np.setdiff1d(np.arange(n), touched)
+        assert np.all(out["err"][rest] == 0), label
+        assert np.array_equal(out["seq_num"].view(np.uint32)[rest], desc["seq_num"][rest]), label
+        assert np.array_equal(out["flow_id"].view(np.uint32)[rest], desc["tmpl"][rest] + 1), label
+    assert (c["err"] == 2).sum() > 1000 and (c["flags"] & 0x04 == 0).sum() >= 16 * 300
+
+
 def test_unpack_stride_matches_offsets(torch, eng):
     """Fixed-stride addressing == explicit offsets (same records)."""
     n, size = 4096, 256
