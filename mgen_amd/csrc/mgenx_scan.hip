@@ -7,20 +7,25 @@
 //   SINK  MgenAppSinkTransport::OnInputReady (src/common/mgenAppSinkTransport.cpp:369-434):
 //         msg_len outside [MIN_SIZE, MAX_SIZE] discards the two length bytes (resync).
 // The framing is a sequential chain p_{i+1} = p_i + L(p_i).  On the GPU:
-//   1. detect: one streaming pass flags plausible starts (L in range, record inside the
-//      stream, version byte == 2) per 64 KiB block into ordered slots (1 B/byte of input);
-//   2. compact + link: candidates in stream order, successor = candidate at p + L
-//      (binary search), or a terminal (stream end / position that is not a candidate);
-//   3. binary lifting (pointer doubling) gives the chain from any candidate in log2 steps,
-//      and the chain from the current start is enumerated in parallel;
+//   1. detect: one coalesced streaming pass (each workgroup a 64 KiB block, 4 KiB per step
+//      through LDS so every position sees its 3 following bytes) flags plausible starts
+//      (L in range, record inside the stream, version byte == 2) into ordered per-block slots;
+//   2. compact (device scan of the block counts) + link: successor = the candidate at p + L,
+//      searched in the target block's own slot list, or a terminal;
+//   3. base-4 lifting (pointer jumping, ceil(log4 n) levels) gives the chain from any
+//      candidate; the chain from offset 0 is enumerated in parallel and reports where it
+//      ends -- with the candidate total, the only device-to-host copies of the common path;
 //   4. where the chain leaves the candidate set (a record with a bad version, SINK garbage,
-//      a partial tail, TCP msg_len < 4) a single-thread resolver walks the reference rule
-//      exactly until it re-enters the set.  Valid streams never need step 4 mid-stream.
+//      a partial tail before the end, TCP msg_len < 4, or a block with more plausible starts
+//      than slots) a single-thread resolver walks the reference rule exactly until it
+//      re-enters the set.  Valid streams never need step 4.
 // Bit-exact with the sequential rule for every input: candidates only shortcut positions
 // the chain would compute anyway.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <vector>
@@ -30,8 +35,8 @@
 namespace mgenx {
 
 constexpr uint32_t kScanBlockBytes = 65536;  // detect block (one workgroup)
-constexpr uint32_t kScanThreads = 256;       // 256 B per thread
-constexpr uint32_t kScanSlots = 2048;        // candidates per block before overflow
+constexpr uint32_t kScanThreads = 256;       // 16 B per thread and step
+constexpr uint32_t kScanSlots = 4096;        // candidates per block before overflow
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 
 struct ScanMode {
@@ -42,119 +47,184 @@ __device__ __forceinline__ uint32_t be16_at(const uint8_t* s, uint64_t p) {
   return ((uint32_t)s[p] << 8) | s[p + 1];
 }
 
-// 1. detect.  Thread t of block b owns positions [b*64K + 256 t, +256); it needs bytes up
-// to 258 past its start (length + version byte of its last position).
+constexpr uint32_t kScanSteps = kScanBlockBytes / (kScanThreads * 16);  // 16
+
+// candidate mask of the 16 positions of one lane's 16-byte chunk w[0..3] (w[4] = the 4 bytes
+// after it); `mine` = stream offset of the chunk
+__device__ __forceinline__ uint32_t detect_hits(const uint32_t (&w)[5], uint64_t mine,
+                                                uint64_t nbytes, ScanMode m) {
+  uint32_t hits = 0;
+#pragma unroll
+  for (int k = 0; k < 5; k++) {
+    const uint32_t x = w[k];
+    const uint32_t z = x ^ 0x02020202u;
+    uint32_t mb = (z - 0x01010101u) & ~z & 0x80808080u;  // bytes == 0x02 (may over-flag)
+    if (k == 0) mb &= 0x80800000u;                       // positions -2, -1 are not ours
+    if (k == 4) mb &= 0x00008080u;                       // positions 16, 17 neither
+    while (mb) {
+      const int bb = __ffs(mb) / 8 - 1;  // byte index in the word
+      mb &= mb - 1;
+      if (((x >> (8 * bb)) & 0xffu) != 2u) continue;
+      const int i = 4 * k + bb - 2;      // position whose version byte this is
+      const uint64_t p = mine + (uint64_t)i;
+      if (p + 4 > nbytes) continue;
+      const uint32_t b0 = (w[i >> 2] >> (8 * (i & 3))) & 0xffu;
+      const int j = i + 1;
+      const uint32_t b1 = (w[j >> 2] >> (8 * (j & 3))) & 0xffu;
+      const uint32_t L = (b0 << 8) | b1;
+      if (L >= m.min_len && L <= m.max_len && p + L <= nbytes) hits |= 1u << i;
+    }
+  }
+  return hits;
+}
+
+// exclusive prefix over the lanes of the wave and the wave total of c (0..16), by ballots
+__device__ __forceinline__ uint32_t wave_excl(uint32_t c, uint32_t& wtot) {
+  uint32_t excl = 0, tot = 0;
+#pragma unroll
+  for (int b = 0; b < 5; b++) {
+    const uint64_t mk = __ballot((c >> b) & 1u);
+    excl += __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u)) << b;
+    tot += (uint32_t)__popcll(mk) << b;
+  }
+  wtot = tot;
+  return excl;
+}
+
+// 1. detect.  Workgroup b scans block b (64 KiB) as 16 steps of 4 KiB; lane t of the
+// workgroup owns bytes [16 t, 16 t + 16) of every step, so each wave load instruction reads
+// 1 KiB contiguously.  All 16 loads are issued up front (64 KiB in flight per workgroup).
+// A position needs the 3 bytes after it: the next lane's first word comes by a lane shift,
+// across waves through LDS.  Candidates go to the block's slots in stream order (step-major,
+// then lane): per-step wave prefixes by ballot, one workgroup barrier for the wave totals.
+// Writes counts[b] (0 when the block overflows its slots, which also sets flags[1]);
+// block 0 also zeroes counts[n_blocks] so the exclusive scan's last entry is the total.
+template <bool NT>
 __global__ void __launch_bounds__(kScanThreads)
 scan_detect_kernel(const uint8_t* __restrict__ s, uint64_t nbytes, ScanMode m,
-                   uint16_t* __restrict__ slots, uint32_t* __restrict__ counts) {
-  __shared__ uint32_t warp_sum[kScanThreads / 64];
-  const uint64_t start = (uint64_t)blockIdx.x * kScanBlockBytes + 256ull * threadIdx.x;
-  // a candidate p needs p + 3 <= nbytes (p + L <= nbytes with L >= 4 implies it)
-  auto is_cand = [&](uint64_t p) -> bool {
-    if (p + 4 > nbytes) return false;
-    if (s[p + 2] != 2) return false;
-    const uint32_t L = be16_at(s, p);
-    return L >= m.min_len && L <= m.max_len && p + L <= nbytes;
-  };
-  // fast screen: positions whose version byte (p + 2) is 0x02, found 4 bytes at a time
-  uint32_t cnt = 0;
-  const bool full = start + 256 + 4 <= nbytes;
-  uint32_t w[65];
-  if (full) {
+                   uint16_t* __restrict__ slots, uint32_t* __restrict__ counts,
+                   uint32_t* __restrict__ flags) {
+  constexpr uint32_t kW = kScanThreads / 64;
+  __shared__ uint32_t first[kScanSteps + 1][kW];  // first word of each wave's chunk per step
+  __shared__ uint32_t wsum[kScanSteps][kW];
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  const uint64_t block0 = (uint64_t)blockIdx.x * kScanBlockBytes;
+  u32x4_t v[kScanSteps];
+  if (block0 + kScanBlockBytes <= nbytes) {
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-      const u32x4_t v = ldu128(s + start + 16 * k);
-      w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
-    }
-    w[64] = ldu32(s + start + 256);
+    for (uint32_t st = 0; st < kScanSteps; st++)
+      v[st] = NT ? ldnt128(s + block0 + st * (kScanThreads * 16) + 16u * t)
+                 : ldu128(s + block0 + st * (kScanThreads * 16) + 16u * t);
   } else {
 #pragma unroll
-    for (int k = 0; k < 65; k++) {
-      uint32_t x = 0;
-      for (int b = 0; b < 4; b++) {
-        const uint64_t q = start + 4 * k + b;
-        if (q < nbytes) x |= (uint32_t)s[q] << (8 * b);
+    for (uint32_t st = 0; st < kScanSteps; st++) {
+      const uint64_t mine = block0 + st * (kScanThreads * 16) + 16u * t;
+      uint32_t w[4] = {0u, 0u, 0u, 0u};
+      if (mine + 16 <= nbytes) {
+        const u32x4_t x = ldu128(s + mine);
+        w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w;
+      } else {
+        for (uint32_t k = 0; k < 16 && mine + k < nbytes; k++)
+          w[k >> 2] |= (uint32_t)s[mine + k] << (8 * (k & 3));
       }
-      w[k] = x;
+      v[st] = u32x4_t{w[0], w[1], w[2], w[3]};
     }
   }
-  // Window byte j (0..259) = byte start + j; position start + i has its version byte at
-  // j = i + 2.  Words without a 0x02 byte are skipped with one SWAR test; the rare others
-  // are checked exactly (static indices: the window stays in registers).
-  auto visit = [&](auto&& emit) {
+  if (lane == 0) {
 #pragma unroll
-    for (int k = 0; k < 65; k++) {
-      const uint32_t x = w[k];
-      const uint32_t t = x ^ 0x02020202u;
-      if (((t - 0x01010101u) & ~t & 0x80808080u) != 0) {
-        for (int b = 0; b < 4; b++) {
-          const int i = 4 * k + b - 2;
-          if (i < 0 || i >= 256 || ((x >> (8 * b)) & 0xffu) != 2u) continue;
-          if (is_cand(start + (uint64_t)i)) emit(i);
+    for (uint32_t st = 0; st < kScanSteps; st++) first[st][wv] = v[st].x;
+  }
+  if (t == 0) {  // the 4 bytes after the block
+    const uint64_t q = block0 + kScanBlockBytes;
+    uint32_t x = 0;
+    for (uint32_t k = 0; k < 4; k++)
+      if (q + k < nbytes) x |= (uint32_t)s[q + k] << (8 * k);
+    first[kScanSteps][0] = x;
+  }
+  __syncthreads();
+  uint32_t hits[kScanSteps];
+#pragma unroll
+  for (uint32_t st = 0; st < kScanSteps; st++) {
+    uint32_t nxt = __shfl_down(v[st].x, 1);
+    if (lane == 63) nxt = wv + 1 < kW ? first[st][wv + 1] : first[st + 1][0];
+    const uint32_t w[5] = {v[st].x, v[st].y, v[st].z, v[st].w, nxt};
+    const uint64_t mine = block0 + st * (kScanThreads * 16) + 16u * t;
+    hits[st] = detect_hits(w, mine, nbytes, m);
+    const uint64_t any = __ballot(hits[st] != 0u);
+    uint32_t wt = 0;
+    if (any) (void)wave_excl(__popc(hits[st]), wt);
+    if (lane == 0) wsum[st][wv] = wt;
+  }
+  __syncthreads();
+  uint32_t total = 0;
+#pragma unroll
+  for (uint32_t st = 0; st < kScanSteps; st++)
+#pragma unroll
+    for (uint32_t k = 0; k < kW; k++) total += wsum[st][k];
+  const bool ovf = total > kScanSlots;
+  if (!ovf && total) {
+    uint16_t* out = slots + (size_t)blockIdx.x * kScanSlots;
+    uint32_t run = 0;
+#pragma unroll
+    for (uint32_t st = 0; st < kScanSteps; st++) {
+      uint32_t before = 0, stot = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < kW; k++) {
+        before += k < wv ? wsum[st][k] : 0u;
+        stot += wsum[st][k];
+      }
+      if (stot) {
+        uint32_t h = hits[st], wt;
+        uint32_t pos = run + before + wave_excl(__popc(h), wt);
+        while (h) {
+          const int i = __ffs(h) - 1;
+          h &= h - 1;
+          out[pos++] = (uint16_t)(16u * (st * kScanThreads + t) + (uint32_t)i);
         }
       }
+      run += stot;
     }
-  };
-  visit([&](int) { cnt++; });
-  // block exclusive scan of the per-thread counts (stream order = thread order)
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  uint32_t incl = cnt;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t o = __shfl_up(incl, d);
-    if (lane >= d) incl += o;
   }
-  if (lane == 63) warp_sum[wv] = incl;
-  __syncthreads();
-  uint32_t wbase = 0;
-  for (int k = 0; k < wv; k++) wbase += warp_sum[k];
-  const uint32_t total = warp_sum[0] + warp_sum[1] + warp_sum[2] + warp_sum[3];
-  uint32_t pos = wbase + incl - cnt;
-  if (threadIdx.x == 0) counts[blockIdx.x] = total > kScanSlots ? kNone : total;
-  if (total > kScanSlots) return;  // overflow: the host resolves this stream sequentially
-  uint16_t* out = slots + (size_t)blockIdx.x * kScanSlots;
-  const uint32_t tofs = 256u * threadIdx.x;
-  visit([&](int i) { out[pos++] = (uint16_t)(tofs + (uint32_t)i); });
+  if (t == 0) {
+    counts[blockIdx.x] = ovf ? 0u : total;
+    if (ovf) flags[1] = 1u;  // same value from every overflowing block
+    if (blockIdx.x == 0) counts[gridDim.x] = 0u;
+  }
 }
 
-// exclusive scan of block counts (single workgroup; n_blocks is small: 16 K per GiB)
-__global__ void __launch_bounds__(1024)
-scan_offsets_kernel(const uint32_t* __restrict__ counts, uint32_t n_blocks,
-                    uint32_t* __restrict__ base, uint32_t* __restrict__ total_out) {
-  __shared__ uint32_t part[1024];
-  __shared__ uint32_t carry;
-  if (threadIdx.x == 0) carry = 0;
-  __syncthreads();
-  bool overflow = false;
-  for (uint32_t b0 = 0; b0 < n_blocks; b0 += 1024) {
-    const uint32_t b = b0 + threadIdx.x;
-    uint32_t c = b < n_blocks ? counts[b] : 0u;
-    if (c == kNone) { overflow = true; c = 0; }
-    part[threadIdx.x] = c;
-    __syncthreads();
-    for (uint32_t d = 1; d < 1024; d <<= 1) {
-      const uint32_t v = threadIdx.x >= d ? part[threadIdx.x - d] : 0u;
-      __syncthreads();
-      part[threadIdx.x] += v;
-      __syncthreads();
-    }
-    if (b < n_blocks) base[b] = carry + part[threadIdx.x] - c;
-    __syncthreads();
-    if (threadIdx.x == 1023) carry += part[1023];
-    __syncthreads();
-  }
-  const int any_ovf = __syncthreads_or(overflow);
-  if (threadIdx.x == 0) total_out[0] = any_ovf ? kNone : carry;
-}
-
+// 2. compact + link, one wave per block: candidate positions into the global sorted
+// array, and each candidate's successor p + L searched in the target block's own slots
+// (sorted, usually a handful).  up0 = successor (self for a terminal), dist0 = 1 if linked.
 __global__ void __launch_bounds__(256)
-scan_compact_kernel(const uint16_t* __restrict__ slots, const uint32_t* __restrict__ counts,
-                    const uint32_t* __restrict__ base, uint64_t* __restrict__ cand) {
-  const uint32_t b = blockIdx.x;
+scan_link_kernel(const uint8_t* __restrict__ s, uint64_t nbytes, const uint16_t* __restrict__ slots,
+                 const uint32_t* __restrict__ counts, const uint32_t* __restrict__ base,
+                 uint32_t n_blocks, uint64_t* __restrict__ cand, uint32_t* __restrict__ up,
+                 uint32_t* __restrict__ dist) {
+  const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= n_blocks) return;
   const uint32_t c = counts[b];
   const uint32_t o = base[b];
-  for (uint32_t k = threadIdx.x; k < c; k += blockDim.x)
-    cand[o + k] = (uint64_t)b * kScanBlockBytes + slots[(size_t)b * kScanSlots + k];
+  for (uint32_t k = threadIdx.x & 63u; k < c; k += 64) {
+    const uint64_t p = (uint64_t)b * kScanBlockBytes + slots[(size_t)b * kScanSlots + k];
+    cand[o + k] = p;
+    const uint64_t nx = p + be16_at(s, p);
+    uint32_t tgt = kNone;
+    if (nx + 2 <= nbytes) {
+      const uint64_t bl = nx / kScanBlockBytes;
+      if (bl < n_blocks) {
+        const uint16_t* ts = slots + (size_t)bl * kScanSlots;
+        const uint32_t key = (uint32_t)(nx % kScanBlockBytes);
+        uint32_t lo = 0, hi = counts[bl];
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (ts[mid] < key) lo = mid + 1; else hi = mid;
+        }
+        if (lo < counts[bl] && ts[lo] == key) tgt = base[bl] + lo;
+      }
+    }
+    up[o + k] = tgt == kNone ? o + k : tgt;
+    dist[o + k] = tgt == kNone ? 0u : 1u;
+  }
 }
 
 __device__ uint32_t find_cand(const uint64_t* cand, uint32_t n, uint64_t p) {
@@ -166,41 +236,51 @@ __device__ uint32_t find_cand(const uint64_t* cand, uint32_t n, uint64_t p) {
   return (lo < n && cand[lo] == p) ? lo : kNone;
 }
 
-// 2. link: up0 = successor (self for a terminal), dist0 = 1 if linked
+// 3. one lifting level (base 4): up_k = up_{k-1}^4, dist_k = the 4 partial distances
+// (a terminal points at itself with distance 0, so both saturate there)
 __global__ void __launch_bounds__(256)
-scan_link_kernel(const uint8_t* __restrict__ s, uint64_t nbytes, const uint64_t* __restrict__ cand,
-                 uint32_t n, uint32_t* __restrict__ up, uint32_t* __restrict__ dist) {
+scan_lift_kernel(const uint32_t* __restrict__ up0, const uint32_t* __restrict__ d0,
+                 uint32_t* __restrict__ up1, uint32_t* __restrict__ d1, uint32_t n) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= n) return;
-  const uint64_t p = cand[c];
-  const uint64_t nx = p + be16_at(s, p);
-  const uint32_t t = (nx + 2 <= nbytes) ? find_cand(cand, n, nx) : kNone;
-  up[c] = t == kNone ? c : t;
-  dist[c] = t == kNone ? 0u : 1u;
+  const uint32_t u1 = up0[c];
+  const uint32_t u2 = up0[u1];
+  const uint32_t u3 = up0[u2];
+  up1[c] = up0[u3];
+  d1[c] = d0[c] + d0[u1] + d0[u2] + d0[u3];
 }
 
-// 3. one doubling level: up_k = up_{k-1} o up_{k-1}, dist_k = dist_{k-1} + dist_{k-1} o up
-__global__ void __launch_bounds__(256)
-scan_double_kernel(const uint32_t* __restrict__ up0, const uint32_t* __restrict__ d0,
-                   uint32_t* __restrict__ up1, uint32_t* __restrict__ d1, uint32_t n) {
-  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= n) return;
-  const uint32_t u = up0[c];
-  up1[c] = up0[u];
-  d1[c] = d0[c] + d0[u];
-}
+// where an enumerated chain ends: its record count and the position after the terminal
+// candidate's record
+struct ChainEnd {
+  uint64_t count, next_pos;
+};
 
-// enumerate the chain from candidate s: record i = lift(s, i), i < count
+// enumerate the chain from candidate `start`: record i (i <= dtop[start]) is `start` lifted
+// by the base-4 digits of i.  With at_zero, only if that candidate sits at offset 0 (else
+// nothing is written and end->count = 0).  Thread 0 reports where the chain ends.
 __global__ void __launch_bounds__(256)
 scan_enum_kernel(const uint8_t* __restrict__ s, const uint64_t* __restrict__ cand,
-                 const uint32_t* __restrict__ ups, uint32_t n, int levels, uint32_t start,
-                 uint64_t count, uint64_t out_base, uint64_t cap, uint64_t* __restrict__ rec_off,
-                 uint32_t* __restrict__ rec_len) {
+                 const uint32_t* __restrict__ ups, const uint32_t* __restrict__ dtop, uint32_t n,
+                 int levels, uint32_t start, int at_zero, uint64_t out_base, uint64_t cap,
+                 uint64_t* __restrict__ rec_off, uint32_t* __restrict__ rec_len,
+                 ChainEnd* __restrict__ end) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool ok = !(at_zero && cand[start] != 0);
+  const uint64_t count = ok ? (uint64_t)dtop[start] + 1 : 0;
+  if (i == 0) {
+    uint64_t nx = 0;
+    if (ok) {
+      const uint64_t tp = cand[ups[(size_t)levels * n + start]];
+      nx = tp + be16_at(s, tp);
+    }
+    end->count = count;
+    end->next_pos = nx;
+  }
   if (i >= count || out_base + i >= cap) return;
   uint32_t node = start;
   for (int k = 0; k < levels; k++)
-    if ((i >> k) & 1) node = ups[(size_t)k * n + node];
+    for (uint32_t d = (uint32_t)(i >> (2 * k)) & 3u; d; d--) node = ups[(size_t)k * n + node];
   const uint64_t p = cand[node];
   rec_off[out_base + i] = p;
   rec_len[out_base + i] = be16_at(s, p);
@@ -321,84 +401,108 @@ extern "C" int mgenx_scan_run(void* wsp, const uint8_t* s, uint64_t nbytes, int 
   uint64_t* d_cand = nullptr;
   uint32_t* d_up = nullptr;
   uint32_t* d_dist = nullptr;
+  uint32_t* d_counts = nullptr;
+  uint32_t* d_base = nullptr;
   int levels = 1;
+  uint32_t nb = 0;
+  struct {
+    uint32_t total, flags;
+  } h_tot = {0, 0};
   if (!overflow) {
-    const uint32_t nb = (uint32_t)n_blocks64;
+    nb = (uint32_t)n_blocks64;
     const size_t slot_b = align256((size_t)nb * kScanSlots * 2);
-    const size_t cnt_b = align256((size_t)nb * 4);
-    if ((e = ensure(ws.slots, slot_b + 2 * cnt_b)) != hipSuccess) return fail(e, "scan workspace");
+    const size_t cnt_b = align256((size_t)(nb + 1) * 4);
+    size_t cub_bytes = 0;
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, cub_bytes, (const uint32_t*)nullptr,
+                                           (uint32_t*)nullptr, (int)(nb + 1), stream);
+    if ((e = ensure(ws.slots, slot_b + 2 * cnt_b + align256(cub_bytes))) != hipSuccess)
+      return fail(e, "scan workspace");
     uint16_t* d_slots = static_cast<uint16_t*>(ws.slots.mem);
-    uint32_t* d_counts = reinterpret_cast<uint32_t*>(static_cast<char*>(ws.slots.mem) + slot_b);
-    uint32_t* d_base = d_counts + cnt_b / 4;
-    hipLaunchKernelGGL(scan_detect_kernel, dim3(nb), dim3(kScanThreads), 0, stream, s, nbytes, m,
-                       d_slots, d_counts);
-    hipLaunchKernelGGL(scan_offsets_kernel, dim3(1), dim3(1024), 0, stream, d_counts, nb, d_base,
-                       d_total);
-    if ((e = hipMemcpyAsync(&n, d_total, 4, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+    d_counts = reinterpret_cast<uint32_t*>(static_cast<char*>(ws.slots.mem) + slot_b);
+    d_base = d_counts + cnt_b / 4;
+    void* d_cub = static_cast<char*>(ws.slots.mem) + slot_b + 2 * cnt_b;
+    if ((e = hipMemsetAsync(d_total, 0, 8, stream)) != hipSuccess) return fail(e, "scan");
+    static const bool nt = getenv("MGENX_SCAN_NT") && atoi(getenv("MGENX_SCAN_NT"));
+    if (nt)
+      hipLaunchKernelGGL(scan_detect_kernel<true>, dim3(nb), dim3(kScanThreads), 0, stream, s,
+                         nbytes, m, d_slots, d_counts, d_total);
+    else
+      hipLaunchKernelGGL(scan_detect_kernel<false>, dim3(nb), dim3(kScanThreads), 0, stream, s,
+                         nbytes, m, d_slots, d_counts, d_total);
+    if ((e = hipcub::DeviceScan::ExclusiveSum(d_cub, cub_bytes, (const uint32_t*)d_counts, d_base,
+                                              (int)(nb + 1), stream)) != hipSuccess)
+      return fail(e, "scan offsets");
+    if ((e = hipMemcpyAsync(d_total, d_base + nb, 4, hipMemcpyDeviceToDevice, stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(&h_tot, d_total, 8, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
         (e = hipStreamSynchronize(stream)) != hipSuccess)
       return fail(e, "scan detect");
-    if (n == kNone) {
+    n = h_tot.total;
+    if (h_tot.flags) {
       overflow = true;
       n = 0;
     } else if (n > 0) {
-      while ((1ull << (levels - 1)) < n) levels++;
-      levels++;  // 2^(levels-1) >= n + 1 > any chain length
+      levels = 1;
+      while ((1ull << (2 * levels)) < n) levels++;  // 4^levels >= n > any chain length
       if ((e = ensure(ws.cand, (size_t)n * 8)) != hipSuccess) return fail(e, "scan workspace");
-      if ((e = ensure(ws.tabs, (size_t)n * 4 * (levels + 2))) != hipSuccess)
+      if ((e = ensure(ws.tabs, (size_t)n * 4 * (levels + 3))) != hipSuccess)
         return fail(e, "scan workspace");
       d_cand = static_cast<uint64_t*>(ws.cand.mem);
-      d_up = static_cast<uint32_t*>(ws.tabs.mem);                 // [levels][n]
-      d_dist = d_up + (size_t)levels * n;                          // 2 x [n] ping-pong
-      hipLaunchKernelGGL(scan_compact_kernel, dim3(nb), dim3(256), 0, stream, d_slots, d_counts,
-                         d_base, d_cand);
+      d_up = static_cast<uint32_t*>(ws.tabs.mem);                 // [levels + 1][n]
+      d_dist = d_up + (size_t)(levels + 1) * n;                    // 2 x [n] ping-pong
+      hipLaunchKernelGGL(scan_link_kernel, dim3((nb + 3) / 4), dim3(256), 0, stream, s, nbytes,
+                         d_slots, d_counts, d_base, nb, d_cand, d_up, d_dist);
       const dim3 g((n + 255) / 256);
-      hipLaunchKernelGGL(scan_link_kernel, g, dim3(256), 0, stream, s, nbytes, d_cand, n, d_up,
-                         d_dist);
-      for (int k = 1; k < levels; k++) {
+      for (int k = 1; k <= levels; k++) {
         uint32_t* d0 = d_dist + (size_t)((k - 1) & 1) * n;
         uint32_t* d1 = d_dist + (size_t)(k & 1) * n;
-        hipLaunchKernelGGL(scan_double_kernel, g, dim3(256), 0, stream, d_up + (size_t)(k - 1) * n,
+        hipLaunchKernelGGL(scan_lift_kernel, g, dim3(256), 0, stream, d_up + (size_t)(k - 1) * n,
                            d0, d_up + (size_t)k * n, d1, n);
       }
     }
   }
   if (overflow) n = 0;  // pathological stream: the resolver walks all of it
-  uint32_t* d_dtop = d_dist ? d_dist + (size_t)((levels - 1) & 1) * n : nullptr;
+  uint32_t* d_dtop = d_dist ? d_dist + (size_t)(levels & 1) * n : nullptr;
+  ChainEnd* d_end = reinterpret_cast<ChainEnd*>(static_cast<char*>(ws.small.mem) + 512);
 
-  // chain walk: from position 0, alternating parallel enumeration and the resolver
+  // chain walk from position 0.  Common case, fully on the device: offset 0 is a candidate,
+  // its chain is enumerated and the enumeration reports where it ends (one copy back).
   uint64_t pos = 0, total = 0;
   uint32_t at = kNone;  // candidate index at pos (if any)
   if (n) {
-    uint64_t c0 = 0;
-    if ((e = hipMemcpyAsync(&c0, d_cand, 8, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+    struct {
+      ChainEnd end;
+    } h = {{0, 0}};
+    hipLaunchKernelGGL(scan_enum_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, s, d_cand,
+                       d_up, d_dtop, n, levels, 0u, 1, (uint64_t)0, cap, rec_off, rec_len, d_end);
+    if ((e = hipMemcpyAsync(&h.end, d_end, sizeof(ChainEnd), hipMemcpyDeviceToHost, stream)) != hipSuccess ||
         (e = hipStreamSynchronize(stream)) != hipSuccess)
       return fail(e, "scan");
-    if (c0 == 0) at = 0;
+    if (h.end.count) {
+      total = h.end.count;
+      pos = h.end.next_pos;
+    }
+  }
+  if (total && pos + 2 > nbytes) {  // the chain ran to the end of the stream: done
+    if ((e = hipGetLastError()) != hipSuccess) return fail(e, "scan launch");
+    out.n_records = total;
+    out.consumed = pos;
+    out.status = 0;
+    out.candidates = n;
+    if (info) *info = out;
+    return MGENX_OK;
   }
   int reason = 1;
   for (int rounds = 0; rounds < (1 << 30); rounds++) {
     if (at != kNone) {
-      // enumerate the candidate chain from `at`
-      uint32_t steps = 0, term = 0;
-      if ((e = hipMemcpyAsync(&steps, d_dtop + at, 4, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
-          (e = hipMemcpyAsync(&term, d_up + (size_t)(levels - 1) * n + at, 4,
-                              hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+      // enumerate the candidate chain from `at` (grid sized by n >= its length)
+      ChainEnd h_end = {0, 0};
+      hipLaunchKernelGGL(scan_enum_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, s, d_cand,
+                         d_up, d_dtop, n, levels, at, 0, total, cap, rec_off, rec_len, d_end);
+      if ((e = hipMemcpyAsync(&h_end, d_end, sizeof(h_end), hipMemcpyDeviceToHost, stream)) != hipSuccess ||
           (e = hipStreamSynchronize(stream)) != hipSuccess)
         return fail(e, "scan");
-      const uint64_t count = (uint64_t)steps + 1;
-      hipLaunchKernelGGL(scan_enum_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0,
-                         stream, s, d_cand, d_up, n, levels, at, count, total, cap, rec_off,
-                         rec_len);
-      total += count;
-      // continue after the terminal candidate's record
-      uint64_t tp = 0;
-      if ((e = hipMemcpyAsync(&tp, d_cand + term, 8, hipMemcpyDeviceToHost, stream)) != hipSuccess)
-        return fail(e, "scan");
-      uint8_t lb[2];
-      if ((e = hipMemcpyAsync(lb, s + tp, 2, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
-          (e = hipStreamSynchronize(stream)) != hipSuccess)
-        return fail(e, "scan");
-      pos = tp + (((uint32_t)lb[0] << 8) | lb[1]);
+      total += h_end.count;
+      pos = h_end.next_pos;
       at = kNone;
       if (pos + 2 > nbytes) { reason = 1; break; }
     }

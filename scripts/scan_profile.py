@@ -34,4 +34,14 @@ for _ in range(5):
     offs, lens, info = eng.stream_scan(stream, SCAN_TCP, cap=n + 1)
 torch.cuda.synchronize()
 print("scan_ms", (time.perf_counter() - t0) / 5 * 1e3, "records", int(info.n_records),
-      "candidates", int(info.candidates))
+      "candidates", int(info.candidates), "nt", os.environ.get("MGENX_SCAN_NT", "0"))
+if len(sys.argv) > 1 and sys.argv[1] == "read":
+    d = Engine(0, diag=True)
+    for _ in range(2):
+        d.stream_read(stream, grid=4096)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(10):
+        d.stream_read(stream, grid=4096)
+    torch.cuda.synchronize()
+    print("stream_read_ms", (time.perf_counter() - t0) / 10 * 1e3)
