@@ -208,12 +208,16 @@ def extra_config4(torch, eng, dev, world, rank, dist):
             "merge": "mgenx_allreduce_flows (RCCL ncclAllReduce sum, 1024 x 64 B)"}
 
 
-def extra_config5(torch, eng, dev):
+def extra_config5(torch, eng, dev, world=1, rank=0, dist=None):
     """TCP stream of 16 KiB records (checksum on): boundary scan + TCP-rule unpack over
-    1 GiB (a 64 MiB oracle-built stream tiled 16x: framing and CRCs stay valid)."""
+    1 GiB per rank (a 64 MiB oracle-built stream tiled 16x: framing and CRCs stay valid).
+    N > 1: one stream of N GiB split into 1-GiB shards (+ 64 KiB halo) framed with the
+    sharded protocol (mgen_amd/shard.py: exits table all-gather over RCCL, then the rank's
+    range); weak scaling, time = max over ranks."""
     from mgen_amd import OPT_TCP, SCAN_TCP, to_device
-    from mgen_amd.workloads import make_templates
     from mgen_amd._abi import DESC_DTYPE
+    from mgen_amd.shard import HALO, EngineScanner, TorchComm, scan_sharded
+    from mgen_amd.workloads import make_templates
     from oracle import oracle as O
     n0 = 4096
     tmpl, pool = make_templates(64)
@@ -225,27 +229,52 @@ def extra_config5(torch, eng, dev):
     desc["msg_len"] = 16384
     desc["flags"] = 4
     s0 = np.asarray(O.tcp_tx_batch(tmpl, desc, np.full(n0, 16384, np.uint32), pool), np.uint8)
-    stream = to_device(s0).repeat(16)
+    tile = to_device(s0, dev.index)
+    shard = tile.repeat(16)
     n = n0 * 16
+    local = torch.cat([shard, tile[:HALO]]) if rank < world - 1 else shard
+    total_bytes = shard.numel() * world
     state = {}
+    if world > 1:
+        comm = TorchComm(dev)
+        scanner = EngineScanner(eng)
 
-    def scan():
-        state["r"] = eng.stream_scan(stream, SCAN_TCP, cap=n + 1)
-    t0 = time.perf_counter()
+        def scan():
+            state["r"] = scan_sharded(scanner, comm, local, total_bytes, SCAN_TCP)
+    else:
+        def scan():
+            offs, lens, info = eng.stream_scan(local, SCAN_TCP, cap=n + 1)
+            state["r"] = (offs, lens, (int(info.n_records), int(info.consumed),
+                                       int(info.status)))
+    scan()
     reps = 5
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
     for _ in range(reps):
         scan()
+    torch.cuda.synchronize()
     scan_ms = (time.perf_counter() - t0) / reps * 1e3
-    offs, lens, info = state["r"]
-    assert int(info.n_records) == n and int(info.consumed) == stream.numel()
+    if world > 1:
+        t = torch.tensor([scan_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        scan_ms = float(t.item())
+    offs, lens, summ = state["r"]
+    assert summ == (n * world, total_bytes, 0), summ
+    assert offs.numel() == n and int(offs[0]) == 0
     cols = eng.alloc_cols(n)
-    ums = timed(torch, lambda: eng.unpack(stream, n, rec_off=offs, rec_len=lens, opts=OPT_TCP,
+    ums = timed(torch, lambda: eng.unpack(local, n, rec_off=offs, rec_len=lens, opts=OPT_TCP,
                                           cols=cols), reps=10)
     assert int((cols["err"] != 0).sum()) == 0
-    b = stream.numel()
-    return {"records": n, "bytes": b, "scan_ms": round(scan_ms, 4),
-            "scan_gbps": round(b / scan_ms / 1e6, 1), "unpack_ms": round(ums, 4),
-            "unpack_gbps": round((b + n * 32) / ums / 1e6, 1), "candidates": int(info.candidates)}
+    b = shard.numel()
+    return {"records_per_rank": n, "bytes_per_rank": b, "ranks": world,
+            "scan_ms": round(scan_ms, 4),
+            "scan_gbps_total": round(world * b / scan_ms / 1e6, 1),
+            "scan_frac_of_peak_per_gpu": round(b / scan_ms / 1e6 / PEAK_HBM_GBPS, 4),
+            "unpack_ms": round(ums, 4),
+            "unpack_gbps": round((b + n * 32) / ums / 1e6, 1),
+            "framing": "sharded (exits all-gather + range)" if world > 1 else "whole stream"}
 
 
 def extra_log(torch, eng, dev, slab):
@@ -434,11 +463,12 @@ def main():
                 extra[name] = fn()
             except Exception as e:  # an extra never hides the headline line
                 extra[name] = {"error": f"{type(e).__name__}: {e}"[:300]}
-        # config 4 on every rank (it has a collective); the rest on rank 0 only
+        # configs 4 and 5 on every rank (they have collectives); the rest on rank 0 only
         guard("config4_flow_reduce", lambda: extra_config4(torch, eng, dev, world, rank, dist))
+        guard("config5_tcp_scan_unpack",
+              lambda: extra_config5(torch, eng, dev, world, rank, dist))
         if rank == 0:
             guard("config3_mixed_pack_unpack", lambda: extra_config3(torch, eng, dev))
-            guard("config5_tcp_scan_unpack", lambda: extra_config5(torch, eng, dev))
             guard("pcie_inclusive_config2", lambda: extra_pcie(torch, eng, dev, slab))
             guard("recv_log_text", lambda: extra_log(torch, eng, dev, slab))
 

@@ -252,6 +252,36 @@ int mgenx_stream_scan(mgenx_ctx* ctx, const uint8_t* dev_stream, uint64_t nbytes
                       uint64_t* dev_rec_off, uint32_t* dev_rec_len, uint64_t cap,
                       mgenx_scan_info* info, void* stream);
 
+/* ---- sharded framing (one stream split over ranks; no reference counterpart: the
+ * reference frames one socket sequentially) ----
+ * Rank r owns the records that START in [a_r, b_r) of the global stream and holds the
+ * bytes [a_r, min(b_r + MGENX_SCAN_HALO, N)) (a record starting before b_r ends within the
+ * halo).  Its chain entry e_r (the first chain position >= a_r) lies below
+ * a_r + MGENX_SCAN_HALO.  Protocol (mgen_amd/shard.py):
+ *   1. mgenx_stream_scan_exits on the local bytes with window = MGENX_SCAN_HALO and
+ *      limit = b_r - a_r: for each candidate entry below the window, where its chain first
+ *      reaches >= limit (dev_exits; bit 63 set = the chain leaves the candidate set first,
+ *      exit unknown).  Unused rows are ~0.
+ *   2. all-gather the (entry, exit) tables; every rank stitches e_0 = 0, e_{r+1} = exit_r(e_r)
+ *      identically; a missing or unknown exit is settled by that rank's
+ *      mgenx_stream_scan_range (its info.consumed is the exit) and one more all-gather.
+ *   3. mgenx_stream_scan_range(entry = e_r - a_r, limit, MGENX_SCAN_REUSE): the rank's
+ *      records (local offsets; add a_r for global ones), on the tables of step 1.
+ * The union over ranks equals mgenx_stream_scan of the whole stream. */
+#define MGENX_SCAN_HALO  65536ull
+#define MGENX_SCAN_REUSE 1   /* flags: reuse the tables of the last build on this context */
+int mgenx_stream_scan_exits(mgenx_ctx* ctx, const uint8_t* dev_stream, uint64_t nbytes, int mode,
+                            uint64_t window, uint64_t limit, uint64_t* dev_entries,
+                            uint64_t* dev_exits, uint32_t cap, uint32_t* candidates,
+                            void* stream);
+/* Records of the chain from `entry` over positions < limit (limit <= nbytes): the scan
+ * rule of mgenx_stream_scan started at `entry`.  info->consumed is where it stopped: the
+ * first chain position >= limit, or the end / error position as for the whole stream. */
+int mgenx_stream_scan_range(mgenx_ctx* ctx, const uint8_t* dev_stream, uint64_t nbytes, int mode,
+                            uint64_t entry, uint64_t limit, int flags, uint64_t* dev_rec_off,
+                            uint32_t* dev_rec_len, uint64_t cap, mgenx_scan_info* info,
+                            void* stream);
+
 /* ---- per-flow receive analytics (MgenAnalytic::Update) ----
  * Restates MgenAnalytic::Init/Update (src/common/mgenAnalytic.cpp:28-258) as called by
  * Mgen::UpdateRecvAnalytics (src/common/mgen.cpp:1027-1070): per flow, an order-dependent

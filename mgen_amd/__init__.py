@@ -29,7 +29,7 @@ EXPORTED_SYMBOLS = (
     "mgenx_abi_version", "mgenx_ctx_create", "mgenx_ctx_destroy", "mgenx_last_error",
     "mgenx_ctx_device", "mgenx_unpack_batch", "mgenx_pack_prepare", "mgenx_set_fill_time",
     "mgenx_pack_batch", "mgenx_pack_msgs", "mgenx_crc32_update", "mgenx_crc32_batch",
-    "mgenx_stream_scan", "mgenx_flow_init", "mgenx_flow_reduce", "mgenx_flow_export",
+    "mgenx_stream_scan", "mgenx_stream_scan_exits", "mgenx_stream_scan_range", "mgenx_flow_init", "mgenx_flow_reduce", "mgenx_flow_export",
     "mgenx_log_recv_text", "mgenx_log_recv_binary", "mgenx_comm_unique_id", "mgenx_comm_init",
     "mgenx_comm_destroy", "mgenx_allreduce_flows", "mgenx_allgather_u64",
     "mgenx_flow_table_create", "mgenx_flow_table_destroy", "mgenx_flow_lookup",
@@ -83,6 +83,10 @@ def load(diag: bool = False):
         L.mgenx_diag_stream_read.argtypes = [P, P, u64, P, i32, P]
         L.mgenx_diag_group_rw.argtypes = [P, P, u64, P, i32, P]
     L.mgenx_stream_scan.argtypes = [P, P, u64, i32, P, P, u64, ctypes.POINTER(ScanInfo), P]
+    L.mgenx_stream_scan_exits.argtypes = [P, P, u64, i32, u64, u64, P, P, u32,
+                                          ctypes.POINTER(u32), P]
+    L.mgenx_stream_scan_range.argtypes = [P, P, u64, i32, u64, u64, i32, P, P, u64,
+                                          ctypes.POINTER(ScanInfo), P]
     L.mgenx_flow_init.argtypes = [P, P, u32, ctypes.c_double, P]
     L.mgenx_flow_reduce.argtypes = [P, P, P, P, P, P, P, P, u32, P, u32, P, u32, P, P]
     L.mgenx_flow_export.argtypes = [P, P, u32, P, P]
@@ -295,6 +299,38 @@ class Engine:
                                         _ptr(lens), cap, ctypes.byref(info),
                                         _stream(self.device))
         self._check(rc, "mgenx_stream_scan")
+        n = min(int(info.n_records), cap)
+        return offs[:n], lens[:n], info
+
+    def stream_scan_exits(self, data, mode, window, limit, cap=4096, nbytes=None):
+        """Step 1 of the sharded framing (mgenx_stream_scan_exits): builds the candidate
+        tables of `data` and returns (entries, exits) uint64 device tensors of `cap` rows
+        (as int64) plus the candidate count."""
+        torch = self.torch
+        nbytes = data.numel() if nbytes is None else nbytes
+        ent = torch.empty(cap, dtype=torch.int64, device=data.device)
+        ext = torch.empty(cap, dtype=torch.int64, device=data.device)
+        cands = ctypes.c_uint32(0)
+        rc = self.lib.mgenx_stream_scan_exits(self.ctx, _ptr(data), nbytes, mode, window, limit,
+                                              _ptr(ent), _ptr(ext), cap, ctypes.byref(cands),
+                                              _stream(self.device))
+        self._check(rc, "mgenx_stream_scan_exits")
+        return ent, ext, int(cands.value)
+
+    def stream_scan_range(self, data, mode, entry, limit, reuse=False, cap=None, nbytes=None):
+        """Records of the chain from `entry` below `limit` (mgenx_stream_scan_range); reuse:
+        the tables of the last build on this engine (same tensor, unchanged)."""
+        torch = self.torch
+        nbytes = data.numel() if nbytes is None else nbytes
+        if cap is None:
+            cap = max(limit - entry, 0) // 4 + 1
+        offs = torch.empty(max(cap, 1), dtype=torch.int64, device=data.device)
+        lens = torch.empty(max(cap, 1), dtype=torch.int32, device=data.device)
+        info = ScanInfo()
+        rc = self.lib.mgenx_stream_scan_range(self.ctx, _ptr(data), nbytes, mode, entry, limit,
+                                              1 if reuse else 0, _ptr(offs), _ptr(lens), cap,
+                                              ctypes.byref(info), _stream(self.device))
+        self._check(rc, "mgenx_stream_scan_range")
         n = min(int(info.n_records), cap)
         return offs[:n], lens[:n], info
 

@@ -93,6 +93,8 @@ def hex_payload(hexstr: str) -> bytes:
 # stream framing (mgenx_stream_scan)
 SCAN_TCP = 0
 SCAN_SINK = 1
+SCAN_HALO = 65536     # MGENX_SCAN_HALO: bytes past a shard a record may extend into
+SCAN_REUSE = 1        # MGENX_SCAN_REUSE
 
 
 class ScanInfo(ctypes.Structure):

@@ -20,6 +20,14 @@ extern "C" void mgenx_scan_ws_free(void* p);
 extern "C" int mgenx_scan_run(void* ws, const uint8_t* s, uint64_t nbytes, int mode,
                               uint64_t* rec_off, uint32_t* rec_len, uint64_t cap,
                               mgenx_scan_info* info, hipStream_t stream, char* err, size_t errn);
+extern "C" int mgenx_scan_exits_run(void* ws, const uint8_t* s, uint64_t nbytes, int mode,
+                                    uint64_t window, uint64_t limit, uint64_t* entries,
+                                    uint64_t* exits, uint32_t cap, uint32_t* candidates,
+                                    hipStream_t stream, char* err, size_t errn);
+extern "C" int mgenx_scan_range_run(void* ws, const uint8_t* s, uint64_t nbytes, int mode,
+                                    uint64_t entry, uint64_t limit, int reuse, uint64_t* rec_off,
+                                    uint32_t* rec_len, uint64_t cap, mgenx_scan_info* info,
+                                    hipStream_t stream, char* err, size_t errn);
 
 extern "C" void* mgenx_log_ws_new();
 extern "C" void mgenx_log_ws_free(void* p);
@@ -383,6 +391,34 @@ int mgenx_stream_scan(mgenx_ctx* ctx, const uint8_t* dev_stream, uint64_t nbytes
   if (!ctx->scan_ws) ctx->scan_ws = mgenx_scan_ws_new();
   return mgenx_scan_run(ctx->scan_ws, dev_stream, nbytes, mode, dev_rec_off, dev_rec_len, cap,
                         info, (hipStream_t)stream, ctx->err, sizeof(ctx->err));
+}
+
+int mgenx_stream_scan_exits(mgenx_ctx* ctx, const uint8_t* dev_stream, uint64_t nbytes, int mode,
+                            uint64_t window, uint64_t limit, uint64_t* dev_entries,
+                            uint64_t* dev_exits, uint32_t cap, uint32_t* candidates,
+                            void* stream) {
+  if (!ctx || !dev_stream || nbytes == 0 || limit > nbytes || (cap && (!dev_entries || !dev_exits)) ||
+      (mode != MGENX_SCAN_TCP && mode != MGENX_SCAN_SINK))
+    return MGENX_EINVAL;
+  hipSetDevice(ctx->device);
+  if (!ctx->scan_ws) ctx->scan_ws = mgenx_scan_ws_new();
+  return mgenx_scan_exits_run(ctx->scan_ws, dev_stream, nbytes, mode, window, limit, dev_entries,
+                              dev_exits, cap, candidates, (hipStream_t)stream, ctx->err,
+                              sizeof(ctx->err));
+}
+
+int mgenx_stream_scan_range(mgenx_ctx* ctx, const uint8_t* dev_stream, uint64_t nbytes, int mode,
+                            uint64_t entry, uint64_t limit, int flags, uint64_t* dev_rec_off,
+                            uint32_t* dev_rec_len, uint64_t cap, mgenx_scan_info* info,
+                            void* stream) {
+  if (!ctx || !dev_stream || nbytes == 0 || limit > nbytes || (cap && (!dev_rec_off || !dev_rec_len)) ||
+      (mode != MGENX_SCAN_TCP && mode != MGENX_SCAN_SINK) || (flags & ~MGENX_SCAN_REUSE))
+    return MGENX_EINVAL;
+  hipSetDevice(ctx->device);
+  if (!ctx->scan_ws) ctx->scan_ws = mgenx_scan_ws_new();
+  return mgenx_scan_range_run(ctx->scan_ws, dev_stream, nbytes, mode, entry, limit,
+                              flags & MGENX_SCAN_REUSE, dev_rec_off, dev_rec_len, cap, info,
+                              (hipStream_t)stream, ctx->err, sizeof(ctx->err));
 }
 
 int mgenx_flow_init(mgenx_ctx* ctx, mgenx_flow_state* dev_flows, uint32_t n_flows,

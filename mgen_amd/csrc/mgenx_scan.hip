@@ -97,13 +97,12 @@ __device__ __forceinline__ uint32_t wave_excl(uint32_t c, uint32_t& wtot) {
 // A position needs the 3 bytes after it: the next lane's first word comes by a lane shift,
 // across waves through LDS.  Candidates go to the block's slots in stream order (step-major,
 // then lane): per-step wave prefixes by ballot, one workgroup barrier for the wave totals.
-// Writes counts[b] (0 when the block overflows its slots, which also sets flags[1]);
-// block 0 also zeroes counts[n_blocks] so the exclusive scan's last entry is the total.
-template <bool NT>
+// Writes counts[b] = candidates (low word) | overflowed << 32 (an overflowing block keeps
+// none), and block 0 zeroes counts[n_blocks]: the exclusive scan's last entry then holds
+// the candidate total and the number of overflowing blocks in one word.
 __global__ void __launch_bounds__(kScanThreads)
 scan_detect_kernel(const uint8_t* __restrict__ s, uint64_t nbytes, ScanMode m,
-                   uint16_t* __restrict__ slots, uint32_t* __restrict__ counts,
-                   uint32_t* __restrict__ flags) {
+                   uint16_t* __restrict__ slots, uint64_t* __restrict__ counts) {
   constexpr uint32_t kW = kScanThreads / 64;
   __shared__ uint32_t first[kScanSteps + 1][kW];  // first word of each wave's chunk per step
   __shared__ uint32_t wsum[kScanSteps][kW];
@@ -113,8 +112,7 @@ scan_detect_kernel(const uint8_t* __restrict__ s, uint64_t nbytes, ScanMode m,
   if (block0 + kScanBlockBytes <= nbytes) {
 #pragma unroll
     for (uint32_t st = 0; st < kScanSteps; st++)
-      v[st] = NT ? ldnt128(s + block0 + st * (kScanThreads * 16) + 16u * t)
-                 : ldu128(s + block0 + st * (kScanThreads * 16) + 16u * t);
+      v[st] = ldnt128(s + block0 + st * (kScanThreads * 16) + 16u * t);  // read once
   } else {
 #pragma unroll
     for (uint32_t st = 0; st < kScanSteps; st++) {
@@ -186,8 +184,7 @@ scan_detect_kernel(const uint8_t* __restrict__ s, uint64_t nbytes, ScanMode m,
     }
   }
   if (t == 0) {
-    counts[blockIdx.x] = ovf ? 0u : total;
-    if (ovf) flags[1] = 1u;  // same value from every overflowing block
+    counts[blockIdx.x] = ovf ? (1ull << 32) : total;
     if (blockIdx.x == 0) counts[gridDim.x] = 0u;
   }
 }
@@ -197,13 +194,13 @@ scan_detect_kernel(const uint8_t* __restrict__ s, uint64_t nbytes, ScanMode m,
 // (sorted, usually a handful).  up0 = successor (self for a terminal), dist0 = 1 if linked.
 __global__ void __launch_bounds__(256)
 scan_link_kernel(const uint8_t* __restrict__ s, uint64_t nbytes, const uint16_t* __restrict__ slots,
-                 const uint32_t* __restrict__ counts, const uint32_t* __restrict__ base,
+                 const uint64_t* __restrict__ counts, const uint64_t* __restrict__ base,
                  uint32_t n_blocks, uint64_t* __restrict__ cand, uint32_t* __restrict__ up,
                  uint32_t* __restrict__ dist) {
   const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= n_blocks) return;
-  const uint32_t c = counts[b];
-  const uint32_t o = base[b];
+  const uint32_t c = (uint32_t)counts[b];
+  const uint32_t o = (uint32_t)base[b];
   for (uint32_t k = threadIdx.x & 63u; k < c; k += 64) {
     const uint64_t p = (uint64_t)b * kScanBlockBytes + slots[(size_t)b * kScanSlots + k];
     cand[o + k] = p;
@@ -214,17 +211,85 @@ scan_link_kernel(const uint8_t* __restrict__ s, uint64_t nbytes, const uint16_t*
       if (bl < n_blocks) {
         const uint16_t* ts = slots + (size_t)bl * kScanSlots;
         const uint32_t key = (uint32_t)(nx % kScanBlockBytes);
-        uint32_t lo = 0, hi = counts[bl];
+        const uint32_t cb = (uint32_t)counts[bl];
+        uint32_t lo = 0, hi = cb;
         while (lo < hi) {
           const uint32_t mid = (lo + hi) >> 1;
           if (ts[mid] < key) lo = mid + 1; else hi = mid;
         }
-        if (lo < counts[bl] && ts[lo] == key) tgt = base[bl] + lo;
+        if (lo < cb && ts[lo] == key) tgt = (uint32_t)base[bl] + lo;
       }
     }
     up[o + k] = tgt == kNone ? o + k : tgt;
     dist[o + k] = tgt == kNone ? 0u : 1u;
   }
+}
+
+// the candidate total / overflow word (exclusive scan's last entry) to host-mapped memory
+__global__ void scan_total_kernel(const uint64_t* __restrict__ last, uint64_t* __restrict__ host) {
+  *host = *last;
+}
+
+// exclusive scan of the block counts in one workgroup, for up to kScanSmall entries
+// (streams up to 2 GiB): wave w scans the contiguous segment [w S, w S + S) as rows of 64
+// (coalesced loads, all in flight; lane-shift scans with a running carry), one barrier for
+// the wave totals, coalesced stores.  The total word (candidates | overflowing blocks << 32)
+// also goes to host-mapped memory.
+constexpr uint32_t kScanSmall = 32768;
+__global__ void __launch_bounds__(1024)
+scan_offsets_kernel(const uint64_t* __restrict__ counts, uint32_t m, uint64_t* __restrict__ base,
+                    uint64_t* __restrict__ host) {
+  constexpr uint32_t kRows = kScanSmall / 1024;
+  __shared__ uint32_t wsum[16], wovf[16];
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  const uint32_t seg = (((m + 15) / 16) + 63) & ~63u;  // S, a multiple of 64
+  const uint32_t rows = seg / 64;
+  // pass 1: wave totals (loads all in flight)
+  uint32_t sum = 0, ovf = 0;
+#pragma unroll
+  for (uint32_t r = 0; r < kRows; r++) {
+    const uint32_t i = wv * seg + r * 64 + lane;
+    const uint64_t c = (r < rows && i < m) ? counts[i] : 0ull;
+    sum += (uint32_t)c;
+    ovf |= (uint32_t)(c >> 32);
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) sum += __shfl_xor(sum, d);
+  const uint64_t any = __ballot(ovf != 0);
+  if (lane == 0) {
+    wsum[wv] = sum;
+    wovf[wv] = any ? 1u : 0u;
+  }
+  __syncthreads();
+  uint32_t carry = 0, total = 0, novf = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 16; k++) {
+    carry += k < wv ? wsum[k] : 0u;
+    total += wsum[k];
+    novf += wovf[k];
+  }
+  // pass 2: rows again (now cached), lane-shift scans with the running carry, stores
+  for (uint32_t r0 = 0; r0 < rows; r0 += 8) {
+    uint32_t v[8];
+#pragma unroll
+    for (uint32_t r = 0; r < 8; r++) {
+      const uint32_t i = wv * seg + (r0 + r) * 64 + lane;
+      v[r] = (r0 + r < rows && i < m) ? (uint32_t)counts[i] : 0u;
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < 8; r++) {
+      uint32_t incl = v[r];
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(incl, d);
+        if (lane >= (uint32_t)d) incl += o;
+      }
+      const uint32_t i = wv * seg + (r0 + r) * 64 + lane;
+      if (r0 + r < rows && i < m) base[i] = carry + incl - v[r];
+      carry += __shfl(incl, 63);
+    }
+  }
+  if (t == 0) *host = (uint64_t)total | ((uint64_t)novf << 32);
 }
 
 __device__ uint32_t find_cand(const uint64_t* cand, uint32_t n, uint64_t p) {
@@ -250,40 +315,87 @@ scan_lift_kernel(const uint32_t* __restrict__ up0, const uint32_t* __restrict__ 
   d1[c] = d0[c] + d0[u1] + d0[u2] + d0[u3];
 }
 
-// where an enumerated chain ends: its record count and the position after the terminal
-// candidate's record
+// where an enumerated chain stops: its record count and the position after its last record
 struct ChainEnd {
   uint64_t count, next_pos;
 };
 
-// enumerate the chain from candidate `start`: record i (i <= dtop[start]) is `start` lifted
-// by the base-4 digits of i.  With at_zero, only if that candidate sits at offset 0 (else
-// nothing is written and end->count = 0).  Thread 0 reports where the chain ends.
+// the last chain node from candidate c whose position is < limit (pos(c) < limit), and the
+// number of records from c to it: greedy descent over the lifting levels (at most 3 jumps
+// per level: 4 would be one jump of the level above)
+__device__ __forceinline__ uint32_t chain_descend(const uint64_t* __restrict__ cand,
+                                                  const uint32_t* __restrict__ ups,
+                                                  const uint32_t* __restrict__ dists, uint32_t n,
+                                                  int levels, uint32_t c, uint64_t limit,
+                                                  uint64_t& count) {
+  uint32_t node = c;
+  uint64_t cnt = 1;
+  for (int k = levels - 1; k >= 0; k--)
+    for (int j = 0; j < 3; j++) {
+      const uint32_t d = dists[(size_t)k * n + node];
+      if (d == 0) break;  // terminal
+      const uint32_t nx = ups[(size_t)k * n + node];
+      if (cand[nx] >= limit) break;
+      node = nx;
+      cnt += d;
+    }
+  count = cnt;
+  return node;
+}
+
+// enumerate the chain from candidate `start` up to (excluding) position `limit`: record i
+// (i <= dtop[start]) is `start` lifted by the base-4 digits of i; positions grow along the
+// chain, so the records below the limit are a prefix.  With at_zero, only if that candidate
+// sits at offset 0 (else nothing is written and end->count = 0).  Thread 0 reports where the
+// enumeration stops.
 __global__ void __launch_bounds__(256)
 scan_enum_kernel(const uint8_t* __restrict__ s, const uint64_t* __restrict__ cand,
-                 const uint32_t* __restrict__ ups, const uint32_t* __restrict__ dtop, uint32_t n,
-                 int levels, uint32_t start, int at_zero, uint64_t out_base, uint64_t cap,
-                 uint64_t* __restrict__ rec_off, uint32_t* __restrict__ rec_len,
+                 const uint32_t* __restrict__ ups, const uint32_t* __restrict__ dists, uint32_t n,
+                 int levels, uint32_t start, int at_zero, uint64_t limit, uint64_t out_base,
+                 uint64_t cap, uint64_t* __restrict__ rec_off, uint32_t* __restrict__ rec_len,
                  ChainEnd* __restrict__ end) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool ok = !(at_zero && cand[start] != 0);
-  const uint64_t count = ok ? (uint64_t)dtop[start] + 1 : 0;
   if (i == 0) {
-    uint64_t nx = 0;
+    uint64_t cnt = 0, nx = 0;
     if (ok) {
-      const uint64_t tp = cand[ups[(size_t)levels * n + start]];
+      const uint64_t tp = cand[chain_descend(cand, ups, dists, n, levels, start, limit, cnt)];
       nx = tp + be16_at(s, tp);
     }
-    end->count = count;
+    end->count = cnt;
     end->next_pos = nx;
   }
-  if (i >= count || out_base + i >= cap) return;
+  if (!ok || i > dists[(size_t)levels * n + start] || out_base + i >= cap) return;
   uint32_t node = start;
   for (int k = 0; k < levels; k++)
     for (uint32_t d = (uint32_t)(i >> (2 * k)) & 3u; d; d--) node = ups[(size_t)k * n + node];
   const uint64_t p = cand[node];
+  if (p >= limit) return;
   rec_off[out_base + i] = p;
   rec_len[out_base + i] = be16_at(s, p);
+}
+
+// exits of the shard protocol: for each candidate c below `window` (the first ones: cand is
+// sorted), the position where its chain first reaches >= limit; bit 63 set when the chain
+// leaves the candidate set before (the exit then needs the sequential walk).  Entries past
+// the window are ~0.
+__global__ void __launch_bounds__(256)
+scan_exits_kernel(const uint8_t* __restrict__ s, const uint64_t* __restrict__ cand,
+                  const uint32_t* __restrict__ ups, const uint32_t* __restrict__ dists, uint32_t n,
+                  int levels, uint64_t window, uint64_t limit, uint32_t cap,
+                  uint64_t* __restrict__ entries, uint64_t* __restrict__ exits) {
+  const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= cap) return;
+  if (c >= n || cand[c] >= window || cand[c] >= limit) {
+    entries[c] = ~0ull;
+    exits[c] = ~0ull;
+    return;
+  }
+  uint64_t cnt;
+  const uint64_t tp = cand[chain_descend(cand, ups, dists, n, levels, c, limit, cnt)];
+  const uint64_t nx = tp + be16_at(s, tp);
+  entries[c] = cand[c];
+  exits[c] = nx | (nx < limit ? (1ull << 63) : 0ull);
 }
 
 // 4. sequential resolver (one thread): the reference rule from position p until the chain
@@ -292,10 +404,12 @@ struct ResolveState {
   uint64_t pos;        // in: start position; out: where it stopped
   uint64_t emitted;    // out: records written
   uint32_t next_cand;  // out: candidate index at `pos` (kNone if none)
-  int32_t reason;      // out: 0 = candidate reached, 1 = end of stream, 2 = TCP error, 3 = steps
+  int32_t reason;      // out: 0 = candidate reached, 1 = end of stream, 2 = TCP error, 3 = steps,
+                       //      4 = position >= limit
 };
 
-__global__ void scan_resolve_kernel(const uint8_t* __restrict__ s, uint64_t nbytes, int sink,
+__global__ void scan_resolve_kernel(const uint8_t* __restrict__ s, uint64_t nbytes, uint64_t limit,
+                                    int sink,
                                     const uint64_t* __restrict__ cand, uint32_t n,
                                     uint64_t out_base, uint64_t cap, uint64_t max_steps,
                                     uint64_t* __restrict__ rec_off, uint32_t* __restrict__ rec_len,
@@ -311,6 +425,7 @@ __global__ void scan_resolve_kernel(const uint8_t* __restrict__ s, uint64_t nbyt
       if (nc != kNone) { reason = 0; break; }
     }
     first = false;
+    if (p >= limit) { reason = 4; break; }
     if (p + 2 > nbytes) { reason = 1; break; }
     const uint32_t L = be16_at(s, p);
     if (sink) {
@@ -362,151 +477,177 @@ size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 }  // namespace
 
 // The workspace lives with the context (grown on demand, freed by mgenx_ctx_destroy via
-// mgenx_scan_release).
+// mgenx_scan_ws_free).  It also keeps the candidate tables of the last stream built, which
+// mgenx_stream_scan_range may reuse on request.
 struct mgenx_scan_ws {
-  ScanWork slots, cand, tabs, small;
+  ScanWork slots, cands, tabs, small;
+  // host-mapped (fine-grained) words the kernels write their results to: [0] candidate
+  // total, [2..3] chain end -- no copy operations on the common path
+  uint64_t* host = nullptr;
+  uint64_t* host_dev = nullptr;
+  // tables of the last build
+  const uint8_t* key_s = nullptr;
+  uint64_t key_n = 0;
+  int key_mode = -1;
+  uint32_t n = 0;      // candidates (0 when a block overflowed: resolver only)
+  int levels = 0;      // lifting levels: ups / dists hold levels + 1 tables of n
+  uint64_t* cand = nullptr;
+  uint32_t* ups = nullptr;
+  uint32_t* dists = nullptr;
 };
 
 extern "C" void* mgenx_scan_ws_new() { return new mgenx_scan_ws(); }
 extern "C" void mgenx_scan_ws_free(void* p) {
   mgenx_scan_ws* w = static_cast<mgenx_scan_ws*>(p);
   if (!w) return;
-  for (ScanWork* x : {&w->slots, &w->cand, &w->tabs, &w->small})
+  for (ScanWork* x : {&w->slots, &w->cands, &w->tabs, &w->small})
     if (x->mem) hipFree(x->mem);
+  if (w->host) hipHostFree(w->host);
   delete w;
 }
 
-// Runs the whole scan (synchronous on `stream`: the record count decides later launches).
-extern "C" int mgenx_scan_run(void* wsp, const uint8_t* s, uint64_t nbytes, int mode,
-                              uint64_t* rec_off, uint32_t* rec_len, uint64_t cap,
-                              mgenx_scan_info* info, hipStream_t stream, char* err, size_t errn) {
-  mgenx_scan_ws& ws = *static_cast<mgenx_scan_ws*>(wsp);
-  const bool sink = mode == MGENX_SCAN_SINK;
-  const ScanMode m = sink ? ScanMode{MGENX_MIN_SIZE, MGENX_MAX_SIZE} : ScanMode{4u, 65535u};
-  mgenx_scan_info out;
-  memset(&out, 0, sizeof(out));
-  auto fail = [&](hipError_t e, const char* what) {
+namespace {
+
+struct Fail {
+  char* err;
+  size_t errn;
+  int operator()(hipError_t e, const char* what) const {
     snprintf(err, errn, "%s: %s", what, hipGetErrorString(e));
     return MGENX_EDEVICE;
-  };
+  }
+};
+
+// detect -> device scan of the block counts -> (one copy back: the candidate total) ->
+// compact + link -> lifting levels.  Leaves the tables in ws (async after the copy).
+int scan_build(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, int mode, hipStream_t stream,
+               const Fail& fail) {
+  const bool sink = mode == MGENX_SCAN_SINK;
+  const ScanMode m = sink ? ScanMode{MGENX_MIN_SIZE, MGENX_MAX_SIZE} : ScanMode{4u, 65535u};
   hipError_t e;
-  // small scratch: resolver state, total
+  ws.key_s = nullptr;
+  ws.n = 0;
+  ws.levels = 0;
+  ws.cand = nullptr;
+  ws.ups = ws.dists = nullptr;
   if ((e = ensure(ws.small, 4096)) != hipSuccess) return fail(e, "scan workspace");
-  ResolveState* d_st = reinterpret_cast<ResolveState*>(ws.small.mem);
-  uint32_t* d_total = reinterpret_cast<uint32_t*>(static_cast<char*>(ws.small.mem) + 256);
-
-  uint32_t n = 0;  // candidates
-  const uint64_t n_blocks64 = (nbytes + kScanBlockBytes - 1) / kScanBlockBytes;
-  bool overflow = n_blocks64 == 0 || n_blocks64 > 0xFFFFFFull;
-  uint64_t* d_cand = nullptr;
-  uint32_t* d_up = nullptr;
-  uint32_t* d_dist = nullptr;
-  uint32_t* d_counts = nullptr;
-  uint32_t* d_base = nullptr;
-  int levels = 1;
-  uint32_t nb = 0;
-  struct {
-    uint32_t total, flags;
-  } h_tot = {0, 0};
-  if (!overflow) {
-    nb = (uint32_t)n_blocks64;
-    const size_t slot_b = align256((size_t)nb * kScanSlots * 2);
-    const size_t cnt_b = align256((size_t)(nb + 1) * 4);
-    size_t cub_bytes = 0;
-    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, cub_bytes, (const uint32_t*)nullptr,
-                                           (uint32_t*)nullptr, (int)(nb + 1), stream);
-    if ((e = ensure(ws.slots, slot_b + 2 * cnt_b + align256(cub_bytes))) != hipSuccess)
+  if (!ws.host) {
+    void* hp = nullptr;
+    if ((e = hipHostMalloc(&hp, 64, hipHostMallocMapped)) != hipSuccess)
       return fail(e, "scan workspace");
-    uint16_t* d_slots = static_cast<uint16_t*>(ws.slots.mem);
-    d_counts = reinterpret_cast<uint32_t*>(static_cast<char*>(ws.slots.mem) + slot_b);
-    d_base = d_counts + cnt_b / 4;
-    void* d_cub = static_cast<char*>(ws.slots.mem) + slot_b + 2 * cnt_b;
-    if ((e = hipMemsetAsync(d_total, 0, 8, stream)) != hipSuccess) return fail(e, "scan");
-    static const bool nt = getenv("MGENX_SCAN_NT") && atoi(getenv("MGENX_SCAN_NT"));
-    if (nt)
-      hipLaunchKernelGGL(scan_detect_kernel<true>, dim3(nb), dim3(kScanThreads), 0, stream, s,
-                         nbytes, m, d_slots, d_counts, d_total);
-    else
-      hipLaunchKernelGGL(scan_detect_kernel<false>, dim3(nb), dim3(kScanThreads), 0, stream, s,
-                         nbytes, m, d_slots, d_counts, d_total);
-    if ((e = hipcub::DeviceScan::ExclusiveSum(d_cub, cub_bytes, (const uint32_t*)d_counts, d_base,
-                                              (int)(nb + 1), stream)) != hipSuccess)
-      return fail(e, "scan offsets");
-    if ((e = hipMemcpyAsync(d_total, d_base + nb, 4, hipMemcpyDeviceToDevice, stream)) != hipSuccess ||
-        (e = hipMemcpyAsync(&h_tot, d_total, 8, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
-        (e = hipStreamSynchronize(stream)) != hipSuccess)
-      return fail(e, "scan detect");
-    n = h_tot.total;
-    if (h_tot.flags) {
-      overflow = true;
-      n = 0;
-    } else if (n > 0) {
-      levels = 1;
-      while ((1ull << (2 * levels)) < n) levels++;  // 4^levels >= n > any chain length
-      if ((e = ensure(ws.cand, (size_t)n * 8)) != hipSuccess) return fail(e, "scan workspace");
-      if ((e = ensure(ws.tabs, (size_t)n * 4 * (levels + 3))) != hipSuccess)
-        return fail(e, "scan workspace");
-      d_cand = static_cast<uint64_t*>(ws.cand.mem);
-      d_up = static_cast<uint32_t*>(ws.tabs.mem);                 // [levels + 1][n]
-      d_dist = d_up + (size_t)(levels + 1) * n;                    // 2 x [n] ping-pong
-      hipLaunchKernelGGL(scan_link_kernel, dim3((nb + 3) / 4), dim3(256), 0, stream, s, nbytes,
-                         d_slots, d_counts, d_base, nb, d_cand, d_up, d_dist);
-      const dim3 g((n + 255) / 256);
-      for (int k = 1; k <= levels; k++) {
-        uint32_t* d0 = d_dist + (size_t)((k - 1) & 1) * n;
-        uint32_t* d1 = d_dist + (size_t)(k & 1) * n;
-        hipLaunchKernelGGL(scan_lift_kernel, g, dim3(256), 0, stream, d_up + (size_t)(k - 1) * n,
-                           d0, d_up + (size_t)k * n, d1, n);
-      }
-    }
+    ws.host = static_cast<uint64_t*>(hp);
+    void* dp = nullptr;
+    if ((e = hipHostGetDevicePointer(&dp, hp, 0)) != hipSuccess) return fail(e, "scan workspace");
+    ws.host_dev = static_cast<uint64_t*>(dp);
   }
-  if (overflow) n = 0;  // pathological stream: the resolver walks all of it
-  uint32_t* d_dtop = d_dist ? d_dist + (size_t)(levels & 1) * n : nullptr;
-  ChainEnd* d_end = reinterpret_cast<ChainEnd*>(static_cast<char*>(ws.small.mem) + 512);
-
-  // chain walk from position 0.  Common case, fully on the device: offset 0 is a candidate,
-  // its chain is enumerated and the enumeration reports where it ends (one copy back).
-  uint64_t pos = 0, total = 0;
-  uint32_t at = kNone;  // candidate index at pos (if any)
-  if (n) {
-    struct {
-      ChainEnd end;
-    } h = {{0, 0}};
-    hipLaunchKernelGGL(scan_enum_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, s, d_cand,
-                       d_up, d_dtop, n, levels, 0u, 1, (uint64_t)0, cap, rec_off, rec_len, d_end);
-    if ((e = hipMemcpyAsync(&h.end, d_end, sizeof(ChainEnd), hipMemcpyDeviceToHost, stream)) != hipSuccess ||
-        (e = hipStreamSynchronize(stream)) != hipSuccess)
-      return fail(e, "scan");
-    if (h.end.count) {
-      total = h.end.count;
-      pos = h.end.next_pos;
-    }
-  }
-  if (total && pos + 2 > nbytes) {  // the chain ran to the end of the stream: done
-    if ((e = hipGetLastError()) != hipSuccess) return fail(e, "scan launch");
-    out.n_records = total;
-    out.consumed = pos;
-    out.status = 0;
-    out.candidates = n;
-    if (info) *info = out;
+  const uint64_t n_blocks64 = (nbytes + kScanBlockBytes - 1) / kScanBlockBytes;
+  if (n_blocks64 == 0 || n_blocks64 > 0xFFFFFFull) {  // nothing to index: resolver only
+    ws.key_s = s;
+    ws.key_n = nbytes;
+    ws.key_mode = mode;
     return MGENX_OK;
   }
+  const uint32_t nb = (uint32_t)n_blocks64;
+  const size_t slot_b = align256((size_t)nb * kScanSlots * 2);
+  const size_t cnt_b = align256((size_t)(nb + 1) * 8);
+  size_t cub_bytes = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, cub_bytes, (const uint64_t*)nullptr,
+                                         (uint64_t*)nullptr, (int)(nb + 1), stream);
+  if ((e = ensure(ws.slots, slot_b + 2 * cnt_b + align256(cub_bytes))) != hipSuccess)
+    return fail(e, "scan workspace");
+  uint16_t* d_slots = static_cast<uint16_t*>(ws.slots.mem);
+  uint64_t* d_counts = reinterpret_cast<uint64_t*>(static_cast<char*>(ws.slots.mem) + slot_b);
+  uint64_t* d_base = d_counts + cnt_b / 8;
+  void* d_cub = static_cast<char*>(ws.slots.mem) + slot_b + 2 * cnt_b;
+  hipLaunchKernelGGL(scan_detect_kernel, dim3(nb), dim3(kScanThreads), 0, stream, s, nbytes, m,
+                     d_slots, d_counts);
+  if (nb + 1 <= kScanSmall) {
+    hipLaunchKernelGGL(scan_offsets_kernel, dim3(1), dim3(1024), 0, stream, d_counts, nb + 1,
+                       d_base, ws.host_dev);
+  } else {
+    if ((e = hipcub::DeviceScan::ExclusiveSum(d_cub, cub_bytes, (const uint64_t*)d_counts, d_base,
+                                              (int)(nb + 1), stream)) != hipSuccess)
+      return fail(e, "scan offsets");
+    hipLaunchKernelGGL(scan_total_kernel, dim3(1), dim3(1), 0, stream, d_base + nb, ws.host_dev);
+  }
+  if ((e = hipStreamSynchronize(stream)) != hipSuccess) return fail(e, "scan detect");
+  struct {
+    uint32_t total, overflowed;  // candidates, overflowing blocks
+  } h_tot;
+  memcpy(&h_tot, (const void*)ws.host, 8);
+  ws.key_s = s;
+  ws.key_n = nbytes;
+  ws.key_mode = mode;
+  if (h_tot.overflowed || h_tot.total == 0) return MGENX_OK;  // resolver only
+  const uint32_t n = h_tot.total;
+  int levels = 1;
+  while ((1ull << (2 * levels)) < n) levels++;  // 4^levels >= n > any chain length
+  if ((e = ensure(ws.cands, (size_t)n * 8)) != hipSuccess) return fail(e, "scan workspace");
+  if ((e = ensure(ws.tabs, (size_t)n * 4 * 2 * (levels + 1))) != hipSuccess)
+    return fail(e, "scan workspace");
+  ws.n = n;
+  ws.levels = levels;
+  ws.cand = static_cast<uint64_t*>(ws.cands.mem);
+  ws.ups = static_cast<uint32_t*>(ws.tabs.mem);        // [levels + 1][n]
+  ws.dists = ws.ups + (size_t)(levels + 1) * n;         // [levels + 1][n]
+  hipLaunchKernelGGL(scan_link_kernel, dim3((nb + 3) / 4), dim3(256), 0, stream, s, nbytes,
+                     d_slots, d_counts, d_base, nb, ws.cand, ws.ups, ws.dists);
+  const dim3 g((n + 255) / 256);
+  for (int k = 1; k <= levels; k++)
+    hipLaunchKernelGGL(scan_lift_kernel, g, dim3(256), 0, stream, ws.ups + (size_t)(k - 1) * n,
+                       ws.dists + (size_t)(k - 1) * n, ws.ups + (size_t)k * n,
+                       ws.dists + (size_t)k * n, n);
+  if ((e = hipGetLastError()) != hipSuccess) return fail(e, "scan launch");
+  return MGENX_OK;
+}
+
+// the chain from `entry` over positions < limit, on the tables of ws.  The common case
+// (entry is candidate 0 at offset 0, or any candidate: at_zero) is one enumeration and one
+// copy back; positions off the candidate set go through the sequential resolver.
+int scan_walk(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, int mode, uint64_t entry,
+              uint64_t limit, uint64_t* rec_off, uint32_t* rec_len, uint64_t cap,
+              mgenx_scan_info* info, hipStream_t stream, const Fail& fail) {
+  const bool sink = mode == MGENX_SCAN_SINK;
+  const uint32_t n = ws.n;
+  const int levels = ws.levels;
+  hipError_t e;
+  mgenx_scan_info out;
+  memset(&out, 0, sizeof(out));
+  ResolveState* d_st = reinterpret_cast<ResolveState*>(ws.small.mem);
+  ChainEnd* d_end = reinterpret_cast<ChainEnd*>(ws.host_dev + 2);
+  const volatile uint64_t* h_end = ws.host + 2;
+  uint64_t pos = entry, total = 0;
+  uint32_t at = kNone;  // candidate index at pos, when known
+  bool done = false;
   int reason = 1;
-  for (int rounds = 0; rounds < (1 << 30); rounds++) {
+  if (n && entry == 0 && entry < limit) {
+    // candidate 0 is offset 0 when offset 0 is a candidate: enumerate speculatively
+    hipLaunchKernelGGL(scan_enum_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, s, ws.cand,
+                       ws.ups, ws.dists, n, levels, 0u, 1, limit, (uint64_t)0, cap, rec_off,
+                       rec_len, d_end);
+    if ((e = hipStreamSynchronize(stream)) != hipSuccess) return fail(e, "scan");
+    const ChainEnd h = {h_end[0], h_end[1]};
+    if (h.count) {
+      total = h.count;
+      pos = h.next_pos;
+      if (pos >= limit) { reason = 4; done = true; }
+      else if (pos + 2 > nbytes) { reason = 1; done = true; }
+    }
+  }
+  for (int rounds = 0; !done && rounds < (1 << 30); rounds++) {
     if (at != kNone) {
       // enumerate the candidate chain from `at` (grid sized by n >= its length)
-      ChainEnd h_end = {0, 0};
-      hipLaunchKernelGGL(scan_enum_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, s, d_cand,
-                         d_up, d_dtop, n, levels, at, 0, total, cap, rec_off, rec_len, d_end);
-      if ((e = hipMemcpyAsync(&h_end, d_end, sizeof(h_end), hipMemcpyDeviceToHost, stream)) != hipSuccess ||
-          (e = hipStreamSynchronize(stream)) != hipSuccess)
-        return fail(e, "scan");
-      total += h_end.count;
-      pos = h_end.next_pos;
+      hipLaunchKernelGGL(scan_enum_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, s,
+                         ws.cand, ws.ups, ws.dists, n, levels, at, 0, limit, total, cap, rec_off,
+                         rec_len, d_end);
+      if ((e = hipStreamSynchronize(stream)) != hipSuccess) return fail(e, "scan");
+      const ChainEnd h = {h_end[0], h_end[1]};
+      total += h.count;
+      pos = h.next_pos;
       at = kNone;
+      if (pos >= limit) { reason = 4; break; }
       if (pos + 2 > nbytes) { reason = 1; break; }
     }
-    // resolver from pos (pos is not a candidate)
+    // resolver from pos (pos is not a candidate, or is the entry itself)
     ResolveState st;
     st.pos = pos;
     st.emitted = 0;
@@ -514,8 +655,8 @@ extern "C" int mgenx_scan_run(void* wsp, const uint8_t* s, uint64_t nbytes, int 
     st.reason = 3;
     if ((e = hipMemcpyAsync(d_st, &st, sizeof(st), hipMemcpyHostToDevice, stream)) != hipSuccess)
       return fail(e, "scan");
-    hipLaunchKernelGGL(scan_resolve_kernel, dim3(1), dim3(1), 0, stream, s, nbytes, (int)sink,
-                       d_cand, n, total, cap, (uint64_t)1 << 20, rec_off, rec_len, d_st);
+    hipLaunchKernelGGL(scan_resolve_kernel, dim3(1), dim3(1), 0, stream, s, nbytes, limit,
+                       (int)sink, ws.cand, n, total, cap, (uint64_t)1 << 20, rec_off, rec_len, d_st);
     if ((e = hipMemcpyAsync(&st, d_st, sizeof(st), hipMemcpyDeviceToHost, stream)) != hipSuccess ||
         (e = hipStreamSynchronize(stream)) != hipSuccess)
       return fail(e, "scan resolve");
@@ -528,11 +669,64 @@ extern "C" int mgenx_scan_run(void* wsp, const uint8_t* s, uint64_t nbytes, int 
     break;
   }
   if ((e = hipGetLastError()) != hipSuccess) return fail(e, "scan launch");
-  if ((e = hipStreamSynchronize(stream)) != hipSuccess) return fail(e, "scan");
   out.n_records = total;
   out.consumed = pos;
   out.status = reason == 2 ? 1 : 0;
   out.candidates = n;
   if (info) *info = out;
   return MGENX_OK;
+}
+
+}  // namespace
+
+// Whole-stream scan from offset 0 (synchronous on `stream`).
+extern "C" int mgenx_scan_run(void* wsp, const uint8_t* s, uint64_t nbytes, int mode,
+                              uint64_t* rec_off, uint32_t* rec_len, uint64_t cap,
+                              mgenx_scan_info* info, hipStream_t stream, char* err, size_t errn) {
+  mgenx_scan_ws& ws = *static_cast<mgenx_scan_ws*>(wsp);
+  const Fail fail{err, errn};
+  int rc = scan_build(ws, s, nbytes, mode, stream, fail);
+  if (rc != MGENX_OK) return rc;
+  return scan_walk(ws, s, nbytes, mode, 0, nbytes, rec_off, rec_len, cap, info, stream, fail);
+}
+
+// One shard of a stream split over ranks: builds the tables and reports, for each candidate
+// below `window`, where its chain leaves [.., limit).
+extern "C" int mgenx_scan_exits_run(void* wsp, const uint8_t* s, uint64_t nbytes, int mode,
+                                    uint64_t window, uint64_t limit, uint64_t* entries,
+                                    uint64_t* exits, uint32_t cap, uint32_t* candidates,
+                                    hipStream_t stream, char* err, size_t errn) {
+  mgenx_scan_ws& ws = *static_cast<mgenx_scan_ws*>(wsp);
+  const Fail fail{err, errn};
+  int rc = scan_build(ws, s, nbytes, mode, stream, fail);
+  if (rc != MGENX_OK) return rc;
+  if (cap)
+    hipLaunchKernelGGL(scan_exits_kernel, dim3((cap + 255) / 256), dim3(256), 0, stream, s,
+                       ws.cand, ws.ups, ws.dists, ws.n, ws.levels, window, limit, cap, entries,
+                       exits);
+  hipError_t e;
+  if ((e = hipGetLastError()) != hipSuccess) return fail(e, "scan launch");
+  if (candidates) *candidates = ws.n;
+  return MGENX_OK;
+}
+
+// The records of [entry, limit) (synchronous).  reuse: the tables of the previous build on
+// this workspace are for this same stream (pointer, size, mode; the caller vouches that the
+// bytes are unchanged).
+extern "C" int mgenx_scan_range_run(void* wsp, const uint8_t* s, uint64_t nbytes, int mode,
+                                    uint64_t entry, uint64_t limit, int reuse, uint64_t* rec_off,
+                                    uint32_t* rec_len, uint64_t cap, mgenx_scan_info* info,
+                                    hipStream_t stream, char* err, size_t errn) {
+  mgenx_scan_ws& ws = *static_cast<mgenx_scan_ws*>(wsp);
+  const Fail fail{err, errn};
+  if (reuse) {
+    if (ws.key_s != s || ws.key_n != nbytes || ws.key_mode != mode) {
+      snprintf(err, errn, "scan range: no tables built for this stream to reuse");
+      return MGENX_EINVAL;
+    }
+  } else {
+    int rc = scan_build(ws, s, nbytes, mode, stream, fail);
+    if (rc != MGENX_OK) return rc;
+  }
+  return scan_walk(ws, s, nbytes, mode, entry, limit, rec_off, rec_len, cap, info, stream, fail);
 }

@@ -4,7 +4,7 @@ set -u
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 120 python scripts/scan_profile.py read > gpurun_out/scan_v0.log 2>&1 || exit 3
-MGENX_SCAN_NT=1 timeout -k 10 120 python scripts/scan_profile.py > gpurun_out/scan_v1.log 2>&1 || exit 3
+
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/scanprof3 -o scan -- python scripts/scan_profile.py > gpurun_out/scanprof3.log 2>&1 || exit 3
-MGENX_SCAN_NT=1 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/scanprof4 -o scan -- python scripts/scan_profile.py > gpurun_out/scanprof4.log 2>&1 || exit 3
-grep -h "scan_ms\|stream_read_ms" gpurun_out/scan_v0.log gpurun_out/scan_v1.log
+
+grep -h "scan_ms\|stream_read_ms" gpurun_out/scan_v0.log

@@ -26,47 +26,11 @@ def eng(torch):
 
 @pytest.fixture(scope="module")
 def gold():
-    import os
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    return dict(np.load(os.path.join(root, "tests", "golden", "udp_matrix.npz"),
-                        allow_pickle=False))
+    from streams import golden
+    return golden()
 
 
-def _desc(gold, n, rng):
-    d = np.zeros(n, gold["desc"].dtype)
-    d["tmpl"] = rng.integers(0, len(gold["tmpl"]), n)
-    d["seq_num"] = np.arange(n)
-    d["tx_sec"] = 1_700_000_000
-    d["tx_usec"] = rng.integers(0, 1_000_000, n)
-    d["flags"] = 4
-    return d
-
-
-def tcp_stream(gold, sizes, rng, checksum=True):
-    from oracle import oracle as O
-    d = _desc(gold, len(sizes), rng)
-    d["msg_len"] = np.minimum(sizes, 65535)
-    return np.asarray(O.tcp_tx_batch(gold["tmpl"], d, np.asarray(sizes, np.uint32), gold["pool"],
-                                      checksum=checksum), np.uint8)
-
-
-def sink_stream(gold, sizes, rng, garbage_every=0):
-    """UDP-packed records back to back (the SINK framing input), optionally with short runs
-    of bytes whose length field is invalid (resynchronisation)."""
-    from oracle import oracle as O
-    d = _desc(gold, len(sizes), rng)
-    d["msg_len"] = sizes
-    offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
-    slab, lens = O.udp_pack_batch(gold["tmpl"], d, gold["pool"], int(np.sum(sizes)),
-                                  rec_off=offs, checksum=True)
-    parts = []
-    for i, (o, s) in enumerate(zip(offs, sizes)):
-        if garbage_every and i % garbage_every == 3:
-            parts.append(np.array([0x00, 0x05, 0xAB, 0xFF, 0x7F, 0xFF][: 2 * (1 + i % 3)],
-                                  np.uint8))
-        if lens[i]:
-            parts.append(slab[int(o):int(o) + int(lens[i])])
-    return np.concatenate(parts)
+from streams import sink_stream, tcp_stream  # noqa: E402
 
 
 def check(torch, eng, stream, mode):
@@ -164,3 +128,137 @@ def test_config5_stream_scan_then_unpack(torch, eng, gold):
     torch.cuda.synchronize()
     assert int((cols["err"] != 0).sum()) == 0
     assert np.array_equal(cols["seq_num"].cpu().numpy().view(np.uint32), np.arange(n))
+
+
+# ---- sharded framing (mgenx_stream_scan_exits / _range, mgen_amd/shard.py) ----
+
+def _corpus():
+    from streams import corpus
+    return corpus()
+
+
+@pytest.mark.parametrize("case", range(7))
+def test_scan_range_vs_sequential(torch, eng, case):
+    """mgenx_stream_scan_range from arbitrary entries below arbitrary limits equals the
+    reference rule started there (tests/shard_ref.walk)."""
+    from mgen_amd import to_device
+    from shard_ref import walk
+    _, s, mode = _corpus()[case]
+    d = to_device(s)
+    rng = np.random.default_rng(SEED + 40 + case)
+    b = s.tobytes()
+    reuse = False
+    for _ in range(6):
+        entry = int(rng.integers(0, len(s) // 2))
+        limit = int(rng.integers(entry, len(s) + 1))
+        offs, lens, info = eng.stream_scan_range(d, mode, entry, limit, reuse=reuse)
+        reuse = True
+        wo, wl, wc, ws = walk(b, mode, entry, limit)
+        assert np.array_equal(offs.cpu().numpy(), np.asarray(wo, np.int64))
+        assert np.array_equal(lens.cpu().numpy(), np.asarray(wl, np.int32))
+        assert (int(info.consumed), int(info.status)) == (wc, ws)
+    # offset 0 to the end is the whole-stream scan
+    offs, lens, info = eng.stream_scan_range(d, mode, 0, len(s))
+    wo, wl, wc, ws = walk(b, mode, 0, len(s))
+    assert np.array_equal(offs.cpu().numpy(), np.asarray(wo, np.int64))
+
+
+def test_scan_range_reuse_needs_tables(torch, eng):
+    from mgen_amd import MgenxError, to_device
+    d = to_device(np.zeros(1000, np.uint8))
+    eng.stream_scan(d, 0)
+    d2 = to_device(np.zeros(1000, np.uint8))
+    with pytest.raises(MgenxError):
+        eng.stream_scan_range(d2, 0, 0, 1000, reuse=True)
+
+
+@pytest.mark.parametrize("case", range(7))
+def test_scan_exits_vs_reference(torch, eng, case):
+    from mgen_amd import to_device
+    from mgen_amd.shard import HALO
+    from shard_ref import RefScanner
+    _, s, mode = _corpus()[case]
+    for a, limit in ((0, len(s) // 2), (len(s) // 3, len(s) // 4)):
+        local = s[a:a + limit + HALO]
+        ent, ext, _ = eng.stream_scan_exits(to_device(local), mode, HALO, limit, cap=4096)
+        want = RefScanner(local.tobytes()).exits(None, mode, HALO, limit)
+        assert np.array_equal(ent.cpu().numpy().view(np.uint64), want[0])
+        assert np.array_equal(ext.cpu().numpy().view(np.uint64), want[1])
+
+
+def _sharded_gpu(s, mode, world):
+    import threading
+
+    from mgen_amd import Engine, to_device
+    from mgen_amd.shard import EngineScanner, ThreadComm, scan_sharded, shard_bounds
+    tc = ThreadComm(world)
+    res, err = [None] * world, []
+
+    def go(r):
+        try:
+            e = Engine(0)
+            a, _, hi = shard_bounds(len(s), world, r)
+            local = to_device(s[a:hi])
+            offs, lens, summ = scan_sharded(EngineScanner(e), tc.rank_view(r), local, len(s),
+                                            mode)
+            o = np.zeros(0, np.int64) if offs is None else offs.cpu().numpy() + a
+            ln = np.zeros(0, np.int32) if lens is None else lens.cpu().numpy()
+            res[r] = (o, ln, summ)
+            e.close()
+        except BaseException as ex:  # noqa: BLE001
+            err.append(ex)
+            tc._bar.abort()
+    th = [threading.Thread(target=go, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    assert not err, err
+    return res
+
+
+@pytest.mark.parametrize("world", [2, 3, 5])
+def test_sharded_scan_gpu_equals_whole(torch, eng, world):
+    """Simulated ranks (threads, one context each) on one GPU: the union of the shards'
+    records and the stitched summary equal the whole-stream scan, on every corpus case."""
+    from mgen_amd import to_device
+    for name, s, mode in _corpus():
+        offs, lens, info = eng.stream_scan(to_device(s), mode)
+        res = _sharded_gpu(s, mode, world)
+        assert np.array_equal(np.concatenate([r[0] for r in res]), offs.cpu().numpy()), name
+        assert np.array_equal(np.concatenate([r[1] for r in res]), lens.cpu().numpy()), name
+        for r in res:
+            assert r[2] == (int(info.n_records), int(info.consumed), int(info.status)), name
+
+
+def test_sharded_scan_config5_shape(torch, eng, gold):
+    """Config 5 records (16 KiB, TCP, checksum on) over a 64 MiB stream in 4 shards."""
+    from mgen_amd import to_device
+    n = 4096
+    rng = np.random.default_rng(SEED + 50)
+    s = tcp_stream(gold, np.full(n, 16384), rng)
+    res = _sharded_gpu(s, 0, 4)
+    assert np.array_equal(np.concatenate([r[0] for r in res]), np.arange(n) * 16384)
+    assert all(r[2] == (n, len(s), 0) for r in res)
+    del to_device
+
+
+def test_scan_beyond_4gib_device_scan_path(torch, eng, gold):
+    """A stream of more than 65535 detect blocks (> 4 GiB) takes the multi-workgroup
+    exclusive scan of the block counts: a valid prefix followed by zero bytes frames as the
+    oracle frames the prefix plus the zero-length error after it."""
+    from oracle import oracle as O
+    rng = np.random.default_rng(SEED + 60)
+    pre = tcp_stream(gold, rng.integers(76, 3000, 50), rng)
+    n = (4 << 30) + 3 * 65536 + 123
+    d = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    d[:len(pre)] = torch.from_numpy(pre).cuda()
+    tail = 5 << 20                                  # records planted near the end too
+    d[n - tail:n - tail + len(pre)] = torch.from_numpy(pre).cuda()
+    offs, lens, info = eng.stream_scan(d, 0, cap=1000)
+    wo, wl, _, wc, ws = O.tcp_scan(np.concatenate([pre, np.zeros(16, np.uint8)]).tobytes())
+    assert np.array_equal(offs.cpu().numpy(), np.asarray(wo, np.int64))
+    assert (int(info.consumed), int(info.status)) == (wc, 1)
+    assert int(info.candidates) >= 2 * len(wo)
+    del d
+    torch.cuda.empty_cache()
