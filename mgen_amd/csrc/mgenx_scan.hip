@@ -97,13 +97,18 @@ __device__ __forceinline__ uint32_t wave_excl(uint32_t c, uint32_t& wtot) {
 // A position needs the 3 bytes after it: the next lane's first word comes by a lane shift,
 // across waves through LDS.  Candidates go to the block's slots in stream order (step-major,
 // then lane): per-step wave prefixes by ballot, one workgroup barrier for the wave totals.
-// Writes counts[b] = candidates (low word) | overflowed << 32 (an overflowing block keeps
-// none), and block 0 zeroes counts[n_blocks]: the exclusive scan's last entry then holds
-// the candidate total and the number of overflowing blocks in one word.
+// Writes counts[b] = candidates (low word) | overflowed << 32 (a block with more candidates
+// than slots writes none), and block 0 zeroes counts[n_blocks]: the exclusive scan's last
+// entry then holds the candidate total and the number of overflowing blocks in one word.
+// kRedo: the second pass over the overflowing blocks only, once the offsets are known:
+// positions go straight to cand[base[b] ...] with no slot limit.
+template <bool kRedo>
 __global__ void __launch_bounds__(kScanThreads)
 scan_detect_kernel(const uint8_t* __restrict__ s, uint64_t nbytes, ScanMode m,
-                   uint16_t* __restrict__ slots, uint64_t* __restrict__ counts) {
+                   uint16_t* __restrict__ slots, uint64_t* __restrict__ counts,
+                   const uint64_t* __restrict__ base, uint64_t* __restrict__ cand) {
   constexpr uint32_t kW = kScanThreads / 64;
+  if (kRedo && !(counts[blockIdx.x] >> 32)) return;
   __shared__ uint32_t first[kScanSteps + 1][kW];  // first word of each wave's chunk per step
   __shared__ uint32_t wsum[kScanSteps][kW];
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
@@ -159,9 +164,10 @@ scan_detect_kernel(const uint8_t* __restrict__ s, uint64_t nbytes, ScanMode m,
   for (uint32_t st = 0; st < kScanSteps; st++)
 #pragma unroll
     for (uint32_t k = 0; k < kW; k++) total += wsum[st][k];
-  const bool ovf = total > kScanSlots;
+  const bool ovf = !kRedo && total > kScanSlots;
   if (!ovf && total) {
     uint16_t* out = slots + (size_t)blockIdx.x * kScanSlots;
+    uint64_t* outc = kRedo ? cand + (uint32_t)base[blockIdx.x] : nullptr;
     uint32_t run = 0;
 #pragma unroll
     for (uint32_t st = 0; st < kScanSteps; st++) {
@@ -177,21 +183,25 @@ scan_detect_kernel(const uint8_t* __restrict__ s, uint64_t nbytes, ScanMode m,
         while (h) {
           const int i = __ffs(h) - 1;
           h &= h - 1;
-          out[pos++] = (uint16_t)(16u * (st * kScanThreads + t) + (uint32_t)i);
+          const uint32_t off = 16u * (st * kScanThreads + t) + (uint32_t)i;
+          if (kRedo) outc[pos++] = block0 + off;
+          else out[pos++] = (uint16_t)off;
         }
       }
       run += stot;
     }
   }
-  if (t == 0) {
-    counts[blockIdx.x] = ovf ? (1ull << 32) : total;
+  if (!kRedo && t == 0) {
+    counts[blockIdx.x] = (uint64_t)total | (ovf ? (1ull << 32) : 0ull);
     if (blockIdx.x == 0) counts[gridDim.x] = 0u;
   }
 }
 
 // 2. compact + link, one wave per block: candidate positions into the global sorted
 // array, and each candidate's successor p + L searched in the target block's own slots
-// (sorted, usually a handful).  up0 = successor (self for a terminal), dist0 = 1 if linked.
+// (sorted, usually a handful) -- or, for a block that overflowed its slots, in its range of
+// cand, written by the second detect pass.  up0 = successor (self for a terminal),
+// dist0 = 1 if linked.
 __global__ void __launch_bounds__(256)
 scan_link_kernel(const uint8_t* __restrict__ s, uint64_t nbytes, const uint16_t* __restrict__ slots,
                  const uint64_t* __restrict__ counts, const uint64_t* __restrict__ base,
@@ -199,25 +209,40 @@ scan_link_kernel(const uint8_t* __restrict__ s, uint64_t nbytes, const uint16_t*
                  uint32_t* __restrict__ dist) {
   const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= n_blocks) return;
-  const uint32_t c = (uint32_t)counts[b];
+  const uint64_t cw = counts[b];
+  const uint32_t c = (uint32_t)cw;
   const uint32_t o = (uint32_t)base[b];
   for (uint32_t k = threadIdx.x & 63u; k < c; k += 64) {
-    const uint64_t p = (uint64_t)b * kScanBlockBytes + slots[(size_t)b * kScanSlots + k];
-    cand[o + k] = p;
+    uint64_t p;
+    if (cw >> 32) {
+      p = cand[o + k];
+    } else {
+      p = (uint64_t)b * kScanBlockBytes + slots[(size_t)b * kScanSlots + k];
+      cand[o + k] = p;
+    }
     const uint64_t nx = p + be16_at(s, p);
     uint32_t tgt = kNone;
     if (nx + 2 <= nbytes) {
       const uint64_t bl = nx / kScanBlockBytes;
       if (bl < n_blocks) {
-        const uint16_t* ts = slots + (size_t)bl * kScanSlots;
-        const uint32_t key = (uint32_t)(nx % kScanBlockBytes);
-        const uint32_t cb = (uint32_t)counts[bl];
+        const uint64_t cbw = counts[bl];
+        const uint32_t cb = (uint32_t)cbw, ob = (uint32_t)base[bl];
         uint32_t lo = 0, hi = cb;
-        while (lo < hi) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (ts[mid] < key) lo = mid + 1; else hi = mid;
+        if (cbw >> 32) {
+          while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (cand[ob + mid] < nx) lo = mid + 1; else hi = mid;
+          }
+          if (lo < cb && cand[ob + lo] == nx) tgt = ob + lo;
+        } else {
+          const uint16_t* ts = slots + (size_t)bl * kScanSlots;
+          const uint32_t key = (uint32_t)(nx % kScanBlockBytes);
+          while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (ts[mid] < key) lo = mid + 1; else hi = mid;
+          }
+          if (lo < cb && ts[lo] == key) tgt = ob + lo;
         }
-        if (lo < cb && ts[lo] == key) tgt = (uint32_t)base[bl] + lo;
       }
     }
     up[o + k] = tgt == kNone ? o + k : tgt;
@@ -251,14 +276,15 @@ scan_offsets_kernel(const uint64_t* __restrict__ counts, uint32_t m, uint64_t* _
     const uint32_t i = wv * seg + r * 64 + lane;
     const uint64_t c = (r < rows && i < m) ? counts[i] : 0ull;
     sum += (uint32_t)c;
-    ovf |= (uint32_t)(c >> 32);
+    ovf += (uint32_t)(c >> 32);
   }
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) sum += __shfl_xor(sum, d);
-  const uint64_t any = __ballot(ovf != 0);
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) ovf += __shfl_xor(ovf, d);
   if (lane == 0) {
     wsum[wv] = sum;
-    wovf[wv] = any ? 1u : 0u;
+    wovf[wv] = ovf;
   }
   __syncthreads();
   uint32_t carry = 0, total = 0, novf = 0;
@@ -489,7 +515,7 @@ struct mgenx_scan_ws {
   const uint8_t* key_s = nullptr;
   uint64_t key_n = 0;
   int key_mode = -1;
-  uint32_t n = 0;      // candidates (0 when a block overflowed: resolver only)
+  uint32_t n = 0;      // candidates (0: resolver only -- none, or a pathologically dense stream)
   int levels = 0;      // lifting levels: ups / dists hold levels + 1 tables of n
   uint64_t* cand = nullptr;
   uint32_t* ups = nullptr;
@@ -558,8 +584,8 @@ int scan_build(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, int mode, h
   uint64_t* d_counts = reinterpret_cast<uint64_t*>(static_cast<char*>(ws.slots.mem) + slot_b);
   uint64_t* d_base = d_counts + cnt_b / 8;
   void* d_cub = static_cast<char*>(ws.slots.mem) + slot_b + 2 * cnt_b;
-  hipLaunchKernelGGL(scan_detect_kernel, dim3(nb), dim3(kScanThreads), 0, stream, s, nbytes, m,
-                     d_slots, d_counts);
+  hipLaunchKernelGGL(scan_detect_kernel<false>, dim3(nb), dim3(kScanThreads), 0, stream, s,
+                     nbytes, m, d_slots, d_counts, (const uint64_t*)nullptr, (uint64_t*)nullptr);
   if (nb + 1 <= kScanSmall) {
     hipLaunchKernelGGL(scan_offsets_kernel, dim3(1), dim3(1024), 0, stream, d_counts, nb + 1,
                        d_base, ws.host_dev);
@@ -577,7 +603,10 @@ int scan_build(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, int mode, h
   ws.key_s = s;
   ws.key_n = nbytes;
   ws.key_mode = mode;
-  if (h_tot.overflowed || h_tot.total == 0) return MGENX_OK;  // resolver only
+  // candidate budget: a stream denser than one plausible start per 16 bytes is left to
+  // the sequential resolver (no valid MGEN stream comes near it: records are >= 28 B)
+  const uint64_t max_cand = nbytes / 16 + 65536;
+  if (h_tot.total == 0 || h_tot.total > max_cand) return MGENX_OK;  // resolver only
   const uint32_t n = h_tot.total;
   int levels = 1;
   while ((1ull << (2 * levels)) < n) levels++;  // 4^levels >= n > any chain length
@@ -589,6 +618,9 @@ int scan_build(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, int mode, h
   ws.cand = static_cast<uint64_t*>(ws.cands.mem);
   ws.ups = static_cast<uint32_t*>(ws.tabs.mem);        // [levels + 1][n]
   ws.dists = ws.ups + (size_t)(levels + 1) * n;         // [levels + 1][n]
+  if (h_tot.overflowed)  // blocks with more candidates than slots: second pass, exact sizes
+    hipLaunchKernelGGL(scan_detect_kernel<true>, dim3(nb), dim3(kScanThreads), 0, stream, s,
+                       nbytes, m, d_slots, d_counts, (const uint64_t*)d_base, ws.cand);
   hipLaunchKernelGGL(scan_link_kernel, dim3((nb + 3) / 4), dim3(256), 0, stream, s, nbytes,
                      d_slots, d_counts, d_base, nb, ws.cand, ws.ups, ws.dists);
   const dim3 g((n + 255) / 256);

@@ -105,11 +105,28 @@ def test_random_bytes(torch, eng, mode):
 
 @pytest.mark.parametrize("mode", [0, 1])
 def test_candidate_overflow_path(torch, eng, mode):
-    """A stream of 0x02 bytes makes every position plausible (slot overflow): the scan
-    falls back to the sequential resolver and still matches."""
+    """A stream of 0x02 bytes makes every position plausible (beyond the candidate budget of
+    one per 16 bytes): the scan falls back to the sequential resolver and still matches."""
     s = np.full(200_000, 2, np.uint8)
     info = check(torch, eng, s, mode)
     assert info.candidates == 0
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_block_slot_overflow_second_pass(torch, eng, gold, mode):
+    """A 64 KiB run of 0x02 bytes inside a valid stream: that block has more candidates than
+    its slots (second detect pass writes them with exact offsets), the stream stays within
+    the candidate budget, and the framing still equals the oracle's."""
+    rng = np.random.default_rng(SEED + 70 + mode)
+    if mode == 0:
+        a = tcp_stream(gold, rng.integers(76, 5000, 400), rng)
+        b = tcp_stream(gold, rng.integers(76, 5000, 400), rng)
+    else:
+        a = sink_stream(gold, rng.integers(28, 8193, 250), rng)
+        b = sink_stream(gold, rng.integers(28, 8193, 250), rng)
+    s = np.concatenate([a, np.full(70_000, 2, np.uint8), b])
+    info = check(torch, eng, s, mode)
+    assert info.candidates > 65536
 
 
 def test_config5_stream_scan_then_unpack(torch, eng, gold):
