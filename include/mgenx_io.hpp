@@ -16,6 +16,7 @@
 #include <arpa/inet.h>
 #include <errno.h>
 #include <netinet/in.h>
+#include <poll.h>
 #include <sys/socket.h>
 #include <sys/time.h>
 #include <time.h>
@@ -59,7 +60,7 @@ class UdpTransport {
 
   // sendmmsg datagram i = base[i * slot .. + lens[i]) to dst; zero-length entries (Pack
   // returned 0: MSG_SEND_FAILED) are skipped, as the reference does not send them.
-  // Returns the number of datagrams sent (all, unless the socket errors out).
+  // Returns the number of datagrams the kernel accepted.
   uint32_t Send(const sockaddr_in& dst, const uint8_t* base, uint32_t slot, const uint32_t* lens,
                 uint32_t n) {
     std::vector<mmsghdr> m;
@@ -79,16 +80,24 @@ class UdpTransport {
       h.msg_hdr.msg_iovlen = 1;
       m.push_back(h);
     }
-    size_t done = 0;
+    // A full socket buffer waits for POLLOUT (bounded); a datagram the kernel refuses
+    // (e.g. EMSGSIZE) is skipped rather than dropping the rest of the batch.
+    size_t done = 0, sent = 0;
     while (done < m.size()) {
       const int r = ::sendmmsg(fd_, m.data() + done, (unsigned)(m.size() - done), 0);
       if (r < 0) {
-        if (errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR) continue;
-        break;
+        if (errno == EINTR) continue;
+        if (errno == EAGAIN || errno == EWOULDBLOCK) {
+          pollfd p = {fd_, POLLOUT, 0};
+          if (::poll(&p, 1, 1000) > 0) continue;
+        }
+        done += 1;  // hard error (or no progress for 1 s): skip this datagram
+        continue;
       }
       done += (size_t)r;
+      sent += (size_t)r;
     }
-    return (uint32_t)done;
+    return (uint32_t)sent;
   }
 
   // recvmmsg up to cap datagrams (non-blocking) into base[i * slot], i = 0..; per datagram:

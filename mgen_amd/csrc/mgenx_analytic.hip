@@ -127,6 +127,11 @@ struct WRing {
     for (int o = 32; o >= 1; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
     return v;
   }
+  __device__ static uint32_t wave_max(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
+    return v;
+  }
   __device__ static uint32_t wave_min(uint32_t v) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o));
@@ -345,6 +350,47 @@ flow_update_wave_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
     }
   };
 
+  // Fast segments: a run of records that are all "plain" -- msg != 0, not duplicates (their
+  // bit is clear in the mask and no earlier record of the run has the same seq), within the
+  // mask span without a restart (0 <= seq - first < 1024, so Set takes its d >= 0 branch and
+  // never clears), not below seq_start, and before the window end -- changes the state in
+  // closed form: their bits are OR-ed into the ring, n/last advance, the integer counters
+  // add, and only the FP64 latency sum/min/max is walked record by record (in order:
+  // bit-exact).  Late (reordered) arrivals qualify.  Anything else -- duplicates, mask
+  // restarts, window ends, seq below seq_start, msg == 0 -- takes the general update above.
+  __shared__ uint32_t scat[4][32];
+  const uint32_t wv = threadIdx.x >> 6;
+  auto fast_segment = [&](const FRec& r, uint32_t k, uint32_t e, uint32_t llo, uint32_t lhi) {
+    const bool in = lane >= k && lane < e;
+    if (lane < 32u) scat[wv][lane] = 0u;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (in) atomicOr(&scat[wv][(r.seq >> 5) & 31u], 1u << (r.seq & 31u));
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (lane < 32u) m.w |= scat[wv][lane];
+    __builtin_amdgcn_wave_barrier();
+    m.n += e - k;
+    const uint32_t dmax = (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)WRing::wave_max(in ? r.seq - m.first : 0u));
+    m.last = m.first + max(dmax, m.last - m.first);
+    // counters: byte_count restarts at the first record when msg_count == 1 (:128-129)
+    const uint32_t bsum = (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)WRing::wave_sum(in ? r.len : 0u));
+    byte_count = (msg_count == 1 ? 0ull : byte_count) + bsum;
+    msg_count += e - k;
+    for (uint32_t j = k; j < e; j++) {
+      const uint64_t lb = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)lhi, (int)j) << 32 |
+                          (uint32_t)__builtin_amdgcn_readlane((int)llo, (int)j);
+      const double latency = __builtin_bit_cast(double, lb);
+      lsum = __dadd_rn(lsum, latency);
+      const bool l0 = latency < lmin;
+      const bool h0 = !l0 && latency > lmax;
+      lmin = l0 ? latency : lmin;
+      lmax = h0 ? latency : lmax;
+    }
+  };
+
   // 64 records per round: lane k loads record order[i0 + k]; the next round's loads are
   // issued before this round is walked
   auto ld = [&](uint32_t base, FRec& r) {
@@ -358,7 +404,31 @@ flow_update_wave_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
     ld(i0 + 64u < e ? i0 + 64u : i0, nxt);
     const uint64_t lbits = __builtin_bit_cast(uint64_t, cur.latency);
     const uint32_t llo = (uint32_t)lbits, lhi = (uint32_t)(lbits >> 32);
-    for (uint32_t k = 0; k < cnt; k++) {
+    // the latest earlier record of this round with the same seq (duplicates inside a run)
+    int32_t prev_eq = -1;
+    for (uint32_t i = 0; i + 1 < cnt; i++) {
+      const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)cur.seq, (int)i);
+      prev_eq = (lane > i && cur.seq == x) ? (int32_t)i : prev_eq;
+    }
+    const bool plain = lane < cnt && cur.len != 0;
+    uint32_t k = 0;
+    while (k < cnt) {
+      uint32_t run = 0;
+      if (valid && msg_count >= 1 && m.n) {
+        const uint32_t word = (uint32_t)__shfl((int)m.w, (int)((cur.seq >> 5) & 31u));
+        const bool in_mask = (word >> (cur.seq & 31u)) & 1u;
+        const bool ok = plain && lane >= k && cur.seq - m.first < kDepth && !in_mask &&
+                        prev_eq < (int32_t)k && (int32_t)(cur.seq - seq_start) >= 0 &&
+                        !tge(Tm{(int64_t)cur.rxs, (int64_t)cur.rxu}, we);
+        const uint64_t okm = __ballot(ok) >> k;
+        run = okm == ~0ull >> k ? 64u - k : (uint32_t)__builtin_ctzll(~okm);
+        run = min(run, cnt - k);
+      }
+      if (run) {
+        fast_segment(cur, k, k + run, llo, lhi);
+        k += run;
+        if (k >= cnt) break;
+      }
       const uint64_t lb = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)lhi, (int)k) << 32 |
                           (uint32_t)__builtin_amdgcn_readlane((int)llo, (int)k);
       update((uint32_t)__builtin_amdgcn_readlane((int)cur.seq, (int)k),
@@ -366,6 +436,7 @@ flow_update_wave_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
              (uint32_t)__builtin_amdgcn_readlane((int)cur.rxu, (int)k),
              (uint32_t)__builtin_amdgcn_readlane((int)cur.len, (int)k),
              __builtin_bit_cast(double, lb));
+      k++;
     }
     cur = nxt;
     i0 += 64u;

@@ -30,7 +30,7 @@ struct FlowKey {  // 48 bytes: the reference key's fields, zero-padded
   uint32_t w[12];
 };
 
-struct FlowSlot {  // 64 bytes
+struct __attribute__((aligned(64))) FlowSlot {  // 64 bytes: one slot never spans two lines
   FlowKey key;
   uint32_t state;      // 0 empty, kSlotBusy being written, else 1 + slot tag
   uint32_t index;      // dense flow index (kSlotBusy until numbered)
@@ -103,6 +103,26 @@ __global__ void flowtab_insert_kernel(FlowSlot* __restrict__ tab, uint32_t cap_m
   }
   const FlowKey k = make_key(c, src, i);
   uint32_t s = key_hash(k) & cap_mask;
+  // 0. read-only probe with plain loads: the common case, a key published by an earlier call
+  //    (is_new clear).  A slot is 64 B inside one cache line and its key is written before
+  //    its state is released, so a stale view of the line is at worst "not there yet" -- the
+  //    atomic path below then decides.  (Acquire loads here would invalidate the caches on
+  //    every probe.)
+  for (uint32_t probe = 0, s0 = s; probe <= cap_mask; probe++, s0 = (s0 + 1) & cap_mask) {
+    const u32x4_t* q = reinterpret_cast<const u32x4_t*>(tab + s0);
+    const u32x4_t q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+    if (q3.x == kSlotEmpty || q3.x == kSlotBusy) break;
+    const bool eq = k.w[0] == q0.x && k.w[1] == q0.y && k.w[2] == q0.z && k.w[3] == q0.w &&
+                    k.w[4] == q1.x && k.w[5] == q1.y && k.w[6] == q1.z && k.w[7] == q1.w &&
+                    k.w[8] == q2.x && k.w[9] == q2.y && k.w[10] == q2.z && k.w[11] == q2.w;
+    if (eq) {
+      if (q3.w == 0u) {  // not new in this call: nothing to record
+        rec_slot[i] = s0;
+        return;
+      }
+      break;
+    }
+  }
   for (uint32_t probe = 0; probe <= cap_mask; probe++, s = (s + 1) & cap_mask) {
     FlowSlot& sl = tab[s];
     uint32_t st = __hip_atomic_load(&sl.state, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);

@@ -179,6 +179,12 @@ __device__ void put_deg(S& s, uint32_t raw) {
   put_u64(s, q % 1000000u, 6);
 }
 
+// A record past the end of the slab (MGENX_ERROR_OOB) is not an MgenMsg::Error: it is
+// logged as ERROR_LENGTH, as include/mgenx.hpp maps it
+__device__ __forceinline__ uint32_t log_error(uint32_t e) {
+  return e == MGENX_ERROR_OOB ? (uint32_t)MGENX_ERROR_LENGTH : e;
+}
+
 template <typename S>
 __device__ void format_line(S& s, const LogRec& r, const uint8_t* rec, const mgenx_addr& src,
                             uint32_t rx_sec, uint32_t rx_usec, int protocol, int ttl,
@@ -187,13 +193,13 @@ __device__ void format_line(S& s, const LogRec& r, const uint8_t* rec, const mge
   if (r.err) {  // LogRecvError (mgenMsg.cpp:713-734)
     put_ts(s, rx_sec, rx_usec, epoch);
     put_str(s, "RERR type>");
-    switch (r.err) {
+    switch (log_error(r.err)) {
       case 0: put_str(s, "none"); break;
       case 1: put_str(s, "version"); break;
       case 2: put_str(s, "checksum"); break;
       case 3: put_str(s, "length"); break;
       case 4: put_str(s, "dstAddr"); break;
-      default: break;  // errorString's initial "" (MGENX_ERROR_OOB)
+      default: break;
     }
     put_str(s, " src>");
     put_addr(s, src.type, src.len, src.addr);
@@ -297,7 +303,7 @@ __device__ void format_binary(S& s, const LogRec& r, const uint8_t* rec, uint64_
     s.put(av ? src.type : 0);
     s.put((uint8_t)alen);
     for (uint32_t k = 0; k < alen && k < 16; k++) s.put(src.addr[k]);
-    put_be(s, r.err, 4);  // htonl(msg_error)
+    put_be(s, log_error(r.err), 4);  // htonl(msg_error)
     return;
   }
   const uint32_t rl = (12u + alen + r.hdr + r.plen) & 0xFFFFu;
@@ -311,8 +317,11 @@ __device__ void format_binary(S& s, const LogRec& r, const uint8_t* rec, uint64_
   s.put((uint8_t)alen);
   for (uint32_t k = 0; k < alen && k < 16; k++) s.put(src.addr[k]);
   const uint32_t ml = (rl - (14u + alen) + 4u) & 0xFFFFu;
+  // hdr + payload_len + 2 bytes: past the message's own msg_len (no checksum, no padding)
+  // the reference writes stale bytes of its receive buffer; here they are zero, so a record
+  // never depends on its neighbour in the slab
   for (uint32_t k = 0; k < ml; k++) {
-    uint8_t b = k < avail ? rec[k] : (uint8_t)0;
+    uint8_t b = (k < avail && k < r.msg_len) ? rec[k] : (uint8_t)0;
     if (k == 3) {
       b &= (uint8_t)~MGENX_FLAG_CHECKSUM;
       if (r.flags & MGENX_FLAG_CHECKSUM_ERROR) b |= MGENX_FLAG_CHECKSUM_ERROR;

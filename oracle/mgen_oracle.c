@@ -1065,8 +1065,8 @@ uint32_t or_log_recv_text(const or_fields* f, const uint8_t* rec, const or_addr*
 /* payload_len, BE rx sec/usec, BE src port, src type/len/address,     */
 /* then recordLength - index + 4 = hdr + payload_len + 2 bytes of the  */
 /* message with CHECKSUM cleared in the flags byte (CHECKSUM_ERROR set */
-/* when flagged).  Bytes past avail (the reference's stale receive     */
-/* buffer) read as zero here: unpinned.                                */
+/* when flagged).  Bytes past avail or past the message's own msg_len */
+/* (the reference's stale receive buffer) read as zero here: unpinned. */
 /* ------------------------------------------------------------------ */
 static uint32_t put_be16(uint8_t* p, uint32_t v) { p[0] = (uint8_t)(v >> 8); p[1] = (uint8_t)v; return 2; }
 static uint32_t put_be32(uint8_t* p, uint32_t v) { put32(p, v); return 4; }
@@ -1104,7 +1104,7 @@ uint32_t or_log_recv_binary(const or_fields* f, const uint8_t* rec, uint64_t ava
     const uint32_t index = 14 + alen;
     const uint32_t ml = (rl - index + 4) & 0xFFFF;
     for (uint32_t i = 0; i < ml; i++) {
-        uint8_t b = i < avail ? rec[i] : 0;
+        uint8_t b = (i < avail && i < f->msg_len) ? rec[i] : 0;
         if (i == 3) {
             b &= (uint8_t)~OR_FLAG_CHECKSUM;
             if (f->flags & OR_FLAG_CHECKSUM_ERROR) b |= OR_FLAG_CHECKSUM_ERROR;

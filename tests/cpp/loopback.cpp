@@ -74,7 +74,7 @@ int main(int argc, char** argv) {
     flow = sb->AddFlow(1, mgenx::IPv4, dst_ip, dport);  // flow 1, GPS 999/999/-999 INVALID
   }
   std::vector<uint8_t> txbuf((size_t)64 * size);
-  uint32_t sent = 0, got = 0;
+  uint32_t sent = 0, got = 0, accepted = 0;  // accepted: datagrams the socket took
   const double t0 = now_s();
   while ((sent < count || got < count) && now_s() - t0 < count / rate + 5.0) {
     // PERIODIC: message k is due at t0 + k / rate
@@ -91,7 +91,7 @@ int main(int argc, char** argv) {
         sb->Clear();
         for (uint32_t j = 0; j < k; j++) sb->Add(flow, sent + j, tv, (uint16_t)size);
         const std::vector<uint32_t>& l = sb->Pack(true, false, 0, size);
-        sender.Send(listener.Local(), sb->Datagram(0), size, l.data(), k);
+        accepted += sender.Send(listener.Local(), sb->Datagram(0), size, l.data(), k);
       } else {
         for (uint32_t j = 0; j < k; j++) {
           or_msg m;
@@ -109,7 +109,7 @@ int main(int argc, char** argv) {
           m.altitude = -999;
           plen[j] = or_udp_pack(&m, txbuf.data() + (size_t)j * size, 1, 0, 0);
         }
-        sender.Send(listener.Local(), txbuf.data(), size, plen.data(), k);
+        accepted += sender.Send(listener.Local(), txbuf.data(), size, plen.data(), k);
       }
       for (uint32_t j = 0; j < k; j++) { txs[sent + j] = (uint32_t)tv.tv_sec; txu[sent + j] = (uint32_t)tv.tv_usec; }
       sent += k;
@@ -172,12 +172,13 @@ int main(int argc, char** argv) {
             time_ok(f.seq_num < count ? f.seq_num : 0, f.tx_sec, f.tx_usec));
     }
   }
-  const bool ok = sent == count && got == count && c.bad_seq == 0 && c.bad_err == 0 &&
+  const bool ok = sent == count && accepted == count && got == count && c.bad_seq == 0 && c.bad_err == 0 &&
                   c.bad_field == 0 && c.bad_time == 0;
-  printf("{\"mode\": \"%s\", \"sent\": %u, \"received\": %u, \"lost\": %d, \"out_of_order\": %u, "
+  printf("{\"mode\": \"%s\", \"sent\": %u, \"send_failed\": %d, \"received\": %u, \"lost\": %d, \"out_of_order\": %u, "
          "\"errors\": %u, \"bad_fields\": %u, \"bad_times\": %u, \"elapsed_s\": %.3f, "
          "\"rate\": %.1f, \"size\": %u, \"ok\": %s}\n",
-         gpu ? "gpu" : "cpu", sent, got, (int)count - (int)got, c.bad_seq, c.bad_err,
+         gpu ? "gpu" : "cpu", sent, (int)sent - (int)accepted, got, (int)accepted - (int)got,
+         c.bad_seq, c.bad_err,
          c.bad_field, c.bad_time, elapsed, rate, size, ok ? "true" : "false");
   delete sb;
   delete rb;

@@ -101,3 +101,57 @@ def test_flow_export_counters(torch, eng):
     assert np.array_equal(c["msg_count"], st["msg_count"])
     assert np.array_equal(c["latency_sum"], st["latency_sum"])
     assert np.array_equal(c["n_reports"], st["n_reports"])
+
+
+def _jumpy_flows(n_flows, per, seed):
+    """Receive-order records whose per-flow sequence increments stress the fast segments:
+    mostly +1, runs of losses, jumps past the 1024-bit mask span (clear and restart inside a
+    segment), increments near 2^24 and 2^31 (int32 wrap of seq - first), zero-length
+    messages, duplicates and local reordering."""
+    rng = np.random.default_rng(seed)
+    cols = {k: [] for k in ("flow_id", "seq", "tx_sec", "tx_usec", "rx_sec", "rx_usec",
+                            "msg_len")}
+    t0 = 1_700_000_000 * 10**6
+    for f in range(n_flows):
+        inc = np.ones(per, np.uint64)
+        u = rng.random(per)
+        inc[u < 0.05] = rng.integers(2, 12, int((u < 0.05).sum()))
+        inc[u < 0.01] = rng.integers(1024, 3000, int((u < 0.01).sum()))
+        inc[u < 0.002] = (1 << 24) + rng.integers(-3, 3, int((u < 0.002).sum()))
+        inc[u < 0.0005] = (1 << 31) + 7
+        seq = (np.cumsum(inc) + np.uint64(rng.integers(0, 1 << 32))) & np.uint64(0xFFFFFFFF)
+        tx = t0 + np.cumsum(rng.exponential(700, per)).astype(np.int64)
+        rx = tx + rng.integers(50, 500, per)
+        ln = np.full(per, 200, np.uint16)
+        ln[rng.random(per) < 0.003] = 0
+        dup = rng.random(per) < 0.004
+        seq = np.concatenate([seq, seq[dup]])
+        tx = np.concatenate([tx, tx[dup]])
+        rx = np.concatenate([rx, rx[dup] + 3])
+        ln = np.concatenate([ln, ln[dup]])
+        o = np.argsort(rx + rng.uniform(-900, 900, rx.size), kind="stable")
+        for k, v in (("seq", seq[o]), ("tx_sec", tx[o] // 10**6), ("tx_usec", tx[o] % 10**6),
+                     ("rx_sec", rx[o] // 10**6), ("rx_usec", rx[o] % 10**6),
+                     ("msg_len", ln[o])):
+            cols[k].append(v)
+        cols["flow_id"].append(np.full(o.size, f + 1))
+    rx_all = np.concatenate([np.asarray(a, np.int64) * 10**6 + b
+                             for a, b in zip(cols["rx_sec"], cols["rx_usec"])])
+    order = np.argsort(rx_all, kind="stable")
+    dt = {"flow_id": np.uint32, "seq": np.uint32, "tx_sec": np.uint32, "tx_usec": np.uint32,
+          "rx_sec": np.uint32, "rx_usec": np.uint32, "msg_len": np.uint16}
+    return {k: np.concatenate(v).astype(dt[k])[order] for k, v in cols.items()}
+
+
+@pytest.mark.parametrize("window", [0.02, 0.5, 30.0])
+def test_flow_reduce_fast_segments_edge_cases(torch, eng, window):
+    """The closed-form runs of plain records (fast segments) against the oracle's
+    record-by-record Update, on sequences built to hit every boundary of the fast path."""
+    from oracle import oracle as O
+    n_flows, per_flow = 40, 64
+    d = _jumpy_flows(n_flows, 6000, seed=int(window * 1000) + 3)
+    st, rep, cnt, _ = run_gpu(torch, eng, d, n_flows, window, per_flow, splits=(0, 5000))
+    of, orep, ocnt = O.flow_reduce_batch(n_flows, d["flow_id"] - 1, d["seq"], d["tx_sec"],
+                                         d["tx_usec"], d["msg_len"], d["rx_sec"],
+                                         d["rx_usec"], window=window, per_flow=per_flow)
+    compare(st, rep, cnt, of, orep, ocnt, per_flow)

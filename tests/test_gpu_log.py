@@ -160,3 +160,66 @@ def test_binary_log_matches_oracle(torch, eng, gold, oracle, mode):
     got = out.cpu().numpy().tobytes()
     assert len(got) == len(want)
     assert got == want
+
+
+def test_binary_log_message_bound_and_oob(torch, eng, oracle):
+    """Records whose msg_len is exactly header + payload (no checksum, no padding) in 256-B
+    slots with non-zero bytes after them: the 2 bytes the binary RECV record copies past the
+    message read as zero (never the neighbour's bytes); a record outside the slab is logged
+    as RERR with ERROR_LENGTH (3) in both forms, as include/mgenx.hpp maps MGENX_ERROR_OOB."""
+    from mgen_amd import ERROR_OOB, to_device
+    from mgen_amd._abi import DESC_DTYPE
+    from mgen_amd.workloads import make_templates
+    n, slot = 64, 256
+    tmpl, pool = make_templates(4, payload=b"\x11\x22\x33\x44\x55")
+    d = np.zeros(n, DESC_DTYPE)
+    d["tmpl"] = np.arange(n) % 4
+    d["seq_num"] = np.arange(n)
+    d["tx_sec"] = 1_700_000_000
+    d["msg_len"] = 200
+    dt, dp = to_device(tmpl), to_device(pool)
+    crc = torch.empty(4, dtype=torch.int32, device="cuda")
+    eng.pack_prepare(dt, 4, dp, crc)
+    slab = torch.full((n * slot,), 0xAB, dtype=torch.uint8, device="cuda")
+    out_len = torch.empty(n, dtype=torch.int32, device="cuda")
+    # first pass: header + payload sizes; then msg_len = exactly that (no padding)
+    eng.pack(dt, crc, to_device(d), n, dp, slab, stride=slot, opts=0, out_len=out_len)
+    c0 = eng.unpack(slab, n, stride=slot, fixed_len=200, ext=True)
+    d["msg_len"] = (c0["hdr_len"].cpu().numpy().astype(np.int64) +
+                    c0["payload_len"].cpu().numpy().view(np.uint16))
+    slab.fill_(0xAB)
+    eng.pack(dt, crc, to_device(d), n, dp, slab, stride=slot, opts=0, out_len=out_len)
+    lens_h = out_len.cpu().numpy().astype(np.int32)
+    offs_h = np.arange(n, dtype=np.int64) * slot
+    offs_h[-1] = n * slot + 100           # the last record lies outside the slab
+    offs, lens = to_device(offs_h), to_device(lens_h)
+    cols = eng.unpack(slab, n, rec_off=offs, rec_len=lens, ext=True)
+    err = cols["err"].cpu().numpy()
+    assert err[-1] == ERROR_OOB and (err[:-1] == 0).all()
+    mlen = cols["msg_len"].cpu().numpy().view(np.uint16).astype(np.int64)
+    hdr = cols["hdr_len"].cpu().numpy().astype(np.int64)
+    plen = cols["payload_len"].cpu().numpy().view(np.uint16).astype(np.int64)
+    assert (mlen[:-1] == hdr[:-1] + plen[:-1]).all()
+    src = np.zeros(n, oracle.ADDR_DTYPE)
+    src["type"], src["len"], src["port"] = 1, 4, 4000
+    src["addr"][:, :4] = [10, 0, 0, 7]
+    rx_s = np.full(n, 1_700_000_002, np.uint32)
+    rx_u = np.arange(n, dtype=np.uint32)
+    out, pos = eng.log_recv_binary(slab, n, cols, to_device(src.view(np.uint8)), to_device(rx_s),
+                                   to_device(rx_u), rec_off=offs, protocol=1)
+    got = out.cpu().numpy().tobytes()
+    pos = pos.cpu().numpy().view(np.uint64)
+    h = slab.cpu().numpy()
+    f = oracle.udp_recv_batch(h, n - 1, rec_off=offs_h[:-1].astype(np.uint64),
+                              rec_len=lens_h[:-1].astype(np.uint32))
+    want = oracle.log_recv_binary(f, h, offs_h[:-1], src[:-1], rx_s[:-1], rx_u[:-1], protocol=1)
+    assert got[:int(pos[n - 1])] == want
+    # every RECV record ends with the 2 zero bytes past its message
+    for i in range(n - 1):
+        rec = got[int(pos[i]):int(pos[i + 1])]
+        assert rec[0] == 1 and rec[-2:] == b"\0\0", i
+    last = got[int(pos[n - 1]):int(pos[n])]
+    assert last[0] == 2 and last[-4:] == (3).to_bytes(4, "big")
+    text, _ = eng.log_recv_text(slab, n, cols, to_device(src.view(np.uint8)), to_device(rx_s),
+                                to_device(rx_u), rec_off=offs)
+    assert text.cpu().numpy().tobytes().split(b"\n")[n - 1].find(b"RERR type>length ") > 0
