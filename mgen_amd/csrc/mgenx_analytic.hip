@@ -8,9 +8,10 @@
 // The state machine is sequential per flow and independent across flows, so:
 //   1. records are ordered by flow, stably (receive order kept): hipCUB radix sort of
 //      (flow index, record index) -- plumbing, not the hot path;
-//   2. their fields are gathered flow-contiguous (24 B per record);
-//   3. one lane per flow runs Update over its records (prefetched 8 at a time), its
-//      1024-bit mask in LDS, transposed (word k of lane t at k * 64 + t: conflict-free).
+//   2. their fields (24 B per record, latency precomputed) are read through the sorted
+//      order, three rounds of 64 in flight;
+//   3. one wave per flow runs Update over its records (see WRing and the fast segments
+//      below).
 // FP64: every product that feeds an add goes through mul_rounded (an empty asm keeps the
 // backend from fusing them into an FMA: neither __dadd_rn/__dmul_rn nor `#pragma clang fp
 // contract(off)` prevented it -- a 1-ulp difference in a report's duration was the
@@ -20,6 +21,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "mgenx_kernels.hpp"
@@ -122,20 +124,26 @@ struct WRing {
     }
     return lane < 32u ? m : 0u;
   }
+  // whole-wave reductions through DPP (quad swaps, half-row and row mirrors, row
+  // broadcasts 15 / 31): the result is complete in lane 63 and returned wave-uniform
+  template <typename Op>
+  __device__ static uint32_t wave_reduce(uint32_t v, uint32_t identity, Op op) {
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)identity, (int)v, 0xB1, 0xF, 0xF, false));
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)identity, (int)v, 0x4E, 0xF, 0xF, false));
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)identity, (int)v, 0x141, 0xF, 0xF, false));
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)identity, (int)v, 0x140, 0xF, 0xF, false));
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)identity, (int)v, 0x142, 0xA, 0xF, false));
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)identity, (int)v, 0x143, 0xC, 0xF, false));
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+  }
   __device__ static uint32_t wave_sum(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
-    return v;
+    return wave_reduce(v, 0u, [](uint32_t a, uint32_t b) { return a + b; });
   }
   __device__ static uint32_t wave_max(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
-    return v;
+    return wave_reduce(v, 0u, [](uint32_t a, uint32_t b) { return max(a, b); });
   }
   __device__ static uint32_t wave_min(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o));
-    return v;
+    return wave_reduce(v, 0xFFFFFFFFu, [](uint32_t a, uint32_t b) { return min(a, b); });
   }
   // clear indices first .. first + count - 1, then re-base `first` on the lowest left
   __device__ void unset_from_first(uint32_t count) {
@@ -208,12 +216,14 @@ __device__ __forceinline__ int64_t uni64(int64_t v) {
 }
 __device__ __forceinline__ Tm uni_t(Tm t) { return Tm{uni64(t.sec), uni64(t.usec)}; }
 
+
+
 __global__ void __launch_bounds__(256)
 flow_update_wave_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
                         const uint32_t* __restrict__ begin, const uint32_t* __restrict__ end,
                         const uint32_t* __restrict__ order, const FRec* __restrict__ recs,
                         mgenx_flow_report* __restrict__ reports, uint32_t per_flow,
-                        uint32_t* __restrict__ report_count) {
+                        uint32_t* __restrict__ report_count, int abl) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t f = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
   if (f >= n_flows) return;
@@ -360,77 +370,105 @@ flow_update_wave_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
   // restarts, window ends, seq below seq_start, msg == 0 -- takes the general update above.
   __shared__ uint32_t scat[4][32];
   const uint32_t wv = threadIdx.x >> 6;
-  auto fast_segment = [&](const FRec& r, uint32_t k, uint32_t e, uint32_t llo, uint32_t lhi) {
-    const bool in = lane >= k && lane < e;
+  // trial: the run's bits into a zeroed LDS copy of the ring; true when two records of the
+  // run share a seq (a duplicate inside the run -- then the run is recomputed exactly)
+  auto scatter = [&](const FRec& r, uint32_t k, uint32_t e) -> bool {
     if (lane < 32u) scat[wv][lane] = 0u;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    if (in) atomicOr(&scat[wv][(r.seq >> 5) & 31u], 1u << (r.seq & 31u));
+    bool clash = false;
+    if (lane >= k && lane < e) {
+      const uint32_t bit = 1u << (r.seq & 31u);
+      clash = (atomicOr(&scat[wv][(r.seq >> 5) & 31u], bit) & bit) != 0u;
+    }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
+    return __ballot(clash) != 0ull;
+  };
+  auto commit = [&](const FRec& r, uint32_t k, uint32_t e, uint32_t llo, uint32_t lhi) {
+    const bool in = lane >= k && lane < e;
     if (lane < 32u) m.w |= scat[wv][lane];
     __builtin_amdgcn_wave_barrier();
     m.n += e - k;
-    const uint32_t dmax = (uint32_t)__builtin_amdgcn_readfirstlane(
-        (int)WRing::wave_max(in ? r.seq - m.first : 0u));
+    const uint32_t dmax = WRing::wave_max(in ? r.seq - m.first : 0u);
     m.last = m.first + max(dmax, m.last - m.first);
     // counters: byte_count restarts at the first record when msg_count == 1 (:128-129)
-    const uint32_t bsum = (uint32_t)__builtin_amdgcn_readfirstlane(
-        (int)WRing::wave_sum(in ? r.len : 0u));
+    const uint32_t bsum = WRing::wave_sum(in ? r.len : 0u);
     byte_count = (msg_count == 1 ? 0ull : byte_count) + bsum;
     msg_count += e - k;
-    for (uint32_t j = k; j < e; j++) {
+    // the sum in record order (bit-exact); min / max as fmin / fmax: the reference's
+    // "if (l < min) min = l; else if (l > max) max = l" is exactly that for latencies
+    // (never NaN, never -0: ProtoTime::Delta of integer fields) with min <= max.
+    // (Measured alternatives, slower: min / max by DPP wave reductions, the loop unrolled
+    // over constant lanes, compare-selects -- the loop is bound by the sum's chain.)
+    double vs = lsum, vmin = lmin, vmax = lmax;
+    const uint32_t ee = (MGENX_DIAG && (abl & 1)) ? k : e;
+    for (uint32_t j = k; j < ee; j++) {
       const uint64_t lb = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)lhi, (int)j) << 32 |
                           (uint32_t)__builtin_amdgcn_readlane((int)llo, (int)j);
       const double latency = __builtin_bit_cast(double, lb);
-      lsum = __dadd_rn(lsum, latency);
-      const bool l0 = latency < lmin;
-      const bool h0 = !l0 && latency > lmax;
-      lmin = l0 ? latency : lmin;
-      lmax = h0 ? latency : lmax;
+      vs = __dadd_rn(vs, latency);
+      vmin = __builtin_fmin(vmin, latency);
+      vmax = __builtin_fmax(vmax, latency);
     }
+    lsum = vs;
+    lmin = vmin;
+    lmax = vmax;
   };
 
-  // 64 records per round: lane k loads record order[i0 + k]; the next round's loads are
-  // issued before this round is walked
-  auto ld = [&](uint32_t base, FRec& r) {
-    r = recs[order[min(base + lane, e - 1u)]];
-  };
-  FRec cur, nxt;
+  // 64 records per round: lane k holds record order[i0 + k]; the record loads of the next
+  // two rounds and the index loads of the one after are in flight while this one is walked
+  auto ldo = [&](uint32_t base) { return order[min(base + lane, e - 1u)]; };
   uint32_t i0 = b;
-  ld(i0, cur);
+  const uint32_t oa = ldo(i0), ob = ldo(i0 + 64u);
+  uint32_t oc = ldo(i0 + 128u);
+  FRec cur = recs[oa], nx1 = recs[ob], nx2;
   while (i0 < e) {
+    nx2 = recs[oc];
+    oc = ldo(i0 + 192u);
     const uint32_t cnt = min(64u, e - i0);
-    ld(i0 + 64u < e ? i0 + 64u : i0, nxt);
     const uint64_t lbits = __builtin_bit_cast(uint64_t, cur.latency);
     const uint32_t llo = (uint32_t)lbits, lhi = (uint32_t)(lbits >> 32);
-    // the latest earlier record of this round with the same seq (duplicates inside a run)
+    // the latest earlier record of this round with the same seq: computed only when a run
+    // turns out to hold a duplicate
     int32_t prev_eq = -1;
-    for (uint32_t i = 0; i + 1 < cnt; i++) {
-      const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)cur.seq, (int)i);
-      prev_eq = (lane > i && cur.seq == x) ? (int32_t)i : prev_eq;
-    }
+    bool have_prev_eq = false;
     const bool plain = lane < cnt && cur.len != 0;
     uint32_t k = 0;
     while (k < cnt) {
       uint32_t run = 0;
-      if (valid && msg_count >= 1 && m.n) {
+      if (valid && msg_count >= 1 && m.n && !(MGENX_DIAG && (abl & 4))) {
         const uint32_t word = (uint32_t)__shfl((int)m.w, (int)((cur.seq >> 5) & 31u));
         const bool in_mask = (word >> (cur.seq & 31u)) & 1u;
-        const bool ok = plain && lane >= k && cur.seq - m.first < kDepth && !in_mask &&
-                        prev_eq < (int32_t)k && (int32_t)(cur.seq - seq_start) >= 0 &&
-                        !tge(Tm{(int64_t)cur.rxs, (int64_t)cur.rxu}, we);
-        const uint64_t okm = __ballot(ok) >> k;
-        run = okm == ~0ull >> k ? 64u - k : (uint32_t)__builtin_ctzll(~okm);
-        run = min(run, cnt - k);
+        const bool ok0 = plain && lane >= k && cur.seq - m.first < kDepth && !in_mask &&
+                         (int32_t)(cur.seq - seq_start) >= 0 &&
+                         !tge(Tm{(int64_t)cur.rxs, (int64_t)cur.rxu}, we);
+        auto run_of = [&](bool ok) {
+          const uint64_t okm = __ballot(ok) >> k;
+          const uint32_t r0 = okm == ~0ull >> k ? 64u - k : (uint32_t)__builtin_ctzll(~okm);
+          return min(r0, cnt - k);
+        };
+        run = run_of(ok0 && (!have_prev_eq || prev_eq < (int32_t)k));
+        if (run && scatter(cur, k, k + run)) {
+          if (!have_prev_eq) {
+            for (uint32_t i = 0; i + 1 < cnt; i++) {
+              const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)cur.seq, (int)i);
+              prev_eq = (lane > i && cur.seq == x) ? (int32_t)i : prev_eq;
+            }
+            have_prev_eq = true;
+          }
+          run = run_of(ok0 && prev_eq < (int32_t)k);
+          if (run) (void)scatter(cur, k, k + run);
+        }
       }
       if (run) {
-        fast_segment(cur, k, k + run, llo, lhi);
+        if (!(MGENX_DIAG && (abl & 8))) commit(cur, k, k + run, llo, lhi);
         k += run;
         if (k >= cnt) break;
       }
       const uint64_t lb = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)lhi, (int)k) << 32 |
                           (uint32_t)__builtin_amdgcn_readlane((int)llo, (int)k);
+      if (!(MGENX_DIAG && (abl & 2)))
       update((uint32_t)__builtin_amdgcn_readlane((int)cur.seq, (int)k),
              (uint32_t)__builtin_amdgcn_readlane((int)cur.rxs, (int)k),
              (uint32_t)__builtin_amdgcn_readlane((int)cur.rxu, (int)k),
@@ -438,7 +476,8 @@ flow_update_wave_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
              __builtin_bit_cast(double, lb));
       k++;
     }
-    cur = nxt;
+    cur = nx1;
+    nx1 = nx2;
     i0 += 64u;
   }
 
@@ -626,9 +665,13 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
   (void)hipMemsetAsync(d_end, 0, fb, stream);
   hipLaunchKernelGGL(flow_bounds_kernel, g, dim3(256), 0, stream, keys_out, n, n_flows, d_begin,
                      d_end);
+  int abl = 0;  // diagnostics build only: ablations of the update kernel (timing studies)
+#if MGENX_DIAG
+  if (const char* a = getenv("MGENX_AN_ABL")) abl = atoi(a);
+#endif
   hipLaunchKernelGGL(flow_update_wave_kernel, dim3((n_flows + 3) / 4), dim3(256), 0, stream,
                      flows, n_flows, d_begin, d_end, vals_out, recs, reports, per_flow,
-                     report_count);
+                     report_count, abl);
   e = hipGetLastError();
   if (e != hipSuccess) {
     snprintf(err, errn, "flow_reduce: %s", hipGetErrorString(e));

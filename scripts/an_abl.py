@@ -1,0 +1,44 @@
+"""Timing of mgenx_flow_reduce on config 4 data with the diagnostics build's update-kernel
+ablations (MGENX_AN_ABL bits: 1 no latency sum loop, 2 no general update, 4 no fast runs,
+8 no run commit).  Results are wrong under ablation; timing only."""
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+if len(sys.argv) == 1:
+    for a in [int(x) for x in os.environ.get("ABLS", "0,1,2,8,3,4").split(",")]:
+        env = dict(os.environ, MGENX_AN_ABL=str(a))
+        r = subprocess.run([sys.executable, __file__, "run"], env=env, capture_output=True,
+                           text=True, timeout=200)
+        print("abl", a, r.stdout.strip()[-200:], r.stderr.strip()[-300:] if r.returncode else "")
+    sys.exit(0)
+
+import torch  # noqa: E402
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from mgen_amd import Engine  # noqa: E402
+from mgen_amd.workloads import poisson_flows  # noqa: E402
+
+eng = Engine(0, diag=True)
+d = poisson_flows(8388608, 1024, mean_gap_us=1000)
+t = {k: torch.from_numpy(v).cuda() for k, v in d.items()}
+idx = torch.from_numpy((d["flow_id"] - 1).astype(np.uint32)).cuda()
+n = len(d["seq"])
+
+
+def run():
+    flows = eng.flow_init(1024, 1.0)
+    eng.flow_reduce(flows, 1024, idx, t["seq"], t["tx_sec"], t["tx_usec"], t["msg_len"],
+                    t["rx_sec"], t["rx_usec"], n=n)
+
+
+run()
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+for _ in range(5):
+    run()
+torch.cuda.synchronize()
+print("reduce_ms", round((time.perf_counter() - t0) / 5 * 1e3, 4))
