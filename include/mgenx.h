@@ -217,6 +217,22 @@ int mgenx_pack_msgs(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
                     const uint32_t* dev_crc_in, uint32_t* dev_out_len, uint32_t* dev_tx_crc,
                     uint32_t* dev_state, uint32_t opts, uint32_t fill_time, void* stream);
 
+/* TCP transmit: the byte stream MgenTcpTransport sends for n messages (SendMessage with
+ * GetNextTxFragmentSize / GetNextTxFragment / SetupNextTxBuffer / CalcTxChecksum,
+ * src/common/mgenTransport.cpp:1320-1400, 1818-1993), back to back.  dev_msg_total[i] is the
+ * message's mgen_msg_len (fragments of <= 65535 bytes past that, CONTINUES / END_OF_MSG);
+ * the descriptor's msg_len is ignored.  A fragment over 8192 bytes is one 8-KiB Pack whose
+ * buffer is re-sent from its start, the CRC (MGENX_PACK_CHECKSUM) covering every byte
+ * before the trailer.  dev_msg_off[i] = the message's offset in the stream (a message whose
+ * first Pack fails, or of length 0, takes no bytes); *total_bytes = the stream length.
+ * Synchronous (the stream layout decides the launches); when the stream would exceed
+ * stream_cap nothing is written, *total_bytes is set and MGENX_EINVAL returned. */
+int mgenx_pack_tcp(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl, const uint32_t* dev_tmpl_crc,
+                   const mgenx_pack_desc* dev_desc, const uint32_t* dev_msg_total, uint32_t n,
+                   const uint8_t* dev_pool, uint8_t* dev_stream, uint64_t stream_cap,
+                   uint64_t* dev_msg_off, uint64_t* total_bytes, uint32_t opts,
+                   uint32_t fill_time, void* stream);
+
 /* MgenMsg::ComputeCRC32(checksum, buffer, len) (mgenMsg.cpp:524-541) over n byte ranges:
  * dev_state_out[i] = the running CRC after feeding dev_data[off[i] .. off[i]+len[i]) to
  * dev_state_in[i] (0 restarts from CRC32_XINIT; no final xor). */

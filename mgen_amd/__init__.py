@@ -28,7 +28,7 @@ DIAG_LIB_PATH = os.path.join(HERE, "libmgenx_diag.so")   # + include/mgenx_diag.
 EXPORTED_SYMBOLS = (
     "mgenx_abi_version", "mgenx_ctx_create", "mgenx_ctx_destroy", "mgenx_last_error",
     "mgenx_ctx_device", "mgenx_unpack_batch", "mgenx_pack_prepare", "mgenx_set_fill_time",
-    "mgenx_pack_batch", "mgenx_pack_msgs", "mgenx_crc32_update", "mgenx_crc32_batch",
+    "mgenx_pack_batch", "mgenx_pack_msgs", "mgenx_pack_tcp", "mgenx_crc32_update", "mgenx_crc32_batch",
     "mgenx_stream_scan", "mgenx_stream_scan_exits", "mgenx_stream_scan_range", "mgenx_flow_init", "mgenx_flow_reduce", "mgenx_flow_export",
     "mgenx_log_recv_text", "mgenx_log_recv_binary", "mgenx_comm_unique_id", "mgenx_comm_init",
     "mgenx_comm_destroy", "mgenx_allreduce_flows", "mgenx_allgather_u64",
@@ -67,6 +67,8 @@ def load(diag: bool = False):
     L.mgenx_pack_batch.argtypes = [P, P, P, P, u32, P, P, u64, P, u64, P, u32, u32, P]
     L.mgenx_pack_msgs.argtypes = [P, P, P, P, u32, P, P, u64, P, u64, P, P, P, P, P, u32, u32,
                                   P]
+    L.mgenx_pack_tcp.argtypes = [P, P, P, P, P, u32, P, P, u64, P, ctypes.POINTER(u64), u32,
+                                 u32, P]
     L.mgenx_crc32_batch.argtypes = [P, P, P, P, u32, P, P]
     L.mgenx_crc32_update.argtypes = [P, P, P, P, u32, P, P, P]
     L.mgenx_ctx_device.argtypes = [P]
@@ -256,6 +258,29 @@ class Engine:
                                       _ptr(state), opts, fill_time, _stream(self.device))
         self._check(rc, "mgenx_pack_msgs")
         return out_len, tx_crc, state
+
+    def pack_tcp(self, tmpl, tmpl_crc, desc, msg_total, n, pool, *, opts=0, fill_time=0,
+                 cap=None):
+        """The MgenTcpTransport transmit stream of n messages (mgenx_pack_tcp): returns
+        (stream uint8 tensor, message offsets int64 tensor)."""
+        torch = self.torch
+        dev = msg_total.device
+        offs = torch.empty(n, dtype=torch.int64, device=dev)
+        total = ctypes.c_uint64(0)
+        if cap is None:  # size query: a first call with no room reports the length
+            rc = self.lib.mgenx_pack_tcp(self.ctx, _ptr(tmpl), _ptr(tmpl_crc), _ptr(desc),
+                                         _ptr(msg_total), n, _ptr(pool), None, 0, _ptr(offs),
+                                         ctypes.byref(total), opts, fill_time,
+                                         _stream(self.device))
+            if rc not in (0, -1):
+                self._check(rc, "mgenx_pack_tcp")
+            cap = int(total.value)
+        out = torch.zeros(max(cap, 1), dtype=torch.uint8, device=dev)
+        rc = self.lib.mgenx_pack_tcp(self.ctx, _ptr(tmpl), _ptr(tmpl_crc), _ptr(desc),
+                                     _ptr(msg_total), n, _ptr(pool), _ptr(out), cap, _ptr(offs),
+                                     ctypes.byref(total), opts, fill_time, _stream(self.device))
+        self._check(rc, "mgenx_pack_tcp")
+        return out[:int(total.value)], offs
 
     def crc32_update(self, data, off, length, n, state_in, out=None):
         """MgenMsg::ComputeCRC32 running states (mgenx_crc32_update)."""

@@ -4,6 +4,8 @@
 // fill stream); every data buffer belongs to the caller.  No entry point allocates,
 // synchronises or copies from host memory except mgenx_ctx_create and
 // mgenx_pack_prepare (table setup), so batch calls can be captured in a hipGraph.
+#include <hipcub/hipcub.hpp>
+
 #include <stdio.h>
 #include <string.h>
 
@@ -68,6 +70,10 @@ struct mgenx_ctx {
   void* scan_ws = nullptr;        // stream-scan workspace (mgenx_scan.hip), grown on demand
   void* flow_ws = nullptr;        // flow-reduce workspace (mgenx_analytic.hip), grown on demand
   void* log_ws = nullptr;         // log-format workspace (mgenx_log.hip), grown on demand
+  void* tcp_ws = nullptr;         // TCP transmit workspace (mgenx_pack_tcp), grown on demand
+  size_t tcp_ws_bytes = 0;
+  uint64_t* tcp_host = nullptr;   // host-mapped words: total bytes, max fragments
+  uint64_t* tcp_host_dev = nullptr;
   int unpack_variant = 0;          // diagnostic kernel ablation (mgenx_set_tuning)
   int pack_variant = 0;
   bool rand_ready = false;
@@ -203,6 +209,8 @@ int mgenx_ctx_destroy(mgenx_ctx* c) {
   if (c->scan_ws) mgenx_scan_ws_free(c->scan_ws);
   if (c->flow_ws) mgenx_flow_ws_free(c->flow_ws);
   if (c->log_ws) mgenx_log_ws_free(c->log_ws);
+  if (c->tcp_ws) hipFree(c->tcp_ws);
+  if (c->tcp_host) hipHostFree(c->tcp_host);
   for (void* p : ps)
     if (p) hipFree(p);
   delete c;
@@ -339,6 +347,116 @@ int mgenx_pack_msgs(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
   return pack_common(ctx, dev_tmpl, dev_tmpl_crc, dev_desc, n, dev_pool, dev_slab, slab_bytes,
                      dev_rec_off, stride, dev_buf_len, dev_crc_in, dev_out_len, dev_tx_crc,
                      dev_state, opts | MGENX_PACK_RAW, fill_time, stream);
+}
+
+// the maximum fragment count and the stream total into host-mapped memory
+__global__ void tcp_totals_kernel(const uint32_t* nfrag, uint32_t n, const uint64_t* off,
+                                  uint64_t* host) {
+  __shared__ uint32_t mx[256];
+  uint32_t m = 0;
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) m = nfrag[i] > m ? nfrag[i] : m;
+  mx[threadIdx.x] = m;
+  __syncthreads();
+  for (uint32_t s = 128; s; s >>= 1) {
+    if (threadIdx.x < s) mx[threadIdx.x] = max(mx[threadIdx.x], mx[threadIdx.x + s]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    host[0] = off[n];
+    host[1] = mx[0];
+  }
+}
+
+static size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+int mgenx_pack_tcp(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl, const uint32_t* dev_tmpl_crc,
+                   const mgenx_pack_desc* dev_desc, const uint32_t* dev_msg_total, uint32_t n,
+                   const uint8_t* dev_pool, uint8_t* dev_stream, uint64_t stream_cap,
+                   uint64_t* dev_msg_off, uint64_t* total_bytes, uint32_t opts,
+                   uint32_t fill_time, void* stream) {
+  if (!ctx || !total_bytes || (opts & ~(uint32_t)(MGENX_PACK_CHECKSUM | MGENX_PACK_RANDOM_FILL)))
+    return MGENX_EINVAL;
+  *total_bytes = 0;
+  if (n == 0) return MGENX_OK;
+  if (!dev_tmpl || !dev_tmpl_crc || !dev_desc || !dev_msg_total || !dev_msg_off)
+    return MGENX_EINVAL;
+  if ((opts & MGENX_PACK_RANDOM_FILL) && (!ctx->rand_ready || ctx->rand_time != fill_time))
+    return MGENX_EINVAL;
+  hipSetDevice(ctx->device);
+  const hipStream_t s = (hipStream_t)stream;
+  hipError_t e;
+  if (!ctx->tcp_host) {
+    void* hp = nullptr;
+    void* dp = nullptr;
+    if ((e = hipHostMalloc(&hp, 64, hipHostMallocMapped)) != hipSuccess) return set_err(ctx, e, "tcp");
+    ctx->tcp_host = static_cast<uint64_t*>(hp);
+    if ((e = hipHostGetDevicePointer(&dp, hp, 0)) != hipSuccess) return set_err(ctx, e, "tcp");
+    ctx->tcp_host_dev = static_cast<uint64_t*>(dp);
+  }
+  // workspace: bytes[n+1], nfrag[n], cub; per round: fd, foff, fbuf, ff, plen, crc, state x2,
+  // roff[3n], rlen[3n], acrc[3n]
+  size_t cub_bytes = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, cub_bytes, (const uint64_t*)nullptr,
+                                         (uint64_t*)nullptr, (int)(n + 1), s);
+  const size_t b8 = a256((size_t)(n + 1) * 8), b4 = a256((size_t)n * 4);
+  const size_t need = b8 + b4 + a256(cub_bytes) + a256((size_t)n * sizeof(mgenx_pack_desc)) +
+                      b8 + 4 * b4 + 2 * b4 + 3 * b8 + 3 * b4 + 3 * b4;
+  if (ctx->tcp_ws_bytes < need) {
+    if (ctx->tcp_ws) hipFree(ctx->tcp_ws);
+    ctx->tcp_ws = nullptr;
+    ctx->tcp_ws_bytes = 0;
+    if ((e = hipMalloc(&ctx->tcp_ws, need)) != hipSuccess) return set_err(ctx, e, "tcp workspace");
+    ctx->tcp_ws_bytes = need;
+  }
+  char* w = static_cast<char*>(ctx->tcp_ws);
+  auto take = [&](size_t b) { char* q = w; w += b; return q; };
+  uint64_t* bytes = (uint64_t*)take(b8);
+  uint32_t* nfrag = (uint32_t*)take(b4);
+  void* cub = take(a256(cub_bytes));
+  mgenx_pack_desc* fd = (mgenx_pack_desc*)take(a256((size_t)n * sizeof(mgenx_pack_desc)));
+  uint64_t* foff = (uint64_t*)take(b8);
+  uint32_t* fbuf = (uint32_t*)take(b4);
+  uint32_t* ff = (uint32_t*)take(b4);
+  uint32_t* plen = (uint32_t*)take(b4);
+  uint32_t* crc = (uint32_t*)take(b4);
+  uint32_t* st[2] = {(uint32_t*)take(b4), (uint32_t*)take(b4)};
+  uint64_t* roff = (uint64_t*)take(3 * b8);
+  uint32_t* rlen = (uint32_t*)take(3 * b4);
+  uint32_t* acrc = (uint32_t*)take(3 * b4);
+  // plan: bytes per message, fragments; offsets by an exclusive scan (the message offsets
+  // are the caller's array: n + 1 entries are not assumed, the scan runs in the workspace)
+  if ((e = mgenx::launch_tcp_plan(dev_tmpl, dev_desc, dev_msg_total, n, bytes, nfrag, s)) != hipSuccess)
+    return set_err(ctx, e, "tcp plan");
+  uint64_t* offs = foff;  // reused below only after the copy out
+  if ((e = hipcub::DeviceScan::ExclusiveSum(cub, cub_bytes, (const uint64_t*)bytes, offs,
+                                            (int)(n + 1), s)) != hipSuccess)
+    return set_err(ctx, e, "tcp scan");
+  if ((e = hipMemcpyAsync(dev_msg_off, offs, (size_t)n * 8, hipMemcpyDeviceToDevice, s)) != hipSuccess)
+    return set_err(ctx, e, "tcp");
+  hipLaunchKernelGGL(tcp_totals_kernel, dim3(1), dim3(256), 0, s, nfrag, n, offs, ctx->tcp_host_dev);
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return set_err(ctx, e, "tcp plan");
+  const uint64_t total = ((volatile uint64_t*)ctx->tcp_host)[0];
+  const uint32_t rounds = (uint32_t)((volatile uint64_t*)ctx->tcp_host)[1];
+  *total_bytes = total;
+  if (total > stream_cap || (total && !dev_stream)) {
+    snprintf(ctx->err, sizeof(ctx->err), "tcp: the stream needs %llu bytes",
+             (unsigned long long)total);
+    return MGENX_EINVAL;
+  }
+  const int ck = (opts & MGENX_PACK_CHECKSUM) ? 1 : 0;
+  for (uint32_t r = 0; r < rounds; r++) {
+    if ((e = mgenx::launch_tcp_frag(dev_desc, dev_msg_total, nfrag, dev_msg_off, n, r, ck,
+                                    st[(r + 1) & 1], fd, foff, fbuf, ff, s)) != hipSuccess)
+      return set_err(ctx, e, "tcp fragments");
+    int rc = pack_common(ctx, dev_tmpl, dev_tmpl_crc, fd, n, dev_pool, dev_stream, stream_cap,
+                         foff, 0, fbuf, nullptr, plen, crc, st[r & 1], opts | MGENX_PACK_RAW,
+                         fill_time, stream);
+    if (rc != MGENX_OK) return rc;
+    if ((e = mgenx::launch_tcp_tail(dev_stream, foff, fbuf, ff, plen, crc, st[r & 1], n, ck, roff,
+                                    rlen, acrc, ctx->d_bytetab, ctx->d_xpow, ctx->d_ia, s)) != hipSuccess)
+      return set_err(ctx, e, "tcp tail");
+  }
+  return MGENX_OK;
 }
 
 int mgenx_ctx_device(const mgenx_ctx* ctx) { return ctx ? ctx->device : -1; }

@@ -64,6 +64,19 @@ hipError_t launch_stream_read(const uint8_t* p, uint64_t bytes, uint32_t* out, i
 hipError_t launch_pack(const PackParams& p, int grid, hipStream_t stream);
 hipError_t launch_pack_prepare(const mgenx_flow_tmpl* tmpl, uint32_t n_tmpl, const uint8_t* pool,
                                const uint32_t* byte_tab, uint32_t* out, hipStream_t stream);
+// TCP transmit (mgenx_tcp.hip)
+hipError_t launch_tcp_plan(const mgenx_flow_tmpl* tmpl, const mgenx_pack_desc* desc,
+                           const uint32_t* msg_total, uint32_t n, uint64_t* bytes,
+                           uint32_t* nfrag, hipStream_t s);
+hipError_t launch_tcp_frag(const mgenx_pack_desc* desc, const uint32_t* msg_total,
+                           const uint32_t* nfrag, const uint64_t* msg_off, uint32_t n, uint32_t r,
+                           int ck, const uint32_t* prev_state, mgenx_pack_desc* fd, uint64_t* foff,
+                           uint32_t* fbuf, uint32_t* ff, hipStream_t s);
+hipError_t launch_tcp_tail(uint8_t* out, const uint64_t* foff, const uint32_t* fbuf,
+                           const uint32_t* ff, const uint32_t* plen, const uint32_t* tx_crc,
+                           const uint32_t* state, uint32_t n, int ck, uint64_t* roff,
+                           uint32_t* rlen, uint32_t* acrc, const uint32_t* byte_tab,
+                           const uint32_t* xpow, const uint32_t* ia, hipStream_t s);
 hipError_t launch_crc32(const uint8_t* data, const uint64_t* off, const uint32_t* len, uint32_t n,
                         const uint32_t* byte_tab, const uint32_t* state_in, uint32_t* out,
                         hipStream_t stream);

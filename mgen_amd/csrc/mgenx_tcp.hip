@@ -1,0 +1,267 @@
+// mgenx_tcp.hip -- MgenTcpTransport's transmit byte stream on gfx950.
+//
+// Reference (restated in oracle/mgen_oracle.c or_tcp_tx): MgenTcpTransport::SendMessage
+// (src/common/mgenTransport.cpp:1320-1400) with GetNextTxFragmentSize :1960-1993,
+// GetNextTxFragment :1878-1951, SetupNextTxBuffer :1818-1852, CalcTxChecksum :1854-1876.
+// A message of mgen_msg_len M goes out as fragments of at most 65535 bytes (65459 when the
+// remainder would leave less than a minimum fragment); a fragment F <= 8192 is one packed
+// buffer with LAST_BUFFER and its checksum; a larger one is ONE 8-KiB Pack (8188 bytes when
+// F - 8192 < 4) whose buffer is then re-sent from its start until F bytes have gone out
+// (8192 per buffer, the last one carrying the CRC over everything before it).
+//
+// GPU form, per round r (fragment r of every message; one round unless M > 65535):
+//   tcp_frag_kernel   fragment descriptors: msg_len = F, Pack's bufferLen B, flags, offset;
+//   raw Pack          (mgenx_pack.hip, MGENX_PACK_RAW) the B-byte buffer P at the fragment
+//                     start, its running CRC and the MgenMsg flags it leaves;
+//   tcp_copy_kernel   P[0 .. s_k) for every later buffer k of the fragment;
+//   crc32 ranges      A(s) = ComputeCRC32 from a restart over P[0 .. s) for the (at most
+//                     three) distinct buffer lengths of the fragment;
+//   tcp_finish_kernel the running CRC chained through the buffers algebraically,
+//                     c' = raw(P[0..s)) ^ x^(8s) * c  (c = 0 restarts, as ComputeCRC32 does),
+//                     and the big-endian trailer.
+#include <hip/hip_runtime.h>
+
+#include "mgenx_kernels.hpp"
+
+namespace mgenx {
+
+constexpr uint32_t kTxBuf = MGENX_TX_BUFFER_SIZE;  // 8192
+constexpr uint32_t kMaxFrag = MGENX_MAX_FRAG_SIZE;  // 65535
+constexpr uint32_t kMinFrag = 76;                   // MIN_FRAG_SIZE (mgenTransport.h)
+
+// fragment r of a message of M bytes: size, offset within the message, flags bits
+__device__ __forceinline__ bool tcp_fragment(uint32_t M, uint32_t r, uint32_t& F, uint32_t& at,
+                                             bool& more) {
+  uint32_t off = 0;
+  for (uint32_t k = 0;; k++) {
+    const uint32_t rem = M - off;
+    if (rem == 0) return false;
+    uint32_t f;
+    if (rem > kMaxFrag) f = rem < kMaxFrag + kMinFrag ? kMaxFrag - kMinFrag : kMaxFrag;
+    else f = rem;
+    if (k == r) {
+      F = f;
+      at = off;
+      more = rem > f;
+      return true;
+    }
+    off += f;
+  }
+}
+
+// per message: stream bytes (0 when the first Pack fails -- no destination, or a first
+// fragment shorter than the address part of the header -- or M == 0) and fragment count
+__global__ void tcp_plan_kernel(const mgenx_flow_tmpl* __restrict__ tmpl,
+                                const mgenx_pack_desc* __restrict__ desc,
+                                const uint32_t* __restrict__ msg_total, uint32_t n,
+                                uint64_t* __restrict__ bytes, uint32_t* __restrict__ nfrag) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > n) return;
+  if (i == n) {  // exclusive-scan tail
+    bytes[n] = 0;
+    return;
+  }
+  const uint32_t M = msg_total[i];
+  const mgenx_flow_tmpl& t = tmpl[desc[i].tmpl];
+  const bool dst_ok = t.dst_type == 1u || t.dst_type == 2u;
+  const uint32_t D = t.dst_len > 16u ? 16u : t.dst_len;
+  uint32_t F0 = 0, at, cnt = 0;
+  bool more;
+  if (M && tcp_fragment(M, 0, F0, at, more)) {
+    const uint32_t B0 = F0 > kTxBuf ? kTxBuf - 4u : F0;  // smallest bufferLen it can get
+    const bool ok = dst_ok && B0 >= 24u + D;
+    if (ok) cnt = (M + (kMaxFrag - kMinFrag) - 1) / (kMaxFrag - kMinFrag) + 1;  // bound
+  }
+  // exact count
+  uint32_t c = 0;
+  if (cnt) {
+    uint32_t F, a;
+    while (tcp_fragment(M, c, F, a, more)) c++;
+  }
+  bytes[i] = c ? (uint64_t)M : 0ull;
+  nfrag[i] = c;
+}
+
+// round r: the pack descriptor of fragment r of each message (msg_len 0 = none this round)
+__global__ void tcp_frag_kernel(const mgenx_pack_desc* __restrict__ desc,
+                                const uint32_t* __restrict__ msg_total,
+                                const uint32_t* __restrict__ nfrag,
+                                const uint64_t* __restrict__ msg_off, uint32_t n, uint32_t r,
+                                int ck, const uint32_t* __restrict__ prev_state,
+                                mgenx_pack_desc* __restrict__ fd, uint64_t* __restrict__ foff,
+                                uint32_t* __restrict__ fbuf, uint32_t* __restrict__ ff) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  mgenx_pack_desc d = desc[i];
+  uint32_t F = 0, at = 0;
+  bool more = false;
+  if (r < nfrag[i]) (void)tcp_fragment(msg_total[i], r, F, at, more);
+  uint32_t B = 0;
+  if (F) {
+    // the MgenMsg flags member: the descriptor's on the first fragment, what the previous
+    // fragment's Pack left afterwards (GetNextTxFragmentSize, :1960-1993)
+    uint32_t fl = r == 0 ? d.flags : (prev_state[i] >> 16) & 0xffu;
+    fl &= ~(uint32_t)MGENX_FLAG_CONTINUES;
+    if (msg_total[i] > kMaxFrag) fl |= more ? MGENX_FLAG_CONTINUES : MGENX_FLAG_END_OF_MSG;
+    if (F > kTxBuf) {  // GetNextTxFragment: Pack into the 8-KiB buffer (:1915-1926)
+      B = (ck && (int32_t)F - (int32_t)kTxBuf < 4 && F != kMinFrag) ? kTxBuf - 4u : kTxBuf;
+    } else {
+      fl |= MGENX_FLAG_LAST_BUFFER;
+      B = F;
+    }
+    d.flags = (uint8_t)fl;
+  }
+  d.msg_len = (uint16_t)F;
+  fd[i] = d;
+  foff[i] = msg_off[i] + at;
+  fbuf[i] = B;
+  ff[i] = F;
+}
+
+// buffer k >= 1 of a fragment of F bytes whose first buffer holds B: (start, size)
+// (SetupNextTxBuffer, :1818-1852); returns false past the last
+__device__ __forceinline__ bool tcp_buffer(uint32_t F, uint32_t B, int ck, uint32_t k,
+                                           uint32_t& start, uint32_t& size, bool& last) {
+  uint32_t pos = B;
+  for (uint32_t j = 1;; j++) {
+    const uint32_t pend = F - pos;
+    if (pend == 0) return false;
+    uint32_t s;
+    bool l = false;
+    if ((ck && pend <= kTxBuf - 4u) || (!ck && pend <= kTxBuf)) {
+      s = pend;
+      l = true;
+    } else {
+      s = (ck && (int32_t)pend - (int32_t)kTxBuf < 4) ? pend - 4u : kTxBuf;
+    }
+    if (j == k) {
+      start = pos;
+      size = s;
+      last = l;
+      return true;
+    }
+    pos += s;
+  }
+}
+
+// copy P[0 .. s) (the last buffer: s - 4 with a checksum) to every later buffer; one
+// workgroup per fragment, 16 bytes per lane per step (P was just written: L2 hits)
+__global__ void __launch_bounds__(256)
+tcp_copy_kernel(uint8_t* __restrict__ out, const uint64_t* __restrict__ foff,
+                const uint32_t* __restrict__ fbuf, const uint32_t* __restrict__ ff,
+                const uint32_t* __restrict__ plen, uint32_t n, int ck) {
+  const uint32_t i = blockIdx.x;
+  if (i >= n) return;
+  const uint32_t F = ff[i], B = fbuf[i];
+  if (F <= B || plen[i] == 0) return;
+  uint8_t* base = out + foff[i];
+  uint32_t start, size;
+  bool last;
+  for (uint32_t k = 1; tcp_buffer(F, B, ck, k, start, size, last); k++) {
+    const uint32_t cnt = (last && ck) ? size - 4u : size;
+    uint8_t* dst = base + start;
+    const uint32_t nv = cnt >> 4;
+    for (uint32_t v = threadIdx.x; v < nv; v += blockDim.x) stu128(dst + 16u * v, ldu128(base + 16u * v));
+    for (uint32_t b = (nv << 4) + threadIdx.x; b < cnt; b += blockDim.x) dst[b] = base[b];
+  }
+}
+
+// CRC ranges: for each fragment the distinct CRC lengths of its later buffers (at most 3:
+// full 8192, one SetupNextTxBuffer-shortened buffer, the last one's size - 4)
+__global__ void tcp_ranges_kernel(const uint64_t* __restrict__ foff, const uint32_t* __restrict__ fbuf,
+                                  const uint32_t* __restrict__ ff, const uint32_t* __restrict__ plen,
+                                  uint32_t n, int ck, uint64_t* __restrict__ roff,
+                                  uint32_t* __restrict__ rlen) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t F = ff[i], B = fbuf[i];
+  uint32_t L[3] = {0u, 0u, 0u};
+  if (ck && F > B && plen[i]) {
+    uint32_t start, size;
+    bool last;
+    for (uint32_t k = 1; tcp_buffer(F, B, ck, k, start, size, last); k++) {
+      const uint32_t c = last ? size - 4u : size;
+      const int slot = last ? 2 : (size == kTxBuf ? 0 : 1);
+      L[slot] = c;
+    }
+  }
+  for (int j = 0; j < 3; j++) {
+    roff[3 * i + j] = foff[i];
+    rlen[3 * i + j] = L[j];
+  }
+}
+
+// the fragment's CRC through its later buffers and the trailer
+__global__ void tcp_finish_kernel(uint8_t* __restrict__ out, const uint64_t* __restrict__ foff,
+                                  const uint32_t* __restrict__ fbuf, const uint32_t* __restrict__ ff,
+                                  const uint32_t* __restrict__ plen, const uint32_t* __restrict__ tx_crc,
+                                  const uint32_t* __restrict__ state, const uint32_t* __restrict__ acrc,
+                                  const uint32_t* __restrict__ xpow, const uint32_t* __restrict__ ia,
+                                  uint32_t n, int ck) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t F = ff[i], B = fbuf[i];
+  if (!ck || !F || plen[i] == 0) return;
+  uint32_t c = tx_crc[i];
+  bool write = true;
+  if (F <= B) {
+    // one buffer: Pack ran with LAST_BUFFER; WriteChecksum only when Pack set CHECKSUM
+    write = ((state[i] >> 16) & MGENX_FLAG_CHECKSUM) != 0u;
+  } else {
+    uint32_t start, size;
+    bool last;
+    for (uint32_t k = 1; tcp_buffer(F, B, ck, k, start, size, last); k++) {
+      const uint32_t s = last ? size - 4u : size;
+      // (the crc32 ranges were run without a state: final xor applied)
+      const uint32_t a = acrc[3 * i + (last ? 2 : (size == kTxBuf ? 0 : 1))] ^ 0xFFFFFFFFu;
+      // ComputeCRC32(c, P, s): a zero running value restarts; raw(P[0..s)) = A(s) ^ ia[s]
+      const uint32_t cr = c == 0u ? 0xFFFFFFFFu : c;
+      if (s) c = a ^ ia[s] ^ multmodp(xpow[s], cr);
+      else c = cr;
+    }
+  }
+  if (write) {
+    const uint32_t v = c ^ 0xFFFFFFFFu;
+    uint8_t* p = out + foff[i] + F - 4u;
+    p[0] = (uint8_t)(v >> 24);
+    p[1] = (uint8_t)(v >> 16);
+    p[2] = (uint8_t)(v >> 8);
+    p[3] = (uint8_t)v;
+  }
+}
+
+hipError_t launch_tcp_plan(const mgenx_flow_tmpl* tmpl, const mgenx_pack_desc* desc,
+                           const uint32_t* msg_total, uint32_t n, uint64_t* bytes,
+                           uint32_t* nfrag, hipStream_t s) {
+  hipLaunchKernelGGL(tcp_plan_kernel, dim3((n + 256) / 256), dim3(256), 0, s, tmpl, desc, msg_total,
+                     n, bytes, nfrag);
+  return hipGetLastError();
+}
+
+hipError_t launch_tcp_frag(const mgenx_pack_desc* desc, const uint32_t* msg_total,
+                           const uint32_t* nfrag, const uint64_t* msg_off, uint32_t n, uint32_t r,
+                           int ck, const uint32_t* prev_state, mgenx_pack_desc* fd, uint64_t* foff,
+                           uint32_t* fbuf, uint32_t* ff, hipStream_t s) {
+  hipLaunchKernelGGL(tcp_frag_kernel, dim3((n + 255) / 256), dim3(256), 0, s, desc, msg_total, nfrag,
+                     msg_off, n, r, ck, prev_state, fd, foff, fbuf, ff);
+  return hipGetLastError();
+}
+
+hipError_t launch_tcp_tail(uint8_t* out, const uint64_t* foff, const uint32_t* fbuf,
+                           const uint32_t* ff, const uint32_t* plen, const uint32_t* tx_crc,
+                           const uint32_t* state, uint32_t n, int ck, uint64_t* roff,
+                           uint32_t* rlen, uint32_t* acrc, const uint32_t* byte_tab,
+                           const uint32_t* xpow, const uint32_t* ia, hipStream_t s) {
+  hipLaunchKernelGGL(tcp_copy_kernel, dim3(n), dim3(256), 0, s, out, foff, fbuf, ff, plen, n, ck);
+  if (ck) {
+    hipLaunchKernelGGL(tcp_ranges_kernel, dim3((n + 255) / 256), dim3(256), 0, s, foff, fbuf, ff,
+                       plen, n, ck, roff, rlen);
+    hipError_t e = launch_crc32(out, roff, rlen, 3 * n, byte_tab, nullptr, acrc, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(tcp_finish_kernel, dim3((n + 255) / 256), dim3(256), 0, s, out, foff, fbuf,
+                       ff, plen, tx_crc, state, acrc, xpow, ia, n, ck);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace mgenx
