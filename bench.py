@@ -210,29 +210,34 @@ def extra_config4(torch, eng, dev, world, rank, dist):
 
 def extra_config5(torch, eng, dev, world=1, rank=0, dist=None):
     """TCP stream of 16 KiB records (checksum on): boundary scan + TCP-rule unpack over
-    1 GiB per rank (a 64 MiB oracle-built stream tiled 16x: framing and CRCs stay valid).
+    1 GiB per rank, the stream built by the GPU TCP transmit path (mgenx_pack_tcp).
     N > 1: one stream of N GiB split into 1-GiB shards (+ 64 KiB halo) framed with the
     sharded protocol (mgen_amd/shard.py: exits table all-gather over RCCL, then the rank's
     range); weak scaling, time = max over ranks."""
-    from mgen_amd import OPT_TCP, SCAN_TCP, to_device
+    from mgen_amd import OPT_TCP, PACK_CHECKSUM, SCAN_TCP, to_device
     from mgen_amd._abi import DESC_DTYPE
     from mgen_amd.shard import HALO, EngineScanner, TorchComm, scan_sharded
     from mgen_amd.workloads import make_templates
-    from oracle import oracle as O
-    n0 = 4096
+    n = 65536                       # 16 KiB records per rank: 1 GiB
+    extra_n = HALO // 16384 if rank < world - 1 else 0   # the next rank's first records
     tmpl, pool = make_templates(64)
-    desc = np.zeros(n0, DESC_DTYPE)
-    desc["tmpl"] = np.arange(n0) % 64
-    desc["seq_num"] = np.arange(n0) // 64
-    desc["tx_sec"] = 1_700_000_000
-    desc["tx_usec"] = np.arange(n0)
-    desc["msg_len"] = 16384
+    desc = np.zeros(n + extra_n, DESC_DTYPE)
+    seq = rank * n + np.arange(n + extra_n)
+    desc["tmpl"] = seq % 64
+    desc["seq_num"] = seq
+    desc["tx_sec"] = 1_700_000_000 + seq // 1_000_000
+    desc["tx_usec"] = seq % 1_000_000
     desc["flags"] = 4
-    s0 = np.asarray(O.tcp_tx_batch(tmpl, desc, np.full(n0, 16384, np.uint32), pool), np.uint8)
-    tile = to_device(s0, dev.index)
-    shard = tile.repeat(16)
-    n = n0 * 16
-    local = torch.cat([shard, tile[:HALO]]) if rank < world - 1 else shard
+    tm, pl = to_device(tmpl, dev.index), to_device(pool, dev.index)
+    tcrc = torch.empty(64, dtype=torch.int32, device=dev)
+    eng.pack_prepare(tm, 64, pl, tcrc)
+    d_desc = to_device(desc, dev.index)
+    d_total = torch.full((n + extra_n,), 16384, dtype=torch.int32, device=dev)
+    # the TCP transmit stream built on the GPU (mgenx_pack_tcp), timed
+    local, toffs = eng.pack_tcp(tm, tcrc, d_desc, d_total, n + extra_n, pl, opts=PACK_CHECKSUM)
+    tx_ms = timed(torch, lambda: eng.pack_tcp(tm, tcrc, d_desc, d_total, n + extra_n, pl,
+                                              opts=PACK_CHECKSUM, out=local, offs=toffs), reps=3)
+    shard = local[:n * 16384]
     total_bytes = shard.numel() * world
     state = {}
     if world > 1:
@@ -274,6 +279,8 @@ def extra_config5(torch, eng, dev, world=1, rank=0, dist=None):
             "scan_frac_of_peak_per_gpu": round(b / scan_ms / 1e6 / PEAK_HBM_GBPS, 4),
             "unpack_ms": round(ums, 4),
             "unpack_gbps": round((b + n * 32) / ums / 1e6, 1),
+            "tcp_tx_ms": round(tx_ms, 4), "tcp_tx_gbps": round(b / tx_ms / 1e6, 1),
+            "stream_source": "mgenx_pack_tcp (GPU TCP transmit, timed as tcp_tx_*)",
             "framing": "sharded (exits all-gather + range)" if world > 1 else "whole stream"}
 
 

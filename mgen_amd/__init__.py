@@ -260,13 +260,16 @@ class Engine:
         return out_len, tx_crc, state
 
     def pack_tcp(self, tmpl, tmpl_crc, desc, msg_total, n, pool, *, opts=0, fill_time=0,
-                 cap=None):
+                 out=None, offs=None):
         """The MgenTcpTransport transmit stream of n messages (mgenx_pack_tcp): returns
-        (stream uint8 tensor, message offsets int64 tensor)."""
+        (stream uint8 tensor, message offsets int64 tensor).  out: a stream buffer to fill
+        (else one is sized by a first call)."""
         torch = self.torch
         dev = msg_total.device
-        offs = torch.empty(n, dtype=torch.int64, device=dev)
+        if offs is None:
+            offs = torch.empty(n, dtype=torch.int64, device=dev)
         total = ctypes.c_uint64(0)
+        cap = None if out is None else out.numel()
         if cap is None:  # size query: a first call with no room reports the length
             rc = self.lib.mgenx_pack_tcp(self.ctx, _ptr(tmpl), _ptr(tmpl_crc), _ptr(desc),
                                          _ptr(msg_total), n, _ptr(pool), None, 0, _ptr(offs),
@@ -275,7 +278,7 @@ class Engine:
             if rc not in (0, -1):
                 self._check(rc, "mgenx_pack_tcp")
             cap = int(total.value)
-        out = torch.zeros(max(cap, 1), dtype=torch.uint8, device=dev)
+            out = torch.zeros(max(cap, 1), dtype=torch.uint8, device=dev)
         rc = self.lib.mgenx_pack_tcp(self.ctx, _ptr(tmpl), _ptr(tmpl_crc), _ptr(desc),
                                      _ptr(msg_total), n, _ptr(pool), _ptr(out), cap, _ptr(offs),
                                      ctypes.byref(total), opts, fill_time, _stream(self.device))

@@ -453,7 +453,8 @@ int mgenx_pack_tcp(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl, const uint32
                          fill_time, stream);
     if (rc != MGENX_OK) return rc;
     if ((e = mgenx::launch_tcp_tail(dev_stream, foff, fbuf, ff, plen, crc, st[r & 1], n, ck, roff,
-                                    rlen, acrc, ctx->d_bytetab, ctx->d_xpow, ctx->d_ia, s)) != hipSuccess)
+                                    rlen, acrc, ctx->d_bytetab, ctx->d_tabs + 1024, ctx->d_xpow,
+                                    ctx->d_ia, s)) != hipSuccess)
       return set_err(ctx, e, "tcp tail");
   }
   return MGENX_OK;
@@ -624,7 +625,8 @@ int mgenx_crc32_batch(mgenx_ctx* ctx, const uint8_t* dev_data, const uint64_t* d
   if (!ctx) return MGENX_EINVAL;
   if (n == 0) return MGENX_OK;
   if (!dev_data || !dev_off || !dev_len || !dev_out) return MGENX_EINVAL;
-  hipError_t e = mgenx::launch_crc32(dev_data, dev_off, dev_len, n, ctx->d_bytetab, nullptr,
+  hipError_t e = mgenx::launch_crc32(dev_data, dev_off, dev_len, n, ctx->d_bytetab,
+                                     ctx->d_tabs + 1024, ctx->d_xpow, nullptr,
                                      dev_out, (hipStream_t)stream);
   return e == hipSuccess ? MGENX_OK : set_err(ctx, e, "crc32");
 }
@@ -635,7 +637,8 @@ int mgenx_crc32_update(mgenx_ctx* ctx, const uint8_t* dev_data, const uint64_t* 
   if (!ctx) return MGENX_EINVAL;
   if (n == 0) return MGENX_OK;
   if (!dev_data || !dev_off || !dev_len || !dev_state_in || !dev_state_out) return MGENX_EINVAL;
-  hipError_t e = mgenx::launch_crc32(dev_data, dev_off, dev_len, n, ctx->d_bytetab, dev_state_in,
+  hipError_t e = mgenx::launch_crc32(dev_data, dev_off, dev_len, n, ctx->d_bytetab,
+                                     ctx->d_tabs + 1024, ctx->d_xpow, dev_state_in,
                                      dev_state_out, (hipStream_t)stream);
   return e == hipSuccess ? MGENX_OK : set_err(ctx, e, "crc32_update");
 }

@@ -109,6 +109,20 @@ __host__ __device__ inline uint32_t multmodp(uint32_t a, uint32_t b) {
   return p;
 }
 
+// x^(8 n) mod P for any n from the [65536] table: low 16 bits from the table, the rest by
+// square-and-multiply of x^(8 * 65536)
+__device__ __forceinline__ uint32_t xpow8(uint32_t n, const uint32_t* xpow) {
+  if (n < 65536u) return xpow[n];
+  uint32_t r = xpow[n & 0xFFFFu];
+  uint32_t sq = xpow[32768];
+  sq = multmodp(sq, sq);
+  for (n >>= 16; n; n >>= 1) {
+    if (n & 1u) r = multmodp(r, sq);
+    sq = multmodp(sq, sq);
+  }
+  return r;
+}
+
 // Byte-mask helpers: bytes [lo, hi) of a little-endian 32-bit word, lo/hi in [0,4].
 __device__ __forceinline__ uint32_t byte_range_mask(int lo, int hi) {
   uint32_t m_hi = hi >= 4 ? 0xFFFFFFFFu : ((1u << (8 * hi)) - 1u);

@@ -378,31 +378,58 @@ hipError_t launch_pack_prepare(const mgenx_flow_tmpl* tmpl, uint32_t n_tmpl, con
 
 }  // namespace mgenx
 
-// Utility: CRC-32 of n byte ranges, one thread per range (byte table in LDS).
+// Utility: CRC-32 of n byte ranges, one WAVE per range: lane k runs the raw CRC (zero
+// register, 4 bytes per step through the A_4 tables in LDS) of its 1/64 of the range, and
+// the 64 partial CRCs combine by the shift operators x^(8 len) (multmodp): crc(A || B) =
+// x^(8|B|) crc(A) ^ crc(B) over GF(2).
 //   state_in == NULL: the standard CRC (init ~0, xorout ~0) -- mgenx_crc32_batch;
 //   state_in != NULL: MgenMsg::ComputeCRC32(checksum, buf, len) (mgenMsg.cpp:524-541): the
 //   running state continues from state_in[i] (0 restarts from ~0), no final xor.
 namespace mgenx {
-__global__ void crc32_kernel(const uint8_t* data, const uint64_t* off, const uint32_t* len,
-                             uint32_t n, const uint32_t* byte_tab, const uint32_t* state_in,
-                             uint32_t* out) {
+__global__ void __launch_bounds__(256)
+crc32_kernel(const uint8_t* __restrict__ data, const uint64_t* __restrict__ off,
+             const uint32_t* __restrict__ len, uint32_t n, const uint32_t* __restrict__ byte_tab,
+             const uint32_t* __restrict__ a4_tab, const uint32_t* __restrict__ xpow,
+             const uint32_t* __restrict__ state_in, uint32_t* __restrict__ out) {
   __shared__ uint32_t s_tab[256];
+  __shared__ uint32_t s_a4[1024];
   for (int e = threadIdx.x; e < 256; e += blockDim.x) s_tab[e] = byte_tab[e];
+  for (int e = threadIdx.x; e < 1024; e += blockDim.x) s_a4[e] = a4_tab[e];
   __syncthreads();
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t i = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (i >= n) return;
   const uint8_t* s = data + off[i];
-  uint32_t c = state_in ? state_in[i] : 0u;
-  if (c == 0u) c = 0xFFFFFFFFu;
-  for (uint32_t k = 0; k < len[i]; k++) c = s_tab[(c ^ s[k]) & 0xffu] ^ (c >> 8);
-  out[i] = state_in ? c : (c ^ 0xFFFFFFFFu);
+  const uint32_t L = len[i];
+  const uint32_t chunk = (((L + 63u) >> 6) + 3u) & ~3u;  // bytes per lane, a multiple of 4
+  const uint32_t lo = min(lane * chunk, L), hi = min(lo + chunk, L);
+  uint32_t c = 0;  // raw CRC (zero register) of this lane's bytes
+  uint32_t k = lo;
+  for (; k + 4u <= hi; k += 4u) {
+    const uint32_t x = c ^ ldu32(s + k);
+    c = s_a4[x & 0xffu] ^ s_a4[256 + ((x >> 8) & 0xffu)] ^ s_a4[512 + ((x >> 16) & 0xffu)] ^
+        s_a4[768 + (x >> 24)];
+  }
+  for (; k < hi; k++) c = s_tab[(c ^ s[k]) & 0xffu] ^ (c >> 8);
+  // shift each partial by the bytes after it, then XOR across the wave
+  const uint32_t after = L - hi;
+  if (c && after) c = multmodp(xpow8(after, xpow), c);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) c ^= (uint32_t)__shfl_xor((int)c, o);
+  if (lane == 0) {
+    uint32_t st = state_in ? state_in[i] : 0u;
+    if (st == 0u) st = 0xFFFFFFFFu;
+    const uint32_t r = c ^ (L ? multmodp(xpow8(L, xpow), st) : st);
+    out[i] = state_in ? r : (r ^ 0xFFFFFFFFu);
+  }
 }
 
 hipError_t launch_crc32(const uint8_t* data, const uint64_t* off, const uint32_t* len, uint32_t n,
-                        const uint32_t* byte_tab, const uint32_t* state_in, uint32_t* out,
-                        hipStream_t stream) {
-  hipLaunchKernelGGL(crc32_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, data, off, len, n,
-                     byte_tab, state_in, out);
+                        const uint32_t* byte_tab, const uint32_t* a4_tab, const uint32_t* xpow,
+                        const uint32_t* state_in, uint32_t* out, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(crc32_kernel, dim3((n + 3) / 4), dim3(256), 0, stream, data, off, len, n,
+                     byte_tab, a4_tab, xpow, state_in, out);
   return hipGetLastError();
 }
 }  // namespace mgenx

@@ -251,12 +251,13 @@ hipError_t launch_tcp_tail(uint8_t* out, const uint64_t* foff, const uint32_t* f
                            const uint32_t* ff, const uint32_t* plen, const uint32_t* tx_crc,
                            const uint32_t* state, uint32_t n, int ck, uint64_t* roff,
                            uint32_t* rlen, uint32_t* acrc, const uint32_t* byte_tab,
-                           const uint32_t* xpow, const uint32_t* ia, hipStream_t s) {
+                           const uint32_t* a4_tab, const uint32_t* xpow, const uint32_t* ia,
+                           hipStream_t s) {
   hipLaunchKernelGGL(tcp_copy_kernel, dim3(n), dim3(256), 0, s, out, foff, fbuf, ff, plen, n, ck);
   if (ck) {
     hipLaunchKernelGGL(tcp_ranges_kernel, dim3((n + 255) / 256), dim3(256), 0, s, foff, fbuf, ff,
                        plen, n, ck, roff, rlen);
-    hipError_t e = launch_crc32(out, roff, rlen, 3 * n, byte_tab, nullptr, acrc, s);
+    hipError_t e = launch_crc32(out, roff, rlen, 3 * n, byte_tab, a4_tab, xpow, nullptr, acrc, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(tcp_finish_kernel, dim3((n + 255) / 256), dim3(256), 0, s, out, foff, fbuf,
                        ff, plen, tx_crc, state, acrc, xpow, ia, n, ck);

@@ -377,3 +377,17 @@ def test_fixed_len_rows_output(torch, eng, gold, size):
     for gname, _, dt in COLMAP[:13]:
         assert np.array_equal(c[gname].view(dt)[:n], r[gname].view(dt)), gname
     assert np.array_equal(c["dst_addr4"][:n], r["dst_addr4"])
+
+
+def test_crc32_batch_long_ranges(torch, eng):
+    """Ranges past the 65536-entry shift table (x^(8n) by square-and-multiply), unaligned
+    starts and lengths not a multiple of 4 or 64."""
+    rng = np.random.default_rng(31)
+    data = rng.integers(0, 256, 3_000_000, dtype=np.uint8)
+    lens = np.array([65535, 65536, 65537, 200_001, 1_048_579, 2_900_000, 63, 5], np.uint32)
+    offs = np.array([1, 7, 100_003, 5, 333, 99_999, 2_999_000, 2_999_990], np.uint64)
+    out = eng.crc32(dev(torch, data), dev(torch, offs).view(torch.int64),
+                    dev(torch, lens).view(torch.int32), len(lens))
+    got = out.cpu().numpy().view(np.uint32)
+    for i in range(len(lens)):
+        assert got[i] == zlib.crc32(data[int(offs[i]):int(offs[i]) + int(lens[i])].tobytes()), i
