@@ -6,7 +6,7 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -Wno-unused-value -Wno-int-to-pointer-cast
 NAMES := mgenx_api mgenx_unpack mgenx_pack mgenx_scan mgenx_analytic mgenx_log mgenx_comm \
-         mgenx_flowtab mgenx_tcp
+         mgenx_flowtab mgenx_tcp mgenx_rx
 HDR := include/mgenx.h include/mgenx_diag.h mgen_amd/csrc/mgenx_common.hpp mgen_amd/csrc/mgenx_kernels.hpp
 OBJ := $(addprefix build/product/,$(addsuffix .o,$(NAMES)))
 DOBJ := $(addprefix build/diag/,$(addsuffix .o,$(NAMES)))

@@ -245,6 +245,42 @@ int mgenx_crc32_update(mgenx_ctx* ctx, const uint8_t* dev_data, const uint64_t* 
 int mgenx_crc32_batch(mgenx_ctx* ctx, const uint8_t* dev_data, const uint64_t* dev_off,
                       const uint32_t* dev_len, uint32_t n, uint32_t* dev_out, void* stream);
 
+/* ---- the TCP receiver's persistent rx_msg ----
+ * MgenTcpTransport decodes every message of a connection into ONE MgenMsg (rx_msg,
+ * src/common/mgenTransport.cpp:1082): ResetRxMsgState (:1501-1513) zeroes only
+ * mgen_msg_len / msg_len / flow_id / seq_num / the error between messages, Unpack runs only
+ * while a log file is open (:2016-2028) and assigns members stage by stage (mgenMsg.cpp:
+ * 315-500), and the CRC check reads the flags rx_msg holds (:1516-1564).  So a record that
+ * stops early keeps the previous record's flags, tx time, destination, header length, GPS
+ * position and payload; with no log file nothing is decoded at all (flow id and sequence
+ * number stay 0) and the CRC is checked only under checksum_force.
+ * mgenx_tcp_rx_persist rewrites n consecutive records of one connection, decoded by
+ * mgenx_unpack_batch(MGENX_OPT_TCP) into core + extended columns with `decoded`, into that
+ * rx_msg view, in place: every member group a record did not assign comes from the latest
+ * earlier record that did, or from *dev_state (rx_msg before the batch; updated to rx_msg
+ * after it).  dev_payload_rec[i] (optional) = the record whose bytes the payload member
+ * points into (MGENX_RX_PREV: before this batch).  Options:
+ *   MGENX_RX_NOLOG  no log file on this connection: no record is decoded (host address
+ *                   and gps_status read invalid; the caller unpacks with
+ *                   MGENX_OPT_CHECKSUM_FORCE to have the CRC verdicts when it needs them);
+ *   MGENX_RX_FORCE  checksum_force (the receiver's setting, for records without flags).
+ * Core columns are required (not the row layout). */
+#define MGENX_RX_NOLOG 0x1
+#define MGENX_RX_FORCE 0x2
+#define MGENX_RX_PREV  0xFFFFFFFFu
+typedef struct {
+    uint32_t tx_sec, tx_usec, lat_raw, lon_raw;
+    int32_t  alt;
+    uint32_t payload_off;
+    uint16_t dst_port, hdr_len, payload_len;
+    uint8_t  flags, dst_type, dst_len, payload_type, rsv[2];
+    uint8_t  dst_addr[16];
+} mgenx_rx_state;                /* 48 bytes; zero = a fresh MgenMsg's members */
+int mgenx_tcp_rx_persist(mgenx_ctx* ctx, const uint8_t* dev_slab, const uint64_t* dev_rec_off,
+                         const uint32_t* dev_rec_len, uint32_t n, const mgenx_cols* cols,
+                         mgenx_rx_state* dev_state, uint32_t* dev_payload_rec, uint32_t opts,
+                         void* stream);
+
 /* ---- stream framing (TCP / SINK record boundaries) ----
  * mgenx_stream_scan finds the record chain of a byte stream from offset 0 exactly as the
  * reference receivers frame it -- TCP: MgenTcpTransport::GetRxNumBytes / OnRecvMsg

@@ -17,7 +17,8 @@ from ._abi import (  # noqa: F401
     FLAG_LAST_BUFFER, OPT_CHECKSUM_FORCE, OPT_SKIP_CRC, OPT_TCP, PACK_CHECKSUM,
     PACK_RANDOM_FILL, SCAN_SINK, SCAN_TCP, ScanInfo, FLOW_COUNTERS_DTYPE, FLOW_REPORT_DTYPE,
     FLOW_STATE_BYTES, FLOW_STATE_DTYPE, REC_DTYPE, PACK_RAW, DEC_MSGLEN, DEC_BASE, DEC_DST,
-    DEC_HDRLEN, DEC_HOST, DEC_GPS, DEC_PTYPE, DEC_PLEN,
+    DEC_HDRLEN, DEC_HOST, DEC_GPS, DEC_PTYPE, DEC_PLEN, RX_NOLOG, RX_FORCE, RX_PREV,
+    RX_STATE_DTYPE, SCAN_HALO, SCAN_REUSE,
 )
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -29,7 +30,7 @@ EXPORTED_SYMBOLS = (
     "mgenx_abi_version", "mgenx_ctx_create", "mgenx_ctx_destroy", "mgenx_last_error",
     "mgenx_ctx_device", "mgenx_unpack_batch", "mgenx_pack_prepare", "mgenx_set_fill_time",
     "mgenx_pack_batch", "mgenx_pack_msgs", "mgenx_pack_tcp", "mgenx_crc32_update", "mgenx_crc32_batch",
-    "mgenx_stream_scan", "mgenx_stream_scan_exits", "mgenx_stream_scan_range", "mgenx_flow_init", "mgenx_flow_reduce", "mgenx_flow_export",
+    "mgenx_tcp_rx_persist", "mgenx_stream_scan", "mgenx_stream_scan_exits", "mgenx_stream_scan_range", "mgenx_flow_init", "mgenx_flow_reduce", "mgenx_flow_export",
     "mgenx_log_recv_text", "mgenx_log_recv_binary", "mgenx_comm_unique_id", "mgenx_comm_init",
     "mgenx_comm_destroy", "mgenx_allreduce_flows", "mgenx_allgather_u64",
     "mgenx_flow_table_create", "mgenx_flow_table_destroy", "mgenx_flow_lookup",
@@ -85,6 +86,7 @@ def load(diag: bool = False):
         L.mgenx_diag_stream_read.argtypes = [P, P, u64, P, i32, P]
         L.mgenx_diag_group_rw.argtypes = [P, P, u64, P, i32, P]
     L.mgenx_stream_scan.argtypes = [P, P, u64, i32, P, P, u64, ctypes.POINTER(ScanInfo), P]
+    L.mgenx_tcp_rx_persist.argtypes = [P, P, P, P, u32, P, P, P, u32, P]
     L.mgenx_stream_scan_exits.argtypes = [P, P, u64, i32, u64, u64, P, P, u32,
                                           ctypes.POINTER(u32), P]
     L.mgenx_stream_scan_range.argtypes = [P, P, u64, i32, u64, u64, i32, P, P, u64,
@@ -175,6 +177,24 @@ class Engine:
                                          _ptr(rec_len), fixed_len, n, ctypes.byref(cs), opts,
                                          _stream(self.device))
         self._check(rc, "mgenx_unpack_batch")
+        return cols
+
+    def rx_state_init(self):
+        """mgenx_rx_state of a fresh MgenMsg (GPS words 10800000 = 0 degrees), on the device."""
+        from ._abi import RX_STATE_DTYPE
+        st = np.zeros(1, RX_STATE_DTYPE)
+        st["lat_raw"] = st["lon_raw"] = 10800000
+        return self.torch.from_numpy(st.view(np.uint8).copy()).to(f"cuda:{self.device}")
+
+    def tcp_rx_persist(self, slab, rec_off, rec_len, n, cols, state, *, payload_rec=None,
+                       opts=0):
+        """The TCP receiver's persistent rx_msg view of n decoded records, in place
+        (mgenx_tcp_rx_persist); state: the 48-B mgenx_rx_state tensor (updated)."""
+        cs = self._cols_struct(cols)
+        rc = self.lib.mgenx_tcp_rx_persist(self.ctx, _ptr(slab), _ptr(rec_off), _ptr(rec_len), n,
+                                           ctypes.byref(cs), _ptr(state), _ptr(payload_rec), opts,
+                                           _stream(self.device))
+        self._check(rc, "mgenx_tcp_rx_persist")
         return cols
 
     # ------------------------------------------------------------ event log

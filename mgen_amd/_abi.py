@@ -93,6 +93,14 @@ def hex_payload(hexstr: str) -> bytes:
 # stream framing (mgenx_stream_scan)
 SCAN_TCP = 0
 SCAN_SINK = 1
+RX_NOLOG = 0x1        # MGENX_RX_NOLOG
+RX_FORCE = 0x2        # MGENX_RX_FORCE
+RX_PREV = 0xFFFFFFFF  # MGENX_RX_PREV
+RX_STATE_DTYPE = np.dtype([
+    ("tx_sec", "<u4"), ("tx_usec", "<u4"), ("lat_raw", "<u4"), ("lon_raw", "<u4"),
+    ("alt", "<i4"), ("payload_off", "<u4"), ("dst_port", "<u2"), ("hdr_len", "<u2"),
+    ("payload_len", "<u2"), ("flags", "u1"), ("dst_type", "u1"), ("dst_len", "u1"),
+    ("payload_type", "u1"), ("rsv", "u1", 2), ("dst_addr", "u1", 16)])   # mgenx_rx_state
 SCAN_HALO = 65536     # MGENX_SCAN_HALO: bytes past a shard a record may extend into
 SCAN_REUSE = 1        # MGENX_SCAN_REUSE
 

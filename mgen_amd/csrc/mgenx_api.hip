@@ -73,6 +73,8 @@ struct mgenx_ctx {
   void* tcp_ws = nullptr;         // TCP transmit workspace (mgenx_pack_tcp), grown on demand
   size_t tcp_ws_bytes = 0;
   uint64_t* tcp_host = nullptr;   // host-mapped words: total bytes, max fragments
+  void* rx_ws = nullptr;          // rx-persist workspace, grown on demand
+  size_t rx_ws_bytes = 0;
   uint64_t* tcp_host_dev = nullptr;
   int unpack_variant = 0;          // diagnostic kernel ablation (mgenx_set_tuning)
   int pack_variant = 0;
@@ -210,6 +212,7 @@ int mgenx_ctx_destroy(mgenx_ctx* c) {
   if (c->flow_ws) mgenx_flow_ws_free(c->flow_ws);
   if (c->log_ws) mgenx_log_ws_free(c->log_ws);
   if (c->tcp_ws) hipFree(c->tcp_ws);
+  if (c->rx_ws) hipFree(c->rx_ws);
   if (c->tcp_host) hipHostFree(c->tcp_host);
   for (void* p : ps)
     if (p) hipFree(p);
@@ -458,6 +461,34 @@ int mgenx_pack_tcp(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl, const uint32
       return set_err(ctx, e, "tcp tail");
   }
   return MGENX_OK;
+}
+
+int mgenx_tcp_rx_persist(mgenx_ctx* ctx, const uint8_t* dev_slab, const uint64_t* dev_rec_off,
+                         const uint32_t* dev_rec_len, uint32_t n, const mgenx_cols* cols,
+                         mgenx_rx_state* dev_state, uint32_t* dev_payload_rec, uint32_t opts,
+                         void* stream) {
+  if (!ctx || !cols || !dev_state || (opts & ~(uint32_t)(MGENX_RX_NOLOG | MGENX_RX_FORCE)))
+    return MGENX_EINVAL;
+  if (n == 0) return MGENX_OK;
+  const mgenx_cols& c = *cols;
+  if (!c.flow_id || !c.seq_num || !c.tx_sec || !c.tx_usec || !c.msg_len || !c.dst_port ||
+      !c.flags || !c.err || !c.dst_type || !c.dst_len || !c.dst_addr4 || !c.payload_len ||
+      !c.payload_type || !c.gps_status || !c.decoded || !dev_slab || !dev_rec_off || !dev_rec_len)
+    return MGENX_EINVAL;
+  hipSetDevice(ctx->device);
+  const size_t need = mgenx::rx_persist_ws_bytes(n);
+  hipError_t e;
+  if (ctx->rx_ws_bytes < need) {  // grows (allocates) only when the batch outgrows it
+    if (ctx->rx_ws) hipFree(ctx->rx_ws);
+    ctx->rx_ws = nullptr;
+    ctx->rx_ws_bytes = 0;
+    if ((e = hipMalloc(&ctx->rx_ws, need)) != hipSuccess) return set_err(ctx, e, "rx workspace");
+    ctx->rx_ws_bytes = need;
+  }
+  e = mgenx::launch_rx_persist(c, n, opts, static_cast<int32_t*>(ctx->rx_ws), dev_state, dev_slab,
+                               dev_rec_off, dev_rec_len, ctx->d_bytetab, dev_payload_rec,
+                               (hipStream_t)stream);
+  return e == hipSuccess ? MGENX_OK : set_err(ctx, e, "rx persist");
 }
 
 int mgenx_ctx_device(const mgenx_ctx* ctx) { return ctx ? ctx->device : -1; }

@@ -64,6 +64,12 @@ hipError_t launch_stream_read(const uint8_t* p, uint64_t bytes, uint32_t* out, i
 hipError_t launch_pack(const PackParams& p, int grid, hipStream_t stream);
 hipError_t launch_pack_prepare(const mgenx_flow_tmpl* tmpl, uint32_t n_tmpl, const uint8_t* pool,
                                const uint32_t* byte_tab, uint32_t* out, hipStream_t stream);
+// TCP receiver's persistent rx_msg (mgenx_rx.hip)
+hipError_t launch_rx_persist(const mgenx_cols& c, uint32_t n, uint32_t opts, int32_t* ws,
+                             mgenx_rx_state* state, const uint8_t* slab, const uint64_t* rec_off,
+                             const uint32_t* rec_len, const uint32_t* byte_tab,
+                             uint32_t* payload_rec, hipStream_t s);
+size_t rx_persist_ws_bytes(uint32_t n);
 // TCP transmit (mgenx_tcp.hip)
 hipError_t launch_tcp_plan(const mgenx_flow_tmpl* tmpl, const mgenx_pack_desc* desc,
                            const uint32_t* msg_total, uint32_t n, uint64_t* bytes,

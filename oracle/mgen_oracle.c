@@ -361,24 +361,32 @@ uint32_t or_tcp_tx(const or_msg* msg, uint8_t* out, int checksum_enable, int ran
 /* ------------------------------------------------------------------ */
 static const uint32_t GPS_RAW_ZERO = 10800000u;   /* (0.0 + 180) * 60000 */
 
-void or_unpack(const uint8_t* buf, uint32_t bufferLen, or_fields* f)
+/* MgenMsg::Unpack on a REUSED MgenMsg (the TCP receiver's rx_msg): only host_addr and
+ * gps_status are reset on entry (mgenMsg.cpp:318-319); every member is assigned stage by
+ * stage below and the unreached ones keep their values.  or_unpack runs it on a fresh
+ * MgenMsg (constructor defaults, mgenMsg.cpp:38-49). */
+uint32_t or_unpack_persist(const uint8_t* buf, uint32_t bufferLen, or_fields* f)
 {
-    memset(f, 0, sizeof(*f));
-    f->version = OR_VERSION;
-    f->lat_raw = f->lon_raw = GPS_RAW_ZERO;
+    uint32_t d = 0;   /* MGENX_DEC_* mask of the members assigned */
+    f->host_type = 0; f->host_len = 0; f->host_port = 0;
+    memset(f->host_addr, 0, sizeof(f->host_addr));
+    f->gps_status = 0;
+    f->ok = 0;
     uint32_t len = 0;
-    if (bufferLen < OR_MIN_SIZE) { f->err = OR_ERROR_LENGTH; return; }   /* :323-328 */
+    if (bufferLen < OR_MIN_SIZE) { f->err = OR_ERROR_LENGTH; return d; }   /* :323-328 */
     f->msg_len = get16(buf); len += 2;
     f->version = buf[len++];
-    if (f->version != OR_VERSION) { f->err = OR_ERROR_VERSION; return; } /* :336-343 */
+    d |= 0x01;
+    if (f->version != OR_VERSION) { f->err = OR_ERROR_VERSION; return d; } /* :336-343 */
     f->flags = buf[len++];
     f->flow_id = get32(buf + len); len += 4;
     f->seq_num = get32(buf + len); len += 4;
     f->tx_sec = get32(buf + len); len += 4;
     f->tx_usec = get32(buf + len); len += 4;
+    d |= 0x02;
     uint16_t dstPort = get16(buf + len); len += 2;
     uint8_t t = buf[len++];
-    if (t != OR_ADDR_IPV4 && t != OR_ADDR_IPV6) { f->err = OR_ERROR_DSTADDR; return; } /* :374-392 */
+    if (t != OR_ADDR_IPV4 && t != OR_ADDR_IPV6) { f->err = OR_ERROR_DSTADDR; return d; } /* :374-392 */
     uint32_t addrLen = buf[len++];
     /* :394-398 -- no bounds check in the reference; bytes past the record are
      * undefined there (stale receive buffer) and read as zero here. */
@@ -387,6 +395,7 @@ void or_unpack(const uint8_t* buf, uint32_t bufferLen, or_fields* f)
     for (uint32_t i = 0; i < addrLen && i < 16; i++)
         f->dst_addr[i] = (len + i < bufferLen) ? buf[len + i] : 0;
     f->dst_port = dstPort;
+    d |= 0x04;
     len += addrLen;
     /* host (:400-443) */
     if ((len + 4) <= bufferLen) {
@@ -400,13 +409,14 @@ void or_unpack(const uint8_t* buf, uint32_t bufferLen, or_fields* f)
                 f->host_len = (uint8_t)addrLen;
                 for (uint32_t i = 0; i < addrLen && i < 16; i++) f->host_addr[i] = buf[len + i];
                 f->host_port = hostPort;
+                d |= 0x10;
             }
             len += addrLen;
         } else {
-            f->hdr_len = (uint16_t)len; f->ok = 1; return;
+            f->hdr_len = (uint16_t)len; f->ok = 1; return d | 0x08;
         }
     } else {
-        f->hdr_len = (uint16_t)len; f->ok = 1; return;
+        f->hdr_len = (uint16_t)len; f->ok = 1; return d | 0x08;
     }
     /* GPS (:446-465) */
     if ((len + 13) <= bufferLen) {
@@ -414,20 +424,23 @@ void or_unpack(const uint8_t* buf, uint32_t bufferLen, or_fields* f)
         f->lon_raw = get32(buf + len); len += 4;
         f->alt = (int32_t)get32(buf + len); len += 4;
         f->gps_status = buf[len++];
+        d |= 0x20;
     } else {
-        f->hdr_len = (uint16_t)len; f->ok = 1; return;
+        f->hdr_len = (uint16_t)len; f->ok = 1; return d | 0x08;
     }
     /* payload_type (:467-475) */
     if ((len + 1) <= bufferLen) {
         f->payload_type = buf[len++];
+        d |= 0x40;
     } else {
-        f->hdr_len = (uint16_t)len; f->ok = 1; return;
+        f->hdr_len = (uint16_t)len; f->ok = 1; return d | 0x08;
     }
     /* payload_len + data (:477-497) */
     if ((len + 2) <= bufferLen) {
         f->payload_len = get16(buf + len);
         len += 2;
         f->hdr_len = (uint16_t)len;
+        d |= 0x80 | 0x08;
         if (f->payload_len != 0 && (len + f->payload_len) <= bufferLen) {
             f->payload_off = (len / 4) * 4;   /* alignedBuffer + len/4 (word floor) */
         } else {
@@ -435,6 +448,15 @@ void or_unpack(const uint8_t* buf, uint32_t bufferLen, or_fields* f)
         }
     }
     f->ok = 1;
+    return d;
+}
+
+void or_unpack(const uint8_t* buf, uint32_t bufferLen, or_fields* f)
+{
+    memset(f, 0, sizeof(*f));
+    f->version = OR_VERSION;
+    f->lat_raw = f->lon_raw = GPS_RAW_ZERO;
+    (void)or_unpack_persist(buf, bufferLen, f);
 }
 
 static int crc_ok(const uint8_t* rec, uint32_t len)
@@ -472,6 +494,35 @@ void or_tcp_recv(const uint8_t* rec, uint32_t L, int checksum_force, or_fields* 
             o->err = OR_ERROR_CHECKSUM;
             o->flags |= OR_FLAG_CHECKSUM_ERROR;
         }
+    }
+}
+
+/* The TCP receiver's persistent rx_msg over n consecutive records of one connection
+ * (mgenTransport.cpp:1082 rx_msg; ResetRxMsgState :1501-1513 between messages, framing
+ * sets msg_len :1714-1720; Unpack on min(len, 8192) bytes only while a log file is open
+ * :2016-2028; CalcRxChecksum :1516-1564 with the flags rx_msg holds).  st: rx_msg before
+ * the batch (updated); out[i]: rx_msg after record i; payload_rec[i]: the record whose
+ * Unpack last assigned the payload (0xFFFFFFFF = before the batch), carried in *pay_src. */
+void or_tcp_rx_persist(const uint8_t* stream, const uint64_t* offs, const uint32_t* lens,
+                       uint32_t n, int log_open, int checksum_force, or_fields* st,
+                       uint32_t* pay_src, or_fields* out, uint32_t* payload_rec)
+{
+    for (uint32_t i = 0; i < n; i++) {
+        const uint8_t* rec = stream + offs[i];
+        const uint32_t L = lens[i];
+        st->flow_id = 0; st->seq_num = 0; st->err = 0; st->ok = 0;   /* ResetRxMsgState */
+        st->msg_len = (uint16_t)L;                                    /* the framing's */
+        if (log_open) {
+            const uint32_t d = or_unpack_persist(rec, L < OR_TX_BUFFER_SIZE ? L : OR_TX_BUFFER_SIZE,
+                                                 st);
+            if (d & 0x80) *pay_src = i;
+        }
+        if ((checksum_force || (st->flags & OR_FLAG_CHECKSUM)) && L >= 4 && !crc_ok(rec, L)) {
+            st->err = OR_ERROR_CHECKSUM;
+            st->flags |= OR_FLAG_CHECKSUM_ERROR;
+        }
+        out[i] = *st;
+        if (payload_rec) payload_rec[i] = *pay_src;
     }
 }
 

@@ -116,6 +116,10 @@ uint32_t or_tcp_tx(const or_msg* msg, uint8_t* out, int checksum_enable, int ran
 
 /* ---- Unpack (mgenMsg.cpp:315-500) ---- */
 void     or_unpack(const uint8_t* buf, uint32_t bufferLen, or_fields* f);
+uint32_t or_unpack_persist(const uint8_t* buf, uint32_t bufferLen, or_fields* f);
+void     or_tcp_rx_persist(const uint8_t* stream, const uint64_t* offs, const uint32_t* lens,
+                           uint32_t n, int log_open, int checksum_force, or_fields* st,
+                           uint32_t* pay_src, or_fields* out, uint32_t* payload_rec);
 
 /* UDP receive (mgenTransport.cpp:958-975) / SINK HandleMgenMessage (2092-2112):
  * Unpack, then CRC over len-4 when forced or CHECKSUM is set. */

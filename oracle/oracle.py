@@ -111,6 +111,9 @@ def lib():
         L.or_tcp_tx.argtypes = [ctypes.POINTER(Msg), P, i32, i32, u32]
         L.or_tcp_tx.restype = u32
         L.or_unpack.argtypes = [P, u32, P]
+        L.or_unpack_persist.argtypes = [P, u32, P]
+        L.or_unpack_persist.restype = u32
+        L.or_tcp_rx_persist.argtypes = [P, P, P, u32, i32, i32, P, ctypes.POINTER(u32), P, P]
         L.or_udp_recv.argtypes = [P, u32, i32, P]
         L.or_tcp_recv.argtypes = [P, u32, i32, P]
         L.or_tcp_scan.argtypes = [P, u64, i32, P, P, P, u32, ctypes.POINTER(u64),
@@ -263,6 +266,30 @@ def _scan(fn, stream, force, extra_status):
     n = fn(_ptr(buf), len(stream), int(force), _ptr(offs), _ptr(lens), _ptr(f), cap,
            ctypes.byref(consumed))
     return offs[:n], lens[:n], f[:n], consumed.value
+
+
+def fresh_fields():
+    """or_fields of a fresh MgenMsg (constructor defaults, mgenMsg.cpp:38-49)."""
+    f = np.zeros(1, FIELDS_DTYPE)
+    f["version"] = 2
+    f["lat_raw"] = f["lon_raw"] = 10800000
+    return f
+
+
+def tcp_rx_persist(stream, offs, lens, log_open=True, force=False, state=None, pay_src=None):
+    """The TCP receiver's persistent rx_msg over consecutive records (or_tcp_rx_persist):
+    returns (fields per record, payload_rec per record, state after, pay_src after)."""
+    stream = np.ascontiguousarray(stream, np.uint8)
+    offs = np.ascontiguousarray(offs, np.uint64)
+    lens = np.ascontiguousarray(lens, np.uint32)
+    n = len(offs)
+    st = fresh_fields() if state is None else np.array(state, FIELDS_DTYPE).reshape(1).copy()
+    ps = ctypes.c_uint32(0xFFFFFFFF if pay_src is None else pay_src)
+    out = np.zeros(n, FIELDS_DTYPE)
+    prec = np.zeros(n, np.uint32)
+    lib().or_tcp_rx_persist(_ptr(stream), _ptr(offs), _ptr(lens), n, int(log_open), int(force),
+                            _ptr(st), ctypes.byref(ps), _ptr(out), _ptr(prec))
+    return out, prec, st, ps.value
 
 
 def tcp_scan(stream: bytes, force=False):
