@@ -334,6 +334,14 @@ int mgenx_stream_scan_range(mgenx_ctx* ctx, const uint8_t* dev_stream, uint64_t 
                             uint32_t* dev_rec_len, uint64_t cap, mgenx_scan_info* info,
                             void* stream);
 
+/* A socket address as recvfrom reports it (ProtoAddress type / length / port / bytes). */
+typedef struct {
+    uint8_t  type;      /* MgenMsg::AddressType: 1 IPv4, 2 IPv6 */
+    uint8_t  len;       /* address length (4 / 16) */
+    uint16_t port;
+    uint8_t  addr[16];  /* network byte order */
+} mgenx_addr;           /* 20 bytes */
+
 /* ---- per-flow receive analytics (MgenAnalytic::Update) ----
  * Restates MgenAnalytic::Init/Update (src/common/mgenAnalytic.cpp:28-258) as called by
  * Mgen::UpdateRecvAnalytics (src/common/mgen.cpp:1027-1070): per flow, an order-dependent
@@ -365,6 +373,73 @@ typedef struct mgenx_flow_report {  /* one closed window (MgenAnalytic::Report) 
   int64_t  rx_sec, rx_usec;         /* receive time of the message that closed it */
 } mgenx_flow_report;
 
+/* ---- MGEN_DATA items: MgenAnalytic::Report and MgenFlowCommand ----
+ * Wire format include/mgenAnalytic.h:14-57 (ProtoPkt fields network order); quantizers
+ * mgenAnalytic.cpp:568-642 -- the device quantizes through tables the context builds with
+ * the host's libm (log, log10, pow), so results equal the reference's host arithmetic.
+ *
+ * mgenx_report_build: the report_msg bytes MgenAnalytic keeps (Init :28-71, the window
+ * close :245-253, GetReport :296-310) for every kept report of mgenx_flow_reduce:
+ * slot f * per_flow + j (j < min(report_count[f], per_flow)) gets 52 bytes (dev_items) and
+ * its length (dev_item_len: 24 / 28 IPv4, 48 / 52 IPv6, per the flow-id flag).  Keys: the
+ * analytic's src / dst / flow id / protocol.  dev_sign[f] carries FLAG_LATENCY_SIGN, which
+ * SetLatencyAve sets and nothing clears (in/out).  dev_offset (optional, per slot): the
+ * seconds GetReport's window offset measures (the send time minus the window end; the
+ * analytics caller itself reports 0). */
+#define MGENX_REPORT_MAX        52
+#define MGENX_PAYLOAD_MGEN_DATA 1    /* MgenMsg::MGEN_DATA payload type (mgenMsg.h:102) */
+#define MGENX_MAX_FLOW          40   /* MgenEvent::FlowStatus::MAX_FLOW (mgenEvent.h:194) */
+typedef struct {
+    mgenx_addr src, dst;
+    uint32_t flow_id;
+    uint8_t  protocol;           /* Protocol: 1 UDP, 2 TCP, 3 SINK */
+    uint8_t  rsv[3];
+} mgenx_report_key;              /* 48 bytes */
+int mgenx_report_build(mgenx_ctx* ctx, const mgenx_flow_report* dev_reports, uint32_t n_flows,
+                       uint32_t per_flow, const uint32_t* dev_report_count,
+                       const mgenx_report_key* dev_keys, uint8_t* dev_sign,
+                       const double* dev_offset, uint8_t* dev_items, uint8_t* dev_item_len,
+                       void* stream);
+/* REPORT log lines of the kept reports, as Mgen::UpdateRecvAnalytics logs them at each
+ * window close (MgenAnalytic::Log, mgenAnalytic.cpp:260-295: the report_msg's key fields,
+ * the analytic's unquantized values, timestamp = the closing message's rx time), in slot
+ * order (flow-major; each flow's lines in time order; empty slots give no line).
+ * Two passes like mgenx_log_recv_text: dev_line_off[n_flows * per_flow + 1]. */
+int mgenx_log_report_text(mgenx_ctx* ctx, const uint8_t* dev_items,
+                          const mgenx_flow_report* dev_reports, uint32_t n_flows,
+                          uint32_t per_flow, const uint32_t* dev_report_count, uint32_t opts,
+                          char* dev_text, uint64_t text_cap, uint64_t* dev_line_off,
+                          void* stream);
+/* MgenTransport::ProcessRecvMessage (mgenTransport.cpp:2132-2191) over the MGEN_DATA
+ * payloads of n decoded records (err == 0, payload_type == MGEN_DATA; columns err,
+ * payload_type, payload_len, payload_off required):
+ *   dev_status[i]   0 walked to the end, 1 invalid MGEN_DATA payload (a flow command
+ *                   longer than the rest), 2 invalid REPORT, 3 an item of length 0 (the
+ *                   reference loops forever on it; the walk stops), 0xFF not MGEN_DATA;
+ *   dev_needs_host[i]  1 when the payload carries flow commands or (with a controller)
+ *                   reports: the host's control plane acts on them (Mgen::ProcessFlowCommand,
+ *                   MgenController::OnRecvReport);
+ *   dev_cmds        pairs (record, flow_id << 2 | status) for every flow whose status is
+ *                   not FLOW_UNCHANGED (MgenFlowCommand::GetStatus, flows 1..MAX_FLOW);
+ *   dev_reps        pairs (record, slab offset of the report item) (MGENX_DATA_CONTROLLER:
+ *                   type bytes > 0x0f are reports, else skipped as generic items);
+ *   dev_totals[2]   the number of commands and reports (only the first cap are written).
+ * Bytes past a payload read as 0. */
+#define MGENX_DATA_CONTROLLER 0x1
+int mgenx_data_walk(mgenx_ctx* ctx, const uint8_t* dev_slab, const uint64_t* dev_rec_off,
+                    uint64_t stride, const mgenx_cols* cols, uint32_t n, uint32_t opts,
+                    uint8_t* dev_status, uint8_t* dev_needs_host, uint32_t* dev_cmds,
+                    uint32_t cmd_cap, uint64_t* dev_reps, uint32_t rep_cap,
+                    uint32_t* dev_totals, void* stream);
+/* REPORT lines of received reports (MgenAnalytic::Report::Log, mgenAnalytic.cpp:747-786):
+ * dev_reps = mgenx_data_walk's pairs; per record the source (the reporter) and rx time.
+ * "sent>" prints the rx time again, as the reference does. */
+int mgenx_log_report_recv_text(mgenx_ctx* ctx, const uint8_t* dev_slab, const uint64_t* dev_reps,
+                               uint32_t n_reps, const mgenx_addr* dev_src,
+                               const uint32_t* dev_rx_sec, const uint32_t* dev_rx_usec,
+                               uint32_t opts, char* dev_text, uint64_t text_cap,
+                               uint64_t* dev_line_off, void* stream);
+
 /* Packed per-flow counters for the multi-GPU merge (one RCCL all-reduce(sum) of
  * n_flows x 64 B: flows are owned by one rank, the others contribute zeros). */
 typedef struct mgenx_flow_counters {
@@ -389,13 +464,6 @@ int mgenx_flow_reduce(mgenx_ctx* ctx, const uint32_t* dev_flow_idx, const uint32
 int mgenx_flow_export(mgenx_ctx* ctx, const mgenx_flow_state* dev_flows, uint32_t n_flows,
                       mgenx_flow_counters* dev_out, void* stream);
 
-/* A socket address as recvfrom reports it (ProtoAddress type / length / port / bytes). */
-typedef struct {
-    uint8_t  type;      /* MgenMsg::AddressType: 1 IPv4, 2 IPv6 */
-    uint8_t  len;       /* address length (4 / 16) */
-    uint16_t port;
-    uint8_t  addr[16];  /* network byte order */
-} mgenx_addr;           /* 20 bytes */
 
 /* ---- MgenAnalyticTable::FindFlow for batches (mgenAnalytic.cpp:312-328) ----
  * A device hash table from the reference's flow key -- dst addr | dst port | src addr |

@@ -18,7 +18,7 @@ from ._abi import (  # noqa: F401
     PACK_RANDOM_FILL, SCAN_SINK, SCAN_TCP, ScanInfo, FLOW_COUNTERS_DTYPE, FLOW_REPORT_DTYPE,
     FLOW_STATE_BYTES, FLOW_STATE_DTYPE, REC_DTYPE, PACK_RAW, DEC_MSGLEN, DEC_BASE, DEC_DST,
     DEC_HDRLEN, DEC_HOST, DEC_GPS, DEC_PTYPE, DEC_PLEN, RX_NOLOG, RX_FORCE, RX_PREV,
-    RX_STATE_DTYPE, SCAN_HALO, SCAN_REUSE,
+    RX_STATE_DTYPE, SCAN_HALO, SCAN_REUSE, ADDR_DTYPE, REPORT_KEY_DTYPE, DATA_CONTROLLER,
 )
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -30,7 +30,8 @@ EXPORTED_SYMBOLS = (
     "mgenx_abi_version", "mgenx_ctx_create", "mgenx_ctx_destroy", "mgenx_last_error",
     "mgenx_ctx_device", "mgenx_unpack_batch", "mgenx_pack_prepare", "mgenx_set_fill_time",
     "mgenx_pack_batch", "mgenx_pack_msgs", "mgenx_pack_tcp", "mgenx_crc32_update", "mgenx_crc32_batch",
-    "mgenx_tcp_rx_persist", "mgenx_stream_scan", "mgenx_stream_scan_exits", "mgenx_stream_scan_range", "mgenx_flow_init", "mgenx_flow_reduce", "mgenx_flow_export",
+    "mgenx_tcp_rx_persist", "mgenx_report_build", "mgenx_log_report_text", "mgenx_data_walk",
+    "mgenx_log_report_recv_text", "mgenx_stream_scan", "mgenx_stream_scan_exits", "mgenx_stream_scan_range", "mgenx_flow_init", "mgenx_flow_reduce", "mgenx_flow_export",
     "mgenx_log_recv_text", "mgenx_log_recv_binary", "mgenx_comm_unique_id", "mgenx_comm_init",
     "mgenx_comm_destroy", "mgenx_allreduce_flows", "mgenx_allgather_u64",
     "mgenx_flow_table_create", "mgenx_flow_table_destroy", "mgenx_flow_lookup",
@@ -87,6 +88,10 @@ def load(diag: bool = False):
         L.mgenx_diag_group_rw.argtypes = [P, P, u64, P, i32, P]
     L.mgenx_stream_scan.argtypes = [P, P, u64, i32, P, P, u64, ctypes.POINTER(ScanInfo), P]
     L.mgenx_tcp_rx_persist.argtypes = [P, P, P, P, u32, P, P, P, u32, P]
+    L.mgenx_report_build.argtypes = [P, P, u32, u32, P, P, P, P, P, P, P]
+    L.mgenx_log_report_text.argtypes = [P, P, P, u32, u32, P, u32, P, u64, P, P]
+    L.mgenx_data_walk.argtypes = [P, P, P, u64, P, u32, u32, P, P, P, u32, P, u32, P, P]
+    L.mgenx_log_report_recv_text.argtypes = [P, P, P, u32, P, P, P, u32, P, u64, P, P]
     L.mgenx_stream_scan_exits.argtypes = [P, P, u64, i32, u64, u64, P, P, u32,
                                           ctypes.POINTER(u32), P]
     L.mgenx_stream_scan_range.argtypes = [P, P, u64, i32, u64, u64, i32, P, P, u64,
@@ -412,6 +417,70 @@ class Engine:
         self._check(self.lib.mgenx_flow_export(self.ctx, _ptr(flows), n_flows, _ptr(out),
                                                _stream(self.device)), "mgenx_flow_export")
         return out
+
+    # ------------------------------------------------------------ MGEN_DATA items
+    def report_build(self, reports, n_flows, per_flow, report_count, keys, sign, offset=None):
+        """MgenAnalytic report_msg bytes for the kept reports (mgenx_report_build): returns
+        (items uint8 [slots*52], lengths uint8 [slots]); sign (uint8 [n_flows]) updated."""
+        torch = self.torch
+        slots = n_flows * per_flow
+        dev = report_count.device
+        items = torch.zeros(max(slots, 1) * 52, dtype=torch.uint8, device=dev)
+        ilen = torch.zeros(max(slots, 1), dtype=torch.uint8, device=dev)
+        self._check(self.lib.mgenx_report_build(self.ctx, _ptr(reports), n_flows, per_flow,
+                                                _ptr(report_count), _ptr(keys), _ptr(sign),
+                                                _ptr(offset), _ptr(items), _ptr(ilen),
+                                                _stream(self.device)), "mgenx_report_build")
+        return items, ilen
+
+    def _two_pass_text(self, call, n, dev, cap):
+        torch = self.torch
+        line_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        for _ in range(2):
+            text = torch.empty(max(cap, 1), dtype=torch.uint8, device=dev)
+            self._check(call(text, cap, line_off), "report text")
+            total = int(line_off[-1].cpu())
+            if total <= cap:
+                return text[:total], line_off
+            cap = total
+        raise MgenxError("report text did not fit")
+
+    def log_report_text(self, items, reports, n_flows, per_flow, report_count, opts=0,
+                        text_cap=None):
+        n = n_flows * per_flow
+        cap = text_cap if text_cap is not None else max(1, n) * 220
+        return self._two_pass_text(
+            lambda t, c, lo: self.lib.mgenx_log_report_text(
+                self.ctx, _ptr(items), _ptr(reports), n_flows, per_flow, _ptr(report_count),
+                opts, _ptr(t), c, _ptr(lo), _stream(self.device)), n, items.device, cap)
+
+    def data_walk(self, slab, n, cols, *, rec_off=None, stride=0, opts=0, cmd_cap=4096,
+                  rep_cap=4096):
+        """ProcessRecvMessage over MGEN_DATA payloads (mgenx_data_walk): returns (status,
+        needs_host, cmds [cap x 2 u32], reps [cap x 2 u64], totals [2])."""
+        torch = self.torch
+        dev = slab.device
+        status = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+        nh = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+        cmds = torch.zeros(max(cmd_cap, 1) * 2, dtype=torch.int32, device=dev)
+        reps = torch.zeros(max(rep_cap, 1) * 2, dtype=torch.int64, device=dev)
+        totals = torch.zeros(2, dtype=torch.int32, device=dev)
+        cs = self._cols_struct(cols)
+        self._check(self.lib.mgenx_data_walk(self.ctx, _ptr(slab), _ptr(rec_off), stride,
+                                             ctypes.byref(cs), n, opts, _ptr(status), _ptr(nh),
+                                             _ptr(cmds), cmd_cap, _ptr(reps), rep_cap,
+                                             _ptr(totals), _stream(self.device)),
+                    "mgenx_data_walk")
+        return status[:n], nh[:n], cmds, reps, totals
+
+    def log_report_recv_text(self, slab, reps, n_reps, src, rx_sec, rx_usec, opts=0,
+                             text_cap=None):
+        cap = text_cap if text_cap is not None else max(1, n_reps) * 300
+        return self._two_pass_text(
+            lambda t, c, lo: self.lib.mgenx_log_report_recv_text(
+                self.ctx, _ptr(slab), _ptr(reps), n_reps, _ptr(src), _ptr(rx_sec),
+                _ptr(rx_usec), opts, _ptr(t), c, _ptr(lo), _stream(self.device)),
+            n_reps, slab.device, cap)
 
     # ------------------------------------------------------------ multi-GPU (RCCL)
     def comm_unique_id(self) -> bytes:

@@ -93,6 +93,11 @@ def hex_payload(hexstr: str) -> bytes:
 # stream framing (mgenx_stream_scan)
 SCAN_TCP = 0
 SCAN_SINK = 1
+ADDR_DTYPE = np.dtype([("type", "u1"), ("len", "u1"), ("port", "<u2"), ("addr", "u1", 16)])
+REPORT_KEY_DTYPE = np.dtype([("src", ADDR_DTYPE), ("dst", ADDR_DTYPE), ("flow_id", "<u4"),
+                             ("protocol", "u1"), ("rsv", "u1", 3)])   # mgenx_report_key
+REPORT_MAX = 52
+DATA_CONTROLLER = 0x1
 RX_NOLOG = 0x1        # MGENX_RX_NOLOG
 RX_FORCE = 0x2        # MGENX_RX_FORCE
 RX_PREV = 0xFFFFFFFF  # MGENX_RX_PREV

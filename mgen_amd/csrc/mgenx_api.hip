@@ -6,6 +6,7 @@
 // mgenx_pack_prepare (table setup), so batch calls can be captured in a hipGraph.
 #include <hipcub/hipcub.hpp>
 
+#include <math.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -32,6 +33,23 @@ extern "C" int mgenx_scan_range_run(void* ws, const uint8_t* s, uint64_t nbytes,
                                     hipStream_t stream, char* err, size_t errn);
 
 extern "C" void* mgenx_log_ws_new();
+extern "C" int mgenx_report_build_run(const mgenx_flow_report* reps, uint32_t n_flows,
+                                      uint32_t per_flow, const uint32_t* count,
+                                      const mgenx_report_key* keys, uint8_t* sign,
+                                      const double* offset, const double* rq, uint8_t* items,
+                                      uint8_t* item_len, hipStream_t stream);
+extern "C" int mgenx_report_lines(void* ws, const uint8_t* items, const mgenx_flow_report* reps,
+                                  const uint32_t* count, uint32_t per_flow, const uint64_t* pairs,
+                                  const uint8_t* slab, const mgenx_addr* reporter,
+                                  const uint32_t* rx_sec, const uint32_t* rx_usec, uint32_t n,
+                                  uint32_t opts, const double* rq, char* text, uint64_t cap,
+                                  uint64_t* line_off, hipStream_t stream, char* err, size_t errn);
+extern "C" int mgenx_data_walk_exec(void* ws, const uint8_t* slab, const uint64_t* rec_off,
+                                    uint64_t stride, const mgenx_cols* cols, uint32_t n,
+                                    uint32_t opts, const double* rq, uint8_t* status,
+                                    uint8_t* needs_host, uint32_t* cmds, uint32_t cmd_cap,
+                                    uint64_t* reps, uint32_t rep_cap, uint32_t* totals,
+                                    hipStream_t stream, char* err, size_t errn);
 extern "C" void mgenx_log_ws_free(void* p);
 extern "C" int mgenx_log_recv_run(void* ws, bool binary, const uint8_t* slab,
                                   uint64_t slab_bytes, const uint64_t* rec_off,
@@ -67,6 +85,7 @@ struct mgenx_ctx {
   uint8_t* d_rtab = nullptr;      // 16 + 65536 + 32 bytes
   uint32_t* d_rcrc = nullptr;     // [65536]
   uint8_t* d_sink = nullptr;      // 1 KiB: column stores of lanes past the batch end
+  double* d_rq = nullptr;         // report quantizer tables (mgenx::kRq*), built with host libm
   void* scan_ws = nullptr;        // stream-scan workspace (mgenx_scan.hip), grown on demand
   void* flow_ws = nullptr;        // flow-reduce workspace (mgenx_analytic.hip), grown on demand
   void* log_ws = nullptr;         // log-format workspace (mgenx_log.hip), grown on demand
@@ -99,6 +118,50 @@ void byte_table(uint32_t t[256]) {
 uint32_t shift_n(const uint32_t t[256], uint32_t s, uint32_t n) {
   for (uint32_t i = 0; i < n; i++) s = t[s & 0xffu] ^ (s >> 8);
   return s;
+}
+
+// MgenAnalytic::Report quantizers (mgenAnalytic.cpp:568-642) as tables built with this
+// host's libm -- the reference's own log / log10 / pow: the device quantizes by threshold
+// search and unquantizes by lookup, so it matches the host bit for bit.
+double rq_scale() { return 1.0 / (pow(1.1, 254) - 1.1); }
+uint8_t host_q_time(double value) {
+  const double S = 1.1, MN = 1.0e-06, MX = 600.0;
+  if (value > S * MX) return 0xff;
+  if (value < MN / 2.0) return 0;
+  if (value < MN) return 1;
+  return (uint8_t)((log(S + (value - MN) / (rq_scale() * (MX - MN))) / log(S)) + 0.5);
+}
+// smallest positive double v in [lo, hi] with pred(v) (pred monotone, false -> true)
+template <typename P>
+double first_true(double lo, double hi, P pred) {
+  uint64_t a, b;
+  memcpy(&a, &lo, 8);
+  memcpy(&b, &hi, 8);
+  while (a < b) {
+    const uint64_t m = a + (b - a) / 2;
+    double v;
+    memcpy(&v, &m, 8);
+    if (pred(v)) b = m; else a = m + 1;
+  }
+  double v;
+  memcpy(&v, &a, 8);
+  return v;
+}
+void build_report_tables(double* rq) {
+  const double S = 1.1, MN = 1.0e-06, MX = 600.0;
+  for (int q = 0; q < 256; q++)
+    rq[mgenx::kRqUnqTime + q] = q == 0 ? 0.0 : (MX - MN) * (pow(S, q) - S) * rq_scale() + MN;
+  // time: T[k] = first v >= MIN with q(v) >= k, k = 2..255 (q(MIN) = 1)
+  for (int k = 0; k < 256; k++) rq[mgenx::kRqThrTime + k] = HUGE_VAL;
+  for (int k = 2; k < 256; k++)
+    rq[mgenx::kRqThrTime + k] = first_true(MN, S * MX, [&](double v) { return host_q_time(v) >= k; });
+  // rate exponent: (int)log10(r) >= e, e = kRqLog10Lo .. kRqLog10Lo + kRqLog10N - 1
+  for (int j = 0; j < mgenx::kRqLog10N; j++) {
+    const int e = mgenx::kRqLog10Lo + j;
+    rq[mgenx::kRqThrLog10 + j] =
+        first_true(1e-300, 1e300, [&](double v) { return (int32_t)log10(v) >= e; });
+  }
+  for (int e = 0; e < mgenx::kRqP10N; e++) rq[mgenx::kRqP10 + e] = pow(10.0, (double)e);
 }
 
 void op_table(const uint32_t t[256], uint32_t n, uint32_t* out /*1024*/) {
@@ -172,6 +235,8 @@ int mgenx_ctx_create(int device, mgenx_ctx** out) {
   }
   for (uint32_t L = 4; L < kN; L++) expect[L] = shift_n(t, ia[L - 4] ^ 0xFFFFFFFFu, 4);
   c->h_expect = expect;
+  std::vector<double> rq(mgenx::kRqDoubles);
+  build_report_tables(rq.data());
 
   struct {
     void** p;
@@ -186,6 +251,7 @@ int mgenx_ctx_create(int device, mgenx_ctx** out) {
       {(void**)&c->d_rtab, 16 + kN + 32, nullptr},
       {(void**)&c->d_rcrc, kN * 4, nullptr},
       {(void**)&c->d_sink, 1024, nullptr},
+      {(void**)&c->d_rq, rq.size() * 8, rq.data()},
   };
   for (auto& a : allocs) {
     if (hipMalloc(a.p, a.bytes) != hipSuccess) {
@@ -207,7 +273,7 @@ int mgenx_ctx_destroy(mgenx_ctx* c) {
   if (!c) return MGENX_EINVAL;
   hipSetDevice(c->device);
   void* ps[] = {c->d_tabs, c->d_expect, c->d_xpow, c->d_ia, c->d_bytetab, c->d_rtab, c->d_rcrc,
-                c->d_sink};
+                c->d_sink, c->d_rq};
   if (c->scan_ws) mgenx_scan_ws_free(c->scan_ws);
   if (c->flow_ws) mgenx_flow_ws_free(c->flow_ws);
   if (c->log_ws) mgenx_log_ws_free(c->log_ws);
@@ -643,6 +709,72 @@ int mgenx_log_recv_binary(mgenx_ctx* ctx, const uint8_t* dev_slab, uint64_t slab
   return log_recv(ctx, true, dev_slab, slab_bytes, dev_rec_off, stride, cols, dev_src,
                   dev_rx_sec, dev_rx_usec, nullptr, n, protocol, 0, (char*)dev_out, out_cap,
                   dev_rec_pos, stream);
+}
+
+int mgenx_report_build(mgenx_ctx* ctx, const mgenx_flow_report* dev_reports, uint32_t n_flows,
+                       uint32_t per_flow, const uint32_t* dev_report_count,
+                       const mgenx_report_key* dev_keys, uint8_t* dev_sign,
+                       const double* dev_offset, uint8_t* dev_items, uint8_t* dev_item_len,
+                       void* stream) {
+  if (!ctx || (n_flows && per_flow && (!dev_reports || !dev_report_count || !dev_keys ||
+                                       !dev_sign || !dev_items || !dev_item_len)))
+    return MGENX_EINVAL;
+  hipSetDevice(ctx->device);
+  return mgenx_report_build_run(dev_reports, n_flows, per_flow, dev_report_count, dev_keys,
+                                dev_sign, dev_offset, ctx->d_rq, dev_items, dev_item_len,
+                                (hipStream_t)stream);
+}
+
+int mgenx_log_report_text(mgenx_ctx* ctx, const uint8_t* dev_items,
+                          const mgenx_flow_report* dev_reports, uint32_t n_flows,
+                          uint32_t per_flow, const uint32_t* dev_report_count, uint32_t opts,
+                          char* dev_text, uint64_t text_cap, uint64_t* dev_line_off,
+                          void* stream) {
+  const uint64_t n = (uint64_t)n_flows * per_flow;
+  if (!ctx || n > 0xFFFFFFFFull || !dev_line_off ||
+      (n && (!dev_items || !dev_reports || !dev_report_count)) || (text_cap && !dev_text))
+    return MGENX_EINVAL;
+  hipSetDevice(ctx->device);
+  if (!ctx->log_ws) ctx->log_ws = mgenx_log_ws_new();
+  return mgenx_report_lines(ctx->log_ws, dev_items, dev_reports, dev_report_count, per_flow,
+                            nullptr, nullptr, nullptr, nullptr, nullptr, (uint32_t)n, opts,
+                            ctx->d_rq, dev_text, text_cap, dev_line_off, (hipStream_t)stream,
+                            ctx->err, sizeof(ctx->err));
+}
+
+int mgenx_data_walk(mgenx_ctx* ctx, const uint8_t* dev_slab, const uint64_t* dev_rec_off,
+                    uint64_t stride, const mgenx_cols* cols, uint32_t n, uint32_t opts,
+                    uint8_t* dev_status, uint8_t* dev_needs_host, uint32_t* dev_cmds,
+                    uint32_t cmd_cap, uint64_t* dev_reps, uint32_t rep_cap,
+                    uint32_t* dev_totals, void* stream) {
+  if (!ctx || !cols || (opts & ~(uint32_t)MGENX_DATA_CONTROLLER)) return MGENX_EINVAL;
+  if (n == 0) return MGENX_OK;
+  if (!dev_slab || (!dev_rec_off && stride == 0 && n > 1) || !cols->err || !cols->payload_type ||
+      !cols->payload_len || !cols->payload_off || !dev_status || !dev_needs_host ||
+      (cmd_cap && !dev_cmds) || (rep_cap && !dev_reps))
+    return MGENX_EINVAL;
+  hipSetDevice(ctx->device);
+  if (!ctx->log_ws) ctx->log_ws = mgenx_log_ws_new();
+  return mgenx_data_walk_exec(ctx->log_ws, dev_slab, dev_rec_off, stride, cols, n, opts,
+                              ctx->d_rq, dev_status, dev_needs_host, dev_cmds, cmd_cap, dev_reps,
+                              rep_cap, dev_totals, (hipStream_t)stream, ctx->err,
+                              sizeof(ctx->err));
+}
+
+int mgenx_log_report_recv_text(mgenx_ctx* ctx, const uint8_t* dev_slab, const uint64_t* dev_reps,
+                               uint32_t n_reps, const mgenx_addr* dev_src,
+                               const uint32_t* dev_rx_sec, const uint32_t* dev_rx_usec,
+                               uint32_t opts, char* dev_text, uint64_t text_cap,
+                               uint64_t* dev_line_off, void* stream) {
+  if (!ctx || !dev_line_off || (n_reps && (!dev_slab || !dev_reps || !dev_src || !dev_rx_sec ||
+                                          !dev_rx_usec)) || (text_cap && !dev_text))
+    return MGENX_EINVAL;
+  hipSetDevice(ctx->device);
+  if (!ctx->log_ws) ctx->log_ws = mgenx_log_ws_new();
+  return mgenx_report_lines(ctx->log_ws, nullptr, nullptr, nullptr, 1, dev_reps, dev_slab,
+                            dev_src, dev_rx_sec, dev_rx_usec, n_reps, opts, ctx->d_rq, dev_text,
+                            text_cap, dev_line_off, (hipStream_t)stream, ctx->err,
+                            sizeof(ctx->err));
 }
 
 int mgenx_flow_export(mgenx_ctx* ctx, const mgenx_flow_state* dev_flows, uint32_t n_flows,

@@ -64,6 +64,16 @@ hipError_t launch_stream_read(const uint8_t* p, uint64_t bytes, uint32_t* out, i
 hipError_t launch_pack(const PackParams& p, int grid, hipStream_t stream);
 hipError_t launch_pack_prepare(const mgenx_flow_tmpl* tmpl, uint32_t n_tmpl, const uint8_t* pool,
                                const uint32_t* byte_tab, uint32_t* out, hipStream_t stream);
+// MgenAnalytic::Report quantizer tables (built on the host at context creation)
+constexpr int kRqUnqTime = 0;          // [256] UnquantizeTimeValue(q)
+constexpr int kRqThrTime = 256;        // [256] first value with QuantizeTimeValue >= k (k >= 2)
+constexpr int kRqLog10Lo = -40;        // (int)log10 thresholds for e = -40 .. 24
+constexpr int kRqLog10N = 65;
+constexpr int kRqThrLog10 = 512;
+constexpr int kRqP10 = 512 + 65;       // [309] pow(10, e)
+constexpr int kRqP10N = 309;
+constexpr int kRqDoubles = 512 + 65 + 309;
+
 // TCP receiver's persistent rx_msg (mgenx_rx.hip)
 hipError_t launch_rx_persist(const mgenx_cols& c, uint32_t n, uint32_t opts, int32_t* ws,
                              mgenx_rx_state* state, const uint8_t* slab, const uint64_t* rec_off,

@@ -17,6 +17,8 @@
 
 #include <stdio.h>
 
+#include <mutex>
+
 #include "mgenx_kernels.hpp"
 
 namespace mgenx {
@@ -413,17 +415,39 @@ __global__ void log_tail_kernel(uint64_t* lens, uint32_t n) {
 
 using namespace mgenx;
 
+// One scratch area per stream (line lengths + scan temporaries), so log calls on one context
+// but different streams never share a buffer; an area grows (hipMalloc) only when a batch
+// outgrows it.
 struct mgenx_log_ws {
   void* mem = nullptr;
   size_t bytes = 0;
+  hipStream_t stream = nullptr;
+  mgenx_log_ws* next = nullptr;
 };
 
 extern "C" void* mgenx_log_ws_new() { return new mgenx_log_ws(); }
 extern "C" void mgenx_log_ws_free(void* p) {
   mgenx_log_ws* w = static_cast<mgenx_log_ws*>(p);
-  if (!w) return;
-  if (w->mem) (void)hipFree(w->mem);
-  delete w;
+  while (w) {
+    mgenx_log_ws* nx = w->next;
+    if (w->mem) (void)hipFree(w->mem);
+    delete w;
+    w = nx;
+  }
+}
+// the area of `stream` (the head is the first stream's; others are chained)
+static mgenx_log_ws& ws_for(void* wsp, hipStream_t stream) {
+  static std::mutex mu;  // the chain is shared by the context's host threads
+  std::lock_guard<std::mutex> lock(mu);
+  mgenx_log_ws* head = static_cast<mgenx_log_ws*>(wsp);
+  if (!head->mem && !head->next && head->bytes == 0) head->stream = stream;
+  for (mgenx_log_ws* w = head; w; w = w->next)
+    if (w->stream == stream) return *w;
+  mgenx_log_ws* w = new mgenx_log_ws();
+  w->stream = stream;
+  w->next = head->next;
+  head->next = w;
+  return *w;
 }
 
 extern "C" int mgenx_log_recv_run(void* wsp, bool binary, const uint8_t* slab,
@@ -434,7 +458,7 @@ extern "C" int mgenx_log_recv_run(void* wsp, bool binary, const uint8_t* slab,
                                        int protocol, uint32_t opts, char* text,
                                        uint64_t text_cap, uint64_t* line_off,
                                        hipStream_t stream, char* err, size_t errn) {
-  mgenx_log_ws& ws = *static_cast<mgenx_log_ws*>(wsp);
+  mgenx_log_ws& ws = ws_for(wsp, stream);
   LogParams p;
   p.slab = slab; p.slab_bytes = slab_bytes; p.rec_off = rec_off; p.stride = stride; p.cols = *cols; p.src = src;
   p.rx_sec = rx_sec; p.rx_usec = rx_usec; p.ttl = ttl; p.n = n; p.protocol = protocol;
@@ -477,4 +501,627 @@ extern "C" int mgenx_log_recv_run(void* wsp, bool binary, const uint8_t* slab,
     return MGENX_EDEVICE;
   }
   return MGENX_OK;
+}
+
+// ====================================================================================
+// MGEN_DATA items: MgenAnalytic::Report (build, parse, REPORT lines) and the payload TLV
+// walk with MgenFlowCommand.  References: mgenAnalytic.cpp:28-71 (Init), :220-254 (the
+// report at a window close), :260-295 (MgenAnalytic::Log), :296-310 (GetReport), :343-566
+// (Report parse / build), :568-642 (quantizers), :747-786 (Report::Log);
+// mgenTransport.cpp:2132-2191 (ProcessRecvMessage); mgenPayload.cpp:276-347
+// (MgenFlowCommand); include/mgenAnalytic.h:14-57 (wire format).  ProtoPkt fields are
+// network byte order.  Restated in oracle/mgen_oracle.c (or_report_*, or_data_walk).
+// ====================================================================================
+namespace mgenx {
+
+struct Rq {
+  const double* t;  // the context's kRq* tables
+};
+
+__device__ __forceinline__ double mulr(double a, double b) {  // no FMA contraction
+  double p = a * b;
+  asm volatile("" : "+v"(p));
+  return p;
+}
+
+// QuantizeTimeValue: the host's log formula through its own thresholds
+__device__ uint8_t rq_q_time(const Rq& r, double v) {
+  if (v > mulr(1.1, 600.0)) return 0xff;
+  if (v < 1.0e-06 / 2.0) return 0;
+  if (v < 1.0e-06) return 1;
+  const double* T = r.t + kRqThrTime;
+  uint32_t lo = 2, hi = 256;  // first k with T[k] > v
+  while (lo < hi) {
+    const uint32_t m = (lo + hi) >> 1;
+    if (T[m] <= v) lo = m + 1; else hi = m;
+  }
+  return (uint8_t)(lo - 1);
+}
+__device__ __forceinline__ double rq_uq_time(const Rq& r, uint8_t q) { return r.t[kRqUnqTime + q]; }
+
+__device__ uint16_t rq_q_rate(const Rq& r, double rate) {
+  if (rate <= 0.0) return 0x01;
+  // (UINT16)(int)log10(rate) from the host's thresholds; outside them the device's log10
+  const double* T = r.t + kRqThrLog10;
+  int32_t e;
+  if (rate < T[0] || !(rate < T[kRqLog10N - 1])) {
+    e = (int32_t)log10(rate);
+  } else {
+    uint32_t lo = 0, hi = kRqLog10N;  // first j with T[j] > rate
+    while (lo < hi) {
+      const uint32_t m = (lo + hi) >> 1;
+      if (T[m] <= rate) lo = m + 1; else hi = m;
+    }
+    e = kRqLog10Lo + (int32_t)lo - 1;
+  }
+  const uint16_t ex = (uint16_t)e;
+  const double p10 = ex < kRqP10N ? r.t[kRqP10 + ex] : __builtin_huge_val();
+  const uint16_t mant = (uint16_t)(int32_t)(mulr(4096.0 / 10.0, rate / p10) + 0.5);
+  return (uint16_t)((mant << 4) | ex);
+}
+__device__ __forceinline__ double rq_uq_rate(const Rq& r, uint16_t q) {
+  return mulr(mulr((double)(q >> 4), 10.0 / 4096.0), r.t[kRqP10 + (q & 0xfu)]);
+}
+__device__ __forceinline__ uint16_t rq_q_loss(double loss) {
+  if (0.0 == loss) return 0;
+  loss = mulr(loss, 65535.0) + 0.5;
+  if (loss < 1.0) return 1;
+  if (loss > 65535.0) return 65535;
+  return (uint16_t)loss;
+}
+__device__ __forceinline__ double rq_uq_loss(uint16_t q) { return (double)q / 65535.0; }
+
+__device__ __forceinline__ void p16(uint8_t* p, uint32_t v) { p[0] = (uint8_t)(v >> 8); p[1] = (uint8_t)v; }
+__device__ __forceinline__ uint32_t g16(const uint8_t* p) { return (uint32_t)p[0] << 8 | p[1]; }
+
+struct RepOff {
+  uint32_t alen, src, dport, sport, fid, ws, lave, lmin, lmax, rate, loss, end;
+};
+__device__ __forceinline__ RepOff rep_off(uint8_t b0, uint8_t b2) {
+  RepOff o;
+  const uint32_t type = b0 >> 4;
+  o.alen = type == 1 ? 4u : (type == 2 ? 16u : 0u);
+  o.src = 4u * (1u + o.alen / 4u);
+  o.dport = o.src + o.alen;
+  o.sport = o.dport + 2u;
+  o.fid = o.sport + 2u;
+  o.ws = o.fid + (((b2 >> 5) & 1u) ? 4u : 0u);
+  o.lave = o.ws + 1u; o.lmin = o.lave + 1u; o.lmax = o.lmin + 1u;
+  o.rate = o.lmax + 1u; o.loss = o.rate + 2u; o.end = o.loss + 2u;
+  return o;
+}
+
+// report_msg after Init (key) and a window close, then GetReport (offset >= 0)
+__device__ uint32_t rep_build(const Rq& r, const mgenx_report_key& k, const mgenx_flow_report& w,
+                              double offset, bool& sign, uint8_t* b /*52*/) {
+  for (int i = 0; i < 52; i++) b[i] = 0;
+  b[0] = (uint8_t)(1u << 4);
+  b[1] = 16;
+  b[0] = (uint8_t)((b[0] & 0xf0u) | (k.protocol & 0x0fu));
+  for (int j = 0; j < 2; j++) {
+    const mgenx_addr& a = j == 0 ? k.dst : k.src;
+    uint32_t alen, type;
+    if (a.type == 1) { type = 1; alen = 4; }
+    else if (a.type == 2) { type = 2; alen = 16; }
+    else continue;
+    b[0] = (uint8_t)((b[0] & 0x0fu) | (type << 4));
+    b[1] = (uint8_t)(16u + 2u * alen);
+    const RepOff o = rep_off(b[0], b[2]);
+    if (j == 0) {
+      for (uint32_t i = 0; i < alen; i++) b[4 + i] = a.addr[i];
+      p16(b + o.dport, a.port);
+    } else {
+      for (uint32_t i = 0; i < alen; i++) b[o.src + i] = a.addr[i];
+      p16(b + o.sport, a.port);
+    }
+  }
+  if (k.flow_id != 1u) {
+    RepOff o = rep_off(b[0], b[2]);
+    const uint32_t rl = o.src + o.alen + 16u;
+    b[2] |= (uint8_t)(1u << 5);
+    o = rep_off(b[0], b[2]);
+    b[o.fid] = (uint8_t)(k.flow_id >> 24); b[o.fid + 1] = (uint8_t)(k.flow_id >> 16);
+    b[o.fid + 2] = (uint8_t)(k.flow_id >> 8); b[o.fid + 3] = (uint8_t)k.flow_id;
+    b[1] = (uint8_t)rl;
+  }
+  const RepOff o = rep_off(b[0], b[2]);
+  b[o.ws] = rq_q_time(r, w.duration);
+  if (w.latency_ave < 0.0) sign = true;
+  if (sign) b[2] |= (uint8_t)(2u << 5);
+  b[o.lave] = rq_q_time(r, fabs(w.latency_ave));
+  b[o.lmin] = rq_q_time(r, fabs(w.latency_ave - w.latency_min));
+  b[o.lmax] = rq_q_time(r, fabs(w.latency_max - w.latency_ave));
+  p16(b + o.rate, rq_q_rate(r, w.rate));
+  p16(b + o.loss, rq_q_loss(w.loss));
+  const uint32_t q = rq_q_time(r, offset < 0.0 ? 0.0 : offset);
+  p16(b + 2, (g16(b + 2) & 0xe000u) | q);
+  return b[1];
+}
+
+struct RepView {
+  bool valid;
+  uint8_t protocol, flags, length;
+  mgenx_addr src, dst;
+  uint32_t flow_id;
+  double offset, window, ave, mn, mx, rate, loss;
+};
+
+// the getters over a report buffer as it is (report type 1 or 2; no length check)
+template <typename B>
+__device__ void rep_view(const Rq& r, const B& byte, RepView& v) {
+  const uint8_t b0 = byte(0), b2 = byte(2);
+  const uint32_t type = b0 >> 4;
+  const RepOff o = rep_off(b0, b2);
+  v.protocol = b0 & 0x0f;
+  v.flags = b2 >> 5;
+  v.length = byte(1);
+  const uint8_t at = type == 1 ? 1 : 2;
+  v.dst.type = at; v.dst.len = (uint8_t)o.alen;
+  v.src.type = at; v.src.len = (uint8_t)o.alen;
+  for (int i = 0; i < 16; i++) {
+    v.dst.addr[i] = (uint32_t)i < o.alen ? byte(4 + i) : 0;
+    v.src.addr[i] = (uint32_t)i < o.alen ? byte(o.src + i) : 0;
+  }
+  v.dst.port = (uint16_t)((uint32_t)byte(o.dport) << 8 | byte(o.dport + 1));
+  v.src.port = (uint16_t)((uint32_t)byte(o.sport) << 8 | byte(o.sport + 1));
+  v.flow_id = (v.flags & 1u) ? ((uint32_t)byte(o.fid) << 24 | (uint32_t)byte(o.fid + 1) << 16 |
+                                (uint32_t)byte(o.fid + 2) << 8 | byte(o.fid + 3))
+                             : 0u;
+  v.offset = rq_uq_time(r, (uint8_t)((((uint32_t)b2 << 8) | byte(3)) & 0x1fffu));
+  v.window = rq_uq_time(r, byte(o.ws));
+  const double ave = rq_uq_time(r, byte(o.lave));
+  v.ave = (v.flags & 2u) ? -ave : ave;
+  v.mn = v.ave - rq_uq_time(r, byte(o.lmin));
+  v.mx = v.ave + rq_uq_time(r, byte(o.lmax));
+  v.rate = rq_uq_rate(r, (uint16_t)((uint32_t)byte(o.rate) << 8 | byte(o.rate + 1)));
+  v.loss = rq_uq_loss((uint16_t)((uint32_t)byte(o.loss) << 8 | byte(o.loss + 1)));
+}
+
+// Report::InitFromBuffer(b, avail) + the getters (byte(k) reads past avail as 0)
+template <typename B>
+__device__ bool rep_parse(const Rq& r, const B& byte, uint32_t avail, RepView& v) {
+  v.valid = false;
+  if (avail < 2 || byte(1) > avail) return false;
+  const uint8_t b0 = byte(0), b2 = byte(2);
+  const uint32_t type = b0 >> 4;
+  if (type != 1 && type != 2) return false;
+  if (byte(1) != rep_off(b0, b2).end) return false;
+  rep_view(r, byte, v);
+  v.valid = true;
+  return true;
+}
+
+// "%lf" of any double as glibc prints it: the exact binary value rounded to 6 decimals,
+// ties to even; inf / nan as "inf" / "nan" with the sign
+template <typename S>
+__device__ void put_f6(S& s, double v) {
+  const uint64_t bits = (uint64_t)__double_as_longlong(v);
+  const bool neg = (bits >> 63) != 0;
+  const uint32_t ex = (uint32_t)((bits >> 52) & 0x7ffu);
+  const uint64_t frac = bits & ((1ull << 52) - 1);
+  if (neg) s.put('-');
+  if (ex == 0x7ffu) {
+    put_str(s, frac ? "nan" : "inf");
+    return;
+  }
+  const uint64_t mant = frac | (ex ? (1ull << 52) : 0ull);
+  const int e = (ex ? (int)ex : 1) - 1075;  // |v| = mant * 2^e
+  if (e <= 40) {
+    // |v| * 1e6 = mant * 1e6 * 2^e < 2^113: 128-bit integer arithmetic
+    const unsigned __int128 P = (unsigned __int128)mant * 1000000u;
+    unsigned __int128 q;
+    if (e >= 0) {
+      q = P << e;
+    } else if (-e >= 100) {
+      q = 0;
+    } else {
+      const int sh = -e;
+      q = P >> sh;
+      const unsigned __int128 rem = P - (q << sh);
+      const unsigned __int128 half = (unsigned __int128)1 << (sh - 1);
+      if (rem > half || (rem == half && (q & 1))) q++;
+    }
+    const unsigned __int128 ip = q / 1000000u;
+    const uint64_t fp = (uint64_t)(q % 1000000u);
+    // integer part: up to 2^93 / 1e6 < 2^74 -- two 64-bit halves in decimal
+    if (ip >> 64) {
+      const uint64_t base = 10000000000000000000ull;  // 1e19
+      const uint64_t hi = (uint64_t)(ip / base), lo = (uint64_t)(ip % base);
+      put_u64(s, hi);
+      put_u64(s, lo, 19);
+    } else {
+      put_u64(s, (uint64_t)ip);
+    }
+    s.put('.');
+    put_u64(s, fp, 6);
+    return;
+  }
+  // |v| >= 2^93: an integer; its decimal digits by long division of mant * 2^e
+  uint32_t w[34];
+  int nw = 0;
+  for (int i = 0; i < 34; i++) w[i] = 0;
+  w[e / 32] = (uint32_t)(mant << (e % 32));
+  w[e / 32 + 1] = (uint32_t)(mant >> (32 - e % 32));
+  w[e / 32 + 2] = (e % 32) ? (uint32_t)(mant >> (64 - e % 32)) : 0u;
+  nw = e / 32 + 3;
+  char dig[330];
+  int nd = 0;
+  for (;;) {
+    while (nw > 0 && w[nw - 1] == 0) nw--;
+    if (nw == 0) break;
+    uint64_t rem = 0;
+    for (int i = nw - 1; i >= 0; i--) {
+      const uint64_t cur = (rem << 32) | w[i];
+      w[i] = (uint32_t)(cur / 1000000000u);
+      rem = cur % 1000000000u;
+    }
+    for (int k = 0; k < 9; k++) {
+      dig[nd++] = (char)('0' + rem % 10);
+      rem /= 10;
+    }
+  }
+  while (nd > 1 && dig[nd - 1] == '0') nd--;
+  for (int i = nd - 1; i >= 0; i--) s.put((uint8_t)dig[i]);
+  put_str(s, ".000000");
+}
+
+__device__ __forceinline__ const char* rep_proto(uint32_t p) {
+  return p == 1 ? "UDP" : p == 2 ? "TCP" : p == 3 ? "SINK" : "???";
+}
+
+template <typename S>
+__device__ void put_rep_head(S& s, const RepView& v) {
+  put_str(s, "REPORT proto>");
+  put_str(s, rep_proto(v.protocol));
+  put_str(s, " flow>");
+  put_u64(s, v.flow_id ? v.flow_id : 1u);
+  put_str(s, " src>");
+  put_addr(s, v.src.type, v.src.len, v.src.addr);
+  s.put('/');
+  put_u64(s, v.src.port);
+  put_str(s, " dst>");
+  put_addr(s, v.dst.type, v.dst.len, v.dst.addr);
+  s.put('/');
+  put_u64(s, v.dst.port);
+  s.put(' ');
+}
+
+template <typename S>
+__device__ void put_rep_values(S& s, double window, double rate, double loss, double ave,
+                               double mn, double mx) {
+  put_str(s, "window>");
+  put_f6(s, window);
+  put_str(s, " rate>");
+  put_f6(s, mulr(rate, 8.0e-03));
+  put_str(s, " kbps loss>");
+  put_f6(s, loss);
+  put_str(s, " latency ave>");
+  put_f6(s, ave);
+  put_str(s, " min>");
+  put_f6(s, mn);
+  put_str(s, " max>");
+  put_f6(s, mx);
+}
+
+struct ItemBytes {
+  const uint8_t* p;
+  uint32_t n;
+  __device__ uint8_t operator()(uint32_t k) const { return k < n ? p[k] : (uint8_t)0; }
+};
+
+// ---- kernels ----
+// one thread per flow, its kept reports in order (FLAG_LATENCY_SIGN is never cleared)
+__global__ void report_build_kernel(const mgenx_flow_report* __restrict__ reps, uint32_t n_flows,
+                                    uint32_t per_flow, const uint32_t* __restrict__ count,
+                                    const mgenx_report_key* __restrict__ keys,
+                                    uint8_t* __restrict__ sign, const double* __restrict__ offset,
+                                    const double* rq, uint8_t* __restrict__ items,
+                                    uint8_t* __restrict__ item_len) {
+  const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= n_flows) return;
+  const Rq r{rq};
+  const mgenx_report_key k = keys[f];
+  bool sg = sign[f] != 0;
+  const uint32_t m = min(count[f], per_flow);
+  for (uint32_t j = 0; j < m; j++) {
+    const size_t slot = (size_t)f * per_flow + j;
+    uint8_t b[52];
+    item_len[slot] = (uint8_t)rep_build(r, k, reps[slot], offset ? offset[slot] : 0.0, sg, b);
+    for (int i = 0; i < 52; i++) items[slot * 52 + i] = b[i];
+  }
+  sign[f] = sg ? 1u : 0u;
+}
+
+struct RepLineParams {
+  const uint8_t* items;             // 52 B per slot (built reports / received report bytes)
+  const mgenx_flow_report* reps;    // analytic lines: the doubles; NULL = received reports
+  const uint32_t* count;            // analytic lines: kept reports per flow
+  uint32_t per_flow;
+  const uint64_t* rep_pairs;        // received: (record, slab offset of the item) pairs
+  const uint8_t* slab;
+  const mgenx_addr* reporter;       // received: per record, the message's source
+  const uint32_t* rx_sec;           // received: per record
+  const uint32_t* rx_usec;
+  uint32_t n;                       // slots
+  uint32_t opts;
+  const double* rq;
+  uint8_t* text;
+  uint64_t text_cap;
+  uint64_t* line_off;
+  uint64_t* lens;
+};
+
+template <typename S>
+__device__ void rep_line(S& s, const RepLineParams& p, uint32_t i) {
+  const Rq r{p.rq};
+  const bool epoch = (p.opts & MGENX_LOG_EPOCH) != 0;
+  RepView v = {};  // deterministic for an invalid item handed in (both passes agree)
+  if (p.reps) {  // MgenAnalytic::Log (mgenAnalytic.cpp:260-295)
+    const uint32_t f = i / p.per_flow, j = i % p.per_flow;
+    if (j >= min(p.count[f], p.per_flow)) return;
+    const mgenx_flow_report& w = p.reps[i];
+    // the getters read the buffer as it is: a report whose addresses were invalid keeps
+    // InitIntoBuffer's IPv4 type and length 16 (mgenAnalytic.cpp:63-67)
+    rep_view(r, ItemBytes{p.items + (size_t)i * 52, 52}, v);
+    put_ts(s, (uint32_t)w.rx_sec, (uint32_t)w.rx_usec, epoch);
+    put_rep_head(s, v);
+    put_rep_values(s, w.duration, w.rate, w.loss, w.latency_ave, w.latency_min, w.latency_max);
+    put_str(s, ", count>");
+    put_u64(s, (uint32_t)w.msg_count);
+    s.put('\n');
+  } else {  // MgenAnalytic::Report::Log (mgenAnalytic.cpp:747-786)
+    const uint64_t rec = p.rep_pairs[2 * (size_t)i];
+    rep_parse(r, ItemBytes{p.slab + p.rep_pairs[2 * (size_t)i + 1], 52}, 52, v);
+    put_ts(s, p.rx_sec[rec], p.rx_usec[rec], epoch);
+    put_rep_head(s, v);
+    put_str(s, "reporter>");
+    const mgenx_addr& a = p.reporter[rec];
+    put_addr(s, a.type, a.len, a.addr);
+    s.put('/');
+    put_u64(s, a.port);
+    put_str(s, " sent>");
+    put_ts(s, p.rx_sec[rec], p.rx_usec[rec], epoch);  // theTime, as the reference prints it
+    put_str(s, "offset>");
+    put_f6(s, v.offset);
+    s.put(' ');
+    put_rep_values(s, v.window, v.rate, v.loss, v.ave, v.mn, v.mx);
+    s.put('\n');
+  }
+}
+
+template <bool kWrite>
+__global__ void __launch_bounds__(kLogThreads) rep_line_kernel(RepLineParams p) {
+  const uint32_t i = blockIdx.x * kLogThreads + threadIdx.x;
+  if (i >= p.n) return;
+  if (!kWrite) {
+    CountSink s;
+    rep_line(s, p, i);
+    p.lens[i] = s.n;
+  } else {
+    const uint64_t off = p.line_off[i], end = p.line_off[i + 1];
+    if (end > p.text_cap) return;
+    WriteSink s{p.text + off};
+    rep_line(s, p, i);
+  }
+}
+
+// MgenFlowCommand::GetStatus (mgenPayload.cpp:326-347)
+template <typename B>
+__device__ uint32_t flowcmd_status(const B& byte, uint32_t base, uint32_t len, uint32_t flow) {
+  const uint32_t N = (2 * flow > 16) ? (2 * flow - 16 - 1) / 32 + 1 : 0;
+  if (2 + 2 + N * 4 > len) return 0;
+  const uint32_t f = flow - 1;
+  uint32_t st = (byte(base + 2 + (f >> 3)) & (0x80u >> (f & 7))) ? 1u : 0u;
+  if (byte(base + 2 + (len - 2) / 2 + (f >> 3)) & (0x80u >> (f & 7))) st |= 2u;
+  return st;
+}
+
+struct WalkParams {
+  const uint8_t* slab;
+  const uint64_t* rec_off;
+  uint64_t stride;
+  mgenx_cols cols;
+  uint32_t n;
+  uint32_t opts;
+  const double* rq;
+  uint8_t* status;        // per record
+  uint8_t* needs_host;    // per record
+  uint32_t* n_cmd;        // per record (pass 1), n + 1
+  uint32_t* n_rep;
+  const uint32_t* cmd_base;  // pass 2
+  const uint32_t* rep_base;
+  uint32_t* cmds;         // 2 words: record, flow << 2 | status
+  uint32_t cmd_cap;
+  uint64_t* reps;         // 2 words: record, slab offset of the report item
+  uint32_t rep_cap;
+};
+
+// MgenTransport::ProcessRecvMessage (mgenTransport.cpp:2132-2191) for record i
+template <bool kWrite>
+__global__ void __launch_bounds__(256) data_walk_kernel(WalkParams p) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p.n) return;
+  const mgenx_cols& c = p.cols;
+  const bool mine = c.err[i] == 0 && c.payload_type[i] == MGENX_PAYLOAD_MGEN_DATA;
+  if (!kWrite) {
+    p.n_cmd[i] = 0;
+    p.n_rep[i] = 0;
+    if (i == 0) { p.n_cmd[p.n] = 0; p.n_rep[p.n] = 0; }
+    p.status[i] = mine ? 0 : 0xff;
+    p.needs_host[i] = 0;
+  }
+  if (!mine) return;
+  const Rq r{p.rq};
+  const uint64_t off0 = (p.rec_off ? p.rec_off[i] : (uint64_t)i * p.stride) + c.payload_off[i];
+  const uint32_t plen = c.payload_len[i];
+  const ItemBytes all{p.slab + off0, plen};
+  uint32_t off = 0, left = plen, nc = 0, nr = 0, st = 0;
+  uint32_t cw = kWrite ? p.cmd_base[i] : 0, rw = kWrite ? p.rep_base[i] : 0;
+  const bool ctl = (p.opts & MGENX_DATA_CONTROLLER) != 0;
+  while (left > 0) {
+    const uint32_t type = all(off);
+    const uint32_t ilen = left > 1 ? all(off + 1) : 0u;
+    if (type == 1) {  // DATA_ITEM_FLOW_CMD
+      if (ilen > left) { st = 1; break; }
+      uint32_t maxf = ilen > 2 ? 8 * (ilen - 2) / 2 : 0;
+      if (maxf > MGENX_MAX_FLOW) maxf = MGENX_MAX_FLOW;
+      for (uint32_t fl = 1; fl <= maxf; fl++) {
+        const uint32_t s2 = flowcmd_status(all, off, ilen, fl);
+        if (!s2) continue;
+        if (kWrite && cw < p.cmd_cap) {
+          p.cmds[2 * (size_t)cw] = i;
+          p.cmds[2 * (size_t)cw + 1] = fl << 2 | s2;
+        }
+        cw++;
+        nc++;
+      }
+      if (ilen == 0) { st = 3; break; }
+      left -= ilen;
+      off += (ilen / 4) * 4;
+    } else if (ctl && type > 0x0f) {
+      RepView v;
+      const ItemBytes it{p.slab + off0 + off, left};
+      if (!rep_parse(r, it, left, v)) { st = 2; break; }
+      if (kWrite && rw < p.rep_cap) {
+        p.reps[2 * (size_t)rw] = i;
+        p.reps[2 * (size_t)rw + 1] = off0 + off;
+      }
+      rw++;
+      nr++;
+      left -= v.length;
+      off += (v.length / 4u) * 4u;
+    } else {
+      if (ilen > left || ilen == 0) { st = 3; break; }
+      left -= ilen;
+      off += (ilen / 4) * 4;
+    }
+  }
+  if (!kWrite) {
+    p.n_cmd[i] = nc;
+    p.n_rep[i] = nr;
+    p.status[i] = (uint8_t)st;
+    p.needs_host[i] = (nc || nr) ? 1u : 0u;
+  }
+}
+
+}  // namespace mgenx
+
+// per-stream scratch for the two-pass line formatters and the walk's scans
+static int rep_ws(mgenx_log_ws& ws, size_t need, void** out, char* err, size_t errn) {
+  if (ws.bytes < need) {
+    if (ws.mem) (void)hipFree(ws.mem);
+    ws.mem = nullptr;
+    ws.bytes = 0;
+    if (hipMalloc(&ws.mem, need) != hipSuccess) {
+      snprintf(err, errn, "report: workspace of %zu bytes", need);
+      return MGENX_EDEVICE;
+    }
+    ws.bytes = need;
+  }
+  *out = ws.mem;
+  return MGENX_OK;
+}
+
+extern "C" int mgenx_report_build_run(const mgenx_flow_report* reps, uint32_t n_flows,
+                                      uint32_t per_flow, const uint32_t* count,
+                                      const mgenx_report_key* keys, uint8_t* sign,
+                                      const double* offset, const double* rq, uint8_t* items,
+                                      uint8_t* item_len, hipStream_t stream) {
+  if (!n_flows || !per_flow) return MGENX_OK;
+  hipLaunchKernelGGL(mgenx::report_build_kernel, dim3((n_flows + 127) / 128), dim3(128), 0, stream,
+                     reps, n_flows, per_flow, count, keys, sign, offset, rq, items, item_len);
+  return hipGetLastError() == hipSuccess ? MGENX_OK : MGENX_EDEVICE;
+}
+
+extern "C" int mgenx_report_lines_run(void* wsp, mgenx::RepLineParams* pp, hipStream_t stream,
+                                      char* err, size_t errn) {
+  mgenx_log_ws& ws = ws_for(wsp, stream);
+  mgenx::RepLineParams& p = *pp;
+  const uint32_t n = p.n;
+  size_t scan_bytes = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, (uint64_t*)nullptr,
+                                         (uint64_t*)nullptr, (int)n + 1, stream);
+  const size_t len_bytes = (((size_t)n + 1) * 8 + 255) & ~(size_t)255;
+  void* mem;
+  int rc = rep_ws(ws, len_bytes + scan_bytes, &mem, err, errn);
+  if (rc != MGENX_OK) return rc;
+  p.lens = static_cast<uint64_t*>(mem);
+  const int grid = (int)((n + mgenx::kLogThreads - 1) / mgenx::kLogThreads);
+  hipLaunchKernelGGL((mgenx::rep_line_kernel<false>), dim3(grid), dim3(mgenx::kLogThreads), 0,
+                     stream, p);
+  hipLaunchKernelGGL(mgenx::log_tail_kernel, dim3(1), dim3(64), 0, stream, p.lens, n);
+  size_t have = scan_bytes;
+  if (hipcub::DeviceScan::ExclusiveSum(static_cast<uint8_t*>(mem) + len_bytes, have, p.lens,
+                                       p.line_off, (int)n + 1, stream) != hipSuccess) {
+    snprintf(err, errn, "report lines: scan failed");
+    return MGENX_EDEVICE;
+  }
+  hipLaunchKernelGGL((mgenx::rep_line_kernel<true>), dim3(grid), dim3(mgenx::kLogThreads), 0,
+                     stream, p);
+  return hipGetLastError() == hipSuccess ? MGENX_OK : MGENX_EDEVICE;
+}
+
+extern "C" int mgenx_data_walk_run(void* wsp, mgenx::WalkParams* pp, uint32_t* totals,
+                                   hipStream_t stream, char* err, size_t errn) {
+  mgenx_log_ws& ws = ws_for(wsp, stream);
+  mgenx::WalkParams& p = *pp;
+  const uint32_t n = p.n;
+  size_t scan_bytes = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, (uint32_t*)nullptr,
+                                         (uint32_t*)nullptr, (int)n + 1, stream);
+  const size_t b4 = (((size_t)n + 1) * 4 + 255) & ~(size_t)255;
+  void* mem;
+  int rc = rep_ws(ws, 4 * b4 + scan_bytes, &mem, err, errn);
+  if (rc != MGENX_OK) return rc;
+  char* m = static_cast<char*>(mem);
+  p.n_cmd = reinterpret_cast<uint32_t*>(m);
+  p.n_rep = reinterpret_cast<uint32_t*>(m + b4);
+  uint32_t* cb = reinterpret_cast<uint32_t*>(m + 2 * b4);
+  uint32_t* rb = reinterpret_cast<uint32_t*>(m + 3 * b4);
+  p.cmd_base = cb;
+  p.rep_base = rb;
+  const dim3 g((n + 255) / 256);
+  hipLaunchKernelGGL((mgenx::data_walk_kernel<false>), g, dim3(256), 0, stream, p);
+  size_t have = scan_bytes;
+  if (hipcub::DeviceScan::ExclusiveSum(m + 4 * b4, have, p.n_cmd, cb, (int)n + 1, stream) !=
+          hipSuccess ||
+      hipcub::DeviceScan::ExclusiveSum(m + 4 * b4, have, p.n_rep, rb, (int)n + 1, stream) !=
+          hipSuccess) {
+    snprintf(err, errn, "data walk: scan failed");
+    return MGENX_EDEVICE;
+  }
+  hipLaunchKernelGGL((mgenx::data_walk_kernel<true>), g, dim3(256), 0, stream, p);
+  if (totals) {
+    if (hipMemcpyAsync(totals, cb + n, 4, hipMemcpyDeviceToDevice, stream) != hipSuccess ||
+        hipMemcpyAsync(totals + 1, rb + n, 4, hipMemcpyDeviceToDevice, stream) != hipSuccess)
+      return MGENX_EDEVICE;
+  }
+  return hipGetLastError() == hipSuccess ? MGENX_OK : MGENX_EDEVICE;
+}
+
+extern "C" int mgenx_report_lines(void* ws, const uint8_t* items, const mgenx_flow_report* reps,
+                                  const uint32_t* count, uint32_t per_flow, const uint64_t* pairs,
+                                  const uint8_t* slab, const mgenx_addr* reporter,
+                                  const uint32_t* rx_sec, const uint32_t* rx_usec, uint32_t n,
+                                  uint32_t opts, const double* rq, char* text, uint64_t cap,
+                                  uint64_t* line_off, hipStream_t stream, char* err, size_t errn) {
+  mgenx::RepLineParams p;
+  p.items = items; p.reps = reps; p.count = count; p.per_flow = per_flow; p.rep_pairs = pairs;
+  p.slab = slab; p.reporter = reporter; p.rx_sec = rx_sec; p.rx_usec = rx_usec; p.n = n;
+  p.opts = opts; p.rq = rq; p.text = reinterpret_cast<uint8_t*>(text); p.text_cap = cap;
+  p.line_off = line_off; p.lens = nullptr;
+  return mgenx_report_lines_run(ws, &p, stream, err, errn);
+}
+
+extern "C" int mgenx_data_walk_exec(void* ws, const uint8_t* slab, const uint64_t* rec_off,
+                                    uint64_t stride, const mgenx_cols* cols, uint32_t n,
+                                    uint32_t opts, const double* rq, uint8_t* status,
+                                    uint8_t* needs_host, uint32_t* cmds, uint32_t cmd_cap,
+                                    uint64_t* reps, uint32_t rep_cap, uint32_t* totals,
+                                    hipStream_t stream, char* err, size_t errn) {
+  mgenx::WalkParams p;
+  p.slab = slab; p.rec_off = rec_off; p.stride = stride; p.cols = *cols; p.n = n; p.opts = opts;
+  p.rq = rq; p.status = status; p.needs_host = needs_host; p.cmds = cmds; p.cmd_cap = cmd_cap;
+  p.reps = reps; p.rep_cap = rep_cap;
+  return mgenx_data_walk_run(ws, &p, totals, stream, err, errn);
 }

@@ -1164,3 +1164,298 @@ uint32_t or_log_recv_binary(const or_fields* f, const uint8_t* rec, uint64_t ava
     }
     return (uint32_t)(p - out);
 }
+
+/* ------------------------------------------------------------------ */
+/* MGEN_DATA items: MgenAnalytic::Report and MgenFlowCommand           */
+/*   quantizers          mgenAnalytic.cpp:568-642                      */
+/*   Report build        Init :28-71, Update :220-254, GetReport :296-310, */
+/*                       InitIntoBuffer/SetDstAddr/SetSrcAddr/SetFlowId :446-566 */
+/*   Report parse        InitFromBuffer :343-373, getters mgenAnalytic.h:167-220 */
+/*   REPORT log lines    MgenAnalytic::Log :260-295, Report::Log :747-786 */
+/*   TLV walk            MgenTransport::ProcessRecvMessage mgenTransport.cpp:2132-2191 */
+/*   flow commands       MgenFlowCommand mgenPayload.cpp:276-347, MAX_FLOW mgenEvent.h:194 */
+/* ProtoPkt getters/setters are network byte order.                    */
+/* ------------------------------------------------------------------ */
+static const double RQ_STRETCH = 1.1, RQ_MIN = 1.0e-06, RQ_MAX = 600.0;
+
+static double rq_scale(void) { return 1.0 / (pow(RQ_STRETCH, 254) - RQ_STRETCH); }
+
+uint8_t or_q_time(double value)
+{
+    if (value > RQ_STRETCH * RQ_MAX) return 0xff;
+    else if (value < RQ_MIN / 2.0) return 0;
+    else if (value < RQ_MIN) return 1;
+    return (uint8_t)((log(RQ_STRETCH + (value - RQ_MIN) / (rq_scale() * (RQ_MAX - RQ_MIN))) /
+                      log(RQ_STRETCH)) + 0.5);
+}
+
+double or_uq_time(uint8_t q)
+{
+    if (0 == q) return 0.0;
+    return (RQ_MAX - RQ_MIN) * (pow(RQ_STRETCH, q) - RQ_STRETCH) * rq_scale() + RQ_MIN;
+}
+
+uint16_t or_q_rate(double rate)
+{
+    if (rate <= 0.0) return 0x01;
+    /* (UINT16)log10(rate): x86-64 gcc converts through int32, so log10 < 0 wraps */
+    uint16_t exponent = (uint16_t)(int32_t)log10(rate);
+    uint16_t mantissa = (uint16_t)(int32_t)((4096.0 / 10.0) * (rate / pow(10.0, (double)exponent)) + 0.5);
+    return (uint16_t)((mantissa << 4) | exponent);
+}
+
+double or_uq_rate(uint16_t q)
+{
+    double mantissa = ((double)(q >> 4)) * (10.0 / 4096.0);
+    double exponent = (double)(q & 0x000f);
+    return mantissa * pow(10.0, exponent);
+}
+
+uint16_t or_q_loss(double loss)
+{
+    if (0.0 == loss) return 0;
+    loss = loss * 65535.0 + 0.5;
+    if (loss < 1.0) return 1;
+    else if (loss > 65535.0) return 65535;
+    return (uint16_t)loss;
+}
+
+double or_uq_loss(uint16_t q) { return ((double)q) / 65535.0; }
+
+static void put16be(uint8_t* p, uint16_t v) { p[0] = (uint8_t)(v >> 8); p[1] = (uint8_t)v; }
+static uint16_t get16be(const uint8_t* p) { return (uint16_t)(p[0] << 8 | p[1]); }
+
+/* offsets of a report whose type byte says addrLen and whose flags say flow id */
+typedef struct { uint32_t alen, src, dport, sport, fid, ws, lave, lmin, lmax, rate, loss, end; } rep_off;
+static rep_off rep_offsets(const uint8_t* b)
+{
+    rep_off o;
+    const uint8_t type = b[0] >> 4;
+    o.alen = type == 1 ? 4 : (type == 2 ? 16 : 0);
+    o.src = 4 * (1 + o.alen / 4);
+    o.dport = o.src + o.alen;
+    o.sport = o.dport + 2;
+    o.fid = o.sport + 2;
+    o.ws = o.fid + (((b[2] >> 5) & 0x01) ? 4 : 0);
+    o.lave = o.ws + 1; o.lmin = o.lave + 1; o.lmax = o.lmin + 1;
+    o.rate = o.lmax + 1; o.loss = o.rate + 2; o.end = o.loss + 2;
+    return o;
+}
+
+/* report_msg of an analytic (key) after Init and one window close, then GetReport(theTime):
+ * offset < 0 leaves the window offset field 0.  *sign: FLAG_LATENCY_SIGN was set before (in)
+ * / is set after (out) -- SetLatencyAve never clears it.  Returns the report length. */
+uint32_t or_report_build(const or_addr* src, const or_addr* dst, uint32_t flow_id, int protocol,
+                         double duration, double lat_ave, double lat_min, double lat_max,
+                         double rate, double loss, double offset, int* sign, uint8_t* b)
+{
+    memset(b, 0, 52);
+    /* InitIntoBuffer(REPORT_FLOW_IPv4): memset 16, type, length 16 */
+    b[0] = (uint8_t)(1 << 4);
+    b[1] = 16;
+    uint32_t pkt_len = 16;
+    b[0] = (uint8_t)((b[0] & 0xf0) | (protocol & 0x0f));            /* SetProtocol */
+    const or_addr* addrs[2] = {dst, src};
+    for (int k = 0; k < 2; k++) {                                   /* SetDstAddr, SetSrcAddr */
+        const or_addr* a = addrs[k];
+        uint32_t alen;
+        uint8_t type;
+        if (a->type == OR_ADDR_IPV4) { type = 1; alen = 4; }
+        else if (a->type == OR_ADDR_IPV6) { type = 2; alen = 16; }
+        else continue;                                               /* error: unchanged */
+        const uint32_t rl = 12 + 4 + 2 * alen;
+        b[0] = (uint8_t)((b[0] & 0x0f) | (type << 4));
+        b[1] = (uint8_t)rl;
+        rep_off o = rep_offsets(b);
+        if (k == 0) { memcpy(b + 4, a->addr, alen); put16be(b + o.dport, a->port); }
+        else { memcpy(b + o.src, a->addr, alen); put16be(b + o.sport, a->port); }
+        pkt_len = rl;
+    }
+    if (flow_id != 1) {                                              /* SetFlowId */
+        rep_off o = rep_offsets(b);
+        const uint32_t rl = o.src + o.alen + 12 + 4;
+        b[2] |= (uint8_t)(0x01 << 5);
+        o = rep_offsets(b);
+        put32(b + o.fid, flow_id);
+        b[1] = (uint8_t)rl;
+        pkt_len = rl;
+    }
+    rep_off o = rep_offsets(b);
+    /* window close (:245-253); SetWindowSize at Init is overwritten here */
+    b[o.ws] = or_q_time(duration);
+    if (lat_ave < 0.0) *sign = 1;
+    if (*sign) b[2] |= (uint8_t)(0x02 << 5);
+    b[o.lave] = or_q_time(fabs(lat_ave));
+    b[o.lmin] = or_q_time(fabs(lat_ave - lat_min));
+    b[o.lmax] = or_q_time(fabs(lat_max - lat_ave));
+    put16be(b + o.rate, or_q_rate(rate));
+    put16be(b + o.loss, or_q_loss(loss));
+    if (offset >= 0.0 || offset < 0.0) {                            /* GetReport */
+        double off = offset < 0.0 ? 0.0 : offset;
+        const uint16_t q = or_q_time(off);
+        const uint16_t field = (uint16_t)((get16be(b + 2) & 0xe000) | q);
+        put16be(b + 2, field);
+    }
+    (void)pkt_len;
+    return (uint32_t)b[1];
+}
+
+typedef struct {
+    uint8_t  valid, type, protocol, flags;
+    uint32_t length;
+    or_addr  src, dst;
+    uint32_t flow_id;         /* GetFlowId(): 0 when the flag is clear */
+    double   window_offset, window_size, lat_ave, lat_min, lat_max, rate, loss;
+} or_report_view;
+
+/* the getters over a report buffer as it is (no length check; report type 1 or 2) */
+static void report_view(const uint8_t* b, or_report_view* v)
+{
+    const uint8_t type = b[0] >> 4;
+    rep_off o = rep_offsets(b);
+    v->type = type;
+    v->protocol = b[0] & 0x0f;
+    v->flags = b[2] >> 5;
+    v->length = b[1];
+    const uint8_t at = type == 1 ? OR_ADDR_IPV4 : OR_ADDR_IPV6;
+    v->dst.type = at; v->dst.len = (uint8_t)o.alen; memcpy(v->dst.addr, b + 4, o.alen);
+    v->dst.port = get16be(b + o.dport);
+    v->src.type = at; v->src.len = (uint8_t)o.alen; memcpy(v->src.addr, b + o.src, o.alen);
+    v->src.port = get16be(b + o.sport);
+    v->flow_id = (v->flags & 0x01) ? get32(b + o.fid) : 0;
+    v->window_offset = or_uq_time((uint8_t)(get16be(b + 2) & 0x1fff));
+    v->window_size = or_uq_time(b[o.ws]);
+    const double ave = or_uq_time(b[o.lave]);
+    v->lat_ave = (v->flags & 0x02) ? -ave : ave;
+    v->lat_min = v->lat_ave - or_uq_time(b[o.lmin]);
+    v->lat_max = v->lat_ave + or_uq_time(b[o.lmax]);
+    v->rate = or_uq_rate(get16be(b + o.rate));
+    v->loss = or_uq_loss(get16be(b + o.loss));
+}
+
+/* Report::InitFromBuffer(buf, avail) and the getters */
+int or_report_parse(const uint8_t* b, uint32_t avail, or_report_view* v)
+{
+    memset(v, 0, sizeof(*v));
+    if (avail < 1) return 0;                                         /* OFFSET_LEN */
+    const uint32_t min_len = avail > 1 ? b[1] : 0;
+    if (min_len > avail) return 0;                                   /* ProtoPkt::InitFromBuffer */
+    if (avail < 2) return 0;                                         /* OFFSET_FLAGS */
+    const uint8_t type = b[0] >> 4;
+    if (type != 1 && type != 2) return 0;
+    rep_off o = rep_offsets(b);
+    if (b[1] != o.end) return 0;
+    report_view(b, v);
+    v->valid = 1;
+    return 1;
+}
+
+static const char* rep_proto(int p)
+{
+    switch (p) { case 1: return "UDP"; case 2: return "TCP"; case 3: return "SINK"; default: return "???"; }
+}
+
+/* MgenAnalytic::Log: the report_msg's key fields, the analytic's report doubles */
+uint32_t or_log_report(const uint8_t* report, double duration, double rate, double loss,
+                       double lat_ave, double lat_min, double lat_max, uint64_t count,
+                       uint32_t sec, uint32_t usec, uint32_t opts, char* out)
+{
+    or_report_view v;
+    char* p = out;
+    /* the getters read the buffer as it is: a report whose addresses were invalid keeps
+     * InitIntoBuffer's IPv4 type and length 16 (mgenAnalytic.cpp:63-67) */
+    memset(&v, 0, sizeof v);
+    report_view(report, &v);
+    p += log_ts(p, sec, usec, (opts & OR_LOG_EPOCH) != 0);
+    const unsigned long fid = v.flow_id ? v.flow_id : 1;
+    p += sprintf(p, "REPORT proto>%s flow>%lu src>", rep_proto(v.protocol), fid);
+    p += log_addr(p, v.src.type, v.src.len, v.src.addr);
+    p += sprintf(p, "/%hu dst>", v.src.port);
+    p += log_addr(p, v.dst.type, v.dst.len, v.dst.addr);
+    p += sprintf(p, "/%hu ", v.dst.port);
+    p += sprintf(p, "window>%lf rate>%lf kbps loss>%lf latency ave>%lf min>%lf max>%lf, count>%u\n",
+                 duration, rate * 8.0e-03, loss, lat_ave, lat_min, lat_max, (unsigned)count);
+    return (uint32_t)(p - out);
+}
+
+/* MgenAnalytic::Report::Log (a received report): "sent>" prints theTime, as the reference
+ * does (mgenAnalytic.cpp:779) */
+uint32_t or_log_report_recv(const uint8_t* report, const or_addr* reporter, uint32_t sec,
+                            uint32_t usec, uint32_t opts, char* out)
+{
+    or_report_view v;
+    char* p = out;
+    or_report_parse(report, 52, &v);
+    const int ep = (opts & OR_LOG_EPOCH) != 0;
+    p += log_ts(p, sec, usec, ep);
+    const unsigned long fid = v.flow_id ? v.flow_id : 1;
+    p += sprintf(p, "REPORT proto>%s flow>%lu src>", rep_proto(v.protocol), fid);
+    p += log_addr(p, v.src.type, v.src.len, v.src.addr);
+    p += sprintf(p, "/%hu dst>", v.src.port);
+    p += log_addr(p, v.dst.type, v.dst.len, v.dst.addr);
+    p += sprintf(p, "/%hu reporter>", v.dst.port);
+    p += log_addr(p, reporter->type, reporter->len, reporter->addr);
+    p += sprintf(p, "/%hu sent>", reporter->port);
+    p += log_ts(p, sec, usec, ep);
+    p += sprintf(p, "offset>%lf ", v.window_offset);
+    p += sprintf(p, "window>%lf rate>%lf kbps loss>%lf latency ave>%lf min>%lf max>%lf\n",
+                 v.window_size, v.rate * 8.0e-03, v.loss, v.lat_ave, v.lat_min, v.lat_max);
+    return (uint32_t)(p - out);
+}
+
+/* MgenFlowCommand::GetStatus(flowId) on an item of length len */
+static int flowcmd_status(const uint8_t* b, uint32_t len, uint32_t flow_id)
+{
+    const uint32_t N = (2 * flow_id > 16) ? (2 * flow_id - 16 - 1) / 32 + 1 : 0;
+    const uint32_t need = 2 + 2 + N * 4;
+    if (need > len) return 0;
+    const uint32_t f = flow_id - 1;
+    int st = 0;
+    if (b[2 + (f >> 3)] & (0x80 >> (f & 7))) st = 1;
+    if (b[2 + (len - 2) / 2 + (f >> 3)] & (0x80 >> (f & 7))) st |= 2;
+    return st;
+}
+
+/* MgenTransport::ProcessRecvMessage over one MGEN_DATA payload.  Flow commands with a
+ * status other than FLOW_UNCHANGED go to cmds (flow id << 2 | status); with a controller,
+ * report items (type byte > 0x0f) are parsed and their payload offsets go to reps.  Returns
+ * 0 = walked to the end, 1 = invalid MGEN_DATA payload, 2 = invalid REPORT, 3 = an item of
+ * length 0 (the reference loops forever there; the walk stops). */
+int or_data_walk(const uint8_t* pay, uint32_t len, int controller, uint32_t* cmds,
+                 uint32_t* n_cmds, uint32_t cap_cmds, uint32_t* reps, uint32_t* n_reps,
+                 uint32_t cap_reps)
+{
+    uint32_t off = 0, left = len;
+    *n_cmds = 0;
+    *n_reps = 0;
+    while (left > 0) {
+        const uint8_t* b = pay + off;
+        const uint8_t type = b[0];
+        const uint32_t ilen = left > 1 ? b[1] : 0;   /* MgenDataItem::InitFromBuffer */
+        if (type == 1) {                              /* DATA_ITEM_FLOW_CMD */
+            if (ilen > left) return 1;
+            uint32_t maxf = ilen > 2 ? 8 * (ilen - 2) / 2 : 0;
+            if (maxf > 40) maxf = 40;                 /* MgenEvent::FlowStatus::MAX_FLOW */
+            for (uint32_t i = 1; i <= maxf; i++) {
+                const int st = flowcmd_status(b, ilen, i);
+                if (st && *n_cmds < cap_cmds) cmds[(*n_cmds)++] = i << 2 | (uint32_t)st;
+                else if (st) (*n_cmds)++;
+            }
+            if (ilen == 0) return 3;
+            left -= ilen;
+            off += (ilen / 4) * 4;
+        } else if (controller && type > 0x0f) {
+            or_report_view v;
+            if (!or_report_parse(b, left, &v)) return 2;
+            if (*n_reps < cap_reps) reps[*n_reps] = off;
+            (*n_reps)++;
+            left -= v.length;
+            off += (v.length / 4) * 4;
+        } else {
+            if (ilen > left || ilen == 0) return 3;   /* GetLength() 0: no progress */
+            left -= ilen;
+            off += (ilen / 4) * 4;
+        }
+    }
+    return 0;
+}

@@ -256,4 +256,24 @@ uint32_t or_log_recv_binary(const or_fields* f, const uint8_t* rec, uint64_t ava
 #ifdef __cplusplus
 }
 #endif
+
+/* ---- MGEN_DATA items: Report quantizers / build / parse, REPORT lines, TLV walk ---- */
+uint8_t  or_q_time(double v);
+double   or_uq_time(uint8_t q);
+uint16_t or_q_rate(double r);
+double   or_uq_rate(uint16_t q);
+uint16_t or_q_loss(double l);
+double   or_uq_loss(uint16_t q);
+uint32_t or_report_build(const or_addr* src, const or_addr* dst, uint32_t flow_id, int protocol,
+                         double duration, double lat_ave, double lat_min, double lat_max,
+                         double rate, double loss, double offset, int* sign, uint8_t* b);
+uint32_t or_log_report(const uint8_t* report, double duration, double rate, double loss,
+                       double lat_ave, double lat_min, double lat_max, uint64_t count,
+                       uint32_t sec, uint32_t usec, uint32_t opts, char* out);
+uint32_t or_log_report_recv(const uint8_t* report, const or_addr* reporter, uint32_t sec,
+                            uint32_t usec, uint32_t opts, char* out);
+int      or_data_walk(const uint8_t* pay, uint32_t len, int controller, uint32_t* cmds,
+                      uint32_t* n_cmds, uint32_t cap_cmds, uint32_t* reps, uint32_t* n_reps,
+                      uint32_t cap_reps);
+
 #endif

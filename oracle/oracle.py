@@ -427,3 +427,83 @@ def log_recv_binary(fields, slab, rec_off, src, rx_sec, rx_usec, protocol=1):
                                  int(rx_sec[i]), int(rx_usec[i]), protocol, _ptr(buf))
         out.append(buf[:n].tobytes())
     return b"".join(out)
+
+
+# ---------------------------------------------------------------- MGEN_DATA items
+def _report_protos():
+    L = lib()
+    if getattr(L, "_rep_ready", False):
+        return L
+    P, u32, i32, d = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_double
+    L.or_q_time.argtypes, L.or_q_time.restype = [d], ctypes.c_uint8
+    L.or_uq_time.argtypes, L.or_uq_time.restype = [ctypes.c_uint8], d
+    L.or_q_rate.argtypes, L.or_q_rate.restype = [d], ctypes.c_uint16
+    L.or_uq_rate.argtypes, L.or_uq_rate.restype = [ctypes.c_uint16], d
+    L.or_q_loss.argtypes, L.or_q_loss.restype = [d], ctypes.c_uint16
+    L.or_uq_loss.argtypes, L.or_uq_loss.restype = [ctypes.c_uint16], d
+    L.or_report_build.argtypes = [P, P, u32, i32, d, d, d, d, d, d, d, ctypes.POINTER(i32), P]
+    L.or_report_build.restype = u32
+    L.or_log_report.argtypes = [P, d, d, d, d, d, d, ctypes.c_uint64, u32, u32, u32, P]
+    L.or_log_report.restype = u32
+    L.or_log_report_recv.argtypes = [P, P, u32, u32, u32, P]
+    L.or_log_report_recv.restype = u32
+    L.or_data_walk.argtypes = [P, u32, i32, P, ctypes.POINTER(u32), u32, P, ctypes.POINTER(u32),
+                               u32]
+    L.or_data_walk.restype = i32
+    L._rep_ready = True
+    return L
+
+
+def q_time(v): return int(_report_protos().or_q_time(float(v)))
+def uq_time(q): return float(_report_protos().or_uq_time(int(q)))
+def q_rate(v): return int(_report_protos().or_q_rate(float(v)))
+def uq_rate(q): return float(_report_protos().or_uq_rate(int(q)))
+def q_loss(v): return int(_report_protos().or_q_loss(float(v)))
+def uq_loss(q): return float(_report_protos().or_uq_loss(int(q)))
+
+
+def report_build(src, dst, flow_id, protocol, duration, lat_ave, lat_min, lat_max, rate, loss,
+                 offset=0.0, sign=0):
+    """report_msg bytes after a window close (+ GetReport): returns (bytes, sign after)."""
+    L = _report_protos()
+    s = np.ascontiguousarray(np.asarray(src, ADDR_DTYPE).reshape(1))
+    t = np.ascontiguousarray(np.asarray(dst, ADDR_DTYPE).reshape(1))
+    b = np.zeros(52, np.uint8)
+    sg = ctypes.c_int(sign)
+    n = L.or_report_build(_ptr(s), _ptr(t), flow_id, protocol, duration, lat_ave, lat_min,
+                          lat_max, rate, loss, offset, ctypes.byref(sg), _ptr(b))
+    return b[:n].tobytes(), sg.value
+
+
+def log_report(report, duration, rate, loss, lat_ave, lat_min, lat_max, count, sec, usec,
+               opts=0):
+    L = _report_protos()
+    r = np.zeros(52, np.uint8)
+    r[:len(report)] = np.frombuffer(report, np.uint8)
+    out = np.zeros(512, np.uint8)
+    n = L.or_log_report(_ptr(r), duration, rate, loss, lat_ave, lat_min, lat_max, count, sec,
+                        usec, opts, _ptr(out))
+    return out[:n].tobytes()
+
+
+def log_report_recv(report, reporter, sec, usec, opts=0):
+    L = _report_protos()
+    r = np.zeros(52, np.uint8)
+    r[:len(report)] = np.frombuffer(report, np.uint8)
+    a = np.ascontiguousarray(np.asarray(reporter, ADDR_DTYPE).reshape(1))
+    out = np.zeros(512, np.uint8)
+    n = L.or_log_report_recv(_ptr(r), _ptr(a), sec, usec, opts, _ptr(out))
+    return out[:n].tobytes()
+
+
+def data_walk(payload: bytes, controller=True, cap=4096):
+    """ProcessRecvMessage over one MGEN_DATA payload: (status, [(flow, status)], [offsets])."""
+    L = _report_protos()
+    p = np.frombuffer(bytes(payload) + b"\0" * 4, np.uint8).copy()
+    cmds = np.zeros(cap, np.uint32)
+    reps = np.zeros(cap, np.uint32)
+    nc, nr = ctypes.c_uint32(0), ctypes.c_uint32(0)
+    st = L.or_data_walk(_ptr(p), len(payload), int(controller), _ptr(cmds), ctypes.byref(nc), cap,
+                        _ptr(reps), ctypes.byref(nr), cap)
+    c = [(int(x) >> 2, int(x) & 3) for x in cmds[:min(nc.value, cap)]]
+    return st, c, [int(x) for x in reps[:min(nr.value, cap)]]
