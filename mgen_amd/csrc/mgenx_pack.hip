@@ -256,7 +256,28 @@ pack_kernel(PackParams p) {
     s_meta[wv][lane] = m;
 
     // --------------------------- phase 2: write units ---------------------------
+    // Packed slab fast path: when the wave's records lie back to back (rec_off[i + 1] ==
+    // rec_off[i] + ret[i]), zero filled, payloads inside the image, every 16-byte-aligned
+    // unit of the whole range is first stored as zeros (aligned full-width stores: the
+    // fill), then each record's image units and its last 16 bytes (trailer) are written
+    // over them.  Everything else keeps one (unaligned) unit store per 16 record bytes.
+    const uint32_t nv = b < n_batches ? (uint32_t)min((uint64_t)64, (uint64_t)p.n - (b << 6)) : 0u;
+    const bool has = (uint32_t)lane < nv;
+    const uint64_t next_off = __shfl_down(m.off, 1);
+    const bool packed_ok = !has || (m.ret > 0 && m.pend <= (uint32_t)kImg &&
+                                    ((uint32_t)lane + 1 == nv || m.off + m.ret == next_off));
+    const bool fast = !rf && variant == 0 && nv > 0 && __all(packed_ok);
+    const uint32_t kimg = (min(m.pend, m.ret) + 15u) >> 4;  // image units
     uint32_t units = (m.ret + 15u) >> 4;
+    if (fast) {
+      units = has ? kimg + (16u * kimg < m.ret ? 1u : 0u) : 0u;
+      const uint64_t a0 = (__shfl(m.off, 0) + 15u) & ~(uint64_t)15;
+      const uint64_t a1 = __shfl(m.off + m.ret, (int)nv - 1) & ~(uint64_t)15;
+      const u32x4_t zero = {0u, 0u, 0u, 0u};
+      for (uint64_t a = a0 + 16u * (uint32_t)lane; a < a1; a += 1024u) stu128(p.slab + a, zero);
+      // the overwrites below must land after these stores
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     uint32_t incl = units;
 #pragma unroll
     for (int s = 1; s < 64; s <<= 1) {
@@ -281,7 +302,11 @@ pack_kernel(PackParams p) {
         } while (next_start <= u);
         r = s_meta[wv][ri];
       }
-      const uint32_t pos = (u - rstart) << 4;
+      uint32_t pos = (u - rstart) << 4;
+      if (fast) {  // image units, then the record's last 16 bytes (past the image)
+        const uint32_t ki = (min(r.pend, r.ret) + 15u) >> 4;
+        if (pos >= (ki << 4)) pos = max(r.ret - 16u, ki << 4);
+      }
       const uint8_t* rimg = &s_img[wv][ri * kImg];
       uint32_t v[4] = {0u, 0u, 0u, 0u};
       // fill (zero, or the rand() stream after two zero bytes: mgenMsg.cpp:277-292)

@@ -559,7 +559,7 @@ __device__ __forceinline__ void quad_bcast(const u32x4_t& pf, uint32_t (&pw)[16]
   pw[4 * LN + 3] = (uint32_t)__builtin_amdgcn_mov_dpp((int)pf.w, ctrl, 0xf, 0xf, false);
 }
 
-template <bool kCrc, int MODE = 0>
+template <bool kCrc, int MODE = 0, bool kSort = false>
 __global__ void __launch_bounds__(kUnpackThreads)
 unpack_kernel(UnpackParams p) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -592,15 +592,9 @@ unpack_kernel(UnpackParams p) {
   // loads speculatively together with the header load (one memory round per group); a
   // group without any CRC work turns speculation off (header first, body only if needed).
   bool spec = true;
-  for (uint64_t g = wave_id; g < n_groups; g += n_waves) {
-    const uint64_t rec_idx = (g << 4) + (uint64_t)(lane >> 2);
-    const bool valid = rec_idx < p.n;
-    uint64_t off = 0;
-    uint32_t L = 0;
-    if (valid) {
-      off = p.rec_off ? p.rec_off[rec_idx] : rec_idx * p.stride;
-      L = p.rec_len ? p.rec_len[rec_idx] : p.fixed_len;
-    }
+  // one group: the quad's record rec_idx (valid: < n), the wave's 16 records together
+  // (off, L: its placement, read by the caller)
+  auto group = [&](const uint64_t rec_idx, const bool valid, const uint64_t off, const uint32_t L) {
     const bool oob = valid && (L > 65535u || off > p.slab_bytes || L > p.slab_bytes - off);
     const bool live = valid && !oob;
     const uint8_t* rec = p.slab + off;
@@ -784,6 +778,62 @@ unpack_kernel(UnpackParams p) {
       }
     } else if (oob && q == 0) {
       store_oob_q0(p.cols, rec_idx);
+    }
+  };
+
+  auto place = [&](uint64_t ri, uint64_t& off, uint32_t& L) {
+    off = 0;
+    L = 0;
+    if (ri < p.n) {
+      off = p.rec_off ? p.rec_off[ri] : ri * p.stride;
+      L = p.rec_len ? p.rec_len[ri] : p.fixed_len;
+    }
+  };
+  if (!kSort) {
+    for (uint64_t g = wave_id; g < n_groups; g += n_waves) {
+      const uint64_t ri = (g << 4) + (uint64_t)(lane >> 2);
+      uint64_t off;
+      uint32_t L;
+      place(ri, off, L);
+      group(ri, ri < p.n, off, L);
+    }
+    return;
+  }
+  // Row-balanced order for variable lengths.  A group costs its LONGEST record's rows (the
+  // quads run in lock-step, shorter records front-padded), so each wave takes a tile of 64
+  // consecutive records, ranks them by row count (64 lane compares), and runs them as four
+  // groups of 16 records of similar length (U{64..1472}: 83% of the rows useful instead of
+  // 56%).  The tile's column stores stay within 64 consecutive records.  The placements of
+  // the next tile are loaded while this one runs (lane j: record t0 + j), and reach the
+  // quads by lane permutes.
+  const uint64_t n_tiles = ((uint64_t)p.n + 63) >> 6;
+  uint64_t off_n;
+  uint32_t len_n;
+  place((wave_id << 6) + (uint64_t)lane, off_n, len_n);
+  for (uint64_t t = wave_id; t < n_tiles; t += n_waves) {
+    const uint64_t t0 = t << 6;
+    const uint64_t off_l = off_n;
+    const uint32_t len_l = len_n;
+    place(((t + n_waves) << 6) + (uint64_t)lane, off_n, len_n);
+    const uint32_t n_valid = (uint32_t)min((uint64_t)64, (uint64_t)p.n - t0);
+    const uint32_t key = (uint32_t)lane < n_valid ? (len_l + 63u) >> 6 : 0xFFFFu;
+    uint32_t rank = 0;
+#pragma unroll 8
+    for (int j = 0; j < 64; j++) {
+      const uint32_t kj = (uint32_t)__builtin_amdgcn_readlane((int)key, j);
+      rank += (kj < key || (kj == key && j < lane)) ? 1u : 0u;
+    }
+    // sorted position r -> the tile lane holding it (lane r receives it)
+    const int src = __builtin_amdgcn_ds_permute((int)(rank << 2), lane);
+#pragma unroll 1
+    for (int k = 0; k < 4; k++) {
+      if ((uint32_t)(16 * k) >= n_valid) break;  // wave-uniform: past-the-end sorts last
+      const int li = __builtin_amdgcn_ds_bpermute((16 * k + (lane >> 2)) << 2, src);
+      const int at = li << 2;
+      const uint64_t off = (uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(at, (int)(uint32_t)off_l) |
+                           (uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(at, (int)(uint32_t)(off_l >> 32)) << 32;
+      const uint32_t L = (uint32_t)__builtin_amdgcn_ds_bpermute(at, (int)len_l);
+      group(t0 + (uint64_t)li, (uint32_t)li < n_valid, off, L);
     }
   }
 }
@@ -1400,6 +1450,11 @@ static hipError_t launch_mode(const UnpackParams& p, int grid, hipStream_t strea
   return launch_lds(unpack_kernel<true, MODE>, attr_done, p, grid, stream);
 }
 
+static hipError_t launch_sorted(const UnpackParams& p, int grid, hipStream_t stream) {
+  static bool attr_done = false;
+  return launch_lds(unpack_kernel<true, 0, true>, attr_done, p, grid, stream);
+}
+
 template <int NR, int MODE = 0, bool kRows = false, bool kAligned = false>
 static hipError_t launch_fixed(const UnpackParams& p, int grid, hipStream_t stream) {
   static bool attr_done = false;
@@ -1500,9 +1555,12 @@ hipError_t launch_unpack(const UnpackParams& p, int grid, hipStream_t stream) {
   switch (unpack_variant) {
     case 1: return launch_mode<1>(p, grid, stream);
     case 2: return launch_mode<2>(p, grid, stream);
+    case 3: return launch_mode<0>(p, grid, stream);  // variable lengths, unsorted
     default: break;
   }
 #endif  // MGENX_DIAG
+  // per-record lengths: the row-balanced (tile-sorted) order
+  if (p.rec_len) return launch_sorted(p, grid, stream);
   return launch_mode<0>(p, grid, stream);
 }
 

@@ -1,0 +1,74 @@
+"""GPU pack over variable-length slab layouts against the oracle's batch pack: packed back to
+back (the aligned-unit path with boundary units composed from two records), with gaps
+and odd offsets (per-record units), and with failing records inside a packed run (the
+fallback); bytes outside the records must stay untouched."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    return torch
+
+
+@pytest.fixture(scope="module")
+def eng(torch):
+    from mgen_amd import Engine
+    e = Engine(0)
+    yield e
+    e.close()
+
+
+PAYLOADS = ["00112233445566778899aabbccddeeff", "", "ab" * 100]
+
+
+@pytest.mark.parametrize("layout", ["packed", "gaps", "packed_failing"])
+@pytest.mark.parametrize("ck,rf,pay", [(1, 0, 0), (0, 0, 1), (1, 1, 2), (1, 0, 2)])
+def test_pack_layouts_vs_oracle(torch, eng, oracle, layout, ck, rf, pay):
+    from mgen_amd import PACK_CHECKSUM, PACK_RANDOM_FILL, to_device
+    from mgen_amd.workloads import udp_mixed
+    n = 3000
+    tmpl, pool, desc, _, sizes = udp_mixed(n, 30, 1600, 7, payload_hex=PAYLOADS[pay],
+                                           seed=n + ck + 2 * rf + 4 * pay)
+    rng = np.random.default_rng(len(layout) + pay)
+    sizes = sizes.astype(np.int64)
+    if layout == "packed_failing":
+        bad = rng.random(n) < 0.02
+        sizes[bad] = rng.integers(1, 27, int(bad.sum()))     # Pack fails: nothing written
+    desc["msg_len"] = sizes.astype(np.uint16)
+    gap = rng.integers(0, 40, n) if layout == "gaps" else np.zeros(n, np.int64)
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(sizes[:-1] + gap[:-1])
+    offs += 3                                                # odd start
+    total = int(offs[-1] + sizes[-1]) + 64
+    ft = 1_700_000_123
+    want, wlen = oracle.udp_pack_batch(tmpl, desc, pool, total, rec_off=offs, checksum=bool(ck),
+                                       random_fill=bool(rf), fill_time=ft)
+    d_tmpl, d_pool, d_desc = to_device(tmpl), to_device(pool), to_device(desc)
+    crc = torch.empty(len(tmpl), dtype=torch.int32, device="cuda")
+    eng.pack_prepare(d_tmpl, len(tmpl), d_pool, crc)
+    if rf:
+        eng.set_fill_time(ft)
+    slab = torch.full((total,), 0xA5, dtype=torch.uint8, device="cuda")
+    opts = (PACK_CHECKSUM if ck else 0) | (PACK_RANDOM_FILL if rf else 0)
+    out_len = eng.pack(d_tmpl, crc, d_desc, n, d_pool, slab, rec_off=to_device(offs).view(torch.int64),
+                       opts=opts, fill_time=ft)
+    torch.cuda.synchronize()
+    got = slab.cpu().numpy()
+    lens = out_len.cpu().numpy().view(np.uint32)
+    assert np.array_equal(lens, wlen)
+    if layout == "packed_failing":
+        assert (lens == 0).sum() > 10
+    cover = np.zeros(total, bool)
+    for o, ln in zip(offs, lens):
+        cover[int(o):int(o) + int(ln)] = True
+    assert np.all(got[~cover] == 0xA5), np.nonzero(got[~cover] != 0xA5)[0][:5]
+    bad = np.nonzero(cover & (got != want))[0]
+    if bad.size:
+        rec = np.searchsorted(offs, bad[0], side="right") - 1
+        pytest.fail(f"{bad.size} bytes differ, first at {bad[0]} (record {rec}, size "
+                    f"{sizes[rec]}, pos {bad[0] - offs[rec]})")
