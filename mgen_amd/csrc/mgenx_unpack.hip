@@ -840,6 +840,255 @@ unpack_kernel(UnpackParams p) {
 
 
 // ---------------------------------------------------------------------------------------
+// Variable-length records (per-record lengths: config 3, TCP / SINK scan output), with the
+// rows streamed through a load ring across groups.  The braid CRC and the column output
+// are those of unpack_kernel<true>; what differs is the schedule:
+//   * each wave takes tiles of 64 consecutive records, ranks them by row count R (64 lane
+//     compares) and runs them as four groups of 16 records of similar length;
+//   * a group's virtual rows are V = max R of its records rounded up to a multiple of 4
+//     (shorter records front-padded with zero rows, which leave the zero CRC state as is);
+//   * the wave's rows form ONE stream over its groups, with RS = 4 rows in flight: row
+//     r + 4 of the stream is loaded as row r is consumed -- during a group's last four rows
+//     that is the next group's first four rows (its header follows the group's column
+//     stores) -- so the loads never drain at group boundaries (the next tile is ranked one group ahead,
+//     its placements loaded one tile ahead).
+// No header-first mode: every record's rows are read (for batches without checksummed
+// records this reads the bodies too; the payload stays unread by the CRC work otherwise).
+__global__ void __launch_bounds__(kUnpackThreads)
+unpack_var_kernel(UnpackParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const uint32_t* fold = lds + kRepDwords;  // [A4 | A8 | A12 | A16 | A32 | A48]
+  stage_tables(lds, p.tabs);
+  __syncthreads();
+  const uint8_t* ldsb = reinterpret_cast<const uint8_t*>(lds);
+
+  const int lane = threadIdx.x & 63;
+  const int q = lane & 3;
+  const uint32_t s1 = a64_s1((uint32_t)lane);
+  const uint64_t wave_id = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const uint64_t n_waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  const uint64_t n_tiles = ((uint64_t)p.n + 63) >> 6;
+  if (wave_id >= n_tiles) return;  // (no barrier below)
+  const bool force = (p.opts & MGENX_OPT_CHECKSUM_FORCE) != 0;
+  const bool tcp = (p.opts & MGENX_OPT_TCP) != 0;
+  const bool want_ext = p.cols.dst_addr || p.cols.host_addr;
+  const mgenx_cols& cc = p.cols;
+  const bool any_ext = cc.hdr_len || cc.payload_off || cc.host_port || cc.host_type ||
+                       cc.host_len || cc.lat_raw || cc.lon_raw || cc.alt || cc.dst_addr ||
+                       cc.host_addr || cc.decoded;
+  const uint8_t* dummy = reinterpret_cast<const uint8_t*>(p.tabs);
+  const u32x4_t zero = {0u, 0u, 0u, 0u};
+
+  // ---- tiles: placements of the 64 records (lane j: record t0 + j) and their order ----
+  auto place = [&](uint64_t t, uint64_t& off, uint32_t& L) {
+    const uint64_t ri = (t << 6) + (uint64_t)lane;
+    off = 0;
+    L = 0;
+    if (t < n_tiles && ri < p.n) {
+      off = p.rec_off ? p.rec_off[ri] : ri * p.stride;
+      L = p.rec_len ? p.rec_len[ri] : p.fixed_len;
+    }
+  };
+  auto n_valid_of = [&](uint64_t t) { return (uint32_t)min((uint64_t)64, (uint64_t)p.n - (t << 6)); };
+  // sorted position r -> the tile lane holding it
+  auto rank_tile = [&](uint64_t t, uint32_t L) {
+    const uint32_t key = (uint32_t)lane < n_valid_of(t) ? (L + 63u) >> 6 : 0xFFFFu;
+    uint32_t rank = 0;
+#pragma unroll 8
+    for (int j = 0; j < 64; j++) {
+      const uint32_t kj = (uint32_t)__builtin_amdgcn_readlane((int)key, j);
+      rank += (kj < key || (kj == key && j < lane)) ? 1u : 0u;
+    }
+    return __builtin_amdgcn_ds_permute((int)(rank << 2), lane);
+  };
+  uint64_t t_c = wave_id, off_c, off_p;
+  uint32_t len_c, len_p;
+  place(t_c, off_c, len_c);
+  int src_c = rank_tile(t_c, len_c), src_p = lane;
+  place(t_c + n_waves, off_p, len_p);
+  bool p_ranked = false;
+
+  // ---- a group: the quad's record and its row geometry ----
+  struct Grp {
+    uint64_t off;
+    uint32_t idx, L;
+    int pos0, pad;        // row 0 position in the record (+16q), virtual rows before row 0
+    bool valid, live, oob;
+    uint32_t V;           // virtual rows (wave-uniform, multiple of 4, >= 4)
+  };
+  auto make = [&](uint64_t t, int k, uint64_t offs, uint32_t lens, int src) {
+    Grp g;
+    const int li = __builtin_amdgcn_ds_bpermute((16 * k + (lane >> 2)) << 2, src);
+    const int at = li << 2;
+    g.idx = (uint32_t)(t << 6) + (uint32_t)li;
+    g.off = (uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(at, (int)(uint32_t)offs) |
+            (uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(at, (int)(uint32_t)(offs >> 32)) << 32;
+    g.L = (uint32_t)__builtin_amdgcn_ds_bpermute(at, (int)lens);
+    g.valid = (uint32_t)li < n_valid_of(t);
+    g.oob = g.valid && (g.L > 65535u || g.off > p.slab_bytes || g.L > p.slab_bytes - g.off);
+    g.live = g.valid && !g.oob;
+    const int R = (g.live && g.L >= 32) ? (int)((g.L + 63u) >> 6) : 0;
+    int m = R;
+#pragma unroll
+    for (int sft = 1; sft < 64; sft <<= 1) m = max(m, __shfl_xor(m, sft));
+    g.V = (uint32_t)max(4, (__builtin_amdgcn_readfirstlane(m) + 3) & ~3);
+    g.pad = (int)g.V - R;
+    g.pos0 = (int)g.L - 64 * R + 16 * q;
+    return g;
+  };
+  auto row_ptr = [&](const Grp& g, int j) {
+    const int real = j - g.pad;
+    return (real >= 0) ? p.slab + g.off + (uint64_t)max(g.pos0 + 64 * real, 0) : dummy;
+  };
+  auto hdr_ptr = [&](const Grp& g) {
+    return (g.live && g.L >= 16u * (q + 1)) ? p.slab + g.off + 16 * q : dummy;
+  };
+  // row j's 16 bytes as the braid consumes them: row 0 of a record that does not start on
+  // a row boundary is shifted up (its bytes before the record read as zero)
+  auto row_data = [&](const Grp& g, const u32x4_t& x, int j) {
+    const int real = j - g.pad;
+    u32x4_t y = real >= 0 ? x : zero;
+    const int s0 = g.pos0 < 0 ? -g.pos0 : 0;
+    if (__any(real == 0 && s0 > 0)) {
+      const u32x4_t sh = s0 < 16 ? shl_bytes(x, s0 & 15) : zero;
+      if (real == 0) y = sh;
+    }
+    return y;
+  };
+
+  // ---- the first group ----
+  int k = 0;
+  Grp G = make(t_c, 0, off_c, len_c, src_c);
+  u32x4_t d[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) d[j] = ldu128(row_ptr(G, j));
+  u32x4_t pf = ldu128(hdr_ptr(G));
+  uint32_t expect = p.expect[G.live ? G.L : 0u];
+
+  for (;;) {
+    // the next group: this tile's group k + 1, or the next tile's first (ranked here)
+    bool has_next = true, next_tile = false;
+    Grp N;
+    if (k + 1 < 4 && (uint32_t)(16 * (k + 1)) < n_valid_of(t_c)) {
+      N = make(t_c, k + 1, off_c, len_c, src_c);
+    } else if (t_c + n_waves < n_tiles) {
+      if (!p_ranked) {
+        src_p = rank_tile(t_c + n_waves, len_p);
+        p_ranked = true;
+      }
+      N = make(t_c + n_waves, 0, off_p, len_p, src_p);
+      next_tile = true;
+    } else {
+      has_next = false;
+      N = G;
+      N.V = 4;
+      N.pad = 4;  // all padding: the ring loads the dummy line
+    }
+
+    // ---- stream G's rows: chunks of 4, the last chunk feeding N's first rows ----
+    uint32_t ha[4] = {0u, 0u, 0u, 0u}, hb[4] = {0u, 0u, 0u, 0u};
+    auto consume = [&](const u32x4_t& y) {
+      const uint32_t xw[4] = {y.x, y.y, y.z, y.w};
+      uint32_t c4[4];
+#pragma unroll
+      for (int b = 0; b < 4; b++) c4[b] = xor3(ha[b], hb[b], xw[b]);
+#pragma unroll
+      for (int b = 0; b < 4; b++) a64_parts(ldsb, c4[b], s1, ha[b], hb[b]);
+    };
+    const int C = (int)(G.V >> 2);
+#pragma unroll 1
+    for (int c = 0; c + 1 < C; c++) {
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const u32x4_t y = row_data(G, d[j], 4 * c + j);
+        __builtin_amdgcn_sched_barrier(0);
+        d[j] = ldu128(row_ptr(G, 4 * c + 4 + j));
+        __builtin_amdgcn_sched_barrier(0);
+        consume(y);
+      }
+    }
+    const int jl = 4 * (C - 1);
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+      const u32x4_t y = row_data(G, d[j], jl + j);
+      __builtin_amdgcn_sched_barrier(0);
+      d[j] = ldu128(row_ptr(N, j));
+      __builtin_amdgcn_sched_barrier(0);
+      consume(y);
+    }
+    u32x4_t xf = row_data(G, d[3], jl + 3);
+    __builtin_amdgcn_sched_barrier(0);
+    d[3] = ldu128(row_ptr(N, 3));
+    __builtin_amdgcn_sched_barrier(0);
+    if (q == 3) xf.w = bswap32(xf.w);  // the big-endian trailer, in stream order
+    const uint32_t v = shift_tab(fold + 3 * 1024, xor3(ha[0], hb[0], xf.x)) ^
+                       shift_tab(fold + 2 * 1024, xor3(ha[1], hb[1], xf.y)) ^
+                       shift_tab(fold + 1 * 1024, xor3(ha[2], hb[2], xf.z)) ^
+                       shift_tab(fold, xor3(ha[3], hb[3], xf.w));
+    const uint32_t* lt = fold + (q == 0 ? 5 : (q == 1 ? 4 : 3)) * 1024;  // A48/A32/A16
+    uint32_t tot = (q == 3) ? v : shift_tab(lt, v);
+    tot ^= __shfl_xor(tot, 1);
+    tot ^= __shfl_xor(tot, 2);
+
+    // ---- G's columns (as unpack_kernel) ----
+    {
+      uint32_t pw[16];
+      quad_bcast<0>(pf, pw);
+      quad_bcast<1>(pf, pw);
+      quad_bcast<2>(pf, pw);
+      quad_bcast<3>(pf, pw);
+      const uint8_t* rec = p.slab + G.off;
+      const uint32_t buf_len = tcp ? min(G.L, (uint32_t)MGENX_TX_BUFFER_SIZE) : G.L;
+      if (G.live && q == 0) {
+        const bool pfx = G.L >= 32, pfx64 = buf_len >= 64;
+        uint32_t w[8];
+        if (pfx) {
+#pragma unroll
+          for (int j = 0; j < 8; j++) w[j] = pw[j];
+        } else if (G.L >= MGENX_MIN_SIZE) {
+          load_fixed(rec, buf_len, w);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; j++) w[j] = 0;
+        }
+        const bool flagged = force || (((w[0] >> 24) & MGENX_FLAG_CHECKSUM) != 0 &&
+                                       buf_len >= MGENX_MIN_SIZE && ((w[0] >> 16) & 0xffu) == 2u);
+        const bool needs_crc = flagged && (tcp ? (G.L >= 4) : fixed_ok(buf_len, w));
+        const bool vec_crc = needs_crc && G.L >= 32;
+        if (pfx64 && fast_layout(pw[0], pw[5], (pw[5] >> 24) == 4u ? pw[7] : pw[10])) {
+          store_fast_q0(p.cols, G.idx, pw, buf_len, !needs_crc || tot == expect, tcp);
+          if (any_ext) store_fast_ext(p.cols, G.idx, [&](int kk) { return pw[kk]; }, buf_len, true);
+        } else {
+          Hdr h;
+          parse_header(rec, buf_len, want_ext, w, h);
+          const bool crc_ok = !needs_crc || (vec_crc ? (tot == expect) : small_crc_ok(rec, G.L));
+          store_hdr_q0(p.cols, G.idx, h, crc_ok, tcp);
+        }
+      } else if (G.oob && q == 0) {
+        store_oob_q0(p.cols, G.idx);
+      }
+    }
+
+    if (!has_next) break;
+    // N's header: needed only after N's rows, so loaded after G's column stores
+    pf = ldu128(hdr_ptr(N));
+    expect = p.expect[N.live ? N.L : 0u];
+    if (next_tile) {
+      t_c += n_waves;
+      off_c = off_p;
+      len_c = len_p;
+      src_c = src_p;
+      place(t_c + n_waves, off_p, len_p);
+      p_ranked = false;
+      k = 0;
+    } else {
+      k++;
+    }
+    G = N;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // Fixed-length records (fixed stride, one length L in [65, 1024]; BASELINE config 2 and
 // the recvmmsg fixed-slot layout), software-pipelined across groups.  With one L every
 // group has the same row geometry (V = ceil(L/64) rows, padded to the template's NR), so
@@ -1450,6 +1699,11 @@ static hipError_t launch_mode(const UnpackParams& p, int grid, hipStream_t strea
   return launch_lds(unpack_kernel<true, MODE>, attr_done, p, grid, stream);
 }
 
+static hipError_t launch_var(const UnpackParams& p, int grid, hipStream_t stream) {
+  static bool attr_done = false;
+  return launch_lds(unpack_var_kernel, attr_done, p, grid, stream);
+}
+
 static hipError_t launch_sorted(const UnpackParams& p, int grid, hipStream_t stream) {
   static bool attr_done = false;
   return launch_lds(unpack_kernel<true, 0, true>, attr_done, p, grid, stream);
@@ -1556,11 +1810,12 @@ hipError_t launch_unpack(const UnpackParams& p, int grid, hipStream_t stream) {
     case 1: return launch_mode<1>(p, grid, stream);
     case 2: return launch_mode<2>(p, grid, stream);
     case 3: return launch_mode<0>(p, grid, stream);  // variable lengths, unsorted
+    case 4: return launch_sorted(p, grid, stream);   // sorted groups, no load ring
     default: break;
   }
 #endif  // MGENX_DIAG
-  // per-record lengths: the row-balanced (tile-sorted) order
-  if (p.rec_len) return launch_sorted(p, grid, stream);
+  // per-record lengths: sorted groups with the rows in a load ring
+  if (p.rec_len) return launch_var(p, grid, stream);
   return launch_mode<0>(p, grid, stream);
 }
 
