@@ -546,6 +546,39 @@ __device__ __forceinline__ void store_core_quad(const UnpackParams& p, uint64_t 
   st_g8(at(u8b, 1), (q & 1) == 0 ? v.ptype : v.gps);
 }
 
+// store_core_quad with the per-lane field picked by AND/OR masks over scalars (a select
+// chain over a struct can be folded back into a dynamic index, which puts it in scratch)
+__device__ __forceinline__ void store_core_quad_m(const UnpackParams& p, uint64_t idx, bool in,
+                                                  int lane, int q, const Core& v) {
+  const uint32_t m0 = 0u - (uint32_t)(q == 0), m1 = 0u - (uint32_t)(q == 1);
+  const uint32_t m2 = 0u - (uint32_t)(q == 2), m3 = 0u - (uint32_t)(q == 3);
+  auto pick = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    return (a & m0) | (b & m1) | (c & m2) | (d & m3);
+  };
+  const uint64_t sink = (uint64_t)p.sink + 8u * (uint32_t)lane;
+  if (p.cols.rows) {
+    const uint32_t lo = pick(v.flow, v.sec, v.dst4, (v.plen & 0xffffu) | v.flags << 16 | v.err << 24);
+    const uint32_t hi = pick(v.seq, v.usec, (v.msg_len & 0xffffu) | v.dport << 16,
+                             v.dtype | v.dlen << 8 | v.ptype << 16 | v.gps << 24);
+    st_g64(in ? (uint64_t)p.cols.rows + idx * 32 + 8u * q : sink, (uint64_t)hi << 32 | lo);
+    return;
+  }
+  const mgenx_cols& c = p.cols;
+  const uint64_t a32 = pick4(q, (uint64_t)c.flow_id, (uint64_t)c.seq_num, (uint64_t)c.tx_sec,
+                             (uint64_t)c.tx_usec);
+  const uint64_t a16 = pick4(q, (uint64_t)c.msg_len, (uint64_t)c.dst_port,
+                             (uint64_t)c.payload_len, (uint64_t)c.payload_len);
+  const uint64_t a8a = pick4(q, (uint64_t)c.flags, (uint64_t)c.err, (uint64_t)c.dst_type,
+                             (uint64_t)c.dst_len);
+  const uint64_t a8b = pick4(q, (uint64_t)c.payload_type, (uint64_t)c.gps_status,
+                             (uint64_t)c.payload_type, (uint64_t)c.gps_status);
+  st_g32(in ? a32 + idx * 4 : sink, pick(v.flow, v.seq, v.sec, v.usec));
+  st_g32(in ? (uint64_t)c.dst_addr4 + idx * 4 : sink, v.dst4);
+  st_g16(in ? a16 + idx * 2 : sink, pick(v.msg_len, v.dport, v.plen, v.plen));
+  st_g8(in ? a8a + idx : sink, pick(v.flags, v.err, v.dtype, v.dlen));
+  st_g8(in ? a8b + idx : sink, pick(v.ptype, v.gps, v.ptype, v.gps));
+}
+
 // MODE (diagnostic ablations, never the product path): 0 = full kernel, 1 = row loads +
 // XOR only (no LDS table lookups), 2 = table lookups on one L1-resident row (no streaming).
 // pw[4*LN .. 4*LN+3] = quad lane LN's 16-byte prefix chunk (DPP quad_perm broadcast; all
@@ -1039,10 +1072,36 @@ unpack_var_kernel(UnpackParams p) {
       quad_bcast<3>(pf, pw);
       const uint8_t* rec = p.slab + G.off;
       const uint32_t buf_len = tcp ? min(G.L, (uint32_t)MGENX_TX_BUFFER_SIZE) : G.L;
-      if (G.live && q == 0) {
-        const bool pfx = G.L >= 32, pfx64 = buf_len >= 64;
+      // fast layouts: every quad lane derives the fields from the prefix words and the
+      // quad stores them branch-free (lane q: column group q); other records: quad lane 0
+      const uint32_t D = pw[5] >> 24;
+      const uint32_t hw = (D == 4u) ? pw[7] : pw[10];
+      const bool fast = G.live && buf_len >= 64 && fast_layout(pw[0], pw[5], hw);
+      {
+        const uint32_t gi = (28u + D + (hw >> 24)) >> 2;
+        const uint32_t g3 = (pw[11] & (0u - (uint32_t)(gi == 8u))) |
+                            (pw[12] & (0u - (uint32_t)(gi == 9u))) |
+                            (pw[14] & (0u - (uint32_t)(gi == 11u))) |
+                            (pw[15] & (0u - (uint32_t)(gi == 12u)));
+        const uint32_t hl = 44u + D + (hw >> 24);
+        Core v;
+        v.plen = bswap16((uint16_t)(g3 >> 16));
+        if (!(v.plen != 0 && hl + v.plen <= buf_len)) v.plen = 0;  // mgenMsg.cpp:488-497
+        const bool needs_crc = force || (((pw[0] >> 24) & MGENX_FLAG_CHECKSUM) != 0);
+        uint8_t flags = (uint8_t)(pw[0] >> 24), err = 0;
+        crc_verdict(!needs_crc || tot == expect, tcp, err, flags);
+        v.flow = bswap32(pw[1]); v.seq = bswap32(pw[2]); v.sec = bswap32(pw[3]);
+        v.usec = bswap32(pw[4]); v.dst4 = pw[6];
+        v.msg_len = bswap16((uint16_t)(pw[0] & 0xffffu));
+        v.dport = bswap16((uint16_t)(pw[5] & 0xffffu));
+        v.flags = flags; v.err = err; v.dtype = (pw[5] >> 16) & 0xffu; v.dlen = D;
+        v.ptype = (g3 >> 8) & 0xffu; v.gps = g3 & 0xffu;
+        store_core_quad_m(p, G.idx, fast, lane, q, v);
+      }
+      if (fast && any_ext) store_fast_ext(p.cols, G.idx, [&](int kk) { return pw[kk]; }, buf_len, q == 0);
+      if (!fast && G.live && q == 0) {
         uint32_t w[8];
-        if (pfx) {
+        if (G.L >= 32) {
 #pragma unroll
           for (int j = 0; j < 8; j++) w[j] = pw[j];
         } else if (G.L >= MGENX_MIN_SIZE) {
@@ -1055,15 +1114,10 @@ unpack_var_kernel(UnpackParams p) {
                                        buf_len >= MGENX_MIN_SIZE && ((w[0] >> 16) & 0xffu) == 2u);
         const bool needs_crc = flagged && (tcp ? (G.L >= 4) : fixed_ok(buf_len, w));
         const bool vec_crc = needs_crc && G.L >= 32;
-        if (pfx64 && fast_layout(pw[0], pw[5], (pw[5] >> 24) == 4u ? pw[7] : pw[10])) {
-          store_fast_q0(p.cols, G.idx, pw, buf_len, !needs_crc || tot == expect, tcp);
-          if (any_ext) store_fast_ext(p.cols, G.idx, [&](int kk) { return pw[kk]; }, buf_len, true);
-        } else {
-          Hdr h;
-          parse_header(rec, buf_len, want_ext, w, h);
-          const bool crc_ok = !needs_crc || (vec_crc ? (tot == expect) : small_crc_ok(rec, G.L));
-          store_hdr_q0(p.cols, G.idx, h, crc_ok, tcp);
-        }
+        Hdr h;
+        parse_header(rec, buf_len, want_ext, w, h);
+        const bool crc_ok = !needs_crc || (vec_crc ? (tot == expect) : small_crc_ok(rec, G.L));
+        store_hdr_q0(p.cols, G.idx, h, crc_ok, tcp);
       } else if (G.oob && q == 0) {
         store_oob_q0(p.cols, G.idx);
       }
@@ -1704,10 +1758,12 @@ static hipError_t launch_var(const UnpackParams& p, int grid, hipStream_t stream
   return launch_lds(unpack_var_kernel, attr_done, p, grid, stream);
 }
 
+#if MGENX_DIAG
 static hipError_t launch_sorted(const UnpackParams& p, int grid, hipStream_t stream) {
   static bool attr_done = false;
   return launch_lds(unpack_kernel<true, 0, true>, attr_done, p, grid, stream);
 }
+#endif
 
 template <int NR, int MODE = 0, bool kRows = false, bool kAligned = false>
 static hipError_t launch_fixed(const UnpackParams& p, int grid, hipStream_t stream) {

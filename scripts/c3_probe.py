@@ -34,7 +34,7 @@ def run(eng, name, sizes_fn):
                             opts=PACK_CHECKSUM, out_len=out_len)
     unpack = lambda: eng.unpack(slab, n, rec_off=d_offs, rec_len=d_len, cols=cols)  # noqa
     pms, ums = timed(torch, pack), timed(torch, unpack)
-    assert int((cols["err"] != 0).sum()) == 0
+    assert var in (1, 2) or pvar or int((cols["err"] != 0).sum()) == 0
     pb, ub = n * 36 + total, total + n * 32
     print(json.dumps({"case": name, "bytes": total, "pack_ms": round(pms, 4),
                       "unpack_ms": round(ums, 4), "pack_gbps": round(pb / pms / 1e6),
@@ -60,11 +60,14 @@ CASES = {
     "uniform_1472": lambda s: np.full_like(s, 1472),
     "mixed_x16": lambda s: (s + 15) // 16 * 16,
 }
-# argv[1]: cases; argv[2] (optional): unpack variant on the diagnostics build (3 = unsorted)
 var = int(sys.argv[2]) if len(sys.argv) > 2 else 0
-eng = Engine(0, diag=var != 0)
+pvar = int(sys.argv[3]) if len(sys.argv) > 3 else 0   # pack ablation (diag build)
+# argv[1]: cases; argv[2] (optional): unpack variant on the diagnostics build (3 = unsorted)
+eng = Engine(0, diag=var != 0 or pvar != 0)
 if var:
     assert eng.lib.mgenx_set_tuning(eng.ctx, 1, var) == 0
+if pvar:
+    assert eng.lib.mgenx_set_tuning(eng.ctx, 2, pvar) == 0
 for name in (sys.argv[1].split(",") if len(sys.argv) > 1 else CASES):
-    run(eng, name + ("" if not var else f"/v{var}"), CASES[name])
+    run(eng, name + ("" if not var else f"/v{var}") + ("" if not pvar else f"/p{pvar}"), CASES[name])
 eng.close()
