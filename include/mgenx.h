@@ -6,6 +6,13 @@
  * reference's caller-owned UINT32 buffers, mgenTransport.cpp:944,1023).  Calls are
  * asynchronous on the caller's hipStream_t (passed as void*), never synchronise and
  * never allocate, so they can be captured in a hipGraph.  One mgenx_ctx per device.
+ * Exceptions, each stated at its entry point: calls whose output size decides later
+ * launches (the stream scans, mgenx_pack_tcp) read small results back, and calls with
+ * scratch grow it (hipMalloc) the first time a larger batch arrives -- warm them up with
+ * the largest batch before capturing a graph.  The log / report / walk formatters keep
+ * one workspace per stream; the stream scans, mgenx_flow_reduce, mgenx_pack_tcp and
+ * mgenx_tcp_rx_persist keep one per context, so those run on one stream at a time per
+ * context (one context per concurrent stream).
  *
  * Return value: 0 = launched, <0 = argument/launch error (MGENX_E*).  Per-record
  * outcomes go to the `err` column with MgenMsg::Error codes (include/mgenMsg.h:63-70).
