@@ -530,6 +530,31 @@ int mgenx_log_recv_binary(mgenx_ctx* ctx, const uint8_t* dev_slab, uint64_t slab
                           uint8_t* dev_out, uint64_t out_cap, uint64_t* dev_rec_pos,
                           void* stream);
 
+/* SEND events (MgenMsg::LogSendEvent, src/common/mgenMsg.cpp:1145-1241) of records packed
+ * by a send path, as the transport logs them after each successful send
+ * (mgenTransport.cpp:1060, 1392, 1805: theTime = the message's tx time):
+ *   text:   "<tx time> SEND proto>P flow>F seq>S srcPort>SP dst>A/port size>N [host>H/port]\n"
+ *           (size = msg_len; TCP: mgen_msg_len from dev_msg_total);
+ *   binary: {SEND_EVENT 3, protocol, BE recordLength [, TCP: BE mgen_msg_len]} and then
+ *           recordLength bytes of the packed message (UDP / SINK) with CHECKSUM cleared,
+ *           recordLength = 12 + dst length + packet_header_len (+ host length + 4 with a
+ *           host); bytes past the packed message read as 0.
+ * dev_src_port[t]: template t's source port (the flow transport's socket port,
+ * mgenFlow.cpp:975-977).  dev_out_len (optional): Pack's return per record -- 0 means the
+ * message was not sent and gets no event.  Two passes as mgenx_log_recv_text:
+ * dev_pos[n + 1] = byte offsets; written only when the total fits out_cap. */
+int mgenx_log_send_text(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
+                        const mgenx_pack_desc* dev_desc, const uint16_t* dev_src_port,
+                        const uint32_t* dev_out_len, const uint32_t* dev_msg_total, uint32_t n,
+                        int protocol, uint32_t opts, char* dev_text, uint64_t text_cap,
+                        uint64_t* dev_line_off, void* stream);
+int mgenx_log_send_binary(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
+                          const mgenx_pack_desc* dev_desc, const uint32_t* dev_out_len,
+                          const uint32_t* dev_msg_total, const uint8_t* dev_slab,
+                          uint64_t slab_bytes, const uint64_t* dev_rec_off, uint64_t stride,
+                          uint32_t n, int protocol, uint8_t* dev_out, uint64_t out_cap,
+                          uint64_t* dev_rec_pos, void* stream);
+
 /* ---- multi-GPU exchange (RCCL over xGMI) ----
  * One communicator per rank (one process per GPU): rank 0 calls mgenx_comm_unique_id and
  * hands the MGENX_COMM_ID_BYTES bytes to every rank (any out-of-band channel), then every

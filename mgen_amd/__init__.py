@@ -31,7 +31,8 @@ EXPORTED_SYMBOLS = (
     "mgenx_ctx_device", "mgenx_unpack_batch", "mgenx_pack_prepare", "mgenx_set_fill_time",
     "mgenx_pack_batch", "mgenx_pack_msgs", "mgenx_pack_tcp", "mgenx_crc32_update", "mgenx_crc32_batch",
     "mgenx_tcp_rx_persist", "mgenx_report_build", "mgenx_log_report_text", "mgenx_data_walk",
-    "mgenx_log_report_recv_text", "mgenx_stream_scan", "mgenx_stream_scan_exits", "mgenx_stream_scan_range", "mgenx_flow_init", "mgenx_flow_reduce", "mgenx_flow_export",
+    "mgenx_log_report_recv_text", "mgenx_log_send_text", "mgenx_log_send_binary",
+    "mgenx_stream_scan", "mgenx_stream_scan_exits", "mgenx_stream_scan_range", "mgenx_flow_init", "mgenx_flow_reduce", "mgenx_flow_export",
     "mgenx_log_recv_text", "mgenx_log_recv_binary", "mgenx_comm_unique_id", "mgenx_comm_init",
     "mgenx_comm_destroy", "mgenx_allreduce_flows", "mgenx_allgather_u64",
     "mgenx_flow_table_create", "mgenx_flow_table_destroy", "mgenx_flow_lookup",
@@ -92,6 +93,8 @@ def load(diag: bool = False):
     L.mgenx_log_report_text.argtypes = [P, P, P, u32, u32, P, u32, P, u64, P, P]
     L.mgenx_data_walk.argtypes = [P, P, P, u64, P, u32, u32, P, P, P, u32, P, u32, P, P]
     L.mgenx_log_report_recv_text.argtypes = [P, P, P, u32, P, P, P, u32, P, u64, P, P]
+    L.mgenx_log_send_text.argtypes = [P, P, P, P, P, P, u32, i32, u32, P, u64, P, P]
+    L.mgenx_log_send_binary.argtypes = [P, P, P, P, P, P, u64, P, u64, u32, i32, P, u64, P, P]
     L.mgenx_stream_scan_exits.argtypes = [P, P, u64, i32, u64, u64, P, P, u32,
                                           ctypes.POINTER(u32), P]
     L.mgenx_stream_scan_range.argtypes = [P, P, u64, i32, u64, u64, i32, P, P, u64,
@@ -444,6 +447,24 @@ class Engine:
                 return text[:total], line_off
             cap = total
         raise MgenxError("report text did not fit")
+
+    def log_send(self, tmpl, desc, n, *, src_port=None, out_len=None, msg_total=None,
+                 slab=None, rec_off=None, stride=0, protocol=1, opts=0, binary=False,
+                 cap=None):
+        """SEND events of n packed records (mgenx_log_send_text / _binary): returns (bytes
+        tensor, offsets tensor of n + 1)."""
+        dev = desc.device
+        cap = cap if cap is not None else max(1, n) * (200 if not binary else 160)
+        if binary:
+            call = lambda t, c, lo: self.lib.mgenx_log_send_binary(  # noqa: E731
+                self.ctx, _ptr(tmpl), _ptr(desc), _ptr(out_len), _ptr(msg_total), _ptr(slab),
+                slab.numel(), _ptr(rec_off), stride, n, protocol, _ptr(t), c, _ptr(lo),
+                _stream(self.device))
+        else:
+            call = lambda t, c, lo: self.lib.mgenx_log_send_text(  # noqa: E731
+                self.ctx, _ptr(tmpl), _ptr(desc), _ptr(src_port), _ptr(out_len),
+                _ptr(msg_total), n, protocol, opts, _ptr(t), c, _ptr(lo), _stream(self.device))
+        return self._two_pass_text(call, n, dev, cap)
 
     def log_report_text(self, items, reports, n_flows, per_flow, report_count, opts=0,
                         text_cap=None):

@@ -44,6 +44,14 @@ extern "C" int mgenx_report_lines(void* ws, const uint8_t* items, const mgenx_fl
                                   const uint32_t* rx_sec, const uint32_t* rx_usec, uint32_t n,
                                   uint32_t opts, const double* rq, char* text, uint64_t cap,
                                   uint64_t* line_off, hipStream_t stream, char* err, size_t errn);
+extern "C" int mgenx_log_send_exec(void* ws, const mgenx_flow_tmpl* tmpl,
+                                   const mgenx_pack_desc* desc, const uint16_t* src_port,
+                                   const uint32_t* out_len, const uint32_t* msg_total,
+                                   const uint8_t* slab, uint64_t slab_bytes,
+                                   const uint64_t* rec_off, uint64_t stride, uint32_t n,
+                                   int protocol, uint32_t opts, bool binary, uint8_t* out,
+                                   uint64_t out_cap, uint64_t* pos, hipStream_t stream,
+                                   char* err, size_t errn);
 extern "C" int mgenx_data_walk_exec(void* ws, const uint8_t* slab, const uint64_t* rec_off,
                                     uint64_t stride, const mgenx_cols* cols, uint32_t n,
                                     uint32_t opts, const double* rq, uint8_t* status,
@@ -709,6 +717,47 @@ int mgenx_log_recv_binary(mgenx_ctx* ctx, const uint8_t* dev_slab, uint64_t slab
   return log_recv(ctx, true, dev_slab, slab_bytes, dev_rec_off, stride, cols, dev_src,
                   dev_rx_sec, dev_rx_usec, nullptr, n, protocol, 0, (char*)dev_out, out_cap,
                   dev_rec_pos, stream);
+}
+
+static int log_send(mgenx_ctx* ctx, bool binary, const mgenx_flow_tmpl* dev_tmpl,
+                    const mgenx_pack_desc* dev_desc, const uint16_t* dev_src_port,
+                    const uint32_t* dev_out_len, const uint32_t* dev_msg_total,
+                    const uint8_t* dev_slab, uint64_t slab_bytes, const uint64_t* dev_rec_off,
+                    uint64_t stride, uint32_t n, int protocol, uint32_t opts, uint8_t* dev_out,
+                    uint64_t out_cap, uint64_t* dev_pos, void* stream) {
+  if (!ctx || !dev_pos) return MGENX_EINVAL;
+  if (n == 0) return hipMemsetAsync(dev_pos, 0, 8, (hipStream_t)stream) == hipSuccess
+                         ? MGENX_OK : MGENX_EDEVICE;
+  if (!dev_tmpl || !dev_desc || (!binary && !dev_src_port) || (out_cap && !dev_out) ||
+      (binary && (!dev_slab || (!dev_rec_off && stride == 0 && n > 1))) || n > 0x7FFFFFFEu)
+    return MGENX_EINVAL;
+  hipSetDevice(ctx->device);
+  if (!ctx->log_ws) ctx->log_ws = mgenx_log_ws_new();
+  return mgenx_log_send_exec(ctx->log_ws, dev_tmpl, dev_desc, dev_src_port, dev_out_len,
+                             dev_msg_total, dev_slab, slab_bytes, dev_rec_off, stride, n,
+                             protocol, opts, binary, dev_out, out_cap, dev_pos,
+                             (hipStream_t)stream, ctx->err, sizeof(ctx->err));
+}
+
+int mgenx_log_send_text(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
+                        const mgenx_pack_desc* dev_desc, const uint16_t* dev_src_port,
+                        const uint32_t* dev_out_len, const uint32_t* dev_msg_total, uint32_t n,
+                        int protocol, uint32_t opts, char* dev_text, uint64_t text_cap,
+                        uint64_t* dev_line_off, void* stream) {
+  return log_send(ctx, false, dev_tmpl, dev_desc, dev_src_port, dev_out_len, dev_msg_total,
+                  nullptr, 0, nullptr, 0, n, protocol, opts, (uint8_t*)dev_text, text_cap,
+                  dev_line_off, stream);
+}
+
+int mgenx_log_send_binary(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
+                          const mgenx_pack_desc* dev_desc, const uint32_t* dev_out_len,
+                          const uint32_t* dev_msg_total, const uint8_t* dev_slab,
+                          uint64_t slab_bytes, const uint64_t* dev_rec_off, uint64_t stride,
+                          uint32_t n, int protocol, uint8_t* dev_out, uint64_t out_cap,
+                          uint64_t* dev_rec_pos, void* stream) {
+  return log_send(ctx, true, dev_tmpl, dev_desc, nullptr, dev_out_len, dev_msg_total, dev_slab,
+                  slab_bytes, dev_rec_off, stride, n, protocol, 0, dev_out, out_cap, dev_rec_pos,
+                  stream);
 }
 
 int mgenx_report_build(mgenx_ctx* ctx, const mgenx_flow_report* dev_reports, uint32_t n_flows,

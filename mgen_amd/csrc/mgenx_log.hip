@@ -1125,3 +1125,162 @@ extern "C" int mgenx_data_walk_exec(void* ws, const uint8_t* slab, const uint64_
   p.reps = reps; p.rep_cap = rep_cap;
   return mgenx_data_walk_run(ws, &p, totals, stream, err, errn);
 }
+
+// ---------------------------------------------------------------------------------------
+// SEND events: MgenMsg::LogSendEvent (mgenMsg.cpp:1145-1241) of the records a send path
+// packed (mgenTransport.cpp:1060: after a successful send, theTime = the tx time; the
+// message's src port = the flow transport's port, mgenFlow.cpp:975-977).  One lane per
+// record, a length pass, a scan, a write pass.
+namespace mgenx {
+
+struct SendParams {
+  const mgenx_flow_tmpl* tmpl;
+  const mgenx_pack_desc* desc;
+  const uint16_t* src_port;   // per template
+  const uint32_t* out_len;    // per record: Pack's return (0 = not sent: no event); NULL = all
+  const uint32_t* msg_total;  // TCP: mgen_msg_len per record (NULL = msg_len)
+  const uint8_t* slab;        // binary: the packed records
+  uint64_t slab_bytes;
+  const uint64_t* rec_off;
+  uint64_t stride;
+  uint32_t n;
+  int protocol;
+  uint32_t opts;
+  bool binary;
+  uint8_t* out;
+  uint64_t out_cap;
+  uint64_t* pos;
+  uint64_t* lens;
+};
+
+__device__ __forceinline__ uint32_t addr_length(uint32_t type) {
+  return type == 1u ? 4u : (type == 2u ? 16u : 0u);  // ProtoAddress::GetLength()
+}
+
+// packet_header_len after Pack(bufferLen = msgLen) (mgenMsg.cpp:97-273, as pack_kernel)
+__device__ uint32_t pack_hdr_len(const mgenx_flow_tmpl& t, uint32_t msgLen) {
+  const uint32_t D = t.dst_len > 16u ? 16u : t.dst_len;
+  const bool hv = t.host_type == 1u || t.host_type == 2u;
+  const uint32_t H = hv ? (t.host_len > 16u ? 16u : t.host_len) : 0u;
+  uint32_t len = 24u + D;
+  if (msgLen < len + H + 4u) return len;
+  len += 4u + H;
+  if (msgLen < len + 13u) return len;
+  len += 13u;
+  if (msgLen < len + 1u) return len;
+  len += 1u;
+  if (msgLen < len + 2u) return len;
+  return len + 2u;
+}
+
+template <typename S>
+__device__ void send_event(S& s, const SendParams& p, uint32_t i) {
+  if (p.out_len && p.out_len[i] == 0) return;  // Pack failed: never sent, never logged
+  const mgenx_pack_desc d = p.desc[i];
+  const mgenx_flow_tmpl& t = p.tmpl[d.tmpl];
+  const bool tcp = p.protocol == MGENX_PROTO_TCP;
+  const uint32_t mml = (tcp && p.msg_total) ? p.msg_total[i] : d.msg_len;
+  const bool hv = t.host_type == 1u || t.host_type == 2u;
+  if (!p.binary) {
+    put_ts(s, d.tx_sec, d.tx_usec, (p.opts & MGENX_LOG_EPOCH) != 0);
+    put_str(s, "SEND proto>");
+    put_str(s, p.protocol == 1 ? "UDP" : p.protocol == 2 ? "TCP" : p.protocol == 3 ? "SINK" : "UNKNOWN");
+    put_str(s, " flow>");
+    put_u64(s, t.flow_id);
+    put_str(s, " seq>");
+    put_u64(s, d.seq_num);
+    put_str(s, " srcPort>");
+    put_u64(s, p.src_port[d.tmpl]);
+    put_str(s, " dst>");
+    put_addr(s, t.dst_type, t.dst_len, t.dst_addr);
+    s.put('/');
+    put_u64(s, t.dst_port);
+    put_str(s, " size>");
+    put_u64(s, tcp ? mml : (uint32_t)d.msg_len);
+    s.put(' ');
+    if (hv) {
+      put_str(s, "host>");
+      put_addr(s, t.host_type, t.host_len, t.host_addr);
+      s.put('/');
+      put_u64(s, t.host_port);
+    }
+    s.put('\n');
+    return;
+  }
+  // binary: {SEND_EVENT, protocol, BE recordLength [, BE mgen_msg_len]} + message bytes
+  uint32_t rl = 12u + addr_length(t.dst_type) + pack_hdr_len(t, d.msg_len);
+  if (hv) rl += addr_length(t.host_type) + 4u;
+  if (tcp) rl += 4u;
+  rl &= 0xFFFFu;
+  s.put(3);
+  s.put((uint8_t)p.protocol);
+  s.put((uint8_t)(rl >> 8));
+  s.put((uint8_t)rl);
+  uint32_t index = 4;
+  if (tcp) {
+    s.put((uint8_t)(mml >> 24)); s.put((uint8_t)(mml >> 16));
+    s.put((uint8_t)(mml >> 8)); s.put((uint8_t)mml);
+    index += 4;
+  }
+  const uint32_t ml = (rl - index + 4u) & 0xFFFFu;
+  const uint64_t off = p.rec_off ? p.rec_off[i] : (uint64_t)i * p.stride;
+  const uint64_t have = p.out_len ? p.out_len[i] : d.msg_len;
+  for (uint32_t k = 0; k < ml; k++) {
+    uint8_t b = (k < have && off + k < p.slab_bytes) ? p.slab[off + k] : (uint8_t)0;
+    if (k == 3) b &= (uint8_t)~MGENX_FLAG_CHECKSUM;  // "Clear CHECKSUM flag for binary logging"
+    s.put(b);
+  }
+}
+
+template <bool kWrite>
+__global__ void __launch_bounds__(kLogThreads) send_kernel(SendParams p) {
+  const uint32_t i = blockIdx.x * kLogThreads + threadIdx.x;
+  if (i >= p.n) return;
+  if (!kWrite) {
+    CountSink s;
+    send_event(s, p, i);
+    p.lens[i] = s.n;
+  } else {
+    const uint64_t off = p.pos[i], end = p.pos[i + 1];
+    if (end > p.out_cap) return;
+    WriteSink s{p.out + off};
+    send_event(s, p, i);
+  }
+}
+
+}  // namespace mgenx
+
+extern "C" int mgenx_log_send_exec(void* wsp, const mgenx_flow_tmpl* tmpl,
+                                   const mgenx_pack_desc* desc, const uint16_t* src_port,
+                                   const uint32_t* out_len, const uint32_t* msg_total,
+                                   const uint8_t* slab, uint64_t slab_bytes,
+                                   const uint64_t* rec_off, uint64_t stride, uint32_t n,
+                                   int protocol, uint32_t opts, bool binary, uint8_t* out,
+                                   uint64_t out_cap, uint64_t* pos, hipStream_t stream,
+                                   char* err, size_t errn) {
+  mgenx_log_ws& ws = ws_for(wsp, stream);
+  mgenx::SendParams p;
+  p.tmpl = tmpl; p.desc = desc; p.src_port = src_port; p.out_len = out_len;
+  p.msg_total = msg_total; p.slab = slab; p.slab_bytes = slab_bytes; p.rec_off = rec_off;
+  p.stride = stride; p.n = n; p.protocol = protocol; p.opts = opts; p.binary = binary;
+  p.out = out; p.out_cap = out_cap; p.pos = pos;
+  size_t scan_bytes = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, (uint64_t*)nullptr,
+                                         (uint64_t*)nullptr, (int)n + 1, stream);
+  const size_t len_bytes = (((size_t)n + 1) * 8 + 255) & ~(size_t)255;
+  void* mem;
+  int rc = rep_ws(ws, len_bytes + scan_bytes, &mem, err, errn);
+  if (rc != MGENX_OK) return rc;
+  p.lens = static_cast<uint64_t*>(mem);
+  const int grid = (int)((n + mgenx::kLogThreads - 1) / mgenx::kLogThreads);
+  hipLaunchKernelGGL(mgenx::send_kernel<false>, dim3(grid), dim3(mgenx::kLogThreads), 0, stream, p);
+  hipLaunchKernelGGL(mgenx::log_tail_kernel, dim3(1), dim3(64), 0, stream, p.lens, n);
+  size_t have = scan_bytes;
+  if (hipcub::DeviceScan::ExclusiveSum(static_cast<uint8_t*>(mem) + len_bytes, have, p.lens,
+                                       pos, (int)n + 1, stream) != hipSuccess) {
+    snprintf(err, errn, "send log: scan failed");
+    return MGENX_EDEVICE;
+  }
+  hipLaunchKernelGGL(mgenx::send_kernel<true>, dim3(grid), dim3(mgenx::kLogThreads), 0, stream, p);
+  return hipGetLastError() == hipSuccess ? MGENX_OK : MGENX_EDEVICE;
+}

@@ -1166,6 +1166,86 @@ uint32_t or_log_recv_binary(const or_fields* f, const uint8_t* rec, uint64_t ava
 }
 
 /* ------------------------------------------------------------------ */
+/* SEND events: MgenMsg::LogSendEvent (mgenMsg.cpp:1145-1241), as the UDP / SINK send   */
+/* path logs them after a successful send (mgenTransport.cpp:1060: theTime = the        */
+/* message's tx time; the message's src port = the flow transport's port,              */
+/* mgenFlow.cpp:975-977).  Binary: bytes past the packed message (the transport's      */
+/* stale txBuffer) read as zero here: unpinned.                                        */
+/* ------------------------------------------------------------------ */
+static uint32_t addr_length(uint8_t type) { return type == OR_ADDR_IPV4 ? 4u : (type == OR_ADDR_IPV6 ? 16u : 0u); }
+
+uint32_t or_log_send_text(const or_tmpl* t, const or_desc* d, uint16_t src_port, int protocol,
+                          uint32_t mgen_msg_len, uint32_t opts, char* out)
+{
+    char* p = out;
+    p += log_ts(p, d->tx_sec, d->tx_usec, (opts & OR_LOG_EPOCH) != 0);
+    p += sprintf(p, "SEND proto>%s flow>%lu seq>%lu srcPort>%hu dst>", log_proto(protocol),
+                 (unsigned long)t->flow_id, (unsigned long)d->seq_num, src_port);
+    p += log_addr(p, t->dst_type, t->dst_len, t->dst_addr);
+    p += sprintf(p, "/%hu", t->dst_port);
+    if (protocol == 2) p += sprintf(p, " size>%lu ", (unsigned long)mgen_msg_len);
+    else p += sprintf(p, " size>%u ", (unsigned)d->msg_len);
+    if (t->host_type == OR_ADDR_IPV4 || t->host_type == OR_ADDR_IPV6) {
+        p += sprintf(p, "host>");
+        p += log_addr(p, t->host_type, t->host_len, t->host_addr);
+        p += sprintf(p, "/%hu\n", t->host_port);
+    } else {
+        p += sprintf(p, "\n");
+    }
+    return (uint32_t)(p - out);
+}
+
+uint32_t or_log_send_binary(const or_tmpl* t, const uint8_t* packed, uint32_t packed_len,
+                            uint32_t hdr_len, int protocol, uint32_t mgen_msg_len, uint8_t* out)
+{
+    uint8_t* p = out;
+    uint32_t rl = 12 + addr_length(t->dst_type) + hdr_len;
+    if (t->host_type == OR_ADDR_IPV4 || t->host_type == OR_ADDR_IPV6) rl += addr_length(t->host_type) + 4;
+    if (protocol == 2) rl += 4;
+    rl &= 0xFFFF;                                   /* UINT16 recordLength */
+    *p++ = 3;                                       /* SEND_EVENT */
+    *p++ = (uint8_t)protocol;
+    p += put_be16(p, rl);
+    uint32_t index = 4;
+    if (protocol == 2) { p += put_be32(p, mgen_msg_len); index += 4; }
+    const uint32_t ml = (rl - index + 4) & 0xFFFF;
+    for (uint32_t i = 0; i < ml; i++) {
+        uint8_t b = i < packed_len ? packed[i] : 0;
+        if (i == 3) b &= (uint8_t)~OR_FLAG_CHECKSUM;   /* "Clear CHECKSUM flag for binary logging" */
+        *p++ = b;
+    }
+    return (uint32_t)(p - out);
+}
+
+/* The SEND events of n records sent by the UDP / SINK path (or_udp_pack_batch's records;
+ * a failed Pack is never sent, so never logged).  binary: 0 text, 1 binary.  Returns the
+ * bytes written to out. */
+uint64_t or_log_send_batch(const or_tmpl* tmpl, const or_desc* desc, uint32_t n,
+                           const uint8_t* pool, const uint16_t* src_port, int protocol,
+                           int checksum_enable, uint32_t opts, int binary, uint8_t* out)
+{
+    static uint8_t buf[65536 + 512];
+    uint64_t pos = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        or_msg m;
+        tmpl_to_msg(&tmpl[desc[i].tmpl], &desc[i], pool, &m);
+        uint32_t tx = 0;
+        uint16_t hl = 0;
+        m.flags |= OR_FLAG_LAST_BUFFER;
+        const uint32_t len = or_pack(&m, buf, m.msg_len, checksum_enable, &tx, 0, 0, &hl);
+        if (len == 0) continue;
+        if (checksum_enable && (m.flags & OR_FLAG_CHECKSUM)) or_write_checksum(&tx, buf, len);
+        const or_tmpl* t = &tmpl[desc[i].tmpl];
+        if (binary)
+            pos += or_log_send_binary(t, buf, len, hl, protocol, m.mgen_msg_len, out + pos);
+        else
+            pos += or_log_send_text(t, &desc[i], src_port[desc[i].tmpl], protocol, m.mgen_msg_len,
+                                    opts, (char*)out + pos);
+    }
+    return pos;
+}
+
+/* ------------------------------------------------------------------ */
 /* MGEN_DATA items: MgenAnalytic::Report and MgenFlowCommand           */
 /*   quantizers          mgenAnalytic.cpp:568-642                      */
 /*   Report build        Init :28-71, Update :220-254, GetReport :296-310, */

@@ -253,6 +253,15 @@ uint32_t or_log_recv_binary(const or_fields* f, const uint8_t* rec, uint64_t ava
                             const or_addr* src, uint32_t rx_sec, uint32_t rx_usec, int protocol,
                             uint8_t* out);
 
+/* MgenMsg::LogSendEvent (mgenMsg.cpp:1145-1241) of the UDP / SINK / TCP send paths. */
+uint32_t or_log_send_text(const or_tmpl* t, const or_desc* d, uint16_t src_port, int protocol,
+                          uint32_t mgen_msg_len, uint32_t opts, char* out);
+uint32_t or_log_send_binary(const or_tmpl* t, const uint8_t* packed, uint32_t packed_len,
+                            uint32_t hdr_len, int protocol, uint32_t mgen_msg_len, uint8_t* out);
+uint64_t or_log_send_batch(const or_tmpl* tmpl, const or_desc* desc, uint32_t n,
+                           const uint8_t* pool, const uint16_t* src_port, int protocol,
+                           int checksum_enable, uint32_t opts, int binary, uint8_t* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -429,6 +429,39 @@ def log_recv_binary(fields, slab, rec_off, src, rx_sec, rx_usec, protocol=1):
     return b"".join(out)
 
 
+def log_send_text(tmpl1, desc1, src_port, protocol=1, mgen_msg_len=None, opts=0):
+    """or_log_send_text for one template / descriptor record (numpy structured scalars)."""
+    L = lib()
+    P, u32, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int
+    L.or_log_send_text.argtypes = [P, P, ctypes.c_uint16, i32, u32, u32, P]
+    L.or_log_send_text.restype = u32
+    t = np.ascontiguousarray(np.asarray(tmpl1).reshape(1))
+    d = np.ascontiguousarray(np.asarray(desc1).reshape(1))
+    out = np.zeros(512, np.uint8)
+    mml = int(d["msg_len"][0]) if mgen_msg_len is None else mgen_msg_len
+    n = L.or_log_send_text(_ptr(t), _ptr(d), src_port, protocol, mml, opts, _ptr(out))
+    return out[:n].tobytes()
+
+
+def log_send_batch(tmpl, desc, pool, src_port, protocol=1, checksum=True, opts=0,
+                   binary=False):
+    """SEND log events (text or binary) of n records sent by the UDP / SINK path."""
+    L = lib()
+    if not getattr(L, "_send_protos", False):
+        P, u32, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int
+        L.or_log_send_batch.argtypes = [P, P, u32, P, P, i32, i32, u32, i32, P]
+        L.or_log_send_batch.restype = ctypes.c_uint64
+        L._send_protos = True
+    tmpl = np.ascontiguousarray(tmpl)
+    desc = np.ascontiguousarray(desc)
+    pool = np.ascontiguousarray(pool if pool is not None and len(pool) else np.zeros(1, np.uint8))
+    sp = np.ascontiguousarray(src_port, np.uint16)
+    out = np.zeros(len(desc) * 400 + 1024, np.uint8)
+    n = L.or_log_send_batch(_ptr(tmpl), _ptr(desc), len(desc), _ptr(pool), _ptr(sp), protocol,
+                            int(checksum), opts, int(binary), _ptr(out))
+    return out[:n].tobytes()
+
+
 # ---------------------------------------------------------------- MGEN_DATA items
 def _report_protos():
     L = lib()
