@@ -1870,8 +1870,13 @@ hipError_t launch_unpack(const UnpackParams& p, int grid, hipStream_t stream) {
     default: break;
   }
 #endif  // MGENX_DIAG
-  // per-record lengths: sorted groups with the rows in a load ring
-  if (p.rec_len) return launch_var(p, grid, stream);
+  // per-record lengths: sorted groups with the rows in a load ring -- when every wave gets
+  // at least two 64-record tiles; fewer, larger records (a 1 GiB stream of 16-KiB TCP
+  // records is 1024 tiles for 4096 waves) keep the general kernel's one group per wave and
+  // its 14-row load blocks, which keep more bytes in flight per record
+  const uint64_t tiles = ((uint64_t)p.n + 63) / 64;
+  const uint64_t waves = (uint64_t)grid * (kUnpackThreads / 64);
+  if (p.rec_len && tiles >= 2 * waves) return launch_var(p, grid, stream);
   return launch_mode<0>(p, grid, stream);
 }
 
