@@ -6,14 +6,14 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -Wno-unused-value -Wno-int-to-pointer-cast
 NAMES := mgenx_api mgenx_unpack mgenx_pack mgenx_scan mgenx_analytic mgenx_log mgenx_comm \
-         mgenx_flowtab mgenx_tcp mgenx_rx
+         mgenx_flowtab mgenx_tcp mgenx_rx mgenx_pcap
 HDR := include/mgenx.h include/mgenx_diag.h mgen_amd/csrc/mgenx_common.hpp mgen_amd/csrc/mgenx_kernels.hpp
 OBJ := $(addprefix build/product/,$(addsuffix .o,$(NAMES)))
 DOBJ := $(addprefix build/diag/,$(addsuffix .o,$(NAMES)))
 LIBS := -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 all: mgen_amd/libmgenx.so mgen_amd/libmgenx_diag.so oracle tests/cpp/host_roundtrip \
-     tests/cpp/loopback tests/cpp/compat_shapes
+     tests/cpp/loopback tests/cpp/compat_shapes tools/pcap2mgen
 
 build/product/%.o: mgen_amd/csrc/%.hip $(HDR)
 	@mkdir -p build/product
@@ -47,6 +47,12 @@ tests/cpp/loopback: tests/cpp/loopback.cpp include/mgenx.hpp include/mgenx_io.hp
 tests/cpp/compat_shapes: tests/cpp/compat_shapes.cpp $(wildcard include/mgenx_compat/*.h) \
 		include/mgenx.h mgen_amd/libmgenx.so
 	$(HOSTCXX) -Iinclude/mgenx_compat $< -o $@ $(HOSTLD)
+
+# the reference's pcap2mgen command line over mgenx::Pcap2Mgen (include/mgenx_pcap.hpp)
+tools/pcap2mgen: tools/pcap2mgen.cpp include/mgenx_pcap.hpp include/mgenx.hpp include/mgenx.h \
+		mgen_amd/libmgenx.so
+	$(HOSTCXX) $< -o $@ -Lmgen_amd -lmgenx -L/opt/rocm/lib -lamdhip64 \
+	    -Wl,-rpath,'$$ORIGIN/../mgen_amd' -Wl,-rpath,/opt/rocm/lib
 
 oracle:
 	$(MAKE) -s -C oracle

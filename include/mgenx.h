@@ -468,6 +468,15 @@ int mgenx_flow_reduce(mgenx_ctx* ctx, const uint32_t* dev_flow_idx, const uint32
                       const uint32_t* dev_rx_usec, uint32_t n, mgenx_flow_state* dev_flows,
                       uint32_t n_flows, mgenx_flow_report* dev_reports, uint32_t per_flow,
                       uint32_t* dev_report_count, void* stream);
+/* mgenx_flow_reduce plus, per kept report slot f * per_flow + k, the input record whose
+ * Update closed the window (dev_report_rec, optional): the record after which the reference
+ * logs the REPORT line (pcap2mgen.cpp:468-470, mgen.cpp:1055-1060). */
+int mgenx_flow_reduce_ex(mgenx_ctx* ctx, const uint32_t* dev_flow_idx, const uint32_t* dev_seq,
+                         const uint32_t* dev_tx_sec, const uint32_t* dev_tx_usec,
+                         const uint16_t* dev_msg_len, const uint32_t* dev_rx_sec,
+                         const uint32_t* dev_rx_usec, uint32_t n, mgenx_flow_state* dev_flows,
+                         uint32_t n_flows, mgenx_flow_report* dev_reports, uint32_t per_flow,
+                         uint32_t* dev_report_count, uint32_t* dev_report_rec, void* stream);
 int mgenx_flow_export(mgenx_ctx* ctx, const mgenx_flow_state* dev_flows, uint32_t n_flows,
                       mgenx_flow_counters* dev_out, void* stream);
 
@@ -487,6 +496,10 @@ int mgenx_flow_table_destroy(mgenx_flow_table* table);
 int mgenx_flow_lookup(mgenx_ctx* ctx, mgenx_flow_table* table, const mgenx_cols* cols,
                       const mgenx_addr* dev_src, uint32_t n, uint32_t* dev_flow_idx,
                       uint32_t* dev_n_flows, void* stream);
+/* The key of every flow index < cap (MgenAnalytic::Init's src / dst / flow id, with
+ * `protocol`): the report_msg keys mgenx_report_build takes (mgenAnalytic.cpp:28-71). */
+int mgenx_flow_keys(mgenx_ctx* ctx, const mgenx_flow_table* table, int protocol,
+                    mgenx_report_key* dev_keys, uint32_t cap, void* stream);
 
 /* ---- event log (MgenMsg::LogRecvEvent / LogRecvError, text form) ----
  * One line per record, as the UDP receive path logs it (src/common/mgenTransport.cpp:
@@ -509,6 +522,8 @@ int mgenx_flow_lookup(mgenx_ctx* ctx, mgenx_flow_table* table, const mgenx_cols*
 #define MGENX_LOG_EPOCH   0x1  /* Mgen::SetEpochTimestamp(true) */
 #define MGENX_LOG_NO_DATA 0x2  /* log_data off */
 #define MGENX_LOG_NO_GPS  0x4  /* log_gps_data off */
+#define MGENX_LOG_SKIP_ERR 0x8 /* records with err != 0 get no line (pcap2mgen.cpp:428-432
+                                  skips a packet Unpack rejects instead of logging RERR) */
 
 int mgenx_log_recv_text(mgenx_ctx* ctx, const uint8_t* dev_slab, const uint64_t* dev_rec_off,
                         uint64_t stride, const mgenx_cols* cols, const mgenx_addr* dev_src,
@@ -554,6 +569,84 @@ int mgenx_log_send_binary(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
                           uint64_t slab_bytes, const uint64_t* dev_rec_off, uint64_t stride,
                           uint32_t n, int protocol, uint8_t* dev_out, uint64_t out_cap,
                           uint64_t* dev_rec_pos, void* stream);
+
+/* ---- one log file from several line sources, in record order ----
+ * The reference writes, per received message, the lines of several loggers in turn: e.g.
+ * pcap2mgen (pcap2mgen.cpp:445-476) logs the analytic's REPORT line when Update closed a
+ * window, then the RECV line, then the REPORT lines of the reports the payload carries.
+ * mgenx_text_interleave concatenates, for record 0, 1, ..., n_rec - 1, each source's lines
+ * of that record in source order.  A source is a text with line offsets (line k =
+ * text[line_off[k], line_off[k+1])) and the record each line belongs to:
+ *   MGENX_TEXT_PER_RECORD  line i is record i's (n_lines = n_rec; empty lines allowed);
+ *   MGENX_TEXT_OWNER       owner[k * index_stride] = line k's record, non-decreasing in k;
+ *   MGENX_TEXT_MAP         index[i] = record i's line (at most one), or MGENX_FLOW_NONE;
+ *   MGENX_TEXT_SCATTER     index[k] = line k's record (at most one line per record, any
+ *                          order; MGENX_FLOW_NONE = no record): e.g. the slots of
+ *                          mgenx_log_report_text with mgenx_flow_reduce_ex's dev_report_rec.
+ * Two passes like mgenx_log_recv_text: dev_rec_off[n_rec + 1] = byte offsets of each record's
+ * output; dev_out is written only when the total fits out_cap.  srcs is a HOST array. */
+#define MGENX_TEXT_PER_RECORD 0
+#define MGENX_TEXT_OWNER      1
+#define MGENX_TEXT_MAP        2
+#define MGENX_TEXT_SCATTER    3
+#define MGENX_TEXT_MAX_SRC    4
+typedef struct {
+    const char*     text;         /* may be NULL only when every line is empty */
+    const uint64_t* line_off;     /* n_lines + 1 entries */
+    uint32_t        n_lines;
+    uint32_t        kind;         /* MGENX_TEXT_* */
+    const uint32_t* index;        /* owner (OWNER), record -> line (MAP), line -> record
+                                     (SCATTER) */
+    uint32_t        index_stride; /* OWNER: u32 elements between owners (1, or 4 for the
+                                     (record, offset) u64 pairs of mgenx_data_walk) */
+    uint32_t        rsv;
+} mgenx_text_src;
+int mgenx_text_interleave(mgenx_ctx* ctx, const mgenx_text_src* srcs, uint32_t n_src,
+                          uint32_t n_rec, char* dev_out, uint64_t out_cap, uint64_t* dev_rec_off,
+                          void* stream);
+
+/* ---- pcap2mgen: captured packets -> MgenMsg records (src/common/pcap2mgen.cpp:252-482) ----
+ * mgenx_pcap_index (HOST memory, no device work: the pcap_next loop, :344) reads the pcap
+ * file header and walks the record headers: the offsets of the first `cap` records' 16-byte
+ * headers go to pkt_off (host memory).  info: link type, flags, records found, bytes consumed
+ * (a record cut short by the end of the buffer ends the walk, as pcap_next returns NULL).
+ * Returns MGENX_EINVAL for a buffer that is not a pcap file.
+ * mgenx_pcap_parse (device) restates, per record, pcap2mgen's frame walk (:346-436) over
+ * protolib's ProtoPktETH / ProtoPktIP / ProtoPktUDP (restated: protolib is not vendored,
+ * so this layer is parity unpinned): DLT_LINUX_SLL (16-byte header) or, for every
+ * other link type as in the reference, Ethernet frames (hdr.len <= 4094 bytes, optional
+ * 802.1Q tag), IPv4 / IPv6, UDP.  Per record:
+ * udp_off / udp_len = the UDP payload (the Unpack buffer; udp_len 0 when status != 0, so
+ * Unpack rejects it), src = IP source + UDP source port (msg.SetSrcAddr, :434-435),
+ * ttl = IPv4 TTL / IPv6 hop limit, rx time = the pcap timestamp (ProtoTime(hdr.ts); a
+ * nanosecond file is read at microsecond precision, as pcap_fopen_offline does). */
+#define MGENX_DLT_EN10MB    1
+#define MGENX_DLT_LINUX_SLL 113
+#define MGENX_PCAP_NSEC    0x1  /* nanosecond timestamps (magic 0xa1b23c4d) */
+#define MGENX_PCAP_SWAPPED 0x2  /* the file's byte order is not the host's */
+#define MGENX_PCAP_UDP       0  /* status: a UDP datagram */
+#define MGENX_PCAP_BAD_ETH   1  /* "invalid Ether frame" (:370-373) */
+#define MGENX_PCAP_NOT_IP    2  /* not IPv4 / IPv6 (:422) */
+#define MGENX_PCAP_BAD_IP    3  /* "bad IP packet" (:388-391) */
+#define MGENX_PCAP_NOT_UDP   4  /* (:425) */
+#define MGENX_PCAP_TRUNCATED 5  /* UDP payload past the captured bytes: skipped (the
+                                   reference reads stale buffer bytes there) */
+#define MGENX_PCAP_OOB       6  /* record past the buffer */
+typedef struct {
+    uint32_t link_type;   /* DLT_* */
+    uint32_t flags;       /* MGENX_PCAP_NSEC | MGENX_PCAP_SWAPPED */
+    uint32_t snaplen;
+    uint32_t rsv;
+    uint64_t n_records;   /* records found (only the first cap offsets are written) */
+    uint64_t consumed;    /* bytes of whole records, file header included */
+} mgenx_pcap_info;
+int mgenx_pcap_index(const uint8_t* buf, uint64_t nbytes, uint64_t* pkt_off, uint64_t cap,
+                     mgenx_pcap_info* info);
+int mgenx_pcap_parse(mgenx_ctx* ctx, const uint8_t* dev_buf, uint64_t buf_bytes,
+                     const uint64_t* dev_pkt_off, uint32_t n, uint32_t link_type,
+                     uint32_t flags, uint64_t* dev_udp_off, uint32_t* dev_udp_len,
+                     mgenx_addr* dev_src, int32_t* dev_ttl, uint32_t* dev_rx_sec,
+                     uint32_t* dev_rx_usec, uint8_t* dev_status, void* stream);
 
 /* ---- multi-GPU exchange (RCCL over xGMI) ----
  * One communicator per rank (one process per GPU): rank 0 calls mgenx_comm_unique_id and

@@ -19,6 +19,8 @@ from ._abi import (  # noqa: F401
     FLOW_STATE_BYTES, FLOW_STATE_DTYPE, REC_DTYPE, PACK_RAW, DEC_MSGLEN, DEC_BASE, DEC_DST,
     DEC_HDRLEN, DEC_HOST, DEC_GPS, DEC_PTYPE, DEC_PLEN, RX_NOLOG, RX_FORCE, RX_PREV,
     RX_STATE_DTYPE, SCAN_HALO, SCAN_REUSE, ADDR_DTYPE, REPORT_KEY_DTYPE, DATA_CONTROLLER,
+    PcapInfo, TextSrc, TEXT_PER_RECORD, TEXT_OWNER, TEXT_MAP, TEXT_SCATTER, PCAP_NSEC, PCAP_SWAPPED, LOG_EPOCH, LOG_NO_DATA, LOG_NO_GPS,
+    LOG_SKIP_ERR, FLOW_NONE, DLT_EN10MB, DLT_LINUX_SLL,
 )
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -36,6 +38,8 @@ EXPORTED_SYMBOLS = (
     "mgenx_log_recv_text", "mgenx_log_recv_binary", "mgenx_comm_unique_id", "mgenx_comm_init",
     "mgenx_comm_destroy", "mgenx_allreduce_flows", "mgenx_allgather_u64",
     "mgenx_flow_table_create", "mgenx_flow_table_destroy", "mgenx_flow_lookup",
+    "mgenx_flow_reduce_ex", "mgenx_flow_keys", "mgenx_text_interleave", "mgenx_pcap_index",
+    "mgenx_pcap_parse",
 )
 DIAG_SYMBOLS = ("mgenx_set_tuning", "mgenx_diag_stream_read", "mgenx_diag_group_rw")
 
@@ -83,6 +87,11 @@ def load(diag: bool = False):
     L.mgenx_flow_table_create.argtypes = [P, u32, ctypes.POINTER(P)]
     L.mgenx_flow_table_destroy.argtypes = [P]
     L.mgenx_flow_lookup.argtypes = [P, P, ctypes.POINTER(MgenxCols), P, u32, P, P, P]
+    L.mgenx_flow_reduce_ex.argtypes = [P, P, P, P, P, P, P, P, u32, P, u32, P, u32, P, P, P]
+    L.mgenx_flow_keys.argtypes = [P, P, i32, P, u32, P]
+    L.mgenx_text_interleave.argtypes = [P, P, u32, u32, P, u64, P, P]
+    L.mgenx_pcap_index.argtypes = [P, u64, P, u64, ctypes.POINTER(PcapInfo)]
+    L.mgenx_pcap_parse.argtypes = [P, P, u64, P, u32, u32, u32, P, P, P, P, P, P, P, P]
     if diag:
         L.mgenx_set_tuning.argtypes = [P, i32, i32]
         L.mgenx_diag_stream_read.argtypes = [P, P, u64, P, i32, P]
@@ -401,18 +410,88 @@ class Engine:
         return flows
 
     def flow_reduce(self, flows, n_flows, flow_idx, seq, tx_sec, tx_usec, msg_len, rx_sec,
-                    rx_usec, n=None, reports=None, per_flow=0, report_count=None):
-        """MgenAnalytic::Update over records in receive order (mgenx_flow_reduce)."""
+                    rx_usec, n=None, reports=None, per_flow=0, report_count=None,
+                    report_rec=None):
+        """MgenAnalytic::Update over records in receive order (mgenx_flow_reduce; with
+        report_rec, mgenx_flow_reduce_ex: the record that closed each kept report)."""
         torch = self.torch
         n = flow_idx.numel() if n is None else n
         if report_count is None:
             report_count = torch.zeros(n_flows, dtype=torch.int32, device=flows.device)
-        rc = self.lib.mgenx_flow_reduce(self.ctx, _ptr(flow_idx), _ptr(seq), _ptr(tx_sec),
-                                        _ptr(tx_usec), _ptr(msg_len), _ptr(rx_sec),
-                                        _ptr(rx_usec), n, _ptr(flows), n_flows, _ptr(reports),
-                                        per_flow, _ptr(report_count), _stream(self.device))
+        if report_rec is None:
+            rc = self.lib.mgenx_flow_reduce(self.ctx, _ptr(flow_idx), _ptr(seq), _ptr(tx_sec),
+                                            _ptr(tx_usec), _ptr(msg_len), _ptr(rx_sec),
+                                            _ptr(rx_usec), n, _ptr(flows), n_flows, _ptr(reports),
+                                            per_flow, _ptr(report_count), _stream(self.device))
+        else:
+            rc = self.lib.mgenx_flow_reduce_ex(self.ctx, _ptr(flow_idx), _ptr(seq), _ptr(tx_sec),
+                                               _ptr(tx_usec), _ptr(msg_len), _ptr(rx_sec),
+                                               _ptr(rx_usec), n, _ptr(flows), n_flows,
+                                               _ptr(reports), per_flow, _ptr(report_count),
+                                               _ptr(report_rec), _stream(self.device))
         self._check(rc, "mgenx_flow_reduce")
         return report_count
+
+    def flow_keys(self, table, n_flows, protocol=1, keys=None):
+        """The report_msg key of every flow index < n_flows (mgenx_flow_keys): a uint8
+        tensor of n_flows x 48 (mgenx_report_key)."""
+        if keys is None:
+            keys = self.torch.zeros(max(n_flows, 1) * REPORT_KEY_DTYPE.itemsize,
+                                    dtype=self.torch.uint8, device=f"cuda:{self.device}")
+        self._check(self.lib.mgenx_flow_keys(self.ctx, table, protocol, _ptr(keys), n_flows,
+                                             _stream(self.device)), "mgenx_flow_keys")
+        return keys
+
+    def text_interleave(self, sources, n_rec, cap=None):
+        """mgenx_text_interleave: sources = [(kind, text, line_off, n_lines, index,
+        index_stride)] (device tensors); returns (text, record offsets of n_rec + 1)."""
+        torch = self.torch
+        arr = (TextSrc * max(1, len(sources)))()
+        keep = []
+        for k, (kind, text, line_off, n_lines, index, stride) in enumerate(sources):
+            arr[k].text = text.data_ptr() if text is not None and text.numel() else None
+            arr[k].line_off = line_off.data_ptr()
+            arr[k].n_lines = n_lines
+            arr[k].kind = kind
+            arr[k].index = index.data_ptr() if index is not None else None
+            arr[k].index_stride = stride
+            keep.append((text, line_off, index))
+        dev = f"cuda:{self.device}"
+        if cap is None:
+            cap = sum(int(t.numel()) for _, t, *_ in sources if t is not None)
+        rec_off = torch.empty(n_rec + 1, dtype=torch.int64, device=dev)
+        for _ in range(2):
+            out = torch.empty(max(cap, 1), dtype=torch.uint8, device=dev)
+            self._check(self.lib.mgenx_text_interleave(self.ctx, arr, len(sources), n_rec,
+                                                       _ptr(out), cap, _ptr(rec_off),
+                                                       _stream(self.device)),
+                        "mgenx_text_interleave")
+            total = int(rec_off[n_rec].item())
+            if total <= cap:
+                return out[:total], rec_off
+            cap = total
+        raise MgenxError("mgenx_text_interleave: output did not fit")
+
+    # ------------------------------------------------------------ pcap2mgen
+    def pcap_parse(self, buf, pkt_off, n, link_type, flags=0):
+        """pcap2mgen's frame walk per record (mgenx_pcap_parse): returns a dict of device
+        tensors udp_off, udp_len, src (n x 20), ttl, rx_sec, rx_usec, status."""
+        torch = self.torch
+        dev = buf.device
+        o = {"udp_off": torch.empty(max(n, 1), dtype=torch.int64, device=dev),
+             "udp_len": torch.empty(max(n, 1), dtype=torch.int32, device=dev),
+             "src": torch.empty(max(n, 1) * 20, dtype=torch.uint8, device=dev),
+             "ttl": torch.empty(max(n, 1), dtype=torch.int32, device=dev),
+             "rx_sec": torch.empty(max(n, 1), dtype=torch.int32, device=dev),
+             "rx_usec": torch.empty(max(n, 1), dtype=torch.int32, device=dev),
+             "status": torch.empty(max(n, 1), dtype=torch.uint8, device=dev)}
+        self._check(self.lib.mgenx_pcap_parse(self.ctx, _ptr(buf), buf.numel(), _ptr(pkt_off), n,
+                                              link_type, flags, _ptr(o["udp_off"]),
+                                              _ptr(o["udp_len"]), _ptr(o["src"]), _ptr(o["ttl"]),
+                                              _ptr(o["rx_sec"]), _ptr(o["rx_usec"]),
+                                              _ptr(o["status"]), _stream(self.device)),
+                    "mgenx_pcap_parse")
+        return o
 
     def flow_export(self, flows, n_flows, out=None):
         if out is None:
@@ -560,6 +639,24 @@ class Engine:
                                         _ptr(out), _stream(self.device))
         self._check(rc, "mgenx_crc32_batch")
         return out
+
+
+def pcap_index(buf) -> tuple:
+    """mgenx_pcap_index over a host pcap image (bytes / numpy uint8): (record header offsets
+    as uint64 numpy array, PcapInfo).  Host work only (the pcap_next loop)."""
+    L = load()
+    b = np.frombuffer(buf, np.uint8) if not isinstance(buf, np.ndarray) else buf
+    info = PcapInfo()
+    rc = L.mgenx_pcap_index(b.ctypes.data_as(ctypes.c_void_p), b.size, None, 0,
+                            ctypes.byref(info))
+    if rc != 0:
+        raise MgenxError("mgenx_pcap_index: not a pcap file")
+    offs = np.zeros(max(1, int(info.n_records)), np.uint64)
+    rc = L.mgenx_pcap_index(b.ctypes.data_as(ctypes.c_void_p), b.size,
+                            offs.ctypes.data_as(ctypes.c_void_p), offs.size, ctypes.byref(info))
+    if rc != 0:
+        raise MgenxError("mgenx_pcap_index failed")
+    return offs[:int(info.n_records)], info
 
 
 def to_device(arr: np.ndarray, device=0):

@@ -136,3 +136,24 @@ FLOW_STATE_DTYPE = np.dtype([
     ("n_reports", "<u8"), ("rsv", "<u8", (2,))])
 assert FLOW_STATE_DTYPE.itemsize == FLOW_STATE_BYTES
 assert FLOW_REPORT_DTYPE.itemsize == 96 and FLOW_COUNTERS_DTYPE.itemsize == 64
+
+
+# ---- pcap2mgen / text interleave (include/mgenx.h) ----
+class PcapInfo(ctypes.Structure):      # mgenx_pcap_info
+    _fields_ = [("link_type", ctypes.c_uint32), ("flags", ctypes.c_uint32),
+                ("snaplen", ctypes.c_uint32), ("rsv", ctypes.c_uint32),
+                ("n_records", ctypes.c_uint64), ("consumed", ctypes.c_uint64)]
+
+
+class TextSrc(ctypes.Structure):       # mgenx_text_src
+    _fields_ = [("text", ctypes.c_void_p), ("line_off", ctypes.c_void_p),
+                ("n_lines", ctypes.c_uint32), ("kind", ctypes.c_uint32),
+                ("index", ctypes.c_void_p), ("index_stride", ctypes.c_uint32),
+                ("rsv", ctypes.c_uint32)]
+
+
+TEXT_PER_RECORD, TEXT_OWNER, TEXT_MAP, TEXT_SCATTER = 0, 1, 2, 3
+LOG_EPOCH, LOG_NO_DATA, LOG_NO_GPS, LOG_SKIP_ERR = 0x1, 0x2, 0x4, 0x8
+FLOW_NONE = 0xFFFFFFFF
+DLT_EN10MB, DLT_LINUX_SLL = 1, 113
+PCAP_NSEC, PCAP_SWAPPED = 0x1, 0x2

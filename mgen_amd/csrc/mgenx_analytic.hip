@@ -223,7 +223,8 @@ flow_update_wave_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
                         const uint32_t* __restrict__ begin, const uint32_t* __restrict__ end,
                         const uint32_t* __restrict__ order, const FRec* __restrict__ recs,
                         mgenx_flow_report* __restrict__ reports, uint32_t per_flow,
-                        uint32_t* __restrict__ report_count, int abl) {
+                        uint32_t* __restrict__ report_count, uint32_t* __restrict__ report_rec,
+                        int abl) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t f = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
   if (f >= n_flows) return;
@@ -245,7 +246,8 @@ flow_update_wave_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
   uint64_t nrep = sp->n_reports;
   uint32_t rcount = report_count[f];
 
-  auto update = [&](uint32_t seq, uint32_t rxs, uint32_t rxu, uint32_t msg, double lat) {
+  auto update = [&](uint32_t seq, uint32_t rxs, uint32_t rxu, uint32_t msg, double lat,
+                    uint32_t rec) {
     const Tm rx = {(int64_t)rxs, (int64_t)rxu};
     if (!valid) {  // mgenAnalytic.cpp:80-99
       valid = true;
@@ -343,6 +345,7 @@ flow_update_wave_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
         rp->latency_max = r_max;
         rp->rx_sec = rx.sec;
         rp->rx_usec = rx.usec;
+        if (report_rec) report_rec[(size_t)f * per_flow + rcount] = rec;
       }
       rcount++;
       nrep++;
@@ -423,8 +426,10 @@ flow_update_wave_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
   const uint32_t oa = ldo(i0), ob = ldo(i0 + 64u);
   uint32_t oc = ldo(i0 + 128u);
   FRec cur = recs[oa], nx1 = recs[ob], nx2;
+  uint32_t ocur = oa, on1 = ob, on2;  // input record indices of cur / nx1 / nx2
   while (i0 < e) {
     nx2 = recs[oc];
+    on2 = oc;
     oc = ldo(i0 + 192u);
     const uint32_t cnt = min(64u, e - i0);
     const uint64_t lbits = __builtin_bit_cast(uint64_t, cur.latency);
@@ -473,11 +478,14 @@ flow_update_wave_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
              (uint32_t)__builtin_amdgcn_readlane((int)cur.rxs, (int)k),
              (uint32_t)__builtin_amdgcn_readlane((int)cur.rxu, (int)k),
              (uint32_t)__builtin_amdgcn_readlane((int)cur.len, (int)k),
-             __builtin_bit_cast(double, lb));
+             __builtin_bit_cast(double, lb),
+             (uint32_t)__builtin_amdgcn_readlane((int)ocur, (int)k));
       k++;
     }
     cur = nx1;
     nx1 = nx2;
+    ocur = on1;
+    on1 = on2;
     i0 += 64u;
   }
 
@@ -618,8 +626,8 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
                                      const uint32_t* rxs, const uint32_t* rxu, uint32_t n,
                                      mgenx_flow_state* flows, uint32_t n_flows,
                                      mgenx_flow_report* reports, uint32_t per_flow,
-                                     uint32_t* report_count, hipStream_t stream, char* err,
-                                     size_t errn) {
+                                     uint32_t* report_count, uint32_t* report_rec,
+                                     hipStream_t stream, char* err, size_t errn) {
   mgenx_flow_ws& ws = *static_cast<mgenx_flow_ws*>(wsp);
   if (n == 0 || n_flows == 0) return MGENX_OK;
   int end_bit = 1;
@@ -671,7 +679,7 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
 #endif
   hipLaunchKernelGGL(flow_update_wave_kernel, dim3((n_flows + 3) / 4), dim3(256), 0, stream,
                      flows, n_flows, d_begin, d_end, vals_out, recs, reports, per_flow,
-                     report_count, abl);
+                     report_count, report_rec, abl);
   e = hipGetLastError();
   if (e != hipSuccess) {
     snprintf(err, errn, "flow_reduce: %s", hipGetErrorString(e));

@@ -59,6 +59,16 @@ extern "C" int mgenx_data_walk_exec(void* ws, const uint8_t* slab, const uint64_
                                     uint64_t* reps, uint32_t rep_cap, uint32_t* totals,
                                     hipStream_t stream, char* err, size_t errn);
 extern "C" void mgenx_log_ws_free(void* p);
+extern "C" int mgenx_text_interleave_run(void* ws, const mgenx_text_src* srcs, uint32_t n_src,
+                                         uint32_t n_rec, char* out, uint64_t cap,
+                                         uint64_t* rec_off, hipStream_t stream, char* err,
+                                         size_t errn);
+extern "C" int mgenx_pcap_parse_run(const uint8_t* dev_buf, uint64_t buf_bytes,
+                                    const uint64_t* dev_pkt_off, uint32_t n, uint32_t link_type,
+                                    uint32_t flags, uint64_t* dev_udp_off, uint32_t* dev_udp_len,
+                                    mgenx_addr* dev_src, int32_t* dev_ttl, uint32_t* dev_rx_sec,
+                                    uint32_t* dev_rx_usec, uint8_t* dev_status,
+                                    hipStream_t stream);
 extern "C" int mgenx_log_recv_run(void* ws, bool binary, const uint8_t* slab,
                                   uint64_t slab_bytes, const uint64_t* rec_off,
                                        uint64_t stride, const mgenx_cols* cols,
@@ -78,8 +88,8 @@ extern "C" int mgenx_flow_reduce_run(void* ws, const uint32_t* flow_idx, const u
                                      const uint32_t* rxs, const uint32_t* rxu, uint32_t n,
                                      mgenx_flow_state* flows, uint32_t n_flows,
                                      mgenx_flow_report* reports, uint32_t per_flow,
-                                     uint32_t* report_count, hipStream_t stream, char* err,
-                                     size_t errn);
+                                     uint32_t* report_count, uint32_t* report_rec,
+                                     hipStream_t stream, char* err, size_t errn);
 
 struct mgenx_ctx {
   int device = 0;
@@ -657,6 +667,17 @@ int mgenx_flow_reduce(mgenx_ctx* ctx, const uint32_t* dev_flow_idx, const uint32
                       const uint32_t* dev_rx_usec, uint32_t n, mgenx_flow_state* dev_flows,
                       uint32_t n_flows, mgenx_flow_report* dev_reports, uint32_t per_flow,
                       uint32_t* dev_report_count, void* stream) {
+  return mgenx_flow_reduce_ex(ctx, dev_flow_idx, dev_seq, dev_tx_sec, dev_tx_usec, dev_msg_len,
+                              dev_rx_sec, dev_rx_usec, n, dev_flows, n_flows, dev_reports,
+                              per_flow, dev_report_count, nullptr, stream);
+}
+
+int mgenx_flow_reduce_ex(mgenx_ctx* ctx, const uint32_t* dev_flow_idx, const uint32_t* dev_seq,
+                         const uint32_t* dev_tx_sec, const uint32_t* dev_tx_usec,
+                         const uint16_t* dev_msg_len, const uint32_t* dev_rx_sec,
+                         const uint32_t* dev_rx_usec, uint32_t n, mgenx_flow_state* dev_flows,
+                         uint32_t n_flows, mgenx_flow_report* dev_reports, uint32_t per_flow,
+                         uint32_t* dev_report_count, uint32_t* dev_report_rec, void* stream) {
   if (!ctx) return MGENX_EINVAL;
   if (n == 0 || n_flows == 0) return MGENX_OK;
   if (!dev_flow_idx || !dev_seq || !dev_tx_sec || !dev_tx_usec || !dev_msg_len ||
@@ -667,7 +688,8 @@ int mgenx_flow_reduce(mgenx_ctx* ctx, const uint32_t* dev_flow_idx, const uint32
   if (!ctx->flow_ws) ctx->flow_ws = mgenx_flow_ws_new();
   return mgenx_flow_reduce_run(ctx->flow_ws, dev_flow_idx, dev_seq, dev_tx_sec, dev_tx_usec,
                                dev_msg_len, dev_rx_sec, dev_rx_usec, n, dev_flows, n_flows,
-                               dev_reports, per_flow, dev_report_count, (hipStream_t)stream,
+                               dev_reports, per_flow, dev_report_count, dev_report_rec,
+                               (hipStream_t)stream,
                                ctx->err, sizeof(ctx->err));
 }
 
@@ -853,6 +875,41 @@ int mgenx_crc32_update(mgenx_ctx* ctx, const uint8_t* dev_data, const uint64_t* 
                                      ctx->d_tabs + 1024, ctx->d_xpow, dev_state_in,
                                      dev_state_out, (hipStream_t)stream);
   return e == hipSuccess ? MGENX_OK : set_err(ctx, e, "crc32_update");
+}
+
+int mgenx_text_interleave(mgenx_ctx* ctx, const mgenx_text_src* srcs, uint32_t n_src,
+                          uint32_t n_rec, char* dev_out, uint64_t out_cap, uint64_t* dev_rec_off,
+                          void* stream) {
+  if (!ctx || !dev_rec_off || n_src > MGENX_TEXT_MAX_SRC || (n_src && !srcs) ||
+      (out_cap && !dev_out) || n_rec > 0x7FFFFFFEu)
+    return MGENX_EINVAL;
+  for (uint32_t s = 0; s < n_src; s++) {
+    const mgenx_text_src& t = srcs[s];
+    if (t.kind > MGENX_TEXT_SCATTER || !t.line_off ||
+        (t.kind != MGENX_TEXT_PER_RECORD && !t.index) ||
+        (t.kind == MGENX_TEXT_OWNER && t.index_stride == 0))
+      return MGENX_EINVAL;
+  }
+  hipSetDevice(ctx->device);
+  if (!ctx->log_ws) ctx->log_ws = mgenx_log_ws_new();
+  return mgenx_text_interleave_run(ctx->log_ws, srcs, n_src, n_rec, dev_out, out_cap,
+                                   dev_rec_off, (hipStream_t)stream, ctx->err, sizeof(ctx->err));
+}
+
+int mgenx_pcap_parse(mgenx_ctx* ctx, const uint8_t* dev_buf, uint64_t buf_bytes,
+                     const uint64_t* dev_pkt_off, uint32_t n, uint32_t link_type,
+                     uint32_t flags, uint64_t* dev_udp_off, uint32_t* dev_udp_len,
+                     mgenx_addr* dev_src, int32_t* dev_ttl, uint32_t* dev_rx_sec,
+                     uint32_t* dev_rx_usec, uint8_t* dev_status, void* stream) {
+  if (!ctx) return MGENX_EINVAL;
+  if (n == 0) return MGENX_OK;
+  if (!dev_buf || !dev_pkt_off || !dev_udp_off || !dev_udp_len || !dev_src || !dev_ttl ||
+      !dev_rx_sec || !dev_rx_usec || !dev_status)
+    return MGENX_EINVAL;
+  hipSetDevice(ctx->device);
+  return mgenx_pcap_parse_run(dev_buf, buf_bytes, dev_pkt_off, n, link_type, flags, dev_udp_off,
+                              dev_udp_len, dev_src, dev_ttl, dev_rx_sec, dev_rx_usec, dev_status,
+                              (hipStream_t)stream);
 }
 
 }  // extern "C"

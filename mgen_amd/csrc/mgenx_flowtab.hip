@@ -198,6 +198,38 @@ __global__ void flowtab_commit_kernel(FlowSlot* __restrict__ tab, const uint32_t
   if (i == 0) n_flows[0] = n_flows[1];
 }
 
+// MgenAnalytic::Init's key fields (mgenAnalytic.cpp:28-71) of every numbered slot: the flow's
+// report_msg key, at its dense index
+__global__ void flowtab_keys_kernel(const FlowSlot* __restrict__ tab, uint32_t cap_slots,
+                                    int protocol, mgenx_report_key* __restrict__ keys,
+                                    uint32_t cap) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= cap_slots) return;
+  const FlowSlot& sl = tab[s];
+  if (sl.state == kSlotEmpty || sl.state == kSlotBusy || sl.index >= cap) return;
+  const FlowKey& k = sl.key;
+  mgenx_report_key o;
+  const uint32_t dl = k.w[8] & 0xFFu, sl_ = k.w[9] & 0xFFu;
+  o.dst.len = (uint8_t)dl;
+  o.dst.type = dl == 4 ? 1 : dl == 16 ? 2 : 0;
+  o.dst.port = (uint16_t)(k.w[8] >> 16);
+  o.src.len = (uint8_t)sl_;
+  o.src.type = sl_ == 4 ? 1 : sl_ == 16 ? 2 : 0;
+  o.src.port = (uint16_t)(k.w[9] >> 16);
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      o.dst.addr[4 * j + b] = (uint8_t)(k.w[j] >> (8 * b));
+      o.src.addr[4 * j + b] = (uint8_t)(k.w[4 + j] >> (8 * b));
+    }
+  }
+  o.flow_id = k.w[10];
+  o.protocol = (uint8_t)protocol;
+  o.rsv[0] = o.rsv[1] = o.rsv[2] = 0;
+  keys[sl.index] = o;
+}
+
 }  // namespace mgenx
 
 using namespace mgenx;
@@ -281,6 +313,15 @@ int mgenx_flow_lookup(mgenx_ctx* ctx, mgenx_flow_table* t, const mgenx_cols* col
   if (dev_n_flows &&
       hipMemcpyAsync(dev_n_flows, t->counters, 4, hipMemcpyDeviceToDevice, s) != hipSuccess)
     return MGENX_EDEVICE;
+  return hipGetLastError() == hipSuccess ? MGENX_OK : MGENX_EDEVICE;
+}
+
+int mgenx_flow_keys(mgenx_ctx* ctx, const mgenx_flow_table* t, int protocol,
+                    mgenx_report_key* dev_keys, uint32_t cap, void* stream) {
+  if (!ctx || !t || (cap && !dev_keys)) return MGENX_EINVAL;
+  if (cap == 0) return MGENX_OK;
+  hipLaunchKernelGGL(flowtab_keys_kernel, dim3((t->cap + 255) / 256), dim3(256), 0,
+                     (hipStream_t)stream, t->slots, t->cap, protocol, dev_keys, cap);
   return hipGetLastError() == hipSuccess ? MGENX_OK : MGENX_EDEVICE;
 }
 

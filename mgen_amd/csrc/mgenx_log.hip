@@ -395,6 +395,11 @@ __global__ void __launch_bounds__(kLogThreads) log_kernel(LogParams p) {
   const uint32_t i = blockIdx.x * kLogThreads + threadIdx.x;
   if (i >= p.n) return;
   const LogRec r = gather(p, i);
+  // MGENX_LOG_SKIP_ERR: a record Unpack rejected gets no line (pcap2mgen.cpp:428-432)
+  if (!kBinary && (p.opts & MGENX_LOG_SKIP_ERR) && r.err) {
+    if (!kWrite) p.lens[i] = 0;
+    return;
+  }
   if (!kWrite) {
     CountSink s;
     format_any<CountSink, kBinary>(s, p, i, r);
@@ -1004,6 +1009,85 @@ __global__ void __launch_bounds__(256) data_walk_kernel(WalkParams p) {
   }
 }
 
+// ---- mgenx_text_interleave: several line sources -> one log in record order ----
+struct TextParams {
+  mgenx_text_src src[MGENX_TEXT_MAX_SRC];
+  uint32_t n_src;
+  uint32_t n_rec;
+  uint8_t* out;
+  uint64_t cap;
+  uint64_t* rec_off;  // n_rec + 1
+  uint64_t* lens;     // n_rec + 1 (workspace)
+};
+
+// first line k in [0, n) whose owner is >= r
+__device__ __forceinline__ uint32_t owner_lb(const mgenx_text_src& t, uint32_t r) {
+  uint32_t lo = 0, hi = t.n_lines;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (t.index[(size_t)mid * t.index_stride] < r) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// record i's lines of source t: [lo, hi)
+__device__ __forceinline__ void text_range(const mgenx_text_src& t, uint32_t i, uint32_t& lo,
+                                           uint32_t& hi) {
+  lo = hi = 0;
+  if (t.kind == MGENX_TEXT_PER_RECORD) {
+    if (i < t.n_lines) { lo = i; hi = i + 1; }
+  } else if (t.kind == MGENX_TEXT_OWNER) {
+    lo = owner_lb(t, i);
+    hi = owner_lb(t, i + 1);
+  } else {
+    const uint32_t l = t.index[i];
+    if (l < t.n_lines) { lo = l; hi = l + 1; }
+  }
+}
+
+// MGENX_TEXT_SCATTER -> a record -> line map (the map is pre-filled with MGENX_FLOW_NONE)
+__global__ void __launch_bounds__(256) text_scatter_kernel(const uint32_t* __restrict__ rec_of_line,
+                                                           uint32_t n_lines, uint32_t n_rec,
+                                                           uint32_t* __restrict__ map) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n_lines) return;
+  const uint32_t r = rec_of_line[k];
+  if (r < n_rec) map[r] = k;
+}
+
+__global__ void __launch_bounds__(256) text_len_kernel(TextParams p) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > p.n_rec) return;
+  uint64_t len = 0;
+  if (i < p.n_rec) {
+    for (uint32_t s = 0; s < p.n_src; s++) {
+      uint32_t lo, hi;
+      text_range(p.src[s], i, lo, hi);
+      if (hi > lo) len += p.src[s].line_off[hi] - p.src[s].line_off[lo];
+    }
+  }
+  p.lens[i] = len;
+}
+
+// one wave per record: each source's bytes copied with the lanes side by side
+__global__ void __launch_bounds__(256) text_copy_kernel(TextParams p) {
+  const uint32_t i = blockIdx.x * 4u + (threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63u;
+  if (i >= p.n_rec) return;
+  uint64_t pos = p.rec_off[i];
+  if (p.rec_off[i + 1] > p.cap) return;  // does not fit: the caller reads rec_off[n]
+  for (uint32_t s = 0; s < p.n_src; s++) {
+    uint32_t lo, hi;
+    text_range(p.src[s], i, lo, hi);
+    if (hi <= lo) continue;
+    const uint64_t a = p.src[s].line_off[lo], b = p.src[s].line_off[hi];
+    const uint8_t* src = reinterpret_cast<const uint8_t*>(p.src[s].text);
+    for (uint64_t k = a + lane; k < b; k += 64) p.out[pos + (k - a)] = src[k];
+    pos += b - a;
+  }
+}
+
 }  // namespace mgenx
 
 // per-stream scratch for the two-pass line formatters and the walk's scans
@@ -1096,6 +1180,58 @@ extern "C" int mgenx_data_walk_run(void* wsp, mgenx::WalkParams* pp, uint32_t* t
         hipMemcpyAsync(totals + 1, rb + n, 4, hipMemcpyDeviceToDevice, stream) != hipSuccess)
       return MGENX_EDEVICE;
   }
+  return hipGetLastError() == hipSuccess ? MGENX_OK : MGENX_EDEVICE;
+}
+
+extern "C" int mgenx_text_interleave_run(void* wsp, const mgenx_text_src* srcs, uint32_t n_src,
+                                         uint32_t n_rec, char* out, uint64_t cap,
+                                         uint64_t* rec_off, hipStream_t stream, char* err,
+                                         size_t errn) {
+  mgenx_log_ws& ws = ws_for(wsp, stream);
+  mgenx::TextParams p;
+  memset(&p, 0, sizeof(p));
+  for (uint32_t s = 0; s < n_src; s++) p.src[s] = srcs[s];
+  p.n_src = n_src; p.n_rec = n_rec; p.out = reinterpret_cast<uint8_t*>(out); p.cap = cap;
+  p.rec_off = rec_off;
+  size_t scan_bytes = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, (uint64_t*)nullptr,
+                                         (uint64_t*)nullptr, (int)n_rec + 1, stream);
+  const size_t len_bytes = (((size_t)n_rec + 1) * 8 + 255) & ~(size_t)255;
+  const size_t map_bytes = (((size_t)n_rec + 1) * 4 + 255) & ~(size_t)255;
+  uint32_t n_scatter = 0;
+  for (uint32_t s = 0; s < n_src; s++) n_scatter += srcs[s].kind == MGENX_TEXT_SCATTER;
+  void* mem;
+  int rc = rep_ws(ws, len_bytes + n_scatter * map_bytes + scan_bytes, &mem, err, errn);
+  if (rc != MGENX_OK) return rc;
+  p.lens = static_cast<uint64_t*>(mem);
+  // scatter sources become record -> line maps in the workspace
+  char* maps = static_cast<char*>(mem) + len_bytes;
+  for (uint32_t s = 0; s < n_src; s++) {
+    if (p.src[s].kind != MGENX_TEXT_SCATTER) continue;
+    uint32_t* map = reinterpret_cast<uint32_t*>(maps);
+    maps += map_bytes;
+    if (hipMemsetAsync(map, 0xFF, (size_t)n_rec * 4 + 4, stream) != hipSuccess) {
+      snprintf(err, errn, "text interleave: memset failed");
+      return MGENX_EDEVICE;
+    }
+    if (p.src[s].n_lines)
+      hipLaunchKernelGGL(mgenx::text_scatter_kernel, dim3((p.src[s].n_lines + 255) / 256),
+                         dim3(256), 0, stream, p.src[s].index, p.src[s].n_lines, n_rec, map);
+    p.src[s].index = map;
+    p.src[s].kind = MGENX_TEXT_MAP;
+  }
+  hipLaunchKernelGGL(mgenx::text_len_kernel, dim3((n_rec + 1 + 255) / 256), dim3(256), 0, stream,
+                     p);
+  size_t have = scan_bytes;
+  if (hipcub::DeviceScan::ExclusiveSum(static_cast<uint8_t*>(mem) + len_bytes +
+                                           n_scatter * map_bytes,
+                                       have, p.lens, rec_off, (int)n_rec + 1,
+                                       stream) != hipSuccess) {
+    snprintf(err, errn, "text interleave: scan failed");
+    return MGENX_EDEVICE;
+  }
+  if (n_rec)
+    hipLaunchKernelGGL(mgenx::text_copy_kernel, dim3((n_rec + 3) / 4), dim3(256), 0, stream, p);
   return hipGetLastError() == hipSuccess ? MGENX_OK : MGENX_EDEVICE;
 }
 

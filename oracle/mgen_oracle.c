@@ -1016,6 +1016,7 @@ uint32_t or_sizeof(int which)
 /* ------------------------------------------------------------------ */
 #include <arpa/inet.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <time.h>
 
 static int log_ts(char* out, uint32_t sec, uint32_t usec, int epoch)
@@ -1538,4 +1539,236 @@ int or_data_walk(const uint8_t* pay, uint32_t len, int controller, uint32_t* cmd
         }
     }
     return 0;
+}
+
+/* ==== pcap2mgen (src/common/pcap2mgen.cpp:252-482) ====================================
+ * The main loop over a pcap file image.  The frame walk restates protolib's ProtoPktETH /
+ * ProtoPktIP / ProtoPktUDP, which is not vendored (parity unpinned at that layer): any
+ * link type other than DLT_LINUX_SLL is read as Ethernet (the reference does the same,
+ * :365-367), frames with hdr.len > 4094 are "invalid Ether frame" (the 4-KiB parse buffer,
+ * :337-340, 369-373), an 802.1Q tag is stepped over, IPv4 needs IHL >= 5 and a total length
+ * within the frame, IPv6 a payload length within it, UDP a length field within the IP payload.
+ * A packet whose UDP payload lies past the captured bytes is skipped (the reference would
+ * read stale bytes of its parse buffer there). */
+static uint32_t pc_u32(const uint8_t* b, int sw)
+{
+    uint32_t v;
+    memcpy(&v, b, 4);
+    return sw ? __builtin_bswap32(v) : v;
+}
+static uint32_t pc_be16(const uint8_t* b) { return (uint32_t)b[0] << 8 | b[1]; }
+
+int or_pcap_frame(const uint8_t* rec, uint32_t link_type, uint32_t flags, uint32_t* udp_off,
+                  uint32_t* udp_len, or_addr* src, int* ttl, uint32_t* sec, uint32_t* usec)
+{
+    const int sw = (flags & 2) != 0;
+    memset(src, 0, sizeof(*src));
+    *ttl = -1;
+    *udp_off = 0;
+    *udp_len = 0;
+    *sec = pc_u32(rec, sw);
+    const uint32_t frac = pc_u32(rec + 4, sw);
+    *usec = (flags & 1) ? frac / 1000u : frac;
+    const uint32_t caplen = pc_u32(rec + 8, sw), wirelen = pc_u32(rec + 12, sw);
+    const uint8_t* d = rec + 16;
+    const uint32_t maxBytes = 4094;
+    const uint32_t num = caplen < maxBytes ? caplen : maxBytes;    /* :346-347 */
+    uint32_t eth_type, ip0, ip_len;
+    if (link_type == 113) {                                         /* DLT_LINUX_SLL :354-364 */
+        if (num < 16) return 1;
+        eth_type = pc_be16(d + 14);
+        ip0 = 16;
+        ip_len = num - 16;
+    } else {                                                        /* ProtoPktETH :368-380 */
+        if (wirelen > maxBytes || wirelen < 14) return 1;
+        if (num < 14) return 5;
+        eth_type = pc_be16(d + 12);
+        uint32_t hl = 14;
+        if (eth_type == 0x8100) {
+            if (wirelen < 18) return 1;
+            if (num < 18) return 5;
+            eth_type = pc_be16(d + 16);
+            hl = 18;
+        }
+        ip0 = hl;
+        ip_len = wirelen - hl;
+    }
+    if (eth_type != 0x0800 && eth_type != 0x86DD) return 2;        /* srcAddr invalid :422 */
+    if (ip_len < 1) return 3;
+    if (ip0 >= num) return 5;
+    const uint32_t ver = d[ip0] >> 4;
+    uint32_t l4, l4_len;
+    if (ver == 4) {                                                 /* ProtoPktIPv4 :395-402 */
+        if (ip_len < 20) return 3;
+        if (ip0 + 20 > num) return 5;
+        const uint32_t ihl = (d[ip0] & 15u) * 4u, tot = pc_be16(d + ip0 + 2);
+        if (ihl < 20 || tot < ihl || tot > ip_len) return 3;
+        *ttl = d[ip0 + 8];
+        src->type = OR_ADDR_IPV4;
+        src->len = 4;
+        memcpy(src->addr, d + ip0 + 12, 4);
+        if (d[ip0 + 9] != 17) return 4;
+        l4 = ip0 + ihl;
+        l4_len = tot - ihl;
+    } else if (ver == 6) {                                          /* ProtoPktIPv6 :403-410 */
+        if (ip_len < 40) return 3;
+        if (ip0 + 40 > num) return 5;
+        const uint32_t pl = pc_be16(d + ip0 + 4);
+        if (40u + pl > ip_len) return 3;
+        *ttl = d[ip0 + 7];
+        src->type = OR_ADDR_IPV6;
+        src->len = 16;
+        memcpy(src->addr, d + ip0 + 8, 16);
+        if (d[ip0 + 6] != 17) return 4;
+        l4 = ip0 + 40;
+        l4_len = pl;
+    } else {
+        return 3;
+    }
+    if (l4_len < 8) return 4;                                       /* ProtoPktUDP :424-425 */
+    if (l4 + 8 > num) return 5;
+    const uint32_t ul = pc_be16(d + l4 + 4);
+    if (ul < 8 || ul > l4_len) return 4;
+    src->port = (uint16_t)pc_be16(d + l4);
+    if (l4 + ul > num) return 5;
+    *udp_off = 16 + l4 + 8;
+    *udp_len = ul - 8;
+    return 0;
+}
+
+typedef struct {
+    or_addr  src, dst;
+    uint32_t flow_id;
+    int      used, sign;
+    or_analytic a;
+} pc_flow;
+
+static int pc_addr_eq(const or_addr* x, const or_addr* y)
+{
+    return x->len == y->len && x->port == y->port && memcmp(x->addr, y->addr, x->len) == 0;
+}
+
+/* MgenAnalyticTable::FindFlow / Insert (mgenAnalytic.cpp:312-328): open addressing */
+static pc_flow* pc_find(pc_flow** tab, uint32_t* cap, uint32_t* n, const or_addr* src,
+                        const or_addr* dst, uint32_t flow_id, double window)
+{
+    if (2 * (*n + 1) > *cap) {
+        uint32_t nc = *cap ? 2 * *cap : 64;
+        pc_flow* nt = (pc_flow*)calloc(nc, sizeof(pc_flow));
+        for (uint32_t i = 0; i < *cap; i++) {
+            if (!(*tab)[i].used) continue;
+            uint32_t h = ((*tab)[i].flow_id * 2654435761u ^ (*tab)[i].src.port ^
+                          (uint32_t)(*tab)[i].dst.port << 16) & (nc - 1);
+            while (nt[h].used) h = (h + 1) & (nc - 1);
+            nt[h] = (*tab)[i];
+        }
+        free(*tab);
+        *tab = nt;
+        *cap = nc;
+    }
+    uint32_t h = (flow_id * 2654435761u ^ src->port ^ (uint32_t)dst->port << 16) & (*cap - 1);
+    while ((*tab)[h].used) {
+        pc_flow* f = &(*tab)[h];
+        if (f->flow_id == flow_id && pc_addr_eq(&f->src, src) && pc_addr_eq(&f->dst, dst)) return f;
+        h = (h + 1) & (*cap - 1);
+    }
+    pc_flow* f = &(*tab)[h];
+    memset(f, 0, sizeof(*f));
+    f->used = 1;
+    f->src = *src;
+    f->dst = *dst;
+    f->flow_id = flow_id;
+    or_analytic_init(&f->a, window);                 /* MgenAnalytic::Init :455 */
+    (*n)++;
+    return f;
+}
+
+static void pc_emit(char* out, uint64_t cap, uint64_t* pos, const char* s, uint32_t len)
+{
+    if (out && *pos + len <= cap) memcpy(out + *pos, s, len);
+    *pos += len;
+}
+
+uint64_t or_pcap2mgen(const uint8_t* file, uint64_t nbytes, int analytics, int log_rx,
+                      double window, uint32_t opts, char* out, uint64_t cap, uint64_t* n_pkts,
+                      uint8_t* status)
+{
+    uint64_t pos = 0, npk = 0;
+    if (n_pkts) *n_pkts = 0;
+    if (nbytes < 24) return 0;
+    uint32_t magic;
+    memcpy(&magic, file, 4);
+    int sw = 0, ns = 0;
+    if (magic == 0xa1b2c3d4u) {}
+    else if (magic == 0xd4c3b2a1u) sw = 1;
+    else if (magic == 0xa1b23c4du) ns = 1;
+    else if (magic == 0x4d3cb2a1u) sw = ns = 1;
+    else return 0;
+    const uint32_t flags = (ns ? 1u : 0u) | (sw ? 2u : 0u);
+    const uint32_t link = pc_u32(file + 20, sw) & 0x0FFFFFFFu;
+    pc_flow* tab = NULL;
+    uint32_t tcap = 0, tn = 0;
+    char* line = (char*)malloc(1 << 16);
+    uint64_t off = 24;
+    while (off + 16 <= nbytes) {                                    /* pcap_next :344 */
+        const uint32_t caplen = pc_u32(file + off + 8, sw);
+        if (off + 16 + (uint64_t)caplen > nbytes) break;
+        const uint8_t* rec = file + off;
+        off += 16 + (uint64_t)caplen;
+        uint32_t uo, ul, sec, usec;
+        or_addr src;
+        int ttl;
+        const int st = or_pcap_frame(rec, link, flags, &uo, &ul, &src, &ttl, &sec, &usec);
+        if (status) status[npk] = (uint8_t)st;
+        npk++;
+        if (st != 0) continue;
+        const uint8_t* pay = rec + uo;
+        or_fields f;
+        or_unpack(pay, ul, &f);                                     /* :428-432 */
+        if (!f.ok) continue;
+        if (analytics) {                                            /* :445-473 */
+            or_addr dst;
+            memset(&dst, 0, sizeof dst);
+            dst.type = f.dst_type;
+            dst.len = f.dst_len;
+            dst.port = f.dst_port;
+            memcpy(dst.addr, f.dst_addr, 16);
+            if (dst.len > 16) dst.len = 16;
+            pc_flow* fl = pc_find(&tab, &tcap, &tn, &src, &dst, f.flow_id, window);
+            const or_time rx = {(int64_t)sec, (int64_t)usec};
+            const or_time tx = {(int64_t)f.tx_sec, (int64_t)f.tx_usec};
+            if (or_analytic_update(&fl->a, rx, f.msg_len, tx, f.seq_num)) {
+                uint8_t rb[52];
+                or_report_build(&fl->src, &fl->dst, fl->flow_id, 1, fl->a.report_duration,
+                                fl->a.report_latency_ave, fl->a.report_latency_min,
+                                fl->a.report_latency_max, fl->a.report_rate_ave,
+                                fl->a.report_loss_ave, -1.0, &fl->sign, rb);
+                const uint32_t n = or_log_report(rb, fl->a.report_duration, fl->a.report_rate_ave,
+                                                 fl->a.report_loss_ave, fl->a.report_latency_ave,
+                                                 fl->a.report_latency_min, fl->a.report_latency_max,
+                                                 fl->a.report_msg_count, sec, usec, opts, line);
+                pc_emit(out, cap, &pos, line, n);
+            }
+        }
+        /* msg.LogRecvEvent(outfile, false, false, log_rx, false, true, payload, flush, ttl, ts) */
+        if (log_rx) {
+            const uint32_t n = or_log_recv_text(&f, pay, &src, sec, usec, 1, ttl,
+                                                opts | OR_LOG_NO_DATA, line);
+            pc_emit(out, cap, &pos, line, n);
+        }
+        if (f.payload_type == 1 && f.payload_len > 0) {             /* mgenMsg.cpp:1104-1137 */
+            uint32_t cmds[64], reps[256], nc = 0, nr = 0;
+            (void)or_data_walk(pay + f.payload_off, f.payload_len, 1, cmds, &nc, 64, reps, &nr,
+                               256);
+            for (uint32_t k = 0; k < nr && k < 256; k++) {
+                const uint32_t n = or_log_report_recv(pay + f.payload_off + reps[k], &src, sec,
+                                                      usec, opts, line);
+                pc_emit(out, cap, &pos, line, n);
+            }
+        }
+    }
+    free(line);
+    free(tab);
+    if (n_pkts) *n_pkts = npk;
+    return pos;
 }

@@ -285,4 +285,18 @@ int      or_data_walk(const uint8_t* pay, uint32_t len, int controller, uint32_t
                       uint32_t* n_cmds, uint32_t cap_cmds, uint32_t* reps, uint32_t* n_reps,
                       uint32_t cap_reps);
 
+/* ---- pcap2mgen (pcap2mgen.cpp:252-482) ----
+ * or_pcap_frame: one pcap record (16-byte header + data) -> the UDP payload's offset from the
+ * record header and length, IP source + UDP source port, TTL / hop limit, timestamp.  Returns
+ * 0 UDP, 1 bad Ethernet frame, 2 not IP, 3 bad IP, 4 not UDP, 5 truncated capture
+ * (flags: 1 nanosecond file, 2 swapped byte order).
+ * or_pcap2mgen: the whole main loop over a file image -> the log text (analytic REPORT lines,
+ * RECV lines when log_rx, received REPORT lines), written to out while it fits `cap`;
+ * returns the full length.  status (optional): or_pcap_frame's result per record. */
+int      or_pcap_frame(const uint8_t* rec, uint32_t link_type, uint32_t flags, uint32_t* udp_off,
+                       uint32_t* udp_len, or_addr* src, int* ttl, uint32_t* sec, uint32_t* usec);
+uint64_t or_pcap2mgen(const uint8_t* file, uint64_t nbytes, int analytics, int log_rx,
+                      double window, uint32_t opts, char* out, uint64_t cap, uint64_t* n_pkts,
+                      uint8_t* status);
+
 #endif

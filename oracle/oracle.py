@@ -540,3 +540,46 @@ def data_walk(payload: bytes, controller=True, cap=4096):
                         _ptr(reps), ctypes.byref(nr), cap)
     c = [(int(x) >> 2, int(x) & 3) for x in cmds[:min(nc.value, cap)]]
     return st, c, [int(x) for x in reps[:min(nr.value, cap)]]
+
+
+# ---------------------------------------------------------------- pcap2mgen
+def _pcap_protos():
+    L = lib()
+    if getattr(L, "_pcap_ready", False):
+        return L
+    P, u32, u64, i32, d = (ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int,
+                           ctypes.c_double)
+    L.or_pcap_frame.argtypes = [P, u32, u32, ctypes.POINTER(u32), ctypes.POINTER(u32), P,
+                                ctypes.POINTER(i32), ctypes.POINTER(u32), ctypes.POINTER(u32)]
+    L.or_pcap_frame.restype = i32
+    L.or_pcap2mgen.argtypes = [P, u64, i32, i32, d, u32, P, u64, ctypes.POINTER(u64), P]
+    L.or_pcap2mgen.restype = u64
+    L._pcap_ready = True
+    return L
+
+
+def pcap_frame(rec: bytes, link_type=1, flags=0):
+    """One pcap record (16-byte header + data): (status, udp_off, udp_len, src, ttl, sec, usec)."""
+    L = _pcap_protos()
+    b = np.frombuffer(bytes(rec) + b"\0" * 8, np.uint8).copy()
+    uo, ul, ttl = ctypes.c_uint32(0), ctypes.c_uint32(0), ctypes.c_int(0)
+    sec, usec = ctypes.c_uint32(0), ctypes.c_uint32(0)
+    src = np.zeros(1, ADDR_DTYPE)
+    st = L.or_pcap_frame(_ptr(b), link_type, flags, ctypes.byref(uo), ctypes.byref(ul),
+                         _ptr(src), ctypes.byref(ttl), ctypes.byref(sec), ctypes.byref(usec))
+    return st, uo.value, ul.value, src[0], ttl.value, sec.value, usec.value
+
+
+def pcap2mgen(file: bytes, analytics=False, log_rx=True, window=1.0, opts=0):
+    """pcap2mgen's whole main loop: (log text, per-record frame status)."""
+    L = _pcap_protos()
+    f = np.frombuffer(bytes(file), np.uint8)
+    npk = ctypes.c_uint64(0)
+    st = np.zeros(max(1, len(file) // 16), np.uint8)
+    need = L.or_pcap2mgen(_ptr(f), len(f), int(analytics), int(log_rx), float(window), opts,
+                          None, 0, ctypes.byref(npk), _ptr(st))
+    out = np.zeros(max(1, need), np.uint8)
+    n = L.or_pcap2mgen(_ptr(f), len(f), int(analytics), int(log_rx), float(window), opts,
+                       _ptr(out), len(out), ctypes.byref(npk), _ptr(st))
+    assert n == need
+    return out[:n].tobytes(), st[:npk.value].copy()
