@@ -533,7 +533,7 @@ int mgenx_log_recv_text(mgenx_ctx* ctx, const uint8_t* dev_slab, const uint64_t*
 /* The binary log form of the same events (MgenMsg::LogRecvEvent / LogRecvError binary
  * branches, src/common/mgenMsg.cpp:652-710, 958-1033): per record an event header (type,
  * protocol, BE length, BE rx time, BE source port, source type/length/address) followed, for
- * RECV, by hdr_len + payload_len + 2 message bytes with CHECKSUM cleared in the flags byte
+ * RECV, by hdr_len + payload_len message bytes with CHECKSUM cleared in the flags byte
  * (the hdr_len extended column is also required); RERR ends with the BE error code.
  * Message bytes past slab_bytes are written as zero (the reference's stale receive buffer).
  * dev_rec_pos has the same meaning as dev_line_off.  The file header line the reference
@@ -647,6 +647,45 @@ int mgenx_pcap_parse(mgenx_ctx* ctx, const uint8_t* dev_buf, uint64_t buf_bytes,
                      uint32_t flags, uint64_t* dev_udp_off, uint32_t* dev_udp_len,
                      mgenx_addr* dev_src, int32_t* dev_ttl, uint32_t* dev_rx_sec,
                      uint32_t* dev_rx_usec, uint8_t* dev_status, void* stream);
+
+/* ---- MgenMsg::ConvertBinaryLog: binary log -> text log (src/common/mgenMsg.cpp:1417-1900) --
+ * mgenx_binlog_index (HOST memory, no device work) checks the header line ("mgen
+ * version=<4|5> ... type=binary_log\n" and its NUL, :1437-1518) and walks the records
+ * {type, protocol, BE recordLength <= 1024, body}: the offsets of the records the reference
+ * converts go to rec_off (host memory), up to the first one it stops at -- info->status:
+ * MGENX_BINLOG_OK (end of file), _HEADER (not a binary log), _TOO_LONG (recordLength > 1024),
+ * _EVENT (RERR or an unknown event type, or an unknown address type: the reference returns
+ * false there, :1586-1590, 1892-1895), _SHORT (the file ends inside a record).
+ * mgenx_convert_binary_log (device) writes the text the reference writes for those records,
+ * in order: RECV (Unpack of the stored message + LogRecvEvent text with the source and event
+ * time, the converter's argument order at :1607 putting log_flush in the ttl slot, then the
+ * REPORT lines of MGEN_DATA items), SEND (Unpack + LogSendEvent text: tx time, srcPort 0),
+ * LISTEN / IGNORE / JOIN / LEAVE / START / STOP / ON / ACCEPT / CONNECT / DISCONNECT / OFF /
+ * SHUTDOWN / RECONNECT lines (:1628-1891).  A RECV / SEND record whose stored message Unpack
+ * rejects (mgen never writes one) gives no line.  flags: MGENX_BINLOG_NO_RX (log_rx off),
+ * MGENX_BINLOG_FLUSH (log_flush on); opts: MGENX_LOG_EPOCH / _NO_DATA / _NO_GPS.
+ * dev_rec_pos[n + 1] = byte offsets of each record's text; dev_text is written only when the
+ * total fits text_cap.  Synchronous (intermediate sizes are read back); the context keeps a
+ * workspace that grows with the log. */
+#define MGENX_BINLOG_OK       0
+#define MGENX_BINLOG_HEADER   1
+#define MGENX_BINLOG_TOO_LONG 2
+#define MGENX_BINLOG_EVENT    3
+#define MGENX_BINLOG_SHORT    4
+#define MGENX_BINLOG_NO_RX  0x1
+#define MGENX_BINLOG_FLUSH  0x2
+typedef struct {
+    uint64_t n_records;   /* records to convert (only the first cap offsets are written) */
+    uint64_t consumed;    /* bytes up to the end of the last of them */
+    int32_t  status;      /* MGENX_BINLOG_* */
+    uint32_t version;     /* the header line's major version */
+} mgenx_binlog_info;
+int mgenx_binlog_index(const uint8_t* buf, uint64_t nbytes, uint64_t* rec_off, uint64_t cap,
+                       mgenx_binlog_info* info);
+int mgenx_convert_binary_log(mgenx_ctx* ctx, const uint8_t* dev_buf, uint64_t buf_bytes,
+                             const uint64_t* dev_rec_off, uint32_t n, uint32_t flags,
+                             uint32_t opts, char* dev_text, uint64_t text_cap,
+                             uint64_t* dev_rec_pos, void* stream);
 
 /* ---- multi-GPU exchange (RCCL over xGMI) ----
  * One communicator per rank (one process per GPU): rank 0 calls mgenx_comm_unique_id and

@@ -20,7 +20,7 @@ from ._abi import (  # noqa: F401
     DEC_HDRLEN, DEC_HOST, DEC_GPS, DEC_PTYPE, DEC_PLEN, RX_NOLOG, RX_FORCE, RX_PREV,
     RX_STATE_DTYPE, SCAN_HALO, SCAN_REUSE, ADDR_DTYPE, REPORT_KEY_DTYPE, DATA_CONTROLLER,
     PcapInfo, TextSrc, TEXT_PER_RECORD, TEXT_OWNER, TEXT_MAP, TEXT_SCATTER, PCAP_NSEC, PCAP_SWAPPED, LOG_EPOCH, LOG_NO_DATA, LOG_NO_GPS,
-    LOG_SKIP_ERR, FLOW_NONE, DLT_EN10MB, DLT_LINUX_SLL,
+    LOG_SKIP_ERR, FLOW_NONE, DLT_EN10MB, DLT_LINUX_SLL, BinlogInfo, BINLOG_NO_RX, BINLOG_FLUSH,
 )
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -39,7 +39,7 @@ EXPORTED_SYMBOLS = (
     "mgenx_comm_destroy", "mgenx_allreduce_flows", "mgenx_allgather_u64",
     "mgenx_flow_table_create", "mgenx_flow_table_destroy", "mgenx_flow_lookup",
     "mgenx_flow_reduce_ex", "mgenx_flow_keys", "mgenx_text_interleave", "mgenx_pcap_index",
-    "mgenx_pcap_parse",
+    "mgenx_pcap_parse", "mgenx_binlog_index", "mgenx_convert_binary_log",
 )
 DIAG_SYMBOLS = ("mgenx_set_tuning", "mgenx_diag_stream_read", "mgenx_diag_group_rw")
 
@@ -92,6 +92,8 @@ def load(diag: bool = False):
     L.mgenx_text_interleave.argtypes = [P, P, u32, u32, P, u64, P, P]
     L.mgenx_pcap_index.argtypes = [P, u64, P, u64, ctypes.POINTER(PcapInfo)]
     L.mgenx_pcap_parse.argtypes = [P, P, u64, P, u32, u32, u32, P, P, P, P, P, P, P, P]
+    L.mgenx_binlog_index.argtypes = [P, u64, P, u64, ctypes.POINTER(BinlogInfo)]
+    L.mgenx_convert_binary_log.argtypes = [P, P, u64, P, u32, u32, u32, P, u64, P, P]
     if diag:
         L.mgenx_set_tuning.argtypes = [P, i32, i32]
         L.mgenx_diag_stream_read.argtypes = [P, P, u64, P, i32, P]
@@ -472,6 +474,27 @@ class Engine:
             cap = total
         raise MgenxError("mgenx_text_interleave: output did not fit")
 
+    # ------------------------------------------------------------ ConvertBinaryLog
+    def convert_binary_log(self, buf, rec_off, n, flags=0, opts=0, cap=None):
+        """MgenMsg::ConvertBinaryLog over records indexed by binlog_index (device tensors):
+        returns (text uint8 tensor, per-record offsets of n + 1).  Synchronous."""
+        torch = self.torch
+        dev = buf.device
+        pos = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        cap = cap if cap is not None else max(1, n) * 200
+        for _ in range(2):
+            out = torch.empty(max(cap, 1), dtype=torch.uint8, device=dev)
+            self._check(self.lib.mgenx_convert_binary_log(self.ctx, _ptr(buf), buf.numel(),
+                                                          _ptr(rec_off), n, flags, opts,
+                                                          _ptr(out), cap, _ptr(pos),
+                                                          _stream(self.device)),
+                        "mgenx_convert_binary_log")
+            total = int(pos[n].item())
+            if total <= cap:
+                return out[:total], pos
+            cap = total
+        raise MgenxError("mgenx_convert_binary_log: text did not fit")
+
     # ------------------------------------------------------------ pcap2mgen
     def pcap_parse(self, buf, pkt_off, n, link_type, flags=0):
         """pcap2mgen's frame walk per record (mgenx_pcap_parse): returns a dict of device
@@ -657,6 +680,41 @@ def pcap_index(buf) -> tuple:
     if rc != 0:
         raise MgenxError("mgenx_pcap_index failed")
     return offs[:int(info.n_records)], info
+
+
+def binlog_index(buf) -> tuple:
+    """mgenx_binlog_index over a host binary log image: (record offsets as uint64 numpy
+    array, BinlogInfo).  Host work only."""
+    L = load()
+    b = np.frombuffer(buf, np.uint8) if not isinstance(buf, np.ndarray) else buf
+    info = BinlogInfo()
+    p = b.ctypes.data_as(ctypes.c_void_p)
+    if L.mgenx_binlog_index(p, b.size, None, 0, ctypes.byref(info)) != 0:
+        raise MgenxError("mgenx_binlog_index failed")
+    offs = np.zeros(max(1, int(info.n_records)), np.uint64)
+    if L.mgenx_binlog_index(p, b.size, offs.ctypes.data_as(ctypes.c_void_p), offs.size,
+                            ctypes.byref(info)) != 0:
+        raise MgenxError("mgenx_binlog_index failed")
+    return offs[:int(info.n_records)], info
+
+
+def convert_binary_log(log, log_rx=True, flush=False, opts=0, device=0) -> tuple:
+    """ConvertBinaryLog of a host binary log image on the GPU: (text bytes, BinlogInfo)."""
+    import torch
+    offs, info = binlog_index(log)
+    n = int(info.n_records)
+    if n == 0:
+        return b"", info
+    eng = Engine(device)
+    try:
+        dev = f"cuda:{device}"
+        buf = torch.from_numpy(np.frombuffer(bytes(log), np.uint8).copy()).to(dev)
+        ro = torch.from_numpy(offs.view(np.int64).copy()).to(dev)
+        flags = (0 if log_rx else BINLOG_NO_RX) | (BINLOG_FLUSH if flush else 0)
+        text, _ = eng.convert_binary_log(buf, ro, n, flags, opts)
+        return text.cpu().numpy().tobytes(), info
+    finally:
+        eng.close()
 
 
 def to_device(arr: np.ndarray, device=0):

@@ -157,3 +157,12 @@ LOG_EPOCH, LOG_NO_DATA, LOG_NO_GPS, LOG_SKIP_ERR = 0x1, 0x2, 0x4, 0x8
 FLOW_NONE = 0xFFFFFFFF
 DLT_EN10MB, DLT_LINUX_SLL = 1, 113
 PCAP_NSEC, PCAP_SWAPPED = 0x1, 0x2
+
+
+class BinlogInfo(ctypes.Structure):    # mgenx_binlog_info
+    _fields_ = [("n_records", ctypes.c_uint64), ("consumed", ctypes.c_uint64),
+                ("status", ctypes.c_int32), ("version", ctypes.c_uint32)]
+
+
+BINLOG_OK, BINLOG_HEADER, BINLOG_TOO_LONG, BINLOG_EVENT, BINLOG_SHORT = 0, 1, 2, 3, 4
+BINLOG_NO_RX, BINLOG_FLUSH = 0x1, 0x2

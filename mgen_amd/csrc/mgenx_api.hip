@@ -91,6 +91,40 @@ extern "C" int mgenx_flow_reduce_run(void* ws, const uint32_t* flow_idx, const u
                                      uint32_t* report_count, uint32_t* report_rec,
                                      hipStream_t stream, char* err, size_t errn);
 
+extern "C" int mgenx_binlog_parse_exec(const uint8_t* buf, const uint64_t* rec_off, uint32_t n,
+                                       uint64_t* msg_off, uint32_t* msg_len, mgenx_addr* src,
+                                       uint32_t* ev_sec, uint32_t* ev_usec, uint32_t* aux,
+                                       uint8_t* kind, uint8_t* proto, hipStream_t stream);
+extern "C" int mgenx_binlog_lines_exec(void* wsp, const uint8_t* buf, const uint64_t* rec_off,
+                                       uint32_t n, uint64_t* msg_off, uint32_t* msg_len,
+                                       mgenx_addr* src, uint32_t* ev_sec, uint32_t* ev_usec,
+                                       uint32_t* aux, uint8_t* kind, uint8_t* proto,
+                                       const mgenx_cols* cols, uint32_t log_rx, uint32_t flush,
+                                       uint32_t opts, char* text, uint64_t cap,
+                                       uint64_t* line_off, hipStream_t stream, char* err,
+                                       size_t errn);
+
+// a device buffer that grows on demand (the composite calls' intermediate arrays)
+struct mgenx_grow {
+  void* p = nullptr;
+  size_t n = 0;
+  void* get(size_t need) {
+    if (n < need) {
+      if (p) (void)hipFree(p);
+      p = nullptr;
+      n = 0;
+      if (hipMalloc(&p, need) != hipSuccess) return nullptr;
+      n = need;
+    }
+    return p;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
 struct mgenx_ctx {
   int device = 0;
   int cu_count = 0;
@@ -115,6 +149,7 @@ struct mgenx_ctx {
   uint64_t* tcp_host_dev = nullptr;
   int unpack_variant = 0;          // diagnostic kernel ablation (mgenx_set_tuning)
   int pack_variant = 0;
+  mgenx_grow bl[5];                // mgenx_convert_binary_log: records, lines, pairs, report text
   bool rand_ready = false;
   uint32_t rand_time = 0;
   char err[256] = {0};
@@ -298,6 +333,7 @@ int mgenx_ctx_destroy(mgenx_ctx* c) {
   if (c->tcp_ws) hipFree(c->tcp_ws);
   if (c->rx_ws) hipFree(c->rx_ws);
   if (c->tcp_host) hipHostFree(c->tcp_host);
+  for (mgenx_grow& g : c->bl) g.release();
   for (void* p : ps)
     if (p) hipFree(p);
   delete c;
@@ -910,6 +946,161 @@ int mgenx_pcap_parse(mgenx_ctx* ctx, const uint8_t* dev_buf, uint64_t buf_bytes,
   return mgenx_pcap_parse_run(dev_buf, buf_bytes, dev_pkt_off, n, link_type, flags, dev_udp_off,
                               dev_udp_len, dev_src, dev_ttl, dev_rx_sec, dev_rx_usec, dev_status,
                               (hipStream_t)stream);
+}
+
+// ---- ConvertBinaryLog (mgenMsg.cpp:1417-1900) ----
+int mgenx_binlog_index(const uint8_t* buf, uint64_t nbytes, uint64_t* rec_off, uint64_t cap,
+                       mgenx_binlog_info* info) {
+  if (!buf || !info || (cap && !rec_off)) return MGENX_EINVAL;
+  memset(info, 0, sizeof(*info));
+  info->status = MGENX_BINLOG_HEADER;
+  // "mgen ... version=<4|5> ... type=binary_log\n" and its NUL (:1437-1518)
+  if (nbytes < 4 || memcmp(buf, "mgen", 4) != 0) return MGENX_OK;
+  char hdr[1024];
+  uint64_t k = 3;
+  memcpy(hdr, buf, 4);
+  while (hdr[k] != '\0') {
+    if (++k >= sizeof(hdr) || k >= nbytes) return MGENX_OK;
+    hdr[k] = (char)buf[k];
+  }
+  const char* v = strstr(hdr, "version=");
+  int version = 0;
+  if (!v || 1 != sscanf(v, "version=%d", &version) || (version != 4 && version != 5))
+    return MGENX_OK;
+  const char* t = strstr(v, "type=");
+  char ftype[128];
+  if (!t || 1 != sscanf(t, "type=%127s", ftype) || strcmp(ftype, "binary_log")) return MGENX_OK;
+  info->version = (uint32_t)version;
+  info->status = MGENX_BINLOG_OK;
+  uint64_t off = k + 1, n = 0;
+  // the record walk (:1521-1555) with the reference's stops: a record over 1024 bytes, a short
+  // record, an event type it does not convert (RERR, unknown), an unknown address type
+  while (off + 4 <= nbytes) {
+    const uint8_t* h = buf + off;
+    const uint32_t ev = h[0], rl = (uint32_t)h[2] << 8 | h[3];
+    if (rl > 1024) { info->status = MGENX_BINLOG_TOO_LONG; break; }
+    if (off + 4 + rl > nbytes) { info->status = MGENX_BINLOG_SHORT; break; }
+    const bool addr_ev = ev == 1 || ev == 6 || ev == 7 || (ev >= 10 && ev <= 16);
+    if (ev == 0 || ev == 2 || ev > 16 || (addr_ev && (rl < 11 || (h[14] != 1 && h[14] != 2)))) {
+      info->status = MGENX_BINLOG_EVENT;
+      break;
+    }
+    if (n < cap) rec_off[n] = off;
+    n++;
+    off += 4 + rl;
+  }
+  info->n_records = n;
+  info->consumed = off;
+  return MGENX_OK;
+}
+
+int mgenx_convert_binary_log(mgenx_ctx* ctx, const uint8_t* dev_buf, uint64_t buf_bytes,
+                             const uint64_t* dev_rec_off, uint32_t n, uint32_t flags,
+                             uint32_t opts, char* dev_text, uint64_t text_cap,
+                             uint64_t* dev_rec_pos, void* stream) {
+  if (!ctx || !dev_rec_pos || (text_cap && !dev_text) || n > 0x7FFFFFFEu) return MGENX_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  hipSetDevice(ctx->device);
+  if (n == 0) return hipMemsetAsync(dev_rec_pos, 0, 8, s) == hipSuccess ? MGENX_OK : MGENX_EDEVICE;
+  if (!dev_buf || !dev_rec_off) return MGENX_EINVAL;
+  if (!ctx->log_ws) ctx->log_ws = mgenx_log_ws_new();
+  // per-record arrays and unpack columns in one block (bl[0])
+  const size_t a8 = ((size_t)n * 8 + 255) & ~(size_t)255, a4 = ((size_t)n * 4 + 255) & ~(size_t)255;
+  const size_t a2 = ((size_t)n * 2 + 255) & ~(size_t)255, a1 = ((size_t)n + 255) & ~(size_t)255;
+  const size_t a16 = ((size_t)n * 16 + 255) & ~(size_t)255, a20 = ((size_t)n * 20 + 255) & ~(size_t)255;
+  const size_t need = a8 + 4 * a4 + a20 + 2 * a1 +                       // parse outputs
+                      8 * a4 + 5 * a2 + 9 * a1 + 2 * a16 + a4;           // columns
+  char* m = static_cast<char*>(ctx->bl[0].get(need));
+  if (!m) return set_err(ctx, hipErrorOutOfMemory, "convert_binary_log workspace");
+  auto take = [&](size_t b) { char* q = m; m += b; return q; };
+  uint64_t* msg_off = (uint64_t*)take(a8);
+  uint32_t* msg_len = (uint32_t*)take(a4);
+  uint32_t* ev_sec = (uint32_t*)take(a4);
+  uint32_t* ev_usec = (uint32_t*)take(a4);
+  uint32_t* aux = (uint32_t*)take(a4);
+  mgenx_addr* src = (mgenx_addr*)take(a20);
+  uint8_t* kind = (uint8_t*)take(a1);
+  uint8_t* proto = (uint8_t*)take(a1);
+  mgenx_cols c;
+  memset(&c, 0, sizeof(c));
+  c.flow_id = (uint32_t*)take(a4); c.seq_num = (uint32_t*)take(a4); c.tx_sec = (uint32_t*)take(a4);
+  c.tx_usec = (uint32_t*)take(a4); c.dst_addr4 = (uint32_t*)take(a4);
+  c.payload_off = (uint32_t*)take(a4); c.lat_raw = (uint32_t*)take(a4);
+  c.lon_raw = (uint32_t*)take(a4); c.alt = (int32_t*)take(a4);
+  c.msg_len = (uint16_t*)take(a2); c.dst_port = (uint16_t*)take(a2);
+  c.payload_len = (uint16_t*)take(a2); c.hdr_len = (uint16_t*)take(a2);
+  c.host_port = (uint16_t*)take(a2);
+  c.flags = (uint8_t*)take(a1); c.err = (uint8_t*)take(a1); c.dst_type = (uint8_t*)take(a1);
+  c.dst_len = (uint8_t*)take(a1); c.payload_type = (uint8_t*)take(a1);
+  c.gps_status = (uint8_t*)take(a1); c.host_type = (uint8_t*)take(a1);
+  c.host_len = (uint8_t*)take(a1);
+  (void)take(a1);
+  c.host_addr = (uint8_t*)take(a16); c.dst_addr = (uint8_t*)take(a16);
+  int rc = mgenx_binlog_parse_exec(dev_buf, dev_rec_off, n, msg_off, msg_len, src, ev_sec, ev_usec,
+                                   aux, kind, proto, s);
+  if (rc != MGENX_OK) return set_err(ctx, hipGetLastError(), "binlog parse");
+  rc = mgenx_unpack_batch(ctx, dev_buf, buf_bytes, msg_off, 0, msg_len, 0, n, &c,
+                          MGENX_OPT_SKIP_CRC, stream);
+  if (rc != MGENX_OK) return rc;
+  const uint32_t log_rx = (flags & MGENX_BINLOG_NO_RX) ? 0u : 1u;
+  const uint32_t flush = (flags & MGENX_BINLOG_FLUSH) ? 1u : 0u;
+  // one line per record: size pass, then the text (bl[1] = line offsets + text)
+  const size_t off_bytes = ((size_t)n + 1) * 8;
+  uint64_t* line_off = (uint64_t*)ctx->bl[1].get(off_bytes + 256);
+  if (!line_off) return set_err(ctx, hipErrorOutOfMemory, "convert_binary_log lines");
+  rc = mgenx_binlog_lines_exec(ctx->log_ws, dev_buf, dev_rec_off, n, msg_off, msg_len, src, ev_sec,
+                               ev_usec, aux, kind, proto, &c, log_rx, flush, opts, nullptr, 0,
+                               line_off, s, ctx->err, sizeof(ctx->err));
+  if (rc != MGENX_OK) return rc;
+  uint64_t total = 0;
+  if (hipMemcpyAsync(&total, line_off + n, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess)
+    return set_err(ctx, hipGetLastError(), "convert_binary_log sync");
+  char* text = (char*)ctx->bl[2].get(total + 64);
+  if (!text) return set_err(ctx, hipErrorOutOfMemory, "convert_binary_log text");
+  rc = mgenx_binlog_lines_exec(ctx->log_ws, dev_buf, dev_rec_off, n, msg_off, msg_len, src, ev_sec,
+                               ev_usec, aux, kind, proto, &c, log_rx, flush, opts, text, total,
+                               line_off, s, ctx->err, sizeof(ctx->err));
+  if (rc != MGENX_OK) return rc;
+  mgenx_text_src srcs[2];
+  memset(srcs, 0, sizeof(srcs));
+  srcs[0].text = text; srcs[0].line_off = line_off; srcs[0].n_lines = n;
+  srcs[0].kind = MGENX_TEXT_PER_RECORD;
+  uint32_t n_src = 1;
+  // REPORT items of MGEN_DATA payloads (LogRecvEvent, mgenMsg.cpp:1104-1137)
+  uint32_t cap = 256, n_reps = 0;
+  uint32_t* totals = nullptr;
+  uint64_t* pairs = nullptr;
+  for (int pass = 0; pass < 2; pass++) {
+    char* w = (char*)ctx->bl[3].get(256 + (size_t)cap * 16 + 2 * a1);
+    if (!w) return set_err(ctx, hipErrorOutOfMemory, "convert_binary_log walk");
+    totals = (uint32_t*)w;
+    pairs = (uint64_t*)(w + 256);
+    uint8_t* wst = (uint8_t*)(w + 256 + (size_t)cap * 16);
+    rc = mgenx_data_walk(ctx, dev_buf, msg_off, 0, &c, n, MGENX_DATA_CONTROLLER, wst, wst + a1,
+                         totals + 8, 0, pairs, cap, totals, stream);
+    if (rc != MGENX_OK) return rc;
+    uint32_t tt[2] = {0, 0};
+    if (hipMemcpyAsync(tt, totals, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      return set_err(ctx, hipGetLastError(), "convert_binary_log sync");
+    n_reps = tt[1];
+    if (n_reps <= cap) break;
+    cap = n_reps;
+  }
+  if (n_reps) {
+    uint64_t* rline = (uint64_t*)ctx->bl[4].get(((size_t)n_reps + 1) * 8 + (size_t)n_reps * 320);
+    if (!rline) return set_err(ctx, hipErrorOutOfMemory, "convert_binary_log reports");
+    char* rtext = (char*)(rline + n_reps + 1);
+    rc = mgenx_log_report_recv_text(ctx, dev_buf, pairs, n_reps, src, ev_sec, ev_usec, opts, rtext,
+                                    (uint64_t)n_reps * 320, rline, stream);
+    if (rc != MGENX_OK) return rc;
+    srcs[1].text = rtext; srcs[1].line_off = rline; srcs[1].n_lines = n_reps;
+    srcs[1].kind = MGENX_TEXT_OWNER; srcs[1].index = (const uint32_t*)pairs;
+    srcs[1].index_stride = 4;
+    n_src = 2;
+  }
+  return mgenx_text_interleave(ctx, srcs, n_src, n, dev_text, text_cap, dev_rec_pos, stream);
 }
 
 }  // extern "C"

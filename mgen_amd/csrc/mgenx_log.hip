@@ -16,6 +16,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <stdio.h>
+#include <string.h>
 
 #include <mutex>
 
@@ -282,8 +283,9 @@ __device__ void format_line(S& s, const LogRec& r, const uint8_t* rec, const mge
 
 // Binary RECV / RERR records (MgenMsg::LogRecvEvent binary branch, mgenMsg.cpp:958-1033;
 // LogRecvError binary branch, :652-710): BE header fields, the source address, then for RECV
-// recordLength - index + 4 = hdr + payload_len + 2 message bytes with CHECKSUM cleared in
-// the flags byte.  Bytes past the slab (the reference's stale receive buffer) are written 0.
+// recordLength - index + 4 = hdr + payload_len message bytes (index = 16 + source address
+// length: eventRecordLength counts from after the 4-byte record header, doc/mgen.xml:
+// 4212-4216) with CHECKSUM cleared in the flags byte.  Bytes past the slab are written 0.
 template <typename S>
 __device__ void put_be(S& s, uint32_t v, int bytes) {
   for (int k = bytes - 1; k >= 0; k--) s.put((uint8_t)(v >> (8 * k)));
@@ -318,10 +320,9 @@ __device__ void format_binary(S& s, const LogRec& r, const uint8_t* rec, uint64_
   s.put(av ? src.type : 0);
   s.put((uint8_t)alen);
   for (uint32_t k = 0; k < alen && k < 16; k++) s.put(src.addr[k]);
-  const uint32_t ml = (rl - (14u + alen) + 4u) & 0xFFFFu;
-  // hdr + payload_len + 2 bytes: past the message's own msg_len (no checksum, no padding)
-  // the reference writes stale bytes of its receive buffer; here they are zero, so a record
-  // never depends on its neighbour in the slab
+  const uint32_t ml = (rl - (16u + alen) + 4u) & 0xFFFFu;  // = hdr + payload_len
+  // a byte past the message's own msg_len (only when msg_len < hdr + payload_len) is written
+  // as zero, so a record never depends on its neighbour in the slab
   for (uint32_t k = 0; k < ml; k++) {
     uint8_t b = (k < avail && k < r.msg_len) ? rec[k] : (uint8_t)0;
     if (k == 3) {
@@ -1088,6 +1089,205 @@ __global__ void __launch_bounds__(256) text_copy_kernel(TextParams p) {
   }
 }
 
+// ---- ConvertBinaryLog (mgenMsg.cpp:1417-1900) -----------------------------------------
+// Record i's header at rec_off[i] (mgenx_binlog_index found it): {type, protocol, BE
+// recordLength} then the body.  binlog_parse_kernel places each RECV / SEND record's stored
+// message for mgenx_unpack_batch; binlog_line_kernel writes every record's line.
+struct BinParams {
+  const uint8_t* buf;
+  const uint64_t* rec_off;
+  uint32_t n;
+  uint64_t* msg_off;      // RECV / SEND: the stored message; others: the record (len 0)
+  uint32_t* msg_len;
+  mgenx_addr* src;        // RECV: the source address and port
+  uint32_t* ev_sec;
+  uint32_t* ev_usec;
+  uint32_t* aux;          // SEND over TCP: mgen_msg_len
+  uint8_t* kind;          // event type
+  uint8_t* proto;
+  mgenx_cols cols;        // the unpack outputs (core + extended)
+  uint32_t log_rx, flush, opts;
+  uint8_t* text;
+  uint64_t text_cap;
+  uint64_t* line_off;     // n + 1
+  uint64_t* lens;         // n + 1 (workspace)
+};
+
+__device__ __forceinline__ uint32_t be16(const uint8_t* b) { return (uint32_t)b[0] << 8 | b[1]; }
+__device__ __forceinline__ uint32_t be32(const uint8_t* b) {
+  return (uint32_t)b[0] << 24 | (uint32_t)b[1] << 16 | (uint32_t)b[2] << 8 | b[3];
+}
+
+__global__ void __launch_bounds__(256) binlog_parse_kernel(BinParams p) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p.n) return;
+  const uint64_t ro = p.rec_off[i];
+  const uint8_t* h = p.buf + ro;
+  const uint8_t* b = h + 4;
+  const uint32_t ev = h[0], proto = h[1], rl = be16(h + 2);
+  p.kind[i] = (uint8_t)ev;
+  p.proto[i] = (uint8_t)proto;
+  p.ev_sec[i] = be32(b);
+  p.ev_usec[i] = be32(b + 4);
+  uint64_t mo = ro;
+  uint32_t ml = 0, aux = 0;
+  mgenx_addr a;
+  a.type = 0; a.len = 0; a.port = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) a.addr[k] = 0;
+  if (ev == 1) {  // RECV (:1560-1609): srcPort, type, length, address, then the message
+    const uint32_t alen = b[11];
+    a.type = b[10];
+    a.len = (uint8_t)(alen < 16 ? alen : 16);
+    a.port = (uint16_t)be16(b + 8);
+    for (uint32_t k = 0; k < a.len; k++) a.addr[k] = b[12 + k];
+    mo = ro + 4 + 12 + alen;
+    ml = rl >= 12 + alen ? rl - 12 - alen : 0u;
+  } else if (ev == 3) {  // SEND (:1610-1627): [BE mgen_msg_len for TCP] then the message
+    const uint32_t idx = proto == 2 ? 4u : 0u;
+    if (proto == 2) aux = be32(b);
+    mo = ro + 4 + idx;
+    ml = rl - idx;  // the stored bytes (the reference passes recordLength: the same header)
+  }
+  p.msg_off[i] = mo;
+  p.msg_len[i] = ml;
+  p.src[i] = a;
+  p.aux[i] = aux;
+}
+
+// "host>%s/%hu" of the ON ... RECONNECT records (:1790-1824, 1887-1888)
+template <typename S>
+__device__ void bl_conn_line(S& s, const BinParams& p, const uint8_t* b, uint32_t ev, uint32_t rl) {
+  const bool epoch = (p.opts & MGENX_LOG_EPOCH) != 0;
+  const uint8_t at = b[10];
+  const uint32_t alen = b[11];
+  const uint8_t* a = b + 12;
+  uint32_t i = 12 + alen;
+  const uint32_t aport = be16(b + 8), dport = be16(b + i);
+  i += 2;
+  const uint32_t fid = be32(b + i);
+  i += 4;
+  bool hvalid = false;
+  uint32_t hport = 0, ht = 0, hl = 0;
+  const uint8_t* ha = nullptr;
+  if (i + 4 <= rl) {
+    hport = be16(b + i);
+    i += 2;
+    ht = b[i++];
+    if (ht != 1 && ht != 2) ht = 0;
+    hl = b[i++];
+    if (i + hl <= rl && ht && hl) { ha = b + i; hvalid = true; }
+  }
+  put_ts(s, be32(b), be32(b + 4), epoch);
+  auto addr = [&]() { put_addr(s, at, (uint8_t)alen, a); s.put('/'); put_u64(s, aport); };
+  auto flow_first = [&](const char* name) {  // "<NAME> flow>F srcPort>P dst>A/p"
+    put_str(s, name); put_str(s, " flow>"); put_u64(s, fid); put_str(s, " srcPort>");
+    put_u64(s, dport); put_str(s, " dst>"); addr();
+  };
+  auto flow_dst = [&](const char* name) {    // "<NAME> flow>F dst>A/p srcPort>P"
+    put_str(s, name); put_str(s, " flow>"); put_u64(s, fid); put_str(s, " dst>"); addr();
+    put_str(s, " srcPort>"); put_u64(s, dport);
+  };
+  auto server = [&](const char* name) {      // "<NAME> src>A/p dstPort>P"
+    put_str(s, name); put_str(s, " src>"); addr(); put_str(s, " dstPort>"); put_u64(s, dport);
+  };
+  switch (ev) {
+    case 10: flow_first("ON"); break;
+    case 11: server("ACCEPT"); break;
+    case 13: flow_first("CONNECT"); break;
+    case 12: if (fid) flow_dst("DISCONNECT"); else server("DISCONNECT"); break;
+    case 16: if (fid) flow_dst("RECONNECT"); else server("RECONNECT"); break;
+    case 15: if (fid) flow_dst("SHUTDOWN"); else server("SHUTDOWN"); break;
+    case 14: if (fid) flow_first("OFF"); else server("OFF"); break;
+    default: break;
+  }
+  if (hvalid) {
+    put_str(s, "host>");
+    put_addr(s, (uint8_t)ht, (uint8_t)hl, ha);
+    s.put('/');
+    put_u64(s, hport);
+  }
+  s.put('\n');
+}
+
+template <typename S>
+__device__ void bl_line(S& s, const BinParams& p, uint32_t i) {
+  const uint8_t* h = p.buf + p.rec_off[i];
+  const uint8_t* b = h + 4;
+  const uint32_t ev = h[0], rl = be16(h + 2);
+  const bool epoch = (p.opts & MGENX_LOG_EPOCH) != 0;
+  const mgenx_cols& c = p.cols;
+  if (ev == 1 || ev == 3) {
+    if (c.err[i] != 0) return;  // a stored message Unpack rejects: no line
+    LogParams lp;
+    lp.cols = c;
+    const LogRec r = gather(lp, i);
+    if (ev == 1) {  // LogRecvEvent (:1607): log_flush lands in the ttl argument
+      if (p.log_rx)
+        format_line(s, r, p.buf + p.msg_off[i], p.src[i], p.ev_sec[i], p.ev_usec[i], p.proto[i],
+                    (int)p.flush, p.opts);
+      return;
+    }
+    // LogSendEvent text (:1211-1236) of the unpacked message; time = its tx_time
+    const uint32_t proto = p.proto[i];
+    put_ts(s, r.sec, r.usec, epoch);
+    put_str(s, "SEND proto>");
+    put_str(s, proto == 1 ? "UDP" : proto == 2 ? "TCP" : proto == 3 ? "SINK" : "UNKNOWN");
+    put_str(s, " flow>"); put_u64(s, r.flow);
+    put_str(s, " seq>"); put_u64(s, r.seq);
+    put_str(s, " srcPort>0 dst>");  // a fresh MgenMsg's source
+    put_addr(s, r.dtype, r.dlen, r.daddr);
+    s.put('/'); put_u64(s, r.dport);
+    put_str(s, " size>"); put_u64(s, proto == 2 ? p.aux[i] : r.msg_len); s.put(' ');
+    if (r.htype == 1 || r.htype == 2) {
+      put_str(s, "host>"); put_addr(s, r.htype, r.hlen, r.haddr); s.put('/'); put_u64(s, r.hport);
+    }
+    s.put('\n');
+    return;
+  }
+  if (ev == 4 || ev == 5) {  // LISTEN / IGNORE (:1628-1656)
+    put_ts(s, be32(b), be32(b + 4), epoch);
+    put_str(s, ev == 4 ? "LISTEN proto>" : "IGNORE proto>");
+    const uint32_t pr = b[8];
+    put_str(s, pr == 1 ? "UDP" : pr == 2 ? "TCP" : pr == 3 ? "SINK" : "UNKNOWN");
+    put_str(s, " port>"); put_u64(s, be16(b + 10)); s.put('\n');
+  } else if (ev == 6 || ev == 7) {  // JOIN / LEAVE (:1657-1711)
+    const uint32_t alen = b[11], gport = be16(b + 8), nl = b[12 + alen];
+    put_ts(s, be32(b), be32(b + 4), epoch);
+    put_str(s, ev == 6 ? "JOIN group>" : "LEAVE group>");
+    put_addr(s, b[10], (uint8_t)alen, b + 12);
+    if (nl) {
+      put_str(s, " interface>");
+      for (uint32_t k = 0; k < nl && b[13 + alen + k]; k++) s.put(b[13 + alen + k]);  // "%s"
+    }
+    if (gport) { put_str(s, " port>"); put_u64(s, gport); }
+    s.put('\n');
+  } else if (ev == 8 || ev == 9) {  // START / STOP (:1712-1729)
+    put_ts(s, be32(b), be32(b + 4), epoch);
+    put_str(s, ev == 8 ? "START\n" : "STOP\n");
+  } else if (ev >= 10 && ev <= 16) {
+    bl_conn_line(s, p, b, ev, rl);
+  }
+}
+
+template <bool kWrite>
+__global__ void __launch_bounds__(kLogThreads) binlog_line_kernel(BinParams p) {
+  const uint32_t i = blockIdx.x * kLogThreads + threadIdx.x;
+  if (i >= p.n) return;
+  if (!kWrite) {
+    // only RECV payloads are walked for REPORT items (LogRecvEvent, :1104-1137)
+    if (p.kind[i] != 1) p.cols.payload_type[i] = 0xFF;
+    CountSink s;
+    bl_line(s, p, i);
+    p.lens[i] = s.n;
+  } else {
+    const uint64_t off = p.line_off[i], end = p.line_off[i + 1];
+    if (end > p.text_cap) return;
+    WriteSink s{p.text + off};
+    bl_line(s, p, i);
+  }
+}
+
 }  // namespace mgenx
 
 // per-stream scratch for the two-pass line formatters and the walk's scans
@@ -1232,6 +1432,69 @@ extern "C" int mgenx_text_interleave_run(void* wsp, const mgenx_text_src* srcs, 
   }
   if (n_rec)
     hipLaunchKernelGGL(mgenx::text_copy_kernel, dim3((n_rec + 3) / 4), dim3(256), 0, stream, p);
+  return hipGetLastError() == hipSuccess ? MGENX_OK : MGENX_EDEVICE;
+}
+
+static mgenx::BinParams bin_params(const uint8_t* buf, const uint64_t* rec_off, uint32_t n,
+                                   uint64_t* msg_off, uint32_t* msg_len, mgenx_addr* src,
+                                   uint32_t* ev_sec, uint32_t* ev_usec, uint32_t* aux,
+                                   uint8_t* kind, uint8_t* proto) {
+  mgenx::BinParams p;
+  memset(&p, 0, sizeof(p));
+  p.buf = buf; p.rec_off = rec_off; p.n = n; p.msg_off = msg_off; p.msg_len = msg_len;
+  p.src = src; p.ev_sec = ev_sec; p.ev_usec = ev_usec; p.aux = aux; p.kind = kind;
+  p.proto = proto;
+  return p;
+}
+
+extern "C" int mgenx_binlog_parse_exec(const uint8_t* buf, const uint64_t* rec_off, uint32_t n,
+                                       uint64_t* msg_off, uint32_t* msg_len, mgenx_addr* src,
+                                       uint32_t* ev_sec, uint32_t* ev_usec, uint32_t* aux,
+                                       uint8_t* kind, uint8_t* proto, hipStream_t stream) {
+  mgenx::BinParams p = bin_params(buf, rec_off, n, msg_off, msg_len, src, ev_sec, ev_usec, aux,
+                                  kind, proto);
+  if (p.n)
+    hipLaunchKernelGGL(mgenx::binlog_parse_kernel, dim3((p.n + 255) / 256), dim3(256), 0, stream,
+                       p);
+  return hipGetLastError() == hipSuccess ? MGENX_OK : MGENX_EDEVICE;
+}
+
+extern "C" int mgenx_binlog_lines_exec(void* wsp, const uint8_t* buf, const uint64_t* rec_off,
+                                       uint32_t n, uint64_t* msg_off, uint32_t* msg_len,
+                                       mgenx_addr* src, uint32_t* ev_sec, uint32_t* ev_usec,
+                                       uint32_t* aux, uint8_t* kind, uint8_t* proto,
+                                       const mgenx_cols* cols, uint32_t log_rx, uint32_t flush,
+                                       uint32_t opts, char* text, uint64_t cap,
+                                       uint64_t* line_off, hipStream_t stream, char* err,
+                                       size_t errn) {
+  mgenx_log_ws& ws = ws_for(wsp, stream);
+  mgenx::BinParams p = bin_params(buf, rec_off, n, msg_off, msg_len, src, ev_sec, ev_usec, aux,
+                                  kind, proto);
+  p.cols = *cols;
+  p.log_rx = log_rx; p.flush = flush; p.opts = opts;
+  p.text = reinterpret_cast<uint8_t*>(text); p.text_cap = cap; p.line_off = line_off;
+  size_t scan_bytes = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, (uint64_t*)nullptr,
+                                         (uint64_t*)nullptr, (int)n + 1, stream);
+  const size_t len_bytes = (((size_t)n + 1) * 8 + 255) & ~(size_t)255;
+  void* mem;
+  int rc = rep_ws(ws, len_bytes + scan_bytes, &mem, err, errn);
+  if (rc != MGENX_OK) return rc;
+  p.lens = static_cast<uint64_t*>(mem);
+  const int grid = (int)((n + mgenx::kLogThreads - 1) / mgenx::kLogThreads);
+  if (n)
+    hipLaunchKernelGGL((mgenx::binlog_line_kernel<false>), dim3(grid), dim3(mgenx::kLogThreads),
+                       0, stream, p);
+  hipLaunchKernelGGL(mgenx::log_tail_kernel, dim3(1), dim3(64), 0, stream, p.lens, n);
+  size_t have = scan_bytes;
+  if (hipcub::DeviceScan::ExclusiveSum(static_cast<uint8_t*>(mem) + len_bytes, have, p.lens,
+                                       p.line_off, (int)n + 1, stream) != hipSuccess) {
+    snprintf(err, errn, "binlog: scan failed");
+    return MGENX_EDEVICE;
+  }
+  if (n)
+    hipLaunchKernelGGL((mgenx::binlog_line_kernel<true>), dim3(grid), dim3(mgenx::kLogThreads),
+                       0, stream, p);
   return hipGetLastError() == hipSuccess ? MGENX_OK : MGENX_EDEVICE;
 }
 

@@ -1115,10 +1115,12 @@ uint32_t or_log_recv_text(const or_fields* f, const uint8_t* rec, const or_addr*
 /*   MgenMsg::LogRecvError binary branch  mgenMsg.cpp:652-710         */
 /* RECV: eventType, protocol, BE recordLength = 12 + srcLen + hdr +    */
 /* payload_len, BE rx sec/usec, BE src port, src type/len/address,     */
-/* then recordLength - index + 4 = hdr + payload_len + 2 bytes of the  */
-/* message with CHECKSUM cleared in the flags byte (CHECKSUM_ERROR set */
-/* when flagged).  Bytes past avail or past the message's own msg_len */
-/* (the reference's stale receive buffer) read as zero here: unpinned. */
+/* then recordLength - index + 4 message bytes, index = 16 + srcLen   */
+/* (the 4-byte record header, 8 time, 2 port, type, length, address): */
+/* hdr + payload_len bytes, as eventRecordLength counts from after the */
+/* header (doc/mgen.xml:4212-4216), with CHECKSUM cleared in the flags */
+/* byte (CHECKSUM_ERROR set when flagged).  Bytes past avail or past   */
+/* the message's own msg_len read as zero here.                        */
 /* ------------------------------------------------------------------ */
 static uint32_t put_be16(uint8_t* p, uint32_t v) { p[0] = (uint8_t)(v >> 8); p[1] = (uint8_t)v; return 2; }
 static uint32_t put_be32(uint8_t* p, uint32_t v) { put32(p, v); return 4; }
@@ -1153,7 +1155,7 @@ uint32_t or_log_recv_binary(const or_fields* f, const uint8_t* rec, uint64_t ava
     *p++ = atype;
     *p++ = (uint8_t)alen;
     memcpy(p, src->addr, alen); p += alen;
-    const uint32_t index = 14 + alen;
+    const uint32_t index = 16 + alen;
     const uint32_t ml = (rl - index + 4) & 0xFFFF;
     for (uint32_t i = 0; i < ml; i++) {
         uint8_t b = (i < avail && i < f->msg_len) ? rec[i] : 0;
@@ -1770,5 +1772,211 @@ uint64_t or_pcap2mgen(const uint8_t* file, uint64_t nbytes, int analytics, int l
     free(line);
     free(tab);
     if (n_pkts) *n_pkts = npk;
+    return pos;
+}
+
+/* ==== ConvertBinaryLog (mgenMsg.cpp:1417-1900) ========================================
+ * The binary log -> text log conversion over a file image.  The header line ("mgen
+ * version=<4|5>... type=binary_log\n\0") is checked, then records {type, protocol, BE
+ * recordLength <= 1024, recordLength bytes} are converted until the end of the file or the
+ * first record the reference rejects (RERR and unknown event types, an unknown address type,
+ * a short record): *status then says why (OR_BL_*), and the text so far is kept, as the
+ * reference has already written it.  RECV: Unpack of the stored message (recordLength - 12 -
+ * srcLen bytes) and LogRecvEvent with the reference's argument order at :1607, which puts
+ * log_flush in the ttl slot ("ttl>0 " / "ttl>1 "); SEND: Unpack and LogSendEvent (srcPort 0:
+ * a fresh MgenMsg's source); LISTEN / IGNORE / JOIN / LEAVE / START / STOP / ON / ACCEPT /
+ * CONNECT / DISCONNECT / OFF / SHUTDOWN / RECONNECT lines as :1628-1891.  A RECV or SEND
+ * record whose stored message Unpack rejects (never written by mgen) gives no line here. */
+enum { OR_BL_OK = 0, OR_BL_HEADER = 1, OR_BL_TOO_LONG = 2, OR_BL_EVENT = 3, OR_BL_SHORT = 4 };
+
+static void bl_addr(or_addr* a, uint8_t type, const uint8_t* p, uint32_t len, uint16_t port)
+{
+    memset(a, 0, sizeof(*a));
+    a->type = type;
+    a->len = (uint8_t)(len > 16 ? 16 : len);
+    memcpy(a->addr, p, a->len);
+    a->port = port;
+}
+
+static uint32_t bl_send_line(const or_fields* f, int protocol, uint32_t mgen_msg_len,
+                             uint32_t opts, char* out)
+{
+    char* p = out;
+    p += log_ts(p, f->tx_sec, f->tx_usec, (opts & OR_LOG_EPOCH) != 0);
+    p += sprintf(p, "SEND proto>%s flow>%lu seq>%lu srcPort>%hu dst>", log_proto(protocol),
+                 (unsigned long)f->flow_id, (unsigned long)f->seq_num, (unsigned short)0);
+    p += log_addr(p, f->dst_type, f->dst_len, f->dst_addr);
+    p += sprintf(p, "/%hu", f->dst_port);
+    if (protocol == 2) p += sprintf(p, " size>%lu ", (unsigned long)mgen_msg_len);
+    else p += sprintf(p, " size>%u ", (unsigned)f->msg_len);
+    if (f->host_type == OR_ADDR_IPV4 || f->host_type == OR_ADDR_IPV6) {
+        p += sprintf(p, "host>");
+        p += log_addr(p, f->host_type, f->host_len, f->host_addr);
+        p += sprintf(p, "/%hu\n", f->host_port);
+    } else {
+        p += sprintf(p, "\n");
+    }
+    return (uint32_t)(p - out);
+}
+
+uint64_t or_convert_binary_log(const uint8_t* file, uint64_t nbytes, int log_rx, int flush,
+                               uint32_t opts, char* out, uint64_t cap, int* status,
+                               uint64_t* n_records)
+{
+    uint64_t pos = 0, nrec = 0;
+    *status = OR_BL_HEADER;
+    if (n_records) *n_records = 0;
+    if (nbytes < 4 || memcmp(file, "mgen", 4) != 0) return 0;
+    char hdr[1024];
+    uint64_t k = 3;
+    memcpy(hdr, file, 4);
+    while (hdr[k] != '\0') {                        /* the header line and its NUL */
+        if (++k >= sizeof hdr || k >= nbytes) return 0;
+        hdr[k] = (char)file[k];
+    }
+    const char* v = strstr(hdr, "version=");
+    int version;
+    if (!v || 1 != sscanf(v, "version=%d", &version) || (version != 4 && version != 5)) return 0;
+    const char* t = strstr(v, "type=");
+    char ftype[128];
+    if (!t || 1 != sscanf(t, "type=%127s", ftype) || strcmp(ftype, "binary_log")) return 0;
+    const int ep = (opts & OR_LOG_EPOCH) != 0;
+    char* line = (char*)malloc(1 << 16);
+    uint64_t off = k + 1;
+    *status = OR_BL_OK;
+    while (1) {
+        if (off + 4 > nbytes) break;                 /* feof: done */
+        const uint8_t* h = file + off;
+        const int ev = h[0], proto = h[1];
+        const uint32_t rl = (uint32_t)h[2] << 8 | h[3];
+        if (rl > 1024) { *status = OR_BL_TOO_LONG; break; }
+        if (off + 4 + rl > nbytes) { *status = OR_BL_SHORT; break; }
+        const uint8_t* b = h + 4;
+        off += 4 + rl;
+        uint32_t n = 0;
+        const uint32_t sec = get32(b), usec = get32(b + 4);
+        if (ev == 1) {                                               /* RECV :1560-1609 */
+            const uint8_t at = b[10];
+            if (at != 1 && at != 2) { *status = OR_BL_EVENT; break; }
+            const uint32_t alen = b[11];
+            or_addr src;
+            bl_addr(&src, at, b + 12, alen, (uint16_t)(b[8] << 8 | b[9]));
+            const uint32_t idx = 12 + alen;
+            or_fields f;
+            or_unpack(b + idx, rl >= idx ? rl - idx : 0, &f);
+            nrec++;
+            if (!f.ok) continue;
+            if (log_rx) {
+                n = or_log_recv_text(&f, b + idx, &src, sec, usec, proto, flush ? 1 : 0, opts,
+                                     line);
+                pc_emit(out, cap, &pos, line, n);
+            }
+            if (f.payload_type == 1 && f.payload_len > 0) {
+                uint32_t cmds[64], reps[256], nc = 0, nr = 0;
+                (void)or_data_walk(b + idx + f.payload_off, f.payload_len, 1, cmds, &nc, 64, reps,
+                                   &nr, 256);
+                for (uint32_t j = 0; j < nr && j < 256; j++) {
+                    n = or_log_report_recv(b + idx + f.payload_off + reps[j], &src, sec, usec, opts,
+                                           line);
+                    pc_emit(out, cap, &pos, line, n);
+                }
+            }
+            continue;
+        }
+        if (ev == 3) {                                               /* SEND :1610-1627 */
+            uint32_t idx = 0, mml = 0;
+            if (proto == 2) { mml = get32(b); idx = 4; }
+            or_fields f;
+            or_unpack(b + idx, rl - idx, &f);    /* the reference passes recordLength */
+            nrec++;
+            if (!f.ok) continue;
+            n = bl_send_line(&f, proto, mml, opts, line);
+            pc_emit(out, cap, &pos, line, n);
+            continue;
+        }
+        char* p = line;
+        if (ev == 4 || ev == 5) {                                    /* LISTEN / IGNORE */
+            p += log_ts(p, sec, usec, ep);
+            p += sprintf(p, "%s proto>%s port>%hu\n", ev == 4 ? "LISTEN" : "IGNORE",
+                         log_proto(b[8]), (unsigned short)(b[10] << 8 | b[11]));
+        } else if (ev == 6 || ev == 7) {                             /* JOIN / LEAVE */
+            const uint8_t at = b[10];
+            if (at != 1 && at != 2) { *status = OR_BL_EVENT; break; }
+            const uint32_t alen = b[11];
+            const uint16_t gport = (uint16_t)(b[8] << 8 | b[9]);
+            uint32_t nl = b[12 + alen];
+            char iface[256];
+            memcpy(iface, b + 13 + alen, nl);
+            iface[nl] = '\0';
+            p += log_ts(p, sec, usec, ep);
+            p += sprintf(p, "%s group>", ev == 6 ? "JOIN" : "LEAVE");
+            p += log_addr(p, at, (uint8_t)alen, b + 12);
+            if (nl) p += sprintf(p, " interface>%s", iface);
+            if (gport) p += sprintf(p, " port>%hu\n", gport);
+            else p += sprintf(p, "\n");
+        } else if (ev == 8 || ev == 9) {                             /* START / STOP */
+            p += log_ts(p, sec, usec, ep);
+            p += sprintf(p, "%s\n", ev == 8 ? "START" : "STOP");
+        } else if (ev >= 10 && ev <= 16) {                           /* :1730-1891 */
+            const uint8_t at = b[10];
+            if (at != 1 && at != 2) { *status = OR_BL_EVENT; break; }
+            const uint32_t alen = b[11];
+            uint32_t i = 12 + alen;
+            char a[64];
+            log_addr(a, at, (uint8_t)alen, b + 12);
+            const uint16_t aport = (uint16_t)(b[8] << 8 | b[9]);
+            const uint16_t dport = (uint16_t)(b[i] << 8 | b[i + 1]);
+            i += 2;
+            const unsigned long fid = get32(b + i);
+            i += 4;
+            int hvalid = 0;
+            uint16_t hport = 0;
+            uint8_t ht = 0;
+            uint32_t hl = 0;
+            char hs[64];
+            if (i + 4 <= rl) {
+                hport = (uint16_t)(b[i] << 8 | b[i + 1]);
+                i += 2;
+                ht = b[i++];
+                if (ht != 1 && ht != 2) ht = 0;
+                hl = b[i++];
+                if (i + hl <= rl && ht && hl) {
+                    log_addr(hs, ht, (uint8_t)hl, b + i);
+                    hvalid = 1;
+                }
+            }
+            p += log_ts(p, sec, usec, ep);
+            switch (ev) {
+                case 10: p += sprintf(p, "ON flow>%lu srcPort>%hu dst>%s/%hu", fid, dport, a, aport); break;
+                case 11: p += sprintf(p, "ACCEPT src>%s/%hu dstPort>%hu", a, aport, dport); break;
+                case 13: p += sprintf(p, "CONNECT flow>%lu srcPort>%hu dst>%s/%hu", fid, dport, a, aport); break;
+                case 12:
+                    if (fid) p += sprintf(p, "DISCONNECT flow>%lu dst>%s/%hu srcPort>%hu", fid, a, aport, dport);
+                    else p += sprintf(p, "DISCONNECT src>%s/%hu dstPort>%hu", a, aport, dport);
+                    break;
+                case 16:
+                    if (fid) p += sprintf(p, "RECONNECT flow>%lu dst>%s/%hu srcPort>%hu", fid, a, aport, dport);
+                    else p += sprintf(p, "RECONNECT src>%s/%hu dstPort>%hu", a, aport, dport);
+                    break;
+                case 15:
+                    if (fid) p += sprintf(p, "SHUTDOWN flow>%lu dst>%s/%hu srcPort>%hu", fid, a, aport, dport);
+                    else p += sprintf(p, "SHUTDOWN src>%s/%hu dstPort>%hu", a, aport, dport);
+                    break;
+                case 14:
+                    if (fid) p += sprintf(p, "OFF flow>%lu srcPort>%hu dst>%s/%hu", fid, dport, a, aport);
+                    else p += sprintf(p, "OFF src>%s/%hu dstPort>%hu", a, aport, dport);
+                    break;
+            }
+            if (hvalid) p += sprintf(p, "host>%s/%hu", hs, hport);
+            p += sprintf(p, "\n");
+        } else {                                    /* RERR (2) and unknown types :1892-1895 */
+            *status = OR_BL_EVENT;
+            break;
+        }
+        nrec++;
+        pc_emit(out, cap, &pos, line, (uint32_t)(p - line));
+    }
+    free(line);
+    if (n_records) *n_records = nrec;
     return pos;
 }

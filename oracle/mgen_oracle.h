@@ -299,4 +299,12 @@ uint64_t or_pcap2mgen(const uint8_t* file, uint64_t nbytes, int analytics, int l
                       double window, uint32_t opts, char* out, uint64_t cap, uint64_t* n_pkts,
                       uint8_t* status);
 
+/* ---- ConvertBinaryLog (mgenMsg.cpp:1417-1900): a binary log file image -> text; *status
+ * 0 ok, 1 bad header line, 2 record longer than 1024, 3 event the reference rejects (RERR,
+ * unknown type, unknown address type), 4 file ends inside a record.  flush = Mgen's
+ * log_flush (the converter passes it as the RECV lines' ttl). */
+uint64_t or_convert_binary_log(const uint8_t* file, uint64_t nbytes, int log_rx, int flush,
+                               uint32_t opts, char* out, uint64_t cap, int* status,
+                               uint64_t* n_records);
+
 #endif

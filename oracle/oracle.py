@@ -583,3 +583,23 @@ def pcap2mgen(file: bytes, analytics=False, log_rx=True, window=1.0, opts=0):
                        _ptr(out), len(out), ctypes.byref(npk), _ptr(st))
     assert n == need
     return out[:n].tobytes(), st[:npk.value].copy()
+
+
+# ---------------------------------------------------------------- ConvertBinaryLog
+def convert_binary_log(log: bytes, log_rx=True, flush=False, opts=0):
+    """MgenMsg::ConvertBinaryLog over a binary log image: (text, status, records)."""
+    L = lib()
+    if not getattr(L, "_bl_ready", False):
+        P, u64, i32, u32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_uint32
+        L.or_convert_binary_log.argtypes = [P, u64, i32, i32, u32, P, u64, ctypes.POINTER(i32),
+                                            ctypes.POINTER(u64)]
+        L.or_convert_binary_log.restype = u64
+        L._bl_ready = True
+    f = np.frombuffer(bytes(log) + b"\0" * 8, np.uint8)
+    st, nr = ctypes.c_int(0), ctypes.c_uint64(0)
+    need = L.or_convert_binary_log(_ptr(f), len(log), int(log_rx), int(flush), opts, None, 0,
+                                   ctypes.byref(st), ctypes.byref(nr))
+    out = np.zeros(max(1, need), np.uint8)
+    L.or_convert_binary_log(_ptr(f), len(log), int(log_rx), int(flush), opts, _ptr(out), len(out),
+                            ctypes.byref(st), ctypes.byref(nr))
+    return out[:need].tobytes(), st.value, nr.value

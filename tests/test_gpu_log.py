@@ -164,9 +164,10 @@ def test_binary_log_matches_oracle(torch, eng, gold, oracle, mode):
 
 def test_binary_log_message_bound_and_oob(torch, eng, oracle):
     """Records whose msg_len is exactly header + payload (no checksum, no padding) in 256-B
-    slots with non-zero bytes after them: the 2 bytes the binary RECV record copies past the
-    message read as zero (never the neighbour's bytes); a record outside the slab is logged
-    as RERR with ERROR_LENGTH (3) in both forms, as include/mgenx.hpp maps MGENX_ERROR_OOB."""
+    slots with non-zero bytes after them: each binary RECV record is exactly 4 +
+    eventRecordLength bytes (doc/mgen.xml:4212-4216) and carries hdr + payload_len message
+    bytes, never a neighbour's; a record outside the slab is logged as RERR with ERROR_LENGTH
+    (3) in both forms, as include/mgenx.hpp maps MGENX_ERROR_OOB."""
     from mgen_amd import ERROR_OOB, to_device
     from mgen_amd._abi import DESC_DTYPE
     from mgen_amd.workloads import make_templates
@@ -214,10 +215,13 @@ def test_binary_log_message_bound_and_oob(torch, eng, oracle):
                               rec_len=lens_h[:-1].astype(np.uint32))
     want = oracle.log_recv_binary(f, h, offs_h[:-1], src[:-1], rx_s[:-1], rx_u[:-1], protocol=1)
     assert got[:int(pos[n - 1])] == want
-    # every RECV record ends with the 2 zero bytes past its message
+    # every RECV record is its header + eventRecordLength bytes, ending with the message's
+    # own last byte
     for i in range(n - 1):
         rec = got[int(pos[i]):int(pos[i + 1])]
-        assert rec[0] == 1 and rec[-2:] == b"\0\0", i
+        assert rec[0] == 1 and len(rec) == 4 + int.from_bytes(rec[2:4], "big"), i
+        m = int(mlen[i])
+        assert rec[-1] == h[offs_h[i] + m - 1] and rec[-m + 4:] == h[offs_h[i] + 4:offs_h[i] + m].tobytes(), i
     last = got[int(pos[n - 1]):int(pos[n])]
     assert last[0] == 2 and last[-4:] == (3).to_bytes(4, "big")
     text, _ = eng.log_recv_text(slab, n, cols, to_device(src.view(np.uint8)), to_device(rx_s),
