@@ -256,6 +256,166 @@ class RecvBatch {
   CoreColumns cols_;
 };
 
+// MgenMsg's getters over one decoded 32-B row (mgenx_rec), as MgenMsgView over columns.
+class MgenRecView {
+ public:
+  explicit MgenRecView(const mgenx_rec& r) : r_(r) {}
+  uint16_t GetMsgLen() const { return r_.msg_len; }
+  uint32_t GetFlowId() const { return r_.flow_id; }
+  unsigned int GetSeqNum() const { return r_.seq_num; }
+  struct timeval GetTxTime() const {
+    struct timeval tv;
+    tv.tv_sec = (time_t)r_.tx_sec;
+    tv.tv_usec = (suseconds_t)r_.tx_usec;
+    return tv;
+  }
+  bool FlagIsSet(uint8_t flag) const { return (r_.flags & flag) != 0; }
+  MsgError GetError() const { return r_.err == MGENX_ERROR_OOB ? ERROR_LENGTH : (MsgError)r_.err; }
+  uint16_t GetDstPort() const { return r_.dst_port; }
+  AddressType GetDstAddrType() const { return (AddressType)r_.dst_type; }
+  uint8_t GetDstAddrLen() const { return r_.dst_len; }
+  uint32_t GetDstAddr4() const { return r_.dst_addr4; }
+  uint8_t GetPayloadType() const { return r_.payload_type; }
+  uint16_t GetPayloadLength() const { return r_.payload_len; }
+  uint8_t GetGPSStatus() const { return r_.gps_status; }
+
+ private:
+  const mgenx_rec& r_;
+};
+
+// ---- receive ring: socket batches overlapped with the GPU ------------------------------
+// The reference's receive loop reads, decodes and checks one datagram at a time
+// (MgenUdpTransport::OnEvent, mgenTransport.cpp:938-1000).  RecvRing keeps `depth` stages of
+// pinned recvmmsg slots; while the socket layer fills stage k on the host, stage k-1's
+// datagrams go H2D, through unpack + CRC check, and come back as 32-B rows, each stage on its
+// own HIP stream (copies and kernels of different stages overlap):
+//   Stage& s = ring.Fill();                        // the next free stage (host side)
+//   s.n = sock.Recv(s.slab, ring.Slot(), ring.Batch(), s.len, s.src, s.rx_sec, s.rx_usec);
+//   ring.Submit();                                 // async: H2D, unpack + CRC, rows D2H
+//   while (const RecvRing::Stage* d = ring.Poll()) { ... d->rows[i] ...; ring.Release(); }
+// Fill() needs a free stage: call Wait() / Release() for the oldest one when all are busy.
+class RecvRing {
+ public:
+  struct Stage {
+    uint8_t* slab = nullptr;        // pinned: Batch() slots of Slot() bytes
+    uint32_t* len = nullptr;        // pinned: datagram lengths
+    mgenx_addr* src = nullptr;      // pinned: recvfrom sources
+    uint32_t* rx_sec = nullptr;     // pinned: receive times
+    uint32_t* rx_usec = nullptr;
+    mgenx_rec* rows = nullptr;      // pinned: decoded rows (valid after Poll / Wait)
+    uint32_t n = 0;                 // datagrams in this stage
+    uint64_t seq = 0;               // submission number
+  };
+
+  RecvRing(Context& ctx, uint32_t batch, uint32_t slot = MGENX_MAX_SIZE, uint32_t depth = 3,
+           uint32_t opts = 0)
+      : ctx_(ctx), batch_(batch), slot_(slot), opts_(opts), st_(depth) {
+    if (depth < 2 || batch == 0) throw Error("RecvRing: depth >= 2 and batch > 0");
+    for (Impl& s : st_) {
+      s.h_slab.Resize((size_t)batch * slot);
+      s.h_len.Resize(batch);
+      s.h_src.Resize(batch);
+      s.h_rxs.Resize(batch);
+      s.h_rxu.Resize(batch);
+      s.h_rows.Resize(batch);
+      s.d_slab.Resize((size_t)batch * slot);
+      s.d_len.Resize(batch);
+      s.d_rows.Resize(batch);
+      check_hip(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking), "hipStreamCreate");
+      check_hip(hipEventCreateWithFlags(&s.done, hipEventDisableTiming), "hipEventCreate");
+      s.v.slab = s.h_slab.data(); s.v.len = s.h_len.data(); s.v.src = s.h_src.data();
+      s.v.rx_sec = s.h_rxs.data(); s.v.rx_usec = s.h_rxu.data(); s.v.rows = s.h_rows.data();
+    }
+  }
+  ~RecvRing() {
+    for (Impl& s : st_) {
+      if (s.stream) (void)hipStreamSynchronize(s.stream);
+      if (s.done) (void)hipEventDestroy(s.done);
+      if (s.stream) (void)hipStreamDestroy(s.stream);
+    }
+  }
+  RecvRing(const RecvRing&) = delete;
+  RecvRing& operator=(const RecvRing&) = delete;
+  uint32_t Batch() const { return batch_; }
+  uint32_t Slot() const { return slot_; }
+  uint32_t InFlight() const { return busy_; }
+
+  Stage& Fill() {
+    if (busy_ == st_.size()) throw Error("RecvRing::Fill: every stage is busy (Wait + Release)");
+    Stage& v = st_[head_].v;
+    v.n = 0;
+    return v;
+  }
+  // hand the filled stage to the GPU (asynchronous on that stage's stream)
+  void Submit() {
+    Impl& s = st_[head_];
+    const uint32_t n = s.v.n;
+    if (n > batch_) throw Error("RecvRing::Submit: n > batch");
+    s.v.seq = next_seq_++;
+    if (n) {
+      check_hip(hipMemcpyAsync(s.d_slab.data(), s.h_slab.data(), (size_t)n * slot_,
+                               hipMemcpyHostToDevice, s.stream), "H2D slab");
+      check_hip(hipMemcpyAsync(s.d_len.data(), s.h_len.data(), (size_t)n * 4,
+                               hipMemcpyHostToDevice, s.stream), "H2D lengths");
+      mgenx_cols c;
+      memset(&c, 0, sizeof(c));
+      c.rows = s.d_rows.data();
+      ctx_.Check(mgenx_unpack_batch(ctx_.get(), s.d_slab.data(), (uint64_t)n * slot_, nullptr,
+                                    slot_, s.d_len.data(), 0, n, &c, opts_, s.stream),
+                 "mgenx_unpack_batch");
+      check_hip(hipMemcpyAsync(s.h_rows.data(), s.d_rows.data(), (size_t)n * sizeof(mgenx_rec),
+                               hipMemcpyDeviceToHost, s.stream), "D2H rows");
+    }
+    check_hip(hipEventRecord(s.done, s.stream), "hipEventRecord");
+    head_ = (head_ + 1) % st_.size();
+    busy_++;
+  }
+  // the oldest submitted stage once its rows are back (nullptr: none, or not yet done)
+  const Stage* Poll() {
+    if (!busy_ || tail_taken_) return nullptr;
+    const hipError_t e = hipEventQuery(st_[tail_].done);
+    if (e == hipErrorNotReady) return nullptr;
+    check_hip(e, "hipEventQuery");
+    tail_taken_ = true;
+    return &st_[tail_].v;
+  }
+  // the oldest submitted stage, waiting for it (nullptr: nothing in flight)
+  const Stage* Wait() {
+    if (!busy_) return nullptr;
+    if (!tail_taken_) check_hip(hipEventSynchronize(st_[tail_].done), "hipEventSynchronize");
+    tail_taken_ = true;
+    return &st_[tail_].v;
+  }
+  // done with the stage Poll / Wait returned: it becomes free for Fill
+  void Release() {
+    if (!tail_taken_) throw Error("RecvRing::Release without Poll / Wait");
+    tail_taken_ = false;
+    tail_ = (tail_ + 1) % st_.size();
+    busy_--;
+  }
+
+ private:
+  struct Impl {
+    PinnedArray<uint8_t> h_slab;
+    PinnedArray<uint32_t> h_len, h_rxs, h_rxu;
+    PinnedArray<mgenx_addr> h_src;
+    PinnedArray<mgenx_rec> h_rows;
+    DeviceArray<uint8_t> d_slab;
+    DeviceArray<uint32_t> d_len;
+    DeviceArray<mgenx_rec> d_rows;
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    Stage v;
+  };
+  Context& ctx_;
+  uint32_t batch_, slot_, opts_;
+  std::vector<Impl> st_;
+  size_t head_ = 0, tail_ = 0;
+  uint32_t busy_ = 0;
+  bool tail_taken_ = false;
+  uint64_t next_seq_ = 0;
+};
+
 // ---- send: flows + per-message descriptors -> packed datagrams --------------------------
 class SendBatch {
  public:

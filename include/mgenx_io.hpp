@@ -16,6 +16,7 @@
 #include <arpa/inet.h>
 #include <errno.h>
 #include <netinet/in.h>
+#include <sys/types.h>
 #include <poll.h>
 #include <sys/socket.h>
 #include <sys/time.h>
@@ -34,17 +35,32 @@ namespace mgenx {
 
 class UdpTransport {
  public:
-  // bind to addr:port (port 0 = ephemeral); non-blocking
+  // bind to addr:port (port 0 = ephemeral); non-blocking.  addr is IPv4 ("127.0.0.1") or
+  // IPv6 ("::1"): the socket family follows it, as ProtoSocket's does for its address.
   explicit UdpTransport(const char* addr = "127.0.0.1", uint16_t port = 0, int rcvbuf = 4 << 20) {
-    fd_ = ::socket(AF_INET, SOCK_DGRAM | SOCK_NONBLOCK, 0);
+    memset(&local_, 0, sizeof(local_));
+    sockaddr_in a4;
+    sockaddr_in6 a6;
+    memset(&a4, 0, sizeof(a4));
+    memset(&a6, 0, sizeof(a6));
+    socklen_t alen;
+    if (inet_pton(AF_INET, addr, &a4.sin_addr) == 1) {
+      a4.sin_family = AF_INET;
+      a4.sin_port = htons(port);
+      memcpy(&local_, &a4, sizeof(a4));
+      alen = sizeof(a4);
+    } else if (inet_pton(AF_INET6, addr, &a6.sin6_addr) == 1) {
+      a6.sin6_family = AF_INET6;
+      a6.sin6_port = htons(port);
+      memcpy(&local_, &a6, sizeof(a6));
+      alen = sizeof(a6);
+    } else {
+      throw std::runtime_error("bad address");
+    }
+    fd_ = ::socket(local_.ss_family, SOCK_DGRAM | SOCK_NONBLOCK, 0);
     if (fd_ < 0) throw std::runtime_error(std::string("socket: ") + strerror(errno));
     (void)::setsockopt(fd_, SOL_SOCKET, SO_RCVBUF, &rcvbuf, sizeof(rcvbuf));
-    sockaddr_in a;
-    memset(&a, 0, sizeof(a));
-    a.sin_family = AF_INET;
-    a.sin_port = htons(port);
-    if (inet_pton(AF_INET, addr, &a.sin_addr) != 1) throw std::runtime_error("bad address");
-    if (::bind(fd_, (sockaddr*)&a, sizeof(a)) != 0)
+    if (::bind(fd_, (sockaddr*)&local_, alen) != 0)
       throw std::runtime_error(std::string("bind: ") + strerror(errno));
     socklen_t l = sizeof(local_);
     ::getsockname(fd_, (sockaddr*)&local_, &l);
@@ -54,15 +70,20 @@ class UdpTransport {
   }
   UdpTransport(const UdpTransport&) = delete;
   UdpTransport& operator=(const UdpTransport&) = delete;
-  uint16_t Port() const { return ntohs(local_.sin_port); }
-  const sockaddr_in& Local() const { return local_; }
+  uint16_t Port() const {
+    return local_.ss_family == AF_INET6 ? ntohs(((const sockaddr_in6&)local_).sin6_port)
+                                        : ntohs(((const sockaddr_in&)local_).sin_port);
+  }
+  const sockaddr_storage& Local() const { return local_; }
+  int Family() const { return local_.ss_family; }
   int fd() const { return fd_; }
 
   // sendmmsg datagram i = base[i * slot .. + lens[i]) to dst; zero-length entries (Pack
   // returned 0: MSG_SEND_FAILED) are skipped, as the reference does not send them.
   // Returns the number of datagrams the kernel accepted.
-  uint32_t Send(const sockaddr_in& dst, const uint8_t* base, uint32_t slot, const uint32_t* lens,
-                uint32_t n) {
+  uint32_t Send(const sockaddr_storage& dst, const uint8_t* base, uint32_t slot,
+                const uint32_t* lens, uint32_t n) {
+    const socklen_t dlen = dst.ss_family == AF_INET6 ? sizeof(sockaddr_in6) : sizeof(sockaddr_in);
     std::vector<mmsghdr> m;
     std::vector<iovec> iov;
     m.reserve(n);
@@ -75,7 +96,7 @@ class UdpTransport {
       mmsghdr h;
       memset(&h, 0, sizeof(h));
       h.msg_hdr.msg_name = (void*)&dst;
-      h.msg_hdr.msg_namelen = sizeof(dst);
+      h.msg_hdr.msg_namelen = dlen;
       h.msg_hdr.msg_iov = &iov[i];
       h.msg_hdr.msg_iovlen = 1;
       m.push_back(h);
@@ -107,7 +128,7 @@ class UdpTransport {
     if (cap == 0) return 0;
     std::vector<mmsghdr> m(cap);
     std::vector<iovec> iov(cap);
-    std::vector<sockaddr_in> from(cap);
+    std::vector<sockaddr_storage> from(cap);
     for (uint32_t i = 0; i < cap; i++) {
       iov[i] = {base + (size_t)i * slot, slot};
       memset(&m[i], 0, sizeof(m[i]));
@@ -122,12 +143,21 @@ class UdpTransport {
     gettimeofday(&now, nullptr);  // ProtoSystemTime after the receive
     for (int i = 0; i < r; i++) {
       lens[i] = m[i].msg_len;
-      if (src) {
+      if (src) {  // recvfrom's source as a ProtoAddress (IPv4 or IPv6)
         memset(&src[i], 0, sizeof(src[i]));
-        src[i].type = 1;
-        src[i].len = 4;
-        src[i].port = ntohs(from[i].sin_port);
-        memcpy(src[i].addr, &from[i].sin_addr, 4);
+        if (from[i].ss_family == AF_INET6) {
+          const sockaddr_in6& f6 = (const sockaddr_in6&)from[i];
+          src[i].type = 2;
+          src[i].len = 16;
+          src[i].port = ntohs(f6.sin6_port);
+          memcpy(src[i].addr, &f6.sin6_addr, 16);
+        } else {
+          const sockaddr_in& f4 = (const sockaddr_in&)from[i];
+          src[i].type = 1;
+          src[i].len = 4;
+          src[i].port = ntohs(f4.sin_port);
+          memcpy(src[i].addr, &f4.sin_addr, 4);
+        }
       }
       if (rx_sec) rx_sec[i] = (uint32_t)now.tv_sec;
       if (rx_usec) rx_usec[i] = (uint32_t)now.tv_usec;
@@ -137,7 +167,7 @@ class UdpTransport {
 
  private:
   int fd_ = -1;
-  sockaddr_in local_{};
+  sockaddr_storage local_{};
 };
 
 }  // namespace mgenx

@@ -11,6 +11,10 @@
 //                                        and unpacks (test infrastructure; no GPU touched)
 //   loopback gpu <count> <rate> <size>   the product path: mgenx SendBatch (GPU pack) and
 //                                        RecvBatch (GPU unpack + CRC) around the same sockets
+//   loopback ring <count> <rate> <size>  GPU pack, and RecvRing: received batches decoded on
+//                                        the GPU while the run goes on (pinned stages, one
+//                                        stream each, H2D / unpack / D2H overlapped)
+//   ... [v6]                             the same over IPv6 loopback (::1)
 // Prints one summary line; exit 0 iff every message arrived once, in order, intact.
 #include <sys/time.h>
 #include <time.h>
@@ -44,19 +48,26 @@ struct Check {
 
 int main(int argc, char** argv) {
   if (argc < 5) {
-    fprintf(stderr, "usage: %s cpu|gpu count rate size\n", argv[0]);
+    fprintf(stderr, "usage: %s cpu|gpu|ring count rate size [v6]\n", argv[0]);
     return 2;
   }
-  const bool gpu = std::string(argv[1]) == "gpu";
+  const bool ring = std::string(argv[1]) == "ring";
+  const bool gpu = ring || std::string(argv[1]) == "gpu";
+  const bool v6 = argc > 5 && std::string(argv[5]) == "v6";
   const uint32_t count = (uint32_t)atoi(argv[2]);
   const double rate = atof(argv[3]);
   const uint32_t size = (uint32_t)atoi(argv[4]);
   const uint32_t slot = MGENX_MAX_SIZE;  // the reference's receive buffer (MAX_SIZE)
 
-  mgenx::UdpTransport listener("127.0.0.1", 0);
-  mgenx::UdpTransport sender("127.0.0.1", 0);
+  mgenx::UdpTransport listener(v6 ? "::1" : "127.0.0.1", 0);
+  mgenx::UdpTransport sender(v6 ? "::1" : "127.0.0.1", 0);
   const uint16_t dport = listener.Port();
-  const uint8_t dst_ip[4] = {127, 0, 0, 1};
+  uint8_t dst_ip[16] = {127, 0, 0, 1};
+  if (v6) {
+    memset(dst_ip, 0, 16);
+    dst_ip[15] = 1;
+  }
+  const uint8_t dst_len = v6 ? 16 : 4;
 
   // receive side: fixed slots (recvmmsg layout) + per-datagram length / source / rx time
   std::vector<uint8_t> cpu_slab(gpu ? 0 : (size_t)(count + 64) * slot);
@@ -65,14 +76,42 @@ int main(int argc, char** argv) {
   std::vector<uint32_t> txs(count), txu(count);
   mgenx::Context* ctx = nullptr;
   mgenx::RecvBatch* rb = nullptr;
+  mgenx::RecvRing* rr = nullptr;
+  uint32_t ring_n = 0, ring_stages = 0, ring_overlap = 0;  // rows checked, stages, stages
+                                                           // done while others were in flight
   mgenx::SendBatch* sb = nullptr;
   uint32_t flow = 0;
   if (gpu) {
     ctx = new mgenx::Context(0);
-    rb = new mgenx::RecvBatch(*ctx, count + 64, slot);
+    if (ring) rr = new mgenx::RecvRing(*ctx, 256, slot, 3);
+    else rb = new mgenx::RecvBatch(*ctx, count + 64, slot);
     sb = new mgenx::SendBatch(*ctx);
-    flow = sb->AddFlow(1, mgenx::IPv4, dst_ip, dport);  // flow 1, GPS 999/999/-999 INVALID
+    flow = sb->AddFlow(1, v6 ? mgenx::IPv6 : mgenx::IPv4, dst_ip, dport);  // flow 1, GPS INVALID
   }
+  Check c;
+  auto time_ok = [&](uint32_t i, uint32_t s, uint32_t u, uint32_t rs, uint32_t ru) {
+    const uint64_t tx = (uint64_t)txs[i] * 1000000u + txu[i];
+    const uint64_t rx = (uint64_t)rs * 1000000u + ru;
+    return s == txs[i] && u == txu[i] && rx >= tx;
+  };
+  auto fields_ok = [&](uint32_t flow_id, uint32_t msg_len, uint32_t port, const void* d4,
+                       uint32_t gps, bool cks, bool last, uint32_t len, uint32_t sport) {
+    return flow_id == 1 && msg_len == size && port == dport && memcmp(d4, dst_ip, 4) == 0 &&
+           gps == 0 && cks && last && len == size && sport == sender.Port();
+  };
+  // RecvRing rows, checked in arrival order as the stages complete
+  auto check_row = [&](const mgenx::RecvRing::Stage* d, uint32_t i) {
+    const mgenx::MgenRecView v(d->rows[i]);
+    const uint32_t d4 = v.GetDstAddr4();
+    const uint32_t sq = v.GetSeqNum();
+    const struct timeval tx = v.GetTxTime();
+    c.Add(ring_n++, sq, v.GetError(),
+          fields_ok(v.GetFlowId(), v.GetMsgLen(), v.GetDstPort(), &d4, v.GetGPSStatus(),
+                    v.FlagIsSet(mgenx::CHECKSUM), v.FlagIsSet(mgenx::LAST_BUFFER), d->len[i],
+                    d->src[i].port) && d->src[i].type == (v6 ? 2 : 1),
+          sq < count && time_ok(sq, (uint32_t)tx.tv_sec, (uint32_t)tx.tv_usec, d->rx_sec[i],
+                                d->rx_usec[i]));
+  };
   std::vector<uint8_t> txbuf((size_t)64 * size);
   uint32_t sent = 0, got = 0, accepted = 0;  // accepted: datagrams the socket took
   const double t0 = now_s();
@@ -103,8 +142,8 @@ int main(int argc, char** argv) {
           m.seq_num = sent + j;
           m.tx_sec = (uint32_t)tv.tv_sec;
           m.tx_usec = (uint32_t)tv.tv_usec;
-          m.dst.type = 1; m.dst.len = 4; m.dst.port = dport;
-          memcpy(m.dst.addr, dst_ip, 4);
+          m.dst.type = v6 ? 2 : 1; m.dst.len = dst_len; m.dst.port = dport;
+          memcpy(m.dst.addr, dst_ip, dst_len);
           m.latitude = m.longitude = 999.0;
           m.altitude = -999;
           plen[j] = or_udp_pack(&m, txbuf.data() + (size_t)j * size, 1, 0, 0);
@@ -115,7 +154,23 @@ int main(int argc, char** argv) {
       sent += k;
     }
     // drain the listener (MgenUdpTransport::OnEvent's while (RecvFrom) loop, batched)
-    for (;;) {
+    if (ring) {
+      for (;;) {
+        if (rr->InFlight() == 3) break;  // every stage busy: decode first
+        mgenx::RecvRing::Stage& st = rr->Fill();
+        st.n = listener.Recv(st.slab, slot, rr->Batch(), st.len, st.src, st.rx_sec, st.rx_usec);
+        if (!st.n) break;
+        got += st.n;
+        rr->Submit();
+      }
+      while (const mgenx::RecvRing::Stage* d = rr->Poll()) {
+        ring_stages++;
+        if (rr->InFlight() > 1) ring_overlap++;
+        for (uint32_t i = 0; i < d->n; i++) check_row(d, i);
+        rr->Release();
+      }
+    }
+    for (; !ring;) {
       const uint32_t room = count + 64 - got;
       uint8_t* base = gpu ? rb->Slot(got) : cpu_slab.data() + (size_t)got * slot;
       const uint32_t r = listener.Recv(base, slot, room < 64 ? room : 64, &lens[got], &src[got],
@@ -138,48 +193,52 @@ int main(int argc, char** argv) {
   const double elapsed = now_s() - t0;
 
   // decode and check: seq 0..count-1 once each, in order; no error; fields as sent
-  Check c;
   const uint32_t n = got < count ? got : count;
-  auto time_ok = [&](uint32_t i, uint32_t s, uint32_t u) {
-    const uint64_t tx = (uint64_t)txs[i] * 1000000u + txu[i];
-    const uint64_t rx = (uint64_t)rxs[i] * 1000000u + rxu[i];
-    return s == txs[i] && u == txu[i] && rx >= tx;
-  };
-  if (gpu) {
+  if (ring) {
+    while (const mgenx::RecvRing::Stage* d = rr->Wait()) {
+      ring_stages++;
+      for (uint32_t i = 0; i < d->n; i++) check_row(d, i);
+      rr->Release();
+    }
+  } else if (gpu) {
     for (uint32_t i = 0; i < got; i++) rb->SetLength(i, lens[i]);
     rb->Unpack(got);
     for (uint32_t i = 0; i < n; i++) {
       const mgenx::MgenMsgView v = (*rb)[i];
       const uint32_t d4 = v.GetDstAddr4();
-      const bool fields = v.GetFlowId() == 1 && v.GetMsgLen() == size && v.GetDstPort() == dport &&
-                          memcmp(&d4, dst_ip, 4) == 0 && v.GetGPSStatus() == 0 &&
-                          v.FlagIsSet(mgenx::CHECKSUM) && v.FlagIsSet(mgenx::LAST_BUFFER) &&
-                          lens[i] == size && src[i].port == sender.Port();
+      const bool fields = fields_ok(v.GetFlowId(), v.GetMsgLen(), v.GetDstPort(), &d4,
+                                    v.GetGPSStatus(), v.FlagIsSet(mgenx::CHECKSUM),
+                                    v.FlagIsSet(mgenx::LAST_BUFFER), lens[i], src[i].port) &&
+                          src[i].type == (v6 ? 2 : 1);
       const struct timeval tx = v.GetTxTime();
       c.Add(i, v.GetSeqNum(), v.GetError(), fields,
             time_ok(v.GetSeqNum() < count ? v.GetSeqNum() : 0, (uint32_t)tx.tv_sec,
-                    (uint32_t)tx.tv_usec));
+                    (uint32_t)tx.tv_usec, rxs[i], rxu[i]));
     }
   } else {
     for (uint32_t i = 0; i < n; i++) {
       or_fields f;
       or_udp_recv(cpu_slab.data() + (size_t)i * slot, lens[i], 0, &f);
-      const bool fields = f.flow_id == 1 && f.msg_len == size && f.dst_port == dport &&
-                          memcmp(f.dst_addr, dst_ip, 4) == 0 && f.gps_status == 0 &&
-                          (f.flags & OR_FLAG_CHECKSUM) && (f.flags & OR_FLAG_LAST_BUFFER) &&
-                          lens[i] == size && src[i].port == sender.Port();
+      const bool fields = fields_ok(f.flow_id, f.msg_len, f.dst_port, f.dst_addr, f.gps_status,
+                                    (f.flags & OR_FLAG_CHECKSUM) != 0,
+                                    (f.flags & OR_FLAG_LAST_BUFFER) != 0, lens[i],
+                                    src[i].port) &&
+                          f.dst_len == dst_len && src[i].type == (v6 ? 2 : 1);
       c.Add(i, f.seq_num, f.err, fields,
-            time_ok(f.seq_num < count ? f.seq_num : 0, f.tx_sec, f.tx_usec));
+            time_ok(f.seq_num < count ? f.seq_num : 0, f.tx_sec, f.tx_usec, rxs[i], rxu[i]));
     }
   }
-  const bool ok = sent == count && accepted == count && got == count && c.bad_seq == 0 && c.bad_err == 0 &&
-                  c.bad_field == 0 && c.bad_time == 0;
+  const bool ok = sent == count && accepted == count && got == count && c.n == count &&
+                  c.bad_seq == 0 && c.bad_err == 0 && c.bad_field == 0 && c.bad_time == 0;
   printf("{\"mode\": \"%s\", \"sent\": %u, \"send_failed\": %d, \"received\": %u, \"lost\": %d, \"out_of_order\": %u, "
          "\"errors\": %u, \"bad_fields\": %u, \"bad_times\": %u, \"elapsed_s\": %.3f, "
-         "\"rate\": %.1f, \"size\": %u, \"ok\": %s}\n",
-         gpu ? "gpu" : "cpu", sent, (int)sent - (int)accepted, got, (int)accepted - (int)got,
+         "\"rate\": %.1f, \"size\": %u, \"v6\": %s, \"ring_stages\": %u, "
+         "\"ring_overlapped\": %u, \"ok\": %s}\n",
+         ring ? "ring" : gpu ? "gpu" : "cpu", sent, (int)sent - (int)accepted, got, (int)accepted - (int)got,
          c.bad_seq, c.bad_err,
-         c.bad_field, c.bad_time, elapsed, rate, size, ok ? "true" : "false");
+         c.bad_field, c.bad_time, elapsed, rate, size, v6 ? "true" : "false", ring_stages,
+         ring_overlap, ok ? "true" : "false");
+  delete rr;
   delete sb;
   delete rb;
   delete ctx;
