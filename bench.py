@@ -306,6 +306,73 @@ def extra_log(torch, eng, dev, slab):
             "note": "two passes (length, write) + scan; includes one D2H read of the total"}
 
 
+def extra_pcap(torch, eng, dev):
+    """pcap2mgen (pcap2mgen.cpp:252-482, analytics on) over a device-resident capture of
+    1,048,576 packets (Ethernet / IPv4 / UDP, 262-B checksummed MGEN messages, 1024 flows,
+    1 us apart): frame parse, Unpack, FindFlow + Update, the analytic REPORT lines, the RECV
+    lines, received REPORT items, per-packet interleave.  Host round trips between stages
+    (flow count, text sizes) included; the capture file's H2D is not."""
+    from mgen_amd.pcap import Pcap2Mgen
+    from mgen_amd.workloads import pcap_capture
+    n = N_REC
+    buf, pkt_off, rec_bytes = pcap_capture(eng, n)
+    p = Pcap2Mgen(eng, analytics=True, window=0.25)
+    text, _ = p.run_device(buf, pkt_off, n, 1, 0)
+    torch.cuda.synchronize()
+    body = text.cpu().numpy().tobytes()
+    assert body.count(b" RECV ") == n, body[:300]
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        p.run_device(buf, pkt_off, n, 1, 0)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / reps * 1e3
+    return {"packets": n, "capture_bytes": buf.numel(), "log_bytes": len(body),
+            "report_lines": body.count(b" REPORT "), "ms": round(ms, 3),
+            "mpkt_per_s": round(n / ms / 1e3, 1),
+            "capture_gbps": round(buf.numel() / ms / 1e6, 1),
+            "note": "device-resident capture; whole pipeline incl. its host size round trips"}
+
+
+def extra_convert(torch, eng, dev, slab):
+    """ConvertBinaryLog (mgenMsg.cpp:1417-1900) of the binary RECV log of the config-2 batch
+    (1,048,576 records written on the GPU by mgenx_log_recv_binary): host record walk
+    (mgenx_binlog_index) and the device conversion timed separately."""
+    import mgen_amd
+    from mgen_amd._abi import COLS_EXT
+    full = eng.alloc_cols(N_REC, ext=True)
+    cols = {name: full[name] for name, _, _ in COLS_EXT}
+    cols["rows"] = eng.alloc_rows(N_REC)
+    eng.unpack(slab, N_REC, stride=REC, fixed_len=REC, cols=cols)
+    src = torch.zeros(N_REC, 20, dtype=torch.uint8, device=dev)
+    src[:, 0], src[:, 1], src[:, 2], src[:, 3] = 1, 4, 0x89, 0xE7
+    src[:, 4], src[:, 7] = 127, 1
+    rx_s = torch.full((N_REC,), 1_700_000_001, dtype=torch.int32, device=dev)
+    rx_u = torch.arange(N_REC, dtype=torch.int32, device=dev) % 1_000_000
+    binrec, _ = eng.log_recv_binary(slab, N_REC, cols, src, rx_s, rx_u, stride=REC)
+    hdr = b"mgen version=5.1.1 type=binary_log\n\0"
+    log = torch.cat([torch.tensor(list(hdr), dtype=torch.uint8, device=dev), binrec])
+    host = log.cpu().numpy()
+    t0 = time.perf_counter()
+    offs, info = mgen_amd.binlog_index(host)
+    idx_ms = (time.perf_counter() - t0) * 1e3
+    assert info.status == 0 and info.n_records == N_REC
+    ro = torch.from_numpy(offs.view(np.int64).copy()).to(dev)
+    text, _ = eng.convert_binary_log(log, ro, N_REC)
+    cap = text.numel()
+    reps = 3
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        eng.convert_binary_log(log, ro, N_REC, cap=cap)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / reps * 1e3
+    return {"records": N_REC, "binary_bytes": log.numel(), "text_bytes": cap,
+            "ms": round(ms, 3), "mrec_per_s": round(N_REC / ms / 1e3, 1),
+            "host_index_ms": round(idx_ms, 3),
+            "note": "device conversion incl. its host size round trips; host index separate"}
+
+
 def extra_pcie(torch, eng, dev, slab):
     """Config 2 from pinned host memory: 8 chunks of 128 MiB, two streams (copy of chunk
     k+1 overlaps the unpack of chunk k), core columns copied back.  Wall-clock GB/s of
@@ -478,6 +545,8 @@ def main():
             guard("config3_mixed_pack_unpack", lambda: extra_config3(torch, eng, dev))
             guard("pcie_inclusive_config2", lambda: extra_pcie(torch, eng, dev, slab))
             guard("recv_log_text", lambda: extra_log(torch, eng, dev, slab))
+            guard("pcap2mgen_1M_packets", lambda: extra_pcap(torch, eng, dev))
+            guard("convert_binary_log_1M", lambda: extra_convert(torch, eng, dev, slab))
 
     traffic_b, traffic_src = load_traffic()
     ms_per_step = elapsed / args.steps * 1e3

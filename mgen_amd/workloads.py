@@ -114,3 +114,58 @@ def poisson_flows(n, n_flows=1024, seed=SEED, loss=0.01, dup=0.001, reorder=8,
         "rx_sec": (rx_i // 10**6).astype(np.uint32), "rx_usec": (rx_i % 10**6).astype(np.uint32),
         "msg_len": np.full(idx.size, msg_len, np.uint16),
     }
+
+
+def pcap_capture(eng, n: int, msg_len: int = 262, n_flows: int = 1024, gap_us: int = 1):
+    """A pcap capture image built on the device (Ethernet / IPv4 / UDP around GPU-packed
+    checksummed MGEN messages): flow f = i mod n_flows from 10.0.f>>8.f&255 port 30000 + f,
+    packet i captured at T0 + i * gap_us, tx 300 us earlier.  Returns (file uint8 tensor,
+    record-header offsets int64 tensor, record bytes)."""
+    import torch
+    from . import PACK_CHECKSUM, to_device
+    dev = f"cuda:{eng.device}"
+    tmpl, pool, d = udp_fixed(n, msg_len, n_flows)
+    t_us = np.arange(n, dtype=np.uint64) * gap_us
+    d["tx_sec"] = (T0 + (t_us + 10**6 - 300) // 10**6 - 1).astype(np.uint32)
+    d["tx_usec"] = ((t_us + 10**6 - 300) % 10**6).astype(np.uint32)
+    d["flags"] = 0
+    dt, dp = to_device(tmpl, eng.device), to_device(pool, eng.device)
+    crc = torch.empty(n_flows, dtype=torch.int32, device=dev)
+    eng.pack_prepare(dt, n_flows, dp, crc)
+    slab = torch.empty(n * msg_len, dtype=torch.uint8, device=dev)
+    eng.pack(dt, crc, to_device(d, eng.device), n, dp, slab, stride=msg_len, opts=PACK_CHECKSUM)
+    R = 16 + 14 + 20 + 8 + msg_len
+    assert R % 4 == 0
+    h = bytearray(58)
+    h[8:12] = (R - 16).to_bytes(4, "little")
+    h[12:16] = (R - 16).to_bytes(4, "little")
+    h[16:22] = bytes([2, 0, 0, 0, 0, 2])
+    h[22:28] = bytes([2, 0, 0, 0, 0, 1])
+    h[28:30] = b"\x08\x00"
+    ip = 16 + 14
+    h[ip:ip + 12] = bytes([0x45, 0, (20 + 8 + msg_len) >> 8, (20 + 8 + msg_len) & 255, 0, 0, 0x40,
+                           0, 64, 17, 0, 0])
+    h[ip + 12:ip + 16] = bytes([10, 0, 0, 0])
+    h[ip + 16:ip + 20] = bytes([127, 0, 0, 1])
+    u = ip + 20
+    h[u + 2:u + 4] = (5000).to_bytes(2, "big")
+    h[u + 4:u + 6] = (8 + msg_len).to_bytes(2, "big")
+    cap = torch.empty(n, R, dtype=torch.uint8, device=dev)
+    cap[:, :58] = torch.tensor(list(h), dtype=torch.uint8, device=dev)
+    cap[:, 58:] = slab.view(n, msg_len)
+    i = torch.arange(n, dtype=torch.int64, device=dev)
+    f = i % n_flows
+    t = T0 * 10**6 + i * gap_us
+    w = cap.view(torch.int32)
+    w[:, 0] = (t // 10**6).to(torch.int32)
+    w[:, 1] = (t % 10**6).to(torch.int32)
+    cap[:, ip + 14] = (f >> 8).to(torch.uint8)
+    cap[:, ip + 15] = (f & 255).to(torch.uint8)
+    sp = 30000 + f
+    cap[:, u] = (sp >> 8).to(torch.uint8)
+    cap[:, u + 1] = (sp & 255).to(torch.uint8)
+    gh = torch.tensor(list((0xA1B2C3D4).to_bytes(4, "little") + (2).to_bytes(2, "little") +
+                           (4).to_bytes(2, "little") + bytes(8) + (65535).to_bytes(4, "little") +
+                           (1).to_bytes(4, "little")), dtype=torch.uint8, device=dev)
+    file = torch.cat([gh, cap.view(-1)])
+    return file, 24 + i * R, R
