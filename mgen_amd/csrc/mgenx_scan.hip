@@ -24,6 +24,8 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
+
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -105,7 +107,7 @@ __device__ __forceinline__ uint32_t wave_excl(uint32_t c, uint32_t& wtot) {
 template <bool kRedo>
 __global__ void __launch_bounds__(kScanThreads)
 scan_detect_kernel(const uint8_t* __restrict__ s, uint64_t nbytes, ScanMode m,
-                   uint16_t* __restrict__ slots, uint64_t* __restrict__ counts,
+                   uint32_t* __restrict__ slots, uint64_t* __restrict__ counts,
                    const uint64_t* __restrict__ base, uint64_t* __restrict__ cand) {
   constexpr uint32_t kW = kScanThreads / 64;
   if (kRedo && !(counts[blockIdx.x] >> 32)) return;
@@ -166,7 +168,7 @@ scan_detect_kernel(const uint8_t* __restrict__ s, uint64_t nbytes, ScanMode m,
     for (uint32_t k = 0; k < kW; k++) total += wsum[st][k];
   const bool ovf = !kRedo && total > kScanSlots;
   if (!ovf && total) {
-    uint16_t* out = slots + (size_t)blockIdx.x * kScanSlots;
+    uint32_t* out = slots + (size_t)blockIdx.x * kScanSlots;
     uint64_t* outc = kRedo ? cand + (uint32_t)base[blockIdx.x] : nullptr;
     uint32_t run = 0;
 #pragma unroll
@@ -184,8 +186,15 @@ scan_detect_kernel(const uint8_t* __restrict__ s, uint64_t nbytes, ScanMode m,
           const int i = __ffs(h) - 1;
           h &= h - 1;
           const uint32_t off = 16u * (st * kScanThreads + t) + (uint32_t)i;
-          if (kRedo) outc[pos++] = block0 + off;
-          else out[pos++] = (uint16_t)off;
+          if (kRedo) {
+            outc[pos++] = block0 + off;
+          } else {
+            // the slot keeps the candidate's length field too, so the link step reads no
+            // stream bytes: re-read here, where the block's bytes were just loaded (keeping
+            // the 16 loaded rows live until this loop instead costs 32 VGPRs and occupancy)
+            const uint32_t L = be16_at(s, block0 + off);
+            out[pos++] = off | (L << 16);
+          }
         }
       }
       run += stot;
@@ -203,24 +212,37 @@ scan_detect_kernel(const uint8_t* __restrict__ s, uint64_t nbytes, ScanMode m,
 // cand, written by the second detect pass.  up0 = successor (self for a terminal),
 // dist0 = 1 if linked.
 __global__ void __launch_bounds__(256)
-scan_link_kernel(const uint8_t* __restrict__ s, uint64_t nbytes, const uint16_t* __restrict__ slots,
+scan_link_kernel(const uint8_t* __restrict__ s, uint64_t nbytes, const uint32_t* __restrict__ slots,
                  const uint64_t* __restrict__ counts, const uint64_t* __restrict__ base,
                  uint32_t n_blocks, uint64_t* __restrict__ cand, uint32_t* __restrict__ up,
-                 uint32_t* __restrict__ dist) {
+                 uint32_t* __restrict__ dist, uint64_t spec_cap) {
   const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= n_blocks) return;
+  // speculative build (tables sized before the candidate total was known): nothing when the
+  // total exceeds them; an overflowing block (its candidates need the second detect pass)
+  // gets terminal entries -- the host sees either case and rebuilds exactly
+  if (spec_cap && base[n_blocks] > spec_cap) return;
   const uint64_t cw = counts[b];
   const uint32_t c = (uint32_t)cw;
   const uint32_t o = (uint32_t)base[b];
+  if (spec_cap && (cw >> 32)) {
+    for (uint32_t k = threadIdx.x & 63u; k < c; k += 64) {
+      up[o + k] = o + k;
+      dist[o + k] = 0u;
+    }
+    return;
+  }
   for (uint32_t k = threadIdx.x & 63u; k < c; k += 64) {
-    uint64_t p;
+    uint64_t p, nx;
     if (cw >> 32) {
       p = cand[o + k];
+      nx = p + be16_at(s, p);
     } else {
-      p = (uint64_t)b * kScanBlockBytes + slots[(size_t)b * kScanSlots + k];
+      const uint32_t sl = slots[(size_t)b * kScanSlots + k];  // offset | length << 16
+      p = (uint64_t)b * kScanBlockBytes + (sl & 0xFFFFu);
+      nx = p + (sl >> 16);
       cand[o + k] = p;
     }
-    const uint64_t nx = p + be16_at(s, p);
     uint32_t tgt = kNone;
     if (nx + 2 <= nbytes) {
       const uint64_t bl = nx / kScanBlockBytes;
@@ -235,13 +257,22 @@ scan_link_kernel(const uint8_t* __restrict__ s, uint64_t nbytes, const uint16_t*
           }
           if (lo < cb && cand[ob + lo] == nx) tgt = ob + lo;
         } else {
-          const uint16_t* ts = slots + (size_t)bl * kScanSlots;
+          const uint32_t* ts = slots + (size_t)bl * kScanSlots;
           const uint32_t key = (uint32_t)(nx % kScanBlockBytes);
-          while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (ts[mid] < key) lo = mid + 1; else hi = mid;
+          if (cb <= 8) {  // the usual handful: all loads side by side, one compare each
+            uint32_t w[8];
+#pragma unroll
+            for (uint32_t j = 0; j < 8; j++) w[j] = j < cb ? ts[j] : 0xFFFFFFFFu;
+#pragma unroll
+            for (uint32_t j = 0; j < 8; j++)
+              if (tgt == kNone && (w[j] & 0xFFFFu) == key && j < cb) tgt = ob + j;
+          } else {
+            while (lo < hi) {
+              const uint32_t mid = (lo + hi) >> 1;
+              if ((ts[mid] & 0xFFFFu) < key) lo = mid + 1; else hi = mid;
+            }
+            if (lo < cb && (ts[lo] & 0xFFFFu) == key) tgt = ob + lo;
           }
-          if (lo < cb && ts[lo] == key) tgt = ob + lo;
         }
       }
     }
@@ -328,43 +359,69 @@ __device__ uint32_t find_cand(const uint64_t* cand, uint32_t n, uint64_t p) {
 }
 
 // 3. one lifting level (base 4): up_k = up_{k-1}^4, dist_k = the 4 partial distances
-// (a terminal points at itself with distance 0, so both saturate there)
+// (a terminal points at itself with distance 0, so both saturate there).  The 2- and 3-jump
+// tables of level k-1 (up2 / up3, d2 / d3) fall out of the same gathers: with them a walk
+// takes one jump per level (enumeration, chain_descend) instead of up to three.
 __global__ void __launch_bounds__(256)
 scan_lift_kernel(const uint32_t* __restrict__ up0, const uint32_t* __restrict__ d0,
-                 uint32_t* __restrict__ up1, uint32_t* __restrict__ d1, uint32_t n) {
+                 uint32_t* __restrict__ up1, uint32_t* __restrict__ d1,
+                 uint32_t* __restrict__ up2, uint32_t* __restrict__ up3,
+                 uint32_t* __restrict__ d2, uint32_t* __restrict__ d3, uint32_t n,
+                 const uint64_t* __restrict__ spec_total) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= n) return;
+  // speculative build: n is the capacity and the candidate count is on the device; its
+  // load goes out beside the first gather (up0 has `n` readable entries either way)
+  const uint64_t t = spec_total ? *spec_total : 0ull;
   const uint32_t u1 = up0[c];
+  const uint32_t dc = d0[c];
+  if (spec_total && (t > n || c >= (uint32_t)t)) return;
   const uint32_t u2 = up0[u1];
+  const uint32_t e1 = d0[u1];
   const uint32_t u3 = up0[u2];
-  up1[c] = up0[u3];
-  d1[c] = d0[c] + d0[u1] + d0[u2] + d0[u3];
+  const uint32_t e2 = d0[u2];
+  const uint32_t u4 = up0[u3];
+  const uint32_t e3 = d0[u3];
+  up1[c] = u4;
+  d1[c] = dc + e1 + e2 + e3;
+  up2[c] = u2;
+  up3[c] = u3;
+  d2[c] = dc + e1;
+  d3[c] = dc + e1 + e2;
 }
+
+// the lifting tables of one build: ups / dists [levels + 1][stride], the 2- and 3-jump tables
+// [levels][stride]
+struct LiftTabs {
+  const uint32_t *ups, *dists, *ups2, *ups3, *dists2, *dists3;
+  uint32_t stride;
+  int levels;
+};
 
 // where an enumerated chain stops: its record count and the position after its last record
 struct ChainEnd {
   uint64_t count, next_pos;
+  uint64_t more;  // the last node has a successor candidate (the descent hit its depth)
 };
 
 // the last chain node from candidate c whose position is < limit (pos(c) < limit), and the
-// number of records from c to it: greedy descent over the lifting levels (at most 3 jumps
-// per level: 4 would be one jump of the level above)
+// number of records from c to it: greedy descent over the lifting levels -- at each level the
+// furthest of 1, 2, 3 jumps that stays below the limit (positions grow along the chain and a
+// terminal repeats itself with distance 0), the three candidates loaded side by side
 __device__ __forceinline__ uint32_t chain_descend(const uint64_t* __restrict__ cand,
-                                                  const uint32_t* __restrict__ ups,
-                                                  const uint32_t* __restrict__ dists, uint32_t n,
-                                                  int levels, uint32_t c, uint64_t limit,
+                                                  const LiftTabs& t, uint32_t c, uint64_t limit,
                                                   uint64_t& count) {
   uint32_t node = c;
   uint64_t cnt = 1;
-  for (int k = levels - 1; k >= 0; k--)
-    for (int j = 0; j < 3; j++) {
-      const uint32_t d = dists[(size_t)k * n + node];
-      if (d == 0) break;  // terminal
-      const uint32_t nx = ups[(size_t)k * n + node];
-      if (cand[nx] >= limit) break;
-      node = nx;
-      cnt += d;
-    }
+  for (int k = t.levels - 1; k >= 0; k--) {
+    const size_t o = (size_t)k * t.stride + node;
+    const uint32_t n1 = t.ups[o], n2 = t.ups2[o], n3 = t.ups3[o];
+    const uint32_t e1 = t.dists[o], e2 = t.dists2[o], e3 = t.dists3[o];
+    const uint64_t p1 = cand[n1], p2 = cand[n2], p3 = cand[n3];
+    if (p3 < limit) { node = n3; cnt += e3; }
+    else if (p2 < limit) { node = n2; cnt += e2; }
+    else if (p1 < limit) { node = n1; cnt += e1; }
+  }
   count = cnt;
   return node;
 }
@@ -376,25 +433,33 @@ __device__ __forceinline__ uint32_t chain_descend(const uint64_t* __restrict__ c
 // enumeration stops.
 __global__ void __launch_bounds__(256)
 scan_enum_kernel(const uint8_t* __restrict__ s, const uint64_t* __restrict__ cand,
-                 const uint32_t* __restrict__ ups, const uint32_t* __restrict__ dists, uint32_t n,
-                 int levels, uint32_t start, int at_zero, uint64_t limit, uint64_t out_base,
+                 LiftTabs t, const uint64_t* __restrict__ spec_total,
+                 uint32_t start, int at_zero, uint64_t limit, uint64_t out_base,
                  uint64_t cap, uint64_t* __restrict__ rec_off, uint32_t* __restrict__ rec_len,
                  ChainEnd* __restrict__ end) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool ok = !(at_zero && cand[start] != 0);
+  // speculative build: tables of `stride` entries, valid only when the total fits them
+  const bool built = !spec_total || (*spec_total != 0 && *spec_total <= t.stride);
+  const bool ok = built && !(at_zero && cand[start] != 0);
   if (i == 0) {
-    uint64_t cnt = 0, nx = 0;
+    uint64_t cnt = 0, nx = 0, more = 0;
     if (ok) {
-      const uint64_t tp = cand[chain_descend(cand, ups, dists, n, levels, start, limit, cnt)];
+      const uint32_t last = chain_descend(cand, t, start, limit, cnt);
+      const uint64_t tp = cand[last];
       nx = tp + be16_at(s, tp);
+      more = t.dists[last] != 0u;
     }
     end->count = cnt;
     end->next_pos = nx;
+    end->more = more;
   }
-  if (!ok || i > dists[(size_t)levels * n + start] || out_base + i >= cap) return;
+  if (!ok || i > t.dists[(size_t)t.levels * t.stride + start] || out_base + i >= cap) return;
   uint32_t node = start;
-  for (int k = 0; k < levels; k++)
-    for (uint32_t d = (uint32_t)(i >> (2 * k)) & 3u; d; d--) node = ups[(size_t)k * n + node];
+  for (int k = 0; k < t.levels; k++) {  // one jump per non-zero base-4 digit of i
+    const uint32_t d = (uint32_t)(i >> (2 * k)) & 3u;
+    const uint32_t* tab = d == 1 ? t.ups : d == 2 ? t.ups2 : t.ups3;
+    if (d) node = tab[(size_t)k * t.stride + node];
+  }
   const uint64_t p = cand[node];
   if (p >= limit) return;
   rec_off[out_base + i] = p;
@@ -407,8 +472,7 @@ scan_enum_kernel(const uint8_t* __restrict__ s, const uint64_t* __restrict__ can
 // the window are ~0.
 __global__ void __launch_bounds__(256)
 scan_exits_kernel(const uint8_t* __restrict__ s, const uint64_t* __restrict__ cand,
-                  const uint32_t* __restrict__ ups, const uint32_t* __restrict__ dists, uint32_t n,
-                  int levels, uint64_t window, uint64_t limit, uint32_t cap,
+                  LiftTabs t, uint32_t n, uint64_t window, uint64_t limit, uint32_t cap,
                   uint64_t* __restrict__ entries, uint64_t* __restrict__ exits) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= cap) return;
@@ -418,7 +482,7 @@ scan_exits_kernel(const uint8_t* __restrict__ s, const uint64_t* __restrict__ ca
     return;
   }
   uint64_t cnt;
-  const uint64_t tp = cand[chain_descend(cand, ups, dists, n, levels, c, limit, cnt)];
+  const uint64_t tp = cand[chain_descend(cand, t, c, limit, cnt)];
   const uint64_t nx = tp + be16_at(s, tp);
   entries[c] = cand[c];
   exits[c] = nx | (nx < limit ? (1ull << 63) : 0ull);
@@ -516,10 +580,23 @@ struct mgenx_scan_ws {
   uint64_t key_n = 0;
   int key_mode = -1;
   uint32_t n = 0;      // candidates (0: resolver only -- none, or a pathologically dense stream)
-  int levels = 0;      // lifting levels: ups / dists hold levels + 1 tables of n
+  int levels = 0;      // lifting levels: ups / dists hold levels + 1 tables of `stride`
+  uint32_t stride = 0; // table stride (n, or the capacity of a speculative build)
   uint64_t* cand = nullptr;
   uint32_t* ups = nullptr;
   uint32_t* dists = nullptr;
+  uint32_t* ups2 = nullptr;   // [levels][stride] 2- and 3-jump tables
+  uint32_t* ups3 = nullptr;
+  uint32_t* dists2 = nullptr;
+  uint32_t* dists3 = nullptr;
+  uint64_t last_records = 0;  // the last whole-stream chain's record count (spec levels)
+  // speculative builds: the next whole-stream scan sizes its tables by spec_cap (from the
+  // last exact build) and runs detect -> link -> lifting -> enumeration without waiting for
+  // the candidate total; spec_total is that total on the device, spec_pending says the
+  // current tables are speculative (the host checks the total after the one sync)
+  uint32_t spec_cap = 0;
+  const uint64_t* spec_total = nullptr;
+  bool spec_pending = false;
 };
 
 extern "C" void* mgenx_scan_ws_new() { return new mgenx_scan_ws(); }
@@ -545,8 +622,50 @@ struct Fail {
 
 // detect -> device scan of the block counts -> (one copy back: the candidate total) ->
 // compact + link -> lifting levels.  Leaves the tables in ws (async after the copy).
+int levels_for(uint64_t n) {
+  int levels = 1;
+  while ((1ull << (2 * levels)) < n) levels++;  // 4^levels >= n > any chain length
+  return levels;
+}
+
+// bytes of the lifting tables for `stride` candidates and `levels` levels
+size_t tab_bytes(uint32_t stride, int levels) {
+  return (size_t)stride * 4 * (2 * (size_t)(levels + 1) + 4 * (size_t)levels);
+}
+
+// carve ws.tabs into the lifting tables; launch the link and the lifting levels
+void lay_tables(mgenx_scan_ws& ws, uint32_t stride, int levels) {
+  ws.stride = stride;
+  ws.levels = levels;
+  ws.cand = static_cast<uint64_t*>(ws.cands.mem);
+  ws.ups = static_cast<uint32_t*>(ws.tabs.mem);
+  ws.dists = ws.ups + (size_t)(levels + 1) * stride;
+  ws.ups2 = ws.dists + (size_t)(levels + 1) * stride;
+  ws.ups3 = ws.ups2 + (size_t)levels * stride;
+  ws.dists2 = ws.ups3 + (size_t)levels * stride;
+  ws.dists3 = ws.dists2 + (size_t)levels * stride;
+}
+
+LiftTabs lift_tabs(const mgenx_scan_ws& ws) {
+  LiftTabs t;
+  t.ups = ws.ups; t.dists = ws.dists; t.ups2 = ws.ups2; t.ups3 = ws.ups3;
+  t.dists2 = ws.dists2; t.dists3 = ws.dists3; t.stride = ws.stride; t.levels = ws.levels;
+  return t;
+}
+
+void launch_lifts(const mgenx_scan_ws& ws, const uint64_t* spec_total, hipStream_t stream) {
+  const uint32_t st = ws.stride;
+  const dim3 g((st + 255) / 256);
+  for (int k = 1; k <= ws.levels; k++) {
+    const size_t a = (size_t)(k - 1) * st, b = (size_t)k * st;
+    hipLaunchKernelGGL(scan_lift_kernel, g, dim3(256), 0, stream, ws.ups + a, ws.dists + a,
+                       ws.ups + b, ws.dists + b, ws.ups2 + a, ws.ups3 + a, ws.dists2 + a,
+                       ws.dists3 + a, st, spec_total);
+  }
+}
+
 int scan_build(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, int mode, hipStream_t stream,
-               const Fail& fail) {
+               const Fail& fail, bool spec = false) {
   const bool sink = mode == MGENX_SCAN_SINK;
   const ScanMode m = sink ? ScanMode{MGENX_MIN_SIZE, MGENX_MAX_SIZE} : ScanMode{4u, 65535u};
   hipError_t e;
@@ -555,6 +674,9 @@ int scan_build(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, int mode, h
   ws.levels = 0;
   ws.cand = nullptr;
   ws.ups = ws.dists = nullptr;
+  ws.stride = 0;
+  ws.spec_pending = false;
+  ws.spec_total = nullptr;
   if ((e = ensure(ws.small, 4096)) != hipSuccess) return fail(e, "scan workspace");
   if (!ws.host) {
     void* hp = nullptr;
@@ -573,14 +695,14 @@ int scan_build(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, int mode, h
     return MGENX_OK;
   }
   const uint32_t nb = (uint32_t)n_blocks64;
-  const size_t slot_b = align256((size_t)nb * kScanSlots * 2);
+  const size_t slot_b = align256((size_t)nb * kScanSlots * 4);
   const size_t cnt_b = align256((size_t)(nb + 1) * 8);
   size_t cub_bytes = 0;
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, cub_bytes, (const uint64_t*)nullptr,
                                          (uint64_t*)nullptr, (int)(nb + 1), stream);
   if ((e = ensure(ws.slots, slot_b + 2 * cnt_b + align256(cub_bytes))) != hipSuccess)
     return fail(e, "scan workspace");
-  uint16_t* d_slots = static_cast<uint16_t*>(ws.slots.mem);
+  uint32_t* d_slots = static_cast<uint32_t*>(ws.slots.mem);
   uint64_t* d_counts = reinterpret_cast<uint64_t*>(static_cast<char*>(ws.slots.mem) + slot_b);
   uint64_t* d_base = d_counts + cnt_b / 8;
   void* d_cub = static_cast<char*>(ws.slots.mem) + slot_b + 2 * cnt_b;
@@ -595,6 +717,29 @@ int scan_build(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, int mode, h
       return fail(e, "scan offsets");
     hipLaunchKernelGGL(scan_total_kernel, dim3(1), dim3(1), 0, stream, d_base + nb, ws.host_dev);
   }
+  if (spec && ws.spec_cap) {
+    // speculative: tables for spec_cap candidates, linked and lifted with the total read on
+    // the device; the caller enumerates and then checks the total (one sync for the scan)
+    const uint32_t cap = ws.spec_cap;
+    // levels for the last chain's length (a longer chain costs another enumeration round
+    // in scan_walk, not correctness)
+    const uint64_t want = ws.last_records ? ws.last_records : cap;  // 4^levels + 1 records
+    const int levels = levels_for(std::min<uint64_t>(want, cap));
+    if ((e = ensure(ws.cands, (size_t)cap * 8)) != hipSuccess ||
+        (e = ensure(ws.tabs, tab_bytes(cap, levels))) != hipSuccess)
+      return fail(e, "scan workspace");
+    ws.key_s = s;
+    ws.key_n = nbytes;
+    ws.key_mode = mode;
+    lay_tables(ws, cap, levels);
+    ws.spec_total = d_base + nb;
+    ws.spec_pending = true;
+    hipLaunchKernelGGL(scan_link_kernel, dim3((nb + 3) / 4), dim3(256), 0, stream, s, nbytes,
+                       d_slots, d_counts, d_base, nb, ws.cand, ws.ups, ws.dists, (uint64_t)cap);
+    launch_lifts(ws, ws.spec_total, stream);
+    if ((e = hipGetLastError()) != hipSuccess) return fail(e, "scan launch");
+    return MGENX_OK;
+  }
   if ((e = hipStreamSynchronize(stream)) != hipSuccess) return fail(e, "scan detect");
   struct {
     uint32_t total, overflowed;  // candidates, overflowing blocks
@@ -608,26 +753,20 @@ int scan_build(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, int mode, h
   const uint64_t max_cand = nbytes / 16 + 65536;
   if (h_tot.total == 0 || h_tot.total > max_cand) return MGENX_OK;  // resolver only
   const uint32_t n = h_tot.total;
-  int levels = 1;
-  while ((1ull << (2 * levels)) < n) levels++;  // 4^levels >= n > any chain length
+  const int levels = levels_for(n);
+  // the next whole-stream scan speculates on about this many candidates
+  ws.spec_cap = (uint32_t)std::min<uint64_t>((uint64_t)n + n / 8 + 1024, 0xFFFFFFF0u);
   if ((e = ensure(ws.cands, (size_t)n * 8)) != hipSuccess) return fail(e, "scan workspace");
-  if ((e = ensure(ws.tabs, (size_t)n * 4 * 2 * (levels + 1))) != hipSuccess)
+  if ((e = ensure(ws.tabs, tab_bytes(n, levels))) != hipSuccess)
     return fail(e, "scan workspace");
   ws.n = n;
-  ws.levels = levels;
-  ws.cand = static_cast<uint64_t*>(ws.cands.mem);
-  ws.ups = static_cast<uint32_t*>(ws.tabs.mem);        // [levels + 1][n]
-  ws.dists = ws.ups + (size_t)(levels + 1) * n;         // [levels + 1][n]
+  lay_tables(ws, n, levels);
   if (h_tot.overflowed)  // blocks with more candidates than slots: second pass, exact sizes
     hipLaunchKernelGGL(scan_detect_kernel<true>, dim3(nb), dim3(kScanThreads), 0, stream, s,
                        nbytes, m, d_slots, d_counts, (const uint64_t*)d_base, ws.cand);
   hipLaunchKernelGGL(scan_link_kernel, dim3((nb + 3) / 4), dim3(256), 0, stream, s, nbytes,
-                     d_slots, d_counts, d_base, nb, ws.cand, ws.ups, ws.dists);
-  const dim3 g((n + 255) / 256);
-  for (int k = 1; k <= levels; k++)
-    hipLaunchKernelGGL(scan_lift_kernel, g, dim3(256), 0, stream, ws.ups + (size_t)(k - 1) * n,
-                       ws.dists + (size_t)(k - 1) * n, ws.ups + (size_t)k * n,
-                       ws.dists + (size_t)k * n, n);
+                     d_slots, d_counts, d_base, nb, ws.cand, ws.ups, ws.dists, (uint64_t)0);
+  launch_lifts(ws, nullptr, stream);
   if ((e = hipGetLastError()) != hipSuccess) return fail(e, "scan launch");
   return MGENX_OK;
 }
@@ -637,10 +776,11 @@ int scan_build(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, int mode, h
 // copy back; positions off the candidate set go through the sequential resolver.
 int scan_walk(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, int mode, uint64_t entry,
               uint64_t limit, uint64_t* rec_off, uint32_t* rec_len, uint64_t cap,
-              mgenx_scan_info* info, hipStream_t stream, const Fail& fail) {
+              mgenx_scan_info* info, hipStream_t stream, const Fail& fail,
+              const ChainEnd* first = nullptr) {
   const bool sink = mode == MGENX_SCAN_SINK;
   const uint32_t n = ws.n;
-  const int levels = ws.levels;
+  const LiftTabs tabs = lift_tabs(ws);
   hipError_t e;
   mgenx_scan_info out;
   memset(&out, 0, sizeof(out));
@@ -651,13 +791,20 @@ int scan_walk(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, int mode, ui
   uint32_t at = kNone;  // candidate index at pos, when known
   bool done = false;
   int reason = 1;
-  if (n && entry == 0 && entry < limit) {
+  if (first) {  // the speculative scan's enumeration from offset 0, already done
+    if (first->count) {
+      total = first->count;
+      pos = first->next_pos;
+      if (pos >= limit) { reason = 4; done = true; }
+      else if (pos + 2 > nbytes) { reason = 1; done = true; }
+    }
+  } else if (n && entry == 0 && entry < limit) {
     // candidate 0 is offset 0 when offset 0 is a candidate: enumerate speculatively
     hipLaunchKernelGGL(scan_enum_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, s, ws.cand,
-                       ws.ups, ws.dists, n, levels, 0u, 1, limit, (uint64_t)0, cap, rec_off,
+                       tabs, (const uint64_t*)nullptr, 0u, 1, limit, (uint64_t)0, cap, rec_off,
                        rec_len, d_end);
     if ((e = hipStreamSynchronize(stream)) != hipSuccess) return fail(e, "scan");
-    const ChainEnd h = {h_end[0], h_end[1]};
+    const ChainEnd h = {h_end[0], h_end[1], h_end[2]};
     if (h.count) {
       total = h.count;
       pos = h.next_pos;
@@ -669,10 +816,10 @@ int scan_walk(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, int mode, ui
     if (at != kNone) {
       // enumerate the candidate chain from `at` (grid sized by n >= its length)
       hipLaunchKernelGGL(scan_enum_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, s,
-                         ws.cand, ws.ups, ws.dists, n, levels, at, 0, limit, total, cap, rec_off,
-                         rec_len, d_end);
+                         ws.cand, tabs, (const uint64_t*)nullptr, at, 0, limit, total, cap,
+                         rec_off, rec_len, d_end);
       if ((e = hipStreamSynchronize(stream)) != hipSuccess) return fail(e, "scan");
-      const ChainEnd h = {h_end[0], h_end[1]};
+      const ChainEnd h = {h_end[0], h_end[1], h_end[2]};
       total += h.count;
       pos = h.next_pos;
       at = kNone;
@@ -702,6 +849,7 @@ int scan_walk(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, int mode, ui
   }
   if ((e = hipGetLastError()) != hipSuccess) return fail(e, "scan launch");
   out.n_records = total;
+  if (entry == 0 && limit == nbytes) ws.last_records = total;
   out.consumed = pos;
   out.status = reason == 2 ? 1 : 0;
   out.candidates = n;
@@ -717,8 +865,44 @@ extern "C" int mgenx_scan_run(void* wsp, const uint8_t* s, uint64_t nbytes, int 
                               mgenx_scan_info* info, hipStream_t stream, char* err, size_t errn) {
   mgenx_scan_ws& ws = *static_cast<mgenx_scan_ws*>(wsp);
   const Fail fail{err, errn};
-  int rc = scan_build(ws, s, nbytes, mode, stream, fail);
+  int rc = scan_build(ws, s, nbytes, mode, stream, fail, /*spec=*/true);
   if (rc != MGENX_OK) return rc;
+  if (ws.spec_pending) {
+    // one sync for the whole scan: the chain from offset 0 enumerated on the speculative
+    // tables; then the total and overflow word says whether they held every candidate
+    const uint32_t scap = ws.stride;
+    ChainEnd* d_end = reinterpret_cast<ChainEnd*>(ws.host_dev + 2);
+    const volatile uint64_t* h_end = ws.host + 2;
+    hipLaunchKernelGGL(scan_enum_kernel, dim3((scap + 255) / 256), dim3(256), 0, stream, s,
+                       ws.cand, lift_tabs(ws), ws.spec_total, 0u, 1, nbytes, (uint64_t)0, cap,
+                       rec_off, rec_len, d_end);
+    hipError_t e;
+    if ((e = hipStreamSynchronize(stream)) != hipSuccess) return fail(e, "scan");
+    uint32_t tot[2];
+    memcpy(tot, (const void*)ws.host, 8);  // candidates, overflowing blocks
+    const uint64_t max_cand = nbytes / 16 + 65536;
+    ws.spec_pending = false;
+    if (tot[1] || tot[0] > scap || tot[0] > max_cand) {
+      // the tables did not hold the stream: exact build (sizes the next speculation)
+      rc = scan_build(ws, s, nbytes, mode, stream, fail, false);
+      if (rc != MGENX_OK) return rc;
+      return scan_walk(ws, s, nbytes, mode, 0, nbytes, rec_off, rec_len, cap, info, stream, fail);
+    }
+    ws.n = tot[0];
+    if (ws.n) {
+      const ChainEnd h = {h_end[0], h_end[1], h_end[2]};
+      // a chain as long as the levels reach (the descent covers 4^levels - 1 jumps) may go
+      // on: rebuild with levels for n instead of continuing round by round on too few levels
+      if (h.count >= (1ull << (2 * ws.levels)) && h.more) {
+        rc = scan_build(ws, s, nbytes, mode, stream, fail, false);
+        if (rc != MGENX_OK) return rc;
+        return scan_walk(ws, s, nbytes, mode, 0, nbytes, rec_off, rec_len, cap, info, stream,
+                         fail);
+      }
+      return scan_walk(ws, s, nbytes, mode, 0, nbytes, rec_off, rec_len, cap, info, stream, fail,
+                       &h);
+    }
+  }
   return scan_walk(ws, s, nbytes, mode, 0, nbytes, rec_off, rec_len, cap, info, stream, fail);
 }
 
@@ -734,8 +918,7 @@ extern "C" int mgenx_scan_exits_run(void* wsp, const uint8_t* s, uint64_t nbytes
   if (rc != MGENX_OK) return rc;
   if (cap)
     hipLaunchKernelGGL(scan_exits_kernel, dim3((cap + 255) / 256), dim3(256), 0, stream, s,
-                       ws.cand, ws.ups, ws.dists, ws.n, ws.levels, window, limit, cap, entries,
-                       exits);
+                       ws.cand, lift_tabs(ws), ws.n, window, limit, cap, entries, exits);
   hipError_t e;
   if ((e = hipGetLastError()) != hipSuccess) return fail(e, "scan launch");
   if (candidates) *candidates = ws.n;
