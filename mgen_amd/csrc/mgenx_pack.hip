@@ -70,9 +70,16 @@ pack_kernel(PackParams p) {
   const uint64_t n_batches = ((uint64_t)p.n + 63) >> 6;
   const uint64_t n_waves = (uint64_t)gridDim.x * kWaves;
 
-  // block-uniform trip count: every wave reaches the same __syncthreads()
-  for (uint64_t base = (uint64_t)blockIdx.x * kWaves; base < n_batches; base += n_waves) {
-    const uint64_t b = base + wv;
+  // Each wave owns its LDS image / meta / prefix rows, so waves run their batches
+  // independently: wave-level ordering only (a block barrier lowers to s_waitcnt vmcnt(0) as
+  // well, which would hold every wave's next meta phase until its stores drained -- keeping
+  // the waves of a CU in lockstep, meta phases and store phases not overlapping)
+  auto wave_sync = [&]() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  for (uint64_t b = (uint64_t)blockIdx.x * kWaves + wv; b < n_batches; b += n_waves) {
     const uint64_t i = (b << 6) + lane;
     PackMeta m;
     m.off = 0; m.ret = 0; m.trailer = 0; m.pend = 0; m.poff = 0; m.hdr = 0;
@@ -263,10 +270,50 @@ pack_kernel(PackParams p) {
     // over them.  Everything else keeps one (unaligned) unit store per 16 record bytes.
     const uint32_t nv = b < n_batches ? (uint32_t)min((uint64_t)64, (uint64_t)p.n - (b << 6)) : 0u;
     const bool has = (uint32_t)lane < nv;
+    // Aligned stride path (config 2, the recvmmsg slot layout): every record of the wave
+    // fills its 16-byte-aligned slot exactly (ret == stride), zero fill, image inside kImg.
+    // Each 16-byte unit of the wave's range is composed once -- zeros, image bytes, or the
+    // trailer -- and stored once: no second pass over lines already written (re-writing a
+    // record's head and tail units after the fill costs 8 % more bytes but a quarter more
+    // time: the lines have left L2 by then and come back as partial writes).
+    const bool stride_ok = !has || (m.ret == (uint32_t)p.stride && m.pend <= (uint32_t)kImg);
+    if (!p.rec_off && !rf && (p.stride & 15u) == 0 && p.stride >= 32 && nv > 0 &&
+        variant == 0 && __all(stride_ok)) {
+      const uint32_t U = (uint32_t)(p.stride >> 4);        // units per record
+      const uint32_t q = 64u / U, rm = 64u % U;            // unit step = q records + rm units
+      uint32_t r = (uint32_t)lane / U, pu = (uint32_t)lane % U;
+      uint8_t* base = p.slab + (b << 6) * p.stride;
+      const uint32_t units = nv * U;
+      for (uint32_t u = lane; u < units; u += 64) {
+        const uint32_t pos = pu << 4;
+        uint32_t v0 = 0u, v1 = 0u, v2 = 0u, v3 = 0u;
+        const uint32_t pend = s_meta[wv][r].pend;             // LDS (record r of the wave)
+        if (pos < pend) {
+          const u32x4_t iv = *reinterpret_cast<const u32x4_t*>(&s_img[wv][r * kImg + pos]);
+          const int lim = (int)pend - (int)pos;
+          const uint32_t m0 = byte_range_mask(0, lim < 0 ? 0 : (lim > 4 ? 4 : lim));
+          const uint32_t m1 = byte_range_mask(0, lim < 4 ? 0 : (lim > 8 ? 4 : lim - 4));
+          const uint32_t m2 = byte_range_mask(0, lim < 8 ? 0 : (lim > 12 ? 4 : lim - 8));
+          const uint32_t m3 = byte_range_mask(0, lim < 12 ? 0 : (lim > 16 ? 4 : lim - 12));
+          v0 = iv.x & m0; v1 = iv.y & m1; v2 = iv.z & m2; v3 = iv.w & m3;
+        }
+        if (pu == U - 1u && s_meta[wv][r].trailer_on) {       // ret - 4 .. ret - 1, big-endian
+          v3 = bswap32(s_meta[wv][r].trailer);
+        }
+        stu128(base + (uint64_t)u * 16u, u32x4_t{v0, v1, v2, v3});
+        pu += rm;
+        r += q;
+        if (pu >= U) { pu -= U; r++; }
+      }
+      wave_sync();
+      continue;
+    }
     const uint64_t next_off = __shfl_down(m.off, 1);
     const bool packed_ok = !has || (m.ret > 0 && m.pend <= (uint32_t)kImg &&
                                     ((uint32_t)lane + 1 == nv || m.off + m.ret == next_off));
-    const bool fast = !rf && variant == 0 && nv > 0 && __all(packed_ok);
+    // (diagnostics: variant 3 = never the fast path, 4 = its zero fill only, 5 = no wait)
+    const bool fast = !rf && (variant == 0 || variant == 4 || variant == 5) && nv > 0 &&
+                      __all(packed_ok);
     const uint32_t kimg = (min(m.pend, m.ret) + 15u) >> 4;  // image units
     uint32_t units = (m.ret + 15u) >> 4;
     if (fast) {
@@ -276,7 +323,7 @@ pack_kernel(PackParams p) {
       const u32x4_t zero = {0u, 0u, 0u, 0u};
       for (uint64_t a = a0 + 16u * (uint32_t)lane; a < a1; a += 1024u) stu128(p.slab + a, zero);
       // the overwrites below must land after these stores
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (!(MGENX_DIAG && variant == 5)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     uint32_t incl = units;
 #pragma unroll
@@ -286,14 +333,14 @@ pack_kernel(PackParams p) {
     }
     s_pre[wv][lane + 1] = incl;
     if (lane == 0) s_pre[wv][0] = 0;
-    __syncthreads();
+    wave_sync();
     const uint32_t total = s_pre[wv][64];
     // Each lane walks units lane, lane+64, ...; its record index only moves forward, so
     // LDS is probed only when the unit leaves the current record.
     int ri = 0;
     uint32_t rstart = 0, next_start = s_pre[wv][1];
     PackMeta r = s_meta[wv][0];
-    for (uint32_t u = lane; u < (variant == 1 ? 0u : total); u += 64) {
+    for (uint32_t u = lane; u < ((variant == 1 || variant == 4) ? 0u : total); u += 64) {
       if (next_start <= u) {
         do {
           ri++;
@@ -369,7 +416,7 @@ pack_kernel(PackParams p) {
           if ((uint32_t)j < rem) dst[j] = (uint8_t)(v[j >> 2] >> ((j & 3) * 8));
       }
     }
-    __syncthreads();
+    wave_sync();  // this batch's LDS reads before the next batch's meta writes
   }
 }
 

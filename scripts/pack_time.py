@@ -1,0 +1,55 @@
+"""Pack timings: config 2 (1M x 1024 B, stride) and config 3 (1M x U{64..1472}, packed)."""
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from mgen_amd import PACK_CHECKSUM, Engine, to_device  # noqa: E402
+from mgen_amd.workloads import udp_fixed, udp_mixed  # noqa: E402
+
+eng = Engine(0)
+dev = "cuda:0"
+
+
+def timed(fn, reps=20):
+    fn()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+n = 1 << 20
+tmpl, pool, desc = udp_fixed(n, 1024)
+dt, dp, dd = to_device(tmpl), to_device(pool), to_device(desc)
+crc = torch.empty(len(tmpl), dtype=torch.int32, device=dev)
+eng.pack_prepare(dt, len(tmpl), dp, crc)
+slab = torch.empty(n * 1024, dtype=torch.uint8, device=dev)
+ol = torch.empty(n, dtype=torch.int32, device=dev)
+ms = timed(lambda: eng.pack(dt, crc, dd, n, dp, slab, stride=1024, opts=PACK_CHECKSUM, out_len=ol))
+print(f"config2 pack_ms {ms:.4f} GB/s {(n * 1044) / ms / 1e6:.1f}")
+tmpl, pool, desc, offs, sizes = udp_mixed(n, 64, 1472, 64, payload_hex="00112233445566778899aabbccddeeff")
+total = int(offs[-1] + sizes[-1])
+dt, dp, dd = to_device(tmpl), to_device(pool), to_device(desc)
+do = to_device(offs).view(torch.int64)
+crc = torch.empty(len(tmpl), dtype=torch.int32, device=dev)
+eng.pack_prepare(dt, len(tmpl), dp, crc)
+slab = torch.empty(total + 64, dtype=torch.uint8, device=dev)
+ms = timed(lambda: eng.pack(dt, crc, dd, n, dp, slab, rec_off=do, opts=PACK_CHECKSUM, out_len=ol))
+print(f"config3 pack_ms {ms:.4f} GB/s {(n * 36 + total) / ms / 1e6:.1f}")
+if len(sys.argv) > 1:
+    d = Engine(0, diag=True)
+    for v in [0, 1, 3, 4, 5]:
+        d.set_pack_variant(v)
+        tmpl, pool, desc = udp_fixed(n, 1024)
+        dt, dp, dd = to_device(tmpl), to_device(pool), to_device(desc)
+        crc = torch.empty(len(tmpl), dtype=torch.int32, device=dev)
+        d.pack_prepare(dt, len(tmpl), dp, crc)
+        slab2 = torch.empty(n * 1024, dtype=torch.uint8, device=dev)
+        ms = timed(lambda: d.pack(dt, crc, dd, n, dp, slab2, stride=1024, opts=PACK_CHECKSUM, out_len=ol))
+        print(f"variant {v} config2 pack_ms {ms:.4f}")
