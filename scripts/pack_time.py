@@ -53,3 +53,15 @@ if len(sys.argv) > 1:
         slab2 = torch.empty(n * 1024, dtype=torch.uint8, device=dev)
         ms = timed(lambda: d.pack(dt, crc, dd, n, dp, slab2, stride=1024, opts=PACK_CHECKSUM, out_len=ol))
         print(f"variant {v} config2 pack_ms {ms:.4f}")
+if len(sys.argv) > 1:
+    tmpl, pool, desc, offs, sizes = udp_mixed(n, 64, 1472, 64, payload_hex="00112233445566778899aabbccddeeff")
+    total = int(offs[-1] + sizes[-1])
+    dt, dp, dd = to_device(tmpl), to_device(pool), to_device(desc)
+    do = to_device(offs).view(torch.int64)
+    crc = torch.empty(len(tmpl), dtype=torch.int32, device=dev)
+    d.pack_prepare(dt, len(tmpl), dp, crc)
+    slab3 = torch.empty(total + 64, dtype=torch.uint8, device=dev)
+    for v in [0, 1, 3, 4, 5]:
+        d.set_pack_variant(v)
+        ms = timed(lambda: d.pack(dt, crc, dd, n, dp, slab3, rec_off=do, opts=PACK_CHECKSUM, out_len=ol))
+        print(f"variant {v} config3 pack_ms {ms:.4f}")
