@@ -443,8 +443,8 @@ static int pack_common(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
   p.tx_crc = dev_tx_crc;
   p.state = dev_state;
   const uint64_t batches = ((uint64_t)n + 63) / 64;
-  uint64_t grid = (batches + 3) / 4;
-  const uint64_t cap = (uint64_t)ctx->cu_count * 4;
+  uint64_t grid = (batches + 3) / 4;                // groups of 4 batches (kProd)
+  const uint64_t cap = (uint64_t)ctx->cu_count * 2;  // 76 KB of LDS per workgroup
   if (grid > cap) grid = cap;
   hipError_t e = mgenx::launch_pack(p, (int)grid, (hipStream_t)stream);
   return e == hipSuccess ? MGENX_OK : set_err(ctx, e, "pack");

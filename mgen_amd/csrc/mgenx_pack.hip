@@ -18,7 +18,8 @@
 
 namespace mgenx {
 
-constexpr int kPackThreads = 256;
+constexpr int kProd = 4;                      // meta (producer) waves per workgroup
+constexpr int kPackThreads = 2 * kProd * 64;  // + as many store (consumer) waves
 constexpr int kImg = 96;  // header image bytes per record (header <= 76, + first payload)
 
 
@@ -30,7 +31,8 @@ struct PackMeta {
   uint32_t poff;     // pool offset of the payload
   uint16_t hdr;      // packet_header_len
   uint8_t trailer_on, rf;
-  uint32_t rsv;
+  uint32_t tx_out;   // tx_checksum after Pack (out: tx_crc)
+  uint32_t state;    // packet_header_len | flags << 16 (out: state)
 };
 
 __device__ __forceinline__ void img_put8(uint8_t* img, uint32_t at, uint32_t v) {
@@ -49,10 +51,15 @@ __device__ __forceinline__ void img_put32(uint8_t* img, uint32_t at, uint32_t v)
 
 __global__ void __launch_bounds__(kPackThreads)
 pack_kernel(PackParams p) {
-  constexpr int kWaves = kPackThreads / 64;
-  __shared__ __attribute__((aligned(16))) uint8_t s_img[kWaves][64 * kImg];
-  __shared__ PackMeta s_meta[kWaves][64];
-  __shared__ uint32_t s_pre[kWaves][65];
+  // Producer / consumer waves: waves 0..kProd-1 run phase 1 (meta: loads and CRC algebra)
+  // of a group of kProd batches into one of two LDS buffers while waves kProd..2kProd-1 run
+  // phase 2 (the slab stores) of the previous group from the other buffer.  A wave that
+  // both loads and stores stalls its next loads behind its own stores (gfx950 counts
+  // stores in vmcnt, in order), so split roles keep the loads and the store stream
+  // overlapped; one fence-free block barrier per stage.
+  __shared__ __attribute__((aligned(16))) uint8_t s_img[2][kProd][64 * kImg];
+  __shared__ PackMeta s_meta[2][kProd][64];
+  __shared__ uint32_t s_pre[kProd][65];
   __shared__ uint32_t s_tab[256];
   __shared__ uint32_t s_a4[1024];
 
@@ -62,31 +69,41 @@ pack_kernel(PackParams p) {
 
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
-  uint8_t* img = &s_img[wv][lane * kImg];
+  const bool producer = wv < kProd;
+  const int slot = wv % kProd;
   const int variant = MGENX_DIAG ? p.variant : 0;  // ablations: diagnostics build only
   const bool ck = (p.opts & MGENX_PACK_CHECKSUM) != 0 && variant != 2;
   const bool rf = (p.opts & MGENX_PACK_RANDOM_FILL) != 0;
   const bool raw = (p.opts & MGENX_PACK_RAW) != 0;  // Pack alone (no UDP send sequence)
   const uint64_t n_batches = ((uint64_t)p.n + 63) >> 6;
-  const uint64_t n_waves = (uint64_t)gridDim.x * kWaves;
+  const uint64_t n_groups = (n_batches + kProd - 1) / kProd;
 
-  // Each wave owns its LDS image / meta / prefix rows, so waves run their batches
-  // independently: wave-level ordering only (a block barrier lowers to s_waitcnt vmcnt(0) as
-  // well, which would hold every wave's next meta phase until its stores drained -- keeping
-  // the waves of a CU in lockstep, meta phases and store phases not overlapping)
   auto wave_sync = [&]() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   };
-  for (uint64_t b = (uint64_t)blockIdx.x * kWaves + wv; b < n_batches; b += n_waves) {
+  // stage s: producers build group blockIdx.x + s * gridDim.x into buffer s & 1, consumers
+  // store group blockIdx.x + (s - 1) * gridDim.x from buffer (s - 1) & 1 (block-uniform)
+  for (uint64_t s = 0;; s++) {
+    const uint64_t gp = (uint64_t)blockIdx.x + s * gridDim.x;
+    const bool prod_live = gp < n_groups;
+    const bool cons_live = s > 0 && gp - gridDim.x < n_groups;
+    if (!prod_live && !cons_live) break;
+    const int buf = (int)((producer ? s : s - 1) & 1);
+    const uint64_t b = (producer ? gp : gp - gridDim.x) * kProd + slot;
+    uint8_t* const S_IMG = &s_img[buf][slot][0];
+    PackMeta* const S_META = s_meta[buf][slot];
     const uint64_t i = (b << 6) + lane;
+    if (!(producer ? prod_live : cons_live) || b >= n_batches) goto stage_end;
+    if (producer) {
+    uint8_t* img = S_IMG + lane * kImg;
     PackMeta m;
     m.off = 0; m.ret = 0; m.trailer = 0; m.pend = 0; m.poff = 0; m.hdr = 0;
-    m.trailer_on = 0; m.rf = rf ? 1 : 0; m.rsv = 0;
+    m.trailer_on = 0; m.rf = rf ? 1 : 0; m.tx_out = 0; m.state = 0;
 
     // ------------------------------ phase 1: meta ------------------------------
-    if (b < n_batches && i < p.n) {
+    if (i < p.n) {
       // Every global read of the record is issued up front, in two dependent rounds:
       // descriptor, then the template (68 B, as 17 words in registers) and the CRC tables
       // indexed by lengths the template fixes.  (Field reads through the template pointer
@@ -254,13 +271,22 @@ pack_kernel(PackParams p) {
         }
       }
       if (m.off > p.slab_bytes || m.ret > p.slab_bytes - m.off) m.ret = 0;  // never write OOB
-      p.out_len[i] = m.ret;
-      if (p.tx_crc) p.tx_crc[i] = tx_out;
+      m.tx_out = tx_out;
       // the MgenMsg members Pack leaves behind: packet_header_len (set on every return but
       // the failing ones) and the flags member (CHECKSUM set, LAST_BUFFER cleared)
-      if (p.state) p.state[i] = (m.ret ? (uint32_t)m.hdr : 0xFFFFu) | (flags & 0xffu) << 16;
+      m.state = (m.ret ? (uint32_t)m.hdr : 0xFFFFu) | (flags & 0xffu) << 16;
     }
-    s_meta[wv][lane] = m;
+    S_META[lane] = m;
+    goto stage_end;
+    }
+    {
+    // consumer
+    const PackMeta m = S_META[lane];
+    if (i < p.n) {
+      p.out_len[i] = m.ret;
+      if (p.tx_crc) p.tx_crc[i] = m.tx_out;
+      if (p.state) p.state[i] = m.state;
+    }
 
     // --------------------------- phase 2: write units ---------------------------
     // Packed slab fast path: when the wave's records lie back to back (rec_off[i + 1] ==
@@ -287,9 +313,9 @@ pack_kernel(PackParams p) {
       for (uint32_t u = lane; u < units; u += 64) {
         const uint32_t pos = pu << 4;
         uint32_t v0 = 0u, v1 = 0u, v2 = 0u, v3 = 0u;
-        const uint32_t pend = s_meta[wv][r].pend;             // LDS (record r of the wave)
+        const uint32_t pend = S_META[r].pend;             // LDS (record r of the wave)
         if (pos < pend) {
-          const u32x4_t iv = *reinterpret_cast<const u32x4_t*>(&s_img[wv][r * kImg + pos]);
+          const u32x4_t iv = *reinterpret_cast<const u32x4_t*>(&S_IMG[r * kImg + pos]);
           const int lim = (int)pend - (int)pos;
           const uint32_t m0 = byte_range_mask(0, lim < 0 ? 0 : (lim > 4 ? 4 : lim));
           const uint32_t m1 = byte_range_mask(0, lim < 4 ? 0 : (lim > 8 ? 4 : lim - 4));
@@ -297,16 +323,15 @@ pack_kernel(PackParams p) {
           const uint32_t m3 = byte_range_mask(0, lim < 12 ? 0 : (lim > 16 ? 4 : lim - 12));
           v0 = iv.x & m0; v1 = iv.y & m1; v2 = iv.z & m2; v3 = iv.w & m3;
         }
-        if (pu == U - 1u && s_meta[wv][r].trailer_on) {       // ret - 4 .. ret - 1, big-endian
-          v3 = bswap32(s_meta[wv][r].trailer);
+        if (pu == U - 1u && S_META[r].trailer_on) {       // ret - 4 .. ret - 1, big-endian
+          v3 = bswap32(S_META[r].trailer);
         }
         stu128(base + (uint64_t)u * 16u, u32x4_t{v0, v1, v2, v3});
         pu += rm;
         r += q;
         if (pu >= U) { pu -= U; r++; }
       }
-      wave_sync();
-      continue;
+      goto stage_end;
     }
     const uint64_t next_off = __shfl_down(m.off, 1);
     const bool packed_ok = !has || (m.ret > 0 && m.pend <= (uint32_t)kImg &&
@@ -331,30 +356,30 @@ pack_kernel(PackParams p) {
       const uint32_t o = __shfl_up(incl, s);
       if (lane >= s) incl += o;
     }
-    s_pre[wv][lane + 1] = incl;
-    if (lane == 0) s_pre[wv][0] = 0;
+    s_pre[slot][lane + 1] = incl;
+    if (lane == 0) s_pre[slot][0] = 0;
     wave_sync();
-    const uint32_t total = s_pre[wv][64];
+    const uint32_t total = s_pre[slot][64];
     // Each lane walks units lane, lane+64, ...; its record index only moves forward, so
     // LDS is probed only when the unit leaves the current record.
     int ri = 0;
-    uint32_t rstart = 0, next_start = s_pre[wv][1];
-    PackMeta r = s_meta[wv][0];
+    uint32_t rstart = 0, next_start = s_pre[slot][1];
+    PackMeta r = S_META[0];
     for (uint32_t u = lane; u < ((variant == 1 || variant == 4) ? 0u : total); u += 64) {
       if (next_start <= u) {
         do {
           ri++;
           rstart = next_start;
-          next_start = s_pre[wv][ri + 1];
+          next_start = s_pre[slot][ri + 1];
         } while (next_start <= u);
-        r = s_meta[wv][ri];
+        r = S_META[ri];
       }
       uint32_t pos = (u - rstart) << 4;
       if (fast) {  // image units, then the record's last 16 bytes (past the image)
         const uint32_t ki = (min(r.pend, r.ret) + 15u) >> 4;
         if (pos >= (ki << 4)) pos = max(r.ret - 16u, ki << 4);
       }
-      const uint8_t* rimg = &s_img[wv][ri * kImg];
+      const uint8_t* rimg = &S_IMG[ri * kImg];
       uint32_t v[4] = {0u, 0u, 0u, 0u};
       // fill (zero, or the rand() stream after two zero bytes: mgenMsg.cpp:277-292)
       if (r.rf) {
@@ -416,7 +441,11 @@ pack_kernel(PackParams p) {
           if ((uint32_t)j < rem) dst[j] = (uint8_t)(v[j >> 2] >> ((j & 3) * 8));
       }
     }
-    wave_sync();  // this batch's LDS reads before the next batch's meta writes
+    }
+  stage_end:
+    // fence-free barrier: __syncthreads()'s vmcnt(0) would drain the consumers' stores
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
   }
 }
 
