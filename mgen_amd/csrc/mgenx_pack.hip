@@ -334,14 +334,108 @@ pack_kernel(PackParams p) {
       goto stage_end;
     }
     const uint64_t next_off = __shfl_down(m.off, 1);
-    const bool packed_ok = !has || (m.ret > 0 && m.pend <= (uint32_t)kImg &&
+    const bool packed_ok = !has || (m.ret >= 16u && m.pend <= (uint32_t)kImg &&
                                     ((uint32_t)lane + 1 == nv || m.off + m.ret == next_off));
-    // (diagnostics: variant 3 = never the fast path, 4 = its zero fill only, 5 = no wait)
-    const bool fast = !rf && (variant == 0 || variant == 4 || variant == 5) && nv > 0 &&
+    // (diagnostics: variant 3 = never the fast path, 4 = fill-then-rewrite scheme, its zero
+    // fill only, 5 = that scheme without its wait, 6 = no aligned-stride path)
+    const bool fast = !rf && (variant == 0 || variant >= 4) && nv > 0 &&
                       __all(packed_ok);
     const uint32_t kimg = (min(m.pend, m.ret) + 15u) >> 4;  // image units
     uint32_t units = (m.ret + 15u) >> 4;
-    if (fast) {
+    if (fast && (variant == 0 || variant == 6)) {
+      // The wave's range is zero-filled with aligned full-width stores, and each record's
+      // special units -- its image units and its last 16 bytes (trailer), record-relative
+      // and unaligned -- are stored over the fill in windows of 64 (one per lane, in slab
+      // order), each window right after the fill has passed its last byte: the partial
+      // overwrites meet their lines still in L2 (rewriting after the whole fill sent them
+      // back to HBM as partial writes).  No wait is needed: a wave's stores to the same
+      // address are performed in program order.  Image units lie wholly inside the record:
+      // one reaching past ret is replaced by the last unit, which carries the image bytes
+      // it overlaps.
+      const uint64_t A0 = __shfl(m.off, 0), A1 = __shfl(m.off + m.ret, (int)nv - 1);
+      const uint64_t ra1 = A1 & ~(uint64_t)15;
+      uint64_t fill = (A0 + 15u) & ~(uint64_t)15;  // next aligned unit to zero (uniform)
+      const uint32_t kin = min(kimg, m.ret >> 4);
+      const uint32_t n_sp = has ? kin + (16u * kin < m.ret ? 1u : 0u) : 0u;
+      uint32_t incl = n_sp;
+#pragma unroll
+      for (int s2 = 1; s2 < 64; s2 <<= 1) {
+        const uint32_t o = __shfl_up(incl, s2);
+        if (lane >= s2) incl += o;
+      }
+      s_pre[slot][lane + 1] = incl;
+      if (lane == 0) s_pre[slot][0] = 0;
+      wave_sync();
+      const uint32_t total = s_pre[slot][64];
+      int ri = 0;
+      uint32_t rstart = 0, next_start = s_pre[slot][1];
+      PackMeta r = S_META[0];
+      const u32x4_t zero = {0u, 0u, 0u, 0u};
+      for (uint32_t base = 0; base < total; base += 64) {
+        const uint32_t u = base + (uint32_t)lane;
+        const bool act = u < total;
+        uint32_t pos = 0;
+        uint64_t end = 0;
+        if (act) {
+          if (next_start <= u) {
+            do {
+              ri++;
+              rstart = next_start;
+              next_start = s_pre[slot][ri + 1];
+            } while (next_start <= u);
+            r = S_META[ri];
+          }
+          const uint32_t k = u - rstart;
+          const uint32_t rki = min((min(r.pend, r.ret) + 15u) >> 4, r.ret >> 4);
+          pos = k < rki ? 16u * k : r.ret - 16u;
+          end = r.off + pos + 16u;
+        }
+        uint64_t wend = end;  // the window's last byte + 1 (wave max)
+#pragma unroll
+        for (int s2 = 32; s2 >= 1; s2 >>= 1) {
+          const uint64_t o = __shfl_xor(wend, s2);
+          wend = o > wend ? o : wend;
+        }
+        const uint64_t fend = min(ra1, (wend + 15u) & ~(uint64_t)15);
+        for (uint64_t a = fill + 16u * (uint32_t)lane; a < fend; a += 1024u)
+          stu128(p.slab + a, zero);
+        if (fend > fill) fill = fend;
+        if (act) {
+          const uint8_t* rimg = &S_IMG[ri * kImg];
+          uint32_t v[4] = {0u, 0u, 0u, 0u};
+          if (pos < r.pend) {
+            const u32x4_t iv = *reinterpret_cast<const u32x4_t*>(rimg + pos);
+            const uint32_t w[4] = {iv.x, iv.y, iv.z, iv.w};
+#pragma unroll
+            for (int kk = 0; kk < 4; kk++) {
+              const int lim = (int)r.pend - (int)pos - 4 * kk;
+              v[kk] = w[kk] & byte_range_mask(0, lim < 0 ? 0 : (lim > 4 ? 4 : lim));
+            }
+          }
+          if (r.trailer_on && pos + 16 > r.ret - 4) {
+            const uint32_t be = bswap32(r.trailer);
+            const int t = (int)r.ret - 4 - (int)pos;
+#pragma unroll
+            for (int kk = 0; kk < 4; kk++) {
+              const int o = t - 4 * kk;
+              uint32_t val = 0u, msk = 0u;
+              if (o >= 0 && o < 4) {
+                val = be << (8 * o);
+                msk = 0xFFFFFFFFu << (8 * o);
+              } else if (o < 0 && o > -4) {
+                val = be >> (-8 * o);
+                msk = 0xFFFFFFFFu >> (-8 * o);
+              }
+              v[kk] = (v[kk] & ~msk) | val;
+            }
+          }
+          stu128(p.slab + r.off + pos, u32x4_t{v[0], v[1], v[2], v[3]});
+        }
+      }
+      for (uint64_t a = fill + 16u * (uint32_t)lane; a < ra1; a += 1024u) stu128(p.slab + a, zero);
+      goto stage_end;
+    }
+    if (fast) {  // (diagnostics: the fill-then-rewrite scheme)
       units = has ? kimg + (16u * kimg < m.ret ? 1u : 0u) : 0u;
       const uint64_t a0 = (__shfl(m.off, 0) + 15u) & ~(uint64_t)15;
       const uint64_t a1 = __shfl(m.off + m.ret, (int)nv - 1) & ~(uint64_t)15;

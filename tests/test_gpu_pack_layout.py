@@ -72,3 +72,31 @@ def test_pack_layouts_vs_oracle(torch, eng, oracle, layout, ck, rf, pay):
         rec = np.searchsorted(offs, bad[0], side="right") - 1
         pytest.fail(f"{bad.size} bytes differ, first at {bad[0]} (record {rec}, size "
                     f"{sizes[rec]}, pos {bad[0] - offs[rec]})")
+
+
+@pytest.mark.parametrize("ck", [1, 0])
+def test_pack_packed_large_vs_oracle(torch, eng, oracle, ck):
+    """Config 3's layout (records back to back, sizes U{64..1472}) at 262,144 records: the
+    fill and the overwritten head / tail units of every wave, byte for byte, on two launches
+    into fresh slabs (the overwrites rely on a wave's same-address store order)."""
+    from mgen_amd import PACK_CHECKSUM, to_device
+    from mgen_amd.workloads import udp_mixed
+    n = 262_144
+    tmpl, pool, desc, offs, sizes = udp_mixed(n, 64, 1472, 64,
+                                              payload_hex="00112233445566778899aabbccddeeff")
+    offs = offs.astype(np.uint64)
+    total = int(offs[-1] + sizes[-1])
+    want, wlen = oracle.udp_pack_batch(tmpl, desc, pool, total, rec_off=offs, checksum=bool(ck))
+    d_tmpl, d_pool, d_desc = to_device(tmpl), to_device(pool), to_device(desc)
+    crc = torch.empty(len(tmpl), dtype=torch.int32, device="cuda")
+    eng.pack_prepare(d_tmpl, len(tmpl), d_pool, crc)
+    d_off = to_device(offs).view(torch.int64)
+    for _ in range(2):
+        slab = torch.full((total,), 0xA5, dtype=torch.uint8, device="cuda")
+        out_len = eng.pack(d_tmpl, crc, d_desc, n, d_pool, slab, rec_off=d_off,
+                           opts=PACK_CHECKSUM if ck else 0)
+        torch.cuda.synchronize()
+        assert np.array_equal(out_len.cpu().numpy().view(np.uint32), wlen)
+        got = slab.cpu().numpy()
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, (bad.size, bad[:5])
