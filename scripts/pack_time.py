@@ -65,3 +65,15 @@ if len(sys.argv) > 1:
         d.set_pack_variant(v)
         ms = timed(lambda: d.pack(dt, crc, dd, n, dp, slab3, rec_off=do, opts=PACK_CHECKSUM, out_len=ol))
         print(f"variant {v} config3 pack_ms {ms:.4f}")
+if len(sys.argv) > 1:
+    # config 3 unpack: columns vs 32-B rows
+    d.set_pack_variant(0)
+    dl = to_device(sizes).view(torch.int32)
+    d.pack(dt, crc, dd, n, dp, slab3, rec_off=do, opts=PACK_CHECKSUM, out_len=ol)
+    cols = d.alloc_cols(n)
+    ms = timed(lambda: d.unpack(slab3, n, rec_off=do, rec_len=dl, cols=cols))
+    print(f"config3 unpack cols_ms {ms:.4f}")
+    rc = {"rows": d.alloc_rows(n)}
+    ms = timed(lambda: d.unpack(slab3, n, rec_off=do, rec_len=dl, cols=rc))
+    print(f"config3 unpack rows_ms {ms:.4f}")
+    assert int(((rc["rows"].view(torch.int32).view(n, 8)[:, 6] >> 24) & 0xFF).sum()) == 0
