@@ -77,3 +77,47 @@ if len(sys.argv) > 1:
     ms = timed(lambda: d.unpack(slab3, n, rec_off=do, rec_len=dl, cols=rc))
     print(f"config3 unpack rows_ms {ms:.4f}")
     assert int(((rc["rows"].view(torch.int32).view(n, 8)[:, 6] >> 24) & 0xFF).sum()) == 0
+if len(sys.argv) > 1:
+    # the same records at 16-byte-aligned starts (gaps of < 16 B): misalignment cost
+    sz = sizes.astype(np.int64)
+    al = (sz + 15) & ~15
+    offs_al = np.zeros(n, np.uint64)
+    offs_al[1:] = np.cumsum(al[:-1])
+    tot_al = int(offs_al[-1] + al[-1]) + 64
+    slab_al = torch.zeros(tot_al, dtype=torch.uint8, device=dev)
+    do_al = to_device(offs_al).view(torch.int64)
+    d.pack(dt, crc, dd, n, dp, slab_al, rec_off=do_al, opts=PACK_CHECKSUM, out_len=ol)
+    rc2 = {"rows": d.alloc_rows(n)}
+    ms = timed(lambda: d.unpack(slab_al, n, rec_off=do_al, rec_len=dl, cols=rc2))
+    print(f"config3 aligned-starts unpack rows_ms {ms:.4f}")
+    assert int(((rc2["rows"].view(torch.int32).view(n, 8)[:, 6] >> 24) & 0xFF).sum()) == 0
+    # 64-byte-aligned starts
+    al = (sz + 63) & ~63
+    offs_al = np.zeros(n, np.uint64)
+    offs_al[1:] = np.cumsum(al[:-1])
+    tot_al = int(offs_al[-1] + al[-1]) + 64
+    slab_al = torch.zeros(tot_al, dtype=torch.uint8, device=dev)
+    do_al = to_device(offs_al).view(torch.int64)
+    d.pack(dt, crc, dd, n, dp, slab_al, rec_off=do_al, opts=PACK_CHECKSUM, out_len=ol)
+    ms = timed(lambda: d.unpack(slab_al, n, rec_off=do_al, rec_len=dl, cols=rc2))
+    print(f"config3 64B-aligned-starts unpack rows_ms {ms:.4f}")
+    # lengths rounded to multiples of 64 (rows exact), aligned
+    sz64 = np.minimum(al, 1472)
+    dl64 = to_device(sz64.astype(np.int32)).view(torch.int32)
+    ms = timed(lambda: d.unpack(slab_al, n, rec_off=do_al, rec_len=dl64, cols=rc2))
+    print(f"config3 64B-aligned, len%64==0 unpack rows_ms {ms:.4f} (CRC errors expected)")
+if len(sys.argv) > 1:
+    # record ENDS on the 16-byte grid (rows are aligned to the record end): row loads aligned
+    ends = np.zeros(n, np.int64)
+    offs_e = np.zeros(n, np.uint64)
+    pe = 0
+    for_i = np.arange(n)
+    e = np.cumsum((sz + 15) & ~15)          # end_i = 16-aligned running end
+    offs_e = (e - sz).astype(np.uint64)
+    tot_e = int(e[-1]) + 64
+    slab_e = torch.zeros(tot_e, dtype=torch.uint8, device=dev)
+    do_e = to_device(offs_e).view(torch.int64)
+    d.pack(dt, crc, dd, n, dp, slab_e, rec_off=do_e, opts=PACK_CHECKSUM, out_len=ol)
+    ms = timed(lambda: d.unpack(slab_e, n, rec_off=do_e, rec_len=dl, cols=rc2))
+    print(f"config3 end-aligned unpack rows_ms {ms:.4f}")
+    assert int(((rc2["rows"].view(torch.int32).view(n, 8)[:, 6] >> 24) & 0xFF).sum()) == 0

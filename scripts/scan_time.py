@@ -1,0 +1,40 @@
+"""Timing: whole-stream scan of bench.py's config-5 stream (GPU TCP transmit, 65,536 x
+16 KiB records), 20 calls after one warm call; run under rocprofv3 --kernel-trace --stats
+to count launches per call."""
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from mgen_amd import PACK_CHECKSUM, SCAN_TCP, Engine, to_device  # noqa: E402
+from mgen_amd._abi import DESC_DTYPE  # noqa: E402
+from mgen_amd.workloads import make_templates  # noqa: E402
+
+n = 65536
+eng = Engine(0)
+tmpl, pool = make_templates(64)
+desc = np.zeros(n, DESC_DTYPE)
+seq = np.arange(n)
+desc["tmpl"] = seq % 64
+desc["seq_num"] = seq
+desc["tx_sec"] = 1_700_000_000
+desc["tx_usec"] = seq % 1_000_000
+desc["flags"] = 4
+tm, pl = to_device(tmpl), to_device(pool)
+tcrc = torch.empty(64, dtype=torch.int32, device="cuda")
+eng.pack_prepare(tm, 64, pl, tcrc)
+d_total = torch.full((n,), 16384, dtype=torch.int32, device="cuda")
+local, _ = eng.pack_tcp(tm, tcrc, to_device(desc), d_total, n, pl, opts=PACK_CHECKSUM)
+offs, lens, info = eng.stream_scan(local, SCAN_TCP, cap=n + 1)
+print("warm", int(info.n_records), int(info.candidates), int(info.resolved), flush=True)
+torch.cuda.synchronize()
+reps = 20
+t0 = time.perf_counter()
+for _ in range(reps):
+    offs, lens, info = eng.stream_scan(local, SCAN_TCP, cap=n + 1)
+torch.cuda.synchronize()
+print("scan_ms", (time.perf_counter() - t0) / reps * 1e3, int(info.n_records), flush=True)
+eng.close()
