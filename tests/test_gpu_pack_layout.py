@@ -100,3 +100,37 @@ def test_pack_packed_large_vs_oracle(torch, eng, oracle, ck):
         got = slab.cpu().numpy()
         bad = np.nonzero(got != want)[0]
         assert bad.size == 0, (bad.size, bad[:5])
+
+
+@pytest.mark.parametrize("n", [1, 3, 64, 65, 300, 1025, 5000])
+@pytest.mark.parametrize("layout", ["stride", "packed"])
+def test_pack_batch_counts_vs_oracle(torch, eng, oracle, n, layout):
+    """Batch counts around the pack kernel's geometry (64-record batches, groups of 4
+    batches per meta/store stage, partial last group): stride slots and back-to-back
+    records, byte for byte with the oracle, bytes outside the records untouched."""
+    from mgen_amd import PACK_CHECKSUM, to_device
+    from mgen_amd.workloads import udp_fixed, udp_mixed
+    if layout == "stride":
+        tmpl, pool, desc = udp_fixed(n, 512)
+        offs = np.arange(n, dtype=np.uint64) * 512
+        sizes = np.full(n, 512, np.int64)
+    else:
+        tmpl, pool, desc, offs, sizes = udp_mixed(n, 64, 1472, 16, seed=n)
+        offs = offs.astype(np.uint64)
+    total = int(offs[-1] + sizes[-1]) + 32
+    want, wlen = oracle.udp_pack_batch(tmpl, desc, pool, total, rec_off=offs, checksum=True)
+    d_tmpl, d_pool, d_desc = to_device(tmpl), to_device(pool), to_device(desc)
+    crc = torch.empty(len(tmpl), dtype=torch.int32, device="cuda")
+    eng.pack_prepare(d_tmpl, len(tmpl), d_pool, crc)
+    slab = torch.full((total,), 0xA5, dtype=torch.uint8, device="cuda")
+    if layout == "stride":
+        out_len = eng.pack(d_tmpl, crc, d_desc, n, d_pool, slab, stride=512, opts=PACK_CHECKSUM)
+    else:
+        out_len = eng.pack(d_tmpl, crc, d_desc, n, d_pool, slab,
+                           rec_off=to_device(offs).view(torch.int64), opts=PACK_CHECKSUM)
+    torch.cuda.synchronize()
+    assert np.array_equal(out_len.cpu().numpy().view(np.uint32), wlen)
+    got = slab.cpu().numpy()
+    end = int(offs[-1] + sizes[-1])
+    assert np.array_equal(got[:end], want[:end])
+    assert np.all(got[end:] == 0xA5)
