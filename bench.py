@@ -248,8 +248,11 @@ def extra_config5(torch, eng, dev, world=1, rank=0, dist=None):
         def scan():
             state["r"] = scan_sharded(scanner, comm, local, total_bytes, SCAN_TCP)
     else:
+        scan_out = (torch.empty(n + 1, dtype=torch.int64, device=dev),
+                    torch.empty(n + 1, dtype=torch.int32, device=dev))
+
         def scan():
-            offs, lens, info = eng.stream_scan(local, SCAN_TCP, cap=n + 1)
+            offs, lens, info = eng.stream_scan(local, SCAN_TCP, out=scan_out)
             state["r"] = (offs, lens, (int(info.n_records), int(info.consumed),
                                        int(info.status)))
     scan()

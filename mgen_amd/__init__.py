@@ -352,15 +352,23 @@ class Engine:
                                           _stream(self.device))
         self._check(rc, "mgenx_diag_group_rw")
 
-    def stream_scan(self, data, mode=SCAN_TCP, cap=None, nbytes=None):
+    def stream_scan(self, data, mode=SCAN_TCP, cap=None, nbytes=None, out=None):
         """TCP / SINK record framing of a device byte stream (mgenx_stream_scan).  Returns
-        (rec_off int64 tensor, rec_len int32 tensor, ScanInfo); synchronous."""
+        (rec_off int64 tensor, rec_len int32 tensor, ScanInfo); synchronous.  out: optional
+        preallocated (rec_off int64, rec_len int32) tensors of equal length (the capacity)."""
         torch = self.torch
         nbytes = data.numel() if nbytes is None else nbytes
-        if cap is None:
-            cap = nbytes // 4 + 1
-        offs = torch.empty(cap, dtype=torch.int64, device=data.device)
-        lens = torch.empty(cap, dtype=torch.int32, device=data.device)
+        if out is not None:
+            offs, lens = out
+            if offs.dtype != torch.int64 or lens.dtype != torch.int32 or \
+                    offs.numel() != lens.numel():
+                raise ValueError("stream_scan out: (int64, int32) tensors of one length")
+            cap = offs.numel()
+        else:
+            if cap is None:
+                cap = nbytes // 4 + 1
+            offs = torch.empty(cap, dtype=torch.int64, device=data.device)
+            lens = torch.empty(cap, dtype=torch.int32, device=data.device)
         info = ScanInfo()
         rc = self.lib.mgenx_stream_scan(self.ctx, _ptr(data), nbytes, mode, _ptr(offs),
                                         _ptr(lens), cap, ctypes.byref(info),

@@ -145,6 +145,13 @@ def test_config5_stream_scan_then_unpack(torch, eng, gold):
     torch.cuda.synchronize()
     assert int((cols["err"] != 0).sum()) == 0
     assert np.array_equal(cols["seq_num"].cpu().numpy().view(np.uint32), np.arange(n))
+    # the same scan into caller-preallocated outputs, twice (speculative tables reused)
+    out = (torch.full((n + 8,), -1, dtype=torch.int64, device="cuda"),
+           torch.full((n + 8,), -1, dtype=torch.int32, device="cuda"))
+    for _ in range(2):
+        o2, l2, i2 = eng.stream_scan(d, SCAN_TCP, out=out)
+        assert int(i2.n_records) == n and int(i2.consumed) == len(s)
+        assert torch.equal(o2, offs) and torch.equal(l2, lens)
 
 
 # ---- sharded framing (mgenx_stream_scan_exits / _range, mgen_amd/shard.py) ----
