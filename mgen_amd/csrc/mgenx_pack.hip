@@ -4,7 +4,9 @@
 // = SetFlag(LAST_BUFFER); Pack(buf, msg_len, checksum_enable, tx_checksum)
 //   (src/common/mgenMsg.cpp:83-313); WriteChecksum if the CHECKSUM flag is set (:502-522).
 //
-// Two phases per wave of 64 records:
+// Two phases per batch of 64 records, run by different waves of a workgroup (meta waves
+// build a group of batches into one LDS buffer while store waves write the previous group
+// from the other, see pack_kernel):
 //   1. meta (lane = record): build the header image (plus the first payload bytes) in LDS,
 //      walk Pack's truncation rules, and compute the CRC-32 algebraically:
 //         crc_raw(H || P || F) = A_|P|+|F|(crc_raw(H)) ^ A_|F|(crc_raw(P)) ^ crc_raw(F)
@@ -12,8 +14,10 @@
 //      crc_raw(random fill prefix) from a per-fill_time table, A_n(x) = x * x^(8n) mod P.
 //      Only the <= 76 header bytes are fed through tables, four at a time:
 //      c <- A_4(c ^ word) (the <= 3 trailing bytes through the byte table).
-//   2. write (lane = 16-byte unit): the wave's records are cut into 16-byte units; every
-//      lane composes one unit from fill / header image / payload / trailer and stores it.
+//   2. write (lane = 16-byte unit): the batch's records are cut into 16-byte units; every
+//      lane composes one unit from fill / header image / payload / trailer and stores it
+//      (fast forms: aligned stride slots composed once; back-to-back records as an aligned
+//      zero fill with the head/tail units written over it in slab-order windows).
 #include "mgenx_kernels.hpp"
 
 namespace mgenx {
