@@ -878,7 +878,7 @@ unpack_kernel(UnpackParams p) {
 // are those of unpack_kernel<true>; what differs is the schedule:
 //   * each wave takes tiles of 64 consecutive records, ranks them by row count R (64 lane
 //     compares) and runs them as four groups of 16 records of similar length;
-//   * a group's virtual rows are V = max R of its records rounded up to a multiple of 4
+//   * a group's virtual rows are V = max R of its records rounded up to an even count >= 4
 //     (shorter records front-padded with zero rows, which leave the zero CRC state as is);
 //   * the wave's rows form ONE stream over its groups, with RS = 4 rows in flight: row
 //     r + 4 of the stream is loaded as row r is consumed -- during a group's last four rows
@@ -947,7 +947,7 @@ unpack_var_kernel(UnpackParams p) {
     uint32_t idx, L;
     int pos0, pad;        // row 0 position in the record (+16q), virtual rows before row 0
     bool valid, live, oob;
-    uint32_t V;           // virtual rows (wave-uniform, multiple of 4, >= 4)
+    uint32_t V;           // virtual rows (wave-uniform, even, >= 4)
   };
   auto make = [&](uint64_t t, int k, uint64_t offs, uint32_t lens, int src) {
     Grp g;
@@ -964,7 +964,7 @@ unpack_var_kernel(UnpackParams p) {
     int m = R;
 #pragma unroll
     for (int sft = 1; sft < 64; sft <<= 1) m = max(m, __shfl_xor(m, sft));
-    g.V = (uint32_t)max(4, (__builtin_amdgcn_readfirstlane(m) + 3) & ~3);
+    g.V = (uint32_t)max(4, (__builtin_amdgcn_readfirstlane(m) + 1) & ~1);
     g.pad = (int)g.V - R;
     g.pos0 = (int)g.L - 64 * R + 16 * q;
     return g;
@@ -991,6 +991,7 @@ unpack_var_kernel(UnpackParams p) {
 
   // ---- the first group ----
   int k = 0;
+  int rho = 0;  // ring slot of the current group's row 0
   Grp G = make(t_c, 0, off_c, len_c, src_c);
   u32x4_t d[4];
 #pragma unroll
@@ -1028,40 +1029,64 @@ unpack_var_kernel(UnpackParams p) {
 #pragma unroll
       for (int b = 0; b < 4; b++) a64_parts(ldsb, c4[b], s1, ha[b], hb[b]);
     };
-    const int C = (int)(G.V >> 2);
-#pragma unroll 1
-    for (int c = 0; c + 1 < C; c++) {
+    // G's row r sits in ring slot (r + rho) & 3 (rho in {0, 2}: V is even, not necessarily a
+    // multiple of 4, so a group may start mid-ring); each variant keeps every slot index
+    // static (a register copy of an in-flight row would make LLVM drain the ring)
+    auto tail = [&](auto RT, int jl) {  // the last 4 rows, reloading N's rows 0..3
+      constexpr int T = decltype(RT)::value;
 #pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const u32x4_t y = row_data(G, d[j], 4 * c + j);
+      for (int j = 0; j < 3; j++) {
+        const u32x4_t y = row_data(G, d[(j + T) & 3], jl + j);
         __builtin_amdgcn_sched_barrier(0);
-        d[j] = ldu128(row_ptr(G, 4 * c + 4 + j));
+        d[(j + T) & 3] = ldu128(row_ptr(N, j));
         __builtin_amdgcn_sched_barrier(0);
         consume(y);
       }
-    }
-    const int jl = 4 * (C - 1);
+      u32x4_t xf = row_data(G, d[(3 + T) & 3], jl + 3);
+      __builtin_amdgcn_sched_barrier(0);
+      d[(3 + T) & 3] = ldu128(row_ptr(N, 3));
+      __builtin_amdgcn_sched_barrier(0);
+      if (q == 3) xf.w = bswap32(xf.w);  // the big-endian trailer, in stream order
+      const uint32_t v = shift_tab(fold + 3 * 1024, xor3(ha[0], hb[0], xf.x)) ^
+                         shift_tab(fold + 2 * 1024, xor3(ha[1], hb[1], xf.y)) ^
+                         shift_tab(fold + 1 * 1024, xor3(ha[2], hb[2], xf.z)) ^
+                         shift_tab(fold, xor3(ha[3], hb[3], xf.w));
+      const uint32_t* lt = fold + (q == 0 ? 5 : (q == 1 ? 4 : 3)) * 1024;  // A48/A32/A16
+      uint32_t t = (q == 3) ? v : shift_tab(lt, v);
+      t ^= __shfl_xor(t, 1);
+      t ^= __shfl_xor(t, 2);
+      return t;
+    };
+    auto run = [&](auto RHO) {
+      constexpr int R0 = decltype(RHO)::value;
+      const int nc = (int)((G.V - 4) >> 2);  // whole chunks before the tail
+#pragma unroll 1
+      for (int c = 0; c < nc; c++) {
 #pragma unroll
-    for (int j = 0; j < 3; j++) {
-      const u32x4_t y = row_data(G, d[j], jl + j);
-      __builtin_amdgcn_sched_barrier(0);
-      d[j] = ldu128(row_ptr(N, j));
-      __builtin_amdgcn_sched_barrier(0);
-      consume(y);
-    }
-    u32x4_t xf = row_data(G, d[3], jl + 3);
-    __builtin_amdgcn_sched_barrier(0);
-    d[3] = ldu128(row_ptr(N, 3));
-    __builtin_amdgcn_sched_barrier(0);
-    if (q == 3) xf.w = bswap32(xf.w);  // the big-endian trailer, in stream order
-    const uint32_t v = shift_tab(fold + 3 * 1024, xor3(ha[0], hb[0], xf.x)) ^
-                       shift_tab(fold + 2 * 1024, xor3(ha[1], hb[1], xf.y)) ^
-                       shift_tab(fold + 1 * 1024, xor3(ha[2], hb[2], xf.z)) ^
-                       shift_tab(fold, xor3(ha[3], hb[3], xf.w));
-    const uint32_t* lt = fold + (q == 0 ? 5 : (q == 1 ? 4 : 3)) * 1024;  // A48/A32/A16
-    uint32_t tot = (q == 3) ? v : shift_tab(lt, v);
-    tot ^= __shfl_xor(tot, 1);
-    tot ^= __shfl_xor(tot, 2);
+        for (int j = 0; j < 4; j++) {
+          const u32x4_t y = row_data(G, d[(j + R0) & 3], 4 * c + j);
+          __builtin_amdgcn_sched_barrier(0);
+          d[(j + R0) & 3] = ldu128(row_ptr(G, 4 * c + 4 + j));
+          __builtin_amdgcn_sched_barrier(0);
+          consume(y);
+        }
+      }
+      const int r0 = 4 * nc;
+      if (G.V & 2u) {  // two rows more, then the tail two slots further round the ring
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+          const u32x4_t y = row_data(G, d[(j + R0) & 3], r0 + j);
+          __builtin_amdgcn_sched_barrier(0);
+          d[(j + R0) & 3] = ldu128(row_ptr(G, r0 + 4 + j));
+          __builtin_amdgcn_sched_barrier(0);
+          consume(y);
+        }
+        return tail(std::integral_constant<int, R0 ^ 2>{}, r0 + 2);
+      }
+      return tail(std::integral_constant<int, R0>{}, r0);
+    };
+    uint32_t tot = rho ? run(std::integral_constant<int, 2>{}) : run(std::integral_constant<int, 0>{});
+    rho = (rho + (int)G.V) & 3;
 
     // ---- G's columns (as unpack_kernel) ----
     {
