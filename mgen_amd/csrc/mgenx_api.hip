@@ -444,7 +444,8 @@ static int pack_common(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
   p.state = dev_state;
   const uint64_t batches = ((uint64_t)n + 63) / 64;
   uint64_t grid = (batches + 3) / 4;                // groups of 4 batches (kProd)
-  const uint64_t cap = (uint64_t)ctx->cu_count * 2;  // 76 KB of LDS per workgroup
+  uint64_t cap = (uint64_t)ctx->cu_count * 2;  // 76 KB of LDS per workgroup
+  if (MGENX_DIAG && ctx->pack_variant >= 7) cap *= (uint64_t)(ctx->pack_variant - 5);  // (diag)
   if (grid > cap) grid = cap;
   hipError_t e = mgenx::launch_pack(p, (int)grid, (hipStream_t)stream);
   return e == hipSuccess ? MGENX_OK : set_err(ctx, e, "pack");
@@ -617,7 +618,7 @@ int mgenx_ctx_device(const mgenx_ctx* ctx) { return ctx ? ctx->device : -1; }
 int mgenx_set_tuning(mgenx_ctx* ctx, int key, int value) {
   if (!ctx) return MGENX_EINVAL;
   if (key == MGENX_TUNE_PACK_VARIANT) {
-    if (value < 0 || value > 6) return MGENX_EINVAL;
+    if (value < 0 || value > 9) return MGENX_EINVAL;
     ctx->pack_variant = value;
     return MGENX_OK;
   }

@@ -308,7 +308,7 @@ pack_kernel(PackParams p) {
     // time: the lines have left L2 by then and come back as partial writes).
     const bool stride_ok = !has || (m.ret == (uint32_t)p.stride && m.pend <= (uint32_t)kImg);
     if (!p.rec_off && !rf && (p.stride & 15u) == 0 && p.stride >= 32 && nv > 0 &&
-        variant == 0 && __all(stride_ok)) {
+        (variant == 0 || variant >= 7) && __all(stride_ok)) {
       const uint32_t U = (uint32_t)(p.stride >> 4);        // units per record
       const uint32_t q = 64u / U, rm = 64u % U;            // unit step = q records + rm units
       uint32_t r = (uint32_t)lane / U, pu = (uint32_t)lane % U;
@@ -346,7 +346,7 @@ pack_kernel(PackParams p) {
                       __all(packed_ok);
     const uint32_t kimg = (min(m.pend, m.ret) + 15u) >> 4;  // image units
     uint32_t units = (m.ret + 15u) >> 4;
-    if (fast && (variant == 0 || variant == 6)) {
+    if (fast && (variant == 0 || variant >= 6)) {
       // The wave's range is zero-filled with aligned full-width stores, and each record's
       // special units -- its image units and its last 16 bytes (trailer), record-relative
       // and unaligned -- are stored over the fill in windows of 64 (one per lane, in slab

@@ -44,7 +44,7 @@ ms = timed(lambda: eng.pack(dt, crc, dd, n, dp, slab, rec_off=do, opts=PACK_CHEC
 print(f"config3 pack_ms {ms:.4f} GB/s {(n * 36 + total) / ms / 1e6:.1f}")
 if len(sys.argv) > 1:
     d = Engine(0, diag=True)
-    for v in [0, 1, 3, 4, 5, 6]:
+    for v in [0, 1, 3, 4, 5, 6, 7, 8, 9]:
         d.set_pack_variant(v)
         tmpl, pool, desc = udp_fixed(n, 1024)
         dt, dp, dd = to_device(tmpl), to_device(pool), to_device(desc)
@@ -61,7 +61,7 @@ if len(sys.argv) > 1:
     crc = torch.empty(len(tmpl), dtype=torch.int32, device=dev)
     d.pack_prepare(dt, len(tmpl), dp, crc)
     slab3 = torch.empty(total + 64, dtype=torch.uint8, device=dev)
-    for v in [0, 1, 3, 4, 5, 6]:
+    for v in [0, 1, 3, 4, 5, 6, 7, 8, 9]:
         d.set_pack_variant(v)
         ms = timed(lambda: d.pack(dt, crc, dd, n, dp, slab3, rec_off=do, opts=PACK_CHECKSUM, out_len=ol))
         print(f"variant {v} config3 pack_ms {ms:.4f}")
