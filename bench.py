@@ -421,10 +421,18 @@ def main():
     ap.add_argument("--no-extras", action="store_true")
     args = ap.parse_args()
 
+    from mgen_amd import launch
+    if launch.needs_launch(args.gpus):
+        # `python bench.py --gpus N` outside torch.distributed.run: start the N ranks as a
+        # child launcher before anything touches the GPU; rank 0 prints the line
+        sys.exit(launch.relaunch(__file__, sys.argv[1:], args.gpus))
+
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus and "WORLD_SIZE" in os.environ:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:

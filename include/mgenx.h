@@ -158,6 +158,18 @@ int mgenx_unpack_batch(mgenx_ctx* ctx, const uint8_t* dev_slab, uint64_t slab_by
                        const uint32_t* dev_rec_len, uint32_t fixed_len, uint32_t n,
                        const mgenx_cols* cols, uint32_t opts, void* stream);
 
+/* Which kernel the last mgenx_unpack_batch on this context launched (host-side record of
+ * the dispatch; a test and profiling aid -- the choice follows the layout, the options and
+ * the batch size, never the data).  0 before the first call. */
+#define MGENX_UNPACK_K_HEADER     1  /* MGENX_OPT_SKIP_CRC: header-only decode */
+#define MGENX_UNPACK_K_GENERAL    2  /* any layout, one group of 16 records per wave */
+#define MGENX_UNPACK_K_VAR        3  /* per-record lengths, >= 2 tiles of 64 records per
+                                        wave: length-ranked groups, load ring (config 3) */
+#define MGENX_UNPACK_K_FIXED      4  /* fixed stride, one length in [65, 1024] */
+#define MGENX_UNPACK_K_FIXED_RING 5  /* fixed 512 / 1024-B records into rows (config 2) */
+#define MGENX_UNPACK_K_OTHER      6  /* a diagnostics-build ablation */
+int mgenx_unpack_last_kernel(const mgenx_ctx* ctx);
+
 /* ------------------------------------------------------------------ */
 /* Pack.  A per-flow template table holds what MgenFlow::SendMessage    */
 /* takes from flow state (mgenFlow.cpp:946-983, 1039-1129); a 20-byte   */

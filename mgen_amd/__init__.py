@@ -21,6 +21,8 @@ from ._abi import (  # noqa: F401
     RX_STATE_DTYPE, SCAN_HALO, SCAN_REUSE, ADDR_DTYPE, REPORT_KEY_DTYPE, DATA_CONTROLLER,
     PcapInfo, TextSrc, TEXT_PER_RECORD, TEXT_OWNER, TEXT_MAP, TEXT_SCATTER, PCAP_NSEC, PCAP_SWAPPED, LOG_EPOCH, LOG_NO_DATA, LOG_NO_GPS,
     LOG_SKIP_ERR, FLOW_NONE, DLT_EN10MB, DLT_LINUX_SLL, BinlogInfo, BINLOG_NO_RX, BINLOG_FLUSH,
+    UNPACK_K_HEADER, UNPACK_K_GENERAL, UNPACK_K_VAR, UNPACK_K_FIXED, UNPACK_K_FIXED_RING,
+    UNPACK_K_OTHER,
 )
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -40,6 +42,7 @@ EXPORTED_SYMBOLS = (
     "mgenx_flow_table_create", "mgenx_flow_table_destroy", "mgenx_flow_lookup",
     "mgenx_flow_reduce_ex", "mgenx_flow_keys", "mgenx_text_interleave", "mgenx_pcap_index",
     "mgenx_pcap_parse", "mgenx_binlog_index", "mgenx_convert_binary_log",
+    "mgenx_unpack_last_kernel",
 )
 DIAG_SYMBOLS = ("mgenx_set_tuning", "mgenx_diag_stream_read", "mgenx_diag_group_rw")
 
@@ -69,6 +72,8 @@ def load(diag: bool = False):
     L.mgenx_last_error.restype = ctypes.c_char_p
     L.mgenx_unpack_batch.argtypes = [P, P, u64, P, u64, P, u32, u32,
                                      ctypes.POINTER(MgenxCols), u32, P]
+    L.mgenx_unpack_last_kernel.argtypes = [P]
+    L.mgenx_unpack_last_kernel.restype = i32
     L.mgenx_pack_prepare.argtypes = [P, P, u32, P, P, P]
     L.mgenx_set_fill_time.argtypes = [P, u32]
     L.mgenx_pack_batch.argtypes = [P, P, P, P, u32, P, P, u64, P, u64, P, u32, u32, P]
@@ -197,6 +202,10 @@ class Engine:
                                          _stream(self.device))
         self._check(rc, "mgenx_unpack_batch")
         return cols
+
+    def last_unpack_kernel(self):
+        """UNPACK_K_* of the kernel the last unpack() launched (mgenx_unpack_last_kernel)."""
+        return int(self.lib.mgenx_unpack_last_kernel(self.ctx))
 
     def rx_state_init(self):
         """mgenx_rx_state of a fresh MgenMsg (GPS words 10800000 = 0 degrees), on the device."""

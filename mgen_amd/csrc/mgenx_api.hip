@@ -148,6 +148,7 @@ struct mgenx_ctx {
   size_t rx_ws_bytes = 0;
   uint64_t* tcp_host_dev = nullptr;
   int unpack_variant = 0;          // diagnostic kernel ablation (mgenx_set_tuning)
+  int unpack_last = 0;             // MGENX_UNPACK_K_* of the last mgenx_unpack_batch
   int pack_variant = 0;
   mgenx_grow bl[5];                // mgenx_convert_binary_log: records, lines, pairs, report text
   bool rand_ready = false;
@@ -372,9 +373,11 @@ int mgenx_unpack_batch(mgenx_ctx* ctx, const uint8_t* dev_slab, uint64_t slab_by
   const uint64_t per_block = (uint64_t)mgenx::unpack_threads() / 64;  // waves per block
   uint64_t grid = (groups + per_block - 1) / per_block;
   if (grid > (uint64_t)ctx->cu_count) grid = ctx->cu_count;
-  hipError_t e = mgenx::launch_unpack(p, (int)grid, (hipStream_t)stream);
+  hipError_t e = mgenx::launch_unpack(p, (int)grid, (hipStream_t)stream, &ctx->unpack_last);
   return e == hipSuccess ? MGENX_OK : set_err(ctx, e, "unpack");
 }
+
+int mgenx_unpack_last_kernel(const mgenx_ctx* ctx) { return ctx ? ctx->unpack_last : 0; }
 
 int mgenx_pack_prepare(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl, uint32_t n_tmpl,
                        const uint8_t* dev_pool, uint32_t* dev_tmpl_crc, void* stream) {

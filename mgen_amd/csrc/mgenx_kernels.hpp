@@ -51,7 +51,7 @@ struct PackParams {
   int variant;               // diagnostic ablation (0 = product path)
 };
 
-hipError_t launch_unpack(const UnpackParams& p, int grid, hipStream_t stream);
+hipError_t launch_unpack(const UnpackParams& p, int grid, hipStream_t stream, int* which);
 // tuning knob (mgenx_set_tuning): 0 = auto (pipelined fixed-length kernel when the batch
 // qualifies), 1/2 = ablations of the general kernel, 3 = general kernel only
 int unpack_threads();

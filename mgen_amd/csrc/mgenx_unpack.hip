@@ -1831,9 +1831,11 @@ static const fixed_launcher kFixedLaunch[17] = MGENX_FIXED_TABLE(false);
 static const fixed_launcher kFixedLaunchRows[17] = MGENX_FIXED_TABLE(true);
 #undef MGENX_FIXED_TABLE
 
-hipError_t launch_unpack(const UnpackParams& p, int grid, hipStream_t stream) {
+hipError_t launch_unpack(const UnpackParams& p, int grid, hipStream_t stream, int* which) {
   const int unpack_variant = p.variant;
+  *which = MGENX_UNPACK_K_OTHER;
   if (p.opts & MGENX_OPT_SKIP_CRC) {
+    *which = MGENX_UNPACK_K_HEADER;
     hipLaunchKernelGGL((unpack_kernel<false>), dim3(grid), dim3(kUnpackThreads), 0, stream, p);
     return hipGetLastError();
   }
@@ -1848,6 +1850,8 @@ hipError_t launch_unpack(const UnpackParams& p, int grid, hipStream_t stream) {
                      p.slab_bytes >= p.fixed_len;
   if (unpack_variant == 0 && fixed) {
     // 256 / 512 / 1024-byte records: the aligned variant (header = row 0)
+    *which = (c.rows && (p.fixed_len == 512 || p.fixed_len == 1024)) ? MGENX_UNPACK_K_FIXED_RING
+                                                                    : MGENX_UNPACK_K_FIXED;
     switch (p.fixed_len) {
       case 256: return c.rows ? launch_fixed<4, 0, true, true>(p, grid, stream)
                               : launch_fixed<4, 0, false, true>(p, grid, stream);
@@ -1901,7 +1905,11 @@ hipError_t launch_unpack(const UnpackParams& p, int grid, hipStream_t stream) {
   // its 14-row load blocks, which keep more bytes in flight per record
   const uint64_t tiles = ((uint64_t)p.n + 63) / 64;
   const uint64_t waves = (uint64_t)grid * (kUnpackThreads / 64);
-  if (p.rec_len && tiles >= 2 * waves) return launch_var(p, grid, stream);
+  if (p.rec_len && tiles >= 2 * waves) {
+    *which = MGENX_UNPACK_K_VAR;
+    return launch_var(p, grid, stream);
+  }
+  *which = MGENX_UNPACK_K_GENERAL;
   return launch_mode<0>(p, grid, stream);
 }
 
