@@ -13,7 +13,8 @@ DOBJ := $(addprefix build/diag/,$(addsuffix .o,$(NAMES)))
 LIBS := -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 all: mgen_amd/libmgenx.so mgen_amd/libmgenx_diag.so oracle tests/cpp/host_roundtrip \
-     tests/cpp/loopback tests/cpp/compat_shapes tools/pcap2mgen
+     tests/cpp/loopback tests/cpp/compat_shapes tests/cpp/compat_shapes_pl tests/cpp/shim_latency \
+     tools/pcap2mgen
 
 build/product/%.o: mgen_amd/csrc/%.hip $(HDR)
 	@mkdir -p build/product
@@ -44,9 +45,22 @@ tests/cpp/loopback: tests/cpp/loopback.cpp include/mgenx.hpp include/mgenx_io.hp
 	    $(HOSTLD)
 
 # the reference's own call shapes compiled against the MgenMsg/MgenPayload/MgenAnalytic shim
-tests/cpp/compat_shapes: tests/cpp/compat_shapes.cpp $(wildcard include/mgenx_compat/*.h) \
-		include/mgenx.h mgen_amd/libmgenx.so
-	$(HOSTCXX) -Iinclude/mgenx_compat $< -o $@ $(HOSTLD)
+COMPAT := $(wildcard include/mgenx_compat/*.h include/mgenx_compat/*.hpp) \
+          include/mgenx_compat/mgenx_compat.cpp
+tests/cpp/compat_shapes: tests/cpp/compat_shapes.cpp $(COMPAT) include/mgenx.h mgen_amd/libmgenx.so
+	$(HOSTCXX) -Iinclude/mgenx_compat $< include/mgenx_compat/mgenx_compat.cpp -o $@ $(HOSTLD)
+
+# per-call latency of the shim's single-message calls (batches of one) and batch forms
+tests/cpp/shim_latency: tests/cpp/shim_latency.cpp $(COMPAT) include/mgenx.h mgen_amd/libmgenx.so
+	$(HOSTCXX) -Iinclude/mgenx_compat $< include/mgenx_compat/mgenx_compat.cpp -o $@ $(HOSTLD)
+
+# the same program through the shim's MGENX_WITH_PROTOLIB branch (what an MGEN build compiles),
+# against protolib / Mgen-shaped test headers (tests/cpp/protolib_shape)
+PLSHAPE := $(wildcard tests/cpp/protolib_shape/*)
+tests/cpp/compat_shapes_pl: tests/cpp/compat_shapes.cpp $(COMPAT) $(PLSHAPE) include/mgenx.h \
+		mgen_amd/libmgenx.so
+	$(HOSTCXX) -DMGENX_WITH_PROTOLIB -Iinclude/mgenx_compat -Itests/cpp/protolib_shape $< \
+	    include/mgenx_compat/mgenx_compat.cpp tests/cpp/protolib_shape/mgen_shape.cpp -o $@ $(HOSTLD)
 
 # the reference's pcap2mgen command line over mgenx::Pcap2Mgen (include/mgenx_pcap.hpp)
 tools/pcap2mgen: tools/pcap2mgen.cpp include/mgenx_pcap.hpp include/mgenx.hpp include/mgenx.h \

@@ -67,6 +67,8 @@ extern "C" {
 #define MGENX_ERROR_LENGTH    3
 #define MGENX_ERROR_DSTADDR   4
 #define MGENX_ERROR_OOB       0x80  /* record lies outside the slab: not touched */
+#define MGENX_ERROR_RERR_NONE 0x40  /* log formatters only: a RERR event of a message whose
+                                       error is ERROR_NONE ("type>none", mgenMsg.cpp:716) */
 
 /* ---- unpack options ---- */
 #define MGENX_OPT_CHECKSUM_FORCE  0x1  /* Mgen checksum_force (mgen.cpp:2076-2087) */
@@ -644,6 +646,10 @@ int mgenx_text_interleave(mgenx_ctx* ctx, const mgenx_text_src* srcs, uint32_t n
 #define MGENX_PCAP_TRUNCATED 5  /* UDP payload past the captured bytes: skipped (the
                                    reference reads stale buffer bytes there) */
 #define MGENX_PCAP_OOB       6  /* record past the buffer */
+#define MGENX_PCAP_SNAPPED   7  /* a UDP datagram cut by the capture's snapshot length whose
+                                   UDP header and >= MIN_SIZE payload bytes were captured:
+                                   mgenx_pcap_snap moves it into scratch, zero-extended to the
+                                   UDP length (then MGENX_PCAP_UDP); left alone it is skipped */
 typedef struct {
     uint32_t link_type;   /* DLT_* */
     uint32_t flags;       /* MGENX_PCAP_NSEC | MGENX_PCAP_SWAPPED */
@@ -651,6 +657,8 @@ typedef struct {
     uint32_t rsv;
     uint64_t n_records;   /* records found (only the first cap offsets are written) */
     uint64_t consumed;    /* bytes of whole records, file header included */
+    uint64_t snap_bytes;  /* scratch mgenx_pcap_snap may need: sum over records captured
+                             short of their wire length of that length, 16-byte rounded */
 } mgenx_pcap_info;
 int mgenx_pcap_index(const uint8_t* buf, uint64_t nbytes, uint64_t* pkt_off, uint64_t cap,
                      mgenx_pcap_info* info);
@@ -659,6 +667,16 @@ int mgenx_pcap_parse(mgenx_ctx* ctx, const uint8_t* dev_buf, uint64_t buf_bytes,
                      uint32_t flags, uint64_t* dev_udp_off, uint32_t* dev_udp_len,
                      mgenx_addr* dev_src, int32_t* dev_ttl, uint32_t* dev_rx_sec,
                      uint32_t* dev_rx_usec, uint8_t* dev_status, void* stream);
+/* A capture taken with a snapshot length (tcpdump -s N) cuts datagrams short; the reference
+ * parses such a frame by its wire length and Unpacks the UDP payload from its parse buffer,
+ * so the MGEN header comes from the captured bytes and the rest of the buffer is stale.
+ * mgenx_pcap_snap copies every MGENX_PCAP_SNAPPED packet's captured UDP payload into
+ * dev_buf[file_bytes, buf_bytes) (scratch after the file image; info.snap_bytes is enough)
+ * zero-extended to its UDP length, points dev_udp_off / dev_udp_len there and sets its
+ * status to MGENX_PCAP_UDP; a packet that does not fit stays SNAPPED.  Asynchronous. */
+int mgenx_pcap_snap(mgenx_ctx* ctx, uint8_t* dev_buf, uint64_t file_bytes, uint64_t buf_bytes,
+                    const uint64_t* dev_pkt_off, uint32_t n, uint32_t flags, uint8_t* dev_status,
+                    uint64_t* dev_udp_off, uint32_t* dev_udp_len, void* stream);
 
 /* ---- MgenMsg::ConvertBinaryLog: binary log -> text log (src/common/mgenMsg.cpp:1417-1900) --
  * mgenx_binlog_index (HOST memory, no device work) checks the header line ("mgen
@@ -667,14 +685,18 @@ int mgenx_pcap_parse(mgenx_ctx* ctx, const uint8_t* dev_buf, uint64_t buf_bytes,
  * converts go to rec_off (host memory), up to the first one it stops at -- info->status:
  * MGENX_BINLOG_OK (end of file), _HEADER (not a binary log), _TOO_LONG (recordLength > 1024),
  * _EVENT (RERR or an unknown event type, or an unknown address type: the reference returns
- * false there, :1586-1590, 1892-1895), _SHORT (the file ends inside a record).
+ * false there, :1586-1590, 1892-1895), _SHORT (the file ends inside a record, or a record is
+ * too short for the fields its type reads -- the event time; RECV 12 + source length; LISTEN
+ * / IGNORE 12; JOIN / LEAVE 13 + group length + name length; ON ... RECONNECT 18 + address
+ * length -- which mgen never writes and the reference would parse from stale buffer bytes).
  * mgenx_convert_binary_log (device) writes the text the reference writes for those records,
  * in order: RECV (Unpack of the stored message + LogRecvEvent text with the source and event
  * time, the converter's argument order at :1607 putting log_flush in the ttl slot, then the
  * REPORT lines of MGEN_DATA items), SEND (Unpack + LogSendEvent text: tx time, srcPort 0),
  * LISTEN / IGNORE / JOIN / LEAVE / START / STOP / ON / ACCEPT / CONNECT / DISCONNECT / OFF /
  * SHUTDOWN / RECONNECT lines (:1628-1891).  A RECV / SEND record whose stored message Unpack
- * rejects (mgen never writes one) gives no line.  flags: MGENX_BINLOG_NO_RX (log_rx off),
+ * rejects (mgen never writes one) is logged all the same, as the reference ignores Unpack's
+ * result: the fields a fresh MgenMsg keeps, RECV's tx time = the event time.  flags: MGENX_BINLOG_NO_RX (log_rx off),
  * MGENX_BINLOG_FLUSH (log_flush on); opts: MGENX_LOG_EPOCH / _NO_DATA / _NO_GPS.
  * dev_rec_pos[n + 1] = byte offsets of each record's text; dev_text is written only when the
  * total fits text_cap.  Synchronous (intermediate sizes are read back); the context keeps a

@@ -70,6 +70,9 @@ class MgenAnalytic {
     double GetLatencyMax() const { return GetLatencyAve() + UnquantizeTimeValue(GetUINT8(OffsetLatencyMax())); }
     double GetRateAve() const { return UnquantizeRate(GetUINT16(OffsetRateAve())); }
     double GetLossFraction() const { return UnquantizeLoss(GetUINT16(OffsetLossFraction())); }
+    // the received-report REPORT line (mgenAnalytic.cpp:747-786; mgenx_compat.cpp)
+    void Log(FILE* filePtr, const ProtoTime& sentTime, const ProtoTime& theTime, bool localTime,
+             const ProtoAddress& reporterAddr) const;
 
     // mgenAnalytic.cpp:446-475
     bool InitIntoBuffer(ReportType reportType, UINT32* bufferPtr = nullptr,
@@ -277,10 +280,10 @@ class MgenAnalytic {
     bool* upd = updated;
     for (unsigned i = 0; i < n; i++) {
       slot[i] = items[i]->slot_;
-      rxs[i] = (uint32_t)rxTime[i].sec();
-      rxu[i] = (uint32_t)rxTime[i].usec();
-      txs[i] = (uint32_t)txTime[i].sec();
-      txu[i] = (uint32_t)txTime[i].usec();
+      rxs[i] = (uint32_t)rxTime[i].GetTimeVal().tv_sec;
+      rxu[i] = (uint32_t)rxTime[i].GetTimeVal().tv_usec;
+      txs[i] = (uint32_t)txTime[i].GetTimeVal().tv_sec;
+      txu[i] = (uint32_t)txTime[i].GetTimeVal().tv_usec;
       len[i] = (uint16_t)msgSize[i];
       seq[i] = seqNum[i];
     }
@@ -294,8 +297,14 @@ class MgenAnalytic {
       if (updated[i]) items[i]->TakeReport(rep[i]);
   }
 
+  // the REPORT line of the last closed window (mgenAnalytic.cpp:260-295; mgenx_compat.cpp)
+  void Log(FILE* filePtr, const ProtoTime& sentTime, const ProtoTime& theTime,
+           bool localTime) const;
+  // the current window's end (include/mgenAnalytic.h:105-106): read from the device state
+  const ProtoTime& GetWindowEnd() const;
+
   const Report& GetReport(const ProtoTime& theTime) {
-    double windowOffset = (theTime.GetValue() - report_start.GetValue()) - report_duration;
+    double windowOffset = (Seconds(theTime) - Seconds(report_start)) - report_duration;
     if (windowOffset < 0.0) windowOffset = 0.0;
     report_msg.SetWindowOffset(windowOffset);
     report_time = theTime;
@@ -330,6 +339,9 @@ class MgenAnalytic {
 
  private:
   static constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
+  static double Seconds(const ProtoTime& t) {  // ProtoTime::GetValue
+    return (double)t.GetTimeVal().tv_sec + 1.0e-06 * (double)t.GetTimeVal().tv_usec;
+  }
   void ClearReport() {
     report_duration = report_rate_ave = report_loss_ave = 0.0;
     report_latency_ave = report_latency_min = report_latency_max = 0.0;
@@ -367,6 +379,7 @@ class MgenAnalytic {
   double report_rate_ave, report_loss_ave;
   double report_latency_ave, report_latency_min, report_latency_max;
   ProtoTime report_time;
+  mutable ProtoTime window_end_;
   UINT32 report_buffer[Report::MAX_LENGTH / sizeof(UINT32)];
   Report report_msg;
 };

@@ -18,9 +18,11 @@
 // MGENX_DEC_* mask) and leaves msg_error alone on success.  One documented difference:
 // a Pack that returns 0 writes no bytes (the reference leaves a partial header behind).
 //
-// The logging members (LogRecvEvent ... ConvertBinaryLog, mgenMsg.cpp:646-1900) are
-// declared with the reference's signatures and defined by the reference's own logging code
-// (or by libmgenx's log formatter for batches: mgenx_log_recv_text/_binary).
+// The logging members (LogRecvEvent ... ConvertBinaryLog, mgenMsg.cpp:646-1900) keep the
+// reference's signatures and are defined in mgenx_compat.cpp (which an MGEN build compiles
+// instead of src/common/mgenMsg.cpp): the per-message events through libmgenx's formatters
+// (mgenx_log_recv_text / _binary, mgenx_log_send_text / _binary), the binary-log conversion
+// through mgenx_convert_binary_log, the TCP connection and DREC events on the host.
 #ifndef _MGEN_MESSAGE
 #define _MGEN_MESSAGE
 
@@ -195,6 +197,9 @@ class MgenMsg {
   bool compute_crc;
 
   enum { FLAGS_OFFSET = 3 };
+
+  // this message's members as one log record (mgenx_compat.cpp)
+  void FillLogRecord(mgenx::compat::LogRecvIn& r) const;
 
   static UINT8 WireType(ProtoAddress::Type t) {
     return t == ProtoAddress::IPv4 ? (UINT8)IPv4 : (t == ProtoAddress::IPv6 ? (UINT8)IPv6 : 0);

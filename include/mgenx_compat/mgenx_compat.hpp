@@ -54,6 +54,25 @@ struct UnpackOut {
   uint8_t dst_addr[16], host_addr[16];
 };
 
+// One RECV / RERR log event: an MgenMsg's members as a decoded record (core.err = 0 for
+// RECV, the MgenMsg::Error for RERR, MGENX_ERROR_RERR_NONE for a RERR of ERROR_NONE), the
+// message bytes the line reads (the DATA payload at payload_off; for binary, the whole
+// header + payload), the source, the event time and the TTL (< 0: unknown).
+struct LogRecvIn {
+  mgenx_rec core;
+  uint16_t hdr_len, host_port;
+  uint8_t host_type, host_len;
+  uint8_t dst_addr[16], host_addr[16];
+  uint32_t lat_raw, lon_raw;
+  int32_t alt;
+  uint32_t payload_off;
+  mgenx_addr src;
+  uint32_t rx_sec, rx_usec;
+  int32_t ttl;
+  const uint8_t* msg;
+  uint32_t msg_bytes;
+};
+
 class Engine {
  public:
   static Engine& Get() {
@@ -310,6 +329,243 @@ class Engine {
       i0 = i1;
     }
   }
+  // the window end a flow slot holds now (MgenAnalytic::GetWindowEnd): one state read-back
+  void FlowWindowEnd(uint32_t slot, int64_t* sec, int64_t* usec) {
+    Init();
+    Reserve(sizeof(mgenx_flow_state));
+    D2H(host_, flows_ + slot, sizeof(mgenx_flow_state));
+    Sync();
+    const mgenx_flow_state* f = (const mgenx_flow_state*)host_;
+    *sec = f->win_end_sec;
+    *usec = f->win_end_usec;
+  }
+
+  // ---- event log lines through libmgenx's formatters (mgenx_log.hip) ------------------
+  // RECV / RERR events (MgenMsg::LogRecvEvent / LogRecvError, mgenMsg.cpp:646-1143) of n
+  // records: mgenx_log_recv_text or, binary, mgenx_log_recv_binary.  Returns the bytes.
+  std::string LogRecv(const LogRecvIn* in, unsigned n, bool binary, int protocol, uint32_t opts) {
+    if (n == 0) return std::string();
+    Init();
+    size_t slab = 0, cap = 0;
+    for (unsigned i = 0; i < n; i++) {
+      slab += Align(in[i].msg_bytes, 16);
+      cap += 512 + 2u * in[i].msg_bytes;  // a line, or a binary record, fits this
+    }
+    Layout L;
+    const size_t o_rows = L.Add(n * sizeof(mgenx_rec)), o_hdr = L.Add(n * 2u);
+    const size_t o_hp = L.Add(n * 2u), o_ht = L.Add(n), o_hl = L.Add(n);
+    const size_t o_da = L.Add(n * 16u), o_ha = L.Add(n * 16u), o_lat = L.Add(n * 4u);
+    const size_t o_lon = L.Add(n * 4u), o_alt = L.Add(n * 4u), o_po = L.Add(n * 4u);
+    const size_t o_src = L.Add(n * sizeof(mgenx_addr)), o_rxs = L.Add(n * 4u);
+    const size_t o_rxu = L.Add(n * 4u), o_ttl = L.Add(n * 4u), o_off = L.Add(n * 8u);
+    const size_t o_slab = L.Add(slab + 16), in_bytes = L.size;
+    const size_t o_pos = L.Add((n + 1) * 8u), o_text = L.Add(cap);
+    Reserve(L.size);
+    uint8_t* h = host_;
+    bool any_ttl = false;
+    size_t s = 0;
+    for (unsigned i = 0; i < n; i++) {
+      const LogRecvIn& r = in[i];
+      ((mgenx_rec*)(h + o_rows))[i] = r.core;
+      ((uint16_t*)(h + o_hdr))[i] = r.hdr_len;
+      ((uint16_t*)(h + o_hp))[i] = r.host_port;
+      h[o_ht + i] = r.host_type;
+      h[o_hl + i] = r.host_len;
+      memcpy(h + o_da + 16u * i, r.dst_addr, 16);
+      memcpy(h + o_ha + 16u * i, r.host_addr, 16);
+      ((uint32_t*)(h + o_lat))[i] = r.lat_raw;
+      ((uint32_t*)(h + o_lon))[i] = r.lon_raw;
+      ((int32_t*)(h + o_alt))[i] = r.alt;
+      ((uint32_t*)(h + o_po))[i] = r.payload_off;
+      ((mgenx_addr*)(h + o_src))[i] = r.src;
+      ((uint32_t*)(h + o_rxs))[i] = r.rx_sec;
+      ((uint32_t*)(h + o_rxu))[i] = r.rx_usec;
+      ((int32_t*)(h + o_ttl))[i] = r.ttl;
+      any_ttl |= r.ttl >= 0;
+      ((uint64_t*)(h + o_off))[i] = s;
+      if (r.msg_bytes) memcpy(h + o_slab + s, r.msg, r.msg_bytes);
+      s += Align(r.msg_bytes, 16);
+    }
+    uint8_t* g = dev_;
+    H2D(g, h, in_bytes);
+    mgenx_cols c;
+    memset(&c, 0, sizeof(c));
+    c.rows = (mgenx_rec*)(g + o_rows);
+    c.hdr_len = (uint16_t*)(g + o_hdr);
+    c.host_port = (uint16_t*)(g + o_hp);
+    c.host_type = g + o_ht;
+    c.host_len = g + o_hl;
+    c.dst_addr = g + o_da;
+    c.host_addr = g + o_ha;
+    c.lat_raw = (uint32_t*)(g + o_lat);
+    c.lon_raw = (uint32_t*)(g + o_lon);
+    c.alt = (int32_t*)(g + o_alt);
+    c.payload_off = (uint32_t*)(g + o_po);
+    const mgenx_addr* src = (const mgenx_addr*)(g + o_src);
+    const uint32_t* rxs = (const uint32_t*)(g + o_rxs);
+    const uint32_t* rxu = (const uint32_t*)(g + o_rxu);
+    const uint64_t* off = (const uint64_t*)(g + o_off);
+    uint64_t* pos = (uint64_t*)(g + o_pos);
+    if (binary)
+      Check(mgenx_log_recv_binary(ctx_, g + o_slab, slab + 16, off, 0, &c, src, rxs, rxu, n,
+                                  protocol, g + o_text, cap, pos, stream_),
+            "mgenx_log_recv_binary");
+    else
+      Check(mgenx_log_recv_text(ctx_, g + o_slab, off, 0, &c, src, rxs, rxu,
+                                any_ttl ? (const int32_t*)(g + o_ttl) : nullptr, n, protocol,
+                                opts, (char*)(g + o_text), cap, pos, stream_),
+            "mgenx_log_recv_text");
+    return ReadText(o_pos, n, o_text, cap);
+  }
+
+  // SEND events (MgenMsg::LogSendEvent, mgenMsg.cpp:1145-1241) of n messages described as a
+  // pack template + descriptor each (the descriptor's tx time is the event time); binary:
+  // the records carry each message's packed bytes (msg[i], msg_bytes[i]).
+  std::string LogSend(const mgenx_flow_tmpl* tmpl, const mgenx_pack_desc* desc,
+                      const uint16_t* src_port, const uint32_t* msg_total,
+                      const uint8_t* const* msg, const uint32_t* msg_bytes, unsigned n,
+                      bool binary, int protocol, uint32_t opts) {
+    if (n == 0) return std::string();
+    Init();
+    size_t slab = 0, cap = 0;
+    for (unsigned i = 0; i < n; i++) {
+      const uint32_t b = binary ? msg_bytes[i] : 0u;
+      slab += Align(b, 16);
+      cap += 512 + b;
+    }
+    Layout L;
+    const size_t o_t = L.Add(n * sizeof(mgenx_flow_tmpl)), o_d = L.Add(n * sizeof(mgenx_pack_desc));
+    const size_t o_sp = L.Add(n * 2u), o_len = L.Add(n * 4u), o_tot = L.Add(n * 4u);
+    const size_t o_off = L.Add(n * 8u), o_slab = L.Add(slab + 16), in_bytes = L.size;
+    const size_t o_pos = L.Add((n + 1) * 8u), o_text = L.Add(cap);
+    Reserve(L.size);
+    uint8_t* h = host_;
+    size_t s = 0;
+    for (unsigned i = 0; i < n; i++) {
+      ((mgenx_flow_tmpl*)(h + o_t))[i] = tmpl[i];
+      mgenx_pack_desc d = desc[i];
+      d.tmpl = i;
+      ((mgenx_pack_desc*)(h + o_d))[i] = d;
+      ((uint16_t*)(h + o_sp))[i] = src_port[i];
+      ((uint32_t*)(h + o_len))[i] = binary ? msg_bytes[i] : 1u;  // "was sent"
+      ((uint32_t*)(h + o_tot))[i] = msg_total[i];
+      ((uint64_t*)(h + o_off))[i] = s;
+      if (binary && msg_bytes[i]) memcpy(h + o_slab + s, msg[i], msg_bytes[i]);
+      s += Align(binary ? msg_bytes[i] : 0u, 16);
+    }
+    uint8_t* g = dev_;
+    H2D(g, h, in_bytes);
+    const mgenx_flow_tmpl* t = (const mgenx_flow_tmpl*)(g + o_t);
+    const mgenx_pack_desc* d = (const mgenx_pack_desc*)(g + o_d);
+    uint64_t* pos = (uint64_t*)(g + o_pos);
+    if (binary)
+      Check(mgenx_log_send_binary(ctx_, t, d, (const uint32_t*)(g + o_len),
+                                  (const uint32_t*)(g + o_tot), g + o_slab, slab + 16,
+                                  (const uint64_t*)(g + o_off), 0, n, protocol, g + o_text, cap,
+                                  pos, stream_),
+            "mgenx_log_send_binary");
+    else
+      Check(mgenx_log_send_text(ctx_, t, d, (const uint16_t*)(g + o_sp),
+                                (const uint32_t*)(g + o_len), (const uint32_t*)(g + o_tot), n,
+                                protocol, opts, (char*)(g + o_text), cap, pos, stream_),
+            "mgenx_log_send_text");
+    return ReadText(o_pos, n, o_text, cap);
+  }
+
+  // REPORT line of an analytic's last window (MgenAnalytic::Log, mgenAnalytic.cpp:260-295):
+  // its report_msg bytes and the unquantized values; the timestamp is rep.rx_sec/usec.
+  std::string LogReport(const uint8_t* item, unsigned item_len, const mgenx_flow_report& rep,
+                        uint32_t opts) {
+    Init();
+    Layout L;
+    const size_t o_item = L.Add(MGENX_REPORT_MAX), o_rep = L.Add(sizeof(mgenx_flow_report));
+    const size_t o_cnt = L.Add(4), in_bytes = L.size, o_pos = L.Add(16), o_text = L.Add(1024);
+    Reserve(L.size);
+    uint8_t* h = host_;
+    memset(h + o_item, 0, MGENX_REPORT_MAX);
+    memcpy(h + o_item, item, item_len < MGENX_REPORT_MAX ? item_len : MGENX_REPORT_MAX);
+    memcpy(h + o_rep, &rep, sizeof(rep));
+    *(uint32_t*)(h + o_cnt) = 1;
+    uint8_t* g = dev_;
+    H2D(g, h, in_bytes);
+    Check(mgenx_log_report_text(ctx_, g + o_item, (const mgenx_flow_report*)(g + o_rep), 1, 1,
+                                (const uint32_t*)(g + o_cnt), opts, (char*)(g + o_text), 1024,
+                                (uint64_t*)(g + o_pos), stream_),
+          "mgenx_log_report_text");
+    return ReadText(o_pos, 1, o_text, 1024);
+  }
+
+  // REPORT line of a received report item (MgenAnalytic::Report::Log, mgenAnalytic.cpp:
+  // 747-786): the item bytes, the reporter (the message's source) and the log time.
+  std::string LogReportRecv(const uint8_t* item, unsigned item_len, const mgenx_addr& reporter,
+                            uint32_t sec, uint32_t usec, uint32_t opts) {
+    Init();
+    Layout L;
+    const size_t o_item = L.Add(MGENX_REPORT_MAX), o_pair = L.Add(16);
+    const size_t o_src = L.Add(sizeof(mgenx_addr)), o_s = L.Add(4), o_u = L.Add(4);
+    const size_t in_bytes = L.size, o_pos = L.Add(16), o_text = L.Add(1024);
+    Reserve(L.size);
+    uint8_t* h = host_;
+    memset(h + o_item, 0, MGENX_REPORT_MAX);
+    memcpy(h + o_item, item, item_len < MGENX_REPORT_MAX ? item_len : MGENX_REPORT_MAX);
+    ((uint64_t*)(h + o_pair))[0] = 0;
+    ((uint64_t*)(h + o_pair))[1] = 0;
+    *(mgenx_addr*)(h + o_src) = reporter;
+    *(uint32_t*)(h + o_s) = sec;
+    *(uint32_t*)(h + o_u) = usec;
+    uint8_t* g = dev_;
+    H2D(g, h, in_bytes);
+    Check(mgenx_log_report_recv_text(ctx_, g + o_item, (const uint64_t*)(g + o_pair), 1,
+                                     (const mgenx_addr*)(g + o_src), (const uint32_t*)(g + o_s),
+                                     (const uint32_t*)(g + o_u), opts, (char*)(g + o_text), 1024,
+                                     (uint64_t*)(g + o_pos), stream_),
+          "mgenx_log_report_recv_text");
+    return ReadText(o_pos, 1, o_text, 1024);
+  }
+
+  // MgenMsg::ConvertBinaryLog (mgenMsg.cpp:1417-1900) of a whole binary log image: the text
+  // and the index status (MGENX_BINLOG_*).
+  std::string ConvertBinaryLog(const uint8_t* file, size_t bytes, uint32_t flags, uint32_t opts,
+                               int* status) {
+    mgenx_binlog_info info;
+    memset(&info, 0, sizeof(info));
+    if (mgenx_binlog_index(file, bytes, nullptr, 0, &info) != MGENX_OK) {
+      *status = MGENX_BINLOG_HEADER;
+      return std::string();
+    }
+    *status = info.status;
+    const uint64_t n = info.n_records;
+    if (n == 0) return std::string();
+    Init();
+    std::vector<uint64_t> offs(n);
+    mgenx_binlog_index(file, bytes, offs.data(), n, &info);
+    // a converted line is at most a few hundred bytes plus twice a DATA payload (<= 1024)
+    uint64_t cap = n * 2560u + 4096u;
+    for (int attempt = 0;; attempt++) {
+    Layout L;
+    const size_t o_file = L.Add(bytes + 16), o_off = L.Add(n * 8u), in_bytes = L.size;
+    const size_t o_pos = L.Add((n + 1) * 8u), o_text = L.Add(cap);
+    Reserve(L.size);
+    memcpy(host_ + o_file, file, bytes);
+    memset(host_ + o_file + bytes, 0, 16);
+    memcpy(host_ + o_off, offs.data(), n * 8u);
+    uint8_t* g = dev_;
+    H2D(g, host_, in_bytes);
+    Check(mgenx_convert_binary_log(ctx_, g + o_file, bytes, (const uint64_t*)(g + o_off),
+                                   (uint32_t)n, flags, opts, (char*)(g + o_text), cap,
+                                   (uint64_t*)(g + o_pos), stream_),
+          "mgenx_convert_binary_log");
+    D2H(host_ + o_pos, g + o_pos, (n + 1) * 8u);
+    Sync();
+    const uint64_t total = ((const uint64_t*)(host_ + o_pos))[n];
+    if (total > cap && attempt == 0) {  // many report lines: once more at the exact size
+      cap = total;
+      continue;
+    }
+    return ReadText(o_pos, (unsigned)n, o_text, cap);
+    }
+  }
+
   const mgenx_flow_state* DevFlows() const { return flows_; }
   mgenx_ctx* Ctx() {
     Init();
@@ -405,6 +661,16 @@ class Engine {
       updated[i] = cnt[slot[i]] != 0;
       if (updated[i]) rep[i] = r[slot[i]];
     }
+  }
+  // the formatters' output: pos[n] bytes at o_text (throws when the capacity was short)
+  std::string ReadText(size_t o_pos, unsigned n, size_t o_text, size_t cap) {
+    D2H(host_ + o_pos, dev_ + o_pos, (n + 1) * 8u);
+    Sync();
+    const uint64_t total = ((const uint64_t*)(host_ + o_pos))[n];
+    if (total > cap) throw Error("mgenx compat: log text larger than its staging capacity");
+    D2H(host_ + o_text, dev_ + o_text, total);
+    Sync();
+    return std::string((const char*)host_ + o_text, total);
   }
   void H2D(void* d, const void* s, size_t b) {
     if (hipMemcpyAsync(d, s, b, hipMemcpyHostToDevice, stream_) != hipSuccess)

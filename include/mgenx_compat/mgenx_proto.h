@@ -6,8 +6,14 @@
 // define MGENX_WITH_PROTOLIB and this header only includes those.  The shim uses nothing
 // of ProtoAddress beyond what MgenMsg::Pack/Unpack use in the reference
 // (src/common/mgenMsg.cpp:128-156, 396-430: GetType, GetLength, GetPort, SetPort,
-// GetRawHostAddress, SetRawHostAddress, IsValid, Invalidate) and of ProtoTime beyond
-// seconds/microseconds.
+// GetRawHostAddress, SetRawHostAddress, IsValid, Invalidate; GetHostString for the TCP
+// connection events) and of ProtoTime beyond seconds/microseconds.
+//
+// Without protolib there is no Mgen either: the logging members (mgenx_compat.cpp) read the
+// log file and its settings from an Mgen, so this header also carries the slice of the
+// reference's Mgen (include/mgen.h:195-216) they use, plus the DrecEvent / MgenBaseEvent
+// getters LogDrecEvent reads (include/mgenEvent.h).  Inside an MGEN build those are the real
+// classes (mgen.h, mgenEvent.h).
 #pragma once
 
 #ifdef MGENX_WITH_PROTOLIB
@@ -15,7 +21,9 @@
 #include "mgenGlobals.h"
 #else
 
+#include <arpa/inet.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <string.h>
 #include <sys/time.h>
 
@@ -66,6 +74,17 @@ class ProtoAddress {
     if (buf && len) memcpy(addr_, buf, len > 16 ? 16 : len);
     return true;
   }
+  // the text form MGEN logs (inet_ntop; "(invalid)" otherwise, as the device formatters)
+  const char* GetHostString(char* buffer = nullptr, unsigned int buflen = 0) const {
+    static thread_local char text[64];
+    char* out = buffer ? buffer : text;
+    const unsigned int cap = buffer ? buflen : (unsigned int)sizeof(text);
+    const char* r = nullptr;
+    if (type_ == IPv4 && len_ == 4) r = inet_ntop(AF_INET, addr_, out, cap);
+    else if (type_ == IPv6 && len_ == 16) r = inet_ntop(AF_INET6, addr_, out, cap);
+    if (!r && cap) snprintf(out, cap, "%s", "(invalid)");
+    return out;
+  }
   bool HostIsEqual(const ProtoAddress& o) const {
     return type_ == o.type_ && len_ == o.len_ && memcmp(addr_, o.addr_, len_) == 0;
   }
@@ -80,23 +99,83 @@ class ProtoAddress {
 
 class ProtoTime {
  public:
-  ProtoTime() : sec_(0), usec_(0) {}
+  ProtoTime() { tv_.tv_sec = 0; tv_.tv_usec = 0; }
   explicit ProtoTime(double seconds) {
-    sec_ = (long)seconds;
-    usec_ = (long)((seconds - (double)sec_) * 1.0e06 + 0.5);
+    tv_.tv_sec = (long)seconds;
+    tv_.tv_usec = (long)((seconds - (double)tv_.tv_sec) * 1.0e06 + 0.5);
   }
-  ProtoTime(const struct timeval& tv) : sec_(tv.tv_sec), usec_(tv.tv_usec) {}
-  unsigned long sec() const { return (unsigned long)sec_; }
-  unsigned long usec() const { return (unsigned long)usec_; }
-  long GetSec() const { return sec_; }
-  long GetUsec() const { return usec_; }
-  double GetValue() const { return (double)sec_ + 1.0e-06 * (double)usec_; }
+  ProtoTime(const struct timeval& tv) : tv_(tv) {}
+  unsigned long sec() const { return (unsigned long)tv_.tv_sec; }
+  unsigned long usec() const { return (unsigned long)tv_.tv_usec; }
+  long GetSec() const { return tv_.tv_sec; }
+  long GetUsec() const { return tv_.tv_usec; }
+  const struct timeval& GetTimeVal() const { return tv_; }
+  double GetValue() const { return (double)tv_.tv_sec + 1.0e-06 * (double)tv_.tv_usec; }
 
  private:
-  long sec_, usec_;
+  struct timeval tv_;
 };
 
 inline void ProtoSystemTime(struct timeval& tv) { gettimeofday(&tv, nullptr); }
+
+// the slice of Mgen (include/mgen.h:195-216) MgenMsg's logging members read
+class Mgen {
+ public:
+  typedef int (*LogFunction)(FILE*, const char*, ...);
+  static LogFunction Log;                                     // fprintf by default
+  static void (*LogTimestamp)(FILE*, const struct timeval&, bool);
+  static void SetEpochTimestamp(bool enable) {
+    LogTimestamp = enable ? LogEpochTimestamp : LogLegacyTimestamp;
+  }
+  static void LogEpochTimestamp(FILE* f, const struct timeval& t, bool localTime);
+  static void LogLegacyTimestamp(FILE* f, const struct timeval& t, bool localTime);
+
+  FILE* GetLogFile() { return log_file; }
+  bool GetLogBinary() { return log_binary; }
+  bool GetLocalTime() { return local_time; }
+  bool GetLogFlush() { return log_flush; }
+  bool GetLogRx() { return log_rx; }
+  bool GetLogData() { return log_data; }
+  bool GetLogGpsData() { return log_gps_data; }
+  bool GetOffsetPending() { return offset_pending; }
+  // settings (the reference sets these from its commands, mgen.cpp:1545-2143)
+  void SetLogFile(FILE* f) { log_file = f; }
+  void SetLogBinary(bool v) { log_binary = v; }
+  void SetLocalTime(bool v) { local_time = v; }
+  void SetLogFlush(bool v) { log_flush = v; }
+  void SetLogRx(bool v) { log_rx = v; }
+  void SetLogData(bool v) { log_data = v; }
+  void SetLogGpsData(bool v) { log_gps_data = v; }
+
+ private:
+  FILE* log_file = nullptr;
+  bool log_binary = false, local_time = false, log_flush = false, log_rx = true;
+  bool log_data = true, log_gps_data = true, offset_pending = false;
+};
+
+// the getters LogDrecEvent reads (include/mgenEvent.h: MgenBaseEvent, DrecEvent)
+class MgenBaseEvent {
+ public:
+  static const char* GetStringFromProtocol(Protocol p) {  // mgenEvent.cpp:75-126
+    return p == UDP ? "UDP" : p == TCP ? "TCP" : p == SINK ? "SINK" : "UNKNOWN";
+  }
+};
+class DrecEvent : public MgenBaseEvent {
+ public:
+  Protocol GetProtocol() const { return protocol; }
+  const ProtoAddress& GetGroupAddress() const { return group_addr; }
+  const ProtoAddress& GetSourceAddress() const { return source_addr; }
+  const char* GetInterface() const { return iface[0] ? iface : nullptr; }
+  void SetProtocol(Protocol p) { protocol = p; }
+  void SetGroupAddress(const ProtoAddress& a) { group_addr = a; }
+  void SetSourceAddress(const ProtoAddress& a) { source_addr = a; }
+  void SetInterface(const char* name) { snprintf(iface, sizeof(iface), "%s", name ? name : ""); }
+
+ private:
+  Protocol protocol = INVALID_PROTOCOL;
+  ProtoAddress group_addr, source_addr;
+  char iface[64] = {0};
+};
 
 // Byte-offset packet view (the ProtoPkt calls MgenDataItem and MgenAnalytic::Report make):
 // Get/Set UINT8/16/32 at byte offsets, network byte order for the wider ones.

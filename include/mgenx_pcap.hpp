@@ -42,18 +42,21 @@ class Pcap2Mgen {
     const uint32_t n = (uint32_t)info.n_records;
     if (n == 0) return std::string();
     hipStream_t s = ctx_.stream();
-    DeviceArray<uint8_t> buf(nbytes);
+    // the file image, then scratch for the packets a snapshot length cut (mgenx_pcap_snap)
+    DeviceArray<uint8_t> buf(nbytes + info.snap_bytes);
     DeviceArray<uint64_t> pkt(n);
     check_hip(hipMemcpyAsync(buf.data(), file, nbytes, hipMemcpyHostToDevice, s), "H2D file");
     check_hip(hipMemcpyAsync(pkt.data(), offs.data(), (size_t)n * 8, hipMemcpyHostToDevice, s),
               "H2D offsets");
-    std::string out = RunDevice(buf.data(), nbytes, pkt.data(), n, info.link_type, info.flags);
+    std::string out = RunDevice(buf.data(), nbytes, pkt.data(), n, info.link_type, info.flags,
+                                nbytes + info.snap_bytes);
     return out;
   }
 
-  // The pipeline over a resident file image (device pointers).
-  std::string RunDevice(const uint8_t* d_buf, uint64_t nbytes, const uint64_t* d_pkt,
-                        uint32_t n, uint32_t link_type, uint32_t flags) {
+  // The pipeline over a resident file image (device pointers).  buf_bytes > nbytes: scratch
+  // after the image for packets cut by the snapshot length (else they are skipped).
+  std::string RunDevice(uint8_t* d_buf, uint64_t nbytes, const uint64_t* d_pkt, uint32_t n,
+                        uint32_t link_type, uint32_t flags, uint64_t buf_bytes = 0) {
     mgenx_ctx* c = ctx_.get();
     hipStream_t s = ctx_.stream();
     DeviceArray<uint64_t> udp_off(n);
@@ -65,6 +68,12 @@ class Pcap2Mgen {
                                 udp_len.data(), src.data(), ttl.data(), rx_sec.data(),
                                 rx_usec.data(), status.data(), s),
                "mgenx_pcap_parse");
+    if (buf_bytes > nbytes) {
+      ctx_.Check(mgenx_pcap_snap(c, d_buf, nbytes, buf_bytes, d_pkt, n, flags, status.data(),
+                                 udp_off.data(), udp_len.data(), s),
+                 "mgenx_pcap_snap");
+      nbytes = buf_bytes;  // the records now reach into the scratch
+    }
     Columns col(n);
     ctx_.Check(mgenx_unpack_batch(c, d_buf, nbytes, udp_off.data(), 0, udp_len.data(), 0, n,
                                   &col.cols, MGENX_OPT_SKIP_CRC, s),

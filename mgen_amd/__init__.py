@@ -42,7 +42,7 @@ EXPORTED_SYMBOLS = (
     "mgenx_flow_table_create", "mgenx_flow_table_destroy", "mgenx_flow_lookup",
     "mgenx_flow_reduce_ex", "mgenx_flow_keys", "mgenx_text_interleave", "mgenx_pcap_index",
     "mgenx_pcap_parse", "mgenx_binlog_index", "mgenx_convert_binary_log",
-    "mgenx_unpack_last_kernel",
+    "mgenx_unpack_last_kernel", "mgenx_pcap_snap",
 )
 DIAG_SYMBOLS = ("mgenx_set_tuning", "mgenx_diag_stream_read", "mgenx_diag_group_rw")
 
@@ -97,6 +97,7 @@ def load(diag: bool = False):
     L.mgenx_text_interleave.argtypes = [P, P, u32, u32, P, u64, P, P]
     L.mgenx_pcap_index.argtypes = [P, u64, P, u64, ctypes.POINTER(PcapInfo)]
     L.mgenx_pcap_parse.argtypes = [P, P, u64, P, u32, u32, u32, P, P, P, P, P, P, P, P]
+    L.mgenx_pcap_snap.argtypes = [P, P, u64, u64, P, u32, u32, P, P, P, P]
     L.mgenx_binlog_index.argtypes = [P, u64, P, u64, ctypes.POINTER(BinlogInfo)]
     L.mgenx_convert_binary_log.argtypes = [P, P, u64, P, u32, u32, u32, P, u64, P, P]
     if diag:
@@ -532,6 +533,15 @@ class Engine:
                                               _ptr(o["status"]), _stream(self.device)),
                     "mgenx_pcap_parse")
         return o
+
+    def pcap_snap(self, buf, file_bytes, pkt_off, n, flags, parsed):
+        """mgenx_pcap_snap: move the SNAPPED packets of `parsed` (pcap_parse's dict) into
+        buf[file_bytes:], zero-extended, in place."""
+        self._check(self.lib.mgenx_pcap_snap(self.ctx, _ptr(buf), file_bytes, buf.numel(),
+                                             _ptr(pkt_off), n, flags, _ptr(parsed["status"]),
+                                             _ptr(parsed["udp_off"]), _ptr(parsed["udp_len"]),
+                                             _stream(self.device)), "mgenx_pcap_snap")
+        return parsed
 
     def flow_export(self, flows, n_flows, out=None):
         if out is None:

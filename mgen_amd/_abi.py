@@ -145,7 +145,8 @@ assert FLOW_REPORT_DTYPE.itemsize == 96 and FLOW_COUNTERS_DTYPE.itemsize == 64
 class PcapInfo(ctypes.Structure):      # mgenx_pcap_info
     _fields_ = [("link_type", ctypes.c_uint32), ("flags", ctypes.c_uint32),
                 ("snaplen", ctypes.c_uint32), ("rsv", ctypes.c_uint32),
-                ("n_records", ctypes.c_uint64), ("consumed", ctypes.c_uint64)]
+                ("n_records", ctypes.c_uint64), ("consumed", ctypes.c_uint64),
+                ("snap_bytes", ctypes.c_uint64)]
 
 
 class TextSrc(ctypes.Structure):       # mgenx_text_src

@@ -69,6 +69,12 @@ extern "C" int mgenx_pcap_parse_run(const uint8_t* dev_buf, uint64_t buf_bytes,
                                     mgenx_addr* dev_src, int32_t* dev_ttl, uint32_t* dev_rx_sec,
                                     uint32_t* dev_rx_usec, uint8_t* dev_status,
                                     hipStream_t stream);
+extern "C" int mgenx_pcap_snap_run(uint8_t* dev_buf, uint64_t file_bytes, uint64_t buf_bytes,
+                                   const uint64_t* dev_pkt_off, uint32_t n, uint32_t flags,
+                                   uint8_t* dev_status, uint64_t* dev_udp_off,
+                                   uint32_t* dev_udp_len, uint64_t* need, void* scan_tmp,
+                                   size_t scan_bytes, hipStream_t stream);
+extern "C" size_t mgenx_pcap_snap_scan_bytes(uint32_t n);
 extern "C" int mgenx_log_recv_run(void* ws, bool binary, const uint8_t* slab,
                                   uint64_t slab_bytes, const uint64_t* rec_off,
                                        uint64_t stride, const mgenx_cols* cols,
@@ -151,6 +157,7 @@ struct mgenx_ctx {
   int unpack_last = 0;             // MGENX_UNPACK_K_* of the last mgenx_unpack_batch
   int pack_variant = 0;
   mgenx_grow bl[5];                // mgenx_convert_binary_log: records, lines, pairs, report text
+  mgenx_grow snap;                 // mgenx_pcap_snap: per-packet sizes + scan scratch
   bool rand_ready = false;
   uint32_t rand_time = 0;
   char err[256] = {0};
@@ -335,6 +342,7 @@ int mgenx_ctx_destroy(mgenx_ctx* c) {
   if (c->rx_ws) hipFree(c->rx_ws);
   if (c->tcp_host) hipHostFree(c->tcp_host);
   for (mgenx_grow& g : c->bl) g.release();
+  c->snap.release();
   for (void* p : ps)
     if (p) hipFree(p);
   delete c;
@@ -952,6 +960,23 @@ int mgenx_pcap_parse(mgenx_ctx* ctx, const uint8_t* dev_buf, uint64_t buf_bytes,
                               (hipStream_t)stream);
 }
 
+int mgenx_pcap_snap(mgenx_ctx* ctx, uint8_t* dev_buf, uint64_t file_bytes, uint64_t buf_bytes,
+                    const uint64_t* dev_pkt_off, uint32_t n, uint32_t flags, uint8_t* dev_status,
+                    uint64_t* dev_udp_off, uint32_t* dev_udp_len, void* stream) {
+  if (!ctx || buf_bytes < file_bytes || n > 0x7FFFFFFEu) return MGENX_EINVAL;
+  if (n == 0) return MGENX_OK;
+  if (!dev_buf || !dev_pkt_off || !dev_status || !dev_udp_off || !dev_udp_len) return MGENX_EINVAL;
+  hipSetDevice(ctx->device);
+  const size_t need_b = (((size_t)n + 1) * 8 + 255) & ~(size_t)255;
+  const size_t scan_b = mgenx_pcap_snap_scan_bytes(n);
+  char* m = static_cast<char*>(ctx->snap.get(need_b + scan_b));
+  if (!m) return set_err(ctx, hipErrorOutOfMemory, "pcap_snap workspace");
+  const int rc = mgenx_pcap_snap_run(dev_buf, file_bytes, buf_bytes, dev_pkt_off, n, flags,
+                                     dev_status, dev_udp_off, dev_udp_len, (uint64_t*)m,
+                                     m + need_b, scan_b, (hipStream_t)stream);
+  return rc == MGENX_OK ? MGENX_OK : set_err(ctx, hipGetLastError(), "pcap_snap");
+}
+
 // ---- ConvertBinaryLog (mgenMsg.cpp:1417-1900) ----
 int mgenx_binlog_index(const uint8_t* buf, uint64_t nbytes, uint64_t* rec_off, uint64_t cap,
                        mgenx_binlog_info* info) {
@@ -985,10 +1010,23 @@ int mgenx_binlog_index(const uint8_t* buf, uint64_t nbytes, uint64_t* rec_off, u
     if (rl > 1024) { info->status = MGENX_BINLOG_TOO_LONG; break; }
     if (off + 4 + rl > nbytes) { info->status = MGENX_BINLOG_SHORT; break; }
     const bool addr_ev = ev == 1 || ev == 6 || ev == 7 || (ev >= 10 && ev <= 16);
-    if (ev == 0 || ev == 2 || ev > 16 || (addr_ev && (rl < 11 || (h[14] != 1 && h[14] != 2)))) {
-      info->status = MGENX_BINLOG_EVENT;
-      break;
+    if (ev == 0 || ev == 2 || ev > 16) { info->status = MGENX_BINLOG_EVENT; break; }
+    // a record too short for the fields its type reads (mgen never writes one; the reference
+    // would parse stale bytes of its read buffer): stop as at a short read, so the device
+    // formatters never read past a record -- the event time (8 bytes), RECV 12 + source
+    // length, LISTEN / IGNORE 12, JOIN / LEAVE 13 + group length + interface name length,
+    // ON ... RECONNECT 18 + address length
+    const uint8_t* b = h + 4;
+    bool shortrec = rl < 8;
+    if (!shortrec) {
+      if (ev == 1) shortrec = rl < 12 || rl < 12u + b[11];
+      else if (ev == 4 || ev == 5) shortrec = rl < 12;
+      else if (ev == 6 || ev == 7)
+        shortrec = rl < 13 || rl < 13u + b[11] || rl < 13u + b[11] + b[12 + b[11]];
+      else if (ev >= 10 && ev <= 16) shortrec = rl < 12 || rl < 18u + b[11];
     }
+    if (shortrec) { info->status = MGENX_BINLOG_SHORT; break; }
+    if (addr_ev && h[14] != 1 && h[14] != 2) { info->status = MGENX_BINLOG_EVENT; break; }
     if (n < cap) rec_off[n] = off;
     n++;
     off += 4 + rl;
@@ -1038,7 +1076,7 @@ int mgenx_convert_binary_log(mgenx_ctx* ctx, const uint8_t* dev_buf, uint64_t bu
   c.dst_len = (uint8_t*)take(a1); c.payload_type = (uint8_t*)take(a1);
   c.gps_status = (uint8_t*)take(a1); c.host_type = (uint8_t*)take(a1);
   c.host_len = (uint8_t*)take(a1);
-  (void)take(a1);
+  c.decoded = (uint8_t*)take(a1);
   c.host_addr = (uint8_t*)take(a16); c.dst_addr = (uint8_t*)take(a16);
   int rc = mgenx_binlog_parse_exec(dev_buf, dev_rec_off, n, msg_off, msg_len, src, ev_sec, ev_usec,
                                    aux, kind, proto, s);

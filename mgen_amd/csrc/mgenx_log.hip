@@ -183,9 +183,11 @@ __device__ void put_deg(S& s, uint32_t raw) {
 }
 
 // A record past the end of the slab (MGENX_ERROR_OOB) is not an MgenMsg::Error: it is
-// logged as ERROR_LENGTH, as include/mgenx.hpp maps it
+// logged as ERROR_LENGTH, as include/mgenx.hpp maps it; MGENX_ERROR_RERR_NONE is a RERR
+// event of an error-free message (LogRecvError called on it): "none", code 0
 __device__ __forceinline__ uint32_t log_error(uint32_t e) {
-  return e == MGENX_ERROR_OOB ? (uint32_t)MGENX_ERROR_LENGTH : e;
+  return e == MGENX_ERROR_OOB ? (uint32_t)MGENX_ERROR_LENGTH
+                              : e == MGENX_ERROR_RERR_NONE ? 0u : e;
 }
 
 template <typename S>
@@ -1218,10 +1220,19 @@ __device__ void bl_line(S& s, const BinParams& p, uint32_t i) {
   const bool epoch = (p.opts & MGENX_LOG_EPOCH) != 0;
   const mgenx_cols& c = p.cols;
   if (ev == 1 || ev == 3) {
-    if (c.err[i] != 0) return;  // a stored message Unpack rejects: no line
     LogParams lp;
     lp.cols = c;
-    const LogRec r = gather(lp, i);
+    LogRec r = gather(lp, i);
+    if (r.err) {
+      // a stored message Unpack rejects: the reference ignores Unpack's result and logs the
+      // line from the members its fresh MgenMsg holds (:1601-1607, 1612-1625) -- the fresh
+      // decode's defaults, and for RECV the event time it set as tx_time before Unpack
+      if (ev == 1 && !(c.decoded[i] & MGENX_DEC_BASE)) {
+        r.sec = p.ev_sec[i];
+        r.usec = p.ev_usec[i];
+      }
+      r.err = 0;
+    }
     if (ev == 1) {  // LogRecvEvent (:1607): log_flush lands in the ttl argument
       if (p.log_rx)
         format_line(s, r, p.buf + p.msg_off[i], p.src[i], p.ev_sec[i], p.ev_usec[i], p.proto[i],

@@ -16,6 +16,8 @@
 
 #include <string.h>
 
+#include <hipcub/hipcub.hpp>
+
 #include "mgenx_kernels.hpp"
 
 namespace mgenx {
@@ -130,18 +132,64 @@ __global__ void __launch_bounds__(256) pcap_parse_kernel(PcapParams p) {
     const uint32_t ul = ld_be16(d, l4 + 4);
     if (ul < 8 || ul > l4_len) { st = MGENX_PCAP_NOT_UDP; break; }
     a.port = (uint16_t)ld_be16(d, l4);
-    if (l4 + ul > num) { st = MGENX_PCAP_TRUNCATED; break; }
+    uoff = l4 + 8;
+    if (l4 + ul > num) {  // cut by the snapshot length: mgenx_pcap_snap zero-extends it
+      st = l4 + 8 + MGENX_MIN_SIZE <= num ? MGENX_PCAP_SNAPPED : MGENX_PCAP_TRUNCATED;
+      break;
+    }
     st = MGENX_PCAP_UDP;
     ulen = ul - 8;
-    uoff = l4 + 8;
   } while (false);
   p.status[i] = (uint8_t)st;
-  p.udp_off[i] = st == MGENX_PCAP_UDP ? ro + 16 + uoff : ro;
+  p.udp_off[i] = (st == MGENX_PCAP_UDP || st == MGENX_PCAP_SNAPPED) ? ro + 16 + uoff : ro;
   p.udp_len[i] = st == MGENX_PCAP_UDP ? ulen : 0u;
   p.src[i] = a;
   p.ttl[i] = ttl;
   p.rx_sec[i] = tsec;
   p.rx_usec[i] = tusec;
+}
+
+// mgenx_pcap_snap: bytes each SNAPPED packet needs in scratch (its UDP payload length, read
+// from the captured UDP header 4 bytes before the payload, 16-byte rounded)
+__global__ void __launch_bounds__(256) pcap_snap_size_kernel(const uint8_t* buf, uint32_t n,
+                                                             const uint8_t* status,
+                                                             const uint64_t* udp_off,
+                                                             uint64_t* need) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > n) return;
+  uint64_t b = 0;
+  if (i < n && status[i] == MGENX_PCAP_SNAPPED) {
+    const uint32_t ul = ld_be16(buf, udp_off[i] - 4);
+    b = ((uint64_t)(ul - 8) + 15) & ~15ull;
+  }
+  need[i] = b;
+}
+
+// one wave per packet (grid-stride): captured bytes, then zeros up to the UDP length
+__global__ void __launch_bounds__(256) pcap_snap_copy_kernel(uint8_t* buf, uint64_t file_bytes,
+                                                             uint64_t buf_bytes,
+                                                             const uint64_t* pkt_off, uint32_t n,
+                                                             uint32_t flags, uint8_t* status,
+                                                             uint64_t* udp_off, uint32_t* udp_len,
+                                                             const uint64_t* dst) {
+  const bool sw = (flags & MGENX_PCAP_SWAPPED) != 0;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t waves = gridDim.x * (blockDim.x / 64);
+  for (uint32_t i = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); i < n; i += waves) {
+    if (status[i] != MGENX_PCAP_SNAPPED) continue;
+    const uint64_t src = udp_off[i];
+    const uint32_t len = ld_be16(buf, src - 4) - 8u;
+    const uint64_t to = file_bytes + dst[i];
+    if (to + len > buf_bytes) continue;  // no room: stays SNAPPED (skipped)
+    const uint64_t ro = pkt_off[i];
+    const uint64_t have = ro + 16 + ld_u32(buf, ro + 8, sw) - src;  // captured payload bytes
+    for (uint32_t k = lane; k < len; k += 64) buf[to + k] = k < have ? buf[src + k] : (uint8_t)0;
+    if (lane == 0) {
+      udp_off[i] = to;
+      udp_len[i] = len;
+      status[i] = MGENX_PCAP_UDP;
+    }
+  }
 }
 
 }  // namespace mgenx
@@ -180,6 +228,8 @@ int mgenx_pcap_index(const uint8_t* buf, uint64_t nbytes, uint64_t* pkt_off, uin
   while (off + 16 <= nbytes) {
     const uint32_t caplen = host_u32(buf + off + 8, sw);
     if (off + 16 + (uint64_t)caplen > nbytes) break;  // short read: pcap_next returns NULL
+    const uint32_t wirelen = host_u32(buf + off + 12, sw);
+    if (caplen < wirelen) info->snap_bytes += ((uint64_t)wirelen + 15) & ~15ull;
     if (n < cap) pkt_off[n] = off;
     n++;
     off += 16 + (uint64_t)caplen;
@@ -201,6 +251,30 @@ int mgenx_pcap_parse_run(const uint8_t* dev_buf, uint64_t buf_bytes, const uint6
   p.status = dev_status;
   hipLaunchKernelGGL(pcap_parse_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, p);
   return hipGetLastError() == hipSuccess ? MGENX_OK : MGENX_EDEVICE;
+}
+
+int mgenx_pcap_snap_run(uint8_t* dev_buf, uint64_t file_bytes, uint64_t buf_bytes,
+                        const uint64_t* dev_pkt_off, uint32_t n, uint32_t flags,
+                        uint8_t* dev_status, uint64_t* dev_udp_off, uint32_t* dev_udp_len,
+                        uint64_t* need, void* scan_tmp, size_t scan_bytes, hipStream_t stream) {
+  hipLaunchKernelGGL(pcap_snap_size_kernel, dim3((n + 256) / 256), dim3(256), 0, stream, dev_buf,
+                     n, dev_status, dev_udp_off, need);
+  size_t have = scan_bytes;
+  if (hipcub::DeviceScan::ExclusiveSum(scan_tmp, have, need, need, (int)n + 1, stream) !=
+      hipSuccess)
+    return MGENX_EDEVICE;
+  const uint32_t blocks = n < 1024u * 4u ? (n + 3) / 4 : 1024u;
+  hipLaunchKernelGGL(pcap_snap_copy_kernel, dim3(blocks), dim3(256), 0, stream, dev_buf,
+                     file_bytes, buf_bytes, dev_pkt_off, n, flags, dev_status, dev_udp_off,
+                     dev_udp_len, need);
+  return hipGetLastError() == hipSuccess ? MGENX_OK : MGENX_EDEVICE;
+}
+
+size_t mgenx_pcap_snap_scan_bytes(uint32_t n) {
+  size_t b = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, (uint64_t*)nullptr, (uint64_t*)nullptr,
+                                         (int)n + 1, (hipStream_t)0);
+  return b;
 }
 
 }  // extern "C"

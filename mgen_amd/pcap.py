@@ -59,23 +59,31 @@ class Pcap2Mgen:
         b = np.frombuffer(bytes(file), np.uint8) if not isinstance(file, np.ndarray) else file
         offs, info = pcap_index(b)
         dev = f"cuda:{self.eng.device}"
-        buf = torch.from_numpy(b.copy()).to(dev)
+        # the file image, then scratch for packets cut by the snapshot length (mgenx_pcap_snap)
+        buf = torch.zeros(b.size + int(info.snap_bytes), dtype=torch.uint8, device=dev)
+        buf[:b.size] = torch.from_numpy(b.copy()).to(dev)
         pkt_off = torch.from_numpy(offs.view(np.int64).copy()).to(dev)
         return buf, pkt_off, info
 
     def run(self, file) -> bytes:
         buf, pkt_off, info = self.upload(file)
-        text, _ = self.run_device(buf, pkt_off, int(info.n_records), info.link_type, info.flags)
+        file_bytes = buf.numel() - int(info.snap_bytes)
+        text, _ = self.run_device(buf, pkt_off, int(info.n_records), info.link_type, info.flags,
+                                  file_bytes=file_bytes)
         return text.cpu().numpy().tobytes()
 
-    def run_device(self, buf, pkt_off, n, link_type, flags):
-        """The device pipeline over a resident file: (text tensor, per-packet offsets)."""
+    def run_device(self, buf, pkt_off, n, link_type, flags, file_bytes=None):
+        """The device pipeline over a resident file: (text tensor, per-packet offsets).
+        file_bytes: the file image's size when buf has scratch after it for snapped packets
+        (None: no scratch; packets cut by the snapshot length are skipped)."""
         eng, torch = self.eng, self.eng.torch
         dev = buf.device
         if n == 0:
             return torch.empty(0, dtype=torch.uint8, device=dev), torch.zeros(
                 1, dtype=torch.int64, device=dev)
         p = eng.pcap_parse(buf, pkt_off, n, link_type, flags)
+        if file_bytes is not None and file_bytes < buf.numel():
+            eng.pcap_snap(buf, file_bytes, pkt_off, n, flags, p)
         cols = eng.unpack(buf, n, rec_off=p["udp_off"], rec_len=p["udp_len"], opts=OPT_SKIP_CRC,
                           ext=True)
         sources = []

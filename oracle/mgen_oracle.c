@@ -1632,9 +1632,19 @@ int or_pcap_frame(const uint8_t* rec, uint32_t link_type, uint32_t flags, uint32
     const uint32_t ul = pc_be16(d + l4 + 4);
     if (ul < 8 || ul > l4_len) return 4;
     src->port = (uint16_t)pc_be16(d + l4);
-    if (l4 + ul > num) return 5;
     *udp_off = 16 + l4 + 8;
     *udp_len = ul - 8;
+    if (l4 + ul > num) {
+        /* cut by the snapshot length: the reference parses the frame by hdr.len and Unpacks
+         * udpPkt's payload from its parse buffer, so the MGEN header comes from the captured
+         * bytes.  With the UDP header and MIN_SIZE payload bytes captured the payload is
+         * unpacked zero-extended to the UDP length (7, SNAPPED; the reference's buffer holds
+         * stale bytes there); shorter captures are skipped (5). */
+        if (l4 + 8 + 28 <= num) return 7;
+        *udp_off = 0;
+        *udp_len = 0;
+        return 5;
+    }
     return 0;
 }
 
@@ -1711,6 +1721,7 @@ uint64_t or_pcap2mgen(const uint8_t* file, uint64_t nbytes, int analytics, int l
     pc_flow* tab = NULL;
     uint32_t tcap = 0, tn = 0;
     char* line = (char*)malloc(1 << 16);
+    uint8_t* snap = (uint8_t*)malloc(65536);
     uint64_t off = 24;
     while (off + 16 <= nbytes) {                                    /* pcap_next :344 */
         const uint32_t caplen = pc_u32(file + off + 8, sw);
@@ -1723,8 +1734,13 @@ uint64_t or_pcap2mgen(const uint8_t* file, uint64_t nbytes, int analytics, int l
         const int st = or_pcap_frame(rec, link, flags, &uo, &ul, &src, &ttl, &sec, &usec);
         if (status) status[npk] = (uint8_t)st;
         npk++;
-        if (st != 0) continue;
+        if (st != 0 && st != 7) continue;
         const uint8_t* pay = rec + uo;
+        if (st == 7) {                     /* SNAPPED: the captured bytes, zero-extended */
+            memset(snap, 0, 65536);
+            memcpy(snap, pay, 16 + pc_u32(rec + 8, sw) - uo);
+            pay = snap;
+        }
         or_fields f;
         or_unpack(pay, ul, &f);                                     /* :428-432 */
         if (!f.ok) continue;
@@ -1770,6 +1786,7 @@ uint64_t or_pcap2mgen(const uint8_t* file, uint64_t nbytes, int analytics, int l
         }
     }
     free(line);
+    free(snap);
     free(tab);
     if (n_pkts) *n_pkts = npk;
     return pos;
@@ -1786,8 +1803,25 @@ uint64_t or_pcap2mgen(const uint8_t* file, uint64_t nbytes, int analytics, int l
  * log_flush in the ttl slot ("ttl>0 " / "ttl>1 "); SEND: Unpack and LogSendEvent (srcPort 0:
  * a fresh MgenMsg's source); LISTEN / IGNORE / JOIN / LEAVE / START / STOP / ON / ACCEPT /
  * CONNECT / DISCONNECT / OFF / SHUTDOWN / RECONNECT lines as :1628-1891.  A RECV or SEND
- * record whose stored message Unpack rejects (never written by mgen) gives no line here. */
+ * record whose stored message Unpack rejects (never written by mgen) is logged all the same,
+ * from the members the fresh MgenMsg keeps, as the reference ignores Unpack's result. */
 enum { OR_BL_OK = 0, OR_BL_HEADER = 1, OR_BL_TOO_LONG = 2, OR_BL_EVENT = 3, OR_BL_SHORT = 4 };
+
+/* A record too short for the fields its type reads (mgen never writes one): the reference
+ * parses its fixed-size read buffer regardless (stale bytes past the record); here the walk
+ * stops at it as at a short read.  Every record holds its event time (8 bytes); RECV 12 +
+ * source length; LISTEN / IGNORE 12; JOIN / LEAVE 13 + group length + interface name
+ * length; ON ... RECONNECT 18 + address length. */
+static int bl_too_short(int ev, const uint8_t* b, uint32_t rl)
+{
+    if (rl < 8) return 1;
+    switch (ev) {
+        case 1: return rl < 12 || rl < 12u + b[11];
+        case 4: case 5: return rl < 12;
+        case 6: case 7: return rl < 13 || rl < 13u + b[11] || rl < 13u + b[11] + b[12 + b[11]];
+        default: return ev >= 10 && ev <= 16 && (rl < 12 || rl < 18u + b[11]);
+    }
+}
 
 static void bl_addr(or_addr* a, uint8_t type, const uint8_t* p, uint32_t len, uint16_t port)
 {
@@ -1852,6 +1886,7 @@ uint64_t or_convert_binary_log(const uint8_t* file, uint64_t nbytes, int log_rx,
         if (rl > 1024) { *status = OR_BL_TOO_LONG; break; }
         if (off + 4 + rl > nbytes) { *status = OR_BL_SHORT; break; }
         const uint8_t* b = h + 4;
+        if (ev != 0 && ev != 2 && ev <= 16 && bl_too_short(ev, b, rl)) { *status = OR_BL_SHORT; break; }
         off += 4 + rl;
         uint32_t n = 0;
         const uint32_t sec = get32(b), usec = get32(b + 4);
@@ -1865,7 +1900,14 @@ uint64_t or_convert_binary_log(const uint8_t* file, uint64_t nbytes, int log_rx,
             or_fields f;
             or_unpack(b + idx, rl >= idx ? rl - idx : 0, &f);
             nrec++;
-            if (!f.ok) continue;
+            if (!f.ok) {
+                /* Unpack's result is ignored (:1606-1607): the line shows the fresh MgenMsg's
+                 * members, tx_time = the event time set before Unpack unless Unpack got to
+                 * the base fields (every error but LENGTH / VERSION) */
+                if (f.err == 3 || f.err == 1) { f.tx_sec = sec; f.tx_usec = usec; }
+                f.err = 0;
+                f.ok = 1;
+            }
             if (log_rx) {
                 n = or_log_recv_text(&f, b + idx, &src, sec, usec, proto, flush ? 1 : 0, opts,
                                      line);
@@ -1889,7 +1931,7 @@ uint64_t or_convert_binary_log(const uint8_t* file, uint64_t nbytes, int log_rx,
             or_fields f;
             or_unpack(b + idx, rl - idx, &f);    /* the reference passes recordLength */
             nrec++;
-            if (!f.ok) continue;
+            if (!f.ok) { f.err = 0; f.ok = 1; }  /* logged anyway, fresh members (:1624-1625) */
             n = bl_send_line(&f, proto, mml, opts, line);
             pc_emit(out, cap, &pos, line, n);
             continue;

@@ -288,7 +288,9 @@ int      or_data_walk(const uint8_t* pay, uint32_t len, int controller, uint32_t
 /* ---- pcap2mgen (pcap2mgen.cpp:252-482) ----
  * or_pcap_frame: one pcap record (16-byte header + data) -> the UDP payload's offset from the
  * record header and length, IP source + UDP source port, TTL / hop limit, timestamp.  Returns
- * 0 UDP, 1 bad Ethernet frame, 2 not IP, 3 bad IP, 4 not UDP, 5 truncated capture
+ * 0 UDP, 1 bad Ethernet frame, 2 not IP, 3 bad IP, 4 not UDP, 5 truncated capture, 7 snapped
+ * (a UDP datagram cut by the snapshot length with its header and >= 28 payload bytes
+ * captured: or_pcap2mgen unpacks the captured bytes zero-extended to the UDP length)
  * (flags: 1 nanosecond file, 2 swapped byte order).
  * or_pcap2mgen: the whole main loop over a file image -> the log text (analytic REPORT lines,
  * RECV lines when log_rx, received REPORT lines), written to out while it fits `cap`;

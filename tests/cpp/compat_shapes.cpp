@@ -8,18 +8,29 @@
 //   analytic Mgen::UpdateRecvAnalytics        src/common/mgen.cpp:1027-1067
 //   batch    the same three through MgenMsg::PackBatch / UnpackBatch and
 //            MgenAnalytic::UpdateBatch (one GPU round trip per batch)
+//   logging  (with <log dir>) the same sends and receives logged through the shim's
+//            MgenMsg::LogSendEvent / LogRecvEvent / LogRecvError (text and binary, as
+//            MgenTransport::LogEvent calls them, mgenTransport.cpp:328-482), the binary log
+//            converted back by MgenMsg::ConvertBinaryLog, Mgen::UpdateRecvAnalytics' whole
+//            body (mgen.cpp:1027-1068) incl. MgenAnalytic::Log and GetWindowEnd, and the TCP
+//            connection / DREC events
 //
-// usage: compat_shapes <input file> <output file>
+// usage: compat_shapes <input file> <output file> [<log dir>]
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
+#include <string>
 #include <vector>
 
 #include "mgenAnalytic.h"
 #include "mgenMsg.h"
 #include "mgenPayload.h"
+#ifdef MGENX_WITH_PROTOLIB  // inside an MGEN build these come from the application
+#include "mgen.h"
+#include "mgenEvent.h"
+#endif
 
 struct Reader {
   std::vector<uint8_t> buf;
@@ -174,6 +185,12 @@ int main(int argc, char** argv) {
 
   FILE* out = fopen(argv[2], "wb");
   if (!out) return 2;
+  const std::string logdir = argc > 3 ? argv[3] : "";
+  auto lopen = [&](const char* name) -> FILE* {
+    return logdir.empty() ? nullptr : fopen((logdir + "/" + name).c_str(), "wb");
+  };
+  FILE* send_txt = lopen("send.txt");
+  FILE* send_bin = lopen("send.bin");
 
   // ---- send shape, message by message (mgenTransport.cpp:1011-1031), checksum off / on
   for (int ck = 0; ck < 2; ck++) {
@@ -193,6 +210,11 @@ int main(int argc, char** argv) {
         theMsg.WriteChecksum(txChecksum, (unsigned char*)txBuffer, (UINT32)len);
       memcpy(slab.data() + offs[i], txBuffer, len);  // socket.SendTo(txBuffer, len, dst)
       lens[i] = len;
+      if (ck && send_txt) {  // LogEvent(SEND_EVENT, &theMsg, txTime, txBuffer) (:1060, 328-350)
+        theMsg.SetSrcAddr(make_addr(1, 4, 5001, (const uint8_t*)"\x7f\x00\x00\x01"));
+        theMsg.LogSendEvent(send_txt, false, false, txBuffer, false, theMsg.GetTxTime());
+        theMsg.LogSendEvent(send_bin, true, false, txBuffer, false, theMsg.GetTxTime());
+      }
     }
     fwrite(lens.data(), 4, n_desc, out);
     fwrite(slab.data(), 1, slab_bytes, out);
@@ -229,10 +251,20 @@ int main(int argc, char** argv) {
   }
 
   // ---- receive shape, datagram by datagram (mgenTransport.cpp:955-975), force off / on
+  FILE* recv_txt = lopen("recv.txt");
+  FILE* recv_bin = lopen("recv.bin");
+  FILE* recv_local = lopen("recv_local.txt");
+  FILE* recv_epoch = lopen("recv_epoch.txt");
+  FILE* recv_ok = lopen("recv_ok.bin");  // a binary log of the good records, for ConvertBinaryLog
+  if (recv_ok) {
+    const char hdr[] = "mgen version=5.1.1 type=binary_log\n";
+    fwrite(hdr, 1, sizeof(hdr), recv_ok);  // with its NUL (mgenMsg.cpp:1452-1463)
+  }
   for (int force = 0; force < 2; force++) {
     std::vector<OutFields> o(n_unp);
     for (uint32_t i = 0; i < n_unp; i++) {
       UINT32 alignedBuffer[65536 / 4];
+      memset(alignedBuffer, 0, sizeof(alignedBuffer));
       const unsigned int len = ulens[i];
       memcpy(alignedBuffer, uslab + uoffs[i], len);
       char* buffer = (char*)alignedBuffer;
@@ -252,6 +284,29 @@ int main(int argc, char** argv) {
         }
       }
       fields_of(theMsg, ok, alignedBuffer, o[i]);
+      if (force == 0 && recv_txt) {
+        // MgenUdpTransport::OnEvent's logging (mgenTransport.cpp:976-994 -> LogEvent)
+        struct timeval now;
+        now.tv_sec = 1700000001 + i / 1000;
+        now.tv_usec = (i * 37) % 1000000;
+        if (!ok || theMsg.GetError()) {
+          theMsg.LogRecvError(recv_txt, false, false, false, now);
+          theMsg.LogRecvError(recv_bin, true, false, false, now);
+        } else {
+          theMsg.SetProtocol(UDP);
+          theMsg.LogRecvEvent(recv_txt, false, false, true, true, true, alignedBuffer, false, -1, now);
+          if (i < 64) {  // local time (TZ of the test) and epoch timestamps
+            theMsg.LogRecvEvent(recv_local, false, true, true, true, true, alignedBuffer, false, -1, now);
+            Mgen::SetEpochTimestamp(true);
+            theMsg.LogRecvEvent(recv_epoch, false, false, true, true, true, alignedBuffer, false, -1, now);
+            Mgen::SetEpochTimestamp(false);
+          }
+          UINT32 copy[65536 / 4];
+          memcpy(copy, alignedBuffer, sizeof(copy));
+          theMsg.LogRecvEvent(recv_bin, true, false, true, true, true, alignedBuffer, false, -1, now);
+          theMsg.LogRecvEvent(recv_ok, true, false, true, true, true, copy, false, -1, now);
+        }
+      }
     }
     fwrite(o.data(), sizeof(OutFields), n_unp, out);
   }
@@ -298,6 +353,8 @@ int main(int argc, char** argv) {
   }
 
   // ---- analytics shape (mgen.cpp:1034-1067), record by record, then as one batch
+  FILE* an_log = lopen("analytic.txt");
+  FILE* an_end = lopen("window_end.bin");
   for (int batch = 0; batch < 2; batch++) {
     MgenAnalyticTable table;
     std::vector<MgenAnalytic*> owned;
@@ -349,6 +406,7 @@ int main(int argc, char** argv) {
         continue;
       }
       const MgenAnalytic::Report& report = analytic->GetReport(rx[i]);
+      if (an_log) analytic->Log(an_log, rx[i], rx[i], false);  // mgen.cpp:1067
       o.updated = 1;
       o.duration = analytic->GetReportDuration();
       o.rate = analytic->GetReportRateAverage();
@@ -360,6 +418,13 @@ int main(int argc, char** argv) {
       memcpy(o.report_item, report.GetBuffer(), report.GetLength() < sizeof(o.report_item) ? report.GetLength() : sizeof(o.report_item));
     }
     fwrite(rep.data(), sizeof(OutReport), n_an, out);
+    if (!batch && an_end) {  // MgenAnalytic::GetWindowEnd of every flow, in creation order
+      for (MgenAnalytic* a : owned) {
+        const ProtoTime& e = a->GetWindowEnd();
+        const int64_t v[2] = {(int64_t)e.GetTimeVal().tv_sec, (int64_t)e.GetTimeVal().tv_usec};
+        fwrite(v, 8, 2, an_end);
+      }
+    }
     for (MgenAnalytic* a : owned) delete a;
   }
 
@@ -384,6 +449,59 @@ int main(int argc, char** argv) {
             (unsigned)cmd.GetStatus(17), (unsigned)cmd.GetStatus(5), cmd.GetMaxFlowId());
   }
   fclose(out);
+  if (!logdir.empty()) {
+    for (FILE* f : {send_txt, send_bin, recv_txt, recv_bin, recv_local, recv_epoch, recv_ok, an_log,
+                    an_end})
+      fclose(f);
+    // ConvertBinaryLog of the good records' binary log (mgenMsg.cpp:1417-1900)
+    Mgen mgen;
+    FILE* conv = lopen("convert.txt");
+    mgen.SetLogFile(conv);
+    const bool cok = MgenMsg().ConvertBinaryLog((logdir + "/recv_ok.bin").c_str(), mgen);
+    fprintf(conv, "#%d\n", cok ? 1 : 0);
+    fclose(conv);
+    // TCP connection events (mgenMsg.cpp:741-944) and DREC events (:1243-1415)
+    FILE* ct = lopen("conn.txt");
+    FILE* cb = lopen("conn.bin");
+    const LogEventType evs[] = {ACCEPT_EVENT, ON_EVENT, CONNECT_EVENT, DISCONNECT_EVENT,
+                                RECONNECT_EVENT, SHUTDOWN_EVENT, OFF_EVENT};
+    struct timeval t0;
+    t0.tv_sec = 1700000123;
+    t0.tv_usec = 4567;
+    for (int host = 0; host < 2; host++)
+      for (int client = 0; client < 2; client++)
+        for (LogEventType ev : evs) {
+          MgenMsg m;
+          m.SetFlowId(7 + host);
+          m.SetDstAddr(make_addr(1, 4, 5000, (const uint8_t*)"\x0a\x00\x00\x01"));
+          m.SetSrcAddr(make_addr(1, 4, 5001, (const uint8_t*)"\x0a\x00\x00\x02"));
+          if (host) m.SetHostAddr(make_addr(2, 16, 6000, (const uint8_t*)"\x20\x01\x0d\xb8\0\0\0\0\0\0\0\0\0\0\0\x01"));
+          m.LogTcpConnectionEvent(ct, false, false, false, ev, client != 0, t0);
+          m.LogTcpConnectionEvent(cb, true, false, false, ev, client != 0, t0);
+        }
+    fclose(ct);
+    fclose(cb);
+    FILE* dt = lopen("drec.txt");
+    FILE* db = lopen("drec.bin");
+    for (int bin = 0; bin < 2; bin++) {
+      Mgen dm;
+      dm.SetLogFile(bin ? db : dt);
+      dm.SetLogBinary(bin != 0);
+      DrecEvent ev;
+      ev.SetProtocol(UDP);
+      MgenMsg().LogDrecEvent(LISTEN_EVENT, &ev, 5000, dm);
+      ev.SetProtocol(TCP);
+      MgenMsg().LogDrecEvent(IGNORE_EVENT, &ev, 5001, dm);
+      ev.SetGroupAddress(make_addr(1, 4, 0, (const uint8_t*)"\xe0\x01\x02\x03"));
+      ev.SetInterface("eth0");
+      MgenMsg().LogDrecEvent(JOIN_EVENT, &ev, 5002, dm);
+      ev.SetSourceAddress(make_addr(1, 4, 0, (const uint8_t*)"\x0a\x00\x00\x09"));
+      ev.SetInterface(nullptr);
+      MgenMsg().LogDrecEvent(LEAVE_EVENT, &ev, 0, dm);
+    }
+    fclose(dt);
+    fclose(db);
+  }
   printf("compat_shapes: %u sends x 3, %u receives x 3, %u analytic updates x 2\n", n_desc, n_unp,
          n_an);
   return 0;

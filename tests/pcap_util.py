@@ -144,3 +144,17 @@ def capture(O, seed=7, n=600, link=1, nsec=False, swapped=False, v6_frac=0.3):
         rec = (sec, frac, frame) if caplen is None else (sec, frac, frame, caplen, len(frame))
         recs.append(rec)
     return pcap(recs, link=link, nsec=nsec, swapped=swapped)
+
+
+def snap(file: bytes, snaplen: int) -> bytes:
+    """The same capture as `tcpdump -s snaplen` would have written it: every record's data
+    cut to snaplen bytes, its wire length kept (native-order, microsecond files)."""
+    out = [file[:16] + struct.pack("<I", snaplen) + file[20:24]]
+    off = 24
+    while off + 16 <= len(file):
+        sec, frac, cap, wire = struct.unpack("<IIII", file[off:off + 16])
+        data = file[off + 16:off + 16 + cap]
+        c = min(cap, snaplen)
+        out.append(struct.pack("<IIII", sec, frac, c, wire) + data[:c])
+        off += 16 + cap
+    return b"".join(out)

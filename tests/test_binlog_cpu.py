@@ -108,3 +108,35 @@ def test_index_matches_oracle_on_mixed_logs():
     _, st, n = O.convert_binary_log(log)
     assert info.status == st == 0 and info.n_records == n == len(parts)
     assert info.consumed == len(log)
+
+
+def _cut(rec: bytes, rl: int) -> bytes:
+    """A record whose recordLength says rl (body truncated to rl bytes)."""
+    import struct
+    return rec[:2] + struct.pack(">H", rl) + rec[4:4 + rl]
+
+
+def short_for_type_cases():
+    """Records too short for the fields their type reads (the device formatters
+    must never read past a record): (label, record)."""
+    v4 = bytes([10, 0, 0, 9])
+    recv = B.recv_records(O, n=1)[0]
+    alen = recv[4 + 11]
+    join = B.join(3, 4, bytes([224, 1, 2, 3]), 5000, b"eth0")
+    conn = B.conn(10, 5, 6, v4, 5001, 4000, 3)
+    return [("recv_addr", _cut(recv, 12 + alen - 1)), ("recv_hdr", _cut(recv, 11)),
+            ("join_name", _cut(join, len(join) - 4 - 2)), ("join_len", _cut(join, 12 + 4)),
+            ("conn", _cut(conn, 18 + 4 - 1)), ("listen", _cut(B.listen(1, 2, 1, 7), 11)),
+            ("start", _cut(B.start(1, 1), 7))]
+
+
+@pytest.mark.parametrize("label", [c[0] for c in short_for_type_cases()])
+def test_short_for_type_records_stop(label):
+    import mgen_amd
+    bad = dict(short_for_type_cases())[label]
+    parts = [B.start(1, 2), B.listen(1, 3, 1, 7)]
+    log = B.binlog(parts + [bad, B.stop(9, 9)])
+    text, st, n = O.convert_binary_log(log)
+    assert st == 4 and n == 2 and text.count(b"\n") == 2
+    offs, info = mgen_amd.binlog_index(log)
+    assert info.status == 4 and info.n_records == 2 and len(offs) == 2

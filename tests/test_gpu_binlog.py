@@ -74,8 +74,8 @@ def test_convert_gpu_written_binary_log(torch, oracle):
     try:
         f = gold["unpack_fields_udp"]
         # records whose stored hdr + payload bytes hold a whole header (>= 28 bytes): a
-        # shorter stored message fails Unpack in the converter (the reference then logs a
-        # line of a fresh MgenMsg's fields; here no line -- documented in mgenx.h)
+        # shorter stored message fails Unpack in the converter, which then logs a fresh
+        # MgenMsg's fields (test_convert_logs_rejected_stored_messages)
         keep = (f["err"] == 0) & (f["hdr_len"].astype(int) + f["payload_len"] >= 28)
         idx = np.nonzero(keep)[0][:2000]
         slab = to_device(gold["unpack_slab"]).view(torch.uint8)
@@ -101,3 +101,52 @@ def test_convert_gpu_written_binary_log(torch, oracle):
         assert conv_recv == direct, _diff(conv_recv, direct)
     finally:
         eng.close()
+
+
+def test_convert_stops_at_records_short_for_their_type(torch, oracle):
+    """A truncated final RECV / JOIN / ON record (recordLength too small for the fields its
+    type reads) ends the conversion as a short read; nothing is read past the record."""
+    import mgen_amd
+    from test_binlog_cpu import short_for_type_cases
+    rng = np.random.default_rng(4)
+    parts = B.recv_records(oracle, n=40) + B.events(rng)
+    for label, bad in short_for_type_cases():
+        log = B.binlog(parts + [bad])
+        want, st, n = oracle.convert_binary_log(log)
+        got, info = mgen_amd.convert_binary_log(log)
+        assert st == info.status == 4 and n == info.n_records == len(parts), label
+        assert got == want, label
+
+
+def test_convert_logs_rejected_stored_messages(torch, oracle):
+    """RECV records whose stored message is shorter than a header (hdr + payload < 28: the
+    converter's Unpack rejects it) are logged anyway, from a fresh MgenMsg's members with the
+    event time as tx time (mgenMsg.cpp:1601-1607), as are SEND records whose stored message
+    fails (:1612-1625).  Device == oracle, byte for byte."""
+    import struct
+    import mgen_amd
+    from streams import golden
+    gold = golden()
+    f = gold["unpack_fields_udp"]
+    short = np.nonzero((f["err"] == 0) & (f["hdr_len"].astype(int) + f["payload_len"] < 28))[0]
+    assert short.size > 5
+    src = np.zeros(short.size, mgen_amd.ADDR_DTYPE)
+    src["type"], src["len"], src["port"] = 1, 4, 4321
+    src["addr"][:, :4] = [192, 168, 1, 7]
+    rx_s = np.full(short.size, 1_700_000_123, np.uint32)
+    rx_u = np.arange(short.size, dtype=np.uint32) * 11
+    recs = oracle.log_recv_binary(f[short], gold["unpack_slab"], gold["unpack_offs"][short], src,
+                                  rx_s, rx_u, protocol=1)
+    # SEND records (UDP and TCP) whose message has a bad version / dst type / is 12 bytes
+    sends = b""
+    for proto, body in ((1, bytes([0, 64, 3]) + bytes(61)), (2, struct.pack(">I", 9000) +
+                        bytes([0, 64, 2, 4]) + bytes(16) + bytes([0, 0, 9, 4]) + bytes(40)),
+                        (3, bytes(12))):
+        sends += struct.pack(">BBH", 3, proto, len(body)) + body
+    rng = np.random.default_rng(9)
+    log = B.binlog([recs, sends] + B.events(rng))
+    want, st, n = oracle.convert_binary_log(log)
+    got, info = mgen_amd.convert_binary_log(log)
+    assert st == info.status == 0 and n == info.n_records
+    assert want.count(b" RECV ") == short.size and want.count(b" SEND ") == 3
+    assert got == want, _diff(got, want)

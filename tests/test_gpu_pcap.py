@@ -226,3 +226,23 @@ def test_pcap2mgen_cli(oracle, tmp_path):
                        timeout=120)
     assert r.returncode == 0, r.stderr
     assert r.stdout == oracle.pcap2mgen(f, analytics=True, log_rx=False)[0]
+
+
+@pytest.mark.parametrize("snaplen,analytics", [(128, True), (96, False), (70, True)])
+def test_snaplen_capture_matches_oracle(eng, oracle, snaplen, analytics):
+    """A capture taken with a snapshot length (tcpdump -s N): the reference parses each frame
+    by its wire length and Unpacks the UDP payload from the captured bytes, so every packet
+    whose UDP header and MIN_SIZE payload bytes were captured still logs its RECV line
+    (payload bytes past the capture read as zero here: mgenx_pcap_snap); shorter captures
+    are skipped.  Device pipeline == oracle, byte for byte."""
+    import mgen_amd
+    from mgen_amd.pcap import Pcap2Mgen
+    f = P.snap(P.capture(oracle, seed=40 + snaplen, n=600), snaplen)
+    _, info = mgen_amd.pcap_index(f)
+    assert info.snap_bytes > 0
+    want, st = oracle.pcap2mgen(f, analytics=analytics, window=0.05)
+    assert (st == 7).sum() > 100, np.bincount(st)
+    got = Pcap2Mgen(eng, analytics=analytics, window=0.05).run(f)
+    assert got == want, _diff(got, want)
+    if snaplen == 128:
+        assert want.count(b" RECV ") > 300

@@ -45,8 +45,8 @@ def test_frame_ipv6_vlan_sll_and_options():
 
 
 @pytest.mark.parametrize("case,status", [
-    ("arp", 2), ("tcp", 4), ("bad_total", 3), ("ver5", 3), ("trunc", 5), ("oversize", 1),
-    ("udp_len_big", 4), ("runt", 1)])
+    ("arp", 2), ("tcp", 4), ("bad_total", 3), ("ver5", 3), ("trunc", 7), ("trunc_hdr", 5),
+    ("oversize", 1), ("udp_len_big", 4), ("runt", 1)])
 def test_frame_skips(case, status):
     pay = bytes(64)
     ip = P.ipv4(P.udp(pay, 1, 2), SRC4, DST4)
@@ -59,9 +59,13 @@ def test_frame_skips(case, status):
         fr = P.eth(P.ipv4(P.udp(pay, 1, 2), SRC4, DST4, total=3000))
     elif case == "ver5":
         fr = P.eth(bytes([0x50]) + ip[1:], etype=0x0800)
-    elif case == "trunc":
+    elif case == "trunc":          # snapped: UDP header + >= 28 payload bytes captured
         fr = P.eth(ip)
         cap = len(fr) - 5
+        wire = len(fr)
+    elif case == "trunc_hdr":      # cut inside the first 28 payload bytes: skipped
+        fr = P.eth(ip)
+        cap = 14 + 20 + 8 + 27
         wire = len(fr)
     elif case == "oversize":
         fr = P.eth(P.ipv4(P.udp(bytes(4100), 1, 2), SRC4, DST4))
@@ -114,8 +118,8 @@ def test_oracle_main_loop_shapes():
     lines = text.split(b"\n")[:-1]
     assert all(LINE.match(l) for l in lines)
     recv = [l for l in lines if b" RECV " in l]
-    # one RECV line per UDP packet whose payload Unpack accepts
-    n_udp = int((st == 0).sum())
+    # one RECV line per UDP packet (snapped ones included) whose payload Unpack accepts
+    n_udp = int(((st == 0) | (st == 7)).sum())
     assert 0 < len(recv) <= n_udp
     assert all(b" ttl>" in l and b" gps>" in l and b" data>" not in l for l in recv)
     # rxlog off: only the REPORT lines of carried reports remain
