@@ -34,7 +34,7 @@ N_REC = 1 << 20
 REC = 1024
 ALGO_BYTES = N_REC * REC + N_REC * 32
 PEAK_HBM_GBPS = 8000.0   # MI355X_MICROARCH.md chip table (spec); 6.29 TB/s measured copy
-ROUND = "r02"
+ROUND = "r03"
 
 
 def cpu_baseline(budget_s=6.0):
@@ -77,7 +77,96 @@ def cpu_baseline(budget_s=6.0):
             "mmsg_per_s": round(n1 / t1 / 1e6, 4),
             "nproc": nproc, "cores_available": avail,
             "all_cores": {"threads": threads, "value": round(gbps_all, 3), "unit": "GB/s",
-                          "records": nall, "ms_median_of_5": round(tall * 1e3, 1)}}
+                          "records": nall, "ms_median_of_5": round(tall * 1e3, 1),
+                          "note": "threads = min(cores available, 16): a one-GPU box's CPU "
+                                  "share is 16 (nproc counts the whole host)"},
+            "configs": cpu_baseline_configs(threads)}
+
+
+def _med5(fn):
+    fn()
+    ts = []
+    for _ in range(5):
+        t = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t)
+    return sorted(ts)[2]
+
+
+def cpu_baseline_configs(threads):
+    """The oracle (C restatement, byte-table CRC as mgenMsg.cpp:538-539) on the configs the GPU
+    extras run, 1 thread and `threads` threads, median of 5 each, on bounded samples:
+      config 3: UDP send sequence (Pack + checksum, 16-B DATA payload, zero fill) and the
+                receive path (Unpack + CRC check) over U{64..1472} records packed back to back;
+      config 4: MgenAnalytic::Update over POISSON flows (1024 flows, 256-B messages);
+      config 5: TCP framing (GetRxNumBytes / OnRecvMsg: sequential by construction) with
+                Unpack + CRC per record, then the framed records' Unpack + CRC spread over
+                the threads (framing stays one thread)."""
+    from oracle import oracle as O
+    from mgen_amd.workloads import poisson_flows, udp_mixed, make_templates
+    out = {}
+    # ---- config 3
+    n = 131072
+    tmpl, pool, desc, offs, sizes = udp_mixed(n, 64, 1472, 64,
+                                              payload_hex="00112233445566778899aabbccddeeff")
+    total = int(offs[-1] + sizes[-1])
+    pack_b, unpack_b = n * 20 + n * 16 + total, total + n * 32
+    res = {}
+    for nt in (1, threads):
+        tp = _med5(lambda: O.udp_pack_batch_mt(tmpl, desc, pool, total, rec_off=offs, nthreads=nt))
+        slab, _ = O.udp_pack_batch_mt(tmpl, desc, pool, total, rec_off=offs, nthreads=nt)
+        tu = _med5(lambda: O.udp_recv_batch(slab, n, rec_off=offs, rec_len=sizes, nthreads=nt))
+        res[nt] = {"pack_gbps": round(pack_b / tp / 1e9, 3), "unpack_gbps": round(unpack_b / tu / 1e9, 3),
+                   "combined_gbps": round((pack_b + unpack_b) / (tp + tu) / 1e9, 3)}
+    out["config3_pack_unpack"] = {"records": n, "bytes": total, "threads_1": res[1],
+                                  f"threads_{threads}": res[threads]}
+    # ---- config 4
+    d = poisson_flows(1 << 20, 1024, mean_gap_us=1000)
+    idx = (d["flow_id"] - 1).astype(np.uint32)
+    nr = len(idx)
+    res = {}
+    for nt in (1, threads):
+        t = _med5(lambda: O.flow_reduce_batch_mt(1024, idx, d["seq"], d["tx_sec"], d["tx_usec"],
+                                                 d["msg_len"], d["rx_sec"], d["rx_usec"],
+                                                 nthreads=nt))
+        res[nt] = {"mrec_per_s": round(nr / t / 1e6, 2), "ms": round(t * 1e3, 1)}
+    out["config4_flow_reduce"] = {"records": nr, "flows": 1024, "threads_1": res[1],
+                                  f"threads_{threads}": res[threads]}
+    # ---- config 5: 4096 x 16 KiB TCP records (checksum on), built by the oracle's TCP send path
+    m = 4096
+    tm, pl = make_templates(64)
+    dsc = np.zeros(m, O.DESC_DTYPE)
+    dsc["tmpl"] = np.arange(m) % 64
+    dsc["seq_num"] = np.arange(m)
+    dsc["tx_sec"] = 1_700_000_000
+    dsc["tx_usec"] = np.arange(m)
+    dsc["flags"] = 4
+    stream = O.tcp_tx_batch(tm, dsc, np.full(m, 16384, np.uint32), pl, checksum=True)
+    L = O.lib()
+    P = ctypes.c_void_p
+    st_offs = np.zeros(m + 1, np.uint64)
+    st_lens = np.zeros(m + 1, np.uint32)
+    fields = np.zeros(m + 1, O.FIELDS_DTYPE)
+    cons, stat = ctypes.c_uint64(0), ctypes.c_int(0)
+
+    def scan(cap):
+        return L.or_tcp_scan(P(stream.ctypes.data), stream.size, 0, P(st_offs.ctypes.data),
+                             P(st_lens.ctypes.data), P(fields.ctypes.data), cap,
+                             ctypes.byref(cons), ctypes.byref(stat))
+    assert scan(m + 1) == m and int(fields["err"][:m].sum()) == 0
+    t1 = _med5(lambda: scan(m + 1))   # framing + Unpack + CRC, one thread (the reference)
+    tf = _med5(lambda: scan(0))       # framing alone
+    so, sl = st_offs[:m].copy(), st_lens[:m].copy()
+    tu = _med5(lambda: O.udp_recv_batch(stream, m, rec_off=so, rec_len=sl, tcp=True,
+                                        nthreads=threads))
+    b = stream.size
+    out["config5_tcp_scan_unpack"] = {
+        "records": m, "bytes": int(b),
+        "threads_1": {"gbps": round(b / t1 / 1e9, 3), "ms": round(t1 * 1e3, 1)},
+        f"threads_{threads}": {"gbps": round(b / (tf + tu) / 1e9, 3),
+                               "ms": round((tf + tu) * 1e3, 1),
+                               "note": "framing on one thread, Unpack + CRC on all"}}
+    return out
 
 
 def load_traffic():
@@ -85,8 +174,13 @@ def load_traffic():
     (FETCH_SIZE / WRITE_SIZE, calibrated; scripts/pmc.sh -> profiles/traffic_<round>.json).
     rocprofv3 counters cannot be collected inside this process, so the figure is read from
     that file and labelled with its source."""
-    path = os.path.join(ROOT, "profiles", f"traffic_{ROUND}.json")
-    if not os.path.exists(path):
+    path = None
+    for rnd in (ROUND, "r02"):   # this round's PMC passes, else the last round's
+        p = os.path.join(ROOT, "profiles", f"traffic_{rnd}.json")
+        if os.path.exists(p):
+            path = p
+            break
+    if path is None:
         return None, None
     try:
         d = json.load(open(path))

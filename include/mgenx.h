@@ -549,11 +549,14 @@ int mgenx_log_recv_text(mgenx_ctx* ctx, const uint8_t* dev_slab, const uint64_t*
  * protocol, BE length, BE rx time, BE source port, source type/length/address) followed, for
  * RECV, by hdr_len + payload_len message bytes with CHECKSUM cleared in the flags byte
  * (the hdr_len extended column is also required); RERR ends with the BE error code.
- * Message bytes past slab_bytes are written as zero (the reference's stale receive buffer).
+ * The message bytes are the receive buffer's: the record's dev_rec_len[i] bytes (the
+ * recvfrom length; when dev_rec_len is NULL, its msg_len field), then zeros where the
+ * reference's buffer holds stale bytes; bytes past slab_bytes are zero too.
  * dev_rec_pos has the same meaning as dev_line_off.  The file header line the reference
  * writes once per log file is the caller's. */
 int mgenx_log_recv_binary(mgenx_ctx* ctx, const uint8_t* dev_slab, uint64_t slab_bytes,
-                          const uint64_t* dev_rec_off, uint64_t stride, const mgenx_cols* cols,
+                          const uint64_t* dev_rec_off, uint64_t stride,
+                          const uint32_t* dev_rec_len, const mgenx_cols* cols,
                           const mgenx_addr* dev_src, const uint32_t* dev_rx_sec,
                           const uint32_t* dev_rx_usec, uint32_t n, int protocol,
                           uint8_t* dev_out, uint64_t out_cap, uint64_t* dev_rec_pos,

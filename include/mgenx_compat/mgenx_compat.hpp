@@ -358,7 +358,7 @@ class Engine {
     const size_t o_lon = L.Add(n * 4u), o_alt = L.Add(n * 4u), o_po = L.Add(n * 4u);
     const size_t o_src = L.Add(n * sizeof(mgenx_addr)), o_rxs = L.Add(n * 4u);
     const size_t o_rxu = L.Add(n * 4u), o_ttl = L.Add(n * 4u), o_off = L.Add(n * 8u);
-    const size_t o_slab = L.Add(slab + 16), in_bytes = L.size;
+    const size_t o_len = L.Add(n * 4u), o_slab = L.Add(slab + 16), in_bytes = L.size;
     const size_t o_pos = L.Add((n + 1) * 8u), o_text = L.Add(cap);
     Reserve(L.size);
     uint8_t* h = host_;
@@ -383,6 +383,7 @@ class Engine {
       ((int32_t*)(h + o_ttl))[i] = r.ttl;
       any_ttl |= r.ttl >= 0;
       ((uint64_t*)(h + o_off))[i] = s;
+      ((uint32_t*)(h + o_len))[i] = r.msg_bytes;
       if (r.msg_bytes) memcpy(h + o_slab + s, r.msg, r.msg_bytes);
       s += Align(r.msg_bytes, 16);
     }
@@ -407,7 +408,8 @@ class Engine {
     const uint64_t* off = (const uint64_t*)(g + o_off);
     uint64_t* pos = (uint64_t*)(g + o_pos);
     if (binary)
-      Check(mgenx_log_recv_binary(ctx_, g + o_slab, slab + 16, off, 0, &c, src, rxs, rxu, n,
+      Check(mgenx_log_recv_binary(ctx_, g + o_slab, slab + 16, off, 0, (const uint32_t*)(g + o_len),
+                                  &c, src, rxs, rxu, n,
                                   protocol, g + o_text, cap, pos, stream_),
             "mgenx_log_recv_binary");
     else

@@ -121,8 +121,8 @@ def load(diag: bool = False):
     L.mgenx_flow_export.argtypes = [P, P, u32, P, P]
     L.mgenx_log_recv_text.argtypes = [P, P, P, u64, ctypes.POINTER(MgenxCols), P, P, P, P, u32,
                                       i32, u32, P, u64, P, P]
-    L.mgenx_log_recv_binary.argtypes = [P, P, u64, P, u64, ctypes.POINTER(MgenxCols), P, P, P,
-                                        u32, i32, P, u64, P, P]
+    L.mgenx_log_recv_binary.argtypes = [P, P, u64, P, u64, P, ctypes.POINTER(MgenxCols), P, P,
+                                        P, u32, i32, P, u64, P, P]
     _libs[path] = L
     return L
 
@@ -252,8 +252,9 @@ class Engine:
         raise MgenxError("mgenx_log_recv_text: text did not fit")
 
     def log_recv_binary(self, slab, n, cols, src, rx_sec, rx_usec, *, rec_off=None, stride=0,
-                        protocol=1, slab_bytes=None, cap=None):
-        """Binary RECV / RERR log records (mgenx_log_recv_binary).  Returns (bytes tensor,
+                        rec_len=None, protocol=1, slab_bytes=None, cap=None):
+        """Binary RECV / RERR log records (mgenx_log_recv_binary; rec_len: the received
+        lengths, else each record's msg_len bounds its bytes).  Returns (bytes tensor,
         record positions tensor of n + 1)."""
         torch = self.torch
         dev = slab.device
@@ -264,7 +265,8 @@ class Engine:
             out = torch.empty(max(cap, 1), dtype=torch.uint8, device=dev)
             cs = self._cols_struct(cols)
             rc = self.lib.mgenx_log_recv_binary(self.ctx, _ptr(slab), sb, _ptr(rec_off), stride,
-                                                ctypes.byref(cs), _ptr(src), _ptr(rx_sec),
+                                                _ptr(rec_len), ctypes.byref(cs), _ptr(src),
+                                                _ptr(rx_sec),
                                                 _ptr(rx_usec), n, protocol, _ptr(out), cap,
                                                 _ptr(pos), _stream(self.device))
             self._check(rc, "mgenx_log_recv_binary")

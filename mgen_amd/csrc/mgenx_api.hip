@@ -77,6 +77,7 @@ extern "C" int mgenx_pcap_snap_run(uint8_t* dev_buf, uint64_t file_bytes, uint64
 extern "C" size_t mgenx_pcap_snap_scan_bytes(uint32_t n);
 extern "C" int mgenx_log_recv_run(void* ws, bool binary, const uint8_t* slab,
                                   uint64_t slab_bytes, const uint64_t* rec_off,
+                                  const uint32_t* rec_len,
                                        uint64_t stride, const mgenx_cols* cols,
                                        const mgenx_addr* src, const uint32_t* rx_sec,
                                        const uint32_t* rx_usec, const int32_t* ttl, uint32_t n,
@@ -529,13 +530,13 @@ int mgenx_pack_tcp(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl, const uint32
     ctx->tcp_host_dev = static_cast<uint64_t*>(dp);
   }
   // workspace: bytes[n+1], nfrag[n], cub; per round: fd, foff, fbuf, ff, plen, crc, state x2,
-  // roff[3n], rlen[3n], acrc[3n]
+  // acrc[3n]
   size_t cub_bytes = 0;
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, cub_bytes, (const uint64_t*)nullptr,
                                          (uint64_t*)nullptr, (int)(n + 1), s);
   const size_t b8 = a256((size_t)(n + 1) * 8), b4 = a256((size_t)n * 4);
   const size_t need = b8 + b4 + a256(cub_bytes) + a256((size_t)n * sizeof(mgenx_pack_desc)) +
-                      b8 + 4 * b4 + 2 * b4 + 3 * b8 + 3 * b4 + 3 * b4;
+                      b8 + 4 * b4 + 2 * b4 + 3 * b4;
   if (ctx->tcp_ws_bytes < need) {
     if (ctx->tcp_ws) hipFree(ctx->tcp_ws);
     ctx->tcp_ws = nullptr;
@@ -555,8 +556,6 @@ int mgenx_pack_tcp(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl, const uint32
   uint32_t* plen = (uint32_t*)take(b4);
   uint32_t* crc = (uint32_t*)take(b4);
   uint32_t* st[2] = {(uint32_t*)take(b4), (uint32_t*)take(b4)};
-  uint64_t* roff = (uint64_t*)take(3 * b8);
-  uint32_t* rlen = (uint32_t*)take(3 * b4);
   uint32_t* acrc = (uint32_t*)take(3 * b4);
   // plan: bytes per message, fragments; offsets by an exclusive scan (the message offsets
   // are the caller's array: n + 1 entries are not assumed, the scan runs in the workspace)
@@ -587,9 +586,10 @@ int mgenx_pack_tcp(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl, const uint32
                          foff, 0, fbuf, nullptr, plen, crc, st[r & 1], opts | MGENX_PACK_RAW,
                          fill_time, stream);
     if (rc != MGENX_OK) return rc;
-    if ((e = mgenx::launch_tcp_tail(dev_stream, foff, fbuf, ff, plen, crc, st[r & 1], n, ck, roff,
-                                    rlen, acrc, ctx->d_bytetab, ctx->d_tabs + 1024, ctx->d_xpow,
-                                    ctx->d_ia, s)) != hipSuccess)
+    if ((e = mgenx::launch_tcp_tail(dev_stream, foff, fbuf, ff, plen, crc, st[r & 1], n, ck,
+                                    (opts & MGENX_PACK_RANDOM_FILL) ? 1 : 0, acrc,
+                                    ctx->d_bytetab, ctx->d_xpow, ctx->d_ia, ctx->d_rcrc, s)) !=
+        hipSuccess)
       return set_err(ctx, e, "tcp tail");
   }
   return MGENX_OK;
@@ -742,7 +742,8 @@ int mgenx_flow_reduce_ex(mgenx_ctx* ctx, const uint32_t* dev_flow_idx, const uin
 }
 
 static int log_recv(mgenx_ctx* ctx, bool binary, const uint8_t* dev_slab, uint64_t slab_bytes,
-                    const uint64_t* dev_rec_off, uint64_t stride, const mgenx_cols* cols,
+                    const uint64_t* dev_rec_off, const uint32_t* dev_rec_len, uint64_t stride,
+                    const mgenx_cols* cols,
                     const mgenx_addr* dev_src, const uint32_t* dev_rx_sec,
                     const uint32_t* dev_rx_usec, const int32_t* dev_ttl, uint32_t n,
                     int protocol, uint32_t opts, char* dev_text, uint64_t text_cap,
@@ -761,7 +762,8 @@ static int log_recv(mgenx_ctx* ctx, bool binary, const uint8_t* dev_slab, uint64
     return MGENX_EINVAL;
   hipSetDevice(ctx->device);
   if (!ctx->log_ws) ctx->log_ws = mgenx_log_ws_new();
-  return mgenx_log_recv_run(ctx->log_ws, binary, dev_slab, slab_bytes, dev_rec_off, stride, cols,
+  return mgenx_log_recv_run(ctx->log_ws, binary, dev_slab, slab_bytes, dev_rec_off, dev_rec_len,
+                            stride, cols,
                             dev_src, dev_rx_sec, dev_rx_usec, dev_ttl, n, protocol, opts,
                             dev_text, text_cap, dev_line_off, (hipStream_t)stream, ctx->err,
                             sizeof(ctx->err));
@@ -773,18 +775,20 @@ int mgenx_log_recv_text(mgenx_ctx* ctx, const uint8_t* dev_slab, const uint64_t*
                         const int32_t* dev_ttl, uint32_t n, int protocol, uint32_t opts,
                         char* dev_text, uint64_t text_cap, uint64_t* dev_line_off,
                         void* stream) {
-  return log_recv(ctx, false, dev_slab, ~0ull, dev_rec_off, stride, cols, dev_src, dev_rx_sec,
+  return log_recv(ctx, false, dev_slab, ~0ull, dev_rec_off, nullptr, stride, cols, dev_src,
+                  dev_rx_sec,
                   dev_rx_usec, dev_ttl, n, protocol, opts, dev_text, text_cap, dev_line_off,
                   stream);
 }
 
 int mgenx_log_recv_binary(mgenx_ctx* ctx, const uint8_t* dev_slab, uint64_t slab_bytes,
-                          const uint64_t* dev_rec_off, uint64_t stride, const mgenx_cols* cols,
+                          const uint64_t* dev_rec_off, uint64_t stride,
+                          const uint32_t* dev_rec_len, const mgenx_cols* cols,
                           const mgenx_addr* dev_src, const uint32_t* dev_rx_sec,
                           const uint32_t* dev_rx_usec, uint32_t n, int protocol,
                           uint8_t* dev_out, uint64_t out_cap, uint64_t* dev_rec_pos,
                           void* stream) {
-  return log_recv(ctx, true, dev_slab, slab_bytes, dev_rec_off, stride, cols, dev_src,
+  return log_recv(ctx, true, dev_slab, slab_bytes, dev_rec_off, dev_rec_len, stride, cols, dev_src,
                   dev_rx_sec, dev_rx_usec, nullptr, n, protocol, 0, (char*)dev_out, out_cap,
                   dev_rec_pos, stream);
 }

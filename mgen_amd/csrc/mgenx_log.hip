@@ -323,10 +323,10 @@ __device__ void format_binary(S& s, const LogRec& r, const uint8_t* rec, uint64_
   s.put((uint8_t)alen);
   for (uint32_t k = 0; k < alen && k < 16; k++) s.put(src.addr[k]);
   const uint32_t ml = (rl - (16u + alen) + 4u) & 0xFFFFu;  // = hdr + payload_len
-  // a byte past the message's own msg_len (only when msg_len < hdr + payload_len) is written
-  // as zero, so a record never depends on its neighbour in the slab
+  // a byte past the received record (avail: its length, or msg_len when the caller has no
+  // lengths) is written as zero, so a record never depends on its neighbour in the slab
   for (uint32_t k = 0; k < ml; k++) {
-    uint8_t b = (k < avail && k < r.msg_len) ? rec[k] : (uint8_t)0;
+    uint8_t b = k < avail ? rec[k] : (uint8_t)0;
     if (k == 3) {
       b &= (uint8_t)~MGENX_FLAG_CHECKSUM;
       if (r.flags & MGENX_FLAG_CHECKSUM_ERROR) b |= MGENX_FLAG_CHECKSUM_ERROR;
@@ -340,6 +340,7 @@ struct LogParams {
   uint64_t slab_bytes;
   const uint64_t* rec_off;
   uint64_t stride;
+  const uint32_t* rec_len;  // binary: the received lengths (NULL: each record's msg_len)
   mgenx_cols cols;
   const mgenx_addr* src;
   const uint32_t* rx_sec;
@@ -385,7 +386,9 @@ __device__ __forceinline__ void format_any(S& s, const LogParams& p, uint32_t i,
   const uint64_t off = p.rec_off ? p.rec_off[i] : (uint64_t)i * p.stride;
   const uint8_t* rec = p.slab + off;
   if (kBinary) {
-    const uint64_t avail = off < p.slab_bytes ? p.slab_bytes - off : 0u;
+    uint64_t avail = off < p.slab_bytes ? p.slab_bytes - off : 0u;
+    const uint64_t len = p.rec_len ? p.rec_len[i] : r.msg_len;
+    if (avail > len) avail = len;
     format_binary(s, r, rec, avail, p.src[i], p.rx_sec[i], p.rx_usec[i], p.protocol);
   } else {
     const int ttl = p.ttl ? p.ttl[i] : -1;
@@ -460,6 +463,7 @@ static mgenx_log_ws& ws_for(void* wsp, hipStream_t stream) {
 
 extern "C" int mgenx_log_recv_run(void* wsp, bool binary, const uint8_t* slab,
                                   uint64_t slab_bytes, const uint64_t* rec_off,
+                                  const uint32_t* rec_len,
                                        uint64_t stride, const mgenx_cols* cols,
                                        const mgenx_addr* src, const uint32_t* rx_sec,
                                        const uint32_t* rx_usec, const int32_t* ttl, uint32_t n,
@@ -468,7 +472,8 @@ extern "C" int mgenx_log_recv_run(void* wsp, bool binary, const uint8_t* slab,
                                        hipStream_t stream, char* err, size_t errn) {
   mgenx_log_ws& ws = ws_for(wsp, stream);
   LogParams p;
-  p.slab = slab; p.slab_bytes = slab_bytes; p.rec_off = rec_off; p.stride = stride; p.cols = *cols; p.src = src;
+  p.slab = slab; p.slab_bytes = slab_bytes; p.rec_off = rec_off; p.rec_len = rec_len;
+  p.stride = stride; p.cols = *cols; p.src = src;
   p.rx_sec = rx_sec; p.rx_usec = rx_usec; p.ttl = ttl; p.n = n; p.protocol = protocol;
   p.opts = opts; p.text = reinterpret_cast<uint8_t*>(text); p.text_cap = text_cap;
   p.line_off = line_off;

@@ -14,8 +14,9 @@
 //   raw Pack          (mgenx_pack.hip, MGENX_PACK_RAW) the B-byte buffer P at the fragment
 //                     start, its running CRC and the MgenMsg flags it leaves;
 //   tcp_copy_kernel   P[0 .. s_k) for every later buffer k of the fragment;
-//   crc32 ranges      A(s) = ComputeCRC32 from a restart over P[0 .. s) for the (at most
-//                     three) distinct buffer lengths of the fragment;
+//   tcp_prefix_kernel A(s) = ComputeCRC32 from a restart over P[0 .. s) for the (at most
+//                     three) distinct buffer lengths of the fragment, from P's header and
+//                     payload bytes and the fill algebra (no re-read of the buffer);
 //   tcp_finish_kernel the running CRC chained through the buffers algebraically,
 //                     c' = raw(P[0..s)) ^ x^(8s) * c  (c = 0 restarts, as ComputeCRC32 does),
 //                     and the big-endian trailer.
@@ -166,28 +167,53 @@ tcp_copy_kernel(uint8_t* __restrict__ out, const uint64_t* __restrict__ foff,
   }
 }
 
-// CRC ranges: for each fragment the distinct CRC lengths of its later buffers (at most 3:
-// full 8192, one SetupNextTxBuffer-shortened buffer, the last one's size - 4)
-__global__ void tcp_ranges_kernel(const uint64_t* __restrict__ foff, const uint32_t* __restrict__ fbuf,
-                                  const uint32_t* __restrict__ ff, const uint32_t* __restrict__ plen,
-                                  uint32_t n, int ck, uint64_t* __restrict__ roff,
-                                  uint32_t* __restrict__ rlen) {
+// A(s) = crc32(P[0 .. s)) for the (at most three) distinct CRC lengths of a fragment's later
+// buffers (full 8192, one SetupNextTxBuffer-shortened buffer, the last one's size - 4),
+// without re-reading the 8-KiB buffer: P is Pack's image -- header (packet_header_len h
+// bytes), the payload it copied (p bytes, read back from the payload_len field that ends a
+// complete header), then fill -- so the prefix CRC walks at most h + p bytes and extends
+// over the fill algebraically: zeros are the shift x^(8q); RANDOM_FILL's fill is two zero
+// bytes and the rand stream, raw CRC rcrc[q - 2] (mgenMsg.cpp:274-293).
+__global__ void tcp_prefix_kernel(const uint8_t* __restrict__ out, const uint64_t* __restrict__ foff,
+                                  const uint32_t* __restrict__ fbuf, const uint32_t* __restrict__ ff,
+                                  const uint32_t* __restrict__ plen,
+                                  const uint32_t* __restrict__ state, uint32_t n, int ck, int rnd,
+                                  const uint32_t* __restrict__ byte_tab,
+                                  const uint32_t* __restrict__ xpow,
+                                  const uint32_t* __restrict__ rcrc, uint32_t* __restrict__ acrc) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t F = ff[i], B = fbuf[i];
   uint32_t L[3] = {0u, 0u, 0u};
-  if (ck && F > B && plen[i]) {
-    uint32_t start, size;
-    bool last;
-    for (uint32_t k = 1; tcp_buffer(F, B, ck, k, start, size, last); k++) {
-      const uint32_t c = last ? size - 4u : size;
-      const int slot = last ? 2 : (size == kTxBuf ? 0 : 1);
-      L[slot] = c;
-    }
+  if (!(ck && F > B && plen[i])) return;
+  uint32_t start, size;
+  bool last;
+  for (uint32_t k = 1; tcp_buffer(F, B, ck, k, start, size, last); k++) {
+    const uint32_t c = last ? size - 4u : size;
+    L[last ? 2 : (size == kTxBuf ? 0 : 1)] = c;
   }
+  const uint8_t* P = out + foff[i];
+  const uint32_t h = state[i] & 0xffffu;
+  uint32_t p = 0;  // payload bytes Pack copied
+  const uint32_t D = P[23];
+  if (24u + D + 4u <= h) {
+    const uint32_t H = P[24u + D + 3u];
+    if (h == 24u + D + 4u + H + 16u) p = (uint32_t)P[h - 2u] << 8 | P[h - 1u];
+  }
+  const uint32_t body = h + p;
+#pragma unroll
   for (int j = 0; j < 3; j++) {
-    roff[3 * i + j] = foff[i];
-    rlen[3 * i + j] = L[j];
+    const uint32_t len = L[j];
+    if (!len) continue;
+    uint32_t c = 0xFFFFFFFFu;
+    const uint32_t m = len < body ? len : body;
+    for (uint32_t k = 0; k < m; k++) c = byte_tab[(c ^ P[k]) & 0xffu] ^ (c >> 8);
+    if (len > body) {
+      const uint32_t q = len - body;
+      c = multmodp(xpow[q], c);
+      if (rnd && q >= 3u) c ^= rcrc[q - 2u];
+    }
+    acrc[3 * i + j] = c ^ 0xFFFFFFFFu;
   }
 }
 
@@ -249,16 +275,13 @@ hipError_t launch_tcp_frag(const mgenx_pack_desc* desc, const uint32_t* msg_tota
 
 hipError_t launch_tcp_tail(uint8_t* out, const uint64_t* foff, const uint32_t* fbuf,
                            const uint32_t* ff, const uint32_t* plen, const uint32_t* tx_crc,
-                           const uint32_t* state, uint32_t n, int ck, uint64_t* roff,
-                           uint32_t* rlen, uint32_t* acrc, const uint32_t* byte_tab,
-                           const uint32_t* a4_tab, const uint32_t* xpow, const uint32_t* ia,
-                           hipStream_t s) {
+                           const uint32_t* state, uint32_t n, int ck, int rnd, uint32_t* acrc,
+                           const uint32_t* byte_tab, const uint32_t* xpow, const uint32_t* ia,
+                           const uint32_t* rcrc, hipStream_t s) {
   hipLaunchKernelGGL(tcp_copy_kernel, dim3(n), dim3(256), 0, s, out, foff, fbuf, ff, plen, n, ck);
   if (ck) {
-    hipLaunchKernelGGL(tcp_ranges_kernel, dim3((n + 255) / 256), dim3(256), 0, s, foff, fbuf, ff,
-                       plen, n, ck, roff, rlen);
-    hipError_t e = launch_crc32(out, roff, rlen, 3 * n, byte_tab, a4_tab, xpow, nullptr, acrc, s);
-    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(tcp_prefix_kernel, dim3((n + 255) / 256), dim3(256), 0, s, out, foff, fbuf,
+                       ff, plen, state, n, ck, rnd, byte_tab, xpow, rcrc, acrc);
     hipLaunchKernelGGL(tcp_finish_kernel, dim3((n + 255) / 256), dim3(256), 0, s, out, foff, fbuf,
                        ff, plen, tx_crc, state, acrc, xpow, ia, n, ck);
   }

@@ -878,6 +878,7 @@ void or_flow_reduce_batch(or_analytic* flows, uint32_t n_flows, const uint32_t* 
 /* Batch layer                                                         */
 /* ------------------------------------------------------------------ */
 #include <pthread.h>
+#include <stdlib.h>
 
 /* A double d with (UINT32)((d + 180.0) * 60000.0) == raw, so Pack's own conversion
  * (mgenMsg.cpp:221,225) reproduces the template's raw word exactly. */
@@ -969,6 +970,92 @@ void or_udp_recv_batch(const uint8_t* slab, const uint64_t* rec_off, uint64_t st
     }
     if (nthreads == 1) { recv_worker(&jobs[0]); return; }
     for (int t = 0; t < nthreads; t++) pthread_create(&th[t], NULL, recv_worker, &jobs[t]);
+    for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+}
+
+/* ---- CPU baselines on several cores (bench.py's cpu_baseline leg) ----
+ * The reference runs one dispatcher thread; these spread the same per-record work over
+ * nthreads host threads to report what all the cores of the box do: contiguous record ranges
+ * for Pack (UDP send sequence, zero fill: RANDOM_FILL's rand() is process-global state) and
+ * flows split by index (f mod nthreads: each thread walks the records in receive order and
+ * updates only its flows, so per-flow order is kept). */
+typedef struct {
+    const or_tmpl* tmpl; const or_desc* desc; const uint8_t* pool; uint8_t* slab;
+    const uint64_t* rec_off; uint64_t stride; int ck; uint32_t* out_len; uint32_t lo, hi;
+} pack_job;
+
+static void* pack_worker(void* p)
+{
+    pack_job* j = (pack_job*)p;
+    uint8_t* scratch = (uint8_t*)malloc(65536 + 512);
+    for (uint32_t i = j->lo; i < j->hi; i++) {
+        or_msg m;
+        tmpl_to_msg(&j->tmpl[j->desc[i].tmpl], &j->desc[i], j->pool, &m);
+        const uint64_t off = j->rec_off ? j->rec_off[i] : (uint64_t)i * j->stride;
+        j->out_len[i] = or_udp_pack(&m, scratch, j->ck, 0, 0);
+        if (j->out_len[i]) memcpy(j->slab + off, scratch, j->out_len[i]);
+    }
+    free(scratch);
+    return NULL;
+}
+
+void or_udp_pack_batch_mt(const or_tmpl* tmpl, const or_desc* desc, uint32_t n,
+                          const uint8_t* pool, uint8_t* slab, const uint64_t* rec_off,
+                          uint64_t stride, int checksum_enable, uint32_t* out_len, int nthreads)
+{
+    (void)table();
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    pack_job jobs[256];
+    pthread_t th[256];
+    for (int t = 0; t < nthreads; t++) {
+        pack_job* j = &jobs[t];
+        j->tmpl = tmpl; j->desc = desc; j->pool = pool; j->slab = slab; j->rec_off = rec_off;
+        j->stride = stride; j->ck = checksum_enable; j->out_len = out_len;
+        j->lo = (uint32_t)((uint64_t)n * t / nthreads);
+        j->hi = (uint32_t)((uint64_t)n * (t + 1) / nthreads);
+    }
+    if (nthreads == 1) { pack_worker(&jobs[0]); return; }
+    for (int t = 0; t < nthreads; t++) pthread_create(&th[t], NULL, pack_worker, &jobs[t]);
+    for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+}
+
+typedef struct {
+    or_analytic* flows; uint32_t n_flows; const uint32_t* idx; const uint32_t* seq;
+    const uint32_t* txs; const uint32_t* txu; const uint16_t* len; const uint32_t* rxs;
+    const uint32_t* rxu; uint32_t n, t, nt; uint32_t* counts;
+} flow_job;
+
+static void* flow_worker(void* p)
+{
+    flow_job* j = (flow_job*)p;
+    for (uint32_t i = 0; i < j->n; i++) {
+        const uint32_t f = j->idx[i];
+        if (f >= j->n_flows || f % j->nt != j->t) continue;
+        or_time rx = {(int64_t)j->rxs[i], (int64_t)j->rxu[i]};
+        or_time tx = {(int64_t)j->txs[i], (int64_t)j->txu[i]};
+        if (or_analytic_update(&j->flows[f], rx, j->len[i], tx, j->seq[i])) j->counts[f]++;
+    }
+    return NULL;
+}
+
+void or_flow_reduce_batch_mt(or_analytic* flows, uint32_t n_flows, const uint32_t* flow_idx,
+                             const uint32_t* seq, const uint32_t* tx_sec, const uint32_t* tx_usec,
+                             const uint16_t* msg_len, const uint32_t* rx_sec,
+                             const uint32_t* rx_usec, uint32_t n, uint32_t* counts, int nthreads)
+{
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    flow_job jobs[256];
+    pthread_t th[256];
+    for (int t = 0; t < nthreads; t++) {
+        flow_job* j = &jobs[t];
+        j->flows = flows; j->n_flows = n_flows; j->idx = flow_idx; j->seq = seq;
+        j->txs = tx_sec; j->txu = tx_usec; j->len = msg_len; j->rxs = rx_sec; j->rxu = rx_usec;
+        j->n = n; j->t = (uint32_t)t; j->nt = (uint32_t)nthreads; j->counts = counts;
+    }
+    if (nthreads == 1) { flow_worker(&jobs[0]); return; }
+    for (int t = 0; t < nthreads; t++) pthread_create(&th[t], NULL, flow_worker, &jobs[t]);
     for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
 }
 
@@ -1119,8 +1206,9 @@ uint32_t or_log_recv_text(const or_fields* f, const uint8_t* rec, const or_addr*
 /* (the 4-byte record header, 8 time, 2 port, type, length, address): */
 /* hdr + payload_len bytes, as eventRecordLength counts from after the */
 /* header (doc/mgen.xml:4212-4216), with CHECKSUM cleared in the flags */
-/* byte (CHECKSUM_ERROR set when flagged).  Bytes past avail or past   */
-/* the message's own msg_len read as zero here.                        */
+/* byte (CHECKSUM_ERROR set when flagged).  avail = the received bytes */
+/* of the record (the receive buffer); bytes past it read as zero here */
+/* (the reference's buffer holds stale bytes there).                   */
 /* ------------------------------------------------------------------ */
 static uint32_t put_be16(uint8_t* p, uint32_t v) { p[0] = (uint8_t)(v >> 8); p[1] = (uint8_t)v; return 2; }
 static uint32_t put_be32(uint8_t* p, uint32_t v) { put32(p, v); return 4; }
@@ -1158,7 +1246,7 @@ uint32_t or_log_recv_binary(const or_fields* f, const uint8_t* rec, uint64_t ava
     const uint32_t index = 16 + alen;
     const uint32_t ml = (rl - index + 4) & 0xFFFF;
     for (uint32_t i = 0; i < ml; i++) {
-        uint8_t b = (i < avail && i < f->msg_len) ? rec[i] : 0;
+        uint8_t b = i < avail ? rec[i] : 0;
         if (i == 3) {
             b &= (uint8_t)~OR_FLAG_CHECKSUM;
             if (f->flags & OR_FLAG_CHECKSUM_ERROR) b |= OR_FLAG_CHECKSUM_ERROR;

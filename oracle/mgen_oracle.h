@@ -285,6 +285,15 @@ int      or_data_walk(const uint8_t* pay, uint32_t len, int controller, uint32_t
                       uint32_t* n_cmds, uint32_t cap_cmds, uint32_t* reps, uint32_t* n_reps,
                       uint32_t cap_reps);
 
+/* ---- CPU baselines over nthreads host threads (bench.py only) ---- */
+void or_udp_pack_batch_mt(const or_tmpl* tmpl, const or_desc* desc, uint32_t n,
+                          const uint8_t* pool, uint8_t* slab, const uint64_t* rec_off,
+                          uint64_t stride, int checksum_enable, uint32_t* out_len, int nthreads);
+void or_flow_reduce_batch_mt(or_analytic* flows, uint32_t n_flows, const uint32_t* flow_idx,
+                             const uint32_t* seq, const uint32_t* tx_sec, const uint32_t* tx_usec,
+                             const uint16_t* msg_len, const uint32_t* rx_sec,
+                             const uint32_t* rx_usec, uint32_t n, uint32_t* counts, int nthreads);
+
 /* ---- pcap2mgen (pcap2mgen.cpp:252-482) ----
  * or_pcap_frame: one pcap record (16-byte header + data) -> the UDP payload's offset from the
  * record header and length, IP source + UDP source port, TTL / hop limit, timestamp.  Returns

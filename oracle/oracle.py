@@ -139,6 +139,8 @@ def lib():
         L.or_log_recv_text.restype = u32
         L.or_log_recv_binary.argtypes = [P, P, u64, P, u32, u32, i32, P]
         L.or_log_recv_binary.restype = u32
+        L.or_udp_pack_batch_mt.argtypes = [P, P, u32, P, P, P, u64, i32, P, i32]
+        L.or_flow_reduce_batch_mt.argtypes = [P, u32, P, P, P, P, P, P, P, u32, P, i32]
         L.or_sizeof.argtypes = [i32]
         L.or_sizeof.restype = u32
         assert L.or_sizeof(0) == TMPL_DTYPE.itemsize, "or_tmpl layout mismatch"
@@ -411,8 +413,9 @@ def log_recv_text(fields, slab, rec_off, src, rx_sec, rx_usec, protocol=1, ttl=N
     return b"".join(out)
 
 
-def log_recv_binary(fields, slab, rec_off, src, rx_sec, rx_usec, protocol=1):
-    """Binary RECV / RERR log records for n received records (bytes past the slab read 0)."""
+def log_recv_binary(fields, slab, rec_off, src, rx_sec, rx_usec, protocol=1, rec_len=None):
+    """Binary RECV / RERR log records for n received records: record i's message bytes are
+    its rec_len[i] received bytes (its msg_len field when rec_len is None), zeros after."""
     L = lib()
     slab = np.ascontiguousarray(slab, np.uint8)
     fields = np.ascontiguousarray(fields)
@@ -421,8 +424,10 @@ def log_recv_binary(fields, slab, rec_off, src, rx_sec, rx_usec, protocol=1):
     buf = np.zeros(65536 + 256, np.uint8)
     for i in range(len(fields)):
         off = int(rec_off[i])
+        have = int(rec_len[i]) if rec_len is not None else int(fields["msg_len"][i])
         n = L.or_log_recv_binary(ctypes.c_void_p(fields.ctypes.data + i * fields.itemsize),
-                                 ctypes.c_void_p(slab.ctypes.data + off), len(slab) - off,
+                                 ctypes.c_void_p(slab.ctypes.data + off),
+                                 max(0, min(len(slab) - off, have)),
                                  ctypes.c_void_p(src.ctypes.data + i * src.itemsize),
                                  int(rx_sec[i]), int(rx_usec[i]), protocol, _ptr(buf))
         out.append(buf[:n].tobytes())
@@ -603,3 +608,32 @@ def convert_binary_log(log: bytes, log_rx=True, flush=False, opts=0):
     L.or_convert_binary_log(_ptr(f), len(log), int(log_rx), int(flush), opts, _ptr(out), len(out),
                             ctypes.byref(st), ctypes.byref(nr))
     return out[:need].tobytes(), st.value, nr.value
+
+
+# ---------------------------------------------------------------- CPU baselines (bench.py)
+def udp_pack_batch_mt(tmpl, desc, pool, slab_bytes, rec_off=None, stride=0, checksum=True,
+                      nthreads=1):
+    """or_udp_pack_batch over nthreads host threads (zero fill)."""
+    n = len(desc)
+    slab = np.zeros(slab_bytes, np.uint8)
+    lens = np.zeros(n, np.uint32)
+    pool = np.ascontiguousarray(pool if pool is not None and len(pool) else np.zeros(1, np.uint8))
+    lib().or_udp_pack_batch_mt(_ptr(tmpl), _ptr(desc), n, _ptr(pool), _ptr(slab), _ptr(rec_off),
+                               stride, int(checksum), _ptr(lens), nthreads)
+    return slab, lens
+
+
+def flow_reduce_batch_mt(n_flows, flow_idx, seq, tx_sec, tx_usec, msg_len, rx_sec, rx_usec,
+                         window=1.0, nthreads=1):
+    """MgenAnalytic::Update per record over n_flows flows on nthreads threads (flows split by
+    index); returns the per-flow report counts."""
+    flows = (Analytic * n_flows)()
+    for f in range(n_flows):
+        lib().or_analytic_init(ctypes.byref(flows[f]), window)
+    cols = [np.ascontiguousarray(x, dt) for x, dt in
+            ((flow_idx, np.uint32), (seq, np.uint32), (tx_sec, np.uint32), (tx_usec, np.uint32),
+             (msg_len, np.uint16), (rx_sec, np.uint32), (rx_usec, np.uint32))]
+    counts = np.zeros(n_flows, np.uint32)
+    lib().or_flow_reduce_batch_mt(flows, n_flows, *[_ptr(c) for c in cols], len(flow_idx),
+                                  _ptr(counts), nthreads)
+    return counts

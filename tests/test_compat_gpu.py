@@ -207,7 +207,8 @@ def test_recv_log_matches_oracle(run, oracle):
         gl, wl = got.split(b"\n"), want.split(b"\n")
         k = next(j for j in range(min(len(gl), len(wl))) if gl[j] != wl[j])
         pytest.fail(f"line {k}: {gl[k][:300]!r} != {wl[k][:300]!r}")
-    wantb = oracle.log_recv_binary(f, g["unpack_slab"], g["unpack_offs"], src, rs, ru, protocol=1)
+    wantb = oracle.log_recv_binary(f, g["unpack_slab"], g["unpack_offs"], src, rs, ru, protocol=1,
+                                   rec_len=g["unpack_lens"])
     assert out["logs"]["recv.bin"] == wantb
 
 
@@ -237,7 +238,8 @@ def test_convert_binary_log_of_shim_log(run, oracle):
     log = out["logs"]["recv_ok.bin"]
     hdr = b"mgen version=5.1.1 type=binary_log\n\0"
     assert log == hdr + oracle.log_recv_binary(f[ok], g["unpack_slab"], g["unpack_offs"][ok],
-                                               src[ok], rs[ok], ru[ok], protocol=1)
+                                               src[ok], rs[ok], ru[ok], protocol=1,
+                                               rec_len=g["unpack_lens"][ok])
     text, status, nrec = oracle.convert_binary_log(log)
     assert nrec == ok.size
     assert out["logs"]["convert.txt"] == text + (b"#1\n" if status == 0 else b"#0\n")

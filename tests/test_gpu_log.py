@@ -160,6 +160,18 @@ def test_binary_log_matches_oracle(torch, eng, gold, oracle, mode):
     got = out.cpu().numpy().tobytes()
     assert len(got) == len(want)
     assert got == want
+    # with the received lengths: a record's bytes past its msg_len field but inside the
+    # datagram are the reference's receive-buffer bytes
+    lens = gold["unpack_lens"]
+    out, _ = eng.log_recv_binary(slab, n, cols, to_device(src.view(np.uint8)),
+                                 to_device(rx_sec), to_device(rx_usec), rec_off=offs,
+                                 rec_len=to_device(lens.astype(np.uint32)).view(torch.int32),
+                                 protocol=proto)
+    want2 = oracle.log_recv_binary(gold[f"unpack_fields_{mode}"], gold["unpack_slab"],
+                                   gold["unpack_offs"], src, rx_sec, rx_usec, protocol=proto,
+                                   rec_len=lens)
+    assert out.cpu().numpy().tobytes() == want2
+    assert want2 != want   # the golden corpus has records whose msg_len field is short
 
 
 def test_binary_log_message_bound_and_oob(torch, eng, oracle):
