@@ -136,6 +136,30 @@ struct WRing {
     v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)identity, (int)v, 0x143, 0xC, 0xF, false));
     return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
   }
+  // the same reduction over doubles (both 32-bit halves moved by the same DPP pattern)
+  template <int CTRL, int RMASK, typename Op>
+  __device__ static double dpp_step_f64(double x, double identity, Op op) {
+    const uint64_t xb = __builtin_bit_cast(uint64_t, x), ib = __builtin_bit_cast(uint64_t, identity);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)ib, (int)(uint32_t)xb,
+                                                              CTRL, RMASK, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)(ib >> 32),
+                                                              (int)(uint32_t)(xb >> 32), CTRL,
+                                                              RMASK, 0xF, false);
+    return op(x, __builtin_bit_cast(double, (uint64_t)hi << 32 | lo));
+  }
+  template <typename Op>
+  __device__ static double wave_reduce_f64(double v, double identity, Op op) {
+    v = dpp_step_f64<0xB1, 0xF>(v, identity, op);
+    v = dpp_step_f64<0x4E, 0xF>(v, identity, op);
+    v = dpp_step_f64<0x141, 0xF>(v, identity, op);
+    v = dpp_step_f64<0x140, 0xF>(v, identity, op);
+    v = dpp_step_f64<0x142, 0xA>(v, identity, op);
+    v = dpp_step_f64<0x143, 0xC>(v, identity, op);
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, 63);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), 63);
+    return __builtin_bit_cast(double, (uint64_t)hi << 32 | lo);
+  }
   __device__ static uint32_t wave_sum(uint32_t v) {
     return wave_reduce(v, 0u, [](uint32_t a, uint32_t b) { return a + b; });
   }
@@ -372,6 +396,7 @@ flow_update_wave_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
   // bit-exact).  Late (reordered) arrivals qualify.  Anything else -- duplicates, mask
   // restarts, window ends, seq below seq_start, msg == 0 -- takes the general update above.
   __shared__ uint32_t scat[4][32];
+  __shared__ double latl[4][64];
   const uint32_t wv = threadIdx.x >> 6;
   // trial: the run's bits into a zeroed LDS copy of the ring; true when two records of the
   // run share a seq (a duplicate inside the run -- then the run is recomputed exactly)
@@ -399,24 +424,26 @@ flow_update_wave_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
     const uint32_t bsum = WRing::wave_sum(in ? r.len : 0u);
     byte_count = (msg_count == 1 ? 0ull : byte_count) + bsum;
     msg_count += e - k;
-    // the sum in record order (bit-exact); min / max as fmin / fmax: the reference's
-    // "if (l < min) min = l; else if (l > max) max = l" is exactly that for latencies
-    // (never NaN, never -0: ProtoTime::Delta of integer fields) with min <= max.
-    // (Measured alternatives, slower: min / max by DPP wave reductions, the loop unrolled
-    // over constant lanes, compare-selects -- the loop is bound by the sum's chain.)
-    double vs = lsum, vmin = lmin, vmax = lmax;
+    // min / max as fmin / fmax -- the reference's "if (l < min) min = l; else if (l > max)
+    // max = l" is exactly that for latencies (never NaN, never -0: ProtoTime::Delta of
+    // integer fields) with min <= max -- so order-free: one DPP wave reduction each.
+    const double lat = __builtin_bit_cast(double, (uint64_t)lhi << 32 | llo);
+    const double inf = __builtin_huge_val();
+    lmin = __builtin_fmin(lmin, WRing::wave_reduce_f64(in ? lat : inf, inf,
+                                                        [](double a, double b) { return __builtin_fmin(a, b); }));
+    lmax = __builtin_fmax(lmax, WRing::wave_reduce_f64(in ? lat : -inf, -inf,
+                                                        [](double a, double b) { return __builtin_fmax(a, b); }));
+    // the sum in record order (bit-exact): the run's latencies staged in LDS and read back
+    // as broadcasts, so the loop is the dependent v_add_f64 chain and independent ds_reads
+    latl[wv][lane] = lat;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    double vs = lsum;
     const uint32_t ee = (MGENX_DIAG && (abl & 1)) ? k : e;
-    for (uint32_t j = k; j < ee; j++) {
-      const uint64_t lb = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)lhi, (int)j) << 32 |
-                          (uint32_t)__builtin_amdgcn_readlane((int)llo, (int)j);
-      const double latency = __builtin_bit_cast(double, lb);
-      vs = __dadd_rn(vs, latency);
-      vmin = __builtin_fmin(vmin, latency);
-      vmax = __builtin_fmax(vmax, latency);
-    }
+#pragma unroll 8
+    for (uint32_t j = k; j < ee; j++) vs = __dadd_rn(vs, latl[wv][j]);
     lsum = vs;
-    lmin = vmin;
-    lmax = vmax;
+    __builtin_amdgcn_wave_barrier();
   };
 
   // 64 records per round: lane k holds record order[i0 + k]; the record loads of the next
