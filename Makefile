@@ -14,7 +14,7 @@ LIBS := -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 all: mgen_amd/libmgenx.so mgen_amd/libmgenx_diag.so oracle tests/cpp/host_roundtrip \
      tests/cpp/loopback tests/cpp/compat_shapes tests/cpp/compat_shapes_pl tests/cpp/shim_latency \
-     tools/pcap2mgen
+     tests/cpp/shard_scan tools/pcap2mgen
 
 build/product/%.o: mgen_amd/csrc/%.hip $(HDR)
 	@mkdir -p build/product
@@ -49,6 +49,10 @@ COMPAT := $(wildcard include/mgenx_compat/*.h include/mgenx_compat/*.hpp) \
           include/mgenx_compat/mgenx_compat.cpp
 tests/cpp/compat_shapes: tests/cpp/compat_shapes.cpp $(COMPAT) include/mgenx.h mgen_amd/libmgenx.so
 	$(HOSTCXX) -Iinclude/mgenx_compat $< include/mgenx_compat/mgenx_compat.cpp -o $@ $(HOSTLD)
+
+# mgenx::ShardedScan over simulated ranks (threads) and a one-rank RCCL communicator
+tests/cpp/shard_scan: tests/cpp/shard_scan.cpp include/mgenx.hpp include/mgenx.h mgen_amd/libmgenx.so
+	$(HOSTCXX) $< -o $@ $(HOSTLD) -lpthread
 
 # per-call latency of the shim's single-message calls (batches of one) and batch forms
 tests/cpp/shim_latency: tests/cpp/shim_latency.cpp $(COMPAT) include/mgenx.h mgen_amd/libmgenx.so

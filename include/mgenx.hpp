@@ -10,7 +10,11 @@
 //   SendBatch      MgenFlow::SendMessage's fields (mgenFlow.cpp:924-1130) + MgenMsg::Pack
 //                  + WriteChecksum in the UDP/SINK send order (mgenTransport.cpp:1011-1031);
 //   FlowAnalytics  Mgen::UpdateRecvAnalytics (mgen.cpp:1027-1070): FindFlow by
-//                  (src, dst, flow id) -> MgenAnalytic::Update per record, reports out.
+//                  (src, dst, flow id) -> MgenAnalytic::Update per record, reports out;
+//   ShardedScan    MgenTcpTransport / MgenAppSinkTransport framing (mgenTransport.cpp:
+//                  1683-1760, mgenAppSinkTransport.cpp:369-434) of ONE stream split over the
+//                  ranks of a job (the stitch protocol of include/mgenx.h, "sharded framing",
+//                  over any ShardComm all-gather: RcclShardComm uses mgenx_allgather_u64).
 // Errors: argument/launch failures throw mgenx::Error (the C ABI returns codes); per-record
 // outcomes are MgenMsg::Error values, as in the reference.
 #pragma once
@@ -20,6 +24,7 @@
 
 #include <cstdint>
 #include <cstring>
+#include <algorithm>
 #include <map>
 #include <stdexcept>
 #include <string>
@@ -588,6 +593,209 @@ class FlowAnalytics {
   DeviceArray<uint32_t> count_;
   DeviceArray<uint32_t> d_idx_, d_rxs_, d_rxu_;
   std::map<std::tuple<std::string, std::string, uint32_t>, uint32_t> index_;
+};
+
+// ---- sharded stream framing: one TCP / SINK stream over the ranks of a job --------------
+// An all-gather of fixed-size u64 vectors among the ranks (host vectors in and out):
+// out[r * in.size() + k] = rank r's in[k].  The framing exchanges two kinds of message:
+// every rank's exit table (2 x kExitCap words) and, rarely, 3 words that settle a chain the
+// tables cannot follow.
+class ShardComm {
+ public:
+  virtual ~ShardComm() = default;
+  virtual int World() const = 0;
+  virtual int Rank() const = 0;
+  virtual std::vector<uint64_t> AllGather(const std::vector<uint64_t>& in) = 0;
+};
+
+// RCCL over xGMI: mgenx_allgather_u64 on the context's stream (device staging buffers).
+class RcclShardComm : public ShardComm {
+ public:
+  RcclShardComm(Context& ctx, mgenx_comm* comm, int world, int rank)
+      : ctx_(ctx), comm_(comm), world_(world), rank_(rank) {}
+  int World() const override { return world_; }
+  int Rank() const override { return rank_; }
+  std::vector<uint64_t> AllGather(const std::vector<uint64_t>& in) override {
+    const size_t n = in.size();
+    d_in_.Resize(n ? n : 1);
+    d_out_.Resize(n * world_ ? n * world_ : 1);
+    std::vector<uint64_t> out(n * world_);
+    hipStream_t s = ctx_.stream();
+    check_hip(hipMemcpyAsync(d_in_.data(), in.data(), n * 8, hipMemcpyHostToDevice, s), "H2D");
+    ctx_.Check(mgenx_allgather_u64(ctx_.get(), comm_, d_in_.data(), d_out_.data(), (uint32_t)n, s),
+               "mgenx_allgather_u64");
+    check_hip(hipMemcpyAsync(out.data(), d_out_.data(), out.size() * 8, hipMemcpyDeviceToHost, s),
+              "D2H");
+    ctx_.Sync();
+    return out;
+  }
+
+ private:
+  Context& ctx_;
+  mgenx_comm* comm_;
+  int world_, rank_;
+  DeviceArray<uint64_t> d_in_, d_out_;
+};
+
+struct ShardScanResult {
+  uint64_t a = 0;          // this rank's first owned byte: local offsets + a = global offsets
+  uint64_t n_local = 0;    // this rank's records (written to the caller's arrays, local offsets)
+  uint64_t n_total = 0;    // the whole stream's summary, as mgenx_stream_scan reports it:
+  uint64_t consumed = 0;   //   records, bytes consumed,
+  int32_t status = 0;      //   status (1 = a TCP record with msg_len < 4 stopped the chain)
+};
+
+// The protocol of include/mgenx.h ("sharded framing"; mgen_amd/shard.py is the same steps):
+// rank r owns the records starting in [a_r, b_r) and holds bytes [a_r, min(b_r + HALO, N)).
+//   1. mgenx_stream_scan_exits: for each candidate entry below a_r + HALO, where its chain
+//      first reaches b_r (bit 63: the chain leaves the candidate set -- exit unknown);
+//   2. all-gather of the tables; every rank stitches e_0 = 0, e_{r+1} = exit_r(e_r)
+//      identically; a missing entry or unknown exit is settled by that rank's sequential
+//      range scan and a 3-word all-gather;
+//   3. mgenx_stream_scan_range from e_r on the tables of step 1: the rank's records.
+// A last all-gather gives every rank the whole-stream summary.  No stream bytes move.
+class ShardedScan {
+ public:
+  static constexpr uint32_t kExitCap = 4096;
+  static constexpr uint64_t kUnknown = 1ull << 63;
+  static constexpr uint64_t kHalo = MGENX_SCAN_HALO;
+
+  ShardedScan(Context& ctx, ShardComm& comm) : ctx_(ctx), comm_(comm) {}
+
+  // rank `rank` owns record starts in [a, b) and holds bytes [a, hi)
+  static void Bounds(uint64_t nbytes, int world, int rank, uint64_t& a, uint64_t& b,
+                     uint64_t& hi) {
+    a = nbytes * (uint64_t)rank / (uint64_t)world;
+    b = nbytes * (uint64_t)(rank + 1) / (uint64_t)world;
+    hi = std::min(b + kHalo, nbytes);
+  }
+
+  // The stitch, identical on every rank.  tables: World() x [entries(kExitCap) |
+  // exits(kExitCap)] (local offsets, unused rows ~0, entries ascending); bounds[r] = (a, b);
+  // settled[r] = (global exit, stopped).  entries[r] = global entry or -1 (the chain
+  // stopped before rank r).  Returns the first rank whose exit a range scan must settle,
+  // or -1 when every entry is known.
+  static int Stitch(const std::vector<uint64_t>& tables,
+                    const std::vector<std::pair<uint64_t, uint64_t>>& bounds,
+                    const std::map<int, std::pair<uint64_t, bool>>& settled,
+                    std::vector<int64_t>& entries) {
+    const int world = (int)bounds.size();
+    entries.assign(world, -1);
+    entries[0] = 0;
+    for (int r = 0; r < world; r++) {
+      const int64_t e = entries[r];
+      if (e < 0) break;
+      const uint64_t a = bounds[r].first, b = bounds[r].second;
+      const bool last = r == world - 1;
+      uint64_t ex;
+      auto it = settled.find(r);
+      if (it != settled.end()) {
+        if (it->second.second || last) break;
+        ex = it->second.first;
+      } else if ((uint64_t)e >= b && !last) {
+        ex = (uint64_t)e;  // a record spans the whole range
+      } else if (last) {
+        break;
+      } else {
+        const uint64_t* ent = tables.data() + (size_t)r * 2 * kExitCap;
+        const uint64_t* exi = ent + kExitCap;
+        const uint64_t want = (uint64_t)e - a;
+        const uint64_t* k = std::lower_bound(ent, ent + kExitCap, want);
+        if (k == ent + kExitCap || *k != want || (exi[k - ent] & kUnknown)) return r;
+        ex = a + exi[k - ent];
+      }
+      entries[r + 1] = (int64_t)ex;
+    }
+    return -1;
+  }
+
+  // d_local: this rank's bytes [a, hi) of a stream of nbytes; the rank's records go to
+  // d_off / d_len (local offsets, at most cap).  Synchronous; collective over the ranks.
+  ShardScanResult Run(const uint8_t* d_local, uint64_t nbytes, int mode, uint64_t* d_off,
+                      uint32_t* d_len, uint64_t cap) {
+    const int world = comm_.World(), rank = comm_.Rank();
+    std::vector<std::pair<uint64_t, uint64_t>> bounds(world);
+    for (int r = 0; r < world; r++) {
+      uint64_t ra, rb, rh;
+      Bounds(nbytes, world, r, ra, rb, rh);
+      bounds[r] = {ra, rb};
+    }
+    uint64_t a, b, hi;
+    Bounds(nbytes, world, rank, a, b, hi);
+    const bool last = rank == world - 1;
+    const uint64_t local = hi - a, limit = last ? local : b - a;
+    mgenx_ctx* c = ctx_.get();
+    hipStream_t s = ctx_.stream();
+    // 1. this rank's exit table
+    d_ent_.Resize(kExitCap);
+    d_ext_.Resize(kExitCap);
+    uint32_t cands = 0;
+    ctx_.Check(mgenx_stream_scan_exits(c, d_local, local, mode, kHalo, limit, d_ent_.data(),
+                                       d_ext_.data(), kExitCap, &cands, s),
+               "mgenx_stream_scan_exits");
+    std::vector<uint64_t> table(2 * kExitCap);
+    check_hip(hipMemcpyAsync(table.data(), d_ent_.data(), kExitCap * 8, hipMemcpyDeviceToHost, s), "D2H");
+    check_hip(hipMemcpyAsync(table.data() + kExitCap, d_ext_.data(), kExitCap * 8,
+                             hipMemcpyDeviceToHost, s), "D2H");
+    ctx_.Sync();
+    // 2. gather, stitch, settle what the tables cannot
+    const std::vector<uint64_t> tables = comm_.AllGather(table);
+    std::map<int, std::pair<uint64_t, bool>> settled;
+    std::vector<int64_t> entries;
+    bool have_mine = false;
+    mgenx_scan_info mine = {};
+    for (;;) {
+      const int need = Stitch(tables, bounds, settled, entries);
+      if (need < 0) break;
+      std::vector<uint64_t> msg(3, 0);
+      if (rank == need) {
+        mine = Range(d_local, local, mode, (uint64_t)entries[rank] - a, limit, d_off, d_len, cap);
+        have_mine = true;
+        const bool stopped = mine.consumed < limit || last;
+        msg = {a + mine.consumed, stopped ? 1ull : 0ull, 1ull};
+      }
+      const std::vector<uint64_t> msgs = comm_.AllGather(msg);
+      settled[need] = {msgs[3 * need], msgs[3 * need + 1] != 0};
+    }
+    // 3. this rank's records
+    const int64_t e = entries[rank];
+    if (!have_mine) {
+      if (e < 0 || ((uint64_t)e >= b && !last)) {
+        mine = {};
+        mine.consumed = e >= 0 ? (uint64_t)e - a : 0;
+      } else {
+        mine = Range(d_local, local, mode, (uint64_t)e - a, limit, d_off, d_len, cap);
+      }
+    }
+    const std::vector<uint64_t> summ =
+        comm_.AllGather({mine.n_records, a + mine.consumed, (uint64_t)(uint32_t)mine.status,
+                         e >= 0 ? 1ull : 0ull});
+    ShardScanResult r;
+    r.a = a;
+    r.n_local = mine.n_records;
+    int reached = 0;
+    for (int q = 0; q < world; q++) {
+      r.n_total += summ[4 * q];
+      if (summ[4 * q + 3]) reached = q;  // the chain stops at the last rank it reached
+    }
+    r.consumed = summ[4 * reached + 1];
+    r.status = (int32_t)summ[4 * reached + 2];
+    return r;
+  }
+
+ private:
+  mgenx_scan_info Range(const uint8_t* d_local, uint64_t local, int mode, uint64_t entry,
+                        uint64_t limit, uint64_t* d_off, uint32_t* d_len, uint64_t cap) {
+    mgenx_scan_info info = {};
+    ctx_.Check(mgenx_stream_scan_range(ctx_.get(), d_local, local, mode, entry, limit,
+                                       MGENX_SCAN_REUSE, d_off, d_len, cap, &info, ctx_.stream()),
+               "mgenx_stream_scan_range");
+    return info;
+  }
+
+  Context& ctx_;
+  ShardComm& comm_;
+  DeviceArray<uint64_t> d_ent_, d_ext_;
 };
 
 }  // namespace mgenx
