@@ -278,6 +278,7 @@ def extra_config4(torch, eng, dev, world, rank, dist):
                                                      flow_idx=fidx, n_flows=nf), reps=5)
     finally:
         eng.flow_table_destroy(table)
+    pipe = pipeline_config4(torch, eng, dev, d, idx, src, state["flows"], n_flows, n)
     ar_ms = None
     if world > 1:
         uid = torch.zeros(128, dtype=torch.uint8, device=dev)
@@ -298,9 +299,65 @@ def extra_config4(torch, eng, dev, world, rank, dist):
     return {"records_total": N4_TOTAL, "records_this_rank": n, "flows": n_flows,
             "reduce_ms": round(ms, 4), "mrec_per_s": round(n / ms / 1e3, 2),
             "findflow_ms": round(lk_ms, 4), "findflow_mrec_per_s": round(n / lk_ms / 1e3, 1),
-            "allreduce_bytes": n_flows * 64,
+            "rows_pipeline": pipe, "allreduce_bytes": n_flows * 64,
             "allreduce_ms": None if ar_ms is None else round(ar_ms, 4),
             "merge": "mgenx_allreduce_flows (RCCL ncclAllReduce sum, 1024 x 64 B)"}
+
+
+def pipeline_config4(torch, eng, dev, d, idx, src, want_flows, n_flows, n):
+    """The receive path of config 4 on the unpack's 32-B rows, no column layout: the rank's
+    records as 256-B datagrams (GPU-packed), mgenx_unpack_batch -> rows, FindFlow keyed from
+    the rows (mgenx_flow_lookup, cols.rows), MgenAnalytic::Update reading the rows
+    (mgenx_flow_reduce_rows).  Checked: every flow's state equals the column path's
+    (`want_flows`, flow ids are the global index there, first-appearance order here)."""
+    from mgen_amd import DESC_DTYPE, FLOW_STATE_BYTES, to_device
+    from mgen_amd.workloads import make_templates
+    msg = 256
+    tmpl, pool = make_templates(n_flows)
+    desc = np.zeros(n, DESC_DTYPE)
+    desc["tmpl"], desc["seq_num"] = idx, d["seq"]
+    desc["tx_sec"], desc["tx_usec"], desc["msg_len"] = d["tx_sec"], d["tx_usec"], msg
+    dt, dp = to_device(tmpl, eng.device), to_device(pool, eng.device)
+    crc = torch.empty(n_flows, dtype=torch.int32, device=dev)
+    eng.pack_prepare(dt, n_flows, dp, crc)
+    slab = torch.empty(n * msg, dtype=torch.uint8, device=dev)
+    eng.pack(dt, crc, to_device(desc, eng.device), n, dp, slab, stride=msg)
+    rows = {"rows": eng.alloc_rows(n)}
+    rx_s = torch.from_numpy(d["rx_sec"]).to(dev)
+    rx_u = torch.from_numpy(d["rx_usec"]).to(dev)
+    fidx = torch.empty(n, dtype=torch.int32, device=dev)
+    nf = torch.zeros(1, dtype=torch.int32, device=dev)
+    table = eng.flow_table(2 * n_flows)
+    box = {}
+    unpack = lambda: eng.unpack(slab, n, stride=msg, fixed_len=msg, cols=rows)  # noqa: E731
+    lookup = lambda: eng.flow_lookup(table, rows, src.reshape(-1), n, flow_idx=fidx,  # noqa
+                                     n_flows=nf)
+
+    def reduce():
+        box["flows"] = eng.flow_init(n_flows, 1.0)
+        eng.flow_reduce_rows(box["flows"], n_flows, fidx, rows["rows"], rx_s, rx_u, n=n)
+
+    def whole():
+        unpack()
+        lookup()
+        reduce()
+    try:
+        whole()
+        torch.cuda.synchronize()
+        assert int(nf.cpu()[0]) == len(np.unique(d["flow_id"]))
+        _, first = np.unique(d["flow_id"], return_index=True)
+        order = d["flow_id"][np.sort(first)] - 1          # dense index -> global flow index
+        got = box["flows"].cpu().numpy().reshape(n_flows, FLOW_STATE_BYTES)
+        want = want_flows.cpu().numpy().reshape(n_flows, FLOW_STATE_BYTES)
+        assert np.array_equal(got[:len(order)], want[order]), "rows pipeline != column path"
+        u_ms, l_ms, r_ms = timed(torch, unpack, 5), timed(torch, lookup, 5), timed(torch, reduce, 5)
+        w_ms = timed(torch, whole, 5)
+    finally:
+        eng.flow_table_destroy(table)
+    return {"datagram_bytes": msg, "unpack_ms": round(u_ms, 4), "findflow_ms": round(l_ms, 4),
+            "reduce_ms": round(r_ms, 4), "end_to_end_ms": round(w_ms, 4),
+            "end_to_end_mrec_per_s": round(n / w_ms / 1e3, 1),
+            "checked": "per-flow state == column-path state (bit-exact)"}
 
 
 def extra_config5(torch, eng, dev, world=1, rank=0, dist=None):

@@ -491,6 +491,14 @@ int mgenx_flow_reduce_ex(mgenx_ctx* ctx, const uint32_t* dev_flow_idx, const uin
                          const uint32_t* dev_rx_usec, uint32_t n, mgenx_flow_state* dev_flows,
                          uint32_t n_flows, mgenx_flow_report* dev_reports, uint32_t per_flow,
                          uint32_t* dev_report_count, uint32_t* dev_report_rec, void* stream);
+/* The same reduction reading seq_num, tx_sec, tx_usec and msg_len from the 32-B rows
+ * mgenx_unpack_batch writes (cols.rows): the unpack -> FindFlow -> Update pipeline without
+ * the column layout.  dev_report_rec as mgenx_flow_reduce_ex (optional). */
+int mgenx_flow_reduce_rows(mgenx_ctx* ctx, const uint32_t* dev_flow_idx, const mgenx_rec* dev_rows,
+                           const uint32_t* dev_rx_sec, const uint32_t* dev_rx_usec, uint32_t n,
+                           mgenx_flow_state* dev_flows, uint32_t n_flows,
+                           mgenx_flow_report* dev_reports, uint32_t per_flow,
+                           uint32_t* dev_report_count, uint32_t* dev_report_rec, void* stream);
 int mgenx_flow_export(mgenx_ctx* ctx, const mgenx_flow_state* dev_flows, uint32_t n_flows,
                       mgenx_flow_counters* dev_out, void* stream);
 
@@ -502,7 +510,11 @@ int mgenx_flow_export(mgenx_ctx* ctx, const mgenx_flow_state* dev_flows, uint32_
  * records (columns dst_addr, dst_len, dst_port, flow_id, and err when given: err != 0 maps
  * to MGENX_FLOW_NONE) with their recvfrom source addresses to dev_flow_idx[i] -- the input
  * mgenx_flow_reduce takes -- and copies the table's flow count to dev_n_flows[0] (optional,
- * device memory).  Keys persist across calls (streaming batches). */
+ * device memory).  Keys persist across calls (streaming batches).
+ * With cols->rows (the 32-B mgenx_rec output) the key fields and err come from the rows;
+ * the destination address from the dst_addr column when given, else from the rows'
+ * dst_addr4 -- exact for IPv4 destinations; a record whose dst_len exceeds 4 then maps to
+ * MGENX_FLOW_NONE (pass dst_addr when IPv6 destinations can occur). */
 #define MGENX_FLOW_NONE 0xFFFFFFFFu
 typedef struct mgenx_flow_table mgenx_flow_table;
 int mgenx_flow_table_create(mgenx_ctx* ctx, uint32_t max_flows, mgenx_flow_table** out);

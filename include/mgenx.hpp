@@ -618,7 +618,7 @@ class RcclShardComm : public ShardComm {
   std::vector<uint64_t> AllGather(const std::vector<uint64_t>& in) override {
     const size_t n = in.size();
     d_in_.Resize(n ? n : 1);
-    d_out_.Resize(n * world_ ? n * world_ : 1);
+    d_out_.Resize(std::max<size_t>(n * world_, 1));
     std::vector<uint64_t> out(n * world_);
     hipStream_t s = ctx_.stream();
     check_hip(hipMemcpyAsync(d_in_.data(), in.data(), n * 8, hipMemcpyHostToDevice, s), "H2D");

@@ -42,7 +42,7 @@ EXPORTED_SYMBOLS = (
     "mgenx_flow_table_create", "mgenx_flow_table_destroy", "mgenx_flow_lookup",
     "mgenx_flow_reduce_ex", "mgenx_flow_keys", "mgenx_text_interleave", "mgenx_pcap_index",
     "mgenx_pcap_parse", "mgenx_binlog_index", "mgenx_convert_binary_log",
-    "mgenx_unpack_last_kernel", "mgenx_pcap_snap",
+    "mgenx_unpack_last_kernel", "mgenx_pcap_snap", "mgenx_flow_reduce_rows",
 )
 DIAG_SYMBOLS = ("mgenx_set_tuning", "mgenx_diag_stream_read", "mgenx_diag_group_rw")
 
@@ -118,6 +118,7 @@ def load(diag: bool = False):
                                           ctypes.POINTER(ScanInfo), P]
     L.mgenx_flow_init.argtypes = [P, P, u32, ctypes.c_double, P]
     L.mgenx_flow_reduce.argtypes = [P, P, P, P, P, P, P, P, u32, P, u32, P, u32, P, P]
+    L.mgenx_flow_reduce_rows.argtypes = [P, P, P, P, P, u32, P, u32, P, u32, P, P, P]
     L.mgenx_flow_export.argtypes = [P, P, u32, P, P]
     L.mgenx_log_recv_text.argtypes = [P, P, P, u64, ctypes.POINTER(MgenxCols), P, P, P, P, u32,
                                       i32, u32, P, u64, P, P]
@@ -452,6 +453,21 @@ class Engine:
                                                _ptr(reports), per_flow, _ptr(report_count),
                                                _ptr(report_rec), _stream(self.device))
         self._check(rc, "mgenx_flow_reduce")
+        return report_count
+
+    def flow_reduce_rows(self, flows, n_flows, flow_idx, rows, rx_sec, rx_usec, n=None,
+                         reports=None, per_flow=0, report_count=None, report_rec=None):
+        """flow_reduce with seq / tx time / msg_len read from the unpack's 32-B rows
+        (mgenx_flow_reduce_rows): the same result as the column form."""
+        torch = self.torch
+        n = flow_idx.numel() if n is None else n
+        if report_count is None:
+            report_count = torch.zeros(n_flows, dtype=torch.int32, device=flows.device)
+        rc = self.lib.mgenx_flow_reduce_rows(self.ctx, _ptr(flow_idx), _ptr(rows), _ptr(rx_sec),
+                                             _ptr(rx_usec), n, _ptr(flows), n_flows,
+                                             _ptr(reports), per_flow, _ptr(report_count),
+                                             _ptr(report_rec), _stream(self.device))
+        self._check(rc, "mgenx_flow_reduce_rows")
         return report_count
 
     def flow_keys(self, table, n_flows, protocol=1, keys=None):

@@ -539,9 +539,11 @@ flow_update_wave_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
 
 // keys: flow index clamped to n_flows (records to skip sort last); vals: record index;
 // recs: the record as the update kernel reads it, with its latency
+// (the record fields come from the columns, or from the unpack's 32-B rows when `rows` is set)
 __global__ void flow_keys_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows,
                                  const uint32_t* __restrict__ seq, const uint32_t* __restrict__ txs,
                                  const uint32_t* __restrict__ txu, const uint16_t* __restrict__ len,
+                                 const mgenx_rec* __restrict__ rows,
                                  const uint32_t* __restrict__ rxs, const uint32_t* __restrict__ rxu,
                                  uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
                                  FRec* __restrict__ recs) {
@@ -550,11 +552,22 @@ __global__ void flow_keys_kernel(const uint32_t* __restrict__ idx, uint32_t n, u
   keys[i] = min(idx[i], n_flows);
   vals[i] = i;
   FRec r;
-  r.seq = seq[i];
+  uint32_t ts, tu;
+  if (rows) {
+    const u32x4_t h = *reinterpret_cast<const u32x4_t*>(rows + i);  // flow, seq, tx_sec, tx_usec
+    r.seq = h.y;
+    ts = h.z;
+    tu = h.w;
+    r.len = rows[i].msg_len;
+  } else {
+    r.seq = seq[i];
+    ts = txs[i];
+    tu = txu[i];
+    r.len = len[i];
+  }
   r.rxs = rxs[i];
   r.rxu = rxu[i];
-  r.len = len[i];
-  r.latency = tdelta(Tm{(int64_t)r.rxs, (int64_t)r.rxu}, Tm{(int64_t)txs[i], (int64_t)txu[i]});
+  r.latency = tdelta(Tm{(int64_t)r.rxs, (int64_t)r.rxu}, Tm{(int64_t)ts, (int64_t)tu});
   recs[i] = r;
 }
 
@@ -650,7 +663,7 @@ static size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const uint32_t* seq,
                                      const uint32_t* txs, const uint32_t* txu, const uint16_t* len,
-                                     const uint32_t* rxs, const uint32_t* rxu, uint32_t n,
+                                     const mgenx_rec* rows, const uint32_t* rxs, const uint32_t* rxu, uint32_t n,
                                      mgenx_flow_state* flows, uint32_t n_flows,
                                      mgenx_flow_report* reports, uint32_t per_flow,
                                      uint32_t* report_count, uint32_t* report_rec,
@@ -689,7 +702,7 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
   void* cub_tmp = take(a256(cub_bytes));
   const dim3 g((n + 255) / 256);
   hipLaunchKernelGGL(flow_keys_kernel, g, dim3(256), 0, stream, flow_idx, n, n_flows, seq, txs,
-                     txu, len, rxs, rxu, keys_in, vals_in, recs);
+                     txu, len, rows, rxs, rxu, keys_in, vals_in, recs);
   hipError_t e = hipcub::DeviceRadixSort::SortPairs(cub_tmp, cub_bytes, keys_in, keys_out,
                                                     vals_in, vals_out, (int)n, 0, end_bit, stream);
   if (e != hipSuccess) {

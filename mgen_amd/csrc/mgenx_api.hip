@@ -92,6 +92,7 @@ extern "C" int mgenx_flow_export_run(const mgenx_flow_state* flows, uint32_t n_f
                                      mgenx_flow_counters* out, hipStream_t stream);
 extern "C" int mgenx_flow_reduce_run(void* ws, const uint32_t* flow_idx, const uint32_t* seq,
                                      const uint32_t* txs, const uint32_t* txu, const uint16_t* len,
+                                     const mgenx_rec* rows,
                                      const uint32_t* rxs, const uint32_t* rxu, uint32_t n,
                                      mgenx_flow_state* flows, uint32_t n_flows,
                                      mgenx_flow_report* reports, uint32_t per_flow,
@@ -735,10 +736,28 @@ int mgenx_flow_reduce_ex(mgenx_ctx* ctx, const uint32_t* dev_flow_idx, const uin
   hipSetDevice(ctx->device);
   if (!ctx->flow_ws) ctx->flow_ws = mgenx_flow_ws_new();
   return mgenx_flow_reduce_run(ctx->flow_ws, dev_flow_idx, dev_seq, dev_tx_sec, dev_tx_usec,
-                               dev_msg_len, dev_rx_sec, dev_rx_usec, n, dev_flows, n_flows,
-                               dev_reports, per_flow, dev_report_count, dev_report_rec,
+                               dev_msg_len, nullptr, dev_rx_sec, dev_rx_usec, n, dev_flows,
+                               n_flows, dev_reports, per_flow, dev_report_count, dev_report_rec,
                                (hipStream_t)stream,
                                ctx->err, sizeof(ctx->err));
+}
+
+int mgenx_flow_reduce_rows(mgenx_ctx* ctx, const uint32_t* dev_flow_idx, const mgenx_rec* dev_rows,
+                           const uint32_t* dev_rx_sec, const uint32_t* dev_rx_usec, uint32_t n,
+                           mgenx_flow_state* dev_flows, uint32_t n_flows,
+                           mgenx_flow_report* dev_reports, uint32_t per_flow,
+                           uint32_t* dev_report_count, uint32_t* dev_report_rec, void* stream) {
+  if (!ctx) return MGENX_EINVAL;
+  if (n == 0 || n_flows == 0) return MGENX_OK;
+  if (!dev_flow_idx || !dev_rows || !dev_rx_sec || !dev_rx_usec || !dev_flows ||
+      !dev_report_count || (per_flow && !dev_reports) || n > 0x7FFFFFFFu)
+    return MGENX_EINVAL;
+  hipSetDevice(ctx->device);
+  if (!ctx->flow_ws) ctx->flow_ws = mgenx_flow_ws_new();
+  return mgenx_flow_reduce_run(ctx->flow_ws, dev_flow_idx, nullptr, nullptr, nullptr, nullptr,
+                               dev_rows, dev_rx_sec, dev_rx_usec, n, dev_flows, n_flows,
+                               dev_reports, per_flow, dev_report_count, dev_report_rec,
+                               (hipStream_t)stream, ctx->err, sizeof(ctx->err));
 }
 
 static int log_recv(mgenx_ctx* ctx, bool binary, const uint8_t* dev_slab, uint64_t slab_bytes,

@@ -48,11 +48,31 @@ __device__ __forceinline__ uint32_t mix32(uint32_t h) {
 }
 
 // key of record i: dst (len, port, 16 addr bytes), src (mgenx_addr), flow id
+// (the 32-B rows of mgenx_unpack_batch carry dst_addr4, the first 4 address bytes: with rows
+// and no dst_addr column an IPv4 destination is keyed exactly; a longer one is not keyed --
+// the caller passes the dst_addr column when IPv6 destinations can occur, see mgenx.h)
 __device__ __forceinline__ FlowKey make_key(const mgenx_cols& c, const mgenx_addr* src, uint32_t i) {
   FlowKey k;
-  const uint32_t* da = reinterpret_cast<const uint32_t*>(c.dst_addr + (size_t)i * 16);
+  uint32_t da[4] = {0u, 0u, 0u, 0u};
+  uint32_t dl, dport, fid;
+  if (c.rows) {
+    const mgenx_rec& r = c.rows[i];
+    dl = r.dst_len;
+    dport = r.dst_port;
+    fid = r.flow_id;
+    da[0] = r.dst_addr4;
+  } else {
+    dl = c.dst_len[i];
+    dport = c.dst_port[i];
+    fid = c.flow_id[i];
+  }
+  if (c.dst_addr) {
+    const uint32_t* dp = reinterpret_cast<const uint32_t*>(c.dst_addr + (size_t)i * 16);
+#pragma unroll
+    for (int j = 0; j < 4; j++) da[j] = dp[j];
+  }
   const uint32_t* sa = reinterpret_cast<const uint32_t*>(src[i].addr);
-  const uint32_t dl = c.dst_len[i], sl = src[i].len;
+  const uint32_t sl = src[i].len;
   // bytes past an address's length are not part of the reference key: masked to zero
   auto mask_to = [](uint32_t word, uint32_t wi, uint32_t len) {
     const uint32_t lo = 4u * wi;
@@ -64,9 +84,9 @@ __device__ __forceinline__ FlowKey make_key(const mgenx_cols& c, const mgenx_add
   for (int j = 0; j < 4; j++) k.w[j] = mask_to(da[j], j, dl);
 #pragma unroll
   for (int j = 0; j < 4; j++) k.w[4 + j] = mask_to(sa[j], j, sl);
-  k.w[8] = dl | (uint32_t)c.dst_port[i] << 16;
+  k.w[8] = dl | dport << 16;
   k.w[9] = sl | (uint32_t)src[i].port << 16;
-  k.w[10] = c.flow_id[i];
+  k.w[10] = fid;
   k.w[11] = 0x4D47u;
   return k;
 }
@@ -97,7 +117,9 @@ __global__ void flowtab_insert_kernel(FlowSlot* __restrict__ tab, uint32_t cap_m
                                       uint32_t* __restrict__ rec_slot, uint32_t* __restrict__ overflow) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  if (c.err && c.err[i] != 0) {
+  const uint32_t err = c.rows ? c.rows[i].err : (c.err ? c.err[i] : 0u);
+  const bool unkeyed = c.rows && !c.dst_addr && c.rows[i].dst_len > 4u;
+  if (err != 0 || unkeyed) {
     rec_slot[i] = kSlotBusy;
     return;
   }
@@ -280,8 +302,8 @@ int mgenx_flow_lookup(mgenx_ctx* ctx, mgenx_flow_table* t, const mgenx_cols* col
   if (!ctx || !t || !cols) return MGENX_EINVAL;
   if (n == 0) return MGENX_OK;
   const mgenx_cols& c = *cols;
-  if (!c.dst_addr || !c.dst_len || !c.dst_port || !c.flow_id || !dev_src || !dev_flow_idx)
-    return MGENX_EINVAL;
+  if (!c.rows && (!c.dst_addr || !c.dst_len || !c.dst_port || !c.flow_id)) return MGENX_EINVAL;
+  if (!dev_src || !dev_flow_idx) return MGENX_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   size_t cub_bytes = 0;
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, cub_bytes, (const uint32_t*)nullptr,

@@ -155,3 +155,48 @@ def test_flow_reduce_fast_segments_edge_cases(torch, eng, window):
                                          d["tx_usec"], d["msg_len"], d["rx_sec"],
                                          d["rx_usec"], window=window, per_flow=per_flow)
     compare(st, rep, cnt, of, orep, ocnt, per_flow)
+
+
+def test_flow_reduce_rows_equals_columns(torch, eng):
+    """mgenx_flow_reduce_rows (seq / tx time / msg_len from the 32-B unpack rows) leaves the
+    same flow state, reports and report records as the column form, which the tests above
+    pin to the oracle."""
+    from mgen_amd import FLOW_REPORT_DTYPE, FLOW_STATE_DTYPE, REC_DTYPE
+    from mgen_amd.workloads import poisson_flows
+    from oracle import oracle as O
+    n_flows, per_flow, window = 96, 8, 0.1
+    d = poisson_flows(150_000, n_flows, mean_gap_us=700, seed=21, loss=0.02, dup=0.01,
+                      reorder=20)
+    n = len(d["seq"])
+    rows = np.zeros(n, REC_DTYPE)
+    rows["flow_id"], rows["seq_num"] = d["flow_id"], d["seq"]
+    rows["tx_sec"], rows["tx_usec"], rows["msg_len"] = d["tx_sec"], d["tx_usec"], d["msg_len"]
+    rows["dst_len"], rows["payload_len"] = 4, 7     # fields the reduction does not read
+    idx = dev(torch, (d["flow_id"] - 1).astype(np.uint32))
+    out = []
+    for use_rows in (False, True):
+        flows = eng.flow_init(n_flows, window)
+        reports = torch.zeros(n_flows * per_flow * 96, dtype=torch.uint8, device="cuda")
+        count = torch.zeros(n_flows, dtype=torch.int32, device="cuda")
+        rrec = torch.zeros(n_flows * per_flow, dtype=torch.int32, device="cuda")
+        if use_rows:
+            eng.flow_reduce_rows(flows, n_flows, idx, dev(torch, rows.view(np.uint8)),
+                                 dev(torch, d["rx_sec"]), dev(torch, d["rx_usec"]),
+                                 reports=reports, per_flow=per_flow, report_count=count,
+                                 report_rec=rrec)
+        else:
+            c = {k: dev(torch, v) for k, v in d.items()}
+            eng.flow_reduce(flows, n_flows, idx, c["seq"], c["tx_sec"], c["tx_usec"],
+                            c["msg_len"], c["rx_sec"], c["rx_usec"], reports=reports,
+                            per_flow=per_flow, report_count=count, report_rec=rrec)
+        torch.cuda.synchronize()
+        out.append((flows.cpu().numpy(), reports.cpu().numpy(), count.cpu().numpy(),
+                    rrec.cpu().numpy()))
+    for a, b in zip(*out):
+        assert np.array_equal(a, b)
+    st = out[1][0].view(FLOW_STATE_DTYPE)
+    rep = out[1][1].view(FLOW_REPORT_DTYPE).reshape(n_flows, per_flow)
+    of, orep, ocnt = O.flow_reduce_batch(n_flows, d["flow_id"] - 1, d["seq"], d["tx_sec"],
+                                         d["tx_usec"], d["msg_len"], d["rx_sec"],
+                                         d["rx_usec"], window=window, per_flow=per_flow)
+    compare(st, rep, out[1][2].view(np.uint32), of, orep, ocnt, per_flow)
