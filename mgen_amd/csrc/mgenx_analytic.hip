@@ -6,12 +6,12 @@
 // (restated in oracle/mgen_oracle.c; parity unpinned at protolib).
 //
 // The state machine is sequential per flow and independent across flows, so:
-//   1. records are ordered by flow, stably (receive order kept): hipCUB radix sort of
-//      (flow index, record index) -- plumbing, not the hot path;
-//   2. their fields (24 B per record, latency precomputed) are read through the sorted
-//      order, three rounds of 64 in flight;
-//   3. one wave per flow runs Update over its records (see WRing and the fast segments
-//      below).
+//   1. every record is written as the 24-B record the update reads (latency precomputed), and
+//      the records are ordered by flow, stably (receive order kept): `order`, a counting sort
+//      (per-tile flow histograms, one scan, a per-tile LDS sort written run by run) for up
+//      to 2047 flows, else a hipCUB radix sort of (flow, record) pairs;
+//   2. one wave per flow runs Update over its records, read through `order` (see WRing and
+//      the fast segments below).
 // FP64: every product that feeds an add goes through mul_rounded (an empty asm keeps the
 // backend from fusing them into an FMA: neither __dadd_rn/__dmul_rn nor `#pragma clang fp
 // contract(off)` prevented it -- a 1-ulp difference in a report's duration was the
@@ -223,13 +223,42 @@ struct WRing {
   }
 };
 
-// One received record as the update kernel reads it (written by flow_keys_kernel in input
-// order, read through the flow-sorted order): 24 bytes.  The latency ProtoTime::Delta(rx, tx)
-// depends on the record alone, so it is computed there, in parallel.
+// One received record as the update kernel reads it (24 B, written in input order, read
+// through `order`); the latency ProtoTime::Delta(rx, tx) depends on the record alone, so it
+// is computed when the record is written, off the per-flow chain.
 struct FRec {
   uint32_t seq, rxs, rxu, len;
   double latency;
 };
+
+// Where a record's fields come from: the columns, or the unpack's 32-B rows when `rows` is set.
+struct RecSrc {
+  const uint32_t *seq, *txs, *txu;
+  const uint16_t* len;
+  const mgenx_rec* rows;
+  const uint32_t *rxs, *rxu;
+};
+__device__ __forceinline__ FRec make_frec(const RecSrc& src, uint32_t i) {
+  FRec r;
+  uint32_t ts, tu;
+  if (src.rows) {
+    const u32x4_t h = *reinterpret_cast<const u32x4_t*>(src.rows + i);  // flow, seq, tx_sec, tx_usec
+    r.seq = h.y;
+    ts = h.z;
+    tu = h.w;
+    r.len = src.rows[i].msg_len;
+  } else {
+    r.seq = src.seq[i];
+    ts = src.txs[i];
+    tu = src.txu[i];
+    r.len = src.len[i];
+  }
+  r.rxs = src.rxs[i];
+  r.rxu = src.rxu[i];
+  r.latency = tdelta(Tm{(int64_t)r.rxs, (int64_t)r.rxu}, Tm{(int64_t)ts, (int64_t)tu});
+  return r;
+}
+
 
 // Wave-uniform values: the window times come out of FP64 arithmetic (VALU), so without
 // these the compiler treats every later compare and branch on them as divergent.
@@ -244,7 +273,7 @@ __device__ __forceinline__ Tm uni_t(Tm t) { return Tm{uni64(t.sec), uni64(t.usec
 
 __global__ void __launch_bounds__(256)
 flow_update_wave_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
-                        const uint32_t* __restrict__ begin, const uint32_t* __restrict__ end,
+                        const uint32_t* __restrict__ bnd, uint32_t bstride,
                         const uint32_t* __restrict__ order, const FRec* __restrict__ recs,
                         mgenx_flow_report* __restrict__ reports, uint32_t per_flow,
                         uint32_t* __restrict__ report_count, uint32_t* __restrict__ report_rec,
@@ -252,7 +281,7 @@ flow_update_wave_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t f = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
   if (f >= n_flows) return;
-  const uint32_t b = begin[f], e = end[f];
+  const uint32_t b = bnd[(size_t)f * bstride], e = bnd[(size_t)(f + 1u) * bstride];
   if (b >= e) return;
   mgenx_flow_state* sp = flows + f;
   const double window = sp->window_size;
@@ -396,7 +425,31 @@ flow_update_wave_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
   // bit-exact).  Late (reordered) arrivals qualify.  Anything else -- duplicates, mask
   // restarts, window ends, seq below seq_start, msg == 0 -- takes the general update above.
   __shared__ uint32_t scat[4][32];
-  __shared__ double latl[4][64];
+  __shared__ alignas(16) double latl[4][64];
+  // Deferred, order-free parts of the fast runs, per lane: latency min / max, bytes, and the
+  // highest seq - first (for `last`).  Folded into the wave-uniform state by flush() only
+  // before a general update and at the end -- not after every run (no wave reductions on
+  // the per-run path).  `first` does not move between flushes (runs never take Set's d < 0
+  // branch), and msg_count == 1 at a run's start only right after a general update, so the
+  // byte restart of :128-129 sees nothing pending.
+  const double inf = __builtin_huge_val();
+  double pmin = inf, pmax = -inf;
+  uint32_t pbytes = 0, pdmax = 0, pruns = 0;
+  bool dirty = false;
+  auto flush = [&]() {
+    if (!dirty) return;
+    lmin = __builtin_fmin(lmin, WRing::wave_reduce_f64(pmin, inf, [](double a, double c) {
+      return __builtin_fmin(a, c); }));
+    lmax = __builtin_fmax(lmax, WRing::wave_reduce_f64(pmax, -inf, [](double a, double c) {
+      return __builtin_fmax(a, c); }));
+    const uint64_t lo = WRing::wave_sum(pbytes & 0xFFFFu), hi = WRing::wave_sum(pbytes >> 16);
+    byte_count += lo + (hi << 16);
+    m.last = m.first + max(WRing::wave_max(pdmax), m.last - m.first);
+    pmin = inf;
+    pmax = -inf;
+    pbytes = pdmax = pruns = 0;
+    dirty = false;
+  };
   const uint32_t wv = threadIdx.x >> 6;
   // trial: the run's bits into a zeroed LDS copy of the ring; true when two records of the
   // run share a seq (a duplicate inside the run -- then the run is recomputed exactly)
@@ -418,32 +471,35 @@ flow_update_wave_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
     if (lane < 32u) m.w |= scat[wv][lane];
     __builtin_amdgcn_wave_barrier();
     m.n += e - k;
-    const uint32_t dmax = WRing::wave_max(in ? r.seq - m.first : 0u);
-    m.last = m.first + max(dmax, m.last - m.first);
-    // counters: byte_count restarts at the first record when msg_count == 1 (:128-129)
-    const uint32_t bsum = WRing::wave_sum(in ? r.len : 0u);
-    byte_count = (msg_count == 1 ? 0ull : byte_count) + bsum;
+    if (msg_count == 1) byte_count = 0;  // :128-129 (nothing pending here, see above)
     msg_count += e - k;
+    const double lat = __builtin_bit_cast(double, (uint64_t)lhi << 32 | llo);
     // min / max as fmin / fmax -- the reference's "if (l < min) min = l; else if (l > max)
     // max = l" is exactly that for latencies (never NaN, never -0: ProtoTime::Delta of
-    // integer fields) with min <= max -- so order-free: one DPP wave reduction each.
-    const double lat = __builtin_bit_cast(double, (uint64_t)lhi << 32 | llo);
-    const double inf = __builtin_huge_val();
-    lmin = __builtin_fmin(lmin, WRing::wave_reduce_f64(in ? lat : inf, inf,
-                                                        [](double a, double b) { return __builtin_fmin(a, b); }));
-    lmax = __builtin_fmax(lmax, WRing::wave_reduce_f64(in ? lat : -inf, -inf,
-                                                        [](double a, double b) { return __builtin_fmax(a, b); }));
+    // integer fields) with min <= max -- so order-free
+    pmin = in ? __builtin_fmin(pmin, lat) : pmin;
+    pmax = in ? __builtin_fmax(pmax, lat) : pmax;
+    pbytes += in ? r.len : 0u;
+    pdmax = in ? max(pdmax, r.seq - m.first) : pdmax;
+    dirty = true;
     // the sum in record order (bit-exact): the run's latencies staged in LDS and read back
-    // as broadcasts, so the loop is the dependent v_add_f64 chain and independent ds_reads
-    latl[wv][lane] = lat;
+    // as broadcasts, two per read, so the loop is the dependent v_add_f64 chain
+    if (in) latl[wv][lane - k] = lat;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     double vs = lsum;
-    const uint32_t ee = (MGENX_DIAG && (abl & 1)) ? k : e;
-#pragma unroll 8
-    for (uint32_t j = k; j < ee; j++) vs = __dadd_rn(vs, latl[wv][j]);
+    const uint32_t run = (MGENX_DIAG && (abl & 1)) ? 0u : e - k;
+    const double2* lp = reinterpret_cast<const double2*>(latl[wv]);
+#pragma unroll 4
+    for (uint32_t j = 0; j < run / 2u; j++) {
+      const double2 v = lp[j];
+      vs = __dadd_rn(vs, v.x);
+      vs = __dadd_rn(vs, v.y);
+    }
+    if (run & 1u) vs = __dadd_rn(vs, latl[wv][run - 1u]);
     lsum = vs;
     __builtin_amdgcn_wave_barrier();
+    if (++pruns == 65536u) flush();  // pbytes per lane stays below 2^32
   };
 
   // 64 records per round: lane k holds record order[i0 + k]; the record loads of the next
@@ -498,6 +554,7 @@ flow_update_wave_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
         k += run;
         if (k >= cnt) break;
       }
+      flush();
       const uint64_t lb = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)lhi, (int)k) << 32 |
                           (uint32_t)__builtin_amdgcn_readlane((int)llo, (int)k);
       if (!(MGENX_DIAG && (abl & 2)))
@@ -516,6 +573,7 @@ flow_update_wave_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
     i0 += 64u;
   }
 
+  flush();
   m.store_relative(sp->mask);
   if (lane == 0) {
     sp->mask_first = m.first;
@@ -537,50 +595,144 @@ flow_update_wave_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
   }
 }
 
-// keys: flow index clamped to n_flows (records to skip sort last); vals: record index;
-// recs: the record as the update kernel reads it, with its latency
-// (the record fields come from the columns, or from the unpack's 32-B rows when `rows` is set)
+// ---- ordering the records by flow, stably: a counting sort (flow count < kCountBins) --
+// The output is `order`: the input index of every record, flow after flow, receive order kept
+// within a flow; the hist kernel also writes every record as the 24-B FRec the update
+// reads (in input order, coalesced; the update gathers them through `order`).
+// (Measured alternatives, config 4: gathering the fields straight from the columns in the
+// update, 0.82 ms; writing the FRecs in flow order from the order kernel, 0.67-0.72 ms.)
+//   hist:  per-tile flow histogram (kTile records per tile), stored flow-major
+//          (hist[flow * n_tiles + tile]);
+//   scan:  exclusive prefix sum of hist = where each (flow, tile) run starts in `order`;
+//   order: each tile is sorted by flow in LDS (stable: waves own contiguous eighths, ranks
+//          inside a 64-record step from ballots on the key bits), then written run by run --
+//          consecutive lanes to consecutive slots -- instead of one scattered 4-B store per
+//          record.  Tiles go to XCDs in contiguous ranges (blockIdx mod 8 = XCD), so the runs
+//          of one flow from neighbouring tiles meet in the same L2 and leave it as whole lines.
+// Records whose flow index is >= n_flows (MGENX_FLOW_NONE) go to the extra last bin and are
+// not written.
+constexpr uint32_t kCountBins = 2048;  // LDS: (9 x bins + kTile) x 4 + kTile x 2 bytes
+constexpr uint32_t kSortWaves = 8;
+constexpr uint32_t kTile = 8192;
+constexpr uint32_t kPart = kTile / kSortWaves;
+
+__global__ void __launch_bounds__(512)
+flow_hist_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows, uint32_t n_tiles,
+                 uint32_t* __restrict__ hist, RecSrc src, FRec* __restrict__ recs) {
+  extern __shared__ uint32_t h[];
+  const uint32_t bins = n_flows + 1u;
+  for (uint32_t k = threadIdx.x; k < bins; k += blockDim.x) h[k] = 0u;
+  __syncthreads();
+  const uint32_t a = blockIdx.x * kTile, e = min(n, a + kTile);
+  for (uint32_t i = a + threadIdx.x; i < e; i += blockDim.x) {
+    atomicAdd(&h[min(idx[i], n_flows)], 1u);
+    recs[i] = make_frec(src, i);  // input order, coalesced
+  }
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < bins; k += blockDim.x) hist[(size_t)k * n_tiles + blockIdx.x] = h[k];
+}
+
+__global__ void __launch_bounds__(512)
+flow_order_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows,
+                  uint32_t n_tiles, const uint32_t* __restrict__ start,
+                  uint32_t* __restrict__ order, uint32_t key_bits) {
+  extern __shared__ uint32_t lds[];
+  const uint32_t bins = n_flows + 1u;
+  uint32_t* cnt = lds;                                // [wave][bin]: counts, then run bases
+  uint32_t* sbase = lds + kSortWaves * bins;          // [bin]: start - tile offset
+  uint32_t* lsorted = sbase + bins;                   // [kTile]: input index, flow-sorted
+  uint16_t* lkey = reinterpret_cast<uint16_t*>(lsorted + kTile);  // [kTile]: its flow
+  __shared__ uint32_t wsum[kSortWaves];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+  // tile: contiguous ranges per XCD (block b runs on XCD b % 8)
+  const uint32_t per = (n_tiles + 7u) / 8u;
+  const uint32_t t = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
+  if (t >= n_tiles) return;  // whole block: no barrier below is reached by anyone
+  for (uint32_t k = tid; k < kSortWaves * bins; k += blockDim.x) cnt[k] = 0u;
+  __syncthreads();
+  const uint32_t t0 = t * kTile, tn = min(n - t0, kTile);
+  const uint32_t a = t0 + w * kPart, e = min(n, a + kPart);
+  uint32_t* my = cnt + w * bins;
+  for (uint32_t i = a + lane; i < e; i += 64u) atomicAdd(&my[min(idx[i], n_flows)], 1u);
+  __syncthreads();
+  // tile offsets: exclusive scan over bins of the tile's counts (thread j owns bins j*B..)
+  const uint32_t B = (bins + blockDim.x - 1u) / blockDim.x;
+  const uint32_t k0 = min(tid * B, bins), k1 = min(k0 + B, bins);
+  uint32_t local = 0;
+  for (uint32_t k = k0; k < k1; k++)
+#pragma unroll
+    for (uint32_t v = 0; v < kSortWaves; v++) local += cnt[v * bins + k];
+  uint32_t incl = local;  // inclusive wave scan
+#pragma unroll
+  for (uint32_t o = 1; o < 64u; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63u) wsum[w] = incl;
+  __syncthreads();
+  uint32_t run = incl - local;
+  for (uint32_t v = 0; v < w; v++) run += wsum[v];
+  for (uint32_t k = k0; k < k1; k++) {
+    sbase[k] = start[(size_t)k * n_tiles + t] - run;
+#pragma unroll
+    for (uint32_t v = 0; v < kSortWaves; v++) {
+      const uint32_t c = cnt[v * bins + k];
+      cnt[v * bins + k] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+  const uint64_t lt = (1ull << lane) - 1ull;
+  for (uint32_t i0 = a; i0 < e; i0 += 64u) {
+    const uint32_t i = i0 + lane;
+    const bool live = i < e;
+    const uint32_t key = live ? min(idx[i], n_flows) : 0u;
+    uint64_t peers = __ballot(live);  // lanes holding the same key
+    for (uint32_t bt = 0; bt < key_bits; bt++) {
+      const bool one = (key >> bt) & 1u;
+      const uint64_t bb = __ballot(one);
+      peers &= one ? bb : ~bb;
+    }
+    const uint32_t rank = (uint32_t)__popcll(peers & lt);
+    const uint32_t base = live ? my[key] : 0u;
+    if (live) {
+      const uint32_t pos = base + rank;
+      lsorted[pos] = i;
+      lkey[pos] = (uint16_t)key;
+      if (rank + 1u == (uint32_t)__popcll(peers)) my[key] = pos + 1u;
+    }
+  }
+  __syncthreads();
+  for (uint32_t j = tid; j < tn; j += blockDim.x) {
+    const uint32_t k = lkey[j];
+    if (k < n_flows) order[sbase[k] + j] = lsorted[j];
+  }
+}
+
+// ---- the general ordering (any flow count): hipCUB radix sort of (flow, record) pairs ----
+// keys: flow index clamped to n_flows (records to skip sort last); vals: record index
 __global__ void flow_keys_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows,
-                                 const uint32_t* __restrict__ seq, const uint32_t* __restrict__ txs,
-                                 const uint32_t* __restrict__ txu, const uint16_t* __restrict__ len,
-                                 const mgenx_rec* __restrict__ rows,
-                                 const uint32_t* __restrict__ rxs, const uint32_t* __restrict__ rxu,
                                  uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
-                                 FRec* __restrict__ recs) {
+                                 RecSrc src, FRec* __restrict__ recs) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   keys[i] = min(idx[i], n_flows);
   vals[i] = i;
-  FRec r;
-  uint32_t ts, tu;
-  if (rows) {
-    const u32x4_t h = *reinterpret_cast<const u32x4_t*>(rows + i);  // flow, seq, tx_sec, tx_usec
-    r.seq = h.y;
-    ts = h.z;
-    tu = h.w;
-    r.len = rows[i].msg_len;
-  } else {
-    r.seq = seq[i];
-    ts = txs[i];
-    tu = txu[i];
-    r.len = len[i];
-  }
-  r.rxs = rxs[i];
-  r.rxu = rxu[i];
-  r.latency = tdelta(Tm{(int64_t)r.rxs, (int64_t)r.rxu}, Tm{(int64_t)ts, (int64_t)tu});
-  recs[i] = r;
+  recs[i] = make_frec(src, i);
 }
 
-// segment bounds of each flow in the sorted keys
+// run starts: bnd[f] = first sorted position with flow >= f (f = 0..n_flows)
 __global__ void flow_bounds_kernel(const uint32_t* __restrict__ keys, uint32_t n, uint32_t n_flows,
-                                   uint32_t* __restrict__ begin, uint32_t* __restrict__ end) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t k = keys[i];
-  if (k < n_flows) {
-    if (i == 0 || keys[i - 1] != k) begin[k] = i;
-    if (i + 1 == n || keys[i + 1] != k) end[k] = i + 1;
+                                   uint32_t* __restrict__ bnd) {
+  const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f > n_flows) return;
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t mid = lo + (hi - lo) / 2u;
+    if (keys[mid] < f) lo = mid + 1u;
+    else hi = mid;
   }
+  bnd[f] = lo;
 }
 
 __global__ void flow_init_kernel(mgenx_flow_state* flows, uint32_t n_flows, double window) {
@@ -670,16 +822,32 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
                                      hipStream_t stream, char* err, size_t errn) {
   mgenx_flow_ws& ws = *static_cast<mgenx_flow_ws*>(wsp);
   if (n == 0 || n_flows == 0) return MGENX_OK;
-  int end_bit = 1;
-  while (end_bit < 32 && (1ull << end_bit) <= n_flows) end_bit++;
+  const RecSrc src = {seq, txs, txu, len, rows, rxs, rxu};
+  int sort_path = (uint64_t)n_flows + 1 <= kCountBins ? 0 : 1;  // 0 counting, 1 radix
+  int sabl = 0;  // diagnostics build only: ordering-only timing (MGENX_AN_SABL)
+#if MGENX_DIAG
+  if (const char* sp = getenv("MGENX_AN_RADIX")) sort_path = atoi(sp) ? 1 : sort_path;
+  if (const char* sa = getenv("MGENX_AN_SABL")) sabl = atoi(sa);
+#endif
+  const uint32_t bins = n_flows + 1u;
+  uint32_t key_bits = 1;
+  while (key_bits < 32 && (1ull << key_bits) <= n_flows) key_bits++;
+  const uint32_t n_tiles = (n + kTile - 1) / kTile;
+  const size_t n_hist = (size_t)bins * n_tiles;
   size_t cub_bytes = 0;
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, (const uint32_t*)nullptr,
-                                           (uint32_t*)nullptr, (const uint32_t*)nullptr,
-                                           (uint32_t*)nullptr, (int)n, 0, end_bit, stream);
-  // layout: keys_in, keys_out, vals_in, vals_out, begin, end, records (24 B), cub
-  const size_t nb = a256((size_t)n * 4), fb = a256((size_t)n_flows * 4);
-  const size_t rb = a256((size_t)n * sizeof(FRec));
-  const size_t need = 4 * nb + 2 * fb + rb + a256(cub_bytes);
+  if (sort_path == 0)
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, cub_bytes, (const uint32_t*)nullptr,
+                                           (uint32_t*)nullptr, (int)n_hist, stream);
+  else
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, (const uint32_t*)nullptr,
+                                             (uint32_t*)nullptr, (const uint32_t*)nullptr,
+                                             (uint32_t*)nullptr, (int)n, 0, (int)key_bits, stream);
+  const size_t nb = a256((size_t)n * 4), rb = a256((size_t)n * sizeof(FRec));
+  const size_t hb = a256(n_hist * 4), bb = a256((size_t)bins * 4);
+  // counting: hist, start, records, order, cub
+  // radix:    keys_in, keys_out, vals_in, order, records, bounds, cub
+  const size_t need = sort_path == 0 ? 2 * hb + rb + nb + a256(cub_bytes)
+                                     : 4 * nb + rb + bb + a256(cub_bytes);
   if (ws.bytes < need) {
     if (ws.mem) (void)hipFree(ws.mem);
     ws.mem = nullptr;
@@ -692,33 +860,66 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
   }
   char* p = static_cast<char*>(ws.mem);
   auto take = [&](size_t b) { char* q = p; p += b; return q; };
-  uint32_t* keys_in = (uint32_t*)take(nb);
-  uint32_t* keys_out = (uint32_t*)take(nb);
-  uint32_t* vals_in = (uint32_t*)take(nb);
-  uint32_t* vals_out = (uint32_t*)take(nb);
-  uint32_t* d_begin = (uint32_t*)take(fb);
-  uint32_t* d_end = (uint32_t*)take(fb);
-  FRec* recs = (FRec*)take(rb);
-  void* cub_tmp = take(a256(cub_bytes));
-  const dim3 g((n + 255) / 256);
-  hipLaunchKernelGGL(flow_keys_kernel, g, dim3(256), 0, stream, flow_idx, n, n_flows, seq, txs,
-                     txu, len, rows, rxs, rxu, keys_in, vals_in, recs);
-  hipError_t e = hipcub::DeviceRadixSort::SortPairs(cub_tmp, cub_bytes, keys_in, keys_out,
-                                                    vals_in, vals_out, (int)n, 0, end_bit, stream);
-  if (e != hipSuccess) {
-    snprintf(err, errn, "flow_reduce sort: %s", hipGetErrorString(e));
-    return MGENX_EDEVICE;
+  const uint32_t* bnd;
+  uint32_t bstride;
+  uint32_t* order;
+  FRec* recs;
+  hipError_t e;
+  if (sort_path == 0) {
+    uint32_t* hist = (uint32_t*)take(hb);
+    uint32_t* start = (uint32_t*)take(hb);
+    recs = (FRec*)take(rb);
+    order = (uint32_t*)take(nb);
+    void* cub_tmp = take(a256(cub_bytes));
+    hipLaunchKernelGGL(flow_hist_kernel, dim3(n_tiles), dim3(512), bins * 4u, stream, flow_idx, n,
+                       n_flows, n_tiles, hist, src, recs);
+    e = hipcub::DeviceScan::ExclusiveSum(cub_tmp, cub_bytes, hist, start, (int)n_hist, stream);
+    if (e != hipSuccess) {
+      snprintf(err, errn, "flow_reduce scan: %s", hipGetErrorString(e));
+      return MGENX_EDEVICE;
+    }
+    // LDS: per-wave counts, bases, the sorted tile (index + 16-bit flow)
+    const uint32_t lds = (kSortWaves * bins + bins + kTile) * 4u + kTile * 2u;
+    static bool lds_set = false;
+    if (!lds_set) {
+      (void)hipFuncSetAttribute((const void*)flow_order_kernel,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 256);
+      lds_set = true;
+    }
+    const uint32_t grid = 8u * ((n_tiles + 7u) / 8u);
+    hipLaunchKernelGGL(flow_order_kernel, dim3(grid), dim3(64 * kSortWaves), lds, stream,
+                       flow_idx, n, n_flows, n_tiles, start, order, key_bits);
+    bnd = start;
+    bstride = n_tiles;
+  } else {
+    uint32_t* keys_in = (uint32_t*)take(nb);
+    uint32_t* keys_out = (uint32_t*)take(nb);
+    uint32_t* vals_in = (uint32_t*)take(nb);
+    order = (uint32_t*)take(nb);
+    recs = (FRec*)take(rb);
+    uint32_t* d_bnd = (uint32_t*)take(bb);
+    void* cub_tmp = take(a256(cub_bytes));
+    hipLaunchKernelGGL(flow_keys_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, flow_idx, n,
+                       n_flows, keys_in, vals_in, src, recs);
+    e = hipcub::DeviceRadixSort::SortPairs(cub_tmp, cub_bytes, keys_in, keys_out, vals_in, order,
+                                           (int)n, 0, (int)key_bits, stream);
+    if (e != hipSuccess) {
+      snprintf(err, errn, "flow_reduce sort: %s", hipGetErrorString(e));
+      return MGENX_EDEVICE;
+    }
+    hipLaunchKernelGGL(flow_bounds_kernel, dim3((bins + 255) / 256), dim3(256), 0, stream, keys_out,
+                       n, n_flows, d_bnd);
+    bnd = d_bnd;
+    bstride = 1;
   }
-  (void)hipMemsetAsync(d_begin, 0, fb, stream);
-  (void)hipMemsetAsync(d_end, 0, fb, stream);
-  hipLaunchKernelGGL(flow_bounds_kernel, g, dim3(256), 0, stream, keys_out, n, n_flows, d_begin,
-                     d_end);
+  if (sabl) return MGENX_OK;  // timing study: ordering only
   int abl = 0;  // diagnostics build only: ablations of the update kernel (timing studies)
 #if MGENX_DIAG
   if (const char* a = getenv("MGENX_AN_ABL")) abl = atoi(a);
 #endif
   hipLaunchKernelGGL(flow_update_wave_kernel, dim3((n_flows + 3) / 4), dim3(256), 0, stream,
-                     flows, n_flows, d_begin, d_end, vals_out, recs, reports, per_flow,
+                     flows, n_flows, bnd, bstride, order, recs,
+                     reports, per_flow,
                      report_count, report_rec, abl);
   e = hipGetLastError();
   if (e != hipSuccess) {

@@ -424,7 +424,8 @@ static int pack_common(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
                        const uint8_t* dev_pool, uint8_t* dev_slab, uint64_t slab_bytes,
                        const uint64_t* dev_rec_off, uint64_t stride, const uint32_t* dev_buf_len,
                        const uint32_t* dev_crc_in, uint32_t* dev_out_len, uint32_t* dev_tx_crc,
-                       uint32_t* dev_state, uint32_t opts, uint32_t fill_time, void* stream) {
+                       uint32_t* dev_state, uint32_t opts, uint32_t fill_time, void* stream,
+                       const uint32_t* dev_frag_len = nullptr, int frag_ck = 0) {
   if (!ctx) return MGENX_EINVAL;
   if (n == 0) return MGENX_OK;
   if (!dev_tmpl || !dev_tmpl_crc || !dev_desc || !dev_slab || !dev_out_len) return MGENX_EINVAL;
@@ -455,6 +456,8 @@ static int pack_common(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
   p.crc_in = dev_crc_in;
   p.tx_crc = dev_tx_crc;
   p.state = dev_state;
+  p.frag_len = dev_frag_len;
+  p.frag_ck = frag_ck;
   const uint64_t batches = ((uint64_t)n + 63) / 64;
   uint64_t grid = (batches + 3) / 4;                // groups of 4 batches (kProd)
   uint64_t cap = (uint64_t)ctx->cu_count * 2;  // 76 KB of LDS per workgroup
@@ -585,7 +588,7 @@ int mgenx_pack_tcp(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl, const uint32
       return set_err(ctx, e, "tcp fragments");
     int rc = pack_common(ctx, dev_tmpl, dev_tmpl_crc, fd, n, dev_pool, dev_stream, stream_cap,
                          foff, 0, fbuf, nullptr, plen, crc, st[r & 1], opts | MGENX_PACK_RAW,
-                         fill_time, stream);
+                         fill_time, stream, ff, ck);
     if (rc != MGENX_OK) return rc;
     if ((e = mgenx::launch_tcp_tail(dev_stream, foff, fbuf, ff, plen, crc, st[r & 1], n, ck,
                                     (opts & MGENX_PACK_RANDOM_FILL) ? 1 : 0, acrc,

@@ -48,6 +48,9 @@ struct PackParams {
   const uint32_t* crc_in;    // MGENX_PACK_RAW: tx_checksum argument on entry (NULL = 0)
   uint32_t* tx_crc;          // optional: tx_checksum after Pack
   uint32_t* state;           // optional: packet_header_len | flags << 16 after Pack
+  const uint32_t* frag_len;  // MGENX_PACK_RAW, TCP: fragment length F; when F > bufferLen the
+                             // later buffers' copies of the image are stored too (NULL = none)
+  int frag_ck;               // the TCP transport's checksum setting (buffer sizes depend on it)
   int variant;               // diagnostic ablation (0 = product path)
 };
 

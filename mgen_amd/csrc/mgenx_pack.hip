@@ -37,7 +37,49 @@ struct PackMeta {
   uint8_t trailer_on, rf;
   uint32_t tx_out;   // tx_checksum after Pack (out: tx_crc)
   uint32_t state;    // packet_header_len | flags << 16 (out: state)
+  uint32_t frag;     // TCP fragment length F > ret: later buffers repeat the image (else 0)
 };
+
+// MgenTcpTransport re-sends a fragment's 8-KiB Pack buffer P until F bytes have gone out
+// (SetupNextTxBuffer, mgenTransport.cpp:1818-1852): later buffer k starts at start[k] and
+// carries P[0 .. cnt[k]) (the last one 4 bytes less with a checksum: its CRC trailer is
+// written afterwards).  At most 8 later buffers (F <= 65535, buffers of >= 8185 bytes).
+constexpr int kMaxRep = 9;
+struct TcpReps {
+  uint32_t start[kMaxRep], cnt[kMaxRep];
+};
+__device__ __forceinline__ TcpReps tcp_reps(uint32_t F, uint32_t B, bool ck) {
+  TcpReps t;
+  uint32_t pb = B;
+  bool done = F <= B;
+#pragma unroll
+  for (int k = 0; k < kMaxRep; k++) {
+    uint32_t st = 0, cnt = 0;
+    if (!done) {
+      const uint32_t pend = F - pb;
+      if (pend == 0) {
+        done = true;
+      } else {
+        uint32_t sz;
+        bool last = false;
+        if ((ck && pend <= MGENX_TX_BUFFER_SIZE - 4u) || (!ck && pend <= MGENX_TX_BUFFER_SIZE)) {
+          sz = pend;
+          last = true;
+        } else {
+          sz = (ck && (int32_t)pend - (int32_t)MGENX_TX_BUFFER_SIZE < 4) ? pend - 4u
+                                                                          : MGENX_TX_BUFFER_SIZE;
+        }
+        st = pb;
+        cnt = (last && ck) ? sz - 4u : sz;
+        pb += sz;
+        done = last;
+      }
+    }
+    t.start[k] = st;
+    t.cnt[k] = cnt < B ? cnt : B;
+  }
+  return t;
+}
 
 __device__ __forceinline__ void img_put8(uint8_t* img, uint32_t at, uint32_t v) {
   if (at < kImg) img[at] = (uint8_t)v;
@@ -104,7 +146,7 @@ pack_kernel(PackParams p) {
     uint8_t* img = S_IMG + lane * kImg;
     PackMeta m;
     m.off = 0; m.ret = 0; m.trailer = 0; m.pend = 0; m.poff = 0; m.hdr = 0;
-    m.trailer_on = 0; m.rf = rf ? 1 : 0; m.tx_out = 0; m.state = 0;
+    m.trailer_on = 0; m.rf = rf ? 1 : 0; m.tx_out = 0; m.state = 0; m.frag = 0;
 
     // ------------------------------ phase 1: meta ------------------------------
     if (i < p.n) {
@@ -275,6 +317,10 @@ pack_kernel(PackParams p) {
         }
       }
       if (m.off > p.slab_bytes || m.ret > p.slab_bytes - m.off) m.ret = 0;  // never write OOB
+      if (p.frag_len && m.ret) {
+        const uint32_t F = p.frag_len[i];
+        if (F > m.ret && F <= p.slab_bytes - m.off) m.frag = F;
+      }
       m.tx_out = tx_out;
       // the MgenMsg members Pack leaves behind: packet_header_len (set on every return but
       // the failing ones) and the flags member (CHECKSUM set, LAST_BUFFER cleared)
@@ -338,7 +384,7 @@ pack_kernel(PackParams p) {
       goto stage_end;
     }
     const uint64_t next_off = __shfl_down(m.off, 1);
-    const bool packed_ok = !has || (m.ret >= 16u && m.pend <= (uint32_t)kImg &&
+    const bool packed_ok = !has || (m.ret >= 16u && m.pend <= (uint32_t)kImg && m.frag == 0u &&
                                     ((uint32_t)lane + 1 == nv || m.off + m.ret == next_off));
     // (diagnostics: variant 3 = never the fast path, 4 = fill-then-rewrite scheme, its zero
     // fill only, 5 = that scheme without its wait, 6 = no aligned-stride path)
@@ -463,6 +509,7 @@ pack_kernel(PackParams p) {
     int ri = 0;
     uint32_t rstart = 0, next_start = s_pre[slot][1];
     PackMeta r = S_META[0];
+    TcpReps reps = tcp_reps(r.frag, r.ret, p.frag_ck != 0);
     for (uint32_t u = lane; u < ((variant == 1 || variant == 4) ? 0u : total); u += 64) {
       if (next_start <= u) {
         do {
@@ -471,6 +518,7 @@ pack_kernel(PackParams p) {
           next_start = s_pre[slot][ri + 1];
         } while (next_start <= u);
         r = S_META[ri];
+        reps = tcp_reps(r.frag, r.ret, p.frag_ck != 0);
       }
       uint32_t pos = (u - rstart) << 4;
       if (fast) {  // image units, then the record's last 16 bytes (past the image)
@@ -537,6 +585,19 @@ pack_kernel(PackParams p) {
 #pragma unroll
         for (int j = 0; j < 16; j++)
           if ((uint32_t)j < rem) dst[j] = (uint8_t)(v[j >> 2] >> ((j & 3) * 8));
+      }
+      // TCP: the same bytes in every later buffer of the fragment (no copy pass re-reading P)
+#pragma unroll
+      for (int k = 0; k < kMaxRep; k++) {
+        if (pos < reps.cnt[k]) {
+          uint8_t* d2 = p.slab + r.off + reps.start[k] + pos;
+          if (pos + 16u <= reps.cnt[k]) {
+            stu128(d2, u32x4_t{v[0], v[1], v[2], v[3]});
+          } else {
+            const uint32_t rem = reps.cnt[k] - pos;
+            for (uint32_t j = 0; j < rem; j++) d2[j] = (uint8_t)(v[j >> 2] >> ((j & 3) * 8));
+          }
+        }
       }
     }
     }

@@ -12,8 +12,9 @@
 // GPU form, per round r (fragment r of every message; one round unless M > 65535):
 //   tcp_frag_kernel   fragment descriptors: msg_len = F, Pack's bufferLen B, flags, offset;
 //   raw Pack          (mgenx_pack.hip, MGENX_PACK_RAW) the B-byte buffer P at the fragment
-//                     start, its running CRC and the MgenMsg flags it leaves;
-//   tcp_copy_kernel   P[0 .. s_k) for every later buffer k of the fragment;
+//                     start, its running CRC and the MgenMsg flags it leaves -- and, as each
+//                     16-byte unit of P is stored, its copies P[0 .. s_k) in every later
+//                     buffer k of the fragment (PackParams.frag_len: no copy pass);
 //   tcp_prefix_kernel A(s) = ComputeCRC32 from a restart over P[0 .. s) for the (at most
 //                     three) distinct buffer lengths of the fragment, from P's header and
 //                     payload bytes and the fill algebra (no re-read of the buffer);
@@ -145,28 +146,6 @@ __device__ __forceinline__ bool tcp_buffer(uint32_t F, uint32_t B, int ck, uint3
   }
 }
 
-// copy P[0 .. s) (the last buffer: s - 4 with a checksum) to every later buffer; one
-// workgroup per fragment, 16 bytes per lane per step (P was just written: L2 hits)
-__global__ void __launch_bounds__(256)
-tcp_copy_kernel(uint8_t* __restrict__ out, const uint64_t* __restrict__ foff,
-                const uint32_t* __restrict__ fbuf, const uint32_t* __restrict__ ff,
-                const uint32_t* __restrict__ plen, uint32_t n, int ck) {
-  const uint32_t i = blockIdx.x;
-  if (i >= n) return;
-  const uint32_t F = ff[i], B = fbuf[i];
-  if (F <= B || plen[i] == 0) return;
-  uint8_t* base = out + foff[i];
-  uint32_t start, size;
-  bool last;
-  for (uint32_t k = 1; tcp_buffer(F, B, ck, k, start, size, last); k++) {
-    const uint32_t cnt = (last && ck) ? size - 4u : size;
-    uint8_t* dst = base + start;
-    const uint32_t nv = cnt >> 4;
-    for (uint32_t v = threadIdx.x; v < nv; v += blockDim.x) stu128(dst + 16u * v, ldu128(base + 16u * v));
-    for (uint32_t b = (nv << 4) + threadIdx.x; b < cnt; b += blockDim.x) dst[b] = base[b];
-  }
-}
-
 // A(s) = crc32(P[0 .. s)) for the (at most three) distinct CRC lengths of a fragment's later
 // buffers (full 8192, one SetupNextTxBuffer-shortened buffer, the last one's size - 4),
 // without re-reading the 8-KiB buffer: P is Pack's image -- header (packet_header_len h
@@ -278,7 +257,6 @@ hipError_t launch_tcp_tail(uint8_t* out, const uint64_t* foff, const uint32_t* f
                            const uint32_t* state, uint32_t n, int ck, int rnd, uint32_t* acrc,
                            const uint32_t* byte_tab, const uint32_t* xpow, const uint32_t* ia,
                            const uint32_t* rcrc, hipStream_t s) {
-  hipLaunchKernelGGL(tcp_copy_kernel, dim3(n), dim3(256), 0, s, out, foff, fbuf, ff, plen, n, ck);
   if (ck) {
     hipLaunchKernelGGL(tcp_prefix_kernel, dim3((n + 255) / 256), dim3(256), 0, s, out, foff, fbuf,
                        ff, plen, state, n, ck, rnd, byte_tab, xpow, rcrc, acrc);

@@ -1,6 +1,8 @@
 """Timing of mgenx_flow_reduce on config 4 data with the diagnostics build's update-kernel
 ablations (MGENX_AN_ABL bits: 1 no latency sum loop, 2 no general update, 4 no fast runs,
-8 no run commit).  Results are wrong under ablation; timing only."""
+8 no run commit; "r" = abl 0 with the radix-sort ordering, MGENX_AN_RADIX; ordering only,
+"s" = the ordering alone, MGENX_AN_SABL).  Results are wrong
+under ablation; timing only."""
 import os
 import subprocess
 import sys
@@ -9,8 +11,10 @@ import time
 import numpy as np
 
 if len(sys.argv) == 1:
-    for a in [int(x) for x in os.environ.get("ABLS", "0,1,2,8,3,4").split(",")]:
-        env = dict(os.environ, MGENX_AN_ABL=str(a))
+    for a in os.environ.get("ABLS", "0,r,1,2,8,3,4").split(","):
+        env = dict(os.environ, MGENX_AN_ABL="0" if a in "rs" else a,
+                   MGENX_AN_RADIX="1" if a == "r" else "0",
+                   MGENX_AN_SABL="1" if a == "s" else "0")
         r = subprocess.run([sys.executable, __file__, "run"], env=env, capture_output=True,
                            text=True, timeout=200)
         print("abl", a, r.stdout.strip()[-200:], r.stderr.strip()[-300:] if r.returncode else "")
@@ -24,6 +28,9 @@ from mgen_amd.workloads import poisson_flows  # noqa: E402
 
 eng = Engine(0, diag=True)
 d = poisson_flows(8388608, 1024, mean_gap_us=1000)
+if os.environ.get("SORTED") == "1":   # input already in flow order: `order` is the identity
+    o = np.argsort(d["flow_id"], kind="stable")
+    d = {k: np.ascontiguousarray(v[o]) for k, v in d.items()}
 t = {k: torch.from_numpy(v).cuda() for k, v in d.items()}
 idx = torch.from_numpy((d["flow_id"] - 1).astype(np.uint32)).cuda()
 n = len(d["seq"])

@@ -3,7 +3,7 @@
 set -u
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_gpu_analytics.py tests/test_gpu_flowtab.py tests/test_gpu_report.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/an_tests.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_analytics.py tests/test_gpu_flowtab.py tests/test_gpu_report.py tests/test_gpu_pcap.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/an_tests.log 2>&1
 rc=$?; tail -3 gpurun_out/an_tests.log
 [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python -u scripts/c4_only.py > gpurun_out/c4.log 2>&1 || exit 1

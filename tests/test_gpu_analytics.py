@@ -200,3 +200,50 @@ def test_flow_reduce_rows_equals_columns(torch, eng):
                                          d["tx_usec"], d["msg_len"], d["rx_sec"],
                                          d["rx_usec"], window=window, per_flow=per_flow)
     compare(st, rep, out[1][2].view(np.uint32), of, orep, ocnt, per_flow)
+
+
+def test_flow_reduce_many_flows_radix_path(torch, eng):
+    """More than 2047 flows: the radix-sort ordering instead of the counting sort (same
+    update kernel), against the oracle."""
+    from mgen_amd.workloads import poisson_flows
+    from oracle import oracle as O
+    n_flows, per_flow = 5000, 4
+    d = poisson_flows(200_000, n_flows, mean_gap_us=20_000, seed=33, reorder=40)
+    st, rep, cnt, _ = run_gpu(torch, eng, d, n_flows, 0.2, per_flow)
+    of, orep, ocnt = O.flow_reduce_batch(n_flows, d["flow_id"] - 1, d["seq"], d["tx_sec"],
+                                         d["tx_usec"], d["msg_len"], d["rx_sec"],
+                                         d["rx_usec"], window=0.2, per_flow=per_flow)
+    assert int(ocnt.sum()) > n_flows
+    compare(st, rep, cnt, of, orep, ocnt, per_flow)
+
+
+def test_flow_reduce_flow_none_and_tile_edges(torch, eng):
+    """Records with MGENX_FLOW_NONE or an index >= n_flows are skipped; batch sizes around the
+    counting sort's 8192-record tile (one short tile, exact tiles, one record past)."""
+    from mgen_amd.workloads import poisson_flows
+    from oracle import oracle as O
+    d = poisson_flows(40_000, 40, mean_gap_us=300, seed=8)
+    n = len(d["seq"])
+    rng = np.random.default_rng(3)
+    idx = (d["flow_id"] - 1).astype(np.uint32)
+    junk = rng.random(n) < 0.1
+    idx[junk] = np.where(rng.random(int(junk.sum())) < 0.5, 0xFFFFFFFF, 40 + 7).astype(np.uint32)
+    keep = ~junk
+    for m in (100, 8192, 16384, 8193, n):
+        flows = eng.flow_init(40, 0.05)
+        reports = torch.zeros(40 * 8 * 96, dtype=torch.uint8, device="cuda")
+        count = torch.zeros(40, dtype=torch.int32, device="cuda")
+        c = {k: dev(torch, v[:m]) for k, v in d.items()}
+        eng.flow_reduce(flows, 40, dev(torch, idx[:m]), c["seq"], c["tx_sec"], c["tx_usec"],
+                        c["msg_len"], c["rx_sec"], c["rx_usec"], reports=reports, per_flow=8,
+                        report_count=count)
+        torch.cuda.synchronize()
+        from mgen_amd import FLOW_REPORT_DTYPE, FLOW_STATE_DTYPE
+        st = flows.cpu().numpy().view(FLOW_STATE_DTYPE)
+        rep = reports.cpu().numpy().view(FLOW_REPORT_DTYPE).reshape(40, 8)
+        k = keep[:m]
+        sub = {key: v[:m][k] for key, v in d.items()}
+        of, orep, ocnt = O.flow_reduce_batch(40, sub["flow_id"] - 1, sub["seq"], sub["tx_sec"],
+                                             sub["tx_usec"], sub["msg_len"], sub["rx_sec"],
+                                             sub["rx_usec"], window=0.05, per_flow=8)
+        compare(st, rep, count.cpu().numpy().view(np.uint32), of, orep, ocnt, 8)
