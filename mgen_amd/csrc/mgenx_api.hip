@@ -490,21 +490,12 @@ int mgenx_pack_msgs(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
 }
 
 // the maximum fragment count and the stream total into host-mapped memory
-__global__ void tcp_totals_kernel(const uint32_t* nfrag, uint32_t n, const uint64_t* off,
-                                  uint64_t* host) {
-  __shared__ uint32_t mx[256];
-  uint32_t m = 0;
-  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) m = nfrag[i] > m ? nfrag[i] : m;
-  mx[threadIdx.x] = m;
-  __syncthreads();
-  for (uint32_t s = 128; s; s >>= 1) {
-    if (threadIdx.x < s) mx[threadIdx.x] = max(mx[threadIdx.x], mx[threadIdx.x + s]);
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    host[0] = off[n];
-    host[1] = mx[0];
-  }
+// the stream length and the round count (the plan kernel's maximum fragment count) for
+// the host, in one 16-byte copy
+__global__ void tcp_totals_kernel(const uint32_t* max_frag, uint32_t n, const uint64_t* off,
+                                  uint64_t* out) {
+  out[0] = off[n];
+  out[1] = *max_frag;
 }
 
 static size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -534,13 +525,13 @@ int mgenx_pack_tcp(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl, const uint32
     ctx->tcp_host_dev = static_cast<uint64_t*>(dp);
   }
   // workspace: bytes[n+1], nfrag[n], cub; per round: fd, foff, fbuf, ff, plen, crc, state x2,
-  // acrc[3n]
+  // acrc[3n]; the maximum fragment count
   size_t cub_bytes = 0;
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, cub_bytes, (const uint64_t*)nullptr,
                                          (uint64_t*)nullptr, (int)(n + 1), s);
   const size_t b8 = a256((size_t)(n + 1) * 8), b4 = a256((size_t)n * 4);
   const size_t need = b8 + b4 + a256(cub_bytes) + a256((size_t)n * sizeof(mgenx_pack_desc)) +
-                      b8 + 4 * b4 + 2 * b4 + 3 * b4;
+                      b8 + 4 * b4 + 2 * b4 + 3 * b4 + 256;
   if (ctx->tcp_ws_bytes < need) {
     if (ctx->tcp_ws) hipFree(ctx->tcp_ws);
     ctx->tcp_ws = nullptr;
@@ -561,9 +552,12 @@ int mgenx_pack_tcp(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl, const uint32
   uint32_t* crc = (uint32_t*)take(b4);
   uint32_t* st[2] = {(uint32_t*)take(b4), (uint32_t*)take(b4)};
   uint32_t* acrc = (uint32_t*)take(3 * b4);
+  uint32_t* max_frag = (uint32_t*)take(256);
   // plan: bytes per message, fragments; offsets by an exclusive scan (the message offsets
   // are the caller's array: n + 1 entries are not assumed, the scan runs in the workspace)
-  if ((e = mgenx::launch_tcp_plan(dev_tmpl, dev_desc, dev_msg_total, n, bytes, nfrag, s)) != hipSuccess)
+  if ((e = hipMemsetAsync(max_frag, 0, 4, s)) != hipSuccess) return set_err(ctx, e, "tcp plan");
+  if ((e = mgenx::launch_tcp_plan(dev_tmpl, dev_desc, dev_msg_total, n, bytes, nfrag, max_frag,
+                                  s)) != hipSuccess)
     return set_err(ctx, e, "tcp plan");
   uint64_t* offs = foff;  // reused below only after the copy out
   if ((e = hipcub::DeviceScan::ExclusiveSum(cub, cub_bytes, (const uint64_t*)bytes, offs,
@@ -571,7 +565,7 @@ int mgenx_pack_tcp(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl, const uint32
     return set_err(ctx, e, "tcp scan");
   if ((e = hipMemcpyAsync(dev_msg_off, offs, (size_t)n * 8, hipMemcpyDeviceToDevice, s)) != hipSuccess)
     return set_err(ctx, e, "tcp");
-  hipLaunchKernelGGL(tcp_totals_kernel, dim3(1), dim3(256), 0, s, nfrag, n, offs, ctx->tcp_host_dev);
+  hipLaunchKernelGGL(tcp_totals_kernel, dim3(1), dim3(1), 0, s, max_frag, n, offs, ctx->tcp_host_dev);
   if ((e = hipStreamSynchronize(s)) != hipSuccess) return set_err(ctx, e, "tcp plan");
   const uint64_t total = ((volatile uint64_t*)ctx->tcp_host)[0];
   const uint32_t rounds = (uint32_t)((volatile uint64_t*)ctx->tcp_host)[1];

@@ -86,7 +86,7 @@ size_t rx_persist_ws_bytes(uint32_t n);
 // TCP transmit (mgenx_tcp.hip)
 hipError_t launch_tcp_plan(const mgenx_flow_tmpl* tmpl, const mgenx_pack_desc* desc,
                            const uint32_t* msg_total, uint32_t n, uint64_t* bytes,
-                           uint32_t* nfrag, hipStream_t s);
+                           uint32_t* nfrag, uint32_t* max_frag, hipStream_t s);
 hipError_t launch_tcp_frag(const mgenx_pack_desc* desc, const uint32_t* msg_total,
                            const uint32_t* nfrag, const uint64_t* msg_off, uint32_t n, uint32_t r,
                            int ck, const uint32_t* prev_state, mgenx_pack_desc* fd, uint64_t* foff,

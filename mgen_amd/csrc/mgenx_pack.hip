@@ -136,13 +136,16 @@ pack_kernel(PackParams p) {
     const bool prod_live = gp < n_groups;
     const bool cons_live = s > 0 && gp - gridDim.x < n_groups;
     if (!prod_live && !cons_live) break;
-    const int buf = (int)((producer ? s : s - 1) & 1);
-    const uint64_t b = (producer ? gp : gp - gridDim.x) * kProd + slot;
+    // a meta wave with no group to build this stage helps its store wave (big TCP path)
+    const bool helper = producer && !prod_live;
+    const bool builds = producer && !helper;
+    const int buf = (int)((builds ? s : s - 1) & 1);
+    const uint64_t b = (builds ? gp : gp - gridDim.x) * kProd + slot;
     uint8_t* const S_IMG = &s_img[buf][slot][0];
     PackMeta* const S_META = s_meta[buf][slot];
     const uint64_t i = (b << 6) + lane;
-    if (!(producer ? prod_live : cons_live) || b >= n_batches) goto stage_end;
-    if (producer) {
+    if (!(builds ? prod_live : cons_live) || b >= n_batches) goto stage_end;
+    if (builds) {
     uint8_t* img = S_IMG + lane * kImg;
     PackMeta m;
     m.off = 0; m.ret = 0; m.trailer = 0; m.pend = 0; m.poff = 0; m.hdr = 0;
@@ -332,7 +335,7 @@ pack_kernel(PackParams p) {
     {
     // consumer
     const PackMeta m = S_META[lane];
-    if (i < p.n) {
+    if (i < p.n && !helper) {
       p.out_len[i] = m.ret;
       if (p.tx_crc) p.tx_crc[i] = m.tx_out;
       if (p.state) p.state[i] = m.state;
@@ -383,6 +386,57 @@ pack_kernel(PackParams p) {
       }
       goto stage_end;
     }
+    // Big TCP buffers (PackParams.frag_len set, every record >= 1 KiB, zero fill, image
+    // holding header + payload): record by record, the wave's 64 lanes over its 16-byte
+    // units -- a unit is its image bytes or zeros, stored in P and in each later buffer of
+    // the fragment.  (The general walk below spends most of its instructions per unit on
+    // finding the unit's record and on the fill / payload / trailer cases.)
+    if (p.frag_len && !rf && nv > 0 &&
+        __all(!has || (m.pend <= (uint32_t)kImg && (m.ret == 0u || m.ret >= 1024u)))) {
+      const bool fck = p.frag_ck != 0;
+      // with a helper (no group built this stage) the two waves take alternate records
+      const uint32_t rstep = prod_live ? 1u : 2u;
+      for (uint32_t rr = helper ? 1u : 0u; rr < nv; rr += rstep) {
+        const PackMeta R = S_META[rr];
+        if (R.ret == 0u) continue;
+        const TcpReps reps = tcp_reps(R.frag, R.ret, fck);
+        const uint8_t* rimg = &S_IMG[rr * kImg];
+        const uint32_t nu = (R.ret + 15u) >> 4;
+        uint8_t* const rbase = p.slab + R.off;
+        for (uint32_t u = (uint32_t)lane; u < nu; u += 64u) {
+          const uint32_t pos = u << 4;
+          uint32_t v[4] = {0u, 0u, 0u, 0u};
+          if (pos < R.pend) {
+            const u32x4_t iv = *reinterpret_cast<const u32x4_t*>(rimg + pos);
+            const uint32_t w[4] = {iv.x, iv.y, iv.z, iv.w};
+#pragma unroll
+            for (int kk = 0; kk < 4; kk++) {
+              const int lim = (int)R.pend - (int)pos - 4 * kk;
+              v[kk] = w[kk] & byte_range_mask(0, lim < 0 ? 0 : (lim > 4 ? 4 : lim));
+            }
+          }
+          const u32x4_t val = {v[0], v[1], v[2], v[3]};
+          if (pos + 16u <= R.ret) {
+            stu128(rbase + pos, val);
+          } else {
+            for (uint32_t j = 0; j < R.ret - pos; j++) rbase[pos + j] = (uint8_t)(v[j >> 2] >> ((j & 3) * 8));
+          }
+#pragma unroll
+          for (int k = 0; k < kMaxRep; k++) {
+            if (pos < reps.cnt[k]) {
+              uint8_t* d2 = rbase + reps.start[k] + pos;
+              if (pos + 16u <= reps.cnt[k]) {
+                stu128(d2, val);
+              } else {
+                for (uint32_t j = 0; j < reps.cnt[k] - pos; j++) d2[j] = (uint8_t)(v[j >> 2] >> ((j & 3) * 8));
+              }
+            }
+          }
+        }
+      }
+      goto stage_end;
+    }
+    if (helper) goto stage_end;  // the other store forms stay single-wave
     const uint64_t next_off = __shfl_down(m.off, 1);
     const bool packed_ok = !has || (m.ret >= 16u && m.pend <= (uint32_t)kImg && m.frag == 0u &&
                                     ((uint32_t)lane + 1 == nv || m.off + m.ret == next_off));

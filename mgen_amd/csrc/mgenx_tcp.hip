@@ -56,32 +56,40 @@ __device__ __forceinline__ bool tcp_fragment(uint32_t M, uint32_t r, uint32_t& F
 __global__ void tcp_plan_kernel(const mgenx_flow_tmpl* __restrict__ tmpl,
                                 const mgenx_pack_desc* __restrict__ desc,
                                 const uint32_t* __restrict__ msg_total, uint32_t n,
-                                uint64_t* __restrict__ bytes, uint32_t* __restrict__ nfrag) {
+                                uint64_t* __restrict__ bytes, uint32_t* __restrict__ nfrag,
+                                uint32_t* __restrict__ max_frag) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i > n) return;
-  if (i == n) {  // exclusive-scan tail
-    bytes[n] = 0;
-    return;
+  uint32_t c = 0;  // fragments (no early return: the block maximum below has a barrier)
+  if (i == n) bytes[n] = 0;  // exclusive-scan tail
+  if (i < n) {
+    const uint32_t M = msg_total[i];
+    const mgenx_flow_tmpl& t = tmpl[desc[i].tmpl];
+    const bool dst_ok = t.dst_type == 1u || t.dst_type == 2u;
+    const uint32_t D = t.dst_len > 16u ? 16u : t.dst_len;
+    uint32_t F0 = 0, at;
+    bool more, ok = false;
+    if (M && tcp_fragment(M, 0, F0, at, more)) {
+      const uint32_t B0 = F0 > kTxBuf ? kTxBuf - 4u : F0;  // smallest bufferLen it can get
+      ok = dst_ok && B0 >= 24u + D;
+    }
+    if (ok) {
+      uint32_t F, a;
+      while (tcp_fragment(M, c, F, a, more)) c++;
+    }
+    bytes[i] = c ? (uint64_t)M : 0ull;
+    nfrag[i] = c;
   }
-  const uint32_t M = msg_total[i];
-  const mgenx_flow_tmpl& t = tmpl[desc[i].tmpl];
-  const bool dst_ok = t.dst_type == 1u || t.dst_type == 2u;
-  const uint32_t D = t.dst_len > 16u ? 16u : t.dst_len;
-  uint32_t F0 = 0, at, cnt = 0;
-  bool more;
-  if (M && tcp_fragment(M, 0, F0, at, more)) {
-    const uint32_t B0 = F0 > kTxBuf ? kTxBuf - 4u : F0;  // smallest bufferLen it can get
-    const bool ok = dst_ok && B0 >= 24u + D;
-    if (ok) cnt = (M + (kMaxFrag - kMinFrag) - 1) / (kMaxFrag - kMinFrag) + 1;  // bound
+  // the round count: a block maximum, one atomic per block (max_frag zeroed by the caller)
+  __shared__ uint32_t wmax[4];
+  uint32_t mx = c;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+  if ((threadIdx.x & 63u) == 0u) wmax[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0u) {
+    mx = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
+    if (mx) atomicMax(max_frag, mx);
   }
-  // exact count
-  uint32_t c = 0;
-  if (cnt) {
-    uint32_t F, a;
-    while (tcp_fragment(M, c, F, a, more)) c++;
-  }
-  bytes[i] = c ? (uint64_t)M : 0ull;
-  nfrag[i] = c;
 }
 
 // round r: the pack descriptor of fragment r of each message (msg_len 0 = none this round)
@@ -237,9 +245,9 @@ __global__ void tcp_finish_kernel(uint8_t* __restrict__ out, const uint64_t* __r
 
 hipError_t launch_tcp_plan(const mgenx_flow_tmpl* tmpl, const mgenx_pack_desc* desc,
                            const uint32_t* msg_total, uint32_t n, uint64_t* bytes,
-                           uint32_t* nfrag, hipStream_t s) {
+                           uint32_t* nfrag, uint32_t* max_frag, hipStream_t s) {
   hipLaunchKernelGGL(tcp_plan_kernel, dim3((n + 256) / 256), dim3(256), 0, s, tmpl, desc, msg_total,
-                     n, bytes, nfrag);
+                     n, bytes, nfrag, max_frag);
   return hipGetLastError();
 }
 
