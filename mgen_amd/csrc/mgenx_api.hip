@@ -586,7 +586,8 @@ int mgenx_pack_tcp(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl, const uint32
     if (rc != MGENX_OK) return rc;
     if ((e = mgenx::launch_tcp_tail(dev_stream, foff, fbuf, ff, plen, crc, st[r & 1], n, ck,
                                     (opts & MGENX_PACK_RANDOM_FILL) ? 1 : 0, acrc,
-                                    ctx->d_bytetab, ctx->d_xpow, ctx->d_ia, ctx->d_rcrc, s)) !=
+                                    ctx->d_bytetab, ctx->d_tabs + 1024, ctx->d_xpow, ctx->d_ia,
+                                    ctx->d_rcrc, s)) !=
         hipSuccess)
       return set_err(ctx, e, "tcp tail");
   }

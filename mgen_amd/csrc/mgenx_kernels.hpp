@@ -94,8 +94,8 @@ hipError_t launch_tcp_frag(const mgenx_pack_desc* desc, const uint32_t* msg_tota
 hipError_t launch_tcp_tail(uint8_t* out, const uint64_t* foff, const uint32_t* fbuf,
                            const uint32_t* ff, const uint32_t* plen, const uint32_t* tx_crc,
                            const uint32_t* state, uint32_t n, int ck, int rnd, uint32_t* acrc,
-                           const uint32_t* byte_tab, const uint32_t* xpow, const uint32_t* ia,
-                           const uint32_t* rcrc, hipStream_t s);
+                           const uint32_t* byte_tab, const uint32_t* a4_tab, const uint32_t* xpow,
+                           const uint32_t* ia, const uint32_t* rcrc, hipStream_t s);
 hipError_t launch_crc32(const uint8_t* data, const uint64_t* off, const uint32_t* len, uint32_t n,
                         const uint32_t* byte_tab, const uint32_t* a4_tab, const uint32_t* xpow,
                         const uint32_t* state_in, uint32_t* out, hipStream_t stream);

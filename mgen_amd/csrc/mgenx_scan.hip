@@ -14,7 +14,9 @@
 //      searched in the target block's own slot list, or a terminal;
 //   3. base-4 lifting (pointer jumping, ceil(log4 n) levels) gives the chain from any
 //      candidate; the chain from offset 0 is enumerated in parallel and reports where it
-//      ends -- with the candidate total, the only device-to-host copies of the common path;
+//      ends -- with the candidate total, the only device-to-host copies of the common path.
+//      A whole-stream scan first checks the regular case (link: every candidate's successor
+//      is the next candidate): the records are then the candidates, and no lifting runs;
 //   4. where the chain leaves the candidate set (a record with a bad version, SINK garbage,
 //      a partial tail before the end, TCP msg_len < 4, or a block with more plausible starts
 //      than slots) a single-thread resolver walks the reference rule exactly until it
@@ -206,6 +208,20 @@ scan_detect_kernel(const uint8_t* __restrict__ s, uint64_t nbytes, ScanMode m,
   }
 }
 
+// the lifting tables of one build: ups / dists [levels + 1][stride], the 2- and 3-jump tables
+// [levels][stride]
+struct LiftTabs {
+  const uint32_t *ups, *dists, *ups2, *ups3, *dists2, *dists3;
+  uint32_t stride;
+  int levels;
+};
+
+// where an enumerated chain stops: its record count and the position after its last record
+struct ChainEnd {
+  uint64_t count, next_pos;
+  uint64_t more;  // the last node has a successor candidate (the descent hit its depth)
+};
+
 // 2. compact + link, one wave per block: candidate positions into the global sorted
 // array, and each candidate's successor p + L searched in the target block's own slots
 // (sorted, usually a handful) -- or, for a block that overflowed its slots, in its range of
@@ -215,9 +231,13 @@ __global__ void __launch_bounds__(256)
 scan_link_kernel(const uint8_t* __restrict__ s, uint64_t nbytes, const uint32_t* __restrict__ slots,
                  const uint64_t* __restrict__ counts, const uint64_t* __restrict__ base,
                  uint32_t n_blocks, uint64_t* __restrict__ cand, uint32_t* __restrict__ up,
-                 uint32_t* __restrict__ dist, uint64_t spec_cap) {
+                 uint32_t* __restrict__ dist, uint64_t spec_cap, uint32_t* __restrict__ irregular) {
   const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= n_blocks) return;
+  // irregular (optional): set unless every candidate's successor is the next candidate and
+  // the last one is terminal -- then the chain from candidate 0 is the whole candidate list
+  const uint64_t n_tot = base[n_blocks];
+  bool odd = false;
   // speculative build (tables sized before the candidate total was known): nothing when the
   // total exceeds them; an overflowing block (its candidates need the second detect pass)
   // gets terminal entries -- the host sees either case and rebuilds exactly
@@ -230,6 +250,7 @@ scan_link_kernel(const uint8_t* __restrict__ s, uint64_t nbytes, const uint32_t*
       up[o + k] = o + k;
       dist[o + k] = 0u;
     }
+    if (irregular && c && (threadIdx.x & 63u) == 0u) *irregular = 1u;
     return;
   }
   for (uint32_t k = threadIdx.x & 63u; k < c; k += 64) {
@@ -278,7 +299,43 @@ scan_link_kernel(const uint8_t* __restrict__ s, uint64_t nbytes, const uint32_t*
     }
     up[o + k] = tgt == kNone ? o + k : tgt;
     dist[o + k] = tgt == kNone ? 0u : 1u;
+    const uint64_t ci = (uint64_t)o + k;
+    odd = odd || (ci + 1 < n_tot ? tgt != o + k + 1 : tgt != kNone);
   }
+  // a plain store of the same value by every irregular wave: no read-modify-write to
+  // serialise on one word (an atomic per wave cost 180 us on a 1-GiB stream)
+  if (irregular && __ballot(odd) && (threadIdx.x & 63u) == 0u) *irregular = 1u;
+}
+
+// The regular case of the chain from offset 0 (no lifting): when the link step found every
+// candidate's successor to be the next candidate (and candidate 0 at offset 0), the records
+// are the candidates themselves.  Otherwise thread 0 reports `more` = 2: the caller lifts.
+__global__ void __launch_bounds__(256)
+scan_enum_regular_kernel(const uint8_t* __restrict__ s, const uint64_t* __restrict__ cand,
+                         const uint64_t* __restrict__ total, const uint32_t* __restrict__ irregular,
+                         uint32_t stride, uint64_t cap, uint64_t* __restrict__ rec_off,
+                         uint32_t* __restrict__ rec_len, ChainEnd* __restrict__ end,
+                         uint32_t* __restrict__ done) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t n = *total;
+  const bool ok = *irregular == 0u && n != 0 && n <= stride && cand[0] == 0;
+  if (i == 0) {
+    *done = ok ? 1u : 0u;  // read by the lifting and enumeration launches that follow
+    if (ok) {
+      const uint64_t tp = cand[n - 1];
+      end->count = n;
+      end->next_pos = tp + be16_at(s, tp);
+      end->more = 0;
+    } else {
+      end->count = 0;
+      end->next_pos = 0;
+      end->more = 2;
+    }
+  }
+  if (!ok || i >= n || i >= cap) return;
+  const uint64_t p = cand[i];
+  rec_off[i] = p;
+  rec_len[i] = be16_at(s, p);
 }
 
 // the candidate total / overflow word (exclusive scan's last entry) to host-mapped memory
@@ -367,9 +424,10 @@ scan_lift_kernel(const uint32_t* __restrict__ up0, const uint32_t* __restrict__ 
                  uint32_t* __restrict__ up1, uint32_t* __restrict__ d1,
                  uint32_t* __restrict__ up2, uint32_t* __restrict__ up3,
                  uint32_t* __restrict__ d2, uint32_t* __restrict__ d3, uint32_t n,
-                 const uint64_t* __restrict__ spec_total) {
+                 const uint64_t* __restrict__ spec_total, const uint32_t* __restrict__ regular) {
   const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= n) return;
+  if (regular && *regular) return;  // the regular chain needs no lifting
   // speculative build: n is the capacity and the candidate count is on the device; its
   // load goes out beside the first gather (up0 has `n` readable entries either way)
   const uint64_t t = spec_total ? *spec_total : 0ull;
@@ -389,20 +447,6 @@ scan_lift_kernel(const uint32_t* __restrict__ up0, const uint32_t* __restrict__ 
   d2[c] = dc + e1;
   d3[c] = dc + e1 + e2;
 }
-
-// the lifting tables of one build: ups / dists [levels + 1][stride], the 2- and 3-jump tables
-// [levels][stride]
-struct LiftTabs {
-  const uint32_t *ups, *dists, *ups2, *ups3, *dists2, *dists3;
-  uint32_t stride;
-  int levels;
-};
-
-// where an enumerated chain stops: its record count and the position after its last record
-struct ChainEnd {
-  uint64_t count, next_pos;
-  uint64_t more;  // the last node has a successor candidate (the descent hit its depth)
-};
 
 // the last chain node from candidate c whose position is < limit (pos(c) < limit), and the
 // number of records from c to it: greedy descent over the lifting levels -- at each level the
@@ -436,8 +480,10 @@ scan_enum_kernel(const uint8_t* __restrict__ s, const uint64_t* __restrict__ can
                  LiftTabs t, const uint64_t* __restrict__ spec_total,
                  uint32_t start, int at_zero, uint64_t limit, uint64_t out_base,
                  uint64_t cap, uint64_t* __restrict__ rec_off, uint32_t* __restrict__ rec_len,
-                 ChainEnd* __restrict__ end) {
+                 ChainEnd* __restrict__ end, const uint32_t* __restrict__ regular) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // after scan_enum_regular_kernel: nothing to do when it found the regular chain
+  if (regular && *regular) return;
   // speculative build: tables of `stride` entries, valid only when the total fits them
   const bool built = !spec_total || (*spec_total != 0 && *spec_total <= t.stride);
   const bool ok = built && !(at_zero && cand[start] != 0);
@@ -653,14 +699,15 @@ LiftTabs lift_tabs(const mgenx_scan_ws& ws) {
   return t;
 }
 
-void launch_lifts(const mgenx_scan_ws& ws, const uint64_t* spec_total, hipStream_t stream) {
+void launch_lifts(const mgenx_scan_ws& ws, const uint64_t* spec_total, hipStream_t stream,
+                  const uint32_t* regular = nullptr) {
   const uint32_t st = ws.stride;
   const dim3 g((st + 255) / 256);
   for (int k = 1; k <= ws.levels; k++) {
     const size_t a = (size_t)(k - 1) * st, b = (size_t)k * st;
     hipLaunchKernelGGL(scan_lift_kernel, g, dim3(256), 0, stream, ws.ups + a, ws.dists + a,
                        ws.ups + b, ws.dists + b, ws.ups2 + a, ws.ups3 + a, ws.dists2 + a,
-                       ws.dists3 + a, st, spec_total);
+                       ws.dists3 + a, st, spec_total, regular);
   }
 }
 
@@ -734,9 +781,13 @@ int scan_build(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, int mode, h
     lay_tables(ws, cap, levels);
     ws.spec_total = d_base + nb;
     ws.spec_pending = true;
+    uint32_t* irregular = reinterpret_cast<uint32_t*>(static_cast<char*>(ws.small.mem) + 2048);
+    if ((e = hipMemsetAsync(irregular, 0, 4, stream)) != hipSuccess) return fail(e, "scan");
     hipLaunchKernelGGL(scan_link_kernel, dim3((nb + 3) / 4), dim3(256), 0, stream, s, nbytes,
-                       d_slots, d_counts, d_base, nb, ws.cand, ws.ups, ws.dists, (uint64_t)cap);
-    launch_lifts(ws, ws.spec_total, stream);
+                       d_slots, d_counts, d_base, nb, ws.cand, ws.ups, ws.dists, (uint64_t)cap,
+                       irregular);
+    // (the lifting levels follow only when the chain is not the candidate list itself:
+    // mgenx_scan_run, after its one sync)
     if ((e = hipGetLastError()) != hipSuccess) return fail(e, "scan launch");
     return MGENX_OK;
   }
@@ -765,7 +816,8 @@ int scan_build(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, int mode, h
     hipLaunchKernelGGL(scan_detect_kernel<true>, dim3(nb), dim3(kScanThreads), 0, stream, s,
                        nbytes, m, d_slots, d_counts, (const uint64_t*)d_base, ws.cand);
   hipLaunchKernelGGL(scan_link_kernel, dim3((nb + 3) / 4), dim3(256), 0, stream, s, nbytes,
-                     d_slots, d_counts, d_base, nb, ws.cand, ws.ups, ws.dists, (uint64_t)0);
+                     d_slots, d_counts, d_base, nb, ws.cand, ws.ups, ws.dists, (uint64_t)0,
+                     (uint32_t*)nullptr);
   launch_lifts(ws, nullptr, stream);
   if ((e = hipGetLastError()) != hipSuccess) return fail(e, "scan launch");
   return MGENX_OK;
@@ -802,7 +854,7 @@ int scan_walk(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, int mode, ui
     // candidate 0 is offset 0 when offset 0 is a candidate: enumerate speculatively
     hipLaunchKernelGGL(scan_enum_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, s, ws.cand,
                        tabs, (const uint64_t*)nullptr, 0u, 1, limit, (uint64_t)0, cap, rec_off,
-                       rec_len, d_end);
+                       rec_len, d_end, (const uint32_t*)nullptr);
     if ((e = hipStreamSynchronize(stream)) != hipSuccess) return fail(e, "scan");
     const ChainEnd h = {h_end[0], h_end[1], h_end[2]};
     if (h.count) {
@@ -817,7 +869,7 @@ int scan_walk(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, int mode, ui
       // enumerate the candidate chain from `at` (grid sized by n >= its length)
       hipLaunchKernelGGL(scan_enum_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, s,
                          ws.cand, tabs, (const uint64_t*)nullptr, at, 0, limit, total, cap,
-                         rec_off, rec_len, d_end);
+                         rec_off, rec_len, d_end, (const uint32_t*)nullptr);
       if ((e = hipStreamSynchronize(stream)) != hipSuccess) return fail(e, "scan");
       const ChainEnd h = {h_end[0], h_end[1], h_end[2]};
       total += h.count;
@@ -873,9 +925,19 @@ extern "C" int mgenx_scan_run(void* wsp, const uint8_t* s, uint64_t nbytes, int 
     const uint32_t scap = ws.stride;
     ChainEnd* d_end = reinterpret_cast<ChainEnd*>(ws.host_dev + 2);
     const volatile uint64_t* h_end = ws.host + 2;
+    const uint32_t* irregular =
+        reinterpret_cast<const uint32_t*>(static_cast<char*>(ws.small.mem) + 2048);
+    uint32_t* regular = reinterpret_cast<uint32_t*>(static_cast<char*>(ws.small.mem) + 2052);
+    hipLaunchKernelGGL(scan_enum_regular_kernel, dim3((scap + 255) / 256), dim3(256), 0, stream,
+                       s, ws.cand, ws.spec_total, irregular, scap, cap, rec_off, rec_len, d_end,
+                       regular);
+    // not the regular chain: the lifting levels on the speculative tables, then the
+    // enumeration from offset 0 -- launched regardless, each returning at once when the
+    // regular kernel already reported the chain (no host round trip to decide)
+    launch_lifts(ws, ws.spec_total, stream, regular);
     hipLaunchKernelGGL(scan_enum_kernel, dim3((scap + 255) / 256), dim3(256), 0, stream, s,
                        ws.cand, lift_tabs(ws), ws.spec_total, 0u, 1, nbytes, (uint64_t)0, cap,
-                       rec_off, rec_len, d_end);
+                       rec_off, rec_len, d_end, (const uint32_t*)regular);
     hipError_t e;
     if ((e = hipStreamSynchronize(stream)) != hipSuccess) return fail(e, "scan");
     uint32_t tot[2];

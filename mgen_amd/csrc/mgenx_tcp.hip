@@ -15,11 +15,11 @@
 //                     start, its running CRC and the MgenMsg flags it leaves -- and, as each
 //                     16-byte unit of P is stored, its copies P[0 .. s_k) in every later
 //                     buffer k of the fragment (PackParams.frag_len: no copy pass);
-//   tcp_prefix_kernel A(s) = ComputeCRC32 from a restart over P[0 .. s) for the (at most
-//                     three) distinct buffer lengths of the fragment, from P's header and
-//                     payload bytes and the fill algebra (no re-read of the buffer);
+//   tcp_prefix_kernel raw(s) = the CRC register over P[0 .. s) from zero for the (at most
+//                     three) distinct buffer lengths of the fragment, from one pass over P's
+//                     header and payload bytes and the fill algebra (no re-read of the buffer);
 //   tcp_finish_kernel the running CRC chained through the buffers algebraically,
-//                     c' = raw(P[0..s)) ^ x^(8s) * c  (c = 0 restarts, as ComputeCRC32 does),
+//                     c' = raw(s) ^ x^(8s) * c  (c = 0 restarts from ~0, as ComputeCRC32 does),
 //                     and the big-endian trailer.
 #include <hip/hip_runtime.h>
 
@@ -154,20 +154,27 @@ __device__ __forceinline__ bool tcp_buffer(uint32_t F, uint32_t B, int ck, uint3
   }
 }
 
-// A(s) = crc32(P[0 .. s)) for the (at most three) distinct CRC lengths of a fragment's later
-// buffers (full 8192, one SetupNextTxBuffer-shortened buffer, the last one's size - 4),
-// without re-reading the 8-KiB buffer: P is Pack's image -- header (packet_header_len h
-// bytes), the payload it copied (p bytes, read back from the payload_len field that ends a
-// complete header), then fill -- so the prefix CRC walks at most h + p bytes and extends
-// over the fill algebraically: zeros are the shift x^(8q); RANDOM_FILL's fill is two zero
-// bytes and the rand stream, raw CRC rcrc[q - 2] (mgenMsg.cpp:274-293).
-__global__ void tcp_prefix_kernel(const uint8_t* __restrict__ out, const uint64_t* __restrict__ foff,
-                                  const uint32_t* __restrict__ fbuf, const uint32_t* __restrict__ ff,
-                                  const uint32_t* __restrict__ plen,
-                                  const uint32_t* __restrict__ state, uint32_t n, int ck, int rnd,
-                                  const uint32_t* __restrict__ byte_tab,
-                                  const uint32_t* __restrict__ xpow,
-                                  const uint32_t* __restrict__ rcrc, uint32_t* __restrict__ acrc) {
+// raw(s) = the CRC register after P[0 .. s) from a zero start (no init, no final xor), for
+// the (at most three) distinct CRC lengths of a fragment's later buffers (full 8192, one
+// SetupNextTxBuffer-shortened buffer, the last one's size - 4), without re-reading the
+// 8-KiB buffer: P is Pack's image -- header (packet_header_len h bytes), the payload it
+// copied (p bytes, read back from the payload_len field that ends a complete header), then
+// fill -- so one pass over the h + p body bytes (four at a time, slicing tables in LDS)
+// serves every length, extended over the fill algebraically: zeros are the shift x^(8q);
+// RANDOM_FILL's fill is two zero bytes and the rand stream, raw CRC rcrc[q - 2]
+// (mgenMsg.cpp:274-293).  A length inside the body (a short fragment) walks its bytes.
+__global__ void __launch_bounds__(256)
+tcp_prefix_kernel(const uint8_t* __restrict__ out, const uint64_t* __restrict__ foff,
+                  const uint32_t* __restrict__ fbuf, const uint32_t* __restrict__ ff,
+                  const uint32_t* __restrict__ plen, const uint32_t* __restrict__ state,
+                  uint32_t n, int ck, int rnd, const uint32_t* __restrict__ byte_tab,
+                  const uint32_t* __restrict__ a4_tab, const uint32_t* __restrict__ xpow,
+                  const uint32_t* __restrict__ rcrc, uint32_t* __restrict__ acrc) {
+  __shared__ uint32_t s_a4[1024];
+  __shared__ uint32_t s_tab[256];
+  for (uint32_t k = threadIdx.x; k < 1024u; k += blockDim.x) s_a4[k] = a4_tab[k];
+  for (uint32_t k = threadIdx.x; k < 256u; k += blockDim.x) s_tab[k] = byte_tab[k];
+  __syncthreads();
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t F = ff[i], B = fbuf[i];
@@ -188,19 +195,31 @@ __global__ void tcp_prefix_kernel(const uint8_t* __restrict__ out, const uint64_
     if (h == 24u + D + 4u + H + 16u) p = (uint32_t)P[h - 2u] << 8 | P[h - 1u];
   }
   const uint32_t body = h + p;
+  auto walk = [&](uint32_t len) {  // raw CRC of P[0 .. len)
+    uint32_t c = 0;
+    const uint32_t nw = len >> 2;
+    for (uint32_t k = 0; k < nw; k++) {
+      const uint32_t x = c ^ ldu32(P + 4u * k);
+      c = s_a4[x & 0xffu] ^ s_a4[256 + ((x >> 8) & 0xffu)] ^ s_a4[512 + ((x >> 16) & 0xffu)] ^
+          s_a4[768 + (x >> 24)];
+    }
+    for (uint32_t k = nw << 2; k < len; k++) c = s_tab[(c ^ P[k]) & 0xffu] ^ (c >> 8);
+    return c;
+  };
+  const uint32_t cb = walk(body);
 #pragma unroll
   for (int j = 0; j < 3; j++) {
     const uint32_t len = L[j];
     if (!len) continue;
-    uint32_t c = 0xFFFFFFFFu;
-    const uint32_t m = len < body ? len : body;
-    for (uint32_t k = 0; k < m; k++) c = byte_tab[(c ^ P[k]) & 0xffu] ^ (c >> 8);
-    if (len > body) {
+    uint32_t c;
+    if (len >= body) {
       const uint32_t q = len - body;
-      c = multmodp(xpow[q], c);
+      c = multmodp(xpow[q], cb);
       if (rnd && q >= 3u) c ^= rcrc[q - 2u];
+    } else {
+      c = walk(len);
     }
-    acrc[3 * i + j] = c ^ 0xFFFFFFFFu;
+    acrc[3 * i + j] = c;
   }
 }
 
@@ -225,11 +244,10 @@ __global__ void tcp_finish_kernel(uint8_t* __restrict__ out, const uint64_t* __r
     bool last;
     for (uint32_t k = 1; tcp_buffer(F, B, ck, k, start, size, last); k++) {
       const uint32_t s = last ? size - 4u : size;
-      // (the crc32 ranges were run without a state: final xor applied)
-      const uint32_t a = acrc[3 * i + (last ? 2 : (size == kTxBuf ? 0 : 1))] ^ 0xFFFFFFFFu;
-      // ComputeCRC32(c, P, s): a zero running value restarts; raw(P[0..s)) = A(s) ^ ia[s]
+      const uint32_t a = acrc[3 * i + (last ? 2 : (size == kTxBuf ? 0 : 1))];  // raw(P[0..s))
+      // ComputeCRC32(c, P, s): a zero running value restarts (from ~0)
       const uint32_t cr = c == 0u ? 0xFFFFFFFFu : c;
-      if (s) c = a ^ ia[s] ^ multmodp(xpow[s], cr);
+      if (s) c = a ^ multmodp(xpow[s], cr);
       else c = cr;
     }
   }
@@ -263,11 +281,11 @@ hipError_t launch_tcp_frag(const mgenx_pack_desc* desc, const uint32_t* msg_tota
 hipError_t launch_tcp_tail(uint8_t* out, const uint64_t* foff, const uint32_t* fbuf,
                            const uint32_t* ff, const uint32_t* plen, const uint32_t* tx_crc,
                            const uint32_t* state, uint32_t n, int ck, int rnd, uint32_t* acrc,
-                           const uint32_t* byte_tab, const uint32_t* xpow, const uint32_t* ia,
-                           const uint32_t* rcrc, hipStream_t s) {
+                           const uint32_t* byte_tab, const uint32_t* a4_tab, const uint32_t* xpow,
+                           const uint32_t* ia, const uint32_t* rcrc, hipStream_t s) {
   if (ck) {
     hipLaunchKernelGGL(tcp_prefix_kernel, dim3((n + 255) / 256), dim3(256), 0, s, out, foff, fbuf,
-                       ff, plen, state, n, ck, rnd, byte_tab, xpow, rcrc, acrc);
+                       ff, plen, state, n, ck, rnd, byte_tab, a4_tab, xpow, rcrc, acrc);
     hipLaunchKernelGGL(tcp_finish_kernel, dim3((n + 255) / 256), dim3(256), 0, s, out, foff, fbuf,
                        ff, plen, tx_crc, state, acrc, xpow, ia, n, ck);
   }
