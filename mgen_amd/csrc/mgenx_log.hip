@@ -1154,7 +1154,9 @@ __global__ void __launch_bounds__(256) binlog_parse_kernel(BinParams p) {
     const uint32_t idx = proto == 2 ? 4u : 0u;
     if (proto == 2) aux = be32(b);
     mo = ro + 4 + idx;
-    ml = rl - idx;  // the stored bytes (the reference passes recordLength: the same header)
+    // the stored bytes: the reference passes recordLength (:1624), whose last 4 bytes after
+    // a TCP SEND's length word are stale read-buffer bytes (:1434); bounded at the record
+    ml = rl - idx;
   }
   p.msg_off[i] = mo;
   p.msg_len[i] = ml;

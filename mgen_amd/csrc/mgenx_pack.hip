@@ -95,6 +95,10 @@ __device__ __forceinline__ void img_put32(uint8_t* img, uint32_t at, uint32_t v)
   img_put8(img, at + 3, v);
 }
 
+// kTcp: the TCP transmit form (PackParams.frag_len: later buffers of a fragment stored from
+// the same units, helper meta waves).  A separate instantiation, so the UDP / SINK paths carry
+// none of its registers (with them in, config 2 pack ran 0.355 ms instead of 0.216).
+template <bool kTcp>
 __global__ void __launch_bounds__(kPackThreads)
 pack_kernel(PackParams p) {
   // Producer / consumer waves: waves 0..kProd-1 run phase 1 (meta: loads and CRC algebra)
@@ -137,7 +141,7 @@ pack_kernel(PackParams p) {
     const bool cons_live = s > 0 && gp - gridDim.x < n_groups;
     if (!prod_live && !cons_live) break;
     // a meta wave with no group to build this stage helps its store wave (big TCP path)
-    const bool helper = producer && !prod_live;
+    const bool helper = kTcp && producer && !prod_live;
     const bool builds = producer && !helper;
     const int buf = (int)((builds ? s : s - 1) & 1);
     const uint64_t b = (builds ? gp : gp - gridDim.x) * kProd + slot;
@@ -320,7 +324,7 @@ pack_kernel(PackParams p) {
         }
       }
       if (m.off > p.slab_bytes || m.ret > p.slab_bytes - m.off) m.ret = 0;  // never write OOB
-      if (p.frag_len && m.ret) {
+      if (kTcp && p.frag_len && m.ret) {
         const uint32_t F = p.frag_len[i];
         if (F > m.ret && F <= p.slab_bytes - m.off) m.frag = F;
       }
@@ -391,7 +395,7 @@ pack_kernel(PackParams p) {
     // units -- a unit is its image bytes or zeros, stored in P and in each later buffer of
     // the fragment.  (The general walk below spends most of its instructions per unit on
     // finding the unit's record and on the fill / payload / trailer cases.)
-    if (p.frag_len && !rf && nv > 0 &&
+    if (kTcp && p.frag_len && !rf && nv > 0 &&
         __all(!has || (m.pend <= (uint32_t)kImg && (m.ret == 0u || m.ret >= 1024u)))) {
       const bool fck = p.frag_ck != 0;
       // with a helper (no group built this stage) the two waves take alternate records
@@ -563,7 +567,8 @@ pack_kernel(PackParams p) {
     int ri = 0;
     uint32_t rstart = 0, next_start = s_pre[slot][1];
     PackMeta r = S_META[0];
-    TcpReps reps = tcp_reps(r.frag, r.ret, p.frag_ck != 0);
+    TcpReps reps;
+    if constexpr (kTcp) reps = tcp_reps(r.frag, r.ret, p.frag_ck != 0);
     for (uint32_t u = lane; u < ((variant == 1 || variant == 4) ? 0u : total); u += 64) {
       if (next_start <= u) {
         do {
@@ -572,7 +577,7 @@ pack_kernel(PackParams p) {
           next_start = s_pre[slot][ri + 1];
         } while (next_start <= u);
         r = S_META[ri];
-        reps = tcp_reps(r.frag, r.ret, p.frag_ck != 0);
+        if constexpr (kTcp) reps = tcp_reps(r.frag, r.ret, p.frag_ck != 0);
       }
       uint32_t pos = (u - rstart) << 4;
       if (fast) {  // image units, then the record's last 16 bytes (past the image)
@@ -641,6 +646,7 @@ pack_kernel(PackParams p) {
           if ((uint32_t)j < rem) dst[j] = (uint8_t)(v[j >> 2] >> ((j & 3) * 8));
       }
       // TCP: the same bytes in every later buffer of the fragment (no copy pass re-reading P)
+      if constexpr (kTcp)
 #pragma unroll
       for (int k = 0; k < kMaxRep; k++) {
         if (pos < reps.cnt[k]) {
@@ -678,7 +684,10 @@ __global__ void pack_prepare_kernel(const mgenx_flow_tmpl* tmpl, uint32_t n_tmpl
 }
 
 hipError_t launch_pack(const PackParams& p, int grid, hipStream_t stream) {
-  hipLaunchKernelGGL(pack_kernel, dim3(grid), dim3(kPackThreads), 0, stream, p);
+  if (p.frag_len)
+    hipLaunchKernelGGL(pack_kernel<true>, dim3(grid), dim3(kPackThreads), 0, stream, p);
+  else
+    hipLaunchKernelGGL(pack_kernel<false>, dim3(grid), dim3(kPackThreads), 0, stream, p);
   return hipGetLastError();
 }
 

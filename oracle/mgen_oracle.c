@@ -2017,7 +2017,12 @@ uint64_t or_convert_binary_log(const uint8_t* file, uint64_t nbytes, int log_rx,
             uint32_t idx = 0, mml = 0;
             if (proto == 2) { mml = get32(b); idx = 4; }
             or_fields f;
-            or_unpack(b + idx, rl - idx, &f);    /* the reference passes recordLength */
+            /* the reference passes recordLength (:1624), i.e. 4 bytes more than the record
+             * holds after a TCP SEND's mgen_msg_len word: those come from its uninitialised
+             * or stale stack buffer (:1434).  Bounded here at the stored bytes: an Unpack
+             * that would reach them (a message cut before its host / GPS fields) stops at
+             * the record end instead (tests/test_gpu_binlog.py pins it). */
+            or_unpack(b + idx, rl - idx, &f);
             nrec++;
             if (!f.ok) { f.err = 0; f.ok = 1; }  /* logged anyway, fresh members (:1624-1625) */
             n = bl_send_line(&f, proto, mml, opts, line);

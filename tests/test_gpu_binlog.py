@@ -150,3 +150,30 @@ def test_convert_logs_rejected_stored_messages(torch, oracle):
     assert st == info.status == 0 and n == info.n_records
     assert want.count(b" RECV ") == short.size and want.count(b" SEND ") == 3
     assert got == want, _diff(got, want)
+
+
+def test_convert_tcp_send_bounded_at_the_record(torch, oracle):
+    """A TCP SEND record's stored message is Unpack-ed over the bytes the record holds.  The
+    reference passes recordLength (mgenMsg.cpp:1624), 4 bytes more than follow the
+    mgen_msg_len word, and those come from its uninitialised / stale read buffer (:1434): the
+    choice pinned here is the record bound.  Messages cut right after the destination address,
+    inside the host fields and inside the GPS fields: no host> field is read past the record,
+    device == oracle byte for byte."""
+    import struct
+    import mgen_amd
+    m = oracle.make_msg(msg_len=300, flow_id=5, seq=77, tx_sec=1_700_000_000, tx_usec=5,
+                        host=("4", bytes([10, 1, 2, 3]), 6000))
+    full = oracle.udp_pack(m, checksum=False)
+    hdr_end = 28  # msg_len .. dst address (IPv4)
+    parts = []
+    for cut in (hdr_end, hdr_end + 2, hdr_end + 4, hdr_end + 8, hdr_end + 12, 60, len(full)):
+        body = struct.pack(">I", 300) + full[:cut]
+        parts.append(struct.pack(">BBH", 3, 2, len(body)) + body)
+    log = B.binlog(parts + B.events(np.random.default_rng(2)))
+    want, st, n = oracle.convert_binary_log(log)
+    got, info = mgen_amd.convert_binary_log(log)
+    assert st == info.status == 0 and n == info.n_records
+    lines = [l for l in want.split(b"\n") if b" SEND " in l]
+    assert len(lines) == 7
+    assert b"host>" not in lines[0] and b"host>10.1.2.3/6000" in lines[-1], lines
+    assert got == want, _diff(got, want)
