@@ -234,7 +234,7 @@ def extra_config3(torch, eng, dev):
 N4_TOTAL = 8 * N_REC   # config 4: 8,388,608 records in total at every N
 
 
-def extra_config4(torch, eng, dev, world, rank, dist):
+def extra_config4(torch, eng, dev, world, rank, dist, rehearse=False):
     """1024 POISSON flows of 256-B messages, 8,388,608 records in total: rank r receives the
     records of the flows it owns (flow_id mod world == r), in receive order, and runs
     MgenAnalytic::Update over them (mgenx_flow_reduce: sort by flow, one wave per flow);
@@ -280,7 +280,14 @@ def extra_config4(torch, eng, dev, world, rank, dist):
         eng.flow_table_destroy(table)
     pipe = pipeline_config4(torch, eng, dev, d, idx, src, state["flows"], n_flows, n)
     ar_ms = None
-    if world > 1:
+    merge = "mgenx_allreduce_flows (RCCL ncclAllReduce sum, 1024 x 64 B)"
+    if world > 1 and rehearse:
+        # dry run: the same sum over gloo (ranks may share one GPU, which RCCL refuses)
+        merge = "rehearsal: gloo all-reduce of the exported counters (not RCCL)"
+        host = torch.from_numpy(counters.cpu().numpy().view(np.int64).copy())
+        dist.all_reduce(host)
+        ar_ms = None
+    elif world > 1:
         uid = torch.zeros(128, dtype=torch.uint8, device=dev)
         if rank == 0:
             uid.copy_(torch.frombuffer(bytearray(eng.comm_unique_id()), dtype=torch.uint8))
@@ -301,7 +308,7 @@ def extra_config4(torch, eng, dev, world, rank, dist):
             "findflow_ms": round(lk_ms, 4), "findflow_mrec_per_s": round(n / lk_ms / 1e3, 1),
             "rows_pipeline": pipe, "allreduce_bytes": n_flows * 64,
             "allreduce_ms": None if ar_ms is None else round(ar_ms, 4),
-            "merge": "mgenx_allreduce_flows (RCCL ncclAllReduce sum, 1024 x 64 B)"}
+            "merge": merge}
 
 
 def pipeline_config4(torch, eng, dev, d, idx, src, want_flows, n_flows, n):
@@ -360,7 +367,7 @@ def pipeline_config4(torch, eng, dev, d, idx, src, want_flows, n_flows, n):
             "checked": "per-flow state == column-path state (bit-exact)"}
 
 
-def extra_config5(torch, eng, dev, world=1, rank=0, dist=None):
+def extra_config5(torch, eng, dev, world=1, rank=0, dist=None, rehearse=False):
     """TCP stream of 16 KiB records (checksum on): boundary scan + TCP-rule unpack over
     1 GiB per rank, the stream built by the GPU TCP transmit path (mgenx_pack_tcp).
     N > 1: one stream of N GiB split into 1-GiB shards (+ 64 KiB halo) framed with the
@@ -393,7 +400,7 @@ def extra_config5(torch, eng, dev, world=1, rank=0, dist=None):
     total_bytes = shard.numel() * world
     state = {}
     if world > 1:
-        comm = TorchComm(dev)
+        comm = TorchComm(None if rehearse else dev)
         scanner = EngineScanner(eng)
 
         def scan():
@@ -417,7 +424,7 @@ def extra_config5(torch, eng, dev, world=1, rank=0, dist=None):
     torch.cuda.synchronize()
     scan_ms = (time.perf_counter() - t0) / reps * 1e3
     if world > 1:
-        t = torch.tensor([scan_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([scan_ms], dtype=torch.float64, device="cpu" if rehearse else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         scan_ms = float(t.item())
     offs, lens, summ = state["r"]
@@ -572,11 +579,16 @@ def main():
     ap.add_argument("--no-extras", action="store_true")
     args = ap.parse_args()
 
+    # MGENX_BENCH_REHEARSE=1: the N-rank protocol on however many GPUs are visible (ranks
+    # share them), torch.distributed over gloo, the RCCL counter merge replaced by a gloo
+    # all-reduce -- a dry run of every collective's order on a one-GPU box; its numbers
+    # mean nothing
+    rehearse = os.environ.get("MGENX_BENCH_REHEARSE") == "1"
     from mgen_amd import launch
     if launch.needs_launch(args.gpus):
         # `python bench.py --gpus N` outside torch.distributed.run: start the N ranks as a
         # child launcher before anything touches the GPU; rank 0 prints the line
-        sys.exit(launch.relaunch(__file__, sys.argv[1:], args.gpus))
+        sys.exit(launch.relaunch(__file__, sys.argv[1:], args.gpus, check_gpus=not rehearse))
 
     import torch
     import torch.distributed as dist
@@ -586,12 +598,19 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if rehearse:
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
     else:
         torch.cuda.set_device(0)
     dev = torch.device(f"cuda:{local}")
+    # collectives of host-side values: device tensors over RCCL, CPU tensors over gloo
+    cdev = torch.device("cpu") if rehearse else dev
 
     from mgen_amd import OPT_SKIP_CRC, PACK_CHECKSUM, Engine, to_device
     from mgen_amd.workloads import udp_fixed
@@ -652,7 +671,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -701,9 +720,10 @@ def main():
             except Exception as e:  # an extra never hides the headline line
                 extra[name] = {"error": f"{type(e).__name__}: {e}"[:300]}
         # configs 4 and 5 on every rank (they have collectives); the rest on rank 0 only
-        guard("config4_flow_reduce", lambda: extra_config4(torch, eng, dev, world, rank, dist))
+        guard("config4_flow_reduce",
+              lambda: extra_config4(torch, eng, dev, world, rank, dist, rehearse))
         guard("config5_tcp_scan_unpack",
-              lambda: extra_config5(torch, eng, dev, world, rank, dist))
+              lambda: extra_config5(torch, eng, dev, world, rank, dist, rehearse))
         if rank == 0:
             guard("config3_mixed_pack_unpack", lambda: extra_config3(torch, eng, dev))
             guard("pcie_inclusive_config2", lambda: extra_pcie(torch, eng, dev, slab))
@@ -734,7 +754,9 @@ def main():
                        "records_per_gpu": N_REC,
                        "record_bytes": REC, "checksum": True, "output": "mgenx_rec rows (32 B)",
                        "algorithmic_bytes_per_step_per_gpu": ALGO_BYTES,
-                       "parallelism": f"flow-sharded x{world} (independent slabs)"},
+                       "parallelism": f"flow-sharded x{world} (independent slabs)",
+                       **({"rehearsal": "ranks share GPUs over gloo: numbers invalid"}
+                          if rehearse else {})},
             "mmsg_per_s": round(world * N_REC * args.steps / elapsed / 1e6, 2),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBPS,
                          "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBPS, 4),

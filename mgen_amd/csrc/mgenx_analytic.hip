@@ -490,13 +490,52 @@ flow_update_wave_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
     double vs = lsum;
     const uint32_t run = (MGENX_DIAG && (abl & 1)) ? 0u : e - k;
     const double2* lp = reinterpret_cast<const double2*>(latl[wv]);
-#pragma unroll 4
-    for (uint32_t j = 0; j < run / 2u; j++) {
-      const double2 v = lp[j];
-      vs = __dadd_rn(vs, v.x);
-      vs = __dadd_rn(vs, v.y);
+    // software-pipelined: the next 8 latencies are read while the current 8 are added (two
+    // register sets, sched barriers keep the reads ahead), so the chain waits on v_add_f64,
+    // not on an LDS round trip every 8 adds.  Reads past `run` hit stale latl entries that
+    // are never added.
+    const uint32_t n8 = run / 8u;
+    auto rd = [&](double2 (&x)[4], uint32_t c) {
+      const uint32_t o = c < 8u ? 4u * c : 0u;
+      x[0] = lp[o]; x[1] = lp[o + 1]; x[2] = lp[o + 2]; x[3] = lp[o + 3];
+    };
+    auto add8 = [&](const double2 (&x)[4]) {
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        vs = __dadd_rn(vs, x[q].x);
+        vs = __dadd_rn(vs, x[q].y);
+      }
+    };
+    double2 A[4], B[4];
+    rd(A, 0);
+    uint32_t c = 0;
+    for (; c + 2u <= n8; c += 2u) {
+      rd(B, c + 1u);
+      __builtin_amdgcn_sched_barrier(0);
+      add8(A);
+      __builtin_amdgcn_sched_barrier(0);
+      rd(A, c + 2u);
+      __builtin_amdgcn_sched_barrier(0);
+      add8(B);
+      __builtin_amdgcn_sched_barrier(0);
     }
-    if (run & 1u) vs = __dadd_rn(vs, latl[wv][run - 1u]);
+    if (c < n8) {  // one whole chunk left in A; the remainder follows in B
+      rd(B, c + 1u);
+      __builtin_amdgcn_sched_barrier(0);
+      add8(A);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int q = 0; q < 4; q++) A[q] = B[q];
+    }
+    // the last run % 8 latencies are in A
+    const uint32_t rem = run & 7u;
+    if (rem > 0u) vs = __dadd_rn(vs, A[0].x);
+    if (rem > 1u) vs = __dadd_rn(vs, A[0].y);
+    if (rem > 2u) vs = __dadd_rn(vs, A[1].x);
+    if (rem > 3u) vs = __dadd_rn(vs, A[1].y);
+    if (rem > 4u) vs = __dadd_rn(vs, A[2].x);
+    if (rem > 5u) vs = __dadd_rn(vs, A[2].y);
+    if (rem > 6u) vs = __dadd_rn(vs, A[3].x);
     lsum = vs;
     __builtin_amdgcn_wave_barrier();
     if (++pruns == 65536u) flush();  // pbytes per lane stays below 2^32
@@ -504,16 +543,20 @@ flow_update_wave_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
 
   // 64 records per round: lane k holds record order[i0 + k]; the record loads of the next
   // two rounds and the index loads of the one after are in flight while this one is walked
+  // (the order index of a round is loaded two rounds before its record gather, so waiting
+  // for it -- loads complete in order -- never waits for a gather issued after the current
+  // round's records)
   auto ldo = [&](uint32_t base) { return order[min(base + lane, e - 1u)]; };
   uint32_t i0 = b;
   const uint32_t oa = ldo(i0), ob = ldo(i0 + 64u);
-  uint32_t oc = ldo(i0 + 128u);
+  uint32_t oc = ldo(i0 + 128u), od = ldo(i0 + 192u);
   FRec cur = recs[oa], nx1 = recs[ob], nx2;
   uint32_t ocur = oa, on1 = ob, on2;  // input record indices of cur / nx1 / nx2
   while (i0 < e) {
     nx2 = recs[oc];
     on2 = oc;
-    oc = ldo(i0 + 192u);
+    oc = od;
+    od = ldo(i0 + 256u);
     const uint32_t cnt = min(64u, e - i0);
     const uint64_t lbits = __builtin_bit_cast(uint64_t, cur.latency);
     const uint32_t llo = (uint32_t)lbits, lhi = (uint32_t)(lbits >> 32);
@@ -611,7 +654,7 @@ flow_update_wave_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
 //          of one flow from neighbouring tiles meet in the same L2 and leave it as whole lines.
 // Records whose flow index is >= n_flows (MGENX_FLOW_NONE) go to the extra last bin and are
 // not written.
-constexpr uint32_t kCountBins = 2048;  // LDS: (9 x bins + kTile) x 4 + kTile x 2 bytes
+constexpr uint32_t kCountBins = 2048;  // LDS: 9 x bins x 4 + kTile x 4 bytes
 constexpr uint32_t kSortWaves = 8;
 constexpr uint32_t kTile = 8192;
 constexpr uint32_t kPart = kTile / kSortWaves;
@@ -624,9 +667,26 @@ flow_hist_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows,
   for (uint32_t k = threadIdx.x; k < bins; k += blockDim.x) h[k] = 0u;
   __syncthreads();
   const uint32_t a = blockIdx.x * kTile, e = min(n, a + kTile);
-  for (uint32_t i = a + threadIdx.x; i < e; i += blockDim.x) {
-    atomicAdd(&h[min(idx[i], n_flows)], 1u);
-    recs[i] = make_frec(src, i);  // input order, coalesced
+  // kHistU records per thread and pass, all their loads issued before any is used (one
+  // load latency per pass instead of one per record)
+  constexpr uint32_t kHistU = 4;
+  for (uint32_t i0 = a + threadIdx.x; i0 < e; i0 += kHistU * blockDim.x) {
+    uint32_t fi[kHistU];
+    FRec r[kHistU];
+#pragma unroll
+    for (uint32_t u = 0; u < kHistU; u++) {
+      const uint32_t i = min(i0 + u * blockDim.x, e - 1u);
+      fi[u] = idx[i];
+      r[u] = make_frec(src, i);
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kHistU; u++) {
+      const uint32_t i = i0 + u * blockDim.x;
+      if (i < e) {
+        atomicAdd(&h[min(fi[u], n_flows)], 1u);
+        recs[i] = r[u];  // input order, coalesced
+      }
+    }
   }
   __syncthreads();
   for (uint32_t k = threadIdx.x; k < bins; k += blockDim.x) hist[(size_t)k * n_tiles + blockIdx.x] = h[k];
@@ -640,8 +700,10 @@ flow_order_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows
   const uint32_t bins = n_flows + 1u;
   uint32_t* cnt = lds;                                // [wave][bin]: counts, then run bases
   uint32_t* sbase = lds + kSortWaves * bins;          // [bin]: start - tile offset
-  uint32_t* lsorted = sbase + bins;                   // [kTile]: input index, flow-sorted
-  uint16_t* lkey = reinterpret_cast<uint16_t*>(lsorted + kTile);  // [kTile]: its flow
+  // [kTile] each: the input index - t0 (13 bits) and the flow, flow-sorted -- 16-bit entries
+  // keep the block at ~70 KB of LDS, two blocks per CU
+  uint16_t* lsorted = reinterpret_cast<uint16_t*>(sbase + bins);
+  uint16_t* lkey = lsorted + kTile;
   __shared__ uint32_t wsum[kSortWaves];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
   // tile: contiguous ranges per XCD (block b runs on XCD b % 8)
@@ -653,7 +715,17 @@ flow_order_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows
   const uint32_t t0 = t * kTile, tn = min(n - t0, kTile);
   const uint32_t a = t0 + w * kPart, e = min(n, a + kPart);
   uint32_t* my = cnt + w * bins;
-  for (uint32_t i = a + lane; i < e; i += 64u) atomicAdd(&my[min(idx[i], n_flows)], 1u);
+  // the wave's kPart keys, loaded once (all in flight together) for both passes below
+  constexpr uint32_t kKeys = kPart / 64u;
+  uint32_t keys[kKeys];
+#pragma unroll
+  for (uint32_t j = 0; j < kKeys; j++) {
+    const uint32_t i = a + 64u * j + lane;
+    keys[j] = i < e ? min(idx[i], n_flows) : 0xFFFFFFFFu;
+  }
+#pragma unroll
+  for (uint32_t j = 0; j < kKeys; j++)
+    if (keys[j] != 0xFFFFFFFFu) atomicAdd(&my[keys[j]], 1u);
   __syncthreads();
   // tile offsets: exclusive scan over bins of the tile's counts (thread j owns bins j*B..)
   const uint32_t B = (bins + blockDim.x - 1u) / blockDim.x;
@@ -683,10 +755,11 @@ flow_order_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows
   }
   __syncthreads();
   const uint64_t lt = (1ull << lane) - 1ull;
-  for (uint32_t i0 = a; i0 < e; i0 += 64u) {
-    const uint32_t i = i0 + lane;
+#pragma unroll
+  for (uint32_t j = 0; j < kKeys; j++) {
+    const uint32_t i = a + 64u * j + lane;
     const bool live = i < e;
-    const uint32_t key = live ? min(idx[i], n_flows) : 0u;
+    const uint32_t key = live ? keys[j] : 0u;
     uint64_t peers = __ballot(live);  // lanes holding the same key
     for (uint32_t bt = 0; bt < key_bits; bt++) {
       const bool one = (key >> bt) & 1u;
@@ -697,7 +770,7 @@ flow_order_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows
     const uint32_t base = live ? my[key] : 0u;
     if (live) {
       const uint32_t pos = base + rank;
-      lsorted[pos] = i;
+      lsorted[pos] = (uint16_t)(i - t0);
       lkey[pos] = (uint16_t)key;
       if (rank + 1u == (uint32_t)__popcll(peers)) my[key] = pos + 1u;
     }
@@ -705,7 +778,7 @@ flow_order_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows
   __syncthreads();
   for (uint32_t j = tid; j < tn; j += blockDim.x) {
     const uint32_t k = lkey[j];
-    if (k < n_flows) order[sbase[k] + j] = lsorted[j];
+    if (k < n_flows) order[sbase[k] + j] = t0 + lsorted[j];
   }
 }
 
@@ -879,7 +952,7 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
       return MGENX_EDEVICE;
     }
     // LDS: per-wave counts, bases, the sorted tile (index + 16-bit flow)
-    const uint32_t lds = (kSortWaves * bins + bins + kTile) * 4u + kTile * 2u;
+    const uint32_t lds = (kSortWaves * bins + bins) * 4u + kTile * 4u;
     static bool lds_set = false;
     if (!lds_set) {
       (void)hipFuncSetAttribute((const void*)flow_order_kernel,

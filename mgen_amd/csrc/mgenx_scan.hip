@@ -106,11 +106,13 @@ __device__ __forceinline__ uint32_t wave_excl(uint32_t c, uint32_t& wtot) {
 // entry then holds the candidate total and the number of overflowing blocks in one word.
 // kRedo: the second pass over the overflowing blocks only, once the offsets are known:
 // positions go straight to cand[base[b] ...] with no slot limit.
-template <bool kRedo>
+// kPlain (diagnostics build, MGENX_SCAN_PLAIN=1): plain instead of non-temporal loads
+template <bool kRedo, bool kPlain = false>
 __global__ void __launch_bounds__(kScanThreads)
 scan_detect_kernel(const uint8_t* __restrict__ s, uint64_t nbytes, ScanMode m,
                    uint32_t* __restrict__ slots, uint64_t* __restrict__ counts,
-                   const uint64_t* __restrict__ base, uint64_t* __restrict__ cand) {
+                   const uint64_t* __restrict__ base, uint64_t* __restrict__ cand,
+                   uint32_t* __restrict__ irregular) {
   constexpr uint32_t kW = kScanThreads / 64;
   if (kRedo && !(counts[blockIdx.x] >> 32)) return;
   __shared__ uint32_t first[kScanSteps + 1][kW];  // first word of each wave's chunk per step
@@ -121,7 +123,8 @@ scan_detect_kernel(const uint8_t* __restrict__ s, uint64_t nbytes, ScanMode m,
   if (block0 + kScanBlockBytes <= nbytes) {
 #pragma unroll
     for (uint32_t st = 0; st < kScanSteps; st++)
-      v[st] = ldnt128(s + block0 + st * (kScanThreads * 16) + 16u * t);  // read once
+      v[st] = kPlain ? ldu128(s + block0 + st * (kScanThreads * 16) + 16u * t)
+                     : ldnt128(s + block0 + st * (kScanThreads * 16) + 16u * t);  // read once
   } else {
 #pragma unroll
     for (uint32_t st = 0; st < kScanSteps; st++) {
@@ -204,7 +207,10 @@ scan_detect_kernel(const uint8_t* __restrict__ s, uint64_t nbytes, ScanMode m,
   }
   if (!kRedo && t == 0) {
     counts[blockIdx.x] = (uint64_t)total | (ovf ? (1ull << 32) : 0ull);
-    if (blockIdx.x == 0) counts[gridDim.x] = 0u;
+    if (blockIdx.x == 0) {
+      counts[gridDim.x] = 0u;
+      if (irregular) *irregular = 0u;  // the link step's flag (it runs after this kernel)
+    }
   }
 }
 
@@ -753,8 +759,15 @@ int scan_build(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, int mode, h
   uint64_t* d_counts = reinterpret_cast<uint64_t*>(static_cast<char*>(ws.slots.mem) + slot_b);
   uint64_t* d_base = d_counts + cnt_b / 8;
   void* d_cub = static_cast<char*>(ws.slots.mem) + slot_b + 2 * cnt_b;
-  hipLaunchKernelGGL(scan_detect_kernel<false>, dim3(nb), dim3(kScanThreads), 0, stream, s,
-                     nbytes, m, d_slots, d_counts, (const uint64_t*)nullptr, (uint64_t*)nullptr);
+  uint32_t* irregular = reinterpret_cast<uint32_t*>(static_cast<char*>(ws.small.mem) + 2048);
+  auto detect = scan_detect_kernel<false>;
+#if MGENX_DIAG
+  if (const char* v = getenv("MGENX_SCAN_PLAIN"))
+    if (atoi(v)) detect = scan_detect_kernel<false, true>;
+#endif
+  hipLaunchKernelGGL(detect, dim3(nb), dim3(kScanThreads), 0, stream, s,
+                     nbytes, m, d_slots, d_counts, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                     spec && ws.spec_cap ? irregular : (uint32_t*)nullptr);
   if (nb + 1 <= kScanSmall) {
     hipLaunchKernelGGL(scan_offsets_kernel, dim3(1), dim3(1024), 0, stream, d_counts, nb + 1,
                        d_base, ws.host_dev);
@@ -781,8 +794,6 @@ int scan_build(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, int mode, h
     lay_tables(ws, cap, levels);
     ws.spec_total = d_base + nb;
     ws.spec_pending = true;
-    uint32_t* irregular = reinterpret_cast<uint32_t*>(static_cast<char*>(ws.small.mem) + 2048);
-    if ((e = hipMemsetAsync(irregular, 0, 4, stream)) != hipSuccess) return fail(e, "scan");
     hipLaunchKernelGGL(scan_link_kernel, dim3((nb + 3) / 4), dim3(256), 0, stream, s, nbytes,
                        d_slots, d_counts, d_base, nb, ws.cand, ws.ups, ws.dists, (uint64_t)cap,
                        irregular);
@@ -814,7 +825,8 @@ int scan_build(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, int mode, h
   lay_tables(ws, n, levels);
   if (h_tot.overflowed)  // blocks with more candidates than slots: second pass, exact sizes
     hipLaunchKernelGGL(scan_detect_kernel<true>, dim3(nb), dim3(kScanThreads), 0, stream, s,
-                       nbytes, m, d_slots, d_counts, (const uint64_t*)d_base, ws.cand);
+                       nbytes, m, d_slots, d_counts, (const uint64_t*)d_base, ws.cand,
+                       (uint32_t*)nullptr);
   hipLaunchKernelGGL(scan_link_kernel, dim3((nb + 3) / 4), dim3(256), 0, stream, s, nbytes,
                      d_slots, d_counts, d_base, nb, ws.cand, ws.ups, ws.dists, (uint64_t)0,
                      (uint32_t*)nullptr);
@@ -933,7 +945,10 @@ extern "C" int mgenx_scan_run(void* wsp, const uint8_t* s, uint64_t nbytes, int 
                        regular);
     // not the regular chain: the lifting levels on the speculative tables, then the
     // enumeration from offset 0 -- launched regardless, each returning at once when the
-    // regular kernel already reported the chain (no host round trip to decide)
+    // regular kernel already reported the chain.  (Deciding on the host instead costs a
+    // second round trip whenever payloads hold plausible record starts -- the TCP transmit
+    // stream's repeated 8-KiB buffers each begin with a header -- 0.306 -> 0.323 ms on
+    // config 5.)
     launch_lifts(ws, ws.spec_total, stream, regular);
     hipLaunchKernelGGL(scan_enum_kernel, dim3((scap + 255) / 256), dim3(256), 0, stream, s,
                        ws.cand, lift_tabs(ws), ws.spec_total, 0u, 1, nbytes, (uint64_t)0, cap,

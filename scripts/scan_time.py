@@ -9,12 +9,15 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from mgen_amd import PACK_CHECKSUM, SCAN_TCP, Engine, to_device  # noqa: E402
+from mgen_amd import PACK_CHECKSUM, PACK_RANDOM_FILL, SCAN_TCP, Engine, to_device  # noqa: E402
 from mgen_amd._abi import DESC_DTYPE  # noqa: E402
 from mgen_amd.workloads import make_templates  # noqa: E402
 
 n = 65536
-eng = Engine(0)
+# DIAG=1: the diagnostics build (its env knobs, e.g. MGENX_SCAN_PLAIN); RF=1: RANDOM_FILL
+# payloads (plausible record starts inside payloads: the lifting path)
+eng = Engine(0, diag=os.environ.get("DIAG") == "1")
+rf = os.environ.get("RF") == "1"
 tmpl, pool = make_templates(64)
 desc = np.zeros(n, DESC_DTYPE)
 seq = np.arange(n)
@@ -27,14 +30,17 @@ tm, pl = to_device(tmpl), to_device(pool)
 tcrc = torch.empty(64, dtype=torch.int32, device="cuda")
 eng.pack_prepare(tm, 64, pl, tcrc)
 d_total = torch.full((n,), 16384, dtype=torch.int32, device="cuda")
-local, _ = eng.pack_tcp(tm, tcrc, to_device(desc), d_total, n, pl, opts=PACK_CHECKSUM)
-offs, lens, info = eng.stream_scan(local, SCAN_TCP, cap=n + 1)
+local, _ = eng.pack_tcp(tm, tcrc, to_device(desc), d_total, n, pl, opts=PACK_CHECKSUM | (PACK_RANDOM_FILL if rf else 0))
+out = (torch.empty(n + 1, dtype=torch.int64, device="cuda"),
+       torch.empty(n + 1, dtype=torch.int32, device="cuda"))
+offs, lens, info = eng.stream_scan(local, SCAN_TCP, out=out)
 print("warm", int(info.n_records), int(info.candidates), int(info.resolved), flush=True)
 torch.cuda.synchronize()
 reps = 20
 t0 = time.perf_counter()
 for _ in range(reps):
-    offs, lens, info = eng.stream_scan(local, SCAN_TCP, cap=n + 1)
+    offs, lens, info = eng.stream_scan(local, SCAN_TCP, out=out)
 torch.cuda.synchronize()
+assert int(info.n_records) == n, int(info.n_records)
 print("scan_ms", (time.perf_counter() - t0) / reps * 1e3, int(info.n_records), flush=True)
 eng.close()
