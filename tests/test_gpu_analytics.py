@@ -247,3 +247,29 @@ def test_flow_reduce_flow_none_and_tile_edges(torch, eng):
                                              sub["tx_usec"], sub["msg_len"], sub["rx_sec"],
                                              sub["rx_usec"], window=0.05, per_flow=8)
         compare(st, rep, count.cpu().numpy().view(np.uint32), of, orep, ocnt, 8)
+
+
+def test_flow_reduce_skewed_flows_tile_runs(torch, eng):
+    """The one-pass tile ordering's record supply: one flow holding most records (runs of
+    thousands per 8192-record tile, windows of 64 tiles far larger than the slot queue), flows
+    absent from whole tiles, a flow with a single record, report_rec pointing at the closing
+    record -- against the oracle."""
+    from mgen_amd.workloads import poisson_flows
+    from oracle import oracle as O
+    big = poisson_flows(420_000, 1, mean_gap_us=50, seed=21, reorder=3)
+    small = poisson_flows(30_000, 6, mean_gap_us=400, seed=22)
+    rng = np.random.default_rng(5)
+    d = {k: np.concatenate([big[k], small[k]]) for k in big}
+    d["flow_id"] = np.concatenate([big["flow_id"], small["flow_id"] + 1])  # flows 1, 2..7
+    perm = np.argsort(rng.random(len(d["seq"])) + np.arange(len(d["seq"])) / 2e4, kind="stable")
+    d = {k: np.ascontiguousarray(v[perm]) for k, v in d.items()}
+    single = {k: v[:1].copy() for k, v in d.items()}
+    single["flow_id"][:] = 8
+    d = {k: np.concatenate([d[k], single[k]]) for k in d}
+    n_flows, per_flow = 8, 64
+    st, rep, cnt, _ = run_gpu(torch, eng, d, n_flows, 0.02, per_flow)
+    of, orep, ocnt = O.flow_reduce_batch(n_flows, d["flow_id"] - 1, d["seq"], d["tx_sec"],
+                                         d["tx_usec"], d["msg_len"], d["rx_sec"],
+                                         d["rx_usec"], window=0.02, per_flow=per_flow)
+    assert int(ocnt[0]) > 5 and of[7].msg_count == 1
+    compare(st, rep, cnt, of, orep, ocnt, per_flow)
