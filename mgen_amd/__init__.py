@@ -58,6 +58,8 @@ def load(diag: bool = False):
     """Load libmgenx.so (or the diagnostics build libmgenx_diag.so); fails loudly when the
     HIP build is missing."""
     path = DIAG_LIB_PATH if diag else LIB_PATH
+    # geometry experiments (scripts/*_exp.sh): another build of the same sources
+    path = os.environ.get("MGENX_LIB_OVERRIDE", path)
     if path in _libs:
         return _libs[path]
     if not os.path.exists(path):

@@ -7,7 +7,7 @@
 //   SINK  MgenAppSinkTransport::OnInputReady (src/common/mgenAppSinkTransport.cpp:369-434):
 //         msg_len outside [MIN_SIZE, MAX_SIZE] discards the two length bytes (resync).
 // The framing is a sequential chain p_{i+1} = p_i + L(p_i).  On the GPU:
-//   1. detect: one coalesced streaming pass (each workgroup a 64 KiB block, 4 KiB per step
+//   1. detect: one coalesced streaming pass (each workgroup a 32 KiB block, 4 KiB per step
 //      through LDS so every position sees its 3 following bytes) flags plausible starts
 //      (L in range, record inside the stream, version byte == 2) into ordered per-block slots;
 //   2. compact (device scan of the block counts) + link: successor = the candidate at p + L,
@@ -38,8 +38,15 @@
 
 namespace mgenx {
 
-constexpr uint32_t kScanBlockBytes = 65536;  // detect block (one workgroup)
-constexpr uint32_t kScanThreads = 256;       // 16 B per thread and step
+// (MGENX_SCAN_BLOCK / MGENX_SCAN_THREADS: build-time overrides for geometry experiments)
+#ifndef MGENX_SCAN_BLOCK
+#define MGENX_SCAN_BLOCK 32768
+#endif
+#ifndef MGENX_SCAN_THREADS
+#define MGENX_SCAN_THREADS 256
+#endif
+constexpr uint32_t kScanBlockBytes = MGENX_SCAN_BLOCK;  // detect block (one workgroup)
+constexpr uint32_t kScanThreads = MGENX_SCAN_THREADS;   // 16 B per thread and step
 constexpr uint32_t kScanSlots = 4096;        // candidates per block before overflow
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 
@@ -95,9 +102,12 @@ __device__ __forceinline__ uint32_t wave_excl(uint32_t c, uint32_t& wtot) {
   return excl;
 }
 
-// 1. detect.  Workgroup b scans block b (64 KiB) as 16 steps of 4 KiB; lane t of the
+// 1. detect.  Workgroup b scans block b (32 KiB) as 8 steps of 4 KiB; lane t of the
 // workgroup owns bytes [16 t, 16 t + 16) of every step, so each wave load instruction reads
-// 1 KiB contiguously.  All 16 loads are issued up front (64 KiB in flight per workgroup).
+// 1 KiB contiguously.  All 8 loads are issued up front (32 KiB in flight per workgroup;
+// 52 VGPRs, 8 waves per SIMD.  64-KiB blocks (16 loads, 84 VGPRs, 5 waves per SIMD) ran the
+// config-5 scan in 0.304 ms, 32 KiB in 0.280-0.285 ms; 512- and 1024-thread blocks were
+// slower: scripts/scan_geom_build.sh + scan_time.py).
 // A position needs the 3 bytes after it: the next lane's first word comes by a lane shift,
 // across waves through LDS.  Candidates go to the block's slots in stream order (step-major,
 // then lane): per-step wave prefixes by ballot, one workgroup barrier for the wave totals.
@@ -233,13 +243,17 @@ struct ChainEnd {
 // (sorted, usually a handful) -- or, for a block that overflowed its slots, in its range of
 // cand, written by the second detect pass.  up0 = successor (self for a terminal),
 // dist0 = 1 if linked.
+constexpr uint32_t kLinkPerWave = 4;  // detect blocks per link wave
 __global__ void __launch_bounds__(256)
 scan_link_kernel(const uint8_t* __restrict__ s, uint64_t nbytes, const uint32_t* __restrict__ slots,
                  const uint64_t* __restrict__ counts, const uint64_t* __restrict__ base,
                  uint32_t n_blocks, uint64_t* __restrict__ cand, uint32_t* __restrict__ up,
                  uint32_t* __restrict__ dist, uint64_t spec_cap, uint32_t* __restrict__ irregular) {
-  const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (b >= n_blocks) return;
+  // 16 lanes per detect block, 4 blocks per wave (a block holds a handful of candidates)
+  const uint32_t b =
+      (blockIdx.x * 4 + (threadIdx.x >> 6)) * kLinkPerWave + ((threadIdx.x & 63u) >> 4);
+  const uint32_t sub = threadIdx.x & 15u;
+  const bool live = b < n_blocks;
   // irregular (optional): set unless every candidate's successor is the next candidate and
   // the last one is terminal -- then the chain from candidate 0 is the whole candidate list
   const uint64_t n_tot = base[n_blocks];
@@ -248,18 +262,17 @@ scan_link_kernel(const uint8_t* __restrict__ s, uint64_t nbytes, const uint32_t*
   // total exceeds them; an overflowing block (its candidates need the second detect pass)
   // gets terminal entries -- the host sees either case and rebuilds exactly
   if (spec_cap && base[n_blocks] > spec_cap) return;
-  const uint64_t cw = counts[b];
+  const uint64_t cw = live ? counts[b] : 0ull;
   const uint32_t c = (uint32_t)cw;
-  const uint32_t o = (uint32_t)base[b];
+  const uint32_t o = live ? (uint32_t)base[b] : 0u;
   if (spec_cap && (cw >> 32)) {
-    for (uint32_t k = threadIdx.x & 63u; k < c; k += 64) {
+    for (uint32_t k = sub; k < c; k += 16) {
       up[o + k] = o + k;
       dist[o + k] = 0u;
     }
-    if (irregular && c && (threadIdx.x & 63u) == 0u) *irregular = 1u;
-    return;
+    if (irregular && c && sub == 0u) *irregular = 1u;
   }
-  for (uint32_t k = threadIdx.x & 63u; k < c; k += 64) {
+  for (uint32_t k = sub; k < c && !(spec_cap && (cw >> 32)); k += 16) {
     uint64_t p, nx;
     if (cw >> 32) {
       p = cand[o + k];
@@ -349,67 +362,74 @@ __global__ void scan_total_kernel(const uint64_t* __restrict__ last, uint64_t* _
   *host = *last;
 }
 
-// exclusive scan of the block counts in one workgroup, for up to kScanSmall entries
-// (streams up to 2 GiB): wave w scans the contiguous segment [w S, w S + S) as rows of 64
-// (coalesced loads, all in flight; lane-shift scans with a running carry), one barrier for
-// the wave totals, coalesced stores.  The total word (candidates | overflowing blocks << 32)
-// also goes to host-mapped memory.
+// exclusive scan of the block counts in one workgroup, for up to kScanSmall blocks (a 1 GiB
+// stream is 32768 detect blocks): the low words go through LDS -- coalesced loads in,
+// thread t then owns the K = ceil(nb / 1024) consecutive entries [t K, t K + K) (one
+// sequential pass, one lane-shift scan of the thread totals per wave, one barrier for the
+// wave totals), writes their prefixes back in place, and the prefixes leave in coalesced
+// rows.  LDS index i sits at i + i / 32, so the K-strided accesses of a wave fall on
+// distinct banks.  (Rows of 64 per wave with a lane-shift scan per row took 23 us for
+// 32768 blocks; reading the K entries straight from global memory, 57 us.)  base[nb] and the
+// host-mapped total word (candidates | overflowing blocks << 32) come from thread 0.
 constexpr uint32_t kScanSmall = 32768;
+constexpr uint32_t kOffLds = (kScanSmall + kScanSmall / 32) * 4;
+__device__ __forceinline__ uint32_t off_pad(uint32_t i) { return i + (i >> 5); }
 __global__ void __launch_bounds__(1024)
-scan_offsets_kernel(const uint64_t* __restrict__ counts, uint32_t m, uint64_t* __restrict__ base,
+scan_offsets_kernel(const uint64_t* __restrict__ counts, uint32_t nb, uint64_t* __restrict__ base,
                     uint64_t* __restrict__ host) {
-  constexpr uint32_t kRows = kScanSmall / 1024;
+  extern __shared__ uint32_t sv[];
   __shared__ uint32_t wsum[16], wovf[16];
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
-  const uint32_t seg = (((m + 15) / 16) + 63) & ~63u;  // S, a multiple of 64
-  const uint32_t rows = seg / 64;
-  // pass 1: wave totals (loads all in flight)
-  uint32_t sum = 0, ovf = 0;
+  uint32_t ovf = 0;
+  constexpr uint32_t kU = 8;  // coalesced rows of 1024 in flight per pass
+  for (uint32_t r0 = 0; r0 < nb; r0 += kU * 1024u) {
+    uint64_t c[kU];
 #pragma unroll
-  for (uint32_t r = 0; r < kRows; r++) {
-    const uint32_t i = wv * seg + r * 64 + lane;
-    const uint64_t c = (r < rows && i < m) ? counts[i] : 0ull;
-    sum += (uint32_t)c;
-    ovf += (uint32_t)(c >> 32);
-  }
+    for (uint32_t u = 0; u < kU; u++) c[u] = counts[min(r0 + u * 1024u + t, nb - 1u)];
 #pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) sum += __shfl_xor(sum, d);
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) ovf += __shfl_xor(ovf, d);
-  if (lane == 0) {
-    wsum[wv] = sum;
-    wovf[wv] = ovf;
+    for (uint32_t u = 0; u < kU; u++) {
+      const uint32_t i = r0 + u * 1024u + t;
+      if (i < nb) {
+        sv[off_pad(i)] = (uint32_t)c[u];
+        ovf += (uint32_t)(c[u] >> 32);
+      }
+    }
   }
   __syncthreads();
-  uint32_t carry = 0, total = 0, novf = 0;
+  const uint32_t K = (nb + 1023u) / 1024u;
+  const uint32_t i0 = min(t * K, nb), i1 = min(i0 + K, nb);
+  uint32_t tot = 0;
+  for (uint32_t i = i0; i < i1; i++) tot += sv[off_pad(i)];
+  uint32_t incl = tot;
+#pragma unroll
+  for (uint32_t d = 1; d < 64u; d <<= 1) {
+    const uint32_t o = (uint32_t)__shfl_up((int)incl, d);
+    if (lane >= d) incl += o;
+  }
+  uint32_t wo = ovf;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) wo += (uint32_t)__shfl_xor((int)wo, d);
+  if (lane == 63u) wsum[wv] = incl;
+  if (lane == 0u) wovf[wv] = wo;
+  __syncthreads();
+  uint32_t run = incl - tot, total = 0, novf = 0;
 #pragma unroll
   for (uint32_t k = 0; k < 16; k++) {
-    carry += k < wv ? wsum[k] : 0u;
+    run += k < wv ? wsum[k] : 0u;
     total += wsum[k];
     novf += wovf[k];
   }
-  // pass 2: rows again (now cached), lane-shift scans with the running carry, stores
-  for (uint32_t r0 = 0; r0 < rows; r0 += 8) {
-    uint32_t v[8];
-#pragma unroll
-    for (uint32_t r = 0; r < 8; r++) {
-      const uint32_t i = wv * seg + (r0 + r) * 64 + lane;
-      v[r] = (r0 + r < rows && i < m) ? (uint32_t)counts[i] : 0u;
-    }
-#pragma unroll
-    for (uint32_t r = 0; r < 8; r++) {
-      uint32_t incl = v[r];
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t o = __shfl_up(incl, d);
-        if (lane >= (uint32_t)d) incl += o;
-      }
-      const uint32_t i = wv * seg + (r0 + r) * 64 + lane;
-      if (r0 + r < rows && i < m) base[i] = carry + incl - v[r];
-      carry += __shfl(incl, 63);
-    }
+  for (uint32_t i = i0; i < i1; i++) {
+    const uint32_t v = sv[off_pad(i)];
+    sv[off_pad(i)] = run;
+    run += v;
   }
-  if (t == 0) *host = (uint64_t)total | ((uint64_t)novf << 32);
+  __syncthreads();
+  for (uint32_t i = t; i < nb; i += 1024u) base[i] = sv[off_pad(i)];
+  if (t == 0) {
+    base[nb] = total;
+    *host = (uint64_t)total | ((uint64_t)novf << 32);
+  }
 }
 
 __device__ uint32_t find_cand(const uint64_t* cand, uint32_t n, uint64_t p) {
@@ -685,6 +705,8 @@ size_t tab_bytes(uint32_t stride, int levels) {
   return (size_t)stride * 4 * (2 * (size_t)(levels + 1) + 4 * (size_t)levels);
 }
 
+uint32_t link_grid(uint32_t nb) { return (nb + 4 * kLinkPerWave - 1) / (4 * kLinkPerWave); }
+
 // carve ws.tabs into the lifting tables; launch the link and the lifting levels
 void lay_tables(mgenx_scan_ws& ws, uint32_t stride, int levels) {
   ws.stride = stride;
@@ -768,8 +790,16 @@ int scan_build(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, int mode, h
   hipLaunchKernelGGL(detect, dim3(nb), dim3(kScanThreads), 0, stream, s,
                      nbytes, m, d_slots, d_counts, (const uint64_t*)nullptr, (uint64_t*)nullptr,
                      spec && ws.spec_cap ? irregular : (uint32_t*)nullptr);
-  if (nb + 1 <= kScanSmall) {
-    hipLaunchKernelGGL(scan_offsets_kernel, dim3(1), dim3(1024), 0, stream, d_counts, nb + 1,
+  if (nb <= kScanSmall) {
+    static bool lds_set = false;
+    if (!lds_set) {
+      if ((e = hipFuncSetAttribute((const void*)scan_offsets_kernel,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kOffLds)) !=
+          hipSuccess)
+        return fail(e, "scan offsets");
+      lds_set = true;
+    }
+    hipLaunchKernelGGL(scan_offsets_kernel, dim3(1), dim3(1024), kOffLds, stream, d_counts, nb,
                        d_base, ws.host_dev);
   } else {
     if ((e = hipcub::DeviceScan::ExclusiveSum(d_cub, cub_bytes, (const uint64_t*)d_counts, d_base,
@@ -794,7 +824,7 @@ int scan_build(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, int mode, h
     lay_tables(ws, cap, levels);
     ws.spec_total = d_base + nb;
     ws.spec_pending = true;
-    hipLaunchKernelGGL(scan_link_kernel, dim3((nb + 3) / 4), dim3(256), 0, stream, s, nbytes,
+    hipLaunchKernelGGL(scan_link_kernel, dim3(link_grid(nb)), dim3(256), 0, stream, s, nbytes,
                        d_slots, d_counts, d_base, nb, ws.cand, ws.ups, ws.dists, (uint64_t)cap,
                        irregular);
     // (the lifting levels follow only when the chain is not the candidate list itself:
@@ -827,7 +857,7 @@ int scan_build(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, int mode, h
     hipLaunchKernelGGL(scan_detect_kernel<true>, dim3(nb), dim3(kScanThreads), 0, stream, s,
                        nbytes, m, d_slots, d_counts, (const uint64_t*)d_base, ws.cand,
                        (uint32_t*)nullptr);
-  hipLaunchKernelGGL(scan_link_kernel, dim3((nb + 3) / 4), dim3(256), 0, stream, s, nbytes,
+  hipLaunchKernelGGL(scan_link_kernel, dim3(link_grid(nb)), dim3(256), 0, stream, s, nbytes,
                      d_slots, d_counts, d_base, nb, ws.cand, ws.ups, ws.dists, (uint64_t)0,
                      (uint32_t*)nullptr);
   launch_lifts(ws, nullptr, stream);
