@@ -279,6 +279,23 @@ def extra_config4(torch, eng, dev, world, rank, dist, rehearse=False):
     finally:
         eng.flow_table_destroy(table)
     pipe = pipeline_config4(torch, eng, dev, d, idx, src, state["flows"], n_flows, n)
+    # one rank's share at N = 8 (flows f with f mod 8 == 0: 128 flows, 1/8 of the records),
+    # timed here at N = 1: the per-flow update does not shrink with N
+    share8 = None
+    if world == 1:
+        own8 = (d["flow_id"] % 8) == 0
+        t8 = {k: torch.from_numpy(np.ascontiguousarray(v[own8])).to(dev) for k, v in d.items()}
+        i8 = torch.from_numpy(np.ascontiguousarray(idx[own8])).to(dev)
+        n8 = int(own8.sum())
+
+        def run8():
+            f8 = eng.flow_init(n_flows, 1.0)
+            eng.flow_reduce(f8, n_flows, i8, t8["seq"], t8["tx_sec"], t8["tx_usec"],
+                            t8["msg_len"], t8["rx_sec"], t8["rx_usec"], n=n8)
+        ms8 = timed(torch, run8, reps=5)
+        share8 = {"records": n8, "flows": n_flows // 8, "reduce_ms": round(ms8, 4),
+                  "mrec_per_s": round(n8 / ms8 / 1e3, 1),
+                  "note": "rank 0's share of config 4 at N = 8, timed on one GPU"}
     ar_ms = None
     merge = "mgenx_allreduce_flows (RCCL ncclAllReduce sum, 1024 x 64 B)"
     if world > 1 and rehearse:
@@ -306,7 +323,7 @@ def extra_config4(torch, eng, dev, world, rank, dist, rehearse=False):
     return {"records_total": N4_TOTAL, "records_this_rank": n, "flows": n_flows,
             "reduce_ms": round(ms, 4), "mrec_per_s": round(n / ms / 1e3, 2),
             "findflow_ms": round(lk_ms, 4), "findflow_mrec_per_s": round(n / lk_ms / 1e3, 1),
-            "rows_pipeline": pipe, "allreduce_bytes": n_flows * 64,
+            "rows_pipeline": pipe, "rank_share_at_8": share8, "allreduce_bytes": n_flows * 64,
             "allreduce_ms": None if ar_ms is None else round(ar_ms, 4),
             "merge": merge}
 

@@ -371,7 +371,7 @@ __global__ void scan_total_kernel(const uint64_t* __restrict__ last, uint64_t* _
 // distinct banks.  (Rows of 64 per wave with a lane-shift scan per row took 23 us for
 // 32768 blocks; reading the K entries straight from global memory, 57 us.)  base[nb] and the
 // host-mapped total word (candidates | overflowing blocks << 32) come from thread 0.
-constexpr uint32_t kScanSmall = 32768;
+constexpr uint32_t kScanSmall = 36864;  // 1.125 GiB of 32-KiB blocks (a 1-GiB shard + its halo)
 constexpr uint32_t kOffLds = (kScanSmall + kScanSmall / 32) * 4;
 __device__ __forceinline__ uint32_t off_pad(uint32_t i) { return i + (i >> 5); }
 __global__ void __launch_bounds__(1024)

@@ -268,9 +268,10 @@ def test_sharded_scan_config5_shape(torch, eng, gold):
 
 
 def test_scan_beyond_4gib_device_scan_path(torch, eng, gold):
-    """A stream of more than 65535 detect blocks (> 4 GiB) takes the multi-workgroup
-    exclusive scan of the block counts: a valid prefix followed by zero bytes frames as the
-    oracle frames the prefix plus the zero-length error after it."""
+    """A stream of more than 36864 detect blocks (> 1.125 GiB of 32-KiB blocks; this one is
+    past 4 GiB, so offsets need 64 bits) takes the multi-workgroup exclusive scan of the block
+    counts: a valid prefix followed by zero bytes frames as the oracle frames the prefix plus
+    the zero-length error after it."""
     from oracle import oracle as O
     rng = np.random.default_rng(SEED + 60)
     pre = tcp_stream(gold, rng.integers(76, 3000, 50), rng)
