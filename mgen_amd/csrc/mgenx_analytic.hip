@@ -782,6 +782,80 @@ flow_order_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows
   }
 }
 
+// scan: start[k * n_tiles + t] = exclusive prefix of hist in flow-major order, in two small
+// kernels (a device-library scan of the ~1M-entry array took 26 us for config 4):
+//   row totals: one block per flow row;
+//   row scan:   one block per flow row, its base = the sum of the earlier rows' totals.
+__global__ void __launch_bounds__(256)
+flow_row_total_kernel(const uint32_t* __restrict__ hist, uint32_t n_tiles,
+                      uint32_t* __restrict__ totals) {
+  __shared__ uint32_t ws[4];
+  const uint32_t* row = hist + (size_t)blockIdx.x * n_tiles;
+  uint32_t v = 0;
+  for (uint32_t t = threadIdx.x; t < n_tiles; t += 256u) v += row[t];
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
+  if ((threadIdx.x & 63u) == 0) ws[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) totals[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+__global__ void __launch_bounds__(1024)
+flow_row_scan_kernel(const uint32_t* __restrict__ hist, uint32_t n_tiles,
+                     const uint32_t* __restrict__ totals, uint32_t* __restrict__ start) {
+  __shared__ uint32_t ws[16];
+  __shared__ uint32_t carry_s;
+  const uint32_t k = blockIdx.x, tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+  // this row's base: the earlier rows' totals
+  uint32_t b = 0;
+  for (uint32_t j = tid; j < k; j += 1024u) b += totals[j];
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) b += (uint32_t)__shfl_xor((int)b, o);
+  if (lane == 0) ws[w] = b;
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t s0 = 0;
+    for (int i = 0; i < 16; i++) s0 += ws[i];
+    carry_s = s0;
+  }
+  __syncthreads();
+  uint32_t carry = carry_s;
+  const uint32_t* row = hist + (size_t)k * n_tiles;
+  uint32_t* out = start + (size_t)k * n_tiles;
+  constexpr uint32_t kPer = 4;
+  for (uint32_t c0 = 0; c0 < n_tiles; c0 += 1024u * kPer) {
+    uint32_t x[kPer], tsum = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < kPer; u++) {
+      const uint32_t t = c0 + tid * kPer + u;
+      x[u] = t < n_tiles ? row[t] : 0u;
+      tsum += x[u];
+    }
+    uint32_t incl = tsum;  // inclusive wave scan of the thread sums
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
+      if (lane >= (uint32_t)o) incl += y;
+    }
+    __syncthreads();  // ws reuse
+    if (lane == 63u) ws[w] = incl;
+    __syncthreads();
+    uint32_t before = carry + incl - tsum, total = 0;
+    for (uint32_t v = 0; v < 16u; v++) {
+      const uint32_t sv = ws[v];
+      before += v < w ? sv : 0u;
+      total += sv;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kPer; u++) {
+      const uint32_t t = c0 + tid * kPer + u;
+      if (t < n_tiles) out[t] = before;
+      before += x[u];
+    }
+    carry += total;
+  }
+}
+
 // ---- the general ordering (any flow count): hipCUB radix sort of (flow, record) pairs ----
 // keys: flow index clamped to n_flows (records to skip sort last); vals: record index
 __global__ void flow_keys_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows,
@@ -909,8 +983,7 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
   const size_t n_hist = (size_t)bins * n_tiles;
   size_t cub_bytes = 0;
   if (sort_path == 0)
-    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, cub_bytes, (const uint32_t*)nullptr,
-                                           (uint32_t*)nullptr, (int)n_hist, stream);
+    cub_bytes = (size_t)bins * 4u;  // the row totals
   else
     (void)hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, (const uint32_t*)nullptr,
                                              (uint32_t*)nullptr, (const uint32_t*)nullptr,
@@ -946,7 +1019,11 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
     void* cub_tmp = take(a256(cub_bytes));
     hipLaunchKernelGGL(flow_hist_kernel, dim3(n_tiles), dim3(512), bins * 4u, stream, flow_idx, n,
                        n_flows, n_tiles, hist, src, recs);
-    e = hipcub::DeviceScan::ExclusiveSum(cub_tmp, cub_bytes, hist, start, (int)n_hist, stream);
+    uint32_t* totals = (uint32_t*)cub_tmp;
+    hipLaunchKernelGGL(flow_row_total_kernel, dim3(bins), dim3(256), 0, stream, hist, n_tiles, totals);
+    hipLaunchKernelGGL(flow_row_scan_kernel, dim3(bins), dim3(1024), 0, stream, hist, n_tiles,
+                       totals, start);
+    e = hipGetLastError();
     if (e != hipSuccess) {
       snprintf(err, errn, "flow_reduce scan: %s", hipGetErrorString(e));
       return MGENX_EDEVICE;

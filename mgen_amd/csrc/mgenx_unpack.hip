@@ -887,7 +887,22 @@ unpack_kernel(UnpackParams p) {
 //     its placements loaded one tile ahead).
 // No header-first mode: every record's rows are read (for batches without checksummed
 // records this reads the bodies too; the payload stays unread by the CRC work otherwise).
-__global__ void __launch_bounds__(kUnpackThreads)
+// Row output (r03): the rows of the last KB groups are held in registers (lo / hi word of
+// the quad lane's 8 bytes and the record index) and stored in one burst every KB groups, as
+// the ring kernel does, instead of one row store per group mixed into the read stream.
+// Config 3 (`scripts/var_shapes.py`): per-group stores 0.250 ms, KB = 4 0.236 ms, every row
+// store sent to one scratch line (MODE 1, the bound of any store schedule) 0.223 ms.  KB = 8
+// spills 23 VGPRs at the 128-VGPR limit of 16 waves per CU (0.240 ms); 12 waves per CU with
+// KB = 8 or 16 fit the registers but lose the loads in flight (0.245-0.253 ms); flushing at
+// each tile's end with the indices recomputed from the rank permutation 0.239 ms;
+// non-temporal row stores 0.241-0.246 ms; tiles handed out by an atomic ticket (dynamic
+// balance) 0.32-0.44 ms.
+// Template knobs (the product instantiation is unpack_var_kernel<kUnpackThreads, 4, 0>):
+//   NT   block size (one block per CU: the LDS tables);
+//   KB   groups of rows held (0: one row store per group);
+//   MODE bit 1 (ablation): every core store to the sink; bit 8: non-temporal row stores.
+template <int NT, int KB, int MODE>
+__global__ void __launch_bounds__(NT)
 unpack_var_kernel(UnpackParams p) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const uint32_t* fold = lds + kRepDwords;  // [A4 | A8 | A12 | A16 | A32 | A48]
@@ -934,12 +949,39 @@ unpack_var_kernel(UnpackParams p) {
     }
     return __builtin_amdgcn_ds_permute((int)(rank << 2), lane);
   };
+  // the wave's tiles: wave_id, + n_waves, ...
   uint64_t t_c = wave_id, off_c, off_p;
+  uint64_t t_p = t_c + n_waves;
   uint32_t len_c, len_p;
   place(t_c, off_c, len_c);
   int src_c = rank_tile(t_c, len_c), src_p = lane;
-  place(t_c + n_waves, off_p, len_p);
+  place(t_p, off_p, len_p);
   bool p_ranked = false;
+
+  // ---- (KB > 0) rows held per group: lo / hi word of the quad lane's 8 bytes, record index
+  // (~0: the record's row is not the burst's -- a slow-layout or out-of-bounds record, stored
+  // at once by quad lane 0)
+  constexpr int KH = KB > 0 ? KB : 1;
+  uint32_t b0[KH], b1[KH], bi[KH];
+#pragma unroll
+  for (int j = 0; j < KH; j++) b0[j] = b1[j] = 0u, bi[j] = 0xFFFFFFFFu;
+  uint32_t held = 0;
+  const bool burst = KB > 0 && p.cols.rows != nullptr && !(MODE & 1);
+  auto st_row = [&](uint64_t a, uint64_t v) {
+    if (MODE & 8) st_g64_nt(a, v);
+    else st_g64(a, v);
+  };
+  auto flush = [&]() {
+#pragma unroll
+    for (int j = 0; j < KH; j++) {
+      const uint32_t back = (uint32_t)(KH - 1 - j);
+      if (back < held)  // wave-uniform
+        st_row(bi[j] != 0xFFFFFFFFu ? (uint64_t)p.cols.rows + (uint64_t)bi[j] * 32 + 8u * q
+                                    : (uint64_t)p.sink + 8u * (uint32_t)lane,
+               (uint64_t)b1[j] << 32 | b0[j]);
+    }
+    held = 0;
+  };
 
   // ---- a group: the quad's record and its row geometry ----
   struct Grp {
@@ -1005,12 +1047,12 @@ unpack_var_kernel(UnpackParams p) {
     Grp N;
     if (k + 1 < 4 && (uint32_t)(16 * (k + 1)) < n_valid_of(t_c)) {
       N = make(t_c, k + 1, off_c, len_c, src_c);
-    } else if (t_c + n_waves < n_tiles) {
+    } else if (t_p < n_tiles) {
       if (!p_ranked) {
-        src_p = rank_tile(t_c + n_waves, len_p);
+        src_p = rank_tile(t_p, len_p);
         p_ranked = true;
       }
-      N = make(t_c + n_waves, 0, off_p, len_p, src_p);
+      N = make(t_p, 0, off_p, len_p, src_p);
       next_tile = true;
     } else {
       has_next = false;
@@ -1121,7 +1163,24 @@ unpack_var_kernel(UnpackParams p) {
         v.dport = bswap16((uint16_t)(pw[5] & 0xffffu));
         v.flags = flags; v.err = err; v.dtype = (pw[5] >> 16) & 0xffu; v.dlen = D;
         v.ptype = (g3 >> 8) & 0xffu; v.gps = g3 & 0xffu;
-        store_core_quad_m(p, G.idx, fast, lane, q, v);
+        if (KB > 0 && burst) {
+          const uint32_t m0 = 0u - (uint32_t)(q == 0), m1 = 0u - (uint32_t)(q == 1);
+          const uint32_t m2 = 0u - (uint32_t)(q == 2), m3 = 0u - (uint32_t)(q == 3);
+          auto pick = [&](uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+            return (a & m0) | (b & m1) | (c & m2) | (d & m3);
+          };
+#pragma unroll
+          for (int j = 0; j < KH - 1; j++) b0[j] = b0[j + 1], b1[j] = b1[j + 1];
+          b0[KH - 1] = pick(v.flow, v.sec, v.dst4, (v.plen & 0xffffu) | v.flags << 16 | v.err << 24);
+          b1[KH - 1] = pick(v.seq, v.usec, (v.msg_len & 0xffffu) | v.dport << 16,
+                            v.dtype | v.dlen << 8 | v.ptype << 16 | v.gps << 24);
+#pragma unroll
+          for (int j = 0; j < KH - 1; j++) bi[j] = bi[j + 1];
+          bi[KH - 1] = fast ? G.idx : 0xFFFFFFFFu;
+          held++;
+        } else {
+          store_core_quad_m(p, G.idx, fast && !(MODE & 1), lane, q, v);
+        }
       }
       if (fast && any_ext) store_fast_ext(p.cols, G.idx, [&](int kk) { return pw[kk]; }, buf_len, q == 0);
       if (!fast && G.live && q == 0) {
@@ -1148,16 +1207,18 @@ unpack_var_kernel(UnpackParams p) {
       }
     }
 
+    if (KB > 0 && burst && held == (uint32_t)KH) flush();
     if (!has_next) break;
     // N's header: needed only after N's rows, so loaded after G's column stores
     pf = ldu128(hdr_ptr(N));
     expect = p.expect[N.live ? N.L : 0u];
     if (next_tile) {
-      t_c += n_waves;
+      t_c = t_p;
+      t_p = t_c + n_waves;
       off_c = off_p;
       len_c = len_p;
       src_c = src_p;
-      place(t_c + n_waves, off_p, len_p);
+      place(t_p, off_p, len_p);
       p_ranked = false;
       k = 0;
     } else {
@@ -1165,6 +1226,7 @@ unpack_var_kernel(UnpackParams p) {
     }
     G = N;
   }
+  if (KB > 0 && burst && held) flush();
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1778,9 +1840,19 @@ static hipError_t launch_mode(const UnpackParams& p, int grid, hipStream_t strea
   return launch_lds(unpack_kernel<true, MODE>, attr_done, p, grid, stream);
 }
 
+template <int NT = kUnpackThreads, int KB = 4, int MODE = 0>
 static hipError_t launch_var(const UnpackParams& p, int grid, hipStream_t stream) {
   static bool attr_done = false;
-  return launch_lds(unpack_var_kernel, attr_done, p, grid, stream);
+  if (!attr_done) {
+    hipError_t e = hipFuncSetAttribute((const void*)unpack_var_kernel<NT, KB, MODE>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)kUnpackLdsBytes);
+    if (e != hipSuccess) return e;
+    attr_done = true;
+  }
+  hipLaunchKernelGGL((unpack_var_kernel<NT, KB, MODE>), dim3(grid), dim3(NT), kUnpackLdsBytes,
+                     stream, p);
+  return hipGetLastError();
 }
 
 #if MGENX_DIAG
@@ -1897,6 +1969,19 @@ hipError_t launch_unpack(const UnpackParams& p, int grid, hipStream_t stream, in
     case 3: return launch_mode<0>(p, grid, stream);  // variable lengths, unsorted
     case 4: return launch_sorted(p, grid, stream);   // sorted groups, no load ring
     default: break;
+  }
+  // var-kernel shapes (20..39): block size, rows held, the store ablation
+  if (p.rec_len && unpack_variant >= 20 && unpack_variant < 40) {
+    *which = MGENX_UNPACK_K_VAR;
+    switch (unpack_variant) {
+      case 20: return launch_var<1024, 0, 1>(p, grid, stream);  // every row store to the sink
+      case 21: return launch_var<1024, 0, 0>(p, grid, stream);  // one row store per group
+      case 22: return launch_var<768, 8, 0>(p, grid, stream);
+      case 23: return launch_var<768, 16, 0>(p, grid, stream);
+      case 27: return launch_var<1024, 8, 0>(p, grid, stream);
+      case 32: return launch_var<1024, 4, 8>(p, grid, stream);  // non-temporal row stores
+      default: break;
+    }
   }
 #endif  // MGENX_DIAG
   // per-record lengths: sorted groups with the rows in a load ring -- when every wave gets
