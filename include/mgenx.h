@@ -320,6 +320,9 @@ typedef struct mgenx_scan_info {
   int32_t  status;      /* 0 = ok, 1 = TCP record with msg_len < 4 (scan stopped there) */
   uint32_t candidates;  /* diagnostic: plausible starts found by the parallel pass */
   uint64_t resolved;    /* diagnostic: records framed by the sequential resolver */
+  uint32_t path;        /* diagnostic: how the chain was found -- 0 lifting (and resolver),
+                           1 every candidate a record, 2 the successor-marked hypothesis */
+  uint32_t reserved;
 } mgenx_scan_info;
 int mgenx_stream_scan(mgenx_ctx* ctx, const uint8_t* dev_stream, uint64_t nbytes, int mode,
                       uint64_t* dev_rec_off, uint32_t* dev_rec_len, uint64_t cap,

@@ -116,7 +116,8 @@ SCAN_REUSE = 1        # MGENX_SCAN_REUSE
 class ScanInfo(ctypes.Structure):
     _fields_ = [("n_records", ctypes.c_uint64), ("consumed", ctypes.c_uint64),
                 ("status", ctypes.c_int32), ("candidates", ctypes.c_uint32),
-                ("resolved", ctypes.c_uint64)]
+                ("resolved", ctypes.c_uint64), ("path", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
 
 
 # per-flow analytics (mgenx_flow_*): layouts of include/mgenx.h

@@ -89,6 +89,21 @@ __device__ __forceinline__ uint32_t detect_hits(const uint32_t (&w)[5], uint64_t
   return hits;
 }
 
+// Copies of a header inside a TCP message: MgenTcpTransport sends a fragment over 8192 bytes
+// as its 8-KiB Pack buffer re-sent from the start (mgenTransport.cpp:1818-1876), so such a
+// message carries its own header again at +8192, +16384, ... -- plausible starts that are not
+// records (config 5's stream has 2 candidates per record, and the chain then needs the
+// lifting).  A candidate whose first 16 bytes equal the 16 bytes 8192 earlier is taken for a
+// copy by the chain hypothesis of scan_mark_* (checked there: a wrong guess only costs the
+// exact path).  (Dropping the copies in detect instead cost detect 172 -> 201 us: the extra
+// dependent loads lengthen every block.)
+constexpr uint64_t kCopyDist = 8192;
+__device__ __forceinline__ bool is_copy(const uint8_t* __restrict__ s, uint64_t nbytes, uint64_t p) {
+  if (p < kCopyDist || p + 16 > nbytes) return false;
+  const u32x4_t a = ldu128(s + p), b = ldu128(s + p - kCopyDist);
+  return a.x == b.x && a.y == b.y && a.z == b.z && a.w == b.w;
+}
+
 // exclusive prefix over the lanes of the wave and the wave total of c (0..16), by ballots
 __device__ __forceinline__ uint32_t wave_excl(uint32_t c, uint32_t& wtot) {
   uint32_t excl = 0, tot = 0;
@@ -248,7 +263,8 @@ __global__ void __launch_bounds__(256)
 scan_link_kernel(const uint8_t* __restrict__ s, uint64_t nbytes, const uint32_t* __restrict__ slots,
                  const uint64_t* __restrict__ counts, const uint64_t* __restrict__ base,
                  uint32_t n_blocks, uint64_t* __restrict__ cand, uint32_t* __restrict__ up,
-                 uint32_t* __restrict__ dist, uint64_t spec_cap, uint32_t* __restrict__ irregular) {
+                 uint32_t* __restrict__ dist, uint64_t spec_cap, uint32_t* __restrict__ irregular,
+                 uint32_t* __restrict__ mark = nullptr, uint32_t epoch = 0) {
   // 16 lanes per detect block, 4 blocks per wave (a block holds a handful of candidates)
   const uint32_t b =
       (blockIdx.x * 4 + (threadIdx.x >> 6)) * kLinkPerWave + ((threadIdx.x & 63u) >> 4);
@@ -318,6 +334,8 @@ scan_link_kernel(const uint8_t* __restrict__ s, uint64_t nbytes, const uint32_t*
     }
     up[o + k] = tgt == kNone ? o + k : tgt;
     dist[o + k] = tgt == kNone ? 0u : 1u;
+    // (chain hypothesis, scan_mark_*: every candidate but a header copy marks its successor)
+    if (mark && tgt != kNone && !is_copy(s, nbytes, p)) mark[tgt] = (epoch << 2) | 1u;
     const uint64_t ci = (uint64_t)o + k;
     odd = odd || (ci + 1 < n_tot ? tgt != o + k + 1 : tgt != kNone);
   }
@@ -334,12 +352,13 @@ scan_enum_regular_kernel(const uint8_t* __restrict__ s, const uint64_t* __restri
                          const uint64_t* __restrict__ total, const uint32_t* __restrict__ irregular,
                          uint32_t stride, uint64_t cap, uint64_t* __restrict__ rec_off,
                          uint32_t* __restrict__ rec_len, ChainEnd* __restrict__ end,
-                         uint32_t* __restrict__ done) {
+                         uint32_t* __restrict__ done, uint64_t* __restrict__ host_regular) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t n = *total;
   const bool ok = *irregular == 0u && n != 0 && n <= stride && cand[0] == 0;
   if (i == 0) {
     *done = ok ? 1u : 0u;  // read by the lifting and enumeration launches that follow
+    if (host_regular) *host_regular = ok ? 1u : 0u;
     if (ok) {
       const uint64_t tp = cand[n - 1];
       end->count = n;
@@ -355,6 +374,178 @@ scan_enum_regular_kernel(const uint8_t* __restrict__ s, const uint64_t* __restri
   const uint64_t p = cand[i];
   rec_off[i] = p;
   rec_len[i] = be16_at(s, p);
+}
+
+// The chain from offset 0 on a speculative TCP build without lifting.  Its hypothesis H = {0}
+// and every candidate that is some candidate's successor (the link step marks them with this
+// scan's epoch): a record start past 0 is its predecessor's successor, while a plausible start
+// inside a payload is almost never where another candidate's record ends.  H is accepted when
+// it is one chain -- candidate 0 at offset 0, succ(h_i) = h_{i+1} in position order, the last
+// one terminal -- which proves that the chain from offset 0 is H exactly.  Three launches over
+// 1024-candidate blocks (the grid is sized by the table capacity; the candidate total is read
+// on the device): counts, then ranks + records + the successor check, then one workgroup that
+// folds the per-block results.
+struct MarkTabs {
+  uint32_t* mark;
+  uint32_t epoch;
+  uint32_t* cnt;   // [blocks] H elements per block
+  uint32_t* fail;  // [blocks] a successor check failed
+  uint32_t* last;  // [blocks] the block's last H element (kNone: none)
+};
+// H = level 2: the successors of level-1 members (a successor of a successor): junk starts
+// inside headers chain in short runs (seq 0x802 = bytes 00 00 08 02 at header offset 8 reads
+// as a length-8 record at offset 9 whose successor at 17 is tx_usec's same bytes), and a
+// second level drops them
+__device__ __forceinline__ bool in_h1(const MarkTabs& m, uint32_t c) {
+  return c == 0u || (m.mark[c] >> 2) == m.epoch;
+}
+__device__ __forceinline__ bool in_h(const MarkTabs& m, uint32_t c) {
+  return c == 0u || m.mark[c] == ((m.epoch << 2) | 2u);
+}
+
+__global__ void __launch_bounds__(1024)
+scan_mark_next_kernel(const uint32_t* __restrict__ up, const uint64_t* __restrict__ total,
+                      uint32_t stride, MarkTabs m) {
+  const uint32_t c = blockIdx.x * 1024u + threadIdx.x;
+  const uint64_t n64 = *total;
+  const uint32_t n = n64 <= stride ? (uint32_t)n64 : 0u;
+  if (c >= n || !in_h1(m, c)) return;
+  const uint32_t t = up[c];
+  if (t != c) m.mark[t] = (m.epoch << 2) | 2u;  // (raises a level-1 mark: in_h1 still holds)
+}
+
+__global__ void __launch_bounds__(1024)
+scan_mark_count_kernel(const uint64_t* __restrict__ total, uint32_t stride, MarkTabs m) {
+  __shared__ uint32_t ws[16];
+  const uint32_t t = threadIdx.x, c = blockIdx.x * 1024u + t;
+  const uint64_t n64 = *total;
+  const uint32_t n = n64 <= stride ? (uint32_t)n64 : 0u;
+  const bool h = c < n && in_h(m, c);
+  const uint64_t b = __ballot(h);
+  if ((t & 63u) == 0u) ws[t >> 6] = (uint32_t)__popcll(b);
+  __syncthreads();
+  if (t == 0) {
+    uint32_t x = 0;
+    for (int k = 0; k < 16; k++) x += ws[k];
+    m.cnt[blockIdx.x] = x;
+  }
+}
+
+__global__ void __launch_bounds__(1024)
+scan_mark_emit_kernel(const uint8_t* __restrict__ s, const uint64_t* __restrict__ cand,
+                      const uint32_t* __restrict__ up, const uint64_t* __restrict__ total,
+                      uint32_t stride, uint64_t cap, uint64_t* __restrict__ rec_off,
+                      uint32_t* __restrict__ rec_len, MarkTabs m) {
+  __shared__ uint32_t ws[16], wf[16];
+  __shared__ uint32_t list[1024];
+  __shared__ uint32_t base_s;
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6, blk = blockIdx.x;
+  const uint64_t n64 = *total;
+  const uint32_t n = n64 <= stride ? (uint32_t)n64 : 0u;
+  const uint32_t c = blk * 1024u + t;
+  const bool h = c < n && in_h(m, c);
+  // this block's first rank: the H counts of the blocks before it
+  uint32_t pre = 0;
+  for (uint32_t k = t; k < blk; k += 1024u) pre += m.cnt[k];
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) pre += (uint32_t)__shfl_xor((int)pre, o);
+  const uint64_t bal = __ballot(h);
+  const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+  if (lane == 0) {
+    ws[wv] = (uint32_t)__popcll(bal);
+    wf[wv] = pre;
+  }
+  __syncthreads();
+  if (t == 0) {
+    uint32_t x = 0;
+    for (int k = 0; k < 16; k++) x += wf[k];
+    base_s = x;
+  }
+  uint32_t local = below, bcnt = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 16; k++) {
+    local += k < wv ? ws[k] : 0u;
+    bcnt += ws[k];
+  }
+  if (h) list[local] = c;
+  __syncthreads();
+  bool fail = false;
+  if (h) {
+    const uint64_t r = (uint64_t)base_s + local;
+    const uint64_t p = cand[c];
+    if (r < cap) {
+      rec_off[r] = p;
+      rec_len[r] = be16_at(s, p);
+    }
+    uint32_t next = kNone;
+    if (local + 1u < bcnt) {
+      next = list[local + 1u];
+    } else {  // the block's last H element: the first H element after the block, if any
+      uint32_t x = (blk + 1u) * 1024u;
+      for (uint32_t steps = 0; x < n && !in_h(m, x); x++)
+        if (++steps > 4096u) { fail = true; break; }  // (give up: the host falls back)
+      next = x < n ? x : kNone;
+      m.last[blk] = c;
+    }
+    fail = fail || up[c] != (next == kNone ? c : next);
+  }
+  const uint64_t fb = __ballot(fail);
+  if (lane == 0) wf[wv] = fb ? 1u : 0u;
+  __syncthreads();
+  if (t == 0) {
+    uint32_t f = 0;
+    for (int k = 0; k < 16; k++) f |= wf[k];
+    m.fail[blk] = f;
+    if (bcnt == 0u) m.last[blk] = kNone;
+  }
+}
+
+__global__ void __launch_bounds__(256)
+scan_mark_final_kernel(const uint8_t* __restrict__ s, const uint64_t* __restrict__ cand,
+                       const uint64_t* __restrict__ total, uint32_t stride, uint32_t blocks,
+                       MarkTabs m, ChainEnd* __restrict__ end, uint64_t* __restrict__ host_regular) {
+  __shared__ uint32_t sm[4], sf[4], sl[4];
+  const uint32_t t = threadIdx.x;
+  const uint64_t n64 = *total;
+  const uint32_t n = n64 <= stride ? (uint32_t)n64 : 0u;
+  const uint32_t nb = (n + 1023u) / 1024u;
+  uint32_t sum = 0, f = 0, lastb = 0;  // lastb: 1 + the last block holding H elements
+  for (uint32_t k = t; k < nb && k < blocks; k += 256u) {
+    const uint32_t x = m.cnt[k];
+    sum += x;
+    f |= m.fail[k];
+    if (x) lastb = max(lastb, k + 1u);
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    sum += (uint32_t)__shfl_xor((int)sum, o);
+    f |= (uint32_t)__shfl_xor((int)f, o);
+    lastb = max(lastb, (uint32_t)__shfl_xor((int)lastb, o));
+  }
+  if ((t & 63u) == 0u) {
+    sm[t >> 6] = sum;
+    sf[t >> 6] = f;
+    sl[t >> 6] = lastb;
+  }
+  __syncthreads();
+  if (t == 0) {
+    const uint32_t msum = sm[0] + sm[1] + sm[2] + sm[3];
+    const uint32_t fl = sf[0] | sf[1] | sf[2] | sf[3];
+    const uint32_t lb = max(max(sl[0], sl[1]), max(sl[2], sl[3]));
+    const bool ok = n != 0u && nb <= blocks && cand[0] == 0 && msum != 0u && fl == 0u && lb != 0u;
+    *host_regular = ok ? 1u : 0u;
+    if (ok) {
+      const uint64_t tp = cand[m.last[lb - 1u]];
+      end->count = msum;
+      end->next_pos = tp + be16_at(s, tp);
+      end->more = 0;
+    } else {
+      end->count = 0;
+      end->next_pos = 0;
+      end->more = 2;
+    }
+  }
 }
 
 // the candidate total / overflow word (exclusive scan's last entry) to host-mapped memory
@@ -669,13 +860,20 @@ struct mgenx_scan_ws {
   uint32_t spec_cap = 0;
   const uint64_t* spec_total = nullptr;
   bool spec_pending = false;
+  // the chain hypothesis (scan_mark_*) in speculative whole-stream TCP scans: `pruned` = the
+  // current speculative tables were built for it.  After a stream where it was not the chain
+  // the next prune_skip scans do not try it (backoff 2, 4, ... 64 scans; reset on success)
+  uint32_t prune_skip = 0, prune_backoff = 0;
+  bool pruned = false;
+  ScanWork marks;        // [spec_cap] successor marks (epoch) + 3 x [blocks] (MarkTabs)
+  uint32_t epoch = 0;
 };
 
 extern "C" void* mgenx_scan_ws_new() { return new mgenx_scan_ws(); }
 extern "C" void mgenx_scan_ws_free(void* p) {
   mgenx_scan_ws* w = static_cast<mgenx_scan_ws*>(p);
   if (!w) return;
-  for (ScanWork* x : {&w->slots, &w->cands, &w->tabs, &w->small})
+  for (ScanWork* x : {&w->slots, &w->cands, &w->tabs, &w->small, &w->marks})
     if (x->mem) hipFree(x->mem);
   if (w->host) hipHostFree(w->host);
   delete w;
@@ -740,7 +938,7 @@ void launch_lifts(const mgenx_scan_ws& ws, const uint64_t* spec_total, hipStream
 }
 
 int scan_build(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, int mode, hipStream_t stream,
-               const Fail& fail, bool spec = false) {
+               const Fail& fail, bool spec = false, bool prune = false) {
   const bool sink = mode == MGENX_SCAN_SINK;
   const ScanMode m = sink ? ScanMode{MGENX_MIN_SIZE, MGENX_MAX_SIZE} : ScanMode{4u, 65535u};
   hipError_t e;
@@ -752,6 +950,7 @@ int scan_build(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, int mode, h
   ws.stride = 0;
   ws.spec_pending = false;
   ws.spec_total = nullptr;
+  ws.pruned = false;
   if ((e = ensure(ws.small, 4096)) != hipSuccess) return fail(e, "scan workspace");
   if (!ws.host) {
     void* hp = nullptr;
@@ -782,6 +981,8 @@ int scan_build(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, int mode, h
   uint64_t* d_base = d_counts + cnt_b / 8;
   void* d_cub = static_cast<char*>(ws.slots.mem) + slot_b + 2 * cnt_b;
   uint32_t* irregular = reinterpret_cast<uint32_t*>(static_cast<char*>(ws.small.mem) + 2048);
+  // the chain hypothesis (scan_mark_*) only in a speculative TCP build (checked: mgenx_scan_run)
+  const bool do_prune = prune && spec && ws.spec_cap && !sink;
   auto detect = scan_detect_kernel<false>;
 #if MGENX_DIAG
   if (const char* v = getenv("MGENX_SCAN_PLAIN"))
@@ -824,9 +1025,26 @@ int scan_build(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, int mode, h
     lay_tables(ws, cap, levels);
     ws.spec_total = d_base + nb;
     ws.spec_pending = true;
+    ws.pruned = do_prune;
+    uint32_t* mark = nullptr;
+    if (do_prune) {
+      const size_t mb = ((size_t)cap + 3 * ((size_t)cap / 1024 + 1)) * 4;
+      if (ws.marks.bytes < mb) {
+        if ((e = ensure(ws.marks, mb)) != hipSuccess ||
+            (e = hipMemsetAsync(ws.marks.mem, 0, mb, stream)) != hipSuccess)
+          return fail(e, "scan workspace");
+        ws.epoch = 0;
+      }
+      if (++ws.epoch >= (1u << 30)) {  // 30-bit epochs (2 level bits): wrapped, clear the marks
+        if ((e = hipMemsetAsync(ws.marks.mem, 0, ws.marks.bytes, stream)) != hipSuccess)
+          return fail(e, "scan workspace");
+        ws.epoch = 1;
+      }
+      mark = static_cast<uint32_t*>(ws.marks.mem);
+    }
     hipLaunchKernelGGL(scan_link_kernel, dim3(link_grid(nb)), dim3(256), 0, stream, s, nbytes,
                        d_slots, d_counts, d_base, nb, ws.cand, ws.ups, ws.dists, (uint64_t)cap,
-                       irregular);
+                       irregular, mark, ws.epoch);
     // (the lifting levels follow only when the chain is not the candidate list itself:
     // mgenx_scan_run, after its one sync)
     if ((e = hipGetLastError()) != hipSuccess) return fail(e, "scan launch");
@@ -959,7 +1177,9 @@ extern "C" int mgenx_scan_run(void* wsp, const uint8_t* s, uint64_t nbytes, int 
                               mgenx_scan_info* info, hipStream_t stream, char* err, size_t errn) {
   mgenx_scan_ws& ws = *static_cast<mgenx_scan_ws*>(wsp);
   const Fail fail{err, errn};
-  int rc = scan_build(ws, s, nbytes, mode, stream, fail, /*spec=*/true);
+  const bool try_chain = ws.prune_skip == 0;
+  if (ws.prune_skip) ws.prune_skip--;
+  int rc = scan_build(ws, s, nbytes, mode, stream, fail, /*spec=*/true, /*prune=*/try_chain);
   if (rc != MGENX_OK) return rc;
   if (ws.spec_pending) {
     // one sync for the whole scan: the chain from offset 0 enumerated on the speculative
@@ -970,25 +1190,54 @@ extern "C" int mgenx_scan_run(void* wsp, const uint8_t* s, uint64_t nbytes, int 
     const uint32_t* irregular =
         reinterpret_cast<const uint32_t*>(static_cast<char*>(ws.small.mem) + 2048);
     uint32_t* regular = reinterpret_cast<uint32_t*>(static_cast<char*>(ws.small.mem) + 2052);
-    hipLaunchKernelGGL(scan_enum_regular_kernel, dim3((scap + 255) / 256), dim3(256), 0, stream,
-                       s, ws.cand, ws.spec_total, irregular, scap, cap, rec_off, rec_len, d_end,
-                       regular);
+    const bool pruned = ws.pruned;
+    if (pruned) {
+      uint32_t* mark = static_cast<uint32_t*>(ws.marks.mem);
+      const uint32_t blocks = scap / 1024 + 1;
+      const MarkTabs mt = {mark, ws.epoch, mark + scap, mark + scap + blocks,
+                           mark + scap + 2 * blocks};
+      hipLaunchKernelGGL(scan_mark_next_kernel, dim3(blocks), dim3(1024), 0, stream, ws.ups,
+                         ws.spec_total, scap, mt);
+      hipLaunchKernelGGL(scan_mark_count_kernel, dim3(blocks), dim3(1024), 0, stream,
+                         ws.spec_total, scap, mt);
+      hipLaunchKernelGGL(scan_mark_emit_kernel, dim3(blocks), dim3(1024), 0, stream, s, ws.cand,
+                         ws.ups, ws.spec_total, scap, cap, rec_off, rec_len, mt);
+      hipLaunchKernelGGL(scan_mark_final_kernel, dim3(1), dim3(256), 0, stream, s, ws.cand,
+                         ws.spec_total, scap, blocks, mt, d_end, ws.host_dev + 5);
+    } else {
+      hipLaunchKernelGGL(scan_enum_regular_kernel, dim3((scap + 255) / 256), dim3(256), 0, stream,
+                         s, ws.cand, ws.spec_total, irregular, scap, cap, rec_off, rec_len, d_end,
+                         regular, ws.host_dev + 5);
+    }
     // not the regular chain: the lifting levels on the speculative tables, then the
     // enumeration from offset 0 -- launched regardless, each returning at once when the
     // regular kernel already reported the chain.  (Deciding on the host instead costs a
     // second round trip whenever payloads hold plausible record starts -- the TCP transmit
     // stream's repeated 8-KiB buffers each begin with a header -- 0.306 -> 0.323 ms on
-    // config 5.)
-    launch_lifts(ws, ws.spec_total, stream, regular);
-    hipLaunchKernelGGL(scan_enum_kernel, dim3((scap + 255) / 256), dim3(256), 0, stream, s,
-                       ws.cand, lift_tabs(ws), ws.spec_total, 0u, 1, nbytes, (uint64_t)0, cap,
-                       rec_off, rec_len, d_end, (const uint32_t*)regular);
+    // config 5.)  A pruned build is used only as the regular chain: no lifting on it.
+    if (!pruned) {
+      launch_lifts(ws, ws.spec_total, stream, regular);
+      hipLaunchKernelGGL(scan_enum_kernel, dim3((scap + 255) / 256), dim3(256), 0, stream, s,
+                         ws.cand, lift_tabs(ws), ws.spec_total, 0u, 1, nbytes, (uint64_t)0, cap,
+                         rec_off, rec_len, d_end, (const uint32_t*)regular);
+    }
     hipError_t e;
     if ((e = hipStreamSynchronize(stream)) != hipSuccess) return fail(e, "scan");
     uint32_t tot[2];
     memcpy(tot, (const void*)ws.host, 8);  // candidates, overflowing blocks
     const uint64_t max_cand = nbytes / 16 + 65536;
     ws.spec_pending = false;
+    const bool regular_chain = ((const volatile uint64_t*)ws.host)[5] != 0;
+    // the regular chain skipped the lifting: these tables are not for mgenx_scan_range reuse
+    if (regular_chain) ws.key_s = nullptr;
+    if (pruned && !regular_chain) {
+      // the hypothesis is not the chain (or not provably): exact build, and a backoff
+      ws.prune_backoff = std::min(std::max(2u * ws.prune_backoff, 2u), 64u);
+      ws.prune_skip = ws.prune_backoff;
+      rc = scan_build(ws, s, nbytes, mode, stream, fail, false);
+      if (rc != MGENX_OK) return rc;
+      return scan_walk(ws, s, nbytes, mode, 0, nbytes, rec_off, rec_len, cap, info, stream, fail);
+    }
     if (tot[1] || tot[0] > scap || tot[0] > max_cand) {
       // the tables did not hold the stream: exact build (sizes the next speculation)
       rc = scan_build(ws, s, nbytes, mode, stream, fail, false);
@@ -996,6 +1245,20 @@ extern "C" int mgenx_scan_run(void* wsp, const uint8_t* s, uint64_t nbytes, int 
       return scan_walk(ws, s, nbytes, mode, 0, nbytes, rec_off, rec_len, cap, info, stream, fail);
     }
     ws.n = tot[0];
+    if (pruned) {
+      ws.prune_backoff = 0;
+      // H is the chain from 0; what follows its terminal goes to the sequential resolver
+      // with no candidate set (no lifting tables were built on the pruned set)
+      const uint32_t n_pruned = ws.n;
+      ws.n = 0;
+      const ChainEnd h = {h_end[0], h_end[1], h_end[2]};
+      rc = scan_walk(ws, s, nbytes, mode, 0, nbytes, rec_off, rec_len, cap, info, stream, fail, &h);
+      if (info) {
+        info->candidates = n_pruned;
+        info->path = 2;
+      }
+      return rc;
+    }
     if (ws.n) {
       const ChainEnd h = {h_end[0], h_end[1], h_end[2]};
       // a chain as long as the levels reach (the descent covers 4^levels - 1 jumps) may go
@@ -1006,8 +1269,10 @@ extern "C" int mgenx_scan_run(void* wsp, const uint8_t* s, uint64_t nbytes, int 
         return scan_walk(ws, s, nbytes, mode, 0, nbytes, rec_off, rec_len, cap, info, stream,
                          fail);
       }
-      return scan_walk(ws, s, nbytes, mode, 0, nbytes, rec_off, rec_len, cap, info, stream, fail,
-                       &h);
+      rc = scan_walk(ws, s, nbytes, mode, 0, nbytes, rec_off, rec_len, cap, info, stream, fail,
+                     &h);
+      if (info && regular_chain) info->path = 1;
+      return rc;
     }
   }
   return scan_walk(ws, s, nbytes, mode, 0, nbytes, rec_off, rec_len, cap, info, stream, fail);

@@ -30,6 +30,8 @@ def timed(fn, reps=20):
 
 
 def sweep(name, slab, d_of, d_len, total):
+    """every variant checked against the product rows once, then timed ROUNDS times in
+    interleaved order (A B C A B C ...): the first timings on a box run slow"""
     eng.set_unpack_variant(0)
     eng.unpack(slab, N, rec_off=d_of, rec_len=d_len, cols=rows)
     torch.cuda.synchronize()
@@ -40,9 +42,17 @@ def sweep(name, slab, d_of, d_len, total):
         eng.unpack(slab, N, rec_off=d_of, rec_len=d_len, cols=rows)
         torch.cuda.synchronize()
         same = bool(torch.equal(rows["rows"], ref))
-        ms = timed(lambda: eng.unpack(slab, N, rec_off=d_of, rec_len=d_len, cols=rows))
-        print(f"{name} variant {v:3d}: {ms:.4f} ms ({total / 1e9 / ms:.2f} TB/s) "
-              f"rows {'== product' if same else 'DIFFER'} kernel {eng.last_unpack_kernel()}",
+        print(f"{name} variant {v:3d}: rows {'== product' if same else 'DIFFER'} "
+              f"kernel {eng.last_unpack_kernel()}", flush=True)
+    res = {v: [] for v in VARIANTS}
+    for _ in range(int(os.environ.get("ROUNDS", "5"))):
+        for v in VARIANTS:
+            eng.set_unpack_variant(v)
+            res[v].append(timed(lambda: eng.unpack(slab, N, rec_off=d_of, rec_len=d_len, cols=rows)))
+    for v in VARIANTS:
+        t = sorted(res[v])
+        print(f"{name} variant {v:3d}: median {t[len(t) // 2]:.4f} ms min {t[0]:.4f} "
+              f"({total / 1e9 / t[len(t) // 2]:.2f} TB/s)  all {' '.join(f'{x:.4f}' for x in res[v])}",
               flush=True)
     eng.set_unpack_variant(0)
 

@@ -145,13 +145,20 @@ def test_config5_stream_scan_then_unpack(torch, eng, gold):
     torch.cuda.synchronize()
     assert int((cols["err"] != 0).sum()) == 0
     assert np.array_equal(cols["seq_num"].cpu().numpy().view(np.uint32), np.arange(n))
-    # the same scan into caller-preallocated outputs, twice (speculative tables reused)
+    # the same scan into caller-preallocated outputs, on a fresh engine (the shared one may be
+    # backing off the chain hypothesis after the error streams above): the first call builds
+    # exactly, the next ones take the successor-marked chain
+    from mgen_amd import Engine
+    e2 = Engine(0)
     out = (torch.full((n + 8,), -1, dtype=torch.int64, device="cuda"),
            torch.full((n + 8,), -1, dtype=torch.int32, device="cuda"))
+    e2.stream_scan(d, SCAN_TCP, out=out)
     for _ in range(2):
-        o2, l2, i2 = eng.stream_scan(d, SCAN_TCP, out=out)
+        o2, l2, i2 = e2.stream_scan(d, SCAN_TCP, out=out)
         assert int(i2.n_records) == n and int(i2.consumed) == len(s)
         assert torch.equal(o2, offs) and torch.equal(l2, lens)
+        assert int(i2.path) == 2  # the successor-marked chain (no lifting)
+    e2.close()
 
 
 # ---- sharded framing (mgenx_stream_scan_exits / _range, mgen_amd/shard.py) ----
@@ -287,3 +294,52 @@ def test_scan_beyond_4gib_device_scan_path(torch, eng, gold):
     assert int(info.candidates) >= 2 * len(wo)
     del d
     torch.cuda.empty_cache()
+
+
+# ---- TCP header-copy pruning (speculative whole-stream scans, mgenx_scan.hip kPrune) ----
+
+def test_pruned_scan_tcp_transmit_stream(torch, gold):
+    """The TCP transmit form of 12-KiB and 20-KiB messages (each re-sends its 8-KiB Pack
+    buffer, so headers repeat 8192 bytes on): repeated scans on one engine -- the first exact,
+    the later ones speculative with the copies pruned -- all equal the oracle's framing."""
+    from mgen_amd import Engine, SCAN_TCP, to_device
+    from oracle import oracle as O
+    rng = np.random.default_rng(SEED + 70)
+    s = tcp_stream(gold, rng.choice([12288, 20480, 16384, 900], 600), rng)
+    wo, wl, _, wc, ws = O.tcp_scan(s.tobytes())
+    e = Engine(0)
+    d = to_device(s)
+    cands = []
+    for k in range(3):
+        offs, lens, info = e.stream_scan(d, SCAN_TCP)
+        assert np.array_equal(offs.cpu().numpy(), np.asarray(wo, np.int64)), k
+        assert np.array_equal(lens.cpu().numpy().view(np.uint32), np.asarray(wl, np.uint32))
+        assert (int(info.consumed), int(info.status)) == (wc, ws)
+        cands.append(int(info.path))
+    # the first call builds exactly; calls 2 and 3 take the successor-marked hypothesis
+    assert cands == [0, 2, 2], cands
+    e.close()
+
+
+def test_pruned_scan_falls_back_on_repeated_records(torch, gold):
+    """Records whose first 16 bytes repeat exactly 8192 bytes later (identical 8-KiB records):
+    pruning drops real record starts, the pruned set is not the chain, and the scan rebuilds
+    without pruning -- the framing still equals the oracle's, on every call."""
+    from mgen_amd import Engine, SCAN_TCP, to_device
+    from oracle import oracle as O
+    rng = np.random.default_rng(SEED + 71)
+    one = tcp_stream(gold, np.array([8192]), rng)
+    s = np.concatenate([tcp_stream(gold, np.array([5000]), rng)] + [one] * 40 +
+                       [tcp_stream(gold, np.array([3000, 700]), rng)])
+    wo, wl, _, wc, ws = O.tcp_scan(s.tobytes())
+    e = Engine(0)
+    d = to_device(s)
+    paths = []
+    for k in range(3):
+        offs, lens, info = e.stream_scan(d, SCAN_TCP)
+        assert np.array_equal(offs.cpu().numpy(), np.asarray(wo, np.int64)), k
+        assert (int(info.consumed), int(info.status)) == (wc, ws)
+        paths.append(int(info.path))
+    # the hypothesis failed on call 2 (exact rebuild, path 0) and backs off on call 3
+    assert paths[:2] == [0, 0] and paths[2] != 2, paths
+    e.close()
