@@ -189,9 +189,12 @@ def load_traffic():
         return None, None
 
 
-def timed(torch, fn, reps=10):
-    """Mean time (ms) of fn() on the current stream, HIP events around reps calls."""
-    fn()
+def timed(torch, fn, reps=10, warm=3):
+    """Mean time (ms) of fn() on the current stream, HIP events around reps calls, after
+    `warm` untimed calls (an extra follows host-side input generation that leaves the GPU
+    idle; its first launches run slow -- scripts/var_shapes.py's interleaved rounds show it)."""
+    for _ in range(warm):
+        fn()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
     for _ in range(reps):
