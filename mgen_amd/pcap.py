@@ -45,6 +45,8 @@ class Pcap2Mgen:
     """pcap2mgen with its options; ``run(file)`` returns the log bytes.  Everything after the
     host index walk runs on the engine's GPU."""
 
+    FIRST_FLOWS = 65536  # flow-table capacity tried first (see run_device)
+
     def __init__(self, engine: Engine, analytics: bool = False, log_rx: bool = True,
                  window: float = 1.0, epoch: bool = False):
         self.eng = engine
@@ -89,10 +91,24 @@ class Pcap2Mgen:
         sources = []
         keep = []
         if self.analytics:
-            table = eng.flow_table(max(n, 1))
+            # a table for up to FIRST_FLOWS flows first (a table for n flows is 64 x 2n bytes to
+            # allocate, clear and free on every run); if it overflowed -- a record of a good
+            # message left without a flow -- the lookup is redone on a table for n flows
+            cap_flows = min(max(n, 1), self.FIRST_FLOWS)
+            table = eng.flow_table(cap_flows)
             try:
                 flow_idx, nfl = eng.flow_lookup(table, cols, p["src"], n)
-                n_flows = int(nfl.item())
+                if cap_flows < n:
+                    lost = ((flow_idx[:n] < 0) & (cols["err"][:n] == 0)).any()
+                    st = torch.stack([nfl[0].to(torch.int64), lost.to(torch.int64)]).cpu()
+                    n_flows, overflow = int(st[0]), bool(st[1])
+                else:
+                    n_flows, overflow = int(nfl.item()), False
+                if overflow:
+                    eng.flow_table_destroy(table)
+                    table = eng.flow_table(max(n, 1))
+                    flow_idx, nfl = eng.flow_lookup(table, cols, p["src"], n)
+                    n_flows = int(nfl.item())
                 if n_flows:
                     per_flow = self._per_flow(p, flow_idx, n, n_flows)
                     flows = eng.flow_init(n_flows, self.window)
