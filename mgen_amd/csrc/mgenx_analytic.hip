@@ -1030,11 +1030,10 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
     }
     // LDS: per-wave counts, bases, the sorted tile (index + 16-bit flow)
     const uint32_t lds = (kSortWaves * bins + bins) * 4u + kTile * 4u;
-    static bool lds_set = false;
-    if (!lds_set) {
-      (void)hipFuncSetAttribute((const void*)flow_order_kernel,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 256);
-      lds_set = true;
+    e = set_max_lds((const void*)flow_order_kernel, 160 * 1024 - 256);
+    if (e != hipSuccess) {
+      snprintf(err, errn, "flow_reduce order: %s", hipGetErrorString(e));
+      return MGENX_EDEVICE;
     }
     const uint32_t grid = 8u * ((n_tiles + 7u) / 8u);
     hipLaunchKernelGGL(flow_order_kernel, dim3(grid), dim3(64 * kSortWaves), lds, stream,

@@ -116,10 +116,17 @@ __device__ __forceinline__ bool key_eq(const FlowKey& a, const FlowSlot& s) {
   return eq;
 }
 
+// Probes per lookup are bounded, and a table takes at most half its slots in keys (its
+// max_flows, rounded up): past that a new key counts as overflow (MGENX_FLOW_NONE) instead of
+// filling the table, whose probe runs would then grow towards the whole table per record.  At
+// load <= 1/2 linear probing's runs stay far below the bound.
+constexpr uint32_t kMaxProbe = 1024;
+
 __global__ void flowtab_insert_kernel(FlowSlot* __restrict__ tab, uint32_t cap_mask, mgenx_cols c,
                                       const mgenx_addr* __restrict__ src, uint32_t n,
                                       uint32_t* __restrict__ rec_slot, uint32_t* __restrict__ overflow,
-                                      uint32_t* __restrict__ flow_idx, uint32_t* __restrict__ n_new) {
+                                      uint32_t* __restrict__ flow_idx, uint32_t* __restrict__ n_new,
+                                      const uint32_t* __restrict__ n_flows_before) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t err = c.rows ? c.rows[i].err : (c.err ? c.err[i] : 0u);
@@ -136,7 +143,8 @@ __global__ void flowtab_insert_kernel(FlowSlot* __restrict__ tab, uint32_t cap_m
   //    its state is released, so a stale view of the line is at worst "not there yet" -- the
   //    atomic path below then decides.  (Acquire loads here would invalidate the caches on
   //    every probe.)
-  for (uint32_t probe = 0, s0 = s; probe <= cap_mask; probe++, s0 = (s0 + 1) & cap_mask) {
+  const uint32_t max_probe = min(cap_mask + 1u, kMaxProbe);
+  for (uint32_t probe = 0, s0 = s; probe < max_probe; probe++, s0 = (s0 + 1) & cap_mask) {
     const u32x4_t* q = reinterpret_cast<const u32x4_t*>(tab + s0);
     const u32x4_t q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
     if (q3.x == kSlotEmpty || q3.x == kSlotBusy) break;
@@ -152,10 +160,17 @@ __global__ void flowtab_insert_kernel(FlowSlot* __restrict__ tab, uint32_t cap_m
       break;
     }
   }
-  for (uint32_t probe = 0; probe <= cap_mask; probe++, s = (s + 1) & cap_mask) {
+  for (uint32_t probe = 0; probe < max_probe; probe++, s = (s + 1) & cap_mask) {
     FlowSlot& sl = tab[s];
     uint32_t st = __hip_atomic_load(&sl.state, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
     if (st == kSlotEmpty) {
+      // the key is not in the table: a new key, if the table has room for one (reserved in
+      // n_new before the claim, released again when another thread claims the slot first)
+      const uint32_t r = __hip_atomic_fetch_add(n_new, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (*n_flows_before + r >= (cap_mask + 1u) / 2u) {
+        __hip_atomic_fetch_sub(n_new, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
       uint32_t exp = kSlotEmpty;
       if (__hip_atomic_compare_exchange_strong(&sl.state, &exp, kSlotBusy, __ATOMIC_ACQ_REL,
                                                __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) {
@@ -166,10 +181,10 @@ __global__ void flowtab_insert_kernel(FlowSlot* __restrict__ tab, uint32_t cap_m
         __hip_atomic_store(&sl.is_new, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&sl.index, kSlotBusy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&sl.state, 1u + s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add(n_new, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         rec_slot[i] = s;
         return;
       }
+      __hip_atomic_fetch_sub(n_new, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       st = exp;
     }
     // a slot being written: wait (bounded) until its key is published
@@ -403,7 +418,7 @@ int mgenx_flow_lookup(mgenx_ctx* ctx, mgenx_flow_table* t, const mgenx_cols* col
   const dim3 g((n + 255) / 256), b(256), gk(nblk), bk(kFtBlock);
   if (hipMemsetAsync(n_new, 0, 4, s) != hipSuccess) return MGENX_EDEVICE;
   hipLaunchKernelGGL(flowtab_insert_kernel, g, b, 0, s, t->slots, t->cap - 1, c, dev_src, n,
-                     rec_slot, t->counters + 2, dev_flow_idx, n_new);
+                     rec_slot, t->counters + 2, dev_flow_idx, n_new, t->counters);
   hipLaunchKernelGGL(flowtab_first_kernel, gk, bk, 0, s, t->slots, rec_slot, n, flag, blk_cnt,
                      n_new);
   hipLaunchKernelGGL(flowtab_offsets_kernel, dim3(1), dim3(1024), 0, s, blk_cnt, nblk, blk_base,

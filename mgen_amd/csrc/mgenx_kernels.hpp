@@ -3,11 +3,31 @@
 
 #include "mgenx_common.hpp"
 
+#include <mutex>
+#include <set>
+#include <utility>
+
 #ifndef MGENX_DIAG
 #define MGENX_DIAG 0
 #endif
 
 namespace mgenx {
+
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device): the attribute is
+// per device, and threaded multi-GPU callers (mgenx::ShardedScan) launch concurrently, so the
+// "done" record is per device and guarded (every entry point sets its context's device first)
+inline hipError_t set_max_lds(const void* fn, int bytes) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  static std::mutex mu;
+  static std::set<std::pair<const void*, int>> done;
+  std::lock_guard<std::mutex> g(mu);
+  if (done.count({fn, dev})) return hipSuccess;
+  e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  if (e == hipSuccess) done.insert({fn, dev});
+  return e;
+}
 
 struct UnpackParams {
   const uint8_t* slab;

@@ -992,14 +992,8 @@ int scan_build(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, int mode, h
                      nbytes, m, d_slots, d_counts, (const uint64_t*)nullptr, (uint64_t*)nullptr,
                      spec && ws.spec_cap ? irregular : (uint32_t*)nullptr);
   if (nb <= kScanSmall) {
-    static bool lds_set = false;
-    if (!lds_set) {
-      if ((e = hipFuncSetAttribute((const void*)scan_offsets_kernel,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kOffLds)) !=
-          hipSuccess)
-        return fail(e, "scan offsets");
-      lds_set = true;
-    }
+    if ((e = set_max_lds((const void*)scan_offsets_kernel, (int)kOffLds)) != hipSuccess)
+      return fail(e, "scan offsets");
     hipLaunchKernelGGL(scan_offsets_kernel, dim3(1), dim3(1024), kOffLds, stream, d_counts, nb,
                        d_base, ws.host_dev);
   } else {

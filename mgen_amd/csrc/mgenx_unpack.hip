@@ -1821,35 +1821,22 @@ unpack_fixed_ring_kernel(UnpackParams p, uint32_t expect) {
 }
 
 template <typename K>
-static hipError_t launch_lds(K kernel, bool& attr_done, const UnpackParams& p, int grid,
-                             hipStream_t stream) {
-  if (!attr_done) {
-    hipError_t e = hipFuncSetAttribute((const void*)kernel,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)kUnpackLdsBytes);
-    if (e != hipSuccess) return e;
-    attr_done = true;
-  }
+static hipError_t launch_lds(K kernel, const UnpackParams& p, int grid, hipStream_t stream) {
+  hipError_t e = set_max_lds((const void*)kernel, (int)kUnpackLdsBytes);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kernel, dim3(grid), dim3(kUnpackThreads), kUnpackLdsBytes, stream, p);
   return hipGetLastError();
 }
 
 template <int MODE>
 static hipError_t launch_mode(const UnpackParams& p, int grid, hipStream_t stream) {
-  static bool attr_done = false;
-  return launch_lds(unpack_kernel<true, MODE>, attr_done, p, grid, stream);
+  return launch_lds(unpack_kernel<true, MODE>, p, grid, stream);
 }
 
 template <int NT = kUnpackThreads, int KB = 4, int MODE = 0>
 static hipError_t launch_var(const UnpackParams& p, int grid, hipStream_t stream) {
-  static bool attr_done = false;
-  if (!attr_done) {
-    hipError_t e = hipFuncSetAttribute((const void*)unpack_var_kernel<NT, KB, MODE>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)kUnpackLdsBytes);
-    if (e != hipSuccess) return e;
-    attr_done = true;
-  }
+  hipError_t e = set_max_lds((const void*)unpack_var_kernel<NT, KB, MODE>, (int)kUnpackLdsBytes);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL((unpack_var_kernel<NT, KB, MODE>), dim3(grid), dim3(NT), kUnpackLdsBytes,
                      stream, p);
   return hipGetLastError();
@@ -1857,21 +1844,14 @@ static hipError_t launch_var(const UnpackParams& p, int grid, hipStream_t stream
 
 #if MGENX_DIAG
 static hipError_t launch_sorted(const UnpackParams& p, int grid, hipStream_t stream) {
-  static bool attr_done = false;
-  return launch_lds(unpack_kernel<true, 0, true>, attr_done, p, grid, stream);
+  return launch_lds(unpack_kernel<true, 0, true>, p, grid, stream);
 }
 #endif
 
 template <int NR, int MODE = 0, bool kRows = false, bool kAligned = false>
 static hipError_t launch_fixed(const UnpackParams& p, int grid, hipStream_t stream) {
-  static bool attr_done = false;
-  if (!attr_done) {
-    hipError_t e = hipFuncSetAttribute((const void*)unpack_fixed_kernel<NR, MODE, kRows, kAligned>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)kUnpackLdsBytes);
-    if (e != hipSuccess) return e;
-    attr_done = true;
-  }
+  hipError_t e = set_max_lds((const void*)unpack_fixed_kernel<NR, MODE, kRows, kAligned>, (int)kUnpackLdsBytes);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL((unpack_fixed_kernel<NR, MODE, kRows, kAligned>), dim3(grid),
                      dim3(kUnpackThreads), kUnpackLdsBytes, stream, p, p.expect_fixed);
   return hipGetLastError();
@@ -1879,14 +1859,8 @@ static hipError_t launch_fixed(const UnpackParams& p, int grid, hipStream_t stre
 
 template <int NR, int RS = 4, int K = 16>
 static hipError_t launch_ring(const UnpackParams& p, int grid, hipStream_t stream) {
-  static bool attr_done = false;
-  if (!attr_done) {
-    hipError_t e = hipFuncSetAttribute((const void*)unpack_fixed_ring_kernel<NR, RS, K>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)kUnpackLdsBytes);
-    if (e != hipSuccess) return e;
-    attr_done = true;
-  }
+  hipError_t e = set_max_lds((const void*)unpack_fixed_ring_kernel<NR, RS, K>, (int)kUnpackLdsBytes);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL((unpack_fixed_ring_kernel<NR, RS, K>), dim3(grid), dim3(kUnpackThreads),
                      kUnpackLdsBytes, stream, p, p.expect_fixed);
   return hipGetLastError();

@@ -106,6 +106,7 @@ class Pcap2Mgen:
                     n_flows, overflow = int(nfl.item()), False
                 if overflow:
                     eng.flow_table_destroy(table)
+                    table = None    # a failing create below must not free it again
                     table = eng.flow_table(max(n, 1))
                     flow_idx, nfl = eng.flow_lookup(table, cols, p["src"], n)
                     n_flows = int(nfl.item())
@@ -129,7 +130,8 @@ class Pcap2Mgen:
                     sources.append((TEXT_SCATTER, rtext, rline, n_flows * per_flow, rep_rec, 1))
                     keep += [reports, count, rep_rec, items]
             finally:
-                eng.flow_table_destroy(table)
+                if table is not None:
+                    eng.flow_table_destroy(table)
         if self.log_rx:  # LogRecvEvent(..., logData false, logGpsData true, ttl, hdr.ts)
             text, line_off = eng.log_recv_text(buf, n, cols, p["src"], p["rx_sec"],
                                                p["rx_usec"], rec_off=p["udp_off"], ttl=p["ttl"],

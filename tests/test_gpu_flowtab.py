@@ -124,3 +124,39 @@ def test_flow_lookup_from_rows(torch, eng):
     finally:
         for t in (want_tab, t_rows, t_both):
             eng.flow_table_destroy(t)
+
+
+def test_flow_lookup_undersized_table_is_bounded(torch, eng):
+    """More distinct keys than a table holds: a table for 64 flows (128 slots)
+    takes 64 keys and maps the rest to MGENX_FLOW_NONE, promptly -- no record walks the whole
+    table -- and the keys it took keep their indices in a second call."""
+    import time
+    n, n_keys = 400_000, 150_000       # more than 2 x pcap2mgen's first table (65,536 flows)
+    fid = (np.arange(n) % n_keys + 1).astype(np.uint32)
+    src = np.zeros((n, 20), np.uint8)
+    src[:, 0], src[:, 1], src[:, 4] = 1, 4, 10
+    d = {"dst_addr": np.tile(np.array([127, 0, 0, 1] + [0] * 12, np.uint8), n),
+         "dst_len": np.full(n, 4, np.uint8), "dst_port": np.full(n, 5000, np.int16),
+         "flow_id": fid.view(np.int32), "err": np.zeros(n, np.uint8)}
+    cols = {k: torch.from_numpy(v.copy()).cuda() for k, v in d.items()}
+    s = torch.from_numpy(src.reshape(-1).copy()).cuda()
+    table = eng.flow_table(64)
+    try:
+        eng.flow_lookup(table, cols, s, n)       # warm
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        idx, nf = eng.flow_lookup(table, cols, s, n)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        got = idx.cpu().numpy().view(np.uint32)
+        held = got != 0xFFFFFFFF
+        k = int(nf.cpu()[0])
+        assert 0 < k <= 64
+        assert len(np.unique(fid[held])) == k and got[held].max() == k - 1
+        # every record of a held key resolves to that key's index
+        first = {}
+        for f, k in zip(fid[held], got[held]):
+            assert first.setdefault(int(f), int(k)) == int(k)
+        assert dt < 0.05, dt
+    finally:
+        eng.flow_table_destroy(table)

@@ -169,3 +169,47 @@ def test_cli_command_errors():
                       (["infile", "/nonexistent/x.pcap"], b"error opening input file")]:
         r = subprocess.run([exe] + args, capture_output=True, timeout=60, input=b"")
         assert r.returncode != 0 and msg in r.stderr, (args, r.stderr)
+
+
+def test_overflow_redo_create_failure_frees_once():
+    """run_device's flow-table redo: when the full-size table cannot be created,
+    the first table is freed once -- not again by the cleanup.  A stand-in engine on CPU tensors
+    drives the host logic up to the failing create."""
+    import torch
+    from mgen_amd.pcap import Pcap2Mgen
+
+    n = 8
+    freed, made = [], []
+
+    class FakeEngine:
+        device = 0
+
+        def __init__(self):
+            self.torch = torch
+
+        def pcap_parse(self, buf, pkt_off, n_, link_type, flags):
+            z = torch.zeros(n_, dtype=torch.int64)
+            return {"udp_off": z, "udp_len": z, "src": z, "rx_sec": z, "rx_usec": z, "ttl": z}
+
+        def unpack(self, buf, n_, **kw):
+            return {"err": torch.zeros(n_, dtype=torch.uint8)}
+
+        def flow_table(self, cap):
+            if made:
+                raise MemoryError("second table")
+            made.append(cap)
+            return "table0"
+
+        def flow_lookup(self, table, cols, src, n_):
+            # every record lost: the first table overflowed
+            return torch.full((n_,), -1, dtype=torch.int32), torch.zeros(1, dtype=torch.int32)
+
+        def flow_table_destroy(self, table):
+            freed.append(table)
+
+    p = Pcap2Mgen(FakeEngine(), analytics=True)
+    p.FIRST_FLOWS = 2
+    with pytest.raises(MemoryError):
+        p.run_device(torch.zeros(16, dtype=torch.uint8), torch.zeros(n, dtype=torch.int64), n,
+                     1, 0)
+    assert made == [2] and freed == ["table0"]
