@@ -223,11 +223,14 @@ struct WRing {
   }
 };
 
-// One received record as the update kernel reads it (24 B, written in input order, read
-// through `order`); the latency ProtoTime::Delta(rx, tx) depends on the record alone, so it
-// is computed when the record is written, off the per-flow chain.
+// One received record as the update kernel reads it: 24 B, written flow-sorted by the ordering
+// step, so the update streams its flow's records instead of gathering them.  The receive time
+// is one 64-bit key, sec << 32 | usec (ProtoTime's >= is the key's >=); the latency
+// ProtoTime::Delta(rx, tx) depends on the record alone, so it is computed there, off the
+// per-flow chain.
 struct FRec {
-  uint32_t seq, rxs, rxu, len;
+  uint64_t rxk;
+  uint32_t seq, len;
   double latency;
 };
 
@@ -253,12 +256,11 @@ __device__ __forceinline__ FRec make_frec(const RecSrc& src, uint32_t i) {
     tu = src.txu[i];
     r.len = src.len[i];
   }
-  r.rxs = src.rxs[i];
-  r.rxu = src.rxu[i];
-  r.latency = tdelta(Tm{(int64_t)r.rxs, (int64_t)r.rxu}, Tm{(int64_t)ts, (int64_t)tu});
+  const uint32_t rs = src.rxs[i], ru = src.rxu[i];
+  r.rxk = (uint64_t)rs << 32 | ru;
+  r.latency = tdelta(Tm{(int64_t)rs, (int64_t)ru}, Tm{(int64_t)ts, (int64_t)tu});
   return r;
 }
-
 
 // Wave-uniform values: the window times come out of FP64 arithmetic (VALU), so without
 // these the compiler treats every later compare and branch on them as divergent.
@@ -268,21 +270,65 @@ __device__ __forceinline__ int64_t uni64(int64_t v) {
   return (int64_t)((uint64_t)hi << 32 | lo);
 }
 __device__ __forceinline__ Tm uni_t(Tm t) { return Tm{uni64(t.sec), uni64(t.usec)}; }
+// the window end as a receive-time key (usec < 10^6 after tadd); an end past the 32-bit seconds
+// range gets the largest key, which only sends records to the exact path (it compares times)
+__device__ __forceinline__ uint64_t tkey(Tm t) {
+  return t.sec > 0xFFFFFFFFll ? ~0ull : ((uint64_t)t.sec << 32 | (uint64_t)t.usec);
+}
 
+// What the latency-sum pass (flow_chain_kernel) needs from the update, per flow and call ...
+struct FlowBatch {
+  uint32_t rc0;         // report_count on entry
+  uint32_t ncl;         // windows closed in this call
+  uint32_t last_close;  // sorted position of the last closing record
+  uint32_t last_zr;     // it restarted the sum at 0.0 instead of at its own latency (below)
+  double lsum0;         // latency_sum on entry
+  uint64_t rsv;
+};
+// ... and per kept report closed in this call
+struct CloseRec {
+  uint32_t pos, zr;     // the closing record (sorted position); zero restart
+  uint64_t mc;          // msg_count at the close: latency_ave's divisor
+};
 
+// ---- MgenAnalytic::Update, one WAVE per flow (mgenAnalytic.cpp:74-258) ----
+// The latency sum is the one FP64 chain whose rounding depends on record order; everything
+// else here is integer bookkeeping and order-free min / max.  So the update walks its flow's
+// records 256 at a time (4 per lane, coalesced) and leaves the sum to flow_chain_kernel: each
+// record's contribution to latency_sum ("lat'": its latency when Update adds or assigns it, else
+// 0.0) goes to lat2[], the closing records and the window msg_counts to CloseRec.  Since
+// latency_sum is 0.0 whenever msg_count is 0, every assignment of a latency to it is an add to
+// 0.0 (exact), and a window's sum is the in-order sum of its records' lat' values -- a window
+// restarts at its closing record's lat' (0.0 for the closing "first actual message" of
+// :165-173, whose local `latency` stays 0.0).
+//
+// Bulk runs: from the current state, a record is "simple" when it does not reach the window end
+// and, if msg != 0, lies inside the mask span (0 <= seq - first < 1024: Set takes its in-span
+// branch and never clears, `first` does not move).  A run of simple records changes the state in
+// closed form: a record is a duplicate when its ring bit is set or an earlier record of the run
+// has its sequence number (an LDS scatter finds clashes; then an LDS table of first positions
+// orders them), else it sets its bit; those at or past seq_start are counted.  Counts move by
+// ballots, bytes / min / max / last by per-lane partials folded before an exact step (flush).
+// The first non-simple record (window end, mask restart, a record below `first`, an empty mask,
+// the first record of a flow) takes the exact update below, and the run restarts after it.
+constexpr uint32_t kUR = 4;             // records per lane and round
+constexpr uint32_t kRound = 64u * kUR;  // records per round
 
 __global__ void __launch_bounds__(256)
-flow_update_wave_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
-                        const uint32_t* __restrict__ bnd, uint32_t bstride,
-                        const uint32_t* __restrict__ order, const FRec* __restrict__ recs,
-                        mgenx_flow_report* __restrict__ reports, uint32_t per_flow,
-                        uint32_t* __restrict__ report_count, uint32_t* __restrict__ report_rec,
-                        int abl) {
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t f = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
+                   const uint32_t* __restrict__ bnd, uint32_t bstride, const FRec* __restrict__ recs,
+                   const uint32_t* __restrict__ order, double* __restrict__ lat2,
+                   mgenx_flow_report* __restrict__ reports, uint32_t per_flow,
+                   uint32_t* __restrict__ report_count, uint32_t* __restrict__ report_rec,
+                   CloseRec* __restrict__ closes, FlowBatch* __restrict__ fbatch) {
+  __shared__ uint32_t scat[4][32];
+  __shared__ uint32_t fo[4][1024];
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint32_t f = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + wv);
   if (f >= n_flows) return;
   const uint32_t b = bnd[(size_t)f * bstride], e = bnd[(size_t)(f + 1u) * bstride];
   if (b >= e) return;
+  for (uint32_t j = lane; j < 1024u; j += 64u) fo[wv][j] = 0xFFFFFFFFu;
   mgenx_flow_state* sp = flows + f;
   const double window = sp->window_size;
   WRing m;
@@ -293,32 +339,37 @@ flow_update_wave_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
   if (!m.n) m.w = 0;
   bool valid = sp->window_valid != 0;
   Tm ws = {sp->win_start_sec, sp->win_start_usec}, we = {sp->win_end_sec, sp->win_end_usec};
+  uint64_t wek = tkey(we);
   uint32_t seq_start = sp->seq_start;
   uint64_t msg_count = sp->msg_count, byte_count = sp->byte_count, dups = sp->dup_count;
-  double lsum = sp->latency_sum, lmin = sp->latency_min, lmax = sp->latency_max;
+  double lmin = sp->latency_min, lmax = sp->latency_max;
   uint64_t nrep = sp->n_reports;
-  uint32_t rcount = report_count[f];
+  const double lsum0 = sp->latency_sum;
+  const uint32_t rc0 = report_count[f];
+  uint32_t rcount = rc0, ncl = 0, last_close = 0, last_zr = 0;
 
-  auto update = [&](uint32_t seq, uint32_t rxs, uint32_t rxu, uint32_t msg, double lat,
-                    uint32_t rec) {
-    const Tm rx = {(int64_t)rxs, (int64_t)rxu};
+  // the exact Update of one record (arguments wave-uniform); returns the record's lat'
+  auto update = [&](uint32_t seq, uint64_t rxk, uint32_t msg, double lat, uint32_t pos) -> double {
+    const Tm rx = {(int64_t)(rxk >> 32), (int64_t)(uint32_t)rxk};
     if (!valid) {  // mgenAnalytic.cpp:80-99
       valid = true;
       ws = rx;
       we = uni_t(tadd(rx, window));
+      wek = tkey(we);
       if (msg != 0) {
         m.set(seq);
         seq_start = seq;
         msg_count = 1;
         byte_count = msg;
-        lsum = lmin = lmax = lat;
-      } else {
-        msg_count = byte_count = 0;
-        lsum = lmin = lmax = 0.0;
+        lmin = lmax = lat;
+        return lat;
       }
-      return;
+      msg_count = byte_count = 0;
+      lmin = lmax = 0.0;
+      return 0.0;
     }
-    double latency = 0.0;
+    double latency = 0.0, contrib = 0.0;
+    uint32_t zr = 0;
     if (msg != 0) {  // :102-178
       if (m.n) {
         if (m.test(seq)) {
@@ -332,12 +383,10 @@ flow_update_wave_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
           }
           if (1 == msg_count) byte_count = msg;
           else byte_count += msg;
-          latency = lat;
+          latency = contrib = lat;
           if (0 == msg_count) {
-            lsum = lmin = lmax = latency;
+            lmin = lmax = latency;
           } else {
-            lsum = __dadd_rn(lsum, latency);
-            // if (latency < lmin) lmin = latency; else if (latency > lmax) lmax = latency;
             // as value selects (a branch here lets LLVM fold the two stores into one store
             // through a selected pointer, which sends lmin/lmax to scratch memory)
             const bool lo = latency < lmin;
@@ -347,30 +396,31 @@ flow_update_wave_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
           }
           msg_count++;
         }
-      } else {
+      } else {  // the first actual message (:165-173): sets the sum, `latency` stays 0.0
         m.clear();
         m.set(seq);
         seq_start = seq;
         byte_count = msg;
-        lsum = lmin = lmax = lat;
+        lmin = lmax = lat;
         msg_count = 1;
+        contrib = lat;
+        zr = 1;
       }
     }
     if (tge(rx, we)) {  // :180-256: report and restart the window
       const uint32_t seq_max = m.n ? m.get_last() : seq_start;
       const double duration = tdelta(rx, ws);
       uint64_t r_count;
-      double r_rate, r_loss, r_ave, r_min, r_max;
+      double r_rate, r_loss, r_min, r_max;
       if (msg_count == 0) {
         r_count = 0;
         r_rate = 0.0;
         r_loss = 1.0;
-        r_ave = r_min = r_max = -1.0;
+        r_min = r_max = -1.0;
       } else if (msg_count == 1) {
         r_count = 1;
         r_rate = __ddiv_rn((double)byte_count, duration);
         r_loss = 0.0;
-        r_ave = lsum;
         r_min = lmin;
         r_max = lmax;
       } else {
@@ -379,12 +429,12 @@ flow_update_wave_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
         const uint32_t delta = seq_max - seq_start;
         r_loss = delta <= 1 ? 0.0
                             : __dsub_rn(1.0, __ddiv_rn((double)msg_count, (double)(delta + 1)));
-        r_ave = __ddiv_rn(lsum, (double)msg_count);
         r_min = lmin;
         r_max = lmax;
       }
-      if (rcount < per_flow && lane == 0) {
-        mgenx_flow_report* rp = reports + (size_t)f * per_flow + rcount;
+      if (rcount < per_flow && lane == 0) {  // latency_ave: flow_chain_kernel
+        const size_t slot = (size_t)f * per_flow + rcount;
+        mgenx_flow_report* rp = reports + slot;
         rp->flow = f;
         rp->index = rcount;
         rp->start_sec = ws.sec;
@@ -393,48 +443,46 @@ flow_update_wave_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
         rp->msg_count = r_count;
         rp->rate = r_rate;
         rp->loss = r_loss;
-        rp->latency_ave = r_ave;
         rp->latency_min = r_min;
         rp->latency_max = r_max;
         rp->rx_sec = rx.sec;
         rp->rx_usec = rx.usec;
-        if (report_rec) report_rec[(size_t)f * per_flow + rcount] = rec;
+        CloseRec c;
+        c.pos = pos;
+        c.zr = zr;
+        c.mc = msg_count;
+        closes[slot] = c;
+        if (report_rec) report_rec[slot] = order[pos];
       }
       rcount++;
       nrep++;
+      ncl++;
+      last_close = pos;
+      last_zr = zr;
       ws = rx;
       we = uni_t(tadd(rx, window));
+      wek = tkey(we);
       seq_start = seq_max;
       if (msg != 0) {
         byte_count = 0;
         msg_count = 1;
-        lsum = lmin = lmax = latency;
+        lmin = lmax = latency;
       } else {
         byte_count = msg_count = 0;
-        lsum = lmin = lmax = 0.0;
+        lmin = lmax = 0.0;
       }
     }
+    return contrib;
   };
 
-  // Fast segments: a run of records that are all "plain" -- msg != 0, not duplicates (their
-  // bit is clear in the mask and no earlier record of the run has the same seq), within the
-  // mask span without a restart (0 <= seq - first < 1024, so Set takes its d >= 0 branch and
-  // never clears), not below seq_start, and before the window end -- changes the state in
-  // closed form: their bits are OR-ed into the ring, n/last advance, the integer counters
-  // add, and only the FP64 latency sum/min/max is walked record by record (in order:
-  // bit-exact).  Late (reordered) arrivals qualify.  Anything else -- duplicates, mask
-  // restarts, window ends, seq below seq_start, msg == 0 -- takes the general update above.
-  __shared__ uint32_t scat[4][32];
-  __shared__ alignas(16) double latl[4][64];
-  // Deferred, order-free parts of the fast runs, per lane: latency min / max, bytes, and the
-  // highest seq - first (for `last`).  Folded into the wave-uniform state by flush() only
-  // before a general update and at the end -- not after every run (no wave reductions on
-  // the per-run path).  `first` does not move between flushes (runs never take Set's d < 0
-  // branch), and msg_count == 1 at a run's start only right after a general update, so the
-  // byte restart of :128-129 sees nothing pending.
+  // Per-lane partials of the bulk runs, folded into the wave-uniform state by flush() before
+  // every exact update and at the end: latency min / max, bytes, and the highest seq - first
+  // (for `last`).  msg_count == 1 (the byte restart of :128-129) and msg_count == 0 (min / max
+  // set by the first counted latency, :132-133) arise only from an exact update, which flushes
+  // first, so at those points nothing is pending.
   const double inf = __builtin_huge_val();
   double pmin = inf, pmax = -inf;
-  uint32_t pbytes = 0, pdmax = 0, pruns = 0;
+  uint32_t pbytes = 0, pdmax = 0, prounds = 0;
   bool dirty = false;
   auto flush = [&]() {
     if (!dirty) return;
@@ -447,173 +495,151 @@ flow_update_wave_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
     m.last = m.first + max(WRing::wave_max(pdmax), m.last - m.first);
     pmin = inf;
     pmax = -inf;
-    pbytes = pdmax = pruns = 0;
+    pbytes = pdmax = prounds = 0;
     dirty = false;
   };
-  const uint32_t wv = threadIdx.x >> 6;
-  // trial: the run's bits into a zeroed LDS copy of the ring; true when two records of the
-  // run share a seq (a duplicate inside the run -- then the run is recomputed exactly)
-  auto scatter = [&](const FRec& r, uint32_t k, uint32_t e) -> bool {
+
+  FRec cur[kUR], nxt[kUR];
+  double latp[kUR];
+  auto ld = [&](uint32_t base, FRec (&r)[kUR]) {  // clamped: lanes past the flow reload its last
+#pragma unroll
+    for (uint32_t q = 0; q < kUR; q++) r[q] = recs[min(base + 64u * q + lane, e - 1u)];
+  };
+
+  // records [k, ev) of the round: a bulk run (every one simple, valid && m.n)
+  auto bulk = [&](uint32_t k, uint32_t ev) {
     if (lane < 32u) scat[wv][lane] = 0u;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    bool clash = false;
-    if (lane >= k && lane < e) {
-      const uint32_t bit = 1u << (r.seq & 31u);
-      clash = (atomicOr(&scat[wv][(r.seq >> 5) & 31u], bit) & bit) != 0u;
+    bool cand[kUR], inring[kUR], clash = false;
+#pragma unroll
+    for (uint32_t q = 0; q < kUR; q++) {
+      const uint32_t p = 64u * q + lane, s = cur[q].seq;
+      cand[q] = p >= k && p < ev && cur[q].len != 0u;
+      const uint32_t word = (uint32_t)__shfl((int)m.w, (int)((s >> 5) & 31u));
+      inring[q] = (word >> (s & 31u)) & 1u;
+      if (cand[q]) {
+        const uint32_t bit = 1u << (s & 31u);
+        clash |= (atomicOr(&scat[wv][(s >> 5) & 31u], bit) & bit) != 0u;
+      }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    return __ballot(clash) != 0ull;
-  };
-  auto commit = [&](const FRec& r, uint32_t k, uint32_t e, uint32_t llo, uint32_t lhi) {
-    const bool in = lane >= k && lane < e;
+    bool indup[kUR];
+#pragma unroll
+    for (uint32_t q = 0; q < kUR; q++) indup[q] = false;
+    if (__ballot(clash)) {  // two records of the run share a sequence number: the first is new
+#pragma unroll
+      for (uint32_t q = 0; q < kUR; q++)
+        if (cand[q]) atomicMin(&fo[wv][cur[q].seq & 1023u], 64u * q + lane);
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (uint32_t q = 0; q < kUR; q++)
+        indup[q] = cand[q] && fo[wv][cur[q].seq & 1023u] < 64u * q + lane;
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (uint32_t q = 0; q < kUR; q++)
+        if (cand[q]) fo[wv][cur[q].seq & 1023u] = 0xFFFFFFFFu;
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
+    uint32_t n_cnt = 0, n_dup = 0, n_new = 0, len1 = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kUR; q++) {
+      const bool dup = cand[q] && (inring[q] || indup[q]);
+      const bool nw = cand[q] && !dup;
+      const bool counted = nw && (int32_t)(cur[q].seq - seq_start) >= 0;
+      const uint64_t cm = __ballot(counted);
+      if (cm && n_cnt == 0)  // the run's first counted record: its size
+        len1 = (uint32_t)__builtin_amdgcn_readlane((int)cur[q].len, (int)__builtin_ctzll(cm));
+      n_cnt += (uint32_t)__popcll(cm);
+      n_dup += (uint32_t)__popcll(__ballot(dup));
+      n_new += (uint32_t)__popcll(__ballot(nw));
+      const double lat = cur[q].latency;
+      pbytes += counted ? cur[q].len : 0u;
+      pmin = counted ? __builtin_fmin(pmin, lat) : pmin;
+      pmax = counted ? __builtin_fmax(pmax, lat) : pmax;
+      pdmax = cand[q] ? max(pdmax, cur[q].seq - m.first) : pdmax;
+      latp[q] = counted ? lat : latp[q];
+    }
+    if (n_cnt) {
+      // :128-129: a counted record arriving at msg_count == 1 replaces byte_count by its size
+      // (nothing is pending then, see above): at 1 the run's bytes replace it; at 0 the first
+      // counted record adds and the second replaces, so the first one's size drops out
+      if (msg_count == 1) byte_count = 0;
+      if (msg_count == 0) {
+        if (n_cnt >= 2) byte_count -= len1;  // byte_count is 0 here; the flush adds it back
+        lmin = inf;                          // :132-133: the first counted latency sets both
+        lmax = -inf;
+      }
+      msg_count += n_cnt;
+    }
+    dups += n_dup;
+    m.n += n_new;
     if (lane < 32u) m.w |= scat[wv][lane];
     __builtin_amdgcn_wave_barrier();
-    m.n += e - k;
-    if (msg_count == 1) byte_count = 0;  // :128-129 (nothing pending here, see above)
-    msg_count += e - k;
-    const double lat = __builtin_bit_cast(double, (uint64_t)lhi << 32 | llo);
-    // min / max as fmin / fmax -- the reference's "if (l < min) min = l; else if (l > max)
-    // max = l" is exactly that for latencies (never NaN, never -0: ProtoTime::Delta of
-    // integer fields) with min <= max -- so order-free
-    pmin = in ? __builtin_fmin(pmin, lat) : pmin;
-    pmax = in ? __builtin_fmax(pmax, lat) : pmax;
-    pbytes += in ? r.len : 0u;
-    pdmax = in ? max(pdmax, r.seq - m.first) : pdmax;
     dirty = true;
-    // the sum in record order (bit-exact): the run's latencies staged in LDS and read back
-    // as broadcasts, two per read, so the loop is the dependent v_add_f64 chain
-    if (in) latl[wv][lane - k] = lat;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    double vs = lsum;
-    const uint32_t run = (MGENX_DIAG && (abl & 1)) ? 0u : e - k;
-    const double2* lp = reinterpret_cast<const double2*>(latl[wv]);
-    // software-pipelined: the next 8 latencies are read while the current 8 are added (two
-    // register sets, sched barriers keep the reads ahead), so the chain waits on v_add_f64,
-    // not on an LDS round trip every 8 adds.  Reads past `run` hit stale latl entries that
-    // are never added.
-    const uint32_t n8 = run / 8u;
-    auto rd = [&](double2 (&x)[4], uint32_t c) {
-      const uint32_t o = c < 8u ? 4u * c : 0u;
-      x[0] = lp[o]; x[1] = lp[o + 1]; x[2] = lp[o + 2]; x[3] = lp[o + 3];
-    };
-    auto add8 = [&](const double2 (&x)[4]) {
-#pragma unroll
-      for (int q = 0; q < 4; q++) {
-        vs = __dadd_rn(vs, x[q].x);
-        vs = __dadd_rn(vs, x[q].y);
-      }
-    };
-    double2 A[4], B[4];
-    rd(A, 0);
-    uint32_t c = 0;
-    for (; c + 2u <= n8; c += 2u) {
-      rd(B, c + 1u);
-      __builtin_amdgcn_sched_barrier(0);
-      add8(A);
-      __builtin_amdgcn_sched_barrier(0);
-      rd(A, c + 2u);
-      __builtin_amdgcn_sched_barrier(0);
-      add8(B);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (c < n8) {  // one whole chunk left in A; the remainder follows in B
-      rd(B, c + 1u);
-      __builtin_amdgcn_sched_barrier(0);
-      add8(A);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int q = 0; q < 4; q++) A[q] = B[q];
-    }
-    // the last run % 8 latencies are in A
-    const uint32_t rem = run & 7u;
-    if (rem > 0u) vs = __dadd_rn(vs, A[0].x);
-    if (rem > 1u) vs = __dadd_rn(vs, A[0].y);
-    if (rem > 2u) vs = __dadd_rn(vs, A[1].x);
-    if (rem > 3u) vs = __dadd_rn(vs, A[1].y);
-    if (rem > 4u) vs = __dadd_rn(vs, A[2].x);
-    if (rem > 5u) vs = __dadd_rn(vs, A[2].y);
-    if (rem > 6u) vs = __dadd_rn(vs, A[3].x);
-    lsum = vs;
-    __builtin_amdgcn_wave_barrier();
-    if (++pruns == 65536u) flush();  // pbytes per lane stays below 2^32
   };
 
-  // 64 records per round: lane k holds record order[i0 + k]; the record loads of the next
-  // two rounds and the index loads of the one after are in flight while this one is walked
-  // (the order index of a round is loaded two rounds before its record gather, so waiting
-  // for it -- loads complete in order -- never waits for a gather issued after the current
-  // round's records)
-  auto ldo = [&](uint32_t base) { return order[min(base + lane, e - 1u)]; };
-  uint32_t i0 = b;
-  const uint32_t oa = ldo(i0), ob = ldo(i0 + 64u);
-  uint32_t oc = ldo(i0 + 128u), od = ldo(i0 + 192u);
-  FRec cur = recs[oa], nx1 = recs[ob], nx2;
-  uint32_t ocur = oa, on1 = ob, on2;  // input record indices of cur / nx1 / nx2
-  while (i0 < e) {
-    nx2 = recs[oc];
-    on2 = oc;
-    oc = od;
-    od = ldo(i0 + 256u);
-    const uint32_t cnt = min(64u, e - i0);
-    const uint64_t lbits = __builtin_bit_cast(uint64_t, cur.latency);
-    const uint32_t llo = (uint32_t)lbits, lhi = (uint32_t)(lbits >> 32);
-    // the latest earlier record of this round with the same seq: computed only when a run
-    // turns out to hold a duplicate
-    int32_t prev_eq = -1;
-    bool have_prev_eq = false;
-    const bool plain = lane < cnt && cur.len != 0;
+  ld(b, cur);
+  ld(b + kRound, nxt);
+  for (uint32_t i0 = b; i0 < e; i0 += kRound) {
+    FRec nx2[kUR];
+    ld(i0 + 2u * kRound, nx2);
+    const uint32_t cnt = min(kRound, e - i0);
+#pragma unroll
+    for (uint32_t q = 0; q < kUR; q++) latp[q] = 0.0;
     uint32_t k = 0;
     while (k < cnt) {
-      uint32_t run = 0;
-      if (valid && msg_count >= 1 && m.n && !(MGENX_DIAG && (abl & 4))) {
-        const uint32_t word = (uint32_t)__shfl((int)m.w, (int)((cur.seq >> 5) & 31u));
-        const bool in_mask = (word >> (cur.seq & 31u)) & 1u;
-        const bool ok0 = plain && lane >= k && cur.seq - m.first < kDepth && !in_mask &&
-                         (int32_t)(cur.seq - seq_start) >= 0 &&
-                         !tge(Tm{(int64_t)cur.rxs, (int64_t)cur.rxu}, we);
-        auto run_of = [&](bool ok) {
-          const uint64_t okm = __ballot(ok) >> k;
-          const uint32_t r0 = okm == ~0ull >> k ? 64u - k : (uint32_t)__builtin_ctzll(~okm);
-          return min(r0, cnt - k);
-        };
-        run = run_of(ok0 && (!have_prev_eq || prev_eq < (int32_t)k));
-        if (run && scatter(cur, k, k + run)) {
-          if (!have_prev_eq) {
-            for (uint32_t i = 0; i + 1 < cnt; i++) {
-              const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)cur.seq, (int)i);
-              prev_eq = (lane > i && cur.seq == x) ? (int32_t)i : prev_eq;
-            }
-            have_prev_eq = true;
-          }
-          run = run_of(ok0 && prev_eq < (int32_t)k);
-          if (run) (void)scatter(cur, k, k + run);
+      uint32_t ev = k;  // the first record from k that takes the exact update
+      if (valid && m.n) {
+        ev = cnt;
+#pragma unroll
+        for (uint32_t q = 0; q < kUR; q++) {
+          const uint32_t p = 64u * q + lane;
+          const bool simple = cur[q].rxk < wek && (cur[q].len == 0u || cur[q].seq - m.first < kDepth);
+          const uint64_t ns = __ballot(p >= k && p < cnt && !simple);
+          if (ns) ev = min(ev, 64u * q + (uint32_t)__builtin_ctzll(ns));
         }
+        if (ev > k) bulk(k, ev);
       }
-      if (run) {
-        if (!(MGENX_DIAG && (abl & 8))) commit(cur, k, k + run, llo, lhi);
-        k += run;
-        if (k >= cnt) break;
-      }
+      if (ev >= cnt) break;
       flush();
-      const uint64_t lb = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)lhi, (int)k) << 32 |
-                          (uint32_t)__builtin_amdgcn_readlane((int)llo, (int)k);
-      if (!(MGENX_DIAG && (abl & 2)))
-      update((uint32_t)__builtin_amdgcn_readlane((int)cur.seq, (int)k),
-             (uint32_t)__builtin_amdgcn_readlane((int)cur.rxs, (int)k),
-             (uint32_t)__builtin_amdgcn_readlane((int)cur.rxu, (int)k),
-             (uint32_t)__builtin_amdgcn_readlane((int)cur.len, (int)k),
-             __builtin_bit_cast(double, lb),
-             (uint32_t)__builtin_amdgcn_readlane((int)ocur, (int)k));
-      k++;
+      const uint32_t q = ev >> 6, l = ev & 63u;
+      uint32_t seq = 0, len = 0, rlo = 0, rhi = 0, llo = 0, lhi = 0;
+#pragma unroll
+      for (uint32_t qq = 0; qq < kUR; qq++) {  // static indices (a dynamic one goes to scratch)
+        const uint32_t s_ = (uint32_t)__builtin_amdgcn_readlane((int)cur[qq].seq, (int)l);
+        const uint32_t n_ = (uint32_t)__builtin_amdgcn_readlane((int)cur[qq].len, (int)l);
+        const uint32_t a_ = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)cur[qq].rxk, (int)l);
+        const uint32_t b_ = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(cur[qq].rxk >> 32), (int)l);
+        const uint64_t lb = __builtin_bit_cast(uint64_t, cur[qq].latency);
+        const uint32_t c_ = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)lb, (int)l);
+        const uint32_t d_ = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(lb >> 32), (int)l);
+        seq = qq == q ? s_ : seq;
+        len = qq == q ? n_ : len;
+        rlo = qq == q ? a_ : rlo;
+        rhi = qq == q ? b_ : rhi;
+        llo = qq == q ? c_ : llo;
+        lhi = qq == q ? d_ : lhi;
+      }
+      const double lp = update(seq, (uint64_t)rhi << 32 | rlo, len,
+                               __builtin_bit_cast(double, (uint64_t)lhi << 32 | llo), i0 + ev);
+#pragma unroll
+      for (uint32_t qq = 0; qq < kUR; qq++) latp[qq] = (qq == q && lane == l) ? lp : latp[qq];
+      k = ev + 1u;
     }
-    cur = nx1;
-    nx1 = nx2;
-    ocur = on1;
-    on1 = on2;
-    i0 += 64u;
+#pragma unroll
+    for (uint32_t q = 0; q < kUR; q++)
+      if (64u * q + lane < cnt) lat2[i0 + 64u * q + lane] = latp[q];
+#pragma unroll
+    for (uint32_t q = 0; q < kUR; q++) {
+      cur[q] = nxt[q];
+      nxt[q] = nx2[q];
+    }
+    if (++prounds == 4096u) flush();  // per-lane bytes stay below 2^32
   }
 
   flush();
@@ -630,28 +656,123 @@ flow_update_wave_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
     sp->msg_count = msg_count;
     sp->byte_count = byte_count;
     sp->dup_count = dups;
-    sp->latency_sum = lsum;
     sp->latency_min = lmin;
     sp->latency_max = lmax;
     sp->n_reports = nrep;
     report_count[f] = rcount;
+    FlowBatch fb;
+    fb.rc0 = rc0;
+    fb.ncl = ncl;
+    fb.last_close = last_close;
+    fb.last_zr = last_zr;
+    fb.lsum0 = lsum0;
+    fb.rsv = 0;
+    fbatch[f] = fb;
+  }
+}
+
+// ---- the latency sums: latency_sum += latency in record order (bit-exact) ----
+// One workgroup per flow, one thread per window the call needs: every kept report closed in this
+// call (its latency_ave) and the window still open at the end (the state's latency_sum).  A window
+// is the in-order sum of its records' lat' values: the first from latency_sum on entry, a later
+// one from its opening record's lat' (0.0 + x is exact; nothing for a zero restart).  The flow's
+// lat' values stream through LDS in pieces, so each thread's dependent v_add_f64 chain reads LDS,
+// not HBM.
+constexpr uint32_t kChainPiece = 4096;  // doubles per LDS piece (32 KiB)
+
+__global__ void __launch_bounds__(256)
+flow_chain_kernel(mgenx_flow_state* __restrict__ flows, const uint32_t* __restrict__ bnd,
+                  uint32_t bstride, const double* __restrict__ lat2,
+                  const FlowBatch* __restrict__ fbatch, const CloseRec* __restrict__ closes,
+                  mgenx_flow_report* __restrict__ reports, uint32_t per_flow,
+                  const uint32_t* __restrict__ report_count) {
+  extern __shared__ double piece[];
+  __shared__ uint32_t span[2];
+  const uint32_t f = blockIdx.x, tid = threadIdx.x;
+  const uint32_t b = bnd[(size_t)f * bstride], e = bnd[(size_t)(f + 1u) * bstride];
+  if (b >= e) return;
+  const FlowBatch fb = fbatch[f];
+  const uint32_t rc1 = report_count[f];
+  const uint32_t kept = min(rc1, per_flow);
+  const uint32_t nslots = kept > fb.rc0 ? kept - fb.rc0 : 0u;
+  const uint32_t m = nslots + 1u;  // + the open window
+  const CloseRec* cl = closes + (size_t)f * per_flow;
+  for (uint32_t w0 = 0; w0 < m; w0 += blockDim.x) {
+    const uint32_t t = w0 + tid, wlast = min(m, w0 + blockDim.x) - 1u;
+    // window t: positions [lo, hi], start value s
+    uint32_t lo = 0, hi = 0;
+    double s = 0.0;
+    const bool has = t < m;
+    if (has) {
+      if (t < nslots) {
+        const uint32_t slot = fb.rc0 + t;
+        hi = cl[slot].pos;
+        if (t == 0) {
+          lo = b;
+          s = fb.lsum0;
+        } else {
+          lo = cl[slot - 1u].pos + (cl[slot - 1u].zr ? 1u : 0u);
+        }
+      } else {
+        hi = e - 1u;
+        if (fb.ncl) {
+          lo = fb.last_close + (fb.last_zr ? 1u : 0u);
+        } else {
+          lo = b;
+          s = fb.lsum0;
+        }
+      }
+    }
+    if (t == w0) span[0] = lo;
+    if (t == wlast) span[1] = hi;
+    __syncthreads();
+    const uint32_t a0 = span[0], z0 = span[1];
+    __syncthreads();
+    for (uint32_t p0 = a0; p0 <= z0 && p0 >= a0; p0 += kChainPiece) {
+      const uint32_t pend = min(z0 + 1u, p0 + kChainPiece);
+      const bool mine = has && lo <= hi && lo < pend && hi >= p0;
+      if (!__syncthreads_or(mine)) continue;
+      for (uint32_t j = tid; j < pend - p0; j += blockDim.x) piece[j] = lat2[p0 + j];
+      __syncthreads();
+      if (mine) {
+        const uint32_t ja = max(lo, p0) - p0, jz = min(hi + 1u, pend) - p0;
+        uint32_t j = ja;
+        for (; j + 8u <= jz; j += 8u) {
+          double x[8];
+#pragma unroll
+          for (int u = 0; u < 8; u++) x[u] = piece[j + u];
+#pragma unroll
+          for (int u = 0; u < 8; u++) s = __dadd_rn(s, x[u]);
+        }
+        for (; j < jz; j++) s = __dadd_rn(s, piece[j]);
+      }
+      __syncthreads();
+    }
+    if (has) {
+      if (t < nslots) {
+        const uint32_t slot = fb.rc0 + t;
+        const uint64_t mc = cl[slot].mc;
+        reports[(size_t)f * per_flow + slot].latency_ave =
+            mc == 0 ? -1.0 : mc == 1 ? s : __ddiv_rn(s, (double)mc);
+      } else {
+        flows[f].latency_sum = s;
+      }
+    }
   }
 }
 
 // ---- ordering the records by flow, stably: a counting sort (flow count < kCountBins) --
-// The output is `order`: the input index of every record, flow after flow, receive order kept
-// within a flow; the hist kernel also writes every record as the 24-B FRec the update
-// reads (in input order, coalesced; the update gathers them through `order`).
-// (Measured alternatives, config 4: gathering the fields straight from the columns in the
-// update, 0.82 ms; writing the FRecs in flow order from the order kernel, 0.67-0.72 ms.)
+// The output is every record as the 24-B FRec the update reads, flow after flow, receive order
+// kept within a flow (and, for report_rec, `order`: the input index at each sorted position).
 //   hist:  per-tile flow histogram (kTile records per tile), stored flow-major
 //          (hist[flow * n_tiles + tile]);
-//   scan:  exclusive prefix sum of hist = where each (flow, tile) run starts in `order`;
+//   scan:  exclusive prefix sum of hist = where each (flow, tile) run starts;
 //   order: each tile is sorted by flow in LDS (stable: waves own contiguous eighths, ranks
-//          inside a 64-record step from ballots on the key bits), then written run by run --
-//          consecutive lanes to consecutive slots -- instead of one scattered 4-B store per
-//          record.  Tiles go to XCDs in contiguous ranges (blockIdx mod 8 = XCD), so the runs
-//          of one flow from neighbouring tiles meet in the same L2 and leave it as whole lines.
+//          inside a 64-record step from ballots on the key bits), then its records are built
+//          from the caller's columns (or rows) -- gathered inside the tile, whose few hundred KB
+//          stay in L2 -- and written run by run, consecutive lanes to consecutive slots.  Tiles go
+//          to XCDs in contiguous ranges (blockIdx mod 8 = XCD), so the runs of one flow from
+//          neighbouring tiles meet in the same L2 and leave it as whole lines.
 // Records whose flow index is >= n_flows (MGENX_FLOW_NONE) go to the extra last bin and are
 // not written.
 constexpr uint32_t kCountBins = 2048;  // LDS: 9 x bins x 4 + kTile x 4 bytes
@@ -661,32 +782,21 @@ constexpr uint32_t kPart = kTile / kSortWaves;
 
 __global__ void __launch_bounds__(512)
 flow_hist_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows, uint32_t n_tiles,
-                 uint32_t* __restrict__ hist, RecSrc src, FRec* __restrict__ recs) {
+                 uint32_t* __restrict__ hist) {
   extern __shared__ uint32_t h[];
   const uint32_t bins = n_flows + 1u;
   for (uint32_t k = threadIdx.x; k < bins; k += blockDim.x) h[k] = 0u;
   __syncthreads();
   const uint32_t a = blockIdx.x * kTile, e = min(n, a + kTile);
-  // kHistU records per thread and pass, all their loads issued before any is used (one
-  // load latency per pass instead of one per record)
-  constexpr uint32_t kHistU = 4;
+  // kHistU keys per thread and pass, all loads issued before any is used
+  constexpr uint32_t kHistU = 8;
   for (uint32_t i0 = a + threadIdx.x; i0 < e; i0 += kHistU * blockDim.x) {
     uint32_t fi[kHistU];
-    FRec r[kHistU];
 #pragma unroll
-    for (uint32_t u = 0; u < kHistU; u++) {
-      const uint32_t i = min(i0 + u * blockDim.x, e - 1u);
-      fi[u] = idx[i];
-      r[u] = make_frec(src, i);
-    }
+    for (uint32_t u = 0; u < kHistU; u++) fi[u] = idx[min(i0 + u * blockDim.x, e - 1u)];
 #pragma unroll
-    for (uint32_t u = 0; u < kHistU; u++) {
-      const uint32_t i = i0 + u * blockDim.x;
-      if (i < e) {
-        atomicAdd(&h[min(fi[u], n_flows)], 1u);
-        recs[i] = r[u];  // input order, coalesced
-      }
-    }
+    for (uint32_t u = 0; u < kHistU; u++)
+      if (i0 + u * blockDim.x < e) atomicAdd(&h[min(fi[u], n_flows)], 1u);
   }
   __syncthreads();
   for (uint32_t k = threadIdx.x; k < bins; k += blockDim.x) hist[(size_t)k * n_tiles + blockIdx.x] = h[k];
@@ -694,8 +804,8 @@ flow_hist_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows,
 
 __global__ void __launch_bounds__(512)
 flow_order_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows,
-                  uint32_t n_tiles, const uint32_t* __restrict__ start,
-                  uint32_t* __restrict__ order, uint32_t key_bits) {
+                  uint32_t n_tiles, const uint32_t* __restrict__ start, RecSrc src,
+                  FRec* __restrict__ recs, uint32_t* __restrict__ order, uint32_t key_bits) {
   extern __shared__ uint32_t lds[];
   const uint32_t bins = n_flows + 1u;
   uint32_t* cnt = lds;                                // [wave][bin]: counts, then run bases
@@ -776,9 +886,29 @@ flow_order_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows
     }
   }
   __syncthreads();
-  for (uint32_t j = tid; j < tn; j += blockDim.x) {
-    const uint32_t k = lkey[j];
-    if (k < n_flows) order[sbase[k] + j] = t0 + lsorted[j];
+  // the records, built from the source (tile-local gathers, kOrdU per thread in flight) and
+  // stored at their sorted positions
+  constexpr uint32_t kOrdU = 4;
+  for (uint32_t j0 = tid; j0 < tn; j0 += kOrdU * blockDim.x) {
+    uint32_t key[kOrdU], src_i[kOrdU];
+    FRec r[kOrdU];
+#pragma unroll
+    for (uint32_t u = 0; u < kOrdU; u++) {
+      const uint32_t j = min(j0 + u * blockDim.x, tn - 1u);
+      key[u] = lkey[j];
+      src_i[u] = t0 + lsorted[j];
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kOrdU; u++) r[u] = make_frec(src, src_i[u]);
+#pragma unroll
+    for (uint32_t u = 0; u < kOrdU; u++) {
+      const uint32_t j = j0 + u * blockDim.x;
+      if (j < tn && key[u] < n_flows) {
+        const uint32_t pos = sbase[key[u]] + j;
+        recs[pos] = r[u];
+        if (order) order[pos] = src_i[u];
+      }
+    }
   }
 }
 
@@ -859,13 +989,19 @@ flow_row_scan_kernel(const uint32_t* __restrict__ hist, uint32_t n_tiles,
 // ---- the general ordering (any flow count): hipCUB radix sort of (flow, record) pairs ----
 // keys: flow index clamped to n_flows (records to skip sort last); vals: record index
 __global__ void flow_keys_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows,
-                                 uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
-                                 RecSrc src, FRec* __restrict__ recs) {
+                                 uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   keys[i] = min(idx[i], n_flows);
   vals[i] = i;
-  recs[i] = make_frec(src, i);
+}
+
+// the sorted records of the radix path: position p < bnd[n_flows] gets record order[p]
+__global__ void flow_gather_kernel(const uint32_t* __restrict__ order, const uint32_t* __restrict__ bnd,
+                                   uint32_t n_flows, RecSrc src, FRec* __restrict__ recs) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= bnd[n_flows]) return;
+  recs[p] = make_frec(src, order[p]);
 }
 
 // run starts: bnd[f] = first sorted position with flow >= f (f = 0..n_flows)
@@ -988,12 +1124,17 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
     (void)hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, (const uint32_t*)nullptr,
                                              (uint32_t*)nullptr, (const uint32_t*)nullptr,
                                              (uint32_t*)nullptr, (int)n, 0, (int)key_bits, stream);
+  const bool want_order = report_rec != nullptr;
   const size_t nb = a256((size_t)n * 4), rb = a256((size_t)n * sizeof(FRec));
   const size_t hb = a256(n_hist * 4), bb = a256((size_t)bins * 4);
-  // counting: hist, start, records, order, cub
-  // radix:    keys_in, keys_out, vals_in, order, records, bounds, cub
-  const size_t need = sort_path == 0 ? 2 * hb + rb + nb + a256(cub_bytes)
-                                     : 4 * nb + rb + bb + a256(cub_bytes);
+  const size_t lb = a256((size_t)n * 8), fbb = a256((size_t)n_flows * sizeof(FlowBatch));
+  const size_t cb = a256((size_t)n_flows * per_flow * sizeof(CloseRec));
+  // both: records (sorted), lat', per-flow batch info, closes
+  // counting: hist, start, order (report_rec only), row totals
+  // radix:    keys_in, keys_out, vals_in, order, bounds, cub
+  const size_t common = rb + lb + fbb + cb;
+  const size_t need = common + (sort_path == 0 ? 2 * hb + (want_order ? nb : 0) + a256(cub_bytes)
+                                               : 4 * nb + bb + a256(cub_bytes));
   if (ws.bytes < need) {
     if (ws.mem) (void)hipFree(ws.mem);
     ws.mem = nullptr;
@@ -1006,20 +1147,21 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
   }
   char* p = static_cast<char*>(ws.mem);
   auto take = [&](size_t b) { char* q = p; p += b; return q; };
+  FRec* recs = (FRec*)take(rb);
+  double* lat2 = (double*)take(lb);
+  FlowBatch* fbatch = (FlowBatch*)take(fbb);
+  CloseRec* closes = (CloseRec*)take(cb);
   const uint32_t* bnd;
   uint32_t bstride;
-  uint32_t* order;
-  FRec* recs;
+  uint32_t* order = nullptr;
   hipError_t e;
   if (sort_path == 0) {
     uint32_t* hist = (uint32_t*)take(hb);
     uint32_t* start = (uint32_t*)take(hb);
-    recs = (FRec*)take(rb);
-    order = (uint32_t*)take(nb);
-    void* cub_tmp = take(a256(cub_bytes));
+    if (want_order) order = (uint32_t*)take(nb);
+    uint32_t* totals = (uint32_t*)take(a256(cub_bytes));
     hipLaunchKernelGGL(flow_hist_kernel, dim3(n_tiles), dim3(512), bins * 4u, stream, flow_idx, n,
-                       n_flows, n_tiles, hist, src, recs);
-    uint32_t* totals = (uint32_t*)cub_tmp;
+                       n_flows, n_tiles, hist);
     hipLaunchKernelGGL(flow_row_total_kernel, dim3(bins), dim3(256), 0, stream, hist, n_tiles, totals);
     hipLaunchKernelGGL(flow_row_scan_kernel, dim3(bins), dim3(1024), 0, stream, hist, n_tiles,
                        totals, start);
@@ -1037,7 +1179,7 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
     }
     const uint32_t grid = 8u * ((n_tiles + 7u) / 8u);
     hipLaunchKernelGGL(flow_order_kernel, dim3(grid), dim3(64 * kSortWaves), lds, stream,
-                       flow_idx, n, n_flows, n_tiles, start, order, key_bits);
+                       flow_idx, n, n_flows, n_tiles, start, src, recs, order, key_bits);
     bnd = start;
     bstride = n_tiles;
   } else {
@@ -1045,11 +1187,10 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
     uint32_t* keys_out = (uint32_t*)take(nb);
     uint32_t* vals_in = (uint32_t*)take(nb);
     order = (uint32_t*)take(nb);
-    recs = (FRec*)take(rb);
     uint32_t* d_bnd = (uint32_t*)take(bb);
     void* cub_tmp = take(a256(cub_bytes));
     hipLaunchKernelGGL(flow_keys_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, flow_idx, n,
-                       n_flows, keys_in, vals_in, src, recs);
+                       n_flows, keys_in, vals_in);
     e = hipcub::DeviceRadixSort::SortPairs(cub_tmp, cub_bytes, keys_in, keys_out, vals_in, order,
                                            (int)n, 0, (int)key_bits, stream);
     if (e != hipSuccess) {
@@ -1058,18 +1199,17 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
     }
     hipLaunchKernelGGL(flow_bounds_kernel, dim3((bins + 255) / 256), dim3(256), 0, stream, keys_out,
                        n, n_flows, d_bnd);
+    hipLaunchKernelGGL(flow_gather_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, order,
+                       d_bnd, n_flows, src, recs);
     bnd = d_bnd;
     bstride = 1;
   }
   if (sabl) return MGENX_OK;  // timing study: ordering only
-  int abl = 0;  // diagnostics build only: ablations of the update kernel (timing studies)
-#if MGENX_DIAG
-  if (const char* a = getenv("MGENX_AN_ABL")) abl = atoi(a);
-#endif
-  hipLaunchKernelGGL(flow_update_wave_kernel, dim3((n_flows + 3) / 4), dim3(256), 0, stream,
-                     flows, n_flows, bnd, bstride, order, recs,
-                     reports, per_flow,
-                     report_count, report_rec, abl);
+  hipLaunchKernelGGL(flow_update_kernel, dim3((n_flows + 3) / 4), dim3(256), 0, stream, flows,
+                     n_flows, bnd, bstride, recs, order, lat2, reports, per_flow, report_count,
+                     report_rec, closes, fbatch);
+  hipLaunchKernelGGL(flow_chain_kernel, dim3(n_flows), dim3(256), kChainPiece * 8u, stream, flows,
+                     bnd, bstride, lat2, fbatch, closes, reports, per_flow, report_count);
   e = hipGetLastError();
   if (e != hipSuccess) {
     snprintf(err, errn, "flow_reduce: %s", hipGetErrorString(e));

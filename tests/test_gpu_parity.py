@@ -208,6 +208,8 @@ def test_full_size_rows_ring_kernel(torch, eng, size):
     c = host_cols(cols, n)
     rows = eng.alloc_rows(n)
     eng.unpack(slab, n, stride=size, fixed_len=size, cols={"rows": rows})
+    from mgen_amd import UNPACK_K_FIXED_RING
+    assert eng.last_unpack_kernel() == UNPACK_K_FIXED_RING   # the kernel under test ran
     torch.cuda.synchronize()
     r = rows_to_cols(rows, n)
     # every record the flips or the flag clears touched, against the oracle; the rest

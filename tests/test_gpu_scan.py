@@ -343,3 +343,72 @@ def test_pruned_scan_falls_back_on_repeated_records(torch, gold):
     # the hypothesis failed on call 2 (exact rebuild, path 0) and backs off on call 3
     assert paths[:2] == [0, 0] and paths[2] != 2, paths
     e.close()
+
+
+# ---- config 5 at its real size (tests had stopped at 64 MiB) ----
+
+def _tcp_tx_stream(torch, eng, n, msg=16384):
+    """n messages of `msg` bytes through the GPU TCP transmit path (mgenx_pack_tcp), as the
+    bench builds config 5: 64 templates, checksum on."""
+    from mgen_amd import PACK_CHECKSUM, to_device
+    from mgen_amd._abi import DESC_DTYPE
+    from mgen_amd.workloads import make_templates
+    tmpl, pool = make_templates(64)
+    desc = np.zeros(n, DESC_DTYPE)
+    seq = np.arange(n)
+    desc["tmpl"], desc["seq_num"] = seq % 64, seq
+    desc["tx_sec"], desc["tx_usec"] = 1_700_000_000 + seq // 1_000_000, seq % 1_000_000
+    desc["flags"] = 4
+    tm, pl = to_device(tmpl), to_device(pool)
+    tcrc = torch.empty(64, dtype=torch.int32, device="cuda")
+    eng.pack_prepare(tm, 64, pl, tcrc)
+    total = torch.full((n,), msg, dtype=torch.int32, device="cuda")
+    stream, _ = eng.pack_tcp(tm, tcrc, to_device(desc), total, n, pl, opts=PACK_CHECKSUM)
+    torch.cuda.synchronize()
+    return stream
+
+
+@pytest.mark.parametrize("n", [65536, 73728, 73730])
+def test_config5_full_size_vs_oracle(torch, eng, n):
+    """BASELINE config 5 at full size: 65,536 x 16 KiB (1 GiB, 32,768 detect blocks), and
+    streams on (36,864 blocks = 1.125 GiB) and just past (36,865) the LDS block-count path's
+    bound (mgenx_scan.hip kScanSmall).  The oracle's sequential framing + Unpack + CRC
+    (or_tcp_scan, mgenTransport.cpp:1683-1760) against mgenx_stream_scan on a fresh engine:
+    the first call (exact build) and the second (the successor-marked chain, path 2)."""
+    import ctypes
+    from mgen_amd import Engine, OPT_TCP, SCAN_TCP
+    from oracle import oracle as O
+    stream = _tcp_tx_stream(torch, eng, n)
+    host = stream.cpu().numpy()
+    assert host.size == n * 16384
+    cap = n + 8
+    wo = np.zeros(cap, np.uint64)
+    wl = np.zeros(cap, np.uint32)
+    wf = np.zeros(cap, O.FIELDS_DTYPE)
+    cons, st = ctypes.c_uint64(0), ctypes.c_int(0)
+    P = ctypes.c_void_p
+    k = O.lib().or_tcp_scan(P(host.ctypes.data), host.size, 0, P(wo.ctypes.data),
+                            P(wl.ctypes.data), P(wf.ctypes.data), cap, ctypes.byref(cons),
+                            ctypes.byref(st))
+    assert k == n and cons.value == host.size and st.value == 0
+    assert int(wf["err"][:n].sum()) == 0
+    e2 = Engine(0)
+    try:
+        paths = []
+        for call in range(2):
+            offs, lens, info = e2.stream_scan(stream, SCAN_TCP)
+            assert int(info.n_records) == n and int(info.consumed) == host.size, call
+            assert int(info.status) == 0
+            assert np.array_equal(offs.cpu().numpy().view(np.uint64), wo[:n]), call
+            assert np.array_equal(lens.cpu().numpy().view(np.uint32), wl[:n]), call
+            paths.append(int(info.path))
+        assert paths == [0, 2], paths
+        cols = e2.unpack(stream, n, rec_off=offs, rec_len=lens, opts=OPT_TCP)
+        torch.cuda.synchronize()
+        for key in ("err", "seq_num", "flow_id", "tx_sec", "tx_usec", "msg_len"):
+            got = cols[key].cpu().numpy().view(wf[key].dtype)
+            assert np.array_equal(got, wf[key][:n]), key
+    finally:
+        e2.close()
+    del stream
+    torch.cuda.empty_cache()
