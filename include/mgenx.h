@@ -266,6 +266,38 @@ int mgenx_crc32_update(mgenx_ctx* ctx, const uint8_t* dev_data, const uint64_t* 
 int mgenx_crc32_batch(mgenx_ctx* ctx, const uint8_t* dev_data, const uint64_t* dev_off,
                       const uint32_t* dev_len, uint32_t n, uint32_t* dev_out, void* stream);
 
+/* ---- the resident single-message worker ----
+ * For callers that stay one message at a time (an unchanged MgenUdpTransport calls
+ * MgenMsg::Unpack once per datagram, mgenTransport.cpp:948-997, and ComputeCRC32 once per
+ * message): a batch entry point per message costs a launch, copies and a synchronisation.
+ * A worker keeps ONE wave resident on the context's device, polling a mailbox in pinned host
+ * memory: a call copies the message into the mailbox, the wave decodes or checksums it and
+ * writes the reply back; the call spins until it arrives.  Host buffers in, results out --
+ * no device pointers.  The wave exits after idle_ms without a request (the next call
+ * relaunches it) and on mgenx_worker_destroy.  A worker serves one caller at a time (the
+ * caller serialises); results equal the batch entry points' on the same bytes.
+ *   mgenx_worker_unpack  <- MgenMsg::Unpack (include/mgenMsg.h:110, mgenMsg.cpp:315-500) on a
+ *                           fresh MgenMsg: the members it assigned (`decoded`, MGENX_DEC_*) and
+ *                           err (MgenMsg::Error; 0 = Unpack returned true); no CRC check
+ *   mgenx_worker_crc32   <- MgenMsg::ComputeCRC32 (include/mgenMsg.h:201-203, mgenMsg.cpp:
+ *                           524-541): the running checksum in and out */
+#define MGENX_WORKER_MAX_BYTES 65536u
+typedef struct {
+    uint32_t flow_id, seq_num, tx_sec, tx_usec, payload_off;
+    uint32_t lat_raw, lon_raw;
+    int32_t  alt;
+    uint16_t msg_len, dst_port, payload_len, hdr_len, host_port;
+    uint8_t  flags, err, dst_type, dst_len, payload_type, gps_status, host_type, host_len;
+    uint8_t  decoded, version, rsv[2];
+    uint8_t  dst_addr[16], host_addr[16];
+} mgenx_unpacked;                    /* 88 bytes */
+typedef struct mgenx_worker mgenx_worker;
+int mgenx_worker_create(mgenx_ctx* ctx, uint32_t idle_ms, mgenx_worker** out);
+int mgenx_worker_destroy(mgenx_worker* w);
+int mgenx_worker_unpack(mgenx_worker* w, const uint8_t* msg, uint32_t len, mgenx_unpacked* out);
+int mgenx_worker_crc32(mgenx_worker* w, const uint8_t* data, uint32_t len, uint32_t state_in,
+                       uint32_t* state_out);
+
 /* ---- the TCP receiver's persistent rx_msg ----
  * MgenTcpTransport decodes every message of a connection into ONE MgenMsg (rx_msg,
  * src/common/mgenTransport.cpp:1082): ResetRxMsgState (:1501-1513) zeroes only

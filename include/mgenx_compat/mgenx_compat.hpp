@@ -7,8 +7,11 @@
 // SURVEY.md 8(b)) to the same code.  A batch is staged in one pinned host arena, copied to
 // the device in one hipMemcpyAsync, processed by libmgenx's gfx950 kernels
 // (mgenx_pack_msgs, mgenx_unpack_batch, mgenx_crc32_update, mgenx_flow_reduce) and copied
-// back in one more; the call returns when the results are in the caller's buffers.  There
-// is no host implementation of the codec here: without a GPU the calls throw.
+// back in one more; the call returns when the results are in the caller's buffers.  A single
+// Unpack or ComputeCRC32 (what an unchanged transport calls per datagram) goes instead to the
+// resident worker (mgenx_worker_*): one wave kept on the device that polls a pinned mailbox,
+// so the call pays no launch and no copy.  There is no host implementation of the codec here:
+// without a GPU the calls throw.
 //
 // One engine per process (device MGENX_DEVICE, default 0), serialised by a mutex: the
 // reference's callers run on one dispatcher thread.
@@ -18,6 +21,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <cstdlib>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -154,9 +158,40 @@ class Engine {
   }
 
   // ---- MgenMsg::Unpack alone (mgenx_unpack_batch, MGENX_OPT_SKIP_CRC) ---------------
+  // One message (the reference's per-datagram call): the resident worker, no launch or copy.
   void Unpack(const uint8_t* const* bufs, const uint16_t* lens, unsigned n, UnpackOut* out) {
     if (n == 0) return;
     Init();
+    if (n == 1 && Worker()) {
+      mgenx_unpacked u;
+      Check(mgenx_worker_unpack(worker_, bufs[0], lens[0], &u), "mgenx_worker_unpack");
+      UnpackOut& r = out[0];
+      r.flow_id = u.flow_id;
+      r.seq_num = u.seq_num;
+      r.tx_sec = u.tx_sec;
+      r.tx_usec = u.tx_usec;
+      r.payload_off = u.payload_off;
+      r.lat_raw = u.lat_raw;
+      r.lon_raw = u.lon_raw;
+      r.alt = u.alt;
+      r.msg_len = u.msg_len;
+      r.dst_port = u.dst_port;
+      r.payload_len = u.payload_len;
+      r.hdr_len = u.hdr_len;
+      r.host_port = u.host_port;
+      r.flags = u.flags;
+      r.err = u.err;
+      r.dst_type = u.dst_type;
+      r.dst_len = u.dst_len;
+      r.payload_type = u.payload_type;
+      r.gps_status = u.gps_status;
+      r.host_type = u.host_type;
+      r.host_len = u.host_len;
+      r.decoded = u.decoded;
+      memcpy(r.dst_addr, u.dst_addr, 16);
+      memcpy(r.host_addr, u.host_addr, 16);
+      return;
+    }
     size_t slab = 0;
     for (unsigned i = 0; i < n; i++) slab += Align(lens[i], 16);
     Layout L;
@@ -256,6 +291,11 @@ class Engine {
                    unsigned n, uint32_t* state_out) {
     if (n == 0) return;
     Init();
+    if (n == 1 && lens[0] <= MGENX_WORKER_MAX_BYTES && Worker()) {
+      Check(mgenx_worker_crc32(worker_, bufs[0], lens[0], state_in[0], state_out),
+            "mgenx_worker_crc32");
+      return;
+    }
     size_t bytes = 0;
     for (unsigned i = 0; i < n; i++) bytes += Align(lens[i], 16);
     Layout L;
@@ -593,6 +633,26 @@ class Engine {
   ~Engine() {
     // process teardown: the HIP runtime may already be gone, so nothing is freed here
   }
+  // the resident single-message worker (mgenx_worker_*), created on first use unless
+  // MGENX_COMPAT_WORKER=0; stopped at exit (before the HIP runtime's own teardown, which
+  // registered its handlers earlier)
+  bool Worker() {
+    if (worker_) return true;
+    if (worker_off_) return false;
+    const char* env = getenv("MGENX_COMPAT_WORKER");
+    if ((env && atoi(env) == 0) || mgenx_worker_create(ctx_, 200, &worker_) != MGENX_OK) {
+      worker_ = nullptr;
+      worker_off_ = true;
+      return false;
+    }
+    std::atexit([] { Get().StopWorker(); });
+    return true;
+  }
+  void StopWorker() {
+    if (worker_) mgenx_worker_destroy(worker_);
+    worker_ = nullptr;
+    worker_off_ = true;
+  }
   void Init() {
     if (ctx_) return;
     const char* dv = getenv("MGENX_DEVICE");
@@ -695,6 +755,8 @@ class Engine {
 
   std::mutex mu_;
   mgenx_ctx* ctx_ = nullptr;
+  mgenx_worker* worker_ = nullptr;
+  bool worker_off_ = false;
   hipStream_t stream_ = nullptr;
   uint8_t* host_ = nullptr;
   uint8_t* dev_ = nullptr;

@@ -22,7 +22,7 @@ from ._abi import (  # noqa: F401
     PcapInfo, TextSrc, TEXT_PER_RECORD, TEXT_OWNER, TEXT_MAP, TEXT_SCATTER, PCAP_NSEC, PCAP_SWAPPED, LOG_EPOCH, LOG_NO_DATA, LOG_NO_GPS,
     LOG_SKIP_ERR, FLOW_NONE, DLT_EN10MB, DLT_LINUX_SLL, BinlogInfo, BINLOG_NO_RX, BINLOG_FLUSH,
     UNPACK_K_HEADER, UNPACK_K_GENERAL, UNPACK_K_VAR, UNPACK_K_FIXED, UNPACK_K_FIXED_RING,
-    UNPACK_K_OTHER,
+    UNPACK_K_OTHER, UNPACKED_DTYPE,
 )
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -43,6 +43,7 @@ EXPORTED_SYMBOLS = (
     "mgenx_flow_reduce_ex", "mgenx_flow_keys", "mgenx_text_interleave", "mgenx_pcap_index",
     "mgenx_pcap_parse", "mgenx_binlog_index", "mgenx_convert_binary_log",
     "mgenx_unpack_last_kernel", "mgenx_pcap_snap", "mgenx_flow_reduce_rows",
+    "mgenx_worker_create", "mgenx_worker_destroy", "mgenx_worker_unpack", "mgenx_worker_crc32",
 )
 DIAG_SYMBOLS = ("mgenx_set_tuning", "mgenx_diag_stream_read", "mgenx_diag_group_rw")
 
@@ -126,6 +127,10 @@ def load(diag: bool = False):
                                       i32, u32, P, u64, P, P]
     L.mgenx_log_recv_binary.argtypes = [P, P, u64, P, u64, P, ctypes.POINTER(MgenxCols), P, P,
                                         P, u32, i32, P, u64, P, P]
+    L.mgenx_worker_create.argtypes = [P, u32, ctypes.POINTER(P)]
+    L.mgenx_worker_destroy.argtypes = [P]
+    L.mgenx_worker_unpack.argtypes = [P, ctypes.c_char_p, u32, P]
+    L.mgenx_worker_crc32.argtypes = [P, ctypes.c_char_p, u32, u32, ctypes.POINTER(u32)]
     _libs[path] = L
     return L
 
@@ -168,6 +173,11 @@ class Engine:
         if rc != 0:
             msg = self.lib.mgenx_last_error(self.ctx)
             raise MgenxError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+    # ------------------------------------------------------------ single messages
+    def worker(self, idle_ms: int = 200):
+        """A resident single-message worker on this engine's device (mgenx_worker_*)."""
+        return Worker(self, idle_ms)
 
     # ------------------------------------------------------------ columns
     def alloc_cols(self, n: int, ext: bool = False):
@@ -769,3 +779,40 @@ def to_device(arr: np.ndarray, device=0):
     import torch
     b = np.ascontiguousarray(arr).view(np.uint8).reshape(-1)
     return torch.from_numpy(b.copy()).to(f"cuda:{device}")
+
+
+class Worker:
+    """mgenx_worker: MgenMsg::Unpack / ComputeCRC32 of one host message per call, served by a
+    wave resident on the device (no launch or copy per call)."""
+
+    def __init__(self, eng: Engine, idle_ms: int = 200):
+        self.eng = eng
+        self.w = ctypes.c_void_p()
+        eng._check(eng.lib.mgenx_worker_create(eng.ctx, idle_ms, ctypes.byref(self.w)),
+                   "mgenx_worker_create")
+
+    def unpack(self, msg: bytes):
+        """One record's mgenx_unpacked (numpy structured scalar, UNPACKED_DTYPE)."""
+        out = np.zeros(1, UNPACKED_DTYPE)
+        self.eng._check(self.eng.lib.mgenx_worker_unpack(self.w, bytes(msg), len(msg),
+                                                         ctypes.c_void_p(out.ctypes.data)),
+                        "mgenx_worker_unpack")
+        return out[0]
+
+    def crc32(self, data: bytes, state: int = 0) -> int:
+        out = ctypes.c_uint32(0)
+        self.eng._check(self.eng.lib.mgenx_worker_crc32(self.w, bytes(data), len(data), state,
+                                                        ctypes.byref(out)),
+                        "mgenx_worker_crc32")
+        return out.value
+
+    def close(self):
+        if self.w:
+            self.eng.lib.mgenx_worker_destroy(self.w)
+            self.w = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -171,3 +171,16 @@ class BinlogInfo(ctypes.Structure):    # mgenx_binlog_info
 
 BINLOG_OK, BINLOG_HEADER, BINLOG_TOO_LONG, BINLOG_EVENT, BINLOG_SHORT = 0, 1, 2, 3, 4
 BINLOG_NO_RX, BINLOG_FLUSH = 0x1, 0x2
+
+
+# mgenx_unpacked (include/mgenx.h): one message decoded by the resident worker
+UNPACKED_DTYPE = np.dtype([
+    ("flow_id", "<u4"), ("seq_num", "<u4"), ("tx_sec", "<u4"), ("tx_usec", "<u4"),
+    ("payload_off", "<u4"), ("lat_raw", "<u4"), ("lon_raw", "<u4"), ("alt", "<i4"),
+    ("msg_len", "<u2"), ("dst_port", "<u2"), ("payload_len", "<u2"), ("hdr_len", "<u2"),
+    ("host_port", "<u2"), ("flags", "u1"), ("err", "u1"), ("dst_type", "u1"), ("dst_len", "u1"),
+    ("payload_type", "u1"), ("gps_status", "u1"), ("host_type", "u1"), ("host_len", "u1"),
+    ("decoded", "u1"), ("version", "u1"), ("rsv", "u1", 2),
+    ("dst_addr", "u1", 16), ("host_addr", "u1", 16),
+], align=True)
+assert UNPACKED_DTYPE.itemsize == 88

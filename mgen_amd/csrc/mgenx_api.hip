@@ -10,6 +10,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <chrono>
 #include <vector>
 
 
@@ -921,6 +922,125 @@ int mgenx_flow_export(mgenx_ctx* ctx, const mgenx_flow_state* dev_flows, uint32_
                       mgenx_flow_counters* dev_out, void* stream) {
   if (!ctx || (n_flows && (!dev_flows || !dev_out))) return MGENX_EINVAL;
   return mgenx_flow_export_run(dev_flows, n_flows, dev_out, (hipStream_t)stream);
+}
+
+// ---- the resident single-message worker (mgenx_worker.hip) ----
+struct mgenx_worker {
+  mgenx_ctx* ctx = nullptr;
+  hipStream_t stream = nullptr;
+  mgenx::WMail* mail = nullptr;      // pinned host memory (mapped, coherent)
+  mgenx::WMail* mail_dev = nullptr;  // the device's view of it
+  uint32_t seq = 0;                  // the last request number issued
+  uint64_t idle_ticks = 0;           // s_memrealtime ticks (100 MHz)
+  bool launched = false;
+};
+
+static uint32_t w_load(const uint32_t* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
+static void w_store(uint32_t* p, uint32_t v) { __atomic_store_n(p, v, __ATOMIC_RELEASE); }
+
+// a worker wave serving requests after `start`: the previous one (if any) has ended -- it
+// clears `alive` as its last act -- so reap it and launch the next
+static int worker_launch(mgenx_worker* w, uint32_t start) {
+  if (w->launched && hipStreamSynchronize(w->stream) != hipSuccess) return MGENX_EDEVICE;
+  w_store(&w->mail->alive, 1u);
+  hipError_t e = mgenx::launch_worker(w->mail_dev, w->ctx->d_tabs + 1024, w->ctx->d_bytetab,
+                                      w->ctx->d_xpow, start, w->idle_ticks, w->stream);
+  if (e != hipSuccess) return set_err(w->ctx, e, "worker launch");
+  w->launched = true;
+  return MGENX_OK;
+}
+
+// post request `op` (its bytes already in mail->data) and wait for the reply
+static int worker_call(mgenx_worker* w, uint32_t op, uint32_t len, uint32_t arg) {
+  hipSetDevice(w->ctx->device);
+  if (!w->launched || !w_load(&w->mail->alive)) {
+    const int rc = worker_launch(w, w->seq);
+    if (rc != MGENX_OK) return rc;
+  }
+  uint32_t r = w->seq + 1u;
+  if (r == 0u) r = 1u;  // 0 is "no request yet"
+  w->seq = r;
+  w->mail->op = op;
+  w->mail->len = len;
+  w->mail->arg = arg;
+  w_store(&w->mail->req, r);
+  // spin on the reply; a wave that ended on its idle timeout just as this request arrived
+  // is relaunched, and serves it first
+  uint64_t spins = 0, relaunches = 0;
+  std::chrono::steady_clock::time_point t0;
+  while (w_load(&w->mail->resp) != r) {
+    if ((++spins & 4095u) == 0u) {
+      if (!w_load(&w->mail->alive) && w_load(&w->mail->resp) != r) {
+        if (++relaunches > 3) return MGENX_EDEVICE;
+        const int rc = worker_launch(w, r - 1u);
+        if (rc != MGENX_OK) return rc;
+      }
+      const auto now = std::chrono::steady_clock::now();
+      if (spins == 4096u) t0 = now;
+      else if (now - t0 > std::chrono::seconds(10)) {  // never answered
+        snprintf(w->ctx->err, sizeof(w->ctx->err), "worker: no reply to request %u", r);
+        return MGENX_EDEVICE;
+      }
+    }
+    __builtin_ia32_pause();
+  }
+  return w_load(&w->mail->status) == 0u ? MGENX_OK : MGENX_EDEVICE;
+}
+
+int mgenx_worker_create(mgenx_ctx* ctx, uint32_t idle_ms, mgenx_worker** out) {
+  if (!ctx || !out) return MGENX_EINVAL;
+  *out = nullptr;
+  hipSetDevice(ctx->device);
+  mgenx_worker* w = new mgenx_worker();
+  w->ctx = ctx;
+  w->idle_ticks = (uint64_t)(idle_ms ? idle_ms : 1u) * 100000ull;
+  if (hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipHostMalloc((void**)&w->mail, sizeof(mgenx::WMail),
+                    hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&w->mail_dev, w->mail, 0) != hipSuccess) {
+    mgenx_worker_destroy(w);
+    return MGENX_ENOMEM;
+  }
+  memset(w->mail, 0, sizeof(mgenx::WMail));
+  *out = w;
+  return MGENX_OK;
+}
+
+int mgenx_worker_destroy(mgenx_worker* w) {
+  if (!w) return MGENX_EINVAL;
+  if (w->launched && w->mail) {
+    hipSetDevice(w->ctx->device);
+    if (w_load(&w->mail->alive)) {  // ask the wave to end; it may end on its own meanwhile
+      uint32_t r = w->seq + 1u;
+      if (r == 0u) r = 1u;
+      w->seq = r;
+      w->mail->op = mgenx::kWorkStop;
+      w_store(&w->mail->req, r);
+    }
+    (void)hipStreamSynchronize(w->stream);
+  }
+  if (w->mail) (void)hipHostFree(w->mail);
+  if (w->stream) (void)hipStreamDestroy(w->stream);
+  delete w;
+  return MGENX_OK;
+}
+
+int mgenx_worker_unpack(mgenx_worker* w, const uint8_t* msg, uint32_t len, mgenx_unpacked* out) {
+  if (!w || !out || (len && !msg) || len > MGENX_WORKER_MAX_BYTES) return MGENX_EINVAL;
+  const uint32_t n = len < mgenx::kWorkerHdrBytes ? len : mgenx::kWorkerHdrBytes;
+  if (n) memcpy(w->mail->data, msg, n);  // Unpack reads the header bytes only
+  const int rc = worker_call(w, mgenx::kWorkUnpack, len, 0u);
+  if (rc == MGENX_OK) memcpy(out, &w->mail->unpacked, sizeof(*out));
+  return rc;
+}
+
+int mgenx_worker_crc32(mgenx_worker* w, const uint8_t* data, uint32_t len, uint32_t state_in,
+                       uint32_t* state_out) {
+  if (!w || !state_out || (len && !data) || len > MGENX_WORKER_MAX_BYTES) return MGENX_EINVAL;
+  if (len) memcpy(w->mail->data, data, len);
+  const int rc = worker_call(w, mgenx::kWorkCrc32, len, state_in);
+  if (rc == MGENX_OK) *state_out = w_load(&w->mail->crc);
+  return rc;
 }
 
 int mgenx_crc32_batch(mgenx_ctx* ctx, const uint8_t* dev_data, const uint64_t* dev_off,

@@ -1,0 +1,138 @@
+"""GPU: the resident single-message worker (mgenx_worker_*) -- MgenMsg::Unpack and
+ComputeCRC32 of one host message per call, served by a wave kept on the device.  Parity:
+every unpack vector of the golden matrix equals the batch kernels' decode of the same bytes
+(mgenx_unpack_batch, MGENX_OPT_SKIP_CRC: Unpack alone, every column); CRC-32 running states
+equal zlib's; the wave's idle exit and relaunch keep answering."""
+import os
+import time
+import zlib
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden", "udp_matrix.npz")
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    return torch
+
+
+@pytest.fixture(scope="module")
+def eng(torch):
+    from mgen_amd import Engine
+    e = Engine(0)
+    yield e
+    e.close()
+
+
+FIELDS = ("flow_id", "seq_num", "tx_sec", "tx_usec", "msg_len", "dst_port", "payload_len",
+          "hdr_len", "host_port", "flags", "err", "dst_type", "dst_len", "payload_type",
+          "gps_status", "host_type", "host_len", "decoded", "lat_raw", "lon_raw", "alt",
+          "payload_off")
+
+
+def test_worker_unpack_equals_batch_on_golden_matrix(torch, eng):
+    from mgen_amd import OPT_SKIP_CRC
+    g = dict(np.load(GOLD, allow_pickle=False))
+    slab, offs, lens = g["unpack_slab"], g["unpack_offs"], g["unpack_lens"]
+    n = len(offs)
+    d = torch.from_numpy(slab.copy()).cuda()
+    cols = eng.unpack(d, n, rec_off=torch.from_numpy(offs.view(np.int64).copy()).cuda(),
+                      rec_len=torch.from_numpy(lens.view(np.int32).copy()).cuda(),
+                      opts=OPT_SKIP_CRC, ext=True)
+    torch.cuda.synchronize()
+    from mgen_amd import UNPACKED_DTYPE
+    # the batch columns as the worker's field types (same widths, unsigned where it is)
+    want = {k: cols[k].cpu().numpy().view(UNPACKED_DTYPE[k]) for k in FIELDS}
+    want["dst_addr"] = cols["dst_addr"].cpu().numpy()
+    want["host_addr"] = cols["host_addr"].cpu().numpy()
+    w = eng.worker()
+    try:
+        for i in range(n):
+            msg = slab[int(offs[i]):int(offs[i]) + int(lens[i])].tobytes()
+            u = w.unpack(msg)
+            for k in FIELDS:
+                assert u[k] == want[k][i], (i, k, u[k], want[k][i])
+            da = want["dst_addr"].reshape(n, 16)[i]
+            ha = want["host_addr"].reshape(n, 16)[i]
+            assert bytes(u["dst_addr"]) == da.tobytes(), i
+            assert bytes(u["host_addr"]) == ha.tobytes(), i
+    finally:
+        w.close()
+
+
+def _crc_state(data: bytes, state: int) -> int:
+    """MgenMsg::ComputeCRC32(checksum, buf, len) (mgenMsg.cpp:524-541) through zlib: the
+    running register starts from ~0 when checksum == 0, and is not finally inverted."""
+    v = zlib.crc32(data, (~state) & 0xFFFFFFFF if state else 0)
+    return (~v) & 0xFFFFFFFF
+
+
+def test_worker_crc32_vs_zlib(torch, eng):
+    rng = np.random.default_rng(7)
+    w = eng.worker()
+    try:
+        for L in (0, 1, 3, 4, 15, 16, 17, 63, 64, 65, 1020, 1024, 8188, 8192, 16383, 16384,
+                  16385, 40000, 65535, 65536):
+            data = rng.integers(0, 256, L, dtype=np.uint8).tobytes()
+            for st in (0, int(rng.integers(1, 1 << 32))):
+                assert w.crc32(data, st) == _crc_state(data, st), (L, st)
+    finally:
+        w.close()
+
+
+def test_worker_idle_exit_and_relaunch(torch, eng):
+    """A wave with a 2 ms idle timeout ends between calls; the next call relaunches it and is
+    answered correctly, many times over, with unpack and crc32 interleaved."""
+    g = dict(np.load(GOLD, allow_pickle=False))
+    slab, offs, lens = g["unpack_slab"], g["unpack_offs"], g["unpack_lens"]
+    w = eng.worker(idle_ms=2)
+    try:
+        first = None
+        for k in range(12):
+            msg = slab[int(offs[k]):int(offs[k]) + int(lens[k])].tobytes()
+            u = w.unpack(msg)
+            if first is None:
+                first = (k, u.copy())
+            assert w.crc32(msg, 0) == _crc_state(msg, 0)
+            time.sleep(0.004 if k % 2 else 0.0)
+        k, u0 = first
+        msg = slab[int(offs[k]):int(offs[k]) + int(lens[k])].tobytes()
+        assert w.unpack(msg).tobytes() == u0.tobytes()
+    finally:
+        w.close()
+
+
+def test_worker_latency_report(torch, eng):
+    """Median per-call time of worker unpack / crc32 of a 1024-B record (printed; the bound
+    is loose: the shim_latency program reports the numbers)."""
+    from mgen_amd.workloads import udp_fixed
+    from oracle import oracle as O
+    tmpl, pool, desc = udp_fixed(4, 1024)
+    slab, _ = O.udp_pack_batch(tmpl, desc, pool, 4 * 1024, stride=1024, checksum=True)
+    msg = slab[:1024].tobytes()
+    w = eng.worker()
+    try:
+        for _ in range(100):
+            w.unpack(msg)
+        ts = []
+        for _ in range(2000):
+            t = time.perf_counter()
+            w.unpack(msg)
+            ts.append(time.perf_counter() - t)
+        tc = []
+        for _ in range(2000):
+            t = time.perf_counter()
+            w.crc32(msg[:1020], 0)
+            tc.append(time.perf_counter() - t)
+        um, cm = np.median(ts) * 1e6, np.median(tc) * 1e6
+        print(f"worker unpack median {um:.2f} us, crc32 median {cm:.2f} us (Python call included)")
+        assert um < 200 and cm < 200
+    finally:
+        w.close()
