@@ -550,9 +550,10 @@ int mgenx_flow_export(mgenx_ctx* ctx, const mgenx_flow_state* dev_flows, uint32_
  * the destination address from the dst_addr column when given, else from the rows'
  * dst_addr4 -- exact for IPv4 destinations; a record whose dst_len exceeds 4 then maps to
  * MGENX_FLOW_NONE (pass dst_addr when IPv6 destinations can occur).
- * A table holds at most its max_flows keys (rounded up to half its power-of-two slot count) and
- * probes at most 1024 slots per lookup: a record whose key finds no room maps to
- * MGENX_FLOW_NONE (an undersized table; the caller redoes the batch on a larger one). */
+ * A table takes new keys while it holds fewer than its max_flows (rounded up to half its
+ * power-of-two slot count; keys created concurrently may pass that bound together) and probes
+ * at most 1024 slots per lookup: a record whose key finds no room maps to MGENX_FLOW_NONE (an
+ * undersized table; the caller redoes the batch on a larger one). */
 #define MGENX_FLOW_NONE 0xFFFFFFFFu
 typedef struct mgenx_flow_table mgenx_flow_table;
 int mgenx_flow_table_create(mgenx_ctx* ctx, uint32_t max_flows, mgenx_flow_table** out);

@@ -164,13 +164,13 @@ __global__ void flowtab_insert_kernel(FlowSlot* __restrict__ tab, uint32_t cap_m
     FlowSlot& sl = tab[s];
     uint32_t st = __hip_atomic_load(&sl.state, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
     if (st == kSlotEmpty) {
-      // the key is not in the table: a new key, if the table has room for one (reserved in
-      // n_new before the claim, released again when another thread claims the slot first)
-      const uint32_t r = __hip_atomic_fetch_add(n_new, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (*n_flows_before + r >= (cap_mask + 1u) / 2u) {
-        __hip_atomic_fetch_sub(n_new, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
+      // the key is not in the table: a new key, if the table has room for one.  (A soft
+      // bound: keys created concurrently may pass it together.  A reservation before the
+      // claim would also count the records of one new key that race for its slot, and refuse
+      // some of them -- the first record among them, which numbers the key.)
+      const uint32_t held = *n_flows_before +
+          __hip_atomic_load(n_new, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (held >= (cap_mask + 1u) / 2u) break;
       uint32_t exp = kSlotEmpty;
       if (__hip_atomic_compare_exchange_strong(&sl.state, &exp, kSlotBusy, __ATOMIC_ACQ_REL,
                                                __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) {
@@ -181,10 +181,10 @@ __global__ void flowtab_insert_kernel(FlowSlot* __restrict__ tab, uint32_t cap_m
         __hip_atomic_store(&sl.is_new, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&sl.index, kSlotBusy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&sl.state, 1u + s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(n_new, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         rec_slot[i] = s;
         return;
       }
-      __hip_atomic_fetch_sub(n_new, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       st = exp;
     }
     // a slot being written: wait (bounded) until its key is published

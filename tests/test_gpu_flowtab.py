@@ -128,8 +128,9 @@ def test_flow_lookup_from_rows(torch, eng):
 
 def test_flow_lookup_undersized_table_is_bounded(torch, eng):
     """More distinct keys than a table holds: a table for 64 flows (128 slots)
-    takes 64 keys and maps the rest to MGENX_FLOW_NONE, promptly -- no record walks the whole
-    table -- and the keys it took keep their indices in a second call."""
+    takes about 64 keys (a soft bound: keys created together may pass it) and maps the rest to
+    MGENX_FLOW_NONE, promptly -- no record walks the whole table -- and the keys it took keep
+    their indices in a second call."""
     import time
     n, n_keys = 400_000, 150_000       # more than 2 x pcap2mgen's first table (65,536 flows)
     fid = (np.arange(n) % n_keys + 1).astype(np.uint32)
@@ -151,7 +152,7 @@ def test_flow_lookup_undersized_table_is_bounded(torch, eng):
         got = idx.cpu().numpy().view(np.uint32)
         held = got != 0xFFFFFFFF
         k = int(nf.cpu()[0])
-        assert 0 < k <= 64
+        assert 64 <= k <= 128
         assert len(np.unique(fid[held])) == k and got[held].max() == k - 1
         # every record of a held key resolves to that key's index
         first = {}
