@@ -280,8 +280,10 @@ int mgenx_crc32_batch(mgenx_ctx* ctx, const uint8_t* dev_data, const uint64_t* d
  *                           fresh MgenMsg: the members it assigned (`decoded`, MGENX_DEC_*) and
  *                           err (MgenMsg::Error; 0 = Unpack returned true); no CRC check
  *   mgenx_worker_crc32   <- MgenMsg::ComputeCRC32 (include/mgenMsg.h:201-203, mgenMsg.cpp:
- *                           524-541): the running checksum in and out */
+ *                           524-541): the running checksum in and out
+ *   mgenx_worker_pack    <- MgenMsg::Pack alone (below) */
 #define MGENX_WORKER_MAX_BYTES 65536u
+#define MGENX_WORKER_PACK_MAX  16384u   /* mgenx_worker_pack's largest bufferLen */
 typedef struct {
     uint32_t flow_id, seq_num, tx_sec, tx_usec, payload_off;
     uint32_t lat_raw, lon_raw;
@@ -297,6 +299,16 @@ int mgenx_worker_destroy(mgenx_worker* w);
 int mgenx_worker_unpack(mgenx_worker* w, const uint8_t* msg, uint32_t len, mgenx_unpacked* out);
 int mgenx_worker_crc32(mgenx_worker* w, const uint8_t* data, uint32_t len, uint32_t state_in,
                        uint32_t* state_out);
+/* MgenMsg::Pack (include/mgenMsg.h:108, mgenMsg.cpp:83-313) of one message, as mgenx_pack_msgs
+ * with n = 1: the message as a template (its payload bytes at `payload`, payload_off ignored)
+ * and a descriptor; bufferLen, the tx_checksum argument, MGENX_PACK_CHECKSUM /
+ * MGENX_PACK_RANDOM_FILL and the fill time.  out (bufferLen bytes) receives *ret bytes
+ * (Pack's return; 0: failed, nothing written); *tx_crc the tx_checksum after; *state
+ * packet_header_len | flags << 16.  bufferLen <= MGENX_WORKER_PACK_MAX. */
+int mgenx_worker_pack(mgenx_worker* w, const mgenx_flow_tmpl* tmpl, const uint8_t* payload,
+                      const mgenx_pack_desc* desc, uint32_t buf_len, uint32_t crc_in,
+                      uint32_t opts, uint32_t fill_time, uint8_t* out, uint32_t* ret,
+                      uint32_t* tx_crc, uint32_t* state);
 
 /* ---- the TCP receiver's persistent rx_msg ----
  * MgenTcpTransport decodes every message of a connection into ONE MgenMsg (rx_msg,

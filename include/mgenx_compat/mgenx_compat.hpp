@@ -8,8 +8,8 @@
 // the device in one hipMemcpyAsync, processed by libmgenx's gfx950 kernels
 // (mgenx_pack_msgs, mgenx_unpack_batch, mgenx_crc32_update, mgenx_flow_reduce) and copied
 // back in one more; the call returns when the results are in the caller's buffers.  A single
-// Unpack or ComputeCRC32 (what an unchanged transport calls per datagram) goes instead to the
-// resident worker (mgenx_worker_*): one wave kept on the device that polls a pinned mailbox,
+// Pack, Unpack or ComputeCRC32 (what an unchanged transport calls per message) goes instead to
+// the resident worker (mgenx_worker_*): one wave kept on the device that polls a pinned mailbox,
 // so the call pays no launch and no copy.  There is no host implementation of the codec here:
 // without a GPU the calls throw.
 //
@@ -91,6 +91,14 @@ class Engine {
             PackOut* out) {
     if (n == 0) return;
     Init();
+    const uint32_t blen0 = in[0].buf_len ? in[0].buf_len : in[0].desc.msg_len;
+    if (n == 1 && blen0 <= MGENX_WORKER_PACK_MAX && Worker()) {  // one message: the worker
+      Check(mgenx_worker_pack(worker_, &in[0].tmpl, in[0].payload, &in[0].desc, blen0,
+                              in[0].crc_in, opts, fill_time, dst[0], &out[0].ret, &out[0].tx_crc,
+                              &out[0].state),
+            "mgenx_worker_pack");
+      return;
+    }
     if ((opts & MGENX_PACK_RANDOM_FILL) && (!fill_set_ || fill_time_ != fill_time)) {
       Check(mgenx_set_fill_time(ctx_, fill_time), "mgenx_set_fill_time");
       fill_set_ = true;

@@ -44,6 +44,7 @@ EXPORTED_SYMBOLS = (
     "mgenx_pcap_parse", "mgenx_binlog_index", "mgenx_convert_binary_log",
     "mgenx_unpack_last_kernel", "mgenx_pcap_snap", "mgenx_flow_reduce_rows",
     "mgenx_worker_create", "mgenx_worker_destroy", "mgenx_worker_unpack", "mgenx_worker_crc32",
+    "mgenx_worker_pack",
 )
 DIAG_SYMBOLS = ("mgenx_set_tuning", "mgenx_diag_stream_read", "mgenx_diag_group_rw")
 
@@ -131,6 +132,8 @@ def load(diag: bool = False):
     L.mgenx_worker_destroy.argtypes = [P]
     L.mgenx_worker_unpack.argtypes = [P, ctypes.c_char_p, u32, P]
     L.mgenx_worker_crc32.argtypes = [P, ctypes.c_char_p, u32, u32, ctypes.POINTER(u32)]
+    L.mgenx_worker_pack.argtypes = [P, P, ctypes.c_char_p, P, u32, u32, u32, u32, P,
+                                    ctypes.POINTER(u32), ctypes.POINTER(u32), ctypes.POINTER(u32)]
     _libs[path] = L
     return L
 
@@ -805,6 +808,20 @@ class Worker:
                                                         ctypes.byref(out)),
                         "mgenx_worker_crc32")
         return out.value
+
+    def pack(self, tmpl, payload: bytes, desc, buf_len: int, crc_in: int = 0, opts: int = 0,
+             fill_time: int = 0):
+        """MgenMsg::Pack of one message (mgenx_worker_pack): (bytes, tx_crc, state).  tmpl /
+        desc: one-element TMPL_DTYPE / DESC_DTYPE arrays."""
+        t = np.ascontiguousarray(tmpl)
+        d = np.ascontiguousarray(desc)
+        out = np.zeros(max(buf_len, 1), np.uint8)
+        ret, tx, st = ctypes.c_uint32(0), ctypes.c_uint32(0), ctypes.c_uint32(0)
+        self.eng._check(self.eng.lib.mgenx_worker_pack(
+            self.w, ctypes.c_void_p(t.ctypes.data), bytes(payload), ctypes.c_void_p(d.ctypes.data),
+            buf_len, crc_in, opts, fill_time, ctypes.c_void_p(out.ctypes.data), ctypes.byref(ret),
+            ctypes.byref(tx), ctypes.byref(st)), "mgenx_worker_pack")
+        return out[:ret.value].tobytes(), tx.value, st.value
 
     def close(self):
         if self.w:

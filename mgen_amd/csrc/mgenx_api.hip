@@ -944,7 +944,8 @@ static int worker_launch(mgenx_worker* w, uint32_t start) {
   if (w->launched && hipStreamSynchronize(w->stream) != hipSuccess) return MGENX_EDEVICE;
   w_store(&w->mail->alive, 1u);
   hipError_t e = mgenx::launch_worker(w->mail_dev, w->ctx->d_tabs + 1024, w->ctx->d_bytetab,
-                                      w->ctx->d_xpow, start, w->idle_ticks, w->stream);
+                                      w->ctx->d_xpow, w->ctx->d_rtab, start, w->idle_ticks,
+                                      w->stream);
   if (e != hipSuccess) return set_err(w->ctx, e, "worker launch");
   w->launched = true;
   return MGENX_OK;
@@ -1032,6 +1033,35 @@ int mgenx_worker_unpack(mgenx_worker* w, const uint8_t* msg, uint32_t len, mgenx
   const int rc = worker_call(w, mgenx::kWorkUnpack, len, 0u);
   if (rc == MGENX_OK) memcpy(out, &w->mail->unpacked, sizeof(*out));
   return rc;
+}
+
+int mgenx_worker_pack(mgenx_worker* w, const mgenx_flow_tmpl* tmpl, const uint8_t* payload,
+                      const mgenx_pack_desc* desc, uint32_t buf_len, uint32_t crc_in,
+                      uint32_t opts, uint32_t fill_time, uint8_t* out, uint32_t* ret,
+                      uint32_t* tx_crc, uint32_t* state) {
+  if (!w || !tmpl || !desc || !ret || !tx_crc || !state || buf_len > MGENX_WORKER_PACK_MAX ||
+      (buf_len && !out) || (tmpl->has_payload && tmpl->payload_len && !payload))
+    return MGENX_EINVAL;
+  if (opts & MGENX_PACK_RANDOM_FILL) {  // the rand() stream of this fill time (cached)
+    const int rc = mgenx_set_fill_time(w->ctx, fill_time);
+    if (rc != MGENX_OK) return rc;
+  }
+  mgenx::WPackReq& q = w->mail->pack;
+  q.tmpl = *tmpl;
+  q.tmpl.payload_off = 0;  // the payload travels in the mailbox
+  q.desc = *desc;
+  q.buf_len = buf_len;
+  q.crc_in = crc_in;
+  q.opts = opts & (MGENX_PACK_CHECKSUM | MGENX_PACK_RANDOM_FILL);
+  q.rsv = 0;
+  if (tmpl->has_payload && tmpl->payload_len) memcpy(w->mail->data, payload, tmpl->payload_len);
+  const int rc = worker_call(w, mgenx::kWorkPack, buf_len, 0u);
+  if (rc != MGENX_OK) return rc;
+  *ret = w_load(&w->mail->ret);
+  *tx_crc = w_load(&w->mail->tx_crc);
+  *state = w_load(&w->mail->state);
+  if (*ret) memcpy(out, w->mail->out, *ret);
+  return MGENX_OK;
 }
 
 int mgenx_worker_crc32(mgenx_worker* w, const uint8_t* data, uint32_t len, uint32_t state_in,

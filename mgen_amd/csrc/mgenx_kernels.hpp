@@ -117,9 +117,15 @@ hipError_t launch_tcp_tail(uint8_t* out, const uint64_t* foff, const uint32_t* f
                            const uint32_t* byte_tab, const uint32_t* a4_tab, const uint32_t* xpow,
                            const uint32_t* ia, const uint32_t* rcrc, hipStream_t s);
 // the resident single-message worker (mgenx_worker.hip): its mailbox in pinned host memory
-constexpr uint32_t kWorkUnpack = 1, kWorkCrc32 = 2, kWorkStop = 0xFFFFFFFFu;
+constexpr uint32_t kWorkUnpack = 1, kWorkCrc32 = 2, kWorkPack = 3, kWorkStop = 0xFFFFFFFFu;
 constexpr uint32_t kWorkerMaxBytes = MGENX_WORKER_MAX_BYTES;
 constexpr uint32_t kWorkerHdrBytes = 1024;  // Unpack reads at most the first 24+255+4+255+19 B
+constexpr uint32_t kWorkerPackMax = MGENX_WORKER_PACK_MAX;  // Pack's bufferLen (built in LDS)
+struct WPackReq {         // mgenx_pack_msgs' inputs for one message (payload in WMail::data)
+  mgenx_flow_tmpl tmpl;   // words 0..16
+  mgenx_pack_desc desc;   // words 17..21
+  uint32_t buf_len, crc_in, opts, rsv;
+};
 struct alignas(64) WMail {
   uint32_t req;     // request number: the host writes it last (0 before the first)
   uint32_t op, len, arg;
@@ -128,14 +134,18 @@ struct alignas(64) WMail {
   uint32_t status;  // 0 served
   uint32_t crc;     // crc32 reply
   uint32_t alive;   // 1 while a launched worker runs (it clears the word when it ends)
-  uint32_t rsv1[12];
+  uint32_t ret, tx_crc, state;  // pack reply (mgenx_pack_msgs' out_len, tx_crc, state)
+  uint32_t rsv1[9];
   mgenx_unpacked unpacked;
   uint8_t rsv2[128 - sizeof(mgenx_unpacked)];
+  WPackReq pack;
+  uint8_t rsv3[128 - sizeof(WPackReq)];
   uint8_t data[kWorkerMaxBytes + 64];  // the message; 64 bytes of slack for whole 16-B loads
+  uint8_t out[kWorkerPackMax + 64];    // a packed message
 };
 hipError_t launch_worker(WMail* m, const uint32_t* a4_tab, const uint32_t* byte_tab,
-                         const uint32_t* xpow, uint32_t start, uint64_t idle_ticks,
-                         hipStream_t stream);
+                         const uint32_t* xpow, const uint8_t* rtab, uint32_t start,
+                         uint64_t idle_ticks, hipStream_t stream);
 hipError_t launch_crc32(const uint8_t* data, const uint64_t* off, const uint32_t* len, uint32_t n,
                         const uint32_t* byte_tab, const uint32_t* a4_tab, const uint32_t* xpow,
                         const uint32_t* state_in, uint32_t* out, hipStream_t stream);

@@ -49,11 +49,38 @@ __device__ __forceinline__ u32x4_t load_masked(const uint8_t* p, uint32_t o, uin
   return v;
 }
 
+static_assert(kWorkerPackMax <= kPiece, "a packed message is built in one LDS piece");
+static_assert(sizeof(WPackReq) == 104, "WPackReq: template, descriptor and four words");
+
+// The wave's raw CRC (zero register) of LDS bytes [0, n): lane partials through the A_4
+// tables, shifted by the bytes after them and XOR-ed (crc(A || B) = x^(8|B|) crc(A) ^ crc(B)).
+__device__ __forceinline__ uint32_t wave_crc_raw(const uint8_t* buf, uint32_t n, uint32_t lane,
+                                                 const uint32_t* s_a4, const uint32_t* s_tab,
+                                                 const uint32_t* xpow) {
+  const uint32_t chunk = (((n + 63u) >> 6) + 3u) & ~3u;
+  const uint32_t lo = min(lane * chunk, n), hi = min(lo + chunk, n);
+  uint32_t c = 0;
+  uint32_t k = lo;
+  for (; k + 4u <= hi; k += 4u) {
+    const uint32_t x = c ^ *reinterpret_cast<const uint32_t*>(buf + k);
+    c = s_a4[x & 0xffu] ^ s_a4[256 + ((x >> 8) & 0xffu)] ^ s_a4[512 + ((x >> 16) & 0xffu)] ^
+        s_a4[768 + (x >> 24)];
+  }
+  for (; k < hi; k++) c = s_tab[(c ^ buf[k]) & 0xffu] ^ (c >> 8);
+  const uint32_t after = n - hi;
+  if (c && after) c = multmodp(xpow8(after, xpow), c);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) c ^= (uint32_t)__shfl_xor((int)c, o);
+  return c;
+}
+
 __global__ void __launch_bounds__(64)
 worker_kernel(WMail* m, const uint32_t* __restrict__ a4_tab, const uint32_t* __restrict__ byte_tab,
-              const uint32_t* __restrict__ xpow, uint32_t start, uint64_t idle_ticks) {
+              const uint32_t* __restrict__ xpow, const uint8_t* __restrict__ rtab, uint32_t start,
+              uint64_t idle_ticks) {
   __shared__ uint32_t s_a4[1024], s_tab[256];
   __shared__ __attribute__((aligned(16))) uint8_t buf[kPiece];
+  __shared__ __attribute__((aligned(16))) uint32_t rq[32];
   const uint32_t lane = threadIdx.x;
   for (uint32_t e = lane; e < 1024u; e += 64u) s_a4[e] = a4_tab[e];
   for (uint32_t e = lane; e < 256u; e += 64u) s_tab[e] = byte_tab[e];
@@ -146,25 +173,145 @@ worker_kernel(WMail* m, const uint32_t* __restrict__ a4_tab, const uint32_t* __r
         for (uint32_t k = 0; k < kPiece / 1024; k++)
           *reinterpret_cast<u32x4_t*>(buf + 1024u * k + 16u * lane) = v[k];
         __syncthreads();
-        const uint32_t chunk = (((pn + 63u) >> 6) + 3u) & ~3u;
-        const uint32_t lo = min(lane * chunk, pn), hi = min(lo + chunk, pn);
-        uint32_t c = 0;
-        uint32_t k = lo;
-        for (; k + 4u <= hi; k += 4u) {
-          const uint32_t x = c ^ *reinterpret_cast<const uint32_t*>(buf + k);
-          c = s_a4[x & 0xffu] ^ s_a4[256 + ((x >> 8) & 0xffu)] ^ s_a4[512 + ((x >> 16) & 0xffu)] ^
-              s_a4[768 + (x >> 24)];
-        }
-        for (; k < hi; k++) c = s_tab[(c ^ buf[k]) & 0xffu] ^ (c >> 8);
-        const uint32_t after = pn - hi;
-        if (c && after) c = multmodp(xpow8(after, xpow), c);
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) c ^= (uint32_t)__shfl_xor((int)c, o);
+        const uint32_t c = wave_crc_raw(buf, pn, lane, s_a4, s_tab, xpow);
         acc = (acc ? multmodp(xpow8(pn, xpow), acc) : 0u) ^ c;
         __syncthreads();
       }
       uint32_t st = arg == 0u ? 0xFFFFFFFFu : arg;  // ComputeCRC32: 0 restarts from ~0
       crc = acc ^ (len ? multmodp(xpow8(len, xpow), st) : st);
+    } else if (op == kWorkPack) {
+      // MgenMsg::Pack alone (mgenMsg.cpp:83-313) as the batch pack kernel's meta phase walks
+      // it (mgenx_pack.hip: layout, truncation, the payload_len zeroing, RANDOM_FILL after two
+      // zero bytes, CHECKSUM flag, ComputeCRC32 over msgLen - 4 with LAST_BUFFER), with the
+      // message built whole in LDS and checksummed by the wave
+      if (lane < 8u)
+        *reinterpret_cast<u32x4_t*>(rq + 4u * lane) =
+            *reinterpret_cast<const u32x4_t*>(reinterpret_cast<const uint8_t*>(&m->pack) + 16u * lane);
+      __syncthreads();
+      const uint32_t* tw = rq;  // the template, 17 words (mgenx_flow_tmpl)
+      const uint32_t d_seq = rq[18], d_sec = rq[19], d_usec = rq[20];
+      const uint32_t d_len = rq[21] & 0xffffu, d_flags = (rq[21] >> 16) & 0xffu;
+      const uint32_t msgLen = rq[22], crc_in = rq[23], popts = rq[24];
+      const bool ck = (popts & MGENX_PACK_CHECKSUM) != 0, rf = (popts & MGENX_PACK_RANDOM_FILL) != 0;
+      const uint32_t t_flow = tw[0], t_dtype = tw[1] & 0xffu, t_dlen = (tw[1] >> 8) & 0xffu;
+      const uint32_t t_dport = tw[1] >> 16;
+      const uint32_t t_htype = tw[6] & 0xffu, t_hlen = (tw[6] >> 8) & 0xffu, t_hport = tw[6] >> 16;
+      const uint32_t t_gps = tw[14] & 0xffu, t_ptype = (tw[14] >> 8) & 0xffu;
+      const uint32_t t_plen = tw[14] >> 16, t_has = tw[16] & 0xffu;
+      uint32_t flags = d_flags;  // Pack alone: the caller's flags (LAST_BUFFER as it set it)
+      const bool dst_ok = t_dtype == 1u || t_dtype == 2u;     // :146-148
+      const uint32_t D = t_dlen > 16u ? 16u : t_dlen;
+      const bool hv = t_htype == 1u || t_htype == 2u;
+      const uint32_t H = hv ? (t_hlen > 16u ? 16u : t_hlen) : 0u;
+      uint32_t len = 24u + D;
+      const bool host_in = msgLen >= len + H + 4u;              // :182-200
+      const bool failed = !dst_ok || (!host_in && msgLen < len);  // :207-210
+      bool trunc = !host_in;
+      const uint32_t host_at = len;
+      if (!trunc) len += 4u + H;
+      const uint32_t gps_at = len;
+      const bool gps_in = !trunc && msgLen >= len + 13u;        // :219-241
+      trunc = trunc || !gps_in;
+      if (!trunc) len += 13u;
+      const uint32_t pt_at = len;
+      const bool pt_in = !trunc && msgLen >= len + 1u;          // :243-251
+      trunc = trunc || !pt_in;
+      if (!trunc) len += 1u;
+      const uint32_t pl_at = len;
+      const bool pl_in = !trunc && msgLen >= len + 2u;          // :252-263
+      trunc = trunc || !pl_in;
+      if (!trunc) len += 2u;
+      const bool pay = !trunc && t_has && msgLen >= len + t_plen;  // :264-273
+      const uint32_t pend = pay ? len + t_plen : len;
+      const uint32_t ret = failed ? 0u : msgLen;
+      const bool rfill = rf && !trunc;  // truncated messages are zero-filled (:205-262)
+      if (ret > kWorkerPackMax) {
+        status = 2;  // too long for the LDS build: the caller takes the batch path
+      } else if (ret) {
+        // 1. fill [0, msgLen): zeros, or from pend two zeros then the rand() stream
+        for (uint32_t o = 16u * lane; o < ret; o += 1024u) {
+          uint32_t w[4] = {0u, 0u, 0u, 0u};
+          if (rfill && o + 16u > pend) {
+#pragma unroll
+            for (int j = 0; j < 16; j++) {
+              const uint32_t b = o + (uint32_t)j;
+              const uint32_t v = b >= pend ? rtab[14u + b - pend] : 0u;
+              w[j >> 2] |= v << (8 * (j & 3));
+            }
+          }
+          *reinterpret_cast<u32x4_t*>(buf + o) = u32x4_t{w[0], w[1], w[2], w[3]};
+        }
+        __syncthreads();
+        // 2. the payload [len, pend) from the mailbox
+        if (pay)
+          for (uint32_t o = 16u * lane; o < t_plen; o += 1024u) {
+            const u32x4_t v = load_masked(m->data + o, o, t_plen);
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+            const uint32_t nb = min(16u, t_plen - o);
+            for (uint32_t j = 0; j < nb; j++) buf[len + o + j] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
+          }
+        // 3. the header (one lane)
+        if (!trunc && ck && msgLen > pend + 4u) flags |= MGENX_FLAG_CHECKSUM;  // :295-301
+        if (lane == 0) {
+          auto put8 = [&](uint32_t at, uint32_t v) { buf[at] = (uint8_t)v; };
+          auto put16 = [&](uint32_t at, uint32_t v) { put8(at, v >> 8); put8(at + 1, v); };
+          auto put32 = [&](uint32_t at, uint32_t v) {
+            put8(at, v >> 24); put8(at + 1, v >> 16); put8(at + 2, v >> 8); put8(at + 3, v);
+          };
+          put16(0, d_len);                                       // mgenMsg.cpp:97-131
+          put8(2, 2);
+          put8(3, flags);
+          put32(4, t_flow);
+          put32(8, d_seq);
+          put32(12, d_sec);
+          put32(16, d_usec);
+          put16(20, t_dport);
+          put8(22, t_dtype);
+          put8(23, D);
+          for (uint32_t k = 0; k < D; k++) put8(24 + k, tw[2 + (k >> 2)] >> (8 * (k & 3)));
+          if (host_in) {
+            put16(host_at, hv ? t_hport : 0u);
+            put8(host_at + 2, hv ? t_htype : 0u);
+            put8(host_at + 3, H);
+            for (uint32_t k = 0; k < H; k++) put8(host_at + 4 + k, tw[7 + (k >> 2)] >> (8 * (k & 3)));
+          }
+          if (gps_in) {
+            put32(gps_at, tw[11]);
+            put32(gps_at + 4, tw[12]);
+            put32(gps_at + 8, tw[13]);
+            put8(gps_at + 12, t_gps);
+          }
+          if (pt_in) put8(pt_at, t_ptype);
+          if (pl_in) put16(pl_at, t_plen);
+          if (!trunc && !pay) {                                  // payload_len zeroed
+            put8(len - 2, 0);
+            put8(len - 1, 0);
+          }
+        }
+        __syncthreads();
+        // 4. ComputeCRC32 (checksum on, a whole header)
+        uint32_t tx = crc_in;
+        if (ck && !trunc) {
+          const uint32_t crc_len = (flags & MGENX_FLAG_LAST_BUFFER) ? msgLen - 4u : msgLen;
+          const uint32_t raw = wave_crc_raw(buf, crc_len, lane, s_a4, s_tab, xpow);
+          const uint32_t init = crc_in == 0u ? 0xFFFFFFFFu : crc_in;  // :530-533
+          tx = raw ^ (crc_len ? multmodp(xpow8(crc_len, xpow), init) : init);
+          flags &= ~(uint32_t)MGENX_FLAG_LAST_BUFFER;
+        }
+        // 5. the message out
+        for (uint32_t o = 16u * lane; o < ret; o += 1024u)
+          *reinterpret_cast<u32x4_t*>(m->out + o) = *reinterpret_cast<const u32x4_t*>(buf + o);
+        if (lane == 0) {
+          st_sys(&m->ret, ret);
+          st_sys(&m->tx_crc, tx);
+          st_sys(&m->state, (uint32_t)len | (flags & 0xffu) << 16);
+        }
+        __syncthreads();
+      } else if (lane == 0) {  // Pack failed: nothing written
+        st_sys(&m->ret, 0u);
+        st_sys(&m->tx_crc, crc_in);
+        st_sys(&m->state, 0xFFFFu | (flags & 0xffu) << 16);
+      }
     } else {
       status = 1;
     }
@@ -180,10 +327,10 @@ worker_kernel(WMail* m, const uint32_t* __restrict__ a4_tab, const uint32_t* __r
 }
 
 hipError_t launch_worker(WMail* m, const uint32_t* a4_tab, const uint32_t* byte_tab,
-                         const uint32_t* xpow, uint32_t start, uint64_t idle_ticks,
-                         hipStream_t stream) {
-  hipLaunchKernelGGL(worker_kernel, dim3(1), dim3(64), 0, stream, m, a4_tab, byte_tab, xpow, start,
-                     idle_ticks);
+                         const uint32_t* xpow, const uint8_t* rtab, uint32_t start,
+                         uint64_t idle_ticks, hipStream_t stream) {
+  hipLaunchKernelGGL(worker_kernel, dim3(1), dim3(64), 0, stream, m, a4_tab, byte_tab, xpow, rtab,
+                     start, idle_ticks);
   return hipGetLastError();
 }
 

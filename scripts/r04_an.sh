@@ -10,7 +10,7 @@ step() {  # step <name> <timeout> <cmd...>
   tail -${TAILN:-15} "gpurun_out/$name.log"
   if [ $rc -ne 0 ]; then echo "STEP $name FAILED rc=$rc"; exit $rc; fi
 }
-step an_tests 600 python -u -m pytest tests/test_gpu_worker.py tests/test_gpu_analytics.py tests/test_gpu_flowtab.py tests/test_gpu_pcap.py tests/test_gpu_report.py tests/test_gpu_comm.py -m gpu -x -v --timeout 120 --timeout-method thread
+step an_tests 600 python -u -m pytest tests/test_gpu_worker.py tests/test_gpu_pack_msgs.py tests/test_gpu_analytics.py tests/test_gpu_flowtab.py tests/test_gpu_pcap.py tests/test_gpu_report.py tests/test_gpu_comm.py -m gpu -x -v --timeout 120 --timeout-method thread
 step c4 180 python -u scripts/c4_only.py
 step c4prof 240 rocprofv3 --kernel-trace --stats -d gpurun_out/c4prof -o c4 -- python3 -u scripts/c4_only.py
 find gpurun_out/c4prof -name '*kernel_stats.csv' -exec cp {} gpurun_out/c4_kernel_stats.csv \;

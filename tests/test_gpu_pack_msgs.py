@@ -204,3 +204,35 @@ def test_decoded_mask_matches_unpack_stages(torch, eng):
     bad = np.nonzero(dec != want)[0]
     assert bad.size == 0, (bad[:8], dec[bad[:8]], want[bad[:8]])
     assert (want & DEC_PLEN).any() and (want == DEC_MSGLEN).any() and not want.all()
+
+
+@pytest.mark.parametrize("checksum,rf", [(False, False), (True, False), (True, True)])
+def test_worker_pack_vs_oracle(torch, eng, oracle, checksum, rf):
+    """The resident worker's single-message Pack (mgenx_worker_pack: what the shim's
+    MgenMsg::Pack calls for one message) over the same matrix, against the oracle's or_pack:
+    return value, every byte, tx_checksum, flags and packet_header_len."""
+    from mgen_amd import PACK_CHECKSUM, PACK_RANDOM_FILL
+    cases = _cases()
+    tmpl, desc, pool = _tmpl_desc(cases)
+    opts = (PACK_CHECKSUM if checksum else 0) | (PACK_RANDOM_FILL if rf else 0)
+    w = eng.worker()
+    try:
+        for i, c in enumerate(cases):
+            t = tmpl[i:i + 1].copy()
+            po, pl = int(t["payload_off"][0]), int(t["payload_len"][0])
+            payload = pool[po:po + pl].tobytes() if t["has_payload"][0] else b""
+            b, tx, st = w.pack(t, payload, desc[i:i + 1], c["buf_len"], c["crc_in"], opts,
+                               FILL_TIME if rf else 0)
+            m = oracle.make_msg(msg_len=c["msg_len"], flow_id=100 + i, seq=c["seq"],
+                                tx_sec=1_700_000_000 + i, tx_usec=1000 * i, flags=c["flags"],
+                                dst=c["dst"], host=c["host"], lat=c["lat"], lon=c["lon"],
+                                alt=c["alt"], gps_status=c["gps"], payload=c["payload"])
+            r, buf, ck, flags, hl = oracle.pack(m, c["buf_len"], checksum=checksum,
+                                                tx_checksum=c["crc_in"], random_fill=rf,
+                                                fill_time=FILL_TIME)
+            assert len(b) == r and tx == ck, (i, c, len(b), r, hex(tx), hex(ck))
+            if r:
+                assert b == buf[:r], (i, c)
+                assert (st >> 16) & 0xFF == flags and st & 0xFFFF == hl, (i, c, hex(st))
+    finally:
+        w.close()
