@@ -409,6 +409,7 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
     }
     if (tge(rx, we)) {  // :180-256: report and restart the window
       const uint32_t seq_max = m.n ? m.get_last() : seq_start;
+      if (rcount < per_flow) {  // a kept report (latency_ave: flow_chain_kernel)
       const double duration = tdelta(rx, ws);
       uint64_t r_count;
       double r_rate, r_loss, r_min, r_max;
@@ -432,7 +433,7 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
         r_min = lmin;
         r_max = lmax;
       }
-      if (rcount < per_flow && lane == 0) {  // latency_ave: flow_chain_kernel
+      if (lane == 0) {
         const size_t slot = (size_t)f * per_flow + rcount;
         mgenx_flow_report* rp = reports + slot;
         rp->flow = f;
@@ -453,6 +454,7 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
         c.mc = msg_count;
         closes[slot] = c;
         if (report_rec) report_rec[slot] = order[pos];
+      }
       }
       rcount++;
       nrep++;
@@ -486,10 +488,12 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
   bool dirty = false;
   auto flush = [&]() {
     if (!dirty) return;
-    lmin = __builtin_fmin(lmin, WRing::wave_reduce_f64(pmin, inf, [](double a, double c) {
-      return __builtin_fmin(a, c); }));
-    lmax = __builtin_fmax(lmax, WRing::wave_reduce_f64(pmax, -inf, [](double a, double c) {
-      return __builtin_fmax(a, c); }));
+    const double rmin = WRing::wave_reduce_f64(pmin, inf, [](double a, double c) {
+      return c < a ? c : a; });
+    const double rmax = WRing::wave_reduce_f64(pmax, -inf, [](double a, double c) {
+      return c > a ? c : a; });
+    lmin = rmin < lmin ? rmin : lmin;
+    lmax = rmax > lmax ? rmax : lmax;
     const uint64_t lo = WRing::wave_sum(pbytes & 0xFFFFu), hi = WRing::wave_sum(pbytes >> 16);
     byte_count += lo + (hi << 16);
     m.last = m.first + max(WRing::wave_max(pdmax), m.last - m.first);
@@ -559,8 +563,10 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
       n_new += (uint32_t)__popcll(__ballot(nw));
       const double lat = cur[q].latency;
       pbytes += counted ? cur[q].len : 0u;
-      pmin = counted ? __builtin_fmin(pmin, lat) : pmin;
-      pmax = counted ? __builtin_fmax(pmax, lat) : pmax;
+      // min / max as compare-selects (latencies are never NaN or -0, so these equal fmin /
+      // fmax, without the canonicalising moves those cost)
+      pmin = (counted && lat < pmin) ? lat : pmin;
+      pmax = (counted && lat > pmax) ? lat : pmax;
       pdmax = cand[q] ? max(pdmax, cur[q].seq - m.first) : pdmax;
       latp[q] = counted ? lat : latp[q];
     }
@@ -606,7 +612,6 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
         if (ev > k) bulk(k, ev);
       }
       if (ev >= cnt) break;
-      flush();
       const uint32_t q = ev >> 6, l = ev & 63u;
       uint32_t seq = 0, len = 0, rlo = 0, rhi = 0, llo = 0, lhi = 0;
 #pragma unroll
@@ -625,8 +630,33 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
         llo = qq == q ? c_ : llo;
         lhi = qq == q ? d_ : lhi;
       }
-      const double lp = update(seq, (uint64_t)rhi << 32 | rlo, len,
-                               __builtin_bit_cast(double, (uint64_t)lhi << 32 | llo), i0 + ev);
+      const uint64_t rxk = (uint64_t)rhi << 32 | rlo;
+      const double lat = __builtin_bit_cast(double, (uint64_t)lhi << 32 | llo);
+      double lp;
+      if (valid && m.n && len != 0u && rxk < wek && (int32_t)(seq - m.first) >= (int32_t)kDepth &&
+          (int32_t)(seq - seq_start) >= 0) {
+        // a mask restart, the common exact step (:118-127): not a duplicate (outside the span),
+        // counted, Set fails, UnsetBits clears every set index (all below seq) -> mask {seq}.
+        // No flush: the pending bytes / min / max stay pending (order-free); only the pending
+        // `last` partials, relative to the old first, are dropped (last = seq now).
+        pdmax = 0;
+        m.w = lane == ((seq >> 5) & 31u) ? (1u << (seq & 31u)) : 0u;
+        m.first = m.last = seq;
+        m.n = 1;
+        if (msg_count == 1) byte_count = len;  // nothing pending at msg_count <= 1
+        else byte_count += len;
+        if (msg_count == 0) {
+          lmin = lmax = lat;
+        } else {
+          lmin = lat < lmin ? lat : lmin;
+          lmax = lat > lmax ? lat : lmax;
+        }
+        msg_count++;
+        lp = lat;
+      } else {
+        flush();
+        lp = update(seq, rxk, len, lat, i0 + ev);
+      }
 #pragma unroll
       for (uint32_t qq = 0; qq < kUR; qq++) latp[qq] = (qq == q && lane == l) ? lp : latp[qq];
       k = ev + 1u;
@@ -767,15 +797,16 @@ flow_chain_kernel(mgenx_flow_state* __restrict__ flows, const uint32_t* __restri
 //   hist:  per-tile flow histogram (kTile records per tile), stored flow-major
 //          (hist[flow * n_tiles + tile]);
 //   scan:  exclusive prefix sum of hist = where each (flow, tile) run starts;
-//   order: each tile is sorted by flow in LDS (stable: waves own contiguous eighths, ranks
-//          inside a 64-record step from ballots on the key bits), then its records are built
-//          from the caller's columns (or rows) -- gathered inside the tile, whose few hundred KB
-//          stay in L2 -- and written run by run, consecutive lanes to consecutive slots.  Tiles go
-//          to XCDs in contiguous ranges (blockIdx mod 8 = XCD), so the runs of one flow from
-//          neighbouring tiles meet in the same L2 and leave it as whole lines.
+//   order: each record's position in its flow-sorted tile (stable: waves own contiguous
+//          eighths, ranks inside a 64-record step from ballots on the key bits); the records are
+//          then built from the caller's columns (or rows) read in input order -- coalesced -- and
+//          scattered to their sorted slots.  (Gathering them in sorted order instead fetched a
+//          line per 4-B column element: 405 us for config 4.)  Tiles go to XCDs in contiguous
+//          ranges (blockIdx mod 8 = XCD), so the runs of one flow from neighbouring tiles meet
+//          in the same L2 and leave it as whole lines.
 // Records whose flow index is >= n_flows (MGENX_FLOW_NONE) go to the extra last bin and are
 // not written.
-constexpr uint32_t kCountBins = 2048;  // LDS: 9 x bins x 4 + kTile x 4 bytes
+constexpr uint32_t kCountBins = 2048;  // LDS: 9 x bins x 4 bytes
 constexpr uint32_t kSortWaves = 8;
 constexpr uint32_t kTile = 8192;
 constexpr uint32_t kPart = kTile / kSortWaves;
@@ -810,10 +841,6 @@ flow_order_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows
   const uint32_t bins = n_flows + 1u;
   uint32_t* cnt = lds;                                // [wave][bin]: counts, then run bases
   uint32_t* sbase = lds + kSortWaves * bins;          // [bin]: start - tile offset
-  // [kTile] each: the input index - t0 (13 bits) and the flow, flow-sorted -- 16-bit entries
-  // keep the block at ~70 KB of LDS, two blocks per CU
-  uint16_t* lsorted = reinterpret_cast<uint16_t*>(sbase + bins);
-  uint16_t* lkey = lsorted + kTile;
   __shared__ uint32_t wsum[kSortWaves];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
   // tile: contiguous ranges per XCD (block b runs on XCD b % 8)
@@ -822,7 +849,7 @@ flow_order_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows
   if (t >= n_tiles) return;  // whole block: no barrier below is reached by anyone
   for (uint32_t k = tid; k < kSortWaves * bins; k += blockDim.x) cnt[k] = 0u;
   __syncthreads();
-  const uint32_t t0 = t * kTile, tn = min(n - t0, kTile);
+  const uint32_t t0 = t * kTile;
   const uint32_t a = t0 + w * kPart, e = min(n, a + kPart);
   uint32_t* my = cnt + w * bins;
   // the wave's kPart keys, loaded once (all in flight together) for both passes below
@@ -864,7 +891,10 @@ flow_order_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows
     }
   }
   __syncthreads();
+  // each record's position in the flow-sorted tile (stable: waves own contiguous eighths,
+  // ranks inside a 64-record step from ballots on the key bits), kept in registers
   const uint64_t lt = (1ull << lane) - 1ull;
+  uint32_t pos[kKeys];
 #pragma unroll
   for (uint32_t j = 0; j < kKeys; j++) {
     const uint32_t i = a + 64u * j + lane;
@@ -878,35 +908,26 @@ flow_order_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows
     }
     const uint32_t rank = (uint32_t)__popcll(peers & lt);
     const uint32_t base = live ? my[key] : 0u;
-    if (live) {
-      const uint32_t pos = base + rank;
-      lsorted[pos] = (uint16_t)(i - t0);
-      lkey[pos] = (uint16_t)key;
-      if (rank + 1u == (uint32_t)__popcll(peers)) my[key] = pos + 1u;
-    }
+    pos[j] = base + rank;
+    if (live && rank + 1u == (uint32_t)__popcll(peers)) my[key] = base + rank + 1u;
   }
-  __syncthreads();
-  // the records, built from the source (tile-local gathers, kOrdU per thread in flight) and
-  // stored at their sorted positions
+  // the records, read in input order (consecutive lanes, consecutive records: coalesced
+  // column loads) and scattered to their sorted slots; a (flow, tile) run's records leave
+  // from one workgroup close together, so their lines merge in L2 before they are written
   constexpr uint32_t kOrdU = 4;
-  for (uint32_t j0 = tid; j0 < tn; j0 += kOrdU * blockDim.x) {
-    uint32_t key[kOrdU], src_i[kOrdU];
+#pragma unroll
+  for (uint32_t j0 = 0; j0 < kKeys; j0 += kOrdU) {
     FRec r[kOrdU];
 #pragma unroll
-    for (uint32_t u = 0; u < kOrdU; u++) {
-      const uint32_t j = min(j0 + u * blockDim.x, tn - 1u);
-      key[u] = lkey[j];
-      src_i[u] = t0 + lsorted[j];
-    }
-#pragma unroll
-    for (uint32_t u = 0; u < kOrdU; u++) r[u] = make_frec(src, src_i[u]);
+    for (uint32_t u = 0; u < kOrdU; u++)
+      r[u] = make_frec(src, min(a + 64u * (j0 + u) + lane, n - 1u));
 #pragma unroll
     for (uint32_t u = 0; u < kOrdU; u++) {
-      const uint32_t j = j0 + u * blockDim.x;
-      if (j < tn && key[u] < n_flows) {
-        const uint32_t pos = sbase[key[u]] + j;
-        recs[pos] = r[u];
-        if (order) order[pos] = src_i[u];
+      const uint32_t i = a + 64u * (j0 + u) + lane;
+      if (i < e && keys[j0 + u] < n_flows) {
+        const uint32_t g = sbase[keys[j0 + u]] + pos[j0 + u];
+        recs[g] = r[u];
+        if (order) order[g] = i;
       }
     }
   }
@@ -1170,8 +1191,8 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
       snprintf(err, errn, "flow_reduce scan: %s", hipGetErrorString(e));
       return MGENX_EDEVICE;
     }
-    // LDS: per-wave counts, bases, the sorted tile (index + 16-bit flow)
-    const uint32_t lds = (kSortWaves * bins + bins) * 4u + kTile * 4u;
+    // LDS: per-wave counts and the run bases
+    const uint32_t lds = (kSortWaves * bins + bins) * 4u;
     e = set_max_lds((const void*)flow_order_kernel, 160 * 1024 - 256);
     if (e != hipSuccess) {
       snprintf(err, errn, "flow_reduce order: %s", hipGetErrorString(e));

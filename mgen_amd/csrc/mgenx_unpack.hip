@@ -742,7 +742,9 @@ unpack_kernel(UnpackParams p) {
 // KB = 8 or 16 fit the registers but lose the loads in flight (0.245-0.253 ms); flushing at
 // each tile's end with the indices recomputed from the rank permutation 0.239 ms;
 // non-temporal row stores 0.241-0.246 ms; tiles handed out by an atomic ticket (dynamic
-// balance) 0.32-0.44 ms.
+// balance) 0.32-0.44 ms; (r04) a tile's 64 rows gathered by lane permutes and stored as 2 KiB
+// of whole lines (two 16-B stores per lane instead of four scattered 8-B ones) 0.2359 ms
+// against 0.2361 (15 VGPRs spilled; the partial-line writes are not what costs).
 // Template knobs (the product instantiation is unpack_var_kernel<kUnpackThreads, 4, 0>):
 //   NT   block size (one block per CU: the LDS tables);
 //   KB   groups of rows held (0: one row store per group);
@@ -827,42 +829,6 @@ unpack_var_kernel(UnpackParams p) {
                (uint64_t)b1[j] << 32 | b0[j]);
     }
     held = 0;
-  };
-  // (MODE & 16) a whole tile's rows held (its 4 groups, every record on the fast layout) leave
-  // as 2 KiB of full lines: two stores of 16 B per lane, 1 KiB each, unit u (record u / 2, half
-  // u & 1) gathered from the two quad lanes holding it by lane permutes -- instead of four
-  // stores of 8 B per lane whose 32-B rows lie scattered over the tile's lines (partial lines)
-  const bool lines_ok = (MODE & 16) && burst && KB == 4 &&
-                        (((uint64_t)p.cols.rows) & 63u) == 0u;
-  auto flush_lines = [&](uint64_t t, int src) -> bool {
-    bool all = held == 4u;
-#pragma unroll
-    for (int j = 0; j < KH; j++) all = all && __ballot(bi[j] == 0xFFFFFFFFu) == 0ull;
-    if (!all) return false;
-    const int rankv = __builtin_amdgcn_ds_permute(src << 2, lane);  // sorted position of record `lane`
-    uint8_t* base = reinterpret_cast<uint8_t*>(p.cols.rows) + (t << 6) * 32u;
-#pragma unroll
-    for (int half = 0; half < 2; half++) {
-      const int u = 64 * half + lane;
-      const int rk = __builtin_amdgcn_ds_bpermute((u >> 1) << 2, rankv);
-      const int j = rk >> 4, la = (4 * (rk & 15) + 2 * (u & 1)) << 2, lb = la + 4;
-      uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
-#pragma unroll
-      for (int jj = 0; jj < KH; jj++) {
-        const uint32_t x0 = (uint32_t)__builtin_amdgcn_ds_bpermute(la, (int)b0[jj]);
-        const uint32_t x1 = (uint32_t)__builtin_amdgcn_ds_bpermute(la, (int)b1[jj]);
-        const uint32_t x2 = (uint32_t)__builtin_amdgcn_ds_bpermute(lb, (int)b0[jj]);
-        const uint32_t x3 = (uint32_t)__builtin_amdgcn_ds_bpermute(lb, (int)b1[jj]);
-        w0 = j == jj ? x0 : w0;
-        w1 = j == jj ? x1 : w1;
-        w2 = j == jj ? x2 : w2;
-        w3 = j == jj ? x3 : w3;
-      }
-      const u32x4_t v = {w0, w1, w2, w3};
-      stu128(base + 16u * (uint32_t)u, v);
-    }
-    held = 0;
-    return true;
   };
 
   // ---- a group: the quad's record and its row geometry ----
@@ -1089,9 +1055,7 @@ unpack_var_kernel(UnpackParams p) {
       }
     }
 
-    if (KB > 0 && burst && held == (uint32_t)KH) {
-      if (!(lines_ok && flush_lines(t_c, src_c))) flush();
-    }
+    if (KB > 0 && burst && held == (uint32_t)KH) flush();
     if (!has_next) break;
     // N's header: needed only after N's rows, so loaded after G's column stores
     pf = ldu128(hdr_ptr(N));
@@ -1838,7 +1802,6 @@ hipError_t launch_unpack(const UnpackParams& p, int grid, hipStream_t stream, in
       case 23: return launch_var<768, 16, 0>(p, grid, stream);
       case 27: return launch_var<1024, 8, 0>(p, grid, stream);
       case 32: return launch_var<1024, 4, 8>(p, grid, stream);  // non-temporal row stores
-      case 33: return launch_var<1024, 4, 16>(p, grid, stream);  // whole-line tile flush
       default: break;
     }
   }

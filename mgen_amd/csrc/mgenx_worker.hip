@@ -88,23 +88,21 @@ worker_kernel(WMail* m, const uint32_t* __restrict__ a4_tab, const uint32_t* __r
   uint32_t last = start;
   uint64_t t_last = __builtin_amdgcn_s_memrealtime();
   for (;;) {
-    uint32_t r = lane == 0 ? ld_sys(&m->req) : 0u;
-    r = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl((int)r, 0));
+    // one 16-byte read of the request words: req, op, len, arg share a cache line and the host
+    // writes op/len/arg before req, so a read that sees the new req sees them too (one host
+    // round trip per poll, not one per word).  Volatile: every poll reaches host memory.
+    u32x4_t hq = {0u, 0u, 0u, 0u};
+    if (lane == 0) hq = *reinterpret_cast<const volatile u32x4_t*>(&m->req);
+    const uint32_t r = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl((int)hq.x, 0));
     if (r == last) {
       if (__builtin_amdgcn_s_memrealtime() - t_last > idle_ticks) break;
       __builtin_amdgcn_s_sleep(2);
       continue;
     }
-    // the request's words (written before `req`, read after its acquire)
-    uint32_t op = 0, len = 0, arg = 0;
-    if (lane == 0) {
-      op = ld_sys(&m->op);
-      len = ld_sys(&m->len);
-      arg = ld_sys(&m->arg);
-    }
-    op = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl((int)op, 0));
-    len = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl((int)len, 0));
-    arg = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl((int)arg, 0));
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the message bytes after the request
+    uint32_t op = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl((int)hq.y, 0));
+    uint32_t len = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl((int)hq.z, 0));
+    const uint32_t arg = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl((int)hq.w, 0));
     if (op == kWorkStop) {
       if (lane == 0) st_sys_release(&m->resp, r);
       break;
@@ -152,11 +150,12 @@ worker_kernel(WMail* m, const uint32_t* __restrict__ a4_tab, const uint32_t* __r
           reinterpret_cast<uint32_t*>(u.dst_addr)[j] = h.dst_addr[j];
           reinterpret_cast<uint32_t*>(u.host_addr)[j] = h.host_addr[j];
         }
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(&u);
-        uint32_t* dst = reinterpret_cast<uint32_t*>(&m->unpacked);
-        for (uint32_t j = 0; j < sizeof(mgenx_unpacked) / 4u; j++) st_sys(dst + j, src[j]);
+        *reinterpret_cast<mgenx_unpacked*>(rq) = u;  // staged in LDS for the lanes' stores
       }
       __syncthreads();
+      if (lane < 6u)  // 96 bytes (the reply area is 128): six 16-byte stores in one instruction
+        *reinterpret_cast<u32x4_t*>(reinterpret_cast<uint8_t*>(&m->unpacked) + 16u * lane) =
+            *reinterpret_cast<const u32x4_t*>(rq + 4u * lane);
     } else if (op == kWorkCrc32) {
       // the span in LDS pieces; each piece's raw CRC from lane partials, folded into the
       // running state: crc(A || B) = x^(8|B|) crc(A) ^ crc(B)
