@@ -799,17 +799,22 @@ flow_chain_kernel(mgenx_flow_state* __restrict__ flows, const uint32_t* __restri
 //   scan:  exclusive prefix sum of hist = where each (flow, tile) run starts;
 //   order: each record's position in its flow-sorted tile (stable: waves own contiguous
 //          eighths, ranks inside a 64-record step from ballots on the key bits); the records are
-//          then built from the caller's columns (or rows) read in input order -- coalesced -- and
-//          scattered to their sorted slots.  (Gathering them in sorted order instead fetched a
-//          line per 4-B column element: 405 us for config 4.)  Tiles go to XCDs in contiguous
-//          ranges (blockIdx mod 8 = XCD), so the runs of one flow from neighbouring tiles meet
-//          in the same L2 and leave it as whole lines.
+//          then built from the caller's columns (or rows) read in input order -- coalesced --
+//          into their sorted slots of the tile in LDS, and written out run by run, consecutive
+//          lanes to consecutive slots.  (Gathering them in sorted order fetched a line per 4-B
+//          column element: 405 us for config 4; scattering them from their input positions
+//          wrote partial lines: 258 us.)  Tiles go to XCDs in contiguous ranges (blockIdx mod
+//          8 = XCD), so the runs of one flow from neighbouring tiles meet in the same L2 and
+//          leave it as whole lines.
 // Records whose flow index is >= n_flows (MGENX_FLOW_NONE) go to the extra last bin and are
 // not written.
-constexpr uint32_t kCountBins = 2048;  // LDS: 9 x bins x 4 bytes
 constexpr uint32_t kSortWaves = 8;
-constexpr uint32_t kTile = 8192;
+constexpr uint32_t kTile = 4096;
 constexpr uint32_t kPart = kTile / kSortWaves;
+// LDS of the order kernel: 9 x bins x 4 bytes of counts and bases, the tile's records (24 B
+// each) and their flows (2 B each) -- within 160 KiB up to 1536 bins
+constexpr uint32_t kCountBins = 1536;
+constexpr uint32_t kOrderLds = kCountBins * 9u * 4u + kTile * (uint32_t)sizeof(FRec) + kTile * 2u;
 
 __global__ void __launch_bounds__(512)
 flow_hist_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows, uint32_t n_tiles,
@@ -912,8 +917,10 @@ flow_order_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows
     if (live && rank + 1u == (uint32_t)__popcll(peers)) my[key] = base + rank + 1u;
   }
   // the records, read in input order (consecutive lanes, consecutive records: coalesced
-  // column loads) and scattered to their sorted slots; a (flow, tile) run's records leave
-  // from one workgroup close together, so their lines merge in L2 before they are written
+  // column loads), built into their sorted slots of the tile in LDS (the input index - t0 in
+  // the high half of `len`, for `order`) ...
+  FRec* lrec = reinterpret_cast<FRec*>(sbase + bins + (bins & 1u));  // 8-byte aligned
+  uint16_t* lkey = reinterpret_cast<uint16_t*>(lrec + kTile);
   constexpr uint32_t kOrdU = 4;
 #pragma unroll
   for (uint32_t j0 = 0; j0 < kKeys; j0 += kOrdU) {
@@ -924,11 +931,26 @@ flow_order_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows
 #pragma unroll
     for (uint32_t u = 0; u < kOrdU; u++) {
       const uint32_t i = a + 64u * (j0 + u) + lane;
-      if (i < e && keys[j0 + u] < n_flows) {
-        const uint32_t g = sbase[keys[j0 + u]] + pos[j0 + u];
-        recs[g] = r[u];
-        if (order) order[g] = i;
+      if (i < e) {
+        r[u].len |= (i - t0) << 16;
+        lrec[pos[j0 + u]] = r[u];
+        lkey[pos[j0 + u]] = (uint16_t)keys[j0 + u];
       }
+    }
+  }
+  __syncthreads();
+  // ... and written out run by run: consecutive lanes, consecutive slots (whole lines but at
+  // the runs' ends; runs of one flow from neighbouring tiles meet in L2).  (Scattering each
+  // record from its input position instead wrote partial lines: 258 us for config 4.)
+  const uint32_t tn = min(n - t0, kTile);
+  for (uint32_t j = tid; j < tn; j += blockDim.x) {
+    const uint32_t k = lkey[j];
+    if (k < n_flows) {
+      FRec r = lrec[j];
+      const uint32_t g = sbase[k] + j;
+      if (order) order[g] = t0 + (r.len >> 16);
+      r.len &= 0xFFFFu;
+      recs[g] = r;
     }
   }
 }
@@ -1191,9 +1213,10 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
       snprintf(err, errn, "flow_reduce scan: %s", hipGetErrorString(e));
       return MGENX_EDEVICE;
     }
-    // LDS: per-wave counts and the run bases
-    const uint32_t lds = (kSortWaves * bins + bins) * 4u;
-    e = set_max_lds((const void*)flow_order_kernel, 160 * 1024 - 256);
+    // LDS: per-wave counts, the run bases, the tile's records and their flows
+    const uint32_t lds = (kSortWaves * bins + bins + (bins & 1u)) * 4u +
+                         kTile * (uint32_t)sizeof(FRec) + kTile * 2u;
+    e = set_max_lds((const void*)flow_order_kernel, (int)kOrderLds + 8);
     if (e != hipSuccess) {
       snprintf(err, errn, "flow_reduce order: %s", hipGetErrorString(e));
       return MGENX_EDEVICE;
