@@ -313,6 +313,7 @@ struct CloseRec {
 // the first record of a flow) takes the exact update below, and the run restarts after it.
 constexpr uint32_t kUR = 4;             // records per lane and round
 constexpr uint32_t kRound = 64u * kUR;  // records per round
+constexpr uint32_t kLatRounds = 4;      // rounds of lat' staged in LDS per store burst
 
 __global__ void __launch_bounds__(256)
 flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
@@ -320,9 +321,11 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
                    const uint32_t* __restrict__ order, double* __restrict__ lat2,
                    mgenx_flow_report* __restrict__ reports, uint32_t per_flow,
                    uint32_t* __restrict__ report_count, uint32_t* __restrict__ report_rec,
-                   CloseRec* __restrict__ closes, FlowBatch* __restrict__ fbatch) {
+                   CloseRec* __restrict__ closes, FlowBatch* __restrict__ fbatch,
+                   uint32_t lat2_sink) {
   __shared__ uint32_t scat[4][32];
   __shared__ uint32_t fo[4][1024];
+  __shared__ double lbuf[4][kLatRounds * kRound];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint32_t f = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + wv);
   if (f >= n_flows) return;
@@ -661,9 +664,23 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
       for (uint32_t qq = 0; qq < kUR; qq++) latp[qq] = (qq == q && lane == l) ? lp : latp[qq];
       k = ev + 1u;
     }
+    // lat' leaves through LDS, kLatRounds rounds at a time: gfx950 counts stores in vmcnt, so
+    // a round's stores would hold up the waits for the next rounds' record loads until they
+    // complete (45% of the kernel's cycles when every round stored)
+    const uint32_t ro = (uint32_t)(((i0 - b) / kRound) % kLatRounds);
 #pragma unroll
-    for (uint32_t q = 0; q < kUR; q++)
-      if (64u * q + lane < cnt) lat2[i0 + 64u * q + lane] = latp[q];
+    for (uint32_t q = 0; q < kUR; q++) lbuf[wv][ro * kRound + 64u * q + lane] = latp[q];
+    if (ro == kLatRounds - 1u || i0 + kRound >= e) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const uint32_t bs = i0 - ro * kRound, bn = i0 + cnt - bs;  // the batch's records
+#pragma unroll
+      for (uint32_t k2 = 0; k2 < kLatRounds * kUR; k2++) {
+        const uint32_t p = 64u * k2 + lane;  // branch-free: lanes past it write the sink slots
+        lat2[p < bn ? bs + p : lat2_sink + lane] = lbuf[wv][p];
+      }
+    }
 #pragma unroll
     for (uint32_t q = 0; q < kUR; q++) {
       cur[q] = nxt[q];
@@ -1170,7 +1187,7 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
   const bool want_order = report_rec != nullptr;
   const size_t nb = a256((size_t)n * 4), rb = a256((size_t)n * sizeof(FRec));
   const size_t hb = a256(n_hist * 4), bb = a256((size_t)bins * 4);
-  const size_t lb = a256((size_t)n * 8), fbb = a256((size_t)n_flows * sizeof(FlowBatch));
+  const size_t lb = a256((size_t)(n + 64) * 8), fbb = a256((size_t)n_flows * sizeof(FlowBatch));
   const size_t cb = a256((size_t)n_flows * per_flow * sizeof(CloseRec));
   // both: records (sorted), lat', per-flow batch info, closes
   // counting: hist, start, order (report_rec only), row totals
@@ -1251,7 +1268,7 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
   if (sabl) return MGENX_OK;  // timing study: ordering only
   hipLaunchKernelGGL(flow_update_kernel, dim3((n_flows + 3) / 4), dim3(256), 0, stream, flows,
                      n_flows, bnd, bstride, recs, order, lat2, reports, per_flow, report_count,
-                     report_rec, closes, fbatch);
+                     report_rec, closes, fbatch, n);
   hipLaunchKernelGGL(flow_chain_kernel, dim3(n_flows), dim3(256), kChainPiece * 8u, stream, flows,
                      bnd, bstride, lat2, fbatch, closes, reports, per_flow, report_count);
   e = hipGetLastError();
