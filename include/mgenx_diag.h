@@ -38,6 +38,11 @@ int mgenx_diag_stream_read(mgenx_ctx* ctx, const uint8_t* dev_data, uint64_t byt
 int mgenx_diag_group_rw(mgenx_ctx* ctx, const uint8_t* dev_data, uint64_t bytes,
                         uint8_t* dev_out, int mode, void* stream);
 
+/* Diagnostic: s_memtime stamps of flow_seg_kernel's workgroup 0, first pass, per wave (8 x
+ * 12: start, walk begun, walk done, scatter done, ring received, ring posted, classified,
+ * aggregates received, replay done); out holds >= 96 values. */
+int mgenx_diag_seg_prof(unsigned long long* out, int n);
+
 #ifdef __cplusplus
 }
 #endif

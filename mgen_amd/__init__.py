@@ -46,7 +46,8 @@ EXPORTED_SYMBOLS = (
     "mgenx_worker_create", "mgenx_worker_destroy", "mgenx_worker_unpack", "mgenx_worker_crc32",
     "mgenx_worker_pack",
 )
-DIAG_SYMBOLS = ("mgenx_set_tuning", "mgenx_diag_stream_read", "mgenx_diag_group_rw")
+DIAG_SYMBOLS = ("mgenx_set_tuning", "mgenx_diag_stream_read", "mgenx_diag_group_rw",
+                "mgenx_diag_seg_prof")
 
 
 class MgenxError(RuntimeError):
@@ -108,6 +109,7 @@ def load(diag: bool = False):
         L.mgenx_set_tuning.argtypes = [P, i32, i32]
         L.mgenx_diag_stream_read.argtypes = [P, P, u64, P, i32, P]
         L.mgenx_diag_group_rw.argtypes = [P, P, u64, P, i32, P]
+        L.mgenx_diag_seg_prof.argtypes = [P, i32]
     L.mgenx_stream_scan.argtypes = [P, P, u64, i32, P, P, u64, ctypes.POINTER(ScanInfo), P]
     L.mgenx_tcp_rx_persist.argtypes = [P, P, P, P, u32, P, P, P, u32, P]
     L.mgenx_report_build.argtypes = [P, P, u32, u32, P, P, P, P, P, P, P]

@@ -273,3 +273,31 @@ def test_flow_reduce_skewed_flows_tile_runs(torch, eng):
                                          d["rx_usec"], window=0.02, per_flow=per_flow)
     assert int(ocnt[0]) > 5 and of[7].msg_count == 1
     compare(st, rep, cnt, of, orep, ocnt, per_flow)
+
+
+@pytest.mark.parametrize("window", [0.001, 0.3])
+def test_flow_reduce_workgroup_path_mixed_lengths(torch, eng, window):
+    """Flows of 1 to 20000 records in one call -- below 2048 records a wave per flow
+    (flow_update_kernel), from 2048 on a workgroup per flow (flow_seg_kernel), the longest in
+    several passes of 8192 records -- with jumpy sequences (mask restarts, records below
+    `first`, wraps, duplicates, reordering) and, at 1 ms, a window closing every record or two
+    (more reports than per_flow keeps); a second call continues from the first's state (the
+    two kernels hand flows to each other).  Against the oracle."""
+    from oracle import oracle as O
+    sets = []
+    for i, per in enumerate((1, 700, 2040, 2048, 2100, 5000, 9000, 20000)):
+        d = _jumpy_flows(1, per, seed=100 + i)
+        d["flow_id"] = d["flow_id"] + i
+        sets.append(d)
+    d = {k: np.concatenate([s[k] for s in sets]) for k in sets[0]}
+    rx = d["rx_sec"].astype(np.int64) * 10**6 + d["rx_usec"]
+    o = np.argsort(rx, kind="stable")
+    d = {k: np.ascontiguousarray(v[o]) for k, v in d.items()}
+    n_flows, per_flow = 8, 4096
+    st, rep, cnt, _ = run_gpu(torch, eng, d, n_flows, window, per_flow,
+                              splits=(0, len(d["seq"]) * 3 // 4))
+    of, orep, ocnt = O.flow_reduce_batch(n_flows, d["flow_id"] - 1, d["seq"], d["tx_sec"],
+                                         d["tx_usec"], d["msg_len"], d["rx_sec"],
+                                         d["rx_usec"], window=window, per_flow=per_flow)
+    assert sum(a.dup_msg_count for a in of) > 0
+    compare(st, rep, cnt, of, orep, ocnt, per_flow)
