@@ -31,6 +31,10 @@ int mgenx_set_tuning(mgenx_ctx* ctx, int key, int value);
  * next to the roofline); dev_scratch holds `grid` words. */
 int mgenx_diag_stream_read(mgenx_ctx* ctx, const uint8_t* dev_data, uint64_t bytes,
                            uint32_t* dev_scratch, int grid, void* stream);
+/* Diagnostic: the same read at `width` bytes per lane (4, 8 or 24), coalesced -- FETCH_SIZE
+ * calibration for the config-4 kernels' access shapes. */
+int mgenx_diag_stream_read_w(mgenx_ctx* ctx, const uint8_t* dev_data, uint64_t bytes,
+                             uint32_t* dev_scratch, int grid, int width, void* stream);
 /* Diagnostic: the fixed-length unpack's memory pattern without its compute -- waves take
  * 16-KiB groups of `data` round-robin (16 loads of 1 KiB each, consumed by XOR) and, when
  * `mode` & 1, store 512 B per group to dev_out (bytes / 32 bytes); `mode` & 2: the stores

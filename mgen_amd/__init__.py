@@ -47,7 +47,7 @@ EXPORTED_SYMBOLS = (
     "mgenx_worker_pack",
 )
 DIAG_SYMBOLS = ("mgenx_set_tuning", "mgenx_diag_stream_read", "mgenx_diag_group_rw",
-                "mgenx_diag_seg_prof")
+                "mgenx_diag_seg_prof", "mgenx_diag_stream_read_w")
 
 
 class MgenxError(RuntimeError):
@@ -110,6 +110,7 @@ def load(diag: bool = False):
         L.mgenx_diag_stream_read.argtypes = [P, P, u64, P, i32, P]
         L.mgenx_diag_group_rw.argtypes = [P, P, u64, P, i32, P]
         L.mgenx_diag_seg_prof.argtypes = [P, i32]
+        L.mgenx_diag_stream_read_w.argtypes = [P, P, u64, P, i32, i32, P]
     L.mgenx_stream_scan.argtypes = [P, P, u64, i32, P, P, u64, ctypes.POINTER(ScanInfo), P]
     L.mgenx_tcp_rx_persist.argtypes = [P, P, P, P, u32, P, P, P, u32, P]
     L.mgenx_report_build.argtypes = [P, P, u32, u32, P, P, P, P, P, P, P]
@@ -375,6 +376,14 @@ class Engine:
         rc = self.lib.mgenx_diag_stream_read(self.ctx, _ptr(data), data.numel(), _ptr(scratch),
                                              grid, _stream(self.device))
         self._check(rc, "mgenx_diag_stream_read")
+
+    def stream_read_w(self, data, width, grid=2048, scratch=None):
+        """Diagnostic: coalesced read at `width` (4, 8, 24) bytes per lane."""
+        if scratch is None:
+            scratch = self.torch.empty(grid, dtype=self.torch.int32, device=data.device)
+        rc = self.lib.mgenx_diag_stream_read_w(self.ctx, _ptr(data), data.numel(), _ptr(scratch),
+                                               grid, width, _stream(self.device))
+        self._check(rc, "mgenx_diag_stream_read_w")
 
     def group_rw(self, data, out, mode=1):
         """Diagnostic: the fixed unpack's read pattern (+ 512-B stores per 16-KiB group)."""

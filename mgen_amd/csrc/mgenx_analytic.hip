@@ -43,11 +43,19 @@ __device__ __forceinline__ double mul_rounded(double a, double b) {
 __device__ __forceinline__ double tdelta(Tm a, Tm b) {  // ProtoTime::Delta(a, b)
   return (double)(a.sec - b.sec) + mul_rounded(1.0e-06, (double)(a.usec - b.usec));
 }
-__device__ __forceinline__ Tm tadd(Tm t, double s) {  // ProtoTime += double
+// ProtoTime += double, split: the double's whole seconds and rounded microseconds depend on the
+// window size alone, so a kernel computes them once per flow (TAdd) and each window close only
+// adds and normalises (no FP64 floor / conversion on the per-flow critical path)
+struct TAdd {
+  int64_t sec, usec;
+};
+__device__ __forceinline__ TAdd tadd_of(double s) {
   const double whole = floor(s);
-  const int64_t us = (int64_t)(mul_rounded(s - whole, 1.0e06) + 0.5);
-  t.sec += (int64_t)whole;
-  t.usec += us;
+  return TAdd{(int64_t)whole, (int64_t)(mul_rounded(s - whole, 1.0e06) + 0.5)};
+}
+__device__ __forceinline__ Tm tadd(Tm t, TAdd a) {
+  t.sec += a.sec;
+  t.usec += a.usec;
   while (t.usec >= 1000000) { t.usec -= 1000000; t.sec += 1; }
   return t;
 }
@@ -333,7 +341,7 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
   if (b >= e || e - b >= long_min) return;  // (long flows: flow_seg_kernel)
   for (uint32_t j = lane; j < 1024u; j += 64u) fo[wv][j] = 0xFFFFFFFFu;
   mgenx_flow_state* sp = flows + f;
-  const double window = sp->window_size;
+  const TAdd window = tadd_of(sp->window_size);
   WRing m;
   m.lane = lane;
   m.first = sp->mask_first;
@@ -729,10 +737,11 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
   }
 }
 
+#if MGENX_DIAG
 // ---- long flows: one WORKGROUP per flow, its records in segments of one wave each ----
 // flow_update_kernel runs a flow's records on one wave, so a call with few, long flows leaves
 // the chip idle and every flow's time is its whole record count times the per-round latency.
-// Here a flow with at least kSegMin records in the call gets a workgroup; its records go in
+// Here a flow with at least MGENX_AN_SEGMIN records in the call gets a workgroup; its records go in
 // chunks of kSegWaves segments, wave w taking segment w (kSegRows rows of 64 records in
 // registers, record q * 64 + lane in row q, lane `lane`).  Update's state splits three ways:
 //   * the skeleton: window (valid, start, end), mask span (nonempty, first, last) and
@@ -755,7 +764,6 @@ constexpr uint32_t kSegRows = 8;                      // rows of 64 records per 
 constexpr uint32_t kSegWaves = 16;                    // segments (waves) per workgroup pass
 constexpr uint32_t kSeg = 64u * kSegRows;
 constexpr uint32_t kSegChunk = kSeg * kSegWaves;
-constexpr uint32_t kSegMin = 2048;                    // records in the call for the workgroup path
 
 // per-record branch codes written by the walk (4 bits; close and seq >= seq_start bits apart)
 enum : uint32_t {
@@ -787,7 +795,18 @@ struct SegPiece {  // a piece of a segment: its counted records' partial, then i
   uint32_t kk, l1, flags, pos, len, rx_sec, rx_usec, sbefore, seq_max, rsv;
 };
 constexpr uint32_t kPieceCap = 6;  // pieces per wave kept in LDS ahead of the aggregate chain
+// the closes of a pass, for its latency sums (P4); a pass with more leaves the flow's sums to
+// flow_chain_kernel
+constexpr uint32_t kCloseCap = 255;
+struct SegClose {
+  uint64_t mc;                 // msg_count at the close: latency_ave's divisor
+  uint32_t pos, zr, slot, kept;  // pass-relative position, zero restart, report slot
+};
 struct SegLds {
+  double lat[kSegChunk];       // the pass's lat' values
+  SegClose cl[kCloseCap];
+  double carry;                // the open window's sum at the pass start
+  uint32_t ncl, p4_off;
   SegPiece pc[kSegWaves][kPieceCap];
   SegSkel sk[kSegWaves + 1];
   SegAgg ag[kSegWaves + 1];
@@ -873,7 +892,8 @@ flow_seg_kernel(mgenx_flow_state* __restrict__ flows, const uint32_t* __restrict
     const uint32_t f = rfl(list[li]);
     const uint32_t b = rfl(bnd[(size_t)f * bstride]), e = rfl(bnd[(size_t)(f + 1u) * bstride]);
     mgenx_flow_state* sp = flows + f;
-    const double window = rfld(sp->window_size);
+    const double wsz = rfld(sp->window_size);
+    const TAdd window = {rfl64(tadd_of(wsz).sec), rfl64(tadd_of(wsz).usec)};
     if (w == 0) {  // the flow's state on entry -> slot 0 of the three chains
       WRing m;
       m.lane = lane;
@@ -904,6 +924,9 @@ flow_seg_kernel(mgenx_flow_state* __restrict__ flows, const uint32_t* __restrict
         a.last_zr = 0;
         sl.ag[0] = a;
         sl.dups = 0;
+        sl.carry = sp->latency_sum;
+        sl.ncl = 0;
+        sl.p4_off = 0;
       }
       if (lane < 32u) sl.ring[0][lane] = m.n ? m.w : 0u;
     }
@@ -948,25 +971,28 @@ flow_seg_kernel(mgenx_flow_state* __restrict__ flows, const uint32_t* __restrict
         uint32_t p = 0;
         SEG_PROF(9);
         while (p < cnt) {
+          // branch-free: every row's event mask (the first event by a scalar select chain), then
+          // the run [p, ev)'s seq >= seq_start bits and its highest seq - first
+          // (bitwise logic with the uniform state folded into operands: no uniform branches,
+          // and fresh() keeps the per-row compares in the loop instead of hoisted SGPR masks)
+          const uint64_t wekv = valid ? wek : 0ull;  // no window yet: every record is an event
+          const uint32_t lim = nz ? kDepth : 0u;      // empty mask: every message is an event
           uint32_t ev = cnt;
 #pragma unroll
-          for (uint32_t q = 0; q < kSegRows; q++) {
-            if (64u * q + 64u <= p) continue;
-            if (64u * q >= cnt) break;
-            const uint32_t pos = 64u * q + lane, sqq = fresh(sq[q]);
-            const bool inr = pos >= p && pos < cnt;
+          for (uint32_t q = kSegRows; q-- > 0;) {
+            const uint32_t pos = 64u * q + fresh(lane), sqq = fresh(sq[q]);
             const uint64_t rxk = (uint64_t)fresh(rkh[q]) << 32 | fresh(rkl[q]);
             const bool msg = fresh(ln[q]) != 0u;
-            const bool simple = valid && rxk < wek && (!msg || (nz && sqq - F < kDepth));
-            const uint64_t mm = __ballot(inr && !simple);
-            const uint32_t evq = mm ? 64u * q + (uint32_t)__builtin_ctzll(mm) : 64u * q + 64u;
-            const bool run = inr && pos < evq && msg;
-            cgb |= (run && (int32_t)(sqq - S) >= 0) ? (1u << (16u + q)) : 0u;
+            const bool simple = (rxk < wekv) & (!msg | (sqq - F < lim));
+            const uint64_t mm = __ballot((pos >= p) & (pos < cnt) & !simple);
+            ev = mm ? 64u * q + (uint32_t)__builtin_ctzll(mm) : ev;
+          }
+#pragma unroll
+          for (uint32_t q = 0; q < kSegRows; q++) {
+            const uint32_t pos = 64u * q + fresh(lane), sqq = fresh(sq[q]);
+            const bool run = (pos >= p) & (pos < ev) & (fresh(ln[q]) != 0u);
+            cgb |= (run & ((int32_t)(sqq - S) >= 0)) ? (1u << (16u + q)) : 0u;
             pdm = run ? max(pdm, sqq - F) : pdm;
-            if (mm) {
-              ev = evq;
-              break;
-            }
           }
           SEG_PROF(10);
           if (nz) L = F + max(L - F, rfl(WRing::wave_max(pdm)));
@@ -1169,7 +1195,10 @@ flow_seg_kernel(mgenx_flow_state* __restrict__ flows, const uint32_t* __restrict
           ndup += (uint32_t)__popcll(__ballot(live && dup));
           const double lat = __builtin_bit_cast(double, (uint64_t)lth[q] << 32 | ltl[q]);
           const double lp = (counted || (live && (c == kCFirstMsg || c == kCOpenMsg))) ? lat : 0.0;
-          if (live) lat2[sb + pos] = lp;
+          if (live) {
+            lat2[sb + pos] = lp;
+            sl.lat[w * kSeg + pos] = lp;
+          }
         }
         if (lane == 0 && ndup) atomicAdd(&sl.dups, (unsigned long long)ndup);
       }
@@ -1187,32 +1216,31 @@ flow_seg_kernel(mgenx_flow_state* __restrict__ flows, const uint32_t* __restrict
         uint32_t p = 0;
         // the piece from p: records up to the next event, and the event; advances the replay
         auto next_piece = [&](SegPiece& pc) {
+          // branch-free, as the walk: the next event, then the run [p, ev)'s partials
           uint32_t ev = cnt;
+#pragma unroll
+          for (uint32_t q = kSegRows; q-- > 0;) {
+            const uint32_t pos = 64u * q + fresh(lane), c = fresh(code_of(q));
+            const uint64_t mm = __ballot((pos >= p) & (pos < cnt) & ((c != kCSimple) | ((cgb >> q) & 1u)));
+            ev = mm ? 64u * q + (uint32_t)__builtin_ctzll(mm) : ev;
+          }
           uint32_t kk = 0, l1 = 0, psum = 0, pdm = 0;
           double pmn = inf, pmx = -inf;
 #pragma unroll
-          for (uint32_t q = 0; q < kSegRows; q++) {
-            if (64u * q + 64u <= p) continue;
-            if (64u * q >= cnt) break;
-            const uint32_t pos = 64u * q + lane, c = fresh(code_of(q));
-            const bool inr = pos >= p && pos < cnt;
-            const uint64_t mm = __ballot(inr && (c != kCSimple || ((cgb >> q) & 1u)));
-            const uint32_t evq = mm ? 64u * q + (uint32_t)__builtin_ctzll(mm) : 64u * q + 64u;
-            const bool run = inr && pos < evq;
-            const bool cn = run && ((cntb >> q) & 1u);
+          for (uint32_t q = kSegRows; q-- > 0;) {  // last row first: l1 ends as the first row's
+            const uint32_t pos = 64u * q + fresh(lane);
+            const bool run = (pos >= p) & (pos < ev);
+            const bool cn = run & ((fresh(cntb) >> q) & 1u);
             const uint64_t cm = __ballot(cn);
             const uint32_t lnq = fresh(ln[q]);
-            if (cm && kk == 0) l1 = (uint32_t)__builtin_amdgcn_readlane((int)lnq, (int)__builtin_ctzll(cm));
+            const uint32_t lf = (uint32_t)__builtin_amdgcn_readlane((int)lnq, cm ? (int)__builtin_ctzll(cm) : 0);
+            l1 = cm ? lf : l1;
             kk += (uint32_t)__popcll(cm);
             const double lat = __builtin_bit_cast(double, (uint64_t)fresh(lth[q]) << 32 | fresh(ltl[q]));
             psum += cn ? lnq : 0u;
-            pmn = (cn && lat < pmn) ? lat : pmn;
-            pmx = (cn && lat > pmx) ? lat : pmx;
-            pdm = (run && lnq != 0u) ? max(pdm, fresh(sq[q]) - F) : pdm;
-            if (mm) {
-              ev = evq;
-              break;
-            }
+            pmn = (cn & (lat < pmn)) ? lat : pmn;
+            pmx = (cn & (lat > pmx)) ? lat : pmx;
+            pdm = (run & (lnq != 0u)) ? max(pdm, fresh(sq[q]) - F) : pdm;
           }
           if (nz) L = F + max(L - F, rfl(WRing::wave_max(pdm)));
           pc.kk = kk;
@@ -1378,6 +1406,21 @@ flow_seg_kernel(mgenx_flow_state* __restrict__ flows, const uint32_t* __restrict
               if (report_rec) report_rec[slot] = order[pc.pos];
             }
           }
+          {  // for P4 (chain order: the list is in record order)
+            const uint32_t ci = rfl(sl.ncl);
+            if (lane == 0) {
+              if (ci < kCloseCap) {
+                SegClose c;
+                c.mc = mc;
+                c.pos = pc.pos - c0;
+                c.zr = zr;
+                c.slot = rcount;
+                c.kept = rcount < per_flow;
+                sl.cl[ci] = c;
+              }
+              sl.ncl = ci + 1u;
+            }
+          }
           rcount++;
           nrep++;
           ncl++;
@@ -1436,6 +1479,47 @@ flow_seg_kernel(mgenx_flow_state* __restrict__ flows, const uint32_t* __restrict
       }
       SEG_PROF(8);
       __syncthreads();
+      // ---- P4: the latency sums of the pass's windows, one thread each, over the lat' values
+      // in LDS (as flow_chain_kernel: a window is the in-order sum of its records' lat'; the
+      // first continues the open window's sum, a later one starts from 0.0 at its opening
+      // record, after it for a zero restart) ----
+      {
+        const uint32_t nclc = sl.ncl, ccnt = min(kSegChunk, e - c0);
+        if (nclc > kCloseCap) {
+          if (threadIdx.x == 0) sl.p4_off = 1u;
+        } else if (!sl.p4_off) {
+          const uint32_t t = threadIdx.x;
+          double s = 0.0;
+          if (t <= nclc) {
+            uint32_t lo = 0;
+            s = sl.carry;
+            if (t > 0) {
+              lo = sl.cl[t - 1u].pos + sl.cl[t - 1u].zr;
+              s = 0.0;
+            }
+            const uint32_t hi1 = t < nclc ? sl.cl[t].pos + 1u : ccnt;  // exclusive
+            uint32_t j = lo;
+            for (; j + 4u <= hi1; j += 4u) {
+              double x[4];
+#pragma unroll
+              for (int u = 0; u < 4; u++) x[u] = sl.lat[j + u];
+#pragma unroll
+              for (int u = 0; u < 4; u++) s = __dadd_rn(s, x[u]);
+            }
+            for (; j < hi1; j++) s = __dadd_rn(s, sl.lat[j]);
+            if (t < nclc) {
+              const SegClose c = sl.cl[t];
+              if (c.kept)
+                reports[(size_t)f * per_flow + c.slot].latency_ave =
+                    c.mc == 0 ? -1.0 : c.mc == 1 ? s : __ddiv_rn(s, (double)c.mc);
+            }
+          }
+          __syncthreads();  // (thread 0 has read the carry)
+          if (t == nclc) sl.carry = s;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) sl.ncl = 0;
+      }
       if (w == 0) {  // the pass's exit is the next one's entry
         if (lane == 0) {
           sl.sk[0] = sl.sk[kSegWaves];
@@ -1477,13 +1561,16 @@ flow_seg_kernel(mgenx_flow_state* __restrict__ flows, const uint32_t* __restrict
         fb.last_close = a.last_close;
         fb.last_zr = a.last_zr;
         fb.lsum0 = sp->latency_sum;
-        fb.rsv = 0;
+        fb.rsv = sl.p4_off ? 0u : 1u;  // 1: the sums are done (flow_chain_kernel skips the flow)
+        if (!sl.p4_off) sp->latency_sum = sl.carry;
         fbatch[f] = fb;
       }
     }
     __syncthreads();
   }
 }
+
+#endif  // MGENX_DIAG
 
 // ---- the latency sums: latency_sum += latency in record order (bit-exact) ----
 // One workgroup per flow, one thread per window the call needs: every kept report closed in this
@@ -1506,6 +1593,7 @@ flow_chain_kernel(mgenx_flow_state* __restrict__ flows, const uint32_t* __restri
   const uint32_t b = bnd[(size_t)f * bstride], e = bnd[(size_t)(f + 1u) * bstride];
   if (b >= e) return;
   const FlowBatch fb = fbatch[f];
+  if (fb.rsv) return;  // flow_seg_kernel summed this flow's windows itself
   const uint32_t rc1 = report_count[f];
   const uint32_t kept = min(rc1, per_flow);
   const uint32_t nslots = kept > fb.rc0 ? kept - fb.rc0 : 0u;
@@ -1578,9 +1666,10 @@ flow_chain_kernel(mgenx_flow_state* __restrict__ flows, const uint32_t* __restri
 // ---- ordering the records by flow, stably: a counting sort (flow count < kCountBins) --
 // The output is every record as the 24-B FRec the update reads, flow after flow, receive order
 // kept within a flow (and, for report_rec, `order`: the input index at each sorted position).
-//   hist:  per-tile flow histogram (kTile records per tile), stored flow-major
-//          (hist[flow * n_tiles + tile]);
-//   scan:  exclusive prefix sum of hist = where each (flow, tile) run starts;
+//   hist:  per-tile flow histogram (kTile records per tile), stored tile-major
+//          (hist[tile * bins + flow]);
+//   scan:  the exclusive prefix of hist in flow-major order = where each (flow, tile) run
+//          starts, also stored tile-major (flow_col* kernels below);
 //   order: each record's position in its flow-sorted tile (stable: waves own contiguous
 //          eighths, ranks inside a 64-record step from ballots on the key bits); the records are
 //          then built from the caller's columns (or rows) read in input order -- coalesced --
@@ -1619,7 +1708,7 @@ flow_hist_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows,
       if (i0 + u * blockDim.x < e) atomicAdd(&h[min(fi[u], n_flows)], 1u);
   }
   __syncthreads();
-  for (uint32_t k = threadIdx.x; k < bins; k += blockDim.x) hist[(size_t)k * n_tiles + blockIdx.x] = h[k];
+  for (uint32_t k = threadIdx.x; k < bins; k += blockDim.x) hist[(size_t)blockIdx.x * bins + k] = h[k];
 }
 
 __global__ void __launch_bounds__(512)
@@ -1676,7 +1765,7 @@ flow_order_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows
   uint32_t run = incl - local;
   for (uint32_t v = 0; v < w; v++) run += wsum[v];
   for (uint32_t k = k0; k < k1; k++) {
-    sbase[k] = start[(size_t)k * n_tiles + t] - run;
+    sbase[k] = start[(size_t)t * bins + k] - run;
 #pragma unroll
     for (uint32_t v = 0; v < kSortWaves; v++) {
       const uint32_t c = cnt[v * bins + k];
@@ -1759,77 +1848,105 @@ flow_order_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows
   }
 }
 
-// scan: start[k * n_tiles + t] = exclusive prefix of hist in flow-major order, in two small
-// kernels (a device-library scan of the ~1M-entry array took 26 us for config 4):
-//   row totals: one block per flow row;
-//   row scan:   one block per flow row, its base = the sum of the earlier rows' totals.
+// scan: start[t * bins + k] = where flow k's records of tile t go -- the exclusive prefix of
+// the tile-major histogram hist[t * bins + k] taken in flow-major order (flow k's runs tile
+// after tile, flows one after another).  Tile-major, so the histogram kernel writes and the
+// order kernel reads one tile's bins contiguously (flow-major arrays made both of them
+// strided: one line per 4-B entry), and start[k] (tile 0) is flow k's first sorted position:
+// the bounds the update kernels read (stride 1).  Three small kernels over chunks of
+// kColTiles tiles: chunk partial sums per flow; one block for the flow totals and their
+// exclusive scan; the chunk scans (each from its flow's base plus the earlier chunks).
+constexpr uint32_t kColTiles = 64;
 __global__ void __launch_bounds__(256)
-flow_row_total_kernel(const uint32_t* __restrict__ hist, uint32_t n_tiles,
-                      uint32_t* __restrict__ totals) {
-  __shared__ uint32_t ws[4];
-  const uint32_t* row = hist + (size_t)blockIdx.x * n_tiles;
-  uint32_t v = 0;
-  for (uint32_t t = threadIdx.x; t < n_tiles; t += 256u) v += row[t];
+flow_colpart_kernel(const uint32_t* __restrict__ hist, uint32_t bins, uint32_t n_tiles,
+                    uint32_t* __restrict__ part) {
+  const uint32_t k = blockIdx.x * 256u + threadIdx.x, c = blockIdx.y;
+  if (k >= bins) return;
+  const uint32_t t0 = c * kColTiles, t1 = min(n_tiles, t0 + kColTiles);
+  uint32_t s = 0;
+  uint32_t t = t0;
+  for (; t + 8u <= t1; t += 8u) {
+    uint32_t x[8];
 #pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
-  if ((threadIdx.x & 63u) == 0) ws[threadIdx.x >> 6] = v;
-  __syncthreads();
-  if (threadIdx.x == 0) totals[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+    for (uint32_t u = 0; u < 8; u++) x[u] = hist[(size_t)(t + u) * bins + k];
+#pragma unroll
+    for (uint32_t u = 0; u < 8; u++) s += x[u];
+  }
+  for (; t < t1; t++) s += hist[(size_t)t * bins + k];
+  part[(size_t)c * bins + k] = s;
 }
 
+// one block: base[k] = records of the flows before k (all chunks' partials summed, then an
+// exclusive scan over the flows; bins <= 2048, two per thread)
 __global__ void __launch_bounds__(1024)
-flow_row_scan_kernel(const uint32_t* __restrict__ hist, uint32_t n_tiles,
-                     const uint32_t* __restrict__ totals, uint32_t* __restrict__ start) {
+flow_colbase_kernel(const uint32_t* __restrict__ part, uint32_t bins, uint32_t n_chunks,
+                    uint32_t* __restrict__ base) {
   __shared__ uint32_t ws[16];
-  __shared__ uint32_t carry_s;
-  const uint32_t k = blockIdx.x, tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
-  // this row's base: the earlier rows' totals
-  uint32_t b = 0;
-  for (uint32_t j = tid; j < k; j += 1024u) b += totals[j];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+  uint32_t tot[2] = {0u, 0u};
 #pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) b += (uint32_t)__shfl_xor((int)b, o);
-  if (lane == 0) ws[w] = b;
-  __syncthreads();
-  if (tid == 0) {
-    uint32_t s0 = 0;
-    for (int i = 0; i < 16; i++) s0 += ws[i];
-    carry_s = s0;
+  for (uint32_t j = 0; j < 2; j++) {
+    const uint32_t k = 2u * tid + j;
+    if (k < bins) {
+      uint32_t c = 0;
+      for (; c + 8u <= n_chunks; c += 8u) {
+        uint32_t x[8];
+#pragma unroll
+        for (uint32_t u = 0; u < 8; u++) x[u] = part[(size_t)(c + u) * bins + k];
+#pragma unroll
+        for (uint32_t u = 0; u < 8; u++) tot[j] += x[u];
+      }
+      for (; c < n_chunks; c++) tot[j] += part[(size_t)c * bins + k];
+    }
   }
+  const uint32_t mine = tot[0] + tot[1];
+  uint32_t incl = mine;
+#pragma unroll
+  for (uint32_t d = 1; d < 64u; d <<= 1) {
+    const uint32_t o = (uint32_t)__shfl_up((int)incl, d);
+    if (lane >= d) incl += o;
+  }
+  if (lane == 63u) ws[w] = incl;
   __syncthreads();
-  uint32_t carry = carry_s;
-  const uint32_t* row = hist + (size_t)k * n_tiles;
-  uint32_t* out = start + (size_t)k * n_tiles;
-  constexpr uint32_t kPer = 4;
-  for (uint32_t c0 = 0; c0 < n_tiles; c0 += 1024u * kPer) {
-    uint32_t x[kPer], tsum = 0;
+  uint32_t b = incl - mine;
+  for (uint32_t v = 0; v < w; v++) b += ws[v];
+  if (2u * tid < bins) base[2u * tid] = b;
+  if (2u * tid + 1u < bins) base[2u * tid + 1u] = b + tot[0];
+}
+
+__global__ void __launch_bounds__(256)
+flow_colscan_kernel(const uint32_t* __restrict__ hist, const uint32_t* __restrict__ part,
+                    const uint32_t* __restrict__ base, uint32_t bins, uint32_t n_tiles,
+                    uint32_t* __restrict__ start) {
+  const uint32_t k = blockIdx.x * 256u + threadIdx.x, c = blockIdx.y;
+  if (k >= bins) return;
+  const uint32_t t0 = c * kColTiles, t1 = min(n_tiles, t0 + kColTiles);
+  uint32_t run = base[k];  // + flow k's records in the chunks before c
+  {
+    uint32_t c2 = 0;
+    for (; c2 + 8u <= c; c2 += 8u) {
+      uint32_t x[8];
 #pragma unroll
-    for (uint32_t u = 0; u < kPer; u++) {
-      const uint32_t t = c0 + tid * kPer + u;
-      x[u] = t < n_tiles ? row[t] : 0u;
-      tsum += x[u];
-    }
-    uint32_t incl = tsum;  // inclusive wave scan of the thread sums
+      for (uint32_t u = 0; u < 8; u++) x[u] = part[(size_t)(c2 + u) * bins + k];
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
-      if (lane >= (uint32_t)o) incl += y;
+      for (uint32_t u = 0; u < 8; u++) run += x[u];
     }
-    __syncthreads();  // ws reuse
-    if (lane == 63u) ws[w] = incl;
-    __syncthreads();
-    uint32_t before = carry + incl - tsum, total = 0;
-    for (uint32_t v = 0; v < 16u; v++) {
-      const uint32_t sv = ws[v];
-      before += v < w ? sv : 0u;
-      total += sv;
-    }
+    for (; c2 < c; c2++) run += part[(size_t)c2 * bins + k];
+  }
+  uint32_t t = t0;
+  for (; t + 8u <= t1; t += 8u) {
+    uint32_t x[8];
 #pragma unroll
-    for (uint32_t u = 0; u < kPer; u++) {
-      const uint32_t t = c0 + tid * kPer + u;
-      if (t < n_tiles) out[t] = before;
-      before += x[u];
+    for (uint32_t u = 0; u < 8; u++) x[u] = hist[(size_t)(t + u) * bins + k];
+#pragma unroll
+    for (uint32_t u = 0; u < 8; u++) {
+      start[(size_t)(t + u) * bins + k] = run;
+      run += x[u];
     }
-    carry += total;
+  }
+  for (; t < t1; t++) {
+    start[(size_t)t * bins + k] = run;
+    run += hist[(size_t)t * bins + k];
   }
 }
 
@@ -1976,8 +2093,8 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
   const uint32_t n_tiles = (n + kTile - 1) / kTile;
   const size_t n_hist = (size_t)bins * n_tiles;
   size_t cub_bytes = 0;
-  if (sort_path == 0)
-    cub_bytes = (size_t)bins * 4u;  // the row totals
+  if (sort_path == 0)  // the chunk partials and their prefixes
+    cub_bytes = (size_t)2u * ((n + kTile - 1) / kTile + kColTiles - 1u) / kColTiles * bins * 4u;
   else
     (void)hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, (const uint32_t*)nullptr,
                                              (uint32_t*)nullptr, (const uint32_t*)nullptr,
@@ -2010,7 +2127,8 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
   double* lat2 = (double*)take(lb);
   FlowBatch* fbatch = (FlowBatch*)take(fbb);
   CloseRec* closes = (CloseRec*)take(cb);
-  uint32_t* long_list = (uint32_t*)take(lfb);  // [0] count, then the flows
+  uint32_t* long_list = (uint32_t*)take(lfb);  // [0] count, then the flows (diagnostics)
+  (void)long_list;
   const uint32_t* bnd;
   uint32_t bstride;
   uint32_t* order = nullptr;
@@ -2022,9 +2140,13 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
     uint32_t* totals = (uint32_t*)take(a256(cub_bytes));
     hipLaunchKernelGGL(flow_hist_kernel, dim3(n_tiles), dim3(512), bins * 4u, stream, flow_idx, n,
                        n_flows, n_tiles, hist);
-    hipLaunchKernelGGL(flow_row_total_kernel, dim3(bins), dim3(256), 0, stream, hist, n_tiles, totals);
-    hipLaunchKernelGGL(flow_row_scan_kernel, dim3(bins), dim3(1024), 0, stream, hist, n_tiles,
-                       totals, start);
+    const uint32_t n_chunks = (n_tiles + kColTiles - 1u) / kColTiles;
+    const dim3 cg((bins + 255u) / 256u, n_chunks);
+    hipLaunchKernelGGL(flow_colpart_kernel, cg, dim3(256), 0, stream, hist, bins, n_tiles, totals);
+    hipLaunchKernelGGL(flow_colbase_kernel, dim3(1), dim3(1024), 0, stream, totals, bins, n_chunks,
+                       totals + (size_t)n_chunks * bins);
+    hipLaunchKernelGGL(flow_colscan_kernel, cg, dim3(256), 0, stream, hist, totals,
+                       totals + (size_t)n_chunks * bins, bins, n_tiles, start);
     e = hipGetLastError();
     if (e != hipSuccess) {
       snprintf(err, errn, "flow_reduce scan: %s", hipGetErrorString(e));
@@ -2041,8 +2163,8 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
     const uint32_t grid = 8u * ((n_tiles + 7u) / 8u);
     hipLaunchKernelGGL(flow_order_kernel, dim3(grid), dim3(64 * kSortWaves), lds, stream,
                        flow_idx, n, n_flows, n_tiles, start, src, recs, order, key_bits, ocut);
-    bnd = start;
-    bstride = n_tiles;
+    bnd = start;  // tile 0's row: flow k starts at start[k]
+    bstride = 1;
   } else {
     uint32_t* keys_in = (uint32_t*)take(nb);
     uint32_t* keys_out = (uint32_t*)take(nb);
@@ -2066,12 +2188,12 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
     bstride = 1;
   }
   if (sabl) return MGENX_OK;  // timing study: ordering only
-  // flows with >= seg_min records in this call: a workgroup each (flow_seg_kernel)
-  uint32_t seg_min = kSegMin;
+  // (diagnostics build: flows with >= MGENX_AN_SEGMIN records in this call get a workgroup
+  // each, flow_seg_kernel)
+  uint32_t seg_min = 0xFFFFFFFFu;
 #if MGENX_DIAG
   if (const char* sm = getenv("MGENX_AN_SEGMIN")) seg_min = (uint32_t)strtoul(sm, nullptr, 10);
-#endif
-  if (seg_min == 0) seg_min = 0xFFFFFFFFu;  // (diagnostics: off)
+  if (seg_min == 0) seg_min = 0xFFFFFFFFu;
   if (seg_min != 0xFFFFFFFFu) {
     if (hipMemsetAsync(long_list, 0, 4, stream) != hipSuccess) {
       snprintf(err, errn, "flow_reduce: memset");
@@ -2083,6 +2205,7 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
                        flows, long_list + 1, long_list, bnd, bstride, recs, order, lat2, reports,
                        per_flow, report_count, report_rec, closes, fbatch);
   }
+#endif
   hipLaunchKernelGGL(flow_update_kernel, dim3((n_flows + 3) / 4), dim3(256), 0, stream, flows,
                      n_flows, bnd, bstride, recs, order, lat2, reports, per_flow, report_count,
                      report_rec, closes, fbatch, n, seg_min);

@@ -11,6 +11,8 @@
 #include <string.h>
 
 #include <chrono>
+#include <emmintrin.h>
+#include <atomic>
 #include <vector>
 
 
@@ -649,6 +651,14 @@ int mgenx_diag_stream_read(mgenx_ctx* ctx, const uint8_t* dev_data, uint64_t byt
   return e == hipSuccess ? MGENX_OK : set_err(ctx, e, "stream_read");
 }
 
+int mgenx_diag_stream_read_w(mgenx_ctx* ctx, const uint8_t* dev_data, uint64_t bytes,
+                             uint32_t* dev_scratch, int grid, int width, void* stream) {
+  if (!ctx || !dev_data || !dev_scratch || grid <= 0) return MGENX_EINVAL;
+  hipError_t e = mgenx::launch_stream_read_w(dev_data, bytes, dev_scratch, grid, width,
+                                             (hipStream_t)stream);
+  return e == hipSuccess ? MGENX_OK : set_err(ctx, e, "stream_read_w");
+}
+
 int mgenx_diag_group_rw(mgenx_ctx* ctx, const uint8_t* dev_data, uint64_t bytes,
                         uint8_t* dev_out, int mode, void* stream) {
   if (!ctx || !dev_data || !dev_out || bytes % 16384 != 0) return MGENX_EINVAL;
@@ -937,6 +947,16 @@ struct mgenx_worker {
 
 static uint32_t w_load(const uint32_t* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
 static void w_store(uint32_t* p, uint32_t v) { __atomic_store_n(p, v, __ATOMIC_RELEASE); }
+// a reply chunk (16 bytes, one load: the worker wrote it with one store) and whether it carries tag r
+struct WChunk {
+  uint32_t w[4];
+};
+static bool w_chunk(const uint32_t* p, uint32_t r, WChunk& c) {
+  const __m128i v = _mm_load_si128(reinterpret_cast<const __m128i*>(p));
+  _mm_storeu_si128(reinterpret_cast<__m128i*>(c.w), v);
+  std::atomic_thread_fence(std::memory_order_acquire);
+  return c.w[3] == r;
+}
 
 // a worker wave serving requests after `start`: the previous one (if any) has ended -- it
 // clears `alive` as its last act -- so reap it and launch the next
@@ -951,28 +971,50 @@ static int worker_launch(mgenx_worker* w, uint32_t start) {
   return MGENX_OK;
 }
 
-// post request `op` (its bytes already in mail->data) and wait for the reply
-static int worker_call(mgenx_worker* w, uint32_t op, uint32_t len, uint32_t arg) {
-  hipSetDevice(w->ctx->device);
+// the request's polled pieces: `pd` (up to kPollData bytes, zero-filled) in pieces 1-15, then
+// piece 0, each with one 16-byte store
+static void w_post(mgenx::WMail* m, uint32_t r, uint32_t op, uint32_t len, uint32_t arg,
+                   const uint8_t* pd, uint32_t pn) {
+  alignas(16) uint8_t piece[16];
+  for (uint32_t k = 1; k < mgenx::kPollPieces; k++) {
+    const uint32_t o = 12u * (k - 1u);
+    const uint32_t c = pn > o ? std::min(12u, pn - o) : 0u;
+    memset(piece, 0, 12);
+    if (c) memcpy(piece, pd + o, c);
+    memcpy(piece + 12, &r, 4);
+    _mm_store_si128(reinterpret_cast<__m128i*>(m->poll + 4u * k),
+                    _mm_load_si128(reinterpret_cast<const __m128i*>(piece)));
+  }
+  std::atomic_thread_fence(std::memory_order_release);
+  const uint32_t p0[4] = {r, op << mgenx::kWorkOpShift | len, arg, 0u};
+  _mm_store_si128(reinterpret_cast<__m128i*>(m->poll), _mm_loadu_si128(reinterpret_cast<const __m128i*>(p0)));
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+}
+
+// post request `op` (bytes beyond the polled ones already in mail->data) and wait for the
+// reply: reply words 24 - 3 * nchunk .. 23 (the last nchunk chunks) into out
+static int worker_call(mgenx_worker* w, uint32_t op, uint32_t len, uint32_t arg, uint32_t nchunk,
+                       uint32_t* out, const uint8_t* pd = nullptr, uint32_t pn = 0) {
   if (!w->launched || !w_load(&w->mail->alive)) {
+    hipSetDevice(w->ctx->device);
     const int rc = worker_launch(w, w->seq);
     if (rc != MGENX_OK) return rc;
   }
   uint32_t r = w->seq + 1u;
   if (r == 0u) r = 1u;  // 0 is "no request yet"
   w->seq = r;
-  w->mail->op = op;
-  w->mail->len = len;
-  w->mail->arg = arg;
-  w_store(&w->mail->req, r);
+  w_post(w->mail, r, op, len, arg, pd, pn);
   // spin on the reply; a wave that ended on its idle timeout just as this request arrived
   // is relaunched, and serves it first
   uint64_t spins = 0, relaunches = 0;
   std::chrono::steady_clock::time_point t0;
-  while (w_load(&w->mail->resp) != r) {
+  WChunk c;
+  const uint32_t* rep = w->mail->reply;
+  while (!w_chunk(rep + 28, r, c)) {
     if ((++spins & 4095u) == 0u) {
-      if (!w_load(&w->mail->alive) && w_load(&w->mail->resp) != r) {
+      if (!w_load(&w->mail->alive) && !w_chunk(rep + 28, r, c)) {
         if (++relaunches > 3) return MGENX_EDEVICE;
+        hipSetDevice(w->ctx->device);
         const int rc = worker_launch(w, r - 1u);
         if (rc != MGENX_OK) return rc;
       }
@@ -985,7 +1027,16 @@ static int worker_call(mgenx_worker* w, uint32_t op, uint32_t len, uint32_t arg)
     }
     __builtin_ia32_pause();
   }
-  return w_load(&w->mail->status) == 0u ? MGENX_OK : MGENX_EDEVICE;
+  // the other chunks of the reply: written by the same store instruction, so at most a few
+  // spins behind the last
+  for (uint32_t k = 0; k < nchunk; k++) {
+    const uint32_t ch = 8u - nchunk + k;
+    WChunk d = c;
+    if (ch != 7u)
+      while (!w_chunk(rep + 4u * ch, r, d)) __builtin_ia32_pause();
+    for (int j = 0; j < 3; j++) out[3u * k + (uint32_t)j] = d.w[j];
+  }
+  return c.w[mgenx::kReplyStatus - 21] == 0u ? MGENX_OK : MGENX_EDEVICE;
 }
 
 int mgenx_worker_create(mgenx_ctx* ctx, uint32_t idle_ms, mgenx_worker** out) {
@@ -1015,8 +1066,7 @@ int mgenx_worker_destroy(mgenx_worker* w) {
       uint32_t r = w->seq + 1u;
       if (r == 0u) r = 1u;
       w->seq = r;
-      w->mail->op = mgenx::kWorkStop;
-      w_store(&w->mail->req, r);
+      w_post(w->mail, r, mgenx::kWorkStop, 0u, 0u, nullptr, 0u);
     }
     (void)hipStreamSynchronize(w->stream);
   }
@@ -1029,9 +1079,13 @@ int mgenx_worker_destroy(mgenx_worker* w) {
 int mgenx_worker_unpack(mgenx_worker* w, const uint8_t* msg, uint32_t len, mgenx_unpacked* out) {
   if (!w || !out || (len && !msg) || len > MGENX_WORKER_MAX_BYTES) return MGENX_EINVAL;
   const uint32_t n = len < mgenx::kWorkerHdrBytes ? len : mgenx::kWorkerHdrBytes;
-  if (n) memcpy(w->mail->data, msg, n);  // Unpack reads the header bytes only
-  const int rc = worker_call(w, mgenx::kWorkUnpack, len, 0u);
-  if (rc == MGENX_OK) memcpy(out, &w->mail->unpacked, sizeof(*out));
+  // Unpack reads the header bytes only: the first kPollData travel in the polled pieces, the
+  // data area is for headers longer than that
+  if (n > mgenx::kPollData) memcpy(w->mail->data, msg, n);
+  uint32_t words[24];
+  const int rc = worker_call(w, mgenx::kWorkUnpack, len, 0u, 8u, words, msg,
+                            n < mgenx::kPollData ? n : mgenx::kPollData);
+  if (rc == MGENX_OK) memcpy(out, words, sizeof(*out));
   return rc;
 }
 
@@ -1046,7 +1100,7 @@ int mgenx_worker_pack(mgenx_worker* w, const mgenx_flow_tmpl* tmpl, const uint8_
     const int rc = mgenx_set_fill_time(w->ctx, fill_time);
     if (rc != MGENX_OK) return rc;
   }
-  mgenx::WPackReq& q = w->mail->pack;
+  mgenx::WPackReq q;
   q.tmpl = *tmpl;
   q.tmpl.payload_off = 0;  // the payload travels in the mailbox
   q.desc = *desc;
@@ -1055,11 +1109,13 @@ int mgenx_worker_pack(mgenx_worker* w, const mgenx_flow_tmpl* tmpl, const uint8_
   q.opts = opts & (MGENX_PACK_CHECKSUM | MGENX_PACK_RANDOM_FILL);
   q.rsv = 0;
   if (tmpl->has_payload && tmpl->payload_len) memcpy(w->mail->data, payload, tmpl->payload_len);
-  const int rc = worker_call(w, mgenx::kWorkPack, buf_len, 0u);
+  uint32_t words[6];  // reply words 18-23
+  const int rc = worker_call(w, mgenx::kWorkPack, buf_len, 0u, 2u, words,
+                            reinterpret_cast<const uint8_t*>(&q), (uint32_t)sizeof(q));
   if (rc != MGENX_OK) return rc;
-  *ret = w_load(&w->mail->ret);
-  *tx_crc = w_load(&w->mail->tx_crc);
-  *state = w_load(&w->mail->state);
+  *ret = words[mgenx::kReplyRet - 18];
+  *tx_crc = words[mgenx::kReplyTx - 18];
+  *state = words[mgenx::kReplyState - 18];
   if (*ret) memcpy(out, w->mail->out, *ret);
   return MGENX_OK;
 }
@@ -1068,8 +1124,9 @@ int mgenx_worker_crc32(mgenx_worker* w, const uint8_t* data, uint32_t len, uint3
                        uint32_t* state_out) {
   if (!w || !state_out || (len && !data) || len > MGENX_WORKER_MAX_BYTES) return MGENX_EINVAL;
   if (len) memcpy(w->mail->data, data, len);
-  const int rc = worker_call(w, mgenx::kWorkCrc32, len, state_in);
-  if (rc == MGENX_OK) *state_out = w_load(&w->mail->crc);
+  uint32_t words[3];  // reply words 21-23
+  const int rc = worker_call(w, mgenx::kWorkCrc32, len, state_in, 1u, words);
+  if (rc == MGENX_OK) *state_out = words[mgenx::kReplyCrc - 21];
   return rc;
 }
 

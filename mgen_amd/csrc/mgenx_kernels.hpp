@@ -83,6 +83,8 @@ hipError_t launch_group_rw(const uint8_t* p, uint64_t bytes, uint8_t* out, int m
                            hipStream_t stream);
 hipError_t launch_stream_read(const uint8_t* p, uint64_t bytes, uint32_t* out, int grid,
                               hipStream_t stream);
+hipError_t launch_stream_read_w(const uint8_t* p, uint64_t bytes, uint32_t* out, int grid,
+                                int width, hipStream_t stream);
 #endif
 hipError_t launch_pack(const PackParams& p, int grid, hipStream_t stream);
 hipError_t launch_pack_prepare(const mgenx_flow_tmpl* tmpl, uint32_t n_tmpl, const uint8_t* pool,
@@ -117,7 +119,7 @@ hipError_t launch_tcp_tail(uint8_t* out, const uint64_t* foff, const uint32_t* f
                            const uint32_t* byte_tab, const uint32_t* a4_tab, const uint32_t* xpow,
                            const uint32_t* ia, const uint32_t* rcrc, hipStream_t s);
 // the resident single-message worker (mgenx_worker.hip): its mailbox in pinned host memory
-constexpr uint32_t kWorkUnpack = 1, kWorkCrc32 = 2, kWorkPack = 3, kWorkStop = 0xFFFFFFFFu;
+constexpr uint32_t kWorkUnpack = 1, kWorkCrc32 = 2, kWorkPack = 3, kWorkStop = 15;
 constexpr uint32_t kWorkerMaxBytes = MGENX_WORKER_MAX_BYTES;
 constexpr uint32_t kWorkerHdrBytes = 1024;  // Unpack reads at most the first 24+255+4+255+19 B
 constexpr uint32_t kWorkerPackMax = MGENX_WORKER_PACK_MAX;  // Pack's bufferLen (built in LDS)
@@ -126,23 +128,31 @@ struct WPackReq {         // mgenx_pack_msgs' inputs for one message (payload in
   mgenx_pack_desc desc;   // words 17..21
   uint32_t buf_len, crc_in, opts, rsv;
 };
+// The request: 16 pieces of 16 bytes that the worker reads whole on every poll, each written by
+// the host with one 16-byte store: piece 0 = {request number, op << 28 | len, arg, 0}, written
+// last; pieces 1-15 = {12 bytes of request data, request number}.  The data are the first
+// kPollData bytes of the message (Unpack: the header, in the common case all of it) or the
+// WPackReq (Pack), so the poll that sees a request brings its data too -- no second round trip
+// to host memory.  A piece whose tag is not the request number was read before the host wrote
+// it: the worker polls again.
+// The reply: 24 words in 8 TAGGED 16-byte chunks, chunk k = {w[3k], w[3k+1], w[3k+2], request
+// number}, each written by one 16-byte store, so the host reads a chunk whole and knows from its
+// tag that it is this request's -- no release fence (a wait for the stores' acknowledgement)
+// between the reply and the worker's next poll.  Words: the mgenx_unpacked (0-21), status (22),
+// crc (23); pack: ret (19), tx_crc (20), state (21), status (22).
+constexpr uint32_t kWorkOpShift = 28, kWorkLenMask = (1u << kWorkOpShift) - 1u;
+constexpr uint32_t kPollPieces = 16, kPollData = 12u * (kPollPieces - 1u);  // 180 bytes
+constexpr uint32_t kReplyStatus = 22, kReplyCrc = 23, kReplyRet = 19, kReplyTx = 20, kReplyState = 21;
 struct alignas(64) WMail {
-  uint32_t req;     // request number: the host writes it last (0 before the first)
-  uint32_t op, len, arg;
-  uint32_t rsv0[12];
-  uint32_t resp;    // reply number: the worker writes it last
-  uint32_t status;  // 0 served
-  uint32_t crc;     // crc32 reply
+  uint32_t poll[4 * kPollPieces];
+  uint32_t resp;    // stop requests: the reply number
   uint32_t alive;   // 1 while a launched worker runs (it clears the word when it ends)
-  uint32_t ret, tx_crc, state;  // pack reply (mgenx_pack_msgs' out_len, tx_crc, state)
-  uint32_t rsv1[9];
-  mgenx_unpacked unpacked;
-  uint8_t rsv2[128 - sizeof(mgenx_unpacked)];
-  WPackReq pack;
-  uint8_t rsv3[128 - sizeof(WPackReq)];
-  uint8_t data[kWorkerMaxBytes + 64];  // the message; 64 bytes of slack for whole 16-B loads
+  uint32_t rsv1[14];
+  uint32_t reply[32];  // 8 tagged chunks
+  uint8_t data[kWorkerMaxBytes + 64];  // the message (beyond the polled bytes); 64 bytes of slack
   uint8_t out[kWorkerPackMax + 64];    // a packed message
 };
+static_assert(sizeof(WPackReq) <= kPollData, "Pack's request travels in the polled pieces");
 hipError_t launch_worker(WMail* m, const uint32_t* a4_tab, const uint32_t* byte_tab,
                          const uint32_t* xpow, const uint8_t* rtab, uint32_t start,
                          uint64_t idle_ticks, hipStream_t stream);

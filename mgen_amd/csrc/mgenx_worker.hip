@@ -34,6 +34,19 @@ __device__ __forceinline__ void st_sys(uint32_t* p, uint32_t v) {
 
 constexpr uint32_t kPiece = 16384;  // bytes of a CRC span staged in LDS at a time
 
+// one 16-byte store that leaves for host memory as one write (system coherent, sc0 sc1): a
+// reply chunk and its tag arrive together
+__device__ __forceinline__ void st_chunk(uint32_t* p, u32x4_t v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+}
+// the polled pieces: lane k < 16 reads piece k (one 16-byte load; volatile: every poll reaches
+// host memory)
+__device__ __forceinline__ u32x4_t poll_pieces(const WMail* m, uint32_t lane) {
+  u32x4_t v = {0u, 0u, 0u, 0u};
+  if (lane < kPollPieces) v = *reinterpret_cast<const volatile u32x4_t*>(m->poll + 4u * lane);
+  return v;
+}
+
 // the 16 mailbox bytes at p (message offset o), bytes at or past n as zero; the mailbox has
 // 64 bytes of slack past its largest message, so the whole 16 are always readable
 __device__ __forceinline__ u32x4_t load_masked(const uint8_t* p, uint32_t o, uint32_t n) {
@@ -88,32 +101,50 @@ worker_kernel(WMail* m, const uint32_t* __restrict__ a4_tab, const uint32_t* __r
   uint32_t last = start;
   uint64_t t_last = __builtin_amdgcn_s_memrealtime();
   for (;;) {
-    // one 16-byte read of the request words: req, op, len, arg share a cache line and the host
-    // writes op/len/arg before req, so a read that sees the new req sees them too (one host
-    // round trip per poll, not one per word).  Volatile: every poll reaches host memory.
-    u32x4_t hq = {0u, 0u, 0u, 0u};
-    if (lane == 0) hq = *reinterpret_cast<const volatile u32x4_t*>(&m->req);
-    const uint32_t r = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl((int)hq.x, 0));
-    if (r == last) {
+    const u32x4_t pc = poll_pieces(m, lane);
+    const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)pc.x, 0);
+    if ((int32_t)(r - last) <= 0) {  // (numbers only grow: an older one is not new)
       if (__builtin_amdgcn_s_memrealtime() - t_last > idle_ticks) break;
       __builtin_amdgcn_s_sleep(2);
       continue;
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the message bytes after the request
-    uint32_t op = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl((int)hq.y, 0));
-    uint32_t len = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl((int)hq.z, 0));
-    const uint32_t arg = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl((int)hq.w, 0));
+    // every data piece written for this request?  (else read before the host wrote it)
+    if (__ballot(lane >= 1u && lane < kPollPieces && pc.w != r)) continue;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the data area after the request
+    const uint32_t ol = (uint32_t)__builtin_amdgcn_readlane((int)pc.y, 0);
+    const uint32_t op = ol >> kWorkOpShift;
+    uint32_t len = ol & kWorkLenMask;
+    const uint32_t arg = (uint32_t)__builtin_amdgcn_readlane((int)pc.z, 0);
+    // the polled data bytes into LDS: piece k's 12 bytes at 12 (k - 1)
+    if (lane >= 1u && lane < kPollPieces) {
+      uint32_t* d = reinterpret_cast<uint32_t*>(buf + 12u * (lane - 1u));
+      d[0] = pc.x;
+      d[1] = pc.y;
+      d[2] = pc.z;
+    }
+    __syncthreads();
     if (op == kWorkStop) {
       if (lane == 0) st_sys_release(&m->resp, r);
       break;
     }
     len = min(len, (uint32_t)kWorkerMaxBytes);
-    uint32_t status = 0, crc = 0;
+    uint32_t status = 0, crc = 0, pk_ret = 0, pk_tx = 0, pk_state = 0;
     if (op == kWorkUnpack) {
-      // the header bytes (at most kWorkerHdrBytes) into LDS, zero past the message
+      // the header bytes (at most kWorkerHdrBytes) in LDS, zero past the message: the polled
+      // bytes when the header lies within them (24 + dst_len + 4 + host_len + 16 <= 180, or
+      // a shorter message), else all of them from the data area
       const uint32_t n = min(len, (uint32_t)kWorkerHdrBytes);
-      for (uint32_t o = 16u * lane; o < kWorkerHdrBytes; o += 1024u)
-        *reinterpret_cast<u32x4_t*>(buf + o) = load_masked(m->data + o, o, n);
+      uint32_t need = 24u + buf[23];
+      if (need + 4u <= min(n, kPollData)) need += 4u + buf[need + 3u] + 16u;
+      else need += 4u;
+      __syncthreads();  // (every lane has read the length bytes)
+      if (min(n, need) <= kPollData) {  // (the host zero-filled the polled bytes past the message)
+        for (uint32_t o = kPollData + 4u * lane; o < kWorkerHdrBytes; o += 256u)
+          *reinterpret_cast<uint32_t*>(buf + o) = 0u;
+      } else {
+        for (uint32_t o = 16u * lane; o < kWorkerHdrBytes; o += 1024u)
+          *reinterpret_cast<u32x4_t*>(buf + o) = load_masked(m->data + o, o, n);
+      }
       __syncthreads();
       if (lane == 0) {
         uint32_t w[8];
@@ -151,11 +182,13 @@ worker_kernel(WMail* m, const uint32_t* __restrict__ a4_tab, const uint32_t* __r
           reinterpret_cast<uint32_t*>(u.host_addr)[j] = h.host_addr[j];
         }
         *reinterpret_cast<mgenx_unpacked*>(rq) = u;  // staged in LDS for the lanes' stores
+        rq[kReplyStatus] = 0u;
+        rq[kReplyCrc] = 0u;
       }
       __syncthreads();
-      if (lane < 6u)  // 96 bytes (the reply area is 128): six 16-byte stores in one instruction
-        *reinterpret_cast<u32x4_t*>(reinterpret_cast<uint8_t*>(&m->unpacked) + 16u * lane) =
-            *reinterpret_cast<const u32x4_t*>(rq + 4u * lane);
+      if (lane < 8u)  // the 8 tagged chunks in one instruction
+        st_chunk(m->reply + 4u * lane, u32x4_t{rq[3u * lane], rq[3u * lane + 1u], rq[3u * lane + 2u], r});
+      __syncthreads();
     } else if (op == kWorkCrc32) {
       // the span in LDS pieces; each piece's raw CRC from lane partials, folded into the
       // running state: crc(A || B) = x^(8|B|) crc(A) ^ crc(B)
@@ -183,9 +216,8 @@ worker_kernel(WMail* m, const uint32_t* __restrict__ a4_tab, const uint32_t* __r
       // it (mgenx_pack.hip: layout, truncation, the payload_len zeroing, RANDOM_FILL after two
       // zero bytes, CHECKSUM flag, ComputeCRC32 over msgLen - 4 with LAST_BUFFER), with the
       // message built whole in LDS and checksummed by the wave
-      if (lane < 8u)
-        *reinterpret_cast<u32x4_t*>(rq + 4u * lane) =
-            *reinterpret_cast<const u32x4_t*>(reinterpret_cast<const uint8_t*>(&m->pack) + 16u * lane);
+      if (lane < 8u)  // the WPackReq, from the polled bytes
+        *reinterpret_cast<u32x4_t*>(rq + 4u * lane) = *reinterpret_cast<const u32x4_t*>(buf + 16u * lane);
       __syncthreads();
       const uint32_t* tw = rq;  // the template, 17 words (mgenx_flow_tmpl)
       const uint32_t d_seq = rq[18], d_sec = rq[19], d_usec = rq[20];
@@ -297,28 +329,25 @@ worker_kernel(WMail* m, const uint32_t* __restrict__ a4_tab, const uint32_t* __r
           tx = raw ^ (crc_len ? multmodp(xpow8(crc_len, xpow), init) : init);
           flags &= ~(uint32_t)MGENX_FLAG_LAST_BUFFER;
         }
-        // 5. the message out
+        // 5. the message out, visible before the reply's tags (release)
         for (uint32_t o = 16u * lane; o < ret; o += 1024u)
           *reinterpret_cast<u32x4_t*>(m->out + o) = *reinterpret_cast<const u32x4_t*>(buf + o);
-        if (lane == 0) {
-          st_sys(&m->ret, ret);
-          st_sys(&m->tx_crc, tx);
-          st_sys(&m->state, (uint32_t)len | (flags & 0xffu) << 16);
-        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        pk_ret = ret;
+        pk_tx = tx;
+        pk_state = (uint32_t)len | (flags & 0xffu) << 16;
         __syncthreads();
-      } else if (lane == 0) {  // Pack failed: nothing written
-        st_sys(&m->ret, 0u);
-        st_sys(&m->tx_crc, crc_in);
-        st_sys(&m->state, 0xFFFFu | (flags & 0xffu) << 16);
+      } else {  // Pack failed: nothing written
+        pk_ret = 0u;
+        pk_tx = crc_in;
+        pk_state = 0xFFFFu | (flags & 0xffu) << 16;
       }
     } else {
       status = 1;
     }
-    if (lane == 0) {
-      st_sys(&m->status, status);
-      st_sys(&m->crc, crc);
-      st_sys_release(&m->resp, r);
-    }
+    if (op != kWorkUnpack && lane < 2u)  // chunks 6 and 7: w18-20 = 0, ret, tx_crc; w21-23 = state, status, crc
+      st_chunk(m->reply + 4u * (6u + lane), lane == 0u ? u32x4_t{0u, pk_ret, pk_tx, r}
+                                                      : u32x4_t{pk_state, status, crc, r});
     last = r;
     t_last = __builtin_amdgcn_s_memrealtime();
   }

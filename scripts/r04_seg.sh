@@ -1,5 +1,6 @@
 #!/bin/bash
-# Round 4: the workgroup-per-flow analytics path -- parity tests, then config-4 timing + trace.
+# Round 4: the workgroup-per-flow analytics path -- parity tests, config-4 timing (product),
+# the diagnostics build's seg off / on and order-phase timing, seg-kernel phase stamps.
 set -u
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -10,8 +11,7 @@ step() {  # step <name> <timeout> <cmd...>
   tail -${TAILN:-15} "gpurun_out/$name.log"
   if [ $rc -ne 0 ]; then echo "STEP $name FAILED rc=$rc"; exit $rc; fi
 }
-#step an_tests 600 python -u -m pytest tests/test_gpu_analytics.py -m gpu -x -q --timeout 120 --timeout-method thread
-#step c4 180 python -u scripts/c4_only.py
-#step c4prof 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/c4prof3 -o c4 -- python3 -u scripts/c4_only.py
-#python3 scripts/c4_dispatch.py gpurun_out/c4prof3/c4_kernel_trace.csv
+step an_tests 600 python -u -m pytest tests/test_gpu_analytics.py -m gpu -x -q --timeout 120 --timeout-method thread
+step c4 180 python -u scripts/c4_only.py
+step ocut 600 python -u scripts/an_ocut.py
 step segprof 300 python -u scripts/seg_prof.py

@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round 4: the resident worker -- parity tests, shim single-call latency.
+set -u
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {  # step <name> <timeout> <cmd...>
+  local name=$1 t=$2; shift 2
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  tail -${TAILN:-15} "gpurun_out/$name.log"
+  if [ $rc -ne 0 ]; then echo "STEP $name FAILED rc=$rc"; exit $rc; fi
+}
+step wk_tests 300 python -u -m pytest tests/test_gpu_worker.py tests/test_gpu_pack_msgs.py tests/test_compat_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread -s
+step shim_lat 120 tests/cpp/shim_latency

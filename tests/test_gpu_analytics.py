@@ -275,15 +275,7 @@ def test_flow_reduce_skewed_flows_tile_runs(torch, eng):
     compare(st, rep, cnt, of, orep, ocnt, per_flow)
 
 
-@pytest.mark.parametrize("window", [0.001, 0.3])
-def test_flow_reduce_workgroup_path_mixed_lengths(torch, eng, window):
-    """Flows of 1 to 20000 records in one call -- below 2048 records a wave per flow
-    (flow_update_kernel), from 2048 on a workgroup per flow (flow_seg_kernel), the longest in
-    several passes of 8192 records -- with jumpy sequences (mask restarts, records below
-    `first`, wraps, duplicates, reordering) and, at 1 ms, a window closing every record or two
-    (more reports than per_flow keeps); a second call continues from the first's state (the
-    two kernels hand flows to each other).  Against the oracle."""
-    from oracle import oracle as O
+def _mixed_lengths():
     sets = []
     for i, per in enumerate((1, 700, 2040, 2048, 2100, 5000, 9000, 20000)):
         d = _jumpy_flows(1, per, seed=100 + i)
@@ -292,7 +284,17 @@ def test_flow_reduce_workgroup_path_mixed_lengths(torch, eng, window):
     d = {k: np.concatenate([s[k] for s in sets]) for k in sets[0]}
     rx = d["rx_sec"].astype(np.int64) * 10**6 + d["rx_usec"]
     o = np.argsort(rx, kind="stable")
-    d = {k: np.ascontiguousarray(v[o]) for k, v in d.items()}
+    return {k: np.ascontiguousarray(v[o]) for k, v in d.items()}
+
+
+@pytest.mark.parametrize("window", [0.001, 0.3])
+def test_flow_reduce_mixed_lengths(torch, eng, window):
+    """Flows of 1 to 20000 records in one call with jumpy sequences (mask restarts, records
+    below `first`, wraps, duplicates, reordering) and, at 1 ms, a window closing every record
+    or two (more reports than per_flow keeps); a second call continues from the first's
+    state.  Against the oracle."""
+    from oracle import oracle as O
+    d = _mixed_lengths()
     n_flows, per_flow = 8, 4096
     st, rep, cnt, _ = run_gpu(torch, eng, d, n_flows, window, per_flow,
                               splits=(0, len(d["seq"]) * 3 // 4))
@@ -301,3 +303,33 @@ def test_flow_reduce_workgroup_path_mixed_lengths(torch, eng, window):
                                          d["rx_usec"], window=window, per_flow=per_flow)
     assert sum(a.dup_msg_count for a in of) > 0
     compare(st, rep, cnt, of, orep, ocnt, per_flow)
+
+
+@pytest.mark.parametrize("window", [0.001, 0.3])
+def test_flow_reduce_workgroup_path_diag(torch, window, monkeypatch):
+    """The workgroup-per-flow path (flow_seg_kernel: segments walked in series, duplicates and
+    aggregates in parallel, the latency sums in LDS), built only into the diagnostics library
+    (measured slower than the wave path), enabled with MGENX_AN_SEGMIN: flows
+    of 2048 records and more take it, shorter ones the wave kernel, and the two hand flows to
+    each other across calls.  Bit-exact against the oracle like the product path."""
+    from mgen_amd import Engine
+    from oracle import oracle as O
+    monkeypatch.setenv("MGENX_AN_SEGMIN", "2048")
+    e = Engine(0, diag=True)
+    try:
+        d = _mixed_lengths()
+        n_flows, per_flow = 8, 4096
+        st, rep, cnt, _ = run_gpu(torch, e, d, n_flows, window, per_flow,
+                                  splits=(0, len(d["seq"]) * 3 // 4))
+        of, orep, ocnt = O.flow_reduce_batch(n_flows, d["flow_id"] - 1, d["seq"], d["tx_sec"],
+                                             d["tx_usec"], d["msg_len"], d["rx_sec"],
+                                             d["rx_usec"], window=window, per_flow=per_flow)
+        compare(st, rep, cnt, of, orep, ocnt, per_flow)
+        d = _jumpy_flows(40, 6000, seed=int(window * 1000) + 3)
+        st, rep, cnt, _ = run_gpu(torch, e, d, 40, window, 64, splits=(0, 5000))
+        of, orep, ocnt = O.flow_reduce_batch(40, d["flow_id"] - 1, d["seq"], d["tx_sec"],
+                                             d["tx_usec"], d["msg_len"], d["rx_sec"],
+                                             d["rx_usec"], window=window, per_flow=64)
+        compare(st, rep, cnt, of, orep, ocnt, 64)
+    finally:
+        e.close()
