@@ -490,9 +490,10 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
 
   // Per-lane partials of the bulk runs, folded into the wave-uniform state by flush() before
   // every exact update and at the end: latency min / max, bytes, and the highest seq - first
-  // (for `last`).  msg_count == 1 (the byte restart of :128-129) and msg_count == 0 (min / max
-  // set by the first counted latency, :132-133) arise only from an exact update, which flushes
-  // first, so at those points nothing is pending.
+  // (for `last`).  msg_count == 0 (min / max set by the first counted latency, :132-133) means
+  // no counted record is pending.  msg_count == 1 (the byte restart of :128-129) also arises
+  // from a run that counted one record from 0, its size pending: a run or a cheap restart
+  // that meets msg_count == 1 with partials pending flushes first.
   const double inf = __builtin_huge_val();
   double pmin = inf, pmax = -inf;
   uint32_t pbytes = 0, pdmax = 0, prounds = 0;
@@ -523,6 +524,10 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
 
   // records [k, ev) of the round: a bulk run (every one simple, valid && m.n)
   auto bulk = [&](uint32_t k, uint32_t ev) {
+    // a run at msg_count == 1 replaces byte_count (:128-129), pending bytes included: a run
+    // before it (the previous round's, or one before a cheap restart) that took msg_count
+    // from 0 to 1 left its one record's size pending -- fold it first
+    if (msg_count == 1 && dirty) flush();
     if (lane < 32u) scat[wv][lane] = 0u;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -661,11 +666,12 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
         // counted, Set fails, UnsetBits clears every set index (all below seq) -> mask {seq}.
         // No flush: the pending bytes / min / max stay pending (order-free); only the pending
         // `last` partials, relative to the old first, are dropped (last = seq now).
+        if (msg_count <= 1 && dirty) flush();  // (the replace at 1 covers pending bytes)
         pdmax = 0;
         m.w = lane == ((seq >> 5) & 31u) ? (1u << (seq & 31u)) : 0u;
         m.first = m.last = seq;
         m.n = 1;
-        if (msg_count == 1) byte_count = len;  // nothing pending at msg_count <= 1
+        if (msg_count == 1) byte_count = len;  // (flushed above: nothing pending)
         else byte_count += len;
         if (msg_count == 0) {
           lmin = lmax = lat;
