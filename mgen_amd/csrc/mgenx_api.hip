@@ -496,8 +496,8 @@ int mgenx_pack_msgs(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
 // the stream length and the round count (the plan kernel's maximum fragment count) for
 // the host, in one 16-byte copy
 __global__ void tcp_totals_kernel(const uint32_t* max_frag, uint32_t n, const uint64_t* off,
-                                  uint64_t* out) {
-  out[0] = off[n];
+                                  const uint64_t* bytes, uint64_t* out) {
+  out[0] = off[n - 1] + bytes[n - 1];  // (the exclusive scan's last offset + its message)
   out[1] = *max_frag;
 }
 
@@ -562,24 +562,13 @@ int mgenx_pack_tcp(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl, const uint32
   if ((e = mgenx::launch_tcp_plan(dev_tmpl, dev_desc, dev_msg_total, n, bytes, nfrag, max_frag,
                                   s)) != hipSuccess)
     return set_err(ctx, e, "tcp plan");
-  uint64_t* offs = foff;  // reused below only after the copy out
-  if ((e = hipcub::DeviceScan::ExclusiveSum(cub, cub_bytes, (const uint64_t*)bytes, offs,
-                                            (int)(n + 1), s)) != hipSuccess)
+  // the message offsets straight into the caller's array (n entries); the total from its last
+  // (a scan of n + 1 into the workspace and a copy out cost a 512-KiB copy for config 5)
+  if ((e = hipcub::DeviceScan::ExclusiveSum(cub, cub_bytes, (const uint64_t*)bytes, dev_msg_off,
+                                            (int)n, s)) != hipSuccess)
     return set_err(ctx, e, "tcp scan");
-  if ((e = hipMemcpyAsync(dev_msg_off, offs, (size_t)n * 8, hipMemcpyDeviceToDevice, s)) != hipSuccess)
-    return set_err(ctx, e, "tcp");
-  hipLaunchKernelGGL(tcp_totals_kernel, dim3(1), dim3(1), 0, s, max_frag, n, offs, ctx->tcp_host_dev);
-  if ((e = hipStreamSynchronize(s)) != hipSuccess) return set_err(ctx, e, "tcp plan");
-  const uint64_t total = ((volatile uint64_t*)ctx->tcp_host)[0];
-  const uint32_t rounds = (uint32_t)((volatile uint64_t*)ctx->tcp_host)[1];
-  *total_bytes = total;
-  if (total > stream_cap || (total && !dev_stream)) {
-    snprintf(ctx->err, sizeof(ctx->err), "tcp: the stream needs %llu bytes",
-             (unsigned long long)total);
-    return MGENX_EINVAL;
-  }
   const int ck = (opts & MGENX_PACK_CHECKSUM) ? 1 : 0;
-  for (uint32_t r = 0; r < rounds; r++) {
+  auto round = [&](uint32_t r) -> int {
     if ((e = mgenx::launch_tcp_frag(dev_desc, dev_msg_total, nfrag, dev_msg_off, n, r, ck,
                                     st[(r + 1) & 1], fd, foff, fbuf, ff, s)) != hipSuccess)
       return set_err(ctx, e, "tcp fragments");
@@ -590,9 +579,27 @@ int mgenx_pack_tcp(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl, const uint32
     if ((e = mgenx::launch_tcp_tail(dev_stream, foff, fbuf, ff, plen, crc, st[r & 1], n, ck,
                                     (opts & MGENX_PACK_RANDOM_FILL) ? 1 : 0, acrc,
                                     ctx->d_bytetab, ctx->d_tabs + 1024, ctx->d_xpow, ctx->d_ia,
-                                    ctx->d_rcrc, s)) !=
-        hipSuccess)
+                                    ctx->d_rcrc, stream_cap, s)) != hipSuccess)
       return set_err(ctx, e, "tcp tail");
+    return MGENX_OK;
+  };
+  hipLaunchKernelGGL(tcp_totals_kernel, dim3(1), dim3(1), 0, s, max_frag, n, dev_msg_off, bytes,
+                     ctx->tcp_host_dev);
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return set_err(ctx, e, "tcp plan");
+  const uint64_t total = ((volatile uint64_t*)ctx->tcp_host)[0];
+  const uint32_t rounds = (uint32_t)((volatile uint64_t*)ctx->tcp_host)[1];
+  *total_bytes = total;
+  if (total > stream_cap || (total && !dev_stream)) {
+    snprintf(ctx->err, sizeof(ctx->err), "tcp: the stream needs %llu bytes",
+             (unsigned long long)total);
+    return MGENX_EINVAL;
+  }
+  // (the rounds return unsynchronised: back-to-back calls keep the GPU busy while the host
+  // enqueues the next plan; packing before the read-back, with one sync at the end instead,
+  // measured 0.314 ms against 0.293 for config 5 in the bench's back-to-back timing)
+  for (uint32_t r = 0; r < rounds; r++) {
+    const int rc = round(r);
+    if (rc != MGENX_OK) return rc;
   }
   return MGENX_OK;
 }

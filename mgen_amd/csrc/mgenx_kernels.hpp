@@ -117,7 +117,7 @@ hipError_t launch_tcp_tail(uint8_t* out, const uint64_t* foff, const uint32_t* f
                            const uint32_t* ff, const uint32_t* plen, const uint32_t* tx_crc,
                            const uint32_t* state, uint32_t n, int ck, int rnd, uint32_t* acrc,
                            const uint32_t* byte_tab, const uint32_t* a4_tab, const uint32_t* xpow,
-                           const uint32_t* ia, const uint32_t* rcrc, hipStream_t s);
+                           const uint32_t* ia, const uint32_t* rcrc, uint64_t cap, hipStream_t s);
 // the resident single-message worker (mgenx_worker.hip): its mailbox in pinned host memory
 constexpr uint32_t kWorkUnpack = 1, kWorkCrc32 = 2, kWorkPack = 3, kWorkStop = 15;
 constexpr uint32_t kWorkerMaxBytes = MGENX_WORKER_MAX_BYTES;

@@ -229,11 +229,12 @@ __global__ void tcp_finish_kernel(uint8_t* __restrict__ out, const uint64_t* __r
                                   const uint32_t* __restrict__ plen, const uint32_t* __restrict__ tx_crc,
                                   const uint32_t* __restrict__ state, const uint32_t* __restrict__ acrc,
                                   const uint32_t* __restrict__ xpow, const uint32_t* __restrict__ ia,
-                                  uint32_t n, int ck) {
+                                  uint32_t n, int ck, uint64_t cap) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t F = ff[i], B = fbuf[i];
   if (!ck || !F || plen[i] == 0) return;
+  if (foff[i] > cap || F > cap - foff[i]) return;  // a stream that does not fit: no store past it
   uint32_t c = tx_crc[i];
   bool write = true;
   if (F <= B) {
@@ -282,12 +283,12 @@ hipError_t launch_tcp_tail(uint8_t* out, const uint64_t* foff, const uint32_t* f
                            const uint32_t* ff, const uint32_t* plen, const uint32_t* tx_crc,
                            const uint32_t* state, uint32_t n, int ck, int rnd, uint32_t* acrc,
                            const uint32_t* byte_tab, const uint32_t* a4_tab, const uint32_t* xpow,
-                           const uint32_t* ia, const uint32_t* rcrc, hipStream_t s) {
+                           const uint32_t* ia, const uint32_t* rcrc, uint64_t cap, hipStream_t s) {
   if (ck) {
     hipLaunchKernelGGL(tcp_prefix_kernel, dim3((n + 255) / 256), dim3(256), 0, s, out, foff, fbuf,
                        ff, plen, state, n, ck, rnd, byte_tab, a4_tab, xpow, rcrc, acrc);
     hipLaunchKernelGGL(tcp_finish_kernel, dim3((n + 255) / 256), dim3(256), 0, s, out, foff, fbuf,
-                       ff, plen, tx_crc, state, acrc, xpow, ia, n, ck);
+                       ff, plen, tx_crc, state, acrc, xpow, ia, n, ck, cap);
   }
   return hipGetLastError();
 }

@@ -71,22 +71,9 @@ if g0:
                         "ratio": round(hbm / algo, 4),
                         "read_bytes": int(k["fetch_kb_raw"] * 1024 * factor),
                         "write_bytes": int(k["write_kb"] * 1024)}
-# config 4 receive pipeline on rows (traffic_probe.py's second part): per-kernel bytes, summed
-n4_file = os.path.join(out_dir, "traffic_probe_n4.txt")
-N4 = int(open(n4_file).read()) if os.path.exists(n4_file) else 0
-if N4:
-    stage = {}
-    for k, v in res.items():
-        for tag in ("unpack_fixed_kernel<4,", "flowtab", "flow_", "radix", "Radix"):
-            if tag in k:
-                stage[k] = {"read_bytes_est": int(2 * v["fetch_kb_raw"] * 1024),
-                            "write_bytes": int(v["write_kb"] * 1024)}
-    out["config4_rows_pipeline"] = {
-        "records": N4, "kernels": stage,
-        "note": "read bytes = FETCH_SIZE x 2 (the guide's streaming-read factor; an estimate "
-                "for the gather / hash accesses)",
-        "algorithmic_bytes": {"unpack": N4 * (256 + 32), "findflow": N4 * (32 + 20 + 4),
-                              "reduce": N4 * (4 + 16 + 8)}}
+# config 4: profiles/r04/traffic_config4.json (scripts/pmc_c4.sh: FETCH calibrated per access
+# shape, per kernel algorithmic bytes)
+out["config4"] = "profiles/r04/traffic_config4.json"
 os.makedirs("profiles", exist_ok=True)
 json.dump(out, open(f"profiles/traffic_{ROUND}.json", "w"), indent=1)
 json.dump(out, open(f"{out_dir}/traffic_{ROUND}.json", "w"), indent=1)   # merged back by gpurun

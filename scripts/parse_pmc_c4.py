@@ -70,8 +70,10 @@ plan = [
     ("flow_update_kernel", 24, n * 24, n * 8),
     ("flow_chain_kernel", 8, n * 8, 0),
     ("unpack_fixed_kernel<4", 16, n * 64, n * 32),
-    ("flowtab", 16, n * (32 + 20), n * 4),
+    ("flowtab_insert_kernel", 16, n * (32 + 20), n * 4),
 ]
+SMALL = ("flowtab_first", "flowtab_offsets", "flowtab_number", "flowtab_resolve",
+         "flowtab_commit", "flow_init", "flow_long")
 out = {"records": n, "flows": F, "fetch_factor_per_shape": {str(k): round(v, 4) for k, v in factors.items()},
        "note": __doc__.split("\n\n")[1].replace("\n", " "), "kernels": {}}
 ROWS_ALGO = {"flow_order_kernel": (n * (32 + 8 + 4) + H, n * 24)}  # rows path: row + rx + index
@@ -108,6 +110,12 @@ for pat, w, ar0, aw0 in plan:
         if t:
             e["algorithmic_TBps"] = round((ar + aw) / (t * 1e-6) / 1e12, 3)
         out["kernels"][name + (" [" + lab + "]" if lab else "")] = e
+# the small steps (FindFlow numbering, flow init): raw counters and times only
+for k in fetch:
+    if any(x in k for x in SMALL):
+        out["kernels"][k.split("(")[0]] = {"launches": len(fetch[k]), "fetch_kb_raw": med(fetch[k]),
+                                           "write_kb": med(write.get(k, [0.0])),
+                                           "time_us": med(dur.get(k, [])), "note": "small step"}
 os.makedirs("profiles/r04", exist_ok=True)
 json.dump(out, open("profiles/r04/traffic_config4.json", "w"), indent=1)
 json.dump(out, open(f"{out_dir}/traffic_config4.json", "w"), indent=1)

@@ -2,9 +2,7 @@
 3 launches each after a 512 MiB flush (> Infinity Cache): the plain stream read of the 1 GiB
 slab, the unpack's read pattern alone (mgenx_diag_group_rw mode 0: exactly the slab bytes in
 the unpack's own access shape -> FETCH_SIZE calibration for that shape), the product unpack
-with 32-B row output (the bench headline), and the same with the SoA columns.  Then config 4's
-receive pipeline on rows (8.4M 256-B datagrams: unpack -> FindFlow from the rows ->
-mgenx_flow_reduce_rows), one flush before each pipeline run."""
+with 32-B row output (the bench headline), and the same with the SoA columns.  (Config 4: scripts/traffic_c4.py.)"""
 import os
 import sys
 
@@ -39,41 +37,4 @@ torch.cuda.synchronize()
 assert int((cols["err"] != 0).sum()) == 0
 del cols, rows, probe, slab
 
-# config 4 on rows
-import numpy as np  # noqa: E402
-from mgen_amd import DESC_DTYPE  # noqa: E402
-from mgen_amd.workloads import make_templates, poisson_flows  # noqa: E402
-NF, MSG = 1024, 256
-d = poisson_flows(8 * N, NF, mean_gap_us=1000)
-n = len(d["seq"])
-tmpl, pool = make_templates(NF)
-desc = np.zeros(n, DESC_DTYPE)
-desc["tmpl"], desc["seq_num"] = d["flow_id"] - 1, d["seq"]
-desc["tx_sec"], desc["tx_usec"], desc["msg_len"] = d["tx_sec"], d["tx_usec"], MSG
-dt, dp = to_device(tmpl), to_device(pool)
-crc = torch.empty(NF, dtype=torch.int32, device="cuda")
-eng.pack_prepare(dt, NF, dp, crc)
-slab = torch.empty(n * MSG, dtype=torch.uint8, device="cuda")
-eng.pack(dt, crc, to_device(desc), n, dp, slab, stride=MSG)
-rows = {"rows": eng.alloc_rows(n)}
-fid = torch.from_numpy(d["flow_id"].astype(np.int64)).cuda()
-src = torch.zeros(n, 20, dtype=torch.uint8, device="cuda")
-src[:, 0], src[:, 1], src[:, 2], src[:, 3], src[:, 4] = 1, 4, 0x89, 0x13, 10
-src[:, 6], src[:, 7] = ((fid >> 8) & 255).to(torch.uint8), (fid & 255).to(torch.uint8)
-rx_s = torch.from_numpy(d["rx_sec"]).cuda()
-rx_u = torch.from_numpy(d["rx_usec"]).cuda()
-fidx = torch.empty(n, dtype=torch.int32, device="cuda")
-nf = torch.zeros(1, dtype=torch.int32, device="cuda")
-table = eng.flow_table(2 * NF)
-for _ in range(3):
-    flush.fill_(1)
-    eng.unpack(slab, n, stride=MSG, fixed_len=MSG, cols=rows)
-    eng.flow_lookup(table, rows, src.reshape(-1), n, flow_idx=fidx, n_flows=nf)
-    flows = eng.flow_init(NF, 1.0)
-    eng.flow_reduce_rows(flows, NF, fidx, rows["rows"], rx_s, rx_u, n=n)
-torch.cuda.synchronize()
-assert int(nf.cpu()[0]) == NF
-eng.flow_table_destroy(table)
-os.makedirs("gpurun_out", exist_ok=True)
-open("gpurun_out/traffic_probe_n4.txt", "w").write(str(n))
-print("traffic probe done", n)
+print("traffic probe done")

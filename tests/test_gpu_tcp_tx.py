@@ -115,3 +115,36 @@ def test_tcp_tx_config5_frames_and_checks(torch, eng, gold):
     torch.cuda.synchronize()
     assert int((cols["err"] != 0).sum()) == 0
     assert np.array_equal(cols["seq_num"].cpu().numpy().view(np.uint32), np.arange(n))
+
+
+def test_tcp_tx_short_buffer_no_store_past_it(torch, eng, gold):
+    """mgenx_pack_tcp with a buffer shorter than the stream reports the length and fails, and
+    stores nothing past the buffer's end (checked on a sentinel region after it); a right-sized
+    call after it is exact, multi-fragment messages included."""
+    import ctypes
+    from mgen_amd import PACK_CHECKSUM, to_device
+    from mgen_amd import _ptr, _stream
+    rng = np.random.default_rng(17)
+    d, total = _case(gold, rng, [16384] * 40 + [200000] * 3)
+    tm, pool = to_device(gold["tmpl"]), to_device(gold["pool"])
+    crc = torch.empty(len(gold["tmpl"]), dtype=torch.int32, device="cuda")
+    eng.pack_prepare(tm, len(gold["tmpl"]), pool, crc)
+    dd, dt = to_device(d), to_device(total)
+    # a one-fragment call first (rounds hint 1), then the multi-round case on a short buffer
+    small_d, small_t = _case(gold, rng, [1000] * 8)
+    eng.pack_tcp(tm, crc, to_device(small_d), to_device(small_t), 8, pool, opts=PACK_CHECKSUM)
+    want, _ = eng.pack_tcp(tm, crc, dd, dt, len(d), pool, opts=PACK_CHECKSUM)
+    want = want.cpu().numpy()
+    n_total = len(want)
+    cap = n_total // 2
+    buf = torch.full((n_total + 65536,), 0xAB, dtype=torch.uint8, device="cuda")
+    offs = torch.empty(len(d), dtype=torch.int64, device="cuda")
+    tot = ctypes.c_uint64(0)
+    rc = eng.lib.mgenx_pack_tcp(eng.ctx, _ptr(tm), _ptr(crc), _ptr(dd), _ptr(dt), len(d),
+                                _ptr(pool), _ptr(buf), cap, _ptr(offs), ctypes.byref(tot),
+                                PACK_CHECKSUM, 0, _stream(eng.device))
+    torch.cuda.synchronize()
+    assert rc != 0 and tot.value == n_total
+    assert bool((buf[cap:] == 0xAB).all())
+    got, _ = eng.pack_tcp(tm, crc, dd, dt, len(d), pool, opts=PACK_CHECKSUM)
+    assert np.array_equal(got.cpu().numpy(), want)
