@@ -59,4 +59,5 @@ for name, v in (("pack_kernel", pk), ("unpack_var_kernel", up)):
                             "ratio": round((rd + wr) / (ar + aw), 4)}
 os.makedirs(f"profiles/{ROUND}", exist_ok=True)
 json.dump(out, open(f"profiles/{ROUND}/traffic_config3.json", "w"), indent=1)
+json.dump(out, open(f"{out_dir}/traffic_config3.json", "w"), indent=1)  # merged back by gpurun
 print(json.dumps(out, indent=1))
