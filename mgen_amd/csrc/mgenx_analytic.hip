@@ -249,25 +249,43 @@ struct RecSrc {
   const mgenx_rec* rows;
   const uint32_t *rxs, *rxu;
 };
-__device__ __forceinline__ FRec make_frec(const RecSrc& src, uint32_t i) {
-  FRec r;
-  uint32_t ts, tu;
-  if (src.rows) {
+// a record's raw fields as loaded (the order kernel keeps the next tile's in registers while it
+// writes the current one: the latency math waits for the loads, so it runs at placement)
+struct RawRec {
+  uint32_t seq, ts, tu, len, rs, ru;
+};
+template <bool kRows>
+__device__ __forceinline__ RawRec load_rec_t(const RecSrc& src, uint32_t i) {
+  RawRec r;
+  if (kRows) {
     const u32x4_t h = *reinterpret_cast<const u32x4_t*>(src.rows + i);  // flow, seq, tx_sec, tx_usec
     r.seq = h.y;
-    ts = h.z;
-    tu = h.w;
+    r.ts = h.z;
+    r.tu = h.w;
     r.len = src.rows[i].msg_len;
   } else {
     r.seq = src.seq[i];
-    ts = src.txs[i];
-    tu = src.txu[i];
+    r.ts = src.txs[i];
+    r.tu = src.txu[i];
     r.len = src.len[i];
   }
-  const uint32_t rs = src.rxs[i], ru = src.rxu[i];
-  r.rxk = (uint64_t)rs << 32 | ru;
-  r.latency = tdelta(Tm{(int64_t)rs, (int64_t)ru}, Tm{(int64_t)ts, (int64_t)tu});
+  r.rs = src.rxs[i];
+  r.ru = src.rxu[i];
   return r;
+}
+__device__ __forceinline__ RawRec load_rec(const RecSrc& src, uint32_t i) {
+  return src.rows ? load_rec_t<true>(src, i) : load_rec_t<false>(src, i);
+}
+__device__ __forceinline__ FRec build_frec(const RawRec& w) {
+  FRec r;
+  r.seq = w.seq;
+  r.len = w.len;
+  r.rxk = (uint64_t)w.rs << 32 | w.ru;
+  r.latency = tdelta(Tm{(int64_t)w.rs, (int64_t)w.ru}, Tm{(int64_t)w.ts, (int64_t)w.tu});
+  return r;
+}
+__device__ __forceinline__ FRec make_frec(const RecSrc& src, uint32_t i) {
+  return build_frec(load_rec(src, i));
 }
 
 // Wave-uniform values: the window times come out of FP64 arithmetic (VALU), so without
@@ -319,6 +337,33 @@ struct CloseRec {
 // ballots, bytes / min / max / last by per-lane partials folded before an exact step (flush).
 // The first non-simple record (window end, mask restart, a record below `first`, an empty mask,
 // the first record of a flow) takes the exact update below, and the run restarts after it.
+#if MGENX_DIAG
+// (diagnostics) cycles of flow_update_kernel's first wave by phase: detect, bulk, exact, lat'
+// store, rounds, exact steps, bulk runs, total
+__device__ unsigned long long g_upd_prof[8];
+#define UPD_T(slot)                                                        \
+  do {                                                                     \
+    if (prof_on) {                                                         \
+      const unsigned long long now_ = __builtin_amdgcn_s_memtime();        \
+      prof[slot] += now_ - prof_t;                                         \
+      prof_t = now_;                                                       \
+    }                                                                      \
+  } while (0)
+#else
+#define UPD_T(slot) \
+  do {              \
+  } while (0)
+#endif
+__device__ __forceinline__ double vmin64(double a, double b) {
+  double r;
+  asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ double vmax64(double a, double b) {
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 constexpr uint32_t kUR = 4;             // records per lane and round
 constexpr uint32_t kRound = 64u * kUR;  // records per round
 constexpr uint32_t kLatRounds = 4;      // rounds of lat' staged in LDS per store burst
@@ -576,35 +621,48 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       __builtin_amdgcn_wave_barrier();
     }
-    uint32_t n_cnt = 0, n_dup = 0, n_new = 0, len1 = 0;
+    // per record group: three ballots and branch-free per-lane partials (no branch per group:
+    // a select the compiler turns into an exec-mask branch costs more than the select)
+    uint32_t n_cnt = 0, n_cand = 0, n_new = 0;
+    uint64_t cms[kUR];
 #pragma unroll
     for (uint32_t q = 0; q < kUR; q++) {
-      const bool dup = cand[q] && (inring[q] || indup[q]);
-      const bool nw = cand[q] && !dup;
-      const bool counted = nw && (int32_t)(cur[q].seq - seq_start) >= 0;
-      const uint64_t cm = __ballot(counted);
-      if (cm && n_cnt == 0)  // the run's first counted record: its size
-        len1 = (uint32_t)__builtin_amdgcn_readlane((int)cur[q].len, (int)__builtin_ctzll(cm));
-      n_cnt += (uint32_t)__popcll(cm);
-      n_dup += (uint32_t)__popcll(__ballot(dup));
+      // (bitwise: && evaluates its right side under an exec mask, a branch)
+      const bool nw = cand[q] & !inring[q] & !indup[q];
+      const bool counted = nw & ((int32_t)(cur[q].seq - seq_start) >= 0);
+      cms[q] = __ballot(counted);
+      n_cnt += (uint32_t)__popcll(cms[q]);
       n_new += (uint32_t)__popcll(__ballot(nw));
+      n_cand += (uint32_t)__popcll(__ballot(cand[q]));
       const double lat = cur[q].latency;
       pbytes += counted ? cur[q].len : 0u;
-      // min / max as compare-selects (latencies are never NaN or -0, so these equal fmin /
-      // fmax, without the canonicalising moves those cost)
-      pmin = (counted && lat < pmin) ? lat : pmin;
-      pmax = (counted && lat > pmax) ? lat : pmax;
-      pdmax = cand[q] ? max(pdmax, cur[q].seq - m.first) : pdmax;
+      // min / max (latencies are never NaN or -0, so v_min / v_max equal the compare-selects;
+      // fmin would canonicalise its operands first)
+      pmin = vmin64(pmin, counted ? lat : inf);
+      pmax = vmax64(pmax, counted ? lat : -inf);
+      pdmax = max(pdmax, cand[q] ? cur[q].seq - m.first : 0u);
       latp[q] = counted ? lat : latp[q];
     }
+    const uint32_t n_dup = n_cand - n_new;
     if (n_cnt) {
       // :128-129: a counted record arriving at msg_count == 1 replaces byte_count by its size
       // (nothing is pending then, see above): at 1 the run's bytes replace it; at 0 the first
       // counted record adds and the second replaces, so the first one's size drops out
       if (msg_count == 1) byte_count = 0;
       if (msg_count == 0) {
-        if (n_cnt >= 2) byte_count -= len1;  // byte_count is 0 here; the flush adds it back
-        lmin = inf;                          // :132-133: the first counted latency sets both
+        if (n_cnt >= 2) {  // the run's first counted record: its size
+          uint32_t len1 = 0;
+          bool got = false;
+#pragma unroll
+          for (uint32_t q = 0; q < kUR; q++) {
+            if (!got && cms[q]) {
+              len1 = (uint32_t)__builtin_amdgcn_readlane((int)cur[q].len, (int)__builtin_ctzll(cms[q]));
+              got = true;
+            }
+          }
+          byte_count -= len1;  // byte_count is 0 here; the flush adds it back
+        }
+        lmin = inf;  // :132-133: the first counted latency sets both
         lmax = -inf;
       }
       msg_count += n_cnt;
@@ -618,10 +676,18 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
 
   ld(b, cur);
   ld(b + kRound, nxt);
+#if MGENX_DIAG
+  const bool prof_on = blockIdx.x == 0 && wv == 0;
+  unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0}, prof_t = __builtin_amdgcn_s_memtime();
+  const unsigned long long prof_t0 = prof_t;
+#endif
   for (uint32_t i0 = b; i0 < e; i0 += kRound) {
     FRec nx2[kUR];
     ld(i0 + 2u * kRound, nx2);
     const uint32_t cnt = min(kRound, e - i0);
+#if MGENX_DIAG
+    prof[4]++;
+#endif
 #pragma unroll
     for (uint32_t q = 0; q < kUR; q++) latp[q] = 0.0;
     uint32_t k = 0;
@@ -632,13 +698,23 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
 #pragma unroll
         for (uint32_t q = 0; q < kUR; q++) {
           const uint32_t p = 64u * q + lane;
-          const bool simple = cur[q].rxk < wek && (cur[q].len == 0u || cur[q].seq - m.first < kDepth);
-          const uint64_t ns = __ballot(p >= k && p < cnt && !simple);
+          const bool simple = (cur[q].rxk < wek) & ((cur[q].len == 0u) | (cur[q].seq - m.first < kDepth));
+          const uint64_t ns = __ballot((p >= k) & (p < cnt) & !simple);  // (bitwise: no exec branches)
           if (ns) ev = min(ev, 64u * q + (uint32_t)__builtin_ctzll(ns));
         }
-        if (ev > k) bulk(k, ev);
+        UPD_T(0);
+        if (ev > k) {
+          bulk(k, ev);
+#if MGENX_DIAG
+          prof[6]++;
+#endif
+        }
+        UPD_T(1);
       }
       if (ev >= cnt) break;
+#if MGENX_DIAG
+      prof[5]++;
+#endif
       const uint32_t q = ev >> 6, l = ev & 63u;
       uint32_t seq = 0, len = 0, rlo = 0, rhi = 0, llo = 0, lhi = 0;
 #pragma unroll
@@ -688,6 +764,7 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
 #pragma unroll
       for (uint32_t qq = 0; qq < kUR; qq++) latp[qq] = (qq == q && lane == l) ? lp : latp[qq];
       k = ev + 1u;
+      UPD_T(2);
     }
     // lat' leaves through LDS, kLatRounds rounds at a time: gfx950 counts stores in vmcnt, so
     // a round's stores would hold up the waits for the next rounds' record loads until they
@@ -712,7 +789,14 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
       nxt[q] = nx2[q];
     }
     if (++prounds == 4096u) flush();  // per-lane bytes stay below 2^32
+    UPD_T(3);
   }
+#if MGENX_DIAG
+  if (prof_on && lane == 0) {
+    prof[7] = __builtin_amdgcn_s_memtime() - prof_t0;
+    for (int k2 = 0; k2 < 8; k2++) g_upd_prof[k2] = prof[k2];
+  }
+#endif
 
   flush();
   m.store_relative(sp->mask);
@@ -1717,141 +1801,230 @@ flow_hist_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows,
   for (uint32_t k = threadIdx.x; k < bins; k += blockDim.x) hist[(size_t)blockIdx.x * bins + k] = h[k];
 }
 
+// inclusive prefix sum over the wave's 64 lanes in DPP steps (rows of 16 by shifts, then the
+// row broadcasts) -- no LDS round trips, unlike __shfl_up
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return v;
+}
+
+// LDS-only block barrier: the block's LDS accesses before it are complete after it, while its
+// global loads and stores stay in flight (__syncthreads' workgroup fence waits for every
+// outstanding global access too, which would drain the next tile's prefetch)
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+constexpr uint32_t kOrdStart = (kCountBins + 511u) / 512u;  // start entries per thread
+#if MGENX_DIAG
+// (diagnostics) cycles of flow_order_kernel's block 0, wave 0 by phase: zero, scan (incl. the
+// count barrier), ranks + placement, prefetch issue, writes, tiles, count (incl. the key wait),
+// total
+__device__ unsigned long long g_ord_prof[8];
+#define ORD_T(slot)                                                        \
+  do {                                                                     \
+    if (prof_on) {                                                         \
+      const unsigned long long now_ = __builtin_amdgcn_s_memtime();        \
+      prof[slot] += now_ - prof_t;                                         \
+      prof_t = now_;                                                       \
+    }                                                                      \
+  } while (0)
+#else
+#define ORD_T(slot) \
+  do {              \
+  } while (0)
+#endif
+
+// Persistent: one block per CU walks its tiles, and the next tile's keys, start row and raw
+// records are loaded while the current tile's runs are written, so the reads of one tile and
+// the writes of the one before share the memory system (one tile per block and phase after
+// phase left the chip reading, then writing: 190 us for config 4).
+template <bool kRows>
 __global__ void __launch_bounds__(512)
 flow_order_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows,
                   uint32_t n_tiles, const uint32_t* __restrict__ start, RecSrc src,
-                  FRec* __restrict__ recs, uint32_t* __restrict__ order, uint32_t key_bits,
-                  uint32_t cut) {  // cut: diagnostics only (phase timing), 0 = the whole kernel
+                  FRec* __restrict__ recs, uint32_t* __restrict__ order, uint32_t key_bits) {
   extern __shared__ uint32_t lds[];
   const uint32_t bins = n_flows + 1u;
   uint32_t* cnt = lds;                                // [wave][bin]: counts, then run bases
   uint32_t* sbase = lds + kSortWaves * bins;          // [bin]: start - tile offset
-  __shared__ uint32_t wsum[kSortWaves];
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
-  // tile: contiguous ranges per XCD (block b runs on XCD b % 8)
-  const uint32_t per = (n_tiles + 7u) / 8u;
-  const uint32_t t = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
-  if (t >= n_tiles) return;  // whole block: no barrier below is reached by anyone
-  for (uint32_t k = tid; k < kSortWaves * bins; k += blockDim.x) cnt[k] = 0u;
-  __syncthreads();
-  const uint32_t t0 = t * kTile;
-  const uint32_t a = t0 + w * kPart, e = min(n, a + kPart);
-  uint32_t* my = cnt + w * bins;
-  // the wave's kPart keys, loaded once (all in flight together) for both passes below
-  constexpr uint32_t kKeys = kPart / 64u;
-  uint32_t keys[kKeys];
-#pragma unroll
-  for (uint32_t j = 0; j < kKeys; j++) {
-    const uint32_t i = a + 64u * j + lane;
-    keys[j] = i < e ? min(idx[i], n_flows) : 0xFFFFFFFFu;
-  }
-#pragma unroll
-  for (uint32_t j = 0; j < kKeys; j++)
-    if (keys[j] != 0xFFFFFFFFu) atomicAdd(&my[keys[j]], 1u);
-  __syncthreads();
-  if (cut == 1) {
-    if (my[lane] == 0xFFFFFFFFu) recs[0].seq = 1u;
-    return;
-  }
-  // tile offsets: exclusive scan over bins of the tile's counts (thread j owns bins j*B..)
-  const uint32_t B = (bins + blockDim.x - 1u) / blockDim.x;
-  const uint32_t k0 = min(tid * B, bins), k1 = min(k0 + B, bins);
-  uint32_t local = 0;
-  for (uint32_t k = k0; k < k1; k++)
-#pragma unroll
-    for (uint32_t v = 0; v < kSortWaves; v++) local += cnt[v * bins + k];
-  uint32_t incl = local;  // inclusive wave scan
-#pragma unroll
-  for (uint32_t o = 1; o < 64u; o <<= 1) {
-    const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
-    if (lane >= o) incl += y;
-  }
-  if (lane == 63u) wsum[w] = incl;
-  __syncthreads();
-  uint32_t run = incl - local;
-  for (uint32_t v = 0; v < w; v++) run += wsum[v];
-  for (uint32_t k = k0; k < k1; k++) {
-    sbase[k] = start[(size_t)t * bins + k] - run;
-#pragma unroll
-    for (uint32_t v = 0; v < kSortWaves; v++) {
-      const uint32_t c = cnt[v * bins + k];
-      cnt[v * bins + k] = run;
-      run += c;
-    }
-  }
-  __syncthreads();
-  if (cut == 2) {
-    if (sbase[tid] == 0xFFFFFFFFu) recs[0].seq = 2u;
-    return;
-  }
-  // each record's position in the flow-sorted tile (stable: waves own contiguous eighths,
-  // ranks inside a 64-record step from ballots on the key bits), kept in registers
-  const uint64_t lt = (1ull << lane) - 1ull;
-  uint32_t pos[kKeys];
-#pragma unroll
-  for (uint32_t j = 0; j < kKeys; j++) {
-    const uint32_t i = a + 64u * j + lane;
-    const bool live = i < e;
-    const uint32_t key = live ? keys[j] : 0u;
-    uint64_t peers = __ballot(live);  // lanes holding the same key
-    for (uint32_t bt = 0; bt < key_bits; bt++) {
-      const bool one = (key >> bt) & 1u;
-      const uint64_t bb = __ballot(one);
-      peers &= one ? bb : ~bb;
-    }
-    const uint32_t rank = (uint32_t)__popcll(peers & lt);
-    const uint32_t base = live ? my[key] : 0u;
-    pos[j] = base + rank;
-    if (live && rank + 1u == (uint32_t)__popcll(peers)) my[key] = base + rank + 1u;
-  }
-  if (cut == 3) {
-    uint32_t x = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < kKeys; j++) x ^= pos[j];
-    if (x == 0xFFFFFFFFu) recs[0].seq = 3u;
-    return;
-  }
-  // the records, read in input order (consecutive lanes, consecutive records: coalesced
-  // column loads), built into their sorted slots of the tile in LDS (the input index - t0 in
-  // the high half of `len`, for `order`) ...
   FRec* lrec = reinterpret_cast<FRec*>(sbase + bins + (bins & 1u));  // 8-byte aligned
   uint16_t* lkey = reinterpret_cast<uint16_t*>(lrec + kTile);
-  constexpr uint32_t kOrdU = 4;
+  __shared__ uint32_t wsum[kSortWaves];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+  // tiles: XCD x (block b runs on XCD b % 8) owns tiles [x * per, (x + 1) * per), its nb blocks
+  // take them nb apart, so the tiles in flight on one XCD are neighbours and the runs of one
+  // flow from adjacent tiles meet in that XCD's L2
+  const uint32_t per = (n_tiles + 7u) / 8u, nb = gridDim.x >> 3;
+  const uint32_t xb = (blockIdx.x & 7u) * per;
+  uint32_t ci = blockIdx.x >> 3;
+  if (ci >= per || xb + ci >= n_tiles) return;  // whole block: no barrier is reached by anyone
+  uint32_t t = xb + ci;
+  uint32_t* my = cnt + w * bins;
+  uint64_t* tab = reinterpret_cast<uint64_t*>(lrec) + (size_t)w * kCountBins;
+  constexpr uint32_t kKeys = kPart / 64u;
+  // scan ownership: thread tid owns bins [k0, k1)
+  const uint32_t B = (bins + blockDim.x - 1u) / blockDim.x;
+  const uint32_t k0 = min(tid * B, bins), k1 = min(k0 + B, bins);
+  uint32_t keys[kKeys], st[kOrdStart];
+  RawRec raw[kKeys];
+  // the wave's kPart keys, the tile's start row (this thread's bins) and its raw records, all
+  // issued together (clamped indices: no branch, nothing waits here)
+  auto fetch = [&](uint32_t tt) {
+    const uint32_t a = tt * kTile + w * kPart;
 #pragma unroll
-  for (uint32_t j0 = 0; j0 < kKeys; j0 += kOrdU) {
-    FRec r[kOrdU];
+    for (uint32_t j = 0; j < kKeys; j++) keys[j] = idx[min(a + 64u * j + lane, n - 1u)];
 #pragma unroll
-    for (uint32_t u = 0; u < kOrdU; u++)
-      r[u] = make_frec(src, min(a + 64u * (j0 + u) + lane, n - 1u));
+    for (uint32_t q = 0; q < kOrdStart; q++)
+      st[q] = start[(size_t)tt * bins + min(k0 + q, bins - 1u)];
 #pragma unroll
-    for (uint32_t u = 0; u < kOrdU; u++) {
-      const uint32_t i = a + 64u * (j0 + u) + lane;
-      if (i < e) {
-        r[u].len |= (i - t0) << 16;
-        lrec[pos[j0 + u]] = r[u];
-        lkey[pos[j0 + u]] = (uint16_t)keys[j0 + u];
+    for (uint32_t j = 0; j < kKeys; j++) raw[j] = load_rec_t<kRows>(src, min(a + 64u * j + lane, n - 1u));
+  };
+  fetch(t);
+  for (uint32_t k = tid; k < kSortWaves * bins; k += blockDim.x) cnt[k] = 0u;
+  const uint64_t lt = (1ull << lane) - 1ull;
+#if MGENX_DIAG
+  const bool prof_on = blockIdx.x == 0 && w == 0;
+  unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0}, prof_t = __builtin_amdgcn_s_memtime();
+  const unsigned long long prof_t0 = prof_t;
+#endif
+  while (true) {
+    const uint32_t t0 = t * kTile;
+    const uint32_t a = t0 + w * kPart, e = min(n, a + kPart);
+    lds_barrier();  // (every wave is past the last tile's writes, which read lrec, and zeroing)
+    ORD_T(0);
+    // the wave's peer table (in lrec, free until the placement): tab[key] collects the lanes
+    // of one 64-record step holding that key
+    for (uint32_t k = lane; k < bins; k += 64u) tab[k] = 0ull;
+#pragma unroll
+    for (uint32_t j = 0; j < kKeys; j++) {
+      keys[j] = a + 64u * j + lane < e ? min(keys[j], n_flows) : 0xFFFFFFFFu;
+      if (keys[j] != 0xFFFFFFFFu) atomicAdd(&my[keys[j]], 1u);
+    }
+    ORD_T(6);
+    lds_barrier();
+    // tile offsets: exclusive scan over bins of the tile's counts
+    uint32_t local = 0;
+    for (uint32_t k = k0; k < k1; k++)
+#pragma unroll
+      for (uint32_t v = 0; v < kSortWaves; v++) local += cnt[v * bins + k];
+    const uint32_t incl = wave_incl_scan(local);
+    if (lane == 63u) wsum[w] = incl;
+    lds_barrier();
+    uint32_t run = incl - local;
+    for (uint32_t v = 0; v < w; v++) run += wsum[v];
+#pragma unroll
+    for (uint32_t q = 0; q < kOrdStart; q++) {
+      const uint32_t k = k0 + q;
+      if (k < k1) {
+        sbase[k] = st[q] - run;
+#pragma unroll
+        for (uint32_t v = 0; v < kSortWaves; v++) {
+          const uint32_t c = cnt[v * bins + k];
+          cnt[v * bins + k] = run;
+          run += c;
+        }
       }
     }
-  }
-  __syncthreads();
-  if (cut == 4) {
-    if (lkey[tid] == 0xFFFFu) recs[0].seq = 4u;
-    return;
-  }
-  // ... and written out run by run: consecutive lanes, consecutive slots (whole lines but at
-  // the runs' ends; runs of one flow from neighbouring tiles meet in L2).  (Scattering each
-  // record from its input position instead wrote partial lines: 258 us for config 4.)
-  const uint32_t tn = min(n - t0, kTile);
-  for (uint32_t j = tid; j < tn; j += blockDim.x) {
-    const uint32_t k = lkey[j];
-    if (k < n_flows) {
-      FRec r = lrec[j];
-      const uint32_t g = sbase[k] + j;
-      if (order) order[g] = t0 + (r.len >> 16);
-      r.len &= 0xFFFFu;
-      recs[g] = r;
+    lds_barrier();
+    ORD_T(1);
+    // each record's position in the flow-sorted tile, stable: waves own contiguous eighths,
+    // and inside a 64-record step a record's rank is the number of lower lanes with its key.
+    // The lanes with one key (`peers`) come from the wave's table (OR in the lane bits, read,
+    // clear: same-wave LDS operations complete in order, and these relaxed atomics on
+    // possibly-equal addresses keep program order); the last lane of each group adds the
+    // group's size to the key's running base and the group reads the old base from it.
+    uint64_t peers[kKeys];
+#pragma unroll
+    for (uint32_t j = 0; j < kKeys; j++) {
+      peers[j] = 0ull;
+      if (keys[j] != 0xFFFFFFFFu) {
+        uint64_t* slot = &tab[keys[j]];
+        __hip_atomic_fetch_or(slot, 1ull << lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        peers[j] = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        __hip_atomic_store(slot, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+      }
     }
+    uint32_t pos[kKeys], old[kKeys];
+#pragma unroll
+    for (uint32_t j = 0; j < kKeys; j++) {  // all the adds in flight together ...
+      const uint32_t rank = (uint32_t)__popcll(peers[j] & lt);
+      const uint32_t size = (uint32_t)__popcll(peers[j]);
+      old[j] = 0u;
+      if (keys[j] != 0xFFFFFFFFu && rank + 1u == size)
+        old[j] = __hip_atomic_fetch_add(&my[keys[j]], size, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_WAVEFRONT);
+      pos[j] = rank;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kKeys; j++) {  // ... then the bases to the groups
+      const uint32_t last = 63u - (uint32_t)__builtin_clzll(peers[j] | 1ull);
+      pos[j] += (uint32_t)__shfl((int)old[j], (int)last);
+    }
+    // the peer table's slots are about to be overwritten by the records: every lane of the
+    // wave is past its last table access once its own ops have completed (in order), but other
+    // waves' tables overlap this wave's record slots
+    lds_barrier();
+    // the records built (latency, input index - t0 in the high half of `len`, for `order`)
+    // into their slots
+#pragma unroll
+    for (uint32_t j = 0; j < kKeys; j++) {
+      if (keys[j] != 0xFFFFFFFFu) {
+        const uint32_t i = a + 64u * j + lane;
+        FRec r = build_frec(raw[j]);
+        r.len |= (i - t0) << 16;
+        lrec[pos[j]] = r;
+        lkey[pos[j]] = (uint16_t)keys[j];
+      }
+    }
+    lds_barrier();
+    ORD_T(2);
+    // the next tile's loads go out before this tile's stores (unconditionally -- the last
+    // pass reloads its own tile -- so the loads land in the loop's registers with no copy,
+    // which would wait for them)
+    ci += nb;
+    const bool more = ci < per && xb + ci < n_tiles;
+    fetch(more ? xb + ci : t);
+    ORD_T(3);
+    // the counts of the next tile start from zero (the ranks above were the last use)
+    for (uint32_t k = tid; k < kSortWaves * bins; k += blockDim.x) cnt[k] = 0u;
+    // this tile's runs: consecutive lanes, consecutive slots (whole lines but at the runs'
+    // ends; runs of one flow from neighbouring tiles meet in L2).  (As 8-B words, consecutive
+    // lanes on consecutive words, the stores cover contiguous 512 B each but take 24 per
+    // thread and three LDS reads a word: slower, 134 vs 130 us for config 4.)
+    const uint32_t tn = min(n - t0, kTile);
+#pragma unroll
+    for (uint32_t u = 0; u < kTile / 512u; u++) {
+      const uint32_t j = tid + 512u * u;
+      const uint32_t k = j < tn ? lkey[j] : 0xFFFFu;
+      if (k < n_flows) {
+        FRec r = lrec[j];
+        const uint32_t g = sbase[k] + j;
+        if (order) order[g] = t0 + (r.len >> 16);
+        r.len &= 0xFFFFu;
+        recs[g] = r;
+      }
+    }
+    ORD_T(4);
+#if MGENX_DIAG
+    prof[5]++;
+#endif
+    if (!more) break;
+    t = xb + ci;
   }
+#if MGENX_DIAG
+  if (prof_on && lane == 0) {
+    prof[7] = __builtin_amdgcn_s_memtime() - prof_t0;
+    for (int k2 = 0; k2 < 8; k2++) g_ord_prof[k2] = prof[k2];
+  }
+#endif
 }
 
 // scan: start[t * bins + k] = where flow k's records of tile t go -- the exclusive prefix of
@@ -2024,6 +2197,7 @@ using namespace mgenx;
 struct mgenx_flow_ws {
   void* mem = nullptr;
   size_t bytes = 0;
+  uint32_t cu = 0;  // the device's CU count (the order kernel's persistent grid)
 };
 
 extern "C" void* mgenx_flow_ws_new() { return new mgenx_flow_ws(); }
@@ -2050,6 +2224,12 @@ static double quantized_window(double value) {
 
 #if MGENX_DIAG
 extern "C" int mgenx_diag_seg_prof(unsigned long long* out, int n) {
+  if (out && n == 16)  // flow_order_kernel's phase cycles (g_ord_prof, 8 entries)
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ord_prof), 64) == hipSuccess ? MGENX_OK
+                                                                              : MGENX_EDEVICE;
+  if (out && n == 8)  // flow_update_kernel's phase cycles (g_upd_prof)
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_upd_prof), 64) == hipSuccess ? MGENX_OK
+                                                                              : MGENX_EDEVICE;
   if (!out || n < (int)(kSegWaves * 12)) return MGENX_EINVAL;
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_seg_prof), kSegWaves * 12 * 8) == hipSuccess
              ? MGENX_OK
@@ -2087,11 +2267,9 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
   const RecSrc src = {seq, txs, txu, len, rows, rxs, rxu};
   int sort_path = (uint64_t)n_flows + 1 <= kCountBins ? 0 : 1;  // 0 counting, 1 radix
   int sabl = 0;      // diagnostics build only: ordering-only timing (MGENX_AN_SABL)
-  uint32_t ocut = 0;  // diagnostics build only: order kernel cut after a phase (MGENX_AN_OCUT)
 #if MGENX_DIAG
   if (const char* sp = getenv("MGENX_AN_RADIX")) sort_path = atoi(sp) ? 1 : sort_path;
   if (const char* sa = getenv("MGENX_AN_SABL")) sabl = atoi(sa);
-  if (const char* oc = getenv("MGENX_AN_OCUT")) ocut = (uint32_t)atoi(oc);
 #endif
   const uint32_t bins = n_flows + 1u;
   uint32_t key_bits = 1;
@@ -2161,14 +2339,28 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
     // LDS: per-wave counts, the run bases, the tile's records and their flows
     const uint32_t lds = (kSortWaves * bins + bins + (bins & 1u)) * 4u +
                          kTile * (uint32_t)sizeof(FRec) + kTile * 2u;
-    e = set_max_lds((const void*)flow_order_kernel, (int)kOrderLds + 8);
+    const void* okern = src.rows ? (const void*)flow_order_kernel<true>
+                                 : (const void*)flow_order_kernel<false>;
+    e = set_max_lds(okern, (int)kOrderLds + 8);
     if (e != hipSuccess) {
       snprintf(err, errn, "flow_reduce order: %s", hipGetErrorString(e));
       return MGENX_EDEVICE;
     }
-    const uint32_t grid = 8u * ((n_tiles + 7u) / 8u);
-    hipLaunchKernelGGL(flow_order_kernel, dim3(grid), dim3(64 * kSortWaves), lds, stream,
-                       flow_idx, n, n_flows, n_tiles, start, src, recs, order, key_bits, ocut);
+    // persistent: one block per CU (LDS allows one), a multiple of 8 (one set per XCD)
+    if (!ws.cu) {
+      int dev = 0, cu = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cu = 256;
+      ws.cu = (uint32_t)max(8, cu);
+    }
+    const uint32_t grid = 8u * min((n_tiles + 7u) / 8u, ws.cu / 8u);
+    if (src.rows)
+      hipLaunchKernelGGL(flow_order_kernel<true>, dim3(grid), dim3(64 * kSortWaves), lds, stream,
+                         flow_idx, n, n_flows, n_tiles, start, src, recs, order, key_bits);
+    else
+      hipLaunchKernelGGL(flow_order_kernel<false>, dim3(grid), dim3(64 * kSortWaves), lds, stream,
+                         flow_idx, n, n_flows, n_tiles, start, src, recs, order, key_bits);
     bnd = start;  // tile 0's row: flow k starts at start[k]
     bstride = 1;
   } else {

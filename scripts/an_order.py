@@ -1,8 +1,7 @@
-"""Phase timing of mgenx_flow_reduce's ordering on config-4 data (diagnostics build): the
-ordering alone (MGENX_AN_SABL=1) with the order kernel cut after phase k (MGENX_AN_OCUT: 1
-counts, 2 scan, 3 ranks, 4 records in LDS, 0 whole), for the full 8M records / 1024 flows and
-rank 0's share at N = 8; then the whole reduce with the workgroup path off / on
-(MGENX_AN_SEGMIN=0 / default).  Results are wrong under a cut; timing only."""
+"""Timing of mgenx_flow_reduce on config-4 data (diagnostics build): the ordering alone
+(MGENX_AN_SABL=1) and the whole reduce, for the full 8M records / 1024 flows and rank 0's share
+at N = 8.  (Round 4's phase cuts of the one-tile-per-block order kernel, MGENX_AN_OCUT, went
+with that kernel.)"""
 import os
 import subprocess
 import sys
@@ -11,8 +10,7 @@ import time
 import numpy as np
 
 if len(sys.argv) == 1:
-    runs = [("cut%s" % c, dict(MGENX_AN_SABL="1", MGENX_AN_OCUT=c)) for c in "12340"]
-    runs += [("seg_off", dict(MGENX_AN_SEGMIN="0")), ("seg_on", {})]
+    runs = [("order_only", dict(MGENX_AN_SABL="1")), ("reduce", {})]
     for name, extra in runs:
         env = dict(os.environ, **extra)
         r = subprocess.run([sys.executable, __file__, "run"], env=env, capture_output=True,
