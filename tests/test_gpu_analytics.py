@@ -333,3 +333,59 @@ def test_flow_reduce_workgroup_path_diag(torch, window, monkeypatch):
         compare(st, rep, cnt, of, orep, ocnt, 64)
     finally:
         e.close()
+
+
+def test_flow_reduce_config4_full_size_vs_oracle(torch, eng):
+    """Config 4 at its full size (8,388,608 records, 1024 POISSON flows): 2048 tiles, so every
+    persistent order block walks several tiles (the next tile's loads in flight while the
+    current one is written), for the column and the row form with report_rec, against the
+    oracle."""
+    from mgen_amd import FLOW_REPORT_DTYPE, FLOW_STATE_DTYPE, REC_DTYPE
+    from mgen_amd.workloads import poisson_flows
+    from oracle import oracle as O
+    n_flows, per_flow, window = 1024, 4, 1.0
+    d = poisson_flows(8_388_608, n_flows, mean_gap_us=1000, seed=44, loss=0.01, dup=0.005,
+                      reorder=10)
+    n = len(d["seq"])
+    assert n > 256 * 4096  # more tiles than one pass of the persistent grid
+    idx = dev(torch, (d["flow_id"] - 1).astype(np.uint32))
+    rows = np.zeros(n, REC_DTYPE)
+    rows["flow_id"], rows["seq_num"] = d["flow_id"], d["seq"]
+    rows["tx_sec"], rows["tx_usec"], rows["msg_len"] = d["tx_sec"], d["tx_usec"], d["msg_len"]
+    out = []
+    for use_rows in (False, True):
+        flows = eng.flow_init(n_flows, window)
+        reports = torch.zeros(n_flows * per_flow * 96, dtype=torch.uint8, device="cuda")
+        count = torch.zeros(n_flows, dtype=torch.int32, device="cuda")
+        rrec = torch.zeros(n_flows * per_flow, dtype=torch.int32, device="cuda")
+        if use_rows:
+            eng.flow_reduce_rows(flows, n_flows, idx, dev(torch, rows.view(np.uint8)),
+                                 dev(torch, d["rx_sec"]), dev(torch, d["rx_usec"]),
+                                 reports=reports, per_flow=per_flow, report_count=count,
+                                 report_rec=rrec)
+        else:
+            c = {k: dev(torch, v) for k, v in d.items()}
+            eng.flow_reduce(flows, n_flows, idx, c["seq"], c["tx_sec"], c["tx_usec"],
+                            c["msg_len"], c["rx_sec"], c["rx_usec"], reports=reports,
+                            per_flow=per_flow, report_count=count, report_rec=rrec)
+        torch.cuda.synchronize()
+        out.append((flows.cpu().numpy(), reports.cpu().numpy(), count.cpu().numpy(),
+                    rrec.cpu().numpy()))
+    for a, b in zip(*out):
+        assert np.array_equal(a, b)
+    st = out[0][0].view(FLOW_STATE_DTYPE)
+    rep = out[0][1].view(FLOW_REPORT_DTYPE).reshape(n_flows, per_flow)
+    cnt = out[0][2].view(np.uint32)
+    of, orep, ocnt = O.flow_reduce_batch(n_flows, d["flow_id"] - 1, d["seq"], d["tx_sec"],
+                                         d["tx_usec"], d["msg_len"], d["rx_sec"],
+                                         d["rx_usec"], window=window, per_flow=per_flow)
+    assert int(ocnt.sum()) > n_flows
+    compare(st, rep, cnt, of, orep, ocnt, per_flow)
+    # report_rec: the input index of each kept report's closing record -- its receive time
+    rrec = out[0][3].view(np.uint32).reshape(n_flows, per_flow)
+    for f in range(0, n_flows, 97):
+        for r in range(min(int(cnt[f]), per_flow)):
+            i = int(rrec[f, r])
+            assert d["flow_id"][i] - 1 == f
+            assert (int(d["rx_sec"][i]), int(d["rx_usec"][i])) == (int(rep[f, r]["rx_sec"]),
+                                                                  int(rep[f, r]["rx_usec"]))
