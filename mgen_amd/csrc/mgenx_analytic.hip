@@ -1850,7 +1850,8 @@ template <bool kRows>
 __global__ void __launch_bounds__(512)
 flow_order_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows,
                   uint32_t n_tiles, const uint32_t* __restrict__ start, RecSrc src,
-                  FRec* __restrict__ recs, uint32_t* __restrict__ order, uint32_t key_bits) {
+                  FRec* __restrict__ recs, uint32_t* __restrict__ order, uint32_t key_bits,
+                  uint32_t seqw) {  // diagnostics timing only (tile-contiguous writes, wrong)
   extern __shared__ uint32_t lds[];
   const uint32_t bins = n_flows + 1u;
   uint32_t* cnt = lds;                                // [wave][bin]: counts, then run bases
@@ -2006,7 +2007,7 @@ flow_order_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows
       const uint32_t k = j < tn ? lkey[j] : 0xFFFFu;
       if (k < n_flows) {
         FRec r = lrec[j];
-        const uint32_t g = sbase[k] + j;
+        const uint32_t g = seqw ? t0 + j : sbase[k] + j;
         if (order) order[g] = t0 + (r.len >> 16);
         r.len &= 0xFFFFu;
         recs[g] = r;
@@ -2267,9 +2268,11 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
   const RecSrc src = {seq, txs, txu, len, rows, rxs, rxu};
   int sort_path = (uint64_t)n_flows + 1 <= kCountBins ? 0 : 1;  // 0 counting, 1 radix
   int sabl = 0;      // diagnostics build only: ordering-only timing (MGENX_AN_SABL)
+  uint32_t oseqw = 0;  // diagnostics build only: order kernel writes tile-contiguous (MGENX_AN_SEQW)
 #if MGENX_DIAG
   if (const char* sp = getenv("MGENX_AN_RADIX")) sort_path = atoi(sp) ? 1 : sort_path;
   if (const char* sa = getenv("MGENX_AN_SABL")) sabl = atoi(sa);
+  if (const char* sw = getenv("MGENX_AN_SEQW")) oseqw = (uint32_t)atoi(sw);
 #endif
   const uint32_t bins = n_flows + 1u;
   uint32_t key_bits = 1;
@@ -2357,10 +2360,10 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
     const uint32_t grid = 8u * min((n_tiles + 7u) / 8u, ws.cu / 8u);
     if (src.rows)
       hipLaunchKernelGGL(flow_order_kernel<true>, dim3(grid), dim3(64 * kSortWaves), lds, stream,
-                         flow_idx, n, n_flows, n_tiles, start, src, recs, order, key_bits);
+                         flow_idx, n, n_flows, n_tiles, start, src, recs, order, key_bits, oseqw);
     else
       hipLaunchKernelGGL(flow_order_kernel<false>, dim3(grid), dim3(64 * kSortWaves), lds, stream,
-                         flow_idx, n, n_flows, n_tiles, start, src, recs, order, key_bits);
+                         flow_idx, n, n_flows, n_tiles, start, src, recs, order, key_bits, oseqw);
     bnd = start;  // tile 0's row: flow k starts at start[k]
     bstride = 1;
   } else {

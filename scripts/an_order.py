@@ -1,6 +1,7 @@
 """Timing of mgenx_flow_reduce on config-4 data (diagnostics build): the ordering alone
 (MGENX_AN_SABL=1) and the whole reduce, for the full 8M records / 1024 flows and rank 0's share
-at N = 8.  (Round 4's phase cuts of the one-tile-per-block order kernel, MGENX_AN_OCUT, went
+at N = 8; with an argument, also the ordering with tile-contiguous writes (MGENX_AN_SEQW=1:
+wrong results, the cost of the scattered runs).  (Round 4's phase cuts of the one-tile-per-block order kernel, MGENX_AN_OCUT, went
 with that kernel.)"""
 import os
 import subprocess
@@ -9,8 +10,10 @@ import time
 
 import numpy as np
 
-if len(sys.argv) == 1:
+if len(sys.argv) == 1 or sys.argv[1] != "run":
     runs = [("order_only", dict(MGENX_AN_SABL="1")), ("reduce", {})]
+    if len(sys.argv) > 1 or os.environ.get("AN_ORDER_SEQW"):
+        runs.append(("order_only_seqw", dict(MGENX_AN_SABL="1", MGENX_AN_SEQW="1")))
     for name, extra in runs:
         env = dict(os.environ, **extra)
         r = subprocess.run([sys.executable, __file__, "run"], env=env, capture_output=True,
