@@ -82,6 +82,8 @@ ROWS_ALGO = {"flow_order_kernel": (n * (32 + 8 + 4) + H, n * 24)}  # rows path: 
 def parts(k, vals):
     """(label, values): a kernel launched by both paths (6 launches) is split in dispatch order."""
     v = vals.get(k, [])
+    if "flow_order_kernel<" in k:  # templated on the source: one name per path
+        return [("rows" if "<true>" in k else "columns", v)]
     if len(v) >= 6 and k.startswith("mgenx::flow_"):
         h = len(v) // 2
         return [("columns", v[:h]), ("rows", v[h:])]
@@ -93,8 +95,9 @@ for pat, w, ar0, aw0 in plan:
       for (lab, fv), (_, wv), (_, tv) in zip(parts(k, fetch), parts(k, write), parts(k, dur) if dur.get(k) else [("", [])] * 2):
         ar, aw = ar0, aw0
         name = k.split("(")[0]
-        if lab == "rows" and name.split("::")[-1] in ROWS_ALGO:
-            ar, aw = ROWS_ALGO[name.split("::")[-1]]
+        base = name.split("::")[-1].split("<")[0]
+        if lab == "rows" and base in ROWS_ALGO:
+            ar, aw = ROWS_ALGO[base]
         fr = med(fv)
         wr = med(wv) or 0.0
         t = med(tv)
@@ -109,7 +112,7 @@ for pat, w, ar0, aw0 in plan:
             e["write_ratio"] = round(int(wr * 1024) / aw, 3) if aw else None
         if t:
             e["algorithmic_TBps"] = round((ar + aw) / (t * 1e-6) / 1e12, 3)
-        out["kernels"][name + (" [" + lab + "]" if lab else "")] = e
+        out["kernels"][name.replace("void ", "").split("<")[0] + (" [" + lab + "]" if lab else "")] = e
 # the small steps (FindFlow numbering, flow init): raw counters and times only
 for k in fetch:
     if any(x in k for x in SMALL):
