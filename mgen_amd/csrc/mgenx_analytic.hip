@@ -1878,17 +1878,22 @@ flow_order_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows
   RawRec raw[kKeys];
   // the wave's kPart keys, the tile's start row (this thread's bins) and its raw records, all
   // issued together (clamped indices: no branch, nothing waits here)
-  auto fetch = [&](uint32_t tt) {
+  // (live == false: the last pass's prefetch, every lane on element 0 -- one line, so the
+  // loads still land in the loop's registers without re-reading a tile)
+  auto fetch = [&](uint32_t tt, bool live) {
     const uint32_t a = tt * kTile + w * kPart;
+    uint32_t ii[kKeys];
 #pragma unroll
-    for (uint32_t j = 0; j < kKeys; j++) keys[j] = idx[min(a + 64u * j + lane, n - 1u)];
+    for (uint32_t j = 0; j < kKeys; j++) ii[j] = live ? min(a + 64u * j + lane, n - 1u) : 0u;
+#pragma unroll
+    for (uint32_t j = 0; j < kKeys; j++) keys[j] = idx[ii[j]];
 #pragma unroll
     for (uint32_t q = 0; q < kOrdStart; q++)
-      st[q] = start[(size_t)tt * bins + min(k0 + q, bins - 1u)];
+      st[q] = start[live ? (size_t)tt * bins + min(k0 + q, bins - 1u) : 0];
 #pragma unroll
-    for (uint32_t j = 0; j < kKeys; j++) raw[j] = load_rec_t<kRows>(src, min(a + 64u * j + lane, n - 1u));
+    for (uint32_t j = 0; j < kKeys; j++) raw[j] = load_rec_t<kRows>(src, ii[j]);
   };
-  fetch(t);
+  fetch(t, true);
   for (uint32_t k = tid; k < kSortWaves * bins; k += blockDim.x) cnt[k] = 0u;
   const uint64_t lt = (1ull << lane) - 1ull;
 #if MGENX_DIAG
@@ -1987,12 +1992,11 @@ flow_order_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows
     }
     lds_barrier();
     ORD_T(2);
-    // the next tile's loads go out before this tile's stores (unconditionally -- the last
-    // pass reloads its own tile -- so the loads land in the loop's registers with no copy,
-    // which would wait for them)
+    // the next tile's loads go out before this tile's stores (unconditionally, so the loads
+    // land in the loop's registers with no copy, which would wait for them)
     ci += nb;
     const bool more = ci < per && xb + ci < n_tiles;
-    fetch(more ? xb + ci : t);
+    fetch(more ? xb + ci : t, more);
     ORD_T(3);
     // the counts of the next tile start from zero (the ranks above were the last use)
     for (uint32_t k = tid; k < kSortWaves * bins; k += blockDim.x) cnt[k] = 0u;
