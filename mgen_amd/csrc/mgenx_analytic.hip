@@ -822,8 +822,88 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
     fb.last_close = last_close;
     fb.last_zr = last_zr;
     fb.lsum0 = lsum0;
-    fb.rsv = 0;
+    fb.rsv = 1;  // the sums are done below (flow_chain_kernel, diagnostics only, skips the flow)
     fbatch[f] = fb;
+  }
+
+  // ---- the latency sums, on this wave: each window's in-order FP64 sum of lat' (lane t takes
+  // window t: [lo, hi] below, as flow_chain_kernel does for a flow), staged through this
+  // wave's lbuf.  The flow's lat' and closes were just written by this wave: every store is
+  // waited for, and the loads read past L1 (agent scope) from the XCD's L2, where they sit --
+  // no separate pass re-reading lat' from HBM.
+  __builtin_amdgcn_s_waitcnt(0);
+  double* piece = &lbuf[wv][0];
+  constexpr uint32_t kPiece = kLatRounds * kRound;
+  const uint32_t kept = min(rcount, per_flow);
+  const uint32_t nslots = kept > rc0 ? kept - rc0 : 0u;
+  const uint32_t nwin = nslots + 1u;  // + the open window
+  const CloseRec* cl = closes + (size_t)f * per_flow;
+  auto ld32 = [](const uint32_t* q) {
+    return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  for (uint32_t w0 = 0; w0 < nwin; w0 += 64u) {
+    const uint32_t t = w0 + lane;
+    const bool has = t < nwin;
+    uint32_t lo = 0, hi = 0;
+    double sum = 0.0;
+    if (has) {
+      if (t < nslots) {
+        const uint32_t slot = rc0 + t;
+        hi = ld32(&cl[slot].pos);
+        if (t == 0) {
+          lo = b;
+          sum = lsum0;
+        } else {
+          lo = ld32(&cl[slot - 1u].pos) + (ld32(&cl[slot - 1u].zr) ? 1u : 0u);
+        }
+      } else {
+        hi = e - 1u;
+        if (ncl) {
+          lo = last_close + (last_zr ? 1u : 0u);
+        } else {
+          lo = b;
+          sum = lsum0;
+        }
+      }
+    }
+    const uint32_t nl = min(nwin - w0, 64u);
+    const uint32_t a0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)lo);
+    const uint32_t z0 = (uint32_t)__builtin_amdgcn_readlane((int)hi, (int)(nl - 1u));
+    for (uint32_t p0 = a0; p0 <= z0 && p0 >= a0; p0 += kPiece) {
+      const uint32_t pend = min(z0 + 1u, p0 + kPiece);
+      const bool mine = has && lo <= hi && lo < pend && hi >= p0;
+      if (!__ballot(mine)) continue;
+      for (uint32_t j = lane; j < pend - p0; j += 64u)
+        piece[j] = __hip_atomic_load(&lat2[p0 + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (mine) {
+        const uint32_t ja = max(lo, p0) - p0, jz = min(hi + 1u, pend) - p0;
+        uint32_t j = ja;
+        for (; j + 8u <= jz; j += 8u) {
+          double x[8];
+#pragma unroll
+          for (int u = 0; u < 8; u++) x[u] = piece[j + u];
+#pragma unroll
+          for (int u = 0; u < 8; u++) sum = __dadd_rn(sum, x[u]);
+        }
+        for (; j < jz; j++) sum = __dadd_rn(sum, piece[j]);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (has) {
+      if (t < nslots) {
+        const uint32_t slot = rc0 + t;
+        const uint64_t mc = __hip_atomic_load(&cl[slot].mc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        reports[(size_t)f * per_flow + slot].latency_ave =
+            mc == 0 ? -1.0 : mc == 1 ? sum : __ddiv_rn(sum, (double)mc);
+      } else {
+        sp->latency_sum = sum;
+      }
+    }
   }
 }
 
@@ -2414,8 +2494,11 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
   hipLaunchKernelGGL(flow_update_kernel, dim3((n_flows + 3) / 4), dim3(256), 0, stream, flows,
                      n_flows, bnd, bstride, recs, order, lat2, reports, per_flow, report_count,
                      report_rec, closes, fbatch, n, seg_min);
-  hipLaunchKernelGGL(flow_chain_kernel, dim3(n_flows), dim3(256), kChainPiece * 8u, stream, flows,
-                     bnd, bstride, lat2, fbatch, closes, reports, per_flow, report_count);
+  // (the update kernel sums its flows' windows itself; the workgroup path's flows may leave
+  // theirs to the chain kernel)
+  if (seg_min != 0xFFFFFFFFu)
+    hipLaunchKernelGGL(flow_chain_kernel, dim3(n_flows), dim3(256), kChainPiece * 8u, stream,
+                       flows, bnd, bstride, lat2, fbatch, closes, reports, per_flow, report_count);
   e = hipGetLastError();
   if (e != hipSuccess) {
     snprintf(err, errn, "flow_reduce: %s", hipGetErrorString(e));
