@@ -302,7 +302,8 @@ __device__ __forceinline__ uint64_t tkey(Tm t) {
   return t.sec > 0xFFFFFFFFll ? ~0ull : ((uint64_t)t.sec << 32 | (uint64_t)t.usec);
 }
 
-// What the latency-sum pass (flow_chain_kernel) needs from the update, per flow and call ...
+// What the latency sums (the update's tail; flow_chain_kernel in the diagnostics workgroup
+// path) need from the update, per flow and call ...
 struct FlowBatch {
   uint32_t rc0;         // report_count on entry
   uint32_t ncl;         // windows closed in this call
@@ -320,7 +321,7 @@ struct CloseRec {
 // ---- MgenAnalytic::Update, one WAVE per flow (mgenAnalytic.cpp:74-258) ----
 // The latency sum is the one FP64 chain whose rounding depends on record order; everything
 // else here is integer bookkeeping and order-free min / max.  So the update walks its flow's
-// records 256 at a time (4 per lane, coalesced) and leaves the sum to flow_chain_kernel: each
+// records 256 at a time (4 per lane, coalesced) and leaves the sum to its tail: each
 // record's contribution to latency_sum ("lat'": its latency when Update adds or assigns it, else
 // 0.0) goes to lat2[], the closing records and the window msg_counts to CloseRec.  Since
 // latency_sum is 0.0 whenever msg_count is 0, every assignment of a latency to it is an add to
@@ -465,7 +466,7 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
     }
     if (tge(rx, we)) {  // :180-256: report and restart the window
       const uint32_t seq_max = m.n ? m.get_last() : seq_start;
-      if (rcount < per_flow) {  // a kept report (latency_ave: flow_chain_kernel)
+      if (rcount < per_flow) {  // a kept report (latency_ave: the tail below)
       const double duration = tdelta(rx, ws);
       uint64_t r_count;
       double r_rate, r_loss, r_min, r_max;
