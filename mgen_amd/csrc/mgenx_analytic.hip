@@ -341,7 +341,7 @@ struct CloseRec {
 #if MGENX_DIAG
 // (diagnostics) cycles of flow_update_kernel's first wave by phase: detect, bulk, exact, lat'
 // store, rounds, exact steps, bulk runs, total
-__device__ unsigned long long g_upd_prof[8];
+__device__ unsigned long long g_upd_prof[10];  // + [8] restart cycles, [9] restarts
 #define UPD_T(slot)                                                        \
   do {                                                                     \
     if (prof_on) {                                                         \
@@ -679,8 +679,10 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
   ld(b + kRound, nxt);
 #if MGENX_DIAG
   const bool prof_on = blockIdx.x == 0 && wv == 0;
-  unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0}, prof_t = __builtin_amdgcn_s_memtime();
+  unsigned long long prof[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
+                     prof_t = __builtin_amdgcn_s_memtime();
   const unsigned long long prof_t0 = prof_t;
+  bool was_rst = false;
 #endif
   for (uint32_t i0 = b; i0 < e; i0 += kRound) {
     FRec nx2[kUR];
@@ -758,14 +760,27 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
         }
         msg_count++;
         lp = lat;
+#if MGENX_DIAG
+        was_rst = true;
+#endif
       } else {
         flush();
         lp = update(seq, rxk, len, lat, i0 + ev);
+#if MGENX_DIAG
+        was_rst = false;
+#endif
       }
 #pragma unroll
       for (uint32_t qq = 0; qq < kUR; qq++) latp[qq] = (qq == q && lane == l) ? lp : latp[qq];
       k = ev + 1u;
-      UPD_T(2);
+#if MGENX_DIAG
+      if (prof_on) {
+        const unsigned long long now_ = __builtin_amdgcn_s_memtime();
+        prof[was_rst ? 8 : 2] += now_ - prof_t;
+        prof[9] += was_rst ? 1 : 0;
+        prof_t = now_;
+      }
+#endif
     }
     // lat' leaves through LDS, kLatRounds rounds at a time: gfx950 counts stores in vmcnt, so
     // a round's stores would hold up the waits for the next rounds' record loads until they
@@ -795,7 +810,7 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
 #if MGENX_DIAG
   if (prof_on && lane == 0) {
     prof[7] = __builtin_amdgcn_s_memtime() - prof_t0;
-    for (int k2 = 0; k2 < 8; k2++) g_upd_prof[k2] = prof[k2];
+    for (int k2 = 0; k2 < 10; k2++) g_upd_prof[k2] = prof[k2];
   }
 #endif
 
@@ -2313,8 +2328,8 @@ extern "C" int mgenx_diag_seg_prof(unsigned long long* out, int n) {
   if (out && n == 16)  // flow_order_kernel's phase cycles (g_ord_prof, 8 entries)
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ord_prof), 64) == hipSuccess ? MGENX_OK
                                                                               : MGENX_EDEVICE;
-  if (out && n == 8)  // flow_update_kernel's phase cycles (g_upd_prof)
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_upd_prof), 64) == hipSuccess ? MGENX_OK
+  if (out && n == 10)  // flow_update_kernel's phase cycles (g_upd_prof)
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_upd_prof), 80) == hipSuccess ? MGENX_OK
                                                                               : MGENX_EDEVICE;
   if (!out || n < (int)(kSegWaves * 12)) return MGENX_EINVAL;
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_seg_prof), kSegWaves * 12 * 8) == hipSuccess

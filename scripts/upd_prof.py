@@ -14,7 +14,8 @@ from mgen_amd.workloads import poisson_flows  # noqa: E402
 
 eng = Engine(0, diag=True)
 d = poisson_flows(8388608, 1024, mean_gap_us=1000)
-names = ["detect", "bulk", "exact", "store", "rounds", "exact_n", "bulk_n", "total"]
+names = ["detect", "bulk", "exact_other", "store", "rounds", "exact_n", "bulk_n", "total",
+         "restart", "restart_n"]
 for name, sel in (("full", None), ("share8", 0)):
     dd = d if sel is None else {k: np.ascontiguousarray(v[(d["flow_id"] % 8) == sel])
                                 for k, v in d.items()}
@@ -25,8 +26,8 @@ for name, sel in (("full", None), ("share8", 0)):
         eng.flow_reduce(flows, 1024, idx, t["seq"], t["tx_sec"], t["tx_usec"], t["msg_len"],
                         t["rx_sec"], t["rx_usec"], n=len(dd["seq"]))
     torch.cuda.synchronize()
-    buf = (ctypes.c_ulonglong * 8)()
-    assert eng.lib.mgenx_diag_seg_prof(buf, 8) == 0
+    buf = (ctypes.c_ulonglong * 10)()
+    assert eng.lib.mgenx_diag_seg_prof(buf, 10) == 0
     a = list(buf)
     print(name, " ".join("%s=%d" % (k, v) for k, v in zip(names, a)))
     if a[4]:
