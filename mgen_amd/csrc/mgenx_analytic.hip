@@ -2265,13 +2265,28 @@ __global__ void flow_bounds_kernel(const uint32_t* __restrict__ keys, uint32_t n
   bnd[f] = lo;
 }
 
+// fresh states: zero but window_size, written as 16-B units by consecutive lanes (one lane per
+// state stored a 256-B struct per lane: 64 lines per store instruction)
+static_assert(sizeof(mgenx_flow_state) % 16 == 0, "flow state in 16-B units");
+static_assert(offsetof(mgenx_flow_state, window_size) % 8 == 0, "window_size 8-B aligned");
 __global__ void flow_init_kernel(mgenx_flow_state* flows, uint32_t n_flows, double window) {
-  const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= n_flows) return;
-  mgenx_flow_state s;
-  memset(&s, 0, sizeof(s));
-  s.window_size = window;
-  flows[f] = s;
+  constexpr uint32_t kUnits = sizeof(mgenx_flow_state) / 16u;
+  constexpr uint32_t kWin = offsetof(mgenx_flow_state, window_size);
+  const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= (uint64_t)n_flows * kUnits) return;
+  const uint32_t b = (uint32_t)(u % kUnits) * 16u;  // byte offset of this unit in its state
+  const uint64_t w = __builtin_bit_cast(uint64_t, window);
+  u32x4_t v = {0u, 0u, 0u, 0u};
+  if (b == (kWin & ~15u)) {
+    if (kWin % 16u == 0u) {
+      v.x = (uint32_t)w;
+      v.y = (uint32_t)(w >> 32);
+    } else {
+      v.z = (uint32_t)w;
+      v.w = (uint32_t)(w >> 32);
+    }
+  }
+  reinterpret_cast<u32x4_t*>(flows)[u] = v;
 }
 
 __global__ void flow_export_kernel(const mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
@@ -2344,7 +2359,8 @@ extern "C" int mgenx_diag_seg_prof(unsigned long long* out, int n) {
 extern "C" int mgenx_flow_init_run(mgenx_flow_state* flows, uint32_t n_flows, double window,
                                    hipStream_t stream) {
   if (!n_flows) return MGENX_OK;
-  hipLaunchKernelGGL(flow_init_kernel, dim3((n_flows + 255) / 256), dim3(256), 0, stream, flows,
+  const uint64_t units = (uint64_t)n_flows * (sizeof(mgenx_flow_state) / 16u);
+  hipLaunchKernelGGL(flow_init_kernel, dim3((uint32_t)((units + 255) / 256)), dim3(256), 0, stream, flows,
                      n_flows, quantized_window(window));
   return hipGetLastError() == hipSuccess ? MGENX_OK : MGENX_EDEVICE;
 }
