@@ -274,8 +274,14 @@ int mgenx_crc32_batch(mgenx_ctx* ctx, const uint8_t* dev_data, const uint64_t* d
  * memory: a call copies the message into the mailbox, the wave decodes or checksums it and
  * writes the reply back; the call spins until it arrives.  Host buffers in, results out --
  * no device pointers.  The wave exits after idle_ms without a request (the next call
- * relaunches it) and on mgenx_worker_destroy.  A worker serves one caller at a time (the
- * caller serialises); results equal the batch entry points' on the same bytes.
+ * relaunches it), on mgenx_worker_stop / mgenx_worker_destroy, and when its context is
+ * destroyed (mgenx_ctx_destroy stops and frees every worker created on it; the handle then
+ * only accepts mgenx_worker_destroy, other calls return MGENX_EINVAL).  While its wave runs
+ * it holds up device-wide synchronisations (hipFree, hipHostFree, hipDeviceSynchronize) until
+ * it idles out: the library's own workspace growth ends every worker's wave first (the next
+ * call relaunches it); a caller about to synchronise the device calls mgenx_worker_stop.
+ * Calls on one worker are serialised by the worker; results equal the batch entry points' on
+ * the same bytes.
  *   mgenx_worker_unpack  <- MgenMsg::Unpack (include/mgenMsg.h:110, mgenMsg.cpp:315-500) on a
  *                           fresh MgenMsg: the members it assigned (`decoded`, MGENX_DEC_*) and
  *                           err (MgenMsg::Error; 0 = Unpack returned true); no CRC check
@@ -296,6 +302,7 @@ typedef struct {
 typedef struct mgenx_worker mgenx_worker;
 int mgenx_worker_create(mgenx_ctx* ctx, uint32_t idle_ms, mgenx_worker** out);
 int mgenx_worker_destroy(mgenx_worker* w);
+int mgenx_worker_stop(mgenx_worker* w);  /* end the wave now (the next call relaunches it) */
 int mgenx_worker_unpack(mgenx_worker* w, const uint8_t* msg, uint32_t len, mgenx_unpacked* out);
 int mgenx_worker_crc32(mgenx_worker* w, const uint8_t* data, uint32_t len, uint32_t state_in,
                        uint32_t* state_out);
@@ -565,7 +572,9 @@ int mgenx_flow_export(mgenx_ctx* ctx, const mgenx_flow_state* dev_flows, uint32_
  * A table takes new keys while it holds fewer than its max_flows (rounded up to half its
  * power-of-two slot count; keys created concurrently may pass that bound together) and probes
  * at most 1024 slots per lookup: a record whose key finds no room maps to MGENX_FLOW_NONE (an
- * undersized table; the caller redoes the batch on a larger one). */
+ * undersized table; the caller redoes the batch on a larger one).  Near the bound that
+ * refusal can be spurious (a record racing the creation of its own key, or a key past the
+ * probe limit): MGENX_FLOW_NONE means "redo on a larger table", never "no such flow". */
 #define MGENX_FLOW_NONE 0xFFFFFFFFu
 typedef struct mgenx_flow_table mgenx_flow_table;
 int mgenx_flow_table_create(mgenx_ctx* ctx, uint32_t max_flows, mgenx_flow_table** out);

@@ -99,11 +99,8 @@ class Engine {
             "mgenx_worker_pack");
       return;
     }
-    if ((opts & MGENX_PACK_RANDOM_FILL) && (!fill_set_ || fill_time_ != fill_time)) {
+    if (opts & MGENX_PACK_RANDOM_FILL)  // (the context caches the stream of its last fill time)
       Check(mgenx_set_fill_time(ctx_, fill_time), "mgenx_set_fill_time");
-      fill_set_ = true;
-      fill_time_ = fill_time;
-    }
     // host staging: [tmpl | desc | buf_len | crc_in | rec_off | pool]
     size_t pool = 0, slab = 0;
     for (unsigned i = 0; i < n; i++) {
@@ -670,10 +667,16 @@ class Engine {
     if (hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess)
       throw Error("hipStreamCreate failed");
   }
+  // a resident worker wave holds up the device-wide synchronisation of hipFree / hipHostFree
+  // until it idles out: end it first (the next single-message call relaunches it)
+  void QuiesceWorker() {
+    if (worker_) (void)mgenx_worker_stop(worker_);
+  }
   void Reserve(size_t bytes) {
     if (bytes <= cap_) return;
     size_t c = cap_ ? cap_ : (1u << 20);
     while (c < bytes) c *= 2;
+    QuiesceWorker();
     if (host_) (void)hipHostFree(host_);
     if (dev_) (void)hipFree(dev_);
     host_ = nullptr;
@@ -691,6 +694,7 @@ class Engine {
                          hipMemcpyDeviceToDevice, stream_) != hipSuccess)
         throw Error("mgenx compat: flow state copy failed");
       Sync();
+      QuiesceWorker();
       (void)hipFree(flows_);
     }
     flows_ = f;
@@ -769,8 +773,6 @@ class Engine {
   uint8_t* host_ = nullptr;
   uint8_t* dev_ = nullptr;
   size_t cap_ = 0;
-  bool fill_set_ = false;
-  uint32_t fill_time_ = 0;
   mgenx_flow_state* flows_ = nullptr;
   uint32_t n_slots_ = 0, slot_cap_ = 0;
   std::vector<uint32_t> free_slots_;

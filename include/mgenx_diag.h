@@ -42,9 +42,9 @@ int mgenx_diag_stream_read_w(mgenx_ctx* ctx, const uint8_t* dev_data, uint64_t b
 int mgenx_diag_group_rw(mgenx_ctx* ctx, const uint8_t* dev_data, uint64_t bytes,
                         uint8_t* dev_out, int mode, void* stream);
 
-/* Diagnostic: s_memtime stamps of flow_seg_kernel's workgroup 0, first pass, per wave (8 x
- * 12: start, walk begun, walk done, scatter done, ring received, ring posted, classified,
- * aggregates received, replay done); out holds >= 96 values. */
+/* Diagnostic: s_memtime phase cycles of the analytics kernels' first wave: n == 10
+ * flow_update_kernel (detect, bulk, exact, lat' stores, rounds, exact steps, bulk runs, total,
+ * restart cycles, restarts); n == 16 flow_order_kernel (8 entries). */
 int mgenx_diag_seg_prof(unsigned long long* out, int n);
 
 #ifdef __cplusplus

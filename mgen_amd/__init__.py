@@ -44,7 +44,7 @@ EXPORTED_SYMBOLS = (
     "mgenx_pcap_parse", "mgenx_binlog_index", "mgenx_convert_binary_log",
     "mgenx_unpack_last_kernel", "mgenx_pcap_snap", "mgenx_flow_reduce_rows",
     "mgenx_worker_create", "mgenx_worker_destroy", "mgenx_worker_unpack", "mgenx_worker_crc32",
-    "mgenx_worker_pack",
+    "mgenx_worker_pack", "mgenx_worker_stop",
 )
 DIAG_SYMBOLS = ("mgenx_set_tuning", "mgenx_diag_stream_read", "mgenx_diag_group_rw",
                 "mgenx_diag_seg_prof", "mgenx_diag_stream_read_w")
@@ -133,6 +133,7 @@ def load(diag: bool = False):
                                         P, u32, i32, P, u64, P, P]
     L.mgenx_worker_create.argtypes = [P, u32, ctypes.POINTER(P)]
     L.mgenx_worker_destroy.argtypes = [P]
+    L.mgenx_worker_stop.argtypes = [P]
     L.mgenx_worker_unpack.argtypes = [P, ctypes.c_char_p, u32, P]
     L.mgenx_worker_crc32.argtypes = [P, ctypes.c_char_p, u32, u32, ctypes.POINTER(u32)]
     L.mgenx_worker_pack.argtypes = [P, P, ctypes.c_char_p, P, u32, u32, u32, u32, P,
@@ -834,7 +835,13 @@ class Worker:
             ctypes.byref(tx), ctypes.byref(st)), "mgenx_worker_pack")
         return out[:ret.value].tobytes(), tx.value, st.value
 
+    def stop(self):
+        """End the resident wave now (the next call relaunches it)."""
+        if self.w:
+            self.eng._check(self.eng.lib.mgenx_worker_stop(self.w), "mgenx_worker_stop")
+
     def close(self):
+        # (after Engine.close the handle only frees itself: mgenx_ctx_destroy stopped the wave)
         if self.w:
             self.eng.lib.mgenx_worker_destroy(self.w)
             self.w = ctypes.c_void_p()

@@ -305,17 +305,7 @@ __device__ __forceinline__ uint64_t tkey(Tm t) {
   return t.sec > 0xFFFFFFFFll ? ~0ull : ((uint64_t)t.sec << 32 | (uint64_t)t.usec);
 }
 
-// What the latency sums (the update's tail; flow_chain_kernel in the diagnostics workgroup
-// path) need from the update, per flow and call ...
-struct FlowBatch {
-  uint32_t rc0;         // report_count on entry
-  uint32_t ncl;         // windows closed in this call
-  uint32_t last_close;  // sorted position of the last closing record
-  uint32_t last_zr;     // it restarted the sum at 0.0 instead of at its own latency (below)
-  double lsum0;         // latency_sum on entry
-  uint64_t rsv;
-};
-// ... and per kept report closed in this call
+// What the latency sums (the update's tail) need per kept report closed in this call
 struct CloseRec {
   uint32_t pos, zr;     // the closing record (sorted position); zero restart
   uint64_t mc;          // msg_count at the close: latency_ave's divisor
@@ -378,8 +368,8 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
                    const uint32_t* __restrict__ order, double* __restrict__ lat2,
                    mgenx_flow_report* __restrict__ reports, uint32_t per_flow,
                    uint32_t* __restrict__ report_count, uint32_t* __restrict__ report_rec,
-                   CloseRec* __restrict__ closes, FlowBatch* __restrict__ fbatch,
-                   uint32_t lat2_sink, uint32_t long_min) {
+                   CloseRec* __restrict__ closes,
+                   uint32_t lat2_sink) {
   __shared__ uint32_t scat[4][32];
   __shared__ uint32_t fo[4][1024];
   __shared__ double lbuf[4][kLatRounds * kRound];
@@ -387,7 +377,7 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
   const uint32_t f = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + wv);
   if (f >= n_flows) return;
   const uint32_t b = bnd[(size_t)f * bstride], e = bnd[(size_t)(f + 1u) * bstride];
-  if (b >= e || e - b >= long_min) return;  // (long flows: flow_seg_kernel)
+  if (b >= e) return;
   for (uint32_t j = lane; j < 1024u; j += 64u) fo[wv][j] = 0xFFFFFFFFu;
   mgenx_flow_state* sp = flows + f;
   const TAdd window = tadd_of(sp->window_size);
@@ -835,18 +825,10 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
     sp->latency_max = lmax;
     sp->n_reports = nrep;
     report_count[f] = rcount;
-    FlowBatch fb;
-    fb.rc0 = rc0;
-    fb.ncl = ncl;
-    fb.last_close = last_close;
-    fb.last_zr = last_zr;
-    fb.lsum0 = lsum0;
-    fb.rsv = 1;  // the sums are done below (flow_chain_kernel, diagnostics only, skips the flow)
-    fbatch[f] = fb;
   }
 
   // ---- the latency sums, on this wave: each window's in-order FP64 sum of lat' (lane t takes
-  // window t: [lo, hi] below, as flow_chain_kernel does for a flow), staged through this
+  // window t: [lo, hi] below), staged through this
   // wave's lbuf.  The flow's lat' and closes were just written by this wave: every store is
   // waited for, and the loads read past L1 (agent scope) from the XCD's L2, where they sit --
   // no separate pass re-reading lat' from HBM.
@@ -926,931 +908,6 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
   }
 }
 
-#if MGENX_DIAG
-// ---- long flows: one WORKGROUP per flow, its records in segments of one wave each ----
-// flow_update_kernel runs a flow's records on one wave, so a call with few, long flows leaves
-// the chip idle and every flow's time is its whole record count times the per-round latency.
-// Here a flow with at least MGENX_AN_SEGMIN records in the call gets a workgroup; its records go in
-// chunks of kSegWaves segments, wave w taking segment w (kSegRows rows of 64 records in
-// registers, record q * 64 + lane in row q, lane `lane`).  Update's state splits three ways:
-//   * the skeleton: window (valid, start, end), mask span (nonempty, first, last) and
-//     seq_start -- what decides which branch of Update a record takes.  It changes only at
-//     EVENTS: a window close, a message outside [first, first + 1024), the first record, the
-//     first message; between events every message lies in that span with `first` fixed (it can
-//     only raise `last`).  So a wave finds its next event with one compare and ballot per row;
-//   * the ring bits: a message in the span is a duplicate when its bit was set before -- by an
-//     earlier record since the ring last restarted (an LDS scatter, as in flow_update_kernel),
-//     or at the segment's entry;
-//   * the window aggregates (msg_count, byte_count, min, max): order-free over the counted
-//     records of a window piece, folded piece by piece with Update's msg_count 0 / 1 quirks.
-// The waves pass three chains through LDS, w -> w + 1: the skeleton (a wave walks its events
-// as soon as the previous walk is done), the ring (after its scatter), the aggregates (after it
-// has classified its records it replays its events, folds its pieces and writes its reports).
-// Only the walks are in series; a wave's scatter, classification and replay overlap the later
-// waves' walks.  lat' goes to lat2 and the kept closes to CloseRec exactly as in
-// flow_update_kernel, so flow_chain_kernel finishes both kinds of flow.
-constexpr uint32_t kSegRows = 8;                      // rows of 64 records per segment
-constexpr uint32_t kSegWaves = 16;                    // segments (waves) per workgroup pass
-constexpr uint32_t kSeg = 64u * kSegRows;
-constexpr uint32_t kSegChunk = kSeg * kSegWaves;
-
-// per-record branch codes written by the walk (4 bits; close and seq >= seq_start bits apart)
-enum : uint32_t {
-  kCSimple = 0,     // no event: a message in the span (new or duplicate), or no message
-  kCInSpan = 1,     // a closing message in the span (new or duplicate)
-  kCBelowAcc = 2,   // below `first`, below seq_start, fits: Set only
-  kCBelowCnt = 3,   // below `first`, at / past seq_start, fits: Set, counted
-  kCRestart = 4,    // outside the span, at / past seq_start: the mask restarts at it, counted
-  kCFirstMsg = 5,   // the first message with the mask empty (:165-173)
-  kCOpenMsg = 6,    // the flow's first record, with a message (:80-99)
-  kCOpenEmpty = 7,  // the flow's first record, without
-  kCDrop = 8,       // outside the span, below seq_start, does not fit: nothing
-  kCNone = 9        // a closing record without a message
-};
-
-struct SegSkel {  // chain A
-  int64_t ws_sec, ws_usec, we_sec, we_usec;
-  uint32_t valid, nz, first, last, seq_start, rsv[3];
-};
-struct SegAgg {   // chain C
-  uint64_t mc, bc, nrep;
-  double lmin, lmax;
-  uint32_t rcount, ncl, last_close, last_zr;
-};
-struct SegPiece {  // a piece of a segment: its counted records' partial, then its event
-  uint64_t sum;
-  double mn, mx, lat;
-  int64_t ws_sec, ws_usec;
-  uint32_t kk, l1, flags, pos, len, rx_sec, rx_usec, sbefore, seq_max, rsv;
-};
-constexpr uint32_t kPieceCap = 6;  // pieces per wave kept in LDS ahead of the aggregate chain
-// the closes of a pass, for its latency sums (P4); a pass with more leaves the flow's sums to
-// flow_chain_kernel
-constexpr uint32_t kCloseCap = 255;
-struct SegClose {
-  uint64_t mc;                 // msg_count at the close: latency_ave's divisor
-  uint32_t pos, zr, slot, kept;  // pass-relative position, zero restart, report slot
-};
-struct SegLds {
-  double lat[kSegChunk];       // the pass's lat' values
-  SegClose cl[kCloseCap];
-  double carry;                // the open window's sum at the pass start
-  uint32_t ncl, p4_off;
-  SegPiece pc[kSegWaves][kPieceCap];
-  SegSkel sk[kSegWaves + 1];
-  SegAgg ag[kSegWaves + 1];
-  uint32_t ring[kSegWaves + 1][32];   // chain B: ring word k at [k]
-  uint32_t rdy[3][kSegWaves + 1];     // chain tokens
-  uint32_t sc[kSegWaves][32];         // the scatter ring of a run
-  uint32_t fo[kSegWaves][1024];       // first position per ring slot (clashes)
-  unsigned long long dups;
-};
-
-__device__ __forceinline__ uint32_t rfl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
-__device__ __forceinline__ int64_t rfl64(int64_t v) { return uni64(v); }
-__device__ __forceinline__ double rfld(double v) {
-  return __builtin_bit_cast(double, (uint64_t)uni64(__builtin_bit_cast(int64_t, v)));
-}
-// a row value the compiler may not hoist out of the event loops (hoisted lane-mask compares of
-// every row are SGPR pairs: they spilled, and each use cost a v_readlane)
-__device__ __forceinline__ uint32_t fresh(uint32_t v) {
-  asm volatile("" : "+v"(v));
-  return v;
-}
-// lane l's value of row q (both wave-uniform): a scalar select ladder over the rows' readlanes
-// (a vector select or a dynamic index became an array in scratch memory)
-__device__ __forceinline__ uint32_t pick(const uint32_t (&v)[kSegRows], uint32_t q, uint32_t l) {
-  uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)v[0], (int)l);
-#pragma unroll
-  for (uint32_t k = 1; k < kSegRows; k++) {
-    uint32_t t = (uint32_t)__builtin_amdgcn_readlane((int)v[k], (int)l);
-    asm volatile("" : "+s"(t));
-    r = q == k ? t : r;
-  }
-  return r;
-}
-__device__ __forceinline__ void seg_wait(uint32_t* flag, uint32_t tok) {
-  while (rfl(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) != tok)
-    __builtin_amdgcn_s_sleep(1);
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-__device__ __forceinline__ void seg_post(uint32_t* flag, uint32_t tok) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __hip_atomic_store(flag, tok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// flows with at least min_len records in the call, listed for flow_seg_kernel
-__global__ void flow_long_kernel(const uint32_t* __restrict__ bnd, uint32_t bstride, uint32_t n_flows,
-                                 uint32_t min_len, uint32_t* __restrict__ list,
-                                 uint32_t* __restrict__ count) {
-  const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= n_flows) return;
-  const uint32_t b = bnd[(size_t)f * bstride], e = bnd[(size_t)(f + 1u) * bstride];
-  if (e > b && e - b >= min_len) list[atomicAdd(count, 1u)] = f;
-}
-
-#if MGENX_DIAG
-// phase timestamps (s_memtime) of workgroup 0's first pass, per wave (mgenx_diag_seg_prof)
-__device__ unsigned long long g_seg_prof[kSegWaves][12];
-#define SEG_PROF(k)                                                                          \
-  do {                                                                                       \
-    if (blockIdx.x == 0 && li == 0 && c0 == b && lane == 0)                                 \
-      g_seg_prof[w][k] = __builtin_amdgcn_s_memtime();                                       \
-  } while (0)
-#else
-#define SEG_PROF(k) \
-  do {              \
-  } while (0)
-#endif
-
-__global__ void __launch_bounds__(64 * kSegWaves)
-flow_seg_kernel(mgenx_flow_state* __restrict__ flows, const uint32_t* __restrict__ list,
-                const uint32_t* __restrict__ list_count, const uint32_t* __restrict__ bnd,
-                uint32_t bstride, const FRec* __restrict__ recs, const uint32_t* __restrict__ order,
-                double* __restrict__ lat2, mgenx_flow_report* __restrict__ reports,
-                uint32_t per_flow, uint32_t* __restrict__ report_count,
-                uint32_t* __restrict__ report_rec, CloseRec* __restrict__ closes,
-                FlowBatch* __restrict__ fbatch) {
-  __shared__ SegLds sl;
-  const uint32_t lane = threadIdx.x & 63u, w = rfl(threadIdx.x >> 6);
-  for (uint32_t j = lane; j < 1024u; j += 64u) sl.fo[w][j] = 0xFFFFFFFFu;
-  if (threadIdx.x < 3u * (kSegWaves + 1u)) (&sl.rdy[0][0])[threadIdx.x] = 0u;
-  uint32_t tok = 0;
-  const uint32_t nlong = *list_count;
-  for (uint32_t li = blockIdx.x; li < nlong; li += gridDim.x) {
-    const uint32_t f = rfl(list[li]);
-    const uint32_t b = rfl(bnd[(size_t)f * bstride]), e = rfl(bnd[(size_t)(f + 1u) * bstride]);
-    mgenx_flow_state* sp = flows + f;
-    const double wsz = rfld(sp->window_size);
-    const TAdd window = {rfl64(tadd_of(wsz).sec), rfl64(tadd_of(wsz).usec)};
-    if (w == 0) {  // the flow's state on entry -> slot 0 of the three chains
-      WRing m;
-      m.lane = lane;
-      m.first = sp->mask_first;
-      m.n = sp->mask_n;
-      m.load_relative(sp->mask);
-      if (lane == 0) {
-        SegSkel k;
-        k.ws_sec = sp->win_start_sec;
-        k.ws_usec = sp->win_start_usec;
-        k.we_sec = sp->win_end_sec;
-        k.we_usec = sp->win_end_usec;
-        k.valid = sp->window_valid != 0;
-        k.nz = m.n != 0;
-        k.first = m.first;
-        k.last = m.last;
-        k.seq_start = sp->seq_start;
-        sl.sk[0] = k;
-        SegAgg a;
-        a.mc = sp->msg_count;
-        a.bc = sp->byte_count;
-        a.nrep = sp->n_reports;
-        a.lmin = sp->latency_min;
-        a.lmax = sp->latency_max;
-        a.rcount = report_count[f];
-        a.ncl = 0;
-        a.last_close = 0;
-        a.last_zr = 0;
-        sl.ag[0] = a;
-        sl.dups = 0;
-        sl.carry = sp->latency_sum;
-        sl.ncl = 0;
-        sl.p4_off = 0;
-      }
-      if (lane < 32u) sl.ring[0][lane] = m.n ? m.w : 0u;
-    }
-    __syncthreads();
-    for (uint32_t c0 = b; c0 < e; c0 += kSegChunk) {
-      tok++;
-      SEG_PROF(0);
-      const uint32_t sb = c0 + w * kSeg;
-      const uint32_t cnt = sb < e ? min(kSeg, e - sb) : 0u;
-      // the segment's records: row q, lane l = record sb + 64 q + l
-      uint32_t rkl[kSegRows], rkh[kSegRows], sq[kSegRows], ln[kSegRows], ltl[kSegRows], lth[kSegRows];
-#pragma unroll
-      for (uint32_t q = 0; q < kSegRows; q++) {
-        FRec r = {};
-        if (64u * q < cnt) r = recs[sb + min(64u * q + lane, cnt - 1u)];
-        rkl[q] = (uint32_t)r.rxk;
-        rkh[q] = (uint32_t)(r.rxk >> 32);
-        sq[q] = r.seq;
-        ln[q] = r.len;
-        const uint64_t lb = __builtin_bit_cast(uint64_t, r.latency);
-        ltl[q] = (uint32_t)lb;
-        lth[q] = (uint32_t)(lb >> 32);
-      }
-      // per lane: codes of rows 0-7 / 8-15 (4 bits each), close bits (0-15) | seq >= seq_start
-      // bits (16-31), duplicate bits, counted bits
-      uint32_t tb0 = 0, tb1 = 0, cgb = 0, dupb = 0, cntb = 0;
-      auto code_of = [&](uint32_t q) -> uint32_t {  // q static
-        return ((q < 8u ? tb0 : tb1) >> (4u * (q & 7u))) & 15u;
-      };
-
-      // ---- P1: the walk (chain A) ----
-      if (w > 0) seg_wait(&sl.rdy[0][w], tok);
-      __builtin_amdgcn_s_setprio(3);  // the walks are the workgroup's critical path
-      SEG_PROF(1);
-      {
-        const SegSkel& k = sl.sk[w];
-        bool valid = rfl(k.valid) != 0, nz = rfl(k.nz) != 0;
-        uint32_t F = rfl(k.first), L = rfl(k.last), S = rfl(k.seq_start);
-        Tm ws = {rfl64(k.ws_sec), rfl64(k.ws_usec)}, we = {rfl64(k.we_sec), rfl64(k.we_usec)};
-        uint64_t wek = tkey(we);
-        uint32_t pdm = 0;
-        uint32_t p = 0;
-        SEG_PROF(9);
-        while (p < cnt) {
-          // branch-free: every row's event mask (the first event by a scalar select chain), then
-          // the run [p, ev)'s seq >= seq_start bits and its highest seq - first
-          // (bitwise logic with the uniform state folded into operands: no uniform branches,
-          // and fresh() keeps the per-row compares in the loop instead of hoisted SGPR masks)
-          const uint64_t wekv = valid ? wek : 0ull;  // no window yet: every record is an event
-          const uint32_t lim = nz ? kDepth : 0u;      // empty mask: every message is an event
-          uint32_t ev = cnt;
-#pragma unroll
-          for (uint32_t q = kSegRows; q-- > 0;) {
-            const uint32_t pos = 64u * q + fresh(lane), sqq = fresh(sq[q]);
-            const uint64_t rxk = (uint64_t)fresh(rkh[q]) << 32 | fresh(rkl[q]);
-            const bool msg = fresh(ln[q]) != 0u;
-            const bool simple = (rxk < wekv) & (!msg | (sqq - F < lim));
-            const uint64_t mm = __ballot((pos >= p) & (pos < cnt) & !simple);
-            ev = mm ? 64u * q + (uint32_t)__builtin_ctzll(mm) : ev;
-          }
-#pragma unroll
-          for (uint32_t q = 0; q < kSegRows; q++) {
-            const uint32_t pos = 64u * q + fresh(lane), sqq = fresh(sq[q]);
-            const bool run = (pos >= p) & (pos < ev) & (fresh(ln[q]) != 0u);
-            cgb |= (run & ((int32_t)(sqq - S) >= 0)) ? (1u << (16u + q)) : 0u;
-            pdm = run ? max(pdm, sqq - F) : pdm;
-          }
-          SEG_PROF(10);
-          if (nz) L = F + max(L - F, rfl(WRing::wave_max(pdm)));
-          pdm = 0;
-          if (ev >= cnt) break;
-          const uint32_t q = ev >> 6, l = ev & 63u;
-          const uint32_t s = pick(sq, q, l);
-          const uint32_t len = pick(ln, q, l);
-          const uint32_t rlo = pick(rkl, q, l);
-          const uint32_t rhi = pick(rkh, q, l);
-          const Tm rx = {(int64_t)rhi, (int64_t)rlo};
-          uint32_t code = kCNone, close = 0, ges = 0;
-          if (!valid) {
-            valid = true;
-            ws = rx;
-            we = uni_t(tadd(rx, window));
-            wek = tkey(we);
-            if (len) {
-              nz = true;
-              F = L = S = s;
-              code = kCOpenMsg;
-            } else {
-              code = kCOpenEmpty;
-            }
-          } else {
-            if (len) {
-              if (!nz) {
-                nz = true;
-                F = L = S = s;
-                code = kCFirstMsg;
-              } else {
-                const int32_t d = (int32_t)(s - F);
-                if (d >= 0 && (uint32_t)d < kDepth) {
-                  if ((uint32_t)d > L - F) L = s;
-                  ges = (int32_t)(s - S) >= 0;
-                  code = kCInSpan;
-                } else {
-                  const bool fits = d < 0 && L - s < kDepth;
-                  if ((int32_t)(s - S) < 0) {
-                    code = fits ? kCBelowAcc : kCDrop;
-                  } else {
-                    code = fits ? kCBelowCnt : kCRestart;
-                    if (!fits) L = s;
-                  }
-                  if (fits || code == kCRestart) F = s;
-                }
-              }
-            }
-            if (tge(rx, we)) {
-              close = 1;
-              S = nz ? L : S;
-              ws = rx;
-              we = uni_t(tadd(rx, window));
-              wek = tkey(we);
-            }
-          }
-          const uint32_t sh = 4u * (q & 7u);
-          if (lane == l) {
-            if (q < 8u) tb0 |= code << sh;
-            else tb1 |= code << sh;
-            cgb |= (close << q) | (ges << (16u + q));
-          }
-          tb0 = fresh(tb0);
-          tb1 = fresh(tb1);
-          cgb = fresh(cgb);
-          p = ev + 1u;
-        }
-        if (lane == 0) {
-          SegSkel o;
-          o.ws_sec = ws.sec;
-          o.ws_usec = ws.usec;
-          o.we_sec = we.sec;
-          o.we_usec = we.usec;
-          o.valid = valid;
-          o.nz = nz;
-          o.first = F;
-          o.last = L;
-          o.seq_start = S;
-          sl.sk[w + 1u] = o;
-        }
-        SEG_PROF(11);
-        seg_post(&sl.rdy[0][w + 1u], tok);
-      }
-      __builtin_amdgcn_s_setprio(0);
-      SEG_PROF(2);
-
-      // ---- P2: duplicates, runs of the ring (chain B) ----
-      {
-        auto is_reset = [](uint32_t c) { return c == kCRestart || c == kCFirstMsg || c == kCOpenMsg; };
-        // first reset at or after position a (cnt when none)
-        auto next_reset = [&](uint32_t a) -> uint32_t {
-          uint32_t r = cnt;
-#pragma unroll
-          for (uint32_t q = 0; q < kSegRows; q++) {
-            if (64u * q + 64u <= a) continue;
-            if (64u * q >= cnt) break;
-            const uint32_t pos = 64u * q + lane;
-            const uint64_t mm = __ballot(pos >= a && pos < cnt && is_reset(code_of(q)));
-            if (mm) {
-              r = 64u * q + (uint32_t)__builtin_ctzll(mm);
-              break;
-            }
-          }
-          return r;
-        };
-        uint32_t* sc = sl.sc[w];
-        uint32_t* fo = sl.fo[w];
-        uint32_t runring = 0;
-        // one run [ra, rb): every candidate (a message that is Set or found set) scatters its bit
-        auto run = [&](uint32_t ra, uint32_t rb) {
-          if (lane < 32u) sc[lane] = 0u;
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          bool clash = false;
-          uint32_t bit[kSegRows], old[kSegRows];
-#pragma unroll
-          for (uint32_t q = 0; q < kSegRows; q++) {
-            const uint32_t pos = 64u * q + lane, c = code_of(q);
-            const bool cand = pos >= ra && pos < rb && ln[q] != 0u && c <= kCOpenMsg;
-            bit[q] = cand ? 1u << (sq[q] & 31u) : 0u;
-          }
-#pragma unroll
-          for (uint32_t q = 0; q < kSegRows; q++) {
-            if (64u * q + 64u <= ra || 64u * q >= rb) continue;
-            old[q] = atomicOr(&sc[(sq[q] >> 5) & 31u], bit[q]);
-          }
-#pragma unroll
-          for (uint32_t q = 0; q < kSegRows; q++) {
-            if (64u * q + 64u <= ra || 64u * q >= rb) continue;
-            clash |= (old[q] & bit[q]) != 0u;
-          }
-          __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          if (__ballot(clash)) {  // two candidates of the run share a sequence number
-#pragma unroll
-            for (uint32_t q = 0; q < kSegRows; q++) {
-              if (64u * q + 64u <= ra || 64u * q >= rb) continue;
-              atomicMin(&fo[sq[q] & 1023u], bit[q] ? 64u * q + lane : 0xFFFFFFFFu);
-            }
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-#pragma unroll
-            for (uint32_t q = 0; q < kSegRows; q++) {
-              if (64u * q + 64u <= ra || 64u * q >= rb) continue;
-              const uint32_t c = code_of(q);
-              const bool later = bit[q] && fo[sq[q] & 1023u] < 64u * q + lane;
-              dupb |= (later && c <= kCInSpan) ? (1u << q) : 0u;
-            }
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-#pragma unroll
-            for (uint32_t q = 0; q < kSegRows; q++) {
-              if (64u * q + 64u <= ra || 64u * q >= rb) continue;
-              if (bit[q]) fo[sq[q] & 1023u] = 0xFFFFFFFFu;
-            }
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-          }
-          runring = lane < 32u ? sc[lane] : 0u;
-          __builtin_amdgcn_wave_barrier();
-        };
-        const uint32_t r0 = next_reset(0);
-        if (r0 > 0) run(0, r0);
-        uint32_t first_ring = runring;
-        for (uint32_t ra = r0; ra < cnt;) {
-          const uint32_t rb = next_reset(ra + 1u);
-          run(ra, rb);
-          ra = rb;
-        }
-        SEG_PROF(3);
-        if (w > 0) seg_wait(&sl.rdy[1][w], tok);
-        SEG_PROF(4);
-        const uint32_t ent = lane < 32u ? sl.ring[w][lane] : 0u;
-        if (r0 > 0) {  // the first run also finds the bits set at the segment's entry
-#pragma unroll
-          for (uint32_t q = 0; q < kSegRows; q++) {
-            if (64u * q >= r0) break;
-            const uint32_t pos = 64u * q + lane, c = code_of(q);
-            const uint32_t wd = (uint32_t)__shfl((int)ent, (int)((sq[q] >> 5) & 31u));
-            const bool hit = pos < r0 && ln[q] != 0u && c <= kCInSpan && ((wd >> (sq[q] & 31u)) & 1u);
-            dupb |= hit ? (1u << q) : 0u;
-          }
-        }
-        const uint32_t ex = r0 < cnt ? runring : (ent | first_ring);
-        if (lane < 32u) sl.ring[w + 1u][lane] = ex;
-        seg_post(&sl.rdy[1][w + 1u], tok);
-        SEG_PROF(5);
-        // counted records, duplicates, lat'
-        uint32_t ndup = 0;
-#pragma unroll
-        for (uint32_t q = 0; q < kSegRows; q++) {
-          if (64u * q >= cnt) break;
-          const uint32_t pos = 64u * q + lane, c = code_of(q);
-          const bool live = pos < cnt, msg = ln[q] != 0u;
-          const bool dup = (dupb >> q) & 1u;
-          const bool ges = (cgb >> (16u + q)) & 1u;
-          const bool counted = live && msg &&
-                               ((c <= kCInSpan && !dup && ges) || c == kCBelowCnt || c == kCRestart);
-          cntb |= counted ? (1u << q) : 0u;
-          ndup += (uint32_t)__popcll(__ballot(live && dup));
-          const double lat = __builtin_bit_cast(double, (uint64_t)lth[q] << 32 | ltl[q]);
-          const double lp = (counted || (live && (c == kCFirstMsg || c == kCOpenMsg))) ? lat : 0.0;
-          if (live) {
-            lat2[sb + pos] = lp;
-            sl.lat[w * kSeg + pos] = lp;
-          }
-        }
-        if (lane == 0 && ndup) atomicAdd(&sl.dups, (unsigned long long)ndup);
-      }
-
-      // ---- P3: the replay.  Before the aggregate chain: the skeleton replayed and every piece's
-      // counted partial (k, bytes, first size, min, max) with its closing event, kPieceCap pieces
-      // into LDS.  In the chain: only the folds, the reports and the resets, per piece. ----
-      SEG_PROF(6);
-      {
-        const double inf = __builtin_huge_val();
-        const SegSkel& k = sl.sk[w];
-        bool nz = rfl(k.nz) != 0;
-        uint32_t F = rfl(k.first), L = rfl(k.last), S = rfl(k.seq_start);
-        Tm ws = {rfl64(k.ws_sec), rfl64(k.ws_usec)};
-        uint32_t p = 0;
-        // the piece from p: records up to the next event, and the event; advances the replay
-        auto next_piece = [&](SegPiece& pc) {
-          // branch-free, as the walk: the next event, then the run [p, ev)'s partials
-          uint32_t ev = cnt;
-#pragma unroll
-          for (uint32_t q = kSegRows; q-- > 0;) {
-            const uint32_t pos = 64u * q + fresh(lane), c = fresh(code_of(q));
-            const uint64_t mm = __ballot((pos >= p) & (pos < cnt) & ((c != kCSimple) | ((cgb >> q) & 1u)));
-            ev = mm ? 64u * q + (uint32_t)__builtin_ctzll(mm) : ev;
-          }
-          uint32_t kk = 0, l1 = 0, psum = 0, pdm = 0;
-          double pmn = inf, pmx = -inf;
-#pragma unroll
-          for (uint32_t q = kSegRows; q-- > 0;) {  // last row first: l1 ends as the first row's
-            const uint32_t pos = 64u * q + fresh(lane);
-            const bool run = (pos >= p) & (pos < ev);
-            const bool cn = run & ((fresh(cntb) >> q) & 1u);
-            const uint64_t cm = __ballot(cn);
-            const uint32_t lnq = fresh(ln[q]);
-            const uint32_t lf = (uint32_t)__builtin_amdgcn_readlane((int)lnq, cm ? (int)__builtin_ctzll(cm) : 0);
-            l1 = cm ? lf : l1;
-            kk += (uint32_t)__popcll(cm);
-            const double lat = __builtin_bit_cast(double, (uint64_t)fresh(lth[q]) << 32 | fresh(ltl[q]));
-            psum += cn ? lnq : 0u;
-            pmn = (cn & (lat < pmn)) ? lat : pmn;
-            pmx = (cn & (lat > pmx)) ? lat : pmx;
-            pdm = (run & (lnq != 0u)) ? max(pdm, fresh(sq[q]) - F) : pdm;
-          }
-          if (nz) L = F + max(L - F, rfl(WRing::wave_max(pdm)));
-          pc.kk = kk;
-          pc.l1 = l1;
-          pc.sum = 0;
-          pc.mn = pc.mx = 0.0;
-          if (kk) {
-            const uint64_t lo = WRing::wave_sum(psum & 0xFFFFu), hi = WRing::wave_sum(psum >> 16);
-            pc.sum = lo + (hi << 16);
-            pc.mn = WRing::wave_reduce_f64(pmn, inf, [](double x, double y) { return y < x ? y : x; });
-            pc.mx = WRing::wave_reduce_f64(pmx, -inf, [](double x, double y) { return y > x ? y : x; });
-          }
-          pc.flags = 0;
-          if (ev >= cnt) {
-            p = cnt;
-            return;
-          }
-          const uint32_t q = ev >> 6, l = ev & 63u;
-          const uint32_t s = pick(sq, q, l);
-          const uint32_t len = pick(ln, q, l);
-          const uint32_t rlo = pick(rkl, q, l);
-          const uint32_t rhi = pick(rkh, q, l);
-          const uint32_t llo = pick(ltl, q, l);
-          const uint32_t lhi = pick(lth, q, l);
-          const uint32_t xb = ((q < 8u ? tb0 : tb1) >> (4u * (q & 7u))) & 15u;
-          const uint32_t code = (uint32_t)__builtin_amdgcn_readlane((int)xb, (int)l);
-          const uint32_t close = (uint32_t)__builtin_amdgcn_readlane((int)((cgb >> q) & 1u), (int)l);
-          const uint32_t counted = (uint32_t)__builtin_amdgcn_readlane((int)((cntb >> q) & 1u), (int)l);
-          const Tm rx = {(int64_t)rhi, (int64_t)rlo};
-          if (code == kCOpenMsg || code == kCFirstMsg) {
-            if (code == kCOpenMsg) ws = rx;
-            nz = true;
-            F = L = S = s;
-          } else if (code == kCOpenEmpty) {
-            ws = rx;
-          } else if (code == kCInSpan) {
-            if (s - F > L - F) L = s;
-          } else if (code == kCBelowAcc || code == kCBelowCnt) {
-            F = s;
-          } else if (code == kCRestart) {
-            F = L = s;
-          }
-          pc.flags = 1u | code << 1 | close << 5 | counted << 6;
-          pc.pos = sb + ev;
-          pc.len = len;
-          pc.lat = __builtin_bit_cast(double, (uint64_t)lhi << 32 | llo);
-          pc.rx_sec = rhi;
-          pc.rx_usec = rlo;
-          pc.ws_sec = ws.sec;
-          pc.ws_usec = ws.usec;
-          pc.sbefore = S;
-          pc.seq_max = nz ? L : S;
-          if (close) {
-            S = pc.seq_max;
-            ws = rx;
-          }
-          p = ev + 1u;
-        };
-        SegPiece* pl = sl.pc[w];
-        uint32_t npc = 0;
-        bool done = cnt == 0;
-        while (!done && npc < kPieceCap) {
-          SegPiece pc;
-          next_piece(pc);
-          if (lane == 0) pl[npc] = pc;
-          npc++;
-          done = !(pc.flags & 1u) && p >= cnt;
-          if (p >= cnt && (pc.flags & 1u)) {  // the segment ends at an event: an empty last piece
-            done = true;
-          }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        SEG_PROF(7);
-        if (w > 0) seg_wait(&sl.rdy[2][w], tok);
-        __builtin_amdgcn_s_setprio(2);
-        const SegAgg& a = sl.ag[w];
-        uint64_t mc = (uint64_t)rfl64((int64_t)a.mc), bc = (uint64_t)rfl64((int64_t)a.bc);
-        uint64_t nrep = (uint64_t)rfl64((int64_t)a.nrep);
-        double lmin = rfld(a.lmin), lmax = rfld(a.lmax);
-        uint32_t rcount = rfl(a.rcount), ncl = rfl(a.ncl), last_close = rfl(a.last_close);
-        uint32_t last_zr = rfl(a.last_zr);
-        // Update's aggregate step for kk counted records (kk >= 1): sizes summing to `sum`, the
-        // first one's l1, latencies within [mn, mx]
-        auto fold = [&](uint32_t kk, uint64_t sum, uint32_t l1, double mn, double mx) {
-          if (mc == 0) {
-            bc = kk == 1u ? bc + l1 : sum - l1;
-            lmin = mn;
-            lmax = mx;
-          } else {
-            bc = mc == 1 ? sum : bc + sum;
-            lmin = mn < lmin ? mn : lmin;
-            lmax = mx > lmax ? mx : lmax;
-          }
-          mc += kk;
-        };
-        auto apply = [&](const SegPiece& pc) {
-          if (pc.kk) fold(pc.kk, pc.sum, pc.l1, pc.mn, pc.mx);
-          if (!(pc.flags & 1u)) return;
-          const uint32_t code = (pc.flags >> 1) & 15u, close = (pc.flags >> 5) & 1u;
-          const bool counted = (pc.flags >> 6) & 1u;
-          const uint32_t len = pc.len;
-          const double lat = pc.lat;
-          uint32_t zr = 0;
-          if (code == kCOpenMsg || code == kCFirstMsg) {
-            mc = 1;
-            bc = len;
-            lmin = lmax = lat;
-            zr = code == kCFirstMsg;
-          } else if (code == kCOpenEmpty) {
-            mc = bc = 0;
-            lmin = lmax = 0.0;
-          } else if (counted) {
-            fold(1u, len, len, lat, lat);
-          }
-          if (!close) return;
-          const double latency = counted ? lat : 0.0;
-          const Tm rx = {(int64_t)pc.rx_sec, (int64_t)pc.rx_usec}, wsc = {pc.ws_sec, pc.ws_usec};
-          if (rcount < per_flow) {
-            const double duration = tdelta(rx, wsc);
-            uint64_t r_count;
-            double r_rate, r_loss, r_min, r_max;
-            if (mc == 0) {
-              r_count = 0;
-              r_rate = 0.0;
-              r_loss = 1.0;
-              r_min = r_max = -1.0;
-            } else if (mc == 1) {
-              r_count = 1;
-              r_rate = __ddiv_rn((double)bc, duration);
-              r_loss = 0.0;
-              r_min = lmin;
-              r_max = lmax;
-            } else {
-              r_count = mc - 1;
-              r_rate = __ddiv_rn((double)bc, duration);
-              const uint32_t delta = pc.seq_max - pc.sbefore;
-              r_loss = delta <= 1 ? 0.0 : __dsub_rn(1.0, __ddiv_rn((double)mc, (double)(delta + 1)));
-              r_min = lmin;
-              r_max = lmax;
-            }
-            if (lane == 0) {
-              const size_t slot = (size_t)f * per_flow + rcount;
-              mgenx_flow_report* rp = reports + slot;
-              rp->flow = f;
-              rp->index = rcount;
-              rp->start_sec = wsc.sec;
-              rp->start_usec = wsc.usec;
-              rp->duration = duration;
-              rp->msg_count = r_count;
-              rp->rate = r_rate;
-              rp->loss = r_loss;
-              rp->latency_min = r_min;
-              rp->latency_max = r_max;
-              rp->rx_sec = rx.sec;
-              rp->rx_usec = rx.usec;
-              CloseRec cr;
-              cr.pos = pc.pos;
-              cr.zr = zr;
-              cr.mc = mc;
-              closes[slot] = cr;
-              if (report_rec) report_rec[slot] = order[pc.pos];
-            }
-          }
-          {  // for P4 (chain order: the list is in record order)
-            const uint32_t ci = rfl(sl.ncl);
-            if (lane == 0) {
-              if (ci < kCloseCap) {
-                SegClose c;
-                c.mc = mc;
-                c.pos = pc.pos - c0;
-                c.zr = zr;
-                c.slot = rcount;
-                c.kept = rcount < per_flow;
-                sl.cl[ci] = c;
-              }
-              sl.ncl = ci + 1u;
-            }
-          }
-          rcount++;
-          nrep++;
-          ncl++;
-          last_close = pc.pos;
-          last_zr = zr;
-          if (len) {
-            bc = 0;
-            mc = 1;
-            lmin = lmax = latency;
-          } else {
-            bc = mc = 0;
-            lmin = lmax = 0.0;
-          }
-        };
-        for (uint32_t i = 0; i < npc; i++) {
-          const SegPiece& src = pl[i];
-          SegPiece pc;
-          pc.kk = rfl(src.kk);
-          pc.l1 = rfl(src.l1);
-          pc.sum = (uint64_t)rfl64((int64_t)src.sum);
-          pc.mn = rfld(src.mn);
-          pc.mx = rfld(src.mx);
-          pc.flags = rfl(src.flags);
-          pc.pos = rfl(src.pos);
-          pc.len = rfl(src.len);
-          pc.lat = rfld(src.lat);
-          pc.rx_sec = rfl(src.rx_sec);
-          pc.rx_usec = rfl(src.rx_usec);
-          pc.ws_sec = rfl64(src.ws_sec);
-          pc.ws_usec = rfl64(src.ws_usec);
-          pc.sbefore = rfl(src.sbefore);
-          pc.seq_max = rfl(src.seq_max);
-          apply(pc);
-        }
-        while (!done) {  // more pieces than LDS holds: the rest in the chain
-          SegPiece pc;
-          next_piece(pc);
-          apply(pc);
-          done = p >= cnt;
-        }
-        if (lane == 0) {
-          SegAgg o;
-          o.mc = mc;
-          o.bc = bc;
-          o.nrep = nrep;
-          o.lmin = lmin;
-          o.lmax = lmax;
-          o.rcount = rcount;
-          o.ncl = ncl;
-          o.last_close = last_close;
-          o.last_zr = last_zr;
-          sl.ag[w + 1u] = o;
-        }
-        seg_post(&sl.rdy[2][w + 1u], tok);
-        __builtin_amdgcn_s_setprio(0);
-      }
-      SEG_PROF(8);
-      __syncthreads();
-      // ---- P4: the latency sums of the pass's windows, one thread each, over the lat' values
-      // in LDS (as flow_chain_kernel: a window is the in-order sum of its records' lat'; the
-      // first continues the open window's sum, a later one starts from 0.0 at its opening
-      // record, after it for a zero restart) ----
-      {
-        const uint32_t nclc = sl.ncl, ccnt = min(kSegChunk, e - c0);
-        if (nclc > kCloseCap) {
-          if (threadIdx.x == 0) sl.p4_off = 1u;
-        } else if (!sl.p4_off) {
-          const uint32_t t = threadIdx.x;
-          double s = 0.0;
-          if (t <= nclc) {
-            uint32_t lo = 0;
-            s = sl.carry;
-            if (t > 0) {
-              lo = sl.cl[t - 1u].pos + sl.cl[t - 1u].zr;
-              s = 0.0;
-            }
-            const uint32_t hi1 = t < nclc ? sl.cl[t].pos + 1u : ccnt;  // exclusive
-            uint32_t j = lo;
-            for (; j + 4u <= hi1; j += 4u) {
-              double x[4];
-#pragma unroll
-              for (int u = 0; u < 4; u++) x[u] = sl.lat[j + u];
-#pragma unroll
-              for (int u = 0; u < 4; u++) s = __dadd_rn(s, x[u]);
-            }
-            for (; j < hi1; j++) s = __dadd_rn(s, sl.lat[j]);
-            if (t < nclc) {
-              const SegClose c = sl.cl[t];
-              if (c.kept)
-                reports[(size_t)f * per_flow + c.slot].latency_ave =
-                    c.mc == 0 ? -1.0 : c.mc == 1 ? s : __ddiv_rn(s, (double)c.mc);
-            }
-          }
-          __syncthreads();  // (thread 0 has read the carry)
-          if (t == nclc) sl.carry = s;
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) sl.ncl = 0;
-      }
-      if (w == 0) {  // the pass's exit is the next one's entry
-        if (lane == 0) {
-          sl.sk[0] = sl.sk[kSegWaves];
-          sl.ag[0] = sl.ag[kSegWaves];
-        }
-        if (lane < 32u) sl.ring[0][lane] = sl.ring[kSegWaves][lane];
-      }
-      __syncthreads();
-    }
-    if (w == 0) {  // the flow's state on exit
-      const SegSkel& k = sl.sk[0];
-      const SegAgg& a = sl.ag[0];
-      WRing m;
-      m.lane = lane;
-      m.w = lane < 32u ? sl.ring[0][lane] : 0u;
-      m.first = rfl(k.first);
-      m.n = rfl(WRing::wave_sum((uint32_t)__popc(m.w)));
-      m.store_relative(sp->mask);
-      if (lane == 0) {
-        sp->mask_first = m.first;
-        sp->mask_n = m.n;
-        sp->window_valid = k.valid;
-        sp->win_start_sec = k.ws_sec;
-        sp->win_start_usec = k.ws_usec;
-        sp->win_end_sec = k.we_sec;
-        sp->win_end_usec = k.we_usec;
-        sp->seq_start = k.seq_start;
-        sp->msg_count = a.mc;
-        sp->byte_count = a.bc;
-        sp->dup_count += sl.dups;
-        sp->latency_min = a.lmin;
-        sp->latency_max = a.lmax;
-        sp->n_reports = a.nrep;
-        const uint32_t rc0 = report_count[f];
-        report_count[f] = a.rcount;
-        FlowBatch fb;
-        fb.rc0 = rc0;
-        fb.ncl = a.ncl;
-        fb.last_close = a.last_close;
-        fb.last_zr = a.last_zr;
-        fb.lsum0 = sp->latency_sum;
-        fb.rsv = sl.p4_off ? 0u : 1u;  // 1: the sums are done (flow_chain_kernel skips the flow)
-        if (!sl.p4_off) sp->latency_sum = sl.carry;
-        fbatch[f] = fb;
-      }
-    }
-    __syncthreads();
-  }
-}
-
-#endif  // MGENX_DIAG
-
-// ---- the latency sums: latency_sum += latency in record order (bit-exact) ----
-// One workgroup per flow, one thread per window the call needs: every kept report closed in this
-// call (its latency_ave) and the window still open at the end (the state's latency_sum).  A window
-// is the in-order sum of its records' lat' values: the first from latency_sum on entry, a later
-// one from its opening record's lat' (0.0 + x is exact; nothing for a zero restart).  The flow's
-// lat' values stream through LDS in pieces, so each thread's dependent v_add_f64 chain reads LDS,
-// not HBM.
-constexpr uint32_t kChainPiece = 4096;  // doubles per LDS piece (32 KiB)
-
-__global__ void __launch_bounds__(256)
-flow_chain_kernel(mgenx_flow_state* __restrict__ flows, const uint32_t* __restrict__ bnd,
-                  uint32_t bstride, const double* __restrict__ lat2,
-                  const FlowBatch* __restrict__ fbatch, const CloseRec* __restrict__ closes,
-                  mgenx_flow_report* __restrict__ reports, uint32_t per_flow,
-                  const uint32_t* __restrict__ report_count) {
-  extern __shared__ double piece[];
-  __shared__ uint32_t span[2];
-  const uint32_t f = blockIdx.x, tid = threadIdx.x;
-  const uint32_t b = bnd[(size_t)f * bstride], e = bnd[(size_t)(f + 1u) * bstride];
-  if (b >= e) return;
-  const FlowBatch fb = fbatch[f];
-  if (fb.rsv) return;  // flow_seg_kernel summed this flow's windows itself
-  const uint32_t rc1 = report_count[f];
-  const uint32_t kept = min(rc1, per_flow);
-  const uint32_t nslots = kept > fb.rc0 ? kept - fb.rc0 : 0u;
-  const uint32_t m = nslots + 1u;  // + the open window
-  const CloseRec* cl = closes + (size_t)f * per_flow;
-  for (uint32_t w0 = 0; w0 < m; w0 += blockDim.x) {
-    const uint32_t t = w0 + tid, wlast = min(m, w0 + blockDim.x) - 1u;
-    // window t: positions [lo, hi], start value s
-    uint32_t lo = 0, hi = 0;
-    double s = 0.0;
-    const bool has = t < m;
-    if (has) {
-      if (t < nslots) {
-        const uint32_t slot = fb.rc0 + t;
-        hi = cl[slot].pos;
-        if (t == 0) {
-          lo = b;
-          s = fb.lsum0;
-        } else {
-          lo = cl[slot - 1u].pos + (cl[slot - 1u].zr ? 1u : 0u);
-        }
-      } else {
-        hi = e - 1u;
-        if (fb.ncl) {
-          lo = fb.last_close + (fb.last_zr ? 1u : 0u);
-        } else {
-          lo = b;
-          s = fb.lsum0;
-        }
-      }
-    }
-    if (t == w0) span[0] = lo;
-    if (t == wlast) span[1] = hi;
-    __syncthreads();
-    const uint32_t a0 = span[0], z0 = span[1];
-    __syncthreads();
-    for (uint32_t p0 = a0; p0 <= z0 && p0 >= a0; p0 += kChainPiece) {
-      const uint32_t pend = min(z0 + 1u, p0 + kChainPiece);
-      const bool mine = has && lo <= hi && lo < pend && hi >= p0;
-      if (!__syncthreads_or(mine)) continue;
-      for (uint32_t j = tid; j < pend - p0; j += blockDim.x) piece[j] = lat2[p0 + j];
-      __syncthreads();
-      if (mine) {
-        const uint32_t ja = max(lo, p0) - p0, jz = min(hi + 1u, pend) - p0;
-        uint32_t j = ja;
-        for (; j + 8u <= jz; j += 8u) {
-          double x[8];
-#pragma unroll
-          for (int u = 0; u < 8; u++) x[u] = piece[j + u];
-#pragma unroll
-          for (int u = 0; u < 8; u++) s = __dadd_rn(s, x[u]);
-        }
-        for (; j < jz; j++) s = __dadd_rn(s, piece[j]);
-      }
-      __syncthreads();
-    }
-    if (has) {
-      if (t < nslots) {
-        const uint32_t slot = fb.rc0 + t;
-        const uint64_t mc = cl[slot].mc;
-        reports[(size_t)f * per_flow + slot].latency_ave =
-            mc == 0 ? -1.0 : mc == 1 ? s : __ddiv_rn(s, (double)mc);
-      } else {
-        flows[f].latency_sum = s;
-      }
-    }
-  }
-}
 
 // ---- ordering the records by flow, stably: a counting sort (flow count < kCountBins) --
 // The output is every record as the 24-B FRec the update reads, flow after flow, receive order
@@ -2323,7 +1380,7 @@ extern "C" void* mgenx_flow_ws_new() { return new mgenx_flow_ws(); }
 extern "C" void mgenx_flow_ws_free(void* p) {
   mgenx_flow_ws* w = static_cast<mgenx_flow_ws*>(p);
   if (!w) return;
-  if (w->mem) (void)hipFree(w->mem);
+  mgenx::dev_free(w->mem);
   delete w;
 }
 
@@ -2349,10 +1406,7 @@ extern "C" int mgenx_diag_seg_prof(unsigned long long* out, int n) {
   if (out && n == 10)  // flow_update_kernel's phase cycles (g_upd_prof)
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_upd_prof), 80) == hipSuccess ? MGENX_OK
                                                                               : MGENX_EDEVICE;
-  if (!out || n < (int)(kSegWaves * 12)) return MGENX_EINVAL;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_seg_prof), kSegWaves * 12 * 8) == hipSuccess
-             ? MGENX_OK
-             : MGENX_EDEVICE;
+  return MGENX_EINVAL;
 }
 #endif
 
@@ -2408,17 +1462,16 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
   const bool want_order = report_rec != nullptr;
   const size_t nb = a256((size_t)n * 4), rb = a256((size_t)n * sizeof(FRec));
   const size_t hb = a256(n_hist * 4), bb = a256((size_t)bins * 4);
-  const size_t lb = a256((size_t)(n + 64) * 8), fbb = a256((size_t)n_flows * sizeof(FlowBatch));
+  const size_t lb = a256((size_t)(n + 64) * 8);
   const size_t cb = a256((size_t)n_flows * per_flow * sizeof(CloseRec));
-  const size_t lfb = a256((size_t)(n_flows + 1) * 4);  // long-flow list and its count
-  // both: records (sorted), lat', per-flow batch info, closes
+  // both: records (sorted), lat', closes
   // counting: hist, start, order (report_rec only), row totals
   // radix:    keys_in, keys_out, vals_in, order, bounds, cub
-  const size_t common = rb + lb + fbb + cb + lfb;
+  const size_t common = rb + lb + cb;
   const size_t need = common + (sort_path == 0 ? 2 * hb + (want_order ? nb : 0) + a256(cub_bytes)
                                                : 4 * nb + bb + a256(cub_bytes));
   if (ws.bytes < need) {
-    if (ws.mem) (void)hipFree(ws.mem);
+    mgenx::dev_free(ws.mem);
     ws.mem = nullptr;
     ws.bytes = 0;
     if (hipMalloc(&ws.mem, need) != hipSuccess) {
@@ -2431,10 +1484,7 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
   auto take = [&](size_t b) { char* q = p; p += b; return q; };
   FRec* recs = (FRec*)take(rb);
   double* lat2 = (double*)take(lb);
-  FlowBatch* fbatch = (FlowBatch*)take(fbb);
   CloseRec* closes = (CloseRec*)take(cb);
-  uint32_t* long_list = (uint32_t*)take(lfb);  // [0] count, then the flows (diagnostics)
-  (void)long_list;
   const uint32_t* bnd;
   uint32_t bstride;
   uint32_t* order = nullptr;
@@ -2508,32 +1558,9 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
     bstride = 1;
   }
   if (sabl) return MGENX_OK;  // timing study: ordering only
-  // (diagnostics build: flows with >= MGENX_AN_SEGMIN records in this call get a workgroup
-  // each, flow_seg_kernel)
-  uint32_t seg_min = 0xFFFFFFFFu;
-#if MGENX_DIAG
-  if (const char* sm = getenv("MGENX_AN_SEGMIN")) seg_min = (uint32_t)strtoul(sm, nullptr, 10);
-  if (seg_min == 0) seg_min = 0xFFFFFFFFu;
-  if (seg_min != 0xFFFFFFFFu) {
-    if (hipMemsetAsync(long_list, 0, 4, stream) != hipSuccess) {
-      snprintf(err, errn, "flow_reduce: memset");
-      return MGENX_EDEVICE;
-    }
-    hipLaunchKernelGGL(flow_long_kernel, dim3((n_flows + 255) / 256), dim3(256), 0, stream, bnd,
-                       bstride, n_flows, seg_min, long_list + 1, long_list);
-    hipLaunchKernelGGL(flow_seg_kernel, dim3(min(n_flows, 2048u)), dim3(64 * kSegWaves), 0, stream,
-                       flows, long_list + 1, long_list, bnd, bstride, recs, order, lat2, reports,
-                       per_flow, report_count, report_rec, closes, fbatch);
-  }
-#endif
   hipLaunchKernelGGL(flow_update_kernel, dim3((n_flows + 3) / 4), dim3(256), 0, stream, flows,
                      n_flows, bnd, bstride, recs, order, lat2, reports, per_flow, report_count,
-                     report_rec, closes, fbatch, n, seg_min);
-  // (the update kernel sums its flows' windows itself; the workgroup path's flows may leave
-  // theirs to the chain kernel)
-  if (seg_min != 0xFFFFFFFFu)
-    hipLaunchKernelGGL(flow_chain_kernel, dim3(n_flows), dim3(256), kChainPiece * 8u, stream,
-                       flows, bnd, bstride, lat2, fbatch, closes, reports, per_flow, report_count);
+                     report_rec, closes, n);
   e = hipGetLastError();
   if (e != hipSuccess) {
     snprintf(err, errn, "flow_reduce: %s", hipGetErrorString(e));

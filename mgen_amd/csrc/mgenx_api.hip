@@ -10,6 +10,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <chrono>
 #include <emmintrin.h>
 #include <atomic>
@@ -121,7 +122,7 @@ struct mgenx_grow {
   size_t n = 0;
   void* get(size_t need) {
     if (n < need) {
-      if (p) (void)hipFree(p);
+      mgenx::dev_free(p);
       p = nullptr;
       n = 0;
       if (hipMalloc(&p, need) != hipSuccess) return nullptr;
@@ -130,7 +131,7 @@ struct mgenx_grow {
     return p;
   }
   void release() {
-    if (p) (void)hipFree(p);
+    mgenx::dev_free(p);
     p = nullptr;
     n = 0;
   }
@@ -165,8 +166,10 @@ struct mgenx_ctx {
   mgenx_grow snap;                 // mgenx_pcap_snap: per-packet sizes + scan scratch
   bool rand_ready = false;
   uint32_t rand_time = 0;
+  std::vector<mgenx_worker*> workers;  // live workers on this context (stopped by ctx destroy)
   char err[256] = {0};
 };
+static void worker_detach(mgenx_worker* w);
 
 namespace {
 
@@ -338,18 +341,21 @@ int mgenx_ctx_create(int device, mgenx_ctx** out) {
 int mgenx_ctx_destroy(mgenx_ctx* c) {
   if (!c) return MGENX_EINVAL;
   hipSetDevice(c->device);
+  // workers first: their waves read this context's tables.  Each is stopped and its mailbox
+  // freed; the handle stays valid for mgenx_worker_destroy, and its calls return MGENX_EINVAL
+  for (mgenx_worker* w : c->workers) worker_detach(w);
+  c->workers.clear();
   void* ps[] = {c->d_tabs, c->d_expect, c->d_xpow, c->d_ia, c->d_bytetab, c->d_rtab, c->d_rcrc,
                 c->d_sink, c->d_rq};
   if (c->scan_ws) mgenx_scan_ws_free(c->scan_ws);
   if (c->flow_ws) mgenx_flow_ws_free(c->flow_ws);
   if (c->log_ws) mgenx_log_ws_free(c->log_ws);
-  if (c->tcp_ws) hipFree(c->tcp_ws);
-  if (c->rx_ws) hipFree(c->rx_ws);
-  if (c->tcp_host) hipHostFree(c->tcp_host);
+  mgenx::dev_free(c->tcp_ws);
+  mgenx::dev_free(c->rx_ws);
+  mgenx::host_free(c->tcp_host);
   for (mgenx_grow& g : c->bl) g.release();
   c->snap.release();
-  for (void* p : ps)
-    if (p) hipFree(p);
+  for (void* p : ps) mgenx::dev_free(p);
   delete c;
   return MGENX_OK;
 }
@@ -527,16 +533,16 @@ int mgenx_pack_tcp(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl, const uint32
     if ((e = hipHostGetDevicePointer(&dp, hp, 0)) != hipSuccess) return set_err(ctx, e, "tcp");
     ctx->tcp_host_dev = static_cast<uint64_t*>(dp);
   }
-  // workspace: bytes[n+1], nfrag[n], cub; per round: fd, foff, fbuf, ff, plen, crc, state x2,
-  // acrc[3n]; the maximum fragment count
+  // workspace: bytes[n], nfrag[n], cub (a scan of n items); per round: fd, foff, fbuf, ff,
+  // plen, crc, state x2, acrc[3n]; the maximum fragment count
   size_t cub_bytes = 0;
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, cub_bytes, (const uint64_t*)nullptr,
-                                         (uint64_t*)nullptr, (int)(n + 1), s);
-  const size_t b8 = a256((size_t)(n + 1) * 8), b4 = a256((size_t)n * 4);
+                                         (uint64_t*)nullptr, (int)n, s);
+  const size_t b8 = a256((size_t)n * 8), b4 = a256((size_t)n * 4);
   const size_t need = b8 + b4 + a256(cub_bytes) + a256((size_t)n * sizeof(mgenx_pack_desc)) +
                       b8 + 4 * b4 + 2 * b4 + 3 * b4 + 256;
   if (ctx->tcp_ws_bytes < need) {
-    if (ctx->tcp_ws) hipFree(ctx->tcp_ws);
+    mgenx::dev_free(ctx->tcp_ws);
     ctx->tcp_ws = nullptr;
     ctx->tcp_ws_bytes = 0;
     if ((e = hipMalloc(&ctx->tcp_ws, need)) != hipSuccess) return set_err(ctx, e, "tcp workspace");
@@ -556,8 +562,8 @@ int mgenx_pack_tcp(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl, const uint32
   uint32_t* st[2] = {(uint32_t*)take(b4), (uint32_t*)take(b4)};
   uint32_t* acrc = (uint32_t*)take(3 * b4);
   uint32_t* max_frag = (uint32_t*)take(256);
-  // plan: bytes per message, fragments; offsets by an exclusive scan (the message offsets
-  // are the caller's array: n + 1 entries are not assumed, the scan runs in the workspace)
+  // plan: bytes per message, fragments; the message offsets by an exclusive scan of n items
+  // straight into the caller's array (n entries)
   if ((e = hipMemsetAsync(max_frag, 0, 4, s)) != hipSuccess) return set_err(ctx, e, "tcp plan");
   if ((e = mgenx::launch_tcp_plan(dev_tmpl, dev_desc, dev_msg_total, n, bytes, nfrag, max_frag,
                                   s)) != hipSuccess)
@@ -620,7 +626,7 @@ int mgenx_tcp_rx_persist(mgenx_ctx* ctx, const uint8_t* dev_slab, const uint64_t
   const size_t need = mgenx::rx_persist_ws_bytes(n);
   hipError_t e;
   if (ctx->rx_ws_bytes < need) {  // grows (allocates) only when the batch outgrows it
-    if (ctx->rx_ws) hipFree(ctx->rx_ws);
+    mgenx::dev_free(ctx->rx_ws);
     ctx->rx_ws = nullptr;
     ctx->rx_ws_bytes = 0;
     if ((e = hipMalloc(&ctx->rx_ws, need)) != hipSuccess) return set_err(ctx, e, "rx workspace");
@@ -950,7 +956,12 @@ struct mgenx_worker {
   uint32_t seq = 0;                  // the last request number issued
   uint64_t idle_ticks = 0;           // s_memrealtime ticks (100 MHz)
   bool launched = false;
+  std::mutex mu;                     // a call and a stop from another thread do not interleave
 };
+
+// every live worker of the process (mgenx::quiesce_workers)
+static std::mutex g_workers_mu;
+static std::vector<mgenx_worker*> g_workers;
 
 static uint32_t w_load(const uint32_t* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
 static void w_store(uint32_t* p, uint32_t v) { __atomic_store_n(p, v, __ATOMIC_RELEASE); }
@@ -1002,6 +1013,7 @@ static void w_post(mgenx::WMail* m, uint32_t r, uint32_t op, uint32_t len, uint3
 // reply: reply words 24 - 3 * nchunk .. 23 (the last nchunk chunks) into out
 static int worker_call(mgenx_worker* w, uint32_t op, uint32_t len, uint32_t arg, uint32_t nchunk,
                        uint32_t* out, const uint8_t* pd = nullptr, uint32_t pn = 0) {
+  // (the caller holds w->mu: the mailbox's data area is written before this call)
   if (!w->launched || !w_load(&w->mail->alive)) {
     hipSetDevice(w->ctx->device);
     const int rc = worker_launch(w, w->seq);
@@ -1051,7 +1063,7 @@ int mgenx_worker_create(mgenx_ctx* ctx, uint32_t idle_ms, mgenx_worker** out) {
   *out = nullptr;
   hipSetDevice(ctx->device);
   mgenx_worker* w = new mgenx_worker();
-  w->ctx = ctx;
+  w->ctx = ctx;  // (not yet in ctx->workers: a failed create is freed by mgenx_worker_destroy)
   w->idle_ticks = (uint64_t)(idle_ms ? idle_ms : 1u) * 100000ull;
   if (hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking) != hipSuccess ||
       hipHostMalloc((void**)&w->mail, sizeof(mgenx::WMail),
@@ -1061,30 +1073,79 @@ int mgenx_worker_create(mgenx_ctx* ctx, uint32_t idle_ms, mgenx_worker** out) {
     return MGENX_ENOMEM;
   }
   memset(w->mail, 0, sizeof(mgenx::WMail));
+  ctx->workers.push_back(w);
+  {
+    std::lock_guard<std::mutex> g(g_workers_mu);
+    g_workers.push_back(w);
+  }
   *out = w;
+  return MGENX_OK;
+}
+
+// end the worker's wave (if one runs) and wait for it: no wave is left polling, so a later
+// device-wide synchronisation (hipFree, hipDeviceSynchronize) does not wait for its idle timeout
+static void worker_stop(mgenx_worker* w) {
+  std::lock_guard<std::mutex> g(w->mu);
+  if (!w->launched || !w->mail || !w->ctx) return;
+  hipSetDevice(w->ctx->device);
+  if (w_load(&w->mail->alive)) {  // ask the wave to end; it may end on its own meanwhile
+    uint32_t r = w->seq + 1u;
+    if (r == 0u) r = 1u;
+    w->seq = r;
+    w_post(w->mail, r, mgenx::kWorkStop, 0u, 0u, nullptr, 0u);
+  }
+  (void)hipStreamSynchronize(w->stream);
+  w->launched = false;
+}
+
+// the wave stopped and the device resources freed; the handle stays (ctx = null)
+static void worker_detach(mgenx_worker* w) {
+  {
+    std::lock_guard<std::mutex> g(g_workers_mu);
+    g_workers.erase(std::remove(g_workers.begin(), g_workers.end(), w), g_workers.end());
+  }
+  worker_stop(w);
+  mgenx::host_free(w->mail);  // (the other workers' waves are ended first)
+  if (w->stream) (void)hipStreamDestroy(w->stream);
+  w->mail = w->mail_dev = nullptr;
+  w->stream = nullptr;
+  w->ctx = nullptr;
+}
+
+extern "C++" {
+namespace mgenx {
+void quiesce_workers() {
+  std::vector<mgenx_worker*> ws;
+  {
+    std::lock_guard<std::mutex> g(g_workers_mu);
+    ws = g_workers;
+  }
+  for (mgenx_worker* w : ws) worker_stop(w);
+}
+}  // namespace mgenx
+}  // extern "C++"
+
+int mgenx_worker_stop(mgenx_worker* w) {
+  if (!w) return MGENX_EINVAL;
+  worker_stop(w);
   return MGENX_OK;
 }
 
 int mgenx_worker_destroy(mgenx_worker* w) {
   if (!w) return MGENX_EINVAL;
-  if (w->launched && w->mail) {
-    hipSetDevice(w->ctx->device);
-    if (w_load(&w->mail->alive)) {  // ask the wave to end; it may end on its own meanwhile
-      uint32_t r = w->seq + 1u;
-      if (r == 0u) r = 1u;
-      w->seq = r;
-      w_post(w->mail, r, mgenx::kWorkStop, 0u, 0u, nullptr, 0u);
-    }
-    (void)hipStreamSynchronize(w->stream);
+  if (w->ctx) {
+    std::vector<mgenx_worker*>& v = w->ctx->workers;
+    v.erase(std::remove(v.begin(), v.end(), w), v.end());
+    worker_detach(w);
   }
-  if (w->mail) (void)hipHostFree(w->mail);
-  if (w->stream) (void)hipStreamDestroy(w->stream);
   delete w;
   return MGENX_OK;
 }
 
 int mgenx_worker_unpack(mgenx_worker* w, const uint8_t* msg, uint32_t len, mgenx_unpacked* out) {
-  if (!w || !out || (len && !msg) || len > MGENX_WORKER_MAX_BYTES) return MGENX_EINVAL;
+  if (!w) return MGENX_EINVAL;
+  std::lock_guard<std::mutex> g(w->mu);
+  if (!w->ctx || !out || (len && !msg) || len > MGENX_WORKER_MAX_BYTES) return MGENX_EINVAL;
   const uint32_t n = len < mgenx::kWorkerHdrBytes ? len : mgenx::kWorkerHdrBytes;
   // Unpack reads the header bytes only: the first kPollData travel in the polled pieces, the
   // data area is for headers longer than that
@@ -1100,7 +1161,9 @@ int mgenx_worker_pack(mgenx_worker* w, const mgenx_flow_tmpl* tmpl, const uint8_
                       const mgenx_pack_desc* desc, uint32_t buf_len, uint32_t crc_in,
                       uint32_t opts, uint32_t fill_time, uint8_t* out, uint32_t* ret,
                       uint32_t* tx_crc, uint32_t* state) {
-  if (!w || !tmpl || !desc || !ret || !tx_crc || !state || buf_len > MGENX_WORKER_PACK_MAX ||
+  if (!w) return MGENX_EINVAL;
+  std::lock_guard<std::mutex> g(w->mu);
+  if (!w->ctx || !tmpl || !desc || !ret || !tx_crc || !state || buf_len > MGENX_WORKER_PACK_MAX ||
       (buf_len && !out) || (tmpl->has_payload && tmpl->payload_len && !payload))
     return MGENX_EINVAL;
   if (opts & MGENX_PACK_RANDOM_FILL) {  // the rand() stream of this fill time (cached)
@@ -1129,7 +1192,9 @@ int mgenx_worker_pack(mgenx_worker* w, const mgenx_flow_tmpl* tmpl, const uint8_
 
 int mgenx_worker_crc32(mgenx_worker* w, const uint8_t* data, uint32_t len, uint32_t state_in,
                        uint32_t* state_out) {
-  if (!w || !state_out || (len && !data) || len > MGENX_WORKER_MAX_BYTES) return MGENX_EINVAL;
+  if (!w) return MGENX_EINVAL;
+  std::lock_guard<std::mutex> g(w->mu);
+  if (!w->ctx || !state_out || (len && !data) || len > MGENX_WORKER_MAX_BYTES) return MGENX_EINVAL;
   if (len) memcpy(w->mail->data, data, len);
   uint32_t words[3];  // reply words 21-23
   const int rc = worker_call(w, mgenx::kWorkCrc32, len, state_in, 1u, words);

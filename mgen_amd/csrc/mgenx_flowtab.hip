@@ -170,10 +170,20 @@ __global__ void flowtab_insert_kernel(FlowSlot* __restrict__ tab, uint32_t cap_m
       // some of them -- the first record among them, which numbers the key.)
       const uint32_t held = *n_flows_before +
           __hip_atomic_load(n_new, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (held >= (cap_mask + 1u) / 2u) break;
       uint32_t exp = kSlotEmpty;
-      if (__hip_atomic_compare_exchange_strong(&sl.state, &exp, kSlotBusy, __ATOMIC_ACQ_REL,
-                                               __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) {
+      if (held >= (cap_mask + 1u) / 2u) {
+        // at the bound only a record that would CREATE its key is refused: a record of a key
+        // another record is creating in this slot right now (it read n_new after that one's
+        // add) sees the claim after a short wait and compares keys below.  A claim later than
+        // the wait still gets a spurious refusal (mgenx.h: the caller redoes the batch).
+        for (int spin = 0; spin < 64 && exp == kSlotEmpty; spin++) {
+          __builtin_amdgcn_s_sleep(1);
+          exp = __hip_atomic_load(&sl.state, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (exp == kSlotEmpty) break;
+        st = exp;
+      } else if (__hip_atomic_compare_exchange_strong(&sl.state, &exp, kSlotBusy, __ATOMIC_ACQ_REL,
+                                                      __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) {
 #pragma unroll
         for (int j = 0; j < 12; j++)
           __hip_atomic_store(&sl.key.w[j], k.w[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -184,8 +194,9 @@ __global__ void flowtab_insert_kernel(FlowSlot* __restrict__ tab, uint32_t cap_m
         __hip_atomic_fetch_add(n_new, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         rec_slot[i] = s;
         return;
+      } else {
+        st = exp;
       }
-      st = exp;
     }
     // a slot being written: wait (bounded) until its key is published
     for (int spin = 0; st == kSlotBusy && spin < 1 << 20; spin++) {
@@ -383,9 +394,9 @@ int mgenx_flow_table_create(mgenx_ctx* ctx, uint32_t max_flows, mgenx_flow_table
 
 int mgenx_flow_table_destroy(mgenx_flow_table* t) {
   if (!t) return MGENX_EINVAL;
-  if (t->slots) (void)hipFree(t->slots);
-  if (t->counters) (void)hipFree(t->counters);
-  if (t->ws) (void)hipFree(t->ws);
+  mgenx::dev_free(t->slots);
+  mgenx::dev_free(t->counters);
+  mgenx::dev_free(t->ws);
   delete t;
   return MGENX_OK;
 }
@@ -404,7 +415,7 @@ int mgenx_flow_lookup(mgenx_ctx* ctx, mgenx_flow_table* t, const mgenx_cols* col
   const size_t bb = ((size_t)nblk * 4 + 255) & ~(size_t)255;
   const size_t need = 2 * nb + 2 * bb + 256;
   if (t->ws_bytes < need) {
-    if (t->ws) (void)hipFree(t->ws);
+    mgenx::dev_free(t->ws);
     t->ws = nullptr;
     t->ws_bytes = 0;
     if (hipMalloc(&t->ws, need) != hipSuccess) return MGENX_ENOMEM;

@@ -13,6 +13,21 @@
 
 namespace mgenx {
 
+// Ends every resident worker wave (mgenx_worker_*, mgenx_api.hip) in the process and waits for
+// them.  hipFree / hipHostFree synchronise the device, so with a wave still polling its mailbox
+// they would wait for its idle timeout: every workspace growth frees through these.
+void quiesce_workers();
+inline void dev_free(void* p) {
+  if (!p) return;
+  quiesce_workers();
+  (void)hipFree(p);
+}
+inline void host_free(void* p) {
+  if (!p) return;
+  quiesce_workers();
+  (void)hipHostFree(p);
+}
+
 // hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device): the attribute is
 // per device, and threaded multi-GPU callers (mgenx::ShardedScan) launch concurrently, so the
 // "done" record is per device and guarded (every entry point sets its context's device first)

@@ -441,7 +441,7 @@ extern "C" void mgenx_log_ws_free(void* p) {
   mgenx_log_ws* w = static_cast<mgenx_log_ws*>(p);
   while (w) {
     mgenx_log_ws* nx = w->next;
-    if (w->mem) (void)hipFree(w->mem);
+    mgenx::dev_free(w->mem);
     delete w;
     w = nx;
   }
@@ -485,7 +485,7 @@ extern "C" int mgenx_log_recv_run(void* wsp, bool binary, const uint8_t* slab,
   const size_t len_bytes = (((size_t)n + 1) * 8 + 255) & ~(size_t)255;
   const size_t need = len_bytes + scan_bytes;
   if (ws.bytes < need) {
-    if (ws.mem) (void)hipFree(ws.mem);
+    mgenx::dev_free(ws.mem);
     ws.mem = nullptr;
     ws.bytes = 0;
     if (hipMalloc(&ws.mem, need) != hipSuccess) {
@@ -1311,7 +1311,7 @@ __global__ void __launch_bounds__(kLogThreads) binlog_line_kernel(BinParams p) {
 // per-stream scratch for the two-pass line formatters and the walk's scans
 static int rep_ws(mgenx_log_ws& ws, size_t need, void** out, char* err, size_t errn) {
   if (ws.bytes < need) {
-    if (ws.mem) (void)hipFree(ws.mem);
+    mgenx::dev_free(ws.mem);
     ws.mem = nullptr;
     ws.bytes = 0;
     if (hipMalloc(&ws.mem, need) != hipSuccess) {

@@ -817,7 +817,7 @@ struct ScanWork {
 
 hipError_t ensure(ScanWork& w, size_t need) {
   if (w.bytes >= need) return hipSuccess;
-  if (w.mem) hipFree(w.mem);
+  mgenx::dev_free(w.mem);
   w.mem = nullptr;
   w.bytes = 0;
   hipError_t e = hipMalloc(&w.mem, need);
@@ -874,8 +874,8 @@ extern "C" void mgenx_scan_ws_free(void* p) {
   mgenx_scan_ws* w = static_cast<mgenx_scan_ws*>(p);
   if (!w) return;
   for (ScanWork* x : {&w->slots, &w->cands, &w->tabs, &w->small, &w->marks})
-    if (x->mem) hipFree(x->mem);
-  if (w->host) hipHostFree(w->host);
+    mgenx::dev_free(x->mem);
+  mgenx::host_free(w->host);
   delete w;
 }
 

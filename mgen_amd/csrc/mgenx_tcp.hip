@@ -234,7 +234,8 @@ __global__ void tcp_finish_kernel(uint8_t* __restrict__ out, const uint64_t* __r
   if (i >= n) return;
   const uint32_t F = ff[i], B = fbuf[i];
   if (!ck || !F || plen[i] == 0) return;
-  if (foff[i] > cap || F > cap - foff[i]) return;  // a stream that does not fit: no store past it
+  // (defensive only: mgenx_pack_tcp refuses a stream past its capacity before any round runs)
+  if (foff[i] > cap || F > cap - foff[i]) return;
   uint32_t c = tx_crc[i];
   bool write = true;
   if (F <= B) {

@@ -306,33 +306,25 @@ def test_flow_reduce_mixed_lengths(torch, eng, window):
 
 
 @pytest.mark.parametrize("window", [0.001, 0.3])
-def test_flow_reduce_workgroup_path_diag(torch, window, monkeypatch):
-    """The workgroup-per-flow path (flow_seg_kernel: segments walked in series, duplicates and
-    aggregates in parallel, the latency sums in LDS), built only into the diagnostics library
-    (measured slower than the wave path), enabled with MGENX_AN_SEGMIN: flows
-    of 2048 records and more take it, shorter ones the wave kernel, and the two hand flows to
-    each other across calls.  Bit-exact against the oracle like the product path."""
-    from mgen_amd import Engine
+def test_flow_reduce_long_and_jumpy_flows(torch, eng, window):
+    """Few long flows (one flow of many thousand records beside short ones) and flows whose
+    sequence numbers jump past the mask span and back: every event kind inside long runs of
+    simple records, split across two calls.  Bit-exact against the oracle."""
     from oracle import oracle as O
-    monkeypatch.setenv("MGENX_AN_SEGMIN", "2048")
-    e = Engine(0, diag=True)
-    try:
-        d = _mixed_lengths()
-        n_flows, per_flow = 8, 4096
-        st, rep, cnt, _ = run_gpu(torch, e, d, n_flows, window, per_flow,
-                                  splits=(0, len(d["seq"]) * 3 // 4))
-        of, orep, ocnt = O.flow_reduce_batch(n_flows, d["flow_id"] - 1, d["seq"], d["tx_sec"],
-                                             d["tx_usec"], d["msg_len"], d["rx_sec"],
-                                             d["rx_usec"], window=window, per_flow=per_flow)
-        compare(st, rep, cnt, of, orep, ocnt, per_flow)
-        d = _jumpy_flows(40, 6000, seed=int(window * 1000) + 3)
-        st, rep, cnt, _ = run_gpu(torch, e, d, 40, window, 64, splits=(0, 5000))
-        of, orep, ocnt = O.flow_reduce_batch(40, d["flow_id"] - 1, d["seq"], d["tx_sec"],
-                                             d["tx_usec"], d["msg_len"], d["rx_sec"],
-                                             d["rx_usec"], window=window, per_flow=64)
-        compare(st, rep, cnt, of, orep, ocnt, 64)
-    finally:
-        e.close()
+    d = _mixed_lengths()
+    n_flows, per_flow = 8, 4096
+    st, rep, cnt, _ = run_gpu(torch, eng, d, n_flows, window, per_flow,
+                              splits=(0, len(d["seq"]) * 3 // 4))
+    of, orep, ocnt = O.flow_reduce_batch(n_flows, d["flow_id"] - 1, d["seq"], d["tx_sec"],
+                                         d["tx_usec"], d["msg_len"], d["rx_sec"],
+                                         d["rx_usec"], window=window, per_flow=per_flow)
+    compare(st, rep, cnt, of, orep, ocnt, per_flow)
+    d = _jumpy_flows(40, 6000, seed=int(window * 1000) + 3)
+    st, rep, cnt, _ = run_gpu(torch, eng, d, 40, window, 64, splits=(0, 5000))
+    of, orep, ocnt = O.flow_reduce_batch(40, d["flow_id"] - 1, d["seq"], d["tx_sec"],
+                                         d["tx_usec"], d["msg_len"], d["rx_sec"],
+                                         d["rx_usec"], window=window, per_flow=64)
+    compare(st, rep, cnt, of, orep, ocnt, 64)
 
 
 def test_flow_reduce_config4_full_size_vs_oracle(torch, eng):

@@ -136,3 +136,110 @@ def test_worker_latency_report(torch, eng):
         assert um < 200 and cm < 200
     finally:
         w.close()
+
+
+def _long_header_records():
+    """Records whose header runs past the worker's 180 polled bytes (dst_len / host_len bytes
+    up to 255: Unpack does not bound them, mgenMsg.cpp:394-398, 425-431), so the worker reads
+    them from the mailbox's data area; plus short and junk records around the boundary."""
+    from mgen_amd.workloads import udp_fixed
+    from oracle import oracle as O
+    tmpl, pool, desc = udp_fixed(2, 1024)
+    slab, _ = O.udp_pack_batch(tmpl, desc, pool, 2 * 1024, stride=1024, checksum=True)
+    base = slab[:1024].copy()
+    rng = np.random.default_rng(11)
+    recs = []
+    for dl in (4, 16, 100, 130, 150, 152, 153, 156, 157, 160, 200, 255):
+        for hl in (0, 4, 16, 40, 255):
+            r = base.copy()
+            r[23] = dl
+            r[24:24 + dl] = rng.integers(0, 256, dl, dtype=np.uint8)
+            h = 24 + dl
+            r[h:h + 2] = (5001 >> 8, 5001 & 255)
+            r[h + 2] = 1 if hl in (4, 40) else 2
+            r[h + 3] = hl
+            r[h + 4:h + 4 + hl] = rng.integers(0, 256, hl, dtype=np.uint8)
+            for L in (1024, min(1024, h + 4 + hl + 16), max(28, h + 10)):
+                recs.append(r[:L].tobytes())
+    for L in (0, 1, 27, 28, 29, 47, 48, 179, 180, 181, 183, 184):
+        recs.append(rng.integers(0, 256, L, dtype=np.uint8).tobytes())
+    return recs
+
+
+def test_worker_unpack_vs_oracle(torch, eng):
+    """mgenx_worker_unpack straight against the oracle's Unpack alone (or_unpack: a fresh
+    MgenMsg, Unpack(buf, len, false, false), no caller CRC -- mgenMsg.cpp:315-500) on every
+    unpack vector of the golden matrix and on headers longer than the polled bytes."""
+    from oracle import oracle as O
+    g = dict(np.load(GOLD, allow_pickle=False))
+    slab, offs, lens = g["unpack_slab"], g["unpack_offs"], g["unpack_lens"]
+    msgs = [slab[int(o):int(o) + int(L)].tobytes() for o, L in zip(offs, lens)]
+    longs = _long_header_records()
+    # which records take the data-area path: the header (24 + dst + 4 + host + 16) past the
+    # 180 bytes that travel with the doorbell
+    def hdr_need(m):
+        if len(m) < 24:
+            return 0
+        need = 24 + m[23]
+        if need + 4 <= min(len(m), 180):
+            need += 4 + m[need + 3] + 16
+        else:
+            need += 4
+        return min(len(m), need)
+    assert sum(hdr_need(m) > 180 for m in longs) >= 20
+    w = eng.worker()
+    try:
+        for i, m in enumerate(msgs + longs):
+            u = w.unpack(m)
+            f = O.unpack(m)
+            for k in FIELDS:
+                if k == "decoded":
+                    continue
+                assert int(u[k]) == int(f[k]), (i, len(m), k, int(u[k]), int(f[k]))
+            assert int(u["err"] == 0) == int(f["ok"]), i
+            assert bytes(u["dst_addr"]) == f["dst_addr"].tobytes(), i
+            assert bytes(u["host_addr"]) == f["host_addr"].tobytes(), i
+    finally:
+        w.close()
+
+
+def test_worker_after_engine_close(torch):
+    """mgenx_ctx_destroy stops and frees the workers made on it; their handles then refuse
+    calls (MgenxError) and still free cleanly."""
+    from mgen_amd import Engine, MgenxError
+    e = Engine(0)
+    w = e.worker(idle_ms=5000)
+    msg = bytes(64)
+    w.unpack(msg)
+    e.close()
+    with pytest.raises(MgenxError):
+        w.unpack(msg)
+    w.close()
+
+
+def test_batch_growth_after_worker_call(torch):
+    """A batch call that grows a workspace (hipFree) right after a worker call: the library ends
+    the resident wave first, so the call does not wait out the wave's idle timeout (5 s here),
+    and the next worker call relaunches it."""
+    from mgen_amd import Engine
+    from mgen_amd.workloads import poisson_flows
+    e = Engine(0)
+    try:
+        w = e.worker(idle_ms=5000)
+        msg = bytes(64)
+        u0 = w.unpack(msg)
+        d = poisson_flows(4096, 8)
+        t = {k: torch.from_numpy(v).cuda() for k, v in d.items()}
+        idx = torch.from_numpy((d["flow_id"] - 1).astype(np.uint32)).cuda()
+        for n in (1024, 4096):  # the second call grows the flow-reduce workspace
+            w.unpack(msg)
+            t0 = time.perf_counter()
+            flows = e.flow_init(8, 1.0)
+            e.flow_reduce(flows, 8, idx, t["seq"], t["tx_sec"], t["tx_usec"], t["msg_len"],
+                          t["rx_sec"], t["rx_usec"], n=n)
+            torch.cuda.synchronize()
+            assert time.perf_counter() - t0 < 2.0, n
+        assert w.unpack(msg).tobytes() == u0.tobytes()
+        w.close()
+    finally:
+        e.close()
