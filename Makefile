@@ -8,10 +8,11 @@ HIPFLAGS ?= -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -Wno-unused-value -Wno
 NAMES := mgenx_api mgenx_unpack mgenx_pack mgenx_scan mgenx_analytic mgenx_log mgenx_comm mgenx_worker \
          mgenx_flowtab mgenx_tcp mgenx_rx mgenx_pcap
 HDR := include/mgenx.h include/mgenx_diag.h mgen_amd/csrc/mgenx_common.hpp mgen_amd/csrc/mgenx_kernels.hpp \
+       mgen_amd/csrc/mgenx_flowsm.hpp \
        mgen_amd/csrc/mgenx_parse.hpp
 OBJ := $(addprefix build/product/,$(addsuffix .o,$(NAMES)))
 DOBJ := $(addprefix build/diag/,$(addsuffix .o,$(NAMES)))
-LIBS := -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+LIBS := -L/opt/rocm/lib -lrccl -lhsa-runtime64 -Wl,-rpath,/opt/rocm/lib
 
 all: mgen_amd/libmgenx.so mgen_amd/libmgenx_diag.so oracle tests/cpp/host_roundtrip \
      tests/cpp/loopback tests/cpp/compat_shapes tests/cpp/compat_shapes_pl tests/cpp/shim_latency \

@@ -287,7 +287,9 @@ int mgenx_crc32_batch(mgenx_ctx* ctx, const uint8_t* dev_data, const uint64_t* d
  *                           err (MgenMsg::Error; 0 = Unpack returned true); no CRC check
  *   mgenx_worker_crc32   <- MgenMsg::ComputeCRC32 (include/mgenMsg.h:201-203, mgenMsg.cpp:
  *                           524-541): the running checksum in and out
- *   mgenx_worker_pack    <- MgenMsg::Pack alone (below) */
+ *   mgenx_worker_recv    <- Unpack + the receive path's ComputeCRC32 in one reply (below)
+ *   mgenx_worker_pack    <- MgenMsg::Pack alone (below)
+ *   mgenx_worker_flow_update <- MgenAnalytic::Update of one record (below) */
 #define MGENX_WORKER_MAX_BYTES 65536u
 #define MGENX_WORKER_PACK_MAX  16384u   /* mgenx_worker_pack's largest bufferLen */
 typedef struct {
@@ -303,9 +305,33 @@ typedef struct mgenx_worker mgenx_worker;
 int mgenx_worker_create(mgenx_ctx* ctx, uint32_t idle_ms, mgenx_worker** out);
 int mgenx_worker_destroy(mgenx_worker* w);
 int mgenx_worker_stop(mgenx_worker* w);  /* end the wave now (the next call relaunches it) */
+/* *flags: MGENX_WORKER_DEVICE_MAILBOX when requests go to fine-grained device memory the host
+ * stores into through the BAR (the runtime granted the CPU access), else pinned host memory
+ * (environment MGENX_WORKER_HOST_MAILBOX=1 forces the latter). */
+#define MGENX_WORKER_DEVICE_MAILBOX 0x1u
+int mgenx_worker_info(const mgenx_worker* w, uint32_t* flags);
 int mgenx_worker_unpack(mgenx_worker* w, const uint8_t* msg, uint32_t len, mgenx_unpacked* out);
 int mgenx_worker_crc32(mgenx_worker* w, const uint8_t* data, uint32_t len, uint32_t state_in,
                        uint32_t* state_out);
+/* The UDP / SINK receive path's two calls in one reply (mgenTransport.cpp:958-965,
+ * 2092-2100): MgenMsg::Unpack as mgenx_worker_unpack, then -- when Unpack succeeded and `force`
+ * (checksum_force) is set or the decoded flags carry CHECKSUM -- ComputeCRC32(0, msg, len - 4):
+ * *crc_done = 1 and *crc_state the running CRC the caller then XORs with CRC32_XOROT and
+ * compares with the trailer (no final xor here, as ComputeCRC32); else *crc_done = 0. */
+int mgenx_worker_recv(mgenx_worker* w, const uint8_t* msg, uint32_t len, uint32_t force,
+                      mgenx_unpacked* out, uint32_t* crc_state, uint32_t* crc_done);
+/* MgenAnalytic::Update (include/mgenAnalytic.h:91-94, mgenAnalytic.cpp:74-258) of ONE record
+ * on the device flow state dev_flows[slot] (mgenx_flow_init / mgenx_flow_reduce's array; the
+ * wave reads and writes it in place, so batch calls before and after on the same stream order
+ * see it): *updated = 1 when the record closed a window, with the report in *report (index =
+ * the flow's report number; latency_ave from the window's in-order latency sum).  Equal to
+ * mgenx_flow_reduce of the same records one call at a time. */
+struct mgenx_flow_state;
+struct mgenx_flow_report;
+int mgenx_worker_flow_update(mgenx_worker* w, struct mgenx_flow_state* dev_flows, uint32_t slot,
+                             uint32_t seq, uint32_t rx_sec, uint32_t rx_usec, uint32_t msg_size,
+                             uint32_t tx_sec, uint32_t tx_usec, uint32_t* updated,
+                             struct mgenx_flow_report* report);
 /* MgenMsg::Pack (include/mgenMsg.h:108, mgenMsg.cpp:83-313) of one message, as mgenx_pack_msgs
  * with n = 1: the message as a template (its payload bytes at `payload`, payload_off ignored)
  * and a descriptor; bufferLen, the tx_checksum argument, MGENX_PACK_CHECKSUM /

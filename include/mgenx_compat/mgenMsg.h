@@ -69,11 +69,12 @@ class MgenMsg {
   }
 
   bool Unpack(UINT32* buffer, UINT16 bufferLen, bool forceChecksum, bool log_data) {
-    (void)forceChecksum;  // unused by the reference too (mgenMsg.cpp:315-500)
+    // forceChecksum is unused by the reference's Unpack (mgenMsg.cpp:315-500); here it tells
+    // the engine that the caller's receive path checksums next (mgenTransport.cpp:960-963)
     (void)log_data;
     MgenMsg* self = this;
     bool ok = false;
-    UnpackBatch(&self, &buffer, &bufferLen, &ok, 1);
+    UnpackBatch(&self, &buffer, &bufferLen, &ok, 1, forceChecksum);
     return ok;
   }
 
@@ -92,7 +93,7 @@ class MgenMsg {
                         bool includeChecksum, UINT32* txChecksums, UINT16* results, unsigned n);
   // results[i] = msgs[i]->Unpack(buffers[i], bufferLens[i], ...)
   static void UnpackBatch(MgenMsg* const* msgs, UINT32* const* buffers, const UINT16* bufferLens,
-                          bool* results, unsigned n);
+                          bool* results, unsigned n, bool forceChecksum = false);
   // checksums[i]: ComputeCRC32(checksums[i], buffers[i], lens[i])
   static void ComputeCRC32Batch(UINT32* checksums, const UINT8* const* buffers,
                                 const UINT32* lens, unsigned n);
@@ -276,14 +277,15 @@ inline void MgenMsg::PackBatch(MgenMsg* const* msgs, UINT32* const* buffers,
 }
 
 inline void MgenMsg::UnpackBatch(MgenMsg* const* msgs, UINT32* const* buffers,
-                                 const UINT16* bufferLens, bool* results, unsigned n) {
+                                 const UINT16* bufferLens, bool* results, unsigned n,
+                                 bool forceChecksum) {
   using mgenx::compat::Engine;
   std::vector<mgenx::compat::UnpackOut> out(n);
   std::vector<const uint8_t*> bufs(n);
   for (unsigned i = 0; i < n; i++) bufs[i] = (const uint8_t*)buffers[i];
   {
     std::lock_guard<std::mutex> g(Engine::Get().Lock());
-    Engine::Get().Unpack(bufs.data(), bufferLens, n, out.data());
+    Engine::Get().Unpack(bufs.data(), bufferLens, n, out.data(), forceChecksum);
   }
   for (unsigned i = 0; i < n; i++) {
     MgenMsg& m = *msgs[i];

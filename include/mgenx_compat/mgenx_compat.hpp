@@ -164,12 +164,27 @@ class Engine {
 
   // ---- MgenMsg::Unpack alone (mgenx_unpack_batch, MGENX_OPT_SKIP_CRC) ---------------
   // One message (the reference's per-datagram call): the resident worker, no launch or copy.
-  void Unpack(const uint8_t* const* bufs, const uint16_t* lens, unsigned n, UnpackOut* out) {
+  // The worker also computes the checksum the receive path asks for next when `force`
+  // (checksum_force, the Unpack argument the callers pass) is set or the message carries
+  // CHECKSUM (mgenTransport.cpp:958-965): ComputeCRC32(0, buf, len - 4) on the same bytes then
+  // returns it without a GPU call (Crc32Update).
+  void Unpack(const uint8_t* const* bufs, const uint16_t* lens, unsigned n, UnpackOut* out,
+              bool force = false) {
     if (n == 0) return;
     Init();
+    crc_cache_.valid = false;
     if (n == 1 && Worker()) {
       mgenx_unpacked u;
-      Check(mgenx_worker_unpack(worker_, bufs[0], lens[0], &u), "mgenx_worker_unpack");
+      uint32_t crc = 0, done = 0;
+      Check(mgenx_worker_recv(worker_, bufs[0], lens[0], force ? 1u : 0u, &u, &crc, &done),
+            "mgenx_worker_recv");
+      if (done) {
+        crc_cache_.valid = true;
+        crc_cache_.ptr = bufs[0];
+        crc_cache_.len = lens[0] - 4u;
+        crc_cache_.bytes.assign(bufs[0], bufs[0] + crc_cache_.len);
+        crc_cache_.crc = crc;
+      }
       UnpackOut& r = out[0];
       r.flow_id = u.flow_id;
       r.seq_num = u.seq_num;
@@ -296,6 +311,13 @@ class Engine {
                    unsigned n, uint32_t* state_out) {
     if (n == 0) return;
     Init();
+    if (n == 1 && crc_cache_.valid && state_in[0] == 0u && bufs[0] == crc_cache_.ptr &&
+        lens[0] == crc_cache_.len && memcmp(bufs[0], crc_cache_.bytes.data(), lens[0]) == 0) {
+      state_out[0] = crc_cache_.crc;  // computed with the Unpack of these bytes (above)
+      crc_cache_.valid = false;
+      return;
+    }
+    crc_cache_.valid = false;
     if (n == 1 && lens[0] <= MGENX_WORKER_MAX_BYTES && Worker()) {
       Check(mgenx_worker_crc32(worker_, bufs[0], lens[0], state_in[0], state_out),
             "mgenx_worker_crc32");
@@ -356,6 +378,14 @@ class Engine {
                   const uint32_t* seq, unsigned n, bool* updated, mgenx_flow_report* rep) {
     if (n == 0) return;
     Init();
+    if (n == 1 && Worker()) {  // one record (the per-message call): the resident worker
+      uint32_t up = 0;
+      Check(mgenx_worker_flow_update(worker_, flows_, slot[0], seq[0], rx_sec[0], rx_usec[0],
+                                     msg_size[0], tx_sec[0], tx_usec[0], &up, &rep[0]),
+            "mgenx_worker_flow_update");
+      updated[0] = up != 0;
+      return;
+    }
     // one batch per run of distinct flows keeps "which record closed which window" exact:
     // a flow closes at most one window per record, and a chunk holds each flow once
     unsigned i0 = 0;
@@ -765,7 +795,15 @@ class Engine {
     }
   }
 
+  struct CrcCache {  // the receive checksum computed with the last single Unpack
+    bool valid = false;
+    const uint8_t* ptr = nullptr;
+    uint32_t len = 0, crc = 0;
+    std::vector<uint8_t> bytes;
+  };
+
   std::mutex mu_;
+  CrcCache crc_cache_;
   mgenx_ctx* ctx_ = nullptr;
   mgenx_worker* worker_ = nullptr;
   bool worker_off_ = false;

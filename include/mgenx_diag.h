@@ -47,6 +47,11 @@ int mgenx_diag_group_rw(mgenx_ctx* ctx, const uint8_t* dev_data, uint64_t bytes,
  * restart cycles, restarts); n == 16 flow_order_kernel (8 entries). */
 int mgenx_diag_seg_prof(unsigned long long* out, int n);
 
+/* Diagnostic: the resident worker's own time for its last Unpack / receive request, in 10-ns
+ * ticks from the poll that saw it: header parsed, checksum done, reply stored; out[3] = the
+ * request number they belong to. */
+int mgenx_diag_worker_stamps(const mgenx_worker* w, uint32_t* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -44,10 +44,11 @@ EXPORTED_SYMBOLS = (
     "mgenx_pcap_parse", "mgenx_binlog_index", "mgenx_convert_binary_log",
     "mgenx_unpack_last_kernel", "mgenx_pcap_snap", "mgenx_flow_reduce_rows",
     "mgenx_worker_create", "mgenx_worker_destroy", "mgenx_worker_unpack", "mgenx_worker_crc32",
-    "mgenx_worker_pack", "mgenx_worker_stop",
+    "mgenx_worker_pack", "mgenx_worker_stop", "mgenx_worker_info", "mgenx_worker_recv",
+    "mgenx_worker_flow_update",
 )
 DIAG_SYMBOLS = ("mgenx_set_tuning", "mgenx_diag_stream_read", "mgenx_diag_group_rw",
-                "mgenx_diag_seg_prof", "mgenx_diag_stream_read_w")
+                "mgenx_diag_seg_prof", "mgenx_diag_stream_read_w", "mgenx_diag_worker_stamps")
 
 
 class MgenxError(RuntimeError):
@@ -111,6 +112,7 @@ def load(diag: bool = False):
         L.mgenx_diag_group_rw.argtypes = [P, P, u64, P, i32, P]
         L.mgenx_diag_seg_prof.argtypes = [P, i32]
         L.mgenx_diag_stream_read_w.argtypes = [P, P, u64, P, i32, i32, P]
+        L.mgenx_diag_worker_stamps.argtypes = [P, P]
     L.mgenx_stream_scan.argtypes = [P, P, u64, i32, P, P, u64, ctypes.POINTER(ScanInfo), P]
     L.mgenx_tcp_rx_persist.argtypes = [P, P, P, P, u32, P, P, P, u32, P]
     L.mgenx_report_build.argtypes = [P, P, u32, u32, P, P, P, P, P, P, P]
@@ -134,6 +136,11 @@ def load(diag: bool = False):
     L.mgenx_worker_create.argtypes = [P, u32, ctypes.POINTER(P)]
     L.mgenx_worker_destroy.argtypes = [P]
     L.mgenx_worker_stop.argtypes = [P]
+    L.mgenx_worker_info.argtypes = [P, ctypes.POINTER(u32)]
+    L.mgenx_worker_recv.argtypes = [P, ctypes.c_char_p, u32, u32, P, ctypes.POINTER(u32),
+                                    ctypes.POINTER(u32)]
+    L.mgenx_worker_flow_update.argtypes = [P, P, u32, u32, u32, u32, u32, u32, u32,
+                                           ctypes.POINTER(u32), P]
     L.mgenx_worker_unpack.argtypes = [P, ctypes.c_char_p, u32, P]
     L.mgenx_worker_crc32.argtypes = [P, ctypes.c_char_p, u32, u32, ctypes.POINTER(u32)]
     L.mgenx_worker_pack.argtypes = [P, P, ctypes.c_char_p, P, u32, u32, u32, u32, P,
@@ -813,6 +820,33 @@ class Worker:
                                                          ctypes.c_void_p(out.ctypes.data)),
                         "mgenx_worker_unpack")
         return out[0]
+
+    def recv(self, msg: bytes, force: bool = False):
+        """The receive path's Unpack + ComputeCRC32(0, msg, len - 4) in one call
+        (mgenx_worker_recv): (mgenx_unpacked, crc state or None when no checksum was due)."""
+        out = np.zeros(1, UNPACKED_DTYPE)
+        crc, done = ctypes.c_uint32(0), ctypes.c_uint32(0)
+        self.eng._check(self.eng.lib.mgenx_worker_recv(self.w, bytes(msg), len(msg), int(force),
+                                                       ctypes.c_void_p(out.ctypes.data),
+                                                       ctypes.byref(crc), ctypes.byref(done)),
+                        "mgenx_worker_recv")
+        return out[0], (crc.value if done.value else None)
+
+    def flow_update(self, flows, slot, seq, rx_sec, rx_usec, msg_size, tx_sec, tx_usec):
+        """MgenAnalytic::Update of one record on device flow state flows[slot]
+        (mgenx_worker_flow_update): the closed window's report (FLOW_REPORT_DTYPE) or None."""
+        rep = np.zeros(1, FLOW_REPORT_DTYPE)
+        up = ctypes.c_uint32(0)
+        self.eng._check(self.eng.lib.mgenx_worker_flow_update(
+            self.w, _ptr(flows), slot, seq & 0xFFFFFFFF, rx_sec, rx_usec, msg_size, tx_sec,
+            tx_usec, ctypes.byref(up), ctypes.c_void_p(rep.ctypes.data)), "mgenx_worker_flow_update")
+        return rep[0] if up.value else None
+
+    def device_mailbox(self) -> bool:
+        """Whether requests go to device memory written through the BAR (mgenx_worker_info)."""
+        f = ctypes.c_uint32(0)
+        self.eng._check(self.eng.lib.mgenx_worker_info(self.w, ctypes.byref(f)), "mgenx_worker_info")
+        return bool(f.value & 1)
 
     def crc32(self, data: bytes, state: int = 0) -> int:
         out = ctypes.c_uint32(0)

@@ -5,6 +5,9 @@
 // synchronises or copies from host memory except mgenx_ctx_create and
 // mgenx_pack_prepare (table setup), so batch calls can be captured in a hipGraph.
 #include <hipcub/hipcub.hpp>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
+#include <immintrin.h>
 
 #include <math.h>
 #include <stdio.h>
@@ -14,6 +17,7 @@
 #include <chrono>
 #include <emmintrin.h>
 #include <atomic>
+#include <mutex>
 #include <vector>
 
 
@@ -951,8 +955,11 @@ int mgenx_flow_export(mgenx_ctx* ctx, const mgenx_flow_state* dev_flows, uint32_
 struct mgenx_worker {
   mgenx_ctx* ctx = nullptr;
   hipStream_t stream = nullptr;
-  mgenx::WMail* mail = nullptr;      // pinned host memory (mapped, coherent)
-  mgenx::WMail* mail_dev = nullptr;  // the device's view of it
+  mgenx::WReq* req = nullptr;       // the host's view of the request block (write only)
+  mgenx::WReq* req_dev = nullptr;   // the device's view of it
+  bool req_in_device = false;       // fine-grained device memory (else pinned host memory)
+  mgenx::WRep* rep = nullptr;       // pinned host memory (mapped, coherent)
+  mgenx::WRep* rep_dev = nullptr;
   uint32_t seq = 0;                  // the last request number issued
   uint64_t idle_ticks = 0;           // s_memrealtime ticks (100 MHz)
   bool launched = false;
@@ -976,14 +983,46 @@ static bool w_chunk(const uint32_t* p, uint32_t r, WChunk& c) {
   return c.w[3] == r;
 }
 
+// The request block in fine-grained device memory that the CPU agent may store into (through
+// the BAR): the request then reaches the wave as posted writes and the wave polls local memory,
+// instead of reading pinned host memory across PCIe on every poll and again for the message
+// (scripts/diag/bar_probe.hip).  Null when the runtime does not grant the CPU access.
+static hsa_status_t find_cpu_agent(hsa_agent_t a, void* out) {
+  hsa_device_type_t t;
+  if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) == HSA_STATUS_SUCCESS && t == HSA_DEVICE_TYPE_CPU) {
+    *static_cast<hsa_agent_t*>(out) = a;
+    return HSA_STATUS_INFO_BREAK;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+static void* device_mailbox(size_t bytes) {
+  if (const char* e = getenv("MGENX_WORKER_HOST_MAILBOX"))
+    if (atoi(e) != 0) return nullptr;
+  static hsa_agent_t cpu = {0};
+  static std::once_flag once;
+  std::call_once(once, [] { (void)hsa_iterate_agents(find_cpu_agent, &cpu); });
+  if (!cpu.handle) return nullptr;
+  void* p = nullptr;
+  if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained) != hipSuccess) return nullptr;
+  if (hsa_amd_agents_allow_access(1, &cpu, nullptr, p) != HSA_STATUS_SUCCESS) {
+    (void)hipFree(p);
+    return nullptr;
+  }
+  return p;
+}
+// host stores into the request block: a device-memory block is written through a
+// write-combining mapping, so the pieces are fenced (sfence) before the doorbell and after it
+static void w_fence() { _mm_sfence(); }
+static void w_copy(uint8_t* dst, const uint8_t* src, size_t n) { memcpy(dst, src, n); }
+
 // a worker wave serving requests after `start`: the previous one (if any) has ended -- it
 // clears `alive` as its last act -- so reap it and launch the next
 static int worker_launch(mgenx_worker* w, uint32_t start) {
   if (w->launched && hipStreamSynchronize(w->stream) != hipSuccess) return MGENX_EDEVICE;
-  w_store(&w->mail->alive, 1u);
-  hipError_t e = mgenx::launch_worker(w->mail_dev, w->ctx->d_tabs + 1024, w->ctx->d_bytetab,
-                                      w->ctx->d_xpow, w->ctx->d_rtab, start, w->idle_ticks,
-                                      w->stream);
+  w_store(&w->rep->alive, 1u);
+  hipError_t e = mgenx::launch_worker(w->req_dev, w->rep_dev, w->ctx->d_tabs + 1024,
+                                      w->ctx->d_bytetab, w->ctx->d_xpow, w->ctx->d_rtab, start,
+                                      w->idle_ticks, w->stream);
   if (e != hipSuccess) return set_err(w->ctx, e, "worker launch");
   w->launched = true;
   return MGENX_OK;
@@ -991,7 +1030,7 @@ static int worker_launch(mgenx_worker* w, uint32_t start) {
 
 // the request's polled pieces: `pd` (up to kPollData bytes, zero-filled) in pieces 1-15, then
 // piece 0, each with one 16-byte store
-static void w_post(mgenx::WMail* m, uint32_t r, uint32_t op, uint32_t len, uint32_t arg,
+static void w_post(mgenx::WReq* m, uint32_t r, uint32_t op, uint32_t len, uint32_t arg,
                    const uint8_t* pd, uint32_t pn) {
   alignas(16) uint8_t piece[16];
   for (uint32_t k = 1; k < mgenx::kPollPieces; k++) {
@@ -1003,18 +1042,21 @@ static void w_post(mgenx::WMail* m, uint32_t r, uint32_t op, uint32_t len, uint3
     _mm_store_si128(reinterpret_cast<__m128i*>(m->poll + 4u * k),
                     _mm_load_si128(reinterpret_cast<const __m128i*>(piece)));
   }
+  w_fence();
   std::atomic_thread_fence(std::memory_order_release);
   const uint32_t p0[4] = {r, op << mgenx::kWorkOpShift | len, arg, 0u};
   _mm_store_si128(reinterpret_cast<__m128i*>(m->poll), _mm_loadu_si128(reinterpret_cast<const __m128i*>(p0)));
+  w_fence();
   std::atomic_thread_fence(std::memory_order_seq_cst);
 }
 
-// post request `op` (bytes beyond the polled ones already in mail->data) and wait for the
-// reply: reply words 24 - 3 * nchunk .. 23 (the last nchunk chunks) into out
-static int worker_call(mgenx_worker* w, uint32_t op, uint32_t len, uint32_t arg, uint32_t nchunk,
-                       uint32_t* out, const uint8_t* pd = nullptr, uint32_t pn = 0) {
-  // (the caller holds w->mu: the mailbox's data area is written before this call)
-  if (!w->launched || !w_load(&w->mail->alive)) {
+// post request `op` (bytes beyond the polled ones already in req->data) and wait for the
+// reply: chunks first_chunk .. 7 + extra into out (3 words each); returns the status word
+static int worker_call(mgenx_worker* w, uint32_t op, uint32_t len, uint32_t arg,
+                       uint32_t first_chunk, uint32_t last_chunk, uint32_t* out,
+                       const uint8_t* pd = nullptr, uint32_t pn = 0, uint32_t* status = nullptr) {
+  // (the caller holds w->mu: the request's data area is written before this call)
+  if (!w->launched || !w_load(&w->rep->alive)) {
     hipSetDevice(w->ctx->device);
     const int rc = worker_launch(w, w->seq);
     if (rc != MGENX_OK) return rc;
@@ -1022,16 +1064,16 @@ static int worker_call(mgenx_worker* w, uint32_t op, uint32_t len, uint32_t arg,
   uint32_t r = w->seq + 1u;
   if (r == 0u) r = 1u;  // 0 is "no request yet"
   w->seq = r;
-  w_post(w->mail, r, op, len, arg, pd, pn);
-  // spin on the reply; a wave that ended on its idle timeout just as this request arrived
-  // is relaunched, and serves it first
+  w_post(w->req, r, op, len, arg, pd, pn);
+  // spin on the reply's chunk 7; a wave that ended on its idle timeout just as this request
+  // arrived is relaunched, and serves it first
   uint64_t spins = 0, relaunches = 0;
   std::chrono::steady_clock::time_point t0;
   WChunk c;
-  const uint32_t* rep = w->mail->reply;
+  const uint32_t* rep = w->rep->reply;
   while (!w_chunk(rep + 28, r, c)) {
     if ((++spins & 4095u) == 0u) {
-      if (!w_load(&w->mail->alive) && !w_chunk(rep + 28, r, c)) {
+      if (!w_load(&w->rep->alive) && !w_chunk(rep + 28, r, c)) {
         if (++relaunches > 3) return MGENX_EDEVICE;
         hipSetDevice(w->ctx->device);
         const int rc = worker_launch(w, r - 1u);
@@ -1047,15 +1089,16 @@ static int worker_call(mgenx_worker* w, uint32_t op, uint32_t len, uint32_t arg,
     __builtin_ia32_pause();
   }
   // the other chunks of the reply: written by the same store instruction, so at most a few
-  // spins behind the last
-  for (uint32_t k = 0; k < nchunk; k++) {
-    const uint32_t ch = 8u - nchunk + k;
+  // spins behind chunk 7
+  for (uint32_t ch = first_chunk; ch <= last_chunk; ch++) {
     WChunk d = c;
     if (ch != 7u)
       while (!w_chunk(rep + 4u * ch, r, d)) __builtin_ia32_pause();
-    for (int j = 0; j < 3; j++) out[3u * k + (uint32_t)j] = d.w[j];
+    for (int j = 0; j < 3; j++) out[3u * (ch - first_chunk) + (uint32_t)j] = d.w[j];
   }
-  return c.w[mgenx::kReplyStatus - 21] == 0u ? MGENX_OK : MGENX_EDEVICE;
+  const uint32_t st = c.w[mgenx::kReplyStatus - 21];
+  if (status) *status = st;
+  return (st & 0xFFu) == 0u ? MGENX_OK : MGENX_EDEVICE;
 }
 
 int mgenx_worker_create(mgenx_ctx* ctx, uint32_t idle_ms, mgenx_worker** out) {
@@ -1065,14 +1108,28 @@ int mgenx_worker_create(mgenx_ctx* ctx, uint32_t idle_ms, mgenx_worker** out) {
   mgenx_worker* w = new mgenx_worker();
   w->ctx = ctx;  // (not yet in ctx->workers: a failed create is freed by mgenx_worker_destroy)
   w->idle_ticks = (uint64_t)(idle_ms ? idle_ms : 1u) * 100000ull;
-  if (hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipHostMalloc((void**)&w->mail, sizeof(mgenx::WMail),
-                    hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
-      hipHostGetDevicePointer((void**)&w->mail_dev, w->mail, 0) != hipSuccess) {
+  bool ok = hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking) == hipSuccess &&
+            hipHostMalloc((void**)&w->rep, sizeof(mgenx::WRep),
+                          hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
+            hipHostGetDevicePointer((void**)&w->rep_dev, w->rep, 0) == hipSuccess;
+  if (ok) {
+    w->req = w->req_dev = static_cast<mgenx::WReq*>(device_mailbox(sizeof(mgenx::WReq)));
+    w->req_in_device = w->req != nullptr;
+    if (!w->req_in_device)
+      ok = hipHostMalloc((void**)&w->req, sizeof(mgenx::WReq),
+                         hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
+           hipHostGetDevicePointer((void**)&w->req_dev, w->req, 0) == hipSuccess;
+  }
+  if (!ok) {
     mgenx_worker_destroy(w);
     return MGENX_ENOMEM;
   }
-  memset(w->mail, 0, sizeof(mgenx::WMail));
+  memset(w->rep, 0, sizeof(mgenx::WRep));
+  alignas(16) const uint8_t zero[16] = {0};
+  for (uint32_t k = 0; k < mgenx::kPollPieces; k++)  // (16-byte stores, also to device memory)
+    _mm_store_si128(reinterpret_cast<__m128i*>(w->req->poll + 4u * k),
+                    _mm_load_si128(reinterpret_cast<const __m128i*>(zero)));
+  w_fence();
   ctx->workers.push_back(w);
   {
     std::lock_guard<std::mutex> g(g_workers_mu);
@@ -1086,13 +1143,13 @@ int mgenx_worker_create(mgenx_ctx* ctx, uint32_t idle_ms, mgenx_worker** out) {
 // device-wide synchronisation (hipFree, hipDeviceSynchronize) does not wait for its idle timeout
 static void worker_stop(mgenx_worker* w) {
   std::lock_guard<std::mutex> g(w->mu);
-  if (!w->launched || !w->mail || !w->ctx) return;
+  if (!w->launched || !w->rep || !w->ctx) return;
   hipSetDevice(w->ctx->device);
-  if (w_load(&w->mail->alive)) {  // ask the wave to end; it may end on its own meanwhile
+  if (w_load(&w->rep->alive)) {  // ask the wave to end; it may end on its own meanwhile
     uint32_t r = w->seq + 1u;
     if (r == 0u) r = 1u;
     w->seq = r;
-    w_post(w->mail, r, mgenx::kWorkStop, 0u, 0u, nullptr, 0u);
+    w_post(w->req, r, mgenx::kWorkStop, 0u, 0u, nullptr, 0u);
   }
   (void)hipStreamSynchronize(w->stream);
   w->launched = false;
@@ -1105,9 +1162,13 @@ static void worker_detach(mgenx_worker* w) {
     g_workers.erase(std::remove(g_workers.begin(), g_workers.end(), w), g_workers.end());
   }
   worker_stop(w);
-  mgenx::host_free(w->mail);  // (the other workers' waves are ended first)
+  // (the other workers' waves are ended first: the frees synchronise the device)
+  if (w->req_in_device) mgenx::dev_free(w->req);
+  else mgenx::host_free(w->req);
+  mgenx::host_free(w->rep);
   if (w->stream) (void)hipStreamDestroy(w->stream);
-  w->mail = w->mail_dev = nullptr;
+  w->req = w->req_dev = nullptr;
+  w->rep = w->rep_dev = nullptr;
   w->stream = nullptr;
   w->ctx = nullptr;
 }
@@ -1142,6 +1203,22 @@ int mgenx_worker_destroy(mgenx_worker* w) {
   return MGENX_OK;
 }
 
+int mgenx_worker_info(const mgenx_worker* w, uint32_t* flags) {
+  if (!w || !flags) return MGENX_EINVAL;
+  *flags = w->req_in_device ? MGENX_WORKER_DEVICE_MAILBOX : 0u;
+  return MGENX_OK;
+}
+
+#if MGENX_DIAG
+int mgenx_diag_worker_stamps(const mgenx_worker* w, uint32_t* out) {
+  if (!w || !w->rep || !out) return MGENX_EINVAL;
+  for (int k = 0; k < 4; k++) out[k] = w->rep->reply[32 + k];
+  return MGENX_OK;
+}
+#endif
+
+static void copy_unpacked(const uint32_t* words, mgenx_unpacked* out) { memcpy(out, words, sizeof(*out)); }
+
 int mgenx_worker_unpack(mgenx_worker* w, const uint8_t* msg, uint32_t len, mgenx_unpacked* out) {
   if (!w) return MGENX_EINVAL;
   std::lock_guard<std::mutex> g(w->mu);
@@ -1149,12 +1226,30 @@ int mgenx_worker_unpack(mgenx_worker* w, const uint8_t* msg, uint32_t len, mgenx
   const uint32_t n = len < mgenx::kWorkerHdrBytes ? len : mgenx::kWorkerHdrBytes;
   // Unpack reads the header bytes only: the first kPollData travel in the polled pieces, the
   // data area is for headers longer than that
-  if (n > mgenx::kPollData) memcpy(w->mail->data, msg, n);
+  if (n > mgenx::kPollData) w_copy(w->req->data, msg, n);
   uint32_t words[24];
-  const int rc = worker_call(w, mgenx::kWorkUnpack, len, 0u, 8u, words, msg,
+  const int rc = worker_call(w, mgenx::kWorkUnpack, len, 0u, 0u, 7u, words, msg,
                             n < mgenx::kPollData ? n : mgenx::kPollData);
-  if (rc == MGENX_OK) memcpy(out, words, sizeof(*out));
+  if (rc == MGENX_OK) copy_unpacked(words, out);
   return rc;
+}
+
+int mgenx_worker_recv(mgenx_worker* w, const uint8_t* msg, uint32_t len, uint32_t force,
+                      mgenx_unpacked* out, uint32_t* crc_state, uint32_t* crc_done) {
+  if (!w) return MGENX_EINVAL;
+  std::lock_guard<std::mutex> g(w->mu);
+  if (!w->ctx || !out || !crc_state || !crc_done || (len && !msg) || len > MGENX_WORKER_MAX_BYTES)
+    return MGENX_EINVAL;
+  // the whole message in the data area (the checksum reads it), its first bytes also polled
+  if (len) w_copy(w->req->data, msg, len);
+  uint32_t words[24], st = 0;
+  const int rc = worker_call(w, mgenx::kWorkRecv, len, force ? 1u : 0u, 0u, 7u, words, msg,
+                            len < mgenx::kPollData ? len : mgenx::kPollData, &st);
+  if (rc != MGENX_OK) return rc;
+  copy_unpacked(words, out);
+  *crc_done = (st & mgenx::kStatusCrc) ? 1u : 0u;
+  *crc_state = *crc_done ? words[mgenx::kReplyCrc] : 0u;
+  return MGENX_OK;
 }
 
 int mgenx_worker_pack(mgenx_worker* w, const mgenx_flow_tmpl* tmpl, const uint8_t* payload,
@@ -1178,15 +1273,15 @@ int mgenx_worker_pack(mgenx_worker* w, const mgenx_flow_tmpl* tmpl, const uint8_
   q.crc_in = crc_in;
   q.opts = opts & (MGENX_PACK_CHECKSUM | MGENX_PACK_RANDOM_FILL);
   q.rsv = 0;
-  if (tmpl->has_payload && tmpl->payload_len) memcpy(w->mail->data, payload, tmpl->payload_len);
+  if (tmpl->has_payload && tmpl->payload_len) w_copy(w->req->data, payload, tmpl->payload_len);
   uint32_t words[6];  // reply words 18-23
-  const int rc = worker_call(w, mgenx::kWorkPack, buf_len, 0u, 2u, words,
+  const int rc = worker_call(w, mgenx::kWorkPack, buf_len, 0u, 6u, 7u, words,
                             reinterpret_cast<const uint8_t*>(&q), (uint32_t)sizeof(q));
   if (rc != MGENX_OK) return rc;
   *ret = words[mgenx::kReplyRet - 18];
   *tx_crc = words[mgenx::kReplyTx - 18];
   *state = words[mgenx::kReplyState - 18];
-  if (*ret) memcpy(out, w->mail->out, *ret);
+  if (*ret) memcpy(out, w->rep->out, *ret);
   return MGENX_OK;
 }
 
@@ -1195,11 +1290,37 @@ int mgenx_worker_crc32(mgenx_worker* w, const uint8_t* data, uint32_t len, uint3
   if (!w) return MGENX_EINVAL;
   std::lock_guard<std::mutex> g(w->mu);
   if (!w->ctx || !state_out || (len && !data) || len > MGENX_WORKER_MAX_BYTES) return MGENX_EINVAL;
-  if (len) memcpy(w->mail->data, data, len);
+  if (len) w_copy(w->req->data, data, len);
   uint32_t words[3];  // reply words 21-23
-  const int rc = worker_call(w, mgenx::kWorkCrc32, len, state_in, 1u, words);
+  const int rc = worker_call(w, mgenx::kWorkCrc32, len, state_in, 7u, 7u, words);
   if (rc == MGENX_OK) *state_out = words[mgenx::kReplyCrc - 21];
   return rc;
+}
+
+int mgenx_worker_flow_update(mgenx_worker* w, mgenx_flow_state* dev_flows, uint32_t slot,
+                             uint32_t seq, uint32_t rx_sec, uint32_t rx_usec, uint32_t msg_size,
+                             uint32_t tx_sec, uint32_t tx_usec, uint32_t* updated,
+                             mgenx_flow_report* report) {
+  if (!w) return MGENX_EINVAL;
+  std::lock_guard<std::mutex> g(w->mu);
+  if (!w->ctx || !dev_flows || !updated || !report) return MGENX_EINVAL;
+  mgenx::WUpdReq q;
+  q.flows = (uint64_t)(uintptr_t)dev_flows;
+  q.slot = slot;
+  q.seq = seq;
+  q.rx_sec = rx_sec;
+  q.rx_usec = rx_usec;
+  q.tx_sec = tx_sec;
+  q.tx_usec = tx_usec;
+  q.msg = msg_size;
+  q.rsv = 0;
+  uint32_t words[27], st = 0;  // reply words 21-47
+  const int rc = worker_call(w, mgenx::kWorkUpdate, 0u, 0u, 7u, 15u, words,
+                            reinterpret_cast<const uint8_t*>(&q), (uint32_t)sizeof(q), &st);
+  if (rc != MGENX_OK) return rc;
+  *updated = (st & mgenx::kStatusClosed) ? 1u : 0u;
+  if (*updated) memcpy(report, words + (mgenx::kReplyReport - 21), sizeof(*report));
+  return MGENX_OK;
 }
 
 int mgenx_crc32_batch(mgenx_ctx* ctx, const uint8_t* dev_data, const uint64_t* dev_off,

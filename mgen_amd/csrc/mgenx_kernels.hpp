@@ -133,42 +133,56 @@ hipError_t launch_tcp_tail(uint8_t* out, const uint64_t* foff, const uint32_t* f
                            const uint32_t* state, uint32_t n, int ck, int rnd, uint32_t* acrc,
                            const uint32_t* byte_tab, const uint32_t* a4_tab, const uint32_t* xpow,
                            const uint32_t* ia, const uint32_t* rcrc, uint64_t cap, hipStream_t s);
-// the resident single-message worker (mgenx_worker.hip): its mailbox in pinned host memory
-constexpr uint32_t kWorkUnpack = 1, kWorkCrc32 = 2, kWorkPack = 3, kWorkStop = 15;
+// the resident single-message worker (mgenx_worker.hip): a request block the host writes (in
+// fine-grained device memory the host stores into through the BAR when the runtime grants the
+// CPU access to it, else in pinned host memory) and a reply block in pinned host memory
+constexpr uint32_t kWorkUnpack = 1, kWorkCrc32 = 2, kWorkPack = 3, kWorkRecv = 4, kWorkUpdate = 5,
+                   kWorkStop = 15;
 constexpr uint32_t kWorkerMaxBytes = MGENX_WORKER_MAX_BYTES;
 constexpr uint32_t kWorkerHdrBytes = 1024;  // Unpack reads at most the first 24+255+4+255+19 B
 constexpr uint32_t kWorkerPackMax = MGENX_WORKER_PACK_MAX;  // Pack's bufferLen (built in LDS)
-struct WPackReq {         // mgenx_pack_msgs' inputs for one message (payload in WMail::data)
+struct WPackReq {         // mgenx_pack_msgs' inputs for one message (payload in WReq::data)
   mgenx_flow_tmpl tmpl;   // words 0..16
   mgenx_pack_desc desc;   // words 17..21
   uint32_t buf_len, crc_in, opts, rsv;
 };
+struct WUpdReq {          // MgenAnalytic::Update of one record on a device flow state
+  uint64_t flows;         // mgenx_flow_state* (device)
+  uint32_t slot, seq, rx_sec, rx_usec, tx_sec, tx_usec, msg, rsv;
+};
 // The request: 16 pieces of 16 bytes that the worker reads whole on every poll, each written by
 // the host with one 16-byte store: piece 0 = {request number, op << 28 | len, arg, 0}, written
 // last; pieces 1-15 = {12 bytes of request data, request number}.  The data are the first
-// kPollData bytes of the message (Unpack: the header, in the common case all of it) or the
-// WPackReq (Pack), so the poll that sees a request brings its data too -- no second round trip
-// to host memory.  A piece whose tag is not the request number was read before the host wrote
-// it: the worker polls again.
-// The reply: 24 words in 8 TAGGED 16-byte chunks, chunk k = {w[3k], w[3k+1], w[3k+2], request
-// number}, each written by one 16-byte store, so the host reads a chunk whole and knows from its
-// tag that it is this request's -- no release fence (a wait for the stores' acknowledgement)
-// between the reply and the worker's next poll.  Words: the mgenx_unpacked (0-21), status (22),
-// crc (23); pack: ret (19), tx_crc (20), state (21), status (22).
+// kPollData bytes of the message (Unpack: the header, in the common case all of it), the
+// WPackReq (Pack) or the WUpdReq (Update), so the poll that sees a request brings its data too.
+// A piece whose tag is not the request number was read before the host wrote it: the worker
+// polls again.
+// The reply: up to 48 words in 16 TAGGED 16-byte chunks, chunk k = {w[3k], w[3k+1], w[3k+2],
+// request number}, each written by one 16-byte store, so the host reads a chunk whole and knows
+// from its tag that it is this request's -- no release fence (a wait for the stores'
+// acknowledgement) between the reply and the worker's next poll.  Chunk 7 ends every reply (the
+// host spins on it).  Words: the mgenx_unpacked (0-21), status (22: low byte 0 = ok; 0x100 the
+// receive CRC was computed, 0x200 a window closed), crc (23); pack: ret (19), tx_crc (20),
+// state (21); update: the mgenx_flow_report (24-47).
 constexpr uint32_t kWorkOpShift = 28, kWorkLenMask = (1u << kWorkOpShift) - 1u;
 constexpr uint32_t kPollPieces = 16, kPollData = 12u * (kPollPieces - 1u);  // 180 bytes
 constexpr uint32_t kReplyStatus = 22, kReplyCrc = 23, kReplyRet = 19, kReplyTx = 20, kReplyState = 21;
-struct alignas(64) WMail {
+constexpr uint32_t kReplyReport = 24, kReplyChunks = 16;
+constexpr uint32_t kStatusCrc = 0x100u, kStatusClosed = 0x200u;
+struct alignas(64) WReq {
   uint32_t poll[4 * kPollPieces];
+  uint8_t data[kWorkerMaxBytes + 64];  // the message (beyond the polled bytes); 64 bytes of slack
+};
+struct alignas(64) WRep {
   uint32_t resp;    // stop requests: the reply number
   uint32_t alive;   // 1 while a launched worker runs (it clears the word when it ends)
   uint32_t rsv1[14];
-  uint32_t reply[32];  // 8 tagged chunks
-  uint8_t data[kWorkerMaxBytes + 64];  // the message (beyond the polled bytes); 64 bytes of slack
-  uint8_t out[kWorkerPackMax + 64];    // a packed message
+  uint32_t reply[4 * kReplyChunks];  // tagged chunks
+  uint8_t out[kWorkerPackMax + 64];  // a packed message
 };
 static_assert(sizeof(WPackReq) <= kPollData, "Pack's request travels in the polled pieces");
-hipError_t launch_worker(WMail* m, const uint32_t* a4_tab, const uint32_t* byte_tab,
+static_assert(sizeof(WUpdReq) <= kPollData, "Update's request travels in the polled pieces");
+hipError_t launch_worker(const WReq* q, WRep* m, const uint32_t* a4_tab, const uint32_t* byte_tab,
                          const uint32_t* xpow, const uint8_t* rtab, uint32_t start,
                          uint64_t idle_ticks, hipStream_t stream);
 hipError_t launch_crc32(const uint8_t* data, const uint64_t* off, const uint32_t* len, uint32_t n,

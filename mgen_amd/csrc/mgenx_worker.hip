@@ -1,26 +1,35 @@
 // mgenx_worker.hip -- the resident single-message worker on gfx950.
 //
-// An unchanged MGEN build calls MgenMsg::Unpack once per datagram inside its RecvFrom loop and
-// MgenMsg::ComputeCRC32 once per message (src/common/mgenTransport.cpp:948-997, 1011-1063).
+// An unchanged MGEN build calls MgenMsg::Unpack once per datagram inside its RecvFrom loop,
+// MgenMsg::ComputeCRC32 once per checksummed message and MgenAnalytic::Update once per received
+// message (src/common/mgenTransport.cpp:948-997, 1011-1063; src/common/mgen.cpp:1027-1070).
 // Through the batch entry points each such call is a launch, two copies and a synchronisation.
-// Here ONE wave stays on the device and polls a mailbox in pinned host memory (WMail): the
-// caller writes the message and a request number, the wave reads the message once (every lane
-// a 16-byte part of it, all in flight together), decodes or checksums it, writes the reply and
-// then the reply number; the caller spins on that.  No launch and no copy per call.
+// Here ONE wave stays on the device and polls a request block the host writes (WReq: in device
+// memory the host stores into through the BAR when it may, else in pinned host memory): the
+// caller writes the message and a request number, the wave reads the message once (every lane a
+// 16-byte part of it, all in flight together), serves it, writes the reply to pinned host
+// memory (WRep) with tags; the caller spins on that.  No launch and no copy per call.
 //   unpack: MgenMsg::Unpack on a fresh MgenMsg (mgenMsg.cpp:315-500) -- parse_header, the
 //           general-layout path of the batch kernels, over an LDS copy of the header bytes;
+//   recv:   Unpack, then the receive path's checksum when forced or CHECKSUM is set
+//           (mgenTransport.cpp:958-965): ComputeCRC32(0, buf, len - 4) in the same reply;
 //   crc32:  MgenMsg::ComputeCRC32 (mgenMsg.cpp:524-541) -- the wave CRC of crc32_kernel
-//           (lane partials through the A_4 tables, combined by x^(8n) shifts) over LDS pieces.
+//           (lane partials through the A_4 tables, combined by x^(8n) shifts) over LDS pieces;
+//   pack:   MgenMsg::Pack alone, built in LDS;
+//   update: MgenAnalytic::Update (mgenAnalytic.cpp:74-258) of one record on a device flow state
+//           (FlowSM, the batch kernels' state machine), the report of a closed window back.
 // The wave always ends: on a stop request, and after `idle_ticks` of wall clock
 // (s_memrealtime, 100 MHz) without a request; the host relaunches it on the next call (the
-// request then pending is served first).  Every store to the mailbox is a vector store.
+// request then pending is served first).  Every store to host memory is a vector store.
 #include "mgenx_kernels.hpp"
 #include "mgenx_parse.hpp"
+#include "mgenx_flowsm.hpp"
 
 namespace mgenx {
 
 static_assert(sizeof(mgenx_unpacked) == 88, "mgenx_unpacked is 88 bytes (include/mgenx.h)");
-static_assert(sizeof(mgenx_unpacked) <= 128, "the mailbox's reply area");
+static_assert(sizeof(mgenx_unpacked) <= 88, "the reply's words 0-21");
+static_assert(sizeof(mgenx_flow_report) == 96, "the reply's words 24-47");
 
 __device__ __forceinline__ uint32_t ld_sys(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -41,7 +50,7 @@ __device__ __forceinline__ void st_chunk(uint32_t* p, u32x4_t v) {
 }
 // the polled pieces: lane k < 16 reads piece k (one 16-byte load; volatile: every poll reaches
 // host memory)
-__device__ __forceinline__ u32x4_t poll_pieces(const WMail* m, uint32_t lane) {
+__device__ __forceinline__ u32x4_t poll_pieces(const WReq* m, uint32_t lane) {
   u32x4_t v = {0u, 0u, 0u, 0u};
   if (lane < kPollPieces) v = *reinterpret_cast<const volatile u32x4_t*>(m->poll + 4u * lane);
   return v;
@@ -88,20 +97,44 @@ __device__ __forceinline__ uint32_t wave_crc_raw(const uint8_t* buf, uint32_t n,
 }
 
 __global__ void __launch_bounds__(64)
-worker_kernel(WMail* m, const uint32_t* __restrict__ a4_tab, const uint32_t* __restrict__ byte_tab,
-              const uint32_t* __restrict__ xpow, const uint8_t* __restrict__ rtab, uint32_t start,
-              uint64_t idle_ticks) {
+worker_kernel(const WReq* q, WRep* m, const uint32_t* __restrict__ a4_tab,
+              const uint32_t* __restrict__ byte_tab, const uint32_t* __restrict__ xpow,
+              const uint8_t* __restrict__ rtab, uint32_t start, uint64_t idle_ticks) {
   __shared__ uint32_t s_a4[1024], s_tab[256];
   __shared__ __attribute__((aligned(16))) uint8_t buf[kPiece];
-  __shared__ __attribute__((aligned(16))) uint32_t rq[32];
+  __shared__ __attribute__((aligned(16))) uint32_t rq[4 * kReplyChunks];
   const uint32_t lane = threadIdx.x;
   for (uint32_t e = lane; e < 1024u; e += 64u) s_a4[e] = a4_tab[e];
   for (uint32_t e = lane; e < 256u; e += 64u) s_tab[e] = byte_tab[e];
   __syncthreads();
   uint32_t last = start;
   uint64_t t_last = __builtin_amdgcn_s_memrealtime();
+  // MgenMsg::ComputeCRC32(st, data, cl) over the request's data area: the span in LDS pieces;
+  // each piece's raw CRC from lane partials, folded into the running state:
+  // crc(A || B) = x^(8|B|) crc(A) ^ crc(B)
+  auto span_crc = [&](uint32_t cl, uint32_t st) -> uint32_t {
+    uint32_t acc = 0;  // raw CRC (zero register) of the bytes so far
+    for (uint32_t p0 = 0; p0 < cl; p0 += kPiece) {
+      const uint32_t pn = min(kPiece, cl - p0);
+      u32x4_t v[kPiece / 1024];
+#pragma unroll
+      for (uint32_t k = 0; k < kPiece / 1024; k++) {  // every load issued before any store
+        const uint32_t o = p0 + 1024u * k + 16u * lane;
+        v[k] = load_masked(q->data + o, o, cl);
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < kPiece / 1024; k++)
+        *reinterpret_cast<u32x4_t*>(buf + 1024u * k + 16u * lane) = v[k];
+      __syncthreads();
+      const uint32_t c = wave_crc_raw(buf, pn, lane, s_a4, s_tab, xpow);
+      acc = (acc ? multmodp(xpow8(pn, xpow), acc) : 0u) ^ c;
+      __syncthreads();
+    }
+    const uint32_t init = st == 0u ? 0xFFFFFFFFu : st;  // ComputeCRC32: 0 restarts from ~0
+    return acc ^ (cl ? multmodp(xpow8(cl, xpow), init) : init);
+  };
   for (;;) {
-    const u32x4_t pc = poll_pieces(m, lane);
+    const u32x4_t pc = poll_pieces(q, lane);
     const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)pc.x, 0);
     if ((int32_t)(r - last) <= 0) {  // (numbers only grow: an older one is not new)
       if (__builtin_amdgcn_s_memrealtime() - t_last > idle_ticks) break;
@@ -110,6 +143,10 @@ worker_kernel(WMail* m, const uint32_t* __restrict__ a4_tab, const uint32_t* __r
     }
     // every data piece written for this request?  (else read before the host wrote it)
     if (__ballot(lane >= 1u && lane < kPollPieces && pc.w != r)) continue;
+#if MGENX_DIAG
+    const uint64_t ts0 = __builtin_amdgcn_s_memrealtime();  // (stamps: chunk 8, diagnostics)
+    uint64_t ts1 = ts0, ts2 = ts0;
+#endif
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the data area after the request
     const uint32_t ol = (uint32_t)__builtin_amdgcn_readlane((int)pc.y, 0);
     const uint32_t op = ol >> kWorkOpShift;
@@ -129,7 +166,7 @@ worker_kernel(WMail* m, const uint32_t* __restrict__ a4_tab, const uint32_t* __r
     }
     len = min(len, (uint32_t)kWorkerMaxBytes);
     uint32_t status = 0, crc = 0, pk_ret = 0, pk_tx = 0, pk_state = 0;
-    if (op == kWorkUnpack) {
+    if (op == kWorkUnpack || op == kWorkRecv) {
       // the header bytes (at most kWorkerHdrBytes) in LDS, zero past the message: the polled
       // bytes when the header lies within them (24 + dst_len + 4 + host_len + 16 <= 180, or
       // a shorter message), else all of them from the data area
@@ -143,7 +180,7 @@ worker_kernel(WMail* m, const uint32_t* __restrict__ a4_tab, const uint32_t* __r
           *reinterpret_cast<uint32_t*>(buf + o) = 0u;
       } else {
         for (uint32_t o = 16u * lane; o < kWorkerHdrBytes; o += 1024u)
-          *reinterpret_cast<u32x4_t*>(buf + o) = load_masked(m->data + o, o, n);
+          *reinterpret_cast<u32x4_t*>(buf + o) = load_masked(q->data + o, o, n);
       }
       __syncthreads();
       if (lane == 0) {
@@ -182,35 +219,86 @@ worker_kernel(WMail* m, const uint32_t* __restrict__ a4_tab, const uint32_t* __r
           reinterpret_cast<uint32_t*>(u.host_addr)[j] = h.host_addr[j];
         }
         *reinterpret_cast<mgenx_unpacked*>(rq) = u;  // staged in LDS for the lanes' stores
-        rq[kReplyStatus] = 0u;
+        static_assert(offsetof(mgenx_unpacked, host_addr) + 16 == 86, "2 bytes of tail padding");
+        rq[21] &= 0xFFFFu;  // the struct's tail padding (bytes 86-87) as zeros, not stale bits
+        // recv: the receive path checksums a decoded message when forced (arg bit 0) or its
+        // CHECKSUM flag is set (mgenTransport.cpp:958-965): ComputeCRC32(0, buf, len - 4)
+        const bool want = op == kWorkRecv && u.err == 0 && len >= 4u &&
+                          ((arg & 1u) || (u.flags & MGENX_FLAG_CHECKSUM));
+        rq[kReplyStatus] = want ? kStatusCrc : 0u;
         rq[kReplyCrc] = 0u;
       }
       __syncthreads();
+#if MGENX_DIAG
+      ts1 = __builtin_amdgcn_s_memrealtime();
+#endif
+      if (rq[kReplyStatus] & kStatusCrc) {  // (the whole message is in the data area)
+        const uint32_t c = span_crc(len - 4u, 0u);
+        if (lane == 0) rq[kReplyCrc] = c;
+        __syncthreads();
+      }
+#if MGENX_DIAG
+      ts2 = __builtin_amdgcn_s_memrealtime();
+      if (lane == 8u) {  // chunk 8: the wave's own time, 10-ns ticks from the request's poll
+        const uint64_t ts3 = __builtin_amdgcn_s_memrealtime();
+        st_chunk(m->reply + 32u, u32x4_t{(uint32_t)(ts1 - ts0), (uint32_t)(ts2 - ts0),
+                                         (uint32_t)(ts3 - ts0), r});
+      }
+#endif
       if (lane < 8u)  // the 8 tagged chunks in one instruction
         st_chunk(m->reply + 4u * lane, u32x4_t{rq[3u * lane], rq[3u * lane + 1u], rq[3u * lane + 2u], r});
       __syncthreads();
     } else if (op == kWorkCrc32) {
-      // the span in LDS pieces; each piece's raw CRC from lane partials, folded into the
-      // running state: crc(A || B) = x^(8|B|) crc(A) ^ crc(B)
-      uint32_t acc = 0;  // raw CRC (zero register) of the bytes so far
-      for (uint32_t p0 = 0; p0 < len; p0 += kPiece) {
-        const uint32_t pn = min(kPiece, len - p0);
-        u32x4_t v[kPiece / 1024];
-#pragma unroll
-        for (uint32_t k = 0; k < kPiece / 1024; k++) {  // every load issued before any store
-          const uint32_t o = p0 + 1024u * k + 16u * lane;
-          v[k] = load_masked(m->data + o, o, len);
+      crc = span_crc(len, arg);
+    } else if (op == kWorkUpdate) {
+      // MgenAnalytic::Update of one record on its device flow state (the request from the
+      // polled bytes, WUpdReq); the state is read after the acquire above and written back
+      // before the reply's release, so batch kernels before and after see it
+      const uint32_t* u = reinterpret_cast<const uint32_t*>(buf);
+      auto uw = [&](int k) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)u[k]); };
+      const uint64_t fp = (uint64_t)uw(0) | (uint64_t)uw(1) << 32;
+      const uint32_t slot = uw(2), seq = uw(3), rs = uw(4), ru = uw(5), ts = uw(6), tu = uw(7);
+      const uint32_t msg = uw(8);
+      __syncthreads();
+      mgenx_flow_state* sp = reinterpret_cast<mgenx_flow_state*>(fp) + slot;
+      FlowSM sm;
+      sm.load(sp, lane);
+      const double lsum0 = sp->latency_sum;
+      const uint64_t nrep0 = sm.nrep;
+      const double lat = tdelta(Tm{(int64_t)rs, (int64_t)ru}, Tm{(int64_t)ts, (int64_t)tu});
+      bool closed = false;
+      FlowClose cl;
+      const double lp = sm.exact(seq, (uint64_t)rs << 32 | ru, msg, lat, [&](const FlowClose& c) {
+        closed = true;
+        cl = c;
+      });
+      // latency_sum in record order: the window's sum before a close, the closing record's
+      // lat' after it (0.0 on a zero restart)
+      const double lsum1 = __dadd_rn(lsum0, lp);
+      sm.store(sp, lane);
+      if (lane == 0) {
+        sp->latency_sum = closed ? (cl.zr ? 0.0 : __dadd_rn(0.0, lp)) : lsum1;
+        if (closed) {
+          mgenx_flow_report rp;
+          rp.flow = slot;
+          rp.index = (uint32_t)nrep0;
+          rp.start_sec = cl.ws.sec;
+          rp.start_usec = cl.ws.usec;
+          rp.duration = cl.duration;
+          rp.msg_count = cl.r_count;
+          rp.rate = cl.r_rate;
+          rp.loss = cl.r_loss;
+          rp.latency_ave = cl.mc == 0 ? -1.0 : cl.mc == 1 ? lsum1 : __ddiv_rn(lsum1, (double)cl.mc);
+          rp.latency_min = cl.r_min;
+          rp.latency_max = cl.r_max;
+          rp.rx_sec = cl.rx.sec;
+          rp.rx_usec = cl.rx.usec;
+          *reinterpret_cast<mgenx_flow_report*>(rq + kReplyReport) = rp;
         }
-#pragma unroll
-        for (uint32_t k = 0; k < kPiece / 1024; k++)
-          *reinterpret_cast<u32x4_t*>(buf + 1024u * k + 16u * lane) = v[k];
-        __syncthreads();
-        const uint32_t c = wave_crc_raw(buf, pn, lane, s_a4, s_tab, xpow);
-        acc = (acc ? multmodp(xpow8(pn, xpow), acc) : 0u) ^ c;
-        __syncthreads();
       }
-      uint32_t st = arg == 0u ? 0xFFFFFFFFu : arg;  // ComputeCRC32: 0 restarts from ~0
-      crc = acc ^ (len ? multmodp(xpow8(len, xpow), st) : st);
+      status = closed ? kStatusClosed : 0u;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // the state written back before the reply
+      __syncthreads();
     } else if (op == kWorkPack) {
       // MgenMsg::Pack alone (mgenMsg.cpp:83-313) as the batch pack kernel's meta phase walks
       // it (mgenx_pack.hip: layout, truncation, the payload_len zeroing, RANDOM_FILL after two
@@ -276,7 +364,7 @@ worker_kernel(WMail* m, const uint32_t* __restrict__ a4_tab, const uint32_t* __r
         // 2. the payload [len, pend) from the mailbox
         if (pay)
           for (uint32_t o = 16u * lane; o < t_plen; o += 1024u) {
-            const u32x4_t v = load_masked(m->data + o, o, t_plen);
+            const u32x4_t v = load_masked(q->data + o, o, t_plen);
             const uint32_t w[4] = {v.x, v.y, v.z, v.w};
             const uint32_t nb = min(16u, t_plen - o);
             for (uint32_t j = 0; j < nb; j++) buf[len + o + j] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
@@ -345,20 +433,27 @@ worker_kernel(WMail* m, const uint32_t* __restrict__ a4_tab, const uint32_t* __r
     } else {
       status = 1;
     }
-    if (op != kWorkUnpack && lane < 2u)  // chunks 6 and 7: w18-20 = 0, ret, tx_crc; w21-23 = state, status, crc
+    if (op == kWorkUpdate) {  // chunks 7-15: w21-23 = 0, status, 0; w24-47 the report
+      if (lane < 9u)
+        st_chunk(m->reply + 4u * (7u + lane),
+                 lane == 0u ? u32x4_t{0u, status, 0u, r}
+                            : u32x4_t{rq[21u + 3u * lane], rq[22u + 3u * lane], rq[23u + 3u * lane], r});
+    } else if (op != kWorkUnpack && op != kWorkRecv && lane < 2u) {
+      // chunks 6 and 7: w18-20 = 0, ret, tx_crc; w21-23 = state, status, crc
       st_chunk(m->reply + 4u * (6u + lane), lane == 0u ? u32x4_t{0u, pk_ret, pk_tx, r}
                                                       : u32x4_t{pk_state, status, crc, r});
+    }
     last = r;
     t_last = __builtin_amdgcn_s_memrealtime();
   }
   if (lane == 0) st_sys_release(&m->alive, 0u);
 }
 
-hipError_t launch_worker(WMail* m, const uint32_t* a4_tab, const uint32_t* byte_tab,
+hipError_t launch_worker(const WReq* q, WRep* m, const uint32_t* a4_tab, const uint32_t* byte_tab,
                          const uint32_t* xpow, const uint8_t* rtab, uint32_t start,
                          uint64_t idle_ticks, hipStream_t stream) {
-  hipLaunchKernelGGL(worker_kernel, dim3(1), dim3(64), 0, stream, m, a4_tab, byte_tab, xpow, rtab,
-                     start, idle_ticks);
+  hipLaunchKernelGGL(worker_kernel, dim3(1), dim3(64), 0, stream, q, m, a4_tab, byte_tab, xpow,
+                     rtab, start, idle_ticks);
   return hipGetLastError();
 }
 

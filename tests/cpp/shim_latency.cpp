@@ -1,7 +1,9 @@
-// shim_latency.cpp -- per-call latency of the drop-in MgenMsg / MgenAnalytic shim: one
-// Pack, Unpack, ComputeCRC32 or Update is a synchronous batch of one (H2D, kernel, D2H), so
-// this measures what a transport that stays one-message-at-a-time pays per message, next
-// to the batch forms (the recvmmsg / sendmmsg handoff) at n = 256 and 4096 per call.
+// shim_latency.cpp -- per-call latency of the drop-in MgenMsg / MgenAnalytic shim: one Pack,
+// Unpack, ComputeCRC32 or Update goes to the resident worker wave (mgenx_worker_*), so this
+// measures what a transport that stays one-message-at-a-time pays per message: the UDP
+// receive path's Unpack + ComputeCRC32(0, buf, len - 4) pair (mgenTransport.cpp:958-975, the
+// checksum checked against the trailer here), MgenAnalytic::Update, Pack -- next to the batch
+// forms (the recvmmsg / sendmmsg handoff) at n = 256 and 4096 per call.
 // Prints one JSON object.  usage: shim_latency [iterations]
 #include <stdio.h>
 #include <stdlib.h>
@@ -51,7 +53,7 @@ int main(int argc, char** argv) {
     MgenMsg r;
     r.Unpack(buf, 1024, false, false);
   }
-  std::vector<double> pack, unpack, crc, update;
+  std::vector<double> pack, unpack, crc, recv, update;
   MgenAnalytic an;
   ProtoAddress s, d;
   s.SetRawHostAddress(ProtoAddress::IPv4, "\x0a\x00\x00\x02", 4);
@@ -75,13 +77,16 @@ int main(int argc, char** argv) {
     struct timeval rx = {1700000000, (suseconds_t)(i + 300)};
     an.Update(ProtoTime(rx), 1024, ProtoTime(r.GetTxTime()), r.GetSeqNum());
     auto t5 = Clock::now();
-    if (!ok || len != 1024) {
+    UINT32 trailer;
+    memcpy(&trailer, (const UINT8*)buf + len - 4u, 4);
+    if (!ok || len != 1024 || (c ^ MgenMsg::CRC32_XOROT) != ntohl(trailer)) {
       fprintf(stderr, "bad round trip at %d\n", i);
       return 1;
     }
     pack.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
     unpack.push_back(std::chrono::duration<double, std::micro>(t3 - t2).count());
     crc.push_back(std::chrono::duration<double, std::micro>(t4 - t3).count());
+    recv.push_back(std::chrono::duration<double, std::micro>(t4 - t2).count());
     update.push_back(std::chrono::duration<double, std::micro>(t5 - t4).count());
   }
   // batch forms: per-message cost at n messages per call
@@ -120,11 +125,22 @@ int main(int argc, char** argv) {
     batch_pack[k] = tp / n;
     batch_unpack[k] = tu / n;
   }
-  printf("{\"iterations\": %d, \"single_call_median_us\": {\"pack\": %.2f, \"unpack\": %.2f, "
-         "\"compute_crc32\": %.2f, \"analytic_update\": %.2f}, "
+  uint32_t wflags = 0;
+  {
+    mgenx_worker* w = nullptr;
+    if (mgenx_worker_create(mgenx::compat::Engine::Get().Ctx(), 10, &w) == MGENX_OK) {
+      mgenx_worker_info(w, &wflags);
+      mgenx_worker_destroy(w);
+    }
+  }
+  printf("{\"iterations\": %d, \"request_block\": \"%s\", "
+         "\"single_call_median_us\": {\"pack\": %.2f, \"unpack\": %.2f, "
+         "\"compute_crc32_after_unpack\": %.2f, \"recv_path_unpack_plus_crc\": %.2f, "
+         "\"analytic_update\": %.2f}, "
          "\"batch_per_msg_us\": {\"pack_256\": %.3f, \"unpack_256\": %.3f, \"pack_4096\": %.3f, "
          "\"unpack_4096\": %.3f}}\n",
-         iters, median_us(pack), median_us(unpack), median_us(crc), median_us(update),
+         iters, (wflags & MGENX_WORKER_DEVICE_MAILBOX) ? "device memory (BAR)" : "pinned host memory",
+         median_us(pack), median_us(unpack), median_us(crc), median_us(recv), median_us(update),
          batch_pack[0], batch_unpack[0], batch_pack[1], batch_unpack[1]);
   return 0;
 }

@@ -220,7 +220,8 @@ def test_worker_after_engine_close(torch):
 def test_batch_growth_after_worker_call(torch):
     """A batch call that grows a workspace (hipFree) right after a worker call: the library ends
     the resident wave first, so the call does not wait out the wave's idle timeout (5 s here),
-    and the next worker call relaunches it."""
+    and the next worker call relaunches it.  A device-wide synchronisation after
+    mgenx_worker_stop does not wait either."""
     from mgen_amd import Engine
     from mgen_amd.workloads import poisson_flows
     e = Engine(0)
@@ -237,9 +238,131 @@ def test_batch_growth_after_worker_call(torch):
             flows = e.flow_init(8, 1.0)
             e.flow_reduce(flows, 8, idx, t["seq"], t["tx_sec"], t["tx_usec"], t["msg_len"],
                           t["rx_sec"], t["rx_usec"], n=n)
-            torch.cuda.synchronize()
+            # (the stream alone: a device-wide synchronisation would wait for the live wave,
+            # as mgenx.h says -- mgenx_worker_stop first)
+            torch.cuda.current_stream().synchronize()
             assert time.perf_counter() - t0 < 2.0, n
         assert w.unpack(msg).tobytes() == u0.tobytes()
+        w.stop()
+        t0 = time.perf_counter()
+        torch.cuda.synchronize()
+        assert time.perf_counter() - t0 < 2.0
         w.close()
     finally:
         e.close()
+
+
+@pytest.mark.parametrize("force", [False, True])
+def test_worker_recv_vs_oracle(torch, eng, force):
+    """mgenx_worker_recv = the UDP receive path (mgenTransport.cpp:958-975): Unpack, then
+    ComputeCRC32(0, buf, len - 4) when forced or CHECKSUM is set, compared by the caller with the
+    big-endian trailer -- against the oracle's or_udp_recv on every golden unpack vector
+    (corrupted CRCs, every error class).  The checksum is returned exactly when the oracle
+    computes one, and equals zlib's."""
+    from oracle import oracle as O
+    g = dict(np.load(GOLD, allow_pickle=False))
+    slab, offs, lens = g["unpack_slab"], g["unpack_offs"], g["unpack_lens"]
+    w = eng.worker()
+    computed = 0
+    try:
+        for i, (o, L) in enumerate(zip(offs, lens)):
+            m = slab[int(o):int(o) + int(L)].tobytes()
+            u, crc = w.recv(m, force)
+            f = O.udp_recv(m, force)
+            ok = int(u["err"]) == 0
+            due = ok and (force or (int(u["flags"]) & 0x04) != 0)
+            assert (crc is not None) == due, i
+            err = int(u["err"])
+            if crc is not None:
+                computed += 1
+                assert crc == _crc_state(m[:-4], 0), i
+                if (crc ^ 0xFFFFFFFF) != int.from_bytes(m[-4:], "big"):
+                    err = 2  # ERROR_CHECKSUM, as the caller sets it (:970-974)
+            assert err == int(f["err"]), (i, err, int(f["err"]))
+            for k in ("flow_id", "seq_num", "msg_len", "flags", "hdr_len", "payload_len"):
+                assert int(u[k]) == int(f[k]), (i, k)
+    finally:
+        w.close()
+    assert computed > 100
+
+
+def test_worker_flow_update_vs_oracle(torch, eng):
+    """mgenx_worker_flow_update, one record per call, equals the oracle's Update over the same
+    records (or_flow_reduce_batch): final states (mask, FP64 latency sum / min / max) and every
+    report, on lossy, reordered, duplicated flows with mask restarts, sequence jumps and
+    zero-length messages; records alternate between the worker and batch calls of
+    mgenx_flow_reduce on the same state array."""
+    from mgen_amd import FLOW_STATE_DTYPE
+    from oracle import oracle as O
+    d = _jumpy_flows_small()
+    n_flows, window = 6, 0.05
+    n = len(d["seq"])
+    flows = eng.flow_init(n_flows, window)
+    w = eng.worker()
+    reps = [[] for _ in range(n_flows)]
+    try:
+        i = 0
+        while i < n:
+            if (i // 700) % 3 == 2:  # a stretch through the batch kernels
+                j = min(n, i + 700)
+                cols = {k: torch.from_numpy(np.ascontiguousarray(v[i:j])).cuda() for k, v in d.items()}
+                idx = torch.from_numpy((d["flow_id"][i:j] - 1).astype(np.uint32)).cuda()
+                per_flow = 64
+                rp = torch.zeros(n_flows * per_flow * 96, dtype=torch.uint8, device="cuda")
+                cnt = torch.zeros(n_flows, dtype=torch.int32, device="cuda")
+                eng.flow_reduce(flows, n_flows, idx, cols["seq"], cols["tx_sec"], cols["tx_usec"],
+                                cols["msg_len"], cols["rx_sec"], cols["rx_usec"], reports=rp,
+                                per_flow=per_flow, report_count=cnt)
+                torch.cuda.synchronize()
+                from mgen_amd import FLOW_REPORT_DTYPE
+                r = rp.cpu().numpy().view(FLOW_REPORT_DTYPE).reshape(n_flows, per_flow)
+                c = cnt.cpu().numpy()
+                for f in range(n_flows):
+                    assert c[f] <= per_flow
+                    reps[f].extend(r[f, :c[f]])
+                i = j
+                continue
+            f = int(d["flow_id"][i]) - 1
+            rep = w.flow_update(flows, f, int(d["seq"][i]), int(d["rx_sec"][i]),
+                                int(d["rx_usec"][i]), int(d["msg_len"][i]), int(d["tx_sec"][i]),
+                                int(d["tx_usec"][i]))
+            if rep is not None:
+                reps[f].append(rep)
+            i += 1
+        torch.cuda.synchronize()
+    finally:
+        w.close()
+    st = flows.cpu().numpy().view(FLOW_STATE_DTYPE)
+    of, orep, ocnt = O.flow_reduce_batch(n_flows, d["flow_id"] - 1, d["seq"], d["tx_sec"],
+                                         d["tx_usec"], d["msg_len"], d["rx_sec"], d["rx_usec"],
+                                         window=window, per_flow=4096)
+    assert int(ocnt.sum()) > 20
+    for f, a in enumerate(of):
+        s = st[f]
+        assert s["msg_count"] == a.msg_count and s["byte_count"] == a.byte_count, f
+        assert s["dup_count"] == a.dup_msg_count and s["n_reports"] == a.n_reports, f
+        assert s["seq_start"] == a.seq_start, f
+        assert s["latency_sum"] == a.latency_sum, (f, s["latency_sum"], a.latency_sum)
+        assert s["latency_min"] == a.latency_min and s["latency_max"] == a.latency_max, f
+        assert s["mask_n"] == a.nset, f
+        if a.nset:
+            assert s["mask_first"] == a.first, f
+            assert s["mask"].tobytes() == bytes(a.bits), f
+        assert len(reps[f]) == int(ocnt[f]), f
+        for k, r in enumerate(reps[f]):
+            o = orep[f, k]
+            for name in ("start_sec", "start_usec", "duration", "msg_count", "rate", "loss",
+                         "latency_ave", "latency_min", "latency_max", "rx_sec", "rx_usec"):
+                assert r[name] == o[name], (f, k, name, r[name], o[name])
+
+
+def _jumpy_flows_small():
+    """~4000 receive-order records over 6 flows: losses, duplicates, reordering, sequence jumps
+    past the mask span and near 2^31, zero-length messages (tests/test_gpu_analytics.py's
+    _jumpy_flows, smaller)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "gpu_analytics_helpers", os.path.join(ROOT, "tests", "test_gpu_analytics.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod._jumpy_flows(6, 700, seed=21)
