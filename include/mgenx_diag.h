@@ -49,7 +49,8 @@ int mgenx_diag_seg_prof(unsigned long long* out, int n);
 
 /* Diagnostic: the resident worker's own time for its last Unpack / receive request, in 10-ns
  * ticks from the poll that saw it: header parsed, checksum done, reply stored; out[3] = the
- * request number they belong to. */
+ * request number they belong to; out[4], out[5] = shader clocks (s_memtime) to the parse and
+ * to the reply (out[7] = the request number); out holds 8 words. */
 int mgenx_diag_worker_stamps(const mgenx_worker* w, uint32_t* out);
 
 #ifdef __cplusplus

@@ -144,7 +144,7 @@ struct mgenx_grow {
 struct mgenx_ctx {
   int device = 0;
   int cu_count = 0;
-  uint32_t* d_tabs = nullptr;     // [A64 | A4 | A8 | A12 | A16 | A32 | A48] 7 x 1024
+  uint32_t* d_tabs = nullptr;     // [A64 | A4 | A8 | A12 | A16 | A32 | A48 | A128 | A256 | A512 | A1024]
   uint32_t* d_expect = nullptr;   // [65536]
   std::vector<uint32_t> h_expect;  // host copy of the expect table
   uint32_t* d_xpow = nullptr;     // [65536]
@@ -292,10 +292,11 @@ int mgenx_ctx_create(int device, mgenx_ctx** out) {
 
   uint32_t t[256];
   byte_table(t);
-  // unpack operator tables: [A64 | A4 | A8 | A12 | A16 | A32 | A48]
-  std::vector<uint32_t> tabs(7 * 1024), xpow(kN), ia(kN), expect(kN, 0);
-  const uint32_t ops[7] = {64, 4, 8, 12, 16, 32, 48};
-  for (int i = 0; i < 7; i++) op_table(t, ops[i], &tabs[1024 * i]);
+  // operator tables: [A64 | A4 | A8 | A12 | A16 | A32 | A48] (unpack), [A128 | A256 | A512 |
+  // A1024] (the worker's shifts by any distance, mgenx::kTabA128..)
+  std::vector<uint32_t> tabs(11 * 1024), xpow(kN), ia(kN), expect(kN, 0);
+  const uint32_t ops[11] = {64, 4, 8, 12, 16, 32, 48, 128, 256, 512, 1024};
+  for (int i = 0; i < 11; i++) op_table(t, ops[i], &tabs[1024 * i]);
   xpow[0] = 0x80000000u;  // x^0
   for (uint32_t n = 1; n < kN; n++) xpow[n] = mgenx::multmodp(xpow[n - 1], 0x00800000u);
   for (uint32_t n = 0; n < kN; n++) ia[n] = mgenx::multmodp(xpow[n], 0xFFFFFFFFu);
@@ -1020,9 +1021,9 @@ static void w_copy(uint8_t* dst, const uint8_t* src, size_t n) { memcpy(dst, src
 static int worker_launch(mgenx_worker* w, uint32_t start) {
   if (w->launched && hipStreamSynchronize(w->stream) != hipSuccess) return MGENX_EDEVICE;
   w_store(&w->rep->alive, 1u);
-  hipError_t e = mgenx::launch_worker(w->req_dev, w->rep_dev, w->ctx->d_tabs + 1024,
-                                      w->ctx->d_bytetab, w->ctx->d_xpow, w->ctx->d_rtab, start,
-                                      w->idle_ticks, w->stream);
+  hipError_t e = mgenx::launch_worker(w->req_dev, w->rep_dev, w->ctx->d_tabs,
+                                      w->ctx->d_bytetab, w->ctx->d_rtab, start, w->idle_ticks,
+                                      w->stream);
   if (e != hipSuccess) return set_err(w->ctx, e, "worker launch");
   w->launched = true;
   return MGENX_OK;
@@ -1212,7 +1213,7 @@ int mgenx_worker_info(const mgenx_worker* w, uint32_t* flags) {
 #if MGENX_DIAG
 int mgenx_diag_worker_stamps(const mgenx_worker* w, uint32_t* out) {
   if (!w || !w->rep || !out) return MGENX_EINVAL;
-  for (int k = 0; k < 4; k++) out[k] = w->rep->reply[32 + k];
+  for (int k = 0; k < 8; k++) out[k] = w->rep->reply[32 + k];
   return MGENX_OK;
 }
 #endif

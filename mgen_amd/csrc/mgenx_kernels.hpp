@@ -182,9 +182,13 @@ struct alignas(64) WRep {
 };
 static_assert(sizeof(WPackReq) <= kPollData, "Pack's request travels in the polled pieces");
 static_assert(sizeof(WUpdReq) <= kPollData, "Update's request travels in the polled pieces");
-hipError_t launch_worker(const WReq* q, WRep* m, const uint32_t* a4_tab, const uint32_t* byte_tab,
-                         const uint32_t* xpow, const uint8_t* rtab, uint32_t start,
-                         uint64_t idle_ticks, hipStream_t stream);
+// the context's operator tables (mgenx_api.hip: A_n(s) = the state after n zero bytes, as 4 x 256
+// byte-indexed entries): [A64 | A4 | A8 | A12 | A16 | A32 | A48 | A128 | A256 | A512 | A1024]
+constexpr uint32_t kTabA64 = 0, kTabA4 = 1, kTabA8 = 2, kTabA16 = 4, kTabA32 = 5, kTabA128 = 7,
+                   kTabA256 = 8, kTabA512 = 9, kTabA1024 = 10, kTabCount = 11;
+hipError_t launch_worker(const WReq* q, WRep* m, const uint32_t* tabs, const uint32_t* byte_tab,
+                         const uint8_t* rtab, uint32_t start, uint64_t idle_ticks,
+                         hipStream_t stream);
 hipError_t launch_crc32(const uint8_t* data, const uint64_t* off, const uint32_t* len, uint32_t n,
                         const uint32_t* byte_tab, const uint32_t* a4_tab, const uint32_t* xpow,
                         const uint32_t* state_in, uint32_t* out, hipStream_t stream);

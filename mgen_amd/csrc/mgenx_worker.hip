@@ -56,11 +56,13 @@ __device__ __forceinline__ u32x4_t poll_pieces(const WReq* m, uint32_t lane) {
   return v;
 }
 
-// the 16 mailbox bytes at p (message offset o), bytes at or past n as zero; the mailbox has
-// 64 bytes of slack past its largest message, so the whole 16 are always readable
+// the 16 request-block bytes at p (message offset o), bytes at or past n as zero; the block has
+// 64 bytes of slack past its largest message, so the whole 16 are always readable.  Volatile:
+// the host wrote them (through the BAR, or to host memory) since any earlier read -- no cache
+// may answer (sc0 sc1), so no acquire fence is needed
 __device__ __forceinline__ u32x4_t load_masked(const uint8_t* p, uint32_t o, uint32_t n) {
   if (o >= n) return u32x4_t{0u, 0u, 0u, 0u};
-  u32x4_t v = *reinterpret_cast<const u32x4_t*>(p);
+  u32x4_t v = *reinterpret_cast<const volatile u32x4_t*>(p);
   if (o + 16u > n) {
     const int k = (int)(n - o);  // 1..15 valid bytes
     v.x &= byte_range_mask(0, k < 4 ? k : 4);
@@ -71,67 +73,119 @@ __device__ __forceinline__ u32x4_t load_masked(const uint8_t* p, uint32_t o, uin
   return v;
 }
 
+// One wave: LDS accesses before it are complete after it; global loads stay in flight (a
+// __syncthreads would also wait for them -- the message's prefetch below)
+__device__ __forceinline__ void lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 static_assert(kWorkerPackMax <= kPiece, "a packed message is built in one LDS piece");
 static_assert(sizeof(WPackReq) == 104, "WPackReq: template, descriptor and four words");
 
-// The wave's raw CRC (zero register) of LDS bytes [0, n): lane partials through the A_4
-// tables, shifted by the bytes after them and XOR-ed (crc(A || B) = x^(8|B|) crc(A) ^ crc(B)).
-__device__ __forceinline__ uint32_t wave_crc_raw(const uint8_t* buf, uint32_t n, uint32_t lane,
-                                                 const uint32_t* s_a4, const uint32_t* s_tab,
-                                                 const uint32_t* xpow) {
-  const uint32_t chunk = (((n + 63u) >> 6) + 3u) & ~3u;
-  const uint32_t lo = min(lane * chunk, n), hi = min(lo + chunk, n);
-  uint32_t c = 0;
-  uint32_t k = lo;
-  for (; k + 4u <= hi; k += 4u) {
-    const uint32_t x = c ^ *reinterpret_cast<const uint32_t*>(buf + k);
-    c = s_a4[x & 0xffu] ^ s_a4[256 + ((x >> 8) & 0xffu)] ^ s_a4[512 + ((x >> 16) & 0xffu)] ^
-        s_a4[768 + (x >> 24)];
+// The shift operators in LDS: s_op[b] = A_(2^b) for b = 2..10 (4 x 256 entries each), the byte
+// table for single zero bytes.  shift(x, D) = the CRC state x after D zero bytes, D < 2048.
+struct WOps {
+  const uint32_t* op;   // [9][1024]: A_4, A_8, ..., A_1024
+  const uint32_t* tab;  // [256]
+  __device__ uint32_t apply(uint32_t b, uint32_t x) const {
+    const uint32_t* t = op + (b - 2u) * 1024u;
+    return t[x & 0xffu] ^ t[256 + ((x >> 8) & 0xffu)] ^ t[512 + ((x >> 16) & 0xffu)] ^ t[768 + (x >> 24)];
   }
-  for (; k < hi; k++) c = s_tab[(c ^ buf[k]) & 0xffu] ^ (c >> 8);
-  const uint32_t after = n - hi;
-  if (c && after) c = multmodp(xpow8(after, xpow), c);
+  __device__ uint32_t byte(uint32_t c, uint32_t v) const { return tab[(c ^ v) & 0xffu] ^ (c >> 8); }
+  __device__ uint32_t shift(uint32_t x, uint32_t D) const {
+#pragma unroll
+    for (uint32_t b = 2; b <= 10; b++)
+      if ((D >> b) & 1u) x = apply(b, x);
+    for (uint32_t k = 0; k < (D & 3u); k++) x = tab[x & 0xffu] ^ (x >> 8);
+    return x;
+  }
+};
+
+// MgenMsg::ComputeCRC32(st, M, n) (mgenMsg.cpp:524-541: st == 0 restarts from ~0; no final xor)
+// on one wave, table lookups only.  Lane l takes the 16-byte blocks at 16 l + 1024 k; a block's
+// raw CRC (zero register) goes through its lane's Horner chain h = A_1024(h) ^ raw(block), and
+// the chain is shifted once by the distance from its last block's end to the message end; the
+// message's one partial block (its last bytes) by byte steps.  The start state enters as a
+// XOR into bytes 0..3 (the register processing M from st = the zero register processing M with
+// LE(st) XOR-ed into its first four bytes).  load16(o) = the 16 message bytes at offset o (any
+// bytes past n; o < n).
+// pre0 (optional): this lane's block of the first 1 KiB, loaded earlier (the request's data
+// prefetched while the header is parsed)
+template <typename Load16>
+__device__ __forceinline__ uint32_t wave_crc(uint32_t n, uint32_t st_in, uint32_t lane,
+                                             const WOps& ops, Load16 load16,
+                                             const u32x4_t* pre0 = nullptr) {
+  const uint32_t st = st_in == 0u ? 0xFFFFFFFFu : st_in;
+  auto word_bytes = [&](uint32_t c, uint32_t w, uint32_t nb) {
+    for (uint32_t j = 0; j < nb; j++) c = ops.byte(c, w >> (8 * j));
+    return c;
+  };
+  if (n < 16u) {  // one short block: byte steps from st on every lane (same result)
+    const u32x4_t v = n ? (pre0 ? u32x4_t{(uint32_t)__builtin_amdgcn_readfirstlane((int)pre0->x),
+                                          (uint32_t)__builtin_amdgcn_readfirstlane((int)pre0->y),
+                                          (uint32_t)__builtin_amdgcn_readfirstlane((int)pre0->z),
+                                          (uint32_t)__builtin_amdgcn_readfirstlane((int)pre0->w)}
+                                : load16(0u))
+                        : u32x4_t{0u, 0u, 0u, 0u};
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t c = st;
+    for (uint32_t j = 0; j < n; j++) c = ops.byte(c, w[j >> 2] >> (8 * (j & 3)));
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
+  }
+  const uint32_t P = (n + 1023u) >> 10;
+  uint32_t h = 0, part = 0, last_end = 0;
+  for (uint32_t k = 0; k < P; k++) {
+    const uint32_t o = 1024u * k + 16u * lane;
+    const uint32_t v = n > o ? min(16u, n - o) : 0u;
+    if (v) {
+      u32x4_t x = (k == 0u && pre0) ? *pre0 : load16(o);
+      if (o == 0u) x.x ^= st;  // (n >= 16: lane 0's first block is whole)
+      if (v == 16u) {
+        uint32_t c = ops.apply(2u, x.x);
+        c = ops.apply(2u, c ^ x.y);
+        c = ops.apply(2u, c ^ x.z);
+        c = ops.apply(2u, c ^ x.w);
+        h = (k ? ops.apply(10u, h) : 0u) ^ c;
+        last_end = o + 16u;
+      } else {  // the message's last bytes
+        const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+        uint32_t c = 0;
+        for (uint32_t q = 0; q < 4; q++) c = word_bytes(c, w[q], v > 4u * q ? min(4u, v - 4u * q) : 0u);
+        part = c;
+      }
+    }
+  }
+  uint32_t c = (last_end ? ops.shift(h, n - last_end) : 0u) ^ part;
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) c ^= (uint32_t)__shfl_xor((int)c, o);
-  return c;
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
 }
 
 __global__ void __launch_bounds__(64)
-worker_kernel(const WReq* q, WRep* m, const uint32_t* __restrict__ a4_tab,
-              const uint32_t* __restrict__ byte_tab, const uint32_t* __restrict__ xpow,
-              const uint8_t* __restrict__ rtab, uint32_t start, uint64_t idle_ticks) {
-  __shared__ uint32_t s_a4[1024], s_tab[256];
+worker_kernel(const WReq* q, WRep* m, const uint32_t* __restrict__ tabs,
+              const uint32_t* __restrict__ byte_tab, const uint8_t* __restrict__ rtab,
+              uint32_t start, uint64_t idle_ticks) {
+  __shared__ uint32_t s_op[9 * 1024], s_tab[256];
   __shared__ __attribute__((aligned(16))) uint8_t buf[kPiece];
   __shared__ __attribute__((aligned(16))) uint32_t rq[4 * kReplyChunks];
   const uint32_t lane = threadIdx.x;
-  for (uint32_t e = lane; e < 1024u; e += 64u) s_a4[e] = a4_tab[e];
+  {  // A_(2^b), b = 2..10, from the context's tables
+    const uint32_t src[9] = {kTabA4, kTabA8, kTabA16, kTabA32, kTabA64, kTabA128, kTabA256,
+                             kTabA512, kTabA1024};
+    for (uint32_t t = 0; t < 9; t++)
+      for (uint32_t e = lane; e < 1024u; e += 64u) s_op[t * 1024u + e] = tabs[src[t] * 1024u + e];
+  }
   for (uint32_t e = lane; e < 256u; e += 64u) s_tab[e] = byte_tab[e];
-  __syncthreads();
+  lds_sync();
+  const WOps ops = {s_op, s_tab};
   uint32_t last = start;
   uint64_t t_last = __builtin_amdgcn_s_memrealtime();
-  // MgenMsg::ComputeCRC32(st, data, cl) over the request's data area: the span in LDS pieces;
-  // each piece's raw CRC from lane partials, folded into the running state:
-  // crc(A || B) = x^(8|B|) crc(A) ^ crc(B)
-  auto span_crc = [&](uint32_t cl, uint32_t st) -> uint32_t {
-    uint32_t acc = 0;  // raw CRC (zero register) of the bytes so far
-    for (uint32_t p0 = 0; p0 < cl; p0 += kPiece) {
-      const uint32_t pn = min(kPiece, cl - p0);
-      u32x4_t v[kPiece / 1024];
-#pragma unroll
-      for (uint32_t k = 0; k < kPiece / 1024; k++) {  // every load issued before any store
-        const uint32_t o = p0 + 1024u * k + 16u * lane;
-        v[k] = load_masked(q->data + o, o, cl);
-      }
-#pragma unroll
-      for (uint32_t k = 0; k < kPiece / 1024; k++)
-        *reinterpret_cast<u32x4_t*>(buf + 1024u * k + 16u * lane) = v[k];
-      __syncthreads();
-      const uint32_t c = wave_crc_raw(buf, pn, lane, s_a4, s_tab, xpow);
-      acc = (acc ? multmodp(xpow8(pn, xpow), acc) : 0u) ^ c;
-      __syncthreads();
-    }
-    const uint32_t init = st == 0u ? 0xFFFFFFFFu : st;  // ComputeCRC32: 0 restarts from ~0
-    return acc ^ (cl ? multmodp(xpow8(cl, xpow), init) : init);
+  // MgenMsg::ComputeCRC32(st, data, cl) over the request's data area
+  auto span_crc = [&](uint32_t cl, uint32_t st, const u32x4_t* pre0) -> uint32_t {
+    return wave_crc(cl, st, lane, ops, [&](uint32_t o) { return load_masked(q->data + o, o, cl); },
+                    pre0);
   };
   for (;;) {
     const u32x4_t pc = poll_pieces(q, lane);
@@ -145,13 +199,17 @@ worker_kernel(const WReq* q, WRep* m, const uint32_t* __restrict__ a4_tab,
     if (__ballot(lane >= 1u && lane < kPollPieces && pc.w != r)) continue;
 #if MGENX_DIAG
     const uint64_t ts0 = __builtin_amdgcn_s_memrealtime();  // (stamps: chunk 8, diagnostics)
-    uint64_t ts1 = ts0, ts2 = ts0;
+    const uint64_t tc0 = __builtin_amdgcn_s_memtime();        // (shader clocks: chunk 9)
+    uint64_t ts1 = ts0, ts2 = ts0, tc1 = tc0;
 #endif
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the data area after the request
     const uint32_t ol = (uint32_t)__builtin_amdgcn_readlane((int)pc.y, 0);
     const uint32_t op = ol >> kWorkOpShift;
     uint32_t len = ol & kWorkLenMask;
     const uint32_t arg = (uint32_t)__builtin_amdgcn_readlane((int)pc.z, 0);
+    // the checksummed span's first KiB, in flight while the header is parsed (receive: the
+    // message less its trailer; crc32: all of it)
+    const uint32_t span = op == kWorkRecv ? (len >= 4u ? len - 4u : 0u) : op == kWorkCrc32 ? len : 0u;
+    const u32x4_t pre = load_masked(q->data + 16u * lane, 16u * lane, min(span, 1024u));
     // the polled data bytes into LDS: piece k's 12 bytes at 12 (k - 1)
     if (lane >= 1u && lane < kPollPieces) {
       uint32_t* d = reinterpret_cast<uint32_t*>(buf + 12u * (lane - 1u));
@@ -159,7 +217,7 @@ worker_kernel(const WReq* q, WRep* m, const uint32_t* __restrict__ a4_tab,
       d[1] = pc.y;
       d[2] = pc.z;
     }
-    __syncthreads();
+    lds_sync();
     if (op == kWorkStop) {
       if (lane == 0) st_sys_release(&m->resp, r);
       break;
@@ -174,7 +232,7 @@ worker_kernel(const WReq* q, WRep* m, const uint32_t* __restrict__ a4_tab,
       uint32_t need = 24u + buf[23];
       if (need + 4u <= min(n, kPollData)) need += 4u + buf[need + 3u] + 16u;
       else need += 4u;
-      __syncthreads();  // (every lane has read the length bytes)
+      lds_sync();  // (every lane has read the length bytes)
       if (min(n, need) <= kPollData) {  // (the host zero-filled the polled bytes past the message)
         for (uint32_t o = kPollData + 4u * lane; o < kWorkerHdrBytes; o += 256u)
           *reinterpret_cast<uint32_t*>(buf + o) = 0u;
@@ -182,7 +240,7 @@ worker_kernel(const WReq* q, WRep* m, const uint32_t* __restrict__ a4_tab,
         for (uint32_t o = 16u * lane; o < kWorkerHdrBytes; o += 1024u)
           *reinterpret_cast<u32x4_t*>(buf + o) = load_masked(q->data + o, o, n);
       }
-      __syncthreads();
+      lds_sync();
       if (lane == 0) {
         uint32_t w[8];
         load_fixed(buf, len, w);
@@ -228,14 +286,15 @@ worker_kernel(const WReq* q, WRep* m, const uint32_t* __restrict__ a4_tab,
         rq[kReplyStatus] = want ? kStatusCrc : 0u;
         rq[kReplyCrc] = 0u;
       }
-      __syncthreads();
+      lds_sync();
 #if MGENX_DIAG
       ts1 = __builtin_amdgcn_s_memrealtime();
+      tc1 = __builtin_amdgcn_s_memtime();
 #endif
       if (rq[kReplyStatus] & kStatusCrc) {  // (the whole message is in the data area)
-        const uint32_t c = span_crc(len - 4u, 0u);
+        const uint32_t c = span_crc(len - 4u, 0u, &pre);
         if (lane == 0) rq[kReplyCrc] = c;
-        __syncthreads();
+        lds_sync();
       }
 #if MGENX_DIAG
       ts2 = __builtin_amdgcn_s_memrealtime();
@@ -244,22 +303,27 @@ worker_kernel(const WReq* q, WRep* m, const uint32_t* __restrict__ a4_tab,
         st_chunk(m->reply + 32u, u32x4_t{(uint32_t)(ts1 - ts0), (uint32_t)(ts2 - ts0),
                                          (uint32_t)(ts3 - ts0), r});
       }
+      if (lane == 9u) {
+        const uint64_t tc3 = __builtin_amdgcn_s_memtime();
+        st_chunk(m->reply + 36u, u32x4_t{(uint32_t)(tc1 - tc0), (uint32_t)(tc3 - tc0), 0u, r});
+      }
 #endif
       if (lane < 8u)  // the 8 tagged chunks in one instruction
         st_chunk(m->reply + 4u * lane, u32x4_t{rq[3u * lane], rq[3u * lane + 1u], rq[3u * lane + 2u], r});
-      __syncthreads();
+      lds_sync();
     } else if (op == kWorkCrc32) {
-      crc = span_crc(len, arg);
+      crc = span_crc(len, arg, &pre);
     } else if (op == kWorkUpdate) {
       // MgenAnalytic::Update of one record on its device flow state (the request from the
-      // polled bytes, WUpdReq); the state is read after the acquire above and written back
-      // before the reply's release, so batch kernels before and after see it
+      // polled bytes, WUpdReq); the state is read after an acquire (batch kernels on any XCD
+      // wrote it) and written back before the reply's release, so later ones see it
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
       const uint32_t* u = reinterpret_cast<const uint32_t*>(buf);
       auto uw = [&](int k) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)u[k]); };
       const uint64_t fp = (uint64_t)uw(0) | (uint64_t)uw(1) << 32;
       const uint32_t slot = uw(2), seq = uw(3), rs = uw(4), ru = uw(5), ts = uw(6), tu = uw(7);
       const uint32_t msg = uw(8);
-      __syncthreads();
+      lds_sync();
       mgenx_flow_state* sp = reinterpret_cast<mgenx_flow_state*>(fp) + slot;
       FlowSM sm;
       sm.load(sp, lane);
@@ -298,15 +362,17 @@ worker_kernel(const WReq* q, WRep* m, const uint32_t* __restrict__ a4_tab,
       }
       status = closed ? kStatusClosed : 0u;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // the state written back before the reply
-      __syncthreads();
+      lds_sync();
     } else if (op == kWorkPack) {
       // MgenMsg::Pack alone (mgenMsg.cpp:83-313) as the batch pack kernel's meta phase walks
       // it (mgenx_pack.hip: layout, truncation, the payload_len zeroing, RANDOM_FILL after two
       // zero bytes, CHECKSUM flag, ComputeCRC32 over msgLen - 4 with LAST_BUFFER), with the
-      // message built whole in LDS and checksummed by the wave
+      // message built whole in LDS and checksummed by the wave.  (Acquire: the RANDOM_FILL
+      // stream in rtab may have been rebuilt for a new fill time since an earlier read.)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
       if (lane < 8u)  // the WPackReq, from the polled bytes
         *reinterpret_cast<u32x4_t*>(rq + 4u * lane) = *reinterpret_cast<const u32x4_t*>(buf + 16u * lane);
-      __syncthreads();
+      lds_sync();
       const uint32_t* tw = rq;  // the template, 17 words (mgenx_flow_tmpl)
       const uint32_t d_seq = rq[18], d_sec = rq[19], d_usec = rq[20];
       const uint32_t d_len = rq[21] & 0xffffu, d_flags = (rq[21] >> 16) & 0xffu;
@@ -360,7 +426,7 @@ worker_kernel(const WReq* q, WRep* m, const uint32_t* __restrict__ a4_tab,
           }
           *reinterpret_cast<u32x4_t*>(buf + o) = u32x4_t{w[0], w[1], w[2], w[3]};
         }
-        __syncthreads();
+        lds_sync();
         // 2. the payload [len, pend) from the mailbox
         if (pay)
           for (uint32_t o = 16u * lane; o < t_plen; o += 1024u) {
@@ -407,14 +473,14 @@ worker_kernel(const WReq* q, WRep* m, const uint32_t* __restrict__ a4_tab,
             put8(len - 1, 0);
           }
         }
-        __syncthreads();
+        lds_sync();
         // 4. ComputeCRC32 (checksum on, a whole header)
         uint32_t tx = crc_in;
         if (ck && !trunc) {
           const uint32_t crc_len = (flags & MGENX_FLAG_LAST_BUFFER) ? msgLen - 4u : msgLen;
-          const uint32_t raw = wave_crc_raw(buf, crc_len, lane, s_a4, s_tab, xpow);
-          const uint32_t init = crc_in == 0u ? 0xFFFFFFFFu : crc_in;  // :530-533
-          tx = raw ^ (crc_len ? multmodp(xpow8(crc_len, xpow), init) : init);
+          tx = wave_crc(crc_len, crc_in, lane, ops, [&](uint32_t o) {  // (:530-533 in wave_crc)
+            return *reinterpret_cast<const u32x4_t*>(buf + o);
+          });
           flags &= ~(uint32_t)MGENX_FLAG_LAST_BUFFER;
         }
         // 5. the message out, visible before the reply's tags (release)
@@ -424,7 +490,7 @@ worker_kernel(const WReq* q, WRep* m, const uint32_t* __restrict__ a4_tab,
         pk_ret = ret;
         pk_tx = tx;
         pk_state = (uint32_t)len | (flags & 0xffu) << 16;
-        __syncthreads();
+        lds_sync();
       } else {  // Pack failed: nothing written
         pk_ret = 0u;
         pk_tx = crc_in;
@@ -449,11 +515,11 @@ worker_kernel(const WReq* q, WRep* m, const uint32_t* __restrict__ a4_tab,
   if (lane == 0) st_sys_release(&m->alive, 0u);
 }
 
-hipError_t launch_worker(const WReq* q, WRep* m, const uint32_t* a4_tab, const uint32_t* byte_tab,
-                         const uint32_t* xpow, const uint8_t* rtab, uint32_t start,
-                         uint64_t idle_ticks, hipStream_t stream) {
-  hipLaunchKernelGGL(worker_kernel, dim3(1), dim3(64), 0, stream, q, m, a4_tab, byte_tab, xpow,
-                     rtab, start, idle_ticks);
+hipError_t launch_worker(const WReq* q, WRep* m, const uint32_t* tabs, const uint32_t* byte_tab,
+                         const uint8_t* rtab, uint32_t start, uint64_t idle_ticks,
+                         hipStream_t stream) {
+  hipLaunchKernelGGL(worker_kernel, dim3(1), dim3(64), 0, stream, q, m, tabs, byte_tab, rtab,
+                     start, idle_ticks);
   return hipGetLastError();
 }
 

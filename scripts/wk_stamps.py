@@ -18,7 +18,7 @@ from oracle import oracle as O  # noqa: E402
 eng = Engine(0, diag=True)
 w = eng.worker()
 out = {"device_mailbox": w.device_mailbox()}
-st = (ctypes.c_uint32 * 4)()
+st = (ctypes.c_uint32 * 8)()
 for size in (64, 256, 1024, 1472, 4096, 8192):
     tmpl, pool, desc = udp_fixed(2, size)
     slab, _ = O.udp_pack_batch(tmpl, desc, pool, 2 * size, stride=size, checksum=True)
@@ -31,9 +31,10 @@ for size in (64, 256, 1024, 1472, 4096, 8192):
         _, c = w.recv(msg)
         host.append(time.perf_counter() - t)
         eng.lib.mgenx_diag_worker_stamps(w.w, st)
-        dev.append((st[0], st[1], st[2]))
+        dev.append((st[0], st[1], st[2], st[4], st[5]))
         assert c is not None
-    d = np.median(np.array(dev), axis=0) * 0.01
+    dd = np.median(np.array(dev, dtype=np.float64), axis=0)
+    d = dd * 0.01
     tu = []
     for _ in range(2000):
         t = time.perf_counter()
@@ -47,6 +48,8 @@ for size in (64, 256, 1024, 1472, 4096, 8192):
     out[str(size)] = {"recv_us": round(np.median(host) * 1e6, 2),
                       "wave_parsed_us": round(d[0], 2), "wave_crc_done_us": round(d[1], 2),
                       "wave_reply_us": round(d[2], 2),
+                      "wave_clocks_to_parse": int(dd[3]), "wave_clocks_to_reply": int(dd[4]),
+                      "sclk_mhz": round(dd[4] / max(d[2], 1e-3), 0),
                       "unpack_us": round(np.median(tu) * 1e6, 2),
                       "crc32_us": round(np.median(tc) * 1e6, 2)}
 w.close()
