@@ -151,6 +151,11 @@ pack_kernel(PackParams p) {
     if (!(builds ? prod_live : cons_live) || b >= n_batches) goto stage_end;
     if (builds) {
     uint8_t* img = S_IMG + lane * kImg;
+    // the image slot starts as zeros: the bytes past pend read as the record's zero fill, so
+    // the aligned-stride store loop loads image units without masking them
+#pragma unroll
+    for (int k = 0; k < kImg / 16; k++)
+      *reinterpret_cast<u32x4_t*>(img + 16 * k) = u32x4_t{0u, 0u, 0u, 0u};
     PackMeta m;
     m.off = 0; m.ret = 0; m.trailer = 0; m.pend = 0; m.poff = 0; m.hdr = 0;
     m.trailer_on = 0; m.rf = rf ? 1 : 0; m.tx_out = 0; m.state = 0; m.frag = 0;
@@ -367,26 +372,31 @@ pack_kernel(PackParams p) {
       uint32_t r = (uint32_t)lane / U, pu = (uint32_t)lane % U;
       uint8_t* base = p.slab + (b << 6) * p.stride;
       const uint32_t units = nv * U;
-      for (uint32_t u = lane; u < units; u += 64) {
-        const uint32_t pos = pu << 4;
-        uint32_t v0 = 0u, v1 = 0u, v2 = 0u, v3 = 0u;
-        const uint32_t pend = S_META[r].pend;             // LDS (record r of the wave)
-        if (pos < pend) {
-          const u32x4_t iv = *reinterpret_cast<const u32x4_t*>(&S_IMG[r * kImg + pos]);
-          const int lim = (int)pend - (int)pos;
-          const uint32_t m0 = byte_range_mask(0, lim < 0 ? 0 : (lim > 4 ? 4 : lim));
-          const uint32_t m1 = byte_range_mask(0, lim < 4 ? 0 : (lim > 8 ? 4 : lim - 4));
-          const uint32_t m2 = byte_range_mask(0, lim < 8 ? 0 : (lim > 12 ? 4 : lim - 8));
-          const uint32_t m3 = byte_range_mask(0, lim < 12 ? 0 : (lim > 16 ? 4 : lim - 12));
-          v0 = iv.x & m0; v1 = iv.y & m1; v2 = iv.z & m2; v3 = iv.w & m3;
+      // record r's trailer word (bytes ret - 4 .. ret - 1, big-endian; 0 without) from the lane
+      // that holds its meta, and its image units from the zero-padded LDS image: a unit is
+      // composed with no per-byte masks and no LDS meta read, and kUnroll units go out per
+      // lane and pass (their image reads first, then the stores)
+      const uint32_t tword = m.trailer_on ? bswap32(m.trailer) : 0u;
+      constexpr uint32_t kUnroll = 4;
+      for (uint32_t u0 = lane; u0 < units; u0 += 64u * kUnroll) {
+        u32x4_t v[kUnroll];
+        uint32_t at[kUnroll];
+#pragma unroll
+        for (uint32_t k = 0; k < kUnroll; k++) {
+          const uint32_t pos = pu << 4;
+          const uint32_t tw = (uint32_t)__shfl((int)tword, (int)min(r, 63u));
+          v[k] = u32x4_t{0u, 0u, 0u, 0u};
+          if (pos < (uint32_t)kImg && r < nv)
+            v[k] = *reinterpret_cast<const u32x4_t*>(&S_IMG[r * kImg + pos]);
+          if (pu == U - 1u && tw) v[k].w = tw;
+          at[k] = u0 + 64u * k;
+          pu += rm;
+          r += q;
+          if (pu >= U) { pu -= U; r++; }
         }
-        if (pu == U - 1u && S_META[r].trailer_on) {       // ret - 4 .. ret - 1, big-endian
-          v3 = bswap32(S_META[r].trailer);
-        }
-        stu128(base + (uint64_t)u * 16u, u32x4_t{v0, v1, v2, v3});
-        pu += rm;
-        r += q;
-        if (pu >= U) { pu -= U; r++; }
+#pragma unroll
+        for (uint32_t k = 0; k < kUnroll; k++)
+          if (at[k] < units) stu128(base + (uint64_t)at[k] * 16u, v[k]);
       }
       goto stage_end;
     }
