@@ -73,12 +73,13 @@ __device__ __forceinline__ u32x4_t load_masked(const uint8_t* p, uint32_t o, uin
   return v;
 }
 
-// One wave: LDS accesses before it are complete after it; global loads stay in flight (a
-// __syncthreads would also wait for them -- the message's prefetch below)
+// Within one wave: its LDS accesses before it are seen by its lanes after it (a wave's LDS
+// operations complete in order; the fences keep the compiler from moving them across).  The
+// worker's two waves never meet at a barrier: each runs its own loop (below).
 __device__ __forceinline__ void lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
 }
 
 static_assert(kWorkerPackMax <= kPiece, "a packed message is built in one LDS piece");
@@ -111,24 +112,16 @@ struct WOps {
 // XOR into bytes 0..3 (the register processing M from st = the zero register processing M with
 // LE(st) XOR-ed into its first four bytes).  load16(o) = the 16 message bytes at offset o (any
 // bytes past n; o < n).
-// pre0 (optional): this lane's block of the first 1 KiB, loaded earlier (the request's data
-// prefetched while the header is parsed)
 template <typename Load16>
 __device__ __forceinline__ uint32_t wave_crc(uint32_t n, uint32_t st_in, uint32_t lane,
-                                             const WOps& ops, Load16 load16,
-                                             const u32x4_t* pre0 = nullptr) {
+                                             const WOps& ops, Load16 load16) {
   const uint32_t st = st_in == 0u ? 0xFFFFFFFFu : st_in;
   auto word_bytes = [&](uint32_t c, uint32_t w, uint32_t nb) {
     for (uint32_t j = 0; j < nb; j++) c = ops.byte(c, w >> (8 * j));
     return c;
   };
   if (n < 16u) {  // one short block: byte steps from st on every lane (same result)
-    const u32x4_t v = n ? (pre0 ? u32x4_t{(uint32_t)__builtin_amdgcn_readfirstlane((int)pre0->x),
-                                          (uint32_t)__builtin_amdgcn_readfirstlane((int)pre0->y),
-                                          (uint32_t)__builtin_amdgcn_readfirstlane((int)pre0->z),
-                                          (uint32_t)__builtin_amdgcn_readfirstlane((int)pre0->w)}
-                                : load16(0u))
-                        : u32x4_t{0u, 0u, 0u, 0u};
+    const u32x4_t v = n ? load16(0u) : u32x4_t{0u, 0u, 0u, 0u};
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
     uint32_t c = st;
     for (uint32_t j = 0; j < n; j++) c = ops.byte(c, w[j >> 2] >> (8 * (j & 3)));
@@ -140,7 +133,7 @@ __device__ __forceinline__ uint32_t wave_crc(uint32_t n, uint32_t st_in, uint32_
     const uint32_t o = 1024u * k + 16u * lane;
     const uint32_t v = n > o ? min(16u, n - o) : 0u;
     if (v) {
-      u32x4_t x = (k == 0u && pre0) ? *pre0 : load16(o);
+      u32x4_t x = load16(o);
       if (o == 0u) x.x ^= st;  // (n >= 16: lane 0's first block is whole)
       if (v == 16u) {
         uint32_t c = ops.apply(2u, x.x);
@@ -149,43 +142,79 @@ __device__ __forceinline__ uint32_t wave_crc(uint32_t n, uint32_t st_in, uint32_
         c = ops.apply(2u, c ^ x.w);
         h = (k ? ops.apply(10u, h) : 0u) ^ c;
         last_end = o + 16u;
-      } else {  // the message's last bytes
+      } else {  // the message's last bytes: whole words through A_4, the rest byte by byte
         const uint32_t w[4] = {x.x, x.y, x.z, x.w};
         uint32_t c = 0;
-        for (uint32_t q = 0; q < 4; q++) c = word_bytes(c, w[q], v > 4u * q ? min(4u, v - 4u * q) : 0u);
-        part = c;
+#pragma unroll
+        for (uint32_t q = 0; q < 3; q++)
+          if (4u * q + 4u <= v) c = ops.apply(2u, c ^ w[q]);
+        const uint32_t qw = v >> 2;
+        const uint32_t tail = qw == 0 ? w[0] : qw == 1 ? w[1] : qw == 2 ? w[2] : w[3];
+        part = word_bytes(c, tail, v & 3u);
       }
     }
   }
-  uint32_t c = (last_end ? ops.shift(h, n - last_end) : 0u) ^ part;
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) c ^= (uint32_t)__shfl_xor((int)c, o);
-  return (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
+  const uint32_t c = (last_end ? ops.shift(h, n - last_end) : 0u) ^ part;
+  return WRing::wave_reduce(c, 0u, [](uint32_t a, uint32_t b) { return a ^ b; });  // (DPP)
 }
 
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(128)
 worker_kernel(const WReq* q, WRep* m, const uint32_t* __restrict__ tabs,
               const uint32_t* __restrict__ byte_tab, const uint8_t* __restrict__ rtab,
               uint32_t start, uint64_t idle_ticks) {
   __shared__ uint32_t s_op[9 * 1024], s_tab[256];
   __shared__ __attribute__((aligned(16))) uint8_t buf[kPiece];
   __shared__ __attribute__((aligned(16))) uint32_t rq[4 * kReplyChunks];
-  const uint32_t lane = threadIdx.x;
+  __shared__ uint64_t s_crc;   // wave 1's last receive checksum: request number << 32 | crc
+  __shared__ uint32_t s_exit;  // wave 0 ended: wave 1 ends too
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   {  // A_(2^b), b = 2..10, from the context's tables
     const uint32_t src[9] = {kTabA4, kTabA8, kTabA16, kTabA32, kTabA64, kTabA128, kTabA256,
                              kTabA512, kTabA1024};
     for (uint32_t t = 0; t < 9; t++)
-      for (uint32_t e = lane; e < 1024u; e += 64u) s_op[t * 1024u + e] = tabs[src[t] * 1024u + e];
+      for (uint32_t e = threadIdx.x; e < 1024u; e += blockDim.x)
+        s_op[t * 1024u + e] = tabs[src[t] * 1024u + e];
   }
-  for (uint32_t e = lane; e < 256u; e += 64u) s_tab[e] = byte_tab[e];
-  lds_sync();
+  for (uint32_t e = threadIdx.x; e < 256u; e += blockDim.x) s_tab[e] = byte_tab[e];
+  if (threadIdx.x == 0) {
+    s_crc = (uint64_t)start << 32;
+    s_exit = 0u;
+  }
+  __syncthreads();  // (the only barrier the two waves share)
   const WOps ops = {s_op, s_tab};
   uint32_t last = start;
   uint64_t t_last = __builtin_amdgcn_s_memrealtime();
+  if (wv == 1) {
+    // Wave 1: the receive path's checksum, in parallel with wave 0's Unpack of the same
+    // request -- it polls the same doorbell and, for a receive request, checksums
+    // len - 4 bytes from the data area and posts the value with the request number.  Wave 0
+    // takes it when the decode says the caller checksums (else it is not used).  It ends when
+    // wave 0 does.
+    for (;;) {
+      if (*reinterpret_cast<volatile uint32_t*>(&s_exit)) break;
+      const u32x4_t pc = poll_pieces(q, lane);
+      const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)pc.x, 0);
+      if ((int32_t)(r - last) <= 0 || __ballot(lane >= 1u && lane < kPollPieces && pc.w != r)) {
+        __builtin_amdgcn_s_sleep(2);
+        continue;
+      }
+      last = r;
+      const uint32_t ol = (uint32_t)__builtin_amdgcn_readlane((int)pc.y, 0);
+      const uint32_t op = ol >> kWorkOpShift;
+      const uint32_t len = min(ol & kWorkLenMask, (uint32_t)kWorkerMaxBytes);
+      if (op == kWorkStop) break;
+      if (op == kWorkRecv && len >= 4u) {
+        const uint32_t cl = len - 4u;
+        const uint32_t c = wave_crc(cl, 0u, lane, ops,
+                                    [&](uint32_t o) { return load_masked(q->data + o, o, cl); });
+        if (lane == 0) *reinterpret_cast<volatile uint64_t*>(&s_crc) = (uint64_t)r << 32 | c;
+      }
+    }
+    return;
+  }
   // MgenMsg::ComputeCRC32(st, data, cl) over the request's data area
-  auto span_crc = [&](uint32_t cl, uint32_t st, const u32x4_t* pre0) -> uint32_t {
-    return wave_crc(cl, st, lane, ops, [&](uint32_t o) { return load_masked(q->data + o, o, cl); },
-                    pre0);
+  auto span_crc = [&](uint32_t cl, uint32_t st) -> uint32_t {
+    return wave_crc(cl, st, lane, ops, [&](uint32_t o) { return load_masked(q->data + o, o, cl); });
   };
   for (;;) {
     const u32x4_t pc = poll_pieces(q, lane);
@@ -206,10 +235,6 @@ worker_kernel(const WReq* q, WRep* m, const uint32_t* __restrict__ tabs,
     const uint32_t op = ol >> kWorkOpShift;
     uint32_t len = ol & kWorkLenMask;
     const uint32_t arg = (uint32_t)__builtin_amdgcn_readlane((int)pc.z, 0);
-    // the checksummed span's first KiB, in flight while the header is parsed (receive: the
-    // message less its trailer; crc32: all of it)
-    const uint32_t span = op == kWorkRecv ? (len >= 4u ? len - 4u : 0u) : op == kWorkCrc32 ? len : 0u;
-    const u32x4_t pre = load_masked(q->data + 16u * lane, 16u * lane, min(span, 1024u));
     // the polled data bytes into LDS: piece k's 12 bytes at 12 (k - 1)
     if (lane >= 1u && lane < kPollPieces) {
       uint32_t* d = reinterpret_cast<uint32_t*>(buf + 12u * (lane - 1u));
@@ -291,9 +316,11 @@ worker_kernel(const WReq* q, WRep* m, const uint32_t* __restrict__ tabs,
       ts1 = __builtin_amdgcn_s_memrealtime();
       tc1 = __builtin_amdgcn_s_memtime();
 #endif
-      if (rq[kReplyStatus] & kStatusCrc) {  // (the whole message is in the data area)
-        const uint32_t c = span_crc(len - 4u, 0u, &pre);
-        if (lane == 0) rq[kReplyCrc] = c;
+      if (rq[kReplyStatus] & kStatusCrc) {  // wave 1's checksum of this request
+        uint64_t v;
+        while (((v = *reinterpret_cast<volatile uint64_t*>(&s_crc)) >> 32) != r)
+          __builtin_amdgcn_s_sleep(1);
+        if (lane == 0) rq[kReplyCrc] = (uint32_t)v;
         lds_sync();
       }
 #if MGENX_DIAG
@@ -312,7 +339,7 @@ worker_kernel(const WReq* q, WRep* m, const uint32_t* __restrict__ tabs,
         st_chunk(m->reply + 4u * lane, u32x4_t{rq[3u * lane], rq[3u * lane + 1u], rq[3u * lane + 2u], r});
       lds_sync();
     } else if (op == kWorkCrc32) {
-      crc = span_crc(len, arg, &pre);
+      crc = span_crc(len, arg);
     } else if (op == kWorkUpdate) {
       // MgenAnalytic::Update of one record on its device flow state (the request from the
       // polled bytes, WUpdReq); the state is read after an acquire (batch kernels on any XCD
@@ -512,13 +539,16 @@ worker_kernel(const WReq* q, WRep* m, const uint32_t* __restrict__ tabs,
     last = r;
     t_last = __builtin_amdgcn_s_memrealtime();
   }
-  if (lane == 0) st_sys_release(&m->alive, 0u);
+  if (lane == 0) {
+    *reinterpret_cast<volatile uint32_t*>(&s_exit) = 1u;  // wave 1 ends too
+    st_sys_release(&m->alive, 0u);
+  }
 }
 
 hipError_t launch_worker(const WReq* q, WRep* m, const uint32_t* tabs, const uint32_t* byte_tab,
                          const uint8_t* rtab, uint32_t start, uint64_t idle_ticks,
                          hipStream_t stream) {
-  hipLaunchKernelGGL(worker_kernel, dim3(1), dim3(64), 0, stream, q, m, tabs, byte_tab, rtab,
+  hipLaunchKernelGGL(worker_kernel, dim3(1), dim3(128), 0, stream, q, m, tabs, byte_tab, rtab,
                      start, idle_ticks);
   return hipGetLastError();
 }
