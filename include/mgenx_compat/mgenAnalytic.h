@@ -3,9 +3,9 @@
 //
 // MgenAnalytic::Update (the per-flow window state machine with its 1024-bit duplicate
 // mask, mgenAnalytic.cpp:74-258) runs on the GPU: each MgenAnalytic owns a device
-// mgenx_flow_state slot, Update is a batch of one through mgenx_flow_reduce, and
-// MgenAnalyticTable::UpdateBatch hands a whole receive batch (in receive order) to the same
-// kernel.  Report building / parsing and the quantizers (mgenAnalytic.cpp:331-642) are the
+// mgenx_flow_state slot, Update of one record goes to the resident worker
+// (mgenx_worker_flow_update), and MgenAnalyticTable::UpdateBatch hands a whole receive batch
+// (in receive order) to mgenx_flow_reduce.  Report building / parsing and the quantizers (mgenAnalytic.cpp:331-642) are the
 // host-side wire format of the MGEN_DATA report item, as in the reference.
 #ifndef _MGEN_ANALYTIC
 #define _MGEN_ANALYTIC

@@ -8,10 +8,11 @@
 // the device in one hipMemcpyAsync, processed by libmgenx's gfx950 kernels
 // (mgenx_pack_msgs, mgenx_unpack_batch, mgenx_crc32_update, mgenx_flow_reduce) and copied
 // back in one more; the call returns when the results are in the caller's buffers.  A single
-// Pack, Unpack or ComputeCRC32 (what an unchanged transport calls per message) goes instead to
-// the resident worker (mgenx_worker_*): one wave kept on the device that polls a pinned mailbox,
-// so the call pays no launch and no copy.  There is no host implementation of the codec here:
-// without a GPU the calls throw.
+// Pack, Unpack, ComputeCRC32 or MgenAnalytic::Update (what an unchanged transport and
+// Mgen::UpdateRecvAnalytics call per message) goes instead to the resident worker
+// (mgenx_worker_*): two waves kept on the device polling a request block, so the call pays no
+// launch and no copy; an Unpack also brings back the checksum the receive path computes next.
+// There is no host implementation of the codec here: without a GPU the calls throw.
 //
 // One engine per process (device MGENX_DEVICE, default 0), serialised by a mutex: the
 // reference's callers run on one dispatcher thread.
