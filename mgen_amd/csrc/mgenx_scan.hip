@@ -48,6 +48,9 @@ namespace mgenx {
 constexpr uint32_t kScanBlockBytes = MGENX_SCAN_BLOCK;  // detect block (one workgroup)
 constexpr uint32_t kScanThreads = MGENX_SCAN_THREADS;   // 16 B per thread and step
 constexpr uint32_t kScanSlots = 4096;        // candidates per block before overflow
+// a slot: in-block offset (bits 0-14) | header copy (bit 15, is_copy) | length << 16
+constexpr uint32_t kSlotOff = 0x7FFFu, kSlotCopy = 0x8000u;
+static_assert(kScanBlockBytes <= 32768, "slot offsets are 15 bits");
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 
 struct ScanMode {
@@ -94,15 +97,11 @@ __device__ __forceinline__ uint32_t detect_hits(const uint32_t (&w)[5], uint64_t
 // message carries its own header again at +8192, +16384, ... -- plausible starts that are not
 // records (config 5's stream has 2 candidates per record, and the chain then needs the
 // lifting).  A candidate whose first 16 bytes equal the 16 bytes 8192 earlier is taken for a
-// copy by the chain hypothesis of scan_mark_* (checked there: a wrong guess only costs the
-// exact path).  (Dropping the copies in detect instead cost detect 172 -> 201 us: the extra
-// dependent loads lengthen every block.)
+// copy by the chain hypothesis of scan_chain_* (checked there: a wrong guess only costs the
+// exact path).  Detect sets that bit in the candidate's slot from two loads side by side (its
+// length re-read is one of them).  (Dropping the copies in detect instead cost detect 172 ->
+// 201 us in round 3: the extra dependent loads lengthened every block.)
 constexpr uint64_t kCopyDist = 8192;
-__device__ __forceinline__ bool is_copy(const uint8_t* __restrict__ s, uint64_t nbytes, uint64_t p) {
-  if (p < kCopyDist || p + 16 > nbytes) return false;
-  const u32x4_t a = ldu128(s + p), b = ldu128(s + p - kCopyDist);
-  return a.x == b.x && a.y == b.y && a.z == b.z && a.w == b.w;
-}
 
 // exclusive prefix over the lanes of the wave and the wave total of c (0..16), by ballots
 __device__ __forceinline__ uint32_t wave_excl(uint32_t c, uint32_t& wtot) {
@@ -221,9 +220,21 @@ scan_detect_kernel(const uint8_t* __restrict__ s, uint64_t nbytes, ScanMode m,
           } else {
             // the slot keeps the candidate's length field too, so the link step reads no
             // stream bytes: re-read here, where the block's bytes were just loaded (keeping
-            // the 16 loaded rows live until this loop instead costs 32 VGPRs and occupancy)
-            const uint32_t L = be16_at(s, block0 + off);
-            out[pos++] = off | (L << 16);
+            // the 16 loaded rows live until this loop instead costs 32 VGPRs and occupancy);
+            // beside it the 16 bytes 8192 earlier, for the header-copy bit (is_copy: two
+            // loads side by side, no extra round trip)
+            const uint64_t p = block0 + off;
+            uint32_t L, cp = 0u;
+            if (p + 16 <= nbytes) {
+              const u32x4_t a = ldu128(s + p);
+              const u32x4_t c = ldu128(s + (p >= kCopyDist ? p - kCopyDist : p));
+              L = ((a.x & 0xFFu) << 8) | ((a.x >> 8) & 0xFFu);
+              cp = p >= kCopyDist && a.x == c.x && a.y == c.y && a.z == c.z && a.w == c.w
+                       ? kSlotCopy : 0u;
+            } else {
+              L = be16_at(s, p);
+            }
+            out[pos++] = off | cp | (L << 16);
           }
         }
       }
@@ -263,8 +274,7 @@ __global__ void __launch_bounds__(256)
 scan_link_kernel(const uint8_t* __restrict__ s, uint64_t nbytes, const uint32_t* __restrict__ slots,
                  const uint64_t* __restrict__ counts, const uint64_t* __restrict__ base,
                  uint32_t n_blocks, uint64_t* __restrict__ cand, uint32_t* __restrict__ up,
-                 uint32_t* __restrict__ dist, uint64_t spec_cap, uint32_t* __restrict__ irregular,
-                 uint32_t* __restrict__ mark = nullptr, uint32_t epoch = 0) {
+                 uint32_t* __restrict__ dist, uint64_t spec_cap, uint32_t* __restrict__ irregular) {
   // 16 lanes per detect block, 4 blocks per wave (a block holds a handful of candidates)
   const uint32_t b =
       (blockIdx.x * 4 + (threadIdx.x >> 6)) * kLinkPerWave + ((threadIdx.x & 63u) >> 4);
@@ -295,7 +305,7 @@ scan_link_kernel(const uint8_t* __restrict__ s, uint64_t nbytes, const uint32_t*
       nx = p + be16_at(s, p);
     } else {
       const uint32_t sl = slots[(size_t)b * kScanSlots + k];  // offset | length << 16
-      p = (uint64_t)b * kScanBlockBytes + (sl & 0xFFFFu);
+      p = (uint64_t)b * kScanBlockBytes + (sl & kSlotOff);
       nx = p + (sl >> 16);
       cand[o + k] = p;
     }
@@ -321,21 +331,19 @@ scan_link_kernel(const uint8_t* __restrict__ s, uint64_t nbytes, const uint32_t*
             for (uint32_t j = 0; j < 8; j++) w[j] = j < cb ? ts[j] : 0xFFFFFFFFu;
 #pragma unroll
             for (uint32_t j = 0; j < 8; j++)
-              if (tgt == kNone && (w[j] & 0xFFFFu) == key && j < cb) tgt = ob + j;
+              if (tgt == kNone && (w[j] & kSlotOff) == key && j < cb) tgt = ob + j;
           } else {
             while (lo < hi) {
               const uint32_t mid = (lo + hi) >> 1;
-              if ((ts[mid] & 0xFFFFu) < key) lo = mid + 1; else hi = mid;
+              if ((ts[mid] & kSlotOff) < key) lo = mid + 1; else hi = mid;
             }
-            if (lo < cb && (ts[lo] & 0xFFFFu) == key) tgt = ob + lo;
+            if (lo < cb && (ts[lo] & kSlotOff) == key) tgt = ob + lo;
           }
         }
       }
     }
     up[o + k] = tgt == kNone ? o + k : tgt;
     dist[o + k] = tgt == kNone ? 0u : 1u;
-    // (chain hypothesis, scan_mark_*: every candidate but a header copy marks its successor)
-    if (mark && tgt != kNone && !is_copy(s, nbytes, p)) mark[tgt] = (epoch << 2) | 1u;
     const uint64_t ci = (uint64_t)o + k;
     odd = odd || (ci + 1 < n_tot ? tgt != o + k + 1 : tgt != kNone);
   }
@@ -376,175 +384,318 @@ scan_enum_regular_kernel(const uint8_t* __restrict__ s, const uint64_t* __restri
   rec_len[i] = be16_at(s, p);
 }
 
-// The chain from offset 0 on a speculative TCP build without lifting.  Its hypothesis H = {0}
-// and every candidate that is some candidate's successor (the link step marks them with this
-// scan's epoch): a record start past 0 is its predecessor's successor, while a plausible start
-// inside a payload is almost never where another candidate's record ends.  H is accepted when
-// it is one chain -- candidate 0 at offset 0, succ(h_i) = h_{i+1} in position order, the last
-// one terminal -- which proves that the chain from offset 0 is H exactly.  Three launches over
-// 1024-candidate blocks (the grid is sized by the table capacity; the candidate total is read
-// on the device): counts, then ranks + records + the successor check, then one workgroup that
-// folds the per-block results.
-struct MarkTabs {
-  uint32_t* mark;
-  uint32_t epoch;
-  uint32_t* cnt;   // [blocks] H elements per block
-  uint32_t* fail;  // [blocks] a successor check failed
-  uint32_t* last;  // [blocks] the block's last H element (kNone: none)
+// The chain from offset 0 on a speculative whole-stream TCP scan, with no candidate table, no
+// link and no lifting.  (Config 5's stream is not regular: the TCP sender re-sends each
+// message's 8-KiB Pack buffer, so every message carries a copy of its header 8192 bytes on.)
+// A hypothesis H is guessed from successor marks and then PROVED:
+//   marks: every candidate p that is not a header copy (is_copy) marks its successor q = p + L
+//   and leaves its length L there (a position marked by two different candidates keeps none);
+//   H = {0} and every marked candidate whose marker is 0 or itself marked (or is not known).
+//   (Junk starts inside headers chain in short runs -- seq 0x802 reads as a length-8 record at
+//   header offset 9 whose successor at 17 is tx_usec's same bytes -- and nothing marks the
+//   junk start, so its successor stays out.)
+// H is the chain from offset 0 exactly when 0 is in H, each member's successor is the next
+// member in position order and the last member's successor is not a candidate: the emit pass
+// checks that while it writes H out in order; otherwise the host rebuilds exactly.  The marks
+// are keyed by stream POSITION in an open-addressing table whose entries carry this scan's
+// epoch (cleared once per 255 scans), so no candidate needs a global number: no block-count
+// scan, no link, and the ranks of H come from one decoupled look-back over the emit groups.
+struct ChainAux {  // one emit group's summary, for the host
+  uint64_t first, last_succ;  // position of its first H member; successor of its last
+  uint32_t nh, ncand, fail, tail_cand;  // tail_cand: last_succ is a candidate
 };
-// H = level 2: the successors of level-1 members (a successor of a successor): junk starts
-// inside headers chain in short runs (seq 0x802 = bytes 00 00 08 02 at header offset 8 reads
-// as a length-8 record at offset 9 whose successor at 17 is tx_usec's same bytes), and a
-// second level drops them
-__device__ __forceinline__ bool in_h1(const MarkTabs& m, uint32_t c) {
-  return c == 0u || (m.mark[c] >> 2) == m.epoch;
-}
-__device__ __forceinline__ bool in_h(const MarkTabs& m, uint32_t c) {
-  return c == 0u || m.mark[c] == ((m.epoch << 2) | 2u);
-}
+struct ChainTabs {
+  uint64_t* hash;    // [hmask + 1]: epoch << 56 | pos << 16 | marker length; 0 = never used
+  uint32_t hmask, epoch;  // epoch: 1 .. 255
+  uint32_t* flags;   // [2] = epoch: a mark of that scan found no free entry
+  uint64_t* status;  // [groups] look-back words: epoch << 40 | kind << 38 | H count
+};
+constexpr int kChainProbes = 32;
+constexpr uint32_t kChainEpochs = 256;
+constexpr uint32_t kChainThreads = 1024;
+constexpr uint32_t kChainBlocks = 4096;  // detect blocks per emit group at most
+constexpr uint32_t kChainList = 4096;    // H members per emit group at most (else: not proved)
+constexpr uint32_t kChainPer = 4;        // candidates per thread and round
+constexpr uint32_t kChainGroups = 1024;
 
-__global__ void __launch_bounds__(1024)
-scan_mark_next_kernel(const uint32_t* __restrict__ up, const uint64_t* __restrict__ total,
-                      uint32_t stride, MarkTabs m) {
-  const uint32_t c = blockIdx.x * 1024u + threadIdx.x;
-  const uint64_t n64 = *total;
-  const uint32_t n = n64 <= stride ? (uint32_t)n64 : 0u;
-  if (c >= n || !in_h1(m, c)) return;
-  const uint32_t t = up[c];
-  if (t != c) m.mark[t] = (m.epoch << 2) | 2u;  // (raises a level-1 mark: in_h1 still holds)
+__device__ __forceinline__ uint32_t chain_slot(uint64_t pos, uint32_t hmask) {
+  return (uint32_t)((pos * 0x9E3779B97F4A7C15ull) >> 32) & hmask;
 }
-
-__global__ void __launch_bounds__(1024)
-scan_mark_count_kernel(const uint64_t* __restrict__ total, uint32_t stride, MarkTabs m) {
-  __shared__ uint32_t ws[16];
-  const uint32_t t = threadIdx.x, c = blockIdx.x * 1024u + t;
-  const uint64_t n64 = *total;
-  const uint32_t n = n64 <= stride ? (uint32_t)n64 : 0u;
-  const bool h = c < n && in_h(m, c);
-  const uint64_t b = __ballot(h);
-  if ((t & 63u) == 0u) ws[t >> 6] = (uint32_t)__popcll(b);
-  __syncthreads();
-  if (t == 0) {
-    uint32_t x = 0;
-    for (int k = 0; k < 16; k++) x += ws[k];
-    m.cnt[blockIdx.x] = x;
-  }
+__device__ __forceinline__ uint64_t ld_agent(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-
-__global__ void __launch_bounds__(1024)
-scan_mark_emit_kernel(const uint8_t* __restrict__ s, const uint64_t* __restrict__ cand,
-                      const uint32_t* __restrict__ up, const uint64_t* __restrict__ total,
-                      uint32_t stride, uint64_t cap, uint64_t* __restrict__ rec_off,
-                      uint32_t* __restrict__ rec_len, MarkTabs m) {
-  __shared__ uint32_t ws[16], wf[16];
-  __shared__ uint32_t list[1024];
-  __shared__ uint32_t base_s;
-  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6, blk = blockIdx.x;
-  const uint64_t n64 = *total;
-  const uint32_t n = n64 <= stride ? (uint32_t)n64 : 0u;
-  const uint32_t c = blk * 1024u + t;
-  const bool h = c < n && in_h(m, c);
-  // this block's first rank: the H counts of the blocks before it
-  uint32_t pre = 0;
-  for (uint32_t k = t; k < blk; k += 1024u) pre += m.cnt[k];
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) pre += (uint32_t)__shfl_xor((int)pre, o);
-  const uint64_t bal = __ballot(h);
-  const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-  if (lane == 0) {
-    ws[wv] = (uint32_t)__popcll(bal);
-    wf[wv] = pre;
-  }
-  __syncthreads();
-  if (t == 0) {
-    uint32_t x = 0;
-    for (int k = 0; k < 16; k++) x += wf[k];
-    base_s = x;
-  }
-  uint32_t local = below, bcnt = 0;
-#pragma unroll
-  for (uint32_t k = 0; k < 16; k++) {
-    local += k < wv ? ws[k] : 0u;
-    bcnt += ws[k];
-  }
-  if (h) list[local] = c;
-  __syncthreads();
-  bool fail = false;
-  if (h) {
-    const uint64_t r = (uint64_t)base_s + local;
-    const uint64_t p = cand[c];
-    if (r < cap) {
-      rec_off[r] = p;
-      rec_len[r] = be16_at(s, p);
+// mark position q with its marker's length L; false when no entry is free within the probe
+// bound.  Linear probing with no deletions: an insert skips only entries of this epoch, so every
+// entry before a key's own on its probe path is of this epoch and a lookup may stop at a stale
+// one.  The CAS decides; a stale first read only costs a retry.
+__device__ bool chain_mark(const ChainTabs& t, uint64_t q, uint32_t L) {
+  const uint64_t key = ((uint64_t)t.epoch << 40) | q;
+  const uint32_t h = chain_slot(q, t.hmask);
+  for (int k = 0; k < kChainProbes; k++) {
+    unsigned long long* a = (unsigned long long*)(t.hash + ((h + k) & t.hmask));
+    uint64_t e = ld_agent((const uint64_t*)a);
+    for (;;) {
+      if ((e >> 56) == t.epoch) {
+        if ((e >> 16) != key) break;  // another position's: next entry
+        const uint32_t d = (uint32_t)(e & 0xFFFFu);
+        if (d != 0u && d != L) atomicAnd(a, ~0xFFFFull);  // two markers: keep none
+        return true;
+      }
+      const uint64_t prev = atomicCAS(a, (unsigned long long)e, (unsigned long long)((key << 16) | L));
+      if (prev == e) return true;  // claimed a stale entry
+      e = prev;                    // raced: look at what is there now
     }
-    uint32_t next = kNone;
-    if (local + 1u < bcnt) {
-      next = list[local + 1u];
-    } else {  // the block's last H element: the first H element after the block, if any
-      uint32_t x = (blk + 1u) * 1024u;
-      for (uint32_t steps = 0; x < n && !in_h(m, x); x++)
-        if (++steps > 4096u) { fail = true; break; }  // (give up: the host falls back)
-      next = x < n ? x : kNone;
-      m.last[blk] = c;
-    }
-    fail = fail || up[c] != (next == kNone ? c : next);
   }
-  const uint64_t fb = __ballot(fail);
-  if (lane == 0) wf[wv] = fb ? 1u : 0u;
-  __syncthreads();
-  if (t == 0) {
-    uint32_t f = 0;
-    for (int k = 0; k < 16; k++) f |= wf[k];
-    m.fail[blk] = f;
-    if (bcnt == 0u) m.last[blk] = kNone;
+  return false;
+}
+// the marker length at q (0: marked by two), or -1: unmarked
+__device__ __forceinline__ int32_t chain_marker(const ChainTabs& t, uint64_t q) {
+  const uint64_t key = ((uint64_t)t.epoch << 40) | q;
+  const uint32_t h = chain_slot(q, t.hmask);
+  for (int k = 0; k < kChainProbes; k++) {
+    const uint64_t e = t.hash[(h + k) & t.hmask];
+    if ((e >> 56) != t.epoch) return -1;
+    if ((e >> 16) == key) return (int32_t)(e & 0xFFFFu);
   }
+  return -1;
 }
 
+// the marks from the detect slots, 16 lanes per detect block (the link kernel's geometry).  A
+// block that overflowed its slots has none: the emit pass fails H then.
 __global__ void __launch_bounds__(256)
-scan_mark_final_kernel(const uint8_t* __restrict__ s, const uint64_t* __restrict__ cand,
-                       const uint64_t* __restrict__ total, uint32_t stride, uint32_t blocks,
-                       MarkTabs m, ChainEnd* __restrict__ end, uint64_t* __restrict__ host_regular) {
-  __shared__ uint32_t sm[4], sf[4], sl[4];
-  const uint32_t t = threadIdx.x;
-  const uint64_t n64 = *total;
-  const uint32_t n = n64 <= stride ? (uint32_t)n64 : 0u;
-  const uint32_t nb = (n + 1023u) / 1024u;
-  uint32_t sum = 0, f = 0, lastb = 0;  // lastb: 1 + the last block holding H elements
-  for (uint32_t k = t; k < nb && k < blocks; k += 256u) {
-    const uint32_t x = m.cnt[k];
-    sum += x;
-    f |= m.fail[k];
-    if (x) lastb = max(lastb, k + 1u);
+scan_chain_mark_kernel(const uint8_t* __restrict__ s, uint64_t nbytes,
+                       const uint32_t* __restrict__ slots, const uint64_t* __restrict__ counts,
+                       uint32_t n_blocks, ChainTabs t) {
+  const uint32_t b =
+      (blockIdx.x * 4 + (threadIdx.x >> 6)) * kLinkPerWave + ((threadIdx.x & 63u) >> 4);
+  const uint32_t sub = threadIdx.x & 15u;
+  if (b >= n_blocks) return;
+  const uint64_t cw = counts[b];
+  if (cw >> 32) return;
+  const uint32_t c = (uint32_t)cw;
+  bool full = false;
+  for (uint32_t k = sub; k < c; k += 16) {
+    const uint32_t sl = slots[(size_t)b * kScanSlots + k];  // offset | length << 16
+    const uint64_t p = (uint64_t)b * kScanBlockBytes + (sl & kSlotOff);
+    const uint64_t q = p + (sl >> 16);
+    if (q < nbytes && !(sl & kSlotCopy) && !chain_mark(t, q, sl >> 16)) full = true;
   }
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-    sum += (uint32_t)__shfl_xor((int)sum, o);
-    f |= (uint32_t)__shfl_xor((int)f, o);
-    lastb = max(lastb, (uint32_t)__shfl_xor((int)lastb, o));
+  if (full) t.flags[2] = t.epoch;
+}
+
+// is position q a candidate (in its detect block's slots; an overflowed block: unknown, yes)
+__device__ bool chain_is_cand(const uint32_t* __restrict__ slots, const uint64_t* __restrict__ counts,
+                              uint32_t n_blocks, uint64_t nbytes, uint64_t q) {
+  if (q >= nbytes) return false;
+  const uint64_t bq = q / kScanBlockBytes;
+  if (bq >= n_blocks) return false;
+  const uint64_t cw = counts[bq];
+  if (cw >> 32) return true;
+  const uint32_t* ts = slots + (size_t)bq * kScanSlots;
+  const uint32_t key = (uint32_t)(q % kScanBlockBytes);
+  uint32_t lo = 0, hi = (uint32_t)cw;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if ((ts[mid] & kSlotOff) < key) lo = mid + 1; else hi = mid;
   }
-  if ((t & 63u) == 0u) {
-    sm[t >> 6] = sum;
-    sf[t >> 6] = f;
-    sl[t >> 6] = lastb;
+  return lo < (uint32_t)cw && (ts[lo] & kSlotOff) == key;
+}
+
+// H in position order: emit group g takes detect blocks [g per_group, (g + 1) per_group): their
+// candidate counts -> an exclusive prefix in LDS, each candidate j of the group -> (block, slot)
+// by a binary search of it, its marks, and the H members -> an LDS list by ballot ranks.  The
+// group's H count goes out as an aggregate, a decoupled look-back over the earlier groups gives
+// its first rank (bounded: a group that never publishes -- dispatch order is not promised --
+// makes this one give up and fail the scan, which the exact path then redoes), and the list is
+// written to rec_off / rec_len while each member's successor is compared with the next member.
+// Each group's summary goes to host memory (ChainAux): the host checks the joins between
+// groups, that 0 is in H and that the last member's successor is not a candidate.
+__device__ __forceinline__ uint64_t chain_word(uint32_t epoch, uint32_t kind, uint64_t v) {
+  return ((uint64_t)epoch << 40) | ((uint64_t)kind << 38) | v;
+}
+constexpr uint32_t kChainSpin = 1u << 18;  // look-back polls before giving up
+__global__ void __launch_bounds__(kChainThreads)
+scan_chain_emit_kernel(const uint32_t* __restrict__ slots, const uint64_t* __restrict__ counts,
+                       uint64_t nbytes, uint32_t n_blocks, uint32_t per_group, ChainTabs t,
+                       uint64_t cap, uint64_t* __restrict__ rec_off, uint32_t* __restrict__ rec_len,
+                       ChainAux* __restrict__ host_aux) {
+  __shared__ uint32_t pre[kChainBlocks + 1];
+  __shared__ uint64_t lpos[kChainList];
+  __shared__ uint16_t llen[kChainList];
+  __shared__ uint32_t wsum[kChainThreads / 64];
+  __shared__ uint32_t sh[2];  // fail, tail candidate
+  __shared__ uint64_t s_prefix;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+  constexpr uint32_t kW = kChainThreads / 64;
+  const uint32_t g = blockIdx.x;
+  const uint32_t b0 = min(g * per_group, n_blocks), b1 = min(b0 + per_group, n_blocks);
+  const uint32_t nblk = b1 - b0;
+  if (tid == 0) {
+    sh[0] = t.flags[2] == t.epoch ? 1u : 0u;  // a mark found no free entry
+    sh[1] = 0u;
+  }
+  // 1. candidate counts -> exclusive prefix (thread t owns K <= 4 consecutive entries)
+  bool fail = false;
+  for (uint32_t i = tid; i < nblk; i += kChainThreads) {
+    const uint64_t w = counts[b0 + i];
+    pre[i] = (uint32_t)w;
+    fail = fail || (w >> 32) != 0u;  // an overflowed block has no slots
   }
   __syncthreads();
-  if (t == 0) {
-    const uint32_t msum = sm[0] + sm[1] + sm[2] + sm[3];
-    const uint32_t fl = sf[0] | sf[1] | sf[2] | sf[3];
-    const uint32_t lb = max(max(sl[0], sl[1]), max(sl[2], sl[3]));
-    const bool ok = n != 0u && nb <= blocks && cand[0] == 0 && msum != 0u && fl == 0u && lb != 0u;
-    *host_regular = ok ? 1u : 0u;
-    if (ok) {
-      const uint64_t tp = cand[m.last[lb - 1u]];
-      end->count = msum;
-      end->next_pos = tp + be16_at(s, tp);
-      end->more = 0;
-    } else {
-      end->count = 0;
-      end->next_pos = 0;
-      end->more = 2;
+  const uint32_t K = (nblk + kChainThreads - 1) / kChainThreads;
+  const uint32_t i0 = min(tid * K, nblk), i1 = min(i0 + K, nblk);
+  uint32_t tot = 0;
+  for (uint32_t i = i0; i < i1; i++) tot += pre[i];
+  uint32_t incl = tot;
+#pragma unroll
+  for (uint32_t d = 1; d < 64u; d <<= 1) {
+    const uint32_t o = (uint32_t)__shfl_up((int)incl, d);
+    if (lane >= d) incl += o;
+  }
+  if (lane == 63u) wsum[wv] = incl;
+  __syncthreads();
+  uint32_t run = incl - tot, C = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kW; k++) {
+    run += k < wv ? wsum[k] : 0u;
+    C += wsum[k];
+  }
+  __syncthreads();  // (wsum is reused below)
+  for (uint32_t i = i0; i < i1; i++) {
+    const uint32_t v = pre[i];
+    pre[i] = run;
+    run += v;
+  }
+  if (tid == 0) pre[nblk] = C;
+  __syncthreads();
+  // 2. the H members in position order (round r: candidates j0 + u 1024 + tid, u-major)
+  uint32_t nh = 0;
+  for (uint32_t j0 = 0; j0 < C; j0 += kChainThreads * kChainPer) {
+    uint32_t sl[kChainPer], blk[kChainPer];
+#pragma unroll
+    for (uint32_t u = 0; u < kChainPer; u++) {
+      const uint32_t j = j0 + u * kChainThreads + tid;
+      sl[u] = 0u;
+      blk[u] = 0u;
+      if (j < C) {
+        uint32_t lo = 0, hi = nblk;  // the last block whose prefix is <= j
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi + 1) >> 1;
+          if (pre[mid] <= j) lo = mid; else hi = mid - 1;
+        }
+        blk[u] = b0 + lo;
+        sl[u] = slots[(size_t)(b0 + lo) * kScanSlots + (j - pre[lo])];
+      }
     }
+    // H: marked, and its marker is 0, marked too, or not known (two markers)
+    uint64_t p[kChainPer];
+    int32_t d[kChainPer];
+#pragma unroll
+    for (uint32_t u = 0; u < kChainPer; u++) {
+      const uint32_t j = j0 + u * kChainThreads + tid;
+      p[u] = (uint64_t)blk[u] * kScanBlockBytes + (sl[u] & kSlotOff);
+      d[u] = j < C && p[u] != 0 ? chain_marker(t, p[u]) : -1;
+    }
+    uint32_t hm = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < kChainPer; u++) {
+      const uint32_t j = j0 + u * kChainThreads + tid;
+      bool h = j < C && p[u] == 0;
+      if (d[u] == 0 || (d[u] > 0 && p[u] == (uint64_t)d[u])) h = true;
+      else if (d[u] > 0) h = chain_marker(t, p[u] - (uint32_t)d[u]) >= 0;
+      hm |= h ? 1u << u : 0u;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kChainPer; u++) {
+      if (j0 + u * kChainThreads >= C) break;
+      const uint64_t bal = __ballot((hm >> u) & 1u);
+      if (lane == 0) wsum[wv] = (uint32_t)__popcll(bal);
+      __syncthreads();
+      uint32_t before = 0, all = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < kW; k++) {
+        before += k < wv ? wsum[k] : 0u;
+        all += wsum[k];
+      }
+      if ((hm >> u) & 1u) {
+        const uint32_t r = nh + before +
+            __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                      __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+        if (r < kChainList) {
+          lpos[r] = p[u];
+          llen[r] = (uint16_t)(sl[u] >> 16);
+        }
+      }
+      nh += all;
+      __syncthreads();  // wsum reused by the next u
+    }
+  }
+  fail = fail || nh > kChainList;
+  const uint32_t nl = min(nh, kChainList);
+  // 3. this group's first rank: aggregate out, decoupled look-back (wave 0), inclusive out;
+  // meanwhile wave 1 asks whether the last member's successor is a candidate (which only
+  // matters for the last nonempty group: there it must not be)
+  if (wv == 1 && lane == 0 && nl)
+    sh[1] = chain_is_cand(slots, counts, n_blocks, nbytes, lpos[nl - 1] + llen[nl - 1]) ? 2u : 0u;
+  if (wv == 0) {
+    if (lane == 0)
+      __hip_atomic_store(&t.status[g], chain_word(t.epoch, g == 0 ? 2u : 1u, nh),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t acc = 0;
+    bool gave_up = false;
+    for (int64_t top = (int64_t)g - 1; top >= 0 && !gave_up; top -= 64) {
+      const int64_t q = top - (int64_t)lane;
+      uint64_t w = 0;
+      if (q >= 0) {
+        uint32_t polls = 0;
+        do {
+          w = ld_agent(&t.status[q]);
+        } while ((uint32_t)(w >> 40) != t.epoch && ++polls < kChainSpin);
+      }
+      const bool here = q < 0 || (uint32_t)(w >> 40) == t.epoch;
+      gave_up = __ballot(!here) != 0;
+      const uint32_t kind = q >= 0 ? (uint32_t)(w >> 38) & 3u : 2u;
+      const uint64_t v = q >= 0 && here ? (w & ((1ull << 38) - 1)) : 0ull;
+      const uint64_t done = __ballot(kind == 2u);  // lanes holding an inclusive word
+      const uint32_t stop = done ? (uint32_t)__ffsll((long long)done) - 1u : 64u;
+      uint64_t mine = lane <= stop ? v : 0ull;
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) mine += __shfl_xor(mine, o);
+      acc += mine;
+      if (done) break;
+    }
+    if (lane == 0) {
+      if (g != 0 && !gave_up)
+        __hip_atomic_store(&t.status[g], chain_word(t.epoch, 2u, acc + nh), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      if (gave_up) sh[0] = 1u;
+      s_prefix = acc;
+    }
+  }
+  __syncthreads();
+  const uint64_t base = s_prefix;
+  // 4. H out in order; each member's successor must be the next member
+  for (uint32_t i = tid; i < nl; i += kChainThreads) {
+    const uint64_t r = base + i;
+    const uint64_t q = lpos[i];
+    const uint32_t L = llen[i];
+    if (r < cap) {
+      rec_off[r] = q;
+      rec_len[r] = L;
+    }
+    if (i + 1 < nl && q + L != lpos[i + 1]) fail = true;
+  }
+  if (__ballot(fail) && lane == 0) atomicOr(&sh[0], 1u);
+  __syncthreads();
+  if (tid == 0) {  // the summary, for the host (after the stream sync)
+    ChainAux a;
+    a.first = nl ? lpos[0] : ~0ull;
+    a.last_succ = nl ? lpos[nl - 1] + llen[nl - 1] : 0ull;
+    a.nh = nh;
+    a.ncand = C;
+    a.fail = sh[0];
+    a.tail_cand = sh[1] >> 1;
+    host_aux[g] = a;
   }
 }
 
@@ -860,22 +1011,24 @@ struct mgenx_scan_ws {
   uint32_t spec_cap = 0;
   const uint64_t* spec_total = nullptr;
   bool spec_pending = false;
-  // the chain hypothesis (scan_mark_*) in speculative whole-stream TCP scans: `pruned` = the
-  // current speculative tables were built for it.  After a stream where it was not the chain
-  // the next prune_skip scans do not try it (backoff 2, 4, ... 64 scans; reset on success)
+  // the chain hypothesis (scan_chain_*) in whole-stream TCP scans once an exact build has
+  // sized spec_cap.  After a stream where it was not the chain the next prune_skip scans do not
+  // try it (backoff 2, 4, ... 64 scans; reset on success)
   uint32_t prune_skip = 0, prune_backoff = 0;
-  bool pruned = false;
-  ScanWork marks;        // [spec_cap] successor marks (epoch) + 3 x [blocks] (MarkTabs)
-  uint32_t epoch = 0;
+  ScanWork chain;        // look-back words + flags + mark table (ChainTabs)
+  uint32_t chain_hmask = 0, chain_epoch = 0;
+  ChainAux* chain_host = nullptr;      // [kChainGroups] emit group summaries (host-mapped)
+  ChainAux* chain_host_dev = nullptr;
 };
 
 extern "C" void* mgenx_scan_ws_new() { return new mgenx_scan_ws(); }
 extern "C" void mgenx_scan_ws_free(void* p) {
   mgenx_scan_ws* w = static_cast<mgenx_scan_ws*>(p);
   if (!w) return;
-  for (ScanWork* x : {&w->slots, &w->cands, &w->tabs, &w->small, &w->marks})
+  for (ScanWork* x : {&w->slots, &w->cands, &w->tabs, &w->small, &w->chain})
     mgenx::dev_free(x->mem);
   mgenx::host_free(w->host);
+  mgenx::host_free(w->chain_host);
   delete w;
 }
 
@@ -901,6 +1054,22 @@ int levels_for(uint64_t n) {
 // bytes of the lifting tables for `stride` candidates and `levels` levels
 size_t tab_bytes(uint32_t stride, int levels) {
   return (size_t)stride * 4 * (2 * (size_t)(levels + 1) + 4 * (size_t)levels);
+}
+
+// the small device area and the host-mapped result words
+int ensure_small(mgenx_scan_ws& ws, const Fail& fail) {
+  hipError_t e;
+  if ((e = ensure(ws.small, 4096)) != hipSuccess) return fail(e, "scan workspace");
+  if (!ws.host) {
+    void* hp = nullptr;
+    if ((e = hipHostMalloc(&hp, 64, hipHostMallocMapped)) != hipSuccess)
+      return fail(e, "scan workspace");
+    ws.host = static_cast<uint64_t*>(hp);
+    void* dp = nullptr;
+    if ((e = hipHostGetDevicePointer(&dp, hp, 0)) != hipSuccess) return fail(e, "scan workspace");
+    ws.host_dev = static_cast<uint64_t*>(dp);
+  }
+  return MGENX_OK;
 }
 
 uint32_t link_grid(uint32_t nb) { return (nb + 4 * kLinkPerWave - 1) / (4 * kLinkPerWave); }
@@ -938,7 +1107,7 @@ void launch_lifts(const mgenx_scan_ws& ws, const uint64_t* spec_total, hipStream
 }
 
 int scan_build(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, int mode, hipStream_t stream,
-               const Fail& fail, bool spec = false, bool prune = false) {
+               const Fail& fail, bool spec = false) {
   const bool sink = mode == MGENX_SCAN_SINK;
   const ScanMode m = sink ? ScanMode{MGENX_MIN_SIZE, MGENX_MAX_SIZE} : ScanMode{4u, 65535u};
   hipError_t e;
@@ -950,17 +1119,7 @@ int scan_build(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, int mode, h
   ws.stride = 0;
   ws.spec_pending = false;
   ws.spec_total = nullptr;
-  ws.pruned = false;
-  if ((e = ensure(ws.small, 4096)) != hipSuccess) return fail(e, "scan workspace");
-  if (!ws.host) {
-    void* hp = nullptr;
-    if ((e = hipHostMalloc(&hp, 64, hipHostMallocMapped)) != hipSuccess)
-      return fail(e, "scan workspace");
-    ws.host = static_cast<uint64_t*>(hp);
-    void* dp = nullptr;
-    if ((e = hipHostGetDevicePointer(&dp, hp, 0)) != hipSuccess) return fail(e, "scan workspace");
-    ws.host_dev = static_cast<uint64_t*>(dp);
-  }
+  if (int rc = ensure_small(ws, fail)) return rc;
   const uint64_t n_blocks64 = (nbytes + kScanBlockBytes - 1) / kScanBlockBytes;
   if (n_blocks64 == 0 || n_blocks64 > 0xFFFFFFull) {  // nothing to index: resolver only
     ws.key_s = s;
@@ -981,8 +1140,6 @@ int scan_build(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, int mode, h
   uint64_t* d_base = d_counts + cnt_b / 8;
   void* d_cub = static_cast<char*>(ws.slots.mem) + slot_b + 2 * cnt_b;
   uint32_t* irregular = reinterpret_cast<uint32_t*>(static_cast<char*>(ws.small.mem) + 2048);
-  // the chain hypothesis (scan_mark_*) only in a speculative TCP build (checked: mgenx_scan_run)
-  const bool do_prune = prune && spec && ws.spec_cap && !sink;
   auto detect = scan_detect_kernel<false>;
 #if MGENX_DIAG
   if (const char* v = getenv("MGENX_SCAN_PLAIN"))
@@ -1019,26 +1176,9 @@ int scan_build(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, int mode, h
     lay_tables(ws, cap, levels);
     ws.spec_total = d_base + nb;
     ws.spec_pending = true;
-    ws.pruned = do_prune;
-    uint32_t* mark = nullptr;
-    if (do_prune) {
-      const size_t mb = ((size_t)cap + 3 * ((size_t)cap / 1024 + 1)) * 4;
-      if (ws.marks.bytes < mb) {
-        if ((e = ensure(ws.marks, mb)) != hipSuccess ||
-            (e = hipMemsetAsync(ws.marks.mem, 0, mb, stream)) != hipSuccess)
-          return fail(e, "scan workspace");
-        ws.epoch = 0;
-      }
-      if (++ws.epoch >= (1u << 30)) {  // 30-bit epochs (2 level bits): wrapped, clear the marks
-        if ((e = hipMemsetAsync(ws.marks.mem, 0, ws.marks.bytes, stream)) != hipSuccess)
-          return fail(e, "scan workspace");
-        ws.epoch = 1;
-      }
-      mark = static_cast<uint32_t*>(ws.marks.mem);
-    }
     hipLaunchKernelGGL(scan_link_kernel, dim3(link_grid(nb)), dim3(256), 0, stream, s, nbytes,
                        d_slots, d_counts, d_base, nb, ws.cand, ws.ups, ws.dists, (uint64_t)cap,
-                       irregular, mark, ws.epoch);
+                       irregular);
     // (the lifting levels follow only when the chain is not the candidate list itself:
     // mgenx_scan_run, after its one sync)
     if ((e = hipGetLastError()) != hipSuccess) return fail(e, "scan launch");
@@ -1163,6 +1303,121 @@ int scan_walk(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, int mode, ui
   return MGENX_OK;
 }
 
+
+// The chain hypothesis (scan_chain_*) on a whole TCP stream: detect, the marks and the emit
+// pass, one sync.  ok = false: H was not the chain (nothing is left to reuse; the
+// caller builds exactly).  Emit groups: enough that each holds about 2048 candidates of the
+// last exact build (spec_cap) and at most kChainBlocks detect blocks.
+bool chain_fits(const mgenx_scan_ws& ws, uint64_t nbytes) {
+  const uint64_t nb = (nbytes + kScanBlockBytes - 1) / kScanBlockBytes;
+  return ws.spec_cap != 0 && nb != 0 && nb <= (uint64_t)kChainGroups * kChainBlocks &&
+         nbytes < (1ull << 40);
+}
+
+int scan_chain(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, uint64_t* rec_off,
+               uint32_t* rec_len, uint64_t cap, mgenx_scan_info* info, hipStream_t stream,
+               const Fail& fail, bool& ok) {
+  ok = false;
+  ws.key_s = nullptr;  // no candidate tables on this path
+  ws.n = 0;
+  ws.levels = 0;
+  ws.cand = nullptr;
+  ws.ups = ws.dists = nullptr;
+  ws.stride = 0;
+  ws.spec_pending = false;
+  ws.spec_total = nullptr;
+  if (int rc = ensure_small(ws, fail)) return rc;
+  hipError_t e;
+  if (!ws.chain_host) {
+    void* hp = nullptr;
+    if ((e = hipHostMalloc(&hp, kChainGroups * sizeof(ChainAux), hipHostMallocMapped)) !=
+        hipSuccess)
+      return fail(e, "scan workspace");
+    ws.chain_host = static_cast<ChainAux*>(hp);
+    void* dp = nullptr;
+    if ((e = hipHostGetDevicePointer(&dp, hp, 0)) != hipSuccess) return fail(e, "scan workspace");
+    ws.chain_host_dev = static_cast<ChainAux*>(dp);
+  }
+  const uint32_t nb = (uint32_t)((nbytes + kScanBlockBytes - 1) / kScanBlockBytes);
+  const size_t slot_b = align256((size_t)nb * kScanSlots * 4);
+  const size_t cnt_b = align256((size_t)(nb + 1) * 8);
+  if ((e = ensure(ws.slots, slot_b + 2 * cnt_b)) != hipSuccess) return fail(e, "scan workspace");
+  uint32_t* d_slots = static_cast<uint32_t*>(ws.slots.mem);
+  uint64_t* d_counts = reinterpret_cast<uint64_t*>(static_cast<char*>(ws.slots.mem) + slot_b);
+  uint32_t groups = std::max<uint32_t>((nb + kChainBlocks - 1) / kChainBlocks,
+                                       (ws.spec_cap + 2047) / 2048);
+  groups = std::min(std::max(groups, 1u), kChainGroups);
+  const uint32_t per_group = (nb + groups - 1) / groups;
+  groups = (nb + per_group - 1) / per_group;
+  // mark table: a power of two >= 2 x the expected candidates; look-back words, summaries and
+  // flags first (fixed offsets), so a table that only grows keeps them
+  uint32_t hs = 4096;
+  while (hs < 2ull * ws.spec_cap && hs < (1u << 30)) hs <<= 1;
+  const size_t head = align256((size_t)kChainGroups * 8 + 64);
+  if (!ws.chain.mem || hs - 1 > ws.chain_hmask) {
+    const size_t need = head + (size_t)hs * 8;
+    if ((e = ensure(ws.chain, need)) != hipSuccess ||
+        (e = hipMemsetAsync(ws.chain.mem, 0, ws.chain.bytes, stream)) != hipSuccess)
+      return fail(e, "scan workspace");
+    ws.chain_hmask = (uint32_t)((ws.chain.bytes - head) / 8);  // (a power of two below)
+    uint32_t m = 1;
+    while ((uint64_t)m * 2 <= ws.chain_hmask) m <<= 1;
+    ws.chain_hmask = m - 1;
+    ws.chain_epoch = 0;
+  }
+  if (++ws.chain_epoch >= kChainEpochs) {  // 8-bit epochs: wrapped, clear every entry
+    if ((e = hipMemsetAsync(ws.chain.mem, 0, ws.chain.bytes, stream)) != hipSuccess)
+      return fail(e, "scan workspace");
+    ws.chain_epoch = 1;
+  }
+  char* base = static_cast<char*>(ws.chain.mem);
+  ChainTabs t;
+  t.status = reinterpret_cast<uint64_t*>(base);
+  t.flags = reinterpret_cast<uint32_t*>(base + (size_t)kChainGroups * 8);
+  t.hash = reinterpret_cast<uint64_t*>(base + head);
+  t.hmask = ws.chain_hmask;
+  t.epoch = ws.chain_epoch;
+  const ScanMode m{4u, 65535u};
+  hipLaunchKernelGGL(scan_detect_kernel<false>, dim3(nb), dim3(kScanThreads), 0, stream, s,
+                     nbytes, m, d_slots, d_counts, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                     (uint32_t*)nullptr);
+  hipLaunchKernelGGL(scan_chain_mark_kernel, dim3(link_grid(nb)), dim3(256), 0, stream, s, nbytes,
+                     (const uint32_t*)d_slots, (const uint64_t*)d_counts, nb, t);
+  hipLaunchKernelGGL(scan_chain_emit_kernel, dim3(groups), dim3(kChainThreads), 0, stream,
+                     (const uint32_t*)d_slots, (const uint64_t*)d_counts, nbytes, nb, per_group, t,
+                     cap, rec_off, rec_len, ws.chain_host_dev);
+  if ((e = hipGetLastError()) != hipSuccess) return fail(e, "scan launch");
+  if ((e = hipStreamSynchronize(stream)) != hipSuccess) return fail(e, "scan");
+  // the joins between groups: each nonempty group starts where the previous one's last member
+  // ends, the first starts at 0, the last one's successor is not a candidate
+  const volatile ChainAux* ha = ws.chain_host;
+  uint64_t th = 0, tc = 0, next = 0;
+  bool bad = false, any = false, tail = false;
+  for (uint32_t g = 0; g < groups; g++) {
+    const uint32_t nh = ha[g].nh;
+    tc += ha[g].ncand;
+    bad = bad || ha[g].fail != 0u;
+    if (!nh) continue;
+    bad = bad || ha[g].first != next;  // (next = 0 before the first nonempty group)
+    any = true;
+    th += nh;
+    next = ha[g].last_succ;
+    tail = ha[g].tail_cand != 0u;
+  }
+  if (bad || !any || tail) return MGENX_OK;
+  ok = true;
+  const uint64_t cands = tc;
+  const ChainEnd h = {th, next, 0};
+  // H is the chain from 0; what follows its terminal goes to the sequential resolver
+  const int rc = scan_walk(ws, s, nbytes, MGENX_SCAN_TCP, 0, nbytes, rec_off, rec_len, cap, info,
+                           stream, fail, &h);
+  if (info) {
+    info->candidates = (uint32_t)std::min<uint64_t>(cands, 0xFFFFFFFFu);
+    info->path = 2;
+  }
+  return rc;
+}
+
 }  // namespace
 
 // Whole-stream scan from offset 0 (synchronous on `stream`).
@@ -1173,7 +1428,22 @@ extern "C" int mgenx_scan_run(void* wsp, const uint8_t* s, uint64_t nbytes, int 
   const Fail fail{err, errn};
   const bool try_chain = ws.prune_skip == 0;
   if (ws.prune_skip) ws.prune_skip--;
-  int rc = scan_build(ws, s, nbytes, mode, stream, fail, /*spec=*/true, /*prune=*/try_chain);
+  int rc;
+  if (try_chain && mode != MGENX_SCAN_SINK && chain_fits(ws, nbytes)) {
+    bool ok = false;
+    rc = scan_chain(ws, s, nbytes, rec_off, rec_len, cap, info, stream, fail, ok);
+    if (rc != MGENX_OK || ok) {
+      if (ok) ws.prune_backoff = 0;
+      return rc;
+    }
+    // the hypothesis is not the chain (or not provably): exact build, and a backoff
+    ws.prune_backoff = std::min(std::max(2u * ws.prune_backoff, 2u), 64u);
+    ws.prune_skip = ws.prune_backoff;
+    rc = scan_build(ws, s, nbytes, mode, stream, fail, false);
+    if (rc != MGENX_OK) return rc;
+    return scan_walk(ws, s, nbytes, mode, 0, nbytes, rec_off, rec_len, cap, info, stream, fail);
+  }
+  rc = scan_build(ws, s, nbytes, mode, stream, fail, /*spec=*/true);
   if (rc != MGENX_OK) return rc;
   if (ws.spec_pending) {
     // one sync for the whole scan: the chain from offset 0 enumerated on the speculative
@@ -1184,37 +1454,19 @@ extern "C" int mgenx_scan_run(void* wsp, const uint8_t* s, uint64_t nbytes, int 
     const uint32_t* irregular =
         reinterpret_cast<const uint32_t*>(static_cast<char*>(ws.small.mem) + 2048);
     uint32_t* regular = reinterpret_cast<uint32_t*>(static_cast<char*>(ws.small.mem) + 2052);
-    const bool pruned = ws.pruned;
-    if (pruned) {
-      uint32_t* mark = static_cast<uint32_t*>(ws.marks.mem);
-      const uint32_t blocks = scap / 1024 + 1;
-      const MarkTabs mt = {mark, ws.epoch, mark + scap, mark + scap + blocks,
-                           mark + scap + 2 * blocks};
-      hipLaunchKernelGGL(scan_mark_next_kernel, dim3(blocks), dim3(1024), 0, stream, ws.ups,
-                         ws.spec_total, scap, mt);
-      hipLaunchKernelGGL(scan_mark_count_kernel, dim3(blocks), dim3(1024), 0, stream,
-                         ws.spec_total, scap, mt);
-      hipLaunchKernelGGL(scan_mark_emit_kernel, dim3(blocks), dim3(1024), 0, stream, s, ws.cand,
-                         ws.ups, ws.spec_total, scap, cap, rec_off, rec_len, mt);
-      hipLaunchKernelGGL(scan_mark_final_kernel, dim3(1), dim3(256), 0, stream, s, ws.cand,
-                         ws.spec_total, scap, blocks, mt, d_end, ws.host_dev + 5);
-    } else {
-      hipLaunchKernelGGL(scan_enum_regular_kernel, dim3((scap + 255) / 256), dim3(256), 0, stream,
-                         s, ws.cand, ws.spec_total, irregular, scap, cap, rec_off, rec_len, d_end,
-                         regular, ws.host_dev + 5);
-    }
+    hipLaunchKernelGGL(scan_enum_regular_kernel, dim3((scap + 255) / 256), dim3(256), 0, stream,
+                       s, ws.cand, ws.spec_total, irregular, scap, cap, rec_off, rec_len, d_end,
+                       regular, ws.host_dev + 5);
     // not the regular chain: the lifting levels on the speculative tables, then the
     // enumeration from offset 0 -- launched regardless, each returning at once when the
     // regular kernel already reported the chain.  (Deciding on the host instead costs a
     // second round trip whenever payloads hold plausible record starts -- the TCP transmit
     // stream's repeated 8-KiB buffers each begin with a header -- 0.306 -> 0.323 ms on
-    // config 5.)  A pruned build is used only as the regular chain: no lifting on it.
-    if (!pruned) {
-      launch_lifts(ws, ws.spec_total, stream, regular);
-      hipLaunchKernelGGL(scan_enum_kernel, dim3((scap + 255) / 256), dim3(256), 0, stream, s,
-                         ws.cand, lift_tabs(ws), ws.spec_total, 0u, 1, nbytes, (uint64_t)0, cap,
-                         rec_off, rec_len, d_end, (const uint32_t*)regular);
-    }
+    // config 5.)
+    launch_lifts(ws, ws.spec_total, stream, regular);
+    hipLaunchKernelGGL(scan_enum_kernel, dim3((scap + 255) / 256), dim3(256), 0, stream, s,
+                       ws.cand, lift_tabs(ws), ws.spec_total, 0u, 1, nbytes, (uint64_t)0, cap,
+                       rec_off, rec_len, d_end, (const uint32_t*)regular);
     hipError_t e;
     if ((e = hipStreamSynchronize(stream)) != hipSuccess) return fail(e, "scan");
     uint32_t tot[2];
@@ -1224,14 +1476,6 @@ extern "C" int mgenx_scan_run(void* wsp, const uint8_t* s, uint64_t nbytes, int 
     const bool regular_chain = ((const volatile uint64_t*)ws.host)[5] != 0;
     // the regular chain skipped the lifting: these tables are not for mgenx_scan_range reuse
     if (regular_chain) ws.key_s = nullptr;
-    if (pruned && !regular_chain) {
-      // the hypothesis is not the chain (or not provably): exact build, and a backoff
-      ws.prune_backoff = std::min(std::max(2u * ws.prune_backoff, 2u), 64u);
-      ws.prune_skip = ws.prune_backoff;
-      rc = scan_build(ws, s, nbytes, mode, stream, fail, false);
-      if (rc != MGENX_OK) return rc;
-      return scan_walk(ws, s, nbytes, mode, 0, nbytes, rec_off, rec_len, cap, info, stream, fail);
-    }
     if (tot[1] || tot[0] > scap || tot[0] > max_cand) {
       // the tables did not hold the stream: exact build (sizes the next speculation)
       rc = scan_build(ws, s, nbytes, mode, stream, fail, false);
@@ -1239,20 +1483,6 @@ extern "C" int mgenx_scan_run(void* wsp, const uint8_t* s, uint64_t nbytes, int 
       return scan_walk(ws, s, nbytes, mode, 0, nbytes, rec_off, rec_len, cap, info, stream, fail);
     }
     ws.n = tot[0];
-    if (pruned) {
-      ws.prune_backoff = 0;
-      // H is the chain from 0; what follows its terminal goes to the sequential resolver
-      // with no candidate set (no lifting tables were built on the pruned set)
-      const uint32_t n_pruned = ws.n;
-      ws.n = 0;
-      const ChainEnd h = {h_end[0], h_end[1], h_end[2]};
-      rc = scan_walk(ws, s, nbytes, mode, 0, nbytes, rec_off, rec_len, cap, info, stream, fail, &h);
-      if (info) {
-        info->candidates = n_pruned;
-        info->path = 2;
-      }
-      return rc;
-    }
     if (ws.n) {
       const ChainEnd h = {h_end[0], h_end[1], h_end[2]};
       // a chain as long as the levels reach (the descent covers 4^levels - 1 jumps) may go

@@ -43,4 +43,16 @@ for _ in range(reps):
 torch.cuda.synchronize()
 assert int(info.n_records) == n, int(info.n_records)
 print("scan_ms", (time.perf_counter() - t0) / reps * 1e3, int(info.n_records), flush=True)
+# the C entry point alone (arguments prepared once): what the Python wrapper adds
+import ctypes  # noqa: E402
+from mgen_amd import _ptr, _stream  # noqa: E402
+from mgen_amd._abi import ScanInfo  # noqa: E402
+args = (eng.ctx, _ptr(local), local.numel(), SCAN_TCP, _ptr(out[0]), _ptr(out[1]), out[0].numel())
+st = _stream(0)
+inf = ScanInfo()
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+for _ in range(reps):
+    eng.lib.mgenx_stream_scan(*args, ctypes.byref(inf), st)
+print("c_call_ms", (time.perf_counter() - t0) / reps * 1e3, int(inf.n_records), int(inf.path), flush=True)
 eng.close()
