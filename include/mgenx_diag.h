@@ -53,6 +53,11 @@ int mgenx_diag_seg_prof(unsigned long long* out, int n);
  * to the reply (out[7] = the request number); out holds 8 words. */
 int mgenx_diag_worker_stamps(const mgenx_worker* w, uint32_t* out);
 
+/* Diagnostic: s_memtime stamps of the scan's chain kernel (scan_chain_kernel), thread 0 of
+ * groups 0..63, 8 per group: start, counts prefix, marks, H list, look-back, end; out holds
+ * 512 words. */
+int mgenx_diag_chain_prof(unsigned long long* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -48,7 +48,8 @@ EXPORTED_SYMBOLS = (
     "mgenx_worker_flow_update",
 )
 DIAG_SYMBOLS = ("mgenx_set_tuning", "mgenx_diag_stream_read", "mgenx_diag_group_rw",
-                "mgenx_diag_seg_prof", "mgenx_diag_stream_read_w", "mgenx_diag_worker_stamps")
+                "mgenx_diag_seg_prof", "mgenx_diag_stream_read_w", "mgenx_diag_worker_stamps",
+                "mgenx_diag_chain_prof")
 
 
 class MgenxError(RuntimeError):
@@ -113,6 +114,7 @@ def load(diag: bool = False):
         L.mgenx_diag_seg_prof.argtypes = [P, i32]
         L.mgenx_diag_stream_read_w.argtypes = [P, P, u64, P, i32, i32, P]
         L.mgenx_diag_worker_stamps.argtypes = [P, P]
+        L.mgenx_diag_chain_prof.argtypes = [P]
     L.mgenx_stream_scan.argtypes = [P, P, u64, i32, P, P, u64, ctypes.POINTER(ScanInfo), P]
     L.mgenx_tcp_rx_persist.argtypes = [P, P, P, P, u32, P, P, P, u32, P]
     L.mgenx_report_build.argtypes = [P, P, u32, u32, P, P, P, P, P, P, P]
@@ -156,7 +158,7 @@ def _ptr(t):
 
 def _stream(device):
     import torch
-    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+    return ctypes.c_void_p(torch._C._cuda_getCurrentRawStream(device))
 
 
 class Engine:

@@ -25,8 +25,11 @@
 // the chain would compute anyway.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <immintrin.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 
 #include <stdio.h>
 #include <stdlib.h>
@@ -388,159 +391,105 @@ scan_enum_regular_kernel(const uint8_t* __restrict__ s, const uint64_t* __restri
 // link and no lifting.  (Config 5's stream is not regular: the TCP sender re-sends each
 // message's 8-KiB Pack buffer, so every message carries a copy of its header 8192 bytes on.)
 // A hypothesis H is guessed from successor marks and then PROVED:
-//   marks: every candidate p that is not a header copy (is_copy) marks its successor q = p + L
-//   and leaves its length L there (a position marked by two different candidates keeps none);
+//   marks: every candidate p that is not a header copy (the slot's copy bit) marks its
+//   successor q = p + L when q is a candidate (a candidate marked by two keeps no marker);
 //   H = {0} and every marked candidate whose marker is 0 or itself marked (or is not known).
 //   (Junk starts inside headers chain in short runs -- seq 0x802 reads as a length-8 record at
 //   header offset 9 whose successor at 17 is tx_usec's same bytes -- and nothing marks the
 //   junk start, so its successor stays out.)
 // H is the chain from offset 0 exactly when 0 is in H, each member's successor is the next
-// member in position order and the last member's successor is not a candidate: the emit pass
-// checks that while it writes H out in order; otherwise the host rebuilds exactly.  The marks
-// are keyed by stream POSITION in an open-addressing table whose entries carry this scan's
-// epoch (cleared once per 255 scans), so no candidate needs a global number: no block-count
-// scan, no link, and the ranks of H come from one decoupled look-back over the emit groups.
-struct ChainAux {  // one emit group's summary, for the host
+// member in position order and the last member's successor is not a candidate: the kernel
+// checks the first two within each group while it writes H out in order, the host the joins
+// between groups and the last successor; otherwise the host rebuilds exactly.
+// A record is shorter than 64 KiB = 2 detect blocks, so every mark that decides H for a group's
+// candidates comes from its own detect blocks or the 4 before them: each group loads those
+// candidates into LDS and marks there -- no candidate numbering across groups, no table in
+// memory, no wait on other groups except the ranks (one decoupled look-back).
+struct ChainAux {  // one group's summary, for the host
   uint64_t first, last_succ;  // position of its first H member; successor of its last
   uint32_t nh, ncand, fail, tail_cand;  // tail_cand: last_succ is a candidate
+  uint32_t epoch, pad;  // written last: the group is done (its records are out)
 };
-struct ChainTabs {
-  uint64_t* hash;    // [hmask + 1]: epoch << 56 | pos << 16 | marker length; 0 = never used
-  uint32_t hmask, epoch;  // epoch: 1 .. 255
-  uint32_t* flags;   // [2] = epoch: a mark of that scan found no free entry
-  uint64_t* status;  // [groups] look-back words: epoch << 40 | kind << 38 | H count
-};
-constexpr int kChainProbes = 32;
-constexpr uint32_t kChainEpochs = 256;
+constexpr uint32_t kChainEpochs = 1u << 22;  // look-back words: epoch << 40 | kind << 38 | count
 constexpr uint32_t kChainThreads = 1024;
-constexpr uint32_t kChainBlocks = 4096;  // detect blocks per emit group at most
-constexpr uint32_t kChainList = 4096;    // H members per emit group at most (else: not proved)
-constexpr uint32_t kChainPer = 4;        // candidates per thread and round
+constexpr uint32_t kChainBlocks = 1024;  // detect blocks per group at most (4 more are loaded)
+constexpr uint32_t kChainCands = 4096;   // candidates per group at most, incl. the 4 blocks before
+constexpr uint32_t kChainPer = kChainCands / kChainThreads;
+constexpr uint32_t kChainBack = 4;       // detect blocks before a group's own whose marks count
+constexpr uint32_t kChainAhead = 2;      // and after them (the last member's successor)
 constexpr uint32_t kChainGroups = 1024;
+constexpr uint32_t kChainSpin = 1u << 18;  // polls of another group's word before giving up
+constexpr uint32_t kMarkMulti = 0xFFFFFFFFu;  // marked by two candidates
 
-__device__ __forceinline__ uint32_t chain_slot(uint64_t pos, uint32_t hmask) {
-  return (uint32_t)((pos * 0x9E3779B97F4A7C15ull) >> 32) & hmask;
-}
 __device__ __forceinline__ uint64_t ld_agent(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// mark position q with its marker's length L; false when no entry is free within the probe
-// bound.  Linear probing with no deletions: an insert skips only entries of this epoch, so every
-// entry before a key's own on its probe path is of this epoch and a lookup may stop at a stale
-// one.  The CAS decides; a stale first read only costs a retry.
-__device__ bool chain_mark(const ChainTabs& t, uint64_t q, uint32_t L) {
-  const uint64_t key = ((uint64_t)t.epoch << 40) | q;
-  const uint32_t h = chain_slot(q, t.hmask);
-  for (int k = 0; k < kChainProbes; k++) {
-    unsigned long long* a = (unsigned long long*)(t.hash + ((h + k) & t.hmask));
-    uint64_t e = ld_agent((const uint64_t*)a);
-    for (;;) {
-      if ((e >> 56) == t.epoch) {
-        if ((e >> 16) != key) break;  // another position's: next entry
-        const uint32_t d = (uint32_t)(e & 0xFFFFu);
-        if (d != 0u && d != L) atomicAnd(a, ~0xFFFFull);  // two markers: keep none
-        return true;
-      }
-      const uint64_t prev = atomicCAS(a, (unsigned long long)e, (unsigned long long)((key << 16) | L));
-      if (prev == e) return true;  // claimed a stale entry
-      e = prev;                    // raced: look at what is there now
-    }
-  }
-  return false;
-}
-// the marker length at q (0: marked by two), or -1: unmarked
-__device__ __forceinline__ int32_t chain_marker(const ChainTabs& t, uint64_t q) {
-  const uint64_t key = ((uint64_t)t.epoch << 40) | q;
-  const uint32_t h = chain_slot(q, t.hmask);
-  for (int k = 0; k < kChainProbes; k++) {
-    const uint64_t e = t.hash[(h + k) & t.hmask];
-    if ((e >> 56) != t.epoch) return -1;
-    if ((e >> 16) == key) return (int32_t)(e & 0xFFFFu);
-  }
-  return -1;
-}
 
-// the marks from the detect slots, 16 lanes per detect block (the link kernel's geometry).  A
-// block that overflowed its slots has none: the emit pass fails H then.
-__global__ void __launch_bounds__(256)
-scan_chain_mark_kernel(const uint8_t* __restrict__ s, uint64_t nbytes,
-                       const uint32_t* __restrict__ slots, const uint64_t* __restrict__ counts,
-                       uint32_t n_blocks, ChainTabs t) {
-  const uint32_t b =
-      (blockIdx.x * 4 + (threadIdx.x >> 6)) * kLinkPerWave + ((threadIdx.x & 63u) >> 4);
-  const uint32_t sub = threadIdx.x & 15u;
-  if (b >= n_blocks) return;
-  const uint64_t cw = counts[b];
-  if (cw >> 32) return;
-  const uint32_t c = (uint32_t)cw;
-  bool full = false;
-  for (uint32_t k = sub; k < c; k += 16) {
-    const uint32_t sl = slots[(size_t)b * kScanSlots + k];  // offset | length << 16
-    const uint64_t p = (uint64_t)b * kScanBlockBytes + (sl & kSlotOff);
-    const uint64_t q = p + (sl >> 16);
-    if (q < nbytes && !(sl & kSlotCopy) && !chain_mark(t, q, sl >> 16)) full = true;
-  }
-  if (full) t.flags[2] = t.epoch;
-}
-
-// is position q a candidate (in its detect block's slots; an overflowed block: unknown, yes)
-__device__ bool chain_is_cand(const uint32_t* __restrict__ slots, const uint64_t* __restrict__ counts,
-                              uint32_t n_blocks, uint64_t nbytes, uint64_t q) {
-  if (q >= nbytes) return false;
-  const uint64_t bq = q / kScanBlockBytes;
-  if (bq >= n_blocks) return false;
-  const uint64_t cw = counts[bq];
-  if (cw >> 32) return true;
-  const uint32_t* ts = slots + (size_t)bq * kScanSlots;
-  const uint32_t key = (uint32_t)(q % kScanBlockBytes);
-  uint32_t lo = 0, hi = (uint32_t)cw;
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if ((ts[mid] & kSlotOff) < key) lo = mid + 1; else hi = mid;
-  }
-  return lo < (uint32_t)cw && (ts[lo] & kSlotOff) == key;
-}
-
-// H in position order: emit group g takes detect blocks [g per_group, (g + 1) per_group): their
-// candidate counts -> an exclusive prefix in LDS, each candidate j of the group -> (block, slot)
-// by a binary search of it, its marks, and the H members -> an LDS list by ballot ranks.  The
-// group's H count goes out as an aggregate, a decoupled look-back over the earlier groups gives
-// its first rank (bounded: a group that never publishes -- dispatch order is not promised --
-// makes this one give up and fail the scan, which the exact path then redoes), and the list is
-// written to rec_off / rec_len while each member's successor is compared with the next member.
-// Each group's summary goes to host memory (ChainAux): the host checks the joins between
-// groups, that 0 is in H and that the last member's successor is not a candidate.
 __device__ __forceinline__ uint64_t chain_word(uint32_t epoch, uint32_t kind, uint64_t v) {
   return ((uint64_t)epoch << 40) | ((uint64_t)kind << 38) | v;
 }
-constexpr uint32_t kChainSpin = 1u << 18;  // look-back polls before giving up
+
+#if MGENX_DIAG
+// s_memtime at the phase ends of scan_chain_kernel, thread 0 of groups 0..63 (diagnostics)
+__device__ unsigned long long g_chain_prof[64 * 8];
+#define CHAIN_STAMP(k)                                                                 \
+  do {                                                                                 \
+    if (tid == 0 && g < 64) g_chain_prof[g * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define CHAIN_STAMP(k) \
+  do {                 \
+  } while (0)
+#endif
+
+// One kernel after detect.  Group g owns detect blocks [g per_group, (g + 1) per_group) and
+// loads the candidates of those and the kChainBack blocks before them into LDS (positions
+// relative to the first loaded block, copy bit in bit 31, lengths):
+//  1. the loaded blocks' candidate counts -> an exclusive prefix; candidate j -> (block, slot)
+//     by a binary search of it;
+//  2. marks: each non-copy candidate finds its successor among the loaded positions (binary
+//     search) and marks it with its own index (an LDS CAS; a second marker leaves kMarkMulti);
+//  3. the H members among its own candidates -> an LDS index list by ballot ranks;
+//  4. its H count as an aggregate, a decoupled look-back over the earlier groups for its first
+//     rank (bounded: dispatch order is not promised -- a group that gives up fails the scan,
+//     which the host then redoes on the exact path), the list out to rec_off / rec_len, each
+//     member's successor compared with the next;
+//  5. its summary to host memory.
 __global__ void __launch_bounds__(kChainThreads)
-scan_chain_emit_kernel(const uint32_t* __restrict__ slots, const uint64_t* __restrict__ counts,
-                       uint64_t nbytes, uint32_t n_blocks, uint32_t per_group, ChainTabs t,
-                       uint64_t cap, uint64_t* __restrict__ rec_off, uint32_t* __restrict__ rec_len,
-                       ChainAux* __restrict__ host_aux) {
-  __shared__ uint32_t pre[kChainBlocks + 1];
-  __shared__ uint64_t lpos[kChainList];
-  __shared__ uint16_t llen[kChainList];
+scan_chain_kernel(const uint32_t* __restrict__ slots, const uint64_t* __restrict__ counts,
+                  uint64_t nbytes, uint32_t n_blocks, uint32_t per_group, uint32_t epoch,
+                  uint64_t* __restrict__ status, uint64_t cap, uint64_t* __restrict__ rec_off,
+                  uint32_t* __restrict__ rec_len, ChainAux* __restrict__ host_aux) {
+  __shared__ uint32_t pre[kChainBlocks + kChainBack + kChainAhead + 1];
+  __shared__ uint32_t cpos[kChainCands];   // position - bx * block bytes | copy << 31
+  __shared__ uint16_t clen[kChainCands];
+  __shared__ uint32_t cmark[kChainCands];  // 0: unmarked; marker index + 1; kMarkMulti
+  __shared__ uint16_t hlist[kChainCands];  // H members (indices), in order
+  __shared__ uint16_t cblk[kChainCands];   // candidate -> loaded block
   __shared__ uint32_t wsum[kChainThreads / 64];
+  __shared__ uint32_t wsum4[kChainPer][kChainThreads / 64];
   __shared__ uint32_t sh[2];  // fail, tail candidate
   __shared__ uint64_t s_prefix;
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
   constexpr uint32_t kW = kChainThreads / 64;
   const uint32_t g = blockIdx.x;
   const uint32_t b0 = min(g * per_group, n_blocks), b1 = min(b0 + per_group, n_blocks);
-  const uint32_t nblk = b1 - b0;
+  const uint32_t bx = b0 >= kChainBack ? b0 - kChainBack : 0u;  // first loaded block
+  const uint32_t nblk = min(b1 + kChainAhead, n_blocks) - bx;     // loaded blocks
+  const uint64_t base_pos = (uint64_t)bx * kScanBlockBytes;
+  CHAIN_STAMP(0);
   if (tid == 0) {
-    sh[0] = t.flags[2] == t.epoch ? 1u : 0u;  // a mark found no free entry
+    sh[0] = 0u;
     sh[1] = 0u;
   }
-  // 1. candidate counts -> exclusive prefix (thread t owns K <= 4 consecutive entries)
+  // 1. candidate counts -> exclusive prefix (thread t owns K <= 3 consecutive entries)
   bool fail = false;
   for (uint32_t i = tid; i < nblk; i += kChainThreads) {
-    const uint64_t w = counts[b0 + i];
+    const uint64_t w = counts[bx + i];
     pre[i] = (uint32_t)w;
     fail = fail || (w >> 32) != 0u;  // an overflowed block has no slots
   }
+  for (uint32_t i = tid; i < kChainCands; i += kChainThreads) cmark[i] = 0u;
   __syncthreads();
   const uint32_t K = (nblk + kChainThreads - 1) / kChainThreads;
   const uint32_t i0 = min(tid * K, nblk), i1 = min(i0 + K, nblk);
@@ -568,79 +517,133 @@ scan_chain_emit_kernel(const uint32_t* __restrict__ slots, const uint64_t* __res
   }
   if (tid == 0) pre[nblk] = C;
   __syncthreads();
-  // 2. the H members in position order (round r: candidates j0 + u 1024 + tid, u-major)
-  uint32_t nh = 0;
-  for (uint32_t j0 = 0; j0 < C; j0 += kChainThreads * kChainPer) {
-    uint32_t sl[kChainPer], blk[kChainPer];
+  const uint32_t own0 = pre[b0 - bx], own1 = pre[b1 - bx];  // the own candidates
+  CHAIN_STAMP(1);
+  if (C > kChainCands) {
+    fail = true;  // (a denser group than planned for: not proved here)
+    C = 0;
+  }
+  // candidate -> its loaded block (thread t writes block t's run of indices)
+  for (uint32_t i = tid; i < nblk && C; i += kChainThreads)
+    for (uint32_t j = pre[i]; j < pre[i + 1]; j++) cblk[j] = (uint16_t)i;
+  __syncthreads();
+  // candidates -> LDS (candidate j = u 1024 + tid; every round's addresses first, then the
+  // loads side by side)
+  uint32_t pos[kChainPer], len[kChainPer];
+  {
+    size_t at[kChainPer];
+    uint32_t blk[kChainPer];
 #pragma unroll
     for (uint32_t u = 0; u < kChainPer; u++) {
-      const uint32_t j = j0 + u * kChainThreads + tid;
-      sl[u] = 0u;
-      blk[u] = 0u;
+      const uint32_t j = min(u * kChainThreads + tid, C ? C - 1u : 0u);
+      blk[u] = C ? cblk[j] : 0u;
+      at[u] = (size_t)(bx + blk[u]) * kScanSlots + (j - pre[blk[u]]);
+    }
+    uint32_t sl[kChainPer];
+#pragma unroll
+    for (uint32_t u = 0; u < kChainPer; u++) sl[u] = C ? slots[at[u]] : 0u;
+#pragma unroll
+    for (uint32_t u = 0; u < kChainPer; u++) {
+      const uint32_t j = u * kChainThreads + tid;
+      pos[u] = blk[u] * kScanBlockBytes + (sl[u] & kSlotOff);
+      len[u] = sl[u] >> 16;
       if (j < C) {
-        uint32_t lo = 0, hi = nblk;  // the last block whose prefix is <= j
-        while (lo < hi) {
-          const uint32_t mid = (lo + hi + 1) >> 1;
-          if (pre[mid] <= j) lo = mid; else hi = mid - 1;
-        }
-        blk[u] = b0 + lo;
-        sl[u] = slots[(size_t)(b0 + lo) * kScanSlots + (j - pre[lo])];
+        cpos[j] = pos[u] | ((sl[u] & kSlotCopy) ? 0x80000000u : 0u);
+        clen[j] = (uint16_t)len[u];
       }
-    }
-    // H: marked, and its marker is 0, marked too, or not known (two markers)
-    uint64_t p[kChainPer];
-    int32_t d[kChainPer];
-#pragma unroll
-    for (uint32_t u = 0; u < kChainPer; u++) {
-      const uint32_t j = j0 + u * kChainThreads + tid;
-      p[u] = (uint64_t)blk[u] * kScanBlockBytes + (sl[u] & kSlotOff);
-      d[u] = j < C && p[u] != 0 ? chain_marker(t, p[u]) : -1;
-    }
-    uint32_t hm = 0;
-#pragma unroll
-    for (uint32_t u = 0; u < kChainPer; u++) {
-      const uint32_t j = j0 + u * kChainThreads + tid;
-      bool h = j < C && p[u] == 0;
-      if (d[u] == 0 || (d[u] > 0 && p[u] == (uint64_t)d[u])) h = true;
-      else if (d[u] > 0) h = chain_marker(t, p[u] - (uint32_t)d[u]) >= 0;
-      hm |= h ? 1u << u : 0u;
-    }
-#pragma unroll
-    for (uint32_t u = 0; u < kChainPer; u++) {
-      if (j0 + u * kChainThreads >= C) break;
-      const uint64_t bal = __ballot((hm >> u) & 1u);
-      if (lane == 0) wsum[wv] = (uint32_t)__popcll(bal);
-      __syncthreads();
-      uint32_t before = 0, all = 0;
-#pragma unroll
-      for (uint32_t k = 0; k < kW; k++) {
-        before += k < wv ? wsum[k] : 0u;
-        all += wsum[k];
-      }
-      if ((hm >> u) & 1u) {
-        const uint32_t r = nh + before +
-            __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-                                      __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-        if (r < kChainList) {
-          lpos[r] = p[u];
-          llen[r] = (uint16_t)(sl[u] >> 16);
-        }
-      }
-      nh += all;
-      __syncthreads();  // wsum reused by the next u
+      if (j >= C || (sl[u] & kSlotCopy)) len[u] = 0u;  // (a copy marks nothing)
     }
   }
-  fail = fail || nh > kChainList;
-  const uint32_t nl = min(nh, kChainList);
-  // 3. this group's first rank: aggregate out, decoupled look-back (wave 0), inclusive out;
-  // meanwhile wave 1 asks whether the last member's successor is a candidate (which only
-  // matters for the last nonempty group: there it must not be)
-  if (wv == 1 && lane == 0 && nl)
-    sh[1] = chain_is_cand(slots, counts, n_blocks, nbytes, lpos[nl - 1] + llen[nl - 1]) ? 2u : 0u;
+  __syncthreads();
+  // the index of loaded position q (relative), or kNone: its block's run of candidates, the
+  // first 8 compared side by side, a binary search past them
+  auto find = [&](uint32_t q) -> uint32_t {
+    const uint32_t qb = q / kScanBlockBytes;
+    if (qb >= nblk) return kNone;
+    const uint32_t lo = pre[qb], hi = pre[qb + 1];
+    uint32_t hit = kNone;
+#pragma unroll
+    for (uint32_t k = 0; k < 8; k++) {
+      const uint32_t i = min(lo + k, kChainCands - 1u);
+      if (lo + k < hi && (cpos[i] & 0x7FFFFFFFu) == q) hit = lo + k;
+    }
+    if (hit == kNone && hi - lo > 8u) {
+      uint32_t a = lo + 8, b = hi;
+      while (a < b) {
+        const uint32_t mid = (a + b) >> 1;
+        if ((cpos[mid] & 0x7FFFFFFFu) < q) a = mid + 1; else b = mid;
+      }
+      if (a < hi && (cpos[a] & 0x7FFFFFFFu) == q) hit = a;
+    }
+    return hit;
+  };
+  // 2. marks: the successor among the loaded candidates
+  uint32_t tgt[kChainPer];
+#pragma unroll
+  for (uint32_t u = 0; u < kChainPer; u++) tgt[u] = len[u] ? find(pos[u] + len[u]) : kNone;
+#pragma unroll
+  for (uint32_t u = 0; u < kChainPer; u++) {
+    if (tgt[u] == kNone) continue;
+    const uint32_t me = u * kChainThreads + tid + 1u;
+    const uint32_t prev = atomicCAS(&cmark[tgt[u]], 0u, me);
+    if (prev != 0u && prev != me) cmark[tgt[u]] = kMarkMulti;
+  }
+  __syncthreads();
+  CHAIN_STAMP(2);
+  // 3. the H members among the own candidates, in order (rank of candidate u 1024 + tid: the
+  // members of the rounds before u, of the waves before, of the lanes before)
+  uint32_t m[kChainPer], kp[kChainPer], km[kChainPer];
+#pragma unroll
+  for (uint32_t u = 0; u < kChainPer; u++) m[u] = cmark[u * kChainThreads + tid];
+#pragma unroll
+  for (uint32_t u = 0; u < kChainPer; u++) {  // the marker: at 0, or marked itself
+    const uint32_t k = m[u] != 0u && m[u] != kMarkMulti ? m[u] - 1u : 0u;
+    kp[u] = cpos[k];
+    km[u] = cmark[k];
+  }
+  uint64_t bal[kChainPer];
+#pragma unroll
+  for (uint32_t u = 0; u < kChainPer; u++) {
+    const uint32_t j = u * kChainThreads + tid;
+    bool h = false;
+    if (j >= own0 && j < own1)
+      h = base_pos + pos[u] == 0 || m[u] == kMarkMulti ||
+          (m[u] != 0u && (base_pos + (kp[u] & 0x7FFFFFFFu) == 0 || km[u] != 0u));
+    bal[u] = __ballot(h);
+    if (lane == 0) wsum4[u][wv] = (uint32_t)__popcll(bal[u]);
+  }
+  __syncthreads();
+  uint32_t nh = 0;
+#pragma unroll
+  for (uint32_t u = 0; u < kChainPer; u++) {
+    uint32_t before = 0, all = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kW; k++) {
+      before += k < wv ? wsum4[u][k] : 0u;
+      all += wsum4[u][k];
+    }
+    if ((bal[u] >> lane) & 1u)
+      hlist[nh + before +
+            __builtin_amdgcn_mbcnt_hi((uint32_t)(bal[u] >> 32),
+                                      __builtin_amdgcn_mbcnt_lo((uint32_t)bal[u], 0u))] =
+          (uint16_t)(u * kChainThreads + tid);
+    nh += all;
+  }
+  __syncthreads();
+  const uint32_t nl = nh;
+  auto hpos = [&](uint32_t i) { return base_pos + (cpos[hlist[i]] & 0x7FFFFFFFu); };
+  CHAIN_STAMP(3);
+  // 4. this group's first rank: aggregate out, decoupled look-back (wave 0), inclusive out;
+  // meanwhile wave 1 asks whether the last member's successor is a candidate (it lies in the
+  // loaded blocks; that only matters for the last nonempty group: there it must not be)
+  if (wv == 1 && lane == 0 && nl) {
+    const uint64_t q = hpos(nl - 1) + clen[hlist[nl - 1]];  // in the loaded blocks, or past the end
+    sh[1] = q < nbytes && find((uint32_t)(q - base_pos)) != kNone ? 1u : 0u;
+  }
   if (wv == 0) {
     if (lane == 0)
-      __hip_atomic_store(&t.status[g], chain_word(t.epoch, g == 0 ? 2u : 1u, nh),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&status[g], chain_word(epoch, g == 0 ? 2u : 1u, nh), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
     uint64_t acc = 0;
     bool gave_up = false;
     for (int64_t top = (int64_t)g - 1; top >= 0 && !gave_up; top -= 64) {
@@ -649,10 +652,10 @@ scan_chain_emit_kernel(const uint32_t* __restrict__ slots, const uint64_t* __res
       if (q >= 0) {
         uint32_t polls = 0;
         do {
-          w = ld_agent(&t.status[q]);
-        } while ((uint32_t)(w >> 40) != t.epoch && ++polls < kChainSpin);
+          w = ld_agent(&status[q]);
+        } while ((uint32_t)(w >> 40) != epoch && ++polls < kChainSpin);
       }
-      const bool here = q < 0 || (uint32_t)(w >> 40) == t.epoch;
+      const bool here = q < 0 || (uint32_t)(w >> 40) == epoch;
       gave_up = __ballot(!here) != 0;
       const uint32_t kind = q >= 0 ? (uint32_t)(w >> 38) & 3u : 2u;
       const uint64_t v = q >= 0 && here ? (w & ((1ull << 38) - 1)) : 0ull;
@@ -666,37 +669,41 @@ scan_chain_emit_kernel(const uint32_t* __restrict__ slots, const uint64_t* __res
     }
     if (lane == 0) {
       if (g != 0 && !gave_up)
-        __hip_atomic_store(&t.status[g], chain_word(t.epoch, 2u, acc + nh), __ATOMIC_RELAXED,
+        __hip_atomic_store(&status[g], chain_word(epoch, 2u, acc + nh), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
       if (gave_up) sh[0] = 1u;
       s_prefix = acc;
     }
   }
   __syncthreads();
-  const uint64_t base = s_prefix;
-  // 4. H out in order; each member's successor must be the next member
+  CHAIN_STAMP(4);
+  const uint64_t rank0 = s_prefix;
+  // H out in order; each member's successor must be the next member
   for (uint32_t i = tid; i < nl; i += kChainThreads) {
-    const uint64_t r = base + i;
-    const uint64_t q = lpos[i];
-    const uint32_t L = llen[i];
+    const uint64_t r = rank0 + i;
+    const uint64_t q = hpos(i);
+    const uint32_t L = clen[hlist[i]];
     if (r < cap) {
       rec_off[r] = q;
       rec_len[r] = L;
     }
-    if (i + 1 < nl && q + L != lpos[i + 1]) fail = true;
+    if (i + 1 < nl && q + L != hpos(i + 1)) fail = true;
   }
   if (__ballot(fail) && lane == 0) atomicOr(&sh[0], 1u);
   __syncthreads();
-  if (tid == 0) {  // the summary, for the host (after the stream sync)
-    ChainAux a;
-    a.first = nl ? lpos[0] : ~0ull;
-    a.last_succ = nl ? lpos[nl - 1] + llen[nl - 1] : 0ull;
-    a.nh = nh;
-    a.ncand = C;
-    a.fail = sh[0];
-    a.tail_cand = sh[1] >> 1;
-    host_aux[g] = a;
+  if (tid == 0) {  // 5. the summary to host memory; its epoch word last (the barrier above
+    // waited for every wave's record stores, the wait below for these)
+    ChainAux* a = host_aux + g;
+    a->first = nl ? hpos(0) : ~0ull;
+    a->last_succ = nl ? hpos(nl - 1) + clen[hlist[nl - 1]] : 0ull;
+    a->nh = nh;
+    a->ncand = own1 - own0;
+    a->fail = sh[0];
+    a->tail_cand = sh[1];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(&a->epoch, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+  CHAIN_STAMP(5);
 }
 
 // the candidate total / overflow word (exclusive scan's last entry) to host-mapped memory
@@ -1015,8 +1022,8 @@ struct mgenx_scan_ws {
   // sized spec_cap.  After a stream where it was not the chain the next prune_skip scans do not
   // try it (backoff 2, 4, ... 64 scans; reset on success)
   uint32_t prune_skip = 0, prune_backoff = 0;
-  ScanWork chain;        // look-back words + flags + mark table (ChainTabs)
-  uint32_t chain_hmask = 0, chain_epoch = 0;
+  ScanWork chain;        // the chain kernel's look-back words
+  uint32_t chain_epoch = 0;
   ChainAux* chain_host = nullptr;      // [kChainGroups] emit group summaries (host-mapped)
   ChainAux* chain_host_dev = nullptr;
 };
@@ -1304,10 +1311,10 @@ int scan_walk(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, int mode, ui
 }
 
 
-// The chain hypothesis (scan_chain_*) on a whole TCP stream: detect, the marks and the emit
-// pass, one sync.  ok = false: H was not the chain (nothing is left to reuse; the
-// caller builds exactly).  Emit groups: enough that each holds about 2048 candidates of the
-// last exact build (spec_cap) and at most kChainBlocks detect blocks.
+// The chain hypothesis (scan_chain_kernel) on a whole TCP stream: detect and one kernel, one
+// sync.  ok = false: H was not the chain (nothing is left to reuse; the
+// caller builds exactly).  Groups: enough that each holds about 2048 candidates of the last
+// exact build (spec_cap; kChainCands is twice that) and at most kChainBlocks detect blocks.
 bool chain_fits(const mgenx_scan_ws& ws, uint64_t nbytes) {
   const uint64_t nb = (nbytes + kScanBlockBytes - 1) / kScanBlockBytes;
   return ws.spec_cap != 0 && nb != 0 && nb <= (uint64_t)kChainGroups * kChainBlocks &&
@@ -1334,6 +1341,7 @@ int scan_chain(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, uint64_t* r
         hipSuccess)
       return fail(e, "scan workspace");
     ws.chain_host = static_cast<ChainAux*>(hp);
+    memset(hp, 0, kChainGroups * sizeof(ChainAux));
     void* dp = nullptr;
     if ((e = hipHostGetDevicePointer(&dp, hp, 0)) != hipSuccess) return fail(e, "scan workspace");
     ws.chain_host_dev = static_cast<ChainAux*>(dp);
@@ -1349,48 +1357,56 @@ int scan_chain(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, uint64_t* r
   groups = std::min(std::max(groups, 1u), kChainGroups);
   const uint32_t per_group = (nb + groups - 1) / groups;
   groups = (nb + per_group - 1) / per_group;
-  // mark table: a power of two >= 2 x the expected candidates; look-back words, summaries and
-  // flags first (fixed offsets), so a table that only grows keeps them
-  uint32_t hs = 4096;
-  while (hs < 2ull * ws.spec_cap && hs < (1u << 30)) hs <<= 1;
-  const size_t head = align256((size_t)kChainGroups * 8 + 64);
-  if (!ws.chain.mem || hs - 1 > ws.chain_hmask) {
-    const size_t need = head + (size_t)hs * 8;
-    if ((e = ensure(ws.chain, need)) != hipSuccess ||
+  // the look-back words (epoch-tagged: cleared only when the 22-bit epoch wraps)
+  if (!ws.chain.mem) {
+    if ((e = ensure(ws.chain, (size_t)kChainGroups * 8)) != hipSuccess ||
         (e = hipMemsetAsync(ws.chain.mem, 0, ws.chain.bytes, stream)) != hipSuccess)
       return fail(e, "scan workspace");
-    ws.chain_hmask = (uint32_t)((ws.chain.bytes - head) / 8);  // (a power of two below)
-    uint32_t m = 1;
-    while ((uint64_t)m * 2 <= ws.chain_hmask) m <<= 1;
-    ws.chain_hmask = m - 1;
     ws.chain_epoch = 0;
   }
-  if (++ws.chain_epoch >= kChainEpochs) {  // 8-bit epochs: wrapped, clear every entry
+  if (++ws.chain_epoch >= kChainEpochs) {
     if ((e = hipMemsetAsync(ws.chain.mem, 0, ws.chain.bytes, stream)) != hipSuccess)
       return fail(e, "scan workspace");
+    memset(ws.chain_host, 0, kChainGroups * sizeof(ChainAux));  // (no kernel of ours runs now)
     ws.chain_epoch = 1;
   }
-  char* base = static_cast<char*>(ws.chain.mem);
-  ChainTabs t;
-  t.status = reinterpret_cast<uint64_t*>(base);
-  t.flags = reinterpret_cast<uint32_t*>(base + (size_t)kChainGroups * 8);
-  t.hash = reinterpret_cast<uint64_t*>(base + head);
-  t.hmask = ws.chain_hmask;
-  t.epoch = ws.chain_epoch;
   const ScanMode m{4u, 65535u};
   hipLaunchKernelGGL(scan_detect_kernel<false>, dim3(nb), dim3(kScanThreads), 0, stream, s,
                      nbytes, m, d_slots, d_counts, (const uint64_t*)nullptr, (uint64_t*)nullptr,
                      (uint32_t*)nullptr);
-  hipLaunchKernelGGL(scan_chain_mark_kernel, dim3(link_grid(nb)), dim3(256), 0, stream, s, nbytes,
-                     (const uint32_t*)d_slots, (const uint64_t*)d_counts, nb, t);
-  hipLaunchKernelGGL(scan_chain_emit_kernel, dim3(groups), dim3(kChainThreads), 0, stream,
-                     (const uint32_t*)d_slots, (const uint64_t*)d_counts, nbytes, nb, per_group, t,
-                     cap, rec_off, rec_len, ws.chain_host_dev);
+  hipLaunchKernelGGL(scan_chain_kernel, dim3(groups), dim3(kChainThreads), 0, stream,
+                     (const uint32_t*)d_slots, (const uint64_t*)d_counts, nbytes, nb, per_group,
+                     ws.chain_epoch, static_cast<uint64_t*>(ws.chain.mem), cap, rec_off, rec_len,
+                     ws.chain_host_dev);
   if ((e = hipGetLastError()) != hipSuccess) return fail(e, "scan launch");
-  if ((e = hipStreamSynchronize(stream)) != hipSuccess) return fail(e, "scan");
+  // done when every group's summary carries this scan's epoch (each group writes it after its
+  // records and summary are out): a spin on host memory instead of the stream's completion
+  // signal.  After a second without them, the stream sync (a fault is reported there).
+  const volatile ChainAux* ha = ws.chain_host;
+  {
+    const auto t0 = std::chrono::steady_clock::now();
+    uint32_t g = 0;
+    for (uint64_t spins = 0; g < groups;) {
+      if (ha[g].epoch == ws.chain_epoch) {
+        g++;
+        continue;
+      }
+      _mm_pause();
+      if ((++spins & 0xFFFF) == 0 &&
+          std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) {
+        if ((e = hipStreamSynchronize(stream)) != hipSuccess) return fail(e, "scan");
+        for (; g < groups && ha[g].epoch == ws.chain_epoch; g++) {
+        }
+        if (g < groups) {
+          snprintf(fail.err, fail.errn, "scan: chain kernel ended without its summaries");
+          return MGENX_EDEVICE;
+        }
+      }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+  }
   // the joins between groups: each nonempty group starts where the previous one's last member
   // ends, the first starts at 0, the last one's successor is not a candidate
-  const volatile ChainAux* ha = ws.chain_host;
   uint64_t th = 0, tc = 0, next = 0;
   bool bad = false, any = false, tail = false;
   for (uint32_t g = 0; g < groups; g++) {
@@ -1419,6 +1435,13 @@ int scan_chain(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, uint64_t* r
 }
 
 }  // namespace
+
+#if MGENX_DIAG
+extern "C" int mgenx_diag_chain_prof(unsigned long long* out) {
+  return out && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_chain_prof), sizeof(g_chain_prof)) ==
+                    hipSuccess ? MGENX_OK : MGENX_EDEVICE;
+}
+#endif
 
 // Whole-stream scan from offset 0 (synchronous on `stream`).
 extern "C" int mgenx_scan_run(void* wsp, const uint8_t* s, uint64_t nbytes, int mode,

@@ -55,4 +55,30 @@ t0 = time.perf_counter()
 for _ in range(reps):
     eng.lib.mgenx_stream_scan(*args, ctypes.byref(inf), st)
 print("c_call_ms", (time.perf_counter() - t0) / reps * 1e3, int(inf.n_records), int(inf.path), flush=True)
+# interleaved: wrapper call, C call (median of 40 each)
+tw, tc = [], []
+for _ in range(40):
+    t = time.perf_counter()
+    eng.stream_scan(local, SCAN_TCP, out=out)
+    tw.append(time.perf_counter() - t)
+    t = time.perf_counter()
+    eng.lib.mgenx_stream_scan(*args, ctypes.byref(inf), st)
+    tc.append(time.perf_counter() - t)
+print("interleaved median us: wrapper %.1f C %.1f" % (np.median(tw) * 1e6, np.median(tc) * 1e6),
+      flush=True)
+
+# the wrapper's pieces, 2000 calls each (us per call)
+def per_call(f, n=2000):
+    t = time.perf_counter()
+    for _ in range(n):
+        f()
+    return round((time.perf_counter() - t) / n * 1e6, 2)
+
+
+print("us: current_stream", per_call(lambda: _stream(0)),
+      "raw_stream", per_call(lambda: torch._C._cuda_getCurrentRawStream(0)),
+      "slice", per_call(lambda: out[0][:n]),
+      "ptr", per_call(lambda: _ptr(local)),
+      "info", per_call(ScanInfo),
+      "numel", per_call(local.numel), flush=True)
 eng.close()
