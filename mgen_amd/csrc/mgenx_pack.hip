@@ -379,24 +379,32 @@ pack_kernel(PackParams p) {
       const uint32_t tword = m.trailer_on ? bswap32(m.trailer) : 0u;
       constexpr uint32_t kUnroll = 4;
       for (uint32_t u0 = lane; u0 < units; u0 += 64u * kUnroll) {
+        // every LDS read and shuffle of the pass first (unconditional, at clamped addresses),
+        // so they go out together and one wait covers them; then the selects and the stores
         u32x4_t v[kUnroll];
-        uint32_t at[kUnroll];
+        uint32_t tw[kUnroll], pos[kUnroll], rr[kUnroll], last[kUnroll];
 #pragma unroll
         for (uint32_t k = 0; k < kUnroll; k++) {
-          const uint32_t pos = pu << 4;
-          const uint32_t tw = (uint32_t)__shfl((int)tword, (int)min(r, 63u));
-          v[k] = u32x4_t{0u, 0u, 0u, 0u};
-          if (pos < (uint32_t)kImg && r < nv)
-            v[k] = *reinterpret_cast<const u32x4_t*>(&S_IMG[r * kImg + pos]);
-          if (pu == U - 1u && tw) v[k].w = tw;
-          at[k] = u0 + 64u * k;
+          pos[k] = pu << 4;
+          rr[k] = r;
+          last[k] = pu == U - 1u;
+          tw[k] = (uint32_t)__shfl((int)tword, (int)min(r, 63u));
+          v[k] = *reinterpret_cast<const u32x4_t*>(
+              &S_IMG[min(r, 63u) * kImg + min(pos[k], (uint32_t)kImg - 16u)]);
           pu += rm;
           r += q;
           if (pu >= U) { pu -= U; r++; }
         }
 #pragma unroll
-        for (uint32_t k = 0; k < kUnroll; k++)
-          if (at[k] < units) stu128(base + (uint64_t)at[k] * 16u, v[k]);
+        for (uint32_t k = 0; k < kUnroll; k++) {
+          if (!(pos[k] < (uint32_t)kImg && rr[k] < nv)) v[k] = u32x4_t{0u, 0u, 0u, 0u};
+          if (last[k] && tw[k]) v[k].w = tw[k];
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < kUnroll; k++) {
+          const uint32_t at = u0 + 64u * k;
+          if (at < units) stu128(base + (uint64_t)at * 16u, v[k]);
+        }
       }
       goto stage_end;
     }
