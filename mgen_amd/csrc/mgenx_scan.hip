@@ -405,11 +405,19 @@ scan_enum_regular_kernel(const uint8_t* __restrict__ s, const uint64_t* __restri
 // candidates comes from its own detect blocks or the 4 before them: each group loads those
 // candidates into LDS and marks there -- no candidate numbering across groups, no table in
 // memory, no wait on other groups except the ranks (one decoupled look-back).
-struct ChainAux {  // one group's summary, for the host
-  uint64_t first, last_succ;  // position of its first H member; successor of its last
-  uint32_t nh, ncand, fail, tail_cand;  // tail_cand: last_succ is a candidate
-  uint32_t epoch, pad;  // written last: the group is done (its records are out)
+// one group's summary for the host, ONE 16-byte granule written by one store (its epoch word
+// comes with it: no ordering between two stores to wait for):
+//   bits   0..39  position of its first H member     66..78  H members (nh)
+//          40..65 last member's successor - first     79..91  own candidates (saturating)
+//          92     not proved here (fail)              93      last successor is a candidate
+//          94..115 epoch
+struct ChainAux {
+  uint64_t lo, hi;
 };
+__host__ __device__ inline uint32_t aux_bits(const ChainAux& a, int at, int n) {
+  const unsigned __int128 v = ((unsigned __int128)a.hi << 64) | a.lo;
+  return (uint32_t)((v >> at) & (((unsigned __int128)1 << n) - 1));
+}
 constexpr uint32_t kChainEpochs = 1u << 22;  // look-back words: epoch << 40 | kind << 38 | count
 constexpr uint32_t kChainThreads = 1024;
 constexpr uint32_t kChainBlocks = 1024;  // detect blocks per group at most (4 more are loaded)
@@ -691,17 +699,20 @@ scan_chain_kernel(const uint32_t* __restrict__ slots, const uint64_t* __restrict
   }
   if (__ballot(fail) && lane == 0) atomicOr(&sh[0], 1u);
   __syncthreads();
-  if (tid == 0) {  // 5. the summary to host memory; its epoch word last (the barrier above
-    // waited for every wave's record stores, the wait below for these)
-    ChainAux* a = host_aux + g;
-    a->first = nl ? hpos(0) : ~0ull;
-    a->last_succ = nl ? hpos(nl - 1) + clen[hlist[nl - 1]] : 0ull;
-    a->nh = nh;
-    a->ncand = own1 - own0;
-    a->fail = sh[0];
-    a->tail_cand = sh[1];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(&a->epoch, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (tid == 0) {  // 5. the summary to host memory: one 16-byte write-through store (the host
+    // reads it while the kernel may still run; the barrier above waited for the record stores)
+    const uint64_t first = nl ? hpos(0) : 0ull;
+    const uint64_t span = nl ? hpos(nl - 1) + clen[hlist[nl - 1]] - first : 0ull;
+    const unsigned __int128 v =
+        (unsigned __int128)(first & ((1ull << 40) - 1)) |
+        ((unsigned __int128)(span & ((1ull << 26) - 1)) << 40) |
+        ((unsigned __int128)min(nh, 8191u) << 66) |
+        ((unsigned __int128)min(own1 - own0, 8191u) << 79) |
+        ((unsigned __int128)(sh[0] != 0u) << 92) | ((unsigned __int128)(sh[1] != 0u) << 93) |
+        ((unsigned __int128)epoch << 94);
+    const u32x4_t w = {(uint32_t)v, (uint32_t)(v >> 32), (uint32_t)(v >> 64), (uint32_t)(v >> 96)};
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(host_aux + g), "v"(w)
+                 : "memory");  // (system coherent: one write to host memory)
   }
   CHAIN_STAMP(5);
 }
@@ -1024,8 +1035,9 @@ struct mgenx_scan_ws {
   uint32_t prune_skip = 0, prune_backoff = 0;
   ScanWork chain;        // the chain kernel's look-back words
   uint32_t chain_epoch = 0;
-  ChainAux* chain_host = nullptr;      // [kChainGroups] emit group summaries (host-mapped)
+  ChainAux* chain_host = nullptr;      // [kChainGroups] group summaries (host-mapped)
   ChainAux* chain_host_dev = nullptr;
+  std::vector<ChainAux> chain_seen;    // the summaries as read
 };
 
 extern "C" void* mgenx_scan_ws_new() { return new mgenx_scan_ws(); }
@@ -1337,6 +1349,8 @@ int scan_chain(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, uint64_t* r
   hipError_t e;
   if (!ws.chain_host) {
     void* hp = nullptr;
+    // (the kernel writes it with write-through stores: the host spins on it while the kernel
+    // runs; a coherent allocation made each scan ~18 us slower on the host side)
     if ((e = hipHostMalloc(&hp, kChainGroups * sizeof(ChainAux), hipHostMallocMapped)) !=
         hipSuccess)
       return fail(e, "scan workspace");
@@ -1382,12 +1396,23 @@ int scan_chain(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, uint64_t* r
   // done when every group's summary carries this scan's epoch (each group writes it after its
   // records and summary are out): a spin on host memory instead of the stream's completion
   // signal.  After a second without them, the stream sync (a fault is reported there).
-  const volatile ChainAux* ha = ws.chain_host;
+  // a summary: one aligned 16-byte load (one granule, as the kernel wrote it)
+  auto aux_at = [&](uint32_t g) {
+    const __m128i x = _mm_load_si128(reinterpret_cast<const __m128i*>(ws.chain_host + g));
+    ChainAux a;
+    a.lo = (uint64_t)_mm_cvtsi128_si64(x);
+    a.hi = (uint64_t)_mm_extract_epi64(x, 1);
+    return a;
+  };
+  std::vector<ChainAux>& ha = ws.chain_seen;
+  ha.resize(groups);
   {
     const auto t0 = std::chrono::steady_clock::now();
     uint32_t g = 0;
     for (uint64_t spins = 0; g < groups;) {
-      if (ha[g].epoch == ws.chain_epoch) {
+      std::atomic_signal_fence(std::memory_order_seq_cst);  // (a fresh load every poll)
+      ha[g] = aux_at(g);
+      if (aux_bits(ha[g], 94, 22) == ws.chain_epoch) {
         g++;
         continue;
       }
@@ -1395,7 +1420,9 @@ int scan_chain(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, uint64_t* r
       if ((++spins & 0xFFFF) == 0 &&
           std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) {
         if ((e = hipStreamSynchronize(stream)) != hipSuccess) return fail(e, "scan");
-        for (; g < groups && ha[g].epoch == ws.chain_epoch; g++) {
+        for (; g < groups; g++) {
+          ha[g] = aux_at(g);
+          if (aux_bits(ha[g], 94, 22) != ws.chain_epoch) break;
         }
         if (g < groups) {
           snprintf(fail.err, fail.errn, "scan: chain kernel ended without its summaries");
@@ -1410,15 +1437,17 @@ int scan_chain(mgenx_scan_ws& ws, const uint8_t* s, uint64_t nbytes, uint64_t* r
   uint64_t th = 0, tc = 0, next = 0;
   bool bad = false, any = false, tail = false;
   for (uint32_t g = 0; g < groups; g++) {
-    const uint32_t nh = ha[g].nh;
-    tc += ha[g].ncand;
-    bad = bad || ha[g].fail != 0u;
+    const ChainAux& a = ha[g];
+    const uint32_t nh = aux_bits(a, 66, 13);
+    tc += aux_bits(a, 79, 13);
+    bad = bad || aux_bits(a, 92, 1) != 0u || nh >= 8191u;
     if (!nh) continue;
-    bad = bad || ha[g].first != next;  // (next = 0 before the first nonempty group)
+    const uint64_t first = a.lo & ((1ull << 40) - 1);
+    bad = bad || first != next;  // (next = 0 before the first nonempty group)
     any = true;
     th += nh;
-    next = ha[g].last_succ;
-    tail = ha[g].tail_cand != 0u;
+    next = first + aux_bits(a, 40, 26);
+    tail = aux_bits(a, 93, 1) != 0u;
   }
   if (bad || !any || tail) return MGENX_OK;
   ok = true;

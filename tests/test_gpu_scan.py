@@ -412,3 +412,93 @@ def test_config5_full_size_vs_oracle(torch, eng, n):
         e2.close()
     del stream
     torch.cuda.empty_cache()
+
+
+# ---- the chain kernel (scan_chain_kernel, path 2) at its edges ----
+
+def _scan_calls(torch, s, calls=3, mode=0):
+    """`calls` whole-stream scans of s on a fresh engine, each against the oracle; the paths."""
+    from mgen_amd import Engine, to_device
+    from oracle import oracle as O
+    wo, wl, _, wc, ws = O.tcp_scan(s.tobytes())
+    e = Engine(0)
+    d = to_device(s)
+    paths = []
+    try:
+        for k in range(calls):
+            offs, lens, info = e.stream_scan(d, mode)
+            assert np.array_equal(offs.cpu().numpy().view(np.uint64), np.asarray(wo, np.uint64)), k
+            assert np.array_equal(lens.cpu().numpy().view(np.uint32), np.asarray(wl, np.uint32)), k
+            assert (int(info.consumed), int(info.status)) == (wc, ws), k
+            paths.append(int(info.path))
+    finally:
+        e.close()
+    return paths
+
+
+def test_chain_dense_small_records(torch, gold):
+    """~64K records of 28..200 B (thousands of candidates per detect block group): the chain
+    groups hold more than kChainCands candidates, the hypothesis is not proved there and the
+    exact path frames the stream -- every call equals the oracle."""
+    rng = np.random.default_rng(SEED + 80)
+    s = tcp_stream(gold, rng.integers(76, 200, 40000), rng)
+    paths = _scan_calls(torch, s, 4)
+    assert paths[0] == 0
+
+
+def test_chain_bad_record_mid_stream(torch, gold):
+    """A config-5-like stream (16-KiB TCP transmit records) with one record's length field
+    broken in the middle: the second call's chain check fails (or proves a shorter chain) and
+    the framing still equals the oracle's -- the zero-length error stops it there."""
+    from mgen_amd import Engine
+    e = Engine(0)
+    try:
+        st = _tcp_tx_stream(torch, e, 512)
+    finally:
+        e.close()
+    s = st.cpu().numpy().copy()
+    k = 300 * 16384
+    s[k] = 0
+    s[k + 1] = 2  # msg_len 2 < 4: the reference's stream error
+    paths = _scan_calls(torch, s, 3)
+    assert paths[0] == 0
+
+
+def test_chain_junk_tail_after_valid_records(torch, gold):
+    """Valid 16-KiB transmit records followed by 100 KiB of random bytes: the chain from 0 ends
+    at the junk, the resolver walks the rest exactly, on the chain path's second call too."""
+    from mgen_amd import Engine
+    e = Engine(0)
+    try:
+        st = _tcp_tx_stream(torch, e, 256)
+    finally:
+        e.close()
+    rng = np.random.default_rng(SEED + 81)
+    s = np.concatenate([st.cpu().numpy(), rng.integers(0, 256, 100 * 1024, dtype=np.uint8)])
+    _scan_calls(torch, s, 3)
+
+
+def test_chain_streams_alternate(torch, gold):
+    """One engine scanning two different transmit streams in turn (the chain path's epochs and
+    group summaries are reused across scans): each call equals the oracle for its stream."""
+    from mgen_amd import Engine, SCAN_TCP
+    from oracle import oracle as O
+    e = Engine(0)
+    try:
+        a = _tcp_tx_stream(torch, e, 384)
+        b = _tcp_tx_stream(torch, e, 200, msg=20480)
+        want = {}
+        for name, st in (("a", a), ("b", b)):
+            wo, wl, _, wc, ws = O.tcp_scan(st.cpu().numpy().tobytes())
+            want[name] = (np.asarray(wo, np.uint64), wc, ws)
+        paths = []
+        for k in range(6):
+            name, st = ("a", a) if k % 2 == 0 else ("b", b)
+            offs, lens, info = e.stream_scan(st, SCAN_TCP)
+            wo, wc, ws = want[name]
+            assert np.array_equal(offs.cpu().numpy().view(np.uint64), wo), k
+            assert (int(info.consumed), int(info.status)) == (wc, ws), k
+            paths.append(int(info.path))
+        assert 2 in paths, paths
+    finally:
+        e.close()
