@@ -159,7 +159,10 @@ struct mgenx_ctx {
   void* log_ws = nullptr;         // log-format workspace (mgenx_log.hip), grown on demand
   void* tcp_ws = nullptr;         // TCP transmit workspace (mgenx_pack_tcp), grown on demand
   size_t tcp_ws_bytes = 0;
-  uint64_t* tcp_host = nullptr;   // host-mapped words: total bytes, max fragments
+  uint64_t* tcp_host = nullptr;   // host-mapped words: the plan's verdict (16 bytes)
+  void* tcp_plan = nullptr;       // the plan's maximum word, skip word and look-back words
+  uint32_t tcp_plan_blocks = 0;   // (look-back words it holds)
+  uint32_t tcp_epoch = 0;         // the plan's epoch (its words are cleared when it wraps)
   void* rx_ws = nullptr;          // rx-persist workspace, grown on demand
   size_t rx_ws_bytes = 0;
   uint64_t* tcp_host_dev = nullptr;
@@ -356,6 +359,7 @@ int mgenx_ctx_destroy(mgenx_ctx* c) {
   if (c->flow_ws) mgenx_flow_ws_free(c->flow_ws);
   if (c->log_ws) mgenx_log_ws_free(c->log_ws);
   mgenx::dev_free(c->tcp_ws);
+  mgenx::dev_free(c->tcp_plan);
   mgenx::dev_free(c->rx_ws);
   mgenx::host_free(c->tcp_host);
   for (mgenx_grow& g : c->bl) g.release();
@@ -439,7 +443,8 @@ static int pack_common(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
                        const uint64_t* dev_rec_off, uint64_t stride, const uint32_t* dev_buf_len,
                        const uint32_t* dev_crc_in, uint32_t* dev_out_len, uint32_t* dev_tx_crc,
                        uint32_t* dev_state, uint32_t opts, uint32_t fill_time, void* stream,
-                       const uint32_t* dev_frag_len = nullptr, int frag_ck = 0) {
+                       const uint32_t* dev_frag_len = nullptr, int frag_ck = 0,
+                       const uint32_t* dev_skip = nullptr) {
   if (!ctx) return MGENX_EINVAL;
   if (n == 0) return MGENX_OK;
   if (!dev_tmpl || !dev_tmpl_crc || !dev_desc || !dev_slab || !dev_out_len) return MGENX_EINVAL;
@@ -472,6 +477,7 @@ static int pack_common(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
   p.state = dev_state;
   p.frag_len = dev_frag_len;
   p.frag_ck = frag_ck;
+  p.skip = dev_skip;
   const uint64_t batches = ((uint64_t)n + 63) / 64;
   uint64_t grid = (batches + 3) / 4;                // groups of 4 batches (kProd)
   uint64_t cap = (uint64_t)ctx->cu_count * 2;  // 76 KB of LDS per workgroup
@@ -503,9 +509,8 @@ int mgenx_pack_msgs(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
                      dev_state, opts | MGENX_PACK_RAW, fill_time, stream);
 }
 
-// the maximum fragment count and the stream total into host-mapped memory
 // the stream length and the round count (the plan kernel's maximum fragment count) for
-// the host, in one 16-byte copy
+// the host, in one 16-byte copy (the exact path)
 __global__ void tcp_totals_kernel(const uint32_t* max_frag, uint32_t n, const uint64_t* off,
                                   const uint64_t* bytes, uint64_t* out) {
   out[0] = off[n - 1] + bytes[n - 1];  // (the exclusive scan's last offset + its message)
@@ -534,18 +539,19 @@ int mgenx_pack_tcp(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl, const uint32
     void* hp = nullptr;
     void* dp = nullptr;
     if ((e = hipHostMalloc(&hp, 64, hipHostMallocMapped)) != hipSuccess) return set_err(ctx, e, "tcp");
+    memset(hp, 0, 64);
     ctx->tcp_host = static_cast<uint64_t*>(hp);
     if ((e = hipHostGetDevicePointer(&dp, hp, 0)) != hipSuccess) return set_err(ctx, e, "tcp");
     ctx->tcp_host_dev = static_cast<uint64_t*>(dp);
   }
   // workspace: bytes[n], nfrag[n], cub (a scan of n items); per round: fd, foff, fbuf, ff,
-  // plen, crc, state x2, acrc[3n]; the maximum fragment count
+  // plen, crc, state x2; the maximum fragment count (exact path)
   size_t cub_bytes = 0;
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, cub_bytes, (const uint64_t*)nullptr,
                                          (uint64_t*)nullptr, (int)n, s);
   const size_t b8 = a256((size_t)n * 8), b4 = a256((size_t)n * 4);
   const size_t need = b8 + b4 + a256(cub_bytes) + a256((size_t)n * sizeof(mgenx_pack_desc)) +
-                      b8 + 4 * b4 + 2 * b4 + 3 * b4 + 256;
+                      b8 + 4 * b4 + 2 * b4 + 256;
   if (ctx->tcp_ws_bytes < need) {
     mgenx::dev_free(ctx->tcp_ws);
     ctx->tcp_ws = nullptr;
@@ -565,51 +571,118 @@ int mgenx_pack_tcp(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl, const uint32
   uint32_t* plen = (uint32_t*)take(b4);
   uint32_t* crc = (uint32_t*)take(b4);
   uint32_t* st[2] = {(uint32_t*)take(b4), (uint32_t*)take(b4)};
-  uint32_t* acrc = (uint32_t*)take(3 * b4);
   uint32_t* max_frag = (uint32_t*)take(256);
-  // plan: bytes per message, fragments; the message offsets by an exclusive scan of n items
-  // straight into the caller's array (n entries)
-  if ((e = hipMemsetAsync(max_frag, 0, 4, s)) != hipSuccess) return set_err(ctx, e, "tcp plan");
-  if ((e = mgenx::launch_tcp_plan(dev_tmpl, dev_desc, dev_msg_total, n, bytes, nfrag, max_frag,
-                                  s)) != hipSuccess)
-    return set_err(ctx, e, "tcp plan");
-  // the message offsets straight into the caller's array (n entries); the total from its last
-  // (a scan of n + 1 into the workspace and a copy out cost a 512-KiB copy for config 5)
-  if ((e = hipcub::DeviceScan::ExclusiveSum(cub, cub_bytes, (const uint64_t*)bytes, dev_msg_off,
-                                            (int)n, s)) != hipSuccess)
-    return set_err(ctx, e, "tcp scan");
+  // the plan's words, in their own allocation (epoch-tagged: they must keep their place
+  // whatever n the next call brings): the skip word, then a look-back word and a maximum word
+  // a block
+  const uint32_t blocks = (n + mgenx::kTcpPlanMsgs - 1) / mgenx::kTcpPlanMsgs;
+  if (ctx->tcp_plan_blocks < blocks) {
+    mgenx::dev_free(ctx->tcp_plan);
+    ctx->tcp_plan = nullptr;
+    ctx->tcp_plan_blocks = 0;
+    const size_t pb = 256 + (size_t)blocks * 16;
+    if ((e = hipMalloc(&ctx->tcp_plan, pb)) != hipSuccess ||
+        (e = hipMemsetAsync(ctx->tcp_plan, 0, pb, s)) != hipSuccess)
+      return set_err(ctx, e, "tcp workspace");
+    ctx->tcp_plan_blocks = blocks;
+  }
+  if (++ctx->tcp_epoch >= mgenx::kTcpPlanEpochs) {  // wrap: clear the words (nothing in flight)
+    if ((e = hipStreamSynchronize(s)) != hipSuccess ||
+        (e = hipMemsetAsync(ctx->tcp_plan, 0, 256 + (size_t)ctx->tcp_plan_blocks * 16, s)) !=
+            hipSuccess)
+      return set_err(ctx, e, "tcp plan");
+    memset(ctx->tcp_host, 0, 64);
+    ctx->tcp_epoch = 1;
+  }
+  const uint32_t epoch = ctx->tcp_epoch;
+  uint32_t* skip = static_cast<uint32_t*>(ctx->tcp_plan);
+  uint64_t* status = reinterpret_cast<uint64_t*>(static_cast<char*>(ctx->tcp_plan) + 256);
+  uint64_t* fmax = status + ctx->tcp_plan_blocks;
   const int ck = (opts & MGENX_PACK_CHECKSUM) ? 1 : 0;
-  auto round = [&](uint32_t r) -> int {
-    if ((e = mgenx::launch_tcp_frag(dev_desc, dev_msg_total, nfrag, dev_msg_off, n, r, ck,
-                                    st[(r + 1) & 1], fd, foff, fbuf, ff, s)) != hipSuccess)
+  // round r: fragment descriptors (round 0's come with the plan), then Pack -- which also
+  // stores the later buffers' copies, runs the CRC on through them and writes the trailer
+  auto round = [&](uint32_t r, const uint32_t* gate) -> int {
+    if (r > 0 && (e = mgenx::launch_tcp_frag(dev_desc, dev_msg_total, nfrag, dev_msg_off, n, r,
+                                             ck, st[(r + 1) & 1], fd, foff, fbuf, ff, s)) !=
+                     hipSuccess)
       return set_err(ctx, e, "tcp fragments");
     int rc = pack_common(ctx, dev_tmpl, dev_tmpl_crc, fd, n, dev_pool, dev_stream, stream_cap,
                          foff, 0, fbuf, nullptr, plen, crc, st[r & 1], opts | MGENX_PACK_RAW,
-                         fill_time, stream, ff, ck);
-    if (rc != MGENX_OK) return rc;
-    if ((e = mgenx::launch_tcp_tail(dev_stream, foff, fbuf, ff, plen, crc, st[r & 1], n, ck,
-                                    (opts & MGENX_PACK_RANDOM_FILL) ? 1 : 0, acrc,
-                                    ctx->d_bytetab, ctx->d_tabs + 1024, ctx->d_xpow, ctx->d_ia,
-                                    ctx->d_rcrc, stream_cap, s)) != hipSuccess)
-      return set_err(ctx, e, "tcp tail");
-    return MGENX_OK;
+                         fill_time, stream, ff, ck, gate);
+    return rc;
   };
-  hipLaunchKernelGGL(tcp_totals_kernel, dim3(1), dim3(1), 0, s, max_frag, n, dev_msg_off, bytes,
-                     ctx->tcp_host_dev);
-  if ((e = hipStreamSynchronize(s)) != hipSuccess) return set_err(ctx, e, "tcp plan");
-  const uint64_t total = ((volatile uint64_t*)ctx->tcp_host)[0];
-  const uint32_t rounds = (uint32_t)((volatile uint64_t*)ctx->tcp_host)[1];
+  // One launch plans every message, scans the offsets straight into the caller's array and
+  // writes round 0's descriptors; round 0 is queued behind it before the host has read the
+  // plan (gated on the device: when the stream exceeds stream_cap, or the plan failed, it
+  // stores nothing), so the GPU never waits for the host between back-to-back calls.  The
+  // host then spins on the plan's 16-byte verdict in host memory (not the stream's
+  // completion: round 0 keeps running), and queues any further rounds.
+  if ((e = mgenx::launch_tcp_plan0(dev_tmpl, dev_desc, dev_msg_total, n, ck, stream_cap, epoch,
+                                   status, fmax, dev_msg_off, nfrag, fd, foff, fbuf, ff, skip,
+                                   ctx->tcp_host_dev, s)) != hipSuccess)
+    return set_err(ctx, e, "tcp plan");
+  const bool spec = dev_stream != nullptr;
+  if (spec) {
+    const int rc = round(0, skip);
+    if (rc != MGENX_OK) return rc;
+  }
+  auto verdict = [&]() {
+    const __m128i x = _mm_load_si128(reinterpret_cast<const __m128i*>(ctx->tcp_host));
+    return std::make_pair((uint64_t)_mm_cvtsi128_si64(x), (uint64_t)_mm_extract_epi64(x, 1));
+  };
+  std::pair<uint64_t, uint64_t> v;
+  {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t spins = 0;; spins++) {
+      std::atomic_signal_fence(std::memory_order_seq_cst);  // (a fresh load every poll)
+      v = verdict();
+      if ((uint32_t)(v.second >> 48) == epoch) break;
+      _mm_pause();
+      if ((spins & 0xFFFF) == 0xFFFF &&
+          std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) {
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return set_err(ctx, e, "tcp plan");
+        v = verdict();
+        if ((uint32_t)(v.second >> 48) != epoch) {
+          snprintf(ctx->err, sizeof(ctx->err), "tcp plan: no verdict");
+          return MGENX_EDEVICE;
+        }
+        break;
+      }
+    }
+  }
+  uint64_t total = v.first;
+  uint32_t rounds = (uint32_t)(v.second & 0x7FFFFFFFu);
+  uint32_t r0 = spec ? 1u : 0u;  // the first round still to queue
+  if ((v.second >> 32) & 1u) {
+    // the exact path (the plan could not vouch for its offsets; round 0 stored nothing): the
+    // plan per message, the offsets by a device-wide scan, the totals read back
+    if ((e = hipMemsetAsync(max_frag, 0, 4, s)) != hipSuccess ||
+        (e = mgenx::launch_tcp_plan(dev_tmpl, dev_desc, dev_msg_total, n, bytes, nfrag, max_frag,
+                                    s)) != hipSuccess ||
+        (e = hipcub::DeviceScan::ExclusiveSum(cub, cub_bytes, (const uint64_t*)bytes, dev_msg_off,
+                                              (int)n, s)) != hipSuccess)
+      return set_err(ctx, e, "tcp plan");
+    hipLaunchKernelGGL(tcp_totals_kernel, dim3(1), dim3(1), 0, s, max_frag, n, dev_msg_off, bytes,
+                       ctx->tcp_host_dev);
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return set_err(ctx, e, "tcp plan");
+    total = ((volatile uint64_t*)ctx->tcp_host)[0];
+    rounds = (uint32_t)((volatile uint64_t*)ctx->tcp_host)[1];
+    ((volatile uint64_t*)ctx->tcp_host)[1] = 0;  // (no stale epoch for the next call)
+    r0 = 0;
+  }
   *total_bytes = total;
   if (total > stream_cap || (total && !dev_stream)) {
     snprintf(ctx->err, sizeof(ctx->err), "tcp: the stream needs %llu bytes",
              (unsigned long long)total);
     return MGENX_EINVAL;
   }
-  // (the rounds return unsynchronised: back-to-back calls keep the GPU busy while the host
-  // enqueues the next plan; packing before the read-back, with one sync at the end instead,
-  // measured 0.314 ms against 0.293 for config 5 in the bench's back-to-back timing)
-  for (uint32_t r = 0; r < rounds; r++) {
-    const int rc = round(r);
+  for (uint32_t r = r0; r < rounds; r++) {
+    if (r == 0) {  // (exact path: round 0's descriptors from the fragment kernel)
+      if ((e = mgenx::launch_tcp_frag(dev_desc, dev_msg_total, nfrag, dev_msg_off, n, 0, ck,
+                                      st[1], fd, foff, fbuf, ff, s)) != hipSuccess)
+        return set_err(ctx, e, "tcp fragments");
+    }
+    const int rc = round(r, nullptr);
     if (rc != MGENX_OK) return rc;
   }
   return MGENX_OK;

@@ -87,6 +87,8 @@ struct PackParams {
                              // later buffers' copies of the image are stored too (NULL = none)
   int frag_ck;               // the TCP transport's checksum setting (buffer sizes depend on it)
   int variant;               // diagnostic ablation (0 = product path)
+  const uint32_t* skip = nullptr;  // TCP: a device word; non-zero = store nothing (the plan's
+                                   // verdict on a launch made before the host has read it)
 };
 
 hipError_t launch_unpack(const UnpackParams& p, int grid, hipStream_t stream, int* which);
@@ -128,11 +130,16 @@ hipError_t launch_tcp_frag(const mgenx_pack_desc* desc, const uint32_t* msg_tota
                            const uint32_t* nfrag, const uint64_t* msg_off, uint32_t n, uint32_t r,
                            int ck, const uint32_t* prev_state, mgenx_pack_desc* fd, uint64_t* foff,
                            uint32_t* fbuf, uint32_t* ff, hipStream_t s);
-hipError_t launch_tcp_tail(uint8_t* out, const uint64_t* foff, const uint32_t* fbuf,
-                           const uint32_t* ff, const uint32_t* plen, const uint32_t* tx_crc,
-                           const uint32_t* state, uint32_t n, int ck, int rnd, uint32_t* acrc,
-                           const uint32_t* byte_tab, const uint32_t* a4_tab, const uint32_t* xpow,
-                           const uint32_t* ia, const uint32_t* rcrc, uint64_t cap, hipStream_t s);
+// the plan, offsets and round 0's descriptors in one launch (kTcpPlanMsgs messages a block),
+// its verdict to *skip and, as one 16-byte write, to host-mapped memory: the stream bytes,
+// then epoch << 48 | fail << 32 | rounds
+constexpr uint32_t kTcpPlanMsgs = 1024;
+constexpr uint32_t kTcpPlanEpochs = 1u << 16;
+hipError_t launch_tcp_plan0(const mgenx_flow_tmpl* tmpl, const mgenx_pack_desc* desc,
+                            const uint32_t* msg_total, uint32_t n, int ck, uint64_t cap,
+                            uint32_t epoch, uint64_t* status, uint64_t* fmax, uint64_t* msg_off,
+                            uint32_t* nfrag, mgenx_pack_desc* fd, uint64_t* foff, uint32_t* fbuf,
+                            uint32_t* ff, uint32_t* skip, uint64_t* host, hipStream_t s);
 // the resident single-message worker (mgenx_worker.hip): a request block the host writes (in
 // fine-grained device memory the host stores into through the BAR when the runtime grants the
 // CPU access to it, else in pinned host memory) and a reply block in pinned host memory

@@ -30,11 +30,11 @@ constexpr int kImg = 96;  // header image bytes per record (header <= 76, + firs
 struct PackMeta {
   uint64_t off;
   uint32_t ret;      // Pack() return (0 = failed, nothing written)
-  uint32_t trailer;  // value written big-endian at ret-4 when trailer_on
+  uint32_t trailer;  // value written big-endian at ret-4 (trailer_on 1) or frag-4 (2)
   uint32_t pend;     // end of header + copied payload
   uint32_t poff;     // pool offset of the payload
   uint16_t hdr;      // packet_header_len
-  uint8_t trailer_on, rf;
+  uint8_t trailer_on, rf;  // trailer_on: 0 none, 1 at ret - 4, 2 at frag - 4 (TCP)
   uint32_t tx_out;   // tx_checksum after Pack (out: tx_crc)
   uint32_t state;    // packet_header_len | flags << 16 (out: state)
   uint32_t frag;     // TCP fragment length F > ret: later buffers repeat the image (else 0)
@@ -95,6 +95,51 @@ __device__ __forceinline__ void img_put32(uint8_t* img, uint32_t at, uint32_t v)
   img_put8(img, at + 3, v);
 }
 
+typedef uint32_t u32x2_u1 __attribute__((ext_vector_type(2), aligned(1)));
+
+// the first rem (< 16) bytes of the unit v at d: at most four stores (8, 4, 2, 1 bytes; the
+// word picked by selects, not by a register index)
+__device__ __forceinline__ void st_part(uint8_t* d, const uint32_t v[4], uint32_t rem) {
+  auto word_at = [&](uint32_t o) {  // the word holding byte o
+    return o < 4u ? v[0] : (o < 8u ? v[1] : (o < 12u ? v[2] : v[3]));
+  };
+  uint32_t o = 0;
+  if (rem & 8u) {
+    *reinterpret_cast<u32x2_u1*>(d) = u32x2_u1{v[0], v[1]};
+    o = 8u;
+  }
+  if (rem & 4u) {
+    *reinterpret_cast<u32_u1*>(d + o) = word_at(o);
+    o += 4u;
+  }
+  if (rem & 2u) {
+    *reinterpret_cast<u16_u1*>(d + o) = (uint16_t)(word_at(o) >> (8u * (o & 3u)));
+    o += 2u;
+  }
+  if (rem & 1u) d[o] = (uint8_t)(word_at(o) >> (8u * (o & 3u)));
+}
+
+// the big-endian trailer word be (memory order MSB..LSB) over the 16-byte unit v at record
+// position pos when it overlaps bytes [at, at + 4), merged word by word with masks (a per-lane
+// register index v[at >> 2] would compile to a waterfall loop over the wave)
+__device__ __forceinline__ void merge_trailer(uint32_t v[4], uint32_t pos, uint32_t at,
+                                              uint32_t be) {
+  const int t = (int)at - (int)pos;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int o = t - 4 * k;
+    uint32_t val = 0u, msk = 0u;
+    if (o >= 0 && o < 4) {
+      val = be << (8 * o);
+      msk = 0xFFFFFFFFu << (8 * o);
+    } else if (o < 0 && o > -4) {
+      val = be >> (-8 * o);
+      msk = 0xFFFFFFFFu >> (-8 * o);
+    }
+    v[k] = (v[k] & ~msk) | val;
+  }
+}
+
 // kTcp: the TCP transmit form (PackParams.frag_len: later buffers of a fragment stored from
 // the same units, helper meta waves).  A separate instantiation, so the UDP / SINK paths carry
 // none of its registers (with them in, config 2 pack ran 0.355 ms instead of 0.216).
@@ -113,6 +158,9 @@ pack_kernel(PackParams p) {
   __shared__ uint32_t s_tab[256];
   __shared__ uint32_t s_a4[1024];
 
+  if constexpr (kTcp) {
+    if (p.skip && *p.skip) return;  // (uniform: the whole grid leaves)
+  }
   for (int e = threadIdx.x; e < 256; e += blockDim.x) s_tab[e] = p.byte_tab[e];
   for (int e = threadIdx.x; e < 1024; e += blockDim.x) s_a4[e] = p.a4_tab[e];
   __syncthreads();
@@ -167,6 +215,8 @@ pack_kernel(PackParams p) {
       // indexed by lengths the template fixes.  (Field reads through the template pointer
       // inside the layout walk would each be a serialised round trip.)
       const mgenx_pack_desc d = p.desc[i];
+      // TCP: the fragment this Pack starts (F > bufferLen: later buffers re-send the image)
+      const uint32_t Ft = (kTcp && p.frag_len) ? p.frag_len[i] : 0u;
       const uint32_t* tp = reinterpret_cast<const uint32_t*>(p.tmpl + d.tmpl);
       uint32_t tw[17];
 #pragma unroll
@@ -223,6 +273,37 @@ pack_kernel(PackParams p) {
         // A_len(init): init = ~0 (ComputeCRC32 restarts from a zero state, :530-533) or
         // the caller's running value
         ia_v = crc_in == 0u ? p.ia[crc_len] : multmodp(p.xpow[crc_len], crc_in);
+      }
+      // TCP, a fragment past its first buffer: the CRC runs on through every later buffer
+      // (SetupNextTxBuffer / CalcTxChecksum, mgenTransport.cpp:1818-1876) and the trailer is
+      // the fragment's last 4 bytes.  Later buffer k carries P[0 .. s_k) under the CRC: s_k is
+      // one of at most three lengths (full 8192, one shortened buffer, the last one's size -
+      // 4), so the powers they take are read here, with the others:
+      //   raw(s) = x^(8(s - pend)) raw(P[0 .. pend)) [^ rcrc[s - pend - 2] with RANDOM_FILL]
+      //   c'     = raw(s) ^ x^(8s) c   (c = 0 restarts from ~0, as ComputeCRC32 does)
+      bool chain = false;
+      uint32_t cl[3] = {0u, 0u, 0u}, xs[3] = {0u, 0u, 0u}, xq[3] = {0u, 0u, 0u},
+               rq[3] = {0u, 0u, 0u};
+      if (kTcp && crc_on && Ft > msgLen && !(flags & MGENX_FLAG_LAST_BUFFER)) {
+        chain = true;
+        uint32_t pos = msgLen;
+        for (int k = 0; k < kMaxRep && pos < Ft; k++) {
+          const uint32_t pd = Ft - pos;
+          const bool last = pd <= MGENX_TX_BUFFER_SIZE - 4u;
+          const uint32_t sz = last ? pd
+                                   : ((int32_t)pd - (int32_t)MGENX_TX_BUFFER_SIZE < 4 ? pd - 4u
+                                                                                      : MGENX_TX_BUFFER_SIZE);
+          cl[last ? 2 : (sz == MGENX_TX_BUFFER_SIZE ? 0 : 1)] = last ? sz - 4u : sz;
+          pos += sz;
+        }
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+          xs[j] = p.xpow[cl[j]];
+          if (cl[j] >= pend) {
+            xq[j] = p.xpow[cl[j] - pend];
+            if (rf && cl[j] - pend >= 3u) rq[j] = p.rcrc[cl[j] - pend - 2u];
+          }
+        }
       }
       // payload bytes that land in the header image (statically unrolled: one round trip)
       const uint32_t pimg = pay ? min(t_plen, (uint32_t)kImg > len ? (uint32_t)kImg - len : 0u) : 0u;
@@ -315,24 +396,57 @@ pack_kernel(PackParams p) {
                 for (uint32_t k = 0; k < seg; k++)
                   c = s_tab[(c ^ p.pool[t_poff + k]) & 0xffu] ^ (c >> 8);
               }
-              if (crc_len > pend) c = multmodp(x_f, c) ^ rc_v;
             }
+            const uint32_t cb = c;  // raw(P[0 .. pend)) when crc_len >= pend
+            if (crc_len > len && crc_len > pend) c = multmodp(x_f, c) ^ rc_v;
             tx_checksum = c ^ ia_v;
             tx_out = tx_checksum;
+            if (chain) {  // (crc_len = msgLen >= pend: no LAST_BUFFER here)
+              uint32_t a[3];
+#pragma unroll
+              for (int j = 0; j < 3; j++) {
+                if (cl[j] >= pend) {
+                  a[j] = multmodp(xq[j], cb) ^ rq[j];
+                } else {  // a short last buffer: its bytes are header / payload bytes
+                  uint32_t r = 0;
+                  for (uint32_t k = 0; k < cl[j]; k++) {
+                    const uint32_t b = k < (uint32_t)kImg ? img[k] : p.pool[t_poff + (k - len)];
+                    r = s_tab[(r ^ b) & 0xffu] ^ (r >> 8);
+                  }
+                  a[j] = r;
+                }
+              }
+              uint32_t cc = tx_checksum, pos = msgLen;
+              for (int k = 0; k < kMaxRep && pos < Ft; k++) {
+                const uint32_t pd = Ft - pos;
+                const bool last = pd <= MGENX_TX_BUFFER_SIZE - 4u;
+                const uint32_t sz = last ? pd
+                                         : ((int32_t)pd - (int32_t)MGENX_TX_BUFFER_SIZE < 4 ? pd - 4u
+                                                                                            : MGENX_TX_BUFFER_SIZE);
+                const int j = last ? 2 : (sz == MGENX_TX_BUFFER_SIZE ? 0 : 1);
+                const uint32_t cr = cc == 0u ? 0xFFFFFFFFu : cc;
+                cc = cl[j] ? a[j] ^ multmodp(xs[j], cr) : cr;
+                pos += sz;
+              }
+              m.trailer_on = 2;
+              m.trailer = cc ^ 0xFFFFFFFFu;
+            }
             flags &= ~(uint32_t)MGENX_FLAG_LAST_BUFFER;
           }
         }
-        // caller: WriteChecksum when checksum_enable and the CHECKSUM member flag is set
-        if (!raw && ck && (flags & MGENX_FLAG_CHECKSUM) && m.ret >= 4) {
+        // caller: WriteChecksum when checksum_enable and the CHECKSUM member flag is set (the
+        // TCP form: a one-buffer fragment, mgenTransport.cpp:1376-1385)
+        if ((!raw || (kTcp && p.frag_len && Ft <= msgLen)) && ck && (flags & MGENX_FLAG_CHECKSUM) &&
+            m.ret >= 4) {
           m.trailer_on = 1;
           m.trailer = tx_checksum ^ 0xFFFFFFFFu;
         }
       }
       if (m.off > p.slab_bytes || m.ret > p.slab_bytes - m.off) m.ret = 0;  // never write OOB
       if (kTcp && p.frag_len && m.ret) {
-        const uint32_t F = p.frag_len[i];
-        if (F > m.ret && F <= p.slab_bytes - m.off) m.frag = F;
+        if (Ft > m.ret && Ft <= p.slab_bytes - m.off) m.frag = Ft;
       }
+      if (m.trailer_on == 2 && !m.frag) m.trailer_on = 0;
       m.tx_out = tx_out;
       // the MgenMsg members Pack leaves behind: packet_header_len (set on every return but
       // the failing ones) and the flags member (CHECKSUM set, LAST_BUFFER cleared)
@@ -376,7 +490,7 @@ pack_kernel(PackParams p) {
       // that holds its meta, and its image units from the zero-padded LDS image: a unit is
       // composed with no per-byte masks and no LDS meta read, and kUnroll units go out per
       // lane and pass (their image reads first, then the stores)
-      const uint32_t tword = m.trailer_on ? bswap32(m.trailer) : 0u;
+      const uint32_t tword = m.trailer_on == 1 ? bswap32(m.trailer) : 0u;
       constexpr uint32_t kUnroll = 4;
       for (uint32_t u0 = lane; u0 < units; u0 += 64u * kUnroll) {
         // every LDS read and shuffle of the pass first (unconditional, at clamped addresses),
@@ -437,11 +551,16 @@ pack_kernel(PackParams p) {
               v[kk] = w[kk] & byte_range_mask(0, lim < 0 ? 0 : (lim > 4 ? 4 : lim));
             }
           }
+          if (R.trailer_on == 1 && pos + 16u > R.ret - 4u)
+            merge_trailer(v, pos, R.ret - 4u, bswap32(R.trailer));
+          if (R.trailer_on == 2 && pos == 0u) {  // the fragment's last 4 bytes (no copy there)
+            *reinterpret_cast<u32_u1*>(rbase + R.frag - 4u) = bswap32(R.trailer);
+          }
           const u32x4_t val = {v[0], v[1], v[2], v[3]};
           if (pos + 16u <= R.ret) {
             stu128(rbase + pos, val);
           } else {
-            for (uint32_t j = 0; j < R.ret - pos; j++) rbase[pos + j] = (uint8_t)(v[j >> 2] >> ((j & 3) * 8));
+            st_part(rbase + pos, v, R.ret - pos);
           }
 #pragma unroll
           for (int k = 0; k < kMaxRep; k++) {
@@ -450,7 +569,7 @@ pack_kernel(PackParams p) {
               if (pos + 16u <= reps.cnt[k]) {
                 stu128(d2, val);
               } else {
-                for (uint32_t j = 0; j < reps.cnt[k] - pos; j++) d2[j] = (uint8_t)(v[j >> 2] >> ((j & 3) * 8));
+                st_part(d2, v, reps.cnt[k] - pos);
               }
             }
           }
@@ -538,23 +657,8 @@ pack_kernel(PackParams p) {
               v[kk] = w[kk] & byte_range_mask(0, lim < 0 ? 0 : (lim > 4 ? 4 : lim));
             }
           }
-          if (r.trailer_on && pos + 16 > r.ret - 4) {
-            const uint32_t be = bswap32(r.trailer);
-            const int t = (int)r.ret - 4 - (int)pos;
-#pragma unroll
-            for (int kk = 0; kk < 4; kk++) {
-              const int o = t - 4 * kk;
-              uint32_t val = 0u, msk = 0u;
-              if (o >= 0 && o < 4) {
-                val = be << (8 * o);
-                msk = 0xFFFFFFFFu << (8 * o);
-              } else if (o < 0 && o > -4) {
-                val = be >> (-8 * o);
-                msk = 0xFFFFFFFFu >> (-8 * o);
-              }
-              v[kk] = (v[kk] & ~msk) | val;
-            }
-          }
+          if (r.trailer_on == 1 && pos + 16 > r.ret - 4)
+            merge_trailer(v, pos, r.ret - 4u, bswap32(r.trailer));
           stu128(p.slab + r.off + pos, u32x4_t{v[0], v[1], v[2], v[3]});
         }
       }
@@ -635,33 +739,17 @@ pack_kernel(PackParams p) {
           }
         }
       }
-      // trailer (big-endian CRC at ret-4), merged word by word with masks: a per-lane
-      // register index (v[at >> 2]) would compile to a waterfall loop over the wave
-      if (r.trailer_on && pos + 16 > r.ret - 4) {
-        const uint32_t be = bswap32(r.trailer);  // memory order b0..b3 = MSB..LSB
-        const int t = (int)r.ret - 4 - (int)pos;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          const int o = t - 4 * k;
-          uint32_t val = 0u, msk = 0u;
-          if (o >= 0 && o < 4) {
-            val = be << (8 * o);
-            msk = 0xFFFFFFFFu << (8 * o);
-          } else if (o < 0 && o > -4) {
-            val = be >> (-8 * o);
-            msk = 0xFFFFFFFFu >> (-8 * o);
-          }
-          v[k] = (v[k] & ~msk) | val;
-        }
+      // trailer (big-endian CRC at ret-4)
+      if (r.trailer_on == 1 && pos + 16 > r.ret - 4)
+        merge_trailer(v, pos, r.ret - 4u, bswap32(r.trailer));
+      if (kTcp && r.trailer_on == 2 && pos == 0u) {  // TCP: the fragment's last 4 bytes
+        *reinterpret_cast<u32_u1*>(p.slab + r.off + r.frag - 4u) = bswap32(r.trailer);
       }
       uint8_t* dst = p.slab + r.off + pos;
       if (pos + 16 <= r.ret) {
         stu128(dst, u32x4_t{v[0], v[1], v[2], v[3]});
       } else {
-        const uint32_t rem = r.ret - pos;
-#pragma unroll
-        for (int j = 0; j < 16; j++)
-          if ((uint32_t)j < rem) dst[j] = (uint8_t)(v[j >> 2] >> ((j & 3) * 8));
+        st_part(dst, v, r.ret - pos);
       }
       // TCP: the same bytes in every later buffer of the fragment (no copy pass re-reading P)
       if constexpr (kTcp)
@@ -672,8 +760,7 @@ pack_kernel(PackParams p) {
           if (pos + 16u <= reps.cnt[k]) {
             stu128(d2, u32x4_t{v[0], v[1], v[2], v[3]});
           } else {
-            const uint32_t rem = reps.cnt[k] - pos;
-            for (uint32_t j = 0; j < rem; j++) d2[j] = (uint8_t)(v[j >> 2] >> ((j & 3) * 8));
+            st_part(d2, v, reps.cnt[k] - pos);
           }
         }
       }
