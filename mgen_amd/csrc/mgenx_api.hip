@@ -481,7 +481,8 @@ static int pack_common(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
   const uint64_t batches = ((uint64_t)n + 63) / 64;
   uint64_t grid = (batches + 3) / 4;                // groups of 4 batches (kProd)
   uint64_t cap = (uint64_t)ctx->cu_count * 2;  // 76 KB of LDS per workgroup
-  if (MGENX_DIAG && ctx->pack_variant >= 7) cap *= (uint64_t)(ctx->pack_variant - 5);  // (diag)
+  if (MGENX_DIAG && ctx->pack_variant >= 7 && ctx->pack_variant <= 9)
+    cap *= (uint64_t)(ctx->pack_variant - 5);  // (diag)
   if (grid > cap) grid = cap;
   hipError_t e = mgenx::launch_pack(p, (int)grid, (hipStream_t)stream);
   return e == hipSuccess ? MGENX_OK : set_err(ctx, e, "pack");
@@ -606,8 +607,9 @@ int mgenx_pack_tcp(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl, const uint32
                                              ck, st[(r + 1) & 1], fd, foff, fbuf, ff, s)) !=
                      hipSuccess)
       return set_err(ctx, e, "tcp fragments");
+    // (round 0's fragments start at the message offsets)
     int rc = pack_common(ctx, dev_tmpl, dev_tmpl_crc, fd, n, dev_pool, dev_stream, stream_cap,
-                         foff, 0, fbuf, nullptr, plen, crc, st[r & 1], opts | MGENX_PACK_RAW,
+                         r == 0 ? dev_msg_off : foff, 0, fbuf, nullptr, plen, crc, st[r & 1], opts | MGENX_PACK_RAW,
                          fill_time, stream, ff, ck, gate);
     return rc;
   };
@@ -618,7 +620,7 @@ int mgenx_pack_tcp(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl, const uint32
   // host then spins on the plan's 16-byte verdict in host memory (not the stream's
   // completion: round 0 keeps running), and queues any further rounds.
   if ((e = mgenx::launch_tcp_plan0(dev_tmpl, dev_desc, dev_msg_total, n, ck, stream_cap, epoch,
-                                   status, fmax, dev_msg_off, nfrag, fd, foff, fbuf, ff, skip,
+                                   status, fmax, dev_msg_off, nfrag, fd, fbuf, ff, skip,
                                    ctx->tcp_host_dev, s)) != hipSuccess)
     return set_err(ctx, e, "tcp plan");
   const bool spec = dev_stream != nullptr;

@@ -138,8 +138,8 @@ constexpr uint32_t kTcpPlanEpochs = 1u << 16;
 hipError_t launch_tcp_plan0(const mgenx_flow_tmpl* tmpl, const mgenx_pack_desc* desc,
                             const uint32_t* msg_total, uint32_t n, int ck, uint64_t cap,
                             uint32_t epoch, uint64_t* status, uint64_t* fmax, uint64_t* msg_off,
-                            uint32_t* nfrag, mgenx_pack_desc* fd, uint64_t* foff, uint32_t* fbuf,
-                            uint32_t* ff, uint32_t* skip, uint64_t* host, hipStream_t s);
+                            uint32_t* nfrag, mgenx_pack_desc* fd, uint32_t* fbuf, uint32_t* ff,
+                            uint32_t* skip, uint64_t* host, hipStream_t s);
 // the resident single-message worker (mgenx_worker.hip): a request block the host writes (in
 // fine-grained device memory the host stores into through the BAR when the runtime grants the
 // CPU access to it, else in pinned host memory) and a reply block in pinned host memory

@@ -155,6 +155,9 @@ pack_kernel(PackParams p) {
   __shared__ __attribute__((aligned(16))) uint8_t s_img[2][kProd][64 * kImg];
   __shared__ PackMeta s_meta[2][kProd][64];
   __shared__ uint32_t s_pre[kProd][65];
+  __shared__ uint32_t s_tw[2][kProd * 64];  // trailer words (joint store: any record's)
+  __shared__ uint32_t s_joint[2][kProd];    // batch fills its slots exactly (joint store)
+  __shared__ uint32_t s_tick[2];            // joint store: the next 4-KB chunk of the group
   __shared__ uint32_t s_tab[256];
   __shared__ uint32_t s_a4[1024];
 
@@ -181,6 +184,67 @@ pack_kernel(PackParams p) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   };
+  // The joint aligned-stride store of group g from LDS buffer jb by every wave that calls it
+  // (the store waves, and the meta waves once their own group is built): 4-KB chunks handed
+  // out by an LDS ticket.  Returns false, storing nothing, unless every record of the group
+  // fills its slot exactly (stride layout, zero fill, image inside kImg: the producers'
+  // verdict per batch).
+  auto joint = [&](uint64_t g, int jb) -> bool {
+    const uint32_t nw = (uint32_t)min((uint64_t)kProd, n_batches - g * kProd);  // its batches
+    bool jall = !p.rec_off && !rf && (p.stride & 15u) == 0 && p.stride >= 32 &&
+                p.stride <= 65536 && (variant == 0 || variant >= 7);
+#pragma unroll
+    for (int k = 0; k < kProd; k++)
+      if ((uint32_t)k < nw && !s_joint[jb][k]) jall = false;
+    if (!jall) return false;
+    const uint32_t U = (uint32_t)(p.stride >> 4);        // units per record
+    const uint32_t q = 64u / U, rm = 64u % U;            // unit step = q records + rm units
+    const uint64_t R0 = g * (uint64_t)(kProd * 64);
+    const uint32_t nrec = (uint32_t)min((uint64_t)(kProd * 64), (uint64_t)p.n - R0);
+    const uint32_t units = nrec * U;
+    uint8_t* const base = p.slab + R0 * p.stride;
+    const uint8_t* const G_IMG = &s_img[jb][0][0];
+    const uint32_t* const G_TW = s_tw[jb];
+    const float invU = 1.0f / (float)U;
+    constexpr uint32_t kUnroll = 4, kChunk = 64u * kUnroll;  // units: 4 KB
+    for (;;) {
+      uint32_t t = 0;
+      if (lane == 0) t = atomicAdd(&s_tick[jb], 1u);
+      const uint32_t c0 = (uint32_t)__shfl((int)t, 0) * kChunk;
+      if (c0 >= units) break;
+      const uint32_t u = c0 + (uint32_t)lane;
+      uint32_t r = (uint32_t)((float)u * invU);
+      if (r * U > u) r--;
+      else if ((r + 1u) * U <= u) r++;
+      uint32_t pu = u - r * U;
+      u32x4_t v[kUnroll];
+      uint32_t tw[kUnroll], pos[kUnroll], rr[kUnroll], last[kUnroll];
+#pragma unroll
+      for (uint32_t k = 0; k < kUnroll; k++) {
+        pos[k] = pu << 4;
+        rr[k] = r;
+        last[k] = pu == U - 1u;
+        const uint32_t rc = min(r, (uint32_t)(kProd * 64) - 1u);
+        tw[k] = G_TW[rc];
+        v[k] = *reinterpret_cast<const u32x4_t*>(
+            &G_IMG[rc * kImg + min(pos[k], (uint32_t)kImg - 16u)]);
+        pu += rm;
+        r += q;
+        if (pu >= U) { pu -= U; r++; }
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < kUnroll; k++) {
+        if (!(pos[k] < (uint32_t)kImg && rr[k] < nrec)) v[k] = u32x4_t{0u, 0u, 0u, 0u};
+        if (last[k] && tw[k]) v[k].w = tw[k];
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < kUnroll; k++) {
+        const uint32_t at = c0 + (uint32_t)lane + 64u * k;
+        if (at < units) stu128(base + (uint64_t)at * 16u, v[k]);
+      }
+    }
+    return true;
+  };
   // stage s: producers build group blockIdx.x + s * gridDim.x into buffer s & 1, consumers
   // store group blockIdx.x + (s - 1) * gridDim.x from buffer (s - 1) & 1 (block-uniform)
   for (uint64_t s = 0;; s++) {
@@ -196,8 +260,16 @@ pack_kernel(PackParams p) {
     uint8_t* const S_IMG = &s_img[buf][slot][0];
     PackMeta* const S_META = s_meta[buf][slot];
     const uint64_t i = (b << 6) + lane;
+    if constexpr (!kTcp) {
+      // a meta wave with no group to build helps store the group of the other buffer
+      if (producer && !prod_live && cons_live) {
+        (void)joint(gp - gridDim.x, (int)((s - 1) & 1));
+        goto stage_end;
+      }
+    }
     if (!(builds ? prod_live : cons_live) || b >= n_batches) goto stage_end;
     if (builds) {
+    if (!kTcp && slot == 0 && lane == 0) s_tick[buf] = 0u;  // (this buffer's store is next stage)
     uint8_t* img = S_IMG + lane * kImg;
     // the image slot starts as zeros: the bytes past pend read as the record's zero fill, so
     // the aligned-stride store loop loads image units without masking them
@@ -453,6 +525,14 @@ pack_kernel(PackParams p) {
       m.state = (m.ret ? (uint32_t)m.hdr : 0xFFFFu) | (flags & 0xffu) << 16;
     }
     S_META[lane] = m;
+    if constexpr (!kTcp) {  // for the joint store: the trailer word, the batch's verdict
+      s_tw[buf][slot * 64 + lane] = m.trailer_on == 1 ? bswap32(m.trailer) : 0u;
+      const bool jok = i >= p.n || (m.ret == (uint32_t)p.stride && m.pend <= (uint32_t)kImg);
+      const bool jall = __all(jok);
+      if (lane == 0) s_joint[buf][slot] = jall ? 1u : 0u;
+      // then help store the group of the other buffer (its verdicts came a stage ago)
+      if (s > 0 && cons_live) (void)joint(gp - gridDim.x, (int)((s - 1) & 1));
+    }
     goto stage_end;
     }
     {
@@ -472,55 +552,22 @@ pack_kernel(PackParams p) {
     // over them.  Everything else keeps one (unaligned) unit store per 16 record bytes.
     const uint32_t nv = b < n_batches ? (uint32_t)min((uint64_t)64, (uint64_t)p.n - (b << 6)) : 0u;
     const bool has = (uint32_t)lane < nv;
-    // Aligned stride path (config 2, the recvmmsg slot layout): every record of the wave
+    // Aligned stride path (config 2, the recvmmsg slot layout): every record of the group
     // fills its 16-byte-aligned slot exactly (ret == stride), zero fill, image inside kImg.
-    // Each 16-byte unit of the wave's range is composed once -- zeros, image bytes, or the
-    // trailer -- and stored once: no second pass over lines already written (re-writing a
-    // record's head and tail units after the fill costs 8 % more bytes but a quarter more
-    // time: the lines have left L2 by then and come back as partial writes).
-    const bool stride_ok = !has || (m.ret == (uint32_t)p.stride && m.pend <= (uint32_t)kImg);
-    if (!p.rec_off && !rf && (p.stride & 15u) == 0 && p.stride >= 32 && nv > 0 &&
-        (variant == 0 || variant >= 7) && __all(stride_ok)) {
-      const uint32_t U = (uint32_t)(p.stride >> 4);        // units per record
-      const uint32_t q = 64u / U, rm = 64u % U;            // unit step = q records + rm units
-      uint32_t r = (uint32_t)lane / U, pu = (uint32_t)lane % U;
-      uint8_t* base = p.slab + (b << 6) * p.stride;
-      const uint32_t units = nv * U;
-      // record r's trailer word (bytes ret - 4 .. ret - 1, big-endian; 0 without) from the lane
-      // that holds its meta, and its image units from the zero-padded LDS image: a unit is
-      // composed with no per-byte masks and no LDS meta read, and kUnroll units go out per
-      // lane and pass (their image reads first, then the stores)
-      const uint32_t tword = m.trailer_on == 1 ? bswap32(m.trailer) : 0u;
-      constexpr uint32_t kUnroll = 4;
-      for (uint32_t u0 = lane; u0 < units; u0 += 64u * kUnroll) {
-        // every LDS read and shuffle of the pass first (unconditional, at clamped addresses),
-        // so they go out together and one wait covers them; then the selects and the stores
-        u32x4_t v[kUnroll];
-        uint32_t tw[kUnroll], pos[kUnroll], rr[kUnroll], last[kUnroll];
-#pragma unroll
-        for (uint32_t k = 0; k < kUnroll; k++) {
-          pos[k] = pu << 4;
-          rr[k] = r;
-          last[k] = pu == U - 1u;
-          tw[k] = (uint32_t)__shfl((int)tword, (int)min(r, 63u));
-          v[k] = *reinterpret_cast<const u32x4_t*>(
-              &S_IMG[min(r, 63u) * kImg + min(pos[k], (uint32_t)kImg - 16u)]);
-          pu += rm;
-          r += q;
-          if (pu >= U) { pu -= U; r++; }
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < kUnroll; k++) {
-          if (!(pos[k] < (uint32_t)kImg && rr[k] < nv)) v[k] = u32x4_t{0u, 0u, 0u, 0u};
-          if (last[k] && tw[k]) v[k].w = tw[k];
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < kUnroll; k++) {
-          const uint32_t at = u0 + 64u * k;
-          if (at < units) stu128(base + (uint64_t)at * 16u, v[k]);
-        }
-      }
-      goto stage_end;
+    // Each 16-byte unit of the range is composed once -- zeros, image bytes (from the
+    // zero-padded LDS image: no per-byte masks), or the trailer -- and stored once: no second
+    // pass over lines already written (re-writing a record's head and tail units after the
+    // fill costs 8 % more bytes but a quarter more time: the lines have left L2 by then and
+    // come back as partial writes).  kUnroll units go out per lane and pass, their LDS reads
+    // issued together first.  The group's range is stored jointly (joint(), above): 4-KB
+    // chunks handed out by an LDS ticket to the store waves and, once their own group is
+    // built, the meta waves, so the workgroup's stores march through one contiguous range
+    // (instead of kProd streams 64 KB apart) with every wave that has nothing else to do.  A
+    // unit's record is found by a float reciprocal (exact after one correction: units <
+    // 2^24), its image bytes and trailer word come from LDS (the producers' s_tw; s_joint:
+    // the batch qualifies).
+    if constexpr (!kTcp) {
+      if (joint(gp - gridDim.x, buf)) goto stage_end;
     }
     // Big TCP buffers (PackParams.frag_len set, every record >= 1 KiB, zero fill, image
     // holding header + payload): record by record, the wave's 64 lanes over its 16-byte

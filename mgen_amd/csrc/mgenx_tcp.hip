@@ -179,9 +179,9 @@ tcp_plan0_kernel(const mgenx_flow_tmpl* __restrict__ tmpl, const mgenx_pack_desc
                  const uint32_t* __restrict__ msg_total, uint32_t n, int ck, uint64_t cap,
                  uint32_t epoch, uint64_t* __restrict__ status, uint64_t* __restrict__ fmax,
                  uint64_t* __restrict__ msg_off, uint32_t* __restrict__ nfrag,
-                 mgenx_pack_desc* __restrict__ fd, uint64_t* __restrict__ foff,
-                 uint32_t* __restrict__ fbuf, uint32_t* __restrict__ ff,
-                 uint32_t* __restrict__ skip, uint64_t* __restrict__ host) {
+                 mgenx_pack_desc* __restrict__ fd, uint32_t* __restrict__ fbuf,
+                 uint32_t* __restrict__ ff, uint32_t* __restrict__ skip,
+                 uint64_t* __restrict__ host) {
   __shared__ uint32_t s_bytes[kTcpPlanMsgs];
   __shared__ uint64_t s_off[kTcpPlanMsgs];
   __shared__ uint64_t wsum[kPlanThreads / 64];
@@ -206,8 +206,21 @@ tcp_plan0_kernel(const mgenx_flow_tmpl* __restrict__ tmpl, const mgenx_pack_desc
     s_bytes[u * kPlanThreads + tid] = c[u] ? M[u] : 0u;
     mx = max(mx, c[u]);
   }
+  // 2. fragment counts and round 0's descriptors (independent of the offsets: out before the
+  // look-back)
+#pragma unroll
+  for (uint32_t u = 0; u < kPlanPer; u++) {
+    const uint32_t i = base + u * kPlanThreads + tid;
+    if (i >= n) continue;
+    mgenx_pack_desc d = desc[i];
+    const uint32_t F = c[u] ? F0[u] : 0u;
+    fbuf[i] = tcp_frag_desc(d, d.flags, M[u], F, M[u] > F, ck);
+    fd[i] = d;
+    ff[i] = F;
+    nfrag[i] = c[u];
+  }
   __syncthreads();
-  // 2. the block's exclusive offsets (thread t: entries 4t .. 4t+3) and its aggregate
+  // 3. the block's exclusive offsets (thread t: entries 4t .. 4t+3) and its aggregate
   uint64_t loc[kPlanPer], tot = 0;
 #pragma unroll
   for (uint32_t k = 0; k < kPlanPer; k++) {
@@ -235,7 +248,7 @@ tcp_plan0_kernel(const mgenx_flow_tmpl* __restrict__ tmpl, const mgenx_pack_desc
   }
 #pragma unroll
   for (uint32_t k = 0; k < kPlanPer; k++) s_off[kPlanPer * tid + k] = run + loc[k];
-  // 3. the block's first offset: aggregate, look-back (wave 0), its fragment maximum (and
+  // 4. the block's first offset: aggregate, look-back (wave 0), its fragment maximum (and
   // failure bit), inclusive
   if (wv == 0) {
     if (lane == 0)  // (an aggregate even for block 0: its inclusive word must follow its maximum)
@@ -309,21 +322,12 @@ tcp_plan0_kernel(const mgenx_flow_tmpl* __restrict__ tmpl, const mgenx_pack_desc
     }
   }
   __syncthreads();
-  // 4. offsets, fragment counts, round 0's descriptors
+  // 5. the offsets (round 0's fragments start at them: Pack reads msg_off as its record offsets)
   const uint64_t first = s_prefix;
 #pragma unroll
   for (uint32_t u = 0; u < kPlanPer; u++) {
     const uint32_t i = base + u * kPlanThreads + tid;
-    if (i >= n) continue;
-    const uint64_t off = first + s_off[u * kPlanThreads + tid];
-    mgenx_pack_desc d = desc[i];
-    const uint32_t F = c[u] ? F0[u] : 0u;
-    fbuf[i] = tcp_frag_desc(d, d.flags, M[u], F, M[u] > F, ck);
-    fd[i] = d;
-    foff[i] = off;
-    ff[i] = F;
-    msg_off[i] = off;
-    nfrag[i] = c[u];
+    if (i < n) msg_off[i] = first + s_off[u * kPlanThreads + tid];
   }
 }
 
@@ -347,11 +351,11 @@ hipError_t launch_tcp_frag(const mgenx_pack_desc* desc, const uint32_t* msg_tota
 hipError_t launch_tcp_plan0(const mgenx_flow_tmpl* tmpl, const mgenx_pack_desc* desc,
                             const uint32_t* msg_total, uint32_t n, int ck, uint64_t cap,
                             uint32_t epoch, uint64_t* status, uint64_t* fmax, uint64_t* msg_off,
-                            uint32_t* nfrag, mgenx_pack_desc* fd, uint64_t* foff, uint32_t* fbuf,
-                            uint32_t* ff, uint32_t* skip, uint64_t* host, hipStream_t s) {
+                            uint32_t* nfrag, mgenx_pack_desc* fd, uint32_t* fbuf, uint32_t* ff,
+                            uint32_t* skip, uint64_t* host, hipStream_t s) {
   hipLaunchKernelGGL(tcp_plan0_kernel, dim3((n + kTcpPlanMsgs - 1) / kTcpPlanMsgs),
                      dim3(kPlanThreads), 0, s, tmpl, desc, msg_total, n, ck, cap, epoch, status,
-                     fmax, msg_off, nfrag, fd, foff, fbuf, ff, skip, host);
+                     fmax, msg_off, nfrag, fd, fbuf, ff, skip, host);
   return hipGetLastError();
 }
 
