@@ -246,8 +246,10 @@ int mgenx_pack_msgs(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
  * buffer is re-sent from its start, the CRC (MGENX_PACK_CHECKSUM) covering every byte
  * before the trailer.  dev_msg_off[i] = the message's offset in the stream (a message whose
  * first Pack fails, or of length 0, takes no bytes); *total_bytes = the stream length.
- * Synchronous (the stream layout decides the launches); when the stream would exceed
- * stream_cap nothing is written, *total_bytes is set and MGENX_EINVAL returned. */
+ * Waits for the plan only (the stream layout decides the launches): it returns once the
+ * stream length is known, with the stores still running on `stream` (stream-ordered, as any
+ * launch).  When the stream would exceed stream_cap nothing is written, *total_bytes is set
+ * and MGENX_EINVAL returned. */
 int mgenx_pack_tcp(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl, const uint32_t* dev_tmpl_crc,
                    const mgenx_pack_desc* dev_desc, const uint32_t* dev_msg_total, uint32_t n,
                    const uint8_t* dev_pool, uint8_t* dev_stream, uint64_t stream_cap,

@@ -97,26 +97,29 @@ __device__ __forceinline__ void img_put32(uint8_t* img, uint32_t at, uint32_t v)
 
 typedef uint32_t u32x2_u1 __attribute__((ext_vector_type(2), aligned(1)));
 
-// the first rem (< 16) bytes of the unit v at d: at most four stores (8, 4, 2, 1 bytes; the
-// word picked by selects, not by a register index)
+// the first rem (< 16) bytes of the unit v at d: at most four stores (8, 4, 2, 1 bytes), the
+// words moved down as they go out (a select on the byte offset becomes an indexed scratch
+// load: the compiler turns such select chains into a stack array)
 __device__ __forceinline__ void st_part(uint8_t* d, const uint32_t v[4], uint32_t rem) {
-  auto word_at = [&](uint32_t o) {  // the word holding byte o
-    return o < 4u ? v[0] : (o < 8u ? v[1] : (o < 12u ? v[2] : v[3]));
-  };
-  uint32_t o = 0;
+  uint32_t a0 = v[0], a1 = v[1];
+  const uint32_t a2 = v[2], a3 = v[3];
   if (rem & 8u) {
-    *reinterpret_cast<u32x2_u1*>(d) = u32x2_u1{v[0], v[1]};
-    o = 8u;
+    *reinterpret_cast<u32x2_u1*>(d) = u32x2_u1{a0, a1};
+    d += 8;
+    a0 = a2;
+    a1 = a3;
   }
   if (rem & 4u) {
-    *reinterpret_cast<u32_u1*>(d + o) = word_at(o);
-    o += 4u;
+    *reinterpret_cast<u32_u1*>(d) = a0;
+    d += 4;
+    a0 = a1;
   }
   if (rem & 2u) {
-    *reinterpret_cast<u16_u1*>(d + o) = (uint16_t)(word_at(o) >> (8u * (o & 3u)));
-    o += 2u;
+    *reinterpret_cast<u16_u1*>(d) = (uint16_t)a0;
+    d += 2;
+    a0 >>= 16;
   }
-  if (rem & 1u) d[o] = (uint8_t)(word_at(o) >> (8u * (o & 3u)));
+  if (rem & 1u) *d = (uint8_t)a0;
 }
 
 // the big-endian trailer word be (memory order MSB..LSB) over the 16-byte unit v at record
@@ -570,57 +573,83 @@ pack_kernel(PackParams p) {
       if (joint(gp - gridDim.x, buf)) goto stage_end;
     }
     // Big TCP buffers (PackParams.frag_len set, every record >= 1 KiB, zero fill, image
-    // holding header + payload): record by record, the wave's 64 lanes over its 16-byte
-    // units -- a unit is its image bytes or zeros, stored in P and in each later buffer of
-    // the fragment.  (The general walk below spends most of its instructions per unit on
-    // finding the unit's record and on the fill / payload / trailer cases.)
+    // holding header + payload): record by record, the wave's 64 lanes walk the whole
+    // FRAGMENT [0, Fe) in 16-byte units, consecutive lanes on consecutive units -- P, then each
+    // later buffer k (P[0 .. cnt_k) again from its start), then the trailer (Fe - 4 .. Fe: the
+    // fragment's CRC, or a one-buffer record's WriteChecksum).  A unit that starts a 16-byte
+    // step into its buffer and ends before the next boundary is an image unit or zeros; the
+    // few others (a buffer start off 16, the trailer) are composed byte by byte.  One store per
+    // unit, each wave instruction 1 KB of contiguous fragment.  (The general walk below spends
+    // most of its instructions per unit on finding the unit's record and on the fill / payload
+    // / trailer cases.)
     if (kTcp && p.frag_len && !rf && nv > 0 &&
         __all(!has || (m.pend <= (uint32_t)kImg && (m.ret == 0u || m.ret >= 1024u)))) {
       const bool fck = p.frag_ck != 0;
-      // with a helper (no group built this stage) the two waves take alternate records
+      // with a helper (no group built this stage) the two waves take alternate records, each
+      // with its own boundary table in LDS
       const uint32_t rstep = prod_live ? 1u : 2u;
+      uint32_t* const bst = &s_pre[slot][helper ? 32 : 0];
       for (uint32_t rr = helper ? 1u : 0u; rr < nv; rr += rstep) {
         const PackMeta R = S_META[rr];
         if (R.ret == 0u) continue;
         const TcpReps reps = tcp_reps(R.frag, R.ret, fck);
         const uint8_t* rimg = &S_IMG[rr * kImg];
-        const uint32_t nu = (R.ret + 15u) >> 4;
+        const uint32_t Fe = R.frag ? R.frag : R.ret;       // the fragment's end
+        const uint32_t T = R.trailer_on ? Fe - 4u : Fe;     // where its trailer starts
+        const uint32_t be = bswap32(R.trailer);             // trailer bytes in memory order
+        // buffer starts: 0 (P), then each later buffer's; nb buffers, bst[nb] = Fe
+        uint32_t nb = 1;
+#pragma unroll
+        for (int k = 0; k < kMaxRep; k++) nb += reps.start[k] ? 1u : 0u;
+        if (lane == 0) bst[0] = 0u;
+#pragma unroll
+        for (int k = 0; k < kMaxRep; k++)
+          if (lane == k + 1 && reps.start[k]) bst[k + 1] = reps.start[k];
+        if (lane == 0) bst[nb] = Fe;
+        wave_sync();
         uint8_t* const rbase = p.slab + R.off;
+        const uint32_t nu = (Fe + 15u) >> 4;
+        uint32_t kb = 0, bcur = 0, bnext = bst[1];
         for (uint32_t u = (uint32_t)lane; u < nu; u += 64u) {
-          const uint32_t pos = u << 4;
-          uint32_t v[4] = {0u, 0u, 0u, 0u};
-          if (pos < R.pend) {
-            const u32x4_t iv = *reinterpret_cast<const u32x4_t*>(rimg + pos);
-            const uint32_t w[4] = {iv.x, iv.y, iv.z, iv.w};
+          const uint32_t x = u << 4;
+          while (x >= bnext && kb + 1u < nb) {
+            kb++;
+            bcur = bnext;
+            bnext = bst[kb + 1];
+          }
+          const uint32_t pos = x - bcur;
+          const u32x4_t iv = *reinterpret_cast<const u32x4_t*>(rimg + min(pos, (uint32_t)kImg - 16u));
+          uint32_t v[4] = {iv.x, iv.y, iv.z, iv.w};
+          if (pos >= (uint32_t)kImg) v[0] = v[1] = v[2] = v[3] = 0u;  // (past pend: zero fill)
+          if ((pos & 15u) != 0u || x + 16u > min(bnext, T)) {
+            // a unit across a boundary or off the 16-byte grid of its buffer: byte by byte
+            uint32_t kk = kb, bc = bcur, bn = bnext;
 #pragma unroll
-            for (int kk = 0; kk < 4; kk++) {
-              const int lim = (int)R.pend - (int)pos - 4 * kk;
-              v[kk] = w[kk] & byte_range_mask(0, lim < 0 ? 0 : (lim > 4 ? 4 : lim));
-            }
-          }
-          if (R.trailer_on == 1 && pos + 16u > R.ret - 4u)
-            merge_trailer(v, pos, R.ret - 4u, bswap32(R.trailer));
-          if (R.trailer_on == 2 && pos == 0u) {  // the fragment's last 4 bytes (no copy there)
-            *reinterpret_cast<u32_u1*>(rbase + R.frag - 4u) = bswap32(R.trailer);
-          }
-          const u32x4_t val = {v[0], v[1], v[2], v[3]};
-          if (pos + 16u <= R.ret) {
-            stu128(rbase + pos, val);
-          } else {
-            st_part(rbase + pos, v, R.ret - pos);
-          }
-#pragma unroll
-          for (int k = 0; k < kMaxRep; k++) {
-            if (pos < reps.cnt[k]) {
-              uint8_t* d2 = rbase + reps.start[k] + pos;
-              if (pos + 16u <= reps.cnt[k]) {
-                stu128(d2, val);
+            for (int j = 0; j < 16; j++) {
+              const uint32_t xb = x + (uint32_t)j;
+              uint32_t byte = 0u;
+              if (xb >= T) {
+                byte = xb < Fe ? (be >> (8u * (xb - T))) & 0xffu : 0u;
               } else {
-                st_part(d2, v, reps.cnt[k] - pos);
+                while (xb >= bn) {
+                  kk++;
+                  bc = bn;
+                  bn = bst[kk + 1];
+                }
+                const uint32_t q = xb - bc;
+                byte = q < (uint32_t)kImg ? rimg[q] : 0u;
               }
+              if ((j & 3) == 0) v[j >> 2] = 0u;
+              v[j >> 2] |= byte << (8 * (j & 3));
             }
+          }
+          if (x + 16u <= Fe) {
+            stu128(rbase + x, u32x4_t{v[0], v[1], v[2], v[3]});
+          } else {
+            st_part(rbase + x, v, Fe - x);
           }
         }
+        wave_sync();  // (the boundary table is rewritten for the next record)
       }
       goto stage_end;
     }
