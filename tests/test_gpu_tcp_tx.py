@@ -148,3 +148,41 @@ def test_tcp_tx_short_buffer_no_store_past_it(torch, eng, gold):
     assert bool((buf[cap:] == 0xAB).all())
     got, _ = eng.pack_tcp(tm, crc, dd, dt, len(d), pool, opts=PACK_CHECKSUM)
     assert np.array_equal(got.cpu().numpy(), want)
+
+
+def test_tcp_tx_plan_overflow_takes_exact_path(torch, eng, gold):
+    """A stream past the one-launch plan's 2^46-byte running totals (16,385 messages of
+    2^32 - 1 bytes) sends mgenx_pack_tcp to its exact path (plan kernel, device-wide scan):
+    the reported length and the message offsets are still exact (uint64), and with no
+    stream buffer the call fails with that length set."""
+    import ctypes
+    from mgen_amd import PACK_CHECKSUM, to_device
+    from mgen_amd import _ptr, _stream
+    rng = np.random.default_rng(23)
+    n = 16385
+    d, total = _case(gold, rng, [0xFFFFFFFF] * n)
+    ok = np.isin(gold["tmpl"]["dst_type"][d["tmpl"]], [1, 2])
+    bytes_ = np.where(ok, np.uint64(0xFFFFFFFF), np.uint64(0))
+    want_total = int(bytes_.sum())
+    assert want_total >= 1 << 46
+    tm, pool = to_device(gold["tmpl"]), to_device(gold["pool"])
+    crc = torch.empty(len(gold["tmpl"]), dtype=torch.int32, device="cuda")
+    eng.pack_prepare(tm, len(gold["tmpl"]), pool, crc)
+    dd, dt = to_device(d), to_device(total)
+    offs = torch.empty(n, dtype=torch.int64, device="cuda")
+    tot = ctypes.c_uint64(0)
+    rc = eng.lib.mgenx_pack_tcp(eng.ctx, _ptr(tm), _ptr(crc), _ptr(dd), _ptr(dt), n,
+                                _ptr(pool), None, 0, _ptr(offs), ctypes.byref(tot),
+                                PACK_CHECKSUM, 0, _stream(eng.device))
+    torch.cuda.synchronize()
+    assert rc != 0 and tot.value == want_total
+    got = offs.cpu().numpy().view(np.uint64)
+    want = np.concatenate([[0], np.cumsum(bytes_)[:-1]]).astype(np.uint64)
+    assert np.array_equal(got, want)
+    # and the one-launch path is back for the next (small) call
+    small_d, small_t = _case(gold, rng, [1000, 20000, 70000])
+    out, offs2 = _gpu(torch, eng, gold, small_d, small_t, PACK_CHECKSUM)
+    from oracle import oracle as O
+    want2 = np.asarray(O.tcp_tx_batch(gold["tmpl"], small_d, small_t, gold["pool"], checksum=True),
+                       np.uint8)
+    assert np.array_equal(out, want2)
