@@ -186,3 +186,34 @@ def test_tcp_tx_plan_overflow_takes_exact_path(torch, eng, gold):
     want2 = np.asarray(O.tcp_tx_batch(gold["tmpl"], small_d, small_t, gold["pool"], checksum=True),
                        np.uint8)
     assert np.array_equal(out, want2)
+
+
+def test_tcp_tx_plan_epoch_wrap(torch, eng, gold):
+    """The one-launch plan tags its look-back words and verdict with a 16-bit epoch, cleared
+    when it wraps: 65,540 back-to-back calls on one context (past the wrap) stay byte-exact,
+    multi-fragment messages included."""
+    import ctypes
+    from mgen_amd import PACK_CHECKSUM, to_device
+    from mgen_amd import _ptr, _stream
+    from oracle import oracle as O
+    rng = np.random.default_rng(31)
+    d, total = _case(gold, rng, [100, 20000, 70000, 9000])
+    want = np.asarray(O.tcp_tx_batch(gold["tmpl"], d, total, gold["pool"], checksum=True),
+                      np.uint8)
+    tm, pool = to_device(gold["tmpl"]), to_device(gold["pool"])
+    crc = torch.empty(len(gold["tmpl"]), dtype=torch.int32, device="cuda")
+    eng.pack_prepare(tm, len(gold["tmpl"]), pool, crc)
+    dd, dt = to_device(d), to_device(total)
+    buf = torch.zeros(len(want), dtype=torch.uint8, device="cuda")
+    offs = torch.empty(len(d), dtype=torch.int64, device="cuda")
+    tot = ctypes.c_uint64(0)
+    args = (eng.ctx, _ptr(tm), _ptr(crc), _ptr(dd), _ptr(dt), len(d), _ptr(pool), _ptr(buf),
+            len(want), _ptr(offs), ctypes.byref(tot), PACK_CHECKSUM, 0, _stream(eng.device))
+    fn = eng.lib.mgenx_pack_tcp
+    for k in range(65540):
+        if k == 65530:  # (the last calls write into a cleared buffer)
+            torch.cuda.synchronize()
+            buf.zero_()
+        assert fn(*args) == 0 and tot.value == len(want), k
+    torch.cuda.synchronize()
+    assert np.array_equal(buf.cpu().numpy(), want)
