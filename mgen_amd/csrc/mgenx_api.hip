@@ -608,10 +608,9 @@ int mgenx_pack_tcp(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl, const uint32
                      hipSuccess)
       return set_err(ctx, e, "tcp fragments");
     // (round 0's fragments start at the message offsets)
-    int rc = pack_common(ctx, dev_tmpl, dev_tmpl_crc, fd, n, dev_pool, dev_stream, stream_cap,
-                         r == 0 ? dev_msg_off : foff, 0, fbuf, nullptr, plen, crc, st[r & 1], opts | MGENX_PACK_RAW,
-                         fill_time, stream, ff, ck, gate);
-    return rc;
+    return pack_common(ctx, dev_tmpl, dev_tmpl_crc, fd, n, dev_pool, dev_stream, stream_cap,
+                       r == 0 ? dev_msg_off : foff, 0, fbuf, nullptr, plen, crc, st[r & 1],
+                       opts | MGENX_PACK_RAW, fill_time, stream, ff, ck, gate);
   };
   // One launch plans every message, scans the offsets straight into the caller's array and
   // writes round 0's descriptors; round 0 is queued behind it before the host has read the
