@@ -584,6 +584,7 @@ pack_kernel(PackParams p) {
     // / trailer cases.)
     if (kTcp && p.frag_len && !rf && nv > 0 &&
         __all(!has || (m.pend <= (uint32_t)kImg && (m.ret == 0u || m.ret >= 1024u)))) {
+      if (MGENX_DIAG && variant == 1) goto stage_end;  // (diagnostics: no store phase)
       const bool fck = p.frag_ck != 0;
       // with a helper (no group built this stage) the two waves take alternate records, each
       // with its own boundary table in LDS

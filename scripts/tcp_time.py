@@ -12,7 +12,10 @@ from mgen_amd._abi import DESC_DTYPE  # noqa: E402
 from mgen_amd.workloads import make_templates  # noqa: E402
 
 n = 65536
-eng = Engine(0)
+# python scripts/tcp_time.py [V]: with V, the diagnostics build at pack variant V
+eng = Engine(0, diag=len(sys.argv) > 1)
+if len(sys.argv) > 1:
+    eng.set_pack_variant(int(sys.argv[1]))
 tmpl, pool = make_templates(64)
 desc = np.zeros(n, DESC_DTYPE)
 seq = np.arange(n)
