@@ -164,12 +164,13 @@ pack_kernel(PackParams p) {
   __shared__ uint32_t s_tab[256];
   __shared__ uint32_t s_a4[1024];
 
-  if constexpr (kTcp) {
-    if (p.skip && *p.skip) return;  // (uniform: the whole grid leaves)
-  }
+  // (TCP: the plan's verdict is read first and acted on after the table loads, so its latency
+  // overlaps theirs; uniform: the whole grid leaves)
+  const bool skip_all = kTcp && p.skip && *p.skip;
   for (int e = threadIdx.x; e < 256; e += blockDim.x) s_tab[e] = p.byte_tab[e];
   for (int e = threadIdx.x; e < 1024; e += blockDim.x) s_a4[e] = p.a4_tab[e];
   __syncthreads();
+  if (skip_all) return;
 
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
