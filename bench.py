@@ -37,7 +37,7 @@ REC = 1024
 ALGO_BYTES = N_REC * REC + N_REC * 32
 PACK_BYTES = N_REC * REC + N_REC * 20   # records written + 20-B descriptors read
 PEAK_HBM_GBPS = 8000.0   # MI355X_MICROARCH.md chip table (spec); 6.29 TB/s measured copy
-ROUND = "r04"
+ROUND = "r06"
 
 
 def cpu_baseline(budget_s=6.0):
@@ -178,7 +178,7 @@ def load_traffic():
     rocprofv3 counters cannot be collected inside this process, so the figure is read from
     that file and labelled with its source."""
     path = None
-    for rnd in (ROUND, "r03"):   # this round's PMC passes, else the last round's
+    for rnd in (ROUND, "r05", "r04", "r03"):   # this round's PMC passes, else the latest earlier
         p = os.path.join(ROOT, "profiles", f"traffic_{rnd}.json")
         if os.path.exists(p):
             path = p

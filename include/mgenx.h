@@ -249,7 +249,9 @@ int mgenx_pack_msgs(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
  * Waits for the plan only (the stream layout decides the launches): it returns once the
  * stream length is known, with the stores still running on `stream` (stream-ordered, as any
  * launch).  When the stream would exceed stream_cap nothing is written, *total_bytes is set
- * and MGENX_EINVAL returned. */
+ * and MGENX_EINVAL returned.  A context's TCP transmit calls must all use ONE stream: the plan
+ * leaves its verdict in a per-context device word that the queued Pack reads, so a call on
+ * another stream could overwrite it before the first call's Pack has read it. */
 int mgenx_pack_tcp(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl, const uint32_t* dev_tmpl_crc,
                    const mgenx_pack_desc* dev_desc, const uint32_t* dev_msg_total, uint32_t n,
                    const uint8_t* dev_pool, uint8_t* dev_stream, uint64_t stream_cap,
@@ -324,8 +326,10 @@ int mgenx_worker_recv(mgenx_worker* w, const uint8_t* msg, uint32_t len, uint32_
                       mgenx_unpacked* out, uint32_t* crc_state, uint32_t* crc_done);
 /* MgenAnalytic::Update (include/mgenAnalytic.h:91-94, mgenAnalytic.cpp:74-258) of ONE record
  * on the device flow state dev_flows[slot] (mgenx_flow_init / mgenx_flow_reduce's array; the
- * wave reads and writes it in place, so batch calls before and after on the same stream order
- * see it): *updated = 1 when the record closed a window, with the report in *report (index =
+ * worker's wave reads and writes it in place).  The wave is NOT on the caller's stream: the
+ * stream that last wrote dev_flows (a queued mgenx_flow_reduce or mgenx_flow_init) must be
+ * synchronised before this call, and later batch work on dev_flows enqueued only after it
+ * returns.  *updated = 1 when the record closed a window, with the report in *report (index =
  * the flow's report number; latency_ave from the window's in-order latency sum).  Equal to
  * mgenx_flow_reduce of the same records one call at a time. */
 struct mgenx_flow_state;

@@ -177,8 +177,14 @@ class Engine {
     if (n == 1 && Worker()) {
       mgenx_unpacked u;
       uint32_t crc = 0, done = 0;
-      Check(mgenx_worker_recv(worker_, bufs[0], lens[0], force ? 1u : 0u, &u, &crc, &done),
-            "mgenx_worker_recv");
+      // the flags byte (offset 3, MgenMsg::FLAGS_OFFSET) decides whether a CRC follows: without
+      // one, Unpack alone copies only the header bytes into the request
+      const bool want_crc = force || (lens[0] > 3u && (bufs[0][3] & MGENX_FLAG_CHECKSUM) != 0u);
+      if (want_crc)
+        Check(mgenx_worker_recv(worker_, bufs[0], lens[0], force ? 1u : 0u, &u, &crc, &done),
+              "mgenx_worker_recv");
+      else
+        Check(mgenx_worker_unpack(worker_, bufs[0], lens[0], &u), "mgenx_worker_unpack");
       if (done) {
         crc_cache_.valid = true;
         crc_cache_.ptr = bufs[0];

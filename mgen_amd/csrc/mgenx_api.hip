@@ -1216,9 +1216,12 @@ int mgenx_worker_create(mgenx_ctx* ctx, uint32_t idle_ms, mgenx_worker** out) {
 
 // end the worker's wave (if one runs) and wait for it: no wave is left polling, so a later
 // device-wide synchronisation (hipFree, hipDeviceSynchronize) does not wait for its idle timeout
+// (the calling thread's current device is restored: growth paths allocate right after a free)
 static void worker_stop(mgenx_worker* w) {
   std::lock_guard<std::mutex> g(w->mu);
   if (!w->launched || !w->rep || !w->ctx) return;
+  int prev = -1;
+  const bool have_prev = hipGetDevice(&prev) == hipSuccess;
   hipSetDevice(w->ctx->device);
   if (w_load(&w->rep->alive)) {  // ask the wave to end; it may end on its own meanwhile
     uint32_t r = w->seq + 1u;
@@ -1228,6 +1231,7 @@ static void worker_stop(mgenx_worker* w) {
   }
   (void)hipStreamSynchronize(w->stream);
   w->launched = false;
+  if (have_prev) hipSetDevice(prev);
 }
 
 // the wave stopped and the device resources freed; the handle stays (ctx = null)
@@ -1250,13 +1254,12 @@ static void worker_detach(mgenx_worker* w) {
 
 extern "C++" {
 namespace mgenx {
-void quiesce_workers() {
-  std::vector<mgenx_worker*> ws;
-  {
-    std::lock_guard<std::mutex> g(g_workers_mu);
-    ws = g_workers;
-  }
-  for (mgenx_worker* w : ws) worker_stop(w);
+// g_workers_mu is held for the whole loop, so no worker is destroyed while it is stopped (a
+// worker call holding w->mu never takes g_workers_mu; worker_detach releases it before its stop)
+void quiesce_workers(int device) {
+  std::lock_guard<std::mutex> g(g_workers_mu);
+  for (mgenx_worker* w : g_workers)
+    if (device < 0 || (w->ctx && w->ctx->device == device)) worker_stop(w);
 }
 }  // namespace mgenx
 }  // extern "C++"

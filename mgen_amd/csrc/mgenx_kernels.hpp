@@ -13,18 +13,21 @@
 
 namespace mgenx {
 
-// Ends every resident worker wave (mgenx_worker_*, mgenx_api.hip) in the process and waits for
-// them.  hipFree / hipHostFree synchronise the device, so with a wave still polling its mailbox
-// they would wait for its idle timeout: every workspace growth frees through these.
-void quiesce_workers();
+// Ends the resident worker waves (mgenx_worker_*, mgenx_api.hip) of `device` (every device when
+// device < 0) and waits for them; the calling thread's current device is left as it was.
+// hipFree / hipHostFree synchronise the device, so with a wave still polling its mailbox they
+// would wait for its idle timeout: every workspace growth frees through these.
+void quiesce_workers(int device);
 inline void dev_free(void* p) {
   if (!p) return;
-  quiesce_workers();
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+  quiesce_workers(dev);  // hipFree synchronises the current device only
   (void)hipFree(p);
 }
 inline void host_free(void* p) {
   if (!p) return;
-  quiesce_workers();
+  quiesce_workers(-1);  // pinned host memory may be mapped on every device
   (void)hipHostFree(p);
 }
 

@@ -5,7 +5,7 @@ set -u
 export TMPDIR=/tmp
 OUT=gpurun_out
 mkdir -p $OUT
-bash scripts/r03_final_prof.sh || exit $?
+bash scripts/archive/r03_final_prof.sh || exit $?
 timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/c4csv -o c4 \
     -- python3 -u scripts/c4_only.py > $OUT/c4csv.log 2>&1 || exit $?
 timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/c5csv -o c5 \

@@ -217,3 +217,42 @@ def test_tcp_tx_plan_epoch_wrap(torch, eng, gold):
         assert fn(*args) == 0 and tot.value == len(want), k
     torch.cuda.synchronize()
     assert np.array_equal(buf.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("checksum", [False, True])
+def test_doc_tcp_fragment_example_on_gpu(torch, eng, oracle, checksum):
+    """doc/mgen.xml:3644-3662 on the device: mgenx_pack_tcp of the 66,559-B message equals
+    or_tcp_tx (a 65,535-B CONTINUES fragment and a 1,024-B END_OF_MSG one, same seq), the TCP
+    framing scan frames exactly those two records, and the RECV log of the TCP-rule unpack
+    prints the doc's two lines (as the code prints them: test_oracle_pins)."""
+    from mgen_amd import OPT_TCP, PACK_CHECKSUM, SCAN_TCP, to_device
+    from mgen_amd._abi import DESC_DTYPE, TMPL_DTYPE
+    from test_oracle_pins import (DOC_DAY, doc_tcp_expected_lines, doc_tcp_msg,
+                                  doc_tcp_recv_inputs)
+    t = np.zeros(1, TMPL_DTYPE)
+    t["flow_id"], t["dst_type"], t["dst_len"], t["dst_port"] = 1, 1, 4, 5000
+    t["dst_addr"][0, :4] = [10, 0, 0, 2]
+    t["lat_raw"] = t["lon_raw"] = 70740000        # (999 + 180) * 60000
+    t["alt"] = -999
+    d = np.zeros(1, DESC_DTYPE)
+    d["seq_num"], d["tx_sec"], d["tx_usec"] = 1, DOC_DAY + 36 * 60 + 11, 377105
+    pool = np.zeros(16, np.uint8)
+    tm, pl = to_device(t), to_device(pool)
+    crc = torch.empty(1, dtype=torch.int32, device="cuda")
+    eng.pack_prepare(tm, 1, pl, crc)
+    out, offs = eng.pack_tcp(tm, crc, to_device(d), to_device(np.array([66559], np.uint32)), 1,
+                             pl, opts=PACK_CHECKSUM if checksum else 0)
+    want = oracle.tcp_tx(doc_tcp_msg(oracle), checksum=checksum)
+    got = out.cpu().numpy().tobytes()
+    assert len(got) == 66559 and got == want
+    so, sl, info = eng.stream_scan(out, SCAN_TCP)
+    assert int(info.n_records) == 2
+    assert so.cpu().numpy().tolist() == [0, 65535] and sl.cpu().numpy().tolist() == [65535, 1024]
+    cols = eng.unpack(out, 2, rec_off=so, rec_len=sl, opts=OPT_TCP, ext=True)
+    torch.cuda.synchronize()
+    assert cols["err"].cpu().numpy().tolist() == [0, 0]
+    src, rx_sec, rx_usec = doc_tcp_recv_inputs(oracle, 2)
+    text, _ = eng.log_recv_text(out, 2, cols, to_device(src.view(np.uint8)), to_device(rx_sec),
+                                to_device(rx_usec), rec_off=so, protocol=2)
+    lines = text.cpu().numpy().tobytes().decode().splitlines(keepends=True)
+    assert lines == doc_tcp_expected_lines()

@@ -122,3 +122,75 @@ def test_hex_payload_rules(oracle):
 def test_quantized_default_window(oracle):
     # MgenAnalytic ctor quantises DEFAULT_WINDOW = 1.0 (mgenAnalytic.cpp:8-16,621-642)
     assert abs(oracle.quantized_window(1.0) - 1.0112109525687343) < 1e-15
+
+
+# doc/mgen.xml:3644-3662: "a TCP mgen message of size 66559 will be received and logged by the
+# receiving node as two messages" -- the fragment rule of MgenTcpTransport::GetNextTxFragmentSize
+# (mgenTransport.cpp:1960-1993: MAX_FRAG_SIZE 65535, MIN_FRAG_SIZE 76, mgenGlobals.h:76-78).
+DOC_TCP_RECV = [
+    "00:33:36.427143 RECV proto>TCP flow>1 seq>1 src>10.0.0.1/35056 dst>10.0.0.2/5000 "
+    "sent>00:36:11.377105 size>65535 gps>INVALID,999.000000,999.000000,-999 flags>0x01",
+    "00:33:36.427499 RECV proto>TCP flow>1 seq>1 src>10.0.0.1/35056 dst>10.0.0.1/5000 "
+    "sent>00:36:11.380137 size>1024 gps>INVALID,999.000000,999.000000,-999 flags>0x02",
+]
+DOC_DAY = 1_700_000_000 - 1_700_000_000 % 86400
+
+
+def doc_tcp_msg(oracle):
+    """The doc's message: flow 1, seq 1, dst 10.0.0.2/5000, 66,559 bytes, sent 00:36:11.377105."""
+    return oracle.make_msg(msg_len=66559, flow_id=1, seq=1, tx_sec=DOC_DAY + 36 * 60 + 11,
+                           tx_usec=377105, dst=("4", bytes([10, 0, 0, 2]), 5000))
+
+
+def doc_tcp_expected_lines():
+    """The doc's RECV lines as this code prints them (code wins):
+      * the line ends with the space the format leaves before "\\n" (mgenMsg.cpp:1090-1101);
+      * `%ld` of the INT32 altitude prints 4294966297 on LP64 (doc/mgen.xml:2948 shows that
+        value; the -999 of :3649 is a 32-bit-long build);
+      * the second fragment carries the FIRST fragment's tx time and the message's dst: the
+        per-fragment SetTxTime is commented out (mgenTransport.cpp:1902-1904) and every
+        fragment is packed from the one tx_msg; the doc's 10.0.0.1 / .380137 are another build.
+    """
+    a, b = (ln.replace(",-999", ",4294966297") + " \n" for ln in DOC_TCP_RECV)
+    b = b.replace("dst>10.0.0.1/5000", "dst>10.0.0.2/5000").replace(
+        "sent>00:36:11.380137", "sent>00:36:11.377105")
+    return [a, b]
+
+
+def doc_tcp_recv_inputs(oracle, n):
+    src = np.zeros(n, oracle.ADDR_DTYPE)
+    src["type"], src["len"], src["port"] = 1, 4, 35056
+    src["addr"][:, :4] = [10, 0, 0, 1]
+    rx_sec = np.full(n, DOC_DAY + 33 * 60 + 36, np.uint32)
+    rx_usec = np.array([427143, 427499][:n], np.uint32)
+    return src, rx_sec, rx_usec
+
+
+@pytest.mark.parametrize("checksum", [False, True])
+def test_doc_tcp_fragment_example(oracle, checksum):
+    """or_tcp_tx splits the 66,559-B message into a 65,535-B fragment (CONTINUES) and a 1,024-B
+    one (END_OF_MSG), same flow and seq; the TCP framing scan recovers exactly those two
+    records and the RECV log prints the doc's two lines (the SEND line: test_send_log_cpu)."""
+    stream = oracle.tcp_tx(doc_tcp_msg(oracle), checksum=checksum)
+    assert len(stream) == 66559
+    assert int.from_bytes(stream[0:2], "big") == 65535
+    assert int.from_bytes(stream[65535:65537], "big") == 1024
+    f0, f1 = stream[3], stream[65535 + 3]
+    ck = 0x04 if checksum else 0
+    # wire flags: fragment 0 is packed without LAST_BUFFER (its 8-KiB buffers are re-sent),
+    # fragment 1 fits one buffer: LAST_BUFFER set before its Pack (mgenTransport.cpp:1931)
+    assert f0 == 0x01 | ck and f1 == 0x02 | 0x08 | ck
+    for o in (0, 65535):
+        assert stream[o + 4:o + 12] == (1).to_bytes(4, "big") + (1).to_bytes(4, "big")
+    if checksum:  # CRC over the whole fragment but its trailer, re-sent buffers included
+        for o, L in ((0, 65535), (65535, 1024)):
+            rec = stream[o:o + L]
+            assert int.from_bytes(rec[-4:], "big") == zlib.crc32(rec[:-4])
+    offs, lens, f, consumed, st = oracle.tcp_scan(stream)
+    assert list(offs) == [0, 65535] and list(lens) == [65535, 1024] and consumed == 66559
+    assert list(f["err"]) == [0, 0] and list(f["seq_num"]) == [1, 1]
+    assert [int(x) & 0x03 for x in f["flags"]] == [0x01, 0x02]
+    src, rx_sec, rx_usec = doc_tcp_recv_inputs(oracle, 2)
+    text = oracle.log_recv_text(f, np.frombuffer(stream, np.uint8), offs, src, rx_sec, rx_usec,
+                                protocol=2).decode()
+    assert text.splitlines(keepends=True) == doc_tcp_expected_lines()
