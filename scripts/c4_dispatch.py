@@ -10,5 +10,5 @@ for r in rows:
     if "flow_" in k and "flowtab" not in k:
         seq.append((k.split("(")[0].replace("mgenx::", ""), int(r["Grid_Size_X"]),
                     (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3))
-for x in seq[:8] + [("...", 0, 0.0)] + seq[-8:]:
+for x in seq[:12] + [("...", 0, 0.0)] + seq[-12:]:
     print(f"{x[0]:24s} {x[1]:9d} {x[2]:8.1f} us")

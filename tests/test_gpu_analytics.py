@@ -381,3 +381,97 @@ def test_flow_reduce_config4_full_size_vs_oracle(torch, eng):
             assert d["flow_id"][i] - 1 == f
             assert (int(d["rx_sec"][i]), int(d["rx_usec"][i])) == (int(rep[f, r]["rx_sec"]),
                                                                   int(rep[f, r]["rx_usec"]))
+
+
+def _epoch_fuzz(n_flows, per, seed, window_us):
+    """Per-flow sequences aimed at the window-parallel update's seams: epoch starts (failed
+    Sets in the counted branch) on closing records and right after them, duplicates of closing
+    records and across epochs, late records below `first` inside the span (first moves down)
+    and far below it (silent failures below seq_start, and restarts when seq_start is older),
+    int32 wraps of seq - first, messages of size 0 (a flow's first record, then the first
+    actual message -- in one window, and closing one), windows of one record and of thousands,
+    rx times out of order."""
+    rng = np.random.default_rng(seed)
+    cols = {k: [] for k in ("flow_id", "seq", "tx_sec", "tx_usec", "rx_sec", "rx_usec",
+                            "msg_len")}
+    t0 = 1_700_000_000 * 10**6
+    for f in range(n_flows):
+        seq = np.zeros(per, np.int64)
+        s = int(rng.integers(0, 1 << 32))
+        hist = []
+        for i in range(per):
+            u = rng.random()
+            if u < 0.05 and hist:
+                s2 = hist[-int(rng.integers(1, min(len(hist), 40) + 1))]  # duplicate
+            elif u < 0.09:
+                s2 = s - int(rng.integers(1, 40))                          # late, in span
+            elif u < 0.11:
+                s2 = s - int(rng.integers(1024, 4000))                     # far below first
+            elif u < 0.14:
+                s = s + int(rng.integers(1024, 3000))                      # restart ahead
+                s2 = s
+            elif u < 0.145:
+                s = s + (1 << 31) + int(rng.integers(-5, 5))               # int32 wrap
+                s2 = s
+            else:
+                s = s + int(rng.integers(1, 3))
+                s2 = s
+            seq[i] = s2
+            hist.append(s2)
+        gaps = rng.exponential(window_us / 40.0, per)
+        big = rng.random(per) < 0.03
+        gaps[big] = rng.uniform(window_us, 3 * window_us, int(big.sum()))   # one-record windows
+        tx = t0 + np.cumsum(gaps).astype(np.int64) + int(rng.integers(0, 10**6))
+        rx = tx + rng.integers(50, 500, per)
+        swap = rng.random(per) < 0.02                                        # rx out of order
+        rx[swap] -= rng.integers(1000, 50_000, int(swap.sum()))
+        ln = np.full(per, 300, np.int64)
+        ln[rng.random(per) < 0.03] = 0
+        if f % 3 == 0:
+            ln[:int(rng.integers(1, 30))] = 0   # first message(s) of size 0, then the first actual
+        for k, v in (("seq", seq & 0xFFFFFFFF), ("tx_sec", tx // 10**6), ("tx_usec", tx % 10**6),
+                     ("rx_sec", rx // 10**6), ("rx_usec", rx % 10**6), ("msg_len", ln)):
+            cols[k].append(v)
+        cols["flow_id"].append(np.full(per, f + 1))
+    # interleave the flows in a receive-like order, each flow's own order kept
+    key = np.concatenate([np.arange(per) + rng.uniform(0, 3, per) for _ in range(n_flows)])
+    order = np.argsort(key, kind="stable")
+    dt = {"flow_id": np.uint32, "seq": np.uint32, "tx_sec": np.uint32, "tx_usec": np.uint32,
+          "rx_sec": np.uint32, "rx_usec": np.uint32, "msg_len": np.uint16}
+    return {k: np.concatenate(v).astype(dt[k])[order] for k, v in cols.items()}
+
+
+@pytest.mark.parametrize("window", [0.01, 0.2, 2.0])
+def test_flow_reduce_epoch_and_window_seams(torch, eng, window):
+    """The window-parallel update against the oracle on sequences built for its seams (epoch
+    starts on and after closing records, duplicates across epochs and of closing records,
+    records below `first`, size-0 first messages, one-record windows), streamed in four calls
+    whose splits fall inside windows and epochs."""
+    from oracle import oracle as O
+    n_flows, per_flow = 24, 512
+    d = _epoch_fuzz(n_flows, 4000, seed=int(window * 100) + 7, window_us=window * 1e6)
+    n = len(d["seq"])
+    st, rep, cnt, _ = run_gpu(torch, eng, d, n_flows, window, per_flow,
+                              splits=(0, 1, n // 3, n // 3 + 5))
+    of, orep, ocnt = O.flow_reduce_batch(n_flows, d["flow_id"] - 1, d["seq"], d["tx_sec"],
+                                         d["tx_usec"], d["msg_len"], d["rx_sec"],
+                                         d["rx_usec"], window=window, per_flow=per_flow)
+    assert sum(a.dup_msg_count for a in of) > 0 and int(ocnt.sum()) > n_flows
+    compare(st, rep, cnt, of, orep, ocnt, per_flow)
+
+
+def test_flow_reduce_rank_share_vs_oracle(torch, eng):
+    """Rank 0's share of config 4 at N = 8 (flows f with f mod 8 == 0: 128 of 1024 flows, 1/8
+    of the records; the other flows untouched) against the oracle."""
+    from mgen_amd.workloads import poisson_flows
+    from oracle import oracle as O
+    n_flows, per_flow = 1024, 16
+    d = poisson_flows(1_048_576, n_flows, mean_gap_us=1000, seed=77)
+    own = (d["flow_id"] % 8) == 0
+    d = {k: np.ascontiguousarray(v[own]) for k, v in d.items()}
+    st, rep, cnt, _ = run_gpu(torch, eng, d, n_flows, 1.0, per_flow)
+    of, orep, ocnt = O.flow_reduce_batch(n_flows, d["flow_id"] - 1, d["seq"], d["tx_sec"],
+                                         d["tx_usec"], d["msg_len"], d["rx_sec"],
+                                         d["rx_usec"], window=1.0, per_flow=per_flow)
+    assert sum(1 for a in of if a.msg_count > 0) == 128 and int(ocnt.sum()) > 0
+    compare(st, rep, cnt, of, orep, ocnt, per_flow)
