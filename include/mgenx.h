@@ -170,6 +170,7 @@ int mgenx_unpack_batch(mgenx_ctx* ctx, const uint8_t* dev_slab, uint64_t slab_by
 #define MGENX_UNPACK_K_FIXED      4  /* fixed stride, one length in [65, 1024] */
 #define MGENX_UNPACK_K_FIXED_RING 5  /* fixed 512 / 1024-B records into rows (config 2) */
 #define MGENX_UNPACK_K_OTHER      6  /* a diagnostics-build ablation */
+#define MGENX_UNPACK_K_LONG       7  /* mean record >= 4 KiB (TCP streams): a wave per record */
 int mgenx_unpack_last_kernel(const mgenx_ctx* ctx);
 
 /* ------------------------------------------------------------------ */

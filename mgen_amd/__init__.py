@@ -22,7 +22,7 @@ from ._abi import (  # noqa: F401
     PcapInfo, TextSrc, TEXT_PER_RECORD, TEXT_OWNER, TEXT_MAP, TEXT_SCATTER, PCAP_NSEC, PCAP_SWAPPED, LOG_EPOCH, LOG_NO_DATA, LOG_NO_GPS,
     LOG_SKIP_ERR, FLOW_NONE, DLT_EN10MB, DLT_LINUX_SLL, BinlogInfo, BINLOG_NO_RX, BINLOG_FLUSH,
     UNPACK_K_HEADER, UNPACK_K_GENERAL, UNPACK_K_VAR, UNPACK_K_FIXED, UNPACK_K_FIXED_RING,
-    UNPACK_K_OTHER, UNPACKED_DTYPE,
+    UNPACK_K_OTHER, UNPACK_K_LONG, UNPACKED_DTYPE,
 )
 
 HERE = os.path.dirname(os.path.abspath(__file__))

@@ -13,7 +13,7 @@ FLAG_CONTINUES, FLAG_END_OF_MSG, FLAG_CHECKSUM, FLAG_LAST_BUFFER, FLAG_CHECKSUM_
 OPT_CHECKSUM_FORCE, OPT_TCP, OPT_SKIP_CRC = 0x1, 0x2, 0x4
 # mgenx_unpack_last_kernel: which kernel the dispatch chose (include/mgenx.h)
 (UNPACK_K_HEADER, UNPACK_K_GENERAL, UNPACK_K_VAR, UNPACK_K_FIXED, UNPACK_K_FIXED_RING,
- UNPACK_K_OTHER) = 1, 2, 3, 4, 5, 6
+ UNPACK_K_OTHER, UNPACK_K_LONG) = 1, 2, 3, 4, 5, 6, 7
 PACK_CHECKSUM, PACK_RANDOM_FILL, PACK_RAW = 0x1, 0x2, 0x4
 # MGENX_DEC_*: members an Unpack assigned (mgenx_cols.decoded)
 DEC_MSGLEN, DEC_BASE, DEC_DST, DEC_HDRLEN = 0x01, 0x02, 0x04, 0x08

@@ -104,19 +104,21 @@ __device__ __forceinline__ FRec make_frec(const RecSrc& src, uint32_t i) {
 //   * the counters restart at every close (:228-242), so each window's msg_count, byte_count
 //     and latency min / max are reductions over its own records, from a start state that only
 //     the closing record of the window before decides.
-// Three kernels:
+// Two kernels:
 //   flow_skel_kernel  one wave per flow walks its records 256 at a time, scalar state only:
-//                     the span test of a run of records is an inclusive prefix min / max of
-//                     seq - first (one wave scan each), the first record that fails it, closes a
-//                     window or needs a special path is done alone.  Out: a flag byte per record
-//                     and the flow's windows (records, epoch of the first record, seqMax and
-//                     seq_start at the close);
-//   flow_win_kernel   one wave per window (8 per flow): the epoch table of the window's first
-//                     record rebuilt in LDS (seq mod 1024 -> first position), the duplicate
-//                     test of each record, the window's counters and report, lat' per record;
-//   flow_sum_kernel   one wave per flow, a lane per window: each window's in-order FP64
-//                     latency sum (the one chain whose rounding depends on record order), and
-//                     the flow state.
+//                     a run of records whose span stays below 1024 (a wave min / max) and holds
+//                     no close and no first message is plain; otherwise inclusive prefix scans
+//                     of seq - first find the first record that fails its Set, and it, a close
+//                     or a first message is done alone.  Out: a flag byte per record and the
+//                     flow's windows (records, epoch of the first record, seqMax and seq_start
+//                     at the close);
+//   flow_win_kernel   one wave per window (8 waves per flow): the epoch table of the window's
+//                     first record rebuilt in LDS (seq mod 1024 -> first position), the
+//                     duplicate test of each record, the window's counters and report, lat' per
+//                     record;
+//                     the window's in-order FP64 latency sum (the one chain whose rounding
+//                     depends on record order), and -- the open window's wave -- the flow's
+//                     state.
 // scripts/flow_decomp.py is the same decomposition on the CPU, checked against the oracle.
 constexpr uint8_t kFIns = 1;      // the record's seq is in the mask after it (Set succeeded)
 constexpr uint8_t kFDupT = 2;     // it takes the duplicate test with its seq inside the span
@@ -136,29 +138,25 @@ struct WinItem {       // one window of a flow (flow f's k-th at wins[bnd[f] + f
   uint32_t seqmax, sst;  // seqMax at the close, the seq_start it is measured from (:174-219)
   uint64_t ws;         // window start, receive-time key
 };
-struct FlowFin {       // per flow, between the kernels
-  uint32_t mask[32];   // the final mask relative to F (the open window's wave)
-  uint32_t mask_n, F, hasmask, nwin;
-  uint32_t ncl, last_close, last_zr, rc0;
-  uint64_t mc, bc, dups;  // the open window's counters; duplicates (every window adds)
-  double lmin, lmax;
+struct FlowFin {       // per flow: the state before the call (flow_skel_kernel copies it, so
+                       // the window waves read it while the open window's wave rewrites the
+                       // flow state), and the skeleton's results
+  uint32_t mask0[32];  // the mask before the call, relative to first0
+  uint32_t first0, n0, F, hasmask;
+  uint32_t nwin, ncl, rc0, rsv;
+  uint64_t mc0, bc0;
+  double lmin0, lmax0, lsum0;
 };
 static_assert(sizeof(WinItem) == 32, "window item");
 
-// What the latency sums need per kept report closed in this call
-struct CloseRec {
-  uint32_t pos, zr;     // the closing record (sorted position); zero restart
-  uint64_t mc;          // msg_count at the close: latency_ave's divisor
-};
 
 __device__ __forceinline__ uint64_t tm_key(Tm t) { return (uint64_t)t.sec << 32 | (uint64_t)t.usec; }
 __device__ __forceinline__ Tm key_tm(uint64_t k) { return Tm{(int64_t)(k >> 32), (int64_t)(uint32_t)k}; }
 
-// inclusive min / max scans over the wave (DPP rows of 16 by shifts, then the row broadcasts;
-// lanes a step does not reach keep their value: `old` is the identity), then shifted one lane
-// up (exclusive: lane 0 gets the identity)
+// inclusive min / max scan over the wave (DPP rows of 16 by shifts, then the row broadcasts;
+// lanes a step does not reach keep their value: `old` is the identity)
 template <bool kMax>
-__device__ __forceinline__ int32_t wave_excl_minmax(int32_t v) {
+__device__ __forceinline__ int32_t wave_incl_minmax(int32_t v) {
   const int32_t id = kMax ? INT32_MIN : INT32_MAX;
   auto op = [](int32_t a, int32_t c) { return kMax ? max(a, c) : min(a, c); };
   v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x111, 0xf, 0xf, false));  // row_shr:1
@@ -167,22 +165,137 @@ __device__ __forceinline__ int32_t wave_excl_minmax(int32_t v) {
   v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x118, 0xf, 0xf, false));  // row_shr:8
   v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x142, 0xa, 0xf, false));  // row_bcast:15
   v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x143, 0xc, 0xf, false));  // row_bcast:31
-  return __builtin_amdgcn_update_dpp(id, v, 0x138, 0xf, 0xf, false);     // wave_shr:1
+  return v;
+}
+__device__ __forceinline__ int32_t wave_min_i32(int32_t v) {
+  return (int32_t)WRing::wave_reduce((uint32_t)v, (uint32_t)INT32_MAX, [](uint32_t a, uint32_t c) {
+    return (uint32_t)min((int32_t)a, (int32_t)c); });
+}
+__device__ __forceinline__ int32_t wave_max_i32(int32_t v) {
+  return (int32_t)WRing::wave_reduce((uint32_t)v, (uint32_t)INT32_MIN, [](uint32_t a, uint32_t c) {
+    return (uint32_t)max((int32_t)a, (int32_t)c); });
 }
 
-// ---- the skeleton: one wave per flow ----
-constexpr uint32_t kSkQ = 4;               // records per lane and chunk (lane l: 4l .. 4l + 3)
-constexpr uint32_t kSkChunk = 64u * kSkQ;  // records per chunk
+#if MGENX_DIAG
+__device__ unsigned long long g_skel_prof[8];
+__device__ unsigned int g_skel_claim;
+#endif
+// ---- the skeleton: one workgroup per flow, its walk on one wave ----
+// The walk is sequential and runs on one wave, so what it costs per record is what counts
+// (measured on config 4: ~2.5 k cycles per 256-record chunk for the per-record span test --
+// about 250 dependent instructions on a lone wave -- whether the records came from registers
+// or LDS).  So the workgroup's four waves do the per-record work in parallel around the walk:
+//   1. stage the flow's records -- the first 16 bytes of each FRec: receive key, seq, length --
+//      into LDS by direct global->LDS loads (kSkSeg records a segment, all in flight at once);
+//   2. summarize each 256-record chunk: its largest receive key, and the lowest / highest
+//      seq - base over its set attempts (base: the chunk's first seq), any non-zero length;
+//   3. wave 0 walks the summaries: a chunk with no close (largest key below the window end), no
+//      first message and a span below 1024 after it (the summary's min / max against first /
+//      last) is plain -- O(1) scalar work; any other chunk takes the per-record path (prefix
+//      scans, the first event alone, as before) on wave 0;
+//   4. the four waves write the plain chunks' flag bytes (the seq_start of each is recorded).
+// The summary test is exact when it passes: every record's seq - first then lies inside the
+// span, where the chunk-relative value plus the chunk base's offset equals it.
+constexpr uint32_t kSkQ = 4;
+constexpr uint32_t kSkChunk = 64u * kSkQ;
+constexpr uint32_t kSkSeg = 4096;  // records staged per segment (64 KiB: two workgroups per CU)
+constexpr uint32_t kSkChunks = kSkSeg / kSkChunk;
+struct SkSum {  // one chunk's summary
+  uint32_t rx_lo, rx_hi, base;
+  int32_t dmin, dmax;
+  uint32_t nz, rsv0, rsv1;
+};
+constexpr size_t kSkLds = (size_t)kSkSeg * 16u + kSkChunks * sizeof(SkSum) + kSkChunks * 8u;
+struct SkLd {
+  uint32_t seq[kSkQ], len[kSkQ];
+  uint64_t rxk[kSkQ];
+};
+typedef __attribute__((address_space(3))) void lds_void_t;
 __global__ void __launch_bounds__(256)
-flow_skel_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
+flow_skel_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows, uint32_t fmul,
                  const uint32_t* __restrict__ bnd, const FRec* __restrict__ recs,
                  uint8_t* __restrict__ rflags, WinItem* __restrict__ wins,
                  FlowFin* __restrict__ fin, uint32_t* __restrict__ report_count) {
+  extern __shared__ u32x4_t skl[];  // kSkSeg staged records {rxk, seq, len}, then summaries
+  SkSum* sums = reinterpret_cast<SkSum*>(skl + kSkSeg);
+  uint32_t* cst = reinterpret_cast<uint32_t*>(sums + kSkChunks);  // [c]: plain, [kSkChunks + c]: sst
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  const uint32_t f = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + wv);
-  if (f >= n_flows) return;
+  // flows to blocks by a multiplicative permutation (fmul coprime with n_flows): blocks go to
+  // the XCDs round robin, and a rank's flows (every 8th) would otherwise all land on one XCD
+  const uint32_t f = (uint32_t)(((uint64_t)blockIdx.x * fmul) % n_flows);
   const uint32_t b = bnd[f], e = bnd[f + 1u];
   if (b >= e) return;
+  // stage records [s, s + kSkSeg) of the flow (every wave), then wait for them (all threads)
+  auto stage = [&](uint32_t s) {
+    const uint32_t ninst = (min(kSkSeg, e - s) + 63u) / 64u;
+    for (uint32_t k = wv; k < ninst; k += 4u) {
+      const FRec* src = recs + min(s + 64u * k + lane, e - 1u);
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_t*)(skl + 64u * k), 16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  };
+  // chunk c of the segment at s: its summary (one wave)
+  auto summarize = [&](uint32_t s, uint32_t c) {
+    const uint32_t i0 = s + c * kSkChunk, se = min(e, s + kSkSeg);
+    const uint32_t base = skl[c * kSkChunk].z;  // the chunk's first seq
+    uint32_t rhi = 0, rlo = 0;
+    int32_t dmn = INT32_MAX, dmx = INT32_MIN;
+    bool nz = false;
+#pragma unroll
+    for (uint32_t q = 0; q < kSkQ; q++) {
+      const uint32_t o = 64u * q + lane;
+      const u32x4_t v = skl[c * kSkChunk + o];
+      const bool in = i0 + o < se;
+      const bool hi_gt = v.y > rhi || (v.y == rhi && v.x > rlo);
+      rlo = (in && hi_gt) ? v.x : rlo;
+      rhi = (in && hi_gt) ? v.y : rhi;
+      const bool att = in && v.w != 0u;
+      const int32_t d = (int32_t)(v.z - base);
+      dmn = att ? min(dmn, d) : dmn;
+      dmx = att ? max(dmx, d) : dmx;
+      nz |= att;
+    }
+    const uint32_t RH = WRing::wave_max(rhi);
+    const uint32_t RL = WRing::wave_max(rhi == RH ? rlo : 0u);
+    const int32_t DMN = wave_min_i32(dmn), DMX = wave_max_i32(dmx);
+    const bool NZ = __ballot(nz) != 0ull;
+    if (lane == 0) {
+      SkSum sm;
+      sm.rx_lo = RL;
+      sm.rx_hi = RH;
+      sm.base = base;
+      sm.dmin = DMN;
+      sm.dmax = DMX;
+      sm.nz = NZ ? 1u : 0u;
+      sm.rsv0 = sm.rsv1 = 0u;
+      sums[c] = sm;
+    }
+  };
+  // the plain chunks' flag bytes (every wave): set attempts, counted at or past seq_start
+  auto plain_flags = [&](uint32_t s, uint32_t c) {
+    const uint32_t i0 = s + c * kSkChunk, se = min(e, s + kSkSeg), sst_c = cst[kSkChunks + c];
+#pragma unroll
+    for (uint32_t q = 0; q < kSkQ; q++) {
+      const uint32_t o = 64u * q + lane;
+      const u32x4_t v = skl[c * kSkChunk + o];
+      const uint32_t ce = (int32_t)(v.z - sst_c) >= 0 ? (uint32_t)kFCe : 0u;
+      if (i0 + o < se) rflags[i0 + o] = (uint8_t)(v.w != 0u ? (uint32_t)(kFIns | kFDupT) | ce : 0u);
+    }
+  };
+  if (wv != 0) {  // the helper waves: stage, summarize, write the plain chunks' flags
+    for (uint32_t s = b; s < e; s += kSkSeg) {
+      stage(s);
+      const uint32_t nch = (min(kSkSeg, e - s) + kSkChunk - 1u) / kSkChunk;
+      for (uint32_t c = wv; c < nch; c += 4u) summarize(s, c);
+      __syncthreads();  // summaries ready
+      __syncthreads();  // wave 0 has walked the segment
+      for (uint32_t c = wv; c < nch; c += 4u)
+        if (cst[c]) plain_flags(s, c);
+      __syncthreads();  // the segment's LDS may be restaged
+    }
+    return;
+  }
   mgenx_flow_state* sp = flows + f;
   const TAdd window = tadd_of(sp->window_size);
   bool valid = sp->window_valid != 0, hasm = sp->mask_n != 0;
@@ -196,79 +309,122 @@ flow_skel_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
   Tm ws = {sp->win_start_sec, sp->win_start_usec}, we = {sp->win_end_sec, sp->win_end_usec};
   uint64_t wek = tkey(we);
   const uint32_t rc0 = report_count[f];
-  uint32_t nwin = 0, ncl = 0, last_close = 0, last_zr = 0;
+  uint32_t nwin = 0, ncl = 0;
   uint32_t win_a = b, win_r = kNoEpoch, cur_es = kNoEpoch;
   WinItem* wl = wins + ((size_t)b + f);
+  FlowFin* fp = fin + f;
+  if (lane < 32u) fp->mask0[lane] = sp->mask[lane];
+  if (lane == 0) {
+    fp->first0 = sp->mask_first;
+    fp->n0 = sp->mask_n;
+    fp->mc0 = sp->msg_count;
+    fp->bc0 = sp->byte_count;
+    fp->lmin0 = sp->latency_min;
+    fp->lmax0 = sp->latency_max;
+    fp->lsum0 = sp->latency_sum;
+  }
+#if MGENX_DIAG
+  // (diagnostics) cycles of the first walk to finish: fast runs, prefix scans, event records,
+  // total, staging (incl. its wait); counts of fast runs, slow runs, events
+  unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0}, prof_t = __builtin_amdgcn_s_memtime();
+  const unsigned long long prof_t0 = prof_t;
+#define SK_T(slot)                                                         \
+  do {                                                                     \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime();          \
+    prof[slot] += now_ - prof_t;                                           \
+    prof_t = now_;                                                         \
+  } while (0)
+#define SK_N(slot) prof[slot]++
+#else
+#define SK_T(slot) do {} while (0)
+#define SK_N(slot) do {} while (0)
+#endif
 
-  // a chunk's records: lane l holds i0 + 4l + q (8-B loads: the 24-B records are 8-B aligned)
-  struct Ld {
-    uint32_t seq[kSkQ], len[kSkQ];
-    uint64_t rxk[kSkQ];
-  };
-  auto ld = [&](uint32_t i0, Ld& r) {  // clamped to the flow's last record
+  uint32_t seg = b;  // the staged segment's first record
+  auto ld = [&](uint32_t i0, SkLd& r) {  // from LDS (lanes past the flow read stale slots)
 #pragma unroll
     for (uint32_t q = 0; q < kSkQ; q++) {
-      const FRec* p = recs + min(i0 + kSkQ * lane + q, e - 1u);
-      r.rxk[q] = p->rxk;
-      const uint64_t sl = *reinterpret_cast<const uint64_t*>(&p->seq);
-      r.seq[q] = (uint32_t)sl;
-      r.len[q] = (uint32_t)(sl >> 32);
+      const u32x4_t v = skl[i0 - seg + 64u * q + lane];
+      r.rxk[q] = (uint64_t)v.y << 32 | v.x;
+      r.seq[q] = v.z;
+      r.len[q] = v.w;
     }
   };
-  Ld cur, nxt;
-  ld(b, cur);
-  ld(b + kSkChunk, nxt);
-  for (uint32_t i0 = b; i0 < e; i0 += kSkChunk) {
-    Ld nx2;
-    ld(i0 + 2u * kSkChunk, nx2);
+  auto chunk = [&](const uint32_t i0, const SkLd& cur) {
     const uint32_t cnt = min(kSkChunk, e - i0);
     uint32_t fl[kSkQ];
 #pragma unroll
     for (uint32_t q = 0; q < kSkQ; q++) fl[q] = 0u;
     uint32_t pos = 0;
     while (pos < cnt) {
-      // the run from pos: prefix min / max of seq - F over its set attempts (every one of them
-      // succeeds up to the first event, so the prefix is the span before each record)
       const int32_t Lr = (int32_t)(L - F);
       int32_t rel[kSkQ];
       bool inr[kSkQ], att[kSkQ];
       int32_t lmn = INT32_MAX, lmx = INT32_MIN;
+      uint64_t evb[kSkQ];  // closes and first messages, per q
+      bool anyev = false;
 #pragma unroll
       for (uint32_t q = 0; q < kSkQ; q++) {
-        const uint32_t o = kSkQ * lane + q;
+        const uint32_t o = 64u * q + lane;
         inr[q] = (o >= pos) & (o < cnt);
         att[q] = inr[q] & (cur.len[q] != 0u);
         rel[q] = (int32_t)(cur.seq[q] - F);
         lmn = att[q] ? min(lmn, rel[q]) : lmn;
         lmx = att[q] ? max(lmx, rel[q]) : lmx;
-      }
-      int32_t cmn = min(0, wave_excl_minmax<false>(lmn));
-      int32_t cmx = max(Lr, wave_excl_minmax<true>(lmx));
-      int32_t imn[kSkQ], imx[kSkQ];
-      uint32_t evq = kSkQ;
-#pragma unroll
-      for (uint32_t q = 0; q < kSkQ; q++) {
-        cmn = att[q] ? min(cmn, rel[q]) : cmn;
-        cmx = att[q] ? max(cmx, rel[q]) : cmx;
-        imn[q] = cmn;
-        imx[q] = cmx;
-        const bool fail = att[q] & valid & hasm & ((int64_t)cmx - (int64_t)cmn >= 1024);
         const bool spec = inr[q] & (!valid | ((cur.len[q] != 0u) & !hasm));
         const bool clo = inr[q] & valid & (cur.rxk[q] >= wek);
-        evq = (evq == kSkQ) & (fail | spec | clo) ? q : evq;
+        evb[q] = __ballot(spec | clo);
+        anyev |= evb[q] != 0ull;
       }
-      const uint32_t ev = (uint32_t)__builtin_amdgcn_readfirstlane(
-          (int)WRing::wave_min(evq < kSkQ ? kSkQ * lane + evq : kSkChunk));
+      const bool mask_ops = valid & hasm;
+      const int32_t tmn = min(0, wave_min_i32(lmn)), tmx = max(Lr, wave_max_i32(lmx));
+      if (!anyev && (!mask_ops || (int64_t)tmx - (int64_t)tmn < 1024)) {
+        // the whole run [pos, cnt) is plain: every Set succeeds
+#pragma unroll
+        for (uint32_t q = 0; q < kSkQ; q++) {
+          const uint32_t ce = (int32_t)(cur.seq[q] - sst) >= 0 ? (uint32_t)kFCe : 0u;
+          fl[q] = att[q] ? (uint32_t)(kFIns | kFDupT) | ce : fl[q];
+        }
+        if (mask_ops) {
+          const uint32_t F2 = F + (uint32_t)tmn;
+          L = F + (uint32_t)tmx;
+          F = F2;
+        }
+        SK_T(0);
+        SK_N(5);
+        break;
+      }
+      SK_T(0);
+      SK_N(6);
+      // each record's span from inclusive prefixes (q-major order: the scans of the four
+      // groups, chained by their totals); the first failing Set, close or first message
+      int32_t imn[kSkQ], imx[kSkQ];
+#pragma unroll
+      for (uint32_t q = 0; q < kSkQ; q++) {
+        imn[q] = wave_incl_minmax<false>(att[q] ? rel[q] : INT32_MAX);
+        imx[q] = wave_incl_minmax<true>(att[q] ? rel[q] : INT32_MIN);
+      }
+      int32_t cmn = 0, cmx = Lr;
+      uint32_t ev = kSkChunk;
+#pragma unroll
+      for (uint32_t q = 0; q < kSkQ; q++) {
+        imn[q] = min(cmn, imn[q]);
+        imx[q] = max(cmx, imx[q]);
+        cmn = __builtin_amdgcn_readlane(imn[q], 63);
+        cmx = __builtin_amdgcn_readlane(imx[q], 63);
+        const bool fail = att[q] & mask_ops & ((int64_t)imx[q] - (int64_t)imn[q] >= 1024);
+        const uint64_t eb = evb[q] | __ballot(fail);
+        if (eb && ev == kSkChunk) ev = 64u * q + (uint32_t)__builtin_ctzll(eb);
+      }
       // the run [pos, ev): plain records
 #pragma unroll
       for (uint32_t q = 0; q < kSkQ; q++) {
-        const uint32_t o = kSkQ * lane + q;
-        const bool plain = att[q] & (o < ev);
+        const uint32_t o = 64u * q + lane;
         const uint32_t ce = (int32_t)(cur.seq[q] - sst) >= 0 ? (uint32_t)kFCe : 0u;
-        fl[q] = plain ? (uint32_t)(kFIns | kFDupT) | ce : fl[q];
+        fl[q] = (att[q] & (o < ev)) ? (uint32_t)(kFIns | kFDupT) | ce : fl[q];
       }
-      if (ev > pos && valid && hasm) {  // the span after the run
-        const uint32_t o1 = ev - 1u, l1 = o1 / kSkQ, q1 = o1 % kSkQ;
+      if (ev > pos && mask_ops) {  // the span after the run
+        const uint32_t o1 = ev - 1u, l1 = o1 & 63u, q1 = o1 >> 6;
         int32_t vmn = imn[0], vmx = imx[0];
 #pragma unroll
         for (uint32_t q = 1; q < kSkQ; q++) {
@@ -281,9 +437,11 @@ flow_skel_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
         L = F + (uint32_t)mx;
         F = F2;
       }
+      SK_T(1);
       if (ev >= cnt) break;
+      SK_N(7);
       // the event record, alone (wave-uniform)
-      const uint32_t le = ev / kSkQ, qe = ev % kSkQ;
+      const uint32_t le = ev & 63u, qe = ev >> 6;
       uint32_t vs = cur.seq[0], vl = cur.len[0];
       uint64_t vr = cur.rxk[0];
 #pragma unroll
@@ -351,8 +509,6 @@ flow_skel_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
           }
           nwin++;
           ncl++;
-          last_close = p;
-          last_zr = (fe & kFFa) ? 1u : 0u;
           sst = seqmax;
           ws = rx;
           we = uni_t(tadd(rx, window));
@@ -365,12 +521,54 @@ flow_skel_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
 #pragma unroll
       for (uint32_t q = 0; q < kSkQ; q++) fl[q] = (lane == le && q == qe) ? fe : fl[q];
       pos = ev + 1u;
+      SK_T(2);
     }
 #pragma unroll
     for (uint32_t q = 0; q < kSkQ; q++)
-      if (kSkQ * lane + q < cnt) rflags[i0 + kSkQ * lane + q] = (uint8_t)fl[q];
-    cur = nxt;
-    nxt = nx2;
+      if (64u * q + lane < cnt) rflags[i0 + 64u * q + lane] = (uint8_t)fl[q];
+  };
+  for (; seg < e; seg += kSkSeg) {
+    stage(seg);
+    const uint32_t nch = (min(kSkSeg, e - seg) + kSkChunk - 1u) / kSkChunk;
+    for (uint32_t c = 0; c < nch; c += 4u) summarize(seg, c);
+    __syncthreads();  // summaries ready
+    SK_T(4);
+    for (uint32_t c = 0; c < nch; c++) {
+      const uint32_t i0 = seg + c * kSkChunk;
+      const SkSum sm = sums[c];  // (every lane reads the same: broadcast)
+      const uint64_t mx_rx = (uint64_t)__builtin_amdgcn_readfirstlane((int)sm.rx_hi) << 32 |
+                             (uint32_t)__builtin_amdgcn_readfirstlane((int)sm.rx_lo);
+      const bool nz = __builtin_amdgcn_readfirstlane((int)sm.nz) != 0;
+      bool plain = valid && mx_rx < wek && (!nz || hasm);
+      int64_t mn = 0, mx = (int32_t)(L - F);
+      if (plain && nz) {
+        const int64_t r0 = (int32_t)((uint32_t)__builtin_amdgcn_readfirstlane((int)sm.base) - F);
+        mn = min((int64_t)0, r0 + __builtin_amdgcn_readfirstlane(sm.dmin));
+        mx = max(mx, r0 + __builtin_amdgcn_readfirstlane(sm.dmax));
+        plain = mx - mn < 1024;
+      }
+      if (lane == 0) {
+        cst[c] = plain ? 1u : 0u;
+        cst[kSkChunks + c] = sst;
+      }
+      if (plain) {
+        if (nz) {
+          const uint32_t F2 = F + (uint32_t)mn;
+          L = F + (uint32_t)mx;
+          F = F2;
+        }
+        SK_T(0);
+        SK_N(5);
+      } else {
+        SkLd B;
+        ld(i0, B);
+        chunk(i0, B);
+      }
+    }
+    __syncthreads();  // the segment is walked
+    for (uint32_t c = 0; c < nch; c += 4u)
+      if (cst[c]) plain_flags(seg, c);
+    __syncthreads();  // the segment's LDS may be restaged
   }
   if (lane == 0) {
     WinItem it;
@@ -381,15 +579,11 @@ flow_skel_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
     it.seqmax = it.sst = 0u;
     it.ws = tm_key(ws);
     wl[nwin] = it;
-    FlowFin* fp = fin + f;
     fp->F = F;
     fp->hasmask = hasm ? 1u : 0u;
     fp->nwin = nwin + 1u;
     fp->ncl = ncl;
-    fp->last_close = last_close;
-    fp->last_zr = last_zr;
     fp->rc0 = rc0;
-    fp->dups = 0ull;
     sp->window_valid = valid ? 1u : 0u;
     sp->win_start_sec = ws.sec;
     sp->win_start_usec = ws.usec;
@@ -399,28 +593,47 @@ flow_skel_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
     sp->n_reports += ncl;
     report_count[f] = rc0 + ncl;
   }
+#if MGENX_DIAG
+  prof[3] = __builtin_amdgcn_s_memtime() - prof_t0;
+  if (lane == 0 && atomicCAS(&g_skel_claim, 0u, 1u) == 0u)
+    for (int k2 = 0; k2 < 8; k2++) g_skel_prof[k2] = prof[k2];
+#endif
+#undef SK_T
+#undef SK_N
 }
 
-// ---- the windows: one wave per window, kWinWaves per flow ----
-constexpr uint32_t kWQ = 4;               // records per lane and chunk (q-major: i0 + 64q + lane)
+#if MGENX_DIAG
+__device__ unsigned long long g_win_prof[8];
+__device__ unsigned int g_win_claim;
+#endif
+// ---- the windows: one wave (a workgroup of its own) per window, kWinWaves per flow ----
+// The wave walks its window's epoch from the epoch's start (records before the window only
+// insert), chunks of 256 records q-major, two chunks in flight in two register sets.  The
+// window's latency sum -- the one FP64 chain whose rounding depends on record order -- is the
+// wave's, in order, over each chunk's lat' read out lane by lane.  The open window's wave writes
+// the flow's state (the others read the state before the call from FlowFin).
+constexpr uint32_t kWQ = 4;
 constexpr uint32_t kWChunk = 64u * kWQ;
-__global__ void __launch_bounds__(64 * kWinWaves)
-flow_win_kernel(const mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
+struct WLd {
+  FRec r[kWQ];
+  uint32_t fl[kWQ];
+};
+__global__ void __launch_bounds__(64)
+flow_win_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
                 const uint32_t* __restrict__ bnd, const FRec* __restrict__ recs,
                 const uint8_t* __restrict__ rflags, const WinItem* __restrict__ wins,
-                FlowFin* __restrict__ fin, double* __restrict__ lat2,
-                mgenx_flow_report* __restrict__ reports, uint32_t per_flow,
-                uint32_t* __restrict__ report_rec, const uint32_t* __restrict__ order,
-                CloseRec* __restrict__ closes) {
-  __shared__ uint32_t tabs[kWinWaves][1024];
-  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  const uint32_t f = blockIdx.x;
+                const FlowFin* __restrict__ fin, mgenx_flow_report* __restrict__ reports,
+                uint32_t per_flow, uint32_t* __restrict__ report_rec,
+                const uint32_t* __restrict__ order) {
+  __shared__ uint32_t T[1024];
+  const uint32_t lane = threadIdx.x;
+  const uint32_t f = blockIdx.x / kWinWaves, wv = blockIdx.x % kWinWaves;
+  if (f >= n_flows) return;
   const uint32_t b = bnd[f], e = bnd[f + 1u];
   if (b >= e) return;
-  const mgenx_flow_state* sp = flows + f;
-  FlowFin* fp = fin + f;
+  mgenx_flow_state* sp = flows + f;
+  const FlowFin* fp = fin + f;
   const uint32_t nwin = fp->nwin, rc0 = fp->rc0;
-  uint32_t* T = tabs[wv];
   auto wsync = [] {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -431,7 +644,23 @@ flow_win_kernel(const mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
     for (uint32_t j = 0; j < 1024u / 64u; j++) T[64u * j + lane] = kTabEmpty;
   };
   const double inf = __builtin_huge_val();
+#if MGENX_DIAG
+  // (diagnostics) cycles of one middle window (k = 1) by phase: setup, insert-only chunks,
+  // duplicate passes, counters, sums, tail, total; chunks
+  unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0}, prof_t = 0, prof_t0 = 0;
+#define WN_T(slot)                                                         \
+  do {                                                                     \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime();          \
+    prof[slot] += now_ - prof_t;                                           \
+    prof_t = now_;                                                         \
+  } while (0)
+#else
+#define WN_T(slot) do {} while (0)
+#endif
   for (uint32_t k = wv; k < nwin; k += kWinWaves) {
+#if MGENX_DIAG
+    prof_t = prof_t0 = __builtin_amdgcn_s_memtime();
+#endif
     const WinItem it = wins[(size_t)b + f + k];
     const bool open = (it.fl & kWinOpen) != 0u;
     const uint32_t a = it.a, end = open ? it.c : it.c + 1u;
@@ -440,9 +669,9 @@ flow_win_kernel(const mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
     uint32_t s0 = it.r;
     if (it.r == kNoEpoch) {  // the call's initial epoch: the stored mask's indices, position 0
       s0 = b;
-      if (sp->mask_n) {
-        const uint32_t F0 = sp->mask_first;
-        uint32_t w = lane < 32u ? sp->mask[lane] : 0u;
+      if (fp->n0) {
+        const uint32_t F0 = fp->first0;
+        uint32_t w = lane < 32u ? fp->mask0[lane] : 0u;
         while (w) {
           const uint32_t j = (uint32_t)__builtin_ctz(w);
           w &= w - 1u;
@@ -451,64 +680,58 @@ flow_win_kernel(const mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
         wsync();
       }
     }
-    // the epoch's records before the window (no epoch starts inside: r is the latest)
-    for (uint32_t i0 = s0; i0 < a; i0 += kWChunk) {
-#pragma unroll
-      for (uint32_t q = 0; q < kWQ; q++) {
-        const uint32_t p = i0 + 64u * q + lane;
-        if (p < a && (rflags[p] & kFIns)) atomicMin(&T[recs[p].seq & 1023u], p + 1u);
-      }
-    }
-    wsync();
-    // the start state: the stored one, or the one the closing record before the window leaves
-    uint64_t mc, bc;
-    double lmin, lmax;
+    // the start state: the stored one, or (below) the one the record before the window leaves
+    uint64_t mc = 0, bc = 0;
+    double lmin = 0.0, lmax = 0.0, sum = 0.0;
     if (a == b) {
-      mc = sp->msg_count;
-      bc = sp->byte_count;
-      lmin = sp->latency_min;
-      lmax = sp->latency_max;
-    } else {
-      const uint32_t c = a - 1u;
-      const FRec rc = recs[c];
-      const uint32_t fc = rflags[c];
-      const bool dup = (fc & kFDupT) && T[rc.seq & 1023u] < c + 1u;
-      const bool counted = (fc & kFCe) && !dup;
-      mc = rc.len ? 1u : 0u;
-      bc = 0u;
-      lmin = lmax = (rc.len != 0u && counted) ? rc.latency : 0.0;
+      mc = fp->mc0;
+      bc = fp->bc0;
+      lmin = fp->lmin0;
+      lmax = fp->lmax0;
+      sum = fp->lsum0;
     }
-    // the window's records
+    const uint32_t tfrom = a > b ? a - 1u : a;  // records from here take the duplicate test
     uint32_t kc = 0, ndup = 0, fpos = 0xFFFFFFFFu, fsize = 0;
     uint64_t ssum = 0;
     double cmn = inf, cmx = -inf;
-    for (uint32_t i0 = a; i0 < end; i0 += kWChunk) {
-      const uint32_t cnt = min(kWChunk, end - i0);
-      FRec r[kWQ];
-      uint32_t fl[kWQ];
+    auto ld = [&](uint32_t i0, WLd& w) {
 #pragma unroll
       for (uint32_t q = 0; q < kWQ; q++) {
-        const uint32_t o = 64u * q + lane, p = min(i0 + o, end - 1u);
-        r[q] = recs[p];
-        fl[q] = o < cnt ? rflags[p] : 0u;
+        const uint32_t p = min(i0 + 64u * q + lane, end - 1u);
+        w.r[q] = recs[p];
+        w.fl[q] = rflags[p];
+      }
+    };
+    auto chunk = [&](const uint32_t i0, const WLd& w) {
+      const uint32_t cnt = min(kWChunk, end - i0);
+      uint32_t fl[kWQ];
+#pragma unroll
+      for (uint32_t q = 0; q < kWQ; q++) fl[q] = 64u * q + lane < cnt ? w.fl[q] : 0u;
+#if MGENX_DIAG
+      prof[7]++;
+#endif
+      if (i0 + cnt <= tfrom) {  // before the tested records: inserts only
+#pragma unroll
+        for (uint32_t q = 0; q < kWQ; q++)
+          if (fl[q] & kFIns) atomicMin(&T[w.r[q].seq & 1023u], i0 + 64u * q + lane + 1u);
+        WN_T(1);
+        return;
       }
       bool dup[kWQ] = {false, false, false, false};
       uint32_t lo = 0;
       while (lo < cnt) {
         // the sub-range [lo, hi): up to the next epoch start after lo
         uint32_t hi = cnt;
+        bool at_es = false;
 #pragma unroll
         for (uint32_t q = 0; q < kWQ; q++) {
           const uint32_t o = 64u * q + lane;
-          const uint64_t es = __ballot((o > lo) & (o < cnt) & ((fl[q] & kFEstart) != 0u));
-          if (es) hi = min(hi, 64u * q + (uint32_t)__builtin_ctzll(es));
+          const bool es = (fl[q] & kFEstart) != 0u;
+          const uint64_t eb = __ballot((o > lo) & es);
+          if (eb) hi = min(hi, 64u * q + (uint32_t)__builtin_ctzll(eb));
+          at_es |= __ballot((o == lo) & es) != 0ull;
         }
-        // an epoch start at lo: the mask is {seq} after it
-        bool at_es = false;
-#pragma unroll
-        for (uint32_t q = 0; q < kWQ; q++)
-          at_es |= __ballot((64u * q + lane == lo) & ((fl[q] & kFEstart) != 0u)) != 0ull;
-        if (at_es) {
+        if (at_es) {  // an epoch start at lo: the mask is {seq} after it
           clear_tab();
           wsync();
         }
@@ -516,47 +739,73 @@ flow_win_kernel(const mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
         for (uint32_t q = 0; q < kWQ; q++) {
           const uint32_t o = 64u * q + lane;
           if ((o >= lo) & (o < hi) & ((fl[q] & kFIns) != 0u))
-            atomicMin(&T[r[q].seq & 1023u], i0 + o + 1u);
+            atomicMin(&T[w.r[q].seq & 1023u], i0 + o + 1u);
         }
         wsync();
 #pragma unroll
         for (uint32_t q = 0; q < kWQ; q++) {
           const uint32_t o = 64u * q + lane;
-          const uint32_t tv = T[r[q].seq & 1023u];
+          const uint32_t tv = T[w.r[q].seq & 1023u];
           const bool mine = (o >= lo) & (o < hi);
           dup[q] = mine ? ((fl[q] & kFDupT) != 0u) & (tv < i0 + o + 1u) : dup[q];
         }
         wsync();
         lo = hi;
       }
-      // counters; a counter restart (first message / first actual message) precedes every
-      // counted record of the window (the mask is empty before it)
+      WN_T(2);
+      // the record before the window: the start state it leaves (:228-242)
+      if (a > b && tfrom >= i0 && tfrom < i0 + cnt) {
+        const uint32_t o = tfrom - i0, l = o & 63u, qq = o >> 6;
+        uint32_t vl = w.r[0].len, vf = fl[0], vd = dup[0];
+        double vt = w.r[0].latency;
+#pragma unroll
+        for (uint32_t q = 1; q < kWQ; q++) {
+          vl = qq == q ? w.r[q].len : vl;
+          vf = qq == q ? fl[q] : vf;
+          vd = qq == q ? (uint32_t)dup[q] : vd;
+          vt = qq == q ? w.r[q].latency : vt;
+        }
+        const uint32_t len = (uint32_t)__builtin_amdgcn_readlane((int)vl, (int)l);
+        const uint32_t fc = (uint32_t)__builtin_amdgcn_readlane((int)vf, (int)l);
+        const bool dc = __builtin_amdgcn_readlane((int)vd, (int)l) != 0;
+        const uint64_t lb = __builtin_bit_cast(uint64_t, vt);
+        const double lat = __builtin_bit_cast(
+            double, (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(lb >> 32), (int)l) << 32 |
+                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)lb, (int)l));
+        const bool counted = (fc & kFCe) && !dc;
+        mc = len ? 1u : 0u;
+        bc = 0u;
+        lmin = lmax = (len != 0u && counted) ? lat : 0.0;
+        sum = counted ? lat : 0.0;  // latency_sum = latency (:236): the record's lat'
+      }
+      // the window's records: counters; a counter restart (first message / first actual
+      // message) precedes every counted record of the window (the mask is empty before it)
       double lp[kWQ];
 #pragma unroll
       for (uint32_t q = 0; q < kWQ; q++) {
         const uint32_t o = 64u * q + lane;
-        const bool live = o < cnt;
+        const uint32_t p = i0 + o;
+        const bool live = (o < cnt) & (p >= a);
         const bool counted = live & ((fl[q] & kFCe) != 0u) & !dup[q];
         const bool fa = live & ((fl[q] & kFFa) != 0u);
         ndup += (live & dup[q]) ? 1u : 0u;
         kc += counted ? 1u : 0u;
-        ssum += counted ? r[q].len : 0u;
-        const uint32_t p = i0 + o;
-        fsize = (counted & (p < fpos)) ? r[q].len : fsize;
+        ssum += counted ? w.r[q].len : 0u;
+        fsize = (counted & (p < fpos)) ? w.r[q].len : fsize;
         fpos = (counted & (p < fpos)) ? p : fpos;
-        cmn = vmin64(cmn, counted ? r[q].latency : inf);
-        cmx = vmax64(cmx, counted ? r[q].latency : -inf);
-        lp[q] = (counted | fa) ? r[q].latency : 0.0;
+        cmn = vmin64(cmn, counted ? w.r[q].latency : inf);
+        cmx = vmax64(cmx, counted ? w.r[q].latency : -inf);
+        lp[q] = (counted | fa) ? w.r[q].latency : 0.0;
       }
 #pragma unroll
       for (uint32_t q = 0; q < kWQ; q++) {
         const uint32_t o = 64u * q + lane;
-        const uint64_t rs = __ballot((o < cnt) & ((fl[q] & (kFFa | kFInit0)) != 0u));
+        const uint64_t rs = __ballot((o < cnt) & (i0 + o >= a) & ((fl[q] & (kFFa | kFInit0)) != 0u));
         if (rs) {
-          const uint32_t l = 63u - (uint32_t)__builtin_clzll(rs);  // the last one (first message
-          // of size 0, then the first actual message: both in one window)
-          const uint32_t len = (uint32_t)__builtin_amdgcn_readlane((int)r[q].len, (int)l);
-          const uint64_t lb = __builtin_bit_cast(uint64_t, r[q].latency);
+          // the last one (a size-0 first message, then the first actual message: one window)
+          const uint32_t l = 63u - (uint32_t)__builtin_clzll(rs);
+          const uint32_t len = (uint32_t)__builtin_amdgcn_readlane((int)w.r[q].len, (int)l);
+          const uint64_t lb = __builtin_bit_cast(uint64_t, w.r[q].latency);
           const uint32_t llo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)lb, (int)l);
           const uint32_t lhi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(lb >> 32), (int)l);
           const double lat = __builtin_bit_cast(double, (uint64_t)lhi << 32 | llo);
@@ -567,20 +816,43 @@ flow_win_kernel(const mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
           lmin = lmax = fa ? lat : 0.0;
         }
       }
+      WN_T(3);
+      // the sum, in record order: lane l's lat' of group q is record i0 + 64q + l, read out
+      // lane by lane (the reads do not wait for the sum: only the adds form the chain); the
+      // records outside the window add 0.0, exactly (a latency sum is never -0.0)
 #pragma unroll
       for (uint32_t q = 0; q < kWQ; q++) {
-        const uint32_t o = 64u * q + lane;
-        if (o < cnt) lat2[i0 + o] = lp[q];
+        const uint64_t bits = __builtin_bit_cast(uint64_t, lp[q]);
+        const int lo = (int)(uint32_t)bits, hi = (int)(uint32_t)(bits >> 32);
+#pragma unroll
+        for (int l = 0; l < 64; l++) {
+          const double x = __builtin_bit_cast(
+              double, (uint64_t)(uint32_t)__builtin_amdgcn_readlane(hi, l) << 32 |
+                          (uint32_t)__builtin_amdgcn_readlane(lo, l));
+          sum = __dadd_rn(sum, x);
+        }
       }
+      WN_T(4);
+    };
+    WN_T(0);
+    WLd A, B;
+    ld(s0, A);
+    ld(s0 + kWChunk, B);
+    for (uint32_t i0 = s0; i0 < end; i0 += 2u * kWChunk) {
+      chunk(i0, A);
+      ld(i0 + 2u * kWChunk, A);
+      if (i0 + kWChunk >= end) break;
+      chunk(i0 + kWChunk, B);
+      ld(i0 + 3u * kWChunk, B);
     }
     // fold the counted records into the start state (:132-153)
     const uint32_t K = (uint32_t)__builtin_amdgcn_readfirstlane((int)WRing::wave_sum(kc));
     const uint32_t D = (uint32_t)__builtin_amdgcn_readfirstlane((int)WRing::wave_sum(ndup));
     if (K) {
-      const uint64_t slo = WRing::wave_sum((uint32_t)(ssum & 0xFFFFFFFFu) & 0xFFFFu) +
-                           ((uint64_t)WRing::wave_sum((uint32_t)(ssum & 0xFFFFFFFFu) >> 16) << 16);
-      const uint64_t shi = (uint64_t)WRing::wave_sum((uint32_t)(ssum >> 32)) << 32;
-      const uint64_t S = slo + shi;
+      const uint32_t slo32 = (uint32_t)ssum;
+      const uint64_t S = (uint64_t)WRing::wave_sum(slo32 & 0xFFFFu) +
+                         ((uint64_t)WRing::wave_sum(slo32 >> 16) << 16) +
+                         ((uint64_t)WRing::wave_sum((uint32_t)(ssum >> 32)) << 32);
       const uint32_t fmin = WRing::wave_min(fpos);
       const uint64_t who = __ballot(fpos == fmin);
       const uint32_t s1 = (uint32_t)__builtin_amdgcn_readlane((int)fsize, (int)__builtin_ctzll(who));
@@ -598,7 +870,11 @@ flow_win_kernel(const mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
       }
       mc += K;
     }
-    if (D && lane == 0) atomicAdd((unsigned long long*)&fp->dups, (unsigned long long)D);
+    sum = __builtin_bit_cast(double, (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(
+                                         (int)(uint32_t)__builtin_bit_cast(uint64_t, sum)) |
+                                     (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(
+                                         (int)(uint32_t)(__builtin_bit_cast(uint64_t, sum) >> 32)) << 32);
+    if (D && lane == 0) atomicAdd((unsigned long long*)&sp->dup_count, (unsigned long long)D);
     if (!open) {
       const uint32_t slot = rc0 + k;
       if (slot < per_flow && lane == 0) {
@@ -635,15 +911,11 @@ flow_win_kernel(const mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
         rp->msg_count = r_count;
         rp->rate = r_rate;
         rp->loss = r_loss;
+        rp->latency_ave = mc == 0 ? -1.0 : mc == 1 ? sum : __ddiv_rn(sum, (double)mc);
         rp->latency_min = r_min;
         rp->latency_max = r_max;
         rp->rx_sec = rx.sec;
         rp->rx_usec = rx.usec;
-        CloseRec c;
-        c.pos = it.c;
-        c.zr = (it.fl & kWinZr) ? 1u : 0u;
-        c.mc = mc;
-        closes[s] = c;
         if (report_rec) report_rec[s] = order[it.c];
       }
     } else {  // the flow's state after the call: counters and the mask (bit i <-> F + i)
@@ -655,117 +927,27 @@ flow_win_kernel(const mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
           word |= T[(F + lane * 32u + j) & 1023u] != kTabEmpty ? 1u << j : 0u;
       }
       const uint32_t nset = (uint32_t)__builtin_amdgcn_readfirstlane((int)WRing::wave_sum((uint32_t)__popc(word)));
-      if (lane < 32u) fp->mask[lane] = word;
+      if (lane < 32u) sp->mask[lane] = word;
       if (lane == 0) {
-        fp->mask_n = nset;
-        fp->mc = mc;
-        fp->bc = bc;
-        fp->lmin = lmin;
-        fp->lmax = lmax;
-      }
-    }
-    wsync();
-  }
-}
-
-// ---- the latency sums, and the flow state: one wave per flow ----
-// Each window's in-order FP64 sum of lat' (lane t takes window t), staged through LDS in pieces
-// of the flow's records; windows: the kept reports of this call, then the open one.
-constexpr uint32_t kPiece = 1024;
-__global__ void __launch_bounds__(256)
-flow_sum_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
-                const uint32_t* __restrict__ bnd, const FlowFin* __restrict__ fin,
-                const double* __restrict__ lat2, mgenx_flow_report* __restrict__ reports,
-                uint32_t per_flow, const CloseRec* __restrict__ closes) {
-  __shared__ double pieces[4][kPiece];
-  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  const uint32_t f = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + wv);
-  if (f >= n_flows) return;
-  const uint32_t b = bnd[f], e = bnd[f + 1u];
-  if (b >= e) return;
-  mgenx_flow_state* sp = flows + f;
-  const FlowFin* fp = fin + f;
-  double* piece = pieces[wv];
-  const double lsum0 = sp->latency_sum;
-  const uint32_t rc0 = fp->rc0, ncl = fp->ncl;
-  const uint32_t rcount = rc0 + ncl;
-  const uint32_t kept = min(rcount, per_flow);
-  const uint32_t nslots = kept > rc0 ? kept - rc0 : 0u;
-  const uint32_t nwin = nslots + 1u;  // + the open window
-  const CloseRec* cl = closes + (size_t)f * per_flow;
-  for (uint32_t w0 = 0; w0 < nwin; w0 += 64u) {
-    const uint32_t t = w0 + lane;
-    const bool has = t < nwin;
-    uint32_t lo = 0, hi = 0;
-    double sum = 0.0;
-    if (has) {
-      if (t < nslots) {
-        const uint32_t slot = rc0 + t;
-        hi = cl[slot].pos;
-        if (t == 0) {
-          lo = b;
-          sum = lsum0;
-        } else {
-          lo = cl[slot - 1u].pos + (cl[slot - 1u].zr ? 1u : 0u);
-        }
-      } else {
-        hi = e - 1u;
-        if (ncl) {
-          lo = fp->last_close + (fp->last_zr ? 1u : 0u);
-        } else {
-          lo = b;
-          sum = lsum0;
-        }
-      }
-    }
-    const uint32_t nl = min(nwin - w0, 64u);
-    const uint32_t a0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)lo);
-    const uint32_t z0 = (uint32_t)__builtin_amdgcn_readlane((int)hi, (int)(nl - 1u));
-    for (uint32_t p0 = a0; p0 <= z0 && p0 >= a0; p0 += kPiece) {
-      const uint32_t pend = min(z0 + 1u, p0 + kPiece);
-      const bool mine = has && lo <= hi && lo < pend && hi >= p0;
-      if (!__ballot(mine)) continue;
-      for (uint32_t j = lane; j < pend - p0; j += 64u) piece[j] = lat2[p0 + j];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (mine) {
-        const uint32_t ja = max(lo, p0) - p0, jz = min(hi + 1u, pend) - p0;
-        uint32_t j = ja;
-        for (; j + 8u <= jz; j += 8u) {
-          double x[8];
-#pragma unroll
-          for (int u = 0; u < 8; u++) x[u] = piece[j + u];
-#pragma unroll
-          for (int u = 0; u < 8; u++) sum = __dadd_rn(sum, x[u]);
-        }
-        for (; j < jz; j++) sum = __dadd_rn(sum, piece[j]);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    if (has) {
-      if (t < nslots) {
-        const uint64_t mc = cl[rc0 + t].mc;
-        reports[(size_t)f * per_flow + rc0 + t].latency_ave =
-            mc == 0 ? -1.0 : mc == 1 ? sum : __ddiv_rn(sum, (double)mc);
-      } else {
+        if (fp->hasmask) sp->mask_first = F;
+        sp->mask_n = nset;
+        sp->msg_count = mc;
+        sp->byte_count = bc;
+        sp->latency_min = lmin;
+        sp->latency_max = lmax;
         sp->latency_sum = sum;
       }
     }
+    wsync();
+#if MGENX_DIAG
+    WN_T(5);
+    prof[6] = __builtin_amdgcn_s_memtime() - prof_t0;
+    if (k == 1 && lane == 0 && atomicCAS(&g_win_claim, 0u, 1u) == 0u)
+      for (int k2 = 0; k2 < 8; k2++) g_win_prof[k2] = prof[k2];
+    for (int k2 = 0; k2 < 8; k2++) prof[k2] = 0;
+#endif
   }
-  // the rest of the state (flow_skel_kernel wrote the window and seq_start fields)
-  if (lane < 32u) sp->mask[lane] = fp->mask[lane];
-  if (lane == 0) {
-    if (fp->hasmask) sp->mask_first = fp->F;
-    sp->mask_n = fp->mask_n;
-    sp->msg_count = fp->mc;
-    sp->byte_count = fp->bc;
-    sp->latency_min = fp->lmin;
-    sp->latency_max = fp->lmax;
-    sp->dup_count += fp->dups;
-  }
+#undef WN_T
 }
 
 // ---- ordering the records by flow, stably: a counting sort (flow count < kCountBins) --
@@ -1259,6 +1441,18 @@ static double quantized_window(double value) {
 
 #if MGENX_DIAG
 extern "C" int mgenx_diag_seg_prof(unsigned long long* out, int n) {
+  if (out && n == 8) {  // flow_skel_kernel's phase cycles (g_skel_prof; the claim reset)
+    const unsigned int zero = 0;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_skel_prof), 64) != hipSuccess) return MGENX_EDEVICE;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_skel_claim), &zero, 4) == hipSuccess ? MGENX_OK
+                                                                               : MGENX_EDEVICE;
+  }
+  if (out && n == 12) {  // flow_win_kernel's phase cycles (g_win_prof; the claim reset)
+    const unsigned int zero = 0;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_win_prof), 64) != hipSuccess) return MGENX_EDEVICE;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_win_claim), &zero, 4) == hipSuccess ? MGENX_OK
+                                                                              : MGENX_EDEVICE;
+  }
   if (out && n == 16)  // flow_order_kernel's phase cycles (g_ord_prof, 8 entries)
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ord_prof), 64) == hipSuccess ? MGENX_OK
                                                                               : MGENX_EDEVICE;
@@ -1318,14 +1512,12 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
   const bool want_order = report_rec != nullptr;
   const size_t nb = a256((size_t)n * 4), rb = a256((size_t)n * sizeof(FRec));
   const size_t hb = a256(n_hist * 4), bb = a256((size_t)bins * 4);
-  const size_t lb = a256((size_t)(n + 64) * 8);
-  const size_t cb = a256((size_t)n_flows * per_flow * sizeof(CloseRec));
   const size_t fb = a256((size_t)n + 256), wb = a256(((size_t)n + n_flows) * sizeof(WinItem));
   const size_t xb = a256((size_t)n_flows * sizeof(FlowFin));
-  // both: records (sorted), lat', closes, record flags, windows, per-flow results
+  // both: records (sorted), record flags, windows, per-flow results
   // counting: hist, start, order (report_rec only), row totals
   // radix:    keys_in, keys_out, vals_in, order, bounds, cub
-  const size_t common = rb + lb + cb + fb + wb + xb;
+  const size_t common = rb + fb + wb + xb;
   const size_t need = common + (sort_path == 0 ? 2 * hb + (want_order ? nb : 0) + a256(cub_bytes)
                                                : 4 * nb + bb + a256(cub_bytes));
   if (ws.bytes < need) {
@@ -1341,8 +1533,6 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
   char* p = static_cast<char*>(ws.mem);
   auto take = [&](size_t b) { char* q = p; p += b; return q; };
   FRec* recs = (FRec*)take(rb);
-  double* lat2 = (double*)take(lb);
-  CloseRec* closes = (CloseRec*)take(cb);
   uint8_t* rflags = (uint8_t*)take(fb);
   WinItem* wins = (WinItem*)take(wb);
   FlowFin* fin = (FlowFin*)take(xb);
@@ -1416,14 +1606,20 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
     bnd = d_bnd;
   }
   if (sabl) return MGENX_OK;  // timing study: ordering only
-  const uint32_t g4 = (n_flows + 3u) / 4u;
-  hipLaunchKernelGGL(flow_skel_kernel, dim3(g4), dim3(256), 0, stream, flows, n_flows, bnd, recs,
-                     rflags, wins, fin, report_count);
-  hipLaunchKernelGGL(flow_win_kernel, dim3(n_flows), dim3(64 * kWinWaves), 0, stream, flows,
-                     n_flows, bnd, recs, rflags, wins, fin, lat2, reports, per_flow, report_rec,
-                     order, closes);
-  hipLaunchKernelGGL(flow_sum_kernel, dim3(g4), dim3(256), 0, stream, flows, n_flows, bnd, fin,
-                     lat2, reports, per_flow, closes);
+  e = set_max_lds((const void*)flow_skel_kernel, (int)kSkLds);
+  if (e != hipSuccess) {
+    snprintf(err, errn, "flow_reduce skeleton: %s", hipGetErrorString(e));
+    return MGENX_EDEVICE;
+  }
+  // block -> flow multiplier: odd, near 0.618 n_flows, coprime with n_flows (a permutation)
+  uint32_t fmul = n_flows > 2 ? (uint32_t)(0.6180339887 * n_flows) | 1u : 1u;
+  auto gcd = [](uint32_t x, uint32_t y) { while (y) { const uint32_t t = x % y; x = y; y = t; } return x; };
+  while (fmul > 1 && gcd(fmul, n_flows) != 1) fmul -= 2;
+  if (fmul == 0) fmul = 1;
+  hipLaunchKernelGGL(flow_skel_kernel, dim3(n_flows), dim3(256), kSkLds, stream, flows, n_flows,
+                     fmul, bnd, recs, rflags, wins, fin, report_count);
+  hipLaunchKernelGGL(flow_win_kernel, dim3(n_flows * kWinWaves), dim3(64), 0, stream, flows,
+                     n_flows, bnd, recs, rflags, wins, fin, reports, per_flow, report_rec, order);
   e = hipGetLastError();
   if (e != hipSuccess) {
     snprintf(err, errn, "flow_reduce: %s", hipGetErrorString(e));

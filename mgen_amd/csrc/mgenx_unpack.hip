@@ -1668,6 +1668,242 @@ unpack_fixed_ring_kernel(UnpackParams p, uint32_t expect) {
   if (held) flush();
 }
 
+// ---------------------------------------------------------------------------------------
+// Long records (TCP streams: config 5's 16-KiB records), one WAVE per record.  The kernels
+// above give a record to a quad, so a wave's load instruction reads 64 bytes from each of 16
+// records -- 16 KiB apart here.  This one covers the record with 1-KiB rows aligned to its
+// end; quad k takes bytes [64k, 64k + 64) of every row, so each load instruction reads 1 KiB
+// contiguously.  The braid CRC is the quad kernels' with A_1024 in place of A_64 (staged in
+// LDS replicated exactly as A_64 is above, so the same one-perm-per-lookup addressing); at the
+// record end a lane folds its four words (A_4, Horner), the quad its lanes (A_16, A_32) and the
+// wave its quads (A_64 .. A_512), and the residue is compared with expect[L].
+// Rows stream through 8 registers: consuming row j of the wave's current 8-row block reloads
+// that register with row j of its next block (the record's next block, or the first block of
+// the wave's next record), so 8 KiB stay in flight per wave.  A record is front-padded with
+// zero rows to whole blocks (a zero braid state stays zero through them).  Quad 0 (lanes 0-3)
+// loads and decodes the header as the general kernel does, under the same receive rules
+// (TCP: Unpack sees min(L, 8192) bytes, mgenTransport.cpp:2016-2031; the CRC covers L - 4).
+constexpr int kLongNB = 8;                                  // rows per block
+constexpr uint32_t kLongMin = 4096;                         // mean record length that picks it
+constexpr int kLongFold = 7;                                // A4 A16 A32 A64 A128 A256 A512
+constexpr size_t kLongLdsBytes = (size_t)(kRepDwords + kLongFold * kSmallTabDwords) * 4u;
+static_assert(kLongLdsBytes <= 160u * 1024u, "long-record tables fit the CU's LDS");
+
+__global__ void __launch_bounds__(kUnpackThreads) unpack_long_kernel(UnpackParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const uint32_t* fold = lds + kRepDwords;
+  const uint32_t *fA4 = fold, *fA16 = fold + 1024, *fA32 = fold + 2048, *fA64 = fold + 3072,
+                 *fA128 = fold + 4096, *fA256 = fold + 5120, *fA512 = fold + 6144;
+  const uint8_t* ldsb = reinterpret_cast<const uint8_t*>(lds);
+  // this thread's table entries: A_1024 (replicated) and the fold operators
+  constexpr int kFoldIdx[kLongFold] = {kTabA4, kTabA16, kTabA32, kTabA64, kTabA128, kTabA256,
+                                       kTabA512};
+  const uint32_t a1024 = p.tabs[kTabA1024 * 1024 + threadIdx.x];
+  uint32_t fr[kLongFold];
+#pragma unroll
+  for (int k = 0; k < kLongFold; k++) fr[k] = p.tabs[kFoldIdx[k] * 1024 + threadIdx.x];
+
+  const int lane = threadIdx.x & 63;
+  const int q = lane & 3, quad = lane >> 2;
+  const uint32_t s1 = a64_s1((uint32_t)lane);
+  const uint32_t wave_id = __builtin_amdgcn_readfirstlane(
+      blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  const uint32_t n_waves = gridDim.x * (blockDim.x >> 6);
+  const bool force = (p.opts & MGENX_OPT_CHECKSUM_FORCE) != 0;
+  const bool tcp = (p.opts & MGENX_OPT_TCP) != 0;
+  const bool want_ext = p.cols.dst_addr || p.cols.host_addr;
+  const mgenx_cols& cc = p.cols;
+  const bool any_ext = cc.hdr_len || cc.payload_off || cc.host_port || cc.host_type ||
+                       cc.host_len || cc.lat_raw || cc.lon_raw || cc.alt || cc.dst_addr ||
+                       cc.host_addr || cc.decoded;
+  const uint8_t* dummy = reinterpret_cast<const uint8_t*>(p.tabs);
+
+  // a record's placement (wave-uniform)
+  struct Rec {
+    uint32_t idx;   // record index (>= n: none)
+    uint64_t off;
+    uint32_t L;
+    bool live;      // inside the slab
+    bool rows;      // its CRC runs on the rows (>= 32 bytes; shorter ones bit by bit)
+    uint32_t nb;    // blocks (>= 1)
+    int64_t r0;     // position of virtual row 0 (record-relative, <= 0)
+  };
+  auto place = [&](uint32_t ri) {
+    Rec r;
+    r.idx = ri;
+    r.off = 0;
+    r.L = 0;
+    if (ri < p.n) {
+      r.off = p.rec_off ? p.rec_off[ri] : (uint64_t)ri * p.stride;
+      r.L = p.rec_len ? p.rec_len[ri] : p.fixed_len;
+    }
+    const bool oob = ri < p.n && (r.L > 65535u || r.off > p.slab_bytes || r.L > p.slab_bytes - r.off);
+    r.live = ri < p.n && !oob;
+    r.rows = r.live && r.L >= 32u;
+    const uint32_t R = r.rows ? (r.L + 1023u) >> 10 : 0u;
+    r.nb = R ? (R + kLongNB - 1u) / kLongNB : 1u;
+    r.r0 = (int64_t)(r.rows ? r.L : 0u) - 1024 * (int64_t)(kLongNB * r.nb);
+    return r;
+  };
+  // row j of block b of record r, this lane's 16 bytes: the address (clamped into the record;
+  // lanes before its start are zeroed at consumption)
+  auto row_pos = [&](const Rec& r, uint32_t b, int j) {
+    return r.r0 + 1024 * (int64_t)(kLongNB * b + (uint32_t)j) + 16 * lane;
+  };
+  auto ld_row = [&](const Rec& r, uint32_t b, int j) {
+    const int64_t pos = row_pos(r, b, j);
+    return ldu128(r.rows && pos >= 0 ? p.slab + r.off + (uint64_t)pos
+                                     : (r.rows && pos > -16 ? p.slab + r.off : dummy));
+  };
+
+  Rec cur = place(wave_id);
+  uint32_t b = 0;
+  u32x4_t d[kLongNB];
+#pragma unroll
+  for (int j = 0; j < kLongNB; j++) {
+    d[j] = ld_row(cur, 0, j);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // stage the tables behind the first block's loads (fence-free barrier: lgkmcnt only)
+  {
+    typedef __attribute__((address_space(3))) u32x4_t lds_u32x4_t;
+    const uint32_t e = threadIdx.x, k = e >> 8, val = e & 255u;
+    const u32x4_t s = {a1024, a1024, a1024, a1024};
+    lds_u32x4_t* dst = (lds_u32x4_t*)((k >> 1) * 65536u + val * 256u + (k & 1u) * 128u);
+#pragma unroll
+    for (int c = 0; c < kRep / 4; c++) dst[c] = s;
+    uint32_t* fl = lds + kRepDwords;
+#pragma unroll
+    for (int k2 = 0; k2 < kLongFold; k2++) fl[k2 * 1024 + e] = fr[k2];
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (cur.idx >= p.n) return;
+
+  uint32_t ha[4] = {0u, 0u, 0u, 0u}, hb[4] = {0u, 0u, 0u, 0u};
+  u32x4_t pf = {0u, 0u, 0u, 0u}, xs = {0u, 0u, 0u, 0u};
+  uint32_t expect = 0;
+  // header prefix (quad 0), expect[L], and the record's first 16 bytes shifted up to where
+  // they sit in the lane whose chunk straddles the record start (L % 16 != 0)
+  auto start_record = [&](const Rec& r) {
+    pf = ldu128((r.live && quad == 0 && r.L >= 16u * (q + 1)) ? p.slab + r.off + 16 * q : dummy);
+    expect = p.expect[r.live ? r.L : 0u];
+    const int s = (int)(16u - (r.L & 15u)) & 15;
+    const u32x4_t x0 = ldu128(r.rows ? p.slab + r.off : dummy);
+    xs = s ? shl_bytes(x0, s) : x0;
+  };
+  start_record(cur);
+  while (true) {
+    // the next block of the wave's stream
+    const bool last = b + 1u == cur.nb;
+    const Rec nx = last ? place(cur.idx + n_waves) : cur;
+    const uint32_t bn = last ? 0u : b + 1u;
+    const bool has_next = nx.idx < p.n;
+    // the first real row may start before the record (or the block is padding): zero the
+    // lanes' bytes before the record start (uniform test: rows at or past the start need none)
+    const bool fix = cur.r0 + 1024 * (int64_t)(kLongNB * b) < 0;
+    u32x4_t xf = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int j = 0; j < kLongNB; j++) {
+      u32x4_t x = d[j];
+      if (fix) {  // lanes before the record: zeros; the straddling lane: xs
+        const int64_t pos = row_pos(cur, b, j);
+        const bool zero = pos <= -16, strad = pos < 0 && pos > -16;
+        x.x = zero ? 0u : (strad ? xs.x : x.x);
+        x.y = zero ? 0u : (strad ? xs.y : x.y);
+        x.z = zero ? 0u : (strad ? xs.z : x.z);
+        x.w = zero ? 0u : (strad ? xs.w : x.w);
+      }
+      if (last && j == kLongNB - 1) {
+        // the record's final row: folded below, not advanced
+        uint32_t f0 = xor3(ha[0], hb[0], x.x), f1 = xor3(ha[1], hb[1], x.y);
+        uint32_t f2 = xor3(ha[2], hb[2], x.z);
+        uint32_t f3 = xor3(ha[3], hb[3], lane == 63 ? bswap32(x.w) : x.w);
+        asm volatile("" : "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3));
+        xf = u32x4_t{f0, f1, f2, f3};
+        __builtin_amdgcn_sched_barrier(0);
+        d[j] = has_next ? ld_row(nx, bn, j) : ldu128(dummy);
+        __builtin_amdgcn_sched_barrier(0);
+      } else {
+        const uint32_t xw[4] = {x.x, x.y, x.z, x.w};
+        uint32_t c4[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) c4[k] = xor3(ha[k], hb[k], xw[k]);
+        __builtin_amdgcn_sched_barrier(0);
+        d[j] = has_next ? ld_row(nx, bn, j) : ldu128(dummy);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = 0; k < 4; k++) a64_parts(ldsb, c4[k], s1, ha[k], hb[k]);
+      }
+    }
+    if (last) {
+      // ---- the record's CRC residue: lane, quad and wave folds ----
+      uint32_t v = shift_tab(fA4, xf.x) ^ xf.y;
+      v = shift_tab(fA4, v) ^ xf.z;
+      v = shift_tab(fA4, v) ^ xf.w;
+      v = shift_tab(fA4, v);  // at the end of the lane's 16 bytes
+      v = (q & 1) ? v : shift_tab(fA16, v);
+      v ^= __shfl_xor(v, 1);
+      v = (q & 2) ? v : shift_tab(fA32, v);
+      v ^= __shfl_xor(v, 2);  // at the end of the quad's 64 bytes
+      v = (quad & 1) ? v : shift_tab(fA64, v);
+      v ^= __shfl_xor(v, 4);
+      v = (quad & 2) ? v : shift_tab(fA128, v);
+      v ^= __shfl_xor(v, 8);
+      v = (quad & 4) ? v : shift_tab(fA256, v);
+      v ^= __shfl_xor(v, 16);
+      v = (quad & 8) ? v : shift_tab(fA512, v);
+      v ^= __shfl_xor(v, 32);  // at the record end, in every lane
+      const uint32_t tot = v;
+      // ---- the header (quad 0) and the outputs, as unpack_kernel's group ----
+      const uint32_t L = cur.L;
+      const bool live = cur.live;
+      const uint8_t* rec = p.slab + cur.off;
+      const uint32_t buf_len = tcp ? min(L, (uint32_t)MGENX_TX_BUFFER_SIZE) : L;
+      uint32_t pw[16];
+      quad_bcast<0>(pf, pw);
+      quad_bcast<1>(pf, pw);
+      quad_bcast<2>(pf, pw);
+      quad_bcast<3>(pf, pw);
+      if (lane == 0) {
+        if (live) {
+          uint32_t w[8];
+          const bool pfx = L >= 32;
+          if (pfx) {
+#pragma unroll
+            for (int j = 0; j < 8; j++) w[j] = pw[j];
+          } else if (L >= MGENX_MIN_SIZE) {
+            load_fixed(rec, buf_len, w);
+          } else {
+#pragma unroll
+            for (int j = 0; j < 8; j++) w[j] = 0;
+          }
+          const bool flagged = force || (((w[0] >> 24) & MGENX_FLAG_CHECKSUM) != 0 &&
+                                         buf_len >= MGENX_MIN_SIZE && ((w[0] >> 16) & 0xffu) == 2u);
+          const bool needs_crc = flagged && (tcp ? (L >= 4) : fixed_ok(buf_len, w));
+          const bool crc_ok = !needs_crc || (cur.rows ? tot == expect : small_crc_ok(rec, L));
+          if (buf_len >= 64 && fast_layout(pw[0], pw[5], (pw[5] >> 24) == 4u ? pw[7] : pw[10])) {
+            store_fast_q0(p.cols, cur.idx, pw, buf_len, crc_ok, tcp);
+            if (any_ext) store_fast_ext(p.cols, cur.idx, [&](int k) { return pw[k]; }, buf_len, true);
+          } else {
+            Hdr h;
+            parse_header(rec, buf_len, want_ext, w, h);
+            store_hdr_q0(p.cols, cur.idx, h, crc_ok, tcp);
+          }
+        } else {
+          store_oob_q0(p.cols, cur.idx);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 4; k++) ha[k] = hb[k] = 0u;
+      if (!has_next) break;
+      start_record(nx);
+    }
+    cur = nx;
+    b = bn;
+  }
+}
+
 template <typename K>
 static hipError_t launch_lds(K kernel, const UnpackParams& p, int grid, hipStream_t stream) {
   hipError_t e = set_max_lds((const void*)kernel, (int)kUnpackLdsBytes);
@@ -1687,6 +1923,13 @@ static hipError_t launch_var(const UnpackParams& p, int grid, hipStream_t stream
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((unpack_var_kernel<NT, KB, MODE>), dim3(grid), dim3(NT), kUnpackLdsBytes,
                      stream, p);
+  return hipGetLastError();
+}
+
+static hipError_t launch_long(const UnpackParams& p, int grid, hipStream_t stream) {
+  hipError_t e = set_max_lds((const void*)unpack_long_kernel, (int)kLongLdsBytes);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(unpack_long_kernel, dim3(grid), dim3(kUnpackThreads), kLongLdsBytes, stream, p);
   return hipGetLastError();
 }
 
@@ -1806,6 +2049,13 @@ hipError_t launch_unpack(const UnpackParams& p, int grid, hipStream_t stream, in
     }
   }
 #endif  // MGENX_DIAG
+  // long records (a TCP stream of 16-KiB records: the mean length from the slab) -- one wave
+  // per record, 1-KiB contiguous loads
+  const uint64_t mean = p.rec_len ? (p.n ? p.slab_bytes / p.n : 0) : p.fixed_len;
+  if (mean >= kLongMin) {
+    *which = MGENX_UNPACK_K_LONG;
+    return launch_long(p, grid, stream);
+  }
   // per-record lengths: sorted groups with the rows in a load ring -- when every wave gets
   // at least two 64-record tiles; fewer, larger records (a 1 GiB stream of 16-KiB TCP
   // records is 1024 tiles for 4096 waves) keep the general kernel's one group per wave and

@@ -376,7 +376,7 @@ def test_config5_full_size_vs_oracle(torch, eng, n):
     (or_tcp_scan, mgenTransport.cpp:1683-1760) against mgenx_stream_scan on a fresh engine:
     the first call (exact build) and the second (the successor-marked chain, path 2)."""
     import ctypes
-    from mgen_amd import Engine, OPT_TCP, SCAN_TCP
+    from mgen_amd import Engine, OPT_TCP, SCAN_TCP, UNPACK_K_LONG
     from oracle import oracle as O
     stream = _tcp_tx_stream(torch, eng, n)
     host = stream.cpu().numpy()
@@ -405,7 +405,9 @@ def test_config5_full_size_vs_oracle(torch, eng, n):
         assert paths == [0, 2], paths
         cols = e2.unpack(stream, n, rec_off=offs, rec_len=lens, opts=OPT_TCP)
         torch.cuda.synchronize()
-        for key in ("err", "seq_num", "flow_id", "tx_sec", "tx_usec", "msg_len"):
+        assert e2.last_unpack_kernel() == UNPACK_K_LONG   # one wave per 16-KiB record
+        for key in ("err", "seq_num", "flow_id", "tx_sec", "tx_usec", "msg_len", "flags",
+                    "dst_port", "payload_len"):
             got = cols[key].cpu().numpy().view(wf[key].dtype)
             assert np.array_equal(got, wf[key][:n]), key
     finally:
