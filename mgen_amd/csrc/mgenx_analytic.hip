@@ -89,866 +89,599 @@ __device__ __forceinline__ FRec make_frec(const RecSrc& src, uint32_t i) {
   return build_frec(load_rec(src, i));
 }
 
-// ---- MgenAnalytic::Update, window-parallel (mgenAnalytic.cpp:74-258) ----
-// The state machine is sequential per flow, but its order-dependent parts separate:
-//   * window closes depend on receive times alone (rxTime >= window_end, :168; the end moves to
-//     rxTime + window_size at each close, :228-230);
-//   * the mask's span (first, last) and seq_start evolve without the mask's bit contents: a Set
-//     fails exactly when it would widen the span to 1024 or more, whatever the bits hold, and a
-//     failed Set in the counted branch (:118-127) clears every set index -- the mask becomes
-//     {seq} (an "epoch start"; so does the first message of a flow, :80-99, and the first actual
-//     message, :156-165);
-//   * within an epoch nothing is cleared and every set index stays inside one 1024-wide span,
-//     so seq mod 1024 names a set index uniquely: a record is a duplicate (:109) exactly when an
-//     earlier record of its epoch set the same sequence number;
-//   * the counters restart at every close (:228-242), so each window's msg_count, byte_count
-//     and latency min / max are reductions over its own records, from a start state that only
-//     the closing record of the window before decides.
-// Two kernels:
-//   flow_skel_kernel  one wave per flow walks its records 256 at a time, scalar state only:
-//                     a run of records whose span stays below 1024 (a wave min / max) and holds
-//                     no close and no first message is plain; otherwise inclusive prefix scans
-//                     of seq - first find the first record that fails its Set, and it, a close
-//                     or a first message is done alone.  Out: a flag byte per record and the
-//                     flow's windows (records, epoch of the first record, seqMax and seq_start
-//                     at the close);
-//   flow_win_kernel   one wave per window (8 waves per flow): the epoch table of the window's
-//                     first record rebuilt in LDS (seq mod 1024 -> first position), the
-//                     duplicate test of each record, the window's counters and report, lat' per
-//                     record;
-//                     the window's in-order FP64 latency sum (the one chain whose rounding
-//                     depends on record order), and -- the open window's wave -- the flow's
-//                     state.
-// scripts/flow_decomp.py is the same decomposition on the CPU, checked against the oracle.
-constexpr uint8_t kFIns = 1;      // the record's seq is in the mask after it (Set succeeded)
-constexpr uint8_t kFDupT = 2;     // it takes the duplicate test with its seq inside the span
-constexpr uint8_t kFCe = 4;       // counted unless a duplicate (:121-154; a restart included)
-constexpr uint8_t kFEstart = 8;   // epoch start: the mask is {seq} after it
-constexpr uint8_t kFFa = 16;      // first message / first actual message: counters restart at it
-constexpr uint8_t kFInit0 = 32;   // first message of the flow, size 0 (:94-98)
-constexpr uint8_t kFClose = 64;   // closes a window
-constexpr uint32_t kNoEpoch = 0xFFFFFFFFu, kWinOpen = 1u, kWinZr = 2u;
-constexpr uint32_t kWinWaves = 8;  // flow_win_kernel: waves (windows in flight) per flow
-constexpr uint32_t kTabEmpty = 0xFFFFFFFFu;
-
-struct WinItem {       // one window of a flow (flow f's k-th at wins[bnd[f] + f + k])
-  uint32_t a, c;       // records [a, c] (c closes it) / open: [a, c) with c = the flow's end
-  uint32_t r;          // the epoch start at record a (kNoEpoch: the call's initial epoch)
-  uint32_t fl;         // kWinOpen, kWinZr (the closing record restarted the sum: :156-165)
-  uint32_t seqmax, sst;  // seqMax at the close, the seq_start it is measured from (:174-219)
-  uint64_t ws;         // window start, receive-time key
+// What the latency sums (the update's tail) need per kept report closed in this call
+struct CloseRec {
+  uint32_t pos, zr;     // the closing record (sorted position); zero restart
+  uint64_t mc;          // msg_count at the close: latency_ave's divisor
 };
-struct FlowFin {       // per flow: the state before the call (flow_skel_kernel copies it, so
-                       // the window waves read it while the open window's wave rewrites the
-                       // flow state), and the skeleton's results
-  uint32_t mask0[32];  // the mask before the call, relative to first0
-  uint32_t first0, n0, F, hasmask;
-  uint32_t nwin, ncl, rc0, rsv;
-  uint64_t mc0, bc0;
-  double lmin0, lmax0, lsum0;
-};
-static_assert(sizeof(WinItem) == 32, "window item");
 
-
-__device__ __forceinline__ uint64_t tm_key(Tm t) { return (uint64_t)t.sec << 32 | (uint64_t)t.usec; }
-__device__ __forceinline__ Tm key_tm(uint64_t k) { return Tm{(int64_t)(k >> 32), (int64_t)(uint32_t)k}; }
-
-// inclusive min / max scan over the wave (DPP rows of 16 by shifts, then the row broadcasts;
-// lanes a step does not reach keep their value: `old` is the identity)
-template <bool kMax>
-__device__ __forceinline__ int32_t wave_incl_minmax(int32_t v) {
-  const int32_t id = kMax ? INT32_MIN : INT32_MAX;
-  auto op = [](int32_t a, int32_t c) { return kMax ? max(a, c) : min(a, c); };
-  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x111, 0xf, 0xf, false));  // row_shr:1
-  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x112, 0xf, 0xf, false));  // row_shr:2
-  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x114, 0xf, 0xf, false));  // row_shr:4
-  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x118, 0xf, 0xf, false));  // row_shr:8
-  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x142, 0xa, 0xf, false));  // row_bcast:15
-  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x143, 0xc, 0xf, false));  // row_bcast:31
-  return v;
-}
-__device__ __forceinline__ int32_t wave_min_i32(int32_t v) {
-  return (int32_t)WRing::wave_reduce((uint32_t)v, (uint32_t)INT32_MAX, [](uint32_t a, uint32_t c) {
-    return (uint32_t)min((int32_t)a, (int32_t)c); });
-}
-__device__ __forceinline__ int32_t wave_max_i32(int32_t v) {
-  return (int32_t)WRing::wave_reduce((uint32_t)v, (uint32_t)INT32_MIN, [](uint32_t a, uint32_t c) {
-    return (uint32_t)max((int32_t)a, (int32_t)c); });
-}
-
+// ---- MgenAnalytic::Update, one WAVE per flow (mgenAnalytic.cpp:74-258) ----
+// The latency sum is the one FP64 chain whose rounding depends on record order; everything
+// else here is integer bookkeeping and order-free min / max.  So the update walks its flow's
+// records 256 at a time (4 per lane, coalesced) and leaves the sum to its tail: each
+// record's contribution to latency_sum ("lat'": its latency when Update adds or assigns it, else
+// 0.0) goes to lat2[], the closing records and the window msg_counts to CloseRec.  Since
+// latency_sum is 0.0 whenever msg_count is 0, every assignment of a latency to it is an add to
+// 0.0 (exact), and a window's sum is the in-order sum of its records' lat' values -- a window
+// restarts at its closing record's lat' (0.0 for the closing "first actual message" of
+// :165-173, whose local `latency` stays 0.0).
+//
+// Bulk runs: from the current state, a record is "simple" when it does not reach the window end
+// and, if msg != 0, lies inside the mask span (0 <= seq - first < 1024: Set takes its in-span
+// branch and never clears, `first` does not move).  A run of simple records changes the state in
+// closed form: a record is a duplicate when its ring bit is set or an earlier record of the run
+// has its sequence number (an LDS scatter finds clashes; then an LDS table of first positions
+// orders them), else it sets its bit; those at or past seq_start are counted.  Counts move by
+// ballots, bytes / min / max / last by per-lane partials folded before an exact step (flush).
+// The first non-simple record (window end, mask restart, a record below `first`, an empty mask,
+// the first record of a flow) takes the exact update below, and the run restarts after it.
 #if MGENX_DIAG
-__device__ unsigned long long g_skel_prof[8];
-__device__ unsigned int g_skel_claim;
+// (diagnostics) cycles of flow_update_kernel's first wave by phase: detect, bulk, exact, lat'
+// store, rounds, exact steps, bulk runs, total
+__device__ unsigned long long g_upd_prof[10];  // + [8] restart cycles, [9] restarts
+#define UPD_T(slot)                                                        \
+  do {                                                                     \
+    if (prof_on) {                                                         \
+      const unsigned long long now_ = __builtin_amdgcn_s_memtime();        \
+      prof[slot] += now_ - prof_t;                                         \
+      prof_t = now_;                                                       \
+    }                                                                      \
+  } while (0)
+#else
+#define UPD_T(slot) \
+  do {              \
+  } while (0)
 #endif
-// ---- the skeleton: one workgroup per flow, its walk on one wave ----
-// The walk is sequential and runs on one wave, so what it costs per record is what counts
-// (measured on config 4: ~2.5 k cycles per 256-record chunk for the per-record span test --
-// about 250 dependent instructions on a lone wave -- whether the records came from registers
-// or LDS).  So the workgroup's four waves do the per-record work in parallel around the walk:
-//   1. stage the flow's records -- the first 16 bytes of each FRec: receive key, seq, length --
-//      into LDS by direct global->LDS loads (kSkSeg records a segment, all in flight at once);
-//   2. summarize each 256-record chunk: its largest receive key, and the lowest / highest
-//      seq - base over its set attempts (base: the chunk's first seq), any non-zero length;
-//   3. wave 0 walks the summaries: a chunk with no close (largest key below the window end), no
-//      first message and a span below 1024 after it (the summary's min / max against first /
-//      last) is plain -- O(1) scalar work; any other chunk takes the per-record path (prefix
-//      scans, the first event alone, as before) on wave 0;
-//   4. the four waves write the plain chunks' flag bytes (the seq_start of each is recorded).
-// The summary test is exact when it passes: every record's seq - first then lies inside the
-// span, where the chunk-relative value plus the chunk base's offset equals it.
-constexpr uint32_t kSkQ = 4;
-constexpr uint32_t kSkChunk = 64u * kSkQ;
-constexpr uint32_t kSkSeg = 4096;  // records staged per segment (64 KiB: two workgroups per CU)
-constexpr uint32_t kSkChunks = kSkSeg / kSkChunk;
-struct SkSum {  // one chunk's summary
-  uint32_t rx_lo, rx_hi, base;
-  int32_t dmin, dmax;
-  uint32_t nz, rsv0, rsv1;
-};
-constexpr size_t kSkLds = (size_t)kSkSeg * 16u + kSkChunks * sizeof(SkSum) + kSkChunks * 8u;
-struct SkLd {
-  uint32_t seq[kSkQ], len[kSkQ];
-  uint64_t rxk[kSkQ];
-};
-typedef __attribute__((address_space(3))) void lds_void_t;
+constexpr uint32_t kUR = 4;             // records per lane and round
+constexpr uint32_t kRound = 64u * kUR;  // records per round
+constexpr uint32_t kLatRounds = 4;      // rounds of lat' staged in LDS per store burst
+
 __global__ void __launch_bounds__(256)
-flow_skel_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows, uint32_t fmul,
-                 const uint32_t* __restrict__ bnd, const FRec* __restrict__ recs,
-                 uint8_t* __restrict__ rflags, WinItem* __restrict__ wins,
-                 FlowFin* __restrict__ fin, uint32_t* __restrict__ report_count) {
-  extern __shared__ u32x4_t skl[];  // kSkSeg staged records {rxk, seq, len}, then summaries
-  SkSum* sums = reinterpret_cast<SkSum*>(skl + kSkSeg);
-  uint32_t* cst = reinterpret_cast<uint32_t*>(sums + kSkChunks);  // [c]: plain, [kSkChunks + c]: sst
+flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
+                   const uint32_t* __restrict__ bnd, uint32_t bstride, const FRec* __restrict__ recs,
+                   const uint32_t* __restrict__ order, double* __restrict__ lat2,
+                   mgenx_flow_report* __restrict__ reports, uint32_t per_flow,
+                   uint32_t* __restrict__ report_count, uint32_t* __restrict__ report_rec,
+                   CloseRec* __restrict__ closes,
+                   uint32_t lat2_sink) {
+  __shared__ uint32_t scat[4][32];
+  __shared__ uint32_t fo[4][1024];
+  __shared__ double lbuf[4][kLatRounds * kRound];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  // flows to blocks by a multiplicative permutation (fmul coprime with n_flows): blocks go to
-  // the XCDs round robin, and a rank's flows (every 8th) would otherwise all land on one XCD
-  const uint32_t f = (uint32_t)(((uint64_t)blockIdx.x * fmul) % n_flows);
-  const uint32_t b = bnd[f], e = bnd[f + 1u];
+  const uint32_t f = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + wv);
+  if (f >= n_flows) return;
+  const uint32_t b = bnd[(size_t)f * bstride], e = bnd[(size_t)(f + 1u) * bstride];
   if (b >= e) return;
-  // stage records [s, s + kSkSeg) of the flow (every wave), then wait for them (all threads)
-  auto stage = [&](uint32_t s) {
-    const uint32_t ninst = (min(kSkSeg, e - s) + 63u) / 64u;
-    for (uint32_t k = wv; k < ninst; k += 4u) {
-      const FRec* src = recs + min(s + 64u * k + lane, e - 1u);
-      __builtin_amdgcn_global_load_lds((const void*)src, (lds_void_t*)(skl + 64u * k), 16, 0, 0);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  };
-  // chunk c of the segment at s: its summary (one wave)
-  auto summarize = [&](uint32_t s, uint32_t c) {
-    const uint32_t i0 = s + c * kSkChunk, se = min(e, s + kSkSeg);
-    const uint32_t base = skl[c * kSkChunk].z;  // the chunk's first seq
-    uint32_t rhi = 0, rlo = 0;
-    int32_t dmn = INT32_MAX, dmx = INT32_MIN;
-    bool nz = false;
-#pragma unroll
-    for (uint32_t q = 0; q < kSkQ; q++) {
-      const uint32_t o = 64u * q + lane;
-      const u32x4_t v = skl[c * kSkChunk + o];
-      const bool in = i0 + o < se;
-      const bool hi_gt = v.y > rhi || (v.y == rhi && v.x > rlo);
-      rlo = (in && hi_gt) ? v.x : rlo;
-      rhi = (in && hi_gt) ? v.y : rhi;
-      const bool att = in && v.w != 0u;
-      const int32_t d = (int32_t)(v.z - base);
-      dmn = att ? min(dmn, d) : dmn;
-      dmx = att ? max(dmx, d) : dmx;
-      nz |= att;
-    }
-    const uint32_t RH = WRing::wave_max(rhi);
-    const uint32_t RL = WRing::wave_max(rhi == RH ? rlo : 0u);
-    const int32_t DMN = wave_min_i32(dmn), DMX = wave_max_i32(dmx);
-    const bool NZ = __ballot(nz) != 0ull;
-    if (lane == 0) {
-      SkSum sm;
-      sm.rx_lo = RL;
-      sm.rx_hi = RH;
-      sm.base = base;
-      sm.dmin = DMN;
-      sm.dmax = DMX;
-      sm.nz = NZ ? 1u : 0u;
-      sm.rsv0 = sm.rsv1 = 0u;
-      sums[c] = sm;
-    }
-  };
-  // the plain chunks' flag bytes (every wave): set attempts, counted at or past seq_start
-  auto plain_flags = [&](uint32_t s, uint32_t c) {
-    const uint32_t i0 = s + c * kSkChunk, se = min(e, s + kSkSeg), sst_c = cst[kSkChunks + c];
-#pragma unroll
-    for (uint32_t q = 0; q < kSkQ; q++) {
-      const uint32_t o = 64u * q + lane;
-      const u32x4_t v = skl[c * kSkChunk + o];
-      const uint32_t ce = (int32_t)(v.z - sst_c) >= 0 ? (uint32_t)kFCe : 0u;
-      if (i0 + o < se) rflags[i0 + o] = (uint8_t)(v.w != 0u ? (uint32_t)(kFIns | kFDupT) | ce : 0u);
-    }
-  };
-  if (wv != 0) {  // the helper waves: stage, summarize, write the plain chunks' flags
-    for (uint32_t s = b; s < e; s += kSkSeg) {
-      stage(s);
-      const uint32_t nch = (min(kSkSeg, e - s) + kSkChunk - 1u) / kSkChunk;
-      for (uint32_t c = wv; c < nch; c += 4u) summarize(s, c);
-      __syncthreads();  // summaries ready
-      __syncthreads();  // wave 0 has walked the segment
-      for (uint32_t c = wv; c < nch; c += 4u)
-        if (cst[c]) plain_flags(s, c);
-      __syncthreads();  // the segment's LDS may be restaged
-    }
-    return;
-  }
+  for (uint32_t j = lane; j < 1024u; j += 64u) fo[wv][j] = 0xFFFFFFFFu;
   mgenx_flow_state* sp = flows + f;
   const TAdd window = tadd_of(sp->window_size);
-  bool valid = sp->window_valid != 0, hasm = sp->mask_n != 0;
-  uint32_t F = sp->mask_first, L = F;
-  if (hasm) {  // last = first + the highest set relative bit
-    const uint32_t w = lane < 32u ? sp->mask[lane] : 0u;
-    const uint32_t top = w ? lane * 32u + (31u - __clz(w)) : 0u;
-    L = F + (uint32_t)__builtin_amdgcn_readfirstlane((int)WRing::wave_max(top));
-  }
-  uint32_t sst = sp->seq_start;
+  WRing m;
+  m.lane = lane;
+  m.first = sp->mask_first;
+  m.n = sp->mask_n;
+  m.load_relative(sp->mask);
+  if (!m.n) m.w = 0;
+  bool valid = sp->window_valid != 0;
   Tm ws = {sp->win_start_sec, sp->win_start_usec}, we = {sp->win_end_sec, sp->win_end_usec};
   uint64_t wek = tkey(we);
+  uint32_t seq_start = sp->seq_start;
+  uint64_t msg_count = sp->msg_count, byte_count = sp->byte_count, dups = sp->dup_count;
+  double lmin = sp->latency_min, lmax = sp->latency_max;
+  uint64_t nrep = sp->n_reports;
+  const double lsum0 = sp->latency_sum;
   const uint32_t rc0 = report_count[f];
-  uint32_t nwin = 0, ncl = 0;
-  uint32_t win_a = b, win_r = kNoEpoch, cur_es = kNoEpoch;
-  WinItem* wl = wins + ((size_t)b + f);
-  FlowFin* fp = fin + f;
-  if (lane < 32u) fp->mask0[lane] = sp->mask[lane];
-  if (lane == 0) {
-    fp->first0 = sp->mask_first;
-    fp->n0 = sp->mask_n;
-    fp->mc0 = sp->msg_count;
-    fp->bc0 = sp->byte_count;
-    fp->lmin0 = sp->latency_min;
-    fp->lmax0 = sp->latency_max;
-    fp->lsum0 = sp->latency_sum;
-  }
-#if MGENX_DIAG
-  // (diagnostics) cycles of the first walk to finish: fast runs, prefix scans, event records,
-  // total, staging (incl. its wait); counts of fast runs, slow runs, events
-  unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0}, prof_t = __builtin_amdgcn_s_memtime();
-  const unsigned long long prof_t0 = prof_t;
-#define SK_T(slot)                                                         \
-  do {                                                                     \
-    const unsigned long long now_ = __builtin_amdgcn_s_memtime();          \
-    prof[slot] += now_ - prof_t;                                           \
-    prof_t = now_;                                                         \
-  } while (0)
-#define SK_N(slot) prof[slot]++
-#else
-#define SK_T(slot) do {} while (0)
-#define SK_N(slot) do {} while (0)
-#endif
+  uint32_t rcount = rc0, ncl = 0, last_close = 0, last_zr = 0;
 
-  uint32_t seg = b;  // the staged segment's first record
-  auto ld = [&](uint32_t i0, SkLd& r) {  // from LDS (lanes past the flow read stale slots)
-#pragma unroll
-    for (uint32_t q = 0; q < kSkQ; q++) {
-      const u32x4_t v = skl[i0 - seg + 64u * q + lane];
-      r.rxk[q] = (uint64_t)v.y << 32 | v.x;
-      r.seq[q] = v.z;
-      r.len[q] = v.w;
+  // the exact Update of one record (arguments wave-uniform); returns the record's lat'
+  auto update = [&](uint32_t seq, uint64_t rxk, uint32_t msg, double lat, uint32_t pos) -> double {
+    const Tm rx = {(int64_t)(rxk >> 32), (int64_t)(uint32_t)rxk};
+    if (!valid) {  // mgenAnalytic.cpp:80-99
+      valid = true;
+      ws = rx;
+      we = uni_t(tadd(rx, window));
+      wek = tkey(we);
+      if (msg != 0) {
+        m.set(seq);
+        seq_start = seq;
+        msg_count = 1;
+        byte_count = msg;
+        lmin = lmax = lat;
+        return lat;
+      }
+      msg_count = byte_count = 0;
+      lmin = lmax = 0.0;
+      return 0.0;
     }
-  };
-  auto chunk = [&](const uint32_t i0, const SkLd& cur) {
-    const uint32_t cnt = min(kSkChunk, e - i0);
-    uint32_t fl[kSkQ];
-#pragma unroll
-    for (uint32_t q = 0; q < kSkQ; q++) fl[q] = 0u;
-    uint32_t pos = 0;
-    while (pos < cnt) {
-      const int32_t Lr = (int32_t)(L - F);
-      int32_t rel[kSkQ];
-      bool inr[kSkQ], att[kSkQ];
-      int32_t lmn = INT32_MAX, lmx = INT32_MIN;
-      uint64_t evb[kSkQ];  // closes and first messages, per q
-      bool anyev = false;
-#pragma unroll
-      for (uint32_t q = 0; q < kSkQ; q++) {
-        const uint32_t o = 64u * q + lane;
-        inr[q] = (o >= pos) & (o < cnt);
-        att[q] = inr[q] & (cur.len[q] != 0u);
-        rel[q] = (int32_t)(cur.seq[q] - F);
-        lmn = att[q] ? min(lmn, rel[q]) : lmn;
-        lmx = att[q] ? max(lmx, rel[q]) : lmx;
-        const bool spec = inr[q] & (!valid | ((cur.len[q] != 0u) & !hasm));
-        const bool clo = inr[q] & valid & (cur.rxk[q] >= wek);
-        evb[q] = __ballot(spec | clo);
-        anyev |= evb[q] != 0ull;
-      }
-      const bool mask_ops = valid & hasm;
-      const int32_t tmn = min(0, wave_min_i32(lmn)), tmx = max(Lr, wave_max_i32(lmx));
-      if (!anyev && (!mask_ops || (int64_t)tmx - (int64_t)tmn < 1024)) {
-        // the whole run [pos, cnt) is plain: every Set succeeds
-#pragma unroll
-        for (uint32_t q = 0; q < kSkQ; q++) {
-          const uint32_t ce = (int32_t)(cur.seq[q] - sst) >= 0 ? (uint32_t)kFCe : 0u;
-          fl[q] = att[q] ? (uint32_t)(kFIns | kFDupT) | ce : fl[q];
-        }
-        if (mask_ops) {
-          const uint32_t F2 = F + (uint32_t)tmn;
-          L = F + (uint32_t)tmx;
-          F = F2;
-        }
-        SK_T(0);
-        SK_N(5);
-        break;
-      }
-      SK_T(0);
-      SK_N(6);
-      // each record's span from inclusive prefixes (q-major order: the scans of the four
-      // groups, chained by their totals); the first failing Set, close or first message
-      int32_t imn[kSkQ], imx[kSkQ];
-#pragma unroll
-      for (uint32_t q = 0; q < kSkQ; q++) {
-        imn[q] = wave_incl_minmax<false>(att[q] ? rel[q] : INT32_MAX);
-        imx[q] = wave_incl_minmax<true>(att[q] ? rel[q] : INT32_MIN);
-      }
-      int32_t cmn = 0, cmx = Lr;
-      uint32_t ev = kSkChunk;
-#pragma unroll
-      for (uint32_t q = 0; q < kSkQ; q++) {
-        imn[q] = min(cmn, imn[q]);
-        imx[q] = max(cmx, imx[q]);
-        cmn = __builtin_amdgcn_readlane(imn[q], 63);
-        cmx = __builtin_amdgcn_readlane(imx[q], 63);
-        const bool fail = att[q] & mask_ops & ((int64_t)imx[q] - (int64_t)imn[q] >= 1024);
-        const uint64_t eb = evb[q] | __ballot(fail);
-        if (eb && ev == kSkChunk) ev = 64u * q + (uint32_t)__builtin_ctzll(eb);
-      }
-      // the run [pos, ev): plain records
-#pragma unroll
-      for (uint32_t q = 0; q < kSkQ; q++) {
-        const uint32_t o = 64u * q + lane;
-        const uint32_t ce = (int32_t)(cur.seq[q] - sst) >= 0 ? (uint32_t)kFCe : 0u;
-        fl[q] = (att[q] & (o < ev)) ? (uint32_t)(kFIns | kFDupT) | ce : fl[q];
-      }
-      if (ev > pos && mask_ops) {  // the span after the run
-        const uint32_t o1 = ev - 1u, l1 = o1 & 63u, q1 = o1 >> 6;
-        int32_t vmn = imn[0], vmx = imx[0];
-#pragma unroll
-        for (uint32_t q = 1; q < kSkQ; q++) {
-          vmn = q1 == q ? imn[q] : vmn;
-          vmx = q1 == q ? imx[q] : vmx;
-        }
-        const int32_t mn = __builtin_amdgcn_readlane(vmn, (int)l1);
-        const int32_t mx = __builtin_amdgcn_readlane(vmx, (int)l1);
-        const uint32_t F2 = F + (uint32_t)mn;
-        L = F + (uint32_t)mx;
-        F = F2;
-      }
-      SK_T(1);
-      if (ev >= cnt) break;
-      SK_N(7);
-      // the event record, alone (wave-uniform)
-      const uint32_t le = ev & 63u, qe = ev >> 6;
-      uint32_t vs = cur.seq[0], vl = cur.len[0];
-      uint64_t vr = cur.rxk[0];
-#pragma unroll
-      for (uint32_t q = 1; q < kSkQ; q++) {
-        vs = qe == q ? cur.seq[q] : vs;
-        vl = qe == q ? cur.len[q] : vl;
-        vr = qe == q ? cur.rxk[q] : vr;
-      }
-      const uint32_t seq = (uint32_t)__builtin_amdgcn_readlane((int)vs, (int)le);
-      const uint32_t len = (uint32_t)__builtin_amdgcn_readlane((int)vl, (int)le);
-      const uint64_t rxk = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)vr, (int)le) |
-                           (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(vr >> 32), (int)le) << 32;
-      const uint32_t p = i0 + ev;
-      const Tm rx = key_tm(rxk);
-      uint32_t fe = 0;
-      if (!valid) {  // :79-100 (no close test)
-        valid = true;
-        ws = rx;
-        we = uni_t(tadd(rx, window));
-        wek = tkey(we);
-        if (len != 0u) {
-          hasm = true;
-          F = L = seq;
-          sst = seq;
-          fe = kFEstart | kFFa | kFIns;
-          cur_es = p;
+    double latency = 0.0, contrib = 0.0;
+    uint32_t zr = 0;
+    if (msg != 0) {  // :102-178
+      if (m.n) {
+        if (m.test(seq)) {
+          dups++;
+        } else if ((int32_t)(seq - seq_start) < 0) {
+          m.set(seq);
         } else {
-          fe = kFInit0;
-        }
-      } else {
-        if (len != 0u) {
-          if (!hasm) {  // the first actual message (:156-165)
-            hasm = true;
-            F = L = seq;
-            sst = seq;
-            fe = kFEstart | kFFa | kFIns;
-            cur_es = p;
+          if (!m.set(seq)) {  // UnsetBits(first, seq - first), then Set (:120-127)
+            m.unset_from_first(seq - m.first);
+            m.set(seq);
+          }
+          if (1 == msg_count) byte_count = msg;
+          else byte_count += msg;
+          latency = contrib = lat;
+          if (0 == msg_count) {
+            lmin = lmax = latency;
           } else {
-            const int32_t r = (int32_t)(seq - F);
-            const int32_t mn = min(0, r), mx = max((int32_t)(L - F), r);
-            if ((int64_t)mx - (int64_t)mn < 1024) {  // Set succeeds
-              fe = kFIns | kFDupT | ((int32_t)(seq - sst) >= 0 ? kFCe : 0u);
-              const uint32_t F2 = F + (uint32_t)mn;
-              L = F + (uint32_t)mx;
-              F = F2;
-            } else if ((int32_t)(seq - sst) >= 0) {  // counted, Set fails: UnsetBits, Set
-              F = L = seq;
-              fe = kFEstart | kFIns | kFCe;
-              cur_es = p;
-            }  // else precedes the window and Set fails: nothing changes
+            // as value selects (a branch here lets LLVM fold the two stores into one store
+            // through a selected pointer, which sends lmin/lmax to scratch memory)
+            const bool lo = latency < lmin;
+            const bool hi = !lo && latency > lmax;
+            lmin = lo ? latency : lmin;
+            lmax = hi ? latency : lmax;
           }
+          msg_count++;
         }
-        if (rxk >= wek) {  // :168-255
-          const uint32_t seqmax = hasm ? L : sst;
-          if (lane == 0) {
-            WinItem it;
-            it.a = win_a;
-            it.c = p;
-            it.r = win_r;
-            it.fl = (fe & kFFa) ? kWinZr : 0u;
-            it.seqmax = seqmax;
-            it.sst = sst;
-            it.ws = tm_key(ws);
-            wl[nwin] = it;
-          }
-          nwin++;
-          ncl++;
-          sst = seqmax;
-          ws = rx;
-          we = uni_t(tadd(rx, window));
-          wek = tkey(we);
-          win_a = p + 1u;
-          win_r = cur_es;
-          fe |= kFClose;
-        }
+      } else {  // the first actual message (:165-173): sets the sum, `latency` stays 0.0
+        m.clear();
+        m.set(seq);
+        seq_start = seq;
+        byte_count = msg;
+        lmin = lmax = lat;
+        msg_count = 1;
+        contrib = lat;
+        zr = 1;
       }
-#pragma unroll
-      for (uint32_t q = 0; q < kSkQ; q++) fl[q] = (lane == le && q == qe) ? fe : fl[q];
-      pos = ev + 1u;
-      SK_T(2);
     }
-#pragma unroll
-    for (uint32_t q = 0; q < kSkQ; q++)
-      if (64u * q + lane < cnt) rflags[i0 + 64u * q + lane] = (uint8_t)fl[q];
-  };
-  for (; seg < e; seg += kSkSeg) {
-    stage(seg);
-    const uint32_t nch = (min(kSkSeg, e - seg) + kSkChunk - 1u) / kSkChunk;
-    for (uint32_t c = 0; c < nch; c += 4u) summarize(seg, c);
-    __syncthreads();  // summaries ready
-    SK_T(4);
-    for (uint32_t c = 0; c < nch; c++) {
-      const uint32_t i0 = seg + c * kSkChunk;
-      const SkSum sm = sums[c];  // (every lane reads the same: broadcast)
-      const uint64_t mx_rx = (uint64_t)__builtin_amdgcn_readfirstlane((int)sm.rx_hi) << 32 |
-                             (uint32_t)__builtin_amdgcn_readfirstlane((int)sm.rx_lo);
-      const bool nz = __builtin_amdgcn_readfirstlane((int)sm.nz) != 0;
-      bool plain = valid && mx_rx < wek && (!nz || hasm);
-      int64_t mn = 0, mx = (int32_t)(L - F);
-      if (plain && nz) {
-        const int64_t r0 = (int32_t)((uint32_t)__builtin_amdgcn_readfirstlane((int)sm.base) - F);
-        mn = min((int64_t)0, r0 + __builtin_amdgcn_readfirstlane(sm.dmin));
-        mx = max(mx, r0 + __builtin_amdgcn_readfirstlane(sm.dmax));
-        plain = mx - mn < 1024;
+    if (tge(rx, we)) {  // :180-256: report and restart the window
+      const uint32_t seq_max = m.n ? m.get_last() : seq_start;
+      if (rcount < per_flow) {  // a kept report (latency_ave: the tail below)
+      const double duration = tdelta(rx, ws);
+      uint64_t r_count;
+      double r_rate, r_loss, r_min, r_max;
+      if (msg_count == 0) {
+        r_count = 0;
+        r_rate = 0.0;
+        r_loss = 1.0;
+        r_min = r_max = -1.0;
+      } else if (msg_count == 1) {
+        r_count = 1;
+        r_rate = __ddiv_rn((double)byte_count, duration);
+        r_loss = 0.0;
+        r_min = lmin;
+        r_max = lmax;
+      } else {
+        r_count = msg_count - 1;
+        r_rate = __ddiv_rn((double)byte_count, duration);
+        const uint32_t delta = seq_max - seq_start;
+        r_loss = delta <= 1 ? 0.0
+                            : __dsub_rn(1.0, __ddiv_rn((double)msg_count, (double)(delta + 1)));
+        r_min = lmin;
+        r_max = lmax;
       }
       if (lane == 0) {
-        cst[c] = plain ? 1u : 0u;
-        cst[kSkChunks + c] = sst;
-      }
-      if (plain) {
-        if (nz) {
-          const uint32_t F2 = F + (uint32_t)mn;
-          L = F + (uint32_t)mx;
-          F = F2;
-        }
-        SK_T(0);
-        SK_N(5);
-      } else {
-        SkLd B;
-        ld(i0, B);
-        chunk(i0, B);
-      }
-    }
-    __syncthreads();  // the segment is walked
-    for (uint32_t c = 0; c < nch; c += 4u)
-      if (cst[c]) plain_flags(seg, c);
-    __syncthreads();  // the segment's LDS may be restaged
-  }
-  if (lane == 0) {
-    WinItem it;
-    it.a = win_a;
-    it.c = e;
-    it.r = win_r;
-    it.fl = kWinOpen;
-    it.seqmax = it.sst = 0u;
-    it.ws = tm_key(ws);
-    wl[nwin] = it;
-    fp->F = F;
-    fp->hasmask = hasm ? 1u : 0u;
-    fp->nwin = nwin + 1u;
-    fp->ncl = ncl;
-    fp->rc0 = rc0;
-    sp->window_valid = valid ? 1u : 0u;
-    sp->win_start_sec = ws.sec;
-    sp->win_start_usec = ws.usec;
-    sp->win_end_sec = we.sec;
-    sp->win_end_usec = we.usec;
-    sp->seq_start = sst;
-    sp->n_reports += ncl;
-    report_count[f] = rc0 + ncl;
-  }
-#if MGENX_DIAG
-  prof[3] = __builtin_amdgcn_s_memtime() - prof_t0;
-  if (lane == 0 && atomicCAS(&g_skel_claim, 0u, 1u) == 0u)
-    for (int k2 = 0; k2 < 8; k2++) g_skel_prof[k2] = prof[k2];
-#endif
-#undef SK_T
-#undef SK_N
-}
-
-#if MGENX_DIAG
-__device__ unsigned long long g_win_prof[8];
-__device__ unsigned int g_win_claim;
-#endif
-// ---- the windows: one wave (a workgroup of its own) per window, kWinWaves per flow ----
-// The wave walks its window's epoch from the epoch's start (records before the window only
-// insert), chunks of 256 records q-major, two chunks in flight in two register sets.  The
-// window's latency sum -- the one FP64 chain whose rounding depends on record order -- is the
-// wave's, in order, over each chunk's lat' read out lane by lane.  The open window's wave writes
-// the flow's state (the others read the state before the call from FlowFin).
-constexpr uint32_t kWQ = 4;
-constexpr uint32_t kWChunk = 64u * kWQ;
-struct WLd {
-  FRec r[kWQ];
-  uint32_t fl[kWQ];
-};
-__global__ void __launch_bounds__(64)
-flow_win_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
-                const uint32_t* __restrict__ bnd, const FRec* __restrict__ recs,
-                const uint8_t* __restrict__ rflags, const WinItem* __restrict__ wins,
-                const FlowFin* __restrict__ fin, mgenx_flow_report* __restrict__ reports,
-                uint32_t per_flow, uint32_t* __restrict__ report_rec,
-                const uint32_t* __restrict__ order) {
-  __shared__ uint32_t T[1024];
-  const uint32_t lane = threadIdx.x;
-  const uint32_t f = blockIdx.x / kWinWaves, wv = blockIdx.x % kWinWaves;
-  if (f >= n_flows) return;
-  const uint32_t b = bnd[f], e = bnd[f + 1u];
-  if (b >= e) return;
-  mgenx_flow_state* sp = flows + f;
-  const FlowFin* fp = fin + f;
-  const uint32_t nwin = fp->nwin, rc0 = fp->rc0;
-  auto wsync = [] {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  };
-  auto clear_tab = [&] {
-#pragma unroll
-    for (uint32_t j = 0; j < 1024u / 64u; j++) T[64u * j + lane] = kTabEmpty;
-  };
-  const double inf = __builtin_huge_val();
-#if MGENX_DIAG
-  // (diagnostics) cycles of one middle window (k = 1) by phase: setup, insert-only chunks,
-  // duplicate passes, counters, sums, tail, total; chunks
-  unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0}, prof_t = 0, prof_t0 = 0;
-#define WN_T(slot)                                                         \
-  do {                                                                     \
-    const unsigned long long now_ = __builtin_amdgcn_s_memtime();          \
-    prof[slot] += now_ - prof_t;                                           \
-    prof_t = now_;                                                         \
-  } while (0)
-#else
-#define WN_T(slot) do {} while (0)
-#endif
-  for (uint32_t k = wv; k < nwin; k += kWinWaves) {
-#if MGENX_DIAG
-    prof_t = prof_t0 = __builtin_amdgcn_s_memtime();
-#endif
-    const WinItem it = wins[(size_t)b + f + k];
-    const bool open = (it.fl & kWinOpen) != 0u;
-    const uint32_t a = it.a, end = open ? it.c : it.c + 1u;
-    clear_tab();
-    wsync();
-    uint32_t s0 = it.r;
-    if (it.r == kNoEpoch) {  // the call's initial epoch: the stored mask's indices, position 0
-      s0 = b;
-      if (fp->n0) {
-        const uint32_t F0 = fp->first0;
-        uint32_t w = lane < 32u ? fp->mask0[lane] : 0u;
-        while (w) {
-          const uint32_t j = (uint32_t)__builtin_ctz(w);
-          w &= w - 1u;
-          T[(F0 + lane * 32u + j) & 1023u] = 0u;
-        }
-        wsync();
-      }
-    }
-    // the start state: the stored one, or (below) the one the record before the window leaves
-    uint64_t mc = 0, bc = 0;
-    double lmin = 0.0, lmax = 0.0, sum = 0.0;
-    if (a == b) {
-      mc = fp->mc0;
-      bc = fp->bc0;
-      lmin = fp->lmin0;
-      lmax = fp->lmax0;
-      sum = fp->lsum0;
-    }
-    const uint32_t tfrom = a > b ? a - 1u : a;  // records from here take the duplicate test
-    uint32_t kc = 0, ndup = 0, fpos = 0xFFFFFFFFu, fsize = 0;
-    uint64_t ssum = 0;
-    double cmn = inf, cmx = -inf;
-    auto ld = [&](uint32_t i0, WLd& w) {
-#pragma unroll
-      for (uint32_t q = 0; q < kWQ; q++) {
-        const uint32_t p = min(i0 + 64u * q + lane, end - 1u);
-        w.r[q] = recs[p];
-        w.fl[q] = rflags[p];
-      }
-    };
-    auto chunk = [&](const uint32_t i0, const WLd& w) {
-      const uint32_t cnt = min(kWChunk, end - i0);
-      uint32_t fl[kWQ];
-#pragma unroll
-      for (uint32_t q = 0; q < kWQ; q++) fl[q] = 64u * q + lane < cnt ? w.fl[q] : 0u;
-#if MGENX_DIAG
-      prof[7]++;
-#endif
-      if (i0 + cnt <= tfrom) {  // before the tested records: inserts only
-#pragma unroll
-        for (uint32_t q = 0; q < kWQ; q++)
-          if (fl[q] & kFIns) atomicMin(&T[w.r[q].seq & 1023u], i0 + 64u * q + lane + 1u);
-        WN_T(1);
-        return;
-      }
-      bool dup[kWQ] = {false, false, false, false};
-      uint32_t lo = 0;
-      while (lo < cnt) {
-        // the sub-range [lo, hi): up to the next epoch start after lo
-        uint32_t hi = cnt;
-        bool at_es = false;
-#pragma unroll
-        for (uint32_t q = 0; q < kWQ; q++) {
-          const uint32_t o = 64u * q + lane;
-          const bool es = (fl[q] & kFEstart) != 0u;
-          const uint64_t eb = __ballot((o > lo) & es);
-          if (eb) hi = min(hi, 64u * q + (uint32_t)__builtin_ctzll(eb));
-          at_es |= __ballot((o == lo) & es) != 0ull;
-        }
-        if (at_es) {  // an epoch start at lo: the mask is {seq} after it
-          clear_tab();
-          wsync();
-        }
-#pragma unroll
-        for (uint32_t q = 0; q < kWQ; q++) {
-          const uint32_t o = 64u * q + lane;
-          if ((o >= lo) & (o < hi) & ((fl[q] & kFIns) != 0u))
-            atomicMin(&T[w.r[q].seq & 1023u], i0 + o + 1u);
-        }
-        wsync();
-#pragma unroll
-        for (uint32_t q = 0; q < kWQ; q++) {
-          const uint32_t o = 64u * q + lane;
-          const uint32_t tv = T[w.r[q].seq & 1023u];
-          const bool mine = (o >= lo) & (o < hi);
-          dup[q] = mine ? ((fl[q] & kFDupT) != 0u) & (tv < i0 + o + 1u) : dup[q];
-        }
-        wsync();
-        lo = hi;
-      }
-      WN_T(2);
-      // the record before the window: the start state it leaves (:228-242)
-      if (a > b && tfrom >= i0 && tfrom < i0 + cnt) {
-        const uint32_t o = tfrom - i0, l = o & 63u, qq = o >> 6;
-        uint32_t vl = w.r[0].len, vf = fl[0], vd = dup[0];
-        double vt = w.r[0].latency;
-#pragma unroll
-        for (uint32_t q = 1; q < kWQ; q++) {
-          vl = qq == q ? w.r[q].len : vl;
-          vf = qq == q ? fl[q] : vf;
-          vd = qq == q ? (uint32_t)dup[q] : vd;
-          vt = qq == q ? w.r[q].latency : vt;
-        }
-        const uint32_t len = (uint32_t)__builtin_amdgcn_readlane((int)vl, (int)l);
-        const uint32_t fc = (uint32_t)__builtin_amdgcn_readlane((int)vf, (int)l);
-        const bool dc = __builtin_amdgcn_readlane((int)vd, (int)l) != 0;
-        const uint64_t lb = __builtin_bit_cast(uint64_t, vt);
-        const double lat = __builtin_bit_cast(
-            double, (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(lb >> 32), (int)l) << 32 |
-                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)lb, (int)l));
-        const bool counted = (fc & kFCe) && !dc;
-        mc = len ? 1u : 0u;
-        bc = 0u;
-        lmin = lmax = (len != 0u && counted) ? lat : 0.0;
-        sum = counted ? lat : 0.0;  // latency_sum = latency (:236): the record's lat'
-      }
-      // the window's records: counters; a counter restart (first message / first actual
-      // message) precedes every counted record of the window (the mask is empty before it)
-      double lp[kWQ];
-#pragma unroll
-      for (uint32_t q = 0; q < kWQ; q++) {
-        const uint32_t o = 64u * q + lane;
-        const uint32_t p = i0 + o;
-        const bool live = (o < cnt) & (p >= a);
-        const bool counted = live & ((fl[q] & kFCe) != 0u) & !dup[q];
-        const bool fa = live & ((fl[q] & kFFa) != 0u);
-        ndup += (live & dup[q]) ? 1u : 0u;
-        kc += counted ? 1u : 0u;
-        ssum += counted ? w.r[q].len : 0u;
-        fsize = (counted & (p < fpos)) ? w.r[q].len : fsize;
-        fpos = (counted & (p < fpos)) ? p : fpos;
-        cmn = vmin64(cmn, counted ? w.r[q].latency : inf);
-        cmx = vmax64(cmx, counted ? w.r[q].latency : -inf);
-        lp[q] = (counted | fa) ? w.r[q].latency : 0.0;
-      }
-#pragma unroll
-      for (uint32_t q = 0; q < kWQ; q++) {
-        const uint32_t o = 64u * q + lane;
-        const uint64_t rs = __ballot((o < cnt) & (i0 + o >= a) & ((fl[q] & (kFFa | kFInit0)) != 0u));
-        if (rs) {
-          // the last one (a size-0 first message, then the first actual message: one window)
-          const uint32_t l = 63u - (uint32_t)__builtin_clzll(rs);
-          const uint32_t len = (uint32_t)__builtin_amdgcn_readlane((int)w.r[q].len, (int)l);
-          const uint64_t lb = __builtin_bit_cast(uint64_t, w.r[q].latency);
-          const uint32_t llo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)lb, (int)l);
-          const uint32_t lhi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(lb >> 32), (int)l);
-          const double lat = __builtin_bit_cast(double, (uint64_t)lhi << 32 | llo);
-          const uint32_t fv = (uint32_t)__builtin_amdgcn_readlane((int)fl[q], (int)l);
-          const bool fa = (fv & kFFa) != 0u;
-          mc = fa ? 1u : 0u;
-          bc = fa ? len : 0u;
-          lmin = lmax = fa ? lat : 0.0;
-        }
-      }
-      WN_T(3);
-      // the sum, in record order: lane l's lat' of group q is record i0 + 64q + l, read out
-      // lane by lane (the reads do not wait for the sum: only the adds form the chain); the
-      // records outside the window add 0.0, exactly (a latency sum is never -0.0)
-#pragma unroll
-      for (uint32_t q = 0; q < kWQ; q++) {
-        const uint64_t bits = __builtin_bit_cast(uint64_t, lp[q]);
-        const int lo = (int)(uint32_t)bits, hi = (int)(uint32_t)(bits >> 32);
-#pragma unroll
-        for (int l = 0; l < 64; l++) {
-          const double x = __builtin_bit_cast(
-              double, (uint64_t)(uint32_t)__builtin_amdgcn_readlane(hi, l) << 32 |
-                          (uint32_t)__builtin_amdgcn_readlane(lo, l));
-          sum = __dadd_rn(sum, x);
-        }
-      }
-      WN_T(4);
-    };
-    WN_T(0);
-    WLd A, B;
-    ld(s0, A);
-    ld(s0 + kWChunk, B);
-    for (uint32_t i0 = s0; i0 < end; i0 += 2u * kWChunk) {
-      chunk(i0, A);
-      ld(i0 + 2u * kWChunk, A);
-      if (i0 + kWChunk >= end) break;
-      chunk(i0 + kWChunk, B);
-      ld(i0 + 3u * kWChunk, B);
-    }
-    // fold the counted records into the start state (:132-153)
-    const uint32_t K = (uint32_t)__builtin_amdgcn_readfirstlane((int)WRing::wave_sum(kc));
-    const uint32_t D = (uint32_t)__builtin_amdgcn_readfirstlane((int)WRing::wave_sum(ndup));
-    if (K) {
-      const uint32_t slo32 = (uint32_t)ssum;
-      const uint64_t S = (uint64_t)WRing::wave_sum(slo32 & 0xFFFFu) +
-                         ((uint64_t)WRing::wave_sum(slo32 >> 16) << 16) +
-                         ((uint64_t)WRing::wave_sum((uint32_t)(ssum >> 32)) << 32);
-      const uint32_t fmin = WRing::wave_min(fpos);
-      const uint64_t who = __ballot(fpos == fmin);
-      const uint32_t s1 = (uint32_t)__builtin_amdgcn_readlane((int)fsize, (int)__builtin_ctzll(who));
-      const double rmin = WRing::wave_reduce_f64(cmn, inf, [](double x, double y) { return y < x ? y : x; });
-      const double rmax = WRing::wave_reduce_f64(cmx, -inf, [](double x, double y) { return y > x ? y : x; });
-      if (mc >= 2u) bc += S;
-      else if (mc == 1u) bc = S;
-      else bc = K == 1u ? (uint64_t)s1 : S - s1;
-      if (mc == 0u) {
-        lmin = rmin;
-        lmax = rmax;
-      } else {
-        lmin = rmin < lmin ? rmin : lmin;
-        lmax = rmax > lmax ? rmax : lmax;
-      }
-      mc += K;
-    }
-    sum = __builtin_bit_cast(double, (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(
-                                         (int)(uint32_t)__builtin_bit_cast(uint64_t, sum)) |
-                                     (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(
-                                         (int)(uint32_t)(__builtin_bit_cast(uint64_t, sum) >> 32)) << 32);
-    if (D && lane == 0) atomicAdd((unsigned long long*)&sp->dup_count, (unsigned long long)D);
-    if (!open) {
-      const uint32_t slot = rc0 + k;
-      if (slot < per_flow && lane == 0) {
-        const Tm rx = key_tm(recs[it.c].rxk), ws = key_tm(it.ws);
-        const double duration = tdelta(rx, ws);
-        uint64_t r_count;
-        double r_rate, r_loss, r_min, r_max;
-        if (mc == 0) {
-          r_count = 0;
-          r_rate = 0.0;
-          r_loss = 1.0;
-          r_min = r_max = -1.0;
-        } else if (mc == 1) {
-          r_count = 1;
-          r_rate = __ddiv_rn((double)bc, duration);
-          r_loss = 0.0;
-          r_min = lmin;
-          r_max = lmax;
-        } else {
-          r_count = mc - 1;
-          r_rate = __ddiv_rn((double)bc, duration);
-          const uint32_t delta = it.seqmax - it.sst;
-          r_loss = delta <= 1 ? 0.0 : __dsub_rn(1.0, __ddiv_rn((double)mc, (double)(uint32_t)(delta + 1u)));
-          r_min = lmin;
-          r_max = lmax;
-        }
-        const size_t s = (size_t)f * per_flow + slot;
-        mgenx_flow_report* rp = reports + s;
+        const size_t slot = (size_t)f * per_flow + rcount;
+        mgenx_flow_report* rp = reports + slot;
         rp->flow = f;
-        rp->index = slot;
+        rp->index = rcount;
         rp->start_sec = ws.sec;
         rp->start_usec = ws.usec;
         rp->duration = duration;
         rp->msg_count = r_count;
         rp->rate = r_rate;
         rp->loss = r_loss;
-        rp->latency_ave = mc == 0 ? -1.0 : mc == 1 ? sum : __ddiv_rn(sum, (double)mc);
         rp->latency_min = r_min;
         rp->latency_max = r_max;
         rp->rx_sec = rx.sec;
         rp->rx_usec = rx.usec;
-        if (report_rec) report_rec[s] = order[it.c];
+        CloseRec c;
+        c.pos = pos;
+        c.zr = zr;
+        c.mc = msg_count;
+        closes[slot] = c;
+        if (report_rec) report_rec[slot] = order[pos];
       }
-    } else {  // the flow's state after the call: counters and the mask (bit i <-> F + i)
-      const uint32_t F = fp->F;
-      uint32_t word = 0;
-      if (lane < 32u && fp->hasmask) {
-#pragma unroll 8
-        for (uint32_t j = 0; j < 32u; j++)
-          word |= T[(F + lane * 32u + j) & 1023u] != kTabEmpty ? 1u << j : 0u;
       }
-      const uint32_t nset = (uint32_t)__builtin_amdgcn_readfirstlane((int)WRing::wave_sum((uint32_t)__popc(word)));
-      if (lane < 32u) sp->mask[lane] = word;
-      if (lane == 0) {
-        if (fp->hasmask) sp->mask_first = F;
-        sp->mask_n = nset;
-        sp->msg_count = mc;
-        sp->byte_count = bc;
-        sp->latency_min = lmin;
-        sp->latency_max = lmax;
+      rcount++;
+      nrep++;
+      ncl++;
+      last_close = pos;
+      last_zr = zr;
+      ws = rx;
+      we = uni_t(tadd(rx, window));
+      wek = tkey(we);
+      seq_start = seq_max;
+      if (msg != 0) {
+        byte_count = 0;
+        msg_count = 1;
+        lmin = lmax = latency;
+      } else {
+        byte_count = msg_count = 0;
+        lmin = lmax = 0.0;
+      }
+    }
+    return contrib;
+  };
+
+  // Per-lane partials of the bulk runs, folded into the wave-uniform state by flush() before
+  // every exact update and at the end: latency min / max, bytes, and the highest seq - first
+  // (for `last`).  msg_count == 0 (min / max set by the first counted latency, :132-133) means
+  // no counted record is pending.  msg_count == 1 (the byte restart of :128-129) also arises
+  // from a run that counted one record from 0, its size pending: a run or a cheap restart
+  // that meets msg_count == 1 with partials pending flushes first.
+  const double inf = __builtin_huge_val();
+  double pmin = inf, pmax = -inf;
+  uint32_t pbytes = 0, pdmax = 0, prounds = 0;
+  bool dirty = false;
+  auto flush = [&]() {
+    if (!dirty) return;
+    const double rmin = WRing::wave_reduce_f64(pmin, inf, [](double a, double c) {
+      return c < a ? c : a; });
+    const double rmax = WRing::wave_reduce_f64(pmax, -inf, [](double a, double c) {
+      return c > a ? c : a; });
+    lmin = rmin < lmin ? rmin : lmin;
+    lmax = rmax > lmax ? rmax : lmax;
+    const uint64_t lo = WRing::wave_sum(pbytes & 0xFFFFu), hi = WRing::wave_sum(pbytes >> 16);
+    byte_count += lo + (hi << 16);
+    m.last = m.first + max(WRing::wave_max(pdmax), m.last - m.first);
+    pmin = inf;
+    pmax = -inf;
+    pbytes = pdmax = prounds = 0;
+    dirty = false;
+  };
+
+  FRec cur[kUR], nxt[kUR];
+  double latp[kUR];
+  auto ld = [&](uint32_t base, FRec (&r)[kUR]) {  // clamped: lanes past the flow reload its last
+#pragma unroll
+    for (uint32_t q = 0; q < kUR; q++) r[q] = recs[min(base + 64u * q + lane, e - 1u)];
+  };
+
+  // records [k, ev) of the round: a bulk run (every one simple, valid && m.n)
+  auto bulk = [&](uint32_t k, uint32_t ev) {
+    // a run at msg_count == 1 replaces byte_count (:128-129), pending bytes included: a run
+    // before it (the previous round's, or one before a cheap restart) that took msg_count
+    // from 0 to 1 left its one record's size pending -- fold it first
+    if (msg_count == 1 && dirty) flush();
+    if (lane < 32u) scat[wv][lane] = 0u;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // every lane issues every LDS op (non-candidates with a zero bit / the identity), so the
+    // four lookups and the four atomics go out back to back under one wait each, with no
+    // branch per record group
+    bool cand[kUR], inring[kUR], clash = false;
+    uint32_t bit[kUR], word[kUR], old[kUR];
+#pragma unroll
+    for (uint32_t q = 0; q < kUR; q++) {
+      const uint32_t p = 64u * q + lane;
+      cand[q] = p >= k && p < ev && cur[q].len != 0u;
+      bit[q] = cand[q] ? 1u << (cur[q].seq & 31u) : 0u;
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < kUR; q++)
+      word[q] = (uint32_t)__shfl((int)m.w, (int)((cur[q].seq >> 5) & 31u));
+#pragma unroll
+    for (uint32_t q = 0; q < kUR; q++) old[q] = atomicOr(&scat[wv][(cur[q].seq >> 5) & 31u], bit[q]);
+#pragma unroll
+    for (uint32_t q = 0; q < kUR; q++) {
+      inring[q] = (word[q] >> (cur[q].seq & 31u)) & 1u;
+      clash |= (old[q] & bit[q]) != 0u;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    bool indup[kUR];
+#pragma unroll
+    for (uint32_t q = 0; q < kUR; q++) indup[q] = false;
+    if (__ballot(clash)) {  // two records of the run share a sequence number: the first is new
+#pragma unroll
+      for (uint32_t q = 0; q < kUR; q++)
+        atomicMin(&fo[wv][cur[q].seq & 1023u], cand[q] ? 64u * q + lane : 0xFFFFFFFFu);
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      uint32_t fv[kUR];
+#pragma unroll
+      for (uint32_t q = 0; q < kUR; q++) fv[q] = fo[wv][cur[q].seq & 1023u];
+#pragma unroll
+      for (uint32_t q = 0; q < kUR; q++) indup[q] = cand[q] && fv[q] < 64u * q + lane;
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (uint32_t q = 0; q < kUR; q++)
+        if (cand[q]) fo[wv][cur[q].seq & 1023u] = 0xFFFFFFFFu;
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
+    // per record group: three ballots and branch-free per-lane partials (no branch per group:
+    // a select the compiler turns into an exec-mask branch costs more than the select)
+    uint32_t n_cnt = 0, n_cand = 0, n_new = 0;
+    uint64_t cms[kUR];
+#pragma unroll
+    for (uint32_t q = 0; q < kUR; q++) {
+      // (bitwise: && evaluates its right side under an exec mask, a branch)
+      const bool nw = cand[q] & !inring[q] & !indup[q];
+      const bool counted = nw & ((int32_t)(cur[q].seq - seq_start) >= 0);
+      cms[q] = __ballot(counted);
+      n_cnt += (uint32_t)__popcll(cms[q]);
+      n_new += (uint32_t)__popcll(__ballot(nw));
+      n_cand += (uint32_t)__popcll(__ballot(cand[q]));
+      const double lat = cur[q].latency;
+      pbytes += counted ? cur[q].len : 0u;
+      // min / max (latencies are never NaN or -0, so v_min / v_max equal the compare-selects;
+      // fmin would canonicalise its operands first)
+      pmin = vmin64(pmin, counted ? lat : inf);
+      pmax = vmax64(pmax, counted ? lat : -inf);
+      pdmax = max(pdmax, cand[q] ? cur[q].seq - m.first : 0u);
+      latp[q] = counted ? lat : latp[q];
+    }
+    const uint32_t n_dup = n_cand - n_new;
+    if (n_cnt) {
+      // :128-129: a counted record arriving at msg_count == 1 replaces byte_count by its size
+      // (nothing is pending then, see above): at 1 the run's bytes replace it; at 0 the first
+      // counted record adds and the second replaces, so the first one's size drops out
+      if (msg_count == 1) byte_count = 0;
+      if (msg_count == 0) {
+        if (n_cnt >= 2) {  // the run's first counted record: its size
+          uint32_t len1 = 0;
+          bool got = false;
+#pragma unroll
+          for (uint32_t q = 0; q < kUR; q++) {
+            if (!got && cms[q]) {
+              len1 = (uint32_t)__builtin_amdgcn_readlane((int)cur[q].len, (int)__builtin_ctzll(cms[q]));
+              got = true;
+            }
+          }
+          byte_count -= len1;  // byte_count is 0 here; the flush adds it back
+        }
+        lmin = inf;  // :132-133: the first counted latency sets both
+        lmax = -inf;
+      }
+      msg_count += n_cnt;
+    }
+    dups += n_dup;
+    m.n += n_new;
+    if (lane < 32u) m.w |= scat[wv][lane];
+    __builtin_amdgcn_wave_barrier();
+    dirty = true;
+  };
+
+  ld(b, cur);
+  ld(b + kRound, nxt);
+#if MGENX_DIAG
+  const bool prof_on = blockIdx.x == 0 && wv == 0;
+  unsigned long long prof[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
+                     prof_t = __builtin_amdgcn_s_memtime();
+  const unsigned long long prof_t0 = prof_t;
+  bool was_rst = false;
+#endif
+  for (uint32_t i0 = b; i0 < e; i0 += kRound) {
+    FRec nx2[kUR];
+    ld(i0 + 2u * kRound, nx2);
+    const uint32_t cnt = min(kRound, e - i0);
+#if MGENX_DIAG
+    prof[4]++;
+#endif
+#pragma unroll
+    for (uint32_t q = 0; q < kUR; q++) latp[q] = 0.0;
+    uint32_t k = 0;
+    while (k < cnt) {
+      uint32_t ev = k;  // the first record from k that takes the exact update
+      if (valid && m.n) {
+        ev = cnt;
+#pragma unroll
+        for (uint32_t q = 0; q < kUR; q++) {
+          const uint32_t p = 64u * q + lane;
+          const bool simple = (cur[q].rxk < wek) & ((cur[q].len == 0u) | (cur[q].seq - m.first < kDepth));
+          const uint64_t ns = __ballot((p >= k) & (p < cnt) & !simple);  // (bitwise: no exec branches)
+          if (ns) ev = min(ev, 64u * q + (uint32_t)__builtin_ctzll(ns));
+        }
+        UPD_T(0);
+        if (ev > k) {
+          bulk(k, ev);
+#if MGENX_DIAG
+          prof[6]++;
+#endif
+        }
+        UPD_T(1);
+      }
+      if (ev >= cnt) break;
+#if MGENX_DIAG
+      prof[5]++;
+#endif
+      const uint32_t q = ev >> 6, l = ev & 63u;
+      uint32_t seq = 0, len = 0, rlo = 0, rhi = 0, llo = 0, lhi = 0;
+#pragma unroll
+      for (uint32_t qq = 0; qq < kUR; qq++) {  // static indices (a dynamic one goes to scratch)
+        const uint32_t s_ = (uint32_t)__builtin_amdgcn_readlane((int)cur[qq].seq, (int)l);
+        const uint32_t n_ = (uint32_t)__builtin_amdgcn_readlane((int)cur[qq].len, (int)l);
+        const uint32_t a_ = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)cur[qq].rxk, (int)l);
+        const uint32_t b_ = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(cur[qq].rxk >> 32), (int)l);
+        const uint64_t lb = __builtin_bit_cast(uint64_t, cur[qq].latency);
+        const uint32_t c_ = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)lb, (int)l);
+        const uint32_t d_ = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(lb >> 32), (int)l);
+        seq = qq == q ? s_ : seq;
+        len = qq == q ? n_ : len;
+        rlo = qq == q ? a_ : rlo;
+        rhi = qq == q ? b_ : rhi;
+        llo = qq == q ? c_ : llo;
+        lhi = qq == q ? d_ : lhi;
+      }
+      const uint64_t rxk = (uint64_t)rhi << 32 | rlo;
+      const double lat = __builtin_bit_cast(double, (uint64_t)lhi << 32 | llo);
+      double lp;
+      if (valid && m.n && len != 0u && rxk < wek && (int32_t)(seq - m.first) >= (int32_t)kDepth &&
+          (int32_t)(seq - seq_start) >= 0) {
+        // a mask restart, the common exact step (:118-127): not a duplicate (outside the span),
+        // counted, Set fails, UnsetBits clears every set index (all below seq) -> mask {seq}.
+        // No flush: the pending bytes / min / max stay pending (order-free); only the pending
+        // `last` partials, relative to the old first, are dropped (last = seq now).
+        if (msg_count <= 1 && dirty) flush();  // (the replace at 1 covers pending bytes)
+        pdmax = 0;
+        m.w = lane == ((seq >> 5) & 31u) ? (1u << (seq & 31u)) : 0u;
+        m.first = m.last = seq;
+        m.n = 1;
+        if (msg_count == 1) byte_count = len;  // (flushed above: nothing pending)
+        else byte_count += len;
+        if (msg_count == 0) {
+          lmin = lmax = lat;
+        } else {
+          lmin = lat < lmin ? lat : lmin;
+          lmax = lat > lmax ? lat : lmax;
+        }
+        msg_count++;
+        lp = lat;
+#if MGENX_DIAG
+        was_rst = true;
+#endif
+      } else {
+        flush();
+        lp = update(seq, rxk, len, lat, i0 + ev);
+#if MGENX_DIAG
+        was_rst = false;
+#endif
+      }
+#pragma unroll
+      for (uint32_t qq = 0; qq < kUR; qq++) latp[qq] = (qq == q && lane == l) ? lp : latp[qq];
+      k = ev + 1u;
+#if MGENX_DIAG
+      if (prof_on) {
+        const unsigned long long now_ = __builtin_amdgcn_s_memtime();
+        prof[was_rst ? 8 : 2] += now_ - prof_t;
+        prof[9] += was_rst ? 1 : 0;
+        prof_t = now_;
+      }
+#endif
+    }
+    // lat' leaves through LDS, kLatRounds rounds at a time: gfx950 counts stores in vmcnt, so
+    // a round's stores would hold up the waits for the next rounds' record loads until they
+    // complete (45% of the kernel's cycles when every round stored)
+    const uint32_t ro = (uint32_t)(((i0 - b) / kRound) % kLatRounds);
+#pragma unroll
+    for (uint32_t q = 0; q < kUR; q++) lbuf[wv][ro * kRound + 64u * q + lane] = latp[q];
+    if (ro == kLatRounds - 1u || i0 + kRound >= e) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const uint32_t bs = i0 - ro * kRound, bn = i0 + cnt - bs;  // the batch's records
+#pragma unroll
+      for (uint32_t k2 = 0; k2 < kLatRounds * kUR; k2++) {
+        const uint32_t p = 64u * k2 + lane;  // branch-free: lanes past it write the sink slots
+        lat2[p < bn ? bs + p : lat2_sink + lane] = lbuf[wv][p];
+      }
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < kUR; q++) {
+      cur[q] = nxt[q];
+      nxt[q] = nx2[q];
+    }
+    if (++prounds == 4096u) flush();  // per-lane bytes stay below 2^32
+    UPD_T(3);
+  }
+#if MGENX_DIAG
+  if (prof_on && lane == 0) {
+    prof[7] = __builtin_amdgcn_s_memtime() - prof_t0;
+    for (int k2 = 0; k2 < 10; k2++) g_upd_prof[k2] = prof[k2];
+  }
+#endif
+
+  flush();
+  m.store_relative(sp->mask);
+  if (lane == 0) {
+    sp->mask_first = m.first;
+    sp->mask_n = m.n;
+    sp->window_valid = valid ? 1u : 0u;
+    sp->win_start_sec = ws.sec;
+    sp->win_start_usec = ws.usec;
+    sp->win_end_sec = we.sec;
+    sp->win_end_usec = we.usec;
+    sp->seq_start = seq_start;
+    sp->msg_count = msg_count;
+    sp->byte_count = byte_count;
+    sp->dup_count = dups;
+    sp->latency_min = lmin;
+    sp->latency_max = lmax;
+    sp->n_reports = nrep;
+    report_count[f] = rcount;
+  }
+
+  // ---- the latency sums, on this wave: each window's in-order FP64 sum of lat' (lane t takes
+  // window t: [lo, hi] below), staged through this
+  // wave's lbuf.  The flow's lat' and closes were just written by this wave: every store is
+  // waited for, and the loads read past L1 (agent scope) from the XCD's L2, where they sit --
+  // no separate pass re-reading lat' from HBM.
+  __builtin_amdgcn_s_waitcnt(0);
+  double* piece = &lbuf[wv][0];
+  constexpr uint32_t kPiece = kLatRounds * kRound;
+  const uint32_t kept = min(rcount, per_flow);
+  const uint32_t nslots = kept > rc0 ? kept - rc0 : 0u;
+  const uint32_t nwin = nslots + 1u;  // + the open window
+  const CloseRec* cl = closes + (size_t)f * per_flow;
+  auto ld32 = [](const uint32_t* q) {
+    return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  for (uint32_t w0 = 0; w0 < nwin; w0 += 64u) {
+    const uint32_t t = w0 + lane;
+    const bool has = t < nwin;
+    uint32_t lo = 0, hi = 0;
+    double sum = 0.0;
+    if (has) {
+      if (t < nslots) {
+        const uint32_t slot = rc0 + t;
+        hi = ld32(&cl[slot].pos);
+        if (t == 0) {
+          lo = b;
+          sum = lsum0;
+        } else {
+          lo = ld32(&cl[slot - 1u].pos) + (ld32(&cl[slot - 1u].zr) ? 1u : 0u);
+        }
+      } else {
+        hi = e - 1u;
+        if (ncl) {
+          lo = last_close + (last_zr ? 1u : 0u);
+        } else {
+          lo = b;
+          sum = lsum0;
+        }
+      }
+    }
+    const uint32_t nl = min(nwin - w0, 64u);
+    const uint32_t a0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)lo);
+    const uint32_t z0 = (uint32_t)__builtin_amdgcn_readlane((int)hi, (int)(nl - 1u));
+    for (uint32_t p0 = a0; p0 <= z0 && p0 >= a0; p0 += kPiece) {
+      const uint32_t pend = min(z0 + 1u, p0 + kPiece);
+      const bool mine = has && lo <= hi && lo < pend && hi >= p0;
+      if (!__ballot(mine)) continue;
+      for (uint32_t j = lane; j < pend - p0; j += 64u)
+        piece[j] = __hip_atomic_load(&lat2[p0 + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (mine) {
+        const uint32_t ja = max(lo, p0) - p0, jz = min(hi + 1u, pend) - p0;
+        uint32_t j = ja;
+        for (; j + 8u <= jz; j += 8u) {
+          double x[8];
+#pragma unroll
+          for (int u = 0; u < 8; u++) x[u] = piece[j + u];
+#pragma unroll
+          for (int u = 0; u < 8; u++) sum = __dadd_rn(sum, x[u]);
+        }
+        for (; j < jz; j++) sum = __dadd_rn(sum, piece[j]);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (has) {
+      if (t < nslots) {
+        const uint32_t slot = rc0 + t;
+        const uint64_t mc = __hip_atomic_load(&cl[slot].mc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        reports[(size_t)f * per_flow + slot].latency_ave =
+            mc == 0 ? -1.0 : mc == 1 ? sum : __ddiv_rn(sum, (double)mc);
+      } else {
         sp->latency_sum = sum;
       }
     }
-    wsync();
-#if MGENX_DIAG
-    WN_T(5);
-    prof[6] = __builtin_amdgcn_s_memtime() - prof_t0;
-    if (k == 1 && lane == 0 && atomicCAS(&g_win_claim, 0u, 1u) == 0u)
-      for (int k2 = 0; k2 < 8; k2++) g_win_prof[k2] = prof[k2];
-    for (int k2 = 0; k2 < 8; k2++) prof[k2] = 0;
-#endif
   }
-#undef WN_T
 }
+
 
 // ---- ordering the records by flow, stably: a counting sort (flow count < kCountBins) --
 // The output is every record as the 24-B FRec the update reads, flow after flow, receive order
@@ -1441,20 +1174,11 @@ static double quantized_window(double value) {
 
 #if MGENX_DIAG
 extern "C" int mgenx_diag_seg_prof(unsigned long long* out, int n) {
-  if (out && n == 8) {  // flow_skel_kernel's phase cycles (g_skel_prof; the claim reset)
-    const unsigned int zero = 0;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_skel_prof), 64) != hipSuccess) return MGENX_EDEVICE;
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_skel_claim), &zero, 4) == hipSuccess ? MGENX_OK
-                                                                               : MGENX_EDEVICE;
-  }
-  if (out && n == 12) {  // flow_win_kernel's phase cycles (g_win_prof; the claim reset)
-    const unsigned int zero = 0;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_win_prof), 64) != hipSuccess) return MGENX_EDEVICE;
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_win_claim), &zero, 4) == hipSuccess ? MGENX_OK
-                                                                              : MGENX_EDEVICE;
-  }
   if (out && n == 16)  // flow_order_kernel's phase cycles (g_ord_prof, 8 entries)
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ord_prof), 64) == hipSuccess ? MGENX_OK
+                                                                              : MGENX_EDEVICE;
+  if (out && n == 10)  // flow_update_kernel's phase cycles (g_upd_prof)
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_upd_prof), 80) == hipSuccess ? MGENX_OK
                                                                               : MGENX_EDEVICE;
   return MGENX_EINVAL;
 }
@@ -1512,12 +1236,12 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
   const bool want_order = report_rec != nullptr;
   const size_t nb = a256((size_t)n * 4), rb = a256((size_t)n * sizeof(FRec));
   const size_t hb = a256(n_hist * 4), bb = a256((size_t)bins * 4);
-  const size_t fb = a256((size_t)n + 256), wb = a256(((size_t)n + n_flows) * sizeof(WinItem));
-  const size_t xb = a256((size_t)n_flows * sizeof(FlowFin));
-  // both: records (sorted), record flags, windows, per-flow results
+  const size_t lb = a256((size_t)(n + 64) * 8);
+  const size_t cb = a256((size_t)n_flows * per_flow * sizeof(CloseRec));
+  // both: records (sorted), lat', closes
   // counting: hist, start, order (report_rec only), row totals
   // radix:    keys_in, keys_out, vals_in, order, bounds, cub
-  const size_t common = rb + fb + wb + xb;
+  const size_t common = rb + lb + cb;
   const size_t need = common + (sort_path == 0 ? 2 * hb + (want_order ? nb : 0) + a256(cub_bytes)
                                                : 4 * nb + bb + a256(cub_bytes));
   if (ws.bytes < need) {
@@ -1533,10 +1257,10 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
   char* p = static_cast<char*>(ws.mem);
   auto take = [&](size_t b) { char* q = p; p += b; return q; };
   FRec* recs = (FRec*)take(rb);
-  uint8_t* rflags = (uint8_t*)take(fb);
-  WinItem* wins = (WinItem*)take(wb);
-  FlowFin* fin = (FlowFin*)take(xb);
+  double* lat2 = (double*)take(lb);
+  CloseRec* closes = (CloseRec*)take(cb);
   const uint32_t* bnd;
+  uint32_t bstride;
   uint32_t* order = nullptr;
   hipError_t e;
   if (sort_path == 0) {
@@ -1584,6 +1308,7 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
       hipLaunchKernelGGL(flow_order_kernel<false>, dim3(grid), dim3(64 * kSortWaves), lds, stream,
                          flow_idx, n, n_flows, n_tiles, start, src, recs, order, key_bits, oseqw);
     bnd = start;  // tile 0's row: flow k starts at start[k]
+    bstride = 1;
   } else {
     uint32_t* keys_in = (uint32_t*)take(nb);
     uint32_t* keys_out = (uint32_t*)take(nb);
@@ -1604,22 +1329,12 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
     hipLaunchKernelGGL(flow_gather_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, order,
                        d_bnd, n_flows, src, recs);
     bnd = d_bnd;
+    bstride = 1;
   }
   if (sabl) return MGENX_OK;  // timing study: ordering only
-  e = set_max_lds((const void*)flow_skel_kernel, (int)kSkLds);
-  if (e != hipSuccess) {
-    snprintf(err, errn, "flow_reduce skeleton: %s", hipGetErrorString(e));
-    return MGENX_EDEVICE;
-  }
-  // block -> flow multiplier: odd, near 0.618 n_flows, coprime with n_flows (a permutation)
-  uint32_t fmul = n_flows > 2 ? (uint32_t)(0.6180339887 * n_flows) | 1u : 1u;
-  auto gcd = [](uint32_t x, uint32_t y) { while (y) { const uint32_t t = x % y; x = y; y = t; } return x; };
-  while (fmul > 1 && gcd(fmul, n_flows) != 1) fmul -= 2;
-  if (fmul == 0) fmul = 1;
-  hipLaunchKernelGGL(flow_skel_kernel, dim3(n_flows), dim3(256), kSkLds, stream, flows, n_flows,
-                     fmul, bnd, recs, rflags, wins, fin, report_count);
-  hipLaunchKernelGGL(flow_win_kernel, dim3(n_flows * kWinWaves), dim3(64), 0, stream, flows,
-                     n_flows, bnd, recs, rflags, wins, fin, reports, per_flow, report_rec, order);
+  hipLaunchKernelGGL(flow_update_kernel, dim3((n_flows + 3) / 4), dim3(256), 0, stream, flows,
+                     n_flows, bnd, bstride, recs, order, lat2, reports, per_flow, report_count,
+                     report_rec, closes, n);
   e = hipGetLastError();
   if (e != hipSuccess) {
     snprintf(err, errn, "flow_reduce: %s", hipGetErrorString(e));
