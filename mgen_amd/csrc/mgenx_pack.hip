@@ -529,6 +529,11 @@ pack_kernel(PackParams p) {
       m.state = (m.ret ? (uint32_t)m.hdr : 0xFFFFu) | (flags & 0xffu) << 16;
     }
     S_META[lane] = m;
+    if constexpr (kTcp) {  // the batch qualifies for the big-buffer walk (read a stage later)
+      const bool tok = i >= p.n || (m.pend <= (uint32_t)kImg && (m.ret == 0u || m.ret >= 1024u));
+      const bool tall = __all(tok);
+      if (lane == 0) s_joint[buf][slot] = tall ? 1u : 0u;
+    }
     if constexpr (!kTcp) {  // for the joint store: the trailer word, the batch's verdict
       s_tw[buf][slot * 64 + lane] = m.trailer_on == 1 ? bswap32(m.trailer) : 0u;
       const bool jok = i >= p.n || (m.ret == (uint32_t)p.stride && m.pend <= (uint32_t)kImg);
@@ -583,19 +588,36 @@ pack_kernel(PackParams p) {
     // unit, each wave instruction 1 KB of contiguous fragment.  (The general walk below spends
     // most of its instructions per unit on finding the unit's record and on the fill / payload
     // / trailer cases.)
+    // The group's records go to its store waves (and helpers) interleaved -- wave w of nco
+    // takes records w, w + nco, ... of the group in slab order -- so the workgroup's stores
+    // stay inside nco neighbouring records instead of one stream per batch 1 MB apart (when
+    // every batch of the group qualifies; else each wave walks its own batch).
+    uint32_t co_nw = 0;
+    if (kTcp && p.frag_len && !rf) {
+      const uint64_t gc = b / kProd;
+      co_nw = (uint32_t)min((uint64_t)kProd, n_batches - gc * kProd);
+#pragma unroll
+      for (int k = 0; k < kProd; k++)
+        if ((uint32_t)k < co_nw && !s_joint[buf][k]) co_nw = 0;
+    }
     if (kTcp && p.frag_len && !rf && nv > 0 &&
-        __all(!has || (m.pend <= (uint32_t)kImg && (m.ret == 0u || m.ret >= 1024u)))) {
+        (co_nw > 0 || __all(!has || (m.pend <= (uint32_t)kImg && (m.ret == 0u || m.ret >= 1024u))))) {
       if (MGENX_DIAG && variant == 1) goto stage_end;  // (diagnostics: no store phase)
       const bool fck = p.frag_ck != 0;
       // with a helper (no group built this stage) the two waves take alternate records, each
       // with its own boundary table in LDS
       const uint32_t rstep = prod_live ? 1u : 2u;
       uint32_t* const bst = &s_pre[slot][helper ? 32 : 0];
-      for (uint32_t rr = helper ? 1u : 0u; rr < nv; rr += rstep) {
-        const PackMeta R = S_META[rr];
+      const uint64_t g0 = (b / kProd) * kProd;  // the group's first batch
+      const uint32_t co_n = co_nw ? (uint32_t)min((uint64_t)co_nw * 64u, (uint64_t)p.n - (g0 << 6)) : nv;
+      const uint32_t co_step = co_nw ? co_nw * rstep : rstep;
+      const uint32_t co_first = co_nw ? (uint32_t)slot + (helper ? co_nw : 0u) : (helper ? 1u : 0u);
+      for (uint32_t gr = co_first; gr < co_n; gr += co_step) {
+        const uint32_t kq = co_nw ? gr >> 6 : (uint32_t)slot, rr = co_nw ? gr & 63u : gr;
+        const PackMeta R = s_meta[buf][kq][rr];
         if (R.ret == 0u) continue;
         const TcpReps reps = tcp_reps(R.frag, R.ret, fck);
-        const uint8_t* rimg = &S_IMG[rr * kImg];
+        const uint8_t* rimg = &s_img[buf][kq][rr * kImg];
         const uint32_t Fe = R.frag ? R.frag : R.ret;       // the fragment's end
         const uint32_t T = R.trailer_on ? Fe - 4u : Fe;     // where its trailer starts
         const uint32_t be = bswap32(R.trailer);             // trailer bytes in memory order
@@ -612,7 +634,23 @@ pack_kernel(PackParams p) {
         uint8_t* const rbase = p.slab + R.off;
         const uint32_t nu = (Fe + 15u) >> 4;
         uint32_t kb = 0, bcur = 0, bnext = bst[1];
-        for (uint32_t u = (uint32_t)lane; u < nu; u += 64u) {
+        // the pass's buffer (wave-uniform): a pass of 64 units that lies in one buffer past
+        // its image and before the trailer is zeros -- stored as such with no per-unit walk
+        // (config 5: 13 of each record's 16 passes)
+        uint32_t ukb = 0, ubc = 0, ubn = bnext;
+        for (uint32_t u0 = 0; u0 < nu; u0 += 64u) {
+          const uint32_t x0 = u0 << 4;
+          while (x0 >= ubn && ukb + 1u < nb) {
+            ukb++;
+            ubc = ubn;
+            ubn = bst[ukb + 1];
+          }
+          if (x0 - ubc >= (uint32_t)kImg && x0 + 1024u <= min(ubn, T)) {
+            stu128(rbase + x0 + 16u * (uint32_t)lane, u32x4_t{0u, 0u, 0u, 0u});
+            continue;
+          }
+          const uint32_t u = u0 + (uint32_t)lane;
+          if (u >= nu) continue;
           const uint32_t x = u << 4;
           while (x >= bnext && kb + 1u < nb) {
             kb++;
