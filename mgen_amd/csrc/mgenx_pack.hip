@@ -249,6 +249,89 @@ pack_kernel(PackParams p) {
     }
     return true;
   };
+  // The big-TCP-buffer walk of one record (batch kq, record rr of LDS buffer cb; bst: the
+  // calling wave's boundary table in LDS): the 64 lanes walk the whole FRAGMENT [0, Fe) in
+  // 16-byte units, consecutive lanes on consecutive units -- P, then each later buffer k
+  // (P[0 .. cnt_k) again from its start), then the trailer.  A pass of 64 units inside one
+  // buffer past its image and before the trailer is zeros, stored with no per-unit walk.
+  auto big_rec = [&](int cb, uint32_t kq, uint32_t rr, uint32_t* bst) {
+      const PackMeta R = s_meta[cb][kq][rr];
+      if (R.ret == 0u) return;
+      const TcpReps reps = tcp_reps(R.frag, R.ret, p.frag_ck != 0);
+      const uint8_t* rimg = &s_img[cb][kq][rr * kImg];
+      const uint32_t Fe = R.frag ? R.frag : R.ret;       // the fragment's end
+      const uint32_t T = R.trailer_on ? Fe - 4u : Fe;     // where its trailer starts
+      const uint32_t be = bswap32(R.trailer);             // trailer bytes in memory order
+      // buffer starts: 0 (P), then each later buffer's; nb buffers, bst[nb] = Fe
+      uint32_t nb = 1;
+#pragma unroll
+      for (int k = 0; k < kMaxRep; k++) nb += reps.start[k] ? 1u : 0u;
+      if (lane == 0) bst[0] = 0u;
+#pragma unroll
+      for (int k = 0; k < kMaxRep; k++)
+        if (lane == k + 1 && reps.start[k]) bst[k + 1] = reps.start[k];
+      if (lane == 0) bst[nb] = Fe;
+      wave_sync();
+      uint8_t* const rbase = p.slab + R.off;
+      const uint32_t nu = (Fe + 15u) >> 4;
+      uint32_t kb = 0, bcur = 0, bnext = bst[1];
+      // the pass's buffer (wave-uniform): a pass of 64 units that lies in one buffer past
+      // its image and before the trailer is zeros -- stored as such with no per-unit walk
+      // (config 5: 13 of each record's 16 passes)
+      uint32_t ukb = 0, ubc = 0, ubn = bnext;
+      for (uint32_t u0 = 0; u0 < nu; u0 += 64u) {
+        const uint32_t x0 = u0 << 4;
+        while (x0 >= ubn && ukb + 1u < nb) {
+          ukb++;
+          ubc = ubn;
+          ubn = bst[ukb + 1];
+        }
+        if (x0 - ubc >= (uint32_t)kImg && x0 + 1024u <= min(ubn, T)) {
+          stu128(rbase + x0 + 16u * (uint32_t)lane, u32x4_t{0u, 0u, 0u, 0u});
+          continue;
+        }
+        const uint32_t u = u0 + (uint32_t)lane;
+        if (u >= nu) continue;
+        const uint32_t x = u << 4;
+        while (x >= bnext && kb + 1u < nb) {
+          kb++;
+          bcur = bnext;
+          bnext = bst[kb + 1];
+        }
+        const uint32_t pos = x - bcur;
+        const u32x4_t iv = *reinterpret_cast<const u32x4_t*>(rimg + min(pos, (uint32_t)kImg - 16u));
+        uint32_t v[4] = {iv.x, iv.y, iv.z, iv.w};
+        if (pos >= (uint32_t)kImg) v[0] = v[1] = v[2] = v[3] = 0u;  // (past pend: zero fill)
+        if ((pos & 15u) != 0u || x + 16u > min(bnext, T)) {
+          // a unit across a boundary or off the 16-byte grid of its buffer: byte by byte
+          uint32_t kk = kb, bc = bcur, bn = bnext;
+#pragma unroll
+          for (int j = 0; j < 16; j++) {
+            const uint32_t xb = x + (uint32_t)j;
+            uint32_t byte = 0u;
+            if (xb >= T) {
+              byte = xb < Fe ? (be >> (8u * (xb - T))) & 0xffu : 0u;
+            } else {
+              while (xb >= bn) {
+                kk++;
+                bc = bn;
+                bn = bst[kk + 1];
+              }
+              const uint32_t q = xb - bc;
+              byte = q < (uint32_t)kImg ? rimg[q] : 0u;
+            }
+            if ((j & 3) == 0) v[j >> 2] = 0u;
+            v[j >> 2] |= byte << (8 * (j & 3));
+          }
+        }
+        if (x + 16u <= Fe) {
+          stu128(rbase + x, u32x4_t{v[0], v[1], v[2], v[3]});
+        } else {
+          st_part(rbase + x, v, Fe - x);
+        }
+      }
+      wave_sync();  // (the boundary table is rewritten for the next record)
+  };
   // stage s: producers build group blockIdx.x + s * gridDim.x into buffer s & 1, consumers
   // store group blockIdx.x + (s - 1) * gridDim.x from buffer (s - 1) & 1 (block-uniform)
   for (uint64_t s = 0;; s++) {
@@ -273,7 +356,7 @@ pack_kernel(PackParams p) {
     }
     if (!(builds ? prod_live : cons_live) || b >= n_batches) goto stage_end;
     if (builds) {
-    if (!kTcp && slot == 0 && lane == 0) s_tick[buf] = 0u;  // (this buffer's store is next stage)
+    if (slot == 0 && lane == 0) s_tick[buf] = 0u;  // (this buffer's store is next stage)
     uint8_t* img = S_IMG + lane * kImg;
     // the image slot starts as zeros: the bytes past pend read as the record's zero fill, so
     // the aligned-stride store loop loads image units without masking them
@@ -533,6 +616,25 @@ pack_kernel(PackParams p) {
       const bool tok = i >= p.n || (m.pend <= (uint32_t)kImg && (m.ret == 0u || m.ret >= 1024u));
       const bool tall = __all(tok);
       if (lane == 0) s_joint[buf][slot] = tall ? 1u : 0u;
+      // then help store the previous group (its verdicts came a stage ago) from the ticket
+      if (p.frag_len && !rf && s > 0 && cons_live && !(MGENX_DIAG && variant == 1)) {
+        const int cb = (int)((s - 1) & 1);
+        const uint64_t gc = gp - gridDim.x;
+        uint32_t co_nw = (uint32_t)min((uint64_t)kProd, n_batches - gc * kProd);
+#pragma unroll
+        for (int k = 0; k < kProd; k++)
+          if ((uint32_t)k < co_nw && !s_joint[cb][k]) co_nw = 0;
+        if (co_nw) {
+          const uint32_t co_n = (uint32_t)min((uint64_t)co_nw * 64u, (uint64_t)p.n - ((gc * kProd) << 6));
+          for (;;) {
+            uint32_t t = 0;
+            if (lane == 0) t = atomicAdd(&s_tick[cb], 1u);
+            const uint32_t gr = (uint32_t)__shfl((int)t, 0);
+            if (gr >= co_n) break;
+            big_rec(cb, gr >> 6, gr & 63u, &s_pre[slot][32]);
+          }
+        }
+      }
     }
     if constexpr (!kTcp) {  // for the joint store: the trailer word, the batch's verdict
       s_tw[buf][slot * 64 + lane] = m.trailer_on == 1 ? bswap32(m.trailer) : 0u;
@@ -603,93 +705,21 @@ pack_kernel(PackParams p) {
     if (kTcp && p.frag_len && !rf && nv > 0 &&
         (co_nw > 0 || __all(!has || (m.pend <= (uint32_t)kImg && (m.ret == 0u || m.ret >= 1024u))))) {
       if (MGENX_DIAG && variant == 1) goto stage_end;  // (diagnostics: no store phase)
-      const bool fck = p.frag_ck != 0;
-      // with a helper (no group built this stage) the two waves take alternate records, each
-      // with its own boundary table in LDS
+      // with a helper (no group built this stage) the two waves share the records, each with
+      // its own boundary table in LDS
       const uint32_t rstep = prod_live ? 1u : 2u;
       uint32_t* const bst = &s_pre[slot][helper ? 32 : 0];
-      const uint64_t g0 = (b / kProd) * kProd;  // the group's first batch
-      const uint32_t co_n = co_nw ? (uint32_t)min((uint64_t)co_nw * 64u, (uint64_t)p.n - (g0 << 6)) : nv;
-      const uint32_t co_step = co_nw ? co_nw * rstep : rstep;
-      const uint32_t co_first = co_nw ? (uint32_t)slot + (helper ? co_nw : 0u) : (helper ? 1u : 0u);
-      for (uint32_t gr = co_first; gr < co_n; gr += co_step) {
-        const uint32_t kq = co_nw ? gr >> 6 : (uint32_t)slot, rr = co_nw ? gr & 63u : gr;
-        const PackMeta R = s_meta[buf][kq][rr];
-        if (R.ret == 0u) continue;
-        const TcpReps reps = tcp_reps(R.frag, R.ret, fck);
-        const uint8_t* rimg = &s_img[buf][kq][rr * kImg];
-        const uint32_t Fe = R.frag ? R.frag : R.ret;       // the fragment's end
-        const uint32_t T = R.trailer_on ? Fe - 4u : Fe;     // where its trailer starts
-        const uint32_t be = bswap32(R.trailer);             // trailer bytes in memory order
-        // buffer starts: 0 (P), then each later buffer's; nb buffers, bst[nb] = Fe
-        uint32_t nb = 1;
-#pragma unroll
-        for (int k = 0; k < kMaxRep; k++) nb += reps.start[k] ? 1u : 0u;
-        if (lane == 0) bst[0] = 0u;
-#pragma unroll
-        for (int k = 0; k < kMaxRep; k++)
-          if (lane == k + 1 && reps.start[k]) bst[k + 1] = reps.start[k];
-        if (lane == 0) bst[nb] = Fe;
-        wave_sync();
-        uint8_t* const rbase = p.slab + R.off;
-        const uint32_t nu = (Fe + 15u) >> 4;
-        uint32_t kb = 0, bcur = 0, bnext = bst[1];
-        // the pass's buffer (wave-uniform): a pass of 64 units that lies in one buffer past
-        // its image and before the trailer is zeros -- stored as such with no per-unit walk
-        // (config 5: 13 of each record's 16 passes)
-        uint32_t ukb = 0, ubc = 0, ubn = bnext;
-        for (uint32_t u0 = 0; u0 < nu; u0 += 64u) {
-          const uint32_t x0 = u0 << 4;
-          while (x0 >= ubn && ukb + 1u < nb) {
-            ukb++;
-            ubc = ubn;
-            ubn = bst[ukb + 1];
-          }
-          if (x0 - ubc >= (uint32_t)kImg && x0 + 1024u <= min(ubn, T)) {
-            stu128(rbase + x0 + 16u * (uint32_t)lane, u32x4_t{0u, 0u, 0u, 0u});
-            continue;
-          }
-          const uint32_t u = u0 + (uint32_t)lane;
-          if (u >= nu) continue;
-          const uint32_t x = u << 4;
-          while (x >= bnext && kb + 1u < nb) {
-            kb++;
-            bcur = bnext;
-            bnext = bst[kb + 1];
-          }
-          const uint32_t pos = x - bcur;
-          const u32x4_t iv = *reinterpret_cast<const u32x4_t*>(rimg + min(pos, (uint32_t)kImg - 16u));
-          uint32_t v[4] = {iv.x, iv.y, iv.z, iv.w};
-          if (pos >= (uint32_t)kImg) v[0] = v[1] = v[2] = v[3] = 0u;  // (past pend: zero fill)
-          if ((pos & 15u) != 0u || x + 16u > min(bnext, T)) {
-            // a unit across a boundary or off the 16-byte grid of its buffer: byte by byte
-            uint32_t kk = kb, bc = bcur, bn = bnext;
-#pragma unroll
-            for (int j = 0; j < 16; j++) {
-              const uint32_t xb = x + (uint32_t)j;
-              uint32_t byte = 0u;
-              if (xb >= T) {
-                byte = xb < Fe ? (be >> (8u * (xb - T))) & 0xffu : 0u;
-              } else {
-                while (xb >= bn) {
-                  kk++;
-                  bc = bn;
-                  bn = bst[kk + 1];
-                }
-                const uint32_t q = xb - bc;
-                byte = q < (uint32_t)kImg ? rimg[q] : 0u;
-              }
-              if ((j & 3) == 0) v[j >> 2] = 0u;
-              v[j >> 2] |= byte << (8 * (j & 3));
-            }
-          }
-          if (x + 16u <= Fe) {
-            stu128(rbase + x, u32x4_t{v[0], v[1], v[2], v[3]});
-          } else {
-            st_part(rbase + x, v, Fe - x);
-          }
+      if (co_nw) {  // the group's records by an LDS ticket (the meta waves join once built)
+        const uint32_t co_n = (uint32_t)min((uint64_t)co_nw * 64u, (uint64_t)p.n - (((b / kProd) * kProd) << 6));
+        for (;;) {
+          uint32_t t = 0;
+          if (lane == 0) t = atomicAdd(&s_tick[buf], 1u);
+          const uint32_t gr = (uint32_t)__shfl((int)t, 0);
+          if (gr >= co_n) break;
+          big_rec(buf, gr >> 6, gr & 63u, bst);
         }
-        wave_sync();  // (the boundary table is rewritten for the next record)
+      } else {  // this wave's batch (a helper takes every other record)
+        for (uint32_t rr = helper ? 1u : 0u; rr < nv; rr += rstep) big_rec(buf, (uint32_t)slot, rr, bst);
       }
       goto stage_end;
     }

@@ -67,5 +67,7 @@ torch.cuda.synchronize()
 out["rows_same"] = bool(torch.equal(f2, w2) and int(n2.cpu()[0]) == int(nf.cpu()[0]))
 eng.flow_table_destroy(table)
 out["mode"] = os.environ.get("MGENX_FT_MODE", "0")
+out["gmul"] = os.environ.get("MGENX_FT_GMUL", "-")
+out["kcap"] = os.environ.get("MGENX_FT_KCAP", "-")
 out["lib"] = os.path.basename(os.environ.get("MGENX_LIB_OVERRIDE", "libmgenx.so"))
 print(json.dumps(out))

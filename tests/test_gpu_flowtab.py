@@ -60,14 +60,16 @@ def _device_inputs(torch, srcs, dsts, si, di, fid, err):
     return cols, t(src.reshape(-1))
 
 
-def test_flow_lookup_matches_reference_key(torch, eng):
-    rng = np.random.default_rng(11)
-    table = eng.flow_table(8192)
+@pytest.mark.parametrize("max_flows,n_src,calls", [(8192, 40, 4), (2048, 12, 3)])
+def test_flow_lookup_matches_reference_key(torch, eng, max_flows, n_src, calls):
+    """max_flows 8192: the large-table path (flag / scan / number kernels); 2048 (4096 slots):
+    the small-table path (keys staged in LDS, the last workgroup numbers the new keys)."""
+    table = eng.flow_table(max_flows)
     ref = {}
     try:
-        for call in range(3):   # keys persist across batches
+        for call in range(calls):   # keys persist across batches; later batches add a few new keys
             srcs, dsts, si, di, fid, err = _batch(np.random.default_rng(100 + call), 50_000,
-                                                  40, 6, 12)
+                                                  n_src, 6, 12)
             cols, src = _device_inputs(torch, srcs, dsts, si, di, fid, err)
             idx, nf = eng.flow_lookup(table, cols, src, len(si))
             torch.cuda.synchronize()
@@ -84,10 +86,11 @@ def test_flow_lookup_matches_reference_key(torch, eng):
             assert int(nf.cpu()[0]) == len(ref)
     finally:
         eng.flow_table_destroy(table)
-    assert 1000 < len(ref) < 8192
+    assert 1000 < len(ref) < max_flows
 
 
-def test_flow_lookup_from_rows(torch, eng):
+@pytest.mark.parametrize("max_flows", [8192, 2048])
+def test_flow_lookup_from_rows(torch, eng, max_flows):
     """FindFlow keyed from the 32-B mgenx_rec rows: IPv4 destinations from dst_addr4 give
     the column form's indices; an IPv6 destination without the dst_addr column is unkeyed
     (MGENX_FLOW_NONE), with it the rows form equals the columns form again."""
@@ -105,7 +108,8 @@ def test_flow_lookup_from_rows(torch, eng):
     rows["seq_num"] = rng.integers(0, 2**32, n, dtype=np.uint64)   # not part of the key
     drows = torch.from_numpy(rows.view(np.uint8).copy()).cuda()
     v6 = np.array([dsts[d][1] > 4 for d in di])
-    want_tab, t_rows, t_both = eng.flow_table(8192), eng.flow_table(8192), eng.flow_table(8192)
+    want_tab, t_rows, t_both = (eng.flow_table(max_flows), eng.flow_table(max_flows),
+                                eng.flow_table(max_flows))
     try:
         want, _ = eng.flow_lookup(want_tab, cols, src, n)
         got, nf = eng.flow_lookup(t_rows, {"rows": drows}, src, n)
