@@ -619,6 +619,14 @@ int mgenx_flow_lookup(mgenx_ctx* ctx, mgenx_flow_table* table, const mgenx_cols*
  * `protocol`): the report_msg keys mgenx_report_build takes (mgenAnalytic.cpp:28-71). */
 int mgenx_flow_keys(mgenx_ctx* ctx, const mgenx_flow_table* table, int protocol,
                     mgenx_report_key* dev_keys, uint32_t cap, void* stream);
+/* The sizes a batch's report slots need, on the device: dev_out[0] = the most records any flow
+ * index < n_flows holds, dev_out[1] / dev_out[2] = the lowest / highest receive time (sec *
+ * 1e6 + usec) over those records (UINT64_MAX / 0 when there are none).  dev_counts: n_flows
+ * words of scratch (cleared here).  pcap2mgen sizes its per-flow report slots from these
+ * (a window closes at most once per record and once per window of capture time). */
+int mgenx_flow_span(mgenx_ctx* ctx, const uint32_t* dev_flow_idx, const uint32_t* dev_rx_sec,
+                    const uint32_t* dev_rx_usec, uint32_t n, uint32_t n_flows,
+                    uint32_t* dev_counts, uint64_t* dev_out, void* stream);
 
 /* ---- event log (MgenMsg::LogRecvEvent / LogRecvError, text form) ----
  * One line per record, as the UDP receive path logs it (src/common/mgenTransport.cpp:

@@ -242,30 +242,23 @@ class Pcap2Mgen {
   }
 
   // report slots per flow: a window closes at most once per record and, since the window
-  // restarts at the closing record, at most once per window length of capture time
+  // restarts at the closing record, at most once per window length of capture time (the
+  // counts and the time range reduced on the device: 24 bytes come back, not the columns)
   uint32_t PerFlow(const uint32_t* d_fidx, const uint32_t* d_sec, const uint32_t* d_usec,
                    uint32_t n, uint32_t n_flows) {
-    std::vector<uint32_t> f(n), sec(n), usec(n);
     hipStream_t s = ctx_.stream();
-    check_hip(hipMemcpyAsync(f.data(), d_fidx, (size_t)n * 4, hipMemcpyDeviceToHost, s), "D2H");
-    check_hip(hipMemcpyAsync(sec.data(), d_sec, (size_t)n * 4, hipMemcpyDeviceToHost, s), "D2H");
-    check_hip(hipMemcpyAsync(usec.data(), d_usec, (size_t)n * 4, hipMemcpyDeviceToHost, s),
-              "D2H");
+    DeviceArray<uint32_t> cnt(n_flows);
+    DeviceArray<uint64_t> d_out(3);
+    ctx_.Check(mgenx_flow_span(ctx_.get(), d_fidx, d_sec, d_usec, n, n_flows, cnt.data(),
+                               d_out.data(), s),
+               "mgenx_flow_span");
+    uint64_t o[3] = {0, 0, 0};
+    check_hip(hipMemcpyAsync(o, d_out.data(), sizeof(o), hipMemcpyDeviceToHost, s), "D2H");
     ctx_.Sync();
-    std::vector<uint32_t> cnt(n_flows, 0);
-    int64_t lo = INT64_MAX, hi = INT64_MIN;
-    for (uint32_t i = 0; i < n; i++) {
-      if (f[i] >= n_flows) continue;
-      cnt[f[i]]++;
-      const int64_t t = (int64_t)sec[i] * 1000000 + usec[i];
-      lo = t < lo ? t : lo;
-      hi = t > hi ? t : hi;
-    }
-    uint32_t most = 1;
-    for (uint32_t k : cnt) most = k > most ? k : most;
+    const uint32_t most = o[0] > 1 ? (uint32_t)o[0] : 1u;
     const double w = o_.window;  // the quantized window is within 5% of the request
-    if (w <= 0.0 || hi < lo) return most;
-    const double by_time = (double)(hi - lo) * 1e-6 / (0.95 * w) + 2.0;
+    if (w <= 0.0 || o[2] < o[1]) return most;
+    const double by_time = (double)(o[2] - o[1]) * 1e-6 / (0.95 * w) + 2.0;
     return by_time < most ? (uint32_t)by_time : most;
   }
 

@@ -40,7 +40,8 @@ EXPORTED_SYMBOLS = (
     "mgenx_log_recv_text", "mgenx_log_recv_binary", "mgenx_comm_unique_id", "mgenx_comm_init",
     "mgenx_comm_destroy", "mgenx_allreduce_flows", "mgenx_allgather_u64",
     "mgenx_flow_table_create", "mgenx_flow_table_destroy", "mgenx_flow_lookup",
-    "mgenx_flow_reduce_ex", "mgenx_flow_keys", "mgenx_text_interleave", "mgenx_pcap_index",
+    "mgenx_flow_reduce_ex", "mgenx_flow_keys", "mgenx_flow_span", "mgenx_text_interleave",
+    "mgenx_pcap_index",
     "mgenx_pcap_parse", "mgenx_binlog_index", "mgenx_convert_binary_log",
     "mgenx_unpack_last_kernel", "mgenx_pcap_snap", "mgenx_flow_reduce_rows",
     "mgenx_worker_create", "mgenx_worker_destroy", "mgenx_worker_unpack", "mgenx_worker_crc32",
@@ -101,6 +102,7 @@ def load(diag: bool = False):
     L.mgenx_flow_lookup.argtypes = [P, P, ctypes.POINTER(MgenxCols), P, u32, P, P, P]
     L.mgenx_flow_reduce_ex.argtypes = [P, P, P, P, P, P, P, P, u32, P, u32, P, u32, P, P, P]
     L.mgenx_flow_keys.argtypes = [P, P, i32, P, u32, P]
+    L.mgenx_flow_span.argtypes = [P, P, P, P, u32, u32, P, P, P]
     L.mgenx_text_interleave.argtypes = [P, P, u32, u32, P, u64, P, P]
     L.mgenx_pcap_index.argtypes = [P, u64, P, u64, ctypes.POINTER(PcapInfo)]
     L.mgenx_pcap_parse.argtypes = [P, P, u64, P, u32, u32, u32, P, P, P, P, P, P, P, P]
@@ -515,6 +517,19 @@ class Engine:
         self._check(self.lib.mgenx_flow_keys(self.ctx, table, protocol, _ptr(keys), n_flows,
                                              _stream(self.device)), "mgenx_flow_keys")
         return keys
+
+    def flow_span(self, flow_idx, rx_sec, rx_usec, n, n_flows):
+        """(most records of any flow index < n_flows, lowest, highest receive time in us) over
+        those records (mgenx_flow_span; (0, 2**64 - 1, 0) when there are none): one read-back."""
+        torch = self.torch
+        dev = flow_idx.device
+        counts = torch.empty(max(n_flows, 1), dtype=torch.int32, device=dev)
+        out = torch.empty(3, dtype=torch.int64, device=dev)
+        self._check(self.lib.mgenx_flow_span(self.ctx, _ptr(flow_idx), _ptr(rx_sec), _ptr(rx_usec),
+                                             n, n_flows, _ptr(counts), _ptr(out),
+                                             _stream(self.device)), "mgenx_flow_span")
+        most, lo, hi = (int(v) & 0xFFFFFFFFFFFFFFFF for v in out.cpu().tolist())
+        return most, lo, hi
 
     def text_interleave(self, sources, n_rec, cap=None):
         """mgenx_text_interleave: sources = [(kind, text, line_off, n_lines, index,

@@ -547,6 +547,59 @@ __global__ void flowtab_keys_kernel(const FlowSlot* __restrict__ tab, uint32_t c
   keys[sl.index] = o;
 }
 
+// mgenx_flow_span: per-flow record counts (global atomics), then the largest count and the
+// receive-time range, each block folding its part first
+__global__ void __launch_bounds__(256)
+flow_span_count_kernel(const uint32_t* __restrict__ fidx, const uint32_t* __restrict__ sec,
+                       const uint32_t* __restrict__ usec, uint32_t n, uint32_t n_flows,
+                       uint32_t* __restrict__ counts, unsigned long long* __restrict__ out) {
+  __shared__ unsigned long long lo_s[4], hi_s[4];
+  unsigned long long lo = ~0ull, hi = 0ull;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t f = fidx[i];
+    if (f >= n_flows) continue;
+    atomicAdd(&counts[f], 1u);
+    const unsigned long long t = (unsigned long long)sec[i] * 1000000ull + usec[i];
+    lo = t < lo ? t : lo;
+    hi = t > hi ? t : hi;
+  }
+  for (int o = 32; o >= 1; o >>= 1) {
+    const unsigned long long a = __shfl_xor(lo, o), b = __shfl_xor(hi, o);
+    lo = a < lo ? a : lo;
+    hi = b > hi ? b : hi;
+  }
+  const uint32_t w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63u) == 0u) {
+    lo_s[w] = lo;
+    hi_s[w] = hi;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < 4; k++) {
+      lo = lo_s[k] < lo ? lo_s[k] : lo;
+      hi = hi_s[k] > hi ? hi_s[k] : hi;
+    }
+    if (lo != ~0ull) atomicMin(&out[1], lo);
+    if (hi != 0ull) atomicMax(&out[2], hi);
+  }
+}
+
+__global__ void __launch_bounds__(256)
+flow_span_max_kernel(const uint32_t* __restrict__ counts, uint32_t n_flows,
+                     unsigned long long* __restrict__ out) {
+  uint32_t m = 0;
+  for (uint32_t f = blockIdx.x * blockDim.x + threadIdx.x; f < n_flows; f += gridDim.x * blockDim.x)
+    m = max(m, counts[f]);
+  for (int o = 32; o >= 1; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+  if ((threadIdx.x & 63u) == 0u && m) atomicMax(&out[0], (unsigned long long)m);
+}
+
+__global__ void flow_span_init_kernel(unsigned long long* out) {
+  out[0] = 0ull;
+  out[1] = ~0ull;
+  out[2] = 0ull;
+}
+
 }  // namespace mgenx
 
 using namespace mgenx;
@@ -670,6 +723,26 @@ int mgenx_flow_keys(mgenx_ctx* ctx, const mgenx_flow_table* t, int protocol,
   if (cap == 0) return MGENX_OK;
   hipLaunchKernelGGL(flowtab_keys_kernel, dim3((t->cap + 255) / 256), dim3(256), 0,
                      (hipStream_t)stream, t->slots, t->cap, protocol, dev_keys, cap);
+  return hipGetLastError() == hipSuccess ? MGENX_OK : MGENX_EDEVICE;
+}
+
+int mgenx_flow_span(mgenx_ctx* ctx, const uint32_t* dev_flow_idx, const uint32_t* dev_rx_sec,
+                    const uint32_t* dev_rx_usec, uint32_t n, uint32_t n_flows,
+                    uint32_t* dev_counts, uint64_t* dev_out, void* stream) {
+  if (!ctx || !dev_out || (n && (!dev_flow_idx || !dev_rx_sec || !dev_rx_usec)) ||
+      (n_flows && !dev_counts))
+    return MGENX_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  unsigned long long* out = reinterpret_cast<unsigned long long*>(dev_out);
+  hipLaunchKernelGGL(flow_span_init_kernel, dim3(1), dim3(1), 0, s, out);
+  if (n && n_flows) {
+    if (hipMemsetAsync(dev_counts, 0, (size_t)n_flows * 4, s) != hipSuccess) return MGENX_EDEVICE;
+    const uint32_t g = std::min((n + 255u) / 256u, 2048u);
+    hipLaunchKernelGGL(flow_span_count_kernel, dim3(g), dim3(256), 0, s, dev_flow_idx, dev_rx_sec,
+                       dev_rx_usec, n, n_flows, dev_counts, out);
+    hipLaunchKernelGGL(flow_span_max_kernel, dim3(std::min((n_flows + 255u) / 256u, 256u)),
+                       dim3(256), 0, s, dev_counts, n_flows, out);
+  }
   return hipGetLastError() == hipSuccess ? MGENX_OK : MGENX_EDEVICE;
 }
 

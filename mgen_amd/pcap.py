@@ -158,17 +158,12 @@ class Pcap2Mgen:
 
     def _per_flow(self, p, flow_idx, n, n_flows) -> int:
         """Report slots per flow: a window closes at most once per record and at most once
-        per window length of capture time (the window restarts at the closing record)."""
-        torch = self.eng.torch
-        ok = (flow_idx[:n] >= 0) & (flow_idx[:n] < n_flows)  # MGENX_FLOW_NONE reads as -1
-        if not bool(ok.any()):
+        per window length of capture time (the window restarts at the closing record).  The
+        counts and the time range are reduced on the device (mgenx_flow_span, one read-back)."""
+        most, lo, hi = self.eng.flow_span(flow_idx, p["rx_sec"], p["rx_usec"], n, n_flows)
+        if most == 0:
             return 1
-        sec = p["rx_sec"][:n].to(torch.int64)[ok]
-        usec = p["rx_usec"][:n].to(torch.int64)[ok]
-        t = sec * 1000000 + usec
-        span = float((t.max() - t.min()).item()) * 1e-6
-        counts = torch.bincount(flow_idx[:n][ok].to(torch.int64), minlength=n_flows)
-        most = int(counts.max().item())
+        span = float(hi - lo) * 1e-6
         w = _quantized_window(self.window)
         by_time = most if w <= 0.0 else int(span / w) + 2
         return max(1, min(most, by_time))

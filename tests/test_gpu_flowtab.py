@@ -165,3 +165,23 @@ def test_flow_lookup_undersized_table_is_bounded(torch, eng):
         assert dt < 0.05, dt
     finally:
         eng.flow_table_destroy(table)
+
+
+def test_flow_span_matches_numpy(torch, eng):
+    """mgenx_flow_span (pcap2mgen's report-slot sizing): the most records of any flow index
+    < n_flows and the receive-time range over those records, against numpy; records with an
+    index past n_flows (MGENX_FLOW_NONE among them) do not count."""
+    rng = np.random.default_rng(5)
+    n, n_flows = 300_000, 777
+    f = rng.integers(0, n_flows + 40, n).astype(np.uint32)
+    f[rng.random(n) < 0.01] = 0xFFFFFFFF
+    sec = rng.integers(1_700_000_000, 1_700_000_900, n).astype(np.uint32)
+    usec = rng.integers(0, 1_000_000, n).astype(np.uint32)
+    t = lambda a: torch.from_numpy(a.view(np.int32).copy()).cuda()  # noqa: E731
+    most, lo, hi = eng.flow_span(t(f), t(sec), t(usec), n, n_flows)
+    ok = f < n_flows
+    tt = sec[ok].astype(np.int64) * 1_000_000 + usec[ok]
+    assert most == int(np.bincount(f[ok], minlength=n_flows).max())
+    assert (lo, hi) == (int(tt.min()), int(tt.max()))
+    most, lo, hi = eng.flow_span(t(f), t(sec), t(usec), n, 0)   # no flow index is < 0
+    assert (most, lo, hi) == (0, 2**64 - 1, 0)
