@@ -480,9 +480,18 @@ static int pack_common(mgenx_ctx* ctx, const mgenx_flow_tmpl* dev_tmpl,
   p.skip = dev_skip;
   const uint64_t batches = ((uint64_t)n + 63) / 64;
   uint64_t grid = (batches + 3) / 4;                // groups of 4 batches (kProd)
-  uint64_t cap = (uint64_t)ctx->cu_count * 2;  // 76 KB of LDS per workgroup
+  // 76 KB of LDS per workgroup: two per CU, except for the aligned-stride layout (the
+  // recvmmsg slots, config 2), whose joint 4-KB-chunk store runs faster with one workgroup --
+  // eight waves -- per CU (config 2: 0.199 against 0.211 ms; config 3's packed slab the other
+  // way: 0.214 against 0.188 ms)
+  const bool stride_layout = !dev_rec_off && !dev_frag_len && !(opts & MGENX_PACK_RANDOM_FILL) &&
+                             (stride & 15u) == 0 && stride >= 32 && stride <= 65536;
+  uint64_t cap = (uint64_t)ctx->cu_count * (stride_layout ? 1u : 2u);
   if (MGENX_DIAG && ctx->pack_variant >= 7 && ctx->pack_variant <= 9)
     cap *= (uint64_t)(ctx->pack_variant - 5);  // (diag)
+#if MGENX_DIAG
+  if (const char* v = getenv("MGENX_PACK_GRID")) cap = (uint64_t)std::max(1, atoi(v));  // (diag)
+#endif
   if (grid > cap) grid = cap;
   hipError_t e = mgenx::launch_pack(p, (int)grid, (hipStream_t)stream);
   return e == hipSuccess ? MGENX_OK : set_err(ctx, e, "pack");
