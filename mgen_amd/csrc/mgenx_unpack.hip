@@ -1689,7 +1689,9 @@ constexpr int kLongFold = 7;                                // A4 A16 A32 A64 A1
 constexpr size_t kLongLdsBytes = (size_t)(kRepDwords + kLongFold * kSmallTabDwords) * 4u;
 static_assert(kLongLdsBytes <= 160u * 1024u, "long-record tables fit the CU's LDS");
 
-__global__ void __launch_bounds__(kUnpackThreads) unpack_long_kernel(UnpackParams p) {
+template <int NB = kLongNB, int NT = kUnpackThreads>
+__global__ void __launch_bounds__(NT) unpack_long_kernel(UnpackParams p) {
+  static_assert(1024 % NT == 0, "table staging: whole passes");
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const uint32_t* fold = lds + kRepDwords;
   const uint32_t *fA4 = fold, *fA16 = fold + 1024, *fA32 = fold + 2048, *fA64 = fold + 3072,
@@ -1702,6 +1704,7 @@ __global__ void __launch_bounds__(kUnpackThreads) unpack_long_kernel(UnpackParam
   uint32_t fr[kLongFold];
 #pragma unroll
   for (int k = 0; k < kLongFold; k++) fr[k] = p.tabs[kFoldIdx[k] * 1024 + threadIdx.x];
+  constexpr int kNB = NB;
 
   const int lane = threadIdx.x & 63;
   const int q = lane & 3, quad = lane >> 2;
@@ -1741,14 +1744,14 @@ __global__ void __launch_bounds__(kUnpackThreads) unpack_long_kernel(UnpackParam
     r.live = ri < p.n && !oob;
     r.rows = r.live && r.L >= 32u;
     const uint32_t R = r.rows ? (r.L + 1023u) >> 10 : 0u;
-    r.nb = R ? (R + kLongNB - 1u) / kLongNB : 1u;
-    r.r0 = (int64_t)(r.rows ? r.L : 0u) - 1024 * (int64_t)(kLongNB * r.nb);
+    r.nb = R ? (R + kNB - 1u) / kNB : 1u;
+    r.r0 = (int64_t)(r.rows ? r.L : 0u) - 1024 * (int64_t)(kNB * r.nb);
     return r;
   };
   // row j of block b of record r, this lane's 16 bytes: the address (clamped into the record;
   // lanes before its start are zeroed at consumption)
   auto row_pos = [&](const Rec& r, uint32_t b, int j) {
-    return r.r0 + 1024 * (int64_t)(kLongNB * b + (uint32_t)j) + 16 * lane;
+    return r.r0 + 1024 * (int64_t)(kNB * b + (uint32_t)j) + 16 * lane;
   };
   auto ld_row = [&](const Rec& r, uint32_t b, int j) {
     const int64_t pos = row_pos(r, b, j);
@@ -1758,23 +1761,27 @@ __global__ void __launch_bounds__(kUnpackThreads) unpack_long_kernel(UnpackParam
 
   Rec cur = place(wave_id);
   uint32_t b = 0;
-  u32x4_t d[kLongNB];
+  u32x4_t d[kNB];
 #pragma unroll
-  for (int j = 0; j < kLongNB; j++) {
+  for (int j = 0; j < kNB; j++) {
     d[j] = ld_row(cur, 0, j);
     __builtin_amdgcn_sched_barrier(0);
   }
   // stage the tables behind the first block's loads (fence-free barrier: lgkmcnt only)
   {
     typedef __attribute__((address_space(3))) u32x4_t lds_u32x4_t;
-    const uint32_t e = threadIdx.x, k = e >> 8, val = e & 255u;
-    const u32x4_t s = {a1024, a1024, a1024, a1024};
-    lds_u32x4_t* dst = (lds_u32x4_t*)((k >> 1) * 65536u + val * 256u + (k & 1u) * 128u);
+    for (uint32_t e = threadIdx.x; e < 1024u; e += NT) {
+      const uint32_t k = e >> 8, val = e & 255u;
+      const uint32_t av = e == threadIdx.x ? a1024 : p.tabs[kTabA1024 * 1024 + e];
+      const u32x4_t s = {av, av, av, av};
+      lds_u32x4_t* dst = (lds_u32x4_t*)((k >> 1) * 65536u + val * 256u + (k & 1u) * 128u);
 #pragma unroll
-    for (int c = 0; c < kRep / 4; c++) dst[c] = s;
-    uint32_t* fl = lds + kRepDwords;
+      for (int c = 0; c < kRep / 4; c++) dst[c] = s;
+      uint32_t* fl = lds + kRepDwords;
 #pragma unroll
-    for (int k2 = 0; k2 < kLongFold; k2++) fl[k2 * 1024 + e] = fr[k2];
+      for (int k2 = 0; k2 < kLongFold; k2++)
+        fl[k2 * 1024 + e] = e == threadIdx.x ? fr[k2] : p.tabs[kFoldIdx[k2] * 1024 + e];
+    }
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -1801,10 +1808,10 @@ __global__ void __launch_bounds__(kUnpackThreads) unpack_long_kernel(UnpackParam
     const bool has_next = nx.idx < p.n;
     // the first real row may start before the record (or the block is padding): zero the
     // lanes' bytes before the record start (uniform test: rows at or past the start need none)
-    const bool fix = cur.r0 + 1024 * (int64_t)(kLongNB * b) < 0;
+    const bool fix = cur.r0 + 1024 * (int64_t)(kNB * b) < 0;
     u32x4_t xf = {0u, 0u, 0u, 0u};
 #pragma unroll
-    for (int j = 0; j < kLongNB; j++) {
+    for (int j = 0; j < kNB; j++) {
       u32x4_t x = d[j];
       if (fix) {  // lanes before the record: zeros; the straddling lane: xs
         const int64_t pos = row_pos(cur, b, j);
@@ -1814,7 +1821,7 @@ __global__ void __launch_bounds__(kUnpackThreads) unpack_long_kernel(UnpackParam
         x.z = zero ? 0u : (strad ? xs.z : x.z);
         x.w = zero ? 0u : (strad ? xs.w : x.w);
       }
-      if (last && j == kLongNB - 1) {
+      if (last && j == kNB - 1) {
         // the record's final row: folded below, not advanced
         uint32_t f0 = xor3(ha[0], hb[0], x.x), f1 = xor3(ha[1], hb[1], x.y);
         uint32_t f2 = xor3(ha[2], hb[2], x.z);
@@ -1926,11 +1933,27 @@ static hipError_t launch_var(const UnpackParams& p, int grid, hipStream_t stream
   return hipGetLastError();
 }
 
-static hipError_t launch_long(const UnpackParams& p, int grid, hipStream_t stream) {
-  hipError_t e = set_max_lds((const void*)unpack_long_kernel, (int)kLongLdsBytes);
+template <int NB = kLongNB, int NT = kUnpackThreads>
+static hipError_t launch_long_t(const UnpackParams& p, int grid, hipStream_t stream) {
+  hipError_t e = set_max_lds((const void*)unpack_long_kernel<NB, NT>, (int)kLongLdsBytes);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(unpack_long_kernel, dim3(grid), dim3(kUnpackThreads), kLongLdsBytes, stream, p);
+  hipLaunchKernelGGL((unpack_long_kernel<NB, NT>), dim3(grid), dim3(NT), kLongLdsBytes, stream, p);
   return hipGetLastError();
+}
+static hipError_t launch_long(const UnpackParams& p, int grid, hipStream_t stream) {
+#if MGENX_DIAG
+  // (diagnostics) shapes: rows per block x threads per workgroup
+  switch (p.variant) {
+    case 40: return launch_long_t<16, 512>(p, grid, stream);
+    case 41: return launch_long_t<8, 512>(p, grid, stream);
+    case 42: return launch_long_t<4, 1024>(p, grid, stream);
+    case 43: return launch_long_t<12, 512>(p, grid, stream);
+    case 44: return launch_long_t<2, 1024>(p, grid, stream);
+    case 45: return launch_long_t<16, 1024>(p, grid, stream);
+    default: break;
+  }
+#endif
+  return launch_long_t<>(p, grid, stream);
 }
 
 #if MGENX_DIAG
