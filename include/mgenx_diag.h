@@ -22,9 +22,12 @@ extern "C" {
  * no stores, 4 = decode without stores, 8 = stores to a scratch line, 16 = the other store
  * cache policy, 32 = stores wrapped onto the first 16K records, 64 = write-through stores,
  * 128 = non-temporal row loads, 256 (with 4) = dummy rows stored after each wave's last
- * group). */
+ * group), 40-45 = long-record kernel shapes (rows per block x threads: 16x512, 8x512,
+ * 4x1024, 12x512, 2x1024, 16x1024). */
 #define MGENX_TUNE_UNPACK_VARIANT 1
-/* MGENX_TUNE_PACK_VARIANT: 0 = product; ablations 1 = no unit stores, 2 = no CRC work. */
+/* MGENX_TUNE_PACK_VARIANT: 0 = product; ablations 1 = no unit stores, 2 = no CRC work, 3-6
+ * store-scheme ablations, 7-9 = grid x2..x4, 10 = the meta waves never help the joint
+ * store.  (Env MGENX_PACK_GRID: the grid, diagnostics build only.) */
 #define MGENX_TUNE_PACK_VARIANT 2
 int mgenx_set_tuning(mgenx_ctx* ctx, int key, int value);
 /* Diagnostic: plain 16-B-per-lane streaming read of `bytes` (the achievable-HBM reference

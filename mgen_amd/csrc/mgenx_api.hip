@@ -732,7 +732,7 @@ int mgenx_ctx_device(const mgenx_ctx* ctx) { return ctx ? ctx->device : -1; }
 int mgenx_set_tuning(mgenx_ctx* ctx, int key, int value) {
   if (!ctx) return MGENX_EINVAL;
   if (key == MGENX_TUNE_PACK_VARIANT) {
-    if (value < 0 || value > 9) return MGENX_EINVAL;
+    if (value < 0 || value > 10) return MGENX_EINVAL;
     ctx->pack_variant = value;
     return MGENX_OK;
   }

@@ -350,7 +350,7 @@ pack_kernel(PackParams p) {
     if constexpr (!kTcp) {
       // a meta wave with no group to build helps store the group of the other buffer
       if (producer && !prod_live && cons_live) {
-        (void)joint(gp - gridDim.x, (int)((s - 1) & 1));
+        if (!(MGENX_DIAG && variant == 10)) (void)joint(gp - gridDim.x, (int)((s - 1) & 1));
         goto stage_end;
       }
     }
@@ -642,7 +642,9 @@ pack_kernel(PackParams p) {
       const bool jall = __all(jok);
       if (lane == 0) s_joint[buf][slot] = jall ? 1u : 0u;
       // then help store the group of the other buffer (its verdicts came a stage ago)
-      if (s > 0 && cons_live) (void)joint(gp - gridDim.x, (int)((s - 1) & 1));
+      // (diagnostics: variant 10 = the meta waves never help)
+      if (s > 0 && cons_live && !(MGENX_DIAG && variant == 10))
+        (void)joint(gp - gridDim.x, (int)((s - 1) & 1));
     }
     goto stage_end;
     }
