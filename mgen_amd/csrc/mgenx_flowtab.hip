@@ -176,7 +176,16 @@ __device__ __forceinline__ void insert_global(FlowSlot* __restrict__ tab, uint32
         flow_idx[i] = q3.y;
         return;
       }
-      break;
+      // created in this call (is_new is written before the state is released, and only the
+      // numbering after the call clears it): the record takes the slot and keeps the key's
+      // first record -- a stale first_rec is never below the current one, so the plain view
+      // only skips atomics that would not lower it.  (The acquire path below invalidates
+      // caches per probe: a fresh table's first call ran 4 ms for config 4 through it.)
+      if (q3.z > i)
+        __hip_atomic_fetch_min(&tab[s0].first_rec, i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      rec_slot[i] = s0;
+      flow_idx[i] = kPend;
+      return;
     }
   }
   for (uint32_t probe = 0; probe < max_probe; probe++, s = (s + 1) & cap_mask) {
