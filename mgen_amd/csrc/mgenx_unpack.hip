@@ -748,7 +748,8 @@ unpack_kernel(UnpackParams p) {
 // Template knobs (the product instantiation is unpack_var_kernel<kUnpackThreads, 4, 0>):
 //   NT   block size (one block per CU: the LDS tables);
 //   KB   groups of rows held (0: one row store per group);
-//   MODE bit 1 (ablation): every core store to the sink; bit 8: non-temporal row stores.
+//   MODE bit 1 (ablation): every core store to the sink; bit 8: non-temporal row stores;
+//   bit 16: every row load 64-byte aligned (wrong data, timing only).
 template <int NT, int KB, int MODE>
 __global__ void __launch_bounds__(NT)
 unpack_var_kernel(UnpackParams p) {
@@ -861,6 +862,10 @@ unpack_var_kernel(UnpackParams p) {
   };
   auto row_ptr = [&](const Grp& g, int j) {
     const int real = j - g.pad;
+    if (MODE & 16) {  // (ablation, timing only: every row load 64-byte aligned, wrong data)
+      const uint64_t a = (g.off + (uint64_t)max(g.pos0 - 16 * q + 64 * real, 0)) & ~(uint64_t)63;
+      return (real >= 0) ? p.slab + a + 16u * (uint32_t)q : dummy;
+    }
     return (real >= 0) ? p.slab + g.off + (uint64_t)max(g.pos0 + 64 * real, 0) : dummy;
   };
   auto hdr_ptr = [&](const Grp& g) {
@@ -2068,6 +2073,7 @@ hipError_t launch_unpack(const UnpackParams& p, int grid, hipStream_t stream, in
       case 23: return launch_var<768, 16, 0>(p, grid, stream);
       case 27: return launch_var<1024, 8, 0>(p, grid, stream);
       case 32: return launch_var<1024, 4, 8>(p, grid, stream);  // non-temporal row stores
+      case 33: return launch_var<1024, 4, 16>(p, grid, stream);  // 64-B-aligned row loads (timing)
       default: break;
     }
   }
