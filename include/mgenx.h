@@ -561,8 +561,9 @@ int mgenx_flow_init(mgenx_ctx* ctx, mgenx_flow_state* dev_flows, uint32_t n_flow
 /* Records i < n with dev_flow_idx[i] < n_flows update flow dev_flow_idx[i], in order.
  * Columns: seq_num, tx_sec, tx_usec, msg_len (from mgenx_unpack_batch); rx time per
  * record in dev_rx_sec/dev_rx_usec.  Reports go to dev_reports[f * per_flow + k] for
- * k < per_flow; dev_report_count[f] (zeroed by the caller) counts all of them.
- * Synchronous on `stream` only when its workspace must grow. */
+ * k < per_flow; dev_report_count[f] (zeroed by the caller) counts all of them.  With
+ * per_flow == 0, dev_reports and dev_report_count may be NULL (the states' n_reports still
+ * count every report).  Synchronous on `stream` only when its workspace must grow. */
 int mgenx_flow_reduce(mgenx_ctx* ctx, const uint32_t* dev_flow_idx, const uint32_t* dev_seq,
                       const uint32_t* dev_tx_sec, const uint32_t* dev_tx_usec,
                       const uint16_t* dev_msg_len, const uint32_t* dev_rx_sec,

@@ -474,10 +474,11 @@ class Engine:
                     rx_usec, n=None, reports=None, per_flow=0, report_count=None,
                     report_rec=None):
         """MgenAnalytic::Update over records in receive order (mgenx_flow_reduce; with
-        report_rec, mgenx_flow_reduce_ex: the record that closed each kept report)."""
+        report_rec, mgenx_flow_reduce_ex: the record that closed each kept report).  Returns
+        report_count (None when per_flow is 0 and none was passed: nothing to count into)."""
         torch = self.torch
         n = flow_idx.numel() if n is None else n
-        if report_count is None:
+        if report_count is None and per_flow:
             report_count = torch.zeros(n_flows, dtype=torch.int32, device=flows.device)
         if report_rec is None:
             rc = self.lib.mgenx_flow_reduce(self.ctx, _ptr(flow_idx), _ptr(seq), _ptr(tx_sec),
@@ -499,7 +500,7 @@ class Engine:
         (mgenx_flow_reduce_rows): the same result as the column form."""
         torch = self.torch
         n = flow_idx.numel() if n is None else n
-        if report_count is None:
+        if report_count is None and per_flow:
             report_count = torch.zeros(n_flows, dtype=torch.int32, device=flows.device)
         rc = self.lib.mgenx_flow_reduce_rows(self.ctx, _ptr(flow_idx), _ptr(rows), _ptr(rx_sec),
                                              _ptr(rx_usec), n, _ptr(flows), n_flows,

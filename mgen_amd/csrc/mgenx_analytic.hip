@@ -169,7 +169,7 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
   double lmin = sp->latency_min, lmax = sp->latency_max;
   uint64_t nrep = sp->n_reports;
   const double lsum0 = sp->latency_sum;
-  const uint32_t rc0 = report_count[f];
+  const uint32_t rc0 = report_count ? report_count[f] : 0u;  // (null: per_flow == 0)
   uint32_t rcount = rc0, ncl = 0, last_close = 0, last_zr = 0;
 
   // the exact Update of one record (arguments wave-uniform); returns the record's lat'
@@ -598,7 +598,7 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
     sp->latency_min = lmin;
     sp->latency_max = lmax;
     sp->n_reports = nrep;
-    report_count[f] = rcount;
+    if (report_count) report_count[f] = rcount;
   }
 
   // ---- the latency sums, on this wave: each window's in-order FP64 sum of lat' (lane t takes
@@ -702,21 +702,30 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
 // Records whose flow index is >= n_flows (MGENX_FLOW_NONE) go to the extra last bin and are
 // not written.
 constexpr uint32_t kSortWaves = 8;
+// Tiles of 512 x kK records (kK keys per lane of each of the 8 waves): 4096 normally; 4608
+// when that takes the persistent grid's walk one round of tiles fewer (rank 0's share of
+// config 4 at N = 8 is 1,048,662 records: 257 tiles of 4096 on 256 blocks put two tiles on
+// one block of every XCD; 228 of 4608 take one round)
 constexpr uint32_t kTile = 4096;
-constexpr uint32_t kPart = kTile / kSortWaves;
+constexpr uint32_t kTileBig = 4608;
 // LDS of the order kernel: 9 x bins x 4 bytes of counts and bases, the tile's records (24 B
-// each) and their flows (2 B each) -- within 160 KiB up to 1536 bins
+// each) and their flows (2 B each) -- within 160 KiB up to 1536 bins at 4096 records, 1223 at
+// 4608
 constexpr uint32_t kCountBins = 1536;
-constexpr uint32_t kOrderLds = kCountBins * 9u * 4u + kTile * (uint32_t)sizeof(FRec) + kTile * 2u;
+constexpr uint32_t order_lds(uint32_t bins, uint32_t tile) {
+  return (kSortWaves * bins + bins + (bins & 1u)) * 4u + tile * ((uint32_t)sizeof(FRec) + 2u);
+}
+constexpr uint32_t kLdsCap = 160u * 1024u - 64u;  // (+ the kernel's static wsum[])
+static_assert(order_lds(kCountBins - 1u, kTile) <= kLdsCap, "order kernel LDS at 4096 records");
 
 __global__ void __launch_bounds__(512)
-flow_hist_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows, uint32_t n_tiles,
+flow_hist_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows, uint32_t tile,
                  uint32_t* __restrict__ hist) {
   extern __shared__ uint32_t h[];
   const uint32_t bins = n_flows + 1u;
   for (uint32_t k = threadIdx.x; k < bins; k += blockDim.x) h[k] = 0u;
   __syncthreads();
-  const uint32_t a = blockIdx.x * kTile, e = min(n, a + kTile);
+  const uint32_t a = blockIdx.x * tile, e = min(n, a + tile);
   // kHistU keys per thread and pass, all loads issued before any is used
   constexpr uint32_t kHistU = 8;
   for (uint32_t i0 = a + threadIdx.x; i0 < e; i0 += kHistU * blockDim.x) {
@@ -776,18 +785,19 @@ __device__ unsigned long long g_ord_prof[8];
 // records are loaded while the current tile's runs are written, so the reads of one tile and
 // the writes of the one before share the memory system (one tile per block and phase after
 // phase left the chip reading, then writing: 190 us for config 4).
-template <bool kRows>
+template <bool kRows, uint32_t kK>
 __global__ void __launch_bounds__(512)
 flow_order_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows,
                   uint32_t n_tiles, const uint32_t* __restrict__ start, RecSrc src,
                   FRec* __restrict__ recs, uint32_t* __restrict__ order, uint32_t key_bits,
                   uint32_t seqw) {  // diagnostics timing only (tile-contiguous writes, wrong)
+  constexpr uint32_t kT = 512u * kK, kPart = kT / kSortWaves;  // tile, records per wave
   extern __shared__ uint32_t lds[];
   const uint32_t bins = n_flows + 1u;
   uint32_t* cnt = lds;                                // [wave][bin]: counts, then run bases
   uint32_t* sbase = lds + kSortWaves * bins;          // [bin]: start - tile offset
   FRec* lrec = reinterpret_cast<FRec*>(sbase + bins + (bins & 1u));  // 8-byte aligned
-  uint16_t* lkey = reinterpret_cast<uint16_t*>(lrec + kTile);
+  uint16_t* lkey = reinterpret_cast<uint16_t*>(lrec + kT);
   __shared__ uint32_t wsum[kSortWaves];
   const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
   // tiles: XCD x (block b runs on XCD b % 8) owns tiles [x * per, (x + 1) * per), its nb blocks
@@ -800,7 +810,7 @@ flow_order_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows
   uint32_t t = xb + ci;
   uint32_t* my = cnt + w * bins;
   uint64_t* tab = reinterpret_cast<uint64_t*>(lrec) + (size_t)w * kCountBins;
-  constexpr uint32_t kKeys = kPart / 64u;
+  constexpr uint32_t kKeys = kK;
   // scan ownership: thread tid owns bins [k0, k1)
   const uint32_t B = (bins + blockDim.x - 1u) / blockDim.x;
   const uint32_t k0 = min(tid * B, bins), k1 = min(k0 + B, bins);
@@ -811,7 +821,7 @@ flow_order_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows
   // (live == false: the last pass's prefetch, every lane on element 0 -- one line, so the
   // loads still land in the loop's registers without re-reading a tile)
   auto fetch = [&](uint32_t tt, bool live) {
-    const uint32_t a = tt * kTile + w * kPart;
+    const uint32_t a = tt * kT + w * kPart;
     uint32_t ii[kKeys];
 #pragma unroll
     for (uint32_t j = 0; j < kKeys; j++) ii[j] = live ? min(a + 64u * j + lane, n - 1u) : 0u;
@@ -832,7 +842,7 @@ flow_order_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows
   const unsigned long long prof_t0 = prof_t;
 #endif
   while (true) {
-    const uint32_t t0 = t * kTile;
+    const uint32_t t0 = t * kT;
     const uint32_t a = t0 + w * kPart, e = min(n, a + kPart);
     lds_barrier();  // (every wave is past the last tile's writes, which read lrec, and zeroing)
     ORD_T(0);
@@ -934,9 +944,9 @@ flow_order_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows
     // ends; runs of one flow from neighbouring tiles meet in L2).  (As 8-B words, consecutive
     // lanes on consecutive words, the stores cover contiguous 512 B each but take 24 per
     // thread and three LDS reads a word: slower, 134 vs 130 us for config 4.)
-    const uint32_t tn = min(n - t0, kTile);
+    const uint32_t tn = min(n - t0, kT);
 #pragma unroll
-    for (uint32_t u = 0; u < kTile / 512u; u++) {
+    for (uint32_t u = 0; u < kK; u++) {
       const uint32_t j = tid + 512u * u;
       const uint32_t k = j < tn ? lkey[j] : 0xFFFFu;
       if (k < n_flows) {
@@ -1224,11 +1234,32 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
   const uint32_t bins = n_flows + 1u;
   uint32_t key_bits = 1;
   while (key_bits < 32 && (1ull << key_bits) <= n_flows) key_bits++;
-  const uint32_t n_tiles = (n + kTile - 1) / kTile;
+  // persistent order grid: one block per CU (LDS allows one), a multiple of 8 (one set per XCD)
+  if (!ws.cu) {
+    int dev = 0, cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cu = 256;
+    ws.cu = (uint32_t)max(8, cu);
+  }
+  // the tile size: 4608 records when its walk is shorter (rounds of tiles per block x records
+  // per tile) and its LDS fits, else 4096
+  auto walk = [&](uint32_t tile) {
+    const uint32_t tiles = (n + tile - 1u) / tile, per = (tiles + 7u) / 8u;
+    const uint32_t nbk = min(per, ws.cu / 8u);
+    return (uint64_t)((per + nbk - 1u) / nbk) * tile;
+  };
+  bool big = order_lds(bins, kTileBig) <= kLdsCap && walk(kTileBig) < walk(kTile);
+#if MGENX_DIAG
+  if (const char* tt = getenv("MGENX_AN_TILE"))  // 4096 / 4608: the tile size forced (A/B)
+    big = atoi(tt) == (int)kTileBig && order_lds(bins, kTileBig) <= kLdsCap;
+#endif
+  const uint32_t tile = big ? kTileBig : kTile;
+  const uint32_t n_tiles = (n + tile - 1) / tile;
   const size_t n_hist = (size_t)bins * n_tiles;
   size_t cub_bytes = 0;
   if (sort_path == 0)  // the chunk partials and their prefixes
-    cub_bytes = (size_t)2u * ((n + kTile - 1) / kTile + kColTiles - 1u) / kColTiles * bins * 4u;
+    cub_bytes = (size_t)2u * ((n_tiles + kColTiles - 1u) / kColTiles) * bins * 4u;
   else
     (void)hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, (const uint32_t*)nullptr,
                                              (uint32_t*)nullptr, (const uint32_t*)nullptr,
@@ -1269,7 +1300,7 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
     if (want_order) order = (uint32_t*)take(nb);
     uint32_t* totals = (uint32_t*)take(a256(cub_bytes));
     hipLaunchKernelGGL(flow_hist_kernel, dim3(n_tiles), dim3(512), bins * 4u, stream, flow_idx, n,
-                       n_flows, n_tiles, hist);
+                       n_flows, tile, hist);
     const uint32_t n_chunks = (n_tiles + kColTiles - 1u) / kColTiles;
     const dim3 cg((bins + 255u) / 256u, n_chunks);
     hipLaunchKernelGGL(flow_colpart_kernel, cg, dim3(256), 0, stream, hist, bins, n_tiles, totals);
@@ -1283,30 +1314,23 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
       return MGENX_EDEVICE;
     }
     // LDS: per-wave counts, the run bases, the tile's records and their flows
-    const uint32_t lds = (kSortWaves * bins + bins + (bins & 1u)) * 4u +
-                         kTile * (uint32_t)sizeof(FRec) + kTile * 2u;
-    const void* okern = src.rows ? (const void*)flow_order_kernel<true>
-                                 : (const void*)flow_order_kernel<false>;
-    e = set_max_lds(okern, (int)kOrderLds + 8);
+    const uint32_t lds = order_lds(bins, tile);
+    const uint32_t grid = 8u * min((n_tiles + 7u) / 8u, ws.cu / 8u);
+    auto launch = [&](auto kern) {
+      hipError_t le = set_max_lds((const void*)kern, (int)kLdsCap);
+      if (le != hipSuccess) return le;
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * kSortWaves), lds, stream, flow_idx, n, n_flows,
+                         n_tiles, start, src, recs, order, key_bits, oseqw);
+      return hipGetLastError();
+    };
+    if (src.rows)
+      e = big ? launch(flow_order_kernel<true, 9>) : launch(flow_order_kernel<true, 8>);
+    else
+      e = big ? launch(flow_order_kernel<false, 9>) : launch(flow_order_kernel<false, 8>);
     if (e != hipSuccess) {
       snprintf(err, errn, "flow_reduce order: %s", hipGetErrorString(e));
       return MGENX_EDEVICE;
     }
-    // persistent: one block per CU (LDS allows one), a multiple of 8 (one set per XCD)
-    if (!ws.cu) {
-      int dev = 0, cu = 0;
-      if (hipGetDevice(&dev) != hipSuccess ||
-          hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        cu = 256;
-      ws.cu = (uint32_t)max(8, cu);
-    }
-    const uint32_t grid = 8u * min((n_tiles + 7u) / 8u, ws.cu / 8u);
-    if (src.rows)
-      hipLaunchKernelGGL(flow_order_kernel<true>, dim3(grid), dim3(64 * kSortWaves), lds, stream,
-                         flow_idx, n, n_flows, n_tiles, start, src, recs, order, key_bits, oseqw);
-    else
-      hipLaunchKernelGGL(flow_order_kernel<false>, dim3(grid), dim3(64 * kSortWaves), lds, stream,
-                         flow_idx, n, n_flows, n_tiles, start, src, recs, order, key_bits, oseqw);
     bnd = start;  // tile 0's row: flow k starts at start[k]
     bstride = 1;
   } else {

@@ -840,8 +840,8 @@ int mgenx_flow_reduce_ex(mgenx_ctx* ctx, const uint32_t* dev_flow_idx, const uin
   if (!ctx) return MGENX_EINVAL;
   if (n == 0 || n_flows == 0) return MGENX_OK;
   if (!dev_flow_idx || !dev_seq || !dev_tx_sec || !dev_tx_usec || !dev_msg_len ||
-      !dev_rx_sec || !dev_rx_usec || !dev_flows || !dev_report_count ||
-      (per_flow && !dev_reports) || n > 0x7FFFFFFFu)
+      !dev_rx_sec || !dev_rx_usec || !dev_flows ||
+      (per_flow && (!dev_reports || !dev_report_count)) || n > 0x7FFFFFFFu)
     return MGENX_EINVAL;
   hipSetDevice(ctx->device);
   if (!ctx->flow_ws) ctx->flow_ws = mgenx_flow_ws_new();
@@ -860,7 +860,7 @@ int mgenx_flow_reduce_rows(mgenx_ctx* ctx, const uint32_t* dev_flow_idx, const m
   if (!ctx) return MGENX_EINVAL;
   if (n == 0 || n_flows == 0) return MGENX_OK;
   if (!dev_flow_idx || !dev_rows || !dev_rx_sec || !dev_rx_usec || !dev_flows ||
-      !dev_report_count || (per_flow && !dev_reports) || n > 0x7FFFFFFFu)
+      (per_flow && (!dev_reports || !dev_report_count)) || n > 0x7FFFFFFFu)
     return MGENX_EINVAL;
   hipSetDevice(ctx->device);
   if (!ctx->flow_ws) ctx->flow_ws = mgenx_flow_ws_new();

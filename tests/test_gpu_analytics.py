@@ -383,6 +383,65 @@ def test_flow_reduce_config4_full_size_vs_oracle(torch, eng):
                                                                   int(rep[f, r]["rx_usec"]))
 
 
+def test_flow_reduce_big_tiles_vs_oracle(torch, eng):
+    """1,100,000 records: on a 256-CU part 4096-record tiles would take the persistent order
+    grid two rounds (269 tiles), so the ordering takes 4608-record tiles (239, the last one
+    ragged) -- column and row forms with report_rec against the oracle; then the same records
+    with per_flow = 0 and no report counts (NULL dev_report_count) give the same states."""
+    from mgen_amd import FLOW_REPORT_DTYPE, FLOW_STATE_DTYPE, REC_DTYPE
+    from mgen_amd.workloads import poisson_flows
+    from oracle import oracle as O
+    n_flows, per_flow, window = 200, 8, 0.5
+    d = poisson_flows(1_100_000, n_flows, mean_gap_us=400, seed=46, loss=0.01, dup=0.005,
+                      reorder=10)
+    n = len(d["seq"])
+    assert 256 * 4096 < n <= 256 * 4608
+    idx = dev(torch, (d["flow_id"] - 1).astype(np.uint32))
+    rows = np.zeros(n, REC_DTYPE)
+    rows["flow_id"], rows["seq_num"] = d["flow_id"], d["seq"]
+    rows["tx_sec"], rows["tx_usec"], rows["msg_len"] = d["tx_sec"], d["tx_usec"], d["msg_len"]
+    c = {k: dev(torch, v) for k, v in d.items()}
+    out = []
+    for use_rows in (False, True):
+        flows = eng.flow_init(n_flows, window)
+        reports = torch.zeros(n_flows * per_flow * 96, dtype=torch.uint8, device="cuda")
+        count = torch.zeros(n_flows, dtype=torch.int32, device="cuda")
+        rrec = torch.zeros(n_flows * per_flow, dtype=torch.int32, device="cuda")
+        if use_rows:
+            eng.flow_reduce_rows(flows, n_flows, idx, dev(torch, rows.view(np.uint8)),
+                                 c["rx_sec"], c["rx_usec"], reports=reports, per_flow=per_flow,
+                                 report_count=count, report_rec=rrec)
+        else:
+            eng.flow_reduce(flows, n_flows, idx, c["seq"], c["tx_sec"], c["tx_usec"],
+                            c["msg_len"], c["rx_sec"], c["rx_usec"], reports=reports,
+                            per_flow=per_flow, report_count=count, report_rec=rrec)
+        torch.cuda.synchronize()
+        out.append((flows.cpu().numpy(), reports.cpu().numpy(), count.cpu().numpy(),
+                    rrec.cpu().numpy()))
+    for a, b in zip(*out):
+        assert np.array_equal(a, b)
+    st = out[0][0].view(FLOW_STATE_DTYPE)
+    rep = out[0][1].view(FLOW_REPORT_DTYPE).reshape(n_flows, per_flow)
+    cnt = out[0][2].view(np.uint32)
+    of, orep, ocnt = O.flow_reduce_batch(n_flows, d["flow_id"] - 1, d["seq"], d["tx_sec"],
+                                         d["tx_usec"], d["msg_len"], d["rx_sec"],
+                                         d["rx_usec"], window=window, per_flow=per_flow)
+    assert int(ocnt.sum()) > n_flows
+    compare(st, rep, cnt, of, orep, ocnt, per_flow)
+    rrec = out[0][3].view(np.uint32).reshape(n_flows, per_flow)
+    for f in range(0, n_flows, 13):
+        for r in range(min(int(cnt[f]), per_flow)):
+            i = int(rrec[f, r])
+            assert d["flow_id"][i] - 1 == f
+            assert (int(d["rx_sec"][i]), int(d["rx_usec"][i])) == (int(rep[f, r]["rx_sec"]),
+                                                                  int(rep[f, r]["rx_usec"]))
+    flows = eng.flow_init(n_flows, window)
+    assert eng.flow_reduce(flows, n_flows, idx, c["seq"], c["tx_sec"], c["tx_usec"],
+                           c["msg_len"], c["rx_sec"], c["rx_usec"]) is None
+    torch.cuda.synchronize()
+    assert np.array_equal(flows.cpu().numpy(), out[0][0])
+
+
 def _epoch_fuzz(n_flows, per, seed, window_us):
     """Per-flow sequences aimed at the window-parallel update's seams: epoch starts (failed
     Sets in the counted branch) on closing records and right after them, duplicates of closing
