@@ -85,6 +85,22 @@ __device__ __forceinline__ FRec build_frec(const RawRec& w) {
   r.latency = tdelta(Tm{(int64_t)w.rs, (int64_t)w.ru}, Tm{(int64_t)w.ts, (int64_t)w.tu});
   return r;
 }
+// a copy the compiler cannot see through (one v_mov per dword)
+__device__ __forceinline__ uint32_t opaque_u32(uint32_t x) {
+  uint32_t y;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(y) : "v"(x));
+  return y;
+}
+__device__ __forceinline__ FRec opaque_frec(const FRec& a) {
+  FRec r;
+  r.rxk = (uint64_t)opaque_u32((uint32_t)(a.rxk >> 32)) << 32 | opaque_u32((uint32_t)a.rxk);
+  r.seq = opaque_u32(a.seq);
+  r.len = opaque_u32(a.len);
+  const uint64_t lb = __builtin_bit_cast(uint64_t, a.latency);
+  r.latency = __builtin_bit_cast(double, (uint64_t)opaque_u32((uint32_t)(lb >> 32)) << 32 |
+                                             opaque_u32((uint32_t)lb));
+  return r;
+}
 __device__ __forceinline__ FRec make_frec(const RecSrc& src, uint32_t i) {
   return build_frec(load_rec(src, i));
 }
@@ -134,7 +150,7 @@ __device__ unsigned long long g_upd_prof[10];  // + [8] restart cycles, [9] rest
 #endif
 constexpr uint32_t kUR = 4;             // records per lane and round
 constexpr uint32_t kRound = 64u * kUR;  // records per round
-constexpr uint32_t kLatRounds = 4;      // rounds of lat' staged in LDS per store burst
+constexpr uint32_t kPiece = 4u * kRound;  // lat' staged in LDS per step of the tail's sums
 
 __global__ void __launch_bounds__(256)
 flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
@@ -146,7 +162,7 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
                    uint32_t lat2_sink) {
   __shared__ uint32_t scat[4][32];
   __shared__ uint32_t fo[4][1024];
-  __shared__ double lbuf[4][kLatRounds * kRound];
+  __shared__ double lbuf[4][kPiece];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint32_t f = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + wv);
   if (f >= n_flows) return;
@@ -328,7 +344,7 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
     dirty = false;
   };
 
-  FRec cur[kUR], nxt[kUR];
+  FRec ra[kUR], rb[kUR];  // the records of two rounds (ping-pong: see the loop below)
   double latp[kUR];
   auto ld = [&](uint32_t base, FRec (&r)[kUR]) {  // clamped: lanes past the flow reload its last
 #pragma unroll
@@ -336,7 +352,7 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
   };
 
   // records [k, ev) of the round: a bulk run (every one simple, valid && m.n)
-  auto bulk = [&](uint32_t k, uint32_t ev) {
+  auto bulk = [&](const FRec (&cur)[kUR], uint32_t k, uint32_t ev) {
     // a run at msg_count == 1 replaces byte_count (:128-129), pending bytes included: a run
     // before it (the previous round's, or one before a cheap restart) that took msg_count
     // from 0 to 1 left its one record's size pending -- fold it first
@@ -442,8 +458,21 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
     dirty = true;
   };
 
-  ld(b, cur);
-  ld(b + kRound, nxt);
+  // each set's loads followed by 4 stores (to the sink slots), as every round ends: the loop
+  // head's wait for ra then has the same 16 operations after it on entry as around the loop
+  // (with fewer on entry, the compiler's count would make every pass drain rb's loads too)
+  auto sink4 = [&]() {
+#pragma unroll
+    for (uint32_t q = 0; q < kUR; q++) lat2[lat2_sink + 64u * q + lane] = 0.0;  // (4 x 64 slots)
+  };
+  ld(b, ra);
+  __builtin_amdgcn_sched_barrier(0);
+  sink4();
+  __builtin_amdgcn_sched_barrier(0);
+  ld(b + kRound, rb);
+  __builtin_amdgcn_sched_barrier(0);
+  sink4();
+  __builtin_amdgcn_sched_barrier(0);
 #if MGENX_DIAG
   const bool prof_on = blockIdx.x == 0 && wv == 0;
   unsigned long long prof[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
@@ -451,10 +480,20 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
   const unsigned long long prof_t0 = prof_t;
   bool was_rst = false;
 #endif
-  for (uint32_t i0 = b; i0 < e; i0 += kRound) {
-    FRec nx2[kUR];
-    ld(i0 + 2u * kRound, nx2);
-    const uint32_t cnt = min(kRound, e - i0);
+  // one round: records [i0, i0 + kRound) from cur, whose registers then take the round two
+  // ahead.  The loop runs it twice per pass with the two register sets swapped, so no
+  // register copy waits on a load issued a round earlier (a rotating cur / nxt / next-next
+  // triple in one loop body made the loop head wait for the previous round's loads, and for
+  // the lat' stores issued after them)
+  auto round = [&](FRec (&set)[kUR], uint32_t i0) {
+    const uint32_t cnt = i0 < e ? min(kRound, e - i0) : 0u;  // (0: a pass's empty second round)
+    // the round's records moved out of the load registers through an opaque move: the waits
+    // for set's loads happen here (vmcnt: only the other set's loads and this round's stores
+    // after them), and the round's inner loop reads no register loaded outside it -- otherwise
+    // the compiler flushes vmcnt(0) before that loop, waiting for the other set's loads too
+    FRec cur[kUR];
+#pragma unroll
+    for (uint32_t q = 0; q < kUR; q++) cur[q] = opaque_frec(set[q]);
 #if MGENX_DIAG
     prof[4]++;
 #endif
@@ -474,7 +513,7 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
         }
         UPD_T(0);
         if (ev > k) {
-          bulk(k, ev);
+          bulk(cur, k, ev);
 #if MGENX_DIAG
           prof[6]++;
 #endif
@@ -549,30 +588,23 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
       }
 #endif
     }
-    // lat' leaves through LDS, kLatRounds rounds at a time: gfx950 counts stores in vmcnt, so
-    // a round's stores would hold up the waits for the next rounds' record loads until they
-    // complete (45% of the kernel's cycles when every round stored)
-    const uint32_t ro = (uint32_t)(((i0 - b) / kRound) % kLatRounds);
-#pragma unroll
-    for (uint32_t q = 0; q < kUR; q++) lbuf[wv][ro * kRound + 64u * q + lane] = latp[q];
-    if (ro == kLatRounds - 1u || i0 + kRound >= e) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      const uint32_t bs = i0 - ro * kRound, bn = i0 + cnt - bs;  // the batch's records
-#pragma unroll
-      for (uint32_t k2 = 0; k2 < kLatRounds * kUR; k2++) {
-        const uint32_t p = 64u * k2 + lane;  // branch-free: lanes past it write the sink slots
-        lat2[p < bn ? bs + p : lat2_sink + lane] = lbuf[wv][p];
-      }
-    }
+    // this round's lat' straight from registers, then the loads of the round two ahead into
+    // cur: every round issues 4 stores and 8 loads in that order, so the wait for a round's
+    // records (vmcnt: 12, the next round's stores and loads) never waits on a store
 #pragma unroll
     for (uint32_t q = 0; q < kUR; q++) {
-      cur[q] = nxt[q];
-      nxt[q] = nx2[q];
+      const uint32_t p = 64u * q + lane;  // branch-free: lanes past the round write sink slots
+      lat2[p < cnt ? i0 + p : lat2_sink + lane] = latp[q];
     }
+    ld(i0 + 2u * kRound, set);
     if (++prounds == 4096u) flush();  // per-lane bytes stay below 2^32
     UPD_T(3);
+  };
+  // (no exit between the two rounds: a path from the first round's end back to the loop head
+  // would leave only its own stores after its loads, and the head's waits would drain them)
+  for (uint32_t i0 = b; i0 < e; i0 += 2u * kRound) {
+    round(ra, i0);
+    round(rb, i0 + kRound);
   }
 #if MGENX_DIAG
   if (prof_on && lane == 0) {
@@ -608,7 +640,6 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
   // no separate pass re-reading lat' from HBM.
   __builtin_amdgcn_s_waitcnt(0);
   double* piece = &lbuf[wv][0];
-  constexpr uint32_t kPiece = kLatRounds * kRound;
   const uint32_t kept = min(rcount, per_flow);
   const uint32_t nslots = kept > rc0 ? kept - rc0 : 0u;
   const uint32_t nwin = nslots + 1u;  // + the open window
@@ -1267,7 +1298,7 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
   const bool want_order = report_rec != nullptr;
   const size_t nb = a256((size_t)n * 4), rb = a256((size_t)n * sizeof(FRec));
   const size_t hb = a256(n_hist * 4), bb = a256((size_t)bins * 4);
-  const size_t lb = a256((size_t)(n + 64) * 8);
+  const size_t lb = a256((size_t)(n + 256) * 8);  // lat' + the update's 256 sink slots
   const size_t cb = a256((size_t)n_flows * per_flow * sizeof(CloseRec));
   // both: records (sorted), lat', closes
   // counting: hist, start, order (report_rec only), row totals
