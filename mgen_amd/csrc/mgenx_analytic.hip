@@ -679,8 +679,17 @@ flow_update_kernel(mgenx_flow_state* __restrict__ flows, uint32_t n_flows,
       const uint32_t pend = min(z0 + 1u, p0 + kPiece);
       const bool mine = has && lo <= hi && lo < pend && hi >= p0;
       if (!__ballot(mine)) continue;
-      for (uint32_t j = lane; j < pend - p0; j += 64u)
-        piece[j] = __hip_atomic_load(&lat2[p0 + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      {  // the piece's 16 loads per lane issued together, then staged (one load, wait, LDS
+         // write per step made 16 serial L2 round trips per 1024 records); branch-free: lanes
+         // past the piece reload its last value into slots nobody reads
+        double x[kPiece / 64u];
+#pragma unroll
+        for (uint32_t u = 0; u < kPiece / 64u; u++)
+          x[u] = __hip_atomic_load(&lat2[min(p0 + lane + 64u * u, pend - 1u)], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (uint32_t u = 0; u < kPiece / 64u; u++) piece[lane + 64u * u] = x[u];
+      }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
