@@ -1114,6 +1114,118 @@ flow_colscan_kernel(const uint32_t* __restrict__ hist, const uint32_t* __restric
   }
 }
 
+// The same scan in one kernel: block j owns flows [16 j, 16 j + 16) down all tiles (16 tile
+// segments x 16 flows = 256 threads): segment sums, the flows' exclusive prefixes inside the
+// block, one decoupled look-back over the blocks before it for the records of all lower flows
+// (epoch-tagged words: epoch << 40 | kind << 38 | count, kind 1 = the block's own total, 2 =
+// inclusive of every block before it), then start[] written down each segment.  Blocks wait
+// only on lower blocks, all resident (<= 96 blocks); a poll count bounds every wait anyway.
+constexpr uint32_t kC1Flows = 16, kC1Segs = 16;
+constexpr uint32_t kC1Epochs = 1u << 22;
+constexpr uint32_t kC1Spin = 1u << 20;
+__global__ void __launch_bounds__(256)
+flow_colscan1_kernel(const uint32_t* __restrict__ hist, uint32_t bins, uint32_t n_tiles,
+                     uint32_t* __restrict__ start, uint64_t* __restrict__ status, uint32_t epoch) {
+  __shared__ uint32_t part[kC1Segs][kC1Flows];
+  __shared__ uint32_t fpre[kC1Flows];
+  __shared__ uint64_t s_excl;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, kk = tid % kC1Flows, sg = tid / kC1Flows;
+  const uint32_t j = blockIdx.x, k = j * kC1Flows + kk;
+  const uint32_t per = (n_tiles + kC1Segs - 1u) / kC1Segs;
+  const uint32_t t0 = min(n_tiles, sg * per), t1 = min(n_tiles, t0 + per);
+  // 1. this thread's segment of its flow
+  uint32_t sum = 0;
+  if (k < bins) {
+    uint32_t t = t0;
+    for (; t + 8u <= t1; t += 8u) {
+      uint32_t x[8];
+#pragma unroll
+      for (uint32_t u = 0; u < 8; u++) x[u] = hist[(size_t)(t + u) * bins + k];
+#pragma unroll
+      for (uint32_t u = 0; u < 8; u++) sum += x[u];
+    }
+    for (; t < t1; t++) sum += hist[(size_t)t * bins + k];
+  }
+  part[sg][kk] = sum;
+  __syncthreads();
+  // 2. per flow: the segments' exclusive prefixes (in place) and the flow's total; then the
+  // block's flows in order
+  if (tid < kC1Flows) {
+    uint32_t run = 0;
+    for (uint32_t q = 0; q < kC1Segs; q++) {
+      const uint32_t v = part[q][tid];
+      part[q][tid] = run;
+      run += v;
+    }
+    fpre[tid] = run;
+  }
+  __syncthreads();
+  if (tid < 64u) {
+    // 3. wave 0: the block's total, its flows' exclusive prefixes, the look-back
+    const uint32_t ft = lane < kC1Flows ? fpre[lane] : 0u;
+    uint32_t incl = ft;
+#pragma unroll
+    for (uint32_t d = 1; d < kC1Flows; d <<= 1) {
+      const uint32_t o = (uint32_t)__shfl_up((int)incl, d);
+      if (lane >= d) incl += o;
+    }
+    const uint32_t agg = (uint32_t)__shfl((int)incl, (int)kC1Flows - 1);
+    if (lane < kC1Flows) fpre[lane] = incl - ft;
+    if (lane == 0)
+      __hip_atomic_store(&status[j], ((uint64_t)epoch << 40) | ((uint64_t)(j == 0 ? 2u : 1u) << 38) | agg,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t acc = 0;
+    bool gave_up = false;
+    for (int64_t top = (int64_t)j - 1; top >= 0 && !gave_up; top -= 64) {
+      const int64_t q = top - (int64_t)lane;
+      uint64_t w = 0;
+      if (q >= 0) {
+        uint32_t polls = 0;
+        do {
+          w = __hip_atomic_load(&status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } while ((uint32_t)(w >> 40) != epoch && ++polls < kC1Spin);
+      }
+      const bool here = q < 0 || (uint32_t)(w >> 40) == epoch;
+      gave_up = __ballot(!here) != 0;
+      const uint32_t kind = q >= 0 ? (uint32_t)(w >> 38) & 3u : 2u;
+      const uint64_t v = q >= 0 && here ? (w & ((1ull << 38) - 1)) : 0ull;
+      const uint64_t done = __ballot(kind == 2u);
+      const uint32_t stop = done ? (uint32_t)__ffsll((long long)done) - 1u : 64u;
+      uint64_t mine = lane <= stop ? v : 0ull;
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) mine += __shfl_xor(mine, o);
+      acc += mine;
+      if (done) break;
+    }
+    if (lane == 0) {
+      if (j != 0)
+        __hip_atomic_store(&status[j], ((uint64_t)epoch << 40) | (2ull << 38) | (acc + agg),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_excl = acc;
+    }
+  }
+  __syncthreads();
+  // 4. start[] down this thread's segment
+  if (k < bins) {
+    uint32_t run = (uint32_t)s_excl + fpre[kk] + part[sg][kk];
+    uint32_t t = t0;
+    for (; t + 8u <= t1; t += 8u) {
+      uint32_t x[8];
+#pragma unroll
+      for (uint32_t u = 0; u < 8; u++) x[u] = hist[(size_t)(t + u) * bins + k];
+#pragma unroll
+      for (uint32_t u = 0; u < 8; u++) {
+        start[(size_t)(t + u) * bins + k] = run;
+        run += x[u];
+      }
+    }
+    for (; t < t1; t++) {
+      start[(size_t)t * bins + k] = run;
+      run += hist[(size_t)t * bins + k];
+    }
+  }
+}
+
 // ---- the general ordering (any flow count): hipCUB radix sort of (flow, record) pairs ----
 // keys: flow index clamped to n_flows (records to skip sort last); vals: record index
 __global__ void flow_keys_kernel(const uint32_t* __restrict__ idx, uint32_t n, uint32_t n_flows,
@@ -1198,6 +1310,8 @@ struct mgenx_flow_ws {
   void* mem = nullptr;
   size_t bytes = 0;
   uint32_t cu = 0;  // the device's CU count (the order kernel's persistent grid)
+  uint64_t* c1_status = nullptr;  // flow_colscan1_kernel's look-back words (epoch-tagged)
+  uint32_t c1_epoch = 0;
 };
 
 extern "C" void* mgenx_flow_ws_new() { return new mgenx_flow_ws(); }
@@ -1205,6 +1319,7 @@ extern "C" void mgenx_flow_ws_free(void* p) {
   mgenx_flow_ws* w = static_cast<mgenx_flow_ws*>(p);
   if (!w) return;
   mgenx::dev_free(w->mem);
+  mgenx::dev_free(w->c1_status);
   delete w;
 }
 
@@ -1341,13 +1456,41 @@ extern "C" int mgenx_flow_reduce_run(void* wsp, const uint32_t* flow_idx, const 
     uint32_t* totals = (uint32_t*)take(a256(cub_bytes));
     hipLaunchKernelGGL(flow_hist_kernel, dim3(n_tiles), dim3(512), bins * 4u, stream, flow_idx, n,
                        n_flows, tile, hist);
-    const uint32_t n_chunks = (n_tiles + kColTiles - 1u) / kColTiles;
-    const dim3 cg((bins + 255u) / 256u, n_chunks);
-    hipLaunchKernelGGL(flow_colpart_kernel, cg, dim3(256), 0, stream, hist, bins, n_tiles, totals);
-    hipLaunchKernelGGL(flow_colbase_kernel, dim3(1), dim3(1024), 0, stream, totals, bins, n_chunks,
-                       totals + (size_t)n_chunks * bins);
-    hipLaunchKernelGGL(flow_colscan_kernel, cg, dim3(256), 0, stream, hist, totals,
-                       totals + (size_t)n_chunks * bins, bins, n_tiles, start);
+    // the single-pass scan (flow_colscan1_kernel) up to 512 tiles: each of its blocks reads
+    // every tile for its 16 flows, which beats three launches for rank 0's share at N = 8
+    // (228 tiles: 0.1259 vs 0.1287 ms, three A/B pairs) but not config 4's 2048 tiles (0.2620
+    // vs 0.2587)
+    bool one = n_tiles <= 512u;
+#if MGENX_DIAG
+    if (const char* c1 = getenv("MGENX_AN_SCAN1")) one = atoi(c1) != 0;  // (A/B)
+#endif
+    if (one) {
+      if (!ws.c1_status) {
+        if (hipMalloc(&ws.c1_status, (kCountBins / kC1Flows + 1) * 8) != hipSuccess) {
+          ws.c1_status = nullptr;
+          snprintf(err, errn, "flow_reduce: scan words");
+          return MGENX_EDEVICE;
+        }
+        ws.c1_epoch = 0;
+      }
+      if (ws.c1_epoch == 0 || ++ws.c1_epoch >= kC1Epochs) {  // (re)start the epochs from zeros
+        if (hipMemsetAsync(ws.c1_status, 0, (kCountBins / kC1Flows + 1) * 8, stream) != hipSuccess) {
+          snprintf(err, errn, "flow_reduce: scan words");
+          return MGENX_EDEVICE;
+        }
+        ws.c1_epoch = 1;
+      }
+      hipLaunchKernelGGL(flow_colscan1_kernel, dim3((bins + kC1Flows - 1u) / kC1Flows), dim3(256), 0,
+                         stream, hist, bins, n_tiles, start, ws.c1_status, ws.c1_epoch);
+    } else {
+      const uint32_t n_chunks = (n_tiles + kColTiles - 1u) / kColTiles;
+      const dim3 cg((bins + 255u) / 256u, n_chunks);
+      hipLaunchKernelGGL(flow_colpart_kernel, cg, dim3(256), 0, stream, hist, bins, n_tiles, totals);
+      hipLaunchKernelGGL(flow_colbase_kernel, dim3(1), dim3(1024), 0, stream, totals, bins, n_chunks,
+                         totals + (size_t)n_chunks * bins);
+      hipLaunchKernelGGL(flow_colscan_kernel, cg, dim3(256), 0, stream, hist, totals,
+                         totals + (size_t)n_chunks * bins, bins, n_tiles, start);
+    }
     e = hipGetLastError();
     if (e != hipSuccess) {
       snprintf(err, errn, "flow_reduce scan: %s", hipGetErrorString(e));

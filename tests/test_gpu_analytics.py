@@ -217,6 +217,24 @@ def test_flow_reduce_many_flows_radix_path(torch, eng):
     compare(st, rep, cnt, of, orep, ocnt, per_flow)
 
 
+@pytest.mark.parametrize("n_flows", [1535, 1040])
+def test_flow_reduce_single_pass_scan_many_blocks(torch, eng, n_flows):
+    """The counting sort's single-pass column scan (<= 512 tiles) at the largest flow counts:
+    96 and 65 blocks of 16 flows, so the look-back spans more than one 64-lane window and a
+    ragged last block -- against the oracle."""
+    from mgen_amd.workloads import poisson_flows
+    from oracle import oracle as O
+    per_flow = 4
+    d = poisson_flows(400_000, n_flows, mean_gap_us=5_000, seed=n_flows, reorder=20)
+    assert (len(d["seq"]) + 4095) // 4096 <= 512
+    st, rep, cnt, _ = run_gpu(torch, eng, d, n_flows, 0.2, per_flow)
+    of, orep, ocnt = O.flow_reduce_batch(n_flows, d["flow_id"] - 1, d["seq"], d["tx_sec"],
+                                         d["tx_usec"], d["msg_len"], d["rx_sec"],
+                                         d["rx_usec"], window=0.2, per_flow=per_flow)
+    assert int(ocnt.sum()) > n_flows
+    compare(st, rep, cnt, of, orep, ocnt, per_flow)
+
+
 def test_flow_reduce_flow_none_and_tile_edges(torch, eng):
     """Records with MGENX_FLOW_NONE or an index >= n_flows are skipped; batch sizes around the
     counting sort's 8192-record tile (one short tile, exact tiles, one record past)."""
